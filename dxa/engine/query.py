@@ -1,0 +1,496 @@
+"""Columnar SELECT execution: FROM/JOIN → WHERE → GROUP BY/aggregates → HAVING → SELECT → DISTINCT →
+set operations → ORDER BY → LIMIT.
+
+This is what ``spark.sql(statement)`` did for each transform statement in the reference
+(DataProcessing/datax-host/src/main/scala/datax/processor/CommonProcessorFactory.scala:249-294); every step runs
+over device columns with the dxa kernels (hash group-by / hash join / string ops).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..ops import groupby as G
+from ..ops import join as J
+from ..sql import ast as A
+from ..sql.parser import parse_query
+from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, Table, concat_columns,
+                     concat_tables, materialize)
+from .expr import (AGG_FUNCS, EvalContext, EvalError, Scope, cast_column, evaluate, output_name, predicate_mask)
+from .types import common_type, is_nested
+
+
+class QueryError(Exception):
+    pass
+
+
+class Catalog:
+    """Case-insensitive registry of named tables/views visible to SQL."""
+
+    def __init__(self):
+        self._t: Dict[str, Table] = {}
+        self._built: Dict[Tuple, J.BuiltSide] = {}
+
+    def register(self, name: str, table: Table):
+        self._t[name.lower()] = table
+
+    def drop(self, name: str):
+        self._t.pop(name.lower(), None)
+
+    def get(self, name: str) -> Optional[Table]:
+        return self._t.get(name.lower())
+
+    def names(self):
+        return list(self._t)
+
+    def __contains__(self, name):
+        return name.lower() in self._t
+
+    # stream–static join support: hash tables over resident reference tables are built once
+    def cached_build(self, key, builder):
+        b = self._built.get(key)
+        if b is None:
+            b = self._built[key] = builder()
+        return b
+
+
+def run_sql(sql: str, catalog: Catalog, ctx: EvalContext) -> Table:
+    return execute(parse_query(sql), catalog, ctx)
+
+
+def execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
+    out, src_scope = _exec_body(q.body, catalog, ctx, want_scope=bool(q.order_by))
+    if q.order_by:
+        out = _order_by(out, q.order_by, ctx, src_scope)
+    if q.limit is not None:
+        out = out.slice(0, q.limit)
+    return out
+
+
+# ---------------------------------------------------------------------------------------------------------------
+
+def _exec_body(body, catalog, ctx, want_scope=False):
+    if isinstance(body, A.Select):
+        return _exec_select(body, catalog, ctx, want_scope)
+    if isinstance(body, A.SetOp):
+        if body.op == "wrap":
+            return execute(body.left, catalog, ctx), None
+        left, _ = _exec_body(body.left, catalog, ctx)
+        right, _ = _exec_body(body.right, catalog, ctx)
+        return _set_op(body, left, right), None
+    if isinstance(body, A.Query):
+        return execute(body, catalog, ctx), None
+    raise QueryError(f"unsupported query body {type(body).__name__}")
+
+
+def _align(left: Table, right: Table) -> Tuple[Table, Table]:
+    if len(left.names) != len(right.names):
+        raise QueryError(f"set operation with {len(left.names)} vs {len(right.names)} columns")
+    lcols, rcols = [], []
+    for a, b in zip(left.columns, right.columns):
+        if a.dtype != b.dtype and not is_nested(a.dtype) and not is_nested(b.dtype):
+            t = common_type(a.dtype, b.dtype)
+            if t == "null":
+                t = "string"
+            a = cast_column(a, t) if a.dtype != t else a
+            b = cast_column(b, t) if b.dtype != t else b
+        if isinstance(a, ConstColumn) and a.value is None and not isinstance(b, ConstColumn):
+            a = ConstColumn(None, b.dtype, a.length, a.device)
+        if isinstance(b, ConstColumn) and b.value is None and not isinstance(a, ConstColumn):
+            b = ConstColumn(None, a.dtype, b.length, b.device)
+        lcols.append(a)
+        rcols.append(b)
+    return (Table(left.names, lcols, left.length, left.device), Table(left.names, rcols, right.length, right.device))
+
+
+def _set_op(op: A.SetOp, left: Table, right: Table) -> Table:
+    left, right = _align(left, right)
+    if op.op == "union":
+        out = concat_tables([left, right])
+        return out if op.all else distinct(out)
+    # INTERSECT / EXCEPT (distinct semantics)
+    l, r = distinct(left), distinct(right)
+    if l.length == 0:
+        return l
+    if r.length == 0:
+        return l if op.op == "except" else l.slice(0, 0)
+    kind = "semi" if op.op == "intersect" else "anti"
+    li, _ = J.hash_join(list(l.columns), list(r.columns), kind)
+    return l.take(li)
+
+
+def distinct(t: Table) -> Table:
+    if t.length == 0 or not t.columns:
+        return t
+    keys = [c for c in t.columns]
+    hashable = [c for c in keys if not isinstance(c, (StructColumn, ArrayColumn))]
+    if len(hashable) != len(keys):
+        # nested columns: compare their JSON text
+        from .serialize import column_json_values
+        from .column import strings_from_pylist
+        hashable = [c if not isinstance(c, (StructColumn, ArrayColumn)) else
+                    strings_from_pylist(column_json_values(c), t.device) for c in keys]
+    g = G.group_rows(hashable)
+    return t.take(g.rep)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# FROM
+# ---------------------------------------------------------------------------------------------------------------
+
+def _relation(src, catalog: Catalog, ctx: EvalContext) -> Scope:
+    if src is None:
+        return Scope([], [], [], 1, ctx.device)
+    if isinstance(src, A.TableRef):
+        name = src.name
+        if src.timewindow:
+            from ..sql.parser import parse_duration_micros
+            name = f"{src.name}_{src.timewindow.replace(' ', '')}"
+        t = catalog.get(name)
+        if t is None:
+            raise QueryError(f"table or view not found: {name}")
+        return Scope.of_table(t, src.alias or src.name.split(".")[-1])
+    if isinstance(src, A.SubqueryRef):
+        t = execute(src.query, catalog, ctx)
+        return Scope.of_table(t, src.alias)
+    if isinstance(src, A.Join):
+        return _join(src, catalog, ctx)
+    raise QueryError(f"unsupported FROM item {type(src).__name__}")
+
+
+def _split_and(e: Optional[A.Expr]) -> List[A.Expr]:
+    if e is None:
+        return []
+    if isinstance(e, A.BinOp) and e.op == "and":
+        return _split_and(e.left) + _split_and(e.right)
+    return [e]
+
+
+def _refs_resolvable(e: A.Expr, scope: Scope) -> bool:
+    for node in A.walk(e):
+        if isinstance(node, A.Ident) and scope.try_resolve(node.parts) is None:
+            return False
+    return True
+
+
+def _join(j: A.Join, catalog, ctx) -> Scope:
+    left = _relation(j.left, catalog, ctx)
+    right = _relation(j.right, catalog, ctx)
+    n_l, n_r = left.length, right.length
+    dev = left.device
+    lkeys, rkeys, residual = [], [], []
+    if j.using:
+        for nm in j.using:
+            lkeys.append(A.Ident((nm,)))
+            rkeys.append(A.Ident((nm,)))
+    for c in _split_and(j.on):
+        if isinstance(c, A.BinOp) and c.op == "=":
+            if _refs_resolvable(c.left, left) and _refs_resolvable(c.right, right) and not \
+                    _refs_resolvable(c.left, right):
+                lkeys.append(c.left)
+                rkeys.append(c.right)
+                continue
+            if _refs_resolvable(c.left, right) and _refs_resolvable(c.right, left) and not \
+                    _refs_resolvable(c.right, right):
+                lkeys.append(c.right)
+                rkeys.append(c.left)
+                continue
+        residual.append(c)
+    kind = j.kind
+    if kind == "cross" or (not lkeys):
+        if kind not in ("cross", "inner"):
+            raise QueryError(f"{kind} join without equi-join keys is not supported")
+        li = torch.arange(n_l, device=dev).repeat_interleave(n_r)
+        ri = torch.arange(n_r, device=dev).repeat(n_l)
+    else:
+        if residual and kind not in ("inner",):
+            raise QueryError("outer joins with non-equi ON conditions are not supported")
+        lk = [materialize(evaluate(e, left, ctx)) for e in lkeys]
+        rk = [materialize(evaluate(e, right, ctx)) for e in rkeys]
+        lk, rk = _coerce_keys(lk, rk)
+        li, ri = J.hash_join(lk, rk, kind if kind != "cross" else "inner")
+    if kind in ("semi", "anti"):
+        return Scope(left.names, [c.take(li) for c in left.cols], left.quals, int(li.shape[0]), dev)
+    cols = []
+    for c in left.cols:
+        cols.append(_take_nullable(c, li))
+    for c in right.cols:
+        cols.append(_take_nullable(c, ri))
+    out = Scope(left.names + right.names, cols, left.quals + right.quals, int(li.shape[0]), dev)
+    if residual:
+        pred = None
+        for c in residual:
+            m = predicate_mask(evaluate(c, out, ctx))
+            pred = m if pred is None else pred & m
+        idx = torch.nonzero(pred).flatten()
+        out = Scope(out.names, [c.take(idx) for c in out.cols], out.quals, int(idx.shape[0]), dev)
+    return out
+
+
+def _coerce_keys(lk, rk):
+    lo, ro = [], []
+    for a, b in zip(lk, rk):
+        if a.dtype != b.dtype:
+            t = common_type(a.dtype, b.dtype)
+            a = cast_column(a, t) if a.dtype != t else a
+            b = cast_column(b, t) if b.dtype != t else b
+        lo.append(a)
+        ro.append(b)
+    return lo, ro
+
+
+def _take_nullable(col: Column, idx: torch.Tensor) -> Column:
+    miss = idx < 0
+    if not bool(miss.any()) if idx.numel() else True:
+        return col.take(idx)
+    safe = torch.where(miss, torch.zeros_like(idx), idx)
+    if col.length == 0:
+        return ConstColumn(None, col.dtype, int(idx.shape[0]), col.device)
+    return col.take(safe).with_valid(~miss)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# SELECT
+# ---------------------------------------------------------------------------------------------------------------
+
+def _contains_agg(e: A.Expr, ctx) -> bool:
+    for node in A.walk(e):
+        if isinstance(node, A.Call) and (node.name in AGG_FUNCS or node.name in ctx.udafs):
+            return True
+    return False
+
+
+def _collect_aggs(e: A.Expr, ctx, out: Dict):
+    if isinstance(e, A.Call) and (e.name in AGG_FUNCS or e.name in ctx.udafs):
+        out.setdefault(e.key(), e)
+        return
+    for c in e.children():
+        _collect_aggs(c, ctx, out)
+
+
+def _expand_items(sel: A.Select, scope: Scope) -> List[Tuple[A.Expr, str]]:
+    items = []
+    for it in sel.items:
+        e = it.expr
+        if isinstance(e, A.Star):
+            if not e.qualifier:
+                for nm, q in zip(scope.names, scope.quals):
+                    items.append((A.Ident(((q,) if q and _dup(scope, nm) else ()) + (nm,)), nm))
+                continue
+            q = e.qualifier
+            if len(q) == 1 and scope.has_qualifier(q[0]):
+                for nm, qq in zip(scope.names, scope.quals):
+                    if (qq or "").lower() == q[0].lower():
+                        items.append((A.Ident((qq, nm)), nm))
+                continue
+            col = scope.resolve(q)
+            if isinstance(col, StructColumn):
+                for nm in col.names:
+                    items.append((A.Ident(q + (nm,)), nm))
+                continue
+            raise QueryError(f"cannot expand {'.'.join(q)}.*")
+        items.append((e, it.alias or output_name(e)))
+    return items
+
+
+def _dup(scope: Scope, nm: str) -> bool:
+    low = nm.lower()
+    return sum(1 for n in scope.names if n.lower() == low) > 1
+
+
+def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
+    scope = _relation(sel.from_, catalog, ctx)
+    if sel.where is not None:
+        mask = predicate_mask(evaluate(sel.where, scope, ctx))
+        idx = torch.nonzero(mask).flatten()
+        scope = Scope(scope.names, [c.take(idx) for c in scope.cols], scope.quals, int(idx.shape[0]), scope.device)
+    items = _expand_items(sel, scope)
+    is_agg = bool(sel.group_by) or any(_contains_agg(e, ctx) for e, _ in items) or (
+        sel.having is not None and _contains_agg(sel.having, ctx))
+    if is_agg:
+        out = _aggregate(sel, items, scope, ctx)
+        src = None
+    else:
+        cols = [evaluate(e, scope, ctx) for e, _ in items]
+        out = Table([nm for _, nm in items], cols, scope.length, scope.device)
+        src = scope
+    if sel.distinct:
+        out = distinct(out)
+        src = None
+    return out, (src if want_scope else None)
+
+
+def _resolve_group_expr(g: A.Expr, scope: Scope, items) -> A.Expr:
+    """GROUP BY may name a select-list alias when the name is not an input column (Spark groupByAliases)."""
+    if isinstance(g, A.Ident) and scope.try_resolve(g.parts) is None and len(g.parts) == 1:
+        for e, nm in items:
+            if nm.lower() == g.parts[0].lower():
+                return e
+    if isinstance(g, A.Literal) and g.type in ("int", "long") and 1 <= g.value <= len(items):
+        return items[g.value - 1][0]    # GROUP BY ordinal
+    return g
+
+
+def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
+    dev = scope.device
+    n = scope.length
+    gexprs = [_resolve_group_expr(g, scope, items) for g in sel.group_by]
+    if gexprs:
+        keys = [materialize(evaluate(g, scope, ctx)) for g in gexprs]
+        keys = [k if not isinstance(k, (StructColumn, ArrayColumn)) else _nested_key(k) for k in keys]
+        groups = G.group_rows(keys)
+    else:
+        # global aggregate: one group, even over zero rows
+        groups = G.Groups(torch.zeros(n, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
+                          torch.zeros(1, dtype=torch.int64, device=dev))
+    aggs: Dict = {}
+    for e, _ in items:
+        _collect_aggs(e, ctx, aggs)
+    if sel.having is not None:
+        _collect_aggs(sel.having, ctx, aggs)
+    subst = {}
+    for k, call in aggs.items():
+        subst[k] = _eval_agg(call, scope, groups, ctx)
+    ng = groups.ngroups
+    if n == 0 and not gexprs:
+        rep_scope = Scope(scope.names, [ConstColumn(None, c.dtype, 1, dev) for c in scope.cols], scope.quals, 1, dev)
+    else:
+        rep_scope = Scope(scope.names, [c.take(groups.rep) for c in scope.cols], scope.quals, ng, dev)
+    cols = [evaluate(e, rep_scope, ctx, subst) for e, _ in items]
+    out = Table([nm for _, nm in items], cols, ng, dev)
+    if sel.having is not None:
+        m = predicate_mask(evaluate(sel.having, rep_scope, ctx, subst))
+        out = out.filter(m)
+    return out
+
+
+def _nested_key(col):
+    from .serialize import column_json_values
+    from .column import strings_from_pylist
+    return strings_from_pylist(column_json_values(col), col.device)
+
+
+def _eval_agg(call: A.Call, scope: Scope, groups: G.Groups, ctx) -> Column:
+    name = call.name
+    n = scope.length
+    udaf = ctx.udafs.get(name)
+    if udaf is not None:
+        args = [materialize(evaluate(a, scope, ctx)) for a in call.args]
+        return udaf.aggregate(args, groups, ctx)
+    if call.star or (name == "count" and not call.args):
+        return G.aggregate(groups, None, "count_star", n)
+    if name == "count" and len(call.args) > 1:
+        raise QueryError("count with multiple arguments is not supported")
+    arg = materialize(evaluate(call.args[0], scope, ctx))
+    if isinstance(arg, ConstColumn):
+        arg = arg.materialize()
+    if call.distinct:
+        if name not in ("count", "sum", "avg", "approx_count_distinct"):
+            name = name  # min/max(DISTINCT x) == min/max(x)
+        else:
+            return _distinct_agg(name, arg, groups, n)
+    if name == "approx_count_distinct":
+        return _distinct_agg("count", arg, groups, n)
+    if name in ("first_value",):
+        name = "first"
+    if name in ("last_value",):
+        name = "last"
+    if name in ("collect_list", "collect_set"):
+        return _collect(groups, arg, name == "collect_set")
+    if name in ("count_if",):
+        m = predicate_mask(arg)
+        return G.aggregate(groups, PrimColumn("long", m.to(torch.int64)), "sum", n)
+    if name in ("bool_and", "every", "bool_or", "any", "some"):
+        v = arg
+        r = G.aggregate(groups, PrimColumn("long", v.data.to(torch.int64), v.valid),
+                        "min" if name in ("bool_and", "every") else "max", n)
+        return PrimColumn("boolean", r.data != 0, r.valid)
+    if name == "mean":
+        name = "avg"
+    return G.aggregate(groups, arg, name, n)
+
+
+def _distinct_agg(name, arg, groups: G.Groups, n):
+    dev = groups.rep.device
+    gcol = PrimColumn("long", groups.gid.to(torch.int64))
+    sub = G.group_rows([gcol, arg])
+    first_rows = sub.rep
+    owner = G.Groups(groups.gid[first_rows], groups.ngroups, groups.rep)
+    vals = arg.take(first_rows)
+    if name == "count":
+        return G.aggregate(owner, vals, "count", int(first_rows.shape[0]))
+    return G.aggregate(owner, vals, "sum" if name == "sum" else "avg", int(first_rows.shape[0]))
+
+
+def _collect(groups: G.Groups, arg, as_set):
+    """collect_list/collect_set → JSON array text per group (host-assisted)."""
+    from .column import strings_from_pylist
+    import json
+    from .serialize import json_value
+    vals = arg.to_pylist()
+    gid = groups.gid.cpu().tolist()
+    out = [[] for _ in range(groups.ngroups)]
+    for v, g in zip(vals, gid):
+        if v is None:
+            continue
+        if as_set and v in out[g]:
+            continue
+        out[g].append(v)
+    from .types import ArrayType
+    return strings_from_pylist([json.dumps([json_value(x, arg.dtype) for x in o], separators=(",", ":"))
+                                for o in out], groups.rep.device, ArrayType(arg.dtype))
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# ORDER BY
+# ---------------------------------------------------------------------------------------------------------------
+
+def _sort_key_tensor(col: Column) -> Tuple[torch.Tensor, torch.Tensor]:
+    col = materialize(col)
+    if isinstance(col, StrColumn):
+        # rank strings on the host (ORDER BY on strings is not a hot path in DataX flows)
+        vals = col.to_pylist()
+        order = sorted(range(len(vals)), key=lambda i: (vals[i] is None, (vals[i] or "").encode("utf-8")))
+        rank = torch.empty(len(vals), dtype=torch.int64)
+        rank[torch.tensor(order, dtype=torch.int64)] = torch.arange(len(vals), dtype=torch.int64)
+        # equal strings must get equal ranks
+        for k in range(1, len(order)):
+            if vals[order[k]] == vals[order[k - 1]]:
+                rank[order[k]] = rank[order[k - 1]]
+        return rank.to(col.device), col.valid_mask()
+    if isinstance(col, PrimColumn):
+        d = col.data
+        if d.dtype == torch.bool:
+            d = d.to(torch.int64)
+        return d, col.valid_mask()
+    raise QueryError(f"cannot ORDER BY {col.dtype}")
+
+
+def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope]) -> Table:
+    if t.length <= 1:
+        return t
+    out_scope = Scope.of_table(t)
+    perm = torch.arange(t.length, device=t.device)
+    for it in reversed(items):
+        e = it.expr
+        if isinstance(e, A.Literal) and e.type in ("int", "long"):
+            col = t.columns[e.value - 1]
+        else:
+            try:
+                col = evaluate(e, out_scope, ctx)
+            except EvalError:
+                if src_scope is None:
+                    raise
+                col = evaluate(e, src_scope, ctx)
+        key, valid = _sort_key_tensor(col)
+        key, valid = key[perm], valid[perm]
+        nulls_first = it.nulls_first if it.nulls_first is not None else it.ascending
+        o = torch.argsort(key, stable=True, descending=not it.ascending)
+        v = valid[o]
+        # move nulls to the requested end, stably
+        nn = torch.nonzero(v).flatten()
+        nl = torch.nonzero(~v).flatten()
+        o = torch.cat([o[nl], o[nn]]) if nulls_first else torch.cat([o[nn], o[nl]])
+        perm = perm[o]
+    return t.take(perm)

@@ -1,0 +1,208 @@
+"""Logical data types and Spark ``StructType`` JSON schema (de)serialisation.
+
+Input schemas in DataX are Spark ``DataType.fromJson`` documents (reference: DataProcessing/datax-host/src/main/
+scala/datax/input/SchemaFile.scala:22-26), optionally carrying SimulatedData/DataGenerator metadata
+(minValue/maxValue/allowedValues/useCurrentTimeMillis, datax-utility/.../DataGenerator.scala:20-26).
+
+Physical mapping (device columns):
+  boolean → torch.bool; int/long → int64; float/double → float64; timestamp → int64 µs since epoch (UTC);
+  date → int64 days; string → (arena uint8, starts int64, lens int32); struct/map → child columns;
+  array → fixed-arity element columns or raw JSON text.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+SCALAR_TYPES = ("boolean", "int", "long", "float", "double", "string", "timestamp", "date", "null", "binary",
+                "decimal")
+INTEGRAL = ("int", "long")
+FRACTIONAL = ("float", "double", "decimal")
+NUMERIC = INTEGRAL + FRACTIONAL
+
+
+@dataclass(frozen=True)
+class StructField:
+    name: str
+    dtype: Any
+    nullable: bool = True
+    metadata: Dict[str, Any] = field(default_factory=dict, compare=False, hash=False)
+
+
+@dataclass(frozen=True)
+class StructType:
+    fields: tuple
+
+    def names(self):
+        return [f.name for f in self.fields]
+
+    def field(self, name: str) -> Optional[StructField]:
+        for f in self.fields:
+            if f.name == name:
+                return f
+        low = name.lower()
+        for f in self.fields:
+            if f.name.lower() == low:
+                return f
+        return None
+
+    def __str__(self):
+        return "struct<" + ",".join(f"{f.name}:{type_str(f.dtype)}" for f in self.fields) + ">"
+
+
+@dataclass(frozen=True)
+class MapType:
+    key: Any
+    value: Any
+    value_contains_null: bool = True
+
+    def __str__(self):
+        return f"map<{type_str(self.key)},{type_str(self.value)}>"
+
+
+@dataclass(frozen=True)
+class ArrayType:
+    element: Any
+    contains_null: bool = True
+
+    def __str__(self):
+        return f"array<{type_str(self.element)}>"
+
+
+def type_str(t) -> str:
+    return t if isinstance(t, str) else str(t)
+
+
+def is_numeric(t) -> bool:
+    return isinstance(t, str) and t in NUMERIC
+
+
+def is_integral(t) -> bool:
+    return isinstance(t, str) and t in INTEGRAL
+
+
+def is_nested(t) -> bool:
+    return isinstance(t, (StructType, MapType, ArrayType))
+
+
+_SPARK_NAMES = {"integer": "int", "bigint": "long", "short": "int", "byte": "int", "smallint": "int",
+                "tinyint": "int", "real": "float", "bool": "boolean", "str": "string", "varchar": "string"}
+
+
+def from_json_obj(o) -> Any:
+    """Spark ``DataType.fromJson`` object → our type."""
+    if isinstance(o, str):
+        t = _SPARK_NAMES.get(o.lower(), o.lower())
+        if t.startswith("decimal"):
+            return "decimal"
+        if t not in SCALAR_TYPES:
+            raise ValueError(f"unsupported data type {o!r}")
+        return t
+    kind = o.get("type")
+    if kind == "struct":
+        return StructType(tuple(StructField(f["name"], from_json_obj(f["type"]), f.get("nullable", True),
+                                            f.get("metadata") or {}) for f in o.get("fields", [])))
+    if kind == "map":
+        return MapType(from_json_obj(o["keyType"]), from_json_obj(o["valueType"]), o.get("valueContainsNull", True))
+    if kind == "array":
+        return ArrayType(from_json_obj(o["elementType"]), o.get("containsNull", True))
+    if isinstance(kind, (str, dict)):
+        return from_json_obj(kind)
+    raise ValueError(f"unsupported schema node {o!r}")
+
+
+def schema_from_json(text: str) -> StructType:
+    t = from_json_obj(json.loads(text))
+    if not isinstance(t, StructType):
+        raise ValueError("input schema must be a struct")
+    return t
+
+
+def to_json_obj(t) -> Any:
+    if isinstance(t, str):
+        return {"int": "integer"}.get(t, t)
+    if isinstance(t, StructType):
+        return {"type": "struct", "fields": [
+            {"name": f.name, "type": to_json_obj(f.dtype), "nullable": f.nullable, "metadata": f.metadata or {}}
+            for f in t.fields]}
+    if isinstance(t, MapType):
+        return {"type": "map", "keyType": to_json_obj(t.key), "valueType": to_json_obj(t.value),
+                "valueContainsNull": t.value_contains_null}
+    if isinstance(t, ArrayType):
+        return {"type": "array", "elementType": to_json_obj(t.element), "containsNull": t.contains_null}
+    raise ValueError(t)
+
+
+def schema_to_json(t: StructType) -> str:
+    return json.dumps(to_json_obj(t))
+
+
+def parse_ddl_schema(text: str) -> StructType:
+    """'deviceId long, deviceType string, MaxEventTime Timestamp' (state-table schema syntax,
+    reference: Services/DataX.Config/DataX.Config.Test/Resource/jobConfig.conf:45)."""
+    fields = []
+    depth = 0
+    cur = ""
+    parts = []
+    for ch in text:
+        if ch in "<(":
+            depth += 1
+        elif ch in ">)":
+            depth -= 1
+        if ch == "," and depth == 0:
+            parts.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        parts.append(cur)
+    for p in parts:
+        bits = p.strip().split(None, 1)
+        if len(bits) != 2:
+            raise ValueError(f"bad schema column {p!r}")
+        name, ty = bits[0].strip("`"), bits[1].strip()
+        fields.append(StructField(name, _ddl_type(ty)))
+    return StructType(tuple(fields))
+
+
+def _ddl_type(ty: str):
+    low = ty.strip().lower()
+    if low.startswith("array<"):
+        return ArrayType(_ddl_type(ty.strip()[6:-1]))
+    if low.startswith("map<"):
+        inner = ty.strip()[4:-1]
+        depth = 0
+        for i, ch in enumerate(inner):
+            if ch in "<(":
+                depth += 1
+            elif ch in ">)":
+                depth -= 1
+            elif ch == "," and depth == 0:
+                return MapType(_ddl_type(inner[:i]), _ddl_type(inner[i + 1:]))
+        raise ValueError(ty)
+    if low.startswith("struct<"):
+        inner = ty.strip()[7:-1]
+        return parse_ddl_schema(inner.replace(":", " "))
+    if low.startswith("decimal"):
+        return "decimal"
+    return from_json_obj(low)
+
+
+def common_type(a, b):
+    """Type widening for binary arithmetic/comparison/union (Spark's findTightestCommonType, simplified)."""
+    if a == b:
+        return a
+    if a == "null":
+        return b
+    if b == "null":
+        return a
+    if is_numeric(a) and is_numeric(b):
+        if a in FRACTIONAL or b in FRACTIONAL:
+            return "double"
+        return "long"
+    if {a, b} <= {"timestamp", "date"}:
+        return "timestamp"
+    if "string" in (a, b) and not is_nested(a) and not is_nested(b):
+        return "string"
+    return a

@@ -1,0 +1,81 @@
+// Shared device helpers for the dxa gfx950 kernels.
+//
+// Everything here is written for CDNA4 (wave64): launch geometry is in multiples of 64 lanes, wave-level
+// reductions use 64-wide shuffles / 64-bit ballots, and inter-workgroup data only crosses kernel boundaries
+// (no in-launch hand-offs), so no release/acquire protocol is needed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DXA_API extern "C" __attribute__((visibility("default")))
+
+namespace dxa {
+
+constexpr int kWave = 64;
+constexpr uint64_t kSeed = 0x5bd1e9955bd1e995ull;
+constexpr uint64_t kGold = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kNullHash = 0x6e756c6c6e756c6cull;   // "nullnull"
+constexpr uint64_t kEmpty = 0xFFFFFFFFFFFFFFFFull;      // empty hash-table slot
+
+__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t hash_i64(uint64_t v) { return fmix64(v ^ kSeed); }
+
+__host__ __device__ __forceinline__ uint64_t hash_combine(uint64_t acc, uint64_t h) {
+  return fmix64(acc ^ (h + kGold + (acc << 6) + (acc >> 2)));
+}
+
+// Never let a real key collide with the empty-slot sentinel.
+__host__ __device__ __forceinline__ uint64_t fix_key(uint64_t h) { return h == kEmpty ? (kEmpty - 1) : h; }
+
+// Unaligned little-endian byte fetch of up to 8 bytes starting at p (n in [1,8]).
+__device__ __forceinline__ uint64_t load_le(const uint8_t* p, int n) {
+  uint64_t w = 0;
+  for (int i = 0; i < n; ++i) w |= (uint64_t)p[i] << (8 * i);
+  return w;
+}
+
+__device__ __forceinline__ uint64_t hash_bytes(const uint8_t* p, int64_t len) {
+  uint64_t h = kSeed ^ ((uint64_t)len * kGold);
+  int64_t i = 0;
+  for (; i + 8 <= len; i += 8) h = fmix64(h ^ load_le(p + i, 8));
+  if (i < len) h = fmix64(h ^ load_le(p + i, (int)(len - i)));
+  return fmix64(h ^ (uint64_t)len);
+}
+
+// FNV-1a 64 — used for JSON key names (matched against host-computed schema hashes).
+__host__ __device__ __forceinline__ uint64_t fnv1a_step(uint64_t h, uint32_t c) {
+  return (h ^ (uint64_t)c) * 0x100000001b3ull;
+}
+constexpr uint64_t kFnvBasis = 0xcbf29ce484222325ull;
+
+__device__ __forceinline__ int grid_stride_blocks(int64_t n, int block, int cap = 256 * 16) {
+  int64_t b = (n + block - 1) / block;
+  if (b < 1) b = 1;
+  return (int)(b < cap ? b : cap);
+}
+
+// Civil date → days since 1970-01-01 (proleptic Gregorian).
+__host__ __device__ __forceinline__ int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = (unsigned)(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + (int64_t)doe - 719468;
+}
+
+}  // namespace dxa
+
+inline int dxa_blocks(int64_t n, int block, int cap = 256 * 16) {
+  int64_t b = (n + block - 1) / block;
+  if (b < 1) b = 1;
+  return (int)(b < cap ? b : cap);
+}

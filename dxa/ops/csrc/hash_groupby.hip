@@ -1,0 +1,420 @@
+// Hashing, hash group-by / aggregation and hash-join kernels for gfx950 (kernels K11, K12, K13 in SURVEY §2.F).
+//
+// Group-by is three launches, none of which spins on another lane (a spin inside one wave64 can deadlock when
+// the publishing lane sits in the same wave):
+//   1. insert   — each row CASes its 64-bit key hash into an open-addressed table (capacity ≥ 2×rows, linear
+//                 probing) and records the slot it landed in;
+//   2. number   — every occupied slot draws a dense group id (one atomic per group, not per row);
+//   3. gather   — row → group id, and representative row = min row index of the group (atomicMin).
+// Aggregation then privatises per-group accumulators in LDS when the group count is small (the IoT flows have
+// 10^1–10^4 groups against 10^6+ rows — global atomics on a handful of hot lines would serialise on the memory
+// side, MI355X_MICROARCH.md "Global float atomics": one row hammered = 14× slower), and flushes one global atomic
+// per (workgroup, group).  Large group counts go straight to global atomics, which then rarely contend.
+//
+// Join: build side rows are inserted the same way (slot per build row), bucketed by counting sort over slots, and
+// probed with a count pass + exclusive scan + write pass.  Exact key equality is re-checked afterwards on the
+// host-visible columns (hash collisions are filtered, never silently merged).
+#include "dxa_common.h"
+
+namespace {
+
+using dxa::fmix64;
+
+// ------------------------------------------------------------------------------------------------------------
+// hashing
+// ------------------------------------------------------------------------------------------------------------
+__global__ void hash_i64_kernel(const int64_t* __restrict__ v, const uint8_t* __restrict__ valid, int64_t n,
+                                uint64_t* __restrict__ out, int combine) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = (valid && !valid[i]) ? dxa::kNullHash : dxa::hash_i64((uint64_t)v[i]);
+    out[i] = combine ? dxa::hash_combine(out[i], h) : h;
+  }
+}
+
+__global__ void hash_f64_kernel(const double* __restrict__ v, const uint8_t* __restrict__ valid, int64_t n,
+                                uint64_t* __restrict__ out, int combine) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h;
+    if (valid && !valid[i]) {
+      h = dxa::kNullHash;
+    } else {
+      double d = v[i];
+      if (d == 0.0) d = 0.0;                       // -0.0 → 0.0
+      uint64_t bits = (uint64_t)__double_as_longlong(d);
+      if (d != d) bits = 0x7ff8000000000000ull;   // canonical NaN
+      h = dxa::hash_i64(bits);
+    }
+    out[i] = combine ? dxa::hash_combine(out[i], h) : h;
+  }
+}
+
+__global__ void hash_str_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                const int32_t* __restrict__ lens, const uint8_t* __restrict__ valid, int64_t n,
+                                uint64_t* __restrict__ out, int combine) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = (valid && !valid[i]) ? dxa::kNullHash : dxa::hash_bytes(arena + starts[i], lens[i]);
+    out[i] = combine ? dxa::hash_combine(out[i], h) : h;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// group-by: insert / number / gather
+// ------------------------------------------------------------------------------------------------------------
+__global__ void table_insert_kernel(const uint64_t* __restrict__ h, int64_t n, uint64_t* __restrict__ keys,
+                                    int64_t cap_mask, int32_t* __restrict__ slot_of_row) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = dxa::fix_key(h[i]);
+    int64_t s = (int64_t)(fmix64(k) & (uint64_t)cap_mask);
+    while (true) {
+      const uint64_t cur = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == k) break;
+      if (cur == dxa::kEmpty) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&keys[s], (unsigned long long)dxa::kEmpty,
+                                        (unsigned long long)k);
+        if (prev == dxa::kEmpty || prev == k) break;
+      }
+      s = (s + 1) & cap_mask;
+    }
+    slot_of_row[i] = (int32_t)s;
+  }
+}
+
+__global__ void table_number_kernel(const uint64_t* __restrict__ keys, int64_t cap, int32_t* __restrict__ gid_of_slot,
+                                    int32_t* __restrict__ counter) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (int64_t)gridDim.x * blockDim.x) {
+    gid_of_slot[s] = keys[s] != dxa::kEmpty ? atomicAdd(counter, 1) : -1;
+  }
+}
+
+__global__ void group_gather_kernel(const int32_t* __restrict__ slot_of_row, const int32_t* __restrict__ gid_of_slot,
+                                    int64_t n, int32_t* __restrict__ gid, int32_t* __restrict__ rep) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t g = gid_of_slot[slot_of_row[i]];
+    gid[i] = g;
+    atomicMin(&rep[g], (int32_t)i);
+  }
+}
+
+// Exact-key verification: flag rows whose key columns differ from their group representative's.
+__global__ void verify_i64_kernel(const int64_t* __restrict__ v, const uint8_t* __restrict__ valid,
+                                  const int32_t* __restrict__ gid, const int32_t* __restrict__ rep, int64_t n,
+                                  int32_t* __restrict__ bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = rep[gid[i]];
+    const bool vi = valid ? valid[i] != 0 : true;
+    const bool vr = valid ? valid[r] != 0 : true;
+    if (vi != vr || (vi && v[i] != v[r])) atomicAdd(bad, 1);
+  }
+}
+
+__global__ void verify_str_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                  const int32_t* __restrict__ lens, const uint8_t* __restrict__ valid,
+                                  const int32_t* __restrict__ gid, const int32_t* __restrict__ rep, int64_t n,
+                                  int32_t* __restrict__ bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = rep[gid[i]];
+    const bool vi = valid ? valid[i] != 0 : true;
+    const bool vr = valid ? valid[r] != 0 : true;
+    bool diff = vi != vr;
+    if (!diff && vi) {
+      const int32_t l = lens[i];
+      if (l != lens[r]) diff = true;
+      else {
+        const uint8_t* a = arena + starts[i];
+        const uint8_t* b = arena + starts[r];
+        for (int32_t k = 0; k < l; ++k)
+          if (a[k] != b[k]) { diff = true; break; }
+      }
+    }
+    if (diff) atomicAdd(bad, 1);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// aggregation
+// ------------------------------------------------------------------------------------------------------------
+enum : int32_t { AGG_SUM = 0, AGG_MIN = 1, AGG_MAX = 2, AGG_COUNT = 3 };
+enum : int32_t { VT_I64 = 0, VT_F64 = 1 };
+
+__device__ __forceinline__ void lds_f64_min(double* p, double v) {
+  unsigned long long* a = (unsigned long long*)p;
+  unsigned long long old = *a, assumed;
+  do {
+    assumed = old;
+    if (__longlong_as_double((long long)assumed) <= v) return;
+    old = atomicCAS(a, assumed, (unsigned long long)__double_as_longlong(v));
+  } while (old != assumed);
+}
+__device__ __forceinline__ void lds_f64_max(double* p, double v) {
+  unsigned long long* a = (unsigned long long*)p;
+  unsigned long long old = *a, assumed;
+  do {
+    assumed = old;
+    if (__longlong_as_double((long long)assumed) >= v) return;
+    old = atomicCAS(a, assumed, (unsigned long long)__double_as_longlong(v));
+  } while (old != assumed);
+}
+
+template <int VT, int OP>
+__device__ __forceinline__ void acc_update(void* accp, int32_t g, const void* vals, int64_t i) {
+  if constexpr (OP == AGG_COUNT) {
+    atomicAdd(((unsigned long long*)accp) + g, 1ull);
+  } else if constexpr (VT == VT_I64) {
+    long long* acc = (long long*)accp;
+    const long long v = ((const long long*)vals)[i];
+    if constexpr (OP == AGG_SUM) atomicAdd((unsigned long long*)&acc[g], (unsigned long long)v);
+    else if constexpr (OP == AGG_MIN) atomicMin(&acc[g], v);
+    else atomicMax(&acc[g], v);
+  } else {
+    double* acc = (double*)accp;
+    const double v = ((const double*)vals)[i];
+    if constexpr (OP == AGG_SUM) atomicAdd(&acc[g], v);
+    else if constexpr (OP == AGG_MIN) lds_f64_min(&acc[g], v);
+    else lds_f64_max(&acc[g], v);
+  }
+}
+
+template <int VT, int OP>
+__device__ __forceinline__ uint64_t identity_bits() {
+  if constexpr (OP == AGG_SUM || OP == AGG_COUNT) return 0ull;
+  if constexpr (VT == VT_I64) return OP == AGG_MIN ? 0x7fffffffffffffffull : 0x8000000000000000ull;
+  return OP == AGG_MIN ? 0x7ff0000000000000ull /* +inf */ : 0xfff0000000000000ull /* -inf */;
+}
+
+// LDS-privatised aggregation: one accumulator array of ngroups per workgroup.
+template <int VT, int OP>
+__global__ __launch_bounds__(256) void agg_lds_kernel(const int32_t* __restrict__ gid, const void* __restrict__ vals,
+                                                      const uint8_t* __restrict__ valid, int64_t n, int32_t ngroups,
+                                                      void* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_acc[];
+  for (int g = threadIdx.x; g < ngroups; g += blockDim.x) lds_acc[g] = identity_bits<VT, OP>();
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    acc_update<VT, OP>((void*)lds_acc, gid[i], vals, i);
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < ngroups; g += blockDim.x) {
+    const unsigned long long b = lds_acc[g];
+    if (b == identity_bits<VT, OP>() && OP != AGG_SUM) continue;
+    if constexpr (OP == AGG_COUNT) {
+      if (b) atomicAdd(((unsigned long long*)out) + g, b);
+    } else if constexpr (VT == VT_I64) {
+      long long* o = (long long*)out;
+      if constexpr (OP == AGG_SUM) { if (b) atomicAdd((unsigned long long*)&o[g], b); }
+      else if constexpr (OP == AGG_MIN) atomicMin(&o[g], (long long)b);
+      else atomicMax(&o[g], (long long)b);
+    } else {
+      double* o = (double*)out;
+      const double v = __longlong_as_double((long long)b);
+      if constexpr (OP == AGG_SUM) { if (b) atomicAdd(&o[g], v); }
+      else if constexpr (OP == AGG_MIN) lds_f64_min(&o[g], v);
+      else lds_f64_max(&o[g], v);
+    }
+  }
+}
+
+template <int VT, int OP>
+__global__ __launch_bounds__(256) void agg_global_kernel(const int32_t* __restrict__ gid, const void* __restrict__ vals,
+                                                         const uint8_t* __restrict__ valid, int64_t n,
+                                                         void* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    acc_update<VT, OP>(out, gid[i], vals, i);
+  }
+}
+
+template <int VT, int OP>
+__global__ void agg_init_kernel(void* out, int32_t ngroups) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < ngroups) ((unsigned long long*)out)[g] = identity_bits<VT, OP>();
+}
+
+template <int VT, int OP>
+int launch_agg(const int32_t* gid, const void* vals, const uint8_t* valid, int64_t n, int32_t ngroups, void* out,
+               hipStream_t s) {
+  hipLaunchKernelGGL((agg_init_kernel<VT, OP>), dim3((ngroups + 255) / 256), dim3(256), 0, s, out, ngroups);
+  if (n <= 0) return (int)hipGetLastError();
+  const size_t lds = (size_t)ngroups * 8;
+  if (ngroups <= 8192) {
+    // ≈ 2 blocks per CU of streaming work; each block then flushes ngroups atomics.
+    int blocks = dxa_blocks(n, 256, ngroups <= 1024 ? 1024 : 512);
+    hipLaunchKernelGGL((agg_lds_kernel<VT, OP>), dim3(blocks), dim3(256), lds, s, gid, vals, valid, n, ngroups, out);
+  } else {
+    hipLaunchKernelGGL((agg_global_kernel<VT, OP>), dim3(dxa_blocks(n, 256, 4096)), dim3(256), 0, s, gid, vals,
+                       valid, n, out);
+  }
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// hash join (build = slot buckets, probe = count + write)
+// ------------------------------------------------------------------------------------------------------------
+__global__ void slot_count_kernel(const int32_t* __restrict__ slot_of_row, int64_t n, int32_t* __restrict__ cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[slot_of_row[i]], 1);
+}
+
+__global__ void slot_scatter_kernel(const int32_t* __restrict__ slot_of_row, int64_t n,
+                                    const int64_t* __restrict__ start, int32_t* __restrict__ cursor,
+                                    int32_t* __restrict__ rows) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = slot_of_row[i];
+    const int32_t k = atomicAdd(&cursor[s], 1);
+    rows[start[s] + k] = (int32_t)i;
+  }
+}
+
+__device__ __forceinline__ int64_t find_slot(const uint64_t* __restrict__ keys, int64_t cap_mask, uint64_t k) {
+  int64_t s = (int64_t)(fmix64(k) & (uint64_t)cap_mask);
+  while (true) {
+    const uint64_t cur = keys[s];
+    if (cur == k) return s;
+    if (cur == dxa::kEmpty) return -1;
+    s = (s + 1) & cap_mask;
+  }
+}
+
+__global__ void probe_count_kernel(const uint64_t* __restrict__ h, const uint8_t* __restrict__ probe_null, int64_t n,
+                                   const uint64_t* __restrict__ keys, int64_t cap_mask,
+                                   const int32_t* __restrict__ cnt, int32_t* __restrict__ slot_out,
+                                   int64_t* __restrict__ out_cnt, int outer) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t s = -1;
+    if (!(probe_null && probe_null[i])) s = find_slot(keys, cap_mask, dxa::fix_key(h[i]));
+    slot_out[i] = (int32_t)s;
+    int64_t c = s >= 0 ? cnt[s] : 0;
+    if (outer && c == 0) c = 1;
+    out_cnt[i] = c;
+  }
+}
+
+__global__ void probe_write_kernel(const int32_t* __restrict__ slot_of_probe, int64_t n,
+                                   const int64_t* __restrict__ out_off, const int64_t* __restrict__ start,
+                                   const int32_t* __restrict__ cnt, const int32_t* __restrict__ rows,
+                                   int64_t* __restrict__ li, int64_t* __restrict__ ri, int outer) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = slot_of_probe[i];
+    int64_t o = out_off[i];
+    const int32_t c = s >= 0 ? cnt[s] : 0;
+    if (c == 0) {
+      if (outer) { li[o] = i; ri[o] = -1; }
+      continue;
+    }
+    const int64_t b = start[s];
+    for (int32_t k = 0; k < c; ++k) {
+      li[o + k] = i;
+      ri[o + k] = rows[b + k];
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------------------------
+DXA_API int dxa_hash_i64(const int64_t* v, const uint8_t* valid, int64_t n, uint64_t* out, int combine, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(hash_i64_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, valid, n, out,
+                     combine);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_hash_f64(const double* v, const uint8_t* valid, int64_t n, uint64_t* out, int combine, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(hash_f64_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, valid, n, out,
+                     combine);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_hash_str(const uint8_t* arena, const int64_t* starts, const int32_t* lens, const uint8_t* valid,
+                         int64_t n, uint64_t* out, int combine, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(hash_str_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     valid, n, out, combine);
+  return (int)hipGetLastError();
+}
+
+// keys: [cap] uint64 (filled with 0xFF by the caller), cap power of two.
+DXA_API int dxa_table_insert(const uint64_t* h, int64_t n, uint64_t* keys, int64_t cap, int32_t* slot_of_row,
+                             void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(table_insert_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, h, n, keys,
+                     cap - 1, slot_of_row);
+  return (int)hipGetLastError();
+}
+
+// counter: [1] int32 zeroed by the caller; rep: [n] int32 filled with INT32_MAX by the caller.
+DXA_API int dxa_group_ids(const uint64_t* keys, int64_t cap, const int32_t* slot_of_row, int64_t n,
+                          int32_t* gid_of_slot, int32_t* counter, int32_t* gid, int32_t* rep, void* st) {
+  hipStream_t s = (hipStream_t)st;
+  hipLaunchKernelGGL(table_number_kernel, dim3(dxa_blocks(cap, 256)), dim3(256), 0, s, keys, cap, gid_of_slot,
+                     counter);
+  if (n > 0)
+    hipLaunchKernelGGL(group_gather_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, s, slot_of_row, gid_of_slot, n,
+                       gid, rep);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_verify_i64(const int64_t* v, const uint8_t* valid, const int32_t* gid, const int32_t* rep, int64_t n,
+                           int32_t* bad, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(verify_i64_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, valid, gid, rep,
+                     n, bad);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_verify_str(const uint8_t* arena, const int64_t* starts, const int32_t* lens, const uint8_t* valid,
+                           const int32_t* gid, const int32_t* rep, int64_t n, int32_t* bad, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(verify_str_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     valid, gid, rep, n, bad);
+  return (int)hipGetLastError();
+}
+
+// op: 0 sum, 1 min, 2 max, 3 count;  vt: 0 int64, 1 double.  out: [ngroups] 8-byte accumulators.
+DXA_API int dxa_aggregate(const int32_t* gid, const void* vals, const uint8_t* valid, int64_t n, int32_t ngroups,
+                          int32_t op, int32_t vt, void* out, void* st) {
+  hipStream_t s = (hipStream_t)st;
+  if (ngroups <= 0) return 0;
+  if (op == AGG_COUNT) return launch_agg<VT_I64, AGG_COUNT>(gid, vals, valid, n, ngroups, out, s);
+  if (vt == VT_I64) {
+    if (op == AGG_SUM) return launch_agg<VT_I64, AGG_SUM>(gid, vals, valid, n, ngroups, out, s);
+    if (op == AGG_MIN) return launch_agg<VT_I64, AGG_MIN>(gid, vals, valid, n, ngroups, out, s);
+    return launch_agg<VT_I64, AGG_MAX>(gid, vals, valid, n, ngroups, out, s);
+  }
+  if (op == AGG_SUM) return launch_agg<VT_F64, AGG_SUM>(gid, vals, valid, n, ngroups, out, s);
+  if (op == AGG_MIN) return launch_agg<VT_F64, AGG_MIN>(gid, vals, valid, n, ngroups, out, s);
+  return launch_agg<VT_F64, AGG_MAX>(gid, vals, valid, n, ngroups, out, s);
+}
+
+DXA_API int dxa_slot_count(const int32_t* slot_of_row, int64_t n, int32_t* cnt, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(slot_count_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, slot_of_row, n, cnt);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_slot_scatter(const int32_t* slot_of_row, int64_t n, const int64_t* start, int32_t* cursor,
+                             int32_t* rows, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(slot_scatter_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, slot_of_row, n,
+                     start, cursor, rows);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_probe_count(const uint64_t* h, const uint8_t* probe_null, int64_t n, const uint64_t* keys, int64_t cap,
+                            const int32_t* cnt, int32_t* slot_out, int64_t* out_cnt, int outer, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(probe_count_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, h, probe_null, n,
+                     keys, cap - 1, cnt, slot_out, out_cnt, outer);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_probe_write(const int32_t* slot_of_probe, int64_t n, const int64_t* out_off, const int64_t* start,
+                            const int32_t* cnt, const int32_t* rows, int64_t* li, int64_t* ri, int outer, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(probe_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, slot_of_probe, n,
+                     out_off, start, cnt, rows, li, ri, outer);
+  return (int)hipGetLastError();
+}

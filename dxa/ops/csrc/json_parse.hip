@@ -1,0 +1,517 @@
+// Schema-directed JSON → columnar parser for gfx950 (kernel K3 in SURVEY.md §2.F).
+//
+// Replaces the reference's per-row `from_json(Raw, rawSchema)` (DataProcessing/datax-host/src/main/scala/datax/
+// processor/CommonProcessorFactory.scala:93).  One lane owns one record: records are 100–800 B, a batch holds
+// 10^5–10^7 of them, so a 256-lane block per 256 records gives thousands of workgroups (≫ 256 CUs × 8 XCDs).
+// Each lane streams its record through a 16-byte register window (one global_load_dwordx4 per 16 chars) and
+// runs a branch-light state machine; keys are FNV-hashed and resolved against a small open-addressed
+// (parent-node, key-hash) lookup table that the compiler keeps in L1/L2.
+//
+// Output is written straight into column slots: 8-byte values (int64 / double bits / timestamp µs), string VIEWS
+// (start offset into the same device buffer + length — the parser never copies string bytes; strings containing
+// escapes are un-escaped in place, which only ever shrinks them), and a validity byte per (node,row).
+//
+// Semantics: missing field / JSON null / type mismatch → null for that field; a syntactically malformed record
+// → every field of the row null and row_ok=0 (the reference is "tolerant to mismatched input schema").
+#include "dxa_common.h"
+
+namespace {
+
+enum : int32_t {
+  FT_STRUCT = 0, FT_BOOL = 1, FT_LONG = 2, FT_DOUBLE = 3, FT_STRING = 4, FT_RAW = 5,
+  FT_TIMESTAMP = 6, FT_INT = 7, FT_DATE = 8,
+};
+
+struct ParseArgs {
+  uint8_t* buf;                 // raw bytes (16-B padded at the end)
+  const int64_t* offs;          // [n+1] record boundaries
+  int64_t n;
+  const uint64_t* lut_keys;     // [lut_cap] 0 = empty
+  const int32_t* lut_node;      // [lut_cap]
+  int32_t lut_cap;
+  const int32_t* node_type;     // [nnodes]
+  const int32_t* val_slot;      // [nnodes] → value row (-1: none)
+  const int32_t* len_slot;      // [nnodes] → length row (-1: none)
+  int32_t nnodes;
+  int64_t* vals;                // [nval][n]
+  int32_t* lens;                // [nlen][n]
+  uint8_t* valid;               // [nnodes][n]  (pre-zeroed)
+  uint8_t* row_ok;              // [n]
+};
+
+__constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+struct Reader {
+  uint8_t* buf;
+  int64_t p, end;
+  uintptr_t wbase;
+  uint4 w;
+
+  __device__ __forceinline__ uint32_t at(int64_t q) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(buf + q);
+    const uintptr_t b = a & ~(uintptr_t)15;
+    if (b != wbase) {
+      wbase = b;
+      w = *reinterpret_cast<const uint4*>(b);
+    }
+    const uint32_t i = (uint32_t)(a - b);
+    const uint32_t d = (i < 8) ? ((i < 4) ? w.x : w.y) : ((i < 12) ? w.z : w.w);
+    return (d >> ((i & 3u) * 8u)) & 0xffu;
+  }
+  __device__ __forceinline__ uint32_t cur() { return p < end ? at(p) : 0u; }
+  __device__ __forceinline__ void skip_ws() {
+    while (p < end) {
+      const uint32_t c = at(p);
+      if (c == ' ' || c == '\n' || c == '\r' || c == '\t') ++p; else break;
+    }
+  }
+};
+
+__device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
+
+// Scan a string whose opening quote is at r.p.  On return r.p is past the closing quote.
+__device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, bool& esc) {
+  ++r.p;
+  s = r.p;
+  esc = false;
+  while (r.p < r.end) {
+    const uint32_t c = r.at(r.p);
+    if (c == '"') { e = r.p; ++r.p; return true; }
+    if (c == '\\') { esc = true; r.p += 2; continue; }
+    ++r.p;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint32_t hexval(uint32_t c) {
+  if (c - '0' < 10u) return c - '0';
+  c |= 0x20u;
+  if (c - 'a' < 6u) return c - 'a' + 10;
+  return 0;
+}
+
+// Un-escape [s,e) in place; returns the decoded length.
+__device__ int64_t unescape_inplace(Reader& r, int64_t s, int64_t e) {
+  uint8_t* b = r.buf;
+  int64_t o = s;
+  int64_t i = s;
+  while (i < e) {
+    uint32_t c = b[i];
+    if (c != '\\') { b[o++] = (uint8_t)c; ++i; continue; }
+    if (i + 1 >= e) break;
+    const uint32_t n = b[i + 1];
+    i += 2;
+    switch (n) {
+      case 'n': b[o++] = '\n'; break;
+      case 't': b[o++] = '\t'; break;
+      case 'r': b[o++] = '\r'; break;
+      case 'b': b[o++] = '\b'; break;
+      case 'f': b[o++] = '\f'; break;
+      case 'u': {
+        if (i + 4 > e) { i = e; break; }
+        uint32_t cp = (hexval(b[i]) << 12) | (hexval(b[i + 1]) << 8) | (hexval(b[i + 2]) << 4) | hexval(b[i + 3]);
+        i += 4;
+        if (cp >= 0xD800 && cp < 0xDC00 && i + 6 <= e && b[i] == '\\' && b[i + 1] == 'u') {
+          const uint32_t lo = (hexval(b[i + 2]) << 12) | (hexval(b[i + 3]) << 8) | (hexval(b[i + 4]) << 4) |
+                              hexval(b[i + 5]);
+          if (lo >= 0xDC00 && lo < 0xE000) {
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            i += 6;
+          }
+        }
+        if (cp < 0x80) {
+          b[o++] = (uint8_t)cp;
+        } else if (cp < 0x800) {
+          b[o++] = (uint8_t)(0xC0 | (cp >> 6));
+          b[o++] = (uint8_t)(0x80 | (cp & 0x3F));
+        } else if (cp < 0x10000) {
+          b[o++] = (uint8_t)(0xE0 | (cp >> 12));
+          b[o++] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+          b[o++] = (uint8_t)(0x80 | (cp & 0x3F));
+        } else {
+          b[o++] = (uint8_t)(0xF0 | (cp >> 18));
+          b[o++] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+          b[o++] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+          b[o++] = (uint8_t)(0x80 | (cp & 0x3F));
+        }
+        break;
+      }
+      default: b[o++] = (uint8_t)n; break;  // \" \\ \/ and unknown
+    }
+  }
+  r.wbase = 0;  // window may cover rewritten bytes
+  return o - s;
+}
+
+// Parse a JSON number at r.p.  Returns false on syntax error.
+__device__ bool scan_number(Reader& r, bool& is_int, bool& overflow, int64_t& iv, double& dv) {
+  bool neg = false;
+  if (r.cur() == '-') { neg = true; ++r.p; }
+  uint64_t mant = 0;
+  int nd = 0, exp10 = 0;
+  bool lost = false, any = false;
+  is_int = true;
+  while (r.p < r.end) {
+    const uint32_t c = r.at(r.p);
+    if (!is_digit(c)) break;
+    any = true;
+    if (nd < 19) { mant = mant * 10 + (c - '0'); if (mant) ++nd; }
+    else { ++exp10; lost = true; }
+    ++r.p;
+  }
+  if (!any) return false;
+  if (r.p < r.end && r.at(r.p) == '.') {
+    is_int = false;
+    ++r.p;
+    bool fd = false;
+    while (r.p < r.end) {
+      const uint32_t c = r.at(r.p);
+      if (!is_digit(c)) break;
+      fd = true;
+      if (nd < 19) { mant = mant * 10 + (c - '0'); if (mant) ++nd; --exp10; }
+      ++r.p;
+    }
+    if (!fd) return false;
+  }
+  if (r.p < r.end && (r.at(r.p) | 0x20u) == 'e') {
+    is_int = false;
+    ++r.p;
+    bool eneg = false;
+    if (r.cur() == '-' || r.cur() == '+') { eneg = r.cur() == '-'; ++r.p; }
+    int e = 0;
+    bool ed = false;
+    while (r.p < r.end && is_digit(r.at(r.p))) {
+      ed = true;
+      if (e < 100000) e = e * 10 + (int)(r.at(r.p) - '0');
+      ++r.p;
+    }
+    if (!ed) return false;
+    exp10 += eneg ? -e : e;
+  }
+  overflow = false;
+  if (is_int) {
+    if (lost) overflow = true;
+    else if (!neg && mant > 9223372036854775807ull) overflow = true;
+    else if (neg && mant > 9223372036854775808ull) overflow = true;
+    iv = neg ? (int64_t)(0ull - mant) : (int64_t)mant;
+  }
+  double d = (double)mant;
+  if (exp10 != 0) {
+    if (mant < (1ull << 53) && exp10 > 0 && exp10 <= 22) d = d * kPow10[exp10];
+    else if (mant < (1ull << 53) && exp10 < 0 && exp10 >= -22) d = d / kPow10[-exp10];
+    else {
+      int e = exp10;
+      while (e > 22) { d *= 1e22; e -= 22; }
+      while (e < -22) { d /= 1e22; e += 22; }
+      d = e >= 0 ? d * kPow10[e] : d / kPow10[-e];
+    }
+  }
+  dv = neg ? -d : d;
+  return true;
+}
+
+// Skip any JSON value at r.p (strings, numbers, literals, nested containers).
+__device__ bool skip_value(Reader& r) {
+  uint32_t c = r.cur();
+  if (c == '"') { int64_t s, e; bool esc; return scan_string(r, s, e, esc); }
+  if (c == '{' || c == '[') {
+    int depth = 0;
+    while (r.p < r.end) {
+      c = r.at(r.p);
+      if (c == '"') { int64_t s, e; bool esc; if (!scan_string(r, s, e, esc)) return false; continue; }
+      if (c == '{' || c == '[') ++depth;
+      else if (c == '}' || c == ']') { if (--depth == 0) { ++r.p; return true; } }
+      ++r.p;
+    }
+    return false;
+  }
+  if (c == '-' || is_digit(c)) {
+    bool ii, of; int64_t iv; double dv;
+    return scan_number(r, ii, of, iv, dv);
+  }
+  if (c == 't' || c == 'n') { r.p += 4; return r.p <= r.end; }
+  if (c == 'f') { r.p += 5; return r.p <= r.end; }
+  return false;
+}
+
+__device__ __forceinline__ int lookup(const ParseArgs& a, int parent, uint64_t name_hash) {
+  uint64_t k = dxa::fmix64(name_hash ^ ((uint64_t)(parent + 1) * dxa::kGold));
+  if (k == 0) k = 1;
+  const uint32_t mask = (uint32_t)a.lut_cap - 1u;
+  uint32_t s = (uint32_t)k & mask;
+  for (int probe = 0; probe < a.lut_cap; ++probe) {
+    const uint64_t kk = a.lut_keys[s];
+    if (kk == k) return a.lut_node[s];
+    if (kk == 0) return -1;
+    s = (s + 1) & mask;
+  }
+  return -1;
+}
+
+// Parse ISO-8601-ish text [s,e): YYYY-MM-DD[(T| )HH:MM[:SS[.ffffff]]][Z|(+|-)HH[:]MM]  → µs since epoch UTC.
+__device__ bool parse_iso_ts(const uint8_t* b, int64_t s, int64_t e, int64_t& out, bool date_only_ok) {
+  auto num = [&](int64_t& i, int digits, int& v) -> bool {
+    v = 0;
+    for (int k = 0; k < digits; ++k) {
+      if (i >= e || !is_digit(b[i])) return false;
+      v = v * 10 + (b[i] - '0');
+      ++i;
+    }
+    return true;
+  };
+  int64_t i = s;
+  int y, mo, d, hh = 0, mi = 0, ss = 0;
+  if (!num(i, 4, y) || i >= e || b[i] != '-') return false;
+  ++i;
+  if (!num(i, 2, mo) || i >= e || b[i] != '-') return false;
+  ++i;
+  if (!num(i, 2, d)) return false;
+  int64_t frac_us = 0;
+  int64_t tz_us = 0;
+  if (i < e && (b[i] == 'T' || b[i] == ' ')) {
+    ++i;
+    if (!num(i, 2, hh) || i >= e || b[i] != ':') return false;
+    ++i;
+    if (!num(i, 2, mi)) return false;
+    if (i < e && b[i] == ':') { ++i; if (!num(i, 2, ss)) return false; }
+    if (i < e && b[i] == '.') {
+      ++i;
+      int64_t scale = 100000;
+      while (i < e && is_digit(b[i])) { frac_us += (b[i] - '0') * scale; scale /= 10; ++i; }
+    }
+    if (i < e && b[i] == 'Z') ++i;
+    else if (i < e && (b[i] == '+' || b[i] == '-')) {
+      const bool neg = b[i] == '-';
+      ++i;
+      int th, tm = 0;
+      if (!num(i, 2, th)) return false;
+      if (i < e && b[i] == ':') ++i;
+      if (i < e) { if (!num(i, 2, tm)) return false; }
+      tz_us = ((int64_t)th * 3600 + tm * 60) * 1000000ll;
+      if (neg) tz_us = -tz_us;
+    }
+  } else if (!date_only_ok) {
+    return false;
+  }
+  if (i != e) return false;
+  if (mo < 1 || mo > 12 || d < 1 || d > 31 || hh > 23 || mi > 59 || ss > 60) return false;
+  const int64_t days = dxa::days_from_civil(y, (unsigned)mo, (unsigned)d);
+  out = ((days * 86400 + hh * 3600 + mi * 60 + ss) * 1000000ll) + frac_us - tz_us;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= a.n) return;
+  const int64_t n = a.n;
+  Reader r;
+  r.buf = a.buf;
+  r.p = a.offs[row];
+  r.end = a.offs[row + 1];
+  r.wbase = 0;
+  r.w = make_uint4(0, 0, 0, 0);
+
+  int stack[16];
+  int depth = 0;
+  bool ok = false;
+
+  r.skip_ws();
+  if (r.cur() != '{') goto done;
+  ++r.p;
+  stack[0] = 0;  // root node
+  depth = 1;
+  a.valid[row] = 1;  // root struct present
+  while (true) {
+    r.skip_ws();
+    uint32_t c = r.cur();
+    if (c == '}') {
+      ++r.p;
+      if (--depth == 0) { ok = true; break; }
+      goto after_value;
+    }
+    if (c != '"') break;
+    {
+      // ---- key
+      ++r.p;
+      uint64_t h = dxa::kFnvBasis;
+      bool closed = false;
+      while (r.p < r.end) {
+        const uint32_t kc = r.at(r.p);
+        if (kc == '"') { ++r.p; closed = true; break; }
+        if (kc == '\\') { h = dxa::fnv1a_step(h, kc); ++r.p; if (r.p < r.end) { h = dxa::fnv1a_step(h, r.at(r.p)); ++r.p; } continue; }
+        h = dxa::fnv1a_step(h, kc);
+        ++r.p;
+      }
+      if (!closed) break;
+      r.skip_ws();
+      if (r.cur() != ':') break;
+      ++r.p;
+      r.skip_ws();
+      const int node = lookup(a, stack[depth - 1], h);
+      c = r.cur();
+      if (node < 0) {
+        if (!skip_value(r)) break;
+        goto after_value;
+      }
+      const int t = a.node_type[node];
+      const int vs = a.val_slot[node];
+      const int ls = a.len_slot[node];
+      if (c == '{' && t == FT_STRUCT) {
+        if (depth >= 16) { if (!skip_value(r)) break; goto after_value; }
+        a.valid[(int64_t)node * n + row] = 1;
+        stack[depth++] = node;
+        ++r.p;
+        continue;
+      }
+      if (c == '{' || c == '[') {
+        const int64_t s = r.p;
+        if (!skip_value(r)) break;
+        if ((t == FT_STRING || t == FT_RAW) && ls >= 0) {
+          a.vals[(int64_t)vs * n + row] = s;
+          a.lens[(int64_t)ls * n + row] = (int32_t)(r.p - s);
+          a.valid[(int64_t)node * n + row] = 1;
+        }
+        goto after_value;
+      }
+      if (c == '"') {
+        int64_t s, e;
+        bool esc;
+        if (!scan_string(r, s, e, esc)) break;
+        if (t == FT_STRING) {
+          const int64_t len = esc ? unescape_inplace(r, s, e) : (e - s);
+          a.vals[(int64_t)vs * n + row] = s;
+          a.lens[(int64_t)ls * n + row] = (int32_t)len;
+          a.valid[(int64_t)node * n + row] = 1;
+        } else if (t == FT_TIMESTAMP || t == FT_DATE) {
+          int64_t us;
+          if (parse_iso_ts(a.buf, s, e, us, true)) {
+            a.vals[(int64_t)vs * n + row] = (t == FT_DATE) ? (us >= 0 ? us / 86400000000ll
+                                                                     : -((-us + 86399999999ll) / 86400000000ll))
+                                                           : us;
+            a.valid[(int64_t)node * n + row] = 1;
+          }
+        }
+        goto after_value;
+      }
+      if (c == '-' || is_digit(c)) {
+        const int64_t s = r.p;
+        bool is_int, of;
+        int64_t iv = 0;
+        double dv = 0.0;
+        if (!scan_number(r, is_int, of, iv, dv)) break;
+        if (t == FT_LONG || t == FT_INT) {
+          if (is_int && !of && (t == FT_LONG || (iv >= -2147483648ll && iv <= 2147483647ll))) {
+            a.vals[(int64_t)vs * n + row] = iv;
+            a.valid[(int64_t)node * n + row] = 1;
+          }
+        } else if (t == FT_DOUBLE) {
+          a.vals[(int64_t)vs * n + row] = __double_as_longlong(dv);
+          a.valid[(int64_t)node * n + row] = 1;
+        } else if (t == FT_TIMESTAMP) {
+          if (is_int && !of) {
+            a.vals[(int64_t)vs * n + row] = iv * 1000000ll;
+            a.valid[(int64_t)node * n + row] = 1;
+          }
+        } else if (t == FT_STRING) {
+          a.vals[(int64_t)vs * n + row] = s;
+          a.lens[(int64_t)ls * n + row] = (int32_t)(r.p - s);
+          a.valid[(int64_t)node * n + row] = 1;
+        }
+        goto after_value;
+      }
+      if (c == 't' || c == 'f') {
+        const int64_t s = r.p;
+        const bool v = (c == 't');
+        r.p += v ? 4 : 5;
+        if (r.p > r.end) break;
+        if (t == FT_BOOL) {
+          a.vals[(int64_t)vs * n + row] = v ? 1 : 0;
+          a.valid[(int64_t)node * n + row] = 1;
+        } else if (t == FT_STRING) {
+          a.vals[(int64_t)vs * n + row] = s;
+          a.lens[(int64_t)ls * n + row] = v ? 4 : 5;
+          a.valid[(int64_t)node * n + row] = 1;
+        }
+        goto after_value;
+      }
+      if (c == 'n') {
+        r.p += 4;
+        if (r.p > r.end) break;
+        goto after_value;
+      }
+      break;  // unexpected token
+    }
+  after_value:
+    r.skip_ws();
+    c = r.cur();
+    if (c == ',') { ++r.p; continue; }
+    if (c == '}') continue;  // closes the current object at loop top
+    break;
+  }
+done:
+  a.row_ok[row] = ok ? 1 : 0;
+  if (!ok) {
+    for (int k = 0; k < a.nnodes; ++k) a.valid[(int64_t)k * n + row] = 0;
+  }
+}
+
+// Newline framing: offsets of '\n'-terminated records in a raw byte stream (blob / socket sources).
+__global__ void count_newlines_kernel(const uint8_t* __restrict__ buf, int64_t len, int64_t chunk,
+                                      int64_t* __restrict__ counts) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = c * chunk;
+  if (s >= len) return;
+  const int64_t e = s + chunk < len ? s + chunk : len;
+  int64_t k = 0;
+  for (int64_t i = s; i < e; ++i) k += buf[i] == '\n';
+  counts[c] = k;
+}
+
+__global__ void write_newlines_kernel(const uint8_t* __restrict__ buf, int64_t len, int64_t chunk,
+                                      const int64_t* __restrict__ base, int64_t* __restrict__ pos) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = c * chunk;
+  if (s >= len) return;
+  const int64_t e = s + chunk < len ? s + chunk : len;
+  int64_t k = base[c];
+  for (int64_t i = s; i < e; ++i)
+    if (buf[i] == '\n') pos[k++] = i;
+}
+
+}  // namespace
+
+DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const uint64_t* lut_keys,
+                           const int32_t* lut_node, int32_t lut_cap, const int32_t* node_type,
+                           const int32_t* val_slot, const int32_t* len_slot, int32_t nnodes, int64_t* vals,
+                           int32_t* lens, uint8_t* valid, uint8_t* row_ok, void* stream) {
+  if (n <= 0) return 0;
+  ParseArgs a{buf, offs, n, lut_keys, lut_node, lut_cap, node_type, val_slot, len_slot, nnodes, vals, lens,
+              valid, row_ok};
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(valid, 0, (size_t)nnodes * (size_t)n, s);
+  if (e != hipSuccess) return (int)e;
+  const int block = 256;
+  const int64_t grid = (n + block - 1) / block;
+  hipLaunchKernelGGL(json_parse_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_count_newlines(const uint8_t* buf, int64_t len, int64_t chunk, int64_t* counts, void* stream) {
+  if (len <= 0) return 0;
+  const int64_t nchunks = (len + chunk - 1) / chunk;
+  const int block = 256;
+  hipLaunchKernelGGL(count_newlines_kernel, dim3((unsigned)((nchunks + block - 1) / block)), dim3(block), 0,
+                     (hipStream_t)stream, buf, len, chunk, counts);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_write_newlines(const uint8_t* buf, int64_t len, int64_t chunk, const int64_t* base, int64_t* pos,
+                               void* stream) {
+  if (len <= 0) return 0;
+  const int64_t nchunks = (len + chunk - 1) / chunk;
+  const int block = 256;
+  hipLaunchKernelGGL(write_newlines_kernel, dim3((unsigned)((nchunks + block - 1) / block)), dim3(block), 0,
+                     (hipStream_t)stream, buf, len, chunk, base, pos);
+  return (int)hipGetLastError();
+}

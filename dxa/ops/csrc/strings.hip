@@ -1,0 +1,316 @@
+// String-column kernels for gfx950: predicates against literals, byte gathers (compaction / concat),
+// CONCAT of views and literals, integer formatting, case mapping and the DataX `stringToTimestamp` UDF
+// (reference: DataProcessing/datax-utility/src/main/scala/datax/utility/ConcurrentDateFormat.scala:14-62).
+//
+// Strings are views (start, len) into a byte arena; producing kernels are two-pass (length, then exclusive scan
+// on the stream, then write), so no kernel ever needs dynamic allocation.
+#include "dxa_common.h"
+
+namespace {
+
+// op: 0 ==, 1 !=, 2 <, 3 <=, 4 >, 5 >= (byte-wise lexicographic, i.e. UTF-8 code-point order), 6 startsWith,
+//     7 endsWith, 8 contains
+__global__ void str_cmp_lit_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                   const int32_t* __restrict__ lens, int64_t n, const uint8_t* __restrict__ lit,
+                                   int32_t lit_len, int32_t op, uint8_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    bool r = false;
+    if (op <= 5) {
+      if (op <= 1 && l != lit_len) {
+        r = (op == 1);
+      } else {
+        const int32_t m = l < lit_len ? l : lit_len;
+        int c = 0;
+        for (int32_t k = 0; k < m; ++k) {
+          if (s[k] != lit[k]) { c = (int)s[k] - (int)lit[k]; break; }
+        }
+        if (c == 0) c = (l > lit_len) - (l < lit_len);
+        switch (op) {
+          case 0: r = c == 0; break;
+          case 1: r = c != 0; break;
+          case 2: r = c < 0; break;
+          case 3: r = c <= 0; break;
+          case 4: r = c > 0; break;
+          default: r = c >= 0; break;
+        }
+      }
+    } else if (op == 6 || op == 7) {
+      if (l >= lit_len) {
+        const uint8_t* b = op == 6 ? s : s + (l - lit_len);
+        r = true;
+        for (int32_t k = 0; k < lit_len; ++k)
+          if (b[k] != lit[k]) { r = false; break; }
+      }
+    } else {
+      for (int32_t st = 0; st + lit_len <= l && !r; ++st) {
+        bool m = true;
+        for (int32_t k = 0; k < lit_len; ++k)
+          if (s[st + k] != lit[k]) { m = false; break; }
+        r = m;
+      }
+    }
+    out[i] = r ? 1 : 0;
+  }
+}
+
+// Column-vs-column equality (join residuals, string = string predicates).
+__global__ void str_eq_col_kernel(const uint8_t* __restrict__ aa, const int64_t* __restrict__ as,
+                                  const int32_t* __restrict__ al, const uint8_t* __restrict__ ba,
+                                  const int64_t* __restrict__ bs, const int32_t* __restrict__ bl, int64_t n,
+                                  uint8_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = al[i];
+    bool r = l == bl[i];
+    if (r) {
+      const uint8_t* a = aa + as[i];
+      const uint8_t* b = ba + bs[i];
+      for (int32_t k = 0; k < l; ++k)
+        if (a[k] != b[k]) { r = false; break; }
+    }
+    out[i] = r;
+  }
+}
+
+// Copy each view's bytes to dst + dst_off[i] (compaction / concat of arenas).
+__global__ void str_gather_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                  const int32_t* __restrict__ lens, int64_t n, const int64_t* __restrict__ dst_off,
+                                  uint8_t* __restrict__ dst) {
+  // one wave per string keeps copies coalesced for long strings and lanes busy for short ones
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const uint8_t* s = arena + starts[i];
+    uint8_t* d = dst + dst_off[i];
+    const int32_t l = lens[i];
+    for (int32_t k = lane; k < l; k += 64) d[k] = s[k];
+  }
+}
+
+// CONCAT(part_0, …, part_{k-1}); each part is either a column view or a literal.  Null in any column part → null.
+struct ConcatPart {
+  const uint8_t* arena;
+  const int64_t* starts;
+  const int32_t* lens;
+  const uint8_t* valid;
+  const uint8_t* lit;
+  int32_t lit_len;
+  int32_t is_lit;
+};
+
+__global__ void concat_len_kernel(const ConcatPart* __restrict__ parts, int32_t k, int64_t n,
+                                  int64_t* __restrict__ out_len, uint8_t* __restrict__ out_valid) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t l = 0;
+    bool ok = true;
+    for (int32_t p = 0; p < k; ++p) {
+      const ConcatPart& c = parts[p];
+      if (c.is_lit) { l += c.lit_len; continue; }
+      if (c.valid && !c.valid[i]) ok = false;
+      l += c.lens[i];
+    }
+    out_len[i] = ok ? l : 0;
+    out_valid[i] = ok;
+  }
+}
+
+__global__ void concat_write_kernel(const ConcatPart* __restrict__ parts, int32_t k, int64_t n,
+                                    const int64_t* __restrict__ off, const uint8_t* __restrict__ ok,
+                                    uint8_t* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!ok[i]) continue;
+    uint8_t* d = dst + off[i];
+    for (int32_t p = 0; p < k; ++p) {
+      const ConcatPart& c = parts[p];
+      const uint8_t* s = c.is_lit ? c.lit : c.arena + c.starts[i];
+      const int32_t l = c.is_lit ? c.lit_len : c.lens[i];
+      for (int32_t q = 0; q < l; ++q) d[q] = s[q];
+      d += l;
+    }
+  }
+}
+
+__device__ __forceinline__ int i64_digits(int64_t v) {
+  uint64_t u = v < 0 ? (0ull - (uint64_t)v) : (uint64_t)v;
+  int d = 1;
+  while (u >= 10) { u /= 10; ++d; }
+  return d + (v < 0);
+}
+
+__global__ void i64_len_kernel(const int64_t* __restrict__ v, int64_t n, int64_t* __restrict__ out_len) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out_len[i] = i64_digits(v[i]);
+}
+
+__global__ void i64_write_kernel(const int64_t* __restrict__ v, int64_t n, const int64_t* __restrict__ off,
+                                 uint8_t* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = v[i];
+    const int nd = i64_digits(x);
+    uint8_t* d = dst + off[i];
+    uint64_t u = x < 0 ? (0ull - (uint64_t)x) : (uint64_t)x;
+    int p = nd - 1;
+    do { d[p--] = (uint8_t)('0' + u % 10); u /= 10; } while (u);
+    if (x < 0) d[0] = '-';
+  }
+}
+
+// mode 0: lower, 1: upper (ASCII; bytes ≥ 0x80 untouched, matching Spark for ASCII data)
+__global__ void case_map_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                const int32_t* __restrict__ lens, int64_t n, const int64_t* __restrict__ off,
+                                uint8_t* __restrict__ dst, int mode) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    uint8_t* d = dst + off[i];
+    const int32_t l = lens[i];
+    for (int32_t k = 0; k < l; ++k) {
+      uint8_t c = s[k];
+      if (mode == 0 && c >= 'A' && c <= 'Z') c += 32;
+      if (mode == 1 && c >= 'a' && c <= 'z') c -= 32;
+      d[k] = c;
+    }
+  }
+}
+
+__device__ __forceinline__ bool dig(uint8_t c) { return (unsigned)(c - '0') < 10u; }
+
+__device__ bool rd(const uint8_t* s, int32_t l, int32_t& i, int minD, int maxD, int& v) {
+  v = 0;
+  int k = 0;
+  while (i < l && k < maxD && dig(s[i])) { v = v * 10 + (s[i] - '0'); ++i; ++k; }
+  return k >= minD;
+}
+
+// stringToTimestamp: java.sql.Timestamp.valueOf ("yyyy-[m]m-[d]d hh:mm:ss[.f…]"), then
+// "yyyy-MM-dd'T'HH:mm:ss'Z'", then "MM/dd/yyyy HH:mm:ss"; anything else → null.  Times are UTC.
+__global__ void str_to_ts_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                 const int32_t* __restrict__ lens, const uint8_t* __restrict__ valid, int64_t n,
+                                 int64_t* __restrict__ out, uint8_t* __restrict__ out_valid) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    bool ok = !(valid && !valid[r]);
+    const uint8_t* s = arena + starts[r];
+    const int32_t l = lens[r];
+    int y = 0, mo = 0, d = 0, hh = 0, mi = 0, ss = 0;
+    int64_t frac = 0;
+    if (ok) {
+      ok = false;
+      int32_t i = 0;
+      // form A / B: yyyy-M-d( |T)HH:mm:ss[.f][Z]
+      if (rd(s, l, i, 4, 4, y) && i < l && s[i] == '-') {
+        ++i;
+        if (rd(s, l, i, 1, 2, mo) && i < l && s[i] == '-') {
+          ++i;
+          if (rd(s, l, i, 1, 2, d) && i < l && (s[i] == ' ' || s[i] == 'T')) {
+            const bool iso = s[i] == 'T';
+            ++i;
+            if (rd(s, l, i, 1, 2, hh) && i < l && s[i] == ':' && (++i, rd(s, l, i, 1, 2, mi)) && i < l &&
+                s[i] == ':' && (++i, rd(s, l, i, 1, 2, ss))) {
+              if (!iso && i < l && s[i] == '.') {
+                ++i;
+                int64_t scale = 100000;
+                int nd = 0;
+                while (i < l && dig(s[i])) { if (scale) { frac += (s[i] - '0') * scale; scale /= 10; } ++i; ++nd; }
+                ok = nd > 0 && i == l;
+              } else if (iso) {
+                ok = (i + 1 == l && s[i] == 'Z');
+              } else {
+                ok = i == l;
+              }
+            }
+          }
+        }
+      }
+      if (!ok) {
+        // form C: MM/dd/yyyy HH:mm:ss
+        i = 0;
+        frac = 0;
+        if (rd(s, l, i, 1, 2, mo) && i < l && s[i] == '/' && (++i, rd(s, l, i, 1, 2, d)) && i < l && s[i] == '/' &&
+            (++i, rd(s, l, i, 4, 4, y)) && i < l && s[i] == ' ' && (++i, rd(s, l, i, 1, 2, hh)) && i < l &&
+            s[i] == ':' && (++i, rd(s, l, i, 1, 2, mi)) && i < l && s[i] == ':' && (++i, rd(s, l, i, 1, 2, ss)))
+          ok = i == l;
+      }
+      if (ok && (mo < 1 || mo > 12 || d < 1 || d > 31 || hh > 23 || mi > 59 || ss > 59)) ok = false;
+    }
+    if (ok) {
+      const int64_t days = dxa::days_from_civil(y, (unsigned)mo, (unsigned)d);
+      out[r] = (days * 86400 + hh * 3600 + mi * 60 + ss) * 1000000ll + frac;
+    } else {
+      out[r] = 0;
+    }
+    out_valid[r] = ok;
+  }
+}
+
+}  // namespace
+
+DXA_API int dxa_str_cmp_lit(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                            const uint8_t* lit, int32_t lit_len, int32_t op, uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_cmp_lit_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     n, lit, lit_len, op, out);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_eq_col(const uint8_t* aa, const int64_t* as, const int32_t* al, const uint8_t* ba,
+                           const int64_t* bs, const int32_t* bl, int64_t n, uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_eq_col_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, aa, as, al, ba, bs,
+                     bl, n, out);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_gather(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                           const int64_t* dst_off, uint8_t* dst, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_gather_kernel, dim3(dxa_blocks(n * 64, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
+                     lens, n, dst_off, dst);
+  return (int)hipGetLastError();
+}
+
+// parts: device array of ConcatPart (k entries) prepared by the host.
+DXA_API int dxa_concat_len(const void* parts, int32_t k, int64_t n, int64_t* out_len, uint8_t* out_valid, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(concat_len_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st,
+                     (const ConcatPart*)parts, k, n, out_len, out_valid);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_concat_write(const void* parts, int32_t k, int64_t n, const int64_t* off, const uint8_t* ok,
+                             uint8_t* dst, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(concat_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st,
+                     (const ConcatPart*)parts, k, n, off, ok, dst);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_concat_part_size() { return (int)sizeof(ConcatPart); }
+
+DXA_API int dxa_i64_to_str_len(const int64_t* v, int64_t n, int64_t* out_len, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(i64_len_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, n, out_len);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_i64_to_str_write(const int64_t* v, int64_t n, const int64_t* off, uint8_t* dst, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(i64_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, n, off, dst);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_case_map(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                         const int64_t* off, uint8_t* dst, int mode, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(case_map_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens, n,
+                     off, dst, mode);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_to_ts(const uint8_t* arena, const int64_t* starts, const int32_t* lens, const uint8_t* valid,
+                          int64_t n, int64_t* out, uint8_t* out_valid, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_to_ts_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     valid, n, out, out_valid);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,233 @@
+"""Hash group-by: row → dense group id, representative rows, and per-group aggregates.
+
+GPU path (hash_groupby.hip): hash → CAS-insert into an open-addressed HBM table → dense ids → LDS-privatised
+aggregation.  Group ids are renumbered by first appearance (representative = minimum row index) so results are
+deterministic and identical to the CPU reference.  Key equality is *verified* against each group's representative
+row after hashing; a 64-bit collision (never observed, but possible) switches that call to an exact host-side
+grouping instead of merging distinct keys.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from . import native as N
+from .hashing import hash_columns
+
+INT32_MAX = 2**31 - 1
+
+
+@dataclass
+class Groups:
+    gid: torch.Tensor        # [n] group id per row (int32 on GPU, int64 on CPU)
+    ngroups: int
+    rep: torch.Tensor        # [ngroups] int64 representative (first) row per group
+
+
+def _next_pow2(x: int) -> int:
+    return 1 << max(6, math.ceil(math.log2(max(1, x))))
+
+
+def _on_gpu(device) -> bool:
+    return torch.device(device).type == "cuda"
+
+
+def group_rows(keys: List) -> Groups:
+    from ..engine.column import materialize, PrimColumn, StrColumn, ConstColumn
+    n = keys[0].length
+    device = keys[0].device
+    if n == 0:
+        return Groups(torch.empty(0, dtype=torch.int64, device=device), 0,
+                      torch.empty(0, dtype=torch.int64, device=device))
+    # constant keys do not partition anything
+    keys = [k for k in keys if not (isinstance(k, ConstColumn))]
+    if not keys:
+        return Groups(torch.zeros(n, dtype=torch.int64, device=device), 1,
+                      torch.zeros(1, dtype=torch.int64, device=device))
+    keys = [materialize(k) for k in keys]
+    h = hash_columns(keys)
+    if _on_gpu(device):
+        st = N.stream_handle(device)
+        cap = _next_pow2(2 * n)
+        table = torch.full((cap,), -1, dtype=torch.int64, device=device)
+        slot = torch.empty(n, dtype=torch.int32, device=device)
+        N.call("dxa_table_insert", N.ptr(h), n, N.ptr(table), cap, N.ptr(slot), st)
+        gid_of_slot = torch.empty(cap, dtype=torch.int32, device=device)
+        scal = torch.zeros(2, dtype=torch.int32, device=device)   # [ngroups, bad]
+        gid = torch.empty(n, dtype=torch.int32, device=device)
+        rep = torch.full((n,), INT32_MAX, dtype=torch.int32, device=device)
+        N.call("dxa_group_ids", N.ptr(table), cap, N.ptr(slot), n, N.ptr(gid_of_slot), N.ptr(scal), N.ptr(gid),
+               N.ptr(rep), st)
+        bad_ptr = scal.data_ptr() + 4
+        for k in keys:
+            if isinstance(k, StrColumn):
+                N.call("dxa_verify_str", N.ptr(k.arena), N.ptr(k.starts), N.ptr(k.lens), N.ptr(N.u8(k.valid)),
+                       N.ptr(gid), N.ptr(rep), n, bad_ptr, st)
+            else:
+                d = k.data
+                if d.dtype != torch.int64:
+                    d = d.view(torch.int64) if d.dtype == torch.float64 else d.to(torch.int64)
+                N.call("dxa_verify_i64", N.ptr(d), N.ptr(N.u8(k.valid)), N.ptr(gid), N.ptr(rep), n, bad_ptr, st)
+        ng, bad = scal.tolist()
+        if bad:
+            return _exact_groups(keys, device)
+        rep = rep[:ng].to(torch.int64)
+        order = torch.argsort(rep)
+        inv = torch.empty(ng, dtype=torch.int32, device=device)
+        inv[order] = torch.arange(ng, dtype=torch.int32, device=device)
+        gid = inv[gid.long()]
+        return Groups(gid, ng, rep[order])
+    # ---- CPU reference
+    uniq, inv = torch.unique(h, return_inverse=True)
+    ng = int(uniq.shape[0])
+    rows = torch.arange(n, dtype=torch.int64, device=device)
+    rep = torch.full((ng,), n, dtype=torch.int64, device=device).scatter_reduce(0, inv, rows, "amin")
+    order = torch.argsort(rep)
+    remap = torch.empty(ng, dtype=torch.int64, device=device)
+    remap[order] = torch.arange(ng, dtype=torch.int64, device=device)
+    gid = remap[inv]
+    rep = rep[order]
+    # verify exact equality against representatives
+    for k in keys:
+        vals = k.to_pylist()
+        rp = rep.tolist()
+        g = gid.tolist()
+        for i in range(n):
+            if vals[i] != vals[rp[g[i]]]:
+                return _exact_groups(keys, device)
+    return Groups(gid, ng, rep)
+
+
+def _exact_groups(keys, device) -> Groups:
+    cols = [k.to_pylist() for k in keys]
+    n = keys[0].length
+    seen = {}
+    gid = []
+    rep = []
+    for i in range(n):
+        t = tuple(c[i] for c in cols)
+        g = seen.get(t)
+        if g is None:
+            g = seen[t] = len(rep)
+            rep.append(i)
+        gid.append(g)
+    dt = torch.int32 if _on_gpu(device) else torch.int64
+    return Groups(torch.tensor(gid, dtype=dt, device=device), len(rep),
+                  torch.tensor(rep, dtype=torch.int64, device=device))
+
+
+_OPS = {"sum": 0, "min": 1, "max": 2, "count": 3}
+
+
+def _agg_raw(groups: Groups, data: Optional[torch.Tensor], valid: Optional[torch.Tensor], op: str,
+             n: int, device) -> torch.Tensor:
+    """One accumulator per group.  data: int64 or float64 tensor (None for COUNT(*))."""
+    ng = groups.ngroups
+    if _on_gpu(device):
+        out = torch.empty(ng, dtype=torch.float64 if (data is not None and data.dtype == torch.float64 and
+                                                      op != "count") else torch.int64, device=device)
+        gid = groups.gid if groups.gid.dtype == torch.int32 else groups.gid.to(torch.int32)
+        vt = 1 if (data is not None and data.dtype == torch.float64) else 0
+        N.call("dxa_aggregate", N.ptr(gid), N.ptr(data), N.ptr(N.u8(valid)), n, ng, _OPS[op], vt, N.ptr(out),
+               N.stream_handle(device))
+        return out
+    gid = groups.gid.to(torch.int64)
+    if valid is not None:
+        keep = valid
+        gid = gid[keep]
+        if data is not None:
+            data = data[keep]
+    if op == "count":
+        return torch.zeros(ng, dtype=torch.int64, device=device).scatter_add_(
+            0, gid, torch.ones_like(gid))
+    if op == "sum":
+        return torch.zeros(ng, dtype=data.dtype, device=device).scatter_add_(0, gid, data)
+    if op == "min":
+        init = torch.full((ng,), float("inf") if data.dtype == torch.float64 else 2**63 - 1, dtype=data.dtype,
+                          device=device)
+        return init.scatter_reduce(0, gid, data, "amin")
+    if op == "max":
+        init = torch.full((ng,), float("-inf") if data.dtype == torch.float64 else -2**63, dtype=data.dtype,
+                          device=device)
+        return init.scatter_reduce(0, gid, data, "amax")
+    raise ValueError(op)
+
+
+def aggregate(groups: Groups, col, func: str, n: int):
+    """Apply one aggregate over the grouped rows.  ``col`` is None for COUNT(*).  Returns a Column of ngroups rows.
+
+    func: count | count_star | sum | min | max | avg | first | last | stddev(_samp|_pop) | var(_samp|_pop)
+    """
+    from ..engine.column import PrimColumn, StrColumn, ConstColumn, materialize, column_from_pylist
+    device = groups.rep.device
+    ng = groups.ngroups
+    if func == "count_star":
+        return PrimColumn("long", _agg_raw(groups, None, None, "count", n, device))
+    col = materialize(col)
+    valid = col.valid
+    if func == "count":
+        return PrimColumn("long", _agg_raw(groups, None, valid, "count", n, device))
+    if func in ("first", "last"):
+        if func == "first":
+            idx = groups.rep
+        else:
+            rows = torch.arange(n, dtype=torch.int64, device=device)
+            idx = torch.full((ng,), -1, dtype=torch.int64, device=device).scatter_reduce(
+                0, groups.gid.to(torch.int64), rows, "amax")
+        return col.take(idx)
+    if isinstance(col, StrColumn) or not isinstance(col, PrimColumn):
+        if func in ("min", "max"):
+            return _host_minmax(groups, col, func, device)
+        raise TypeError(f"{func} over {col.dtype} is not supported")
+    dt = col.dtype
+    data = col.data
+    if data.dtype == torch.bool:
+        data = data.to(torch.int64)
+    cnt = None
+    if valid is not None:
+        cnt = _agg_raw(groups, None, valid, "count", n, device)
+    if func == "sum":
+        out = _agg_raw(groups, data, valid, "sum", n, device)
+        rdt = "double" if data.dtype == torch.float64 else "long"
+        return PrimColumn(rdt, out, None if cnt is None else cnt > 0)
+    if func in ("min", "max"):
+        out = _agg_raw(groups, data, valid, func, n, device)
+        if col.dtype == "boolean":
+            out = out.to(torch.bool)
+        return PrimColumn(dt, out, None if cnt is None else cnt > 0)
+    if func in ("avg", "mean"):
+        s = _agg_raw(groups, data.to(torch.float64) if data.dtype != torch.float64 else data, valid, "sum", n, device)
+        c = cnt if cnt is not None else _agg_raw(groups, None, None, "count", n, device)
+        return PrimColumn("double", s / c.clamp(min=1).to(torch.float64), c > 0)
+    if func in ("stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std"):
+        x = data.to(torch.float64)
+        s = _agg_raw(groups, x, valid, "sum", n, device)
+        s2 = _agg_raw(groups, x * x, valid, "sum", n, device)
+        c = (cnt if cnt is not None else _agg_raw(groups, None, None, "count", n, device)).to(torch.float64)
+        mean = s / c.clamp(min=1)
+        m2 = (s2 - c * mean * mean).clamp(min=0)
+        pop = func.endswith("_pop")
+        denom = c if pop else (c - 1)
+        var = m2 / denom.clamp(min=1)
+        out = var.sqrt() if func.startswith("std") else var
+        ok = c > (0 if pop else 1)
+        return PrimColumn("double", out, ok)
+    raise ValueError(f"unsupported aggregate {func}")
+
+
+def _host_minmax(groups, col, func, device):
+    """MIN/MAX over strings (and other non-numeric types): host-assisted, rarely on a hot path."""
+    from ..engine.column import column_from_pylist
+    vals = col.to_pylist()
+    gid = groups.gid.cpu().tolist()
+    best = [None] * groups.ngroups
+    for v, g in zip(vals, gid):
+        if v is None:
+            continue
+        b = best[g]
+        if b is None or (v < b if func == "min" else v > b):
+            best[g] = v
+    return column_from_pylist(best, col.dtype, device)

@@ -1,0 +1,118 @@
+"""Row hashing of key columns (group-by / join / distinct / shuffle partitioning).
+
+GPU: ``dxa_hash_{i64,f64,str}`` kernels (hash_groupby.hip).  CPU: a bit-exact numpy re-implementation of the same
+functions so GPU results can be differential-tested against it.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+import torch
+
+from . import native as N
+
+SEED = np.uint64(0x5bd1e9955bd1e995)
+GOLD = np.uint64(0x9E3779B97F4A7C15)
+NULL_HASH = np.uint64(0x6e756c6c6e756c6c)
+C1 = np.uint64(0xff51afd7ed558ccd)
+C2 = np.uint64(0xc4ceb9fe1a85ec53)
+
+
+def _fmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(33))
+        x = x * C1
+        x = x ^ (x >> np.uint64(33))
+        x = x * C2
+        x = x ^ (x >> np.uint64(33))
+    return x
+
+
+def _hash_i64_np(v: np.ndarray) -> np.ndarray:
+    return _fmix64(v.astype(np.int64).view(np.uint64) ^ SEED)
+
+
+def _combine_np(acc: np.ndarray, h: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        return _fmix64(acc ^ (h + GOLD + (acc << np.uint64(6)) + (acc >> np.uint64(2))))
+
+
+def _hash_bytes_np(b: bytes) -> np.uint64:
+    n = len(b)
+    with np.errstate(over="ignore"):
+        h = SEED ^ (np.uint64(n) * GOLD)
+        i = 0
+        while i + 8 <= n:
+            w = np.uint64(int.from_bytes(b[i:i + 8], "little"))
+            h = _fmix64(np.array([h ^ w], dtype=np.uint64))[0]
+            i += 8
+        if i < n:
+            w = np.uint64(int.from_bytes(b[i:], "little"))
+            h = _fmix64(np.array([h ^ w], dtype=np.uint64))[0]
+        return _fmix64(np.array([h ^ np.uint64(n)], dtype=np.uint64))[0]
+
+
+def _col_hash_np(col) -> np.ndarray:
+    from ..engine.column import PrimColumn, StrColumn, ConstColumn, materialize
+    col = materialize(col)
+    n = col.length
+    if isinstance(col, StrColumn):
+        arena = col.arena.cpu().numpy().tobytes()
+        starts = col.starts.cpu().numpy()
+        lens = col.lens.cpu().numpy()
+        out = np.empty(n, dtype=np.uint64)
+        for i in range(n):
+            s = int(starts[i])
+            out[i] = _hash_bytes_np(arena[s:s + int(lens[i])])
+    elif isinstance(col, PrimColumn):
+        d = col.data.cpu()
+        if d.dtype == torch.float64:
+            a = d.numpy().copy()
+            a[a == 0.0] = 0.0
+            bits = a.view(np.uint64).copy()
+            bits[np.isnan(a)] = np.uint64(0x7ff8000000000000)
+            out = _fmix64(bits ^ SEED)
+        else:
+            out = _hash_i64_np(d.to(torch.int64).numpy())
+    else:
+        raise TypeError(f"cannot hash column {col!r}")
+    if col.valid is not None:
+        v = col.valid.cpu().numpy()
+        out = np.where(v, out, NULL_HASH)
+    return out
+
+
+def hash_columns(cols: List) -> torch.Tensor:
+    """64-bit row hash over one or more key columns → int64 tensor (bit pattern of the uint64 hash)."""
+    from ..engine.column import PrimColumn, StrColumn, materialize
+    assert cols
+    n = cols[0].length
+    device = cols[0].device
+    if torch.device(device).type == "cuda":
+        out = torch.empty(n, dtype=torch.int64, device=device)
+        if n == 0:
+            return out
+        st = N.stream_handle(device)
+        for j, c in enumerate(cols):
+            c = materialize(c)
+            comb = 1 if j else 0
+            if isinstance(c, StrColumn):
+                N.call("dxa_hash_str", N.ptr(c.arena), N.ptr(c.starts), N.ptr(c.lens), N.ptr(N.u8(c.valid)), n,
+                       N.ptr(out), comb, st)
+            elif isinstance(c, PrimColumn):
+                d = c.data
+                if d.dtype == torch.float64:
+                    N.call("dxa_hash_f64", N.ptr(d), N.ptr(N.u8(c.valid)), n, N.ptr(out), comb, st)
+                else:
+                    if d.dtype != torch.int64:
+                        d = d.to(torch.int64)
+                    N.call("dxa_hash_i64", N.ptr(d), N.ptr(N.u8(c.valid)), n, N.ptr(out), comb, st)
+            else:
+                raise TypeError(f"cannot hash column {c!r}")
+        return out
+    acc = None
+    for c in cols:
+        h = _col_hash_np(c)
+        acc = h if acc is None else _combine_np(acc, h)
+    return torch.from_numpy(acc.view(np.int64).copy()).to(device)

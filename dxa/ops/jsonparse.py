@@ -1,0 +1,328 @@
+"""Schema-directed JSON parsing of a batch of raw events into a nested ``StructColumn`` (the reference's
+``from_json(Raw, rawSchema)``, DataProcessing/datax-host/src/main/scala/datax/processor/CommonProcessorFactory.scala:93).
+
+A ``ParsePlan`` flattens the Spark schema into nodes (structs and leaves) and an open-addressed
+(parent, FNV-1a(key)) lookup table consumed by the ``dxa_json_parse`` kernel.  Leaves can be pruned: fields no query
+references are left out of the table, so the kernel skips their values without writing a column.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Set, Tuple
+
+import numpy as np
+import torch
+
+from . import native as N
+from ..engine.types import ArrayType, MapType, StructField, StructType
+
+FT = {"struct": 0, "boolean": 1, "long": 2, "double": 3, "float": 3, "decimal": 3, "string": 4, "raw": 5,
+      "timestamp": 6, "int": 7, "date": 8}
+
+FNV_BASIS = 0xcbf29ce484222325
+FNV_PRIME = 0x100000001b3
+M64 = (1 << 64) - 1
+GOLD = 0x9E3779B97F4A7C15
+
+
+def _fnv1a(b: bytes) -> int:
+    h = FNV_BASIS
+    for c in b:
+        h = ((h ^ c) * FNV_PRIME) & M64
+    return h
+
+
+def _fmix64(x: int) -> int:
+    x ^= x >> 33
+    x = (x * 0xff51afd7ed558ccd) & M64
+    x ^= x >> 33
+    x = (x * 0xc4ceb9fe1a85ec53) & M64
+    x ^= x >> 33
+    return x
+
+
+def _to_i64(x: int) -> int:
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+@dataclass
+class Node:
+    path: Tuple[str, ...]
+    parent: int
+    name: str
+    dtype: object
+    code: int
+    val_slot: int = -1
+    len_slot: int = -1
+
+
+class ParsePlan:
+    def __init__(self, schema: StructType, keep: Optional[Set[Tuple[str, ...]]] = None):
+        self.schema = schema
+        self.nodes: List[Node] = [Node((), -1, "", schema, 0)]
+        self.keep = keep
+        self._build(schema, 0, ())
+        nv = nl = 0
+        for nd in self.nodes[1:]:
+            if nd.code != 0:
+                nd.val_slot = nv
+                nv += 1
+                if nd.code in (4, 5):
+                    nd.len_slot = nl
+                    nl += 1
+        self.nval, self.nlen = nv, nl
+        cap = 1 << max(4, math.ceil(math.log2(max(2, 2 * len(self.nodes)))))
+        keys = [0] * cap
+        node_of = [-1] * cap
+        for idx, nd in enumerate(self.nodes[1:], start=1):
+            k = _fmix64(_fnv1a(nd.name.encode("utf-8")) ^ (((nd.parent + 1) * GOLD) & M64))
+            if k == 0:
+                k = 1
+            s = k & (cap - 1)
+            while keys[s] != 0:
+                s = (s + 1) & (cap - 1)
+            keys[s] = k
+            node_of[s] = idx
+        self.lut_keys = [_to_i64(k) for k in keys]
+        self.lut_node = node_of
+        self.cap = cap
+        self._dev: Dict[str, Tuple[torch.Tensor, ...]] = {}
+
+    def _wanted(self, path) -> bool:
+        if self.keep is None:
+            return True
+        return any(k[:len(path)] == path or path[:len(k)] == k for k in self.keep)
+
+    def _build(self, st: StructType, parent: int, prefix):
+        for f in st.fields:
+            path = prefix + (f.name,)
+            if not self._wanted(path):
+                continue
+            if isinstance(f.dtype, StructType):
+                self.nodes.append(Node(path, parent, f.name, f.dtype, 0))
+                self._build(f.dtype, len(self.nodes) - 1, path)
+            elif isinstance(f.dtype, (MapType, ArrayType)):
+                self.nodes.append(Node(path, parent, f.name, f.dtype, FT["raw"]))
+            else:
+                self.nodes.append(Node(path, parent, f.name, f.dtype, FT.get(f.dtype, FT["string"])))
+
+    def device_tables(self, device):
+        key = str(device)
+        t = self._dev.get(key)
+        if t is None:
+            t = (torch.tensor(self.lut_keys, dtype=torch.int64, device=device),
+                 torch.tensor(self.lut_node, dtype=torch.int32, device=device),
+                 torch.tensor([n.code for n in self.nodes], dtype=torch.int32, device=device),
+                 torch.tensor([n.val_slot for n in self.nodes], dtype=torch.int32, device=device),
+                 torch.tensor([n.len_slot for n in self.nodes], dtype=torch.int32, device=device))
+            self._dev[key] = t
+        return t
+
+
+def frame_records(records: Sequence[bytes], device="cpu", pin: bool = False):
+    """Pack raw event payloads into one padded byte buffer + offsets (host-side framing)."""
+    lens = np.fromiter((len(r) for r in records), dtype=np.int64, count=len(records))
+    offs = np.zeros(len(records) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    blob = b"".join(records) + b"\0" * 16
+    buf = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    o = torch.from_numpy(offs)
+    if pin:
+        buf, o = buf.pin_memory(), o.pin_memory()
+    if torch.device(device).type != "cpu":
+        buf, o = buf.to(device, non_blocking=True), o.to(device, non_blocking=True)
+    return buf, o
+
+
+def frame_lines_gpu(buf: torch.Tensor, length: int) -> torch.Tensor:
+    """Record offsets for '\\n'-delimited data already on the device (newline framing kernel)."""
+    chunk = 4096
+    nch = (length + chunk - 1) // chunk
+    counts = torch.empty(nch, dtype=torch.int64, device=buf.device)
+    st = N.stream_handle(buf.device)
+    N.call("dxa_count_newlines", N.ptr(buf), length, chunk, N.ptr(counts), st)
+    base = torch.cumsum(counts, 0) - counts
+    total = int(counts.sum().item())
+    pos = torch.empty(total, dtype=torch.int64, device=buf.device)
+    N.call("dxa_write_newlines", N.ptr(buf), length, chunk, N.ptr(base), N.ptr(pos), st)
+    ends = torch.cat([pos + 1, torch.tensor([length], dtype=torch.int64, device=buf.device)])
+    starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=buf.device), pos + 1])
+    keep = (ends - starts) > 1  # drop empty lines
+    starts, ends = starts[keep], ends[keep]
+    # contiguous offsets: record i = [offs[i], offs[i+1]); dropped empty lines only hold whitespace
+    return torch.cat([starts, ends[-1:]]) if starts.numel() else torch.zeros(1, dtype=torch.int64, device=buf.device)
+
+
+def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan):
+    """Parse records ``buf[offs[i]:offs[i+1]]`` → (Raw StructColumn, row_ok bool tensor)."""
+    n = int(offs.shape[0]) - 1
+    device = buf.device
+    if device.type == "cuda":
+        return _parse_gpu(buf, offs, n, plan)
+    return _parse_cpu(buf, offs, n, plan)
+
+
+def _parse_gpu(buf, offs, n, plan: ParsePlan):
+    lut_k, lut_n, types, vslot, lslot = plan.device_tables(buf.device)
+    nn = len(plan.nodes)
+    vals = torch.empty((max(1, plan.nval), max(n, 1)), dtype=torch.int64, device=buf.device)
+    lens = torch.empty((max(1, plan.nlen), max(n, 1)), dtype=torch.int32, device=buf.device)
+    valid = torch.empty((nn, max(n, 1)), dtype=torch.uint8, device=buf.device)
+    row_ok = torch.empty(max(n, 1), dtype=torch.uint8, device=buf.device)
+    if n:
+        N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
+               N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
+               N.stream_handle(buf.device))
+    vals, lens, valid, row_ok = vals[:, :n], lens[:, :n], valid[:, :n].view(torch.bool), row_ok[:n].view(torch.bool)
+    return _assemble(plan, buf, vals, lens, valid, n), row_ok
+
+
+def _assemble(plan: ParsePlan, arena, vals, lens, valid, n):
+    from ..engine.column import PrimColumn, StrColumn, JsonColumn, StructColumn
+    device = arena.device
+    cols: Dict[int, object] = {}
+    for idx in range(len(plan.nodes) - 1, 0, -1):
+        nd = plan.nodes[idx]
+        v = valid[idx]
+        if nd.code == 0:
+            kids = [(plan.nodes[j].name, cols[j]) for j in range(len(plan.nodes)) if plan.nodes[j].parent == idx]
+            cols[idx] = StructColumn([k for k, _ in kids], [c for _, c in kids], n, v, False, None, device)
+            continue
+        raw = vals[nd.val_slot]
+        if nd.code == FT["string"]:
+            cols[idx] = StrColumn(arena, raw, lens[nd.len_slot], v)
+        elif nd.code == FT["raw"]:
+            cols[idx] = JsonColumn(arena, raw, lens[nd.len_slot], v, nd.dtype)
+        elif nd.code == FT["double"]:
+            cols[idx] = PrimColumn(nd.dtype if nd.dtype in ("double", "float", "decimal") else "double",
+                                   raw.view(torch.float64), v)
+        elif nd.code == FT["boolean"]:
+            cols[idx] = PrimColumn("boolean", raw != 0, v)
+        else:
+            cols[idx] = PrimColumn(nd.dtype, raw, v)
+    kids = [(plan.nodes[j].name, cols[j]) for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == 0]
+    return StructColumn([k for k, _ in kids], [c for _, c in kids], n, valid[0], False, None, device)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# CPU reference (Python json) — same null/mismatch semantics as the kernel
+# ------------------------------------------------------------------------------------------------------------------
+def _iso_to_us(s: str) -> Optional[int]:
+    import re
+    import datetime as dt
+    m = re.match(r"^(\d{4})-(\d{2})-(\d{2})(?:[T ](\d{2}):(\d{2})(?::(\d{2}))?(?:\.(\d+))?(Z|[+-]\d{2}:?(?:\d{2})?)?)?$",
+                 s)
+    if not m:
+        return None
+    y, mo, d = int(m.group(1)), int(m.group(2)), int(m.group(3))
+    hh = int(m.group(4) or 0)
+    mi = int(m.group(5) or 0)
+    ss = int(m.group(6) or 0)
+    frac = int(((m.group(7) or "") + "000000")[:6])
+    tz = m.group(8)
+    if not (1 <= mo <= 12 and 1 <= d <= 31 and hh <= 23 and mi <= 59 and ss <= 60):
+        return None
+    days = (dt.date(y, mo, 1) - dt.date(1970, 1, 1)).days + d - 1
+    us = (days * 86400 + hh * 3600 + mi * 60 + ss) * 1_000_000 + frac
+    if tz and tz != "Z":
+        sign = -1 if tz[0] == "-" else 1
+        digits = tz[1:].replace(":", "")
+        th = int(digits[:2])
+        tm = int(digits[2:4] or 0)
+        us -= sign * (th * 3600 + tm * 60) * 1_000_000
+    return us
+
+
+def _convert(v, dtype):
+    """Python JSON value → storage value for a leaf, or None (null / mismatch)."""
+    if v is None:
+        return None
+    if dtype in ("long", "int"):
+        if isinstance(v, bool) or not isinstance(v, int):
+            return None
+        if dtype == "int" and not (-2**31 <= v < 2**31):
+            return None
+        if not (-2**63 <= v < 2**63):
+            return None
+        return v
+    if dtype in ("double", "float", "decimal"):
+        if isinstance(v, bool) or not isinstance(v, (int, float)):
+            return None
+        return float(v)
+    if dtype == "boolean":
+        return v if isinstance(v, bool) else None
+    if dtype == "string":
+        if isinstance(v, str):
+            return v
+        return json.dumps(v, separators=(",", ":")) if not isinstance(v, bool) else ("true" if v else "false")
+    if dtype == "timestamp":
+        if isinstance(v, bool):
+            return None
+        if isinstance(v, int):
+            return v * 1_000_000
+        if isinstance(v, str):
+            return _iso_to_us(v)
+        return None
+    if dtype == "date":
+        if isinstance(v, str):
+            us = _iso_to_us(v)
+            return None if us is None else us // 86_400_000_000
+        return None
+    if isinstance(dtype, (MapType, ArrayType)):
+        if isinstance(dtype, MapType) and isinstance(v, dict):
+            return json.dumps(v, separators=(",", ":"))
+        if isinstance(dtype, ArrayType) and isinstance(v, list):
+            return json.dumps(v, separators=(",", ":"))
+        return None
+    return None
+
+
+def _parse_cpu(buf, offs, n, plan: ParsePlan):
+    from ..engine.column import column_from_pylist, strings_from_pylist, PrimColumn, StructColumn, JsonColumn
+    data = buf.cpu().numpy().tobytes()
+    o = offs.cpu().tolist()
+    recs = []
+    ok = []
+    for i in range(n):
+        try:
+            d = json.loads(data[o[i]:o[i + 1]].decode("utf-8"))
+            if not isinstance(d, dict):
+                raise ValueError
+            recs.append(d)
+            ok.append(True)
+        except Exception:
+            recs.append(None)
+            ok.append(False)
+
+    def build(idx, getters):
+        kids = [j for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == idx]
+        names, cols = [], []
+        for j in kids:
+            nd = plan.nodes[j]
+            vals = [None if g is None else g.get(nd.name) for g in getters]
+            if nd.code == 0:
+                sub = [v if isinstance(v, dict) else None for v in vals]
+                col = build(j, sub)
+                valid = torch.tensor([v is not None for v in sub], dtype=torch.bool)
+                col = col.with_valid(valid)
+            else:
+                conv = [_convert(v, nd.dtype) for v in vals]
+                if nd.code == FT["raw"]:
+                    col = strings_from_pylist(conv, "cpu", nd.dtype)
+                elif nd.dtype in ("float", "decimal"):
+                    col = column_from_pylist(conv, "double", "cpu")
+                    col.dtype = nd.dtype
+                else:
+                    col = column_from_pylist(conv, nd.dtype, "cpu")
+                if col.valid is None:
+                    col.valid = torch.ones(n, dtype=torch.bool)
+            names.append(nd.name)
+            cols.append(col)
+        return StructColumn(names, cols, n, None, False, None, "cpu")
+
+    root = build(0, recs)
+    row_ok = torch.tensor(ok, dtype=torch.bool)
+    root.valid = row_ok
+    return root, row_ok

@@ -1,0 +1,131 @@
+"""ctypes binding to the in-tree gfx950 kernel library (``dxa/ops/_native/libdxa_kernels.so``).
+
+The library is a plain C ABI over HIP kernels; it is loaded *after* ``import torch`` so its ``libamdhip64.so.7``
+dependency resolves (by SONAME) to the HIP runtime torch already mapped — one runtime, one set of streams, and our
+kernels run on torch's current stream with torch-allocated HBM buffers.
+
+GPU tensors always take the native path; if the library is missing on a GPU box we raise instead of silently
+falling back to slower PyTorch code (``DXA_ALLOW_FALLBACK=1`` is for debugging only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_LIB = None
+_LOCK = threading.Lock()
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "_native" / "libdxa_kernels.so"
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_p = ctypes.c_void_p
+
+_SIGS = {
+    "dxa_json_parse": [c_p, c_p, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_p],
+    "dxa_count_newlines": [c_p, c_i64, c_i64, c_p, c_p],
+    "dxa_write_newlines": [c_p, c_i64, c_i64, c_p, c_p, c_p],
+    "dxa_hash_i64": [c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],
+    "dxa_hash_f64": [c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],
+    "dxa_hash_str": [c_p, c_p, c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],
+    "dxa_table_insert": [c_p, c_i64, c_p, c_i64, c_p, c_p],
+    "dxa_group_ids": [c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
+    "dxa_verify_i64": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
+    "dxa_verify_str": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
+    "dxa_aggregate": [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p],
+    "dxa_slot_count": [c_p, c_i64, c_p, c_p],
+    "dxa_slot_scatter": [c_p, c_i64, c_p, c_p, c_p, c_p],
+    "dxa_probe_count": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int, c_p],
+    "dxa_probe_write": [c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, ctypes.c_int, c_p],
+    "dxa_str_cmp_lit": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p],
+    "dxa_str_eq_col": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
+    "dxa_str_gather": [c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
+    "dxa_concat_len": [c_p, c_i32, c_i64, c_p, c_p, c_p],
+    "dxa_concat_write": [c_p, c_i32, c_i64, c_p, c_p, c_p, c_p],
+    "dxa_concat_part_size": [],
+    "dxa_i64_to_str_len": [c_p, c_i64, c_p, c_p],
+    "dxa_i64_to_str_write": [c_p, c_i64, c_p, c_p, c_p],
+    "dxa_case_map": [c_p, c_p, c_p, c_i64, c_p, c_p, ctypes.c_int, c_p],
+    "dxa_str_to_ts": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
+}
+
+# optional symbols (added by later kernels); bound if present
+_OPTIONAL_SIGS = {}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def register_sigs(sigs: dict):
+    _OPTIONAL_SIGS.update(sigs)
+
+
+def lib():
+    """Load (building first if needed and hipcc is present) the kernel library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if not LIB_PATH.exists() or os.environ.get("DXA_REBUILD") == "1":
+            from .build import build
+            build()
+        L = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        for name, args in {**_SIGS, **_OPTIONAL_SIGS}.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                if name in _SIGS:
+                    raise NativeError(f"symbol {name} missing from {LIB_PATH}")
+                continue
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _LIB = L
+        return L
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def ptr(t) -> int:
+    if t is None:
+        return 0
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args):
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        raise NativeError(f"{name} failed with HIP error {rc}")
+    return rc
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """True when ``t`` lives on the GPU (the native HIP path is mandatory there)."""
+    if t.is_cuda:
+        if os.environ.get("DXA_ALLOW_FALLBACK") == "1" and not available():
+            return False
+        return True
+    return False
+
+
+def u8(mask):
+    """bool mask → uint8 view for kernels (bool and uint8 share the 1-byte layout)."""
+    if mask is None:
+        return None
+    return mask.view(torch.uint8) if mask.dtype == torch.bool else mask

@@ -1,0 +1,263 @@
+"""String-column operations: compaction/concatenation of arenas, literal predicates, CONCAT, casts, case mapping,
+``stringToTimestamp``.  GPU → strings.hip kernels; CPU → straightforward torch/Python reference code.
+"""
+from __future__ import annotations
+
+import ctypes
+import datetime as _dt
+import re
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from . import native as N
+
+_CMP_OPS = {"=": 0, "!=": 1, "<": 2, "<=": 3, ">": 4, ">=": 5, "startswith": 6, "endswith": 7, "contains": 8}
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _offsets(lens: torch.Tensor):
+    """Exclusive scan of lengths → (offsets int64, total bytes)."""
+    if lens.numel() == 0:
+        return torch.zeros(0, dtype=torch.int64, device=lens.device), 0
+    cs = torch.cumsum(lens.to(torch.int64), 0)
+    total = int(cs[-1].item())
+    return cs - lens.to(torch.int64), total
+
+
+def _alloc_arena(total: int, device) -> torch.Tensor:
+    return torch.zeros(total + 16, dtype=torch.uint8, device=device)
+
+
+def compact(col):
+    """Densely repack the bytes a StrColumn references (drops the rest of its arena)."""
+    off, total = _offsets(col.lens)
+    dst = _alloc_arena(total, col.device)
+    n = col.length
+    if n and total:
+        if _gpu(col.starts):
+            N.call("dxa_str_gather", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(off), N.ptr(dst),
+                   N.stream_handle(col.device))
+        else:
+            src = col.arena
+            idx = torch.repeat_interleave(col.starts - off, col.lens.to(torch.int64)) + torch.arange(
+                total, dtype=torch.int64)
+            dst[:total] = src[idx]
+    return type(col)(dst, off, col.lens.clone(), col.valid, col.dtype)
+
+
+def concat(cols: Sequence, valid: Optional[torch.Tensor]):
+    """Row-concatenate StrColumns (may reference different arenas) into one compact column."""
+    device = cols[0].device
+    lens = torch.cat([c.lens for c in cols])
+    off, total = _offsets(lens)
+    dst = _alloc_arena(total, device)
+    pos = 0
+    for c in cols:
+        n = c.length
+        if n:
+            o = off[pos:pos + n].contiguous()
+            if _gpu(c.starts):
+                N.call("dxa_str_gather", N.ptr(c.arena), N.ptr(c.starts), N.ptr(c.lens), n, N.ptr(o), N.ptr(dst),
+                       N.stream_handle(device))
+            else:
+                tot = int(c.lens.to(torch.int64).sum().item())
+                if tot:
+                    # destination positions are contiguous from o[0]
+                    srcpos = torch.repeat_interleave(c.starts, c.lens.to(torch.int64)) + (
+                        torch.arange(tot) - torch.repeat_interleave(o - o[0], c.lens.to(torch.int64)))
+                    dst[int(o[0]):int(o[0]) + tot] = c.arena[srcpos]
+        pos += n
+    return type(cols[0])(dst, off, lens.to(torch.int32), valid, cols[0].dtype)
+
+
+def cmp_literal(col, lit: str, op: str) -> torch.Tensor:
+    """Byte-wise comparison of every string against a literal → bool mask (nulls handled by the caller)."""
+    code = _CMP_OPS[op]
+    lb = lit.encode("utf-8")
+    n = col.length
+    if _gpu(col.starts):
+        out = torch.empty(n, dtype=torch.bool, device=col.device)
+        if n:
+            lt = torch.frombuffer(bytearray(lb + b"\0"), dtype=torch.uint8).to(col.device, non_blocking=True)
+            N.call("dxa_str_cmp_lit", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(lt), len(lb),
+                   code, N.ptr(out.view(torch.uint8)), N.stream_handle(col.device))
+        return out
+    vals = _raw_bytes(col)
+    f = {
+        0: lambda s: s == lb, 1: lambda s: s != lb, 2: lambda s: s < lb, 3: lambda s: s <= lb,
+        4: lambda s: s > lb, 5: lambda s: s >= lb, 6: lambda s: s.startswith(lb), 7: lambda s: s.endswith(lb),
+        8: lambda s: lb in s,
+    }[code]
+    return torch.tensor([f(s) for s in vals], dtype=torch.bool)
+
+
+def _raw_bytes(col) -> List[bytes]:
+    arena = col.arena.cpu().numpy().tobytes()
+    return [arena[s:s + l] for s, l in zip(col.starts.cpu().tolist(), col.lens.cpu().tolist())]
+
+
+def eq_columns(a, b) -> torch.Tensor:
+    n = a.length
+    if _gpu(a.starts):
+        out = torch.empty(n, dtype=torch.bool, device=a.device)
+        if n:
+            N.call("dxa_str_eq_col", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), N.ptr(b.arena), N.ptr(b.starts),
+                   N.ptr(b.lens), n, N.ptr(out.view(torch.uint8)), N.stream_handle(a.device))
+        return out
+    return torch.tensor([x == y for x, y in zip(_raw_bytes(a), _raw_bytes(b))], dtype=torch.bool)
+
+
+def compare_columns(a, b, op: str) -> torch.Tensor:
+    """General (host-assisted) string column comparison for < <= > >=; equality uses eq_columns."""
+    if op in ("=", "!="):
+        eq = eq_columns(a, b)
+        return eq if op == "=" else ~eq
+    va, vb = _raw_bytes(a), _raw_bytes(b)
+    f = {"<": lambda x, y: x < y, "<=": lambda x, y: x <= y, ">": lambda x, y: x > y, ">=": lambda x, y: x >= y}[op]
+    return torch.tensor([f(x, y) for x, y in zip(va, vb)], dtype=torch.bool, device=a.device)
+
+
+class _ConcatPart(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("starts", ctypes.c_void_p), ("lens", ctypes.c_void_p),
+                ("valid", ctypes.c_void_p), ("lit", ctypes.c_void_p), ("lit_len", ctypes.c_int32),
+                ("is_lit", ctypes.c_int32)]
+
+
+def concat_strings(parts: List[Union[str, object]], n: int, device):
+    """CONCAT over string columns and literals (Spark: any null input → null)."""
+    from ..engine.column import StrColumn, and_valid
+    device = torch.device(device)
+    if device.type == "cuda":
+        lits = []
+        arr = (_ConcatPart * len(parts))()
+        keep = []
+        for i, p in enumerate(parts):
+            if isinstance(p, str):
+                b = p.encode("utf-8")
+                t = torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8).to(device)
+                keep.append(t)
+                arr[i] = _ConcatPart(0, 0, 0, 0, t.data_ptr(), len(b), 1)
+            else:
+                v = N.u8(p.valid)
+                keep.append(v)
+                arr[i] = _ConcatPart(p.arena.data_ptr(), p.starts.data_ptr(), p.lens.data_ptr(),
+                                     0 if v is None else v.data_ptr(), 0, 0, 0)
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
+        lens = torch.empty(n, dtype=torch.int64, device=device)
+        ok = torch.empty(n, dtype=torch.bool, device=device)
+        st = N.stream_handle(device)
+        N.call("dxa_concat_len", N.ptr(raw), len(parts), n, N.ptr(lens), N.ptr(ok.view(torch.uint8)), st)
+        off, total = _offsets(lens)
+        dst = _alloc_arena(total, device)
+        N.call("dxa_concat_write", N.ptr(raw), len(parts), n, N.ptr(off), N.ptr(ok.view(torch.uint8)), N.ptr(dst), st)
+        valid = None if all(isinstance(p, str) or p.valid is None for p in parts) else ok
+        col = StrColumn(dst, off, lens.to(torch.int32), valid)
+        col._keep = (keep, raw)
+        return col
+    cols = [None if isinstance(p, str) else p.to_pylist() for p in parts]
+    out = []
+    for i in range(n):
+        s = []
+        null = False
+        for p, c in zip(parts, cols):
+            if c is None:
+                s.append(p)
+            elif c[i] is None:
+                null = True
+                break
+            else:
+                s.append(c[i])
+        out.append(None if null else "".join(s))
+    from ..engine.column import strings_from_pylist
+    return strings_from_pylist(out, device)
+
+
+def from_int64(data: torch.Tensor, valid):
+    """CAST(long AS STRING)."""
+    from ..engine.column import StrColumn, strings_from_pylist
+    n = data.shape[0]
+    if _gpu(data):
+        st = N.stream_handle(data.device)
+        lens = torch.empty(n, dtype=torch.int64, device=data.device)
+        N.call("dxa_i64_to_str_len", N.ptr(data), n, N.ptr(lens), st)
+        off, total = _offsets(lens)
+        dst = _alloc_arena(total, data.device)
+        N.call("dxa_i64_to_str_write", N.ptr(data), n, N.ptr(off), N.ptr(dst), st)
+        return StrColumn(dst, off, lens.to(torch.int32), valid)
+    vals = data.tolist()
+    v = valid.tolist() if valid is not None else [True] * n
+    return strings_from_pylist([str(x) if ok else None for x, ok in zip(vals, v)], data.device)
+
+
+def case_map(col, upper: bool):
+    from ..engine.column import StrColumn, strings_from_pylist
+    n = col.length
+    if _gpu(col.starts):
+        off, total = _offsets(col.lens)
+        dst = _alloc_arena(total, col.device)
+        N.call("dxa_case_map", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(off), N.ptr(dst),
+               1 if upper else 0, N.stream_handle(col.device))
+        return StrColumn(dst, off, col.lens.clone(), col.valid)
+    vals = col.to_pylist()
+    return strings_from_pylist([None if v is None else (_ascii_upper(v) if upper else _ascii_lower(v))
+                                for v in vals], col.device)
+
+
+def _ascii_upper(s):
+    return "".join(c.upper() if "a" <= c <= "z" else c for c in s)
+
+
+def _ascii_lower(s):
+    return "".join(c.lower() if "A" <= c <= "Z" else c for c in s)
+
+
+_TS_A = re.compile(r"^(\d{4})-(\d{1,2})-(\d{1,2}) (\d{1,2}):(\d{1,2}):(\d{1,2})(?:\.(\d+))?$")
+_TS_B = re.compile(r"^(\d{4})-(\d{1,2})-(\d{1,2})T(\d{1,2}):(\d{1,2}):(\d{1,2})Z$")
+_TS_C = re.compile(r"^(\d{1,2})/(\d{1,2})/(\d{4}) (\d{1,2}):(\d{1,2}):(\d{1,2})$")
+
+
+def py_string_to_timestamp_us(s: Optional[str]) -> Optional[int]:
+    """Reference semantics of DataX's ``stringToTimestamp`` (ConcurrentDateFormat.scala:38-62), UTC."""
+    if not s:
+        return None
+    frac = 0
+    m = _TS_A.match(s)
+    if m:
+        y, mo, d, hh, mi, ss = (int(x) for x in m.groups()[:6])
+        if m.group(7):
+            frac = int((m.group(7) + "000000")[:6])
+    else:
+        m = _TS_B.match(s)
+        if m:
+            y, mo, d, hh, mi, ss = (int(x) for x in m.groups())
+        else:
+            m = _TS_C.match(s)
+            if not m:
+                return None
+            mo, d, y, hh, mi, ss = (int(x) for x in m.groups())
+    if not (1 <= mo <= 12 and 1 <= d <= 31 and hh <= 23 and mi <= 59 and ss <= 59):
+        return None
+    try:
+        days = (_dt.date(y, mo, 1) - _dt.date(1970, 1, 1)).days + d - 1
+    except ValueError:
+        return None
+    return (days * 86400 + hh * 3600 + mi * 60 + ss) * 1_000_000 + frac
+
+
+def to_timestamp(col):
+    from ..engine.column import PrimColumn
+    n = col.length
+    if _gpu(col.starts):
+        out = torch.empty(n, dtype=torch.int64, device=col.device)
+        ok = torch.empty(n, dtype=torch.bool, device=col.device)
+        N.call("dxa_str_to_ts", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), N.ptr(N.u8(col.valid)), n,
+               N.ptr(out), N.ptr(ok.view(torch.uint8)), N.stream_handle(col.device))
+        return PrimColumn("timestamp", out, ok)
+    vals = [py_string_to_timestamp_us(v) for v in col.to_pylist()]
+    data = torch.tensor([0 if v is None else v for v in vals], dtype=torch.int64)
+    return PrimColumn("timestamp", data, torch.tensor([v is not None for v in vals], dtype=torch.bool))

@@ -1,0 +1,266 @@
+"""AST node types for the DataX-SQL dialect (the Spark-SQL subset the reference's flows use).
+
+The reference hands every transform statement to ``spark.sql`` (DataProcessing/datax-host/src/main/scala/datax/
+processor/CommonProcessorFactory.scala:249-294).  We own the whole front-end instead: these nodes are produced by
+``dxa.sql.parser`` and consumed by the columnar planner in ``dxa.engine.query``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple, Any
+
+
+class Expr:
+    """Base expression node.  ``key()`` gives a structural identity used to match GROUP BY expressions."""
+
+    def key(self):
+        raise NotImplementedError
+
+    def children(self) -> List["Expr"]:
+        return []
+
+
+@dataclass(eq=False)
+class Literal(Expr):
+    value: Any
+    type: str  # 'long' | 'int' | 'double' | 'string' | 'boolean' | 'null' | 'decimal'
+
+    def key(self):
+        return ("lit", self.type, self.value)
+
+
+@dataclass(eq=False)
+class Ident(Expr):
+    """Possibly-dotted identifier: ``a``, ``t.a``, ``Raw.deviceDetails.deviceId``."""
+    parts: Tuple[str, ...]
+
+    def key(self):
+        return ("id",) + tuple(p.lower() for p in self.parts)
+
+    @property
+    def name(self):
+        return self.parts[-1]
+
+
+@dataclass(eq=False)
+class Star(Expr):
+    qualifier: Tuple[str, ...] = ()
+
+    def key(self):
+        return ("star",) + self.qualifier
+
+
+@dataclass(eq=False)
+class Call(Expr):
+    name: str          # lower-cased function name
+    args: List[Expr]
+    distinct: bool = False
+    star: bool = False  # COUNT(*)
+
+    def key(self):
+        return ("call", self.name, self.distinct, self.star) + tuple(a.key() for a in self.args)
+
+    def children(self):
+        return list(self.args)
+
+
+@dataclass(eq=False)
+class BinOp(Expr):
+    op: str            # '+','-','*','/','%','=','!=','<','<=','>','>=','and','or','||','<=>','&','|','^','div'
+    left: Expr
+    right: Expr
+
+    def key(self):
+        return ("bin", self.op, self.left.key(), self.right.key())
+
+    def children(self):
+        return [self.left, self.right]
+
+
+@dataclass(eq=False)
+class UnaryOp(Expr):
+    op: str            # 'not', '-', '+', '~'
+    operand: Expr
+
+    def key(self):
+        return ("un", self.op, self.operand.key())
+
+    def children(self):
+        return [self.operand]
+
+
+@dataclass(eq=False)
+class IsNull(Expr):
+    operand: Expr
+    negated: bool = False
+
+    def key(self):
+        return ("isnull", self.negated, self.operand.key())
+
+    def children(self):
+        return [self.operand]
+
+
+@dataclass(eq=False)
+class InList(Expr):
+    operand: Expr
+    items: List[Expr]
+    negated: bool = False
+
+    def key(self):
+        return ("in", self.negated, self.operand.key()) + tuple(i.key() for i in self.items)
+
+    def children(self):
+        return [self.operand] + list(self.items)
+
+
+@dataclass(eq=False)
+class Between(Expr):
+    operand: Expr
+    low: Expr
+    high: Expr
+    negated: bool = False
+
+    def key(self):
+        return ("between", self.negated, self.operand.key(), self.low.key(), self.high.key())
+
+    def children(self):
+        return [self.operand, self.low, self.high]
+
+
+@dataclass(eq=False)
+class Like(Expr):
+    operand: Expr
+    pattern: Expr
+    negated: bool = False
+    regex: bool = False  # RLIKE
+
+    def key(self):
+        return ("like", self.negated, self.regex, self.operand.key(), self.pattern.key())
+
+    def children(self):
+        return [self.operand, self.pattern]
+
+
+@dataclass(eq=False)
+class Case(Expr):
+    operand: Optional[Expr]
+    whens: List[Tuple[Expr, Expr]]
+    default: Optional[Expr]
+
+    def key(self):
+        return ("case", self.operand.key() if self.operand else None,
+                tuple((w.key(), t.key()) for w, t in self.whens), self.default.key() if self.default else None)
+
+    def children(self):
+        out = [self.operand] if self.operand else []
+        for w, t in self.whens:
+            out += [w, t]
+        if self.default:
+            out.append(self.default)
+        return out
+
+
+@dataclass(eq=False)
+class Cast(Expr):
+    operand: Expr
+    to: str
+
+    def key(self):
+        return ("cast", self.to, self.operand.key())
+
+    def children(self):
+        return [self.operand]
+
+
+@dataclass(eq=False)
+class Subscript(Expr):
+    """``base[index]`` on maps / arrays, and ``base.field`` on a non-identifier base (e.g. ``RuleObject.x`` after a call)."""
+    base: Expr
+    index: Expr
+    dot: bool = False
+
+    def key(self):
+        return ("sub", self.dot, self.base.key(), self.index.key())
+
+    def children(self):
+        return [self.base, self.index]
+
+
+@dataclass(eq=False)
+class Interval(Expr):
+    micros: int
+
+    def key(self):
+        return ("interval", self.micros)
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Relations / statements
+# ----------------------------------------------------------------------------------------------------------------
+
+@dataclass(eq=False)
+class SelectItem:
+    expr: Expr
+    alias: Optional[str] = None
+
+
+@dataclass(eq=False)
+class TableRef:
+    name: str
+    alias: Optional[str] = None
+    timewindow: Optional[str] = None   # DataX extension: FROM t TIMEWINDOW('5 minutes')
+
+
+@dataclass(eq=False)
+class SubqueryRef:
+    query: "Query"
+    alias: Optional[str] = None
+
+
+@dataclass(eq=False)
+class Join:
+    left: Any
+    right: Any
+    kind: str          # 'inner' | 'left' | 'right' | 'full' | 'cross' | 'semi' | 'anti'
+    on: Optional[Expr] = None
+    using: Optional[List[str]] = None
+
+
+@dataclass(eq=False)
+class OrderItem:
+    expr: Expr
+    ascending: bool = True
+    nulls_first: Optional[bool] = None
+
+
+@dataclass(eq=False)
+class Select:
+    items: List[SelectItem]
+    from_: Any = None
+    where: Optional[Expr] = None
+    group_by: List[Expr] = field(default_factory=list)
+    having: Optional[Expr] = None
+    distinct: bool = False
+
+
+@dataclass(eq=False)
+class SetOp:
+    op: str            # 'union' | 'intersect' | 'except'
+    all: bool
+    left: Any
+    right: Any
+
+
+@dataclass(eq=False)
+class Query:
+    body: Any          # Select | SetOp
+    order_by: List[OrderItem] = field(default_factory=list)
+    limit: Optional[int] = None
+
+
+def walk(e: Expr):
+    """Pre-order traversal of an expression tree."""
+    yield e
+    for c in e.children():
+        yield from walk(c)

@@ -1,0 +1,643 @@
+"""Tokenizer + recursive-descent parser for the DataX-SQL dialect.
+
+Supported surface (everything the reference's fixtures and sample flows exercise, plus the usual Spark-SQL
+operators): SELECT [DISTINCT] … FROM … [JOIN … ON …] [WHERE] [GROUP BY] [HAVING] [ORDER BY] [LIMIT];
+UNION [ALL] / INTERSECT / EXCEPT; sub-queries in FROM; CASE, CAST, IN, BETWEEN, LIKE/RLIKE, IS [NOT] NULL;
+back-ticked identifiers, nested field access (``a.b.c``), map/array subscripts, ``t.*``; the DataX
+``TIMEWINDOW('5 minutes')`` FROM-suffix (reference rewrite: Services/DataX.Flow/DataX.Flow.CodegenRules/Engine.cs:595-627).
+
+Anything outside the subset raises ``SqlError`` with the offending position — we fail loudly rather than guess.
+"""
+from __future__ import annotations
+
+import re
+from typing import List, Optional
+
+from . import ast as A
+
+
+class SqlError(Exception):
+    pass
+
+
+KEYWORDS = {
+    "select", "distinct", "from", "where", "group", "by", "having", "order", "limit", "as", "and", "or", "not",
+    "in", "is", "null", "true", "false", "case", "when", "then", "else", "end", "cast", "join", "inner", "left",
+    "right", "full", "outer", "cross", "on", "using", "union", "all", "intersect", "except", "asc", "desc",
+    "between", "like", "rlike", "regexp", "nulls", "first", "last", "semi", "anti", "timewindow", "interval", "div",
+}
+
+_TOKEN_RE = re.compile(r"""
+    (?P<ws>\s+|--[^\n]*) |
+    (?P<num>(?:\d+\.\d*|\.\d+|\d+)(?:[eE][+-]?\d+)?[LlDdSsYy]?(?:BD)?) |
+    (?P<str>'(?:[^'\\]|\\.|'')*'|"(?:[^"\\]|\\.|"")*") |
+    (?P<bq>`(?:[^`]|``)*`) |
+    (?P<id>[A-Za-z_][A-Za-z0-9_$]*) |
+    (?P<op><=>|<>|!=|==|<=|>=|\|\||&&|[-+*/%=<>(),.;\[\]~&|^!:])
+""", re.VERBOSE)
+
+
+class Tok:
+    __slots__ = ("kind", "text", "pos")
+
+    def __init__(self, kind, text, pos):
+        self.kind, self.text, self.pos = kind, text, pos
+
+    def __repr__(self):
+        return f"Tok({self.kind},{self.text!r})"
+
+
+def _unquote(s: str) -> str:
+    q = s[0]
+    body = s[1:-1]
+    out = []
+    i = 0
+    while i < len(body):
+        c = body[i]
+        if c == "\\" and i + 1 < len(body):
+            n = body[i + 1]
+            out.append({"n": "\n", "t": "\t", "r": "\r", "0": "\0", "b": "\b"}.get(n, n))
+            i += 2
+            continue
+        if c == q and i + 1 < len(body) and body[i + 1] == q:
+            out.append(q)
+            i += 2
+            continue
+        out.append(c)
+        i += 1
+    return "".join(out)
+
+
+def tokenize(sql: str) -> List[Tok]:
+    toks: List[Tok] = []
+    pos = 0
+    while pos < len(sql):
+        m = _TOKEN_RE.match(sql, pos)
+        if not m:
+            raise SqlError(f"unexpected character {sql[pos]!r} at {pos} in: {sql[max(0, pos - 30):pos + 30]!r}")
+        kind = m.lastgroup
+        text = m.group(kind)
+        if kind == "ws":
+            pass
+        elif kind == "id":
+            low = text.lower()
+            toks.append(Tok("kw" if low in KEYWORDS else "id", text, pos))
+        elif kind == "bq":
+            toks.append(Tok("id", text[1:-1].replace("``", "`"), pos))
+        elif kind == "str":
+            toks.append(Tok("str", _unquote(text), pos))
+        else:
+            toks.append(Tok(kind, text, pos))
+        pos = m.end()
+    toks.append(Tok("eof", "", pos))
+    return toks
+
+
+_INTERVAL_UNITS = {
+    "microsecond": 1, "microseconds": 1, "millisecond": 1000, "milliseconds": 1000,
+    "second": 1_000_000, "seconds": 1_000_000, "minute": 60_000_000, "minutes": 60_000_000,
+    "hour": 3_600_000_000, "hours": 3_600_000_000, "day": 86_400_000_000, "days": 86_400_000_000,
+    "week": 7 * 86_400_000_000, "weeks": 7 * 86_400_000_000,
+}
+
+
+def parse_duration_micros(text: str) -> int:
+    """'5 minutes' / '60 second' / '1 hour 30 minutes' → microseconds (reference: SettingDictionary.getDuration)."""
+    parts = text.strip().lower().split()
+    if len(parts) == 1:
+        m = re.match(r"^(\d+)\s*([a-z]+)$", parts[0])
+        if m:
+            parts = [m.group(1), m.group(2)]
+        elif re.match(r"^\d+$", parts[0]):
+            return int(parts[0]) * 1_000_000
+    if len(parts) % 2:
+        raise SqlError(f"bad duration {text!r}")
+    total = 0
+    for i in range(0, len(parts), 2):
+        n = float(parts[i])
+        unit = parts[i + 1]
+        if unit not in _INTERVAL_UNITS:
+            raise SqlError(f"bad duration unit {unit!r} in {text!r}")
+        total += int(n * _INTERVAL_UNITS[unit])
+    return total
+
+
+class Parser:
+    def __init__(self, sql: str):
+        self.sql = sql
+        self.toks = tokenize(sql)
+        self.i = 0
+
+    # -- token helpers -------------------------------------------------------------------------------------------
+    @property
+    def cur(self) -> Tok:
+        return self.toks[self.i]
+
+    def peek(self, k=1) -> Tok:
+        return self.toks[min(self.i + k, len(self.toks) - 1)]
+
+    def is_kw(self, *words, tok=None) -> bool:
+        t = tok or self.cur
+        return t.kind == "kw" and t.text.lower() in words
+
+    def is_op(self, *ops, tok=None) -> bool:
+        t = tok or self.cur
+        return t.kind == "op" and t.text in ops
+
+    def advance(self) -> Tok:
+        t = self.cur
+        self.i += 1
+        return t
+
+    def accept_kw(self, *words) -> bool:
+        if self.is_kw(*words):
+            self.i += 1
+            return True
+        return False
+
+    def accept_op(self, *ops) -> bool:
+        if self.is_op(*ops):
+            self.i += 1
+            return True
+        return False
+
+    def expect_kw(self, word):
+        if not self.accept_kw(word):
+            self.error(f"expected {word.upper()}")
+
+    def expect_op(self, op):
+        if not self.accept_op(op):
+            self.error(f"expected '{op}'")
+
+    def error(self, msg):
+        t = self.cur
+        raise SqlError(f"{msg} at position {t.pos} near {self.sql[max(0, t.pos - 40):t.pos + 40]!r}")
+
+    def ident(self) -> str:
+        t = self.cur
+        if t.kind == "id":
+            self.i += 1
+            return t.text
+        # non-reserved keywords usable as identifiers
+        if t.kind == "kw" and t.text.lower() in ("first", "last", "semi", "anti", "nulls", "timewindow", "interval",
+                                                   "div", "regexp"):
+            self.i += 1
+            return t.text
+        self.error("expected identifier")
+
+    # -- statements ----------------------------------------------------------------------------------------------
+    def parse_query(self) -> A.Query:
+        body = self.parse_set_expr()
+        q = A.Query(body=body)
+        if self.accept_kw("order"):
+            self.expect_kw("by")
+            q.order_by = self.parse_order_items()
+        if self.accept_kw("limit"):
+            t = self.advance()
+            if t.kind != "num":
+                self.error("expected LIMIT count")
+            q.limit = int(t.text)
+        return q
+
+    def parse_order_items(self):
+        items = []
+        while True:
+            e = self.parse_expr()
+            asc = True
+            if self.accept_kw("desc"):
+                asc = False
+            else:
+                self.accept_kw("asc")
+            nf = None
+            if self.accept_kw("nulls"):
+                if self.accept_kw("first"):
+                    nf = True
+                else:
+                    self.expect_kw("last")
+                    nf = False
+            items.append(A.OrderItem(e, asc, nf))
+            if not self.accept_op(","):
+                return items
+
+    def parse_set_expr(self):
+        left = self.parse_set_term()
+        while self.is_kw("union", "except") or (self.is_kw("intersect")):
+            op = self.advance().text.lower()
+            is_all = self.accept_kw("all")
+            if not is_all:
+                self.accept_kw("distinct")
+            right = self.parse_set_term()
+            left = A.SetOp(op, is_all, left, right)
+        return left
+
+    def parse_set_term(self):
+        if self.is_op("("):
+            # parenthesised query
+            save = self.i
+            self.advance()
+            if self.is_kw("select") or self.is_op("("):
+                q = self.parse_query()
+                self.expect_op(")")
+                if q.order_by or q.limit is not None:
+                    return A.SetOp("wrap", True, q, None)
+                return q.body
+            self.i = save
+        return self.parse_select()
+
+    def parse_select(self) -> A.Select:
+        self.expect_kw("select")
+        distinct = self.accept_kw("distinct")
+        if not distinct:
+            self.accept_kw("all")
+        items = []
+        while True:
+            items.append(self.parse_select_item())
+            if not self.accept_op(","):
+                break
+        sel = A.Select(items=items, distinct=distinct)
+        if self.accept_kw("from"):
+            sel.from_ = self.parse_from()
+        if self.accept_kw("where"):
+            sel.where = self.parse_expr()
+        if self.accept_kw("group"):
+            self.expect_kw("by")
+            while True:
+                sel.group_by.append(self.parse_expr())
+                if not self.accept_op(","):
+                    break
+        if self.accept_kw("having"):
+            sel.having = self.parse_expr()
+        return sel
+
+    def parse_select_item(self) -> A.SelectItem:
+        if self.is_op("*"):
+            self.advance()
+            return A.SelectItem(A.Star())
+        # qualified star  a.b.*
+        j = self.i
+        quals = []
+        while self.toks[j].kind in ("id",) and self.toks[j + 1].kind == "op" and self.toks[j + 1].text == ".":
+            quals.append(self.toks[j].text)
+            if self.toks[j + 2].kind == "op" and self.toks[j + 2].text == "*":
+                self.i = j + 3
+                return A.SelectItem(A.Star(tuple(quals)))
+            j += 2
+        e = self.parse_expr()
+        alias = None
+        if self.accept_kw("as"):
+            alias = self.ident()
+        elif self.cur.kind == "id":
+            alias = self.advance().text
+        return A.SelectItem(e, alias)
+
+    def parse_from(self):
+        left = self.parse_table_primary()
+        while True:
+            if self.accept_op(","):
+                right = self.parse_table_primary()
+                left = A.Join(left, right, "cross")
+                continue
+            kind = None
+            save = self.i
+            if self.accept_kw("join"):
+                kind = "inner"
+            elif self.accept_kw("inner"):
+                self.expect_kw("join")
+                kind = "inner"
+            elif self.accept_kw("cross"):
+                self.expect_kw("join")
+                kind = "cross"
+            elif self.is_kw("left", "right", "full"):
+                side = self.advance().text.lower()
+                if side == "left" and self.accept_kw("semi"):
+                    kind = "semi"
+                elif side == "left" and self.accept_kw("anti"):
+                    kind = "anti"
+                else:
+                    self.accept_kw("outer")
+                    kind = side
+                self.expect_kw("join")
+            if kind is None:
+                self.i = save
+                return left
+            right = self.parse_table_primary()
+            on = None
+            using = None
+            if self.accept_kw("on"):
+                on = self.parse_expr()
+            elif self.accept_kw("using"):
+                self.expect_op("(")
+                using = [self.ident()]
+                while self.accept_op(","):
+                    using.append(self.ident())
+                self.expect_op(")")
+            left = A.Join(left, right, kind, on, using)
+
+    def parse_table_primary(self):
+        if self.accept_op("("):
+            q = self.parse_query()
+            self.expect_op(")")
+            alias = None
+            if self.accept_kw("as"):
+                alias = self.ident()
+            elif self.cur.kind == "id":
+                alias = self.advance().text
+            return A.SubqueryRef(q, alias)
+        name = self.ident()
+        while self.accept_op("."):
+            name += "." + self.ident()
+        tw = None
+        if self.accept_kw("timewindow"):
+            self.expect_op("(")
+            t = self.advance()
+            if t.kind != "str":
+                self.error("TIMEWINDOW expects a string literal")
+            tw = t.text
+            self.expect_op(")")
+        alias = None
+        if self.accept_kw("as"):
+            alias = self.ident()
+        elif self.cur.kind == "id":
+            alias = self.advance().text
+        return A.TableRef(name, alias, tw)
+
+    # -- expressions ---------------------------------------------------------------------------------------------
+    def parse_expr(self) -> A.Expr:
+        return self.parse_or()
+
+    def parse_or(self):
+        e = self.parse_and()
+        while self.accept_kw("or"):
+            e = A.BinOp("or", e, self.parse_and())
+        return e
+
+    def parse_and(self):
+        e = self.parse_not()
+        while self.accept_kw("and") or self.accept_op("&&"):
+            e = A.BinOp("and", e, self.parse_not())
+        return e
+
+    def parse_not(self):
+        if self.accept_kw("not") or self.accept_op("!"):
+            return A.UnaryOp("not", self.parse_not())
+        return self.parse_predicate()
+
+    def parse_predicate(self):
+        e = self.parse_bitor()
+        while True:
+            if self.is_op("=", "==", "!=", "<>", "<", "<=", ">", ">=", "<=>"):
+                op = self.advance().text
+                op = {"==": "=", "<>": "!="}.get(op, op)
+                e = A.BinOp(op, e, self.parse_bitor())
+                continue
+            neg = False
+            save = self.i
+            if self.accept_kw("not"):
+                neg = True
+            if self.accept_kw("in"):
+                self.expect_op("(")
+                items = [self.parse_expr()]
+                while self.accept_op(","):
+                    items.append(self.parse_expr())
+                self.expect_op(")")
+                e = A.InList(e, items, neg)
+                continue
+            if self.accept_kw("between"):
+                lo = self.parse_bitor()
+                self.expect_kw("and")
+                hi = self.parse_bitor()
+                e = A.Between(e, lo, hi, neg)
+                continue
+            if self.accept_kw("like"):
+                e = A.Like(e, self.parse_bitor(), neg, False)
+                continue
+            if self.accept_kw("rlike", "regexp"):
+                e = A.Like(e, self.parse_bitor(), neg, True)
+                continue
+            if neg:
+                self.i = save
+                return e
+            if self.accept_kw("is"):
+                n = self.accept_kw("not")
+                if self.accept_kw("null"):
+                    e = A.IsNull(e, n)
+                elif self.accept_kw("true"):
+                    e = A.BinOp("<=>", e, A.Literal(True, "boolean"))
+                    if n:
+                        e = A.UnaryOp("not", e)
+                elif self.accept_kw("false"):
+                    e = A.BinOp("<=>", e, A.Literal(False, "boolean"))
+                    if n:
+                        e = A.UnaryOp("not", e)
+                else:
+                    self.error("expected NULL after IS")
+                continue
+            return e
+
+    def parse_bitor(self):
+        e = self.parse_bitxor()
+        while self.is_op("|") and not self.is_op("||"):
+            self.advance()
+            e = A.BinOp("|", e, self.parse_bitxor())
+        return e
+
+    def parse_bitxor(self):
+        e = self.parse_bitand()
+        while self.accept_op("^"):
+            e = A.BinOp("^", e, self.parse_bitand())
+        return e
+
+    def parse_bitand(self):
+        e = self.parse_additive()
+        while self.accept_op("&"):
+            e = A.BinOp("&", e, self.parse_additive())
+        return e
+
+    def parse_additive(self):
+        e = self.parse_mult()
+        while self.is_op("+", "-", "||"):
+            op = self.advance().text
+            e = A.BinOp(op, e, self.parse_mult())
+        return e
+
+    def parse_mult(self):
+        e = self.parse_unary()
+        while self.is_op("*", "/", "%") or self.is_kw("div"):
+            op = self.advance().text.lower()
+            e = A.BinOp(op, e, self.parse_unary())
+        return e
+
+    def parse_unary(self):
+        if self.is_op("-"):
+            self.advance()
+            operand = self.parse_unary()
+            if isinstance(operand, A.Literal) and operand.type in ("long", "int", "double", "decimal"):
+                return A.Literal(-operand.value, operand.type)
+            return A.UnaryOp("-", operand)
+        if self.accept_op("+"):
+            return self.parse_unary()
+        if self.accept_op("~"):
+            return A.UnaryOp("~", self.parse_unary())
+        return self.parse_postfix()
+
+    def parse_postfix(self):
+        e = self.parse_primary()
+        while True:
+            if self.accept_op("["):
+                idx = self.parse_expr()
+                self.expect_op("]")
+                e = A.Subscript(e, idx)
+            elif self.is_op(".") and not isinstance(e, A.Ident):
+                self.advance()
+                name = self.ident()
+                e = A.Subscript(e, A.Literal(name, "string"), dot=True)
+            else:
+                return e
+
+    def parse_primary(self) -> A.Expr:
+        t = self.cur
+        if t.kind == "num":
+            self.advance()
+            return _number_literal(t.text)
+        if t.kind == "str":
+            self.advance()
+            s = t.text
+            # adjacent string literals concatenate
+            while self.cur.kind == "str":
+                s += self.advance().text
+            return A.Literal(s, "string")
+        if self.is_op("("):
+            self.advance()
+            if self.is_kw("select"):
+                self.error("scalar sub-queries are not supported")
+            e = self.parse_expr()
+            self.expect_op(")")
+            return e
+        if t.kind == "kw":
+            w = t.text.lower()
+            if w == "null":
+                self.advance()
+                return A.Literal(None, "null")
+            if w in ("true", "false"):
+                self.advance()
+                return A.Literal(w == "true", "boolean")
+            if w == "case":
+                return self.parse_case()
+            if w == "cast":
+                self.advance()
+                self.expect_op("(")
+                e = self.parse_expr()
+                self.expect_kw("as")
+                ty = self.parse_type_name()
+                self.expect_op(")")
+                return A.Cast(e, ty)
+            if w == "interval":
+                self.advance()
+                if self.cur.kind == "str":
+                    return A.Interval(parse_duration_micros(self.advance().text))
+                n = self.advance()
+                unit = self.ident()
+                return A.Interval(parse_duration_micros(f"{n.text} {unit}"))
+            if w in ("left", "right", "first", "last") and self.is_op("(", tok=self.peek()):
+                pass  # function named like a keyword
+            elif w not in ("first", "last", "timewindow", "div", "regexp", "semi", "anti", "nulls"):
+                self.error(f"unexpected keyword {t.text}")
+        if t.kind in ("id", "kw"):
+            name = self.advance().text
+            if self.is_op("("):
+                return self.parse_call(name)
+            parts = [name]
+            while self.is_op(".") and self.peek().kind in ("id", "kw") and not self.is_op("*", tok=self.peek()):
+                self.advance()
+                parts.append(self.advance().text)
+            return A.Ident(tuple(parts))
+        self.error("unexpected token")
+
+    def parse_type_name(self) -> str:
+        name = self.ident().lower()
+        if self.accept_op("("):
+            depth = 1
+            while depth:
+                t = self.advance()
+                if t.kind == "eof":
+                    self.error("unterminated type")
+                if self.is_op("(", tok=t):
+                    depth += 1
+                elif self.is_op(")", tok=t):
+                    depth -= 1
+        return {"integer": "int", "bigint": "long", "smallint": "int", "tinyint": "int", "real": "float",
+                "varchar": "string", "char": "string", "text": "string", "bool": "boolean",
+                "numeric": "decimal", "dec": "decimal"}.get(name, name)
+
+    def parse_case(self):
+        self.expect_kw("case")
+        operand = None
+        if not self.is_kw("when"):
+            operand = self.parse_expr()
+        whens = []
+        while self.accept_kw("when"):
+            c = self.parse_expr()
+            self.expect_kw("then")
+            whens.append((c, self.parse_expr()))
+        default = None
+        if self.accept_kw("else"):
+            default = self.parse_expr()
+        self.expect_kw("end")
+        return A.Case(operand, whens, default)
+
+    def parse_call(self, name):
+        self.expect_op("(")
+        low = name.lower()
+        if self.accept_op(")"):
+            return A.Call(low, [])
+        if self.is_op("*") and self.is_op(")", tok=self.peek()):
+            self.advance()
+            self.advance()
+            return A.Call(low, [], star=True)
+        distinct = self.accept_kw("distinct")
+        args = [self.parse_expr()]
+        while self.accept_op(","):
+            args.append(self.parse_expr())
+        self.expect_op(")")
+        return A.Call(low, args, distinct=distinct)
+
+
+def _number_literal(text: str) -> A.Literal:
+    up = text.upper()
+    if up.endswith("BD"):
+        return A.Literal(float(text[:-2]), "double")
+    suffix = up[-1]
+    if suffix in "LSY":
+        return A.Literal(int(text[:-1]), "long")
+    if suffix == "D":
+        return A.Literal(float(text[:-1]), "double")
+    if any(c in text for c in ".eE"):
+        return A.Literal(float(text), "double")
+    v = int(text)
+    return A.Literal(v, "int" if -2**31 <= v < 2**31 else "long")
+
+
+def parse_query(sql: str) -> A.Query:
+    p = Parser(sql.strip().rstrip(";"))
+    q = p.parse_query()
+    if p.cur.kind != "eof":
+        p.error("unexpected trailing input")
+    return q
+
+
+def parse_expression(sql: str) -> A.Expr:
+    p = Parser(sql)
+    e = p.parse_expr()
+    if p.cur.kind != "eof":
+        p.error("unexpected trailing input")
+    return e
+
+
+def parse_select_item(sql: str) -> A.SelectItem:
+    """One projection line (reference projection files hold one ``selectExpr`` per line,
+    DataProcessing/datax-host/src/main/scala/datax/handler/ProjectionHandler.scala:23-36)."""
+    p = Parser(sql)
+    it = p.parse_select_item()
+    if p.cur.kind != "eof":
+        p.error("unexpected trailing input")
+    return it
