@@ -476,6 +476,12 @@ class Table:
         self.length = int(length)
         self._device = torch.device(device) if device is not None else (
             columns[0].device if columns else torch.device("cpu"))
+        self.dist = "replicated"     # distribution across ranks (see dxa.parallel)
+
+    def _like(self, names, cols, length) -> "Table":
+        t = Table(names, cols, length, self._device)
+        t.dist = self.dist
+        return t
 
     @property
     def device(self):
@@ -505,7 +511,7 @@ class Table:
         return StructType(tuple(StructField(n, c.dtype) for n, c in zip(self.names, self.columns)))
 
     def take(self, idx: torch.Tensor) -> "Table":
-        return Table(self.names, [c.take(idx) for c in self.columns], int(idx.shape[0]), self._device)
+        return self._like(self.names, [c.take(idx) for c in self.columns], int(idx.shape[0]))
 
     def filter(self, mask: torch.Tensor) -> "Table":
         idx = torch.nonzero(mask, as_tuple=False).flatten()
@@ -516,7 +522,7 @@ class Table:
         return self.take(idx)
 
     def select(self, names: List[str]) -> "Table":
-        return Table(names, [self.column(n) for n in names], self.length, self._device)
+        return self._like(names, [self.column(n) for n in names], self.length)
 
     def with_column(self, name: str, col: Column) -> "Table":
         i = self.index_of(name)
@@ -526,7 +532,7 @@ class Table:
         else:
             names.append(name)
             cols.append(col)
-        return Table(names, cols, self.length, self._device)
+        return self._like(names, cols, self.length)
 
     def to(self, device) -> "Table":
         return Table(self.names, [c.to(device) for c in self.columns], self.length, device)

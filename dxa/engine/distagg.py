@@ -1,0 +1,177 @@
+"""Distributed GROUP BY (two-phase over RCCL) for partitioned inputs — see ``dxa.parallel``.
+
+Phase 1 (rank-local): group the rank's rows and compute *partial* states of every aggregate (count, sum, min, max,
+sum of squares …).  Phase 2: route each partial group to ``hash(keys) % world`` with one all-to-all, re-group on the
+owner and *merge* the partial states.  Aggregates that have no mergeable partial state (COUNT DISTINCT,
+collect_list/set, user UDAFs) fall back to shuffling the input rows by key hash and aggregating once on the owner —
+still one exchange, just a bigger one.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .. import parallel as P
+from ..ops import groupby as G
+from ..ops.hashing import hash_columns
+from ..sql import ast as A
+from .column import ConstColumn, PrimColumn, Table, materialize
+
+DECOMPOSABLE = {"count", "sum", "min", "max", "avg", "mean", "first", "last", "first_value", "last_value",
+                "stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std", "count_if",
+                "bool_and", "bool_or", "every", "any", "some"}
+
+
+def decomposable(calls: Dict, ctx) -> bool:
+    for call in calls.values():
+        if call.name in ctx.udafs or call.distinct or call.name not in DECOMPOSABLE:
+            return False
+    return True
+
+
+def _partials(call: A.Call, scope, groups: G.Groups, ctx) -> List[Tuple[str, PrimColumn, str]]:
+    """[(partial name suffix, partial column, merge op)] for one aggregate call."""
+    from .expr import evaluate, predicate_mask
+    n = scope.length
+    name = call.name
+    if call.star or (name == "count" and not call.args):
+        return [("cnt", G.aggregate(groups, None, "count_star", n), "sum")]
+    arg = materialize(evaluate(call.args[0], scope, ctx))
+    if isinstance(arg, ConstColumn):
+        arg = arg.materialize()
+    if name == "count":
+        return [("cnt", G.aggregate(groups, arg, "count", n), "sum")]
+    if name == "count_if":
+        m = predicate_mask(arg)
+        return [("cnt", G.aggregate(groups, PrimColumn("long", m.to(torch.int64)), "sum", n), "sum")]
+    if name in ("bool_and", "every", "bool_or", "any", "some"):
+        r = G.aggregate(groups, PrimColumn("long", arg.data.to(torch.int64), arg.valid),
+                        "min" if name in ("bool_and", "every") else "max", n)
+        return [("v", r, "min" if name in ("bool_and", "every") else "max")]
+    if name in ("first", "first_value", "last", "last_value"):
+        f = "first" if name.startswith("first") else "last"
+        return [("v", G.aggregate(groups, arg, f, n), f)]
+    cnt = G.aggregate(groups, arg, "count", n)
+    if name in ("sum", "min", "max"):
+        return [("v", G.aggregate(groups, arg, name, n), name), ("cnt", cnt, "sum")]
+    if name in ("avg", "mean"):
+        x = PrimColumn("double", arg.data.to(torch.float64), arg.valid)
+        return [("s", G.aggregate(groups, x, "sum", n), "sum"), ("cnt", cnt, "sum")]
+    # variance family: sum, sum of squares, count
+    x = arg.data.to(torch.float64)
+    return [("s", G.aggregate(groups, PrimColumn("double", x, arg.valid), "sum", n), "sum"),
+            ("s2", G.aggregate(groups, PrimColumn("double", x * x, arg.valid), "sum", n), "sum"),
+            ("cnt", cnt, "sum")]
+
+
+def _finish(call: A.Call, merged: Dict[str, PrimColumn]) -> PrimColumn:
+    name = call.name
+    if "v" in merged:
+        v = merged["v"]
+        if name in ("bool_and", "every", "bool_or", "any", "some"):
+            return PrimColumn("boolean", v.data != 0, v.valid)
+        if "cnt" in merged:
+            return v.with_valid(merged["cnt"].data > 0)
+        return v
+    if set(merged) == {"cnt"}:
+        c = merged["cnt"]
+        return PrimColumn("long", c.data, None)
+    c = merged["cnt"].data.to(torch.float64)
+    s = merged["s"].data
+    if name in ("avg", "mean"):
+        return PrimColumn("double", s / c.clamp(min=1), c > 0)
+    s2 = merged["s2"].data
+    mean = s / c.clamp(min=1)
+    m2 = (s2 - c * mean * mean).clamp(min=0)
+    pop = name.endswith("_pop")
+    var = m2 / (c if pop else (c - 1)).clamp(min=1)
+    out = var.sqrt() if name.startswith("std") else var
+    return PrimColumn("double", out, c > (0 if pop else 1))
+
+
+def distributed_aggregate(gexprs, keys, aggs: Dict, scope, ctx):
+    """Returns (key columns, {agg key → final column}, ngroups, dist tag)."""
+    from .expr import evaluate
+    dev = scope.device
+    n = scope.length
+    if gexprs:
+        groups = G.group_rows(keys)
+    else:
+        groups = G.Groups(torch.zeros(n, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
+                          torch.zeros(1, dtype=torch.int64, device=dev))
+    names: List[str] = []
+    cols = []
+    key_names = []
+    for i, k in enumerate(keys):
+        nm = f"__k{i}"
+        key_names.append(nm)
+        names.append(nm)
+        cols.append(k.take(groups.rep) if groups.ngroups and n else k.take(groups.rep[:0]))
+    plan = {}
+    for ak, call in aggs.items():
+        parts = _partials(call, scope, groups, ctx)
+        plan[ak] = []
+        for suffix, col, op in parts:
+            nm = f"__a{len(plan)}_{suffix}"
+            plan[ak].append((nm, suffix, op))
+            names.append(nm)
+            cols.append(col)
+    ng_local = groups.ngroups if (gexprs or n) else 0
+    if not gexprs and n == 0:
+        # an empty rank contributes no partial row
+        cols = [c.take(torch.empty(0, dtype=torch.int64, device=dev)) for c in cols]
+        ng_local = 0
+    partial = Table(names, cols, ng_local, dev)
+    if gexprs:
+        dest = P.owner_of(hash_columns([partial.column(k) for k in key_names])) if ng_local else \
+            torch.empty(0, dtype=torch.int64, device=dev)
+        got = P.shuffle_table(partial, dest)
+        tag = P.HASHED
+    else:
+        got = P.allgather_table(partial)
+        tag = P.REPLICATED
+    m = got.length
+    if gexprs:
+        g2 = G.group_rows([got.column(k) for k in key_names]) if m else G.Groups(
+            torch.empty(0, dtype=torch.int64, device=dev), 0, torch.empty(0, dtype=torch.int64, device=dev))
+    else:
+        g2 = G.Groups(torch.zeros(m, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
+                      torch.zeros(1, dtype=torch.int64, device=dev))
+    ng = g2.ngroups
+    out_keys = [got.column(k).take(g2.rep) for k in key_names] if gexprs else []
+    finals = {}
+    for ak, call in aggs.items():
+        merged = {}
+        for nm, suffix, op in plan[ak]:
+            c = got.column(nm)
+            if m == 0:
+                merged[suffix] = _empty_merge(c, op, ng, dev)
+            else:
+                merged[suffix] = G.aggregate(g2, c, op, m)
+        finals[ak] = _finish(call, merged)
+    return out_keys, finals, ng, tag
+
+
+def _empty_merge(c, op, ng, dev):
+    if op == "sum":
+        return PrimColumn(c.dtype, torch.zeros(ng, dtype=c.data.dtype if hasattr(c, "data") else torch.int64,
+                                               device=dev))
+    return PrimColumn(c.dtype, torch.zeros(ng, dtype=c.data.dtype if hasattr(c, "data") else torch.int64,
+                                           device=dev), torch.zeros(ng, dtype=torch.bool, device=dev))
+
+
+def shuffle_rows_by_keys(scope, keys, ctx):
+    """Non-decomposable fallback: route input rows to the owner of their key hash."""
+    from .expr import Scope
+    dev = scope.device
+    names = [f"__c{i}" for i in range(len(scope.cols))] + [f"__k{i}" for i in range(len(keys))]
+    t = Table(names, list(scope.cols) + list(keys), scope.length, dev)
+    if keys:
+        dest = P.owner_of(hash_columns(keys)) if scope.length else torch.empty(0, dtype=torch.int64, device=dev)
+        got = P.shuffle_table(t, dest)
+    else:
+        got = P.allgather_table(t)
+    nc = len(scope.cols)
+    new_scope = Scope(scope.names, got.columns[:nc], scope.quals, got.length, dev)
+    return new_scope, got.columns[nc:]

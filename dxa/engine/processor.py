@@ -1,0 +1,273 @@
+"""The micro-batch executor: raw events → projected table → windowed views / state tables / transform SQL →
+outputs + metrics.  This is the reference's ``CommonProcessorFactory`` (DataProcessing/datax-host/src/main/scala/
+datax/processor/CommonProcessorFactory.scala:42-660) re-designed for one MI355X per process:
+
+* the raw batch arrives as ONE device byte buffer + record offsets (``RawBatch``); JSON parsing, projection,
+  every transform statement and the window/state bookkeeping run on device columns;
+* views are materialised once per batch and dropped at batch end (the reference caches views referenced more than
+  once — every view here is already materialised, so that is free);
+* outputs serialise on the host thread pool; metrics use the reference's names (``Input_DataXProcessedInput_Events_
+  Count``, ``Latency-Process``, ``Latency-Batch``, ``Output_<name>_Sink_*``);
+* multi-GPU: ``dxa.parallel`` hooks the group-by / distinct / join operators with RCCL exchanges (see
+  ``dxa.parallel.distributed``) — the processor itself is rank-local.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import logging
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from .. import parallel as P
+from ..config import settings as S
+from ..config.secrets import resolve
+from ..io import fs
+from ..ops.jsonparse import ParsePlan, parse
+from ..sql.transform import COMMAND_COMMAND, parse_transform
+from .column import ConstColumn, PrimColumn, StructColumn, Table, concat_tables
+from .expr import EvalContext, EvalError
+from .query import Catalog, execute, run_sql
+from .serialize import table_to_json_lines
+from .state import create_state_tables
+from .types import MapType, StructType, schema_from_json
+from .windows import TimeWindowConf, WindowStore
+
+log = logging.getLogger("dxa.processor")
+
+
+@dataclass
+class RawBatch:
+    """One micro-batch of raw event payloads resident on the device."""
+    buf: torch.Tensor            # uint8, 16-byte padded
+    offs: torch.Tensor           # int64 [n+1]
+    n: int
+    properties: Optional[Any] = None          # per-event Properties map column (or None → {})
+    system_properties: Optional[Any] = None   # per-event SystemProperties map column (or None → {})
+    file_info: Optional[Dict[str, Any]] = None
+    source_bytes: int = 0
+
+
+def _read_lines(path: str) -> List[str]:
+    return fs.read_lines(resolve(path))
+
+
+class Processor:
+    def __init__(self, settings: S.SettingDictionary, device="cpu", metric_store=None, udfs=None, udafs=None,
+                 normalizer=None, pre_projection=None, parse_prune: bool = True):
+        self.settings = settings
+        self.device = torch.device(device)
+        self.name = settings.job_name()
+        d = settings
+        # ---- input schema + projection + transform
+        schema_ref = d.get(S.INPUT_PREFIX + "blobschemafile")
+        if schema_ref is None:
+            raise S.SettingError("datax.job.input.default.blobschemafile is required")
+        schema_text = resolve(schema_ref)
+        if not schema_text.lstrip().startswith("{"):
+            schema_text = fs.read_text(schema_text)
+        self.raw_schema: StructType = schema_from_json(schema_text)
+        self.projections: List[List[str]] = []
+        for p in d.get_string_seq(S.PROCESS_PREFIX + "projection") or []:
+            lines = [l.strip().rstrip(",") for l in _read_lines(p) if l.strip() and not l.strip().startswith("--")]
+            self.projections.append([l.lstrip("﻿") for l in lines])
+        self.transform = None
+        tpath = d.get(S.PROCESS_PREFIX + "transform")
+        if tpath:
+            self.transform = parse_transform(_read_lines(tpath))
+        self.windows = TimeWindowConf.from_settings(d)
+        self.window_store = WindowStore(self.windows) if self.windows.enabled else None
+        self.state_tables = create_state_tables(d, self.device)
+        # ---- extensions
+        from ..udf.registry import build_udfs
+        self.udfs, self.udafs, self.udf_refreshers = build_udfs(d, udfs or {}, udafs or {})
+        self.normalizer = normalizer
+        self.pre_projection = pre_projection
+        self.append_props = {k: v for k, v in d.sub_dictionary(S.PROCESS_PREFIX + "appendproperty.").items()}
+        # ---- reference data (resident across batches: stream–static joins build their hash tables once)
+        self.reference: Dict[str, Table] = self._load_reference_data()
+        # ---- outputs + metrics
+        from ..io.sinks import build_outputs
+        from ..telemetry.metrics import MetricLogger
+        self.outputs = build_outputs(d)
+        self.metric_logger = MetricLogger.from_settings(d, metric_store)
+        self.parse_plan = ParsePlan(self.raw_schema, self._needed_raw_paths() if parse_prune else None)
+        self.batches = 0
+        self.last_metrics: Dict[str, float] = {}
+        self.last_views: Dict[str, Table] = {}
+        self.keep_views = False
+        self.stage_times: Dict[str, float] = {}
+
+    # ------------------------------------------------------------------------------------------------------------
+    def _load_reference_data(self) -> Dict[str, Table]:
+        out = {}
+        for name, sub in self.settings.group_by_sub_namespace(S.INPUT_PREFIX + "referencedata.").items():
+            fmt = (sub.get("format") or "csv").lower()
+            path = resolve(sub.get_string("path"))
+            if fmt not in ("csv", "tsv"):
+                raise ValueError(f"unsupported reference data format {fmt}")
+            from ..io.refdata import load_csv
+            out[name] = load_csv(path, sub.get("delimiter") or ("\t" if fmt == "tsv" else ","),
+                                 (sub.get("header") or "true").lower() == "true", self.device)
+        return out
+
+    def _needed_raw_paths(self):
+        """Projection pushdown into the JSON parser: which ``Raw`` leaves can any statement reference?
+
+        Conservative: if any projection line / statement / output could see the whole Raw struct (``Raw``,
+        ``Raw.*`` followed by ``*`` downstream, to_json of rows, …) we keep everything."""
+        import re
+        texts = [l for p in self.projections for l in p]
+        if not texts:
+            return None
+        if any(re.search(r"\bRaw\s*\.\s*\*", t) for t in texts):
+            # Raw.* expands every field into the projected table: keep all leaves unless SQL proves otherwise
+            return None
+        keep = set()
+        for t in texts:
+            for m in re.finditer(r"\bRaw((?:\s*\.\s*[A-Za-z_`][A-Za-z0-9_`]*)+)", t):
+                parts = tuple(p.strip().strip("`") for p in m.group(1).split(".") if p.strip())
+                keep.add(parts)
+            if re.search(r"\bRaw\b(?!\s*\.)", t):
+                return None
+        return keep or None
+
+    # ------------------------------------------------------------------------------------------------------------
+    def project(self, raw: RawBatch, batch_time_us: int, ctx: EvalContext) -> Table:
+        t0 = time.perf_counter()
+        buf = raw.buf
+        if self.normalizer is not None:
+            buf = self.normalizer(buf, raw.offs)
+        raw_col, row_ok = parse(buf, raw.offs, self.parse_plan)
+        self.stage_times["parse"] = time.perf_counter() - t0
+        n = raw.n
+        dev = self.device
+        empty_map = MapType("string", "string")
+        props = raw.properties if raw.properties is not None else ConstColumn({}, empty_map, n, dev)
+        sysprops = raw.system_properties if raw.system_properties is not None else ConstColumn({}, empty_map, n, dev)
+        pp = dict(self.append_props)
+        pp.update({"BatchTime": _fmt_ts(batch_time_us), "CPTime": _fmt_ts(int(time.time() * 1e6)),
+                   "CPExecutor": str(torch.cuda.current_device() if dev.type == "cuda" else "driver")})
+        if raw.file_info:
+            pp["InputTime"] = str(raw.file_info.get("fileTime", ""))
+            pp["Partition"] = str(raw.file_info.get("outputFileName", ""))
+        names = ["Raw", "Properties", "SystemProperties", f"{S.NAME_PREFIX}Properties"]
+        cols = [raw_col, props, sysprops, ConstColumn(pp, empty_map, n, dev)]
+        internal = f"__{S.NAME_PREFIX}_"
+        if raw.file_info:
+            names.append(f"{internal}FileInfo")
+            cols.append(ConstColumn(dict(raw.file_info), empty_map, n, dev))
+        table = Table(names, cols, n, dev)
+        if self.pre_projection is not None:
+            table = self.pre_projection(table, ctx)
+        for step in self.projections:
+            preserved = [nm for nm in table.names if nm.startswith(internal)]
+            cat = Catalog()
+            cat.register("__dxa_input", table)
+            items = step + [f"`{p}`" for p in preserved if not any(p in s for s in step)]
+            table = run_sql("SELECT " + ", ".join(items) + " FROM __dxa_input", cat, ctx)
+        self.stage_times["project"] = time.perf_counter() - t0
+        return table
+
+    def route(self, projected: Table, batch_time_us: int, interval_us: int, ctx: EvalContext,
+              partition_time: _dt.datetime) -> Dict[str, float]:
+        metrics: Dict[str, float] = {}
+        base = f"{S.NAME_PREFIX}ProcessedInput"
+        cat = Catalog()
+        for name, t in self.reference.items():
+            cat.register(name, t)
+        cat._built = getattr(self, "_ref_built", {})
+        self._ref_built = cat._built
+        metrics["Input_Normalized_Events_Count"] = projected.length
+        part = P.PARTITIONED if P.active() else P.REPLICATED
+        projected.dist = part
+        if self.window_store is not None:
+            views, cnt = self.window_store.process(projected, batch_time_us, interval_us)
+            for k, v in views.items():
+                v.dist = part
+                cat.register(k, v)
+            metrics[f"Input_{base}_Events_Count"] = cnt
+        else:
+            cat.register(base, projected)
+            metrics[f"Input_{base}_Events_Count"] = projected.length
+        for name, st in self.state_tables.items():
+            cat.register(name, st.active)
+        views: Dict[str, Table] = {}
+        t0 = time.perf_counter()
+        if self.transform is not None:
+            from ..sql.parser import parse_query
+            for cmd in self.transform.commands:
+                if cmd.command_type == COMMAND_COMMAND:
+                    self._run_command(cmd.text)
+                    continue
+                q = parse_query(cmd.text)
+                result = execute(q, cat, ctx)
+                st = self.state_tables.get(cmd.name)
+                if st is not None:
+                    result = st.overwrite(result)
+                cat.register(cmd.name, result)
+                views[cmd.name] = result
+        self.stage_times["transform"] = time.perf_counter() - t0
+        # outputs (in parallel on the host pool)
+        t1 = time.perf_counter()
+        futures = []
+        from ..io.sinks import _pool
+        for op in self.outputs:
+            t = views.get(op.name) or cat.get(op.name)
+            if t is None:
+                raise EvalError(f"could not find data set name '{op.name}' for output '{op.name}'")
+            if P.active() and P.dist_of(t) == P.REPLICATED and P.rank() != 0:
+                t = t.slice(0, 0)      # replicated results are written once, by rank 0
+            futures.append((op.name, _pool.submit(op.output, t, partition_time, ctx)))
+        for name, f in futures:
+            for k, v in f.result().items():
+                metrics[f"Output_{name}_{k}"] = float(v)
+        if P.active():
+            # batch metrics are job-wide: one all-reduce of the count vector (timings stay per-rank)
+            keys = sorted(metrics)
+            vec = torch.tensor([float(metrics[k]) for k in keys], dtype=torch.float64, device=self.device)
+            P.all_reduce_sum(vec)
+            metrics = dict(zip(keys, vec.tolist()))
+        self.stage_times["output"] = time.perf_counter() - t1
+        for st in self.state_tables.values():
+            st.persist()
+        if self.keep_views:
+            self.last_views = {**{k: cat.get(k) for k in cat.names()}, **views}
+        return metrics
+
+    def _run_command(self, text: str):
+        low = text.strip().lower()
+        if low.startswith(("set ", "cache ", "uncache ", "refresh ", "clear cache")) or not low:
+            return
+        raise EvalError(f"unsupported command statement: {text}")
+
+    def process_batch(self, raw: RawBatch, batch_time_us: int, interval_us: int,
+                      partition_time: Optional[_dt.datetime] = None) -> Dict[str, float]:
+        t0 = time.perf_counter()
+        ctx = EvalContext(now_us=int(time.time() * 1e6), udfs=self.udfs, udafs=self.udafs, device=self.device)
+        for refresh in self.udf_refreshers:
+            refresh(batch_time_us)
+        try:
+            projected = self.project(raw, batch_time_us, ctx)
+            metrics = self.route(projected, batch_time_us, interval_us, ctx,
+                                 partition_time or _dt.datetime.utcnow())
+            metrics["Latency-Process"] = time.perf_counter() - t0
+            metrics["Latency-Batch"] = (time.time() * 1e6 - batch_time_us) / 1e6
+            if P.rank() == 0:
+                self.metric_logger.send_batch_metrics(metrics, batch_time_us // 1000)
+            self.last_metrics = metrics
+            self.batches += 1
+            return metrics
+        except Exception:
+            log.exception("batch %s failed", batch_time_us)
+            from ..telemetry.appinsights import track_exception
+            track_exception("ProcessDataFrame", batch_time_us)
+            raise
+
+
+def _fmt_ts(us: int) -> str:
+    t = _dt.datetime(1970, 1, 1) + _dt.timedelta(microseconds=int(us))
+    return t.strftime("%Y-%m-%d %H:%M:%S.") + f"{t.microsecond // 1000:03d}"

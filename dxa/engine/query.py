@@ -13,6 +13,8 @@ import torch
 
 from ..ops import groupby as G
 from ..ops import join as J
+from .. import parallel as P
+from ..ops.hashing import hash_columns
 from ..sql import ast as A
 from ..sql.parser import parse_query
 from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, Table, concat_columns,
@@ -59,8 +61,18 @@ def run_sql(sql: str, catalog: Catalog, ctx: EvalContext) -> Table:
     return execute(parse_query(sql), catalog, ctx)
 
 
+def _gathered(t: Table) -> Table:
+    g = P.allgather_table(t)
+    g.dist = P.REPLICATED
+    return g
+
+
 def execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
     out, src_scope = _exec_body(q.body, catalog, ctx, want_scope=bool(q.order_by))
+    if (q.order_by or q.limit is not None) and P.active() and P.dist_of(out) != P.REPLICATED:
+        # a total order / global LIMIT needs every row: gather (outputs of this shape are small in DataX flows)
+        out = _gathered(out)
+        src_scope = None
     if q.order_by:
         out = _order_by(out, q.order_by, ctx, src_scope)
     if q.limit is not None:
@@ -105,9 +117,21 @@ def _align(left: Table, right: Table) -> Tuple[Table, Table]:
 
 
 def _set_op(op: A.SetOp, left: Table, right: Table) -> Table:
+    ld, rd = P.dist_of(left), P.dist_of(right)
     left, right = _align(left, right)
+    if P.active() and (ld != P.REPLICATED) != (rd != P.REPLICATED):
+        # mixing a partitioned and a replicated input: keep the replicated rows once (on rank 0)
+        if ld == P.REPLICATED and P.rank() != 0:
+            left = left.slice(0, 0)
+        if rd == P.REPLICATED and P.rank() != 0:
+            right = right.slice(0, 0)
+    if P.active() and op.op != "union" and (ld != P.REPLICATED or rd != P.REPLICATED):
+        left = _gathered(left) if ld != P.REPLICATED else left
+        right = _gathered(right) if rd != P.REPLICATED else right
+        ld = rd = P.REPLICATED
     if op.op == "union":
         out = concat_tables([left, right])
+        out.dist = P.REPLICATED if (ld == P.REPLICATED and rd == P.REPLICATED) else P.PARTITIONED
         return out if op.all else distinct(out)
     # INTERSECT / EXCEPT (distinct semantics)
     l, r = distinct(left), distinct(right)
@@ -121,6 +145,17 @@ def _set_op(op: A.SetOp, left: Table, right: Table) -> Table:
 
 
 def distinct(t: Table) -> Table:
+    if P.active() and P.dist_of(t) != P.REPLICATED and t.columns:
+        keys = [c if not isinstance(c, (StructColumn, ArrayColumn)) else _nested_key(c) for c in t.columns]
+        dest = P.owner_of(hash_columns(keys)) if t.length else torch.empty(0, dtype=torch.int64, device=t.device)
+        t = P.shuffle_table(t, dest)
+        out = _local_distinct(t)
+        out.dist = P.HASHED
+        return out
+    return _local_distinct(t)
+
+
+def _local_distinct(t: Table) -> Table:
     if t.length == 0 or not t.columns:
         return t
     keys = [c for c in t.columns]
@@ -141,7 +176,9 @@ def distinct(t: Table) -> Table:
 
 def _relation(src, catalog: Catalog, ctx: EvalContext) -> Scope:
     if src is None:
-        return Scope([], [], [], 1, ctx.device)
+        sc = Scope([], [], [], 1, ctx.device)
+        sc.dist = P.REPLICATED
+        return sc
     if isinstance(src, A.TableRef):
         name = src.name
         if src.timewindow:
@@ -150,10 +187,14 @@ def _relation(src, catalog: Catalog, ctx: EvalContext) -> Scope:
         t = catalog.get(name)
         if t is None:
             raise QueryError(f"table or view not found: {name}")
-        return Scope.of_table(t, src.alias or src.name.split(".")[-1])
+        sc = Scope.of_table(t, src.alias or src.name.split(".")[-1])
+        sc.dist = P.dist_of(t)
+        return sc
     if isinstance(src, A.SubqueryRef):
         t = execute(src.query, catalog, ctx)
-        return Scope.of_table(t, src.alias)
+        sc = Scope.of_table(t, src.alias)
+        sc.dist = P.dist_of(t)
+        return sc
     if isinstance(src, A.Join):
         return _join(src, catalog, ctx)
     raise QueryError(f"unsupported FROM item {type(src).__name__}")
@@ -198,6 +239,22 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
                 continue
         residual.append(c)
     kind = j.kind
+    ldist, rdist = getattr(left, "dist", P.REPLICATED), getattr(right, "dist", P.REPLICATED)
+    out_dist = P.REPLICATED
+    if P.active() and (ldist != P.REPLICATED or rdist != P.REPLICATED):
+        if ldist != P.REPLICATED and rdist != P.REPLICATED and lkeys:
+            # co-partition both sides by the join-key hash (Spark's shuffle hash join)
+            left = _shuffle_scope(left, [materialize(evaluate(e, left, ctx)) for e in lkeys])
+            right = _shuffle_scope(right, [materialize(evaluate(e, right, ctx)) for e in rkeys], ref=left)
+            out_dist = P.HASHED
+        elif ldist != P.REPLICATED and kind in ("inner", "left", "semi", "anti", "cross"):
+            out_dist = ldist            # partitioned ⨝ replicated: rank-local
+        elif rdist != P.REPLICATED and kind in ("inner", "right", "cross"):
+            out_dist = rdist
+        else:
+            left = _gather_scope(left) if ldist != P.REPLICATED else left
+            right = _gather_scope(right) if rdist != P.REPLICATED else right
+        n_l, n_r = left.length, right.length
     if kind == "cross" or (not lkeys):
         if kind not in ("cross", "inner"):
             raise QueryError(f"{kind} join without equi-join keys is not supported")
@@ -211,7 +268,9 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         lk, rk = _coerce_keys(lk, rk)
         li, ri = J.hash_join(lk, rk, kind if kind != "cross" else "inner")
     if kind in ("semi", "anti"):
-        return Scope(left.names, [c.take(li) for c in left.cols], left.quals, int(li.shape[0]), dev)
+        out = Scope(left.names, [c.take(li) for c in left.cols], left.quals, int(li.shape[0]), dev)
+        out.dist = out_dist
+        return out
     cols = []
     for c in left.cols:
         cols.append(_take_nullable(c, li))
@@ -225,6 +284,24 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
             pred = m if pred is None else pred & m
         idx = torch.nonzero(pred).flatten()
         out = Scope(out.names, [c.take(idx) for c in out.cols], out.quals, int(idx.shape[0]), dev)
+    out.dist = out_dist
+    return out
+
+
+def _shuffle_scope(scope: Scope, keys, ref=None) -> Scope:
+    """Repartition a scope's rows by the hash of ``keys`` (RCCL all-to-all)."""
+    from .distagg import shuffle_rows_by_keys
+    keys, _ = _coerce_keys(keys, keys)
+    new_scope, _ = shuffle_rows_by_keys(scope, keys, None)
+    new_scope.dist = P.HASHED
+    return new_scope
+
+
+def _gather_scope(scope: Scope) -> Scope:
+    t = Table([f"__c{i}" for i in range(len(scope.cols))], scope.cols, scope.length, scope.device)
+    g = P.allgather_table(t)
+    out = Scope(scope.names, g.columns, scope.quals, g.length, scope.device)
+    out.dist = P.REPLICATED
     return out
 
 
@@ -301,10 +378,12 @@ def _dup(scope: Scope, nm: str) -> bool:
 
 def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     scope = _relation(sel.from_, catalog, ctx)
+    sdist = getattr(scope, "dist", P.REPLICATED)
     if sel.where is not None:
         mask = predicate_mask(evaluate(sel.where, scope, ctx))
         idx = torch.nonzero(mask).flatten()
         scope = Scope(scope.names, [c.take(idx) for c in scope.cols], scope.quals, int(idx.shape[0]), scope.device)
+        scope.dist = sdist
     items = _expand_items(sel, scope)
     is_agg = bool(sel.group_by) or any(_contains_agg(e, ctx) for e, _ in items) or (
         sel.having is not None and _contains_agg(sel.having, ctx))
@@ -314,6 +393,7 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     else:
         cols = [evaluate(e, scope, ctx) for e, _ in items]
         out = Table([nm for _, nm in items], cols, scope.length, scope.device)
+        out.dist = sdist
         src = scope
     if sel.distinct:
         out = distinct(out)
@@ -336,9 +416,13 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
     dev = scope.device
     n = scope.length
     gexprs = [_resolve_group_expr(g, scope, items) for g in sel.group_by]
+    keys = []
     if gexprs:
         keys = [materialize(evaluate(g, scope, ctx)) for g in gexprs]
         keys = [k if not isinstance(k, (StructColumn, ArrayColumn)) else _nested_key(k) for k in keys]
+    if P.active() and getattr(scope, "dist", P.REPLICATED) != P.REPLICATED:
+        return _aggregate_distributed(sel, items, scope, ctx, gexprs, keys)
+    if gexprs:
         groups = G.group_rows(keys)
     else:
         # global aggregate: one group, even over zero rows
@@ -362,6 +446,37 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
     if sel.having is not None:
         m = predicate_mask(evaluate(sel.having, rep_scope, ctx, subst))
         out = out.filter(m)
+    return out
+
+
+def _aggregate_distributed(sel, items, scope, ctx, gexprs, keys) -> Table:
+    """GROUP BY over a partitioned input: two-phase RCCL aggregation (or a key shuffle for non-mergeable aggregates).
+    Select expressions may only use group expressions and aggregates (Spark's rule)."""
+    from . import distagg as D
+    dev = scope.device
+    aggs: Dict = {}
+    for e, _ in items:
+        _collect_aggs(e, ctx, aggs)
+    if sel.having is not None:
+        _collect_aggs(sel.having, ctx, aggs)
+    if D.decomposable(aggs, ctx):
+        out_keys, finals, ng, tag = D.distributed_aggregate(gexprs, keys, aggs, scope, ctx)
+        subst = dict(finals)
+        for g, k in zip(gexprs, out_keys):
+            subst[g.key()] = k
+        empty = Scope([], [], [], ng, dev)
+        cols = [evaluate(e, empty, ctx, subst) for e, _ in items]
+        out = Table([nm for _, nm in items], cols, ng, dev)
+        if sel.having is not None:
+            out = out.filter(predicate_mask(evaluate(sel.having, empty, ctx, subst)))
+        out.dist = tag
+        return out
+    # non-decomposable: move rows to their key owner, then aggregate locally
+    new_scope, new_keys = D.shuffle_rows_by_keys(scope, keys, ctx)
+    new_scope.dist = P.REPLICATED    # rows of a key now live on one rank: local aggregation is exact
+    sel2 = A.Select(sel.items, None, None, sel.group_by, sel.having, False)
+    out = _aggregate(sel2, items, new_scope, ctx)
+    out.dist = P.HASHED if gexprs else P.REPLICATED
     return out
 
 

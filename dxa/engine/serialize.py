@@ -127,6 +127,13 @@ def column_json_values(col: Column) -> List[Optional[str]]:
 
 
 def table_to_json_lines(t: Table) -> List[str]:
+    from ..ops import serialize as native_ser
+    if native_ser.available():
+        return native_ser.table_lines(t)
+    return table_to_json_lines_py(t)
+
+
+def table_to_json_lines_py(t: Table) -> List[str]:
     cols = [(_jstr(nm), _frag_values(c)) for nm, c in zip(t.names, t.columns)]
     out = []
     for i in range(t.length):

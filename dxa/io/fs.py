@@ -1,0 +1,87 @@
+"""Filesystem helpers (the reference's HadoopClient, DataProcessing/datax-host/src/main/scala/datax/fs/
+HadoopClient.scala:33-815): read (gzip-aware), atomic write via temp-then-rename, write with timeout, list.
+
+Only local / mounted paths are supported (``file://`` prefix optional); ``wasbs://``/``hdfs://`` URIs are mapped under
+``DXA_FS_ROOT`` (default ``./.dxa_fs``) so reference job configs run unchanged on a single node.
+"""
+from __future__ import annotations
+
+import gzip
+import os
+import re
+import tempfile
+import threading
+from concurrent.futures import ThreadPoolExecutor, TimeoutError as _Timeout
+from pathlib import Path
+from typing import List, Optional
+
+_REMOTE = re.compile(r"^(wasbs?|abfss?|hdfs|adl|dbfs|s3a?)://(.*)$", re.I)
+_pool = ThreadPoolExecutor(max_workers=5, thread_name_prefix="dxa-fs")
+
+
+def local_path(path: str) -> Path:
+    if path.startswith("file://"):
+        return Path(path[7:])
+    m = _REMOTE.match(path)
+    if m:
+        root = Path(os.environ.get("DXA_FS_ROOT", ".dxa_fs"))
+        rest = m.group(2).replace("@", "/")
+        return root / m.group(1).lower() / rest
+    return Path(path)
+
+
+def read_bytes(path: str) -> bytes:
+    p = local_path(path)
+    data = p.read_bytes()
+    if path.endswith(".gz") or data[:2] == b"\x1f\x8b":
+        data = gzip.decompress(data)
+    return data
+
+
+def read_text(path: str) -> str:
+    return read_bytes(path).decode("utf-8-sig")
+
+
+def read_lines(path: str) -> List[str]:
+    return read_text(path).splitlines()
+
+
+def write_atomic(path: str, data: bytes | str, gzip_it: bool = False) -> Path:
+    """Write to a temp file in the destination folder, then rename (never leaves a partial file)."""
+    p = local_path(path)
+    p.parent.mkdir(parents=True, exist_ok=True)
+    if isinstance(data, str):
+        data = data.encode("utf-8")
+    if gzip_it:
+        data = gzip.compress(data)
+    fd, tmp = tempfile.mkstemp(prefix="." + p.name + ".", dir=str(p.parent))
+    with os.fdopen(fd, "wb") as f:
+        f.write(data)
+    os.replace(tmp, p)
+    return p
+
+
+def write_with_timeout(path: str, data: bytes | str, timeout_s: float, gzip_it: bool = False) -> Path:
+    fut = _pool.submit(write_atomic, path, data, gzip_it)
+    return fut.result(timeout=timeout_s)
+
+
+def exists(path: str) -> bool:
+    return local_path(path).exists()
+
+
+def list_files(path: str, recursive: bool = False) -> List[str]:
+    p = local_path(path)
+    if not p.exists():
+        return []
+    it = p.rglob("*") if recursive else p.iterdir()
+    return sorted(str(x) for x in it if x.is_file())
+
+
+def delete(path: str):
+    p = local_path(path)
+    if p.is_dir():
+        import shutil
+        shutil.rmtree(p)
+    elif p.exists():
+        p.unlink()

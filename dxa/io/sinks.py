@@ -1,0 +1,297 @@
+"""Output operators: ``datax.job.output.<name>.<sink>.*`` → sink writers with the reference's metric names.
+
+Reference: DataProcessing/datax-host/src/main/scala/datax/sink/OutputManager.scala:22-160 (operators, per-sink flag
+columns, ``to_json(struct(*))``, ``Sink_InputEvents`` / ``Sink_<S>_All|Filtered`` metrics), BlobSinker.scala:30-226
+(folder templating with ``%1$tY``… / ``${quarterBucket}`` / ``${minuteBucket}`` / ``${target}``, gzip by default),
+EventHubStreamPoster.scala (200-event chunks, newline-joined), HttpPoster.scala (200-event JSON arrays),
+CosmosDBSinker.scala, SqlSinker.scala.
+
+Sinks available on a single node without cloud services: blob → local/mounted folder; eventhub → a local spool
+folder per hub (or an http(s) endpoint); httppost → real HTTP; cosmosdb → JSON document folder per
+database/collection; sql → SQLite (``sqlite:///path``); plus ``file``, ``console``, ``memory`` and ``null``.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import gzip
+import json
+import os
+import re
+import threading
+import time
+import uuid
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+from ..config.secrets import resolve
+from ..engine.column import Table
+from ..engine.serialize import table_to_json_lines
+from . import fs
+
+SINK_PREFIX = "Sink_"
+_pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="dxa-sink")
+
+
+def java_time_format(fmt: str, ts: _dt.datetime) -> str:
+    """Subset of ``String.format(fmt, timestamp)`` used in DataX folder templates (``%1$tY/%1$tm/%1$td/%1$tH``…)."""
+    table = {"Y": f"{ts.year:04d}", "m": f"{ts.month:02d}", "d": f"{ts.day:02d}", "H": f"{ts.hour:02d}",
+             "M": f"{ts.minute:02d}", "S": f"{ts.second:02d}", "y": f"{ts.year % 100:02d}", "j": f"{ts.timetuple().tm_yday:03d}",
+             "L": f"{ts.microsecond // 1000:03d}", "e": str(ts.day), "k": str(ts.hour)}
+    return re.sub(r"%(?:1\$)?t([A-Za-z])", lambda m: table.get(m.group(1), m.group(0)), fmt)
+
+
+def blob_folder(fmt: Optional[str], ts: _dt.datetime, target: Optional[str] = None) -> Optional[str]:
+    if not fmt:
+        return None
+    quarter = ["00", "15", "30", "45"][min(3, round(ts.minute / 15))]
+    minute_bucket = ts.strftime("%H%M%S")
+    out = java_time_format(fmt, ts)
+    out = out.replace("${quarterBucket}", quarter).replace("${minuteBucket}", minute_bucket)
+    out = out.replace("${target}", target or "UNKNOWN")
+    return out.rstrip("/") + "/"
+
+
+def eventhub_send(conn: str, payload: bytes, hub: str = "default"):
+    """EventHub emulation: ``http(s)://`` connection → POST; anything else → spool file under DXA_FS_ROOT."""
+    if conn.startswith("http://") or conn.startswith("https://"):
+        import urllib.request
+        urllib.request.urlopen(urllib.request.Request(conn, data=payload, method="POST"), timeout=5).read()
+        return
+    m = re.search(r"EntityPath=([^;]+)", conn)
+    name = m.group(1) if m else hub
+    root = os.environ.get("DXA_FS_ROOT", ".dxa_fs")
+    path = os.path.join(root, "eventhub", name, f"{int(time.time() * 1000)}-{uuid.uuid4().hex[:8]}.bin")
+    fs.write_atomic(path, payload)
+
+
+@dataclass
+class Sink:
+    name: str                                  # metric name component, e.g. "Blobs"
+    write: Callable[[List[str], Table, _dt.datetime, str], int]
+    filter_expr: Optional[str] = None
+    as_json: bool = True
+
+
+def _chunks(xs, n):
+    for i in range(0, len(xs), n):
+        yield xs[i:i + n]
+
+
+def _blob_sink(d, output_name) -> Optional[Sink]:
+    groups = {g: sd.get("folder") for g, sd in d.group_by_sub_namespace("group.").items()}
+    if not groups:
+        return None
+    compression = (d.get("compressiontype") or "gzip").lower()
+    fmt = (d.get("format") or "json").lower()
+    group_eval = d.get("groupevaluation")
+
+    def write(lines, table, ts, target):
+        total = 0
+        for g, folder in groups.items():
+            folder = blob_folder(resolve(folder), ts, target)
+            data = "\n".join(lines)
+            suffix = ".json" + (".gz" if compression != "none" else "")
+            path = folder + f"part-{uuid.uuid4().hex[:12]}{suffix}"
+            if lines:
+                fs.write_with_timeout(path, data, timeout_s=float(os.environ.get("DATAX_BlobWriterTimeout", 10)),
+                                      gzip_it=compression != "none")
+            total += len(lines)
+        return total
+    return Sink("Blobs", write, group_eval)
+
+
+def _eventhub_sink(d, output_name) -> Optional[Sink]:
+    conn = d.get("connectionstring")
+    if not conn:
+        return None
+    compression = (d.get("compressiontype") or "gzip").lower()
+
+    def write(lines, table, ts, target):
+        c = resolve(conn)
+        for chunk in _chunks(lines, 200):
+            payload = "\n".join(chunk).encode()
+            if compression != "none":
+                payload = gzip.compress(payload)
+            eventhub_send(c, payload, output_name)
+        return len(lines)
+    return Sink("EventHub", write, d.get("filter"))
+
+
+def _http_sink(d, output_name) -> Optional[Sink]:
+    ep = d.get("endpoint")
+    if not ep:
+        return None
+    headers = {k: v for k, v in d.sub_dictionary("header.").items()}
+
+    def write(lines, table, ts, target):
+        from ..telemetry.metrics import http_post_json
+        for chunk in _chunks(lines, 200):
+            http_post_json(resolve(ep), chunk, headers)
+        return len(lines)
+    return Sink("HttpPost", write, d.get("filter"))
+
+
+def _cosmos_sink(d, output_name) -> Optional[Sink]:
+    conn = d.get("connectionstring")
+    if not conn:
+        return None
+    db = d.get("database") or "db"
+    coll = d.get("collection") or output_name
+
+    def write(lines, table, ts, target):
+        root = os.environ.get("DXA_FS_ROOT", ".dxa_fs")
+        folder = os.path.join(root, "cosmosdb", db, coll)
+        os.makedirs(folder, exist_ok=True)
+        for line in lines:
+            doc = json.loads(line)
+            doc.setdefault("id", str(uuid.uuid4()))
+            fs.write_atomic(os.path.join(folder, doc["id"] + ".json"), json.dumps(doc))
+        return len(lines)
+    return Sink("CosmosDB", write, d.get("filter"))
+
+
+def _sql_sink(d, output_name) -> Optional[Sink]:
+    conn = d.get("connectionstring")
+    if not conn:
+        return None
+    table_name = d.get("table") or output_name
+    lock = threading.Lock()
+
+    def write(lines, table, ts, target):
+        import sqlite3
+        c = resolve(conn)
+        path = c[len("sqlite:///"):] if c.startswith("sqlite:///") else os.path.join(
+            os.environ.get("DXA_FS_ROOT", ".dxa_fs"), "sql.db")
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        rows = table.to_pylist()
+        if not rows:
+            return 0
+        cols = table.names
+        with lock, sqlite3.connect(path) as db:
+            db.execute(f'CREATE TABLE IF NOT EXISTS "{table_name}" (' + ",".join(f'"{c}"' for c in cols) + ")")
+            db.executemany(f'INSERT INTO "{table_name}" VALUES (' + ",".join("?" * len(cols)) + ")",
+                           [[_sql_val(r[c]) for c in cols] for r in rows])
+        return len(rows)
+    return Sink("SqlSink", write, d.get("filter"), as_json=False)
+
+
+def _sql_val(v):
+    if isinstance(v, (dict, list)):
+        return json.dumps(v, default=str)
+    if isinstance(v, (_dt.datetime, _dt.date)):
+        return v.isoformat()
+    return v
+
+
+MEMORY_SINKS: Dict[str, List[str]] = {}
+
+
+def _file_sink(d, output_name) -> Optional[Sink]:
+    path = d.get("path")
+    if not path:
+        return None
+
+    def write(lines, table, ts, target):
+        p = fs.local_path(java_time_format(path, ts))
+        p.parent.mkdir(parents=True, exist_ok=True)
+        with open(p, "a") as f:
+            if lines:
+                f.write("\n".join(lines) + "\n")
+        return len(lines)
+    return Sink("File", write, d.get("filter"))
+
+
+def _console_sink(d, output_name) -> Optional[Sink]:
+    def write(lines, table, ts, target):
+        for l in lines[: int(d.get("maxrows") or 20)]:
+            print(f"[{output_name}] {l}")
+        return len(lines)
+    return Sink("Console", write, d.get("filter"))
+
+
+def _memory_sink(d, output_name) -> Optional[Sink]:
+    def write(lines, table, ts, target):
+        MEMORY_SINKS.setdefault(output_name, []).extend(lines)
+        return len(lines)
+    return Sink("Memory", write, d.get("filter"))
+
+
+def _null_sink(d, output_name) -> Optional[Sink]:
+    return Sink("Null", lambda lines, table, ts, target: len(lines), d.get("filter"))
+
+
+SINK_FACTORIES: Dict[str, Callable] = {
+    "blob": _blob_sink, "eventhub": _eventhub_sink, "httppost": _http_sink, "cosmosdb": _cosmos_sink,
+    "sql": _sql_sink, "file": _file_sink, "console": _console_sink, "memory": _memory_sink, "null": _null_sink,
+}
+
+
+def register_sink(kind: str, factory: Callable):
+    SINK_FACTORIES[kind.lower()] = factory
+
+
+class OutputOperator:
+    def __init__(self, name: str, sinks: List[Sink], processed_schema_path: Optional[str] = None):
+        self.name = name
+        self.sinks = sinks
+        self.processed_schema_path = processed_schema_path
+        self._schema_written = False
+
+    def output(self, table: Table, partition_time: _dt.datetime, ctx=None, target: Optional[str] = None
+               ) -> Dict[str, int]:
+        from ..config.settings import NAME_PREFIX
+        internal = f"__{NAME_PREFIX}_"
+        keep = [i for i, n in enumerate(table.names) if not n.startswith(internal)]
+        t = Table([table.names[i] for i in keep], [table.columns[i] for i in keep], table.length, table.device)
+        if self.processed_schema_path and not self._schema_written:
+            from ..engine.types import to_json_obj
+            fs.write_atomic(self.processed_schema_path, json.dumps(to_json_obj(t.schema()), indent=2))
+            self._schema_written = True
+        n = t.length
+        metrics = {f"{SINK_PREFIX}InputEvents": n}
+        if n == 0:
+            return metrics
+        lines_all = table_to_json_lines(t) if any(s.as_json for s in self.sinks) else None
+
+        def run(s: Sink):
+            lines, sub = lines_all, t
+            if s.filter_expr:
+                from ..engine.expr import EvalContext, Scope, evaluate, predicate_mask
+                from ..sql.parser import parse_expression
+                m = predicate_mask(evaluate(parse_expression(s.filter_expr), Scope.of_table(t), ctx or EvalContext()))
+                idx = m.nonzero().flatten()
+                sub = t.take(idx)
+                lines = [lines_all[i] for i in idx.tolist()] if lines_all is not None else None
+                cnt = s.write(lines, sub, partition_time, target)
+                return {f"{SINK_PREFIX}{s.name}_Filtered": cnt}
+            cnt = s.write(lines, sub, partition_time, target)
+            return {f"{SINK_PREFIX}{s.name}_All": cnt}
+
+        if len(self.sinks) == 1:
+            metrics.update(run(self.sinks[0]))
+        else:
+            for r in _pool.map(run, self.sinks):
+                for k, v in r.items():
+                    metrics[k] = metrics.get(k, 0) + v
+        return metrics
+
+
+def build_outputs(d) -> List[OutputOperator]:
+    from ..config.settings import OUTPUT_PREFIX
+    ops = []
+    for name, sub in d.group_by_sub_namespace(OUTPUT_PREFIX).items():
+        if name == "default":
+            continue
+        sinks = []
+        for kind, sd in sub.group_by_sub_namespace().items():
+            f = SINK_FACTORIES.get(kind.lower())
+            if f is None:
+                continue
+            s = f(sd, name)
+            if s is not None:
+                sinks.append(s)
+        if not sinks:
+            raise ValueError(f"no sink is defined for output '{name}'!")
+        ops.append(OutputOperator(name, sinks, sub.get("processedschemapath")))
+    return ops

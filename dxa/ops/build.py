@@ -50,7 +50,8 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     headers = sorted(CSRC.glob("*.h"))
     stamp = OUT_DIR / "build.stamp"
     digest = _digest(hip_srcs + host_srcs + headers)
-    if not force and LIB.exists() and HOST_LIB.exists() and stamp.exists() and stamp.read_text() == digest:
+    if not force and LIB.exists() and (HOST_LIB.exists() or not host_srcs) and stamp.exists() and \
+            stamp.read_text() == digest:
         return LIB
     objs = []
 

@@ -1,0 +1,206 @@
+// Schema-driven synthetic JSON event generator for gfx950 (kernel K24) — the MI355X-side
+// SimulatedData source (reference generators: Services/DataX.SimulatedData/DataX.SimulatedData.DataGenService/
+// DataGen.cs:54-227 and DataProcessing/datax-utility/src/main/scala/datax/utility/DataGenerator.scala:27-167).
+//
+// A host compiler turns a schema into a tiny op program + literal pool; one lane renders one event.  Two passes:
+// lengths (no stores) → exclusive scan on the stream → render into the final buffer, so events are packed
+// back-to-back with exact offsets, ready for the JSON parser.  Randomness is counter-based (fmix64 of
+// seed/event/op), hence deterministic and identical to the host reference implementation.
+#include "dxa_common.h"
+
+namespace {
+
+enum : int32_t {
+  OP_LIT = 0,        // a: pool offset, b: length
+  OP_INT = 1,        // a,b: [min, max) as int64 via (a | b<<32) pairs in ext
+  OP_DBL = 2,        // ext: min(double), max(double); a: decimals
+  OP_CHOICE = 3,     // a: table start (entries of (off,len) in table array), b: count
+  OP_TS_MS = 4,      // epoch millis = base_ms + row * step_us / 1000
+  OP_TS_STR = 5,     // a: format (0 "MM/dd/yyyy HH:mm:ss", 1 "yyyy-MM-ddTHH:mm:ssZ", 2 "yyyy-MM-dd HH:mm:ss")
+  OP_BOOL = 6,
+  OP_ALNUM = 7,      // a: length
+  OP_NULLP = 8,      // a: probability per mille of emitting `null` instead of the next b ops
+};
+
+struct Op {
+  int32_t code, a, b, pad;
+  int64_t x, y;      // int range / double bits
+};
+
+struct GenArgs {
+  const Op* ops;
+  int32_t nops;
+  const uint8_t* pool;
+  const int32_t* table;   // (off,len) pairs for OP_CHOICE
+  uint64_t seed;
+  int64_t row0;           // global index of the first event (for multi-batch determinism)
+  int64_t n;
+  int64_t base_ms;
+  int64_t step_us;
+  const int64_t* offs;    // write pass: [n+1]
+  uint8_t* out;           // write pass
+  int64_t* lens;          // length pass
+};
+
+__device__ __forceinline__ uint64_t rnd(uint64_t seed, int64_t row, int k) {
+  return dxa::fmix64(seed ^ dxa::fmix64((uint64_t)row * dxa::kGold + (uint64_t)k * 0x632BE59BD9B4E019ull));
+}
+
+template <bool WRITE>
+struct Emitter {
+  uint8_t* p;
+  int64_t len;
+  __device__ __forceinline__ void put(uint8_t c) {
+    if (WRITE) p[len] = c;
+    ++len;
+  }
+  __device__ __forceinline__ void put_u64(uint64_t v) {
+    char tmp[20];
+    int k = 0;
+    do { tmp[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+    while (k) put((uint8_t)tmp[--k]);
+  }
+  __device__ __forceinline__ void put_i64(int64_t v) {
+    if (v < 0) { put('-'); put_u64(0ull - (uint64_t)v); } else put_u64((uint64_t)v);
+  }
+  __device__ __forceinline__ void put2(int v) { put((uint8_t)('0' + v / 10)); put((uint8_t)('0' + v % 10)); }
+};
+
+__device__ void civil(int64_t days, int64_t& y, int& m, int& d) {
+  days += 719468;
+  const int64_t era = (days >= 0 ? days : days - 146096) / 146097;
+  const unsigned doe = (unsigned)(days - era * 146097);
+  const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  y = (int64_t)yoe + era * 400;
+  const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const unsigned mp = (5 * doy + 2) / 153;
+  d = (int)(doy - (153 * mp + 2) / 5 + 1);
+  m = (int)(mp < 10 ? mp + 3 : mp - 9);
+  if (m <= 2) ++y;
+}
+
+template <bool WRITE>
+__device__ int64_t render(const GenArgs& g, int64_t i, uint8_t* dst) {
+  Emitter<WRITE> e{dst, 0};
+  const int64_t row = g.row0 + i;
+  int skip = 0;
+  for (int k = 0; k < g.nops; ++k) {
+    const Op op = g.ops[k];
+    if (skip > 0) { --skip; continue; }
+    switch (op.code) {
+      case OP_LIT:
+        for (int q = 0; q < op.b; ++q) e.put(g.pool[op.a + q]);
+        break;
+      case OP_INT: {
+        const uint64_t span = (uint64_t)(op.y - op.x);
+        const int64_t v = op.x + (int64_t)(span ? rnd(g.seed, row, k) % span : 0);
+        e.put_i64(v);
+        break;
+      }
+      case OP_DBL: {
+        const double lo = __longlong_as_double(op.x), hi = __longlong_as_double(op.y);
+        const double u = (double)(rnd(g.seed, row, k) >> 11) * (1.0 / 9007199254740992.0);
+        const double v = lo + u * (hi - lo);
+        int64_t scale = 1;
+        for (int q = 0; q < op.a; ++q) scale *= 10;
+        const int64_t fixed = (int64_t)llround(v * (double)scale);
+        const bool neg = fixed < 0;
+        const uint64_t af = neg ? (0ull - (uint64_t)fixed) : (uint64_t)fixed;
+        if (neg) e.put('-');
+        e.put_u64(af / (uint64_t)scale);
+        if (op.a > 0) {
+          e.put('.');
+          uint64_t frac = af % (uint64_t)scale;
+          int64_t div = scale / 10;
+          for (int q = 0; q < op.a; ++q) { e.put((uint8_t)('0' + (frac / (uint64_t)div) % 10)); div = div > 1 ? div / 10 : 1; }
+        }
+        break;
+      }
+      case OP_CHOICE: {
+        const int idx = (int)(rnd(g.seed, row, k) % (uint64_t)op.b);
+        const int off = g.table[2 * (op.a + idx)], len = g.table[2 * (op.a + idx) + 1];
+        for (int q = 0; q < len; ++q) e.put(g.pool[off + q]);
+        break;
+      }
+      case OP_TS_MS:
+        e.put_i64(g.base_ms + (row * g.step_us) / 1000 + op.x);
+        break;
+      case OP_TS_STR: {
+        const int64_t secs = (g.base_ms + (row * g.step_us) / 1000) / 1000 + op.x;
+        int64_t days = secs >= 0 ? secs / 86400 : -((-secs + 86399) / 86400);
+        int64_t sod = secs - days * 86400;
+        int64_t y; int m, d;
+        civil(days, y, m, d);
+        const int hh = (int)(sod / 3600), mi = (int)(sod / 60 % 60), ss = (int)(sod % 60);
+        e.put('"');
+        if (op.a == 0) {
+          e.put2(m); e.put('/'); e.put2(d); e.put('/'); e.put_i64(y); e.put(' ');
+        } else {
+          e.put_i64(y); e.put('-'); e.put2(m); e.put('-'); e.put2(d); e.put(op.a == 1 ? 'T' : ' ');
+        }
+        e.put2(hh); e.put(':'); e.put2(mi); e.put(':'); e.put2(ss);
+        if (op.a == 1) e.put('Z');
+        e.put('"');
+        break;
+      }
+      case OP_BOOL:
+        if (rnd(g.seed, row, k) & 1) { e.put('t'); e.put('r'); e.put('u'); e.put('e'); }
+        else { e.put('f'); e.put('a'); e.put('l'); e.put('s'); e.put('e'); }
+        break;
+      case OP_ALNUM: {
+        e.put('"');
+        uint64_t r = rnd(g.seed, row, k);
+        for (int q = 0; q < op.a; ++q) {
+          if ((q & 7) == 7) r = dxa::fmix64(r + q);
+          const int c = (int)(r % 62);
+          r /= 62;
+          e.put((uint8_t)(c < 10 ? '0' + c : (c < 36 ? 'A' + c - 10 : 'a' + c - 36)));
+        }
+        e.put('"');
+        break;
+      }
+      case OP_NULLP:
+        if ((int)(rnd(g.seed, row, k) % 1000) < op.a) {
+          e.put('n'); e.put('u'); e.put('l'); e.put('l');
+          skip = op.b;
+        }
+        break;
+      default:
+        break;
+    }
+  }
+  return e.len;
+}
+
+__global__ __launch_bounds__(256) void gen_len_kernel(GenArgs g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.n) return;
+  g.lens[i] = render<false>(g, i, nullptr);
+}
+
+__global__ __launch_bounds__(256) void gen_write_kernel(GenArgs g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.n) return;
+  render<true>(g, i, g.out + g.offs[i]);
+}
+
+}  // namespace
+
+DXA_API int dxa_datagen_op_size() { return (int)sizeof(Op); }
+
+DXA_API int dxa_datagen_lengths(const void* ops, int32_t nops, const uint8_t* pool, const int32_t* table, uint64_t seed,
+                                int64_t row0, int64_t n, int64_t base_ms, int64_t step_us, int64_t* lens, void* st) {
+  if (n <= 0) return 0;
+  GenArgs g{(const Op*)ops, nops, pool, table, seed, row0, n, base_ms, step_us, nullptr, nullptr, lens};
+  hipLaunchKernelGGL(gen_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, g);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_datagen_write(const void* ops, int32_t nops, const uint8_t* pool, const int32_t* table, uint64_t seed,
+                              int64_t row0, int64_t n, int64_t base_ms, int64_t step_us, const int64_t* offs,
+                              uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  GenArgs g{(const Op*)ops, nops, pool, table, seed, row0, n, base_ms, step_us, offs, out, nullptr};
+  hipLaunchKernelGGL(gen_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, g);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,182 @@
+"""Binding for the native row serialiser (``libdxa_host.so`` / host_serialize.cpp).
+
+Columns are brought to host memory once (one D2H copy per buffer), described as a flat ``SerNode`` tree and rendered
+by worker threads; the result is one newline-separated JSON blob that sinks can write without per-row Python work.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import threading
+from typing import List, Optional, Tuple
+
+import torch
+
+from .build import HOST_LIB
+
+_LIB = None
+_lock = threading.Lock()
+
+K_I64, K_F64, K_BOOL, K_STR, K_TS, K_DATE, K_CONST, K_STRUCT, K_MAP, K_ARRAY, K_RAW, K_NULL = range(12)
+
+
+class SerNode(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("nchildren", ctypes.c_int32), ("child0", ctypes.c_int32),
+                ("drop_nulls", ctypes.c_int32), ("name", ctypes.c_char_p), ("name_len", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("data", ctypes.c_void_p), ("valid", ctypes.c_void_p),
+                ("arena", ctypes.c_void_p), ("starts", ctypes.c_void_p), ("lens", ctypes.c_void_p),
+                ("const_text", ctypes.c_char_p), ("const_len", ctypes.c_int32), ("pad2", ctypes.c_int32)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        with _lock:
+            if _LIB is None:
+                if not HOST_LIB.exists():
+                    from .build import build
+                    build()
+                L = ctypes.CDLL(str(HOST_LIB))
+                L.dxa_serialize_rows.restype = ctypes.c_void_p
+                L.dxa_serialize_rows.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                                 ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+                L.dxa_host_free.argtypes = [ctypes.c_void_p]
+                L.dxa_java_double.argtypes = [ctypes.c_double, ctypes.c_char_p, ctypes.c_int]
+                if L.dxa_sernode_size() != ctypes.sizeof(SerNode):
+                    raise RuntimeError("SerNode layout mismatch")
+                _LIB = L
+    return _LIB
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def _quoted(name: str) -> bytes:
+    return json.dumps(name, ensure_ascii=False).encode("utf-8")
+
+
+class _Builder:
+    def __init__(self):
+        self.nodes: List[dict] = []
+        self.keep = []
+
+    def _host(self, t: Optional[torch.Tensor]):
+        if t is None:
+            return 0
+        h = t.detach()
+        if h.is_cuda:
+            h = h.cpu()
+        h = h.contiguous()
+        self.keep.append(h)
+        return h.data_ptr()
+
+    def add(self, col, name: Optional[str]) -> int:
+        from ..engine.column import (ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn)
+        from ..engine.serialize import _scalar_text
+        idx = len(self.nodes)
+        nd = {"kind": K_NULL, "nchildren": 0, "child0": 0, "drop_nulls": 0, "name": _quoted(name) if name else b"",
+              "data": 0, "valid": 0, "arena": 0, "starts": 0, "lens": 0, "const": b""}
+        self.nodes.append(nd)
+        if isinstance(col, ConstColumn):
+            if col.value is None:
+                nd["kind"] = K_NULL
+            else:
+                nd["kind"] = K_CONST
+                nd["const"] = _scalar_text(col.value, col.dtype).encode("utf-8")
+            return idx
+        nd["valid"] = self._host(col.valid.view(torch.uint8) if col.valid is not None else None)
+        if isinstance(col, StrColumn):
+            nd["kind"] = K_RAW if isinstance(col, JsonColumn) else K_STR
+            nd["arena"] = self._host(col.arena)
+            nd["starts"] = self._host(col.starts)
+            nd["lens"] = self._host(col.lens)
+            return idx
+        if isinstance(col, PrimColumn):
+            dt = col.dtype
+            d = col.data
+            if dt == "boolean":
+                nd["kind"] = K_BOOL
+                d = d.to(torch.uint8) if d.dtype == torch.bool else (d != 0).to(torch.uint8)
+            elif dt in ("int", "long"):
+                nd["kind"] = K_I64
+            elif dt == "timestamp":
+                nd["kind"] = K_TS
+            elif dt == "date":
+                nd["kind"] = K_DATE
+            else:
+                nd["kind"] = K_F64
+                d = d.to(torch.float64)
+            nd["data"] = self._host(d)
+            return idx
+        if isinstance(col, (StructColumn, ArrayColumn)):
+            kids = list(zip(col.names, col.children)) if isinstance(col, StructColumn) else \
+                [(None, e) for e in col.elements]
+            nd["kind"] = (K_MAP if col.is_map else K_STRUCT) if isinstance(col, StructColumn) else K_ARRAY
+            nd["drop_nulls"] = 1 if isinstance(col, ArrayColumn) and col.drop_nulls else 0
+            nd["nchildren"] = len(kids)
+            # children must be contiguous: reserve slots first, then fill recursively
+            first = len(self.nodes)
+            nd["child0"] = first
+            placeholders = []
+            for nm, _ in kids:
+                self.nodes.append(None)
+                placeholders.append(nm)
+            for j, (nm, c) in enumerate(kids):
+                sub = _Builder()
+                sub.keep = self.keep
+                sub.nodes = self.nodes
+                # build child in place: append at end, then move into its reserved slot
+                k = sub.add(c, nm if isinstance(col, StructColumn) else None)
+                self.nodes[first + j] = self.nodes[k]
+                self.nodes[k] = {"kind": K_NULL, "nchildren": 0, "child0": 0, "drop_nulls": 0, "name": b"",
+                                 "data": 0, "valid": 0, "arena": 0, "starts": 0, "lens": 0, "const": b""}
+            return idx
+        raise TypeError(f"cannot serialise {col!r}")
+
+
+def serialize_table(table, nthreads: Optional[int] = None) -> Tuple[bytes, List[int]]:
+    """Render every row → (blob of newline-terminated JSON lines, per-line lengths)."""
+    L = lib()
+    b = _Builder()
+    top = [b.add(c, n) for n, c in zip(table.names, table.columns)]
+    arr = (SerNode * max(1, len(b.nodes)))()
+    names = []
+    for i, nd in enumerate(b.nodes):
+        names.append((nd["name"], nd["const"]))
+        arr[i] = SerNode(nd["kind"], nd["nchildren"], nd["child0"], nd["drop_nulls"], nd["name"], len(nd["name"]), 0,
+                         nd["data"], nd["valid"], nd["arena"], nd["starts"], nd["lens"], nd["const"],
+                         len(nd["const"]), 0)
+    tops = (ctypes.c_int32 * max(1, len(top)))(*top)
+    n = table.length
+    line_len = (ctypes.c_int64 * max(1, n))()
+    out_len = ctypes.c_int64(0)
+    threads = nthreads or min(16, os.cpu_count() or 4)
+    ptr = L.dxa_serialize_rows(ctypes.addressof(arr), len(b.nodes), ctypes.addressof(tops), len(top), n, threads,
+                               ctypes.addressof(line_len), ctypes.addressof(out_len))
+    try:
+        blob = ctypes.string_at(ptr, out_len.value)
+    finally:
+        L.dxa_host_free(ptr)
+    return blob, list(line_len[:n])
+
+
+def table_lines(table) -> List[str]:
+    blob, lens = serialize_table(table)
+    out = []
+    pos = 0
+    for l in lens:
+        out.append(blob[pos:pos + l].decode("utf-8"))
+        pos += l + 1
+    return out
+
+
+def java_double(d: float) -> str:
+    buf = ctypes.create_string_buffer(64)
+    n = lib().dxa_java_double(d, buf, 64)
+    return buf.raw[:n].decode()

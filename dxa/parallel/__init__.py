@@ -1,0 +1,75 @@
+"""Multi-GPU execution: one engine process per MI355X, RCCL (``torch.distributed`` "nccl" backend) over xGMI.
+
+The reference scales by data-partition parallelism with Spark hash exchanges under GROUP BY / JOIN / DISTINCT
+(SURVEY §2.G X2), broadcasts for small tables (X3) and driver reductions for counts/metrics (X5).  Here:
+
+* every rank owns a disjoint share of the stream (its source partitions) and runs the full per-batch plan;
+* tables carry a distribution tag — ``partitioned`` (rank-local share), ``hashed`` (partitioned by a key hash) or
+  ``replicated`` (identical on every rank: reference data, constants, global aggregates);
+* GROUP BY over partitioned input is two-phase: rank-local partial aggregates → ONE variable-size all-to-all of a
+  packed [rows × cols] int64 matrix (+ one for string bytes) routed by ``hash(keys) % world`` → merge on the owner.
+  Only partials cross xGMI (kilobytes per batch for the IoT flow), so the exchange is latency-, not link-bound;
+* joins of two partitioned inputs shuffle both sides by join-key hash; partitioned ⨝ replicated joins are local;
+* batch metrics are summed with one all-reduce; rank 0 emits them.
+
+``init`` is a no-op for world size 1, which keeps the single-GPU path free of collectives.  Multi-process CPU
+tests run the same code over gloo.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+_GROUP = None
+_WORLD = 1
+_RANK = 0
+_DEVICE = None
+
+PARTITIONED = "partitioned"
+HASHED = "hashed"
+REPLICATED = "replicated"
+
+
+def init(group=None, device=None):
+    global _GROUP, _WORLD, _RANK, _DEVICE
+    import torch.distributed as dist
+    _GROUP = group or dist.group.WORLD
+    _WORLD = dist.get_world_size(_GROUP)
+    _RANK = dist.get_rank(_GROUP)
+    _DEVICE = torch.device(device) if device is not None else None
+
+
+def shutdown():
+    global _GROUP, _WORLD, _RANK
+    _GROUP, _WORLD, _RANK = None, 1, 0
+
+
+def active() -> bool:
+    return _WORLD > 1
+
+
+def world() -> int:
+    return _WORLD
+
+
+def rank() -> int:
+    return _RANK
+
+
+def owner_of(h: torch.Tensor) -> torch.Tensor:
+    """Owning rank of each 64-bit key hash."""
+    return (h & 0x7FFFFFFFFFFFFFFF) % _WORLD
+
+
+def dist_of(table) -> str:
+    return getattr(table, "dist", REPLICATED)
+
+
+def set_dist(table, d: str):
+    table.dist = d
+    return table
+
+
+from .exchange import (all_reduce_sum, allgather_table, broadcast_table, shuffle_table,  # noqa: E402
+                       split_by_destination)

@@ -1,0 +1,249 @@
+"""Row exchange between ranks over RCCL (xGMI) / gloo: variable-size all-to-all of columnar tables.
+
+A table is flattened into (a) one [rows × C] int64 matrix — every fixed-width leaf becomes one column (doubles
+bit-cast, booleans widened), every string leaf contributes its byte lengths, validity travels as 63-bit masks — and
+(b) one byte stream per string leaf.  Rows are stably sorted by destination so each destination's block is
+contiguous; a single ``all_to_all_single`` moves the matrix (plus one per string leaf and one tiny one for the
+counts).  Sized for xGMI: all blocks of a rank leave in one collective, so the 7 links are driven concurrently and the
+per-call latency is paid once per exchange, not per column.
+"""
+from __future__ import annotations
+
+from typing import Any, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+
+def _g():
+    from . import _GROUP
+    return _GROUP
+
+
+def _w():
+    from . import _WORLD
+    return _WORLD
+
+
+def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
+    if _w() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_g())
+    return t
+
+
+def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
+    if _w() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_g())
+    return t
+
+
+def _a2a_counts(counts: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(counts)
+    dist.all_to_all_single(out, counts, group=_g())
+    return out
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# flatten / rebuild
+# ---------------------------------------------------------------------------------------------------------------
+
+class _Leaf:
+    __slots__ = ("kind", "dtype", "col", "mcol", "vbit", "value", "torch_dtype")
+
+    def __init__(self, kind, dtype, col=None, value=None):
+        self.kind, self.dtype, self.col, self.value = kind, dtype, col, value
+        self.mcol = -1
+        self.vbit = -1
+        self.torch_dtype = None
+
+
+def _flatten(col, leaves: List[_Leaf], spec: list):
+    """Walk a column tree; record leaves (data-bearing) and a rebuild spec."""
+    from ..engine.column import ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn
+    if isinstance(col, ConstColumn):
+        spec.append(("const", col.value, col.dtype))
+        return
+    if isinstance(col, StructColumn):
+        has_valid = col.valid is not None
+        vleaf = None
+        if has_valid:
+            vleaf = len(leaves)
+            leaves.append(_Leaf("valid_only", "boolean", col))
+        sub = []
+        for c in col.children:
+            _flatten(c, leaves, sub)
+        spec.append(("struct", col.names, col.is_map, col.dtype, vleaf, sub))
+        return
+    if isinstance(col, ArrayColumn):
+        has_valid = col.valid is not None
+        vleaf = None
+        if has_valid:
+            vleaf = len(leaves)
+            leaves.append(_Leaf("valid_only", "boolean", col))
+        sub = []
+        for c in col.elements:
+            _flatten(c, leaves, sub)
+        spec.append(("array", col.drop_nulls, vleaf, sub))
+        return
+    if isinstance(col, StrColumn):
+        spec.append(("str", len(leaves), type(col), col.dtype))
+        leaves.append(_Leaf("str", col.dtype, col))
+        return
+    if isinstance(col, PrimColumn):
+        spec.append(("prim", len(leaves), col.dtype))
+        lf = _Leaf("prim", col.dtype, col)
+        lf.torch_dtype = col.data.dtype
+        leaves.append(lf)
+        return
+    raise TypeError(f"cannot exchange column {col!r}")
+
+
+def _rebuild(spec_item, leaves_out, n, device):
+    from ..engine.column import ArrayColumn, ConstColumn, PrimColumn, StrColumn, StructColumn
+    kind = spec_item[0]
+    if kind == "const":
+        return ConstColumn(spec_item[1], spec_item[2], n, device)
+    if kind == "prim" or kind == "str":
+        return leaves_out[spec_item[1]]
+    if kind == "struct":
+        _, names, is_map, dtype, vleaf, sub = spec_item
+        kids = [_rebuild(s, leaves_out, n, device) for s in sub]
+        valid = leaves_out[vleaf] if vleaf is not None else None
+        return StructColumn(names, kids, n, valid, is_map, dtype, device)
+    if kind == "array":
+        _, drop, vleaf, sub = spec_item
+        els = [_rebuild(s, leaves_out, n, device) for s in sub]
+        valid = leaves_out[vleaf] if vleaf is not None else None
+        return ArrayColumn(els, n, valid, drop, device)
+    raise ValueError(kind)
+
+
+def split_by_destination(dest: torch.Tensor, world: int):
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=world).to(torch.int64)
+    return order, counts
+
+
+def shuffle_table(table, dest: torch.Tensor):
+    """Send row i to rank dest[i]; returns the rows this rank receives (in source-rank order)."""
+    from ..engine.column import PrimColumn, StrColumn, Table
+    W = _w()
+    device = table.device
+    n = table.length
+    order, counts = split_by_destination(dest.to(torch.int64), W)
+    t = table.take(order)
+    leaves: List[_Leaf] = []
+    spec: list = []
+    for c in t.columns:
+        _flatten(c, leaves, spec)
+    # matrix columns
+    mats = []
+    nvalid = 0
+    for lf in leaves:
+        c = lf.col
+        if lf.kind == "prim":
+            d = c.data
+            if d.dtype == torch.float64:
+                d = d.view(torch.int64)
+            elif d.dtype != torch.int64:
+                d = d.to(torch.int64)
+            lf.mcol = len(mats)
+            mats.append(d)
+        elif lf.kind == "str":
+            lf.mcol = len(mats)
+            mats.append(c.lens.to(torch.int64))
+        if c.valid is not None:
+            lf.vbit = nvalid
+            nvalid += 1
+    nmask = (nvalid + 62) // 63
+    masks = [torch.zeros(n, dtype=torch.int64, device=device) for _ in range(nmask)]
+    for lf in leaves:
+        if lf.vbit >= 0:
+            w, b = divmod(lf.vbit, 63)
+            masks[w] |= lf.col.valid.to(torch.int64) << b
+    mat_cols = mats + masks
+    C = len(mat_cols)
+    recv_counts = _a2a_counts(counts)
+    n_out = int(recv_counts.sum().item())
+    if C:
+        send = torch.stack(mat_cols, 1).contiguous() if n else torch.empty((0, C), dtype=torch.int64, device=device)
+        recv = torch.empty((n_out, C), dtype=torch.int64, device=device)
+        dist.all_to_all_single(recv, send, recv_counts.tolist(), counts.tolist(), group=_g())
+    else:
+        recv = torch.empty((n_out, 0), dtype=torch.int64, device=device)
+    # string bytes
+    str_out = {}
+    cpu_counts = counts.tolist()
+    rc = recv_counts.tolist()
+    bounds = [0]
+    for x in cpu_counts:
+        bounds.append(bounds[-1] + x)
+    rbounds = [0]
+    for x in rc:
+        rbounds.append(rbounds[-1] + x)
+    for li, lf in enumerate(leaves):
+        if lf.kind != "str":
+            continue
+        sc = lf.col.compact()
+        lens64 = sc.lens.to(torch.int64)
+        cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=device), torch.cumsum(lens64, 0)])
+        byte_bounds = cs[torch.tensor(bounds, dtype=torch.int64, device=device)].tolist()
+        send_bytes = [byte_bounds[i + 1] - byte_bounds[i] for i in range(W)]
+        sb = torch.tensor(send_bytes, dtype=torch.int64, device=device)
+        rb = _a2a_counts(sb)
+        total = int(rb.sum().item())
+        out = torch.zeros(total + 16, dtype=torch.uint8, device=device)
+        dist.all_to_all_single(out[:total], sc.arena[:byte_bounds[-1]].contiguous(), rb.tolist(), send_bytes,
+                               group=_g())
+        rlens = recv[:, lf.mcol]
+        starts = torch.cumsum(rlens, 0) - rlens
+        str_out[li] = (out, starts, rlens.to(torch.int32))
+    # rebuild leaves
+    leaves_out = {}
+    for li, lf in enumerate(leaves):
+        valid = None
+        if lf.vbit >= 0:
+            w, b = divmod(lf.vbit, 63)
+            valid = ((recv[:, len(mats) + w] >> b) & 1).to(torch.bool)
+        if lf.kind == "prim":
+            d = recv[:, lf.mcol].contiguous()
+            if lf.torch_dtype == torch.float64:
+                d = d.view(torch.float64)
+            elif lf.torch_dtype == torch.bool:
+                d = d.to(torch.bool)
+            leaves_out[li] = PrimColumn(lf.dtype, d, valid)
+        elif lf.kind == "str":
+            arena, starts, lens = str_out[li]
+            leaves_out[li] = type(lf.col)(arena, starts, lens, valid, lf.col.dtype)
+        else:   # valid_only
+            leaves_out[li] = valid if valid is not None else None
+    cols = [_rebuild(s, leaves_out, n_out, device) for s in spec]
+    out = Table(t.names, cols, n_out, device)
+    return out
+
+
+def allgather_table(table):
+    """Every rank receives the concatenation of all ranks' rows (rank order)."""
+    from ..engine.column import Table
+    W = _w()
+    if W <= 1:
+        return table
+    n = table.length
+    idx = torch.arange(n, device=table.device).repeat(W)
+    dest = torch.arange(W, device=table.device).repeat_interleave(n)
+    return shuffle_table(table.take(idx), dest)
+
+
+def broadcast_table(table, src: int = 0):
+    from . import _RANK
+    W = _w()
+    if W <= 1:
+        return table
+    if _RANK == src:
+        n = table.length
+        idx = torch.arange(n, device=table.device).repeat(W)
+        dest = torch.arange(W, device=table.device).repeat_interleave(n)
+        return shuffle_table(table.take(idx), dest)
+    empty = table.take(torch.empty(0, dtype=torch.int64, device=table.device))
+    return shuffle_table(empty, torch.empty(0, dtype=torch.int64, device=table.device))

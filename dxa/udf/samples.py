@@ -1,0 +1,74 @@
+"""Ports of the reference UDF samples (DataProcessing/datax-udf-samples/src/main/scala/datax/sample/**)."""
+from __future__ import annotations
+
+import datetime as _dt
+
+from .api import FunctionUDF, Generator, RowUDF, StringNormalizer, UDAF
+
+
+class UdfHelloWorld(RowUDF):
+    """udf/UdfHelloWorld.scala:9-13 — ``"hello, " + p1``."""
+    return_type = "string"
+
+    def call(self, p1):
+        return "hello, " + str(p1)
+
+
+class DynamicUdfHelloWorld(Generator):
+    """dynamicudf/DynamicUdfHelloWorld.scala:15-27 — a counter bumped by every on_interval()."""
+
+    def __init__(self):
+        self.counter = 1
+        self.timestamp = _dt.datetime.utcnow()
+
+    def initialize(self, settings):
+        def fn(s):
+            return f"Hello {s}, my counter is {self.counter}, timestamp at {self.timestamp}"
+
+        def on_interval(batch_time_us):
+            self.timestamp = _dt.datetime(1970, 1, 1) + _dt.timedelta(microseconds=batch_time_us)
+            self.counter += 1
+        return FunctionUDF(fn, "string"), on_interval
+
+
+class RemoveInvalidChars(StringNormalizer):
+    """normalizer/RemoveInvalidChars.scala:12-17 — control chars [\\x00-\\x08\\x0E-\\x1F] → '#'."""
+
+    def byte_map(self):
+        m = list(range(256))
+        for c in list(range(0x00, 0x09)) + list(range(0x0E, 0x20)):
+            m[c] = ord("#")
+        return m
+
+    def normalize(self, s):
+        return "".join("#" if (ord(c) <= 0x08 or 0x0E <= ord(c) <= 0x1F) else c for c in s)
+
+
+class UdafLastThreshold(UDAF):
+    """udaf/UdafLastThreshold.scala:11-56 — the row with the latest eventTime (ties → later row)."""
+    from ..engine.types import StructField, StructType
+    return_type = StructType((StructField("eventTime", "timestamp"), StructField("thresholdType", "string"),
+                              StructField("val1", "string"), StructField("val2", "string")))
+
+    def initialize(self):
+        return None
+
+    def update(self, buf, event_time, threshold_type=None, val1=None, val2=None):
+        if event_time is None:
+            return buf
+        if buf is None or buf["eventTime"] <= event_time:
+            return {"eventTime": event_time, "thresholdType": threshold_type, "val1": val1, "val2": val2}
+        return buf
+
+    def merge(self, buf, other):
+        if other is None:
+            return buf
+        return self.update(buf, other["eventTime"], other["thresholdType"], other["val1"], other["val2"])
+
+
+REFERENCE_CLASS_MAP = {
+    "datax.sample.udf.UdfHelloWorld": UdfHelloWorld,
+    "datax.sample.dynamicudf.DynamicUdfHelloWorld": DynamicUdfHelloWorld,
+    "datax.sample.normalizer.RemoveInvalidChars": RemoveInvalidChars,
+    "datax.sample.udaf.UdafLastThreshold": UdafLastThreshold,
+}
