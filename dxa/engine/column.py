@@ -172,6 +172,8 @@ class StrColumn(Column):
         return sops.compact(self)
 
     def to_pylist(self):
+        if self.arena.numel() > 4 * self.length * 64 + 4096 and not getattr(self, "_compact", False):
+            return self.compact().to_pylist()     # never copy a whole raw-input arena to the host
         arena = self.arena.cpu().numpy().tobytes()
         starts = self.starts.cpu().tolist()
         lens = self.lens.cpu().tolist()

@@ -16,6 +16,7 @@ from __future__ import annotations
 import datetime as _dt
 import json
 import logging
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -37,6 +38,7 @@ from .types import MapType, StructType, schema_from_json
 from .windows import TimeWindowConf, WindowStore
 
 log = logging.getLogger("dxa.processor")
+_SYNC_STAGES = os.environ.get("DXA_SYNC_STAGES") == "1"
 
 
 @dataclass
@@ -142,6 +144,7 @@ class Processor:
         if self.normalizer is not None:
             buf = self.normalizer(buf, raw.offs)
         raw_col, row_ok = parse(buf, raw.offs, self.parse_plan)
+        self._sync()
         self.stage_times["parse"] = time.perf_counter() - t0
         n = raw.n
         dev = self.device
@@ -169,6 +172,7 @@ class Processor:
             cat.register("__dxa_input", table)
             items = step + [f"`{p}`" for p in preserved if not any(p in s for s in step)]
             table = run_sql("SELECT " + ", ".join(items) + " FROM __dxa_input", cat, ctx)
+        self._sync()
         self.stage_times["project"] = time.perf_counter() - t0
         return table
 
@@ -210,6 +214,7 @@ class Processor:
                     result = st.overwrite(result)
                 cat.register(cmd.name, result)
                 views[cmd.name] = result
+        self._sync()
         self.stage_times["transform"] = time.perf_counter() - t0
         # outputs (in parallel on the host pool)
         t1 = time.perf_counter()
@@ -231,12 +236,18 @@ class Processor:
             vec = torch.tensor([float(metrics[k]) for k in keys], dtype=torch.float64, device=self.device)
             P.all_reduce_sum(vec)
             metrics = dict(zip(keys, vec.tolist()))
+        self._sync()
         self.stage_times["output"] = time.perf_counter() - t1
         for st in self.state_tables.values():
             st.persist()
         if self.keep_views:
             self.last_views = {**{k: cat.get(k) for k in cat.names()}, **views}
         return metrics
+
+    def _sync(self):
+        """Stage attribution (DXA_SYNC_STAGES=1): make per-stage wall times include their device work."""
+        if _SYNC_STAGES and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     def _run_command(self, text: str):
         low = text.strip().lower()

@@ -456,6 +456,19 @@ done:
   }
 }
 
+// Per-node null counts (one 64-lane ballot per node per wave, one atomic per node per wave) so the host can drop
+// validity masks of columns that turned out complete — every later operator then skips its null handling.
+__global__ __launch_bounds__(256) void null_count_kernel(const uint8_t* __restrict__ valid, int64_t n, int32_t nnodes,
+                                                         unsigned long long* __restrict__ nulls) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = row < n;
+  for (int k = 0; k < nnodes; ++k) {
+    const bool isnull = in && valid[(int64_t)k * n + row] == 0;
+    const unsigned long long m = __ballot(isnull);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nulls[k], (unsigned long long)__popcll(m));
+  }
+}
+
 // Newline framing: offsets of '\n'-terminated records in a raw byte stream (blob / socket sources).
 __global__ void count_newlines_kernel(const uint8_t* __restrict__ buf, int64_t len, int64_t chunk,
                                       int64_t* __restrict__ counts) {
@@ -494,6 +507,15 @@ DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const u
   const int block = 256;
   const int64_t grid = (n + block - 1) / block;
   hipLaunchKernelGGL(json_parse_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_null_counts(const uint8_t* valid, int64_t n, int32_t nnodes, unsigned long long* nulls, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(nulls, 0, sizeof(unsigned long long) * (size_t)nnodes, s);
+  if (e != hipSuccess) return (int)e;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(null_count_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, valid, n, nnodes, nulls);
   return (int)hipGetLastError();
 }
 

@@ -175,17 +175,22 @@ def _parse_gpu(buf, offs, n, plan: ParsePlan):
         N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
                N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
                N.stream_handle(buf.device))
+    nulls = [1] * nn
+    if n:
+        cnt = torch.empty(nn, dtype=torch.int64, device=buf.device)
+        N.call("dxa_null_counts", N.ptr(valid), n, nn, N.ptr(cnt), N.stream_handle(buf.device))
+        nulls = cnt.tolist()   # one tiny D2H per batch
     vals, lens, valid, row_ok = vals[:, :n], lens[:, :n], valid[:, :n].view(torch.bool), row_ok[:n].view(torch.bool)
-    return _assemble(plan, buf, vals, lens, valid, n), row_ok
+    return _assemble(plan, buf, vals, lens, valid, n, nulls), row_ok
 
 
-def _assemble(plan: ParsePlan, arena, vals, lens, valid, n):
+def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
     from ..engine.column import PrimColumn, StrColumn, JsonColumn, StructColumn
     device = arena.device
     cols: Dict[int, object] = {}
     for idx in range(len(plan.nodes) - 1, 0, -1):
         nd = plan.nodes[idx]
-        v = valid[idx]
+        v = valid[idx] if (nulls is None or nulls[idx]) else None   # complete columns carry no mask
         if nd.code == 0:
             kids = [(plan.nodes[j].name, cols[j]) for j in range(len(plan.nodes)) if plan.nodes[j].parent == idx]
             cols[idx] = StructColumn([k for k, _ in kids], [c for _, c in kids], n, v, False, None, device)
@@ -203,7 +208,8 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n):
         else:
             cols[idx] = PrimColumn(nd.dtype, raw, v)
     kids = [(plan.nodes[j].name, cols[j]) for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == 0]
-    return StructColumn([k for k, _ in kids], [c for _, c in kids], n, valid[0], False, None, device)
+    root_valid = valid[0] if (nulls is None or nulls[0]) else None
+    return StructColumn([k for k, _ in kids], [c for _, c in kids], n, root_valid, False, None, device)
 
 
 # ------------------------------------------------------------------------------------------------------------------

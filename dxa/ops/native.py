@@ -28,6 +28,7 @@ c_p = ctypes.c_void_p
 _SIGS = {
     "dxa_json_parse": [c_p, c_p, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_p],
     "dxa_count_newlines": [c_p, c_i64, c_i64, c_p, c_p],
+    "dxa_null_counts": [c_p, c_i64, c_i32, c_p, c_p],
     "dxa_write_newlines": [c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_hash_i64": [c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],
     "dxa_hash_f64": [c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],
@@ -51,6 +52,9 @@ _SIGS = {
     "dxa_i64_to_str_write": [c_p, c_i64, c_p, c_p, c_p],
     "dxa_case_map": [c_p, c_p, c_p, c_i64, c_p, c_p, ctypes.c_int, c_p],
     "dxa_str_to_ts": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
+    "dxa_datagen_op_size": [],
+    "dxa_datagen_lengths": [c_p, c_i32, c_p, c_p, ctypes.c_uint64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "dxa_datagen_write": [c_p, c_i32, c_p, c_p, ctypes.c_uint64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p],
 }
 
 # optional symbols (added by later kernels); bound if present
@@ -62,7 +66,15 @@ class NativeError(RuntimeError):
 
 
 def register_sigs(sigs: dict):
+    """Declare argument types for extra symbols; applied immediately if the library is already loaded (an unbound
+    ctypes function would silently pass 64-bit arguments as C ints)."""
     _OPTIONAL_SIGS.update(sigs)
+    if _LIB is not None:
+        for name, args in sigs.items():
+            fn = getattr(_LIB, name, None)
+            if fn is not None:
+                fn.argtypes = args
+                fn.restype = ctypes.c_int
 
 
 def lib():

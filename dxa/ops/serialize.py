@@ -93,6 +93,10 @@ class _Builder:
         nd["valid"] = self._host(col.valid.view(torch.uint8) if col.valid is not None else None)
         if isinstance(col, StrColumn):
             nd["kind"] = K_RAW if isinstance(col, JsonColumn) else K_STR
+            if col.arena.numel() > 4 * col.length * 64 + 4096 and not getattr(col, "_compact", False):
+                # views into a large arena (e.g. the batch's raw input buffer): gather only the referenced bytes
+                # on the device before the D2H copy
+                col = col.compact()
             nd["arena"] = self._host(col.arena)
             nd["starts"] = self._host(col.starts)
             nd["lens"] = self._host(col.lens)

@@ -47,7 +47,9 @@ def compact(col):
             idx = torch.repeat_interleave(col.starts - off, col.lens.to(torch.int64)) + torch.arange(
                 total, dtype=torch.int64)
             dst[:total] = src[idx]
-    return type(col)(dst, off, col.lens.clone(), col.valid, col.dtype)
+    out = type(col)(dst, off, col.lens.clone(), col.valid, col.dtype)
+    out._compact = True
+    return out
 
 
 def concat(cols: Sequence, valid: Optional[torch.Tensor]):
