@@ -1,0 +1,71 @@
+"""Engine entry point — one process per MI355X (the reference's DirectStreamingApp / DirectLocalStreamingApp /
+DirectKafkaStreamingApp / BlobStreamingApp / BatchApp ``main``s, DataProcessing/datax-host/src/main/scala/datax/app/*).
+
+    python -m dxa.app conf=/path/job.conf [app=local|file|socket|queue|batch] [maxBatches=N] [realtime=false]
+            [driverLogLevel=WARN] [checkpointEnabled=true]
+    # multi-GPU: python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m dxa.app conf=…
+
+Arguments follow the reference's ``k=v`` convention; ``DATAX_*`` environment variables are merged
+(ConfigManager.scala:61-81).  Batch mode takes ``processStartTime=… processEndTime=… partitionIncrement=<minutes>``
+and ``datax.job.input.default.blob.<name>.path`` templates.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import logging
+import os
+import sys
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    import torch
+    from .config import settings as S
+    d = S.settings_from_arguments(argv)
+    d = S.load_config(d)
+    args = S.named_args(argv)
+    logging.basicConfig(level=getattr(logging, (args.get("driverLogLevel") or "WARN").upper(), logging.WARN),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        from .ops import native
+        native.lib()
+    else:
+        device = torch.device("cpu")
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl" if device.type == "cuda" else "gloo")
+        from . import parallel
+        parallel.init(dist.group.WORLD, device)
+    from .engine.host import BlobBatchingHost, StreamingHost
+    from .engine.processor import Processor
+    from .io.sources import build_source
+    from .telemetry.metrics import MetricStore
+    proc = Processor(d, device, metric_store=MetricStore.default())
+    app = (args.get("app") or "").lower() or None
+    if app == "batch":
+        start = _dt.datetime.fromisoformat(args["processStartTime"])
+        end = _dt.datetime.fromisoformat(args["processEndTime"])
+        inc = _dt.timedelta(minutes=float(args.get("partitionIncrement", 60)))
+        paths = [sub.get_string("path") for sub in d.group_by_sub_namespace(S.INPUT_PREFIX + "blob.").values()]
+        res = BlobBatchingHost(proc, device, paths, start, end, inc).run()
+        print(json.dumps({"batches": len(res)}), flush=True)
+        return 0
+    src = build_source(d, device, app)
+    interval = float(d.get(S.INPUT_PREFIX + "streaming.intervalinseconds") or 60)
+    host = StreamingHost(proc, src, interval, int(args["maxBatches"]) if "maxBatches" in args else None,
+                         realtime=(args.get("realtime", "true").lower() == "true"))
+    import signal
+    signal.signal(signal.SIGTERM, lambda *_: host.stop())
+    hist = host.run()
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({"batches": len(hist), "last": hist[-1] if hist else None}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
