@@ -48,10 +48,17 @@ def main(argv=None):
     proc = Processor(d, device, metric_store=MetricStore.default())
     app = (args.get("app") or "").lower() or None
     if app == "batch":
-        start = _dt.datetime.fromisoformat(args["processStartTime"])
-        end = _dt.datetime.fromisoformat(args["processEndTime"])
-        inc = _dt.timedelta(minutes=float(args.get("partitionIncrement", 60)))
-        paths = [sub.get_string("path") for sub in d.group_by_sub_namespace(S.INPUT_PREFIX + "blob.").values()]
+        from .config.secrets import resolve
+        from .service.scheduler import _parse_time
+        blobs = list(d.group_by_sub_namespace(S.INPUT_PREFIX + "blob.").values())
+        first = blobs[0] if blobs else None
+
+        def pick(key, conf_key, default=None):
+            return args.get(key) or (first.get(conf_key) if first is not None else None) or default
+        start = _parse_time(pick("processStartTime", "processstarttime"))
+        end = _parse_time(pick("processEndTime", "processendtime"))
+        inc = _dt.timedelta(minutes=float(pick("partitionIncrement", "partitionincrement", 60)))
+        paths = [resolve(sub.get_string("path")) for sub in blobs]
         res = BlobBatchingHost(proc, device, paths, start, end, inc).run()
         print(json.dumps({"batches": len(res)}), flush=True)
         return 0

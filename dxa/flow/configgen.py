@@ -73,6 +73,13 @@ def _secret(s: Session, kind: str, value: Optional[str]) -> Optional[str]:
 # stages
 # ---------------------------------------------------------------------------------------------------------------
 
+def _try_resolve(v: str) -> str:
+    try:
+        return secrets.resolve(v) or ""
+    except Exception:  # noqa: BLE001 — unresolvable secret: fall back to the raw reference
+        return v or ""
+
+
 def s200_merge_defaults(s: Session):
     from .templates import default_flow
     base = default_flow(s.name)
@@ -280,6 +287,16 @@ def s600_job_config(s: Session):
                                  "topics": props.get("inputEventhubName"), "groupId": s.name,
                                  "checkpointDir": os.path.join(t["checkpointDir"], "kafka"),
                                  "maxRate": t["inputMaxRate"] or None}
+    if inp.get("mode", "streaming").lower() == "batching":
+        from ..service.scheduler import partition_increment
+        blobs = []
+        for i, b in enumerate(inp.get("batch") or []):
+            bp = b.get("properties") or {}
+            path = bp.get("path") or ""
+            blobs.append({"name": f"input{i}", "path": path, "format": bp.get("formatType") or "json",
+                          "compressiontype": bp.get("compressionType") or "none",
+                          "partitionincrement": str(partition_increment(_try_resolve(path)))})
+        job["input"]["blob"] = blobs
     elif kind == "local":
         job["input"]["local"] = {"schemaFile": s.paths["schema"],
                                  "eventsPerBatch": str(props.get("eventsPerBatch") or t["inputMaxRate"] or 100)}

@@ -162,6 +162,9 @@ DEFAULT_SPEC: Dict = {
                 "schemaFile": "schemafile", "eventsPerBatch": "eventsperbatch", "seed": "seed"}},
             "streaming": {"type": "object", "namespace": "streaming", "fields": {
                 "checkpointDir": "checkpointdir", "intervalInSeconds": "intervalinseconds"}},
+            "blob": _scoped("blob", {"path": "path", "format": "format", "compressiontype": "compressiontype",
+                                     "processstarttime": "processstarttime", "processendtime": "processendtime",
+                                     "partitionincrement": "partitionincrement"}),
             "sources": {"type": "map", "namespace": "source", "fields": {"target": "target",
                                                                           "catalogPrefix": "catalogprefix"}},
             "referenceData": _scoped("referencedata", {"path": "path", "format": "format", "header": "header",

@@ -1,0 +1,190 @@
+"""Local job management: start / stop / restart / sync engine processes (the reference's SparkJobOperation +
+LocalSparkClient: Services/DataX.Config/DataX.Config/InternalService/SparkJobOperation.cs:29-268 and
+DataX.Config.Local/LocalSparkClient.cs:20-206).
+
+A job runs as ``python -m dxa.app conf=<job.conf>`` — or, for ``gpus > 1``, under ``torch.distributed.run`` with one
+rank per MI355X.  Liveness = PID alive AND its recorded start time matches (PID reuse safe).  States follow the
+reference: Idle → Starting → Running → Success / Error; ``start`` first ensures the job is not running (polling up
+to 30 × 1 s), ``restart_all_with_retries`` retries failed starts.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+from .store import DocumentStore
+
+IDLE, STARTING, RUNNING, SUCCESS, ERROR = "Idle", "Starting", "Running", "Success", "Error"
+_COLL = "sparkJobs"
+
+
+def _proc_start_time(pid: int) -> Optional[float]:
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return float(fields[19])      # starttime in clock ticks since boot
+    except (OSError, IndexError, ValueError):
+        return None
+
+
+class JobManager:
+    def __init__(self, store: DocumentStore, log_dir: str, python: str = sys.executable):
+        self.store = store
+        self.log_dir = log_dir
+        self.python = python
+        self._procs: Dict[str, subprocess.Popen] = {}
+        self._lock = threading.Lock()
+        os.makedirs(log_dir, exist_ok=True)
+
+    # -- entity management ------------------------------------------------------------------------------------------
+    def upsert(self, job: Dict[str, Any]) -> Dict[str, Any]:
+        old = self.store.get(_COLL, job["name"]) or {}
+        merged = {**old, **job}
+        merged.setdefault("state", IDLE)
+        self.store.upsert(_COLL, job["name"], merged)
+        return merged
+
+    def get(self, name: str) -> Optional[Dict[str, Any]]:
+        j = self.store.get(_COLL, name)
+        return self._sync(j) if j else None
+
+    def get_all(self) -> List[Dict[str, Any]]:
+        return [self._sync(j) for j in self.store.get_all(_COLL)]
+
+    def get_by_names(self, names: List[str]) -> List[Dict[str, Any]]:
+        return [j for j in (self.get(n) for n in names) if j]
+
+    def delete(self, name: str):
+        self.stop(name)
+        self.store.delete(_COLL, name)
+
+    # -- lifecycle --------------------------------------------------------------------------------------------------
+    def _command(self, job: Dict[str, Any]) -> List[str]:
+        args = [f"conf={job['confPath']}"]
+        if job.get("app"):
+            args.append(f"app={job['app']}")
+        for k, v in (job.get("args") or {}).items():
+            args.append(f"{k}={v}")
+        gpus = int(job.get("gpus", 1))
+        if gpus > 1:
+            return [self.python, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+                    "--master-addr", "127.0.0.1", "--master-port", str(job.get("port", 29600)), "-m", "dxa.app"] + args
+        return [self.python, "-m", "dxa.app"] + args
+
+    def start(self, name: str, ensure_stopped_retries: int = 30) -> Dict[str, Any]:
+        job = self.store.get(_COLL, name)
+        if job is None:
+            raise KeyError(f"job {name} not found")
+        for _ in range(ensure_stopped_retries):
+            job = self._sync(job)
+            if job["state"] in (IDLE, SUCCESS, ERROR):
+                break
+            time.sleep(1.0)
+        else:
+            raise RuntimeError(f"job {name} is still {job['state']}")
+        log_path = os.path.join(self.log_dir, f"{name}.log")
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+        with open(log_path, "ab") as logf:
+            p = subprocess.Popen(self._command(job), stdout=logf, stderr=subprocess.STDOUT, env=env,
+                                 start_new_session=True)
+        with self._lock:
+            self._procs[name] = p
+        job.update(state=STARTING, pid=p.pid, pidStart=_proc_start_time(p.pid), startedAt=time.time(),
+                   log=log_path)
+        self.store.upsert(_COLL, name, job)
+        return job
+
+    def stop(self, name: str, timeout: float = 30.0) -> Optional[Dict[str, Any]]:
+        job = self.store.get(_COLL, name)
+        if job is None:
+            return None
+        pid = job.get("pid")
+        if pid and self._alive(job):
+            try:
+                os.killpg(pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+            t0 = time.time()
+            while self._alive(job) and time.time() - t0 < timeout:
+                self._reap(name)
+                time.sleep(0.2)
+            if self._alive(job):
+                try:
+                    os.killpg(pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+        self._reap(name)
+        job.update(state=IDLE, pid=None)
+        self.store.upsert(_COLL, name, job)
+        return job
+
+    def restart(self, name: str) -> Dict[str, Any]:
+        self.stop(name)
+        return self.start(name)
+
+    def restart_all_with_retries(self, names: Optional[List[str]] = None, retries: int = 3) -> Dict[str, str]:
+        out = {}
+        for j in (self.get_by_names(names) if names else self.get_all()):
+            for attempt in range(retries):
+                try:
+                    self.restart(j["name"])
+                    out[j["name"]] = STARTING
+                    break
+                except Exception as e:  # noqa: BLE001
+                    out[j["name"]] = f"{ERROR}: {e}"
+                    time.sleep(1.0)
+        return out
+
+    def sync_all(self) -> List[Dict[str, Any]]:
+        return self.get_all()
+
+    # -- state ------------------------------------------------------------------------------------------------------
+    def _reap(self, name):
+        with self._lock:
+            p = self._procs.get(name)
+        if p is not None and p.poll() is not None:
+            with self._lock:
+                self._procs.pop(name, None)
+            return p.returncode
+        return None
+
+    def _alive(self, job) -> bool:
+        pid = job.get("pid")
+        if not pid:
+            return False
+        st = _proc_start_time(pid)
+        if st is None or (job.get("pidStart") is not None and st != job.get("pidStart")):
+            return False
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                state = f.read().rsplit(")", 1)[1].split()[0]
+            return state != "Z"
+        except OSError:
+            return False
+
+    def _sync(self, job: Dict[str, Any]) -> Dict[str, Any]:
+        name = job["name"]
+        rc = self._reap(name)
+        state = job.get("state", IDLE)
+        if state in (STARTING, RUNNING):
+            if self._alive(job):
+                state = RUNNING
+            else:
+                if rc is None:
+                    with self._lock:
+                        p = self._procs.get(name)
+                    rc = p.returncode if p is not None else None
+                state = SUCCESS if rc == 0 else ERROR
+                job["pid"] = None
+            if state != job.get("state"):
+                job["state"] = state
+                self.store.upsert(_COLL, name, job)
+        return job
