@@ -1,16 +1,25 @@
 #!/usr/bin/env python3
-"""Flagship benchmark: SimulatedData IoT stream → JSON parse → projection → SQL group-by aggregate + alert view →
-outputs, one micro-batch per step, one process per MI355X (BASELINE.json config 2; metric "events/sec (node) +
-p99 latency").
+"""Flagship benchmark: SimulatedData IoT stream → JSON parse → projection → SQL → outputs, one micro-batch per step,
+one process per MI355X (BASELINE.json metric "events/sec (node) + p99 latency").
 
-Each step is a complete micro-batch exactly as the streaming host runs it: the batch's raw JSON bytes are copied from
-pinned host memory into HBM (the ingest boundary — events arrive from the network into host memory), parsed
-(32 leaf columns), projected (``stringToTimestamp`` + ``Raw.*``), aggregated by (deviceId, deviceType, homeId) with 9
-aggregates, filtered into an alert view, both outputs serialised to JSON lines, and the batch metrics emitted.
-With N>1 ranks the group-by is two-phase: rank-local partial aggregates are exchanged by key hash over RCCL
-all-to-all and merged by the owning rank (weak scaling: events per GPU per step are fixed).
+``--flow`` picks the BASELINE configuration (default ``groupby`` = config 2, the headline):
 
-    python bench.py                       # 1 GPU, defaults
+* ``groupby`` — 32-col JSON parse, projection, GROUP BY (deviceId, deviceType, homeId) with 9 aggregates, alert view,
+  JSON outputs (config 2);
+* ``window``  — the same aggregate over a 5-minute sliding window with a 1-s slide (config 3; answered from cached
+  per-pane partial aggregates, merged across ranks with one RCCL all-to-all of partials);
+* ``join``    — stream–static hash join against a 100M-row reference table resident in HBM (config 4);
+* ``full``    — codegen'd rules + windowed SQL with a device UDF + reference join + accumulator state (config 5).
+
+Each step is a complete micro-batch exactly as the streaming host runs it.  Sources: ``pinned`` — the batch's raw
+JSON bytes are copied from pinned host memory into HBM every step (events arrive from the network into host memory;
+default for groupby/join); ``gpu-sim`` — the SimulatedData generator renders the next batch on the GPU with event
+times inside that batch's second (needed by the windowed flows, whose windows must see advancing event time; its
+cost is inside the timed step).  Batch times advance one interval per step on a simulated clock.
+With N>1 ranks, per-GPU work is fixed (weak scaling); GROUP BYs are two-phase over RCCL.
+
+    python bench.py                                   # 1 GPU, config 2
+    python bench.py --flow window                     # config 3 (warms up 305 steps to fill the 5-min window)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 """
 from __future__ import annotations
@@ -24,19 +33,39 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+DEFAULT_EVENTS = {"groupby": 2_000_000, "window": 1_000_000, "join": 2_000_000, "full": 1_000_000}
+DEFAULT_WARMUP = {"groupby": 5, "window": 305, "join": 3, "full": 305}
+DEFAULT_SOURCE = {"groupby": "pinned", "window": "gpu-sim", "join": "pinned", "full": "gpu-sim"}
+MODEL = {
+    "groupby": "SimulatedData IoT flow: 32-col JSON parse + projection + GROUP BY (deviceId, deviceType, homeId) "
+               "9 aggregates + alert view + JSON outputs",
+    "window": "SimulatedData IoT flow: 32-col JSON parse + projection + 5-min sliding-window GROUP BY (1-s slide) "
+              "9 aggregates + alert view",
+    "join": "SimulatedData IoT flow: 32-col JSON parse + stream-static hash join vs {ref}-row HBM-resident "
+            "reference table + GROUP BY",
+    "full": "SimulatedData IoT flow: rules (ProcessRules codegen) + 5-min windowed SQL with device UDF + "
+            "reference join + accumulator state table",
+}
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--events-per-batch", type=int, default=2_000_000, help="events per GPU per micro-batch")
-    ap.add_argument("--pool", type=int, default=3, help="distinct pre-generated batches cycled through")
-    ap.add_argument("--source", choices=["pinned", "device"], default="pinned",
-                    help="pinned: H2D copy of raw bytes every step (default); device: NIC-direct style, bytes already"
-                         " in HBM")
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--flow", choices=list(DEFAULT_EVENTS), default="groupby")
+    ap.add_argument("--events-per-batch", type=int, default=None, help="events per GPU per micro-batch")
+    ap.add_argument("--ref-rows", type=int, default=100_000_000, help="reference table rows (join flow)")
+    ap.add_argument("--pool", type=int, default=3, help="distinct pre-generated batches cycled (pinned source)")
+    ap.add_argument("--source", choices=["pinned", "device", "gpu-sim"], default=None,
+                    help="pinned: H2D copy of raw bytes every step; device: bytes already in HBM; gpu-sim: GPU "
+                         "generator renders each batch")
     ap.add_argument("--profile-stages", action="store_true")
     args = ap.parse_args()
+    flow = args.flow
+    warmup = DEFAULT_WARMUP[flow] if args.warmup is None else args.warmup
+    E = args.events_per_batch or DEFAULT_EVENTS[flow]
+    source = args.source or DEFAULT_SOURCE[flow]
 
     import torch
     import torch.distributed as dist
@@ -48,9 +77,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    on_gpu = device.type == "cuda"
 
     from dxa.ops import native
-    if device.type == "cuda":
+    if on_gpu:
         native.lib()
     from dxa.engine.processor import Processor, RawBatch
     from dxa.models import iot
@@ -60,67 +90,96 @@ def main():
     if world > 1:
         parallel.init(dist.group.WORLD, device)
 
-    E = args.events_per_batch
-    proc = Processor(iot.flow_settings(workdir=f"/tmp/dxa_bench_{rank}"), device)
+    proc = Processor(iot.flow_settings(workdir=f"/tmp/dxa_bench_{flow}_{rank}", variant=flow,
+                                       ref_rows=args.ref_rows), device)
+    t_ref = time.perf_counter()
+    if flow == "join":
+        proc.reference["RefDevices"] = iot.reference_table(args.ref_rows, device)
+    if on_gpu:
+        torch.cuda.synchronize(device)
+    ref_s = time.perf_counter() - t_ref
     prog = iot.program()
-    pool = []
+    interval_us = 1_000_000
+    clock0_us = (int(time.time()) - 3600) * 1_000_000      # simulated clock, aligned to the interval
+
+    def batch_time(i):
+        return clock0_us + i * interval_us
+
     t_gen = time.perf_counter()
-    base_ms = int(time.time() * 1000)
-    for p in range(args.pool):
-        buf, offs = generate(prog, E, device, seed=1000 * rank + p + 1, row0=p * E, base_ms=base_ms)
-        if args.source == "pinned" and device.type == "cuda":
-            pool.append((buf.cpu().pin_memory(), offs.cpu().pin_memory()))
-            del buf, offs
-        else:
-            pool.append((buf, offs))
-    if device.type == "cuda":
+    pool = []
+    if source in ("pinned", "device"):
+        base_ms = clock0_us // 1000
+        for p in range(args.pool):
+            buf, offs = generate(prog, E, device, seed=1000 * rank + p + 1, row0=p * E, base_ms=base_ms)
+            if source == "pinned" and on_gpu:
+                pool.append((buf.cpu().pin_memory(), offs.cpu().pin_memory()))
+                del buf, offs
+            else:
+                pool.append((buf, offs))
+    if on_gpu:
         torch.cuda.synchronize(device)
     gen_s = time.perf_counter() - t_gen
-    avg_bytes = float(pool[0][1][-1].item()) / E
 
-    copy_stream = torch.cuda.Stream(device) if (device.type == "cuda" and args.source == "pinned") else None
+    side = torch.cuda.Stream(device) if (on_gpu and source in ("pinned", "gpu-sim")) else None
     staged = {}
+    sizes = []
 
     def stage(i):
+        """Make batch i's raw bytes available in HBM — on a side stream, overlapping batch i-1's processing."""
+        if source == "gpu-sim":
+            def gen():
+                bt_ms = batch_time(i) // 1000
+                return generate(prog, E, device, seed=7919 * rank + i + 1, row0=i * E, base_ms=bt_ms - 1000,
+                                step_us=max(1, interval_us // E))
+            if side is None:
+                staged[i] = gen() + (None,)
+                return
+            with torch.cuda.stream(side):
+                db, do = gen()
+                ev = torch.cuda.Event()
+                ev.record(side)
+            staged[i] = (db, do, ev)
+            return
         hb, ho = pool[i % len(pool)]
-        if copy_stream is None:
+        if side is None:
             staged[i] = (hb, ho, None)
             return
-        with torch.cuda.stream(copy_stream):
+        with torch.cuda.stream(side):
             db = hb.to(device, non_blocking=True)
             do = ho.to(device, non_blocking=True)
             ev = torch.cuda.Event()
-            ev.record(copy_stream)
+            ev.record(side)
         staged[i] = (db, do, ev)
 
     lat = []
-    interval_us = 1_000_000
 
     def step(i):
         db, do, ev = staged.pop(i)
         if ev is not None:
-            torch.cuda.current_stream(device).wait_event(ev)
-            db.record_stream(torch.cuda.current_stream(device))
-            do.record_stream(torch.cuda.current_stream(device))
-        stage(i + 1)   # prefetch the next batch's bytes while this one is processed
-        bt = int(time.time() * 1e6)
-        m = proc.process_batch(RawBatch(db, do, E), bt, interval_us)
+            cur = torch.cuda.current_stream(device)
+            cur.wait_event(ev)
+            db.record_stream(cur)
+            do.record_stream(cur)
+        stage(i + 1)
+        m = proc.process_batch(RawBatch(db, do, E), batch_time(i), interval_us)
         lat.append(m["Latency-Process"])
+        sizes.append(db.shape[0])
         return m
 
     stage(0)
-    for i in range(args.warmup):
+    for i in range(warmup):
         step(i)
-    if device.type == "cuda":
+    if on_gpu:
         torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     lat.clear()
+    sizes.clear()
     t0 = time.perf_counter()
     last = None
-    for i in range(args.warmup, args.warmup + args.steps):
+    for i in range(warmup, warmup + args.steps):
         last = step(i)
-    if device.type == "cuda":
+    if on_gpu:
         torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -143,30 +202,39 @@ def main():
 
     total_events = E * world * args.steps
     value = total_events / elapsed
+    avg_bytes = (sum(sizes) / len(sizes) - 16) / E if sizes else None
     out = {
         "metric": "events/sec (node) + p99 latency, SimulatedData IoT Flow",
         "value": value,
         "unit": "events/s",
         "n_gpus": world,
         "steps": args.steps,
-        "warmup": args.warmup,
+        "warmup": warmup,
         "ms_per_step": elapsed / args.steps * 1000.0,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp64/int64 columns (no reduced precision)",
         "data": "synthetic (SimulatedData-schema JSON generated on device, random seeds per rank/batch)",
-        "config": {"model": "SimulatedData IoT flow: 32-col JSON parse + projection + GROUP BY (deviceId, deviceType,"
-                            " homeId) 9 aggregates + alert view + JSON outputs",
+        "config": {"model": MODEL[flow].format(ref=args.ref_rows), "flow": flow,
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
-                   "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1), "source": args.source},
+                   "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,
+                   "source": source, "batch_interval_s": interval_us / 1e6},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),
         "events_per_sec_per_gpu": value / world,
         "vs_target_1M_events_per_sec_per_gpu": value / world / 1e6,
-        "output_groups": last.get("Output_DeviceSummary_Sink_InputEvents") if last else None,
         "generation_s": round(gen_s, 3),
     }
+    if last:
+        out["last_batch_outputs"] = {k: v for k, v in last.items() if k.startswith("Output_")}
+    if flow == "join":
+        out["reference_build_s"] = round(ref_s, 3)
+    if flow in ("window", "full") and proc.window_store is not None:
+        out["window_panes"] = len(proc.window_store.past)
+        out["window_retained_rows"] = proc.window_store.retained_rows()
+    if on_gpu:
+        out["max_hbm_allocated_gb"] = round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
     if args.profile_stages:
         out["stage_s"] = {k: round(v, 5) for k, v in proc.stage_times.items()}
     if rank == 0:

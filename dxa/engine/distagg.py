@@ -90,16 +90,18 @@ def _finish(call: A.Call, merged: Dict[str, PrimColumn]) -> PrimColumn:
     return PrimColumn("double", out, c > (0 if pop else 1))
 
 
-def distributed_aggregate(gexprs, keys, aggs: Dict, scope, ctx):
-    """Returns (key columns, {agg key → final column}, ngroups, dist tag)."""
-    from .expr import evaluate
+def _one_group(n, dev):
+    return G.Groups(torch.zeros(n, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
+                    torch.zeros(1, dtype=torch.int64, device=dev))
+
+
+def local_partials(gexprs, keys, aggs: Dict, scope, ctx):
+    """Phase 1: (partial table, plan, key names).  One row per local group: key columns ``__k<i>`` and partial
+    states ``__a<j>_<suffix>``; ``plan[agg key] = [(column, suffix, merge op)]``.  An empty global aggregate
+    contributes no row."""
     dev = scope.device
     n = scope.length
-    if gexprs:
-        groups = G.group_rows(keys)
-    else:
-        groups = G.Groups(torch.zeros(n, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
-                          torch.zeros(1, dtype=torch.int64, device=dev))
+    groups = G.group_rows(keys) if gexprs else _one_group(n, dev)
     names: List[str] = []
     cols = []
     key_names = []
@@ -119,37 +121,47 @@ def distributed_aggregate(gexprs, keys, aggs: Dict, scope, ctx):
             cols.append(col)
     ng_local = groups.ngroups if (gexprs or n) else 0
     if not gexprs and n == 0:
-        # an empty rank contributes no partial row
         cols = [c.take(torch.empty(0, dtype=torch.int64, device=dev)) for c in cols]
         ng_local = 0
-    partial = Table(names, cols, ng_local, dev)
-    if gexprs:
-        dest = P.owner_of(hash_columns([partial.column(k) for k in key_names])) if ng_local else \
+    return Table(names, cols, ng_local, dev), plan, key_names
+
+
+def exchange_partials(partial: Table, key_names: List[str], grouped: bool) -> Tuple[Table, str]:
+    """Route partial groups to their key owner (grouped) or to every rank (global aggregate)."""
+    dev = partial.device
+    if grouped:
+        dest = P.owner_of(hash_columns([partial.column(k) for k in key_names])) if partial.length else \
             torch.empty(0, dtype=torch.int64, device=dev)
-        got = P.shuffle_table(partial, dest)
-        tag = P.HASHED
-    else:
-        got = P.allgather_table(partial)
-        tag = P.REPLICATED
+        return P.shuffle_table(partial, dest), P.HASHED
+    return P.allgather_table(partial), P.REPLICATED
+
+
+def merge_partials(got: Table, plan, key_names: List[str], aggs: Dict, grouped: bool):
+    """Phase 2: re-group partial rows and merge their states → (key columns, {agg key → final column}, ngroups)."""
+    dev = got.device
     m = got.length
-    if gexprs:
+    if grouped:
         g2 = G.group_rows([got.column(k) for k in key_names]) if m else G.Groups(
             torch.empty(0, dtype=torch.int64, device=dev), 0, torch.empty(0, dtype=torch.int64, device=dev))
     else:
-        g2 = G.Groups(torch.zeros(m, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
-                      torch.zeros(1, dtype=torch.int64, device=dev))
+        g2 = _one_group(m, dev)
     ng = g2.ngroups
-    out_keys = [got.column(k).take(g2.rep) for k in key_names] if gexprs else []
+    out_keys = [got.column(k).take(g2.rep) for k in key_names] if grouped else []
     finals = {}
     for ak, call in aggs.items():
         merged = {}
         for nm, suffix, op in plan[ak]:
             c = got.column(nm)
-            if m == 0:
-                merged[suffix] = _empty_merge(c, op, ng, dev)
-            else:
-                merged[suffix] = G.aggregate(g2, c, op, m)
+            merged[suffix] = _empty_merge(c, op, ng, dev) if m == 0 else G.aggregate(g2, c, op, m)
         finals[ak] = _finish(call, merged)
+    return out_keys, finals, ng
+
+
+def distributed_aggregate(gexprs, keys, aggs: Dict, scope, ctx):
+    """Returns (key columns, {agg key → final column}, ngroups, dist tag)."""
+    partial, plan, key_names = local_partials(gexprs, keys, aggs, scope, ctx)
+    got, tag = exchange_partials(partial, key_names, bool(gexprs))
+    out_keys, finals, ng = merge_partials(got, plan, key_names, aggs, bool(gexprs))
     return out_keys, finals, ng, tag
 
 

@@ -182,6 +182,7 @@ class Processor:
         base = f"{S.NAME_PREFIX}ProcessedInput"
         cat = Catalog()
         for name, t in self.reference.items():
+            t.static = True
             cat.register(name, t)
         cat._built = getattr(self, "_ref_built", {})
         self._ref_built = cat._built
@@ -253,6 +254,14 @@ class Processor:
         low = text.strip().lower()
         if low.startswith(("set ", "cache ", "uncache ", "refresh ", "clear cache")) or not low:
             return
+        if low.startswith("create table"):
+            # accumulator DDL: the state table itself is configured (datax.job.process.statetable.*) and loaded at
+            # start-up, so the statement is a no-op here — as Spark's CREATE TABLE IF NOT EXISTS on an existing table
+            import re
+            m = re.match(r"create\s+table\s+(?:if\s+not\s+exists\s+)?([A-Za-z_][A-Za-z0-9_]*)", low)
+            if m and any(n.lower() == m.group(1) for n in self.state_tables):
+                return
+            raise EvalError(f"CREATE TABLE for an unconfigured accumulator: {text.strip()[:80]}")
         raise EvalError(f"unsupported command statement: {text}")
 
     def process_batch(self, raw: RawBatch, batch_time_us: int, interval_us: int,

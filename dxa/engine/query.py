@@ -51,6 +51,8 @@ class Catalog:
 
     # stream–static join support: hash tables over resident reference tables are built once
     def cached_build(self, key, builder):
+        """Memoise per-table derived structures (join build sides of static tables).  Values hold a reference to
+        their table so the ``id()`` in the key cannot be reused while cached."""
         b = self._built.get(key)
         if b is None:
             b = self._built[key] = builder()
@@ -215,6 +217,15 @@ def _refs_resolvable(e: A.Expr, scope: Scope) -> bool:
     return True
 
 
+def _static_table(src, catalog):
+    """(name, table) when ``src`` names a resident reference table (``Table.static``)."""
+    if isinstance(src, A.TableRef) and not src.timewindow:
+        t = catalog.get(src.name)
+        if t is not None and getattr(t, "static", False):
+            return src.name, t
+    return None
+
+
 def _join(j: A.Join, catalog, ctx) -> Scope:
     left = _relation(j.left, catalog, ctx)
     right = _relation(j.right, catalog, ctx)
@@ -266,7 +277,13 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         lk = [materialize(evaluate(e, left, ctx)) for e in lkeys]
         rk = [materialize(evaluate(e, right, ctx)) for e in rkeys]
         lk, rk = _coerce_keys(lk, rk)
-        li, ri = J.hash_join(lk, rk, kind if kind != "cross" else "inner")
+        built = None
+        static = _static_table(j.right, catalog)
+        if static is not None and kind in ("inner", "left", "semi", "anti") and rdist == P.REPLICATED:
+            # stream–static join: the reference table's hash table is built once and reused every batch
+            ck = (static[0], id(static[1]), tuple(e.key() for e in rkeys), tuple(c.dtype for c in rk))
+            built = catalog.cached_build(ck, lambda: (static[1], J.build_side(rk)))[1]
+        li, ri = J.hash_join(lk, rk, kind if kind != "cross" else "inner", built)
     if kind in ("semi", "anti"):
         out = Scope(left.names, [c.take(li) for c in left.cols], left.quals, int(li.shape[0]), dev)
         out.dist = out_dist
@@ -376,7 +393,101 @@ def _dup(scope: Scope, nm: str) -> bool:
     return sum(1 for n in scope.names if n.lower() == low) > 1
 
 
+NONDETERMINISTIC = {"rand", "random", "randn", "uuid", "now", "current_timestamp", "current_date",
+                    "unix_timestamp", "monotonically_increasing_id", "spark_partition_id"}
+
+
+def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
+    """GROUP BY over a window view answered from per-pane partial aggregates (see ``windows.PanedTable``).
+    Returns None when the query does not qualify (non-decomposable aggregates, no aggregation, …)."""
+    from . import distagg as D
+    from .windows import PanedTable
+    if not t.panes:
+        return None
+    proto = t.panes[0].table
+    empty = proto.take(torch.empty(0, dtype=torch.int64, device=proto.device))
+    items = _expand_items(sel, Scope.of_table(empty, alias))
+    aggs: Dict = {}
+    for e, _ in items:
+        _collect_aggs(e, ctx, aggs)
+    if sel.having is not None:
+        _collect_aggs(sel.having, ctx, aggs)
+    if not aggs and not sel.group_by:
+        return None
+    if not D.decomposable(aggs, ctx):
+        return None
+    exprs = [e for e, _ in items] + list(sel.group_by) + ([sel.where] if sel.where is not None else []) + (
+        [sel.having] if sel.having is not None else [])
+    cacheable = True
+    for e in exprs:
+        for node in A.walk(e):
+            if isinstance(node, A.Call) and (node.name in NONDETERMINISTIC or (
+                    node.name in ctx.udfs and not getattr(ctx.udfs[node.name], "deterministic", False))):
+                cacheable = False
+    fp = repr((alias, [e.key() for e in exprs], sel.where is not None, [nm for _, nm in items]))
+    gexprs = None
+    plan = key_names = None
+    parts = []
+    for pane, full in t.pieces():
+        cached = pane.partials.get(fp) if (full and cacheable) else None
+        if cached is None:
+            src = pane.table if full else t.clipped(pane)
+            scope = Scope.of_table(src, alias)
+            if sel.where is not None:
+                mask = predicate_mask(evaluate(sel.where, scope, ctx))
+                idx = torch.nonzero(mask).flatten()
+                scope = Scope(scope.names, [c.take(idx) for c in scope.cols], scope.quals, int(idx.shape[0]),
+                              scope.device)
+            gx = [_resolve_group_expr(g, scope, items) for g in sel.group_by]
+            keys = [materialize(evaluate(g, scope, ctx)) for g in gx]
+            if any(isinstance(k, (StructColumn, ArrayColumn)) for k in keys):
+                return None
+            partial, pl, kn = D.local_partials(gx, keys, aggs, scope, ctx)
+            cached = (partial, pl, kn, gx)
+            if full and cacheable:
+                pane.partials[fp] = cached
+        partial, plan, key_names, gexprs = cached
+        if partial.length:
+            parts.append(partial)
+    if plan is None:
+        return None
+    dev = proto.device
+    grouped = bool(sel.group_by)
+    got = concat_tables(parts) if parts else cached[0]
+    tag = P.REPLICATED
+    if P.active() and t.dist != P.REPLICATED:
+        got, tag = D.exchange_partials(got, key_names, grouped)
+    out_keys, finals, ng = D.merge_partials(got, plan, key_names, aggs, grouped)
+    subst = dict(finals)
+    for g, k in zip(gexprs, out_keys):
+        subst[g.key()] = k
+    escope = Scope([], [], [], ng, dev)
+    cols = [evaluate(e, escope, ctx, subst) for e, _ in items]
+    out = Table([nm for _, nm in items], cols, ng, dev)
+    if sel.having is not None:
+        out = out.filter(predicate_mask(evaluate(sel.having, escope, ctx, subst)))
+    out.dist = tag if grouped else P.REPLICATED
+    return out
+
+
+def _lookup(src: A.TableRef, catalog: Catalog):
+    name = src.name
+    if src.timewindow:
+        name = f"{src.name}_{src.timewindow.replace(' ', '')}"
+    return catalog.get(name)
+
+
 def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
+    if isinstance(sel.from_, A.TableRef) and not want_scope:
+        from .windows import PanedTable
+        t = _lookup(sel.from_, catalog)
+        if isinstance(t, PanedTable):
+            try:
+                out = _paned_aggregate(sel, t, sel.from_.alias or sel.from_.name.split(".")[-1], ctx)
+            except EvalError:
+                out = None
+            if out is not None:
+                return (distinct(out) if sel.distinct else out), None
     scope = _relation(sel.from_, catalog, ctx)
     sdist = getattr(scope, "dist", P.REPLICATED)
     if sel.where is not None:

@@ -66,6 +66,78 @@ def _compact_table(t: Table) -> Table:
     return Table(t.names, [comp(c) for c in t.columns], t.length, t.device)
 
 
+@dataclass
+class Pane:
+    """One retained micro-batch: its rows, event-time bounds of its valid rows, and cached per-query partials."""
+    key: int
+    table: Table
+    lo: int                  # min event time of rows with a valid timestamp
+    hi: int                  # max event time
+    all_valid: bool          # every row has a timestamp
+    partials: Dict[str, Table] = field(default_factory=dict)
+
+    def inside(self, lo: Optional[int], hi: Optional[int]) -> bool:
+        """All rows fall in [lo, hi): the pane can be used unfiltered (and its cached partials reused)."""
+        return self.all_valid and self.table.length > 0 and (lo is None or self.lo >= lo) and (
+            hi is None or self.hi < hi)
+
+    def outside(self, lo: Optional[int], hi: Optional[int]) -> bool:
+        return self.table.length == 0 or self.lo > self.hi or (lo is not None and self.hi < lo) or (
+            hi is not None and self.lo >= hi)
+
+
+class PanedTable(Table):
+    """A window view = union of panes clipped to [lo, hi), kept *virtual*: nothing is concatenated unless a consumer
+    needs rows.  Decomposable GROUP BY queries over it are answered from per-pane partial aggregates (cached on the
+    pane for panes wholly inside the window), so a 5-minute / 1-second sliding aggregate costs one new pane's
+    partials + the boundary panes + a merge of (panes × groups) partial rows, instead of re-aggregating 300 batches."""
+
+    def __init__(self, store: "WindowStore", panes: List[Pane], lo: Optional[int], hi: Optional[int], names,
+                 device):
+        self.store = store
+        self.panes = panes
+        self.lo, self.hi = lo, hi
+        self.names = list(names)
+        self._device = torch.device(device)
+        self.dist = panes[0].table.dist if panes else "replicated"
+        self._mat: Optional[Table] = None
+        self._len: Optional[int] = None
+
+    def pieces(self) -> List[Tuple[Pane, bool]]:
+        """(pane, fully inside) for every pane that intersects the range."""
+        return [(p, p.inside(self.lo, self.hi)) for p in self.panes if not p.outside(self.lo, self.hi)]
+
+    def clipped(self, pane: Pane) -> Table:
+        return self.store._range(pane.table, self.lo, self.hi)
+
+    def _materialize(self) -> Table:
+        if self._mat is None:
+            parts = [p.table if full else self.clipped(p) for p, full in self.pieces()]
+            parts = [t for t in parts if t.length] or [self.panes[0].table.slice(0, 0)]
+            t = concat_tables(parts)
+            self._mat = Table(self.names, t.columns, t.length, self._device)
+            self._len = t.length
+        return self._mat
+
+    @property
+    def columns(self):
+        return self._materialize().columns
+
+    @property
+    def length(self):
+        if self._len is None:
+            n = 0
+            for p, full in self.pieces():
+                n += p.table.length if full else self.clipped(p).length
+            self._len = n
+        return self._len
+
+    def _like(self, names, cols, length) -> Table:
+        t = Table(names, cols, length, self._device)
+        t.dist = self.dist
+        return t
+
+
 class WindowStore:
     def __init__(self, conf: TimeWindowConf):
         self.conf = conf
@@ -95,29 +167,43 @@ class WindowStore:
             return t
         return t.filter(m)
 
+    def _pane(self, key: int, t: Table) -> Pane:
+        if t.length == 0:
+            return Pane(key, t, 0, -1, True)
+        ts, ok = self._ts(t)
+        big = torch.iinfo(torch.int64).max
+        stats = torch.stack([torch.where(ok, ts, torch.full_like(ts, big)).min(),
+                             torch.where(ok, ts, torch.full_like(ts, -big)).max(),
+                             ok.sum()]).tolist()
+        return Pane(key, t, int(stats[0]), int(stats[1]), int(stats[2]) == t.length)
+
     def process(self, projected: Table, batch_time_us: int, interval_us: int):
-        """Returns (views: name → Table, current_count)."""
+        """Returns (views: name → Table, current_count).  Window views are ``PanedTable``s (virtual unions)."""
         c = self.conf
         E = batch_time_us - c.watermark_us
         S = E - c.max_window_us
         kept = self._range(projected, E, None)
         kept = _compact_table(kept)
+        kept.dist = projected.dist
         cut = batch_time_us - (c.watermark_us + c.max_window_us)
         for t in [t for t in self.past if t <= cut]:
             del self.past[t]
+        cur = self._pane(batch_time_us, kept)
         if len(self.past) > 1 or (not c.legacy_union_quirk and self.past):
-            U = concat_tables([kept] + list(self.past.values()))
+            panes = [cur] + list(self.past.values())
         else:
-            U = kept
+            panes = [cur]
         from ..config.settings import NAME_PREFIX
         base = f"{NAME_PREFIX}ProcessedInput"
-        views = {f"{base}_Window": self._range(U, S, E)}
+        names = projected.names
+        dev = projected.device
+        views = {f"{base}_Window": PanedTable(self, panes, S, E, names, dev)}
         for name, w in c.windows.items():
-            views[name] = self._range(U, E - w, E)
-        views[base] = self._range(U, E - interval_us, E)
+            views[name] = PanedTable(self, panes, E - w, E, names, dev)
+        views[base] = PanedTable(self, panes, E - interval_us, E, names, dev)
         views[f"{base}_Batch"] = projected
-        self.past[batch_time_us] = kept
+        self.past[batch_time_us] = cur
         return views, kept.length
 
     def retained_rows(self) -> int:
-        return sum(t.length for t in self.past.values())
+        return sum(p.table.length for p in self.past.values())

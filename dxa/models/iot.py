@@ -115,32 +115,212 @@ def leaf_count(fields=IOT_FIELDS) -> int:
     return sum(leaf_count(f["properties"]) if f["type"] == "struct" else 1 for f in fields)
 
 
+WINDOW_TRANSFORM = """--DataXQuery--
+DeviceWindow = SELECT deviceDetails.deviceId,
+        deviceDetails.deviceType,
+        deviceDetails.homeId,
+        COUNT(*) AS EventCount,
+        MAX(eventTimeStamp) AS MaxEventTime,
+        MIN(deviceDetails.status) AS MinReading,
+        MAX(deviceDetails.status) AS MaxReading,
+        AVG(telemetry.temperature) AS AvgTemperature,
+        MAX(telemetry.temperature) AS MaxTemperature,
+        AVG(telemetry.humidity) AS AvgHumidity,
+        SUM(telemetry.power) AS TotalPower,
+        MIN(telemetry.batteryLevel) AS MinBattery
+    FROM DataXProcessedInput TIMEWINDOW('5 minutes')
+    GROUP BY deviceId, deviceType, homeId
+
+--DataXQuery--
+HotDeviceAlerts = SELECT MaxEventTime AS EventTime,
+        'HotDevice5min' AS MetricName,
+        MaxTemperature AS Metric,
+        'iotbench' AS Product,
+        CONCAT('device ', deviceId, ' home ', homeId) AS Pivot1
+    FROM DeviceWindow
+    WHERE MaxTemperature > 44.99
+"""
+
+REF_ROWS = 100_000_000
+
+JOIN_TRANSFORM = """--DataXQuery--
+Enriched = SELECT r.zone AS zone,
+        r.tier AS tier,
+        deviceDetails.deviceType AS deviceType,
+        telemetry.power AS power,
+        telemetry.temperature AS temperature
+    FROM DataXProcessedInput
+    JOIN RefDevices r ON sequenceNumber % {ref_rows} = r.refKey
+
+--DataXQuery--
+ZoneSummary = SELECT zone, tier, deviceType,
+        COUNT(*) AS EventCount,
+        SUM(power) AS TotalPower,
+        AVG(temperature) AS AvgTemperature,
+        MAX(temperature) AS MaxTemperature
+    FROM Enriched
+    GROUP BY zone, tier, deviceType
+"""
+
+FULL_USER_CODE = """--DataXStates--
+CREATE TABLE DeviceState (deviceId long, homeId long, deviceType string, LastSeen timestamp, EventCount long,
+    MaxTemperature double);
+
+--DataXQuery--
+DeviceWindow = SELECT deviceDetails.deviceId AS deviceId,
+        deviceDetails.homeId AS homeId,
+        deviceDetails.deviceType AS deviceType,
+        COUNT(*) AS EventCount,
+        MAX(eventTimeStamp) AS LastSeen,
+        AVG(telemetry.temperature) AS AvgTemperature,
+        MAX(telemetry.temperature) AS MaxTemperature,
+        AVG(healthScore(telemetry.batteryLevel, telemetry.signalStrength)) AS AvgHealth
+    FROM DataXProcessedInput TIMEWINDOW('5 minutes')
+    GROUP BY deviceId, homeId, deviceType;
+
+--DataXQuery--
+DeviceNamed = SELECT w.deviceId, w.homeId, w.deviceType, w.EventCount, w.LastSeen, w.MaxTemperature, w.AvgHealth,
+        d.deviceName
+    FROM DeviceWindow w
+    JOIN myDevicesRefdata d ON w.deviceId = d.deviceId AND w.homeId = d.homeId;
+
+--DataXQuery--
+DeviceState = SELECT deviceId, homeId, deviceType,
+        MAX(LastSeen) AS LastSeen,
+        MAX(EventCount) AS EventCount,
+        MAX(MaxTemperature) AS MaxTemperature
+    FROM (SELECT deviceId, homeId, deviceType, LastSeen, EventCount, MaxTemperature FROM DeviceWindow
+          UNION ALL
+          SELECT deviceId, homeId, deviceType, LastSeen, EventCount, MaxTemperature FROM DeviceState) s
+    GROUP BY deviceId, homeId, deviceType;
+
+--DataXQuery--
+Tagged = ProcessRules(DataXProcessedInput);
+
+--DataXQuery--
+UnhealthyDevices = SELECT deviceName, deviceType, homeId, AvgHealth
+    FROM DeviceNamed
+    WHERE AvgHealth < 45;
+
+OUTPUT UnhealthyDevices TO Metrics;
+"""
+
+FULL_RULES = [
+    {"$ruleId": "hot", "$productId": "iotbench", "$ruleType": "SimpleRule", "$ruleDescription": "hot device",
+     "$severity": "Critical", "$condition": "telemetry.temperature > 44.5", "$tagname": "Tag", "$tag": "Hot",
+     "$isAlert": True, "$alertsinks": ["Metrics"], "schemaTableName": "DataXProcessedInput"},
+    {"$ruleId": "lowbat", "$productId": "iotbench", "$ruleType": "SimpleRule", "$ruleDescription": "battery low",
+     "$severity": "Medium", "$condition": "telemetry.batteryLevel < 1.0 AND deviceDetails.status = 1",
+     "$tagname": "Tag", "$tag": "LowBattery", "$isAlert": True, "$alertsinks": ["Metrics"],
+     "schemaTableName": "DataXProcessedInput"},
+    {"$ruleId": "noisy", "$productId": "iotbench", "$ruleType": "SimpleRule", "$ruleDescription": "noisy room",
+     "$severity": "Low", "$condition": "telemetry.noise > 109.9", "$tagname": "Tag", "$tag": "Noisy",
+     "$isAlert": False, "schemaTableName": "DataXProcessedInput"},
+]
+
+VARIANTS = ("groupby", "window", "join", "full")
+
+
 def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Optional[Dict[str, str]] = None,
-                  name: str = "iotbench") -> SettingDictionary:
+                  name: str = "iotbench", variant: str = "groupby", ref_rows: int = REF_ROWS) -> SettingDictionary:
+    """Job settings for one of the benchmark flows (BASELINE.json configs 2-5):
+
+    * ``groupby`` — per-batch GROUP BY + alert view (config 2);
+    * ``window``  — the same aggregate over a 5-minute sliding window, 1-s slide (config 3);
+    * ``join``    — stream–static join against a ``ref_rows``-row reference table resident in HBM (config 4;
+      the table itself is built on device by ``reference_table``);
+    * ``full``    — rules (codegen'd ProcessRules + alerts) + windowed SQL with a device UDF + reference-data join +
+      accumulator state table (config 5).
+    """
     from ..engine.types import schema_to_json
+    if variant not in VARIANTS:
+        raise ValueError(f"unknown flow variant {variant}")
     workdir = workdir or tempfile.mkdtemp(prefix="dxa_iot_")
     os.makedirs(workdir, exist_ok=True)
     paths = {"schema": os.path.join(workdir, "inputschema.json"),
              "projection": os.path.join(workdir, "projection.txt"),
              "transform": os.path.join(workdir, f"{name}-combined.txt")}
-    with open(paths["schema"], "w") as f:
-        f.write(schema_to_json(iot_spark_schema()))
-    with open(paths["projection"], "w") as f:
-        f.write(PROJECTION)
-    with open(paths["transform"], "w") as f:
-        f.write(TRANSFORM)
+    outputs = {"groupby": ["DeviceSummary", "HotDeviceAlerts"], "window": ["DeviceWindow", "HotDeviceAlerts"],
+               "join": ["ZoneSummary"], "full": ["DeviceNamed", "DeviceState"]}[variant]
     d = {
         "datax.job.name": name,
         "datax.job.input.default.blobschemafile": paths["schema"],
         "datax.job.input.default.streaming.intervalinseconds": "1",
         "datax.job.process.projection": paths["projection"],
         "datax.job.process.transform": paths["transform"],
-        f"datax.job.output.DeviceSummary.{sink}.enabled": "true",
-        f"datax.job.output.HotDeviceAlerts.{sink}.enabled": "true",
     }
+    if variant == "groupby":
+        transform = TRANSFORM
+    elif variant == "window":
+        transform = WINDOW_TRANSFORM
+    elif variant == "join":
+        transform = JOIN_TRANSFORM.format(ref_rows=ref_rows)
+    else:
+        from ..sql.codegen import generate_code
+        rc = generate_code(FULL_USER_CODE, FULL_RULES, "iotbench")
+        transform = rc.code
+        for tables, _sink in rc.outputs:
+            outputs += [t.strip() for t in tables.split(",") if t.strip() not in outputs]
+        ref = os.path.join(workdir, "devices.csv")
+        with open(ref, "w") as f:
+            f.write("deviceId,homeId,deviceName\n")
+            for dv in range(1, N_DEVICES + 1):
+                for h in range(1, N_HOMES + 1):
+                    f.write(f"{dv},{h},device-{dv}-home-{h}\n")
+        d.update({
+            "datax.job.input.default.referencedata.myDevicesRefdata.path": ref,
+            "datax.job.input.default.referencedata.myDevicesRefdata.format": "csv",
+            "datax.job.input.default.referencedata.myDevicesRefdata.header": "true",
+            "datax.job.process.jar.udf.healthScore.class": "dxa.udf.samples:HealthScore",
+            "datax.job.process.statetable.DeviceState.schema":
+                "deviceId long, homeId long, deviceType string, LastSeen timestamp, EventCount long, "
+                "MaxTemperature double",
+            "datax.job.process.statetable.DeviceState.location": os.path.join(workdir, "state", "DeviceState"),
+        })
+    if variant in ("window", "full"):
+        d.update({
+            "datax.job.process.timewindow.DataXProcessedInput_5minutes.windowduration": "5 minutes",
+            "datax.job.process.watermark": "2 second",
+            "datax.job.process.timestampcolumn": "eventTimeStamp",
+        })
+    for o in dict.fromkeys(outputs):
+        d[f"datax.job.output.{o}.{sink}.enabled"] = "true"
+    with open(paths["schema"], "w") as f:
+        f.write(schema_to_json(iot_spark_schema()))
+    with open(paths["projection"], "w") as f:
+        f.write(PROJECTION)
+    with open(paths["transform"], "w") as f:
+        f.write(transform)
     if extra:
         d.update(extra)
     return SettingDictionary(d)
+
+
+def reference_table(n_rows: int, device):
+    """Synthetic device-registry reference table resident in HBM: refKey (0..n-1, shuffled), zone (0..999),
+    tier (one of 4 strings, stored as views into a shared 24-byte arena)."""
+    from ..engine.column import PrimColumn, StrColumn, Table
+    device = torch.device(device)
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    keys = torch.randperm(n_rows, generator=g).to(device) if n_rows <= 4_000_000 else \
+        _device_perm(n_rows, device)
+    zone = (keys * 2654435761) % 1000
+    tiers = [b"bronze", b"silver", b"gold", b"platinum"]
+    arena = torch.tensor(list(b"".join(tiers)), dtype=torch.uint8, device=device)
+    tstart = torch.tensor([0, 6, 12, 16], dtype=torch.int64, device=device)
+    tlen = torch.tensor([6, 6, 4, 8], dtype=torch.int32, device=device)
+    ti = keys % 4
+    tier = StrColumn(arena, tstart[ti], tlen[ti])
+    t = Table(["refKey", "zone", "tier"], [PrimColumn("long", keys), PrimColumn("long", zone), tier], n_rows,
+              device)
+    return t
+
+
+def _device_perm(n: int, device):
+    """A bijective shuffle of 0..n-1 without a host round trip: sort by a hash of the index."""
+    i = torch.arange(n, dtype=torch.int64, device=device)
+    h = (i * -7046029254386353131) ^ ((i >> 29) * 0x632BE59BD9B4E019)
+    return torch.argsort(h)
 
 
 def program():

@@ -66,6 +66,25 @@ class UdafLastThreshold(UDAF):
         return self.update(buf, other["eventTime"], other["thresholdType"], other["val1"], other["val2"])
 
 
+class HealthScore:
+    """Device-side UDF (the MI355X counterpart of a Scala UDF): ``healthScore(batteryLevel, signalStrength)`` →
+    0..100 from battery percentage and RSSI in dBm, evaluated on whole columns with torch ops (no host round trip)."""
+    return_type = "double"
+    deterministic = True          # pure function of its inputs: window partials that use it can be cached
+
+    def __call__(self, cols, ctx, n, device):
+        import torch
+        from ..engine.column import ConstColumn, PrimColumn
+        b, s = [c.materialize() if isinstance(c, ConstColumn) else c for c in cols]
+        bat = b.data.to(torch.float64).clamp(0, 100)
+        sig = ((s.data.to(torch.float64) + 110.0) * (100.0 / 70.0)).clamp(0, 100)
+        valid = None
+        for c in (b, s):
+            if c.valid is not None:
+                valid = c.valid if valid is None else valid & c.valid
+        return PrimColumn("double", 0.7 * bat + 0.3 * sig, valid)
+
+
 REFERENCE_CLASS_MAP = {
     "datax.sample.udf.UdfHelloWorld": UdfHelloWorld,
     "datax.sample.dynamicudf.DynamicUdfHelloWorld": DynamicUdfHelloWorld,

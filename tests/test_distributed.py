@@ -64,6 +64,8 @@ def _worker(rank, world, port, q):
             if P.dist_of(out) != P.REPLICATED:
                 out = P.allgather_table(out)
             results.append(out.to_pylist())
+        # paned window aggregation over partitioned panes (partials exchanged, not rows)
+        results.append(_window_results(t, P))
         # raw shuffle round trip
         dest = torch.tensor([i % world for i in range(t.length)], dtype=torch.int64)
         got = P.shuffle_table(t, dest)
@@ -74,6 +76,35 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
     except Exception:
         q.put((rank, None, traceback.format_exc()))
+
+
+WINDOW_QUERIES = ["SELECT k, COUNT(*) AS c, SUM(v) AS sv, AVG(v) AS av FROM WV GROUP BY k",
+                  "SELECT COUNT(*) AS c, MIN(v) AS mn FROM WV"]
+
+
+def _window_results(t, P):
+    from dxa.engine.column import PrimColumn
+    from dxa.engine.expr import EvalContext
+    from dxa.engine.query import Catalog, run_sql
+    from dxa.engine.windows import TimeWindowConf, WindowStore
+    S = 1_000_000
+    store = WindowStore(TimeWindowConf({"WV": 10 * S}, True, "ts", 0, 10 * S, False))
+    views = None
+    for b in range(4):
+        T = (100 + b) * S
+        ts = PrimColumn("timestamp", torch.full((t.length,), T + 1, dtype=torch.int64))
+        tb = t.with_column("ts", ts)
+        tb.dist = t.dist
+        views, _ = store.process(tb, T, S)
+    cat = Catalog()
+    cat.register("WV", views["WV"])
+    out = []
+    for qsql in WINDOW_QUERIES:
+        r = run_sql(qsql, cat, EvalContext())
+        if P.active() and P.dist_of(r) != P.REPLICATED:
+            r = P.allgather_table(r)
+        out.append(r.to_pylist())
+    return out
 
 
 def _free_port():
@@ -112,6 +143,11 @@ def test_two_rank_queries_match_single_process():
         expect = _canon(run_sql(qsql, cat, EvalContext()).to_pylist())
         for r in (0, 1):
             assert _canon(res[r][i]) == expect, (qsql, r)
+    # windowed: 3 earlier batches (the current one is after E) of all rows
+    expect_w = _window_results(Table.from_pylist(rows, schema), type("NoP", (), {"active": staticmethod(lambda: False)}))
+    for r in (0, 1):
+        for i in range(len(WINDOW_QUERIES)):
+            assert _canon(res[r][len(QUERIES)][i]) == _canon(expect_w[i]), (WINDOW_QUERIES[i], r)
     # shuffle round trip preserves the multiset of rows
     for r in (0, 1):
         assert _canon(res[r][-1]) == _canon(rows)
