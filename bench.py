@@ -61,6 +61,8 @@ def main():
                     help="pinned: H2D copy of raw bytes every step; device: bytes already in HBM; gpu-sim: GPU "
                          "generator renders each batch")
     ap.add_argument("--profile-stages", action="store_true")
+    ap.add_argument("--sync-outputs", action="store_true",
+                    help="finish each batch's sink writes before the next batch starts (default: pipelined)")
     args = ap.parse_args()
     flow = args.flow
     warmup = DEFAULT_WARMUP[flow] if args.warmup is None else args.warmup
@@ -91,7 +93,7 @@ def main():
         parallel.init(dist.group.WORLD, device)
 
     proc = Processor(iot.flow_settings(workdir=f"/tmp/dxa_bench_{flow}_{rank}", variant=flow,
-                                       ref_rows=args.ref_rows), device)
+                                       ref_rows=args.ref_rows), device, pipeline_outputs=not args.sync_outputs)
     t_ref = time.perf_counter()
     if flow == "join":
         proc.reference["RefDevices"] = iot.reference_table(args.ref_rows, device)
@@ -152,6 +154,7 @@ def main():
         staged[i] = (db, do, ev)
 
     lat = []
+    proc.on_batch_complete = lambda bt, m: lat.append(m["Latency-Process"])
 
     def step(i):
         db, do, ev = staged.pop(i)
@@ -162,13 +165,13 @@ def main():
             do.record_stream(cur)
         stage(i + 1)
         m = proc.process_batch(RawBatch(db, do, E), batch_time(i), interval_us)
-        lat.append(m["Latency-Process"])
         sizes.append(db.shape[0])
         return m
 
     stage(0)
     for i in range(warmup):
         step(i)
+    proc.drain()
     if on_gpu:
         torch.cuda.synchronize(device)
     if world > 1:
@@ -178,7 +181,8 @@ def main():
     t0 = time.perf_counter()
     last = None
     for i in range(warmup, warmup + args.steps):
-        last = step(i)
+        step(i)
+    last = proc.drain() or proc.last_metrics           # the last batch's outputs complete inside the timed region
     if on_gpu:
         torch.cuda.synchronize(device)
     if world > 1:
@@ -219,7 +223,8 @@ def main():
         "config": {"model": MODEL[flow].format(ref=args.ref_rows), "flow": flow,
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
                    "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,
-                   "source": source, "batch_interval_s": interval_us / 1e6},
+                   "source": source, "batch_interval_s": interval_us / 1e6,
+                   "outputs": "sync" if args.sync_outputs else "pipelined (batch t sinks overlap batch t+1)"},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),
         "events_per_sec_per_gpu": value / world,

@@ -157,6 +157,26 @@ def merge_partials(got: Table, plan, key_names: List[str], aggs: Dict, grouped: 
     return out_keys, finals, ng
 
 
+def combine_partials(got: Table, plan, key_names: List[str], grouped: bool) -> Table:
+    """Merge partial rows into fewer partial rows of the *same* layout (partial states stay partial) — used to
+    pre-combine blocks of window panes."""
+    dev = got.device
+    m = got.length
+    if m == 0:
+        return got
+    g2 = G.group_rows([got.column(k) for k in key_names]) if grouped else _one_group(m, dev)
+    names, cols = [], []
+    for k in key_names:
+        names.append(k)
+        cols.append(got.column(k).take(g2.rep))
+    for entries in plan.values():
+        for nm, _suffix, op in entries:
+            names.append(nm)
+            cols.append(G.aggregate(g2, got.column(nm), op, m))
+    t = Table(names, cols, g2.ngroups, dev)
+    return t
+
+
 def distributed_aggregate(gexprs, keys, aggs: Dict, scope, ctx):
     """Returns (key columns, {agg key → final column}, ngroups, dist tag)."""
     partial, plan, key_names = local_partials(gexprs, keys, aggs, scope, ctx)

@@ -51,6 +51,8 @@ class StreamingHost:
         pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dxa-prefetch") if self.pipeline else None
         next_time = self._batch_time(int(time.time() * 1e6)) + (self.interval_us if self.realtime else 0)
         prefetched = None
+        prev_cb = self.processor.on_batch_complete
+        self.processor.on_batch_complete = self._completed
         try:
             while not self._stop.is_set():
                 if self.max_batches is not None and self.batches >= self.max_batches:
@@ -70,23 +72,27 @@ class StreamingHost:
                 if raw is None:
                     break
                 try:
-                    metrics = self.processor.process_batch(raw, bt, self.interval_us,
-                                                           _dt.datetime.utcfromtimestamp(bt / 1e6))
+                    self.processor.process_batch(raw, bt, self.interval_us, _dt.datetime.utcfromtimestamp(bt / 1e6))
                 except Exception:
                     log.exception("batch failed; stopping the job (restart resumes from the last checkpoint)")
                     time.sleep(1.0)
                     raise
-                self.source.commit(bt)
                 self.batches += 1
-                self.history.append(metrics)
-                if self.on_batch:
-                    self.on_batch(bt, metrics)
                 next_time = bt + self.interval_us
+            self.processor.drain()
         finally:
+            self.processor.on_batch_complete = prev_cb
             if pool is not None:
                 pool.shutdown(wait=False, cancel_futures=True)
             self.source.close()
         return self.history
+
+    def _completed(self, bt: int, metrics: Dict[str, float]):
+        """A batch's outputs are written: only now are its source offsets committed (at-least-once)."""
+        self.source.commit(bt)
+        self.history.append(metrics)
+        if self.on_batch:
+            self.on_batch(bt, metrics)
 
 
 _TOKEN = re.compile(r"\{([^}]+)\}")

@@ -59,7 +59,8 @@ def _read_lines(path: str) -> List[str]:
 
 class Processor:
     def __init__(self, settings: S.SettingDictionary, device="cpu", metric_store=None, udfs=None, udafs=None,
-                 normalizer=None, pre_projection=None, parse_prune: bool = True):
+                 normalizer=None, pre_projection=None, parse_prune: bool = True,
+                 pipeline_outputs: Optional[bool] = None):
         self.settings = settings
         self.device = torch.device(device)
         self.name = settings.job_name()
@@ -102,6 +103,13 @@ class Processor:
         self.last_views: Dict[str, Table] = {}
         self.keep_views = False
         self.stage_times: Dict[str, float] = {}
+        self._parsed: Dict[str, object] = {}
+        # output pipelining: batch t's sink work overlaps batch t+1's device work (at most one batch in flight)
+        self.pipeline_outputs = pipeline_outputs if pipeline_outputs is not None else \
+            d.get_bool(S.PROCESS_PREFIX + "pipelineoutputs", False)
+        self._inflight: Optional[_InFlight] = None
+        self.completed: List = []
+        self.on_batch_complete = None
 
     # ------------------------------------------------------------------------------------------------------------
     def _load_reference_data(self) -> Dict[str, Table]:
@@ -177,7 +185,8 @@ class Processor:
         return table
 
     def route(self, projected: Table, batch_time_us: int, interval_us: int, ctx: EvalContext,
-              partition_time: _dt.datetime) -> Dict[str, float]:
+              partition_time: _dt.datetime, t_start: Optional[float] = None) -> Dict[str, float]:
+        t_start = time.perf_counter() if t_start is None else t_start
         metrics: Dict[str, float] = {}
         base = f"{S.NAME_PREFIX}ProcessedInput"
         cat = Catalog()
@@ -208,27 +217,56 @@ class Processor:
                 if cmd.command_type == COMMAND_COMMAND:
                     self._run_command(cmd.text)
                     continue
-                q = parse_query(cmd.text)
+                q = self._parsed.get(cmd.text)
+                if q is None:
+                    q = self._parsed[cmd.text] = parse_query(cmd.text)     # parsed once, reused every batch
+                ts = time.perf_counter() if _SYNC_STAGES else 0.0
                 result = execute(q, cat, ctx)
+                if _SYNC_STAGES:
+                    self._sync()
+                    self.stage_times[f"sql:{cmd.name}"] = time.perf_counter() - ts
                 st = self.state_tables.get(cmd.name)
                 if st is not None:
+                    self._complete_inflight()      # the previous batch's state flip must be durable first
                     result = st.overwrite(result)
                 cat.register(cmd.name, result)
                 views[cmd.name] = result
         self._sync()
         self.stage_times["transform"] = time.perf_counter() - t0
-        # outputs (in parallel on the host pool)
+        # outputs: device half staged here (filters + async D2H into pinned memory), host half (JSON rendering +
+        # sink writes) on the output pool — pipelined, it overlaps the next batch's GPU work
         t1 = time.perf_counter()
-        futures = []
-        from ..io.sinks import _pool
+        staged = []
         for op in self.outputs:
             t = views.get(op.name) or cat.get(op.name)
             if t is None:
                 raise EvalError(f"could not find data set name '{op.name}' for output '{op.name}'")
             if P.active() and P.dist_of(t) == P.REPLICATED and P.rank() != 0:
                 t = t.slice(0, 0)      # replicated results are written once, by rank 0
-            futures.append((op.name, _pool.submit(op.output, t, partition_time, ctx)))
-        for name, f in futures:
+            staged.append((op.name, op.stage(t, ctx)))
+        self._complete_inflight()
+        from ..io.sinks import _pool
+        fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(st.finish, partition_time))
+                                                 for name, st in staged], t_start)
+        self._inflight = fl
+        self.stage_times["output_stage"] = time.perf_counter() - t1
+        if self.keep_views:
+            self.last_views = {**{k: cat.get(k) for k in cat.names()}, **views}
+        if not self.pipeline_outputs:
+            self._complete_inflight()
+            self._sync()
+            self.stage_times["output"] = time.perf_counter() - t1
+        return fl.metrics
+
+    def _complete_inflight(self):
+        """Finish the in-flight batch: collect sink counts, all-reduce the batch metrics across ranks, persist state
+        tables (after outputs, as the reference), stamp latencies, emit metrics and fire ``on_batch_complete``."""
+        fl = self._inflight
+        if fl is None:
+            return None
+        self._inflight = None
+        metrics = fl.metrics
+        for name, f in fl.futures:
             for k, v in f.result().items():
                 metrics[f"Output_{name}_{k}"] = float(v)
         if P.active():
@@ -236,14 +274,25 @@ class Processor:
             keys = sorted(metrics)
             vec = torch.tensor([float(metrics[k]) for k in keys], dtype=torch.float64, device=self.device)
             P.all_reduce_sum(vec)
-            metrics = dict(zip(keys, vec.tolist()))
-        self._sync()
-        self.stage_times["output"] = time.perf_counter() - t1
+            metrics.update(zip(keys, vec.tolist()))
         for st in self.state_tables.values():
             st.persist()
-        if self.keep_views:
-            self.last_views = {**{k: cat.get(k) for k in cat.names()}, **views}
+        metrics["Latency-Process"] = time.perf_counter() - fl.t0
+        metrics["Latency-Batch"] = (time.time() * 1e6 - fl.batch_time_us) / 1e6
+        if P.rank() == 0:
+            self.metric_logger.send_batch_metrics(metrics, fl.batch_time_us // 1000)
+        self.last_metrics = metrics
+        self.completed.append((fl.batch_time_us, metrics))
+        del self.completed[:-64]
+        if self.on_batch_complete is not None:
+            self.on_batch_complete(fl.batch_time_us, metrics)
         return metrics
+
+    def drain(self) -> Optional[Dict[str, float]]:
+        """Complete the in-flight batch (pipelined mode); returns its metrics."""
+        m = self._complete_inflight()
+        self._sync()
+        return m
 
     def _sync(self):
         """Stage attribution (DXA_SYNC_STAGES=1): make per-stage wall times include their device work."""
@@ -266,6 +315,10 @@ class Processor:
 
     def process_batch(self, raw: RawBatch, batch_time_us: int, interval_us: int,
                       partition_time: Optional[_dt.datetime] = None) -> Dict[str, float]:
+        """Run one micro-batch.  Synchronous mode returns the batch's complete metrics.  Pipelined mode
+        (``pipeline_outputs``) returns as soon as the batch's outputs are staged — its metrics (with sink counts and
+        ``Latency-Process`` measured to output completion) arrive through ``on_batch_complete`` / ``completed``
+        when the next batch (or ``drain()``) completes it."""
         t0 = time.perf_counter()
         ctx = EvalContext(now_us=int(time.time() * 1e6), udfs=self.udfs, udafs=self.udafs, device=self.device)
         for refresh in self.udf_refreshers:
@@ -273,19 +326,28 @@ class Processor:
         try:
             projected = self.project(raw, batch_time_us, ctx)
             metrics = self.route(projected, batch_time_us, interval_us, ctx,
-                                 partition_time or _dt.datetime.utcnow())
-            metrics["Latency-Process"] = time.perf_counter() - t0
-            metrics["Latency-Batch"] = (time.time() * 1e6 - batch_time_us) / 1e6
-            if P.rank() == 0:
-                self.metric_logger.send_batch_metrics(metrics, batch_time_us // 1000)
-            self.last_metrics = metrics
+                                 partition_time or _dt.datetime.utcnow(), t0)
             self.batches += 1
             return metrics
         except Exception:
             log.exception("batch %s failed", batch_time_us)
+            try:
+                self._complete_inflight()       # the previous batch still gets its outputs and metrics
+            except Exception:  # noqa: BLE001
+                self._inflight = None
             from ..telemetry.appinsights import track_exception
             track_exception("ProcessDataFrame", batch_time_us)
             raise
+
+
+class _InFlight:
+    __slots__ = ("batch_time_us", "metrics", "futures", "t0")
+
+    def __init__(self, batch_time_us, metrics, futures, t0):
+        self.batch_time_us = batch_time_us
+        self.metrics = metrics
+        self.futures = futures
+        self.t0 = t0
 
 
 def _fmt_ts(us: int) -> str:

@@ -397,6 +397,13 @@ NONDETERMINISTIC = {"rand", "random", "randn", "uuid", "now", "current_timestamp
                     "unix_timestamp", "monotonically_increasing_id", "spark_partition_id"}
 
 
+BLOCK = 16
+
+
+class _NotPaned(Exception):
+    pass
+
+
 def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     """GROUP BY over a window view answered from per-pane partial aggregates (see ``windows.PanedTable``).
     Returns None when the query does not qualify (non-decomposable aggregates, no aggregation, …)."""
@@ -425,10 +432,9 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
                     node.name in ctx.udfs and not getattr(ctx.udfs[node.name], "deterministic", False))):
                 cacheable = False
     fp = repr((alias, [e.key() for e in exprs], sel.where is not None, [nm for _, nm in items]))
-    gexprs = None
-    plan = key_names = None
-    parts = []
-    for pane, full in t.pieces():
+    state = {}
+
+    def pane_partial(pane, full):
         cached = pane.partials.get(fp) if (full and cacheable) else None
         if cached is None:
             src = pane.table if full else t.clipped(pane)
@@ -441,19 +447,48 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
             gx = [_resolve_group_expr(g, scope, items) for g in sel.group_by]
             keys = [materialize(evaluate(g, scope, ctx)) for g in gx]
             if any(isinstance(k, (StructColumn, ArrayColumn)) for k in keys):
-                return None
+                raise _NotPaned()
             partial, pl, kn = D.local_partials(gx, keys, aggs, scope, ctx)
             cached = (partial, pl, kn, gx)
             if full and cacheable:
                 pane.partials[fp] = cached
-        partial, plan, key_names, gexprs = cached
-        if partial.length:
-            parts.append(partial)
-    if plan is None:
+        state["meta"] = cached[1:]
+        return cached[0]
+
+    # complete blocks of BLOCK consecutive in-window panes are pre-combined once and reused until a member is
+    # evicted, so a 300-pane window merges ~20 block partials + the loose panes at its edges instead of 300 tables
+    store = t.store
+    span = BLOCK * max(1, store.interval_us)
+    parts = []
+    by_block: Dict[int, list] = {}
+    try:
+        for pane, full in t.pieces():
+            if full and cacheable and store.interval_us:
+                by_block.setdefault(pane.key // span, []).append(pane)
+            else:
+                parts.append(pane_partial(pane, full))
+        for bid, panes in by_block.items():
+            if len(panes) == BLOCK:
+                members = tuple(sorted(p.key for p in panes))
+                ent = store.blocks.get((fp, bid))
+                if ent is None or ent[0] != members:
+                    ps = [pane_partial(p, True) for p in panes]
+                    pl, kn, _ = state["meta"]
+                    ent = (members, D.combine_partials(concat_tables(ps), pl, kn, bool(sel.group_by)), state["meta"])
+                    store.blocks[(fp, bid)] = ent
+                state.setdefault("meta", ent[2])
+                parts.append(ent[1])
+            else:
+                parts.extend(pane_partial(p, True) for p in panes)
+    except _NotPaned:
         return None
+    if "meta" not in state:
+        return None
+    plan, key_names, gexprs = state["meta"]
+    parts = [p for p in parts if p.length] or parts[:1]
     dev = proto.device
     grouped = bool(sel.group_by)
-    got = concat_tables(parts) if parts else cached[0]
+    got = concat_tables(parts)
     tag = P.REPLICATED
     if P.active() and t.dist != P.REPLICATED:
         got, tag = D.exchange_partials(got, key_names, grouped)

@@ -19,6 +19,11 @@ from .column import Table
 from .types import StructType, parse_ddl_schema
 
 
+from concurrent.futures import ThreadPoolExecutor
+
+_writer = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dxa-state")
+
+
 class StateTable:
     def __init__(self, name: str, schema: StructType, location: str, device):
         self.name = name
@@ -49,34 +54,42 @@ class StateTable:
         if not fs.exists(p):
             return Table.empty(self.schema, self.device)
         import pyarrow.parquet as pq
-        at = pq.read_table(str(fs.local_path(p)))
-        rows = at.to_pylist()
-        return Table.from_pylist(rows, self.schema, self.device)
+        from ..io.arrow import table_from_arrow
+        return table_from_arrow(pq.read_table(str(fs.local_path(p))), self.schema, self.device)
 
     def overwrite(self, t: Table):
-        """INSERT OVERWRITE standby + flip (returns the new active table)."""
+        """INSERT OVERWRITE standby + flip (returns the new active table).  The standby Parquet copy is written by
+        a background writer from pinned host buffers; ``persist`` (after the batch's outputs) waits for it before
+        it flips ``metadata.info``, so the metadata never names a partially written copy."""
+        from ..io.arrow import to_host_async
         t = _conform(t, self.schema)
-        self._write(self.params["standby"], t)
+        self._wait_write()
+        host, ev = to_host_async(t)
+        self._pending = _writer.submit(self._write, self.params["standby"], host, ev)
         self.params = {"active": self.params["standby"], "standby": self.params["active"]}
         self.modified = not self.modified
         self.active = t
         return t
 
-    def _write(self, suffix: str, t: Table):
-        import pyarrow as pa
+    def _wait_write(self):
+        p = getattr(self, "_pending", None)
+        if p is not None:
+            self._pending = None
+            p.result()
+
+    def _write(self, suffix: str, t: Table, event=None):
         import pyarrow.parquet as pq
-        from .column import datetime_to_us
-        data = t.to_pydict()
-        arrays = {}
-        for f in self.schema.fields:
-            arrays[f.name] = data.get(f.name, [None] * t.length)
+        from ..io.arrow import table_to_arrow
+        if event is not None:
+            event.synchronize()
         p = fs.local_path(self._path(suffix))
         p.parent.mkdir(parents=True, exist_ok=True)
         tmp = p.with_suffix(".tmp")
-        pq.write_table(pa.table(arrays), str(tmp))
+        pq.write_table(table_to_arrow(t, self.schema), str(tmp))
         tmp.replace(p)
 
     def persist(self):
+        self._wait_write()
         if self.modified:
             fs.write_atomic(self.meta_file, "\n".join(f"{k}={v}" for k, v in self.params.items()))
             self.modified = False

@@ -141,7 +141,9 @@ class PanedTable(Table):
 class WindowStore:
     def __init__(self, conf: TimeWindowConf):
         self.conf = conf
-        self.past: Dict[int, Table] = {}     # batch time µs → retained rows
+        self.past: Dict[int, Pane] = {}      # batch time µs → retained pane
+        self.interval_us = 0
+        self.blocks: Dict = {}               # (query fingerprint, block id) → pre-combined partials of a pane block
 
     def _ts(self, t: Table) -> Tuple[torch.Tensor, torch.Tensor]:
         c = t.column(self.conf.timestamp_column)
@@ -188,6 +190,11 @@ class WindowStore:
         cut = batch_time_us - (c.watermark_us + c.max_window_us)
         for t in [t for t in self.past if t <= cut]:
             del self.past[t]
+        self.interval_us = interval_us
+        if self.blocks:
+            live = set(self.past)
+            for k in [k for k, ent in self.blocks.items() if not live.issuperset(ent[0])]:
+                del self.blocks[k]
         cur = self._pane(batch_time_us, kept)
         if len(self.past) > 1 or (not c.legacy_union_quirk and self.past):
             panes = [cur] + list(self.past.values())

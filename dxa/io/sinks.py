@@ -30,7 +30,8 @@ from ..engine.serialize import table_to_json_lines
 from . import fs
 
 SINK_PREFIX = "Sink_"
-_pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="dxa-sink")
+_pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="dxa-output")       # one task per output
+_sink_pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="dxa-sink")    # per-sink fan-out inside one
 
 
 def java_time_format(fmt: str, ts: _dt.datetime) -> str:
@@ -73,6 +74,12 @@ class Sink:
     as_json: bool = True
 
 
+def _joined(lines) -> str:
+    """Newline-joined documents; a blob-backed ``JsonLines`` is joined without per-line objects."""
+    text = getattr(lines, "text", None)
+    return text() if text is not None else "\n".join(lines)
+
+
 def _chunks(xs, n):
     for i in range(0, len(xs), n):
         yield xs[i:i + n]
@@ -90,10 +97,10 @@ def _blob_sink(d, output_name) -> Optional[Sink]:
         total = 0
         for g, folder in groups.items():
             folder = blob_folder(resolve(folder), ts, target)
-            data = "\n".join(lines)
+            data = _joined(lines)
             suffix = ".json" + (".gz" if compression != "none" else "")
             path = folder + f"part-{uuid.uuid4().hex[:12]}{suffix}"
-            if lines:
+            if len(lines):
                 fs.write_with_timeout(path, data, timeout_s=float(os.environ.get("DATAX_BlobWriterTimeout", 10)),
                                       gzip_it=compression != "none")
             total += len(lines)
@@ -196,8 +203,8 @@ def _file_sink(d, output_name) -> Optional[Sink]:
         p = fs.local_path(java_time_format(path, ts))
         p.parent.mkdir(parents=True, exist_ok=True)
         with open(p, "a") as f:
-            if lines:
-                f.write("\n".join(lines) + "\n")
+            if len(lines):
+                f.write(_joined(lines) + "\n")
         return len(lines)
     return Sink("File", write, d.get("filter"))
 
@@ -238,9 +245,11 @@ class OutputOperator:
         self.processed_schema_path = processed_schema_path
         self._schema_written = False
 
-    def output(self, table: Table, partition_time: _dt.datetime, ctx=None, target: Optional[str] = None
-               ) -> Dict[str, int]:
+    def stage(self, table: Table, ctx=None) -> "StagedOutput":
+        """Device-side half of an output (runs on the batch's thread/stream): drop internal columns, evaluate
+        per-sink filters, and start the async D2H copies of what each sink will serialize."""
         from ..config.settings import NAME_PREFIX
+        from ..ops import serialize as native_ser
         internal = f"__{NAME_PREFIX}_"
         keep = [i for i, n in enumerate(table.names) if not n.startswith(internal)]
         t = Table([table.names[i] for i in keep], [table.columns[i] for i in keep], table.length, table.device)
@@ -248,30 +257,84 @@ class OutputOperator:
             from ..engine.types import to_json_obj
             fs.write_atomic(self.processed_schema_path, json.dumps(to_json_obj(t.schema()), indent=2))
             self._schema_written = True
-        n = t.length
-        metrics = {f"{SINK_PREFIX}InputEvents": n}
-        if n == 0:
-            return metrics
-        lines_all = table_to_json_lines(t) if any(s.as_json for s in self.sinks) else None
+        st = StagedOutput(self, t.length)
+        if t.length == 0:
+            return st
+        native = native_ser.available()
 
-        def run(s: Sink):
-            lines, sub = lines_all, t
+        def capture(sub):
+            if native:
+                return native_ser.stage_table(sub)
+            return table_to_json_lines(sub)            # pure-Python fallback renders eagerly
+
+        whole = None
+        for s in self.sinks:
+            sub = t
             if s.filter_expr:
                 from ..engine.expr import EvalContext, Scope, evaluate, predicate_mask
                 from ..sql.parser import parse_expression
                 m = predicate_mask(evaluate(parse_expression(s.filter_expr), Scope.of_table(t), ctx or EvalContext()))
-                idx = m.nonzero().flatten()
-                sub = t.take(idx)
-                lines = [lines_all[i] for i in idx.tolist()] if lines_all is not None else None
-                cnt = s.write(lines, sub, partition_time, target)
-                return {f"{SINK_PREFIX}{s.name}_Filtered": cnt}
-            cnt = s.write(lines, sub, partition_time, target)
-            return {f"{SINK_PREFIX}{s.name}_All": cnt}
+                sub = t.take(m.nonzero().flatten())
+                payload = capture(sub) if s.as_json else _HostRows(sub)
+            elif s.as_json:
+                if whole is None:
+                    whole = capture(t)
+                payload = whole
+            else:
+                payload = _HostRows(t)
+            st.items.append((s, payload))
+        return st
 
-        if len(self.sinks) == 1:
-            metrics.update(run(self.sinks[0]))
+    def output(self, table: Table, partition_time: _dt.datetime, ctx=None, target: Optional[str] = None
+               ) -> Dict[str, int]:
+        return self.stage(table, ctx).finish(partition_time, target)
+
+
+class _HostRows:
+    """Rows of a (sub)table materialised on the host for sinks that take rows rather than JSON (SQL)."""
+
+    def __init__(self, t: Table):
+        self.names = list(t.names)
+        self.rows = t.to_pylist()
+        self.length = len(self.rows)
+
+    def to_pylist(self):
+        return self.rows
+
+
+class StagedOutput:
+    def __init__(self, op: OutputOperator, n: int):
+        self.op = op
+        self.n = n
+        self.items: List = []
+
+    def finish(self, partition_time: _dt.datetime, target: Optional[str] = None) -> Dict[str, int]:
+        """Host-side half: render JSON (waits only for this output's D2H copies) and write every sink."""
+        metrics = {f"{SINK_PREFIX}InputEvents": self.n}
+        if self.n == 0:
+            return metrics
+        rendered = {}
+
+        def lines_of(payload):
+            if isinstance(payload, _HostRows):
+                return None, payload
+            key = id(payload)
+            if key not in rendered:
+                rendered[key] = payload.render() if hasattr(payload, "render") else payload
+            return rendered[key], None
+
+        def run(item):
+            s, payload = item
+            lines, rows = lines_of(payload)
+            cnt = s.write(lines if lines is not None else [], rows, partition_time, target)
+            return {f"{SINK_PREFIX}{s.name}_{'Filtered' if s.filter_expr else 'All'}": cnt}
+
+        if len(self.items) == 1:
+            metrics.update(run(self.items[0]))
         else:
-            for r in _pool.map(run, self.sinks):
+            for s, payload in self.items:        # render shared payloads once, before fanning out
+                lines_of(payload)
+            for r in _sink_pool.map(run, self.items):
                 for k, v in r.items():
                     metrics[k] = metrics.get(k, 0) + v
         return metrics

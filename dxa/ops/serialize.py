@@ -11,6 +11,7 @@ import os
 import threading
 from typing import List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from .build import HOST_LIB
@@ -62,16 +63,25 @@ def _quoted(name: str) -> bytes:
 
 
 class _Builder:
+    """Describes a table as a SerNode tree over *host* buffers.  Device buffers are copied with non-blocking D2H
+    copies into pinned memory on the current stream; ``event`` marks their completion, so the rendering can run on
+    a host worker while the GPU already works on the next batch."""
+
     def __init__(self):
         self.nodes: List[dict] = []
         self.keep = []
+        self.device_copies = False
 
     def _host(self, t: Optional[torch.Tensor]):
         if t is None:
             return 0
         h = t.detach()
         if h.is_cuda:
-            h = h.cpu()
+            src = h.contiguous()
+            h = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+            h.copy_(src, non_blocking=True)
+            self.keep.append(src)            # the source must outlive the async copy
+            self.device_copies = True
         h = h.contiguous()
         self.keep.append(h)
         return h.data_ptr()
@@ -144,40 +154,103 @@ class _Builder:
         raise TypeError(f"cannot serialise {col!r}")
 
 
+class Staged:
+    """A table captured for serialization: host-side SerNode tree + the event its D2H copies complete on."""
+
+    def __init__(self, table):
+        b = _Builder()
+        self.top = [b.add(c, n) for n, c in zip(table.names, table.columns)]
+        self.builder = b
+        self.n = table.length
+        self.event = None
+        if b.device_copies:
+            self.event = torch.cuda.Event()
+            self.event.record(torch.cuda.current_stream(table.device))
+
+    def render(self, nthreads: Optional[int] = None) -> "JsonLines":
+        if self.event is not None:
+            self.event.synchronize()
+        L = lib()
+        b = self.builder
+        arr = (SerNode * max(1, len(b.nodes)))()
+        for i, nd in enumerate(b.nodes):
+            arr[i] = SerNode(nd["kind"], nd["nchildren"], nd["child0"], nd["drop_nulls"], nd["name"],
+                             len(nd["name"]), 0, nd["data"], nd["valid"], nd["arena"], nd["starts"], nd["lens"],
+                             nd["const"], len(nd["const"]), 0)
+        tops = (ctypes.c_int32 * max(1, len(self.top)))(*self.top)
+        n = self.n
+        line_len = np.zeros(max(1, n), dtype=np.int64)
+        out_len = ctypes.c_int64(0)
+        threads = nthreads or min(16, os.cpu_count() or 4)
+        ptr = L.dxa_serialize_rows(ctypes.addressof(arr), len(b.nodes), ctypes.addressof(tops), len(self.top), n,
+                                   threads, line_len.ctypes.data, ctypes.addressof(out_len))
+        try:
+            blob = ctypes.string_at(ptr, out_len.value)
+        finally:
+            L.dxa_host_free(ptr)
+        self.builder = None                 # release pinned buffers
+        return JsonLines(blob, line_len[:n])
+
+
+class JsonLines:
+    """Newline-terminated JSON lines held as one blob (what sinks write) + per-line lengths.  Behaves as a
+    read-only sequence of ``str`` (decoded lazily) for sinks that want individual documents."""
+
+    def __init__(self, blob: bytes, lens):
+        self.blob = blob
+        self.lens = np.asarray(lens, dtype=np.int64)
+        self._starts = None
+
+    def __len__(self):
+        return int(self.lens.shape[0])
+
+    def _offsets(self):
+        if self._starts is None:
+            self._starts = np.concatenate([[0], np.cumsum(self.lens + 1)[:-1]]) if len(self) else \
+                np.zeros(0, dtype=np.int64)
+        return self._starts
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        s = int(self._offsets()[i])
+        return self.blob[s:s + int(self.lens[i])].decode("utf-8")
+
+    def __iter__(self):
+        if self.blob.count(b"\n") == len(self):      # no raw newlines inside documents: split in one pass
+            return iter(self.blob.decode("utf-8").split("\n")[:len(self)])
+        return (self[i] for i in range(len(self)))
+
+    def text(self) -> str:
+        """All lines joined by newlines (no trailing newline) — ``"\\n".join(lines)`` without per-line objects."""
+        return self.blob[:-1].decode("utf-8") if self.blob else ""
+
+    def data(self) -> bytes:
+        return self.blob[:-1] if self.blob else b""
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return f"JsonLines(n={len(self)}, bytes={len(self.blob)})"
+
+
+def stage_table(table) -> Staged:
+    return Staged(table)
+
+
 def serialize_table(table, nthreads: Optional[int] = None) -> Tuple[bytes, List[int]]:
     """Render every row → (blob of newline-terminated JSON lines, per-line lengths)."""
-    L = lib()
-    b = _Builder()
-    top = [b.add(c, n) for n, c in zip(table.names, table.columns)]
-    arr = (SerNode * max(1, len(b.nodes)))()
-    names = []
-    for i, nd in enumerate(b.nodes):
-        names.append((nd["name"], nd["const"]))
-        arr[i] = SerNode(nd["kind"], nd["nchildren"], nd["child0"], nd["drop_nulls"], nd["name"], len(nd["name"]), 0,
-                         nd["data"], nd["valid"], nd["arena"], nd["starts"], nd["lens"], nd["const"],
-                         len(nd["const"]), 0)
-    tops = (ctypes.c_int32 * max(1, len(top)))(*top)
-    n = table.length
-    line_len = (ctypes.c_int64 * max(1, n))()
-    out_len = ctypes.c_int64(0)
-    threads = nthreads or min(16, os.cpu_count() or 4)
-    ptr = L.dxa_serialize_rows(ctypes.addressof(arr), len(b.nodes), ctypes.addressof(tops), len(top), n, threads,
-                               ctypes.addressof(line_len), ctypes.addressof(out_len))
-    try:
-        blob = ctypes.string_at(ptr, out_len.value)
-    finally:
-        L.dxa_host_free(ptr)
-    return blob, list(line_len[:n])
+    jl = Staged(table).render(nthreads)
+    return jl.blob, jl.lens.tolist()
 
 
 def table_lines(table) -> List[str]:
-    blob, lens = serialize_table(table)
-    out = []
-    pos = 0
-    for l in lens:
-        out.append(blob[pos:pos + l].decode("utf-8"))
-        pos += l + 1
-    return out
+    return list(Staged(table).render())
 
 
 def java_double(d: float) -> str:

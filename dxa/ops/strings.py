@@ -30,7 +30,9 @@ def _offsets(lens: torch.Tensor):
 
 
 def _alloc_arena(total: int, device) -> torch.Tensor:
-    return torch.zeros(total + 16, dtype=torch.uint8, device=device)
+    a = torch.empty(total + 16, dtype=torch.uint8, device=device)
+    a[total:].zero_()            # every byte below total is written by the producer; the pad feeds 16-B reads
+    return a
 
 
 def compact(col):

@@ -234,7 +234,8 @@ def generate(prog: GenProgram, n: int, device, seed: int = 1, row0: int = 0, bas
     offs = torch.zeros(n + 1, dtype=torch.int64, device=device)
     torch.cumsum(lens, 0, out=offs[1:])
     total = int(offs[-1].item())
-    buf = torch.zeros(total + 16, dtype=torch.uint8, device=device)
+    buf = torch.empty(total + 16, dtype=torch.uint8, device=device)
+    buf[total:].zero_()          # the parser's 16-B read window needs zero padding; the rest is fully written
     N.call("dxa_datagen_write", N.ptr(ops), len(prog.ops), N.ptr(pool), N.ptr(tab), seed & (2**64 - 1), row0, n,
            base_ms, step_us, N.ptr(offs), N.ptr(buf), st)
     return buf, offs
@@ -281,7 +282,7 @@ def render_cpu(prog: GenProgram, row: int, seed: int, base_ms: int, step_us: int
             u = (_rnd(seed, row, k) >> 11) * (1.0 / 9007199254740992.0)
             v = lo + u * (hi - lo)
             scale = 10 ** a
-            fixed = int(np.round(np.float64(v * scale))) if False else _llround(v * scale)
+            fixed = _llround(v * scale)
             neg = fixed < 0
             af = -fixed if neg else fixed
             s = ("-" if neg else "") + str(af // scale)

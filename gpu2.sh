@@ -1,11 +1,20 @@
+# GPU validation: kernel tests, then one bench per BASELINE flow (each step time-limited, stop on first failure)
 set -o pipefail
 mkdir -p gpurun_out
-R=$PWD
-python -m dxa.ops.build
-timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
-DXA_SYNC_STAGES=1 timeout -k 10 400 python bench.py --steps 10 --warmup 3 --profile-stages > gpurun_out/bench_sync.log 2>&1 || exit 1
-timeout -k 10 400 python bench.py --steps 10 --warmup 3 --profile-stages > gpurun_out/bench1.log 2>&1 || exit 1
-tail -2 gpurun_out/gpu_tests.log; cat gpurun_out/bench_sync.log gpurun_out/bench1.log | grep metric | python -c "
+python -m dxa.ops.build || exit 1
+timeout -k 10 300 python -m pytest tests/ -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+for f in groupby join window full; do
+  timeout -k 10 420 python bench.py --flow $f --steps 20 --profile-stages > gpurun_out/bench_$f.log 2>&1 || { tail -20 gpurun_out/bench_$f.log; exit 1; }
+  grep metric gpurun_out/bench_$f.log | python -c "
 import sys,json
 for l in sys.stdin:
-    d=json.loads(l); print(round(d['value']/1e6,2),'M ev/s', round(d['ms_per_step'],1),'ms', d.get('stage_s'), d['p99_latency_process_ms'])"
+    d=json.loads(l); print('$f', round(d['value']/1e6,2),'M ev/s', round(d['ms_per_step'],2),'ms p99', round(d['p99_latency_process_ms'],2), d.get('max_hbm_allocated_gb'), d.get('stage_s'), d.get('reference_build_s'), d.get('window_panes'))"
+done
+for f in window full; do
+  DXA_SYNC_STAGES=1 timeout -k 10 420 python bench.py --flow $f --steps 10 --profile-stages > gpurun_out/bench_sync_$f.log 2>&1 || { tail -20 gpurun_out/bench_sync_$f.log; exit 1; }
+  grep metric gpurun_out/bench_sync_$f.log | python -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l); print('sync $f', round(d['ms_per_step'],2), {k: round(v*1000,2) for k,v in d['stage_s'].items()})"
+done

@@ -42,9 +42,11 @@ def _canon(t):
     return sorted(out)
 
 
-@pytest.mark.parametrize("quirk", [True, False])
-def test_paned_aggregate_matches_materialized(quirk):
+@pytest.mark.parametrize("quirk,block", [(True, 16), (False, 16), (False, 2), (True, 3)])
+def test_paned_aggregate_matches_materialized(quirk, block, monkeypatch):
     import numpy as np
+    import dxa.engine.query as Q
+    monkeypatch.setattr(Q, "BLOCK", block)
     rng = np.random.default_rng(7)
     conf = TimeWindowConf({"W": 5 * S}, True, "ts", 2 * S, 5 * S, quirk)
     store = WindowStore(conf)
@@ -62,8 +64,10 @@ def test_paned_aggregate_matches_materialized(quirk):
             cat2.register("W", mat)
             ref = run_sql(q, cat2, ctx)
             assert _canon(paned) == _canon(ref), (b, q)
-    # fully-inside panes were answered from cached partials
+    # fully-inside panes were answered from cached partials (and pre-combined blocks when blocks are small)
     assert any(p.partials for p in store.past.values())
+    if block <= 3:
+        assert store.blocks
 
 
 def test_window_ranges_and_eviction():
