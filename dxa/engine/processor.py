@@ -246,8 +246,9 @@ class Processor:
             staged.append((op.name, op.stage(t, ctx)))
         self._complete_inflight()
         from ..io.sinks import _pool
-        fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(st.finish, partition_time))
+        fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(_timed, st.finish, partition_time))
                                                  for name, st in staged], t_start)
+        fl.t_staged = time.perf_counter()
         self._inflight = fl
         self.stage_times["output_stage"] = time.perf_counter() - t1
         if self.keep_views:
@@ -266,8 +267,11 @@ class Processor:
             return None
         self._inflight = None
         metrics = fl.metrics
+        t_done = fl.t_staged
         for name, f in fl.futures:
-            for k, v in f.result().items():
+            res, t_end = f.result()
+            t_done = max(t_done, t_end)
+            for k, v in res.items():
                 metrics[f"Output_{name}_{k}"] = float(v)
         if P.active():
             # batch metrics are job-wide: one all-reduce of the count vector (timings stay per-rank)
@@ -277,7 +281,9 @@ class Processor:
             metrics.update(zip(keys, vec.tolist()))
         for st in self.state_tables.values():
             st.persist()
-        metrics["Latency-Process"] = time.perf_counter() - fl.t0
+        # processing latency = batch start → its last sink write finished (measured where the write finished, not
+        # where the completion was observed)
+        metrics["Latency-Process"] = t_done - fl.t0
         metrics["Latency-Batch"] = (time.time() * 1e6 - fl.batch_time_us) / 1e6
         if P.rank() == 0:
             self.metric_logger.send_batch_metrics(metrics, fl.batch_time_us // 1000)
@@ -340,14 +346,20 @@ class Processor:
             raise
 
 
+def _timed(fn, *args):
+    out = fn(*args)
+    return out, time.perf_counter()
+
+
 class _InFlight:
-    __slots__ = ("batch_time_us", "metrics", "futures", "t0")
+    __slots__ = ("batch_time_us", "metrics", "futures", "t0", "t_staged")
 
     def __init__(self, batch_time_us, metrics, futures, t0):
         self.batch_time_us = batch_time_us
         self.metrics = metrics
         self.futures = futures
         self.t0 = t0
+        self.t_staged = t0
 
 
 def _fmt_ts(us: int) -> str:
