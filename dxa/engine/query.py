@@ -76,7 +76,13 @@ def execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
         out = _gathered(out)
         src_scope = None
     if q.order_by:
-        out = _order_by(out, q.order_by, ctx, src_scope)
+        aliases = {}
+        if isinstance(q.body, A.Select):
+            # ORDER BY may repeat a select expression (e.g. ``R.owner`` after GROUP BY R.owner): map it to its column
+            for it in q.body.items:
+                if not isinstance(it.expr, A.Star):
+                    aliases.setdefault(it.expr.key(), it.alias or output_name(it.expr))
+        out = _order_by(out, q.order_by, ctx, src_scope, aliases)
     if q.limit is not None:
         out = out.slice(0, q.limit)
     return out
@@ -728,7 +734,8 @@ def _sort_key_tensor(col: Column) -> Tuple[torch.Tensor, torch.Tensor]:
     raise QueryError(f"cannot ORDER BY {col.dtype}")
 
 
-def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope]) -> Table:
+def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope],
+              aliases: Optional[Dict] = None) -> Table:
     if t.length <= 1:
         return t
     out_scope = Scope.of_table(t)
@@ -741,9 +748,13 @@ def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope
             try:
                 col = evaluate(e, out_scope, ctx)
             except EvalError:
-                if src_scope is None:
+                named = (aliases or {}).get(e.key())
+                if named is not None and t.column(named) is not None:
+                    col = t.column(named)
+                elif src_scope is None:
                     raise
-                col = evaluate(e, src_scope, ctx)
+                else:
+                    col = evaluate(e, src_scope, ctx)
         key, valid = _sort_key_tensor(col)
         key, valid = key[perm], valid[perm]
         nulls_first = it.nulls_first if it.nulls_first is not None else it.ascending

@@ -136,7 +136,7 @@ def s500_projection(s: Session):
     props = s.gui.get("input", {}).get("properties", {})
     snippet = props.get("normalizationSnippet") or "Raw.*"
     lines = [l.strip() for l in snippet.replace("\r\n", "\n").split("\n") if l.strip()]
-    s.files["projection"] = "\n".join(lines) + "\n"
+    s.files["projection"] = "\n".join(lines)          # byte-identical to the reference (no trailing newline)
 
 
 def s500_schema(s: Session):

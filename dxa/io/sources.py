@@ -303,5 +303,9 @@ def build_source(settings, device, kind: Optional[str] = None) -> Source:
         return SocketSource(device, inp.get("socket.host") or "127.0.0.1", int(inp.get("socket.port") or 9999))
     if kind == "queue":
         return QueueSource(device)
-    raise SourceError(f"input kind '{kind}' needs a client library that is not available in this deployment "
-                      f"(EventHub/Kafka); use local, file, socket or REST ingest inputs")
+    if kind in ("kafka", "eventhub", "kafkaeventhub", "iothub"):
+        from .. import parallel as P
+        from .kafka import build_kafka_source
+        return build_kafka_source(inp, device, "eventhub" if kind in ("eventhub", "iothub") else "kafka",
+                                  P.rank(), P.world())
+    raise SourceError(f"unknown input kind '{kind}'")

@@ -11,6 +11,7 @@ add ``file`` (JSON lines) and an in-process ``MetricStore`` (the Redis-compatibl
 from __future__ import annotations
 
 import bisect
+from dataclasses import dataclass
 import json
 import socket
 import threading
@@ -69,22 +70,49 @@ class MetricStore:
             return [k for k in self._sets if fnmatch.fnmatch(k, pattern)]
 
 
+@dataclass
+class RedisServerConf:
+    name: str
+    host: str
+    port: int
+    key: Optional[str]
+    timeout: int
+    use_ssl: bool
+    is_cluster: bool
+
+
+def parse_redis_connection_string(conn: str) -> Optional[RedisServerConf]:
+    """``<host>:<port>,password=<p>,ssl=True|False,cluster=True|False,timeout=<ms>`` with the reference's defaults
+    (ssl and cluster on, 3000 ms) — RedisBase.scala:32-58."""
+    if not conn:
+        return None
+    parts = conn.split(",")
+    hp = parts[0].strip().split(":")
+    if len(hp) != 2:
+        raise ValueError("Malformed format of host and port in redis connection string")
+    opts = {}
+    for p in parts[1:]:
+        pos = p.find("=")
+        if pos <= 0:
+            raise ValueError("Malformed format of parts in redis connection string")
+        opts[p[:pos].strip()] = p[pos + 1:]
+
+    def flag(k):
+        return opts.get(k, "True").strip().lower() == "true"
+    return RedisServerConf(hp[0], hp[0], int(hp[1]), opts.get("password"), int(opts.get("timeout", "3000")),
+                           flag("ssl"), flag("cluster"))
+
+
 class RedisClient:
     """Minimal RESP client (``host:port,password=…,ssl=…``, reference RedisBase.scala:32-58)."""
 
-    def __init__(self, conn: str, timeout: float = 5.0):
-        parts = [p.strip() for p in conn.split(",") if p.strip()]
-        hostport = parts[0]
-        opts = {}
-        for p in parts[1:]:
-            if "=" in p:
-                k, v = p.split("=", 1)
-                opts[k.strip().lower()] = v.strip()
-        host, _, port = hostport.partition(":")
-        self.host, self.port = host, int(port or 6379)
-        self.password = opts.get("password")
-        self.use_ssl = opts.get("ssl", "false").lower() == "true"
-        self.timeout = float(opts.get("timeout", timeout * 1000)) / 1000.0 if "timeout" in opts else timeout
+    def __init__(self, conn: str, timeout: Optional[float] = None):
+        conf = parse_redis_connection_string(conn)
+        self.conf = conf
+        self.host, self.port = conf.host, conf.port
+        self.password = conf.key
+        self.use_ssl = conf.use_ssl
+        self.timeout = timeout if timeout is not None else conf.timeout / 1000.0
         self._sock = None
         self._lock = threading.Lock()
 

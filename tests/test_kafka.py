@@ -1,0 +1,123 @@
+"""Kafka protocol client, native record-batch codec, Kafka source (rank partition assignment, max rate, offsets
+checkpoint + restore) and the simulated producer — against the in-process fake broker."""
+import json
+import os
+
+import pytest
+import torch
+
+from dxa.io import kafka as K
+from tests.kafka_fake import FakeBroker
+
+
+def test_crc32c_known_vector():
+    assert K.crc32c(b"123456789") == 0xE3069283
+
+
+def test_batch_roundtrip():
+    vals = [b'{"a":1}', b"", b'{"b":"xyz"}'] + [b"x" * 300]
+    batch = K.encode_batch(vals, timestamp_ms=1)
+    buf, offs, recoffs, nxt = K.decode_records(batch, 0)
+    got = [bytes(buf[offs[i]:offs[i + 1]]) for i in range(len(vals))]
+    assert got == vals and recoffs.tolist() == [0, 1, 2, 3] and nxt == 4
+    assert (buf[int(offs[-1]):] == 0).all() and len(buf) == int(offs[-1]) + 16
+    # records below the fetch offset are dropped; a truncated trailing batch is ignored
+    buf, offs, recoffs, nxt = K.decode_records(batch + batch[:30], 2)
+    assert recoffs.tolist() == [2, 3]
+    bad = bytearray(batch)
+    bad[-1] ^= 0xFF
+    with pytest.raises(K.KafkaError):
+        K.decode_records(bytes(bad), 0)
+
+
+@pytest.fixture()
+def broker():
+    b = FakeBroker(["iot"], partitions=3)
+    yield b
+    b.close()
+
+
+def _produce(broker, n_per_part):
+    c = K.KafkaClient(f"127.0.0.1:{broker.port}")
+    for p in range(3):
+        for chunk in range(2):
+            c.produce("iot", p, [json.dumps({"p": p, "i": chunk * 1000 + i}).encode()
+                                 for i in range(n_per_part // 2)])
+    return c
+
+
+def test_client_metadata_offsets_fetch(broker):
+    c = _produce(broker, 10)
+    assert c.metadata(["iot"]) == {"iot": [0, 1, 2]}
+    assert c.list_offset("iot", 1, K.EARLIEST) == 0 and c.list_offset("iot", 1, K.LATEST) == 10
+    recs, hw = c.fetch("iot", 2, 7)
+    _, offs, recoffs, nxt = K.decode_records(recs, 7)
+    assert hw == 10 and recoffs.tolist() == [7, 8, 9] and nxt == 10
+
+
+def test_kafka_source_batches_checkpoint_restore(broker, tmp_path):
+    from dxa.ops.jsonparse import ParsePlan, parse
+    from dxa.engine.types import StructField, StructType
+    _produce(broker, 10)
+    ck = str(tmp_path / "ck")
+    src = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", ck, max_rate=4)
+    raw = src.next_batch(1_000_000)
+    assert raw.n == 12                                            # 3 partitions x max_rate 4
+    col, ok = parse(raw.buf, raw.offs, ParsePlan(StructType((StructField("p", "long"), StructField("i", "long")))))
+    assert sorted(col.child("p").data.tolist()) == [0] * 4 + [1] * 4 + [2] * 4
+    # not committed → the same records again
+    assert src.next_batch(2_000_000).n == 12
+    src.commit(2_000_000)
+    assert open(os.path.join(ck, "offsets.txt")).read().splitlines()[0].startswith("2000,iot,")
+    assert src.next_batch(3_000_000).n == 12
+    src.commit(3_000_000)
+    # a restarted source resumes from the checkpoint: 10 - 8 = 2 left per partition
+    src2 = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", ck, max_rate=4)
+    assert src2.next_batch(4_000_000).n == 6
+    src2.commit(4_000_000)
+    assert src2.next_batch(5_000_000).n == 0
+
+
+def test_rank_partition_assignment(broker):
+    _produce(broker, 4)
+    a = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", rank=0, world=2)
+    b = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", rank=1, world=2)
+    assert a.parts == [("iot", 0), ("iot", 2)] and b.parts == [("iot", 1)]
+    assert a.next_batch(0).n + b.next_batch(0).n == 12
+
+
+def test_sasl_plain_and_eventhub_settings():
+    b = FakeBroker(["hub"], partitions=1, sasl_password="Endpoint=sb://x/;EntityPath=hub")
+    try:
+        c = K.KafkaClient(f"127.0.0.1:{b.port}", sasl=("$ConnectionString", "Endpoint=sb://x/;EntityPath=hub"))
+        assert c.metadata(["hub"]) == {"hub": [0]}
+        with pytest.raises(K.KafkaError):
+            K.KafkaClient(f"127.0.0.1:{b.port}", sasl=("$ConnectionString", "wrong")).metadata(["hub"])
+    finally:
+        b.close()
+    es = K.eventhub_kafka_settings("Endpoint=sb://myns.servicebus.windows.net/;SharedAccessKeyName=k;"
+                                   "SharedAccessKey=s;EntityPath=telemetry")
+    assert es["bootstrap"] == "myns.servicebus.windows.net:9093" and es["topic"] == "telemetry"
+    assert es["sasl"][0] == "$ConnectionString" and es["use_ssl"]
+
+
+def test_simulated_producer(broker):
+    from dxa.simulate.kafka_producer import program_from_schema_text, run
+    schema = json.dumps({"type": "struct", "fields": [
+        {"name": "v", "type": "double", "nullable": False, "metadata": {"minValue": 1.0, "maxValue": 2.0}}]})
+    c = K.KafkaClient(f"127.0.0.1:{broker.port}")
+    sent = run(c, ["iot"], program_from_schema_text(schema), rate=5, seconds=0.01)
+    assert sent == 5
+    total = sum(c.list_offset("iot", p, K.LATEST) for p in range(3))
+    assert total == 5
+
+
+def test_build_source_from_settings(broker, tmp_path):
+    from dxa.config.settings import SettingDictionary
+    from dxa.io.sources import build_source
+    _produce(broker, 2)
+    d = SettingDictionary({"datax.job.input.default.kafka.bootstrapservers": f"127.0.0.1:{broker.port}",
+                           "datax.job.input.default.kafka.topics": "iot",
+                           "datax.job.input.default.kafka.checkpointdir": str(tmp_path / "k")})
+    src = build_source(d, "cpu")
+    assert isinstance(src, K.KafkaSource) and src.next_batch(0).n == 6
