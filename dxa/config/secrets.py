@@ -64,3 +64,17 @@ def store(vault: str, name: str, value: str) -> str:
     with _lock:
         _cache[ref] = value
     return ref
+
+
+def delete_prefix(vault: str, prefix: str) -> int:
+    """Remove every secret of ``vault`` whose name starts with ``prefix`` (flow deletion; DataX.Flow.DeleteHelper)."""
+    d = Path(os.environ.get("DXA_SECRETS_DIR", ".dxa_secrets")) / vault
+    n = 0
+    if d.is_dir():
+        for p in d.iterdir():
+            if p.name.startswith(prefix):
+                p.unlink()
+                n += 1
+                with _lock:
+                    _cache.pop(f"keyvault://{vault}/{p.name}", None)
+    return n

@@ -159,6 +159,11 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         for j in flow.get("jobNames", []):
             st.jobs.delete(j)
         st.store.delete("flows", name)
+        # DeleteHelper: runtime configs, checkpoints/state and the flow's generated secrets go with it
+        import shutil
+        from ..config import secrets
+        shutil.rmtree(os.path.join(st.root, "runtime", name), ignore_errors=True)
+        secrets.delete_prefix("dxa", f"{name}-")
         return True
 
     @route("flow/schedulebatch")

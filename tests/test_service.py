@@ -270,3 +270,45 @@ def test_schedulebatch_route_creates_slot_jobs(client, monkeypatch):
     assert "datax.job.input.default.blob.input0.partitionincrement=" in conf
     saved = client.post("/api/flow/get", json={"name": flow["name"]}).json()["result"]
     assert saved["gui"]["batchList"][1]["disabled"] is True
+
+
+# -- ScenarioTester / DataXScenarios ---------------------------------------------------------------------------------
+def test_scenario_runner_semantics():
+    from dxa.service.scenarios import ScenarioResult, StepResult, scenario_from_json, step
+
+    @step("stepOk")
+    def ok(ctx):
+        ctx["seq"] = ctx.get("seq", 0) + 1
+        ctx["stepOk"] = ctx["seq"]
+        return StepResult(True, "stepOk")
+
+    @step("stepFail")
+    def fail(ctx):
+        ctx["seq"] = ctx.get("seq", 0) + 1
+        ctx["stepFail"] = ctx["seq"]
+        raise RuntimeError("boom")
+
+    ctx = {}
+    r = ScenarioResult("s", scenario_from_json("s", "[{'action':'stepFail'}, {'action':'stepOk'}]")).run(ctx)
+    assert r.failed and ctx["stepFail"] == 1 and ctx["stepOk"] == 2          # later steps still run
+    assert not ScenarioResult("s", [ok]).run({}).failed
+    with pytest.raises(KeyError):
+        scenario_from_json("s", "[{'action':'nope'}]")
+
+
+def test_save_deploy_and_query_scenarios(client, monkeypatch):
+    from dxa.service.scenarios import QUERY_AND_SCHEMA, SAVE_AND_DEPLOY, STEPS, run_parallel
+    st = client.app.state.dxa
+    started = []
+    monkeypatch.setattr(st.jobs, "start", lambda name, *a, **k: started.append(name) or {"name": name})
+    monkeypatch.setattr(st.jobs, "restart", lambda name: {"name": name})
+    monkeypatch.setattr(st.jobs, "stop", lambda name, *a, **k: {"name": name})
+    events = [json.dumps({"deviceId": i, "deviceType": "A", "temp": 1.5}) for i in range(10)]
+    ctx = {"client": client, "flow": mini_flow("scn"), "events": events, "suffix": ""}
+    res = run_parallel("deploy", [STEPS[s] for s in SAVE_AND_DEPLOY], ctx, 3)
+    assert all(not r.failed for r in res), [(s.description, s.exception, s.result) for r in res
+                                             for s in r.step_results]
+    assert len(started) == 3
+    res = run_parallel("query", [STEPS[s] for s in QUERY_AND_SCHEMA], ctx, 2)
+    assert all(not r.failed for r in res), [(s.description, s.exception, s.result) for r in res
+                                             for s in r.step_results]
