@@ -107,8 +107,24 @@ def _spark_type(f):
             "datetime": "string"}[t]
 
 
+def _generator_metadata(f) -> dict:
+    """DataGenerator-style field metadata (minValue/maxValue, allowedValues, datetimeStringFormat) so the Spark
+    schema alone drives realistic synthetic events (local source, LiveQuery samples)."""
+    md = {}
+    if "valueList" in f:
+        md["allowedValues"] = f["valueList"]
+    if "minRange" in f:
+        md["minValue"], md["maxValue"] = f["minRange"], f["maxRange"]
+    if f["type"].lower() == "datetime":
+        md["datetimeStringFormat"] = f.get("datetimeStringFormat", "yyyy-MM-ddTHH:mm:ssZ")
+    return md
+
+
 def iot_spark_schema() -> StructType:
-    return StructType(tuple(StructField(f["name"], _spark_type(f)) for f in IOT_FIELDS))
+    def field(f):
+        return StructField(f["name"], _spark_type(f), True, _generator_metadata(f)) \
+            if f["type"] != "struct" else StructField(f["name"], StructType(tuple(field(p) for p in f["properties"])))
+    return StructType(tuple(field(f) for f in IOT_FIELDS))
 
 
 def leaf_count(fields=IOT_FIELDS) -> int:

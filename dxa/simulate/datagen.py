@@ -195,7 +195,9 @@ def _compile_value(prog: GenProgram, t, md: dict, null_permille: int):
         vals = md["allowedValues"]
         prog.choice([json.dumps(str(v)) if t == "string" else _num_text(v) for v in vals])
         return
-    if t == "string":
+    if t == "string" and md.get("datetimeStringFormat"):
+        prog.op(OP_TS_STR, _TS_FORMATS.get(md["datetimeStringFormat"], 1), 0, int(md.get("utcAddSeconds") or 0), 0)
+    elif t == "string":
         prog.op(OP_ALNUM, int(md.get("maxLength", 10)))
     elif t in ("long", "int"):
         if md.get("useCurrentTimeMillis"):

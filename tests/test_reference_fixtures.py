@@ -133,3 +133,20 @@ def test_default_spec_is_a_superset_of_reference_spec():
     ref = _props(os.path.join(CFG, "jobConfig.conf"))
     missing = [k for k in ref if k not in ours]
     assert not missing, missing[:10]
+
+
+def test_utility_helpers():
+    from concurrent.futures import ThreadPoolExecutor
+    from dxa import utils as U
+    assert U.named_args(["conf=a=b", "x=1", "bad"]) == {"conf": "a=b", "x": "1"}
+    assert U.sanitize_column_name("a.b") == "`a.b`" and U.sanitize_column_name("ab") == "ab"
+    assert U.inflate(U.deflate("hello\nworld")) == "hello\nworld"
+    assert U.inflate_bytes(U.deflate_lines(["a", "b"])) == "a\nb"
+    assert U.merge_map_of_counts({"a": 1}, {"a": 2, "b": 3}) == {"a": 3, "b": 3}
+    assert U.flatten_map_of_counts({"o": {"x": 1}}) == {"o_x": 1}
+    assert U.add_property(None, "k", "v") == {"k": "v"} and U.add_property({"a": "1"}, "k", None) == {"a": "1"}
+    assert U.ip_octet("10.1.2.3", 2) == 2 and U.ip_octet("", 0) == 0
+    with ThreadPoolExecutor(2) as ex:
+        assert U.fail_fast([ex.submit(lambda: 1), ex.submit(lambda: 2)]) == [1, 2]
+        with pytest.raises(ZeroDivisionError):
+            U.fail_fast([ex.submit(lambda: 1 / 0)])
