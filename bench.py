@@ -9,7 +9,8 @@ one process per MI355X (BASELINE.json metric "events/sec (node) + p99 latency").
 * ``window``  — the same aggregate over a 5-minute sliding window with a 1-s slide (config 3; answered from cached
   per-pane partial aggregates, merged across ranks with one RCCL all-to-all of partials);
 * ``join``    — stream–static hash join against a 100M-row reference table resident in HBM (config 4);
-* ``full``    — codegen'd rules + windowed SQL with a device UDF + reference join + accumulator state (config 5).
+* ``full``    — codegen'd rules + windowed SQL with a device UDF + reference join + accumulator state (config 5);
+* ``passthrough`` — tag rules on every event and every event written as JSON (config 1's shape at full rate).
 
 Each step is a complete micro-batch exactly as the streaming host runs it.  Sources: ``pinned`` — the batch's raw
 JSON bytes are copied from pinned host memory into HBM every step (events arrive from the network into host memory;
@@ -33,9 +34,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-DEFAULT_EVENTS = {"groupby": 2_000_000, "window": 1_000_000, "join": 2_000_000, "full": 1_000_000}
-DEFAULT_WARMUP = {"groupby": 5, "window": 305, "join": 3, "full": 305}
-DEFAULT_SOURCE = {"groupby": "pinned", "window": "gpu-sim", "join": "pinned", "full": "gpu-sim"}
+DEFAULT_EVENTS = {"groupby": 2_000_000, "window": 1_000_000, "join": 2_000_000, "full": 1_000_000,
+                  "passthrough": 1_000_000}
+DEFAULT_WARMUP = {"groupby": 5, "window": 305, "join": 3, "full": 305, "passthrough": 3}
+DEFAULT_SOURCE = {"groupby": "pinned", "window": "gpu-sim", "join": "pinned", "full": "gpu-sim",
+                  "passthrough": "pinned"}
 MODEL = {
     "groupby": "SimulatedData IoT flow: 32-col JSON parse + projection + GROUP BY (deviceId, deviceType, homeId) "
                "9 aggregates + alert view + JSON outputs",
@@ -45,6 +48,8 @@ MODEL = {
             "reference table + GROUP BY",
     "full": "SimulatedData IoT flow: rules (ProcessRules codegen) + 5-min windowed SQL with device UDF + "
             "reference join + accumulator state table",
+    "passthrough": "SimulatedData IoT flow: tag rules on every event + every tagged event serialised to JSON "
+                   "(config 1 shape at full rate)",
 }
 
 

@@ -234,7 +234,13 @@ FULL_RULES = [
      "$isAlert": False, "schemaTableName": "DataXProcessedInput"},
 ]
 
-VARIANTS = ("groupby", "window", "join", "full")
+PASSTHROUGH_USER_CODE = """--DataXQuery--
+Tagged = ProcessRules(DataXProcessedInput);
+
+OUTPUT Tagged TO Events;
+"""
+
+VARIANTS = ("groupby", "window", "join", "full", "passthrough")
 
 
 def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Optional[Dict[str, str]] = None,
@@ -246,7 +252,9 @@ def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Opti
     * ``join``    — stream–static join against a ``ref_rows``-row reference table resident in HBM (config 4;
       the table itself is built on device by ``reference_table``);
     * ``full``    — rules (codegen'd ProcessRules + alerts) + windowed SQL with a device UDF + reference-data join +
-      accumulator state table (config 5).
+      accumulator state table (config 5);
+    * ``passthrough`` — the hello-world shape of config 1 at full rate: tag rules on every event, every tagged
+      event serialised to JSON and written (exercises the device JSON serializer).
     """
     from ..engine.types import schema_to_json
     if variant not in VARIANTS:
@@ -257,7 +265,7 @@ def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Opti
              "projection": os.path.join(workdir, "projection.txt"),
              "transform": os.path.join(workdir, f"{name}-combined.txt")}
     outputs = {"groupby": ["DeviceSummary", "HotDeviceAlerts"], "window": ["DeviceWindow", "HotDeviceAlerts"],
-               "join": ["ZoneSummary"], "full": ["DeviceNamed", "DeviceState"]}[variant]
+               "join": ["ZoneSummary"], "full": ["DeviceNamed", "DeviceState"], "passthrough": ["Tagged"]}[variant]
     d = {
         "datax.job.name": name,
         "datax.job.input.default.blobschemafile": paths["schema"],
@@ -271,6 +279,10 @@ def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Opti
         transform = WINDOW_TRANSFORM
     elif variant == "join":
         transform = JOIN_TRANSFORM.format(ref_rows=ref_rows)
+    elif variant == "passthrough":
+        from ..sql.codegen import generate_code
+        transform = generate_code(PASSTHROUGH_USER_CODE, [dict(r, **{"$isAlert": False}) for r in FULL_RULES],
+                                  "iotbench").code
     else:
         from ..sql.codegen import generate_code
         rc = generate_code(FULL_USER_CODE, FULL_RULES, "iotbench")

@@ -154,20 +154,185 @@ class _Builder:
         raise TypeError(f"cannot serialise {col!r}")
 
 
+class DevNode(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("nchildren", ctypes.c_int32), ("child0", ctypes.c_int32),
+                ("drop_nulls", ctypes.c_int32), ("name_off", ctypes.c_int32), ("name_len", ctypes.c_int32),
+                ("const_off", ctypes.c_int32), ("const_len", ctypes.c_int32), ("data", ctypes.c_void_p),
+                ("valid", ctypes.c_void_p), ("arena", ctypes.c_void_p), ("starts", ctypes.c_void_p),
+                ("lens", ctypes.c_void_p)]
+
+
+class _DevBuilder:
+    """SerNode tree over *device* buffers for the GPU serializer (json_serialize.hip); names and constant values go
+    into one text pool."""
+
+    def __init__(self):
+        self.nodes: List[dict] = []
+        self.text = bytearray()
+        self.keep = []
+
+    def _t(self, b: bytes):
+        off = len(self.text)
+        self.text += b
+        return off, len(b)
+
+    def _dev(self, t: Optional[torch.Tensor]):
+        if t is None:
+            return 0
+        t = t.contiguous()
+        self.keep.append(t)
+        return t.data_ptr()
+
+    def _blank(self):
+        return {"kind": K_NULL, "nchildren": 0, "child0": 0, "drop_nulls": 0, "name": (0, 0), "const": (0, 0),
+                "data": 0, "valid": 0, "arena": 0, "starts": 0, "lens": 0}
+
+    def add(self, col, name: Optional[str]) -> int:
+        from ..engine.column import (ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn)
+        from ..engine.serialize import _scalar_text
+        idx = len(self.nodes)
+        nd = self._blank()
+        if name:
+            nd["name"] = self._t(_quoted(name))
+        self.nodes.append(nd)
+        if isinstance(col, ConstColumn):
+            if col.value is not None:
+                nd["kind"] = K_CONST
+                nd["const"] = self._t(_scalar_text(col.value, col.dtype).encode("utf-8"))
+            return idx
+        if col.valid is not None:
+            nd["valid"] = self._dev(col.valid.view(torch.uint8) if col.valid.dtype == torch.bool else col.valid)
+        if isinstance(col, StrColumn):
+            nd["kind"] = K_RAW if isinstance(col, JsonColumn) else K_STR
+            nd["arena"] = self._dev(col.arena)
+            nd["starts"] = self._dev(col.starts.to(torch.int64))
+            nd["lens"] = self._dev(col.lens.to(torch.int32))
+            return idx
+        if isinstance(col, PrimColumn):
+            dt, d = col.dtype, col.data
+            if dt == "boolean":
+                nd["kind"] = K_BOOL
+                d = d.to(torch.uint8)
+            elif dt in ("int", "long"):
+                nd["kind"] = K_I64
+                d = d.to(torch.int64)
+            elif dt == "timestamp":
+                nd["kind"] = K_TS
+            elif dt == "date":
+                nd["kind"] = K_DATE
+                d = d.to(torch.int64)
+            else:
+                nd["kind"] = K_F64
+                d = d.to(torch.float64)
+            nd["data"] = self._dev(d)
+            return idx
+        if isinstance(col, (StructColumn, ArrayColumn)):
+            kids = list(zip(col.names, col.children)) if isinstance(col, StructColumn) else \
+                [(None, e) for e in col.elements]
+            nd["kind"] = (K_MAP if col.is_map else K_STRUCT) if isinstance(col, StructColumn) else K_ARRAY
+            nd["drop_nulls"] = 1 if isinstance(col, ArrayColumn) and col.drop_nulls else 0
+            nd["nchildren"] = len(kids)
+            first = len(self.nodes)
+            nd["child0"] = first
+            for _ in kids:
+                self.nodes.append(None)
+            for j, (nm, c) in enumerate(kids):
+                k = self.add(c, nm if isinstance(col, StructColumn) else None)
+                self.nodes[first + j] = self.nodes[k]
+                self.nodes[k] = self._blank()
+            return idx
+        raise TypeError(f"cannot serialise {col!r}")
+
+    def device_arrays(self, device):
+        arr = (DevNode * max(1, len(self.nodes)))()
+        for i, nd in enumerate(self.nodes):
+            arr[i] = DevNode(nd["kind"], nd["nchildren"], nd["child0"], nd["drop_nulls"], nd["name"][0],
+                             nd["name"][1], nd["const"][0], nd["const"][1], nd["data"], nd["valid"], nd["arena"],
+                             nd["starts"], nd["lens"])
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device, non_blocking=False)
+        text = torch.frombuffer(bytearray(bytes(self.text) + b"\0"), dtype=torch.uint8).to(device)
+        return raw, text
+
+
+_side_streams = {}
+_side_lock = threading.Lock()
+
+
+def _side_stream(device):
+    with _side_lock:
+        s = _side_streams.get(device)
+        if s is None:
+            s = _side_streams[device] = torch.cuda.Stream(device)
+        return s
+
+
+def gpu_serializer_enabled(device) -> bool:
+    if device.type != "cuda" or os.environ.get("DXA_GPU_SERIALIZE", "1") == "0":
+        return False
+    try:
+        from . import native
+        native.lib()
+        return True
+    except Exception:  # noqa: BLE001
+        return False
+
+
 class Staged:
-    """A table captured for serialization: host-side SerNode tree + the event its D2H copies complete on."""
+    """A table captured for serialization.  On the GPU the rows are rendered by the device serializer on a side
+    stream (ordered after the producing work by an event) and the blob comes back with one D2H copy; otherwise the
+    columns are copied to pinned host memory (async) and rendered by the native host serializer.  ``render`` may
+    run on any host thread."""
 
     def __init__(self, table):
+        self.n = table.length
+        self.event = None
+        self.gpu = gpu_serializer_enabled(table.device)
+        if self.gpu:
+            self.table = table
+            self.device = table.device
+            self.event = torch.cuda.Event()
+            self.event.record(torch.cuda.current_stream(table.device))
+            return
         b = _Builder()
         self.top = [b.add(c, n) for n, c in zip(table.names, table.columns)]
         self.builder = b
-        self.n = table.length
-        self.event = None
         if b.device_copies:
             self.event = torch.cuda.Event()
             self.event.record(torch.cuda.current_stream(table.device))
 
+    def _render_gpu(self) -> "JsonLines":
+        from . import native as N
+        dev = self.device
+        n = self.n
+        side = _side_stream(dev)
+        with torch.cuda.stream(side):
+            side.wait_event(self.event)
+            b = _DevBuilder()
+            top = [b.add(c, nm) for nm, c in zip(self.table.names, self.table.columns)]
+            nodes, text = b.device_arrays(dev)
+            top_t = torch.tensor(top, dtype=torch.int32).to(dev)
+            st = N.stream_handle(dev)
+            lens = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+            N.call("dxa_serialize_lengths", N.ptr(nodes), N.ptr(top_t), len(top), N.ptr(text), n, N.ptr(lens), st)
+            ends = torch.cumsum(lens[:n], 0)
+            offs = ends - lens[:n]
+            host_lens = torch.empty(n, dtype=torch.int64, pin_memory=True)
+            host_lens.copy_(lens[:n], non_blocking=True)
+            side.synchronize()
+            total = int(ends[-1].item()) if n else 0
+            out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+            N.call("dxa_serialize_write", N.ptr(nodes), N.ptr(top_t), len(top), N.ptr(text), n, N.ptr(offs),
+                   N.ptr(out), st)
+            host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+            host.copy_(out[:total], non_blocking=True)
+            side.synchronize()
+        self.table = None
+        blob = host.numpy().tobytes()
+        return JsonLines(blob, host_lens.numpy() - 1)
+
     def render(self, nthreads: Optional[int] = None) -> "JsonLines":
+        if self.gpu:
+            return self._render_gpu()
         if self.event is not None:
             self.event.synchronize()
         L = lib()

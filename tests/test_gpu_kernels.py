@@ -168,3 +168,58 @@ def test_full_query_matches_cpu(gpu):
                     assert y[k] == pytest.approx(x[k], rel=1e-12)   # float sums: atomic order differs
                 else:
                     assert x[k] == y[k]
+
+
+def _serializer_table(device):
+    from dxa.engine.column import ArrayColumn, ConstColumn, StructColumn
+    from dxa.engine.types import MapType
+    rnd = random.Random(5)
+    n = 3000
+    longs = column_from_pylist([None if rnd.random() < 0.1 else rnd.randint(-2**62, 2**62) for _ in range(n)], "long")
+    specials = [0.0, -0.0, 1e7, 9999999.999, 1e-3, 0.00099, 5e-324, 1.7976931348623157e308, 100.0, 0.1, 1e22,
+                float("inf"), float("-inf"), float("nan")]
+    dbl = [rnd.choice(specials) if rnd.random() < 0.2 else rnd.uniform(-1, 1) * 10 ** rnd.randint(-20, 20)
+           for _ in range(n)]
+    dbls = column_from_pylist([None if rnd.random() < 0.05 else d for d in dbl], "double")
+    strs = strings_from_pylist([None if rnd.random() < 0.1 else rnd.choice(["plain", 'q"uote', "back\\slash",
+                                "tab\tnl\n", "ctl\x01\x1f", "unié", ""]) for _ in range(n)], "cpu")
+    bools = column_from_pylist([None if rnd.random() < 0.1 else rnd.random() < 0.5 for _ in range(n)], "boolean")
+    ts = column_from_pylist([None if rnd.random() < 0.1 else rnd.randint(-10**15, 4 * 10**15) for _ in range(n)],
+                            "timestamp")
+    struct = StructColumn(["a", "b"], [longs, strs], n, None)
+    mp = StructColumn(["k1", "k2"], [strs, dbls], n, None, True, MapType("string", "string"))
+    arr = ArrayColumn([longs, dbls], n, None, True)
+    const = ConstColumn("x\"y", "string", n, "cpu")
+    t = Table(["l", "d", "s", "b", "t", "st", "m", "arr", "c", "nul"],
+              [longs, dbls, strs, bools, ts, struct, mp, arr, const, ConstColumn(None, "string", n, "cpu")], n)
+    return t
+
+
+def test_gpu_serializer_matches_host(gpu, monkeypatch):
+    from dxa.ops import serialize as ser
+    t = _serializer_table("cpu")
+    host = ser.Staged(t).render()                     # CPU table → host serializer
+    gt = t.to(gpu)
+    st = ser.Staged(gt)
+    assert st.gpu
+    dev = st.render()
+    assert dev.blob == host.blob
+    assert dev.lens.tolist() == host.lens.tolist()
+
+
+def test_gpu_java_double_matches_host(gpu):
+    import ctypes
+    import numpy as np
+    from dxa.ops import native as N
+    from dxa.ops.serialize import java_double
+    rng = np.random.default_rng(3)
+    vals = np.concatenate([rng.standard_normal(50000) * 10.0 ** rng.integers(-300, 300, 50000),
+                           rng.integers(0, 2**63, 50000, dtype=np.int64).view(np.float64)])
+    vals = vals[np.isfinite(vals)]
+    d = torch.from_numpy(vals).to(gpu)
+    out = torch.zeros(32 * len(vals), dtype=torch.uint8, device=gpu)
+    lens = torch.zeros(len(vals), dtype=torch.int32, device=gpu)
+    N.call("dxa_java_double_dev", N.ptr(d), len(vals), N.ptr(out), N.ptr(lens), N.stream_handle(gpu))
+    o, l = out.cpu().numpy(), lens.cpu().numpy()
+    bad = [v for i, v in enumerate(vals) if bytes(o[32 * i:32 * i + l[i]]).decode() != java_double(float(v))]
+    assert not bad, bad[:5]

@@ -150,3 +150,26 @@ def test_utility_helpers():
         assert U.fail_fast([ex.submit(lambda: 1), ex.submit(lambda: 2)]) == [1, 2]
         with pytest.raises(ZeroDivisionError):
             U.fail_fast([ex.submit(lambda: 1 / 0)])
+
+
+def test_device_double_formatter_on_host():
+    """The __host__ __device__ Ryu/Java formatter of the GPU serializer, run on the CPU, equals the host formatter."""
+    import ctypes
+    import numpy as np
+    from dxa.ops import native as N
+    from dxa.ops.serialize import java_double
+    try:
+        L = N.lib()
+    except Exception:
+        pytest.skip("kernel library not built")
+    rng = np.random.default_rng(7)
+    vals = np.concatenate([rng.standard_normal(20000) * 10.0 ** rng.integers(-300, 300, 20000),
+                           rng.integers(0, 2**63, 20000, dtype=np.int64).view(np.float64),
+                           np.array([0.0, -0.0, 1e7, 9999999.0, 1e-3, 0.00099, 5e-324, 2.2250738585072014e-308,
+                                     1.7976931348623157e308, 0.1, 0.3, 1e22, 1e23, 2.0 ** 53])])
+    vals = vals[np.isfinite(vals)]
+    out = np.zeros(32 * len(vals), dtype=np.uint8)
+    lens = np.zeros(len(vals), dtype=np.int32)
+    L.dxa_java_double_hostcheck(vals.ctypes.data, len(vals), out.ctypes.data, lens.ctypes.data)
+    bad = [v for i, v in enumerate(vals) if bytes(out[32 * i:32 * i + lens[i]]).decode() != java_double(float(v))]
+    assert not bad, bad[:5]
