@@ -52,6 +52,8 @@ def write_atomic(path: str, data: bytes | str, gzip_it: bool = False) -> Path:
     p.parent.mkdir(parents=True, exist_ok=True)
     if isinstance(data, str):
         data = data.encode("utf-8")
+    elif isinstance(data, memoryview) and gzip_it:
+        data = bytes(data)
     if gzip_it:
         data = gzip.compress(data)
     fd, tmp = tempfile.mkstemp(prefix="." + p.name + ".", dir=str(p.parent))

@@ -74,10 +74,10 @@ class Sink:
     as_json: bool = True
 
 
-def _joined(lines) -> str:
-    """Newline-joined documents; a blob-backed ``JsonLines`` is joined without per-line objects."""
-    text = getattr(lines, "text", None)
-    return text() if text is not None else "\n".join(lines)
+def _joined(lines):
+    """Newline-joined documents; a blob-backed ``JsonLines`` yields a zero-copy buffer (no per-line objects)."""
+    data = getattr(lines, "data", None)
+    return data() if data is not None else "\n".join(lines)
 
 
 def _chunks(xs, n):
@@ -202,9 +202,11 @@ def _file_sink(d, output_name) -> Optional[Sink]:
     def write(lines, table, ts, target):
         p = fs.local_path(java_time_format(path, ts))
         p.parent.mkdir(parents=True, exist_ok=True)
-        with open(p, "a") as f:
+        with open(p, "ab") as f:
             if len(lines):
-                f.write(_joined(lines) + "\n")
+                d = _joined(lines)
+                f.write(d.encode("utf-8") if isinstance(d, str) else d)
+                f.write(b"\n")
         return len(lines)
     return Sink("File", write, d.get("filter"))
 

@@ -327,8 +327,7 @@ class Staged:
             host.copy_(out[:total], non_blocking=True)
             side.synchronize()
         self.table = None
-        blob = host.numpy().tobytes()
-        return JsonLines(blob, host_lens.numpy() - 1)
+        return JsonLines(host.numpy(), host_lens.numpy() - 1)     # the pinned buffer itself, no copy
 
     def render(self, nthreads: Optional[int] = None) -> "JsonLines":
         if self.gpu:
@@ -358,13 +357,28 @@ class Staged:
 
 
 class JsonLines:
-    """Newline-terminated JSON lines held as one blob (what sinks write) + per-line lengths.  Behaves as a
-    read-only sequence of ``str`` (decoded lazily) for sinks that want individual documents."""
+    """Newline-terminated JSON lines held as one buffer (what sinks write) + per-line lengths.  The buffer may be
+    ``bytes`` or a uint8 numpy array (e.g. the pinned D2H target of the device serializer — no extra host copy);
+    behaves as a read-only sequence of ``str`` (decoded lazily) for sinks that want individual documents."""
 
-    def __init__(self, blob: bytes, lens):
-        self.blob = blob
+    def __init__(self, blob, lens):
+        self._buf = blob
+        self._bytes = blob if isinstance(blob, (bytes, bytearray)) else None
         self.lens = np.asarray(lens, dtype=np.int64)
         self._starts = None
+
+    @property
+    def blob(self) -> bytes:
+        if self._bytes is None:
+            self._bytes = np.asarray(self._buf).tobytes()
+        return self._bytes
+
+    def nbytes(self) -> int:
+        return len(self._buf)
+
+    def view(self) -> memoryview:
+        """Zero-copy view of the whole newline-terminated buffer."""
+        return memoryview(self._buf if self._bytes is None else self._bytes).cast("B")
 
     def __len__(self):
         return int(self.lens.shape[0])
@@ -383,25 +397,28 @@ class JsonLines:
         if not 0 <= i < len(self):
             raise IndexError(i)
         s = int(self._offsets()[i])
-        return self.blob[s:s + int(self.lens[i])].decode("utf-8")
+        return bytes(self.view()[s:s + int(self.lens[i])]).decode("utf-8")
 
     def __iter__(self):
-        if self.blob.count(b"\n") == len(self):      # no raw newlines inside documents: split in one pass
-            return iter(self.blob.decode("utf-8").split("\n")[:len(self)])
+        b = self.blob
+        if b.count(b"\n") == len(self):              # no raw newlines inside documents: split in one pass
+            return iter(b.decode("utf-8").split("\n")[:len(self)])
         return (self[i] for i in range(len(self)))
 
     def text(self) -> str:
         """All lines joined by newlines (no trailing newline) — ``"\\n".join(lines)`` without per-line objects."""
-        return self.blob[:-1].decode("utf-8") if self.blob else ""
+        return bytes(self.data()).decode("utf-8")
 
-    def data(self) -> bytes:
-        return self.blob[:-1] if self.blob else b""
+    def data(self):
+        """Newline-joined documents without the trailing newline, as a zero-copy buffer."""
+        n = self.nbytes()
+        return self.view()[:n - 1] if n else memoryview(b"")
 
     def __eq__(self, other):
         return list(self) == list(other)
 
     def __repr__(self):
-        return f"JsonLines(n={len(self)}, bytes={len(self.blob)})"
+        return f"JsonLines(n={len(self)}, bytes={self.nbytes()})"
 
 
 def stage_table(table) -> Staged:
