@@ -87,6 +87,14 @@ class Processor:
         # ---- extensions
         from ..udf.registry import build_udfs
         self.udfs, self.udafs, self.udf_refreshers = build_udfs(d, udfs or {}, udafs or {})
+        from ..udf.registry import _instantiate
+        if normalizer is None and d.get(S.PROCESS_PREFIX + "inputnormalizer"):
+            normalizer = _instantiate(d.get(S.PROCESS_PREFIX + "inputnormalizer"))          # InputNormalizerHandler
+        if pre_projection is None and d.get(S.PROCESS_PREFIX + "preprojection"):
+            pp = _instantiate(d.get(S.PROCESS_PREFIX + "preprojection"))                    # PreProjectionHandler
+            init = getattr(pp, "initialize", None)
+            pp = init(d) if init is not None else pp
+            pre_projection = pp if callable(pp) and not hasattr(pp, "process") else pp.process
         self.normalizer = normalizer
         self.pre_projection = pre_projection
         self.append_props = {k: v for k, v in d.sub_dictionary(S.PROCESS_PREFIX + "appendproperty.").items()}
@@ -149,9 +157,10 @@ class Processor:
     def project(self, raw: RawBatch, batch_time_us: int, ctx: EvalContext) -> Table:
         t0 = time.perf_counter()
         buf = raw.buf
+        offs = raw.offs
         if self.normalizer is not None:
-            buf = self.normalizer(buf, raw.offs)
-        raw_col, row_ok = parse(buf, raw.offs, self.parse_plan)
+            buf, offs = self.normalizer(buf, offs)
+        raw_col, row_ok = parse(buf, offs, self.parse_plan)
         self._sync()
         self.stage_times["parse"] = time.perf_counter() - t0
         n = raw.n

@@ -314,3 +314,36 @@ DXA_API int dxa_str_to_ts(const uint8_t* arena, const int64_t* starts, const int
                      valid, n, out, out_valid);
   return (int)hipGetLastError();
 }
+
+// Input normaliser byte map (kernel K2: e.g. control characters → '#', RemoveInvalidChars.scala:12-17): every byte
+// of the raw batch goes through a 256-entry table held in LDS; 16 bytes per lane per iteration (dwordx4 loads and
+// stores), grid-stride so one launch covers any batch size.
+__global__ __launch_bounds__(256) void byte_map_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                       int64_t n, const uint8_t* __restrict__ map) {
+  __shared__ uint8_t lut[256];
+  lut[threadIdx.x] = map[threadIdx.x];
+  __syncthreads();
+  const int64_t nvec = n / 16;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    uint4 w = reinterpret_cast<const uint4*>(src)[v];
+    uint32_t* p = reinterpret_cast<uint32_t*>(&w);
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = p[k];
+      p[k] = (uint32_t)lut[x & 0xff] | ((uint32_t)lut[(x >> 8) & 0xff] << 8) | ((uint32_t)lut[(x >> 16) & 0xff] << 16) |
+             ((uint32_t)lut[x >> 24] << 24);
+    }
+    reinterpret_cast<uint4*>(dst)[v] = w;
+  }
+  for (int64_t i = nvec * 16 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = lut[src[i]];
+}
+
+DXA_API int dxa_byte_map(const uint8_t* src, uint8_t* dst, int64_t n, const uint8_t* map, void* st) {
+  if (n <= 0) return 0;
+  if ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) return -1;      // callers pass 16-B aligned allocations
+  int64_t blocks = (n / 16 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(byte_map_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)st, src, dst, n, map);
+  return (int)hipGetLastError();
+}

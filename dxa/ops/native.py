@@ -26,6 +26,7 @@ c_i32 = ctypes.c_int32
 c_p = ctypes.c_void_p
 
 _SIGS = {
+    "dxa_byte_map": [c_p, c_p, c_i64, c_p, c_p],
     "dxa_serialize_lengths": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p],
     "dxa_serialize_write": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],

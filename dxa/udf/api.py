@@ -93,14 +93,40 @@ class UDAF:
 
 
 class StringNormalizer:
-    """Raw-event normaliser applied before JSON parsing.  ``byte_map()`` (256 entries) runs as a device kernel;
-    ``normalize(str)`` is the per-string host fallback."""
+    """Raw-event normaliser applied before JSON parsing (``datax.job.process.inputnormalizer``,
+    InputNormalizerHandler.scala).  A ``byte_map()`` (256 entries) runs as the device byte-map kernel over the whole
+    raw batch in one pass; otherwise ``normalize(str)`` is applied per event on the host (re-framed afterwards)."""
 
     def byte_map(self) -> Optional[List[int]]:
         return None
 
     def normalize(self, s: str) -> str:
         return s
+
+    def __call__(self, buf: torch.Tensor, offs: torch.Tensor):
+        """Normalise a framed raw batch → (buf, offs)."""
+        m = self.byte_map()
+        if m is not None:
+            return apply_byte_map(buf, m), offs
+        data = bytes(buf.cpu().numpy())
+        o = offs.cpu().tolist()
+        recs = [self.normalize(data[o[i]:o[i + 1]].decode("utf-8", "replace")).encode() for i in range(len(o) - 1)]
+        from ..ops.jsonparse import frame_records
+        return frame_records(recs, device=buf.device)
+
+
+def apply_byte_map(buf: torch.Tensor, table: List[int]) -> torch.Tensor:
+    lut = torch.tensor(table, dtype=torch.uint8)
+    if buf.is_cuda:
+        from ..ops import native as N
+        out = torch.empty_like(buf)
+        lut = lut.to(buf.device)
+        try:
+            N.call("dxa_byte_map", N.ptr(buf), N.ptr(out), buf.numel(), N.ptr(lut), N.stream_handle(buf.device))
+            return out
+        except N.NativeError:          # unaligned view: fall through to the tensor-op path
+            pass
+    return lut.to(buf.device)[buf.long()]
 
 
 class PreProjectionProcessor:

@@ -62,3 +62,28 @@ def test_app_entry_point(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     last = json.loads(r.stdout.strip().splitlines()[-1])
     assert last["batches"] == 2 and last["last"]["Input_DataXProcessedInput_Events_Count"] > 0
+
+
+def test_input_normalizer_and_preprojection(tmp_path):
+    """``datax.job.process.inputnormalizer`` (RemoveInvalidChars: control chars → '#') runs before parsing and
+    ``datax.job.process.preprojection`` gets the raw table before projection."""
+    from dxa.config.settings import SettingDictionary
+    from dxa.engine.processor import Processor
+    from dxa.ops.jsonparse import frame_records
+    from dxa.engine.processor import RawBatch
+    schema = json.dumps({"type": "struct", "fields": [{"name": "s", "type": "string", "nullable": True,
+                                                       "metadata": {}}]})
+    (tmp_path / "schema.json").write_text(schema)
+    (tmp_path / "proj.txt").write_text("Raw.s AS s")
+    (tmp_path / "t.txt").write_text("--DataXQuery--\nOut = SELECT s FROM DataXProcessedInput")
+    d = SettingDictionary({
+        "datax.job.name": "norm", "datax.job.input.default.blobschemafile": str(tmp_path / "schema.json"),
+        "datax.job.process.projection": str(tmp_path / "proj.txt"),
+        "datax.job.process.transform": str(tmp_path / "t.txt"),
+        "datax.job.process.inputnormalizer": "datax.sample.normalizer.RemoveInvalidChars",
+        "datax.job.output.Out.memory.enabled": "true"})
+    proc = Processor(d, "cpu")
+    buf, offs = frame_records([b'{"s":"a\x01b"}', b'{"s":"ok"}'])
+    proc.keep_views = True
+    proc.process_batch(RawBatch(buf, offs, 2), 0, 1_000_000)
+    assert proc.last_views["Out"].column("s").to_pylist() == ["a#b", "ok"]

@@ -223,3 +223,14 @@ def test_gpu_java_double_matches_host(gpu):
     o, l = out.cpu().numpy(), lens.cpu().numpy()
     bad = [v for i, v in enumerate(vals) if bytes(o[32 * i:32 * i + l[i]]).decode() != java_double(float(v))]
     assert not bad, bad[:5]
+
+
+def test_byte_map_kernel_matches_cpu(gpu):
+    from dxa.udf.api import apply_byte_map
+    from dxa.udf.samples import RemoveInvalidChars
+    table = RemoveInvalidChars().byte_map()
+    for n in (0, 5, 16, 1000, 1 << 20, (1 << 20) + 7):
+        buf = torch.randint(0, 256, (n,), dtype=torch.uint8)
+        want = apply_byte_map(buf, table)
+        got = apply_byte_map(buf.to(gpu), table).cpu()
+        assert torch.equal(got, want), n
