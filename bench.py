@@ -80,10 +80,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    if world > 1:
+        if device.type == "cuda":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=device)          # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")                              # CPU rehearsal of the same code path
     on_gpu = device.type == "cuda"
 
     from dxa.ops import native

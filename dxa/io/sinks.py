@@ -313,6 +313,9 @@ class StagedOutput:
     def finish(self, partition_time: _dt.datetime, target: Optional[str] = None) -> Dict[str, int]:
         """Host-side half: render JSON (waits only for this output's D2H copies) and write every sink."""
         metrics = {f"{SINK_PREFIX}InputEvents": self.n}
+        # the key set must not depend on the data: ranks all-reduce the batch metrics as one vector
+        for s in self.op.sinks:
+            metrics[f"{SINK_PREFIX}{s.name}_{'Filtered' if s.filter_expr else 'All'}"] = 0
         if self.n == 0:
             return metrics
         rendered = {}

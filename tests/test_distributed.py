@@ -151,3 +151,23 @@ def test_two_rank_queries_match_single_process():
     # shuffle round trip preserves the multiset of rows
     for r in (0, 1):
         assert _canon(res[r][-1]) == _canon(rows)
+
+
+@pytest.mark.parametrize("flow", ["groupby", "window"])
+def test_bench_two_ranks_gloo(flow, tmp_path):
+    """bench.py's multi-rank path (the driver's N-GPU scaling run) rehearsed on CPU: two ranks, gloo, one JSON line
+    whose value aggregates both ranks — catches collective mismatches before they reach RCCL."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "bench.py"), "--gpus", "2", "--flow", flow, "--events-per-batch", "500",
+                        "--steps", "2", "--warmup", "3"], capture_output=True, text=True, env=env, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1000 and out["value"] > 0
