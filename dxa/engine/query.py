@@ -410,6 +410,12 @@ class _NotPaned(Exception):
     pass
 
 
+class _EmptyPane:
+    def __init__(self, table):
+        self.table = table
+        self.partials = {}
+
+
 def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     """GROUP BY over a window view answered from per-pane partial aggregates (see ``windows.PanedTable``).
     Returns None when the query does not qualify (non-decomposable aggregates, no aggregation, …)."""
@@ -486,9 +492,11 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
                 parts.append(ent[1])
             else:
                 parts.extend(pane_partial(p, True) for p in panes)
+        if "meta" not in state:
+            # nothing of this rank's window is in range: still produce (empty) partials, so every rank runs the
+            # same exchange — the choice of plan must not depend on a rank's data
+            parts.append(pane_partial(_EmptyPane(empty), False))
     except _NotPaned:
-        return None
-    if "meta" not in state:
         return None
     plan, key_names, gexprs = state["meta"]
     parts = [p for p in parts if p.length] or parts[:1]

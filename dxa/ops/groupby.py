@@ -168,6 +168,13 @@ def aggregate(groups: Groups, col, func: str, n: int):
         return PrimColumn("long", _agg_raw(groups, None, None, "count", n, device))
     col = materialize(col)
     valid = col.valid
+    if n == 0 and func != "count":
+        # only the global aggregate has a group with no rows: every aggregate but COUNT is NULL there (Spark)
+        rdt = {"avg": "double", "stddev": "double", "stddev_samp": "double", "stddev_pop": "double",
+               "variance": "double", "var_samp": "double", "var_pop": "double", "std": "double"}.get(func, col.dtype)
+        if func == "sum" and col.dtype in ("int", "short", "byte"):
+            rdt = "long"
+        return ConstColumn(None, rdt, ng, device).materialize()
     if func == "count":
         return PrimColumn("long", _agg_raw(groups, None, valid, "count", n, device))
     if func in ("first", "last"):
