@@ -765,6 +765,9 @@ def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope
                     col = evaluate(e, src_scope, ctx)
         key, valid = _sort_key_tensor(col)
         key, valid = key[perm], valid[perm]
+        # null slots hold arbitrary bytes (device buffers are not zeroed): give them one key so the stable sort keeps
+        # their order from the previous (more significant) keys
+        key = torch.where(valid, key, torch.zeros_like(key))
         nulls_first = it.nulls_first if it.nulls_first is not None else it.ascending
         o = torch.argsort(key, stable=True, descending=not it.ascending)
         v = valid[o]

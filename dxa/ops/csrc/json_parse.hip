@@ -37,6 +37,13 @@ struct ParseArgs {
   int32_t* lens;                // [nlen][n]
   uint8_t* valid;               // [nnodes][n]  (pre-zeroed)
   uint8_t* row_ok;              // [n]
+  // key-order speculation: producers emit keys in a fixed order, so the next key is predicted (schema order,
+  // re-synchronised after every key) and checked with 8-byte compares instead of a byte-serial hash
+  const int32_t* first_child;   // [nnodes] first kept child of a struct node (-1: none)
+  const int32_t* next_sib;      // [nnodes] next kept sibling (-1: none)
+  const int32_t* key_word;      // [nnodes] offset (in u64 words) of the node's key text
+  const int32_t* key_len;       // [nnodes] key length in bytes
+  const uint64_t* key_words;    // key texts, zero padded to 8-byte words
 };
 
 __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
@@ -69,6 +76,30 @@ struct Reader {
 };
 
 __device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
+
+// 8 bytes at any address (two aligned loads + funnel shift); the batch buffer carries 16 bytes of tail padding.
+__device__ __forceinline__ uint64_t load8(const uint8_t* base, int64_t q) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base + q);
+  const uintptr_t b = a & ~(uintptr_t)7;
+  const uint64_t lo = *reinterpret_cast<const uint64_t*>(b);
+  const uint32_t sh = (uint32_t)(a - b) * 8u;
+  if (sh == 0) return lo;
+  const uint64_t hi = *reinterpret_cast<const uint64_t*>(b + 8);
+  return (lo >> sh) | (hi << (64u - sh));
+}
+
+// Does the key text at q equal the L-byte literal (followed by the closing quote)?
+__device__ __forceinline__ bool key_matches(const uint8_t* buf, int64_t q, int64_t end, const uint64_t* kw, int L) {
+  if (q + L >= end) return false;
+  int i = 0;
+  for (; i + 8 <= L; i += 8)
+    if (load8(buf, q + i) != kw[i >> 3]) return false;
+  const uint64_t tail = load8(buf, q + i);
+  const int rem = L - i;                                   // 0..7 bytes of key, then the quote
+  const uint64_t mask = rem == 7 ? ~0ull : ((1ull << (8 * (rem + 1))) - 1);
+  const uint64_t want = (rem ? kw[i >> 3] : 0ull) | ((uint64_t)'"' << (8 * rem));
+  return ((tail ^ want) & mask) == 0;
+}
 
 // Scan a string whose opening quote is at r.p.  On return r.p is past the closing quote.
 __device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, bool& esc) {
@@ -235,6 +266,47 @@ __device__ bool skip_value(Reader& r) {
   return false;
 }
 
+// Hash one escape sequence of a key (r.p at the backslash) as the bytes it decodes to, so "a\u0062" finds "ab".
+__device__ uint64_t hash_escape(Reader& r, uint64_t h) {
+  ++r.p;
+  if (r.p >= r.end) return h;
+  const uint32_t n = r.at(r.p);
+  ++r.p;
+  uint32_t cp;
+  switch (n) {
+    case 'n': return dxa::fnv1a_step(h, '\n');
+    case 't': return dxa::fnv1a_step(h, '\t');
+    case 'r': return dxa::fnv1a_step(h, '\r');
+    case 'b': return dxa::fnv1a_step(h, '\b');
+    case 'f': return dxa::fnv1a_step(h, '\f');
+    case 'u':
+      if (r.p + 4 > r.end) { r.p = r.end; return h; }
+      cp = (hexval(r.at(r.p)) << 12) | (hexval(r.at(r.p + 1)) << 8) | (hexval(r.at(r.p + 2)) << 4) |
+           hexval(r.at(r.p + 3));
+      r.p += 4;
+      if (cp >= 0xD800 && cp < 0xDC00 && r.p + 6 <= r.end && r.at(r.p) == '\\' && r.at(r.p + 1) == 'u') {
+        const uint32_t lo = (hexval(r.at(r.p + 2)) << 12) | (hexval(r.at(r.p + 3)) << 8) |
+                            (hexval(r.at(r.p + 4)) << 4) | hexval(r.at(r.p + 5));
+        if (lo >= 0xDC00 && lo < 0xE000) { cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); r.p += 6; }
+      }
+      if (cp < 0x80) return dxa::fnv1a_step(h, cp);
+      if (cp < 0x800) {
+        h = dxa::fnv1a_step(h, 0xC0 | (cp >> 6));
+        return dxa::fnv1a_step(h, 0x80 | (cp & 0x3F));
+      }
+      if (cp < 0x10000) {
+        h = dxa::fnv1a_step(h, 0xE0 | (cp >> 12));
+        h = dxa::fnv1a_step(h, 0x80 | ((cp >> 6) & 0x3F));
+        return dxa::fnv1a_step(h, 0x80 | (cp & 0x3F));
+      }
+      h = dxa::fnv1a_step(h, 0xF0 | (cp >> 18));
+      h = dxa::fnv1a_step(h, 0x80 | ((cp >> 12) & 0x3F));
+      h = dxa::fnv1a_step(h, 0x80 | ((cp >> 6) & 0x3F));
+      return dxa::fnv1a_step(h, 0x80 | (cp & 0x3F));
+    default: return dxa::fnv1a_step(h, n);            // \" \\ \/ and unknown escapes: the character itself
+  }
+}
+
 __device__ __forceinline__ int lookup(const ParseArgs& a, int parent, uint64_t name_hash) {
   uint64_t k = dxa::fmix64(name_hash ^ ((uint64_t)(parent + 1) * dxa::kGold));
   if (k == 0) k = 1;
@@ -313,6 +385,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
   r.w = make_uint4(0, 0, 0, 0);
 
   int stack[16];
+  int expect[16];
   int depth = 0;
   bool ok = false;
 
@@ -320,6 +393,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
   if (r.cur() != '{') goto done;
   ++r.p;
   stack[0] = 0;  // root node
+  expect[0] = a.first_child[0];
   depth = 1;
   a.valid[row] = 1;  // root struct present
   while (true) {
@@ -332,23 +406,31 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
     }
     if (c != '"') break;
     {
-      // ---- key
+      // ---- key: speculate the expected key first, fall back to hashing the key text
       ++r.p;
-      uint64_t h = dxa::kFnvBasis;
-      bool closed = false;
-      while (r.p < r.end) {
-        const uint32_t kc = r.at(r.p);
-        if (kc == '"') { ++r.p; closed = true; break; }
-        if (kc == '\\') { h = dxa::fnv1a_step(h, kc); ++r.p; if (r.p < r.end) { h = dxa::fnv1a_step(h, r.at(r.p)); ++r.p; } continue; }
-        h = dxa::fnv1a_step(h, kc);
-        ++r.p;
+      int node = -1;
+      const int ex = expect[depth - 1];
+      if (ex >= 0 && key_matches(a.buf, r.p, r.end, a.key_words + a.key_word[ex], a.key_len[ex])) {
+        node = ex;
+        r.p += a.key_len[ex] + 1;
+      } else {
+        uint64_t h = dxa::kFnvBasis;
+        bool closed = false;
+        while (r.p < r.end) {
+          const uint32_t kc = r.at(r.p);
+          if (kc == '"') { ++r.p; closed = true; break; }
+          if (kc == '\\') { h = hash_escape(r, h); continue; }
+          h = dxa::fnv1a_step(h, kc);
+          ++r.p;
+        }
+        if (!closed) break;
+        node = lookup(a, stack[depth - 1], h);
       }
-      if (!closed) break;
+      if (node >= 0) expect[depth - 1] = a.next_sib[node];
       r.skip_ws();
       if (r.cur() != ':') break;
       ++r.p;
       r.skip_ws();
-      const int node = lookup(a, stack[depth - 1], h);
       c = r.cur();
       if (node < 0) {
         if (!skip_value(r)) break;
@@ -360,6 +442,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
       if (c == '{' && t == FT_STRUCT) {
         if (depth >= 16) { if (!skip_value(r)) break; goto after_value; }
         a.valid[(int64_t)node * n + row] = 1;
+        expect[depth] = a.first_child[node];
         stack[depth++] = node;
         ++r.p;
         continue;
@@ -497,10 +580,12 @@ __global__ void write_newlines_kernel(const uint8_t* __restrict__ buf, int64_t l
 DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const uint64_t* lut_keys,
                            const int32_t* lut_node, int32_t lut_cap, const int32_t* node_type,
                            const int32_t* val_slot, const int32_t* len_slot, int32_t nnodes, int64_t* vals,
-                           int32_t* lens, uint8_t* valid, uint8_t* row_ok, void* stream) {
+                           int32_t* lens, uint8_t* valid, uint8_t* row_ok, const int32_t* first_child,
+                           const int32_t* next_sib, const int32_t* key_word, const int32_t* key_len,
+                           const uint64_t* key_words, void* stream) {
   if (n <= 0) return 0;
   ParseArgs a{buf, offs, n, lut_keys, lut_node, lut_cap, node_type, val_slot, len_slot, nnodes, vals, lens,
-              valid, row_ok};
+              valid, row_ok, first_child, next_sib, key_word, key_len, key_words};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(valid, 0, (size_t)nnodes * (size_t)n, s);
   if (e != hipSuccess) return (int)e;

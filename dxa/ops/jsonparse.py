@@ -88,6 +88,24 @@ class ParsePlan:
         self.lut_keys = [_to_i64(k) for k in keys]
         self.lut_node = node_of
         self.cap = cap
+        # key-order speculation tables: children in schema order, key texts as zero-padded 8-byte words
+        nn = len(self.nodes)
+        self.first_child = [-1] * nn
+        self.next_sib = [-1] * nn
+        last = {}
+        for idx, nd in enumerate(self.nodes[1:], start=1):
+            if nd.parent in last:
+                self.next_sib[last[nd.parent]] = idx
+            else:
+                self.first_child[nd.parent] = idx
+            last[nd.parent] = idx
+        words, self.key_word, self.key_len = [], [0] * nn, [0] * nn
+        for idx, nd in enumerate(self.nodes):
+            b = nd.name.encode("utf-8")
+            self.key_word[idx], self.key_len[idx] = len(words), len(b)
+            b += b"\0" * (-len(b) % 8)
+            words += [int.from_bytes(b[i:i + 8], "little") for i in range(0, len(b), 8)]
+        self.key_words = [_to_i64(w) for w in words] or [0]
         self._dev: Dict[str, Tuple[torch.Tensor, ...]] = {}
 
     def _wanted(self, path) -> bool:
@@ -116,7 +134,12 @@ class ParsePlan:
                  torch.tensor(self.lut_node, dtype=torch.int32, device=device),
                  torch.tensor([n.code for n in self.nodes], dtype=torch.int32, device=device),
                  torch.tensor([n.val_slot for n in self.nodes], dtype=torch.int32, device=device),
-                 torch.tensor([n.len_slot for n in self.nodes], dtype=torch.int32, device=device))
+                 torch.tensor([n.len_slot for n in self.nodes], dtype=torch.int32, device=device),
+                 torch.tensor(self.first_child, dtype=torch.int32, device=device),
+                 torch.tensor(self.next_sib, dtype=torch.int32, device=device),
+                 torch.tensor(self.key_word, dtype=torch.int32, device=device),
+                 torch.tensor(self.key_len, dtype=torch.int32, device=device),
+                 torch.tensor(self.key_words, dtype=torch.int64, device=device))
             self._dev[key] = t
         return t
 
@@ -165,7 +188,7 @@ def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan):
 
 
 def _parse_gpu(buf, offs, n, plan: ParsePlan):
-    lut_k, lut_n, types, vslot, lslot = plan.device_tables(buf.device)
+    lut_k, lut_n, types, vslot, lslot, fchild, nsib, kword, klen, kwords = plan.device_tables(buf.device)
     nn = len(plan.nodes)
     vals = torch.empty((max(1, plan.nval), max(n, 1)), dtype=torch.int64, device=buf.device)
     lens = torch.empty((max(1, plan.nlen), max(n, 1)), dtype=torch.int32, device=buf.device)
@@ -174,7 +197,7 @@ def _parse_gpu(buf, offs, n, plan: ParsePlan):
     if n:
         N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
                N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
-               N.stream_handle(buf.device))
+               N.ptr(fchild), N.ptr(nsib), N.ptr(kword), N.ptr(klen), N.ptr(kwords), N.stream_handle(buf.device))
     nulls = [1] * nn
     if n:
         cnt = torch.empty(nn, dtype=torch.int64, device=buf.device)

@@ -234,3 +234,31 @@ def test_byte_map_kernel_matches_cpu(gpu):
         want = apply_byte_map(buf, table)
         got = apply_byte_map(buf.to(gpu), table).cpu()
         assert torch.equal(got, want), n
+
+
+def test_json_parse_key_order_speculation(gpu):
+    """Keys out of schema order, unknown keys, escaped key text and prefix-sharing names must all resolve exactly
+    like the CPU reference (the kernel predicts the next key and falls back to hashing on a miss)."""
+    rnd = random.Random(11)
+    schema = schema_from_json(json.dumps({"type": "struct", "fields": [
+        {"name": "a", "type": "long"}, {"name": "ab", "type": "string"}, {"name": "abcdefgh", "type": "double"},
+        {"name": "abcdefghi", "type": "long"},
+        {"name": "s", "type": {"type": "struct", "fields": [{"name": "x", "type": "long"},
+                                                             {"name": "y", "type": "string"}]}}]}))
+    recs = []
+    for i in range(4000):
+        items = [("a", i), ("ab", f"v{i}"), ("abcdefgh", i * 0.5), ("abcdefghi", -i),
+                 ("s", {"y": "q", "x": i}), ("zz_unknown", [1, 2])]
+        if rnd.random() < 0.5:
+            rnd.shuffle(items)
+        d = "{" + ",".join(json.dumps(k) + ":" + json.dumps(v) for k, v in items) + "}"
+        if rnd.random() < 0.1:
+            d = d.replace('"ab":', '"a\\u0062":')          # escaped key text
+        recs.append(d.encode())
+    plan = ParsePlan(schema)
+    b, o = frame_records(recs)
+    cpu_raw, cpu_ok = parse(b, o, plan)
+    bg, og = frame_records(recs, device=gpu)
+    gpu_raw, gpu_ok = parse(bg, og, plan)
+    assert torch.equal(cpu_ok.cpu(), gpu_ok.cpu())
+    assert cpu_raw.to_pylist() == gpu_raw.to_pylist()
