@@ -36,6 +36,7 @@ from .serialize import table_to_json_lines
 from .state import create_state_tables
 from .types import MapType, StructType, schema_from_json
 from .windows import TimeWindowConf, WindowStore
+from ..telemetry import tracing
 
 log = logging.getLogger("dxa.processor")
 _SYNC_STAGES = os.environ.get("DXA_SYNC_STAGES") == "1"
@@ -160,7 +161,8 @@ class Processor:
         offs = raw.offs
         if self.normalizer is not None:
             buf, offs = self.normalizer(buf, offs)
-        raw_col, row_ok = parse(buf, offs, self.parse_plan)
+        with tracing.stage("parse"):
+            raw_col, row_ok = parse(buf, offs, self.parse_plan)
         self._sync()
         self.stage_times["parse"] = time.perf_counter() - t0
         n = raw.n
@@ -208,7 +210,8 @@ class Processor:
         part = P.PARTITIONED if P.active() else P.REPLICATED
         projected.dist = part
         if self.window_store is not None:
-            views, cnt = self.window_store.process(projected, batch_time_us, interval_us)
+            with tracing.stage("windows", self.stage_times):
+                views, cnt = self.window_store.process(projected, batch_time_us, interval_us)
             for k, v in views.items():
                 v.dist = part
                 cat.register(k, v)
@@ -230,7 +233,8 @@ class Processor:
                 if q is None:
                     q = self._parsed[cmd.text] = parse_query(cmd.text)     # parsed once, reused every batch
                 ts = time.perf_counter() if _SYNC_STAGES else 0.0
-                result = execute(q, cat, ctx)
+                with tracing.stage(f"sql:{cmd.name}"):
+                    result = execute(q, cat, ctx)
                 if _SYNC_STAGES:
                     self._sync()
                     self.stage_times[f"sql:{cmd.name}"] = time.perf_counter() - ts
@@ -258,6 +262,7 @@ class Processor:
         fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(_timed, st.finish, partition_time))
                                                  for name, st in staged], t_start)
         fl.t_staged = time.perf_counter()
+        fl.stages = dict(self.stage_times)
         self._inflight = fl
         self.stage_times["output_stage"] = time.perf_counter() - t1
         if self.keep_views:
@@ -290,6 +295,7 @@ class Processor:
             metrics.update(zip(keys, vec.tolist()))
         for st in self.state_tables.values():
             st.persist()
+        metrics.update(tracing.stage_metrics(fl.stages))          # per-rank stage timings (not all-reduced)
         # processing latency = batch start → its last sink write finished (measured where the write finished, not
         # where the completion was observed)
         metrics["Latency-Process"] = t_done - fl.t0
@@ -339,6 +345,7 @@ class Processor:
         for refresh in self.udf_refreshers:
             refresh(batch_time_us)
         try:
+            _maybe_inject_fault(self.batches)
             projected = self.project(raw, batch_time_us, ctx)
             metrics = self.route(projected, batch_time_us, interval_us, ctx,
                                  partition_time or _dt.datetime.utcnow(), t0)
@@ -355,13 +362,31 @@ class Processor:
             raise
 
 
+def _maybe_inject_fault(batch_index: int):
+    """Fault injection for recovery tests: ``DXA_FAULT_INJECT=batch=<k>[,once=<marker file>]`` fails the k-th batch of
+    this process (with ``once``: only until the marker exists, i.e. the first attempt)."""
+    spec = os.environ.get("DXA_FAULT_INJECT")
+    if not spec:
+        return
+    opts = dict(kv.split("=", 1) for kv in spec.split(",") if "=" in kv)
+    if int(opts.get("batch", -1)) != batch_index:
+        return
+    marker = opts.get("once")
+    if marker:
+        if os.path.exists(marker):
+            return
+        with open(marker, "w") as f:
+            f.write("injected\n")
+    raise RuntimeError(f"injected fault at batch {batch_index}")
+
+
 def _timed(fn, *args):
     out = fn(*args)
     return out, time.perf_counter()
 
 
 class _InFlight:
-    __slots__ = ("batch_time_us", "metrics", "futures", "t0", "t_staged")
+    __slots__ = ("batch_time_us", "metrics", "futures", "t0", "t_staged", "stages")
 
     def __init__(self, batch_time_us, metrics, futures, t0):
         self.batch_time_us = batch_time_us
@@ -369,6 +394,7 @@ class _InFlight:
         self.futures = futures
         self.t0 = t0
         self.t_staged = t0
+        self.stages = {}
 
 
 def _fmt_ts(us: int) -> str:

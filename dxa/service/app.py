@@ -57,6 +57,10 @@ class ServiceState:
         os.environ.setdefault("DXA_SECRETS_DIR", os.path.join(self.root, "secrets"))
         self.store = DocumentStore(os.path.join(self.root, "local.db"))
         self.jobs = JobManager(self.store, os.path.join(self.root, "logs"))
+        from .jobs import Supervisor
+        self.supervisor = Supervisor(self.jobs)
+        if os.environ.get("DXA_SUPERVISE", "1") == "1":
+            self.supervisor.start()
         self.kernels = KernelManager(device)
         self.metrics = MetricStore.default()
         self.metrics_endpoint = metrics_endpoint

@@ -89,6 +89,7 @@ class JobManager:
             raise RuntimeError(f"job {name} is still {job['state']}")
         log_path = os.path.join(self.log_dir, f"{name}.log")
         env = dict(os.environ)
+        env.update({k: str(v) for k, v in (job.get("env") or {}).items()})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
@@ -188,3 +189,54 @@ class JobManager:
                 job["state"] = state
                 self.store.upsert(_COLL, name, job)
         return job
+
+
+class Supervisor(threading.Thread):
+    """Restarts failed streaming jobs from their last checkpoint (the role YARN attempt retries played for the
+    reference: defaultSparkJob.json ``spark.yarn.maxAppAttempts`` + ``attemptFailuresValidityInterval``).
+
+    A job in state Error with ``autoRestart`` (default on, off for batch jobs) is restarted after an exponential
+    backoff; more than ``max_restarts`` failures inside ``window_s`` marks it ``Failed`` and stops restarting."""
+
+    def __init__(self, jobs: JobManager, period_s: float = 5.0, max_restarts: int = 5, window_s: float = 3600.0,
+                 backoff_s: float = 2.0, max_backoff_s: float = 120.0):
+        super().__init__(daemon=True, name="dxa-supervisor")
+        self.jobs = jobs
+        self.period_s = period_s
+        self.max_restarts = max_restarts
+        self.window_s = window_s
+        self.backoff_s = backoff_s
+        self.max_backoff_s = max_backoff_s
+        self._stop = threading.Event()
+        self.restarts: Dict[str, List[float]] = {}
+
+    def check_once(self, now: Optional[float] = None) -> List[str]:
+        now = time.time() if now is None else now
+        restarted = []
+        for job in self.jobs.get_all():
+            name = job["name"]
+            if job.get("state") != ERROR or not job.get("autoRestart", job.get("app") != "batch"):
+                continue
+            hist = [t for t in self.restarts.get(name, []) if now - t < self.window_s]
+            if len(hist) >= self.max_restarts:
+                job["state"] = "Failed"
+                self.jobs.store.upsert(_COLL, name, job)
+                continue
+            delay = min(self.max_backoff_s, self.backoff_s * (2 ** len(hist)))
+            if hist and now - hist[-1] < delay:
+                continue
+            try:
+                self.jobs.start(name)
+                hist.append(now)
+                restarted.append(name)
+            except Exception:  # noqa: BLE001 — try again next period
+                pass
+            self.restarts[name] = hist
+        return restarted
+
+    def run(self):
+        while not self._stop.wait(self.period_s):
+            self.check_once()
+
+    def stop(self):
+        self._stop.set()

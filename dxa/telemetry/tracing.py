@@ -1,0 +1,51 @@
+"""Stage tracing: named ranges around every micro-batch stage.
+
+* ``DXA_TRACE=1`` emits ROCm-tracer ranges (roctx, through ``torch.cuda.nvtx`` on ROCm builds) so
+  ``rocprofv3 --marker-trace`` / ``--kernel-trace`` timelines show parse / project / window / each SQL statement /
+  output staging per batch (SURVEY §5 "roctx ranges per batch stage").
+* Stage wall times are always recorded and exported with the batch metrics as ``Latency-Stage-<name>`` (seconds), so
+  they reach the metric store and the dashboard like the reference's ``Latency-Process``.
+* ``logger()`` returns a logger whose name carries the rank suffix (the reference's ``-P<partition>-T<attempt>``
+  executor logger suffix, SparkEnvVariables.scala:14-17).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from contextlib import contextmanager
+from typing import Dict, Optional
+
+_TRACE = os.environ.get("DXA_TRACE") == "1"
+_nvtx = None
+if _TRACE:
+    try:
+        import torch
+        if torch.cuda.is_available():
+            _nvtx = torch.cuda.nvtx
+    except Exception:  # noqa: BLE001 — tracing is best effort
+        _nvtx = None
+
+
+@contextmanager
+def stage(name: str, times: Optional[Dict[str, float]] = None):
+    """Time (and, with DXA_TRACE=1, mark) one stage; ``times[name]`` receives the wall seconds."""
+    if _nvtx is not None:
+        _nvtx.range_push(name)
+    t0 = time.perf_counter()
+    try:
+        yield
+    finally:
+        if times is not None:
+            times[name] = time.perf_counter() - t0
+        if _nvtx is not None:
+            _nvtx.range_pop()
+
+
+def stage_metrics(times: Dict[str, float]) -> Dict[str, float]:
+    return {f"Latency-Stage-{k}": float(v) for k, v in times.items()}
+
+
+def logger(name: str) -> logging.Logger:
+    rank = os.environ.get("RANK")
+    return logging.getLogger(f"{name}-R{rank}" if rank is not None else name)

@@ -38,6 +38,7 @@ def client(tmp_path, monkeypatch):
     from fastapi.testclient import TestClient
     from dxa.service.app import create_app
     monkeypatch.setenv("DXA_SECRETS_DIR", str(tmp_path / "secrets"))
+    monkeypatch.setenv("DXA_SUPERVISE", "0")          # tests drive the supervisor by hand
     return TestClient(create_app(str(tmp_path / "root")))
 
 
@@ -312,3 +313,43 @@ def test_save_deploy_and_query_scenarios(client, monkeypatch):
     res = run_parallel("query", [STEPS[s] for s in QUERY_AND_SCHEMA], ctx, 2)
     assert all(not r.failed for r in res), [(s.description, s.exception, s.result) for r in res
                                              for s in r.step_results]
+
+
+@pytest.mark.timeout(300)
+def test_supervisor_restarts_failed_job_from_checkpoint(client, tmp_path):
+    """Fault injection fails the first attempt at batch 1; the supervisor restarts the job, which then completes
+    (SURVEY §5 failure detection / recovery)."""
+    from dxa.service.jobs import Supervisor
+    client.post("/api/flow/save", json=mini_flow("flaky"))
+    client.post("/api/flow/generateconfigs", json={"name": "flaky"})
+    st = client.app.state.dxa
+    marker = str(tmp_path / "fault.marker")
+    st.jobs.upsert({"name": "flaky", "args": {"maxBatches": "3", "realtime": "false"},
+                    "env": {"DXA_FAULT_INJECT": f"batch=1,once={marker}"}})
+
+    def wait_final():
+        t0 = time.time()
+        while time.time() - t0 < 240:
+            s = st.jobs.get("flaky")["state"]
+            if s in ("Success", "Error", "Failed"):
+                return s
+            time.sleep(0.3)
+        return None
+
+    st.jobs.start("flaky")
+    assert wait_final() == "Error" and os.path.exists(marker)
+    sup = Supervisor(st.jobs, backoff_s=0.0)
+    assert sup.check_once() == ["flaky"]
+    assert wait_final() == "Success"
+    log = open(st.jobs.get("flaky")["log"]).read()
+    assert "injected fault at batch 1" in log and '"batches": 3' in log
+    assert "Latency-Stage-parse" in log                       # stage timings are exported with batch metrics
+    # a job that keeps failing is given up after max_restarts
+    st.jobs.upsert({"name": "flaky", "env": {"DXA_FAULT_INJECT": "batch=0"}})
+    sup2 = Supervisor(st.jobs, backoff_s=0.0, max_restarts=1)
+    st.jobs.start("flaky")
+    assert wait_final() == "Error"
+    assert sup2.check_once() == ["flaky"]
+    assert wait_final() == "Error"
+    sup2.check_once()
+    assert st.jobs.get("flaky")["state"] == "Failed"
