@@ -20,6 +20,7 @@ from ..sql.parser import parse_query
 from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, Table, concat_columns,
                      concat_tables, materialize)
 from .expr import (AGG_FUNCS, EvalContext, EvalError, Scope, cast_column, evaluate, output_name, predicate_mask)
+from . import windowfn as W
 from .types import common_type, is_nested
 
 
@@ -433,6 +434,8 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
         _collect_aggs(sel.having, ctx, aggs)
     if not aggs and not sel.group_by:
         return None
+    if any(W.window_calls(e) for e, _ in items):
+        return None
     if not D.decomposable(aggs, ctx):
         return None
     exprs = [e for e, _ in items] + list(sel.group_by) + ([sel.where] if sel.where is not None else []) + (
@@ -547,11 +550,16 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     items = _expand_items(sel, scope)
     is_agg = bool(sel.group_by) or any(_contains_agg(e, ctx) for e, _ in items) or (
         sel.having is not None and _contains_agg(sel.having, ctx))
+    wcalls = [w for e, _ in items for w in W.window_calls(e)]
+    if wcalls and P.active() and sdist != P.REPLICATED:
+        scope = _window_repartition(scope, wcalls, ctx, is_agg)
+        sdist = scope.dist
     if is_agg:
         out = _aggregate(sel, items, scope, ctx)
         src = None
     else:
-        cols = [evaluate(e, scope, ctx) for e, _ in items]
+        subst = _window_columns(wcalls, lambda x: evaluate(x, scope, ctx), scope.length, scope.device, {})
+        cols = [evaluate(e, scope, ctx, subst or None) for e, _ in items]
         out = Table([nm for _, nm in items], cols, scope.length, scope.device)
         out.dist = sdist
         src = scope
@@ -601,12 +609,47 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
         rep_scope = Scope(scope.names, [ConstColumn(None, c.dtype, 1, dev) for c in scope.cols], scope.quals, 1, dev)
     else:
         rep_scope = Scope(scope.names, [c.take(groups.rep) for c in scope.cols], scope.quals, ng, dev)
-    cols = [evaluate(e, rep_scope, ctx, subst) for e, _ in items]
-    out = Table([nm for _, nm in items], cols, ng, dev)
+    m = None
     if sel.having is not None:
         m = predicate_mask(evaluate(sel.having, rep_scope, ctx, subst))
+    wcalls = [w for e, _ in items for w in W.window_calls(e)]
+    if wcalls:
+        # window functions see the grouped rows after HAVING (Spark evaluates them last)
+        if m is not None:
+            keep = torch.nonzero(m).flatten()
+            rep_scope = Scope(rep_scope.names, [c.take(keep) for c in rep_scope.cols], rep_scope.quals,
+                              int(keep.shape[0]), dev)
+            subst = {k: c.take(keep) for k, c in subst.items()}
+            ng, m = rep_scope.length, None
+        _window_columns(wcalls, lambda x: evaluate(x, rep_scope, ctx, subst), rep_scope.length, dev, subst)
+    cols = [evaluate(e, rep_scope, ctx, subst) for e, _ in items]
+    out = Table([nm for _, nm in items], cols, rep_scope.length, dev)
+    if m is not None:
         out = out.filter(m)
     return out
+
+
+def _window_columns(wcalls, ev, n, dev, subst: Dict) -> Dict:
+    """Evaluate every window call once (keyed by expression) into ``subst``."""
+    for w in wcalls:
+        if w.key() not in subst:
+            try:
+                subst[w.key()] = W.evaluate_window(w, ev, n, dev)
+            except W.WindowError as ex:
+                raise QueryError(str(ex)) from ex
+    return subst
+
+
+def _window_repartition(scope: Scope, wcalls, ctx, is_agg: bool) -> Scope:
+    """Make a partitioned scope exact for window functions: rows of one window partition must live on one rank.
+    Shuffle by the PARTITION BY keys when every window call shares them; otherwise (no PARTITION BY, differing
+    specs, or windows over aggregated rows) gather everything to every rank."""
+    parts = {tuple(p.key() for p in w.partition) for w in wcalls}
+    if is_agg or len(parts) != 1 or not wcalls[0].partition:
+        return _gather_scope(scope)
+    keys = [materialize(evaluate(p, scope, ctx)) for p in wcalls[0].partition]
+    keys = [k if not isinstance(k, (StructColumn, ArrayColumn)) else _nested_key(k) for k in keys]
+    return _shuffle_scope(scope, keys)
 
 
 def _aggregate_distributed(sel, items, scope, ctx, gexprs, keys) -> Table:

@@ -65,6 +65,24 @@ class Call(Expr):
 
 
 @dataclass(eq=False)
+class WindowCall(Expr):
+    """``func(args) OVER (PARTITION BY ... ORDER BY ... [ROWS|RANGE frame])``.  ``frame`` is ``(kind, start, end)``
+    with each bound ``(type, offset)``: type in unbounded_preceding / preceding / current / following /
+    unbounded_following."""
+    func: Call
+    partition: List[Expr] = field(default_factory=list)
+    order: List["OrderItem"] = field(default_factory=list)
+    frame: Optional[tuple] = None
+
+    def key(self):
+        return ("over", self.func.key(), tuple(p.key() for p in self.partition),
+                tuple((o.expr.key(), o.ascending, o.nulls_first) for o in self.order), self.frame)
+
+    def children(self):
+        return list(self.func.args) + list(self.partition) + [o.expr for o in self.order]
+
+
+@dataclass(eq=False)
 class BinOp(Expr):
     op: str            # '+','-','*','/','%','=','!=','<','<=','>','>=','and','or','||','<=>','&','|','^','div'
     left: Expr

@@ -589,17 +589,76 @@ class Parser:
         self.expect_op("(")
         low = name.lower()
         if self.accept_op(")"):
-            return A.Call(low, [])
+            return self._maybe_over(A.Call(low, []))
         if self.is_op("*") and self.is_op(")", tok=self.peek()):
             self.advance()
             self.advance()
-            return A.Call(low, [], star=True)
+            return self._maybe_over(A.Call(low, [], star=True))
         distinct = self.accept_kw("distinct")
         args = [self.parse_expr()]
         while self.accept_op(","):
             args.append(self.parse_expr())
         self.expect_op(")")
-        return A.Call(low, args, distinct=distinct)
+        return self._maybe_over(A.Call(low, args, distinct=distinct))
+
+    def is_word(self, *words, tok=None) -> bool:
+        t = tok or self.cur
+        return t.kind in ("id", "kw") and t.text.lower() in words
+
+    def accept_word(self, *words) -> bool:
+        if self.is_word(*words):
+            self.i += 1
+            return True
+        return False
+
+    def _maybe_over(self, call):
+        """``call OVER (PARTITION BY ... ORDER BY ... frame)`` (Spark window functions)."""
+        if not (self.is_word("over") and self.is_op("(", tok=self.peek())):
+            return call
+        self.advance()
+        self.expect_op("(")
+        part, order, frame = [], [], None
+        if self.accept_word("partition"):
+            self.expect_kw("by")
+            part.append(self.parse_expr())
+            while self.accept_op(","):
+                part.append(self.parse_expr())
+        if self.is_kw("order") or self.is_word("sort"):
+            self.advance()
+            self.expect_kw("by")
+            order = self.parse_order_items()
+        if self.is_word("rows", "range"):
+            kind = self.advance().text.lower()
+            if self.accept_kw("between"):
+                lo = self._frame_bound()
+                self.expect_kw("and")
+                hi = self._frame_bound()
+            else:
+                lo, hi = self._frame_bound(), ("current", 0)
+            frame = (kind, lo, hi)
+        self.expect_op(")")
+        return A.WindowCall(call, part, order, frame)
+
+    def _frame_bound(self):
+        if self.accept_word("unbounded"):
+            if self.accept_word("preceding"):
+                return ("unbounded_preceding", 0)
+            if self.accept_word("following"):
+                return ("unbounded_following", 0)
+            self.error("expected PRECEDING or FOLLOWING")
+        if self.accept_word("current"):
+            if not self.accept_word("row"):
+                self.error("expected ROW")
+            return ("current", 0)
+        t = self.advance()
+        if t.kind != "num":
+            self.error("expected a frame offset")
+        k = int(t.text.rstrip("lL"))
+        if self.accept_word("preceding"):
+            return ("preceding", k)
+        if self.accept_word("following"):
+            return ("following", k)
+        self.error("expected PRECEDING or FOLLOWING")
 
 
 def _number_literal(text: str) -> A.Literal:

@@ -1,5 +1,6 @@
 """Multi-process (gloo, world_size 2) tests of the RCCL-style exchange paths: two-phase distributed GROUP BY,
-non-decomposable shuffle aggregation, DISTINCT, partitioned ⨝ partitioned joins and the table shuffle itself.
+non-decomposable shuffle aggregation, DISTINCT, partitioned ⨝ partitioned joins, window functions (OVER) and the
+table shuffle itself.
 Each rank holds half of the rows; results must equal a single-process run over all rows."""
 import json
 import os
@@ -19,6 +20,11 @@ QUERIES = [
     "SELECT DISTINCT s FROM T",
     "SELECT a.k, COUNT(*) AS c FROM T a JOIN T2 b ON a.k = b.k GROUP BY a.k",
     "SELECT k, SUM(v) AS sv FROM T WHERE v > 0 GROUP BY k HAVING COUNT(*) > 3",
+    # window functions: shuffled by PARTITION BY keys, or gathered without one / over grouped rows
+    "SELECT k, s, v, RANK() OVER (PARTITION BY k ORDER BY v DESC) AS r, SUM(v) OVER (PARTITION BY k) AS tot, "
+    "MAX(v) OVER (PARTITION BY k ORDER BY v ROWS BETWEEN 2 PRECEDING AND CURRENT ROW) AS m3 FROM T",
+    "SELECT k, v, DENSE_RANK() OVER (ORDER BY k) AS dr, COUNT(*) OVER () AS n FROM T",
+    "SELECT k, SUM(v) AS sv, RANK() OVER (ORDER BY k DESC) AS r FROM T GROUP BY k",
 ]
 
 
