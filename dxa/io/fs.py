@@ -1,8 +1,10 @@
 """Filesystem helpers (the reference's HadoopClient, DataProcessing/datax-host/src/main/scala/datax/fs/
 HadoopClient.scala:33-815): read (gzip-aware), atomic write via temp-then-rename, write with timeout, list.
 
-Only local / mounted paths are supported (``file://`` prefix optional); ``wasbs://``/``hdfs://`` URIs are mapped under
-``DXA_FS_ROOT`` (default ``./.dxa_fs``) so reference job configs run unchanged on a single node.
+``wasbs://container@account.blob.<suffix>/path`` URLs whose account key is known (``io/azure.storage_key_for``) go to
+Azure Blob storage over its REST API. Every other ``wasbs://``/``hdfs://``/… URI is mapped under ``DXA_FS_ROOT``
+(default ``./.dxa_fs``), so reference job configs run unchanged on a single node. Local paths (optional ``file://``
+prefix) are used as they are.
 """
 from __future__ import annotations
 
@@ -30,9 +32,20 @@ def local_path(path: str) -> Path:
     return Path(path)
 
 
+def _remote(path: str):
+    if not _REMOTE.match(path):
+        return None
+    from .azure import blob_client_for_url
+    return blob_client_for_url(path)
+
+
 def read_bytes(path: str) -> bytes:
-    p = local_path(path)
-    data = p.read_bytes()
+    r = _remote(path)
+    if r is not None:
+        client, container, blob = r
+        data = client.get_blob(container, blob)
+    else:
+        data = local_path(path).read_bytes()
     if path.endswith(".gz") or data[:2] == b"\x1f\x8b":
         data = gzip.decompress(data)
     return data
@@ -47,15 +60,22 @@ def read_lines(path: str) -> List[str]:
 
 
 def write_atomic(path: str, data: bytes | str, gzip_it: bool = False) -> Path:
-    """Write to a temp file in the destination folder, then rename (never leaves a partial file)."""
-    p = local_path(path)
-    p.parent.mkdir(parents=True, exist_ok=True)
+    """Write to a temp file in the destination folder, then rename (never leaves a partial file).  A blob PUT is
+    atomic on the service side, so remote paths are written in one request."""
     if isinstance(data, str):
         data = data.encode("utf-8")
     elif isinstance(data, memoryview) and gzip_it:
         data = bytes(data)
     if gzip_it:
         data = gzip.compress(data)
+    r = _remote(path)
+    if r is not None:
+        client, container, blob = r
+        client.put_blob(container, blob, data, "application/json" if ".json" in path else "application/octet-stream",
+                        "gzip" if gzip_it else None)
+        return Path(path)
+    p = local_path(path)
+    p.parent.mkdir(parents=True, exist_ok=True)
     fd, tmp = tempfile.mkstemp(prefix="." + p.name + ".", dir=str(p.parent))
     with os.fdopen(fd, "wb") as f:
         f.write(data)
@@ -69,10 +89,23 @@ def write_with_timeout(path: str, data: bytes | str, timeout_s: float, gzip_it: 
 
 
 def exists(path: str) -> bool:
+    r = _remote(path)
+    if r is not None:
+        client, container, blob = r
+        return bool([n for n in client.list_blobs(container, blob) if n == blob or n.startswith(blob.rstrip("/") + "/")])
     return local_path(path).exists()
 
 
 def list_files(path: str, recursive: bool = False) -> List[str]:
+    r = _remote(path)
+    if r is not None:
+        client, container, blob = r
+        prefix = blob.rstrip("/") + "/" if blob else ""
+        base = path[: len(path) - len(blob)] if blob else path.rstrip("/") + "/"
+        names = client.list_blobs(container, prefix)
+        if not recursive:
+            names = [n for n in names if "/" not in n[len(prefix):]]
+        return sorted(base + n for n in names)
     p = local_path(path)
     if not p.exists():
         return []
@@ -81,6 +114,13 @@ def list_files(path: str, recursive: bool = False) -> List[str]:
 
 
 def delete(path: str):
+    r = _remote(path)
+    if r is not None:
+        client, container, blob = r
+        for n in client.list_blobs(container, blob):
+            if n == blob or n.startswith(blob.rstrip("/") + "/"):
+                client.delete_blob(container, n)
+        return
     p = local_path(path)
     if p.is_dir():
         import shutil

@@ -53,8 +53,20 @@ def blob_folder(fmt: Optional[str], ts: _dt.datetime, target: Optional[str] = No
     return out.rstrip("/") + "/"
 
 
-def eventhub_send(conn: str, payload: bytes, hub: str = "default"):
-    """EventHub emulation: ``http(s)://`` connection → POST; anything else → spool file under DXA_FS_ROOT."""
+_eh_senders: Dict[str, object] = {}
+
+
+def eventhub_send(conn: str, payload: bytes, hub: str = "default", properties: Optional[Dict[str, str]] = None):
+    """Send one event: an Event Hubs connection string (``Endpoint=sb://…;SharedAccessKey…``) → REST send
+    (``io/azure.EventHubSender``, the reference's EventHubSenderPool); ``http(s)://`` → POST; anything else → spool
+    file under DXA_FS_ROOT."""
+    from . import azure
+    if azure.is_eventhub_connection(conn):
+        sender = _eh_senders.get(conn)
+        if sender is None:
+            sender = _eh_senders.setdefault(conn, azure.EventHubSender(conn, hub))
+        sender.send(payload, properties)
+        return
     if conn.startswith("http://") or conn.startswith("https://"):
         import urllib.request
         urllib.request.urlopen(urllib.request.Request(conn, data=payload, method="POST"), timeout=5).read()
@@ -113,6 +125,7 @@ def _eventhub_sink(d, output_name) -> Optional[Sink]:
     if not conn:
         return None
     compression = (d.get("compressiontype") or "gzip").lower()
+    props = dict(d.sub_dictionary("appendproperty.").items()) or None
 
     def write(lines, table, ts, target):
         c = resolve(conn)
@@ -120,7 +133,7 @@ def _eventhub_sink(d, output_name) -> Optional[Sink]:
             payload = "\n".join(chunk).encode()
             if compression != "none":
                 payload = gzip.compress(payload)
-            eventhub_send(c, payload, output_name)
+            eventhub_send(c, payload, output_name, props)
         return len(lines)
     return Sink("EventHub", write, d.get("filter"))
 
@@ -147,6 +160,16 @@ def _cosmos_sink(d, output_name) -> Optional[Sink]:
     coll = d.get("collection") or output_name
 
     def write(lines, table, ts, target):
+        from . import azure
+        c = resolve(conn)
+        if azure.is_cosmos_connection(c):
+            # document upserts through the REST API (CosmosDBSinker's upsert mode)
+            client = azure.CosmosClient(c)
+            for line in lines:
+                doc = json.loads(line)
+                doc.setdefault("id", str(uuid.uuid4()))
+                client.upsert(db, coll, doc)
+            return len(lines)
         root = os.environ.get("DXA_FS_ROOT", ".dxa_fs")
         folder = os.path.join(root, "cosmosdb", db, coll)
         os.makedirs(folder, exist_ok=True)
