@@ -53,6 +53,13 @@ MODEL = {
 }
 
 
+def _cpu_lines(raw, length):
+    """CPU rehearsal of the newline framing (record offsets of '\\n'-terminated events)."""
+    import torch
+    nl = torch.nonzero(raw[:length] == 10).flatten()
+    return torch.cat([torch.zeros(1, dtype=torch.int64), nl + 1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,12 +69,15 @@ def main():
     ap.add_argument("--events-per-batch", type=int, default=None, help="events per GPU per micro-batch")
     ap.add_argument("--ref-rows", type=int, default=100_000_000, help="reference table rows (join flow)")
     ap.add_argument("--pool", type=int, default=3, help="distinct pre-generated batches cycled (pinned source)")
-    ap.add_argument("--source", choices=["pinned", "device", "gpu-sim"], default=None,
-                    help="pinned: H2D copy of raw bytes every step; device: bytes already in HBM; gpu-sim: GPU "
+    ap.add_argument("--source", choices=["pinned", "pinned-lz4", "device", "gpu-sim"], default=None,
+                    help="pinned: H2D copy of raw bytes every step; pinned-lz4: H2D copy of an LZ4 frame of JSON "
+                         "lines, decoded + newline-framed on the GPU; device: bytes already in HBM; gpu-sim: GPU "
                          "generator renders each batch")
     ap.add_argument("--profile-stages", action="store_true")
     ap.add_argument("--sync-outputs", action="store_true",
                     help="finish each batch's sink writes before the next batch starts (default: pipelined)")
+    ap.add_argument("--torch-profile", default=None, metavar="PATH",
+                    help="run the timed steps under torch.profiler and write op/stage tables to PATH")
     args = ap.parse_args()
     flow = args.flow
     warmup = DEFAULT_WARMUP[flow] if args.warmup is None else args.warmup
@@ -117,6 +127,19 @@ def main():
 
     t_gen = time.perf_counter()
     pool = []
+    comp_bytes = []
+    if source == "pinned-lz4":
+        from dxa.ops import lz4
+        from dxa.ops.jsonparse import frame_lines_gpu
+        prog_nl = iot.program(newline=True)
+        base_ms = clock0_us // 1000
+        for p in range(args.pool):
+            buf, offs = generate(prog_nl, E, device, seed=1000 * rank + p + 1, row0=p * E, base_ms=base_ms)
+            total = int(offs[-1])
+            frame = lz4.compress_frame(buf[:total].cpu(), lz4.DEFAULT_BLOCK, threads=16)
+            del buf, offs
+            comp_bytes.append(frame.size)
+            pool.append(lz4.DeviceFrame.from_frame(frame, lz4.DEFAULT_BLOCK, pin=on_gpu))
     if source in ("pinned", "device"):
         base_ms = clock0_us // 1000
         for p in range(args.pool):
@@ -130,7 +153,7 @@ def main():
         torch.cuda.synchronize(device)
     gen_s = time.perf_counter() - t_gen
 
-    side = torch.cuda.Stream(device) if (on_gpu and source in ("pinned", "gpu-sim")) else None
+    side = torch.cuda.Stream(device) if (on_gpu and source in ("pinned", "pinned-lz4", "gpu-sim")) else None
     staged = {}
     sizes = []
 
@@ -149,6 +172,21 @@ def main():
                 ev = torch.cuda.Event()
                 ev.record(side)
             staged[i] = (db, do, ev)
+            return
+        if source == "pinned-lz4":
+            fr = pool[i % len(pool)]
+            if side is None:
+                raw = lz4.decompress_device(fr)
+                staged[i] = (raw, frame_lines_gpu(raw, fr.content_size, expected=E) if on_gpu else
+                             _cpu_lines(raw, fr.content_size), None)
+                return
+            with torch.cuda.stream(side):
+                dfr = fr.to(device, non_blocking=True)
+                raw = lz4.decompress_device(dfr)
+                offs = frame_lines_gpu(raw, fr.content_size, expected=E)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            staged[i] = (raw, offs, ev)
             return
         hb, ho = pool[i % len(pool)]
         if side is None:
@@ -186,6 +224,13 @@ def main():
         dist.barrier()
     lat.clear()
     sizes.clear()
+    prof = None
+    if args.torch_profile:
+        from dxa.telemetry import tracing
+        tracing.enable_profiler_ranges()
+        acts = [torch.profiler.ProfilerActivity.CPU] + ([torch.profiler.ProfilerActivity.CUDA] if on_gpu else [])
+        prof = torch.profiler.profile(activities=acts)
+        prof.__enter__()
     t0 = time.perf_counter()
     last = None
     for i in range(warmup, warmup + args.steps):
@@ -193,6 +238,15 @@ def main():
     last = proc.drain() or proc.last_metrics           # the last batch's outputs complete inside the timed region
     if on_gpu:
         torch.cuda.synchronize(device)
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        ka = prof.key_averages()
+        with open(args.torch_profile, "w") as f:
+            f.write(f"# {flow}: {args.steps} steps (profiled run; timings include profiler overhead)\n")
+            f.write(ka.table(sort_by="cuda_time_total" if on_gpu else "cpu_time_total", row_limit=60,
+                             max_name_column_width=60))
+            f.write("\n# by self CPU time\n")
+            f.write(ka.table(sort_by="self_cpu_time_total", row_limit=40, max_name_column_width=60))
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -239,6 +293,9 @@ def main():
         "vs_target_1M_events_per_sec_per_gpu": value / world / 1e6,
         "generation_s": round(gen_s, 3),
     }
+    if comp_bytes:
+        out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)
+        out["config"]["lz4_ratio"] = round((sum(sizes) / len(sizes) - 16) / (sum(comp_bytes) / len(comp_bytes)), 2)
     if last:
         out["last_batch_outputs"] = {k: v for k, v in last.items() if k.startswith("Output_")}
     if flow == "join":

@@ -53,7 +53,7 @@ def _lib():
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.dxa_kafka_encode.restype = ctypes.c_void_p
         L.dxa_kafka_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
-                                       ctypes.c_void_p]
+                                       ctypes.c_int32, ctypes.c_void_p]
         _LIB = L
     return _LIB
 
@@ -62,8 +62,11 @@ def crc32c(data: bytes) -> int:
     return int(_lib().dxa_crc32c(data, len(data)))
 
 
-def encode_batch(values: Sequence[bytes], timestamp_ms: Optional[int] = None) -> bytes:
-    """One uncompressed v2 record batch holding ``values`` (null keys)."""
+CODECS = {"none": 0, "gzip": 1, "lz4": 3}
+
+
+def encode_batch(values: Sequence[bytes], timestamp_ms: Optional[int] = None, compression: str = "none") -> bytes:
+    """One v2 record batch holding ``values`` (null keys); ``compression`` none / gzip / lz4."""
     vals = b"".join(values)
     offs = np.zeros(len(values) + 1, dtype=np.int64)
     if values:
@@ -71,7 +74,10 @@ def encode_batch(values: Sequence[bytes], timestamp_ms: Optional[int] = None) ->
     out_len = ctypes.c_int64(0)
     L = _lib()
     ptr = L.dxa_kafka_encode(vals, offs.ctypes.data, len(values),
-                             int(time.time() * 1000) if timestamp_ms is None else timestamp_ms, ctypes.byref(out_len))
+                             int(time.time() * 1000) if timestamp_ms is None else timestamp_ms,
+                             CODECS[compression.lower()], ctypes.byref(out_len))
+    if not ptr:
+        raise KafkaError(f"record batch encode failed ({compression})")
     try:
         return ctypes.string_at(ptr, out_len.value)
     finally:
@@ -79,7 +85,7 @@ def encode_batch(values: Sequence[bytes], timestamp_ms: Optional[int] = None) ->
 
 
 _ERRS = {-2: "unsupported message format (magic != 2)", -3: "CRC mismatch", -4: "gzip decode failed",
-         -5: "unsupported compression codec (snappy/lz4/zstd)"}
+         -5: "unsupported compression codec (snappy/zstd)", -6: "lz4 decode failed"}
 
 
 def decode_records(record_set: bytes, min_offset: int, pad: int = 16, verify_crc: bool = True
@@ -358,8 +364,9 @@ class KafkaClient:
                 return recs, hw
         return b"", offset
 
-    def produce(self, topic: str, partition: int, values: Sequence[bytes], acks: int = 1) -> int:
-        batch = encode_batch(values)
+    def produce(self, topic: str, partition: int, values: Sequence[bytes], acks: int = 1,
+                compression: str = "none") -> int:
+        batch = encode_batch(values, compression=compression)
         body = _W().str(None).i16(acks).i32(30000).array(
             [topic], lambda w, t: w.str(t).array([partition], lambda w2, p: w2.i32(p).bytes(batch))).b
         r = self._leader(topic, partition).request(API_PRODUCE, 3, bytes(body))

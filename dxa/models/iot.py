@@ -351,9 +351,14 @@ def _device_perm(n: int, device):
     return torch.argsort(h)
 
 
-def program():
+def program(newline: bool = False):
+    """Generator program for the IoT event; ``newline=True`` terminates every event with '\\n' (JSON-lines
+    payloads: blob files, compressed ingest frames)."""
     from ..simulate.datagen import compile_simulated
-    return compile_simulated(IOT_FIELDS)
+    prog = compile_simulated(IOT_FIELDS)
+    if newline:
+        prog.lit(b"\n")
+    return prog
 
 
 def smoke_batch(device, n: int = 4096):

@@ -50,6 +50,16 @@ __device__ __forceinline__ uint64_t hash_bytes(const uint8_t* p, int64_t len) {
   return fmix64(h ^ (uint64_t)len);
 }
 
+// Byte i (0..15) of a 16-byte register window.  Written as a select between two 64-bit halves plus a shift: the
+// "pick one of four dwords" form is rewritten by the compiler into a dynamically indexed private array, which it
+// then places in LDS or scratch (bank-conflicting per-lane traffic on every byte).
+__device__ __forceinline__ uint32_t window_byte(const uint4& w, uint32_t i) {
+  const uint64_t lo = ((uint64_t)w.y << 32) | w.x;
+  const uint64_t hi = ((uint64_t)w.w << 32) | w.z;
+  const uint64_t x = (i & 8u) ? hi : lo;
+  return (uint32_t)(x >> ((i & 7u) * 8u)) & 0xffu;
+}
+
 // FNV-1a 64 — used for JSON key names (matched against host-computed schema hashes).
 __host__ __device__ __forceinline__ uint64_t fnv1a_step(uint64_t h, uint32_t c) {
   return (h ^ (uint64_t)c) * 0x100000001b3ull;

@@ -16,6 +16,8 @@
 #include <vector>
 #include <zlib.h>
 
+#include "dxa_lz4.h"
+
 namespace {
 
 uint32_t g_crc_table[8][256];
@@ -102,6 +104,37 @@ bool gunzip(const uint8_t* src, size_t n, std::string& out) {
   return true;
 }
 
+// Kafka codec 3: the records section is one LZ4 frame (Java producers omit the content size).
+bool lz4_unframe(const uint8_t* src, size_t n, std::string& out) {
+  int64_t content = -1, frame_end = 0;
+  int32_t max_block = 0;
+  const int64_t nb = dxa::lz4::frame_blocks(src, (int64_t)n, nullptr, nullptr, nullptr, 0, &content, &max_block,
+                                            &frame_end);
+  if (nb == -1) return false;
+  const int64_t cap = content >= 0 ? content : (nb > 0 ? nb : 1) * (int64_t)max_block;
+  out.resize((size_t)cap);
+  const int64_t m = dxa::lz4::decompress_frame(src, (int64_t)n, (uint8_t*)&out[0], cap);
+  if (m < 0) return false;
+  out.resize((size_t)m);
+  return true;
+}
+
+bool gzip_bytes(const std::string& in, std::string& out) {
+  z_stream zs;
+  std::memset(&zs, 0, sizeof zs);
+  if (deflateInit2(&zs, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+  out.resize(deflateBound(&zs, (uLong)in.size()) + 32);
+  zs.next_in = (Bytef*)in.data();
+  zs.avail_in = (uInt)in.size();
+  zs.next_out = (Bytef*)&out[0];
+  zs.avail_out = (uInt)out.size();
+  const int rc = deflate(&zs, Z_FINISH);
+  deflateEnd(&zs);
+  if (rc != Z_STREAM_END) return false;
+  out.resize(zs.total_out);
+  return true;
+}
+
 struct Sink {
   // two-pass: count/size, then copy
   bool write;
@@ -175,8 +208,13 @@ int walk_batches(const uint8_t* data, int64_t len, int64_t min_offset, int64_t m
         if (!gunzip(recs, (size_t)(bend - recs), raw)) return -4;
         rc = walk_records((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + raw.size(), count, base,
                           min_offset, s);
+      } else if (codec == 3) {
+        std::string raw;
+        if (!lz4_unframe(recs, (size_t)(bend - recs), raw)) return -6;
+        rc = walk_records((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + raw.size(), count, base,
+                          min_offset, s);
       } else {
-        return -5;                                     // snappy / lz4 / zstd: not built in
+        return -5;                                     // snappy / zstd: not built in
       }
       if (rc) return rc;
     }
@@ -213,9 +251,10 @@ __attribute__((visibility("default"))) int dxa_kafka_extract(const uint8_t* data
   return rc;
 }
 
-// Encode n values (vals + offs[n+1]) as one uncompressed v2 batch (baseOffset 0); returns malloc'd bytes.
+// Encode n values (vals + offs[n+1]) as one v2 batch (codec 0 none, 1 gzip, 3 lz4) (baseOffset 0); returns malloc'd bytes.
 __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode(const uint8_t* vals, const int64_t* offs, int64_t n,
-                                                                int64_t timestamp_ms, int64_t* out_len) {
+                                                                int64_t timestamp_ms, int32_t codec,
+                                                                int64_t* out_len) {
   std::string recs;
   for (int64_t i = 0; i < n; ++i) {
     std::string r;
@@ -230,8 +269,22 @@ __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode(const uint8_t* 
     put_varlong(recs, (int64_t)r.size());
     recs += r;
   }
+  if (codec == 1) {
+    std::string z;
+    if (!gzip_bytes(recs, z)) return nullptr;
+    recs.swap(z);
+  } else if (codec == 3) {
+    std::string z((size_t)dxa::lz4::frame_bound((int64_t)recs.size(), 64 * 1024), '\0');
+    const int64_t m = dxa::lz4::compress_frame((const uint8_t*)recs.data(), (int64_t)recs.size(), (uint8_t*)&z[0],
+                                               (int64_t)z.size(), 64 * 1024, 1);
+    if (m < 0) return nullptr;
+    z.resize((size_t)m);
+    recs.swap(z);
+  } else if (codec != 0) {
+    return nullptr;
+  }
   std::string body;                     // from attributes to the end (CRC domain)
-  put_be(body, 0, 2);                   // attributes: no compression, CreateTime
+  put_be(body, (uint64_t)codec, 2);     // attributes: compression codec, CreateTime
   put_be(body, (uint64_t)(n > 0 ? n - 1 : 0), 4);
   put_be(body, (uint64_t)timestamp_ms, 8);
   put_be(body, (uint64_t)timestamp_ms, 8);

@@ -73,6 +73,7 @@ class ParsePlan:
                     nd.len_slot = nl
                     nl += 1
         self.nval, self.nlen = nv, nl
+        self.max_depth = max((len(nd.path) for nd in self.nodes if nd.code == 0), default=0)
         cap = 1 << max(4, math.ceil(math.log2(max(2, 2 * len(self.nodes)))))
         keys = [0] * cap
         node_of = [-1] * cap
@@ -159,23 +160,39 @@ def frame_records(records: Sequence[bytes], device="cpu", pin: bool = False):
     return buf, o
 
 
-def frame_lines_gpu(buf: torch.Tensor, length: int) -> torch.Tensor:
-    """Record offsets for '\\n'-delimited data already on the device (newline framing kernel)."""
-    chunk = 4096
-    nch = (length + chunk - 1) // chunk
-    counts = torch.empty(nch, dtype=torch.int64, device=buf.device)
-    st = N.stream_handle(buf.device)
-    N.call("dxa_count_newlines", N.ptr(buf), length, chunk, N.ptr(counts), st)
+def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = None) -> torch.Tensor:
+    """Record offsets for '\\n'-delimited data already on the device (newline framing kernels).
+
+    With ``expected`` (the producer's record count, e.g. from a batch header) there is no host synchronisation: every
+    record must end with a newline and offsets are ``[0, nl_0 + 1, nl_1 + 1, ...]``.  Without it the count is read
+    back and empty lines are dropped."""
+    seg = 1 << 16
+    nseg = (length + seg - 1) // seg
+    dev = buf.device
+    if buf.data_ptr() % 16:
+        buf = buf.clone()
+    counts = torch.empty(max(nseg, 1), dtype=torch.int64, device=dev)
+    st = N.stream_handle(dev)
+    if length:
+        N.call("dxa_count_newlines", N.ptr(buf), length, seg, N.ptr(counts), st)
+    counts = counts[:nseg]
     base = torch.cumsum(counts, 0) - counts
-    total = int(counts.sum().item())
-    pos = torch.empty(total, dtype=torch.int64, device=buf.device)
-    N.call("dxa_write_newlines", N.ptr(buf), length, chunk, N.ptr(base), N.ptr(pos), st)
-    ends = torch.cat([pos + 1, torch.tensor([length], dtype=torch.int64, device=buf.device)])
-    starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=buf.device), pos + 1])
+    total = expected if expected is not None else (int(counts.sum().item()) if nseg else 0)
+    pos = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    if length:
+        N.call("dxa_write_newlines", N.ptr(buf), length, seg, N.ptr(base), N.ptr(pos), total, st)
+    pos = pos[:total]
+    if expected is not None:
+        offs = torch.empty(total + 1, dtype=torch.int64, device=dev)
+        offs[0] = 0
+        offs[1:] = pos + 1
+        return offs
+    ends = torch.cat([pos + 1, torch.tensor([length], dtype=torch.int64, device=dev)])
+    starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos + 1])
     keep = (ends - starts) > 1  # drop empty lines
     starts, ends = starts[keep], ends[keep]
     # contiguous offsets: record i = [offs[i], offs[i+1]); dropped empty lines only hold whitespace
-    return torch.cat([starts, ends[-1:]]) if starts.numel() else torch.zeros(1, dtype=torch.int64, device=buf.device)
+    return torch.cat([starts, ends[-1:]]) if starts.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
 
 
 def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan):
@@ -187,7 +204,14 @@ def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan):
     return _parse_cpu(buf, offs, n, plan)
 
 
+GPU_MAX_DEPTH = 8      # json_parse.hip kMaxDepth: struct nesting tracked in registers
+
+
 def _parse_gpu(buf, offs, n, plan: ParsePlan):
+    if plan.max_depth >= GPU_MAX_DEPTH:
+        # schemas nested deeper than the kernel's register stack parse on the host (same semantics)
+        col, ok = _parse_cpu(buf.cpu(), offs.cpu(), n, plan)
+        return col.to(buf.device), ok.to(buf.device)
     lut_k, lut_n, types, vslot, lslot, fchild, nsib, kword, klen, kwords = plan.device_tables(buf.device)
     nn = len(plan.nodes)
     vals = torch.empty((max(1, plan.nval), max(n, 1)), dtype=torch.int64, device=buf.device)

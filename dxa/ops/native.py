@@ -27,6 +27,8 @@ c_p = ctypes.c_void_p
 
 _SIGS = {
     "dxa_byte_map": [c_p, c_p, c_i64, c_p, c_p],
+    "dxa_lz4_block_sizes": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
+    "dxa_lz4_decode": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
     "dxa_serialize_lengths": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p],
     "dxa_serialize_write": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],
@@ -35,7 +37,7 @@ _SIGS = {
                        c_p, c_p, c_p, c_p, c_p, c_p],
     "dxa_count_newlines": [c_p, c_i64, c_i64, c_p, c_p],
     "dxa_null_counts": [c_p, c_i64, c_i32, c_p, c_p],
-    "dxa_write_newlines": [c_p, c_i64, c_i64, c_p, c_p, c_p],
+    "dxa_write_newlines": [c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p],
     "dxa_hash_i64": [c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],
     "dxa_hash_f64": [c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],
     "dxa_hash_str": [c_p, c_p, c_p, c_p, c_i64, c_p, ctypes.c_int, c_p],

@@ -35,7 +35,7 @@ def program_from_schema_text(text: str):
 
 
 def run(client: KafkaClient, topics: List[str], prog, rate: int, seconds: Optional[float], device="cpu",
-        seed: int = 1) -> int:
+        seed: int = 1, compression: str = "none") -> int:
     meta = client.metadata(topics)
     sent, row, t_end = 0, 0, None if seconds is None else time.time() + seconds
     tick = 0
@@ -45,7 +45,7 @@ def run(client: KafkaClient, topics: List[str], prog, rate: int, seconds: Option
             parts = meta.get(t) or [0]
             events = render_events(prog, rate, device, seed, row)
             row += rate
-            client.produce(t, parts[tick % len(parts)], events)
+            client.produce(t, parts[tick % len(parts)], events, compression=compression)
             sent += len(events)
         tick += 1
         time.sleep(max(0.0, 1.0 - (time.time() - t0)))
@@ -60,6 +60,8 @@ def main(argv=None):
     ap.add_argument("--schema", required=True, help="Spark schema JSON (DataGenerator metadata) or SimulatedData")
     ap.add_argument("--rate", type=int, default=10, help="events per second per topic")
     ap.add_argument("--seconds", type=float, default=None)
+    ap.add_argument("--compression", choices=["none", "gzip", "lz4"], default="none",
+                    help="record batch compression (Kafka compression.type)")
     args = ap.parse_args(argv)
     with open(args.schema) as f:
         prog = program_from_schema_text(f.read())
@@ -71,7 +73,7 @@ def main(argv=None):
         client = KafkaClient(args.bootstrap)
         topics = [t for t in args.topics.split(",") if t]
     device = "cuda" if torch.cuda.is_available() else "cpu"
-    n = run(client, topics, prog, args.rate, args.seconds, device)
+    n = run(client, topics, prog, args.rate, args.seconds, device, compression=args.compression)
     print(json.dumps({"sent": n}))
 
 

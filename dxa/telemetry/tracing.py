@@ -27,17 +27,32 @@ if _TRACE:
         _nvtx = None
 
 
+_record_function = None
+
+
+def enable_profiler_ranges():
+    """Also open a ``torch.profiler.record_function`` range per stage (``bench.py --torch-profile``)."""
+    global _record_function
+    import torch
+    _record_function = torch.profiler.record_function
+
+
 @contextmanager
 def stage(name: str, times: Optional[Dict[str, float]] = None):
     """Time (and, with DXA_TRACE=1, mark) one stage; ``times[name]`` receives the wall seconds."""
     if _nvtx is not None:
         _nvtx.range_push(name)
+    rf = _record_function(name) if _record_function is not None else None
+    if rf is not None:
+        rf.__enter__()
     t0 = time.perf_counter()
     try:
         yield
     finally:
         if times is not None:
             times[name] = time.perf_counter() - t0
+        if rf is not None:
+            rf.__exit__(None, None, None)
         if _nvtx is not None:
             _nvtx.range_pop()
 
