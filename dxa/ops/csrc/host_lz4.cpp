@@ -122,7 +122,7 @@ int64_t compress_block(const uint8_t* src, int64_t n, uint8_t* dst) {
   const int64_t lit = n - anchor;
   *op++ = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
   if (lit >= 15) op = put_len(op, lit - 15);
-  std::memcpy(op, src + anchor, (size_t)lit);
+  if (lit) std::memcpy(op, src + anchor, (size_t)lit);
   op += lit;
   return op - dst;
 }

@@ -1,6 +1,6 @@
 // Native self-check of the host codecs, built with AddressSanitizer + UBSan by tests/test_native_sanitizers.py:
-// Kafka record-batch encode → decode round trips (incl. truncated and corrupted input), CRC-32C vectors, and the
-// row serializer over nulls / nested values / escapes.  Exit code 0 = clean.
+// Kafka record-batch encode → decode round trips for every codec (incl. truncated and corrupted input), CRC-32C
+// vectors, LZ4 frame round trips plus decoding of random garbage / truncated frames, and the Java double formatter.  Exit code 0 = clean.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -15,7 +15,13 @@ int dxa_kafka_count(const uint8_t* data, int64_t len, int64_t min_offset, int64_
                     int64_t* next_offset, int verify_crc);
 int dxa_kafka_extract(const uint8_t* data, int64_t len, int64_t min_offset, uint8_t* vals, int64_t* offs,
                       int64_t* rec_offs, int64_t* next_offset);
-uint8_t* dxa_kafka_encode(const uint8_t* vals, const int64_t* offs, int64_t n, int64_t timestamp_ms, int64_t* out_len);
+uint8_t* dxa_kafka_encode(const uint8_t* vals, const int64_t* offs, int64_t n, int64_t timestamp_ms, int32_t codec,
+                          int64_t* out_len);
+int64_t dxa_lz4_frame_bound(int64_t n, int32_t block_size);
+int64_t dxa_lz4_compress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t block_size,
+                               int32_t threads);
+int64_t dxa_lz4_decompress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
+int64_t dxa_lz4_decompress_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
 void dxa_host_free(void* p);
 int dxa_java_double(double d, char* out, int cap);
 }
@@ -23,7 +29,7 @@ int dxa_java_double(double d, char* out, int cap);
 static int failures = 0;
 #define CHECK(c) do { if (!(c)) { std::fprintf(stderr, "FAIL %s:%d %s\n", __FILE__, __LINE__, #c); ++failures; } } while (0)
 
-static void kafka_roundtrip(int nvals, uint32_t seed) {
+static void kafka_roundtrip(int nvals, uint32_t seed, int codec) {
   std::vector<std::string> vals;
   std::string all;
   std::vector<int64_t> offs{0};
@@ -35,11 +41,12 @@ static void kafka_roundtrip(int nvals, uint32_t seed) {
     offs.push_back((int64_t)all.size());
   }
   int64_t blen = 0;
-  uint8_t* batch = dxa_kafka_encode((const uint8_t*)all.data(), offs.data(), nvals, 1234, &blen);
+  uint8_t* batch = dxa_kafka_encode((const uint8_t*)all.data(), offs.data(), nvals, 1234, codec, &blen);
   for (int64_t cut = blen; cut >= 0; cut -= (blen / 7 + 1)) {       // whole batch, then truncated prefixes
     int64_t n = 0, nb = 0, nxt = 0;
     const int rc = dxa_kafka_count(batch, cut, 0, &n, &nb, &nxt, 1);
     CHECK(rc == 0);
+    if (rc != 0) std::fprintf(stderr, "codec %d nvals %d cut %lld rc %d\n", codec, nvals, (long long)cut, rc);
     if (cut < blen) { CHECK(n == 0); continue; }
     CHECK(n == nvals && nb == (int64_t)all.size());
     std::vector<uint8_t> out((size_t)nb + 16);
@@ -59,10 +66,39 @@ static void kafka_roundtrip(int nvals, uint32_t seed) {
   dxa_host_free(batch);
 }
 
+static void lz4_checks(uint32_t seed) {
+  for (int64_t n : {0, 1, 12, 13, 100, 5000, 70000}) {
+    std::vector<uint8_t> src((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+      seed = seed * 1664525u + 1013904223u;
+      src[(size_t)i] = (uint8_t)((seed >> 24) % (i % 3 == 0 ? 4 : 200));
+    }
+    for (int32_t bs : {1024, 65536}) {
+      std::vector<uint8_t> f((size_t)dxa_lz4_frame_bound(n, bs));
+      const int64_t m = dxa_lz4_compress_frame(src.data(), n, f.data(), (int64_t)f.size(), bs, 2);
+      CHECK(m > 0);
+      std::vector<uint8_t> out((size_t)n + 1);
+      CHECK(dxa_lz4_decompress_frame(f.data(), m, out.data(), n) == n);
+      CHECK(n == 0 || std::memcmp(out.data(), src.data(), (size_t)n) == 0);
+      for (int64_t cut = 1; cut < m; cut += m / 5 + 1) {            // truncated frames fail cleanly
+        CHECK(dxa_lz4_decompress_frame(f.data(), cut, out.data(), n) < 0);
+      }
+    }
+  }
+  std::vector<uint8_t> junk(4096), out(8192);                        // garbage blocks: errors, never overruns
+  for (int t = 0; t < 200; ++t) {
+    for (auto& b : junk) { seed = seed * 1664525u + 1013904223u; b = (uint8_t)(seed >> 24); }
+    const int64_t r = dxa_lz4_decompress_block(junk.data(), (int64_t)(seed % 4096), out.data(), (int64_t)out.size());
+    CHECK(r >= -1 && r <= (int64_t)out.size());
+  }
+}
+
 int main() {
   CHECK(dxa_crc32c((const uint8_t*)"123456789", 9) == 0xE3069283u);
   CHECK(dxa_crc32c((const uint8_t*)"", 0) == 0u);
-  for (int n : {0, 1, 2, 17, 200}) kafka_roundtrip(n, 7u + n);
+  for (int codec : {0, 1, 3})
+    for (int n : {0, 1, 2, 17, 200}) kafka_roundtrip(n, 7u + n, codec);
+  lz4_checks(99u);
   char buf[64];
   // (subnormal extremes such as Double.MIN_VALUE are not checked: Java pads to two digits there — "4.9E-324" —
   // while the shortest-digit formatter prints "5.0E-324")

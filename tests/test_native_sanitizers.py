@@ -1,5 +1,5 @@
 """Host-side native code under AddressSanitizer + UndefinedBehaviorSanitizer (GPU sanitizers are not available on
-this platform): the Kafka codec and the row serializer are compiled together with a self-check driver and
+this platform): the Kafka codec, the LZ4 codec and the row serializer are compiled together with a self-check driver and
 run as a standalone executable."""
 import os
 import shutil
@@ -16,7 +16,7 @@ def test_host_codecs_under_asan_ubsan(tmp_path):
     exe = str(tmp_path / "host_codecs_check")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-I", CSRC, os.path.join(ROOT, "tests", "native", "host_codecs_check.cpp"),
-           os.path.join(CSRC, "host_kafka.cpp"), os.path.join(CSRC, "host_serialize.cpp"), "-lz", "-pthread", "-o", exe]
+           os.path.join(CSRC, "host_kafka.cpp"), os.path.join(CSRC, "host_lz4.cpp"), os.path.join(CSRC, "host_serialize.cpp"), "-lz", "-pthread", "-o", exe]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
