@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--events-per-batch", type=int, default=None, help="events per GPU per micro-batch")
     ap.add_argument("--ref-rows", type=int, default=100_000_000, help="reference table rows (join flow)")
     ap.add_argument("--pool", type=int, default=3, help="distinct pre-generated batches cycled (pinned source)")
+    ap.add_argument("--lz4-chunks", type=int, default=4, help="pinned-lz4: copy/decode pipeline depth per batch")
     ap.add_argument("--source", choices=["pinned", "pinned-lz4", "device", "gpu-sim"], default=None,
                     help="pinned: H2D copy of raw bytes every step; pinned-lz4: H2D copy of an LZ4 frame of JSON "
                          "lines, decoded + newline-framed on the GPU; device: bytes already in HBM; gpu-sim: GPU "
@@ -154,6 +155,8 @@ def main():
     gen_s = time.perf_counter() - t_gen
 
     side = torch.cuda.Stream(device) if (on_gpu and source in ("pinned", "pinned-lz4", "gpu-sim")) else None
+    ingest = lz4.ChunkedIngest(device, chunks=args.lz4_chunks, copy_stream=side) \
+        if (on_gpu and source == "pinned-lz4") else None
     staged = {}
     sizes = []
 
@@ -180,12 +183,13 @@ def main():
                 staged[i] = (raw, frame_lines_gpu(raw, fr.content_size, expected=E) if on_gpu else
                              _cpu_lines(raw, fr.content_size), None)
                 return
-            with torch.cuda.stream(side):
-                dfr = fr.to(device, non_blocking=True)
-                raw = lz4.decompress_device(dfr)
+            # chunked: chunk k's H2D copy overlaps chunk k-1's decode (copy and decode streams)
+            raw, _ = ingest.stage(fr)
+            ds = ingest.decode_stream
+            with torch.cuda.stream(ds):
                 offs = frame_lines_gpu(raw, fr.content_size, expected=E)
                 ev = torch.cuda.Event()
-                ev.record(side)
+                ev.record(ds)
             staged[i] = (raw, offs, ev)
             return
         hb, ho = pool[i % len(pool)]
@@ -200,6 +204,7 @@ def main():
         staged[i] = (db, do, ev)
 
     lat = []
+    host_trace = [] if os.environ.get("DXA_BENCH_HOST_TRACE") else None
     proc.on_batch_complete = lambda bt, m: lat.append(m["Latency-Process"])
 
     def step(i):
@@ -209,8 +214,12 @@ def main():
             cur.wait_event(ev)
             db.record_stream(cur)
             do.record_stream(cur)
+        t_s = time.perf_counter()
         stage(i + 1)
+        t_p = time.perf_counter()
         m = proc.process_batch(RawBatch(db, do, E), batch_time(i), interval_us)
+        if host_trace is not None:
+            host_trace.append((i, round((t_p - t_s) * 1e3, 2), round((time.perf_counter() - t_p) * 1e3, 2)))
         sizes.append(db.shape[0])
         return m
 
@@ -296,6 +305,8 @@ def main():
     if comp_bytes:
         out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)
         out["config"]["lz4_ratio"] = round((sum(sizes) / len(sizes) - 16) / (sum(comp_bytes) / len(comp_bytes)), 2)
+    if host_trace is not None:
+        out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
     if last:
         out["last_batch_outputs"] = {k: v for k, v in last.items() if k.startswith("Output_")}
     if flow == "join":

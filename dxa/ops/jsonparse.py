@@ -184,8 +184,8 @@ def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = No
     pos = pos[:total]
     if expected is not None:
         offs = torch.empty(total + 1, dtype=torch.int64, device=dev)
-        offs[0] = 0
-        offs[1:] = pos + 1
+        offs[:1].zero_()            # a kernel: `offs[0] = 0` is a host-synchronous scalar copy on this stack
+        torch.add(pos, 1, out=offs[1:])
         return offs
     ends = torch.cat([pos + 1, torch.tensor([length], dtype=torch.int64, device=dev)])
     starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos + 1])

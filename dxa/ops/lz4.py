@@ -1,7 +1,7 @@
 """LZ4 frames: host codec (``host_lz4.cpp``) and the device block decoder (``lz4.hip``).
 
 Compressed ingest: a batch of newline-delimited events travels host → HBM as an LZ4 frame (≈2.5x fewer PCIe bytes
-for SimulatedData-shaped JSON), is decoded by one lane per 16 KiB block, and framed into records on the device.
+for SimulatedData-shaped JSON), is decoded by one wave per 16 KiB block (LDS-staged), and framed into records on the device.
 The same frames are Kafka's compression codec 3 payload (``io/kafka.py``).
 """
 from __future__ import annotations
@@ -150,7 +150,7 @@ def frame_table(data) -> FrameTable:
 @dataclass
 class DeviceFrame:
     """An LZ4 frame staged for the device: frame bytes + block table (host pinned or already in HBM)."""
-    data: torch.Tensor            # uint8 frame bytes (padded by 16)
+    data: torch.Tensor            # uint8 frame bytes (padded by 32: decoder lanes read ahead of the block end)
     comp_off: torch.Tensor
     comp_len: torch.Tensor
     stored: torch.Tensor
@@ -158,11 +158,12 @@ class DeviceFrame:
     out_len: Optional[torch.Tensor]
     content_size: int
     max_block: int
+    max_out: int = -1             # largest decompressed block when out_len is known (sizes the LDS staging)
 
     @staticmethod
     def from_frame(frame: np.ndarray, block_size: Optional[int] = DEFAULT_BLOCK, pin: bool = False) -> "DeviceFrame":
         t = frame_table(frame)
-        padded = np.zeros(frame.size + 16, dtype=np.uint8)
+        padded = np.zeros(frame.size + 32, dtype=np.uint8)
         padded[:frame.size] = frame
         oo = t.out_offsets(block_size)
 
@@ -170,12 +171,13 @@ class DeviceFrame:
             x = torch.from_numpy(np.ascontiguousarray(x))
             return x.pin_memory() if pin else x
         return DeviceFrame(T(padded), T(t.comp_off), T(t.comp_len), T(t.stored),
-                           T(oo[0]) if oo else None, T(oo[1]) if oo else None, t.content_size, t.max_block)
+                           T(oo[0]) if oo else None, T(oo[1]) if oo else None, t.content_size, t.max_block,
+                           int(oo[1].max()) if oo and oo[1].size else -1)
 
     def to(self, device, non_blocking: bool = True) -> "DeviceFrame":
         f = lambda x: None if x is None else x.to(device, non_blocking=non_blocking)  # noqa: E731
         return DeviceFrame(f(self.data), f(self.comp_off), f(self.comp_len), f(self.stored), f(self.out_off),
-                           f(self.out_len), self.content_size, self.max_block)
+                           f(self.out_len), self.content_size, self.max_block, self.max_out)
 
     def tensors(self):
         return [x for x in (self.data, self.comp_off, self.comp_len, self.stored, self.out_off, self.out_len)
@@ -187,7 +189,7 @@ def decompress_device(fr: DeviceFrame, check: bool = False) -> torch.Tensor:
     synchronisation when the block sizes are known (``out_off``); ``check=True`` verifies every block's status."""
     dev = fr.data.device
     if dev.type != "cuda":
-        raw = decompress_frame(fr.data.numpy()[:-16])
+        raw = decompress_frame(fr.data.numpy()[:-32])
         out = torch.zeros(len(raw) + 16, dtype=torch.uint8)
         out[:len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
         return out
@@ -201,14 +203,88 @@ def decompress_device(fr: DeviceFrame, check: bool = False) -> torch.Tensor:
         ln = ln[:nb]
         off = torch.cumsum(ln, 0) - ln
         total = int(ln.sum().item()) if nb else 0
+        max_out = int(ln.max().item()) if nb else 0
         if nb and bool((status[:nb] != 0).any()):
             raise Lz4Error("malformed LZ4 block")
     else:
-        off, ln, total = fr.out_off, fr.out_len, fr.content_size
+        off, ln, total, max_out = fr.out_off, fr.out_len, fr.content_size, fr.max_out
     out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
     out[total:].zero_()
     N.call("dxa_lz4_decode", N.ptr(fr.data), N.ptr(fr.comp_off), N.ptr(fr.comp_len), N.ptr(fr.stored), N.ptr(off),
-           N.ptr(ln), nb, N.ptr(out), N.ptr(status), st)
+           N.ptr(ln), nb, max_out, N.ptr(out), N.ptr(status), st)
     if check and nb and bool((status[:nb] != 0).any()):
         raise Lz4Error(f"LZ4 block decode failed: status {status[:nb].unique().tolist()}")
     return out
+
+
+class ChunkedIngest:
+    """Pipelined compressed ingest of a pinned host frame: the frame is cut into ``chunks`` runs of whole blocks;
+    chunk k's H2D copy (copy stream) overlaps chunk k-1's decode (decode stream), so the critical path is about
+    max(copy, decode) instead of copy + decode.  Blocks read up to 32 bytes past their end, which may land in the
+    next chunk while its copy is still in flight — the decoder never uses those bytes.
+
+    ``stage(frame)`` returns ``(raw, done_event)``: ``raw`` is the decompressed batch (+16 zero bytes) on the
+    device, valid on any stream that waits on ``done_event``."""
+
+    def __init__(self, device, chunks: int = 8, copy_stream=None, decode_stream=None):
+        # HIP multiplexes streams onto GPU_MAX_HW_QUEUES (4) hardware queues: callers that already own a copy
+        # stream should pass it, so the pipeline adds one stream, not two
+        self.device = device
+        self.chunks = max(1, chunks)
+        self.copy_stream = copy_stream or torch.cuda.Stream(device)
+        self.decode_stream = decode_stream or torch.cuda.Stream(device)
+
+    def stage(self, fr: "DeviceFrame"):
+        dev = self.device
+        if fr.out_off is None:
+            raise Lz4Error("chunked ingest needs frames with known block sizes")
+        nb = int(fr.comp_off.shape[0])
+        total = fr.content_size
+        # Allocation streams: `out`/`status` belong to the decode stream (consumers on other streams must
+        # record_stream `out`); the compressed staging buffer belongs to the copy stream that fills it and is
+        # recorded on the decode stream, so it is not recycled while a decode still reads it.
+        with torch.cuda.stream(self.decode_stream):
+            out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+            status = torch.empty(max(nb, 1), dtype=torch.int32, device=dev)
+        with torch.cuda.stream(self.copy_stream):
+            ddata = torch.empty(fr.data.shape[0], dtype=torch.uint8, device=dev)
+        with torch.cuda.stream(self.copy_stream):
+            # block tables are small: one copy up front
+            tabs = [x.to(dev, non_blocking=True) for x in (fr.comp_off, fr.comp_len, fr.stored, fr.out_off,
+                                                           fr.out_len)]
+            tab_ev = torch.cuda.Event()
+            tab_ev.record(self.copy_stream)
+        comp_off_h = fr.comp_off.numpy() if fr.comp_off.device.type == "cpu" else fr.comp_off.cpu().numpy()
+        bounds = np.linspace(0, nb, self.chunks + 1).astype(np.int64)
+        nbytes = int(fr.data.shape[0])
+        st = self.decode_stream.cuda_stream
+        self.decode_stream.wait_event(tab_ev)
+        with torch.cuda.stream(self.decode_stream):
+            out[total:].zero_()
+        for k in range(self.chunks):
+            b0, b1 = int(bounds[k]), int(bounds[k + 1])
+            if b1 <= b0:
+                continue
+            lo = 0 if k == 0 else int(comp_off_h[b0])
+            hi = nbytes if b1 == nb else int(comp_off_h[b1])
+            if fr.data.device.type == "cpu":
+                if not fr.data.is_pinned():
+                    raise Lz4Error("chunked ingest needs a pinned host frame")
+                N.call("dxa_memcpy_h2d_async", ddata.data_ptr() + lo, fr.data.data_ptr() + lo, hi - lo,
+                       self.copy_stream.cuda_stream)
+            else:
+                with torch.cuda.stream(self.copy_stream):
+                    ddata[lo:hi].copy_(fr.data[lo:hi], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+            self.decode_stream.wait_event(ev)
+            co, cl, sd, oo, ol = tabs
+            N.call("dxa_lz4_decode", N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
+                   N.ptr(oo[b0:b1]), N.ptr(ol[b0:b1]), b1 - b0, fr.max_out, N.ptr(out), N.ptr(status[b0:b1]), st)
+        done = torch.cuda.Event()
+        done.record(self.decode_stream)
+        for t in (ddata, *tabs):
+            t.record_stream(self.decode_stream)
+        # the host frame must outlive its async copies
+        self._inflight = [(e, f) for e, f in getattr(self, "_inflight", []) if not e.query()] + [(done, fr)]
+        return out, done

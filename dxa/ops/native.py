@@ -28,7 +28,8 @@ c_p = ctypes.c_void_p
 _SIGS = {
     "dxa_byte_map": [c_p, c_p, c_i64, c_p, c_p],
     "dxa_lz4_block_sizes": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
-    "dxa_lz4_decode": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
+    "dxa_lz4_decode": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
+    "dxa_memcpy_h2d_async": [c_p, c_p, c_i64, c_p],
     "dxa_serialize_lengths": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p],
     "dxa_serialize_write": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],

@@ -153,3 +153,53 @@ def test_gpu_newline_framing():
     offs2 = frame_lines_gpu(d, len(blob)).cpu().tolist()
     recs = [blob[offs2[i]:offs2[i + 1]].strip() for i in range(len(offs2) - 1)]
     assert recs == [ln for ln in lines if ln]
+
+
+@pytest.mark.gpu
+def test_gpu_lz4_wave_decoder_edge_cases():
+    """The wave-per-block LDS decoder against the host codec: incompressible literal runs longer than the 512-B
+    register window, RLE runs (offset 1), short periods (offset < 64), long matches, odd block sizes (unaligned
+    16-B flush), and > 64 KiB blocks (per-lane fallback)."""
+    assert torch.cuda.is_available()
+    dev = torch.device("cuda", 0)
+    rnd = random.Random(11)
+    parts = []
+    for i in range(300):
+        k = i % 6
+        if k == 0:
+            parts.append(bytes(rnd.getrandbits(8) for _ in range(rnd.choice([1, 63, 64, 65, 300, 700, 2000]))))
+        elif k == 1:
+            parts.append(bytes([rnd.getrandbits(8)]) * rnd.choice([4, 5, 19, 64, 65, 1000, 5000]))
+        elif k == 2:
+            per = bytes(rnd.getrandbits(8) for _ in range(rnd.choice([2, 3, 7, 31, 63, 64, 65])))
+            parts.append(per * rnd.choice([3, 10, 40]))
+        elif k == 3:
+            parts.append(b'{"deviceId":%d,"temperature":%d.5,"status":"ok"}\n' % (i, i * 7))
+        else:
+            parts.append(parts[rnd.randrange(len(parts))])
+    data = b"".join(parts)
+    for block in (1000, 4096, 16384, 40000, 65536, 131072):
+        f = lz4.compress_frame(data, block)
+        for known in (block, None):
+            fr = lz4.DeviceFrame.from_frame(f, known).to(dev)
+            out = lz4.decompress_device(fr, check=True)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            assert got[:len(data)].tobytes() == data, (block, known)
+            assert not got[len(data):].any()
+
+
+@pytest.mark.gpu
+def test_gpu_lz4_chunked_ingest():
+    """Pinned host frame → chunked H2D copy / decode pipeline equals the host codec's output."""
+    assert torch.cuda.is_available()
+    dev = torch.device("cuda", 0)
+    data = b"".join(_samples(3)) * 4
+    f = lz4.compress_frame(data, 4096)
+    fr = lz4.DeviceFrame.from_frame(f, 4096, pin=True)
+    for chunks in (1, 3, 8):
+        ing = lz4.ChunkedIngest(dev, chunks=chunks)
+        out, ev = ing.stage(fr)
+        torch.cuda.current_stream(dev).wait_event(ev)
+        got = out.cpu().numpy()
+        assert got[:len(data)].tobytes() == data and not got[len(data):].any()
