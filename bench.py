@@ -12,9 +12,11 @@ one process per MI355X (BASELINE.json metric "events/sec (node) + p99 latency").
 * ``full``    — codegen'd rules + windowed SQL with a device UDF + reference join + accumulator state (config 5);
 * ``passthrough`` — tag rules on every event and every event written as JSON (config 1's shape at full rate).
 
-Each step is a complete micro-batch exactly as the streaming host runs it.  Sources: ``pinned`` — the batch's raw
-JSON bytes are copied from pinned host memory into HBM every step (events arrive from the network into host memory;
-default for groupby/join); ``gpu-sim`` — the SimulatedData generator renders the next batch on the GPU with event
+Each step is a complete micro-batch exactly as the streaming host runs it.  Sources: ``pinned-lz4`` (default for
+groupby/join/passthrough) — each batch arrives in pinned host memory as an LZ4 frame of newline-delimited JSON events
+(the payload format of an LZ4-compressed Kafka record batch; compressed by the producer, outside the step) and every
+step copies the compressed bytes into HBM, decompresses them on the GPU, frames the records and processes them;
+``pinned`` — the raw JSON bytes are copied into HBM every step (≈2.4x more PCIe bytes); ``gpu-sim`` — the SimulatedData generator renders the next batch on the GPU with event
 times inside that batch's second (needed by the windowed flows, whose windows must see advancing event time; its
 cost is inside the timed step).  Batch times advance one interval per step on a simulated clock.
 With N>1 ranks, per-GPU work is fixed (weak scaling); GROUP BYs are two-phase over RCCL.
@@ -37,8 +39,8 @@ sys.path.insert(0, ROOT)
 DEFAULT_EVENTS = {"groupby": 2_000_000, "window": 1_000_000, "join": 2_000_000, "full": 1_000_000,
                   "passthrough": 1_000_000}
 DEFAULT_WARMUP = {"groupby": 5, "window": 305, "join": 3, "full": 305, "passthrough": 3}
-DEFAULT_SOURCE = {"groupby": "pinned", "window": "gpu-sim", "join": "pinned", "full": "gpu-sim",
-                  "passthrough": "pinned"}
+DEFAULT_SOURCE = {"groupby": "pinned-lz4", "window": "gpu-sim", "join": "pinned-lz4", "full": "gpu-sim",
+                  "passthrough": "pinned-lz4"}
 MODEL = {
     "groupby": "SimulatedData IoT flow: 32-col JSON parse + projection + GROUP BY (deviceId, deviceType, homeId) "
                "9 aggregates + alert view + JSON outputs",
@@ -290,7 +292,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp64/int64 columns (no reduced precision)",
-        "data": "synthetic (SimulatedData-schema JSON generated on device, random seeds per rank/batch)",
+        "data": "synthetic (SimulatedData-schema JSON generated on device, random seeds per rank/batch"
+                + ("; delivered as LZ4-framed batches in pinned host memory, decompressed on the GPU in every step)"
+                   if source == "pinned-lz4" else ")"),
         "config": {"model": MODEL[flow].format(ref=args.ref_rows), "flow": flow,
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
                    "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,

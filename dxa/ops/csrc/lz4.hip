@@ -341,21 +341,21 @@ __global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t
   if (lane == 0) status[b] = rc;
 }
 
-// ---- G lanes per block, output straight to HBM ------------------------------------------------------------
+// ---- 16 lanes per block, output straight to HBM -----------------------------------------------------------
 // Bench blocks have ~1400 sequences of ~1.7 literal + ~10 match bytes, so neither 64-wide copies nor a
 // wave-uniform (scalar-unit) parser pays: the per-CU scalar unit serialises every wave's header chain.  Here a
-// group of G lanes owns one block and keeps its sequence state in VGPRs, so one VALU instruction advances 64/G
+// group of 16 lanes owns one block and keeps its sequence state in VGPRs, so one VALU instruction advances four
 // blocks, and with no LDS per block every block of a batch can be resident at once (latency hidden by
-// occupancy instead of by a window).  Per sequence:
-//   * the group loads G consecutive input bytes (lane k: byte p+k) and pulls header bytes out with ds_bpermute;
-//     the next token usually sits in the same load (a sequence is ~5 compressed bytes);
-//   * literals: lane k stores byte k (from the loaded bytes when they fit, else a direct load);
-//   * match: lane k copies out[s0 + (i mod off)] -> out[op + i], G bytes per step.  Sources precede op; a
-//     `s_waitcnt vmcnt(0)` before the copy makes every earlier store visible (a CU's lanes share one L1, so a
-//     same-wave hand-off needs no cache maintenance).  `done` tracks the output prefix known complete at the
-//     last such wait, so the wait is only taken when a source reaches past it — about once per `off` bytes
-//     (~600 B, a record) for JSON, not once per sequence.
-template <int G>
+// occupancy).
+//   * Input window: lane k of the group holds dword k of a 64-byte window (one coalesced dword load per lane,
+//     refilled every ~10 sequences); a byte at window offset r is ds_bpermute(lane r/4) >> 8*(r%4).
+//   * Fast path (lit < 15, match code < 15, header + literals inside the window — nearly every JSON sequence):
+//     straight-line code — token, per-lane literal byte and the 2 offset bytes from the window, then a
+//     <= 18-byte match copy as two 16-lane steps.  Anything else takes the general path.
+//   * Match sources precede op; a `s_waitcnt vmcnt(0)` before the copy makes earlier stores visible (a CU's
+//     lanes share one L1, so a same-wave hand-off needs no cache maintenance).  `done` tracks the output prefix
+//     known complete at the last such wait, so the wait is only taken when a source reaches past it — about
+//     once per `off` bytes (~600 B, one record) for JSON.
 __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __restrict__ src,
                                                                const int64_t* __restrict__ comp_off,
                                                                const int32_t* __restrict__ comp_len,
@@ -364,10 +364,10 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
                                                                const int64_t* __restrict__ out_len, int64_t nb,
                                                                uint8_t* __restrict__ dst,
                                                                int32_t* __restrict__ status) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t b = t / G;
+  constexpr int G = 16;
+  const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const int gl = (int)(threadIdx.x & (G - 1));
-  const int gbase4 = (int)((threadIdx.x & 63) & ~(G - 1)) << 2;      // ds_bpermute byte address of lane 0
+  const int gbase = (int)((threadIdx.x & 63) & ~(G - 1));             // group's first lane in the wave
   if (b >= nb) return;                                                 // whole groups exit together
   const int32_t n = comp_len[b];
   const int64_t cap64 = out_len[b];
@@ -383,56 +383,91 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     return;
   }
   const int32_t cap = (int32_t)cap64;
-  // frames carry >= 16 readable bytes past any block; lanes >= 16 read garbage they never use (G = 32 reads
-  // up to 31 past the block: the device frame is padded by 32)
-  int32_t xb = 0;                                                      // input position of lane 0's byte
-  uint32_t x = in[gl];
-  auto get = [&](int32_t p) -> uint32_t {                              // group-uniform p
-    if (p - xb >= G) {
-      xb = p;
-      x = in[p + gl];
-    }
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(gbase4 + ((p - xb) << 2), (int)x) & 0xffu;
+  // positions are counted from a0 = `in` rounded down to 4 B; frames carry >= 16 readable bytes past a block
+  const int32_t shift = (int32_t)(reinterpret_cast<uintptr_t>(in) & 3);
+  const uint8_t* a0 = in - shift;
+  const int32_t lim = shift + n + 16;
+  auto ld = [&](int32_t w0) -> uint32_t {
+    const int32_t q = w0 + 4 * gl;
+    return (q + 4 <= lim) ? *reinterpret_cast<const uint32_t*>(a0 + q) : 0u;
   };
-  int32_t ip = 0, op = 0, rc = LZ_OK, done = 0;
-  while (ip < n) {
-    const uint32_t token = get(ip);
-    ++ip;
+  auto wbyte = [&](uint32_t X, int32_t r) -> uint32_t {               // window byte r (per-lane r allowed)
+    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((gbase + ((r >> 2) & (G - 1))) << 2, (int)X);
+    return (v >> ((r & 3) * 8)) & 0xffu;
+  };
+  int32_t xb = 0;
+  uint32_t X = ld(0);
+  auto get = [&](int32_t p) -> uint32_t {                              // general path: byte at position p
+    if (p - xb >= 4 * G) {
+      xb = p & ~3;
+      X = ld(xb);
+    }
+    return wbyte(X, p - xb);
+  };
+  const int32_t iend = shift + n;
+  int32_t ip = shift, op = 0, rc = LZ_OK, done = 0;
+  while (ip < iend) {
+    if (ip - xb > 4 * G - 16) {                                       // keep >= 16 bytes of lookahead
+      xb = ip & ~3;
+      X = ld(xb);
+    }
+    const int32_t r = ip - xb;
+    const uint32_t token = wbyte(X, r);
     int32_t lit = (int32_t)(token >> 4);
+    const int32_t mlc = (int32_t)(token & 15);
+    if (lit < 15 && mlc < 15 && r + lit + 3 <= 4 * G && iend - ip >= lit + 3 && cap - op >= lit + mlc + 4) {
+      // ---- fast path
+      const uint32_t lv = wbyte(X, r + 1 + gl);
+      const int32_t off = (int32_t)(wbyte(X, r + 1 + lit) | (wbyte(X, r + 2 + lit) << 8));
+      if (gl < lit) out[op + gl] = (uint8_t)lv;
+      ip += lit + 3;
+      op += lit;
+      if (off == 0 || off > op) { rc = LZ_OFFSET; break; }
+      const int32_t ml = mlc + 4;
+      const int32_t s0 = op - off;
+      if (s0 + (off < ml ? off : ml) > done) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        done = op;
+      }
+      if (off >= ml) {
+        if (gl < ml) out[op + gl] = out[s0 + gl];
+        if (gl + G < ml) out[op + G + gl] = out[s0 + G + gl];
+      } else {
+        const uint32_t o = (uint32_t)off;
+        if (gl < ml) out[op + gl] = out[s0 + (int32_t)((uint32_t)gl % o)];
+        if (gl + G < ml) out[op + G + gl] = out[s0 + (int32_t)((uint32_t)(gl + G) % o)];
+      }
+      op += ml;
+      continue;
+    }
+    // ---- general path
+    ++ip;
     if (lit == 15) {
       uint32_t e;
       do {
-        if (ip >= n) { rc = LZ_TRUNC; break; }
+        if (ip >= iend) { rc = LZ_TRUNC; break; }
         e = get(ip);
         ++ip;
         lit += (int32_t)e;
       } while (e == 255);
       if (rc != LZ_OK) break;
     }
-    if (lit > n - ip) { rc = LZ_TRUNC; break; }
+    if (lit > iend - ip) { rc = LZ_TRUNC; break; }
     if (lit > cap - op) { rc = LZ_OVERFLOW; break; }
-    if (lit > 0) {
-      if (ip - xb + lit <= G) {                                        // literals already loaded
-        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(gbase4 + ((ip - xb + gl) & (G - 1)) * 4,
-                                                                  (int)x);
-        if (gl < lit) out[op + gl] = (uint8_t)v;
-      } else {
-        for (int32_t c = 0; c < lit; c += G)
-          if (c + gl < lit) out[op + c + gl] = in[ip + c + gl];
-      }
-    }
+    for (int32_t c = 0; c < lit; c += G)
+      if (c + gl < lit) out[op + c + gl] = a0[ip + c + gl];
     ip += lit;
     op += lit;
-    if (ip >= n) break;                                                // last sequence: literals only
-    if (n - ip < 2) { rc = LZ_TRUNC; break; }
+    if (ip >= iend) break;                                             // last sequence: literals only
+    if (iend - ip < 2) { rc = LZ_TRUNC; break; }
     const int32_t off = (int32_t)(get(ip) | (get(ip + 1) << 8));
     ip += 2;
     if (off == 0 || off > op) { rc = LZ_OFFSET; break; }
-    int32_t ml = (int32_t)(token & 15);
+    int32_t ml = mlc;
     if (ml == 15) {
       uint32_t e;
       do {
-        if (ip >= n) { rc = LZ_TRUNC; break; }
+        if (ip >= iend) { rc = LZ_TRUNC; break; }
         e = get(ip);
         ++ip;
         ml += (int32_t)e;
@@ -442,8 +477,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     ml += 4;
     if (ml > cap - op) { rc = LZ_OVERFLOW; break; }
     const int32_t s0 = op - off;
-    const int32_t span = off < ml ? off : ml;                          // sources: [s0, s0 + span)
-    if (s0 + span > done) {
+    if (s0 + (off < ml ? off : ml) > done) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       done = op;
     }
@@ -478,12 +512,12 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
                            void* status, void* st) {
   if (nb <= 0) return 0;
   const hipStream_t s = (hipStream_t)st;
-  // DXA_LZ4_LANES selects the decoder for measurements: 16 (default) or 8 lanes per block, 64 = one wave per
-  // block with LDS-staged output, 1 = one lane per block
+  // DXA_LZ4_LANES selects the decoder for measurements: 16 lanes per block (default), 64 = one wave per block
+  // with LDS-staged output, 1 = one lane per block
   static const int lanes = [] {
     const char* e = getenv("DXA_LZ4_LANES");
     const int v = e ? atoi(e) : 16;
-    return (v == 1 || v == 8 || v == 16 || v == 32 || v == 64) ? v : 16;
+    return (v == 1 || v == 16 || v == 64) ? v : 16;
   }();
   const uint8_t* s8 = (const uint8_t*)src;
   const int64_t* co = (const int64_t*)comp_off;
@@ -491,18 +525,10 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
   const uint8_t* sd = (const uint8_t*)stored;
   const int64_t* oo = (const int64_t*)out_off;
   const int64_t* ol = (const int64_t*)out_len;
-  if (lanes == 16 || lanes == 8 || lanes == 32) {
-    const int64_t threads = nb * lanes;
-    const dim3 grid((unsigned)((threads + 255) / 256));
-    if (lanes == 32)
-      hipLaunchKernelGGL(lz4_decode_group_kernel<32>, grid, dim3(256), 0, s, s8, co, cl, sd, oo, ol, nb,
-                         (uint8_t*)dst, (int32_t*)status);
-    else if (lanes == 16)
-      hipLaunchKernelGGL(lz4_decode_group_kernel<16>, grid, dim3(256), 0, s, s8, co, cl, sd, oo, ol, nb,
-                         (uint8_t*)dst, (int32_t*)status);
-    else
-      hipLaunchKernelGGL(lz4_decode_group_kernel<8>, grid, dim3(256), 0, s, s8, co, cl, sd, oo, ol, nb,
-                         (uint8_t*)dst, (int32_t*)status);
+  if (lanes == 16) {
+    const int64_t threads = nb * 16;
+    hipLaunchKernelGGL(lz4_decode_group_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8, co, cl,
+                       sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status);
     return (int)hipGetLastError();
   }
   const int64_t lb = (max_out + 15) & ~(int64_t)15;         // LDS bytes per wave (16-B aligned slices)
