@@ -19,6 +19,7 @@ import torch
 
 from ..sql import ast as A
 from . import functions as F
+from . import jit as _jit_mod
 from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn,
                      TORCH_DTYPE, and_valid, column_from_pylist, concat_columns, materialize, strings_from_pylist)
 from .types import (ArrayType, MapType, StructType, common_type, is_integral, is_nested, is_numeric)
@@ -219,13 +220,18 @@ def _coerce_const_for(col_other: Column, const: ConstColumn) -> ConstColumn:
 # evaluator
 # ---------------------------------------------------------------------------------------------------------------
 
-def evaluate(e: A.Expr, scope: Scope, ctx: EvalContext, subst: Optional[Dict] = None) -> Column:
+def evaluate(e: A.Expr, scope: Scope, ctx: EvalContext, subst: Optional[Dict] = None, _jit: bool = True) -> Column:
     """Evaluate ``e`` over every row of ``scope``.  ``subst`` maps expression keys to precomputed columns
-    (aggregate results)."""
+    (aggregate results).  Scalar operator trees over large device batches run as one generated kernel
+    (``jit.py``); ``_jit=False`` evaluates this node with tensor ops (its children may still fuse)."""
     if subst:
         k = e.key()
         if k in subst:
             return subst[k]
+    if _jit and _jit_mod.eligible(e, scope):
+        r = _jit_mod.try_fused(e, scope, ctx, subst, evaluate)
+        if r is not None:
+            return r
     n, dev = scope.length, scope.device
     if isinstance(e, A.Literal):
         t = e.type
@@ -377,11 +383,18 @@ def _arith(op: str, a: Column, b: Column, n, dev) -> Column:
         yt = y if torch.is_tensor(y) else torch.full((n,), y, device=dev,
                                                      dtype=torch.float64 if st == "double" else torch.int64)
         zero = yt == 0
-        ys = torch.where(zero, torch.ones_like(yt), yt)
+        # integer x % -1 / x div -1 are computed without dividing (INT64_MIN / -1 traps on the host)
+        neg1 = (yt == -1) if yt.dtype == torch.int64 else None
+        bad = zero if neg1 is None else zero | neg1
+        ys = torch.where(bad, torch.ones_like(yt), yt)
         if op == "%":
             r = torch.fmod(xt, ys)
+            if neg1 is not None:
+                r = torch.where(neg1, torch.zeros_like(r), r)
         else:
             r = torch.div(xt, ys, rounding_mode="trunc").to(torch.int64)
+            if neg1 is not None:
+                r = torch.where(neg1, -xt, r)
             rt = "long"
         if bool(zero.any()):
             valid = and_valid(valid, ~zero)

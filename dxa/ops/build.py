@@ -62,7 +62,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(compile_one, hip_srcs))
-    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(LIB)])
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-lhiprtc", "-o", str(LIB)])
     if host_srcs:
         _run(["g++", *HOST_FLAGS, "-shared", *map(str, host_srcs), "-I", str(CSRC), "-lz", "-o", str(HOST_LIB)])
     for o in objs:
