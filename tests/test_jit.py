@@ -130,7 +130,11 @@ def test_gpu_fused_kernels_match_evaluator():
     for i, sql in enumerate(EXPRS):
         scope = _table(n if i % 2 else 70_000, i, dev)
         e = parse_expression(sql)
-        want = evaluate(e, scope, ctx, _jit=False)
+        jit.ENABLED = False
+        try:
+            want = evaluate(e, scope, ctx)                 # tensor evaluator only
+        finally:
+            jit.ENABLED = True
         got = evaluate(e, scope, ctx)                      # JIT hook (eligible: cuda, >= 64K rows)
         assert _norm(got, scope.length) == _norm(want, scope.length), sql
     assert jit.STATS["fused"] - before >= 12               # the hipRTC path actually ran

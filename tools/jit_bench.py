@@ -49,12 +49,12 @@ def main():
         e = parse_expression(sql)
         res = {}
         for mode in ("off", "on"):
-            use = mode == "on"
-            evaluate(e, scope, ctx, _jit=use)
+            jit.ENABLED = mode == "on"
+            evaluate(e, scope, ctx)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.reps):
-                evaluate(e, scope, ctx, _jit=use)
+                evaluate(e, scope, ctx)
             torch.cuda.synchronize()
             res[mode] = (time.perf_counter() - t0) / a.reps * 1e3
         print(json.dumps({"expr": sql, "rows": n, "tensor_ms": round(res["off"], 3), "fused_ms": round(res["on"], 3),
