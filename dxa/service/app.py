@@ -334,6 +334,10 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         from .web import INDEX_HTML
         return INDEX_HTML
 
+    # node-side Livy-compatible batch API (remote job submission: job_clients.LivyClient)
+    from .job_clients import batch_routes
+    batch_routes(app, st.jobs)
+
     @app.get("/api/health")
     def health():
         return ok({"time": time.time()})

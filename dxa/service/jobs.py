@@ -3,7 +3,9 @@ LocalSparkClient: Services/DataX.Config/DataX.Config/InternalService/SparkJobOpe
 DataX.Config.Local/LocalSparkClient.cs:20-206).
 
 A job runs as ``python -m dxa.app conf=<job.conf>`` — or, for ``gpus > 1``, under ``torch.distributed.run`` with one
-rank per MI355X.  Liveness = PID alive AND its recorded start time matches (PID reuse safe).  States follow the
+rank per MI355X.  A job with a ``client`` field (``{"type": "livy" | "databricks", "connectionString": …}``) runs
+remotely instead: it is submitted through ``job_clients`` (e.g. to another node's Livy-compatible ``/batches``
+endpoint) and its state is synced from there.  Liveness = PID alive AND its recorded start time matches (PID reuse safe).  States follow the
 reference: Idle → Starting → Running → Success / Error; ``start`` first ensures the job is not running (polling up
 to 30 × 1 s), ``restart_all_with_retries`` retries failed starts.
 """
@@ -76,10 +78,33 @@ class JobManager:
                     "--master-addr", "127.0.0.1", "--master-port", str(job.get("port", 29600)), "-m", "dxa.app"] + args
         return [self.python, "-m", "dxa.app"] + args
 
+    def _remote(self, job):
+        spec = job.get("client")
+        if not spec:
+            return None
+        from .job_clients import make_client
+        return make_client(spec, getattr(self, "http", None))
+
+    def _remote_job_data(self, job) -> Dict[str, Any]:
+        if job.get("jobData"):
+            return job["jobData"]
+        args = [f"conf={job['confPath']}"] + [f"{k}={v}" for k, v in (job.get("args") or {}).items()]
+        return {"name": job["name"], "file": "dxa.app", "args": args, "conf": {"gpus": int(job.get("gpus", 1))}}
+
     def start(self, name: str, ensure_stopped_retries: int = 30) -> Dict[str, Any]:
         job = self.store.get(_COLL, name)
         if job is None:
             raise KeyError(f"job {name} not found")
+        client = self._remote(job)
+        if client is not None:
+            job = self._sync(job)
+            if job["state"] in (STARTING, RUNNING):
+                raise RuntimeError(f"job {name} is still {job['state']}")
+            res = client.submit(self._remote_job_data(job))
+            job.update(state=res.state if res.state != IDLE else STARTING, clientCache=res.client_cache,
+                       remoteId=res.job_id, links=res.links, note=res.note, startedAt=time.time())
+            self.store.upsert(_COLL, name, job)
+            return job
         for _ in range(ensure_stopped_retries):
             job = self._sync(job)
             if job["state"] in (IDLE, SUCCESS, ERROR):
@@ -107,6 +132,14 @@ class JobManager:
         job = self.store.get(_COLL, name)
         if job is None:
             return None
+        client = self._remote(job)
+        if client is not None:
+            if job.get("clientCache"):
+                res = client.stop(job["clientCache"])
+                job.update(note=res.note)
+            job.update(state=IDLE)
+            self.store.upsert(_COLL, name, job)
+            return job
         pid = job.get("pid")
         if pid and self._alive(job):
             try:
@@ -173,6 +206,16 @@ class JobManager:
 
     def _sync(self, job: Dict[str, Any]) -> Dict[str, Any]:
         name = job["name"]
+        client = self._remote(job)
+        if client is not None:
+            if job.get("clientCache") and job.get("state") in (STARTING, RUNNING):
+                res = client.get(job["clientCache"])
+                if res.state != job.get("state"):
+                    job.update(state=res.state, note=res.note)
+                    if res.client_cache is not None:
+                        job["clientCache"] = res.client_cache
+                    self.store.upsert(_COLL, name, job)
+            return job
         rc = self._reap(name)
         state = job.get("state", IDLE)
         if state in (STARTING, RUNNING):
