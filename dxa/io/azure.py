@@ -309,6 +309,53 @@ class CosmosClient:
         _request("POST", f"{self.endpoint}/{link}/docs", json.dumps(doc).encode(), hdrs, self.timeout)
 
 
+    # -- reads / deletes (design-time document store: dxa/service/store.py CosmosDocumentStore) -------------------
+    def _hdrs(self, verb: str, rtype: str, link: str, partition: Optional[str] = None) -> Dict[str, str]:
+        date = _rfc1123()
+        h = {"Authorization": cosmos_auth(verb, rtype, link, date, self.key), "x-ms-date": date,
+             "x-ms-version": COSMOS_API_VERSION}
+        if partition is not None:
+            h["x-ms-documentdb-partitionkey"] = json.dumps([partition])
+        return h
+
+    def get(self, db: str, coll: str, doc_id: str, partition: Optional[str] = None) -> Optional[Dict]:
+        link = f"dbs/{db}/colls/{coll}/docs/{doc_id}"
+        try:
+            _, _, body = _request("GET", f"{self.endpoint}/{urllib.parse.quote(link)}", None,
+                                  self._hdrs("GET", "docs", link, partition), self.timeout)
+        except AzureError as e:
+            if e.status == 404:
+                return None
+            raise
+        return json.loads(body)
+
+    def delete(self, db: str, coll: str, doc_id: str, partition: Optional[str] = None) -> bool:
+        link = f"dbs/{db}/colls/{coll}/docs/{doc_id}"
+        try:
+            _request("DELETE", f"{self.endpoint}/{urllib.parse.quote(link)}", None,
+                     self._hdrs("DELETE", "docs", link, partition), self.timeout)
+        except AzureError as e:
+            if e.status == 404:
+                return False
+            raise
+        return True
+
+    def list(self, db: str, coll: str) -> List[Dict]:
+        """All documents of a collection (ReadFeed, following continuation tokens)."""
+        link = f"dbs/{db}/colls/{coll}"
+        out: List[Dict] = []
+        cont = None
+        while True:
+            h = self._hdrs("GET", "docs", link)
+            if cont:
+                h["x-ms-continuation"] = cont
+            _, rh, body = _request("GET", f"{self.endpoint}/{link}/docs", None, h, self.timeout)
+            out.extend(json.loads(body).get("Documents", []))
+            cont = {k.lower(): v for k, v in rh.items()}.get("x-ms-continuation")
+            if not cont:
+                return out
+
+
 def is_cosmos_connection(conn: str) -> bool:
     p = _conn_parts(conn)
     return "accountendpoint" in p and "accountkey" in p

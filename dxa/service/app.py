@@ -55,7 +55,9 @@ class ServiceState:
         self.root = os.path.abspath(root)
         os.makedirs(self.root, exist_ok=True)
         os.environ.setdefault("DXA_SECRETS_DIR", os.path.join(self.root, "secrets"))
-        self.store = DocumentStore(os.path.join(self.root, "local.db"))
+        # DXA_DESIGN_STORE=cosmos:<conn>;Database=<db> shares flows/jobs across control planes; default local SQLite
+        from .store import open_store
+        self.store = open_store(os.environ.get("DXA_DESIGN_STORE") or os.path.join(self.root, "local.db"))
         self.jobs = JobManager(self.store, os.path.join(self.root, "logs"))
         from .jobs import Supervisor
         self.supervisor = Supervisor(self.jobs)

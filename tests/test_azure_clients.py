@@ -88,17 +88,33 @@ def _make_handler(state: _Fake):
                 if (container, blob) not in state.blobs:
                     return self._reply(404)
                 return self._reply(200, state.blobs[(container, blob)][0], "application/octet-stream")
-            if parts[1] == "dbs":                                   # /dbs/<db>/colls/<c>/docs
-                link = "/".join(parts[1:5])
+            if parts[1] == "dbs":                                   # /dbs/<db>/colls/<c>/docs[/<id>]
+                by_id = len(parts) > 6
+                link = urllib.parse.unquote("/".join(parts[1:7] if by_id else parts[1:5]))
                 date = self.headers.get("x-ms-date")
                 want = urllib.parse.quote("type=master&ver=1.0&sig=" + _hmac_b64(
-                    base64.b64decode(KEY), f"post\ndocs\n{link}\n{date.lower()}\n\n"), safe="")
-                if self.headers.get("Authorization") != want or self.headers.get("x-ms-documentdb-is-upsert") != "True":
+                    base64.b64decode(KEY), f"{self.command.lower()}\ndocs\n{link}\n{date.lower()}\n\n"), safe="")
+                if self.headers.get("Authorization") != want or (
+                        self.command == "POST" and self.headers.get("x-ms-documentdb-is-upsert") != "True"):
                     state.errors.append(("cosmos-auth", self.path))
                     return self._reply(401)
-                doc = json.loads(self._body())
-                state.docs[(parts[2], parts[4], doc["id"])] = doc
-                return self._reply(201, b"{}", "application/json")
+                db, coll = parts[2], parts[4]
+                if self.command == "POST":
+                    doc = json.loads(self._body())
+                    state.docs[(db, coll, doc["id"])] = doc
+                    return self._reply(201, b"{}", "application/json")
+                if by_id:
+                    key = (db, coll, urllib.parse.unquote(parts[6]))
+                    if key not in state.docs:
+                        return self._reply(404, b"{}", "application/json")
+                    if self.command == "DELETE":
+                        del state.docs[key]
+                        return self._reply(204)
+                    return self._reply(200, json.dumps({**state.docs[key], "_rid": "x", "_etag": "e"}).encode(),
+                                       "application/json")
+                docs = [d for (d0, c0, _), d in sorted(state.docs.items()) if (d0, c0) == (db, coll)]
+                return self._reply(200, json.dumps({"Documents": docs, "_count": len(docs)}).encode(),
+                                   "application/json")
             if len(parts) == 3 and parts[2] == "messages":            # /<hub>/messages
                 tok = self.headers.get("Authorization", "")
                 fields = dict(kv.split("=", 1) for kv in tok[len("SharedAccessSignature "):].split("&"))
@@ -206,3 +222,20 @@ def test_cosmos_sink_upserts(fake):
     assert not fake.errors
     assert fake.docs[("iot", "devices", "d1")] == {"id": "d1", "t": 2}   # upsert keeps the last write
     assert ("iot", "devices", "d2") in fake.docs
+
+
+def test_cosmos_document_store_round_trip(fake):
+    """The control plane's design-time store over Cosmos DB: flows saved by one control plane are visible to another."""
+    from dxa.service.store import CosmosDocumentStore, open_store
+    conn = f"AccountEndpoint=http://127.0.0.1:{fake.port}/;AccountKey={KEY};"
+    a = open_store(f"cosmos:{conn}Database=dx")
+    assert isinstance(a, CosmosDocumentStore) and a.db == "dx"
+    a.upsert("flows", "iot", {"name": "iot", "gui": {"x": 1}})
+    a.upsert("flows", "home", {"name": "home"})
+    b = CosmosDocumentStore(conn, "dx")
+    assert b.get("flows", "iot") == {"name": "iot", "gui": {"x": 1}}
+    assert [d["name"] for d in b.get_all("flows")] == ["home", "iot"]
+    assert b.get("flows", "nope") is None
+    assert b.delete("flows", "home") and not b.delete("flows", "home")
+    assert [d["name"] for d in a.get_all("flows")] == ["iot"]
+    assert not fake.errors
