@@ -3,7 +3,8 @@ DataProcessing/datax-host/src/main/scala/datax/securedsetting/KeyVaultClient.sca
 
 Resolution order, cached per process: environment variable ``DXA_SECRET_<VAULT>_<SECRET>`` (non-alphanumerics →
 ``_``, upper-case), then the JSON file ``$DXA_SECRETS_FILE`` (``{"vault/secret": "value"}``), then the local
-secret directory ``$DXA_SECRETS_DIR/<vault>/<secret>``.  Unresolvable references raise.
+secret directory ``$DXA_SECRETS_DIR/<vault>/<secret>``, then — for ``keyvault://`` when ``DXA_KEYVAULT_URL`` is
+set — Azure Key Vault over REST (``keyvault.py``: MSI or client-credentials token).  Unresolvable references raise.
 """
 from __future__ import annotations
 
@@ -48,6 +49,14 @@ def resolve(value: Optional[str]) -> Optional[str]:
         p = Path(os.environ.get("DXA_SECRETS_DIR", ".dxa_secrets")) / vault / name
         if p.exists():
             out = p.read_text().strip()
+    if out is None and value.startswith("keyvault://"):
+        from .keyvault import KeyVaultError, default_client
+        kv = default_client()
+        if kv is not None:
+            try:
+                out = kv.get_secret(vault, name)
+            except KeyVaultError as e:
+                raise SecretError(f"cannot resolve secret {value}: {e}") from None
     if out is None:
         raise SecretError(f"cannot resolve secret {value}")
     with _lock:
