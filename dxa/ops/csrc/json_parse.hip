@@ -46,6 +46,8 @@ struct ParseArgs {
   const uint64_t* key_words;    // key texts, zero padded to 8-byte words
 };
 
+__constant__ uint64_t kPow10i[9] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                                    100000000ull};
 __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                   1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
@@ -101,17 +103,40 @@ __device__ __forceinline__ bool key_matches(const uint8_t* buf, int64_t q, int64
   return ((tail ^ want) & mask) == 0;
 }
 
-// Scan a string whose opening quote is at r.p.  On return r.p is past the closing quote.
+// SWAR byte tests on 8 bytes (little-endian: byte 0 = first char): high bit of each byte lane flags the property.
+__device__ __forceinline__ uint64_t swar_eq(uint64_t x, uint64_t pat) {
+  const uint64_t v = x ^ pat;
+  return (v - 0x0101010101010101ull) & ~v & 0x8080808080808080ull;   // exact for the lowest flagged byte
+}
+__device__ __forceinline__ uint64_t swar_nondigit(uint64_t x) {
+  return ((x + 0x4646464646464646ull) | (x - 0x3030303030303030ull)) & 0x8080808080808080ull;
+}
+// Value of the k (1..8) leading digit characters of x (byte 0 = most significant digit): the digits are shifted to
+// the top bytes and the zero bytes below them read as leading '0's of an 8-digit number.
+__device__ __forceinline__ uint64_t swar_digits(uint64_t x, int k) {
+  uint64_t v = (x - 0x3030303030303030ull) << (8 * (8 - k));
+  v = ((v & 0x0F0F0F0F0F0F0F0Full) * 2561) >> 8;
+  v = ((v & 0x00FF00FF00FF00FFull) * 6553601) >> 16;
+  return ((v & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+}
+
+// Scan a string whose opening quote is at r.p.  On return r.p is past the closing quote.  Eight bytes per step:
+// the first quote or backslash is found with SWAR compares (a string of ~10 chars is one or two steps).
 __device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, bool& esc) {
   ++r.p;
   s = r.p;
   esc = false;
   while (r.p < r.end) {
-    const uint32_t c = r.at(r.p);
-    if (c == '"') { e = r.p; ++r.p; return true; }
-    if (c == '\\') { esc = true; r.p += 2; continue; }
-    ++r.p;
+    const uint64_t x = load8(r.buf, r.p);
+    const uint64_t m = swar_eq(x, 0x2222222222222222ull) | swar_eq(x, 0x5C5C5C5C5C5C5C5Cull);
+    if (m == 0) { r.p += 8; continue; }
+    r.p += __builtin_ctzll(m) >> 3;
+    if (r.p >= r.end) break;
+    if (((x >> (8 * ((__builtin_ctzll(m) >> 3)))) & 0xff) == '"') { e = r.p; ++r.p; return true; }
+    esc = true;
+    r.p += 2;                                             // backslash + escaped char
   }
+  r.p = r.end;
   return false;
 }
 
@@ -175,35 +200,66 @@ __device__ int64_t unescape_inplace(Reader& r, int64_t s, int64_t e) {
   return o - s;
 }
 
+// Run of decimal digits at r.p, accumulated into (mant, nd, exp10) exactly as a digit-serial loop would: at most
+// 19 significant digits kept (leading zeros are not significant); integer-part digits beyond that raise exp10 and
+// set `lost`; fraction digits beyond it are dropped.  Eight characters per step (SWAR digit test + conversion).
+__device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, int& exp10, bool& lost, bool frac) {
+  bool any = false;
+  while (r.p < r.end) {
+    const uint64_t x = load8(r.buf, r.p);
+    const uint64_t nm = swar_nondigit(x);
+    int k = nm ? (__builtin_ctzll(nm) >> 3) : 8;
+    if (k > r.end - r.p) k = (int)(r.end - r.p);
+    if (k == 0) break;
+    any = true;
+    const uint64_t chunk = swar_digits(x, k);
+    int sig = k;                                          // significant digits this chunk adds
+    if (mant == 0) {
+      if (chunk == 0) {
+        sig = 0;
+      } else {
+        const uint64_t nz = (x - 0x3030303030303030ull) & ((k == 8) ? ~0ull : ((1ull << (8 * k)) - 1));
+        sig = k - (__builtin_ctzll(nz) >> 3);           // drop leading zero digits
+      }
+    }
+    if (nd + sig <= 19) {
+      mant = mant * kPow10i[k] + chunk;
+      nd += sig;
+      if (frac) exp10 -= k;
+      r.p += k;
+    } else {
+      // the 19-digit boundary falls inside this chunk: finish digit by digit
+      for (int i = 0; i < k; ++i) {
+        const uint32_t c = (uint32_t)((x >> (8 * i)) & 0xff);
+        if (nd < 19) {
+          mant = mant * 10 + (c - '0');
+          if (mant) ++nd;
+          if (frac) --exp10;
+        } else if (!frac) {
+          ++exp10;
+          lost = true;
+        }
+      }
+      r.p += k;
+    }
+    if (k < 8) break;
+  }
+  return any;
+}
+
 // Parse a JSON number at r.p.  Returns false on syntax error.
 __device__ bool scan_number(Reader& r, bool& is_int, bool& overflow, int64_t& iv, double& dv) {
   bool neg = false;
   if (r.cur() == '-') { neg = true; ++r.p; }
   uint64_t mant = 0;
   int nd = 0, exp10 = 0;
-  bool lost = false, any = false;
+  bool lost = false;
   is_int = true;
-  while (r.p < r.end) {
-    const uint32_t c = r.at(r.p);
-    if (!is_digit(c)) break;
-    any = true;
-    if (nd < 19) { mant = mant * 10 + (c - '0'); if (mant) ++nd; }
-    else { ++exp10; lost = true; }
-    ++r.p;
-  }
-  if (!any) return false;
+  if (!scan_digits(r, mant, nd, exp10, lost, false)) return false;
   if (r.p < r.end && r.at(r.p) == '.') {
     is_int = false;
     ++r.p;
-    bool fd = false;
-    while (r.p < r.end) {
-      const uint32_t c = r.at(r.p);
-      if (!is_digit(c)) break;
-      fd = true;
-      if (nd < 19) { mant = mant * 10 + (c - '0'); if (mant) ++nd; --exp10; }
-      ++r.p;
-    }
-    if (!fd) return false;
+    if (!scan_digits(r, mant, nd, exp10, lost, true)) return false;
   }
   if (r.p < r.end && (r.at(r.p) | 0x20u) == 'e') {
     is_int = false;

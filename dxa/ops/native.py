@@ -19,7 +19,7 @@ import torch
 _LIB = None
 _LOCK = threading.Lock()
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "_native" / "libdxa_kernels.so"
+LIB_PATH = Path(os.environ.get("DXA_NATIVE_LIB") or (_HERE / "_native" / "libdxa_kernels.so"))  # override: A/B runs
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
