@@ -353,7 +353,8 @@ __global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t
 //     straight-line code — token, per-lane literal byte and the 2 offset bytes from the window, then a
 //     <= 18-byte match copy as two 16-lane steps.  Anything else takes the general path.
 //   * Match sources precede op; a `s_waitcnt vmcnt(0)` before the copy makes earlier stores visible (a CU's
-//     lanes share one L1, so a same-wave hand-off needs no cache maintenance).  `done` tracks the output prefix
+//     lanes share one L1, so a same-wave hand-off needs no cache maintenance).  Fast-path match bytes are stored
+//     one sequence late (software pipelining), so their load latency overlaps the next header parse.  `done` tracks the output prefix
 //     known complete at the last such wait, so the wait is only taken when a source reaches past it — about
 //     once per `off` bytes (~600 B, one record) for JSON.
 __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __restrict__ src,
@@ -406,6 +407,8 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   };
   const int32_t iend = shift + n;
   int32_t ip = shift, op = 0, rc = LZ_OK, done = 0;
+  int32_t pdst = 0, pml = 0;                                           // pending (loaded, not yet stored) match
+  uint32_t pv0 = 0, pv1 = 0;
   while (ip < iend) {
     if (ip - xb > 4 * G - 16) {                                       // keep >= 16 bytes of lookahead
       xb = ip & ~3;
@@ -416,7 +419,10 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     int32_t lit = (int32_t)(token >> 4);
     const int32_t mlc = (int32_t)(token & 15);
     if (lit < 15 && mlc < 15 && r + lit + 3 <= 4 * G && iend - ip >= lit + 3 && cap - op >= lit + mlc + 4) {
-      // ---- fast path
+      // ---- fast path.  The match copy is software-pipelined: this sequence's match bytes are loaded now and
+      // stored during the next sequence (after that one's loads are issued), so the load latency overlaps the
+      // next header parse instead of stalling the group.  A source that reaches into the still-pending bytes
+      // flushes them first.
       const uint32_t lv = wbyte(X, r + 1 + gl);
       const int32_t off = (int32_t)(wbyte(X, r + 1 + lit) | (wbyte(X, r + 2 + lit) << 8));
       if (gl < lit) out[op + gl] = (uint8_t)lv;
@@ -425,20 +431,40 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       if (off == 0 || off > op) { rc = LZ_OFFSET; break; }
       const int32_t ml = mlc + 4;
       const int32_t s0 = op - off;
-      if (s0 + (off < ml ? off : ml) > done) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        done = op;
+      const int32_t src_end = s0 + (off < ml ? off : ml);
+      if (pml > 0 && src_end > pdst) {                                 // source overlaps the pending bytes
+        if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
+        if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
+        pml = 0;
       }
+      if (src_end > done) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        done = pml > 0 ? pdst : op;
+      }
+      uint32_t v0 = 0, v1 = 0;
       if (off >= ml) {
-        if (gl < ml) out[op + gl] = out[s0 + gl];
-        if (gl + G < ml) out[op + G + gl] = out[s0 + G + gl];
+        if (gl < ml) v0 = out[s0 + gl];
+        if (gl + G < ml) v1 = out[s0 + G + gl];
       } else {
         const uint32_t o = (uint32_t)off;
-        if (gl < ml) out[op + gl] = out[s0 + (int32_t)((uint32_t)gl % o)];
-        if (gl + G < ml) out[op + G + gl] = out[s0 + (int32_t)((uint32_t)(gl + G) % o)];
+        if (gl < ml) v0 = out[s0 + (int32_t)((uint32_t)gl % o)];
+        if (gl + G < ml) v1 = out[s0 + (int32_t)((uint32_t)(gl + G) % o)];
       }
+      if (pml > 0) {                                                   // previous sequence's match bytes
+        if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
+        if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
+      }
+      pdst = op;
+      pml = ml;
+      pv0 = v0;
+      pv1 = v1;
       op += ml;
       continue;
+    }
+    if (pml > 0) {                                                     // general path: no pending bytes
+      if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
+      if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
+      pml = 0;
     }
     // ---- general path
     ++ip;
@@ -491,6 +517,10 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       }
     }
     op += ml;
+  }
+  if (pml > 0) {
+    if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
+    if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
   }
   if (rc == LZ_OK && op != cap) rc = LZ_SIZE;
   if (gl == 0) status[b] = rc;

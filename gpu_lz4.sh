@@ -4,7 +4,5 @@ timeout -k 10 300 python -u -m pytest tests/test_lz4.py -x -q -m gpu --timeout 1
 tail -1 gpurun_out/lz4_tests.log
 timeout -k 10 200 python tools/lz4_bench.py > gpurun_out/lz4_micro_16.log 2>&1 || { tail -20 gpurun_out/lz4_micro_16.log; exit 1; }
 grep gbps gpurun_out/lz4_micro_16.log
-for C in 4; do
-  DXA_BENCH_HOST_TRACE=1 timeout -k 10 300 python bench.py --flow groupby --source pinned-lz4 --lz4-chunks $C --steps 20 > gpurun_out/lz4b_$C.log 2>&1 || { tail -20 gpurun_out/lz4b_$C.log; exit 1; }
-  grep metric gpurun_out/lz4b_$C.log | python -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['value']/1e6, d['ms_per_step'], d['p99_latency_process_ms'])"
-done
+timeout -k 10 300 python bench.py --steps 20 > gpurun_out/lz4b.log 2>&1 || { tail -20 gpurun_out/lz4b.log; exit 1; }
+grep metric gpurun_out/lz4b.log | python -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['value']/1e6, d['ms_per_step'], d['p99_latency_process_ms'])"
