@@ -107,6 +107,9 @@ class Processor:
         self.outputs = build_outputs(d)
         self.metric_logger = MetricLogger.from_settings(d, metric_store)
         self.parse_plan = ParsePlan(self.raw_schema, self._needed_raw_paths() if parse_prune else None)
+        # input rebalance across ranks (reference: datax.job.input.default.eventhub.repartition → rdd.repartition)
+        rp = d.get(S.INPUT_PREFIX + "eventhub.repartition") or d.get(S.INPUT_PREFIX + "repartition")
+        self.repartition = bool(rp) and rp.strip().lower() not in ("0", "false", "")
         self.batches = 0
         self.last_metrics: Dict[str, float] = {}
         self.last_views: Dict[str, Table] = {}
@@ -191,6 +194,9 @@ class Processor:
             cat.register("__dxa_input", table)
             items = step + [f"`{p}`" for p in preserved if not any(p in s for s in step)]
             table = run_sql("SELECT " + ", ".join(items) + " FROM __dxa_input", cat, ctx)
+        if self.repartition and P.active():
+            with tracing.stage("repartition", self.stage_times):
+                table = P.rebalance_table(table)
         self._sync()
         self.stage_times["project"] = time.perf_counter() - t0
         return table

@@ -247,3 +247,21 @@ def broadcast_table(table, src: int = 0):
         return shuffle_table(table.take(idx), dest)
     empty = table.take(torch.empty(0, dtype=torch.int64, device=table.device))
     return shuffle_table(empty, torch.empty(0, dtype=torch.int64, device=table.device))
+
+
+def rebalance_table(table):
+    """Round-robin full shuffle: global row g goes to rank g % W, so every rank ends up with an equal share of the
+    batch however skewed the source partitions were (the reference's optional input ``rdd.repartition(n)``,
+    DataProcessing/datax-host/src/main/scala/datax/host/StreamingHost.scala:68-69).  One all-gather of row counts
+    gives each rank its global row offset; the rows move in one all-to-all (``shuffle_table``)."""
+    from . import _RANK
+    W = _w()
+    if W <= 1:
+        return table
+    device = table.device
+    n = table.length
+    counts = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(W)]
+    dist.all_gather(counts, torch.tensor([n], dtype=torch.int64, device=device), group=_g())
+    offset = int(sum(int(c.item()) for c in counts[:_RANK]))
+    dest = (torch.arange(n, dtype=torch.int64, device=device) + offset) % W
+    return shuffle_table(table, dest)

@@ -77,6 +77,10 @@ def _worker(rank, world, port, q):
         got = P.shuffle_table(t, dest)
         back = P.allgather_table(got)
         results.append(back.to_pylist())
+        # round-robin rebalance of a skewed batch (input repartition): 300 + 100 rows → 200 + 200
+        skew = Table.from_pylist(rows[:300] if rank == 0 else rows[300:], schema)
+        reb = P.rebalance_table(skew)
+        results.append((reb.length, P.allgather_table(reb).to_pylist()))
         q.put((rank, results, None))
         dist.barrier()
         dist.destroy_process_group()
@@ -156,7 +160,11 @@ def test_two_rank_queries_match_single_process():
             assert _canon(res[r][len(QUERIES)][i]) == _canon(expect_w[i]), (WINDOW_QUERIES[i], r)
     # shuffle round trip preserves the multiset of rows
     for r in (0, 1):
-        assert _canon(res[r][-1]) == _canon(rows)
+        assert _canon(res[r][-2]) == _canon(rows)
+    # rebalance: equal shares, same multiset
+    for r in (0, 1):
+        n_r, everything = res[r][-1]
+        assert n_r == 200 and _canon(everything) == _canon(rows)
 
 
 @pytest.mark.parametrize("flow", ["groupby", "window"])
