@@ -46,6 +46,57 @@ struct ParseArgs {
   const uint64_t* key_words;    // key texts, zero padded to 8-byte words
 };
 
+// The same arguments as explicitly global (address space 1) pointers.  Pointers read out of a by-value struct
+// argument are otherwise generic, and every record-byte load and column store becomes a FLAT op — counted in
+// both vmcnt and lgkmcnt, so each LDS wait also drains the lane's outstanding global loads.
+#define G1 __attribute__((address_space(1)))
+typedef G1 uint8_t gu8;
+struct GArgs {
+  gu8* buf;
+  const G1 int64_t* offs;
+  int64_t n;
+  const G1 uint64_t* lut_keys;
+  const G1 int32_t* lut_node;
+  int32_t lut_cap;
+  const G1 int32_t* node_type;
+  const G1 int32_t* val_slot;
+  const G1 int32_t* len_slot;
+  int32_t nnodes;
+  G1 int64_t* vals;
+  G1 int32_t* lens;
+  gu8* valid;
+  gu8* row_ok;
+  const G1 int32_t* first_child;
+  const G1 int32_t* next_sib;
+  const G1 int32_t* key_word;
+  const G1 int32_t* key_len;
+  const G1 uint64_t* key_words;
+};
+
+__device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
+  GArgs g;
+  g.buf = (gu8*)p.buf;
+  g.offs = (const G1 int64_t*)p.offs;
+  g.n = p.n;
+  g.lut_keys = (const G1 uint64_t*)p.lut_keys;
+  g.lut_node = (const G1 int32_t*)p.lut_node;
+  g.lut_cap = p.lut_cap;
+  g.node_type = (const G1 int32_t*)p.node_type;
+  g.val_slot = (const G1 int32_t*)p.val_slot;
+  g.len_slot = (const G1 int32_t*)p.len_slot;
+  g.nnodes = p.nnodes;
+  g.vals = (G1 int64_t*)p.vals;
+  g.lens = (G1 int32_t*)p.lens;
+  g.valid = (gu8*)p.valid;
+  g.row_ok = (gu8*)p.row_ok;
+  g.first_child = (const G1 int32_t*)p.first_child;
+  g.next_sib = (const G1 int32_t*)p.next_sib;
+  g.key_word = (const G1 int32_t*)p.key_word;
+  g.key_len = (const G1 int32_t*)p.key_len;
+  g.key_words = (const G1 uint64_t*)p.key_words;
+  return g;
+}
+
 __constant__ uint64_t kPow10i[9] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
                                     100000000ull};
 __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
@@ -54,19 +105,25 @@ __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
 constexpr int kMaxDepth = 8;
 
 struct Reader {
-  uint8_t* buf;
+  gu8* buf;
   int64_t p, end;
   uintptr_t wbase;
-  uint4 w;
+  uint64_t wlo, whi;                                      // 16-byte window (one global_load_dwordx4)
 
   __device__ __forceinline__ uint32_t at(int64_t q) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(buf + q);
-    const uintptr_t b = a & ~(uintptr_t)15;
-    if (b != wbase) {
-      wbase = b;
-      w = *reinterpret_cast<const uint4*>(b);
+    const uint32_t o = (uint32_t)(a & 15);
+    if (a - o != wbase) {
+      wbase = a - o;
+      const G1 uint64_t* w = (const G1 uint64_t*)(buf + q - o);   // pointer arithmetic: stays global
+      wlo = w[0];
+      whi = w[1];
     }
-    return dxa::window_byte(w, (uint32_t)(a - b));
+    // mask blend, not a select: a select of two adjacent fields is turned into a dynamically indexed private
+    // array (scratch) by the compiler
+    const uint64_t m = 0ull - (uint64_t)((o >> 3) & 1u);
+    const uint64_t x = wlo ^ ((wlo ^ whi) & m);
+    return (uint32_t)(x >> ((o & 7u) * 8u)) & 0xffu;
   }
   __device__ __forceinline__ uint32_t cur() { return p < end ? at(p) : 0u; }
   __device__ __forceinline__ void skip_ws() {
@@ -80,18 +137,18 @@ struct Reader {
 __device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
 
 // 8 bytes at any address (two aligned loads + funnel shift); the batch buffer carries 16 bytes of tail padding.
-__device__ __forceinline__ uint64_t load8(const uint8_t* base, int64_t q) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(base + q);
-  const uintptr_t b = a & ~(uintptr_t)7;
-  const uint64_t lo = *reinterpret_cast<const uint64_t*>(b);
-  const uint32_t sh = (uint32_t)(a - b) * 8u;
+__device__ __forceinline__ uint64_t load8(const gu8* base, int64_t q) {
+  const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(base + q) & 7);
+  const G1 uint64_t* w = (const G1 uint64_t*)(base + q - o);
+  const uint64_t lo = w[0];
+  const uint32_t sh = o * 8u;
   if (sh == 0) return lo;
-  const uint64_t hi = *reinterpret_cast<const uint64_t*>(b + 8);
+  const uint64_t hi = w[1];
   return (lo >> sh) | (hi << (64u - sh));
 }
 
 // Does the key text at q equal the L-byte literal (followed by the closing quote)?
-__device__ __forceinline__ bool key_matches(const uint8_t* buf, int64_t q, int64_t end, const uint64_t* kw, int L) {
+__device__ __forceinline__ bool key_matches(const gu8* buf, int64_t q, int64_t end, const G1 uint64_t* kw, int L) {
   if (q + L >= end) return false;
   int i = 0;
   for (; i + 8 <= L; i += 8)
@@ -148,8 +205,8 @@ __device__ __forceinline__ uint32_t hexval(uint32_t c) {
 }
 
 // Un-escape [s,e) in place; returns the decoded length.
-__device__ int64_t unescape_inplace(Reader& r, int64_t s, int64_t e) {
-  uint8_t* b = r.buf;
+__device__ __forceinline__ int64_t unescape_inplace(Reader& r, int64_t s, int64_t e) {
+  gu8* b = r.buf;
   int64_t o = s;
   int64_t i = s;
   while (i < e) {
@@ -248,7 +305,7 @@ __device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, 
 }
 
 // Parse a JSON number at r.p.  Returns false on syntax error.
-__device__ bool scan_number(Reader& r, bool& is_int, bool& overflow, int64_t& iv, double& dv) {
+__device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overflow, int64_t& iv, double& dv) {
   bool neg = false;
   if (r.cur() == '-') { neg = true; ++r.p; }
   uint64_t mant = 0;
@@ -299,7 +356,7 @@ __device__ bool scan_number(Reader& r, bool& is_int, bool& overflow, int64_t& iv
 }
 
 // Skip any JSON value at r.p (strings, numbers, literals, nested containers).
-__device__ bool skip_value(Reader& r) {
+__device__ __forceinline__ bool skip_value(Reader& r) {
   uint32_t c = r.cur();
   if (c == '"') { int64_t s, e; bool esc; return scan_string(r, s, e, esc); }
   if (c == '{' || c == '[') {
@@ -323,7 +380,7 @@ __device__ bool skip_value(Reader& r) {
 }
 
 // Hash one escape sequence of a key (r.p at the backslash) as the bytes it decodes to, so "a\u0062" finds "ab".
-__device__ uint64_t hash_escape(Reader& r, uint64_t h) {
+__device__ __forceinline__ uint64_t hash_escape(Reader& r, uint64_t h) {
   ++r.p;
   if (r.p >= r.end) return h;
   const uint32_t n = r.at(r.p);
@@ -363,7 +420,7 @@ __device__ uint64_t hash_escape(Reader& r, uint64_t h) {
   }
 }
 
-__device__ __forceinline__ int lookup(const ParseArgs& a, int parent, uint64_t name_hash) {
+__device__ __forceinline__ int lookup(const GArgs& a, int parent, uint64_t name_hash) {
   uint64_t k = dxa::fmix64(name_hash ^ ((uint64_t)(parent + 1) * dxa::kGold));
   if (k == 0) k = 1;
   const uint32_t mask = (uint32_t)a.lut_cap - 1u;
@@ -378,7 +435,7 @@ __device__ __forceinline__ int lookup(const ParseArgs& a, int parent, uint64_t n
 }
 
 // Parse ISO-8601-ish text [s,e): YYYY-MM-DD[(T| )HH:MM[:SS[.ffffff]]][Z|(+|-)HH[:]MM]  → µs since epoch UTC.
-__device__ bool parse_iso_ts(const uint8_t* b, int64_t s, int64_t e, int64_t& out, bool date_only_ok) {
+__device__ __forceinline__ bool parse_iso_ts(const gu8* b, int64_t s, int64_t e, int64_t& out, bool date_only_ok) {
   auto num = [&](int64_t& i, int digits, int& v) -> bool {
     v = 0;
     for (int k = 0; k < digits; ++k) {
@@ -429,7 +486,8 @@ __device__ bool parse_iso_ts(const uint8_t* b, int64_t s, int64_t e, int64_t& ou
   return true;
 }
 
-__global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
+__global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
+  const GArgs a = to_global(pa);
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= a.n) return;
   const int64_t n = a.n;
@@ -438,19 +496,25 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
   r.p = a.offs[row];
   r.end = a.offs[row + 1];
   r.wbase = 0;
-  r.w = make_uint4(0, 0, 0, 0);
+  r.wlo = r.whi = 0;
 
   // schema-tracked nesting is kept in registers (deeper objects are skipped as unknown values)
-  int stack[kMaxDepth];
-  int expect[kMaxDepth];
+  // nesting state in LDS, [level][lane] (consecutive lanes → consecutive banks): dynamically indexed per-lane
+  // arrays would otherwise take 16 VGPRs (or a compiler-chosen LDS layout with bank conflicts)
+  __shared__ int s_stack[kMaxDepth][256];
+  __shared__ int s_expect[kMaxDepth][256];
+  int* stack_ = &s_stack[0][threadIdx.x];
+  int* expect_ = &s_expect[0][threadIdx.x];
+#define stack(i) stack_[(i) * 256]
+#define expect(i) expect_[(i) * 256]
   int depth = 0;
   bool ok = false;
 
   r.skip_ws();
   if (r.cur() != '{') goto done;
   ++r.p;
-  stack[0] = 0;  // root node
-  expect[0] = a.first_child[0];
+  stack(0) = 0;  // root node
+  expect(0) = a.first_child[0];
   depth = 1;
   a.valid[row] = 1;  // root struct present
   while (true) {
@@ -466,7 +530,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
       // ---- key: speculate the expected key first, fall back to hashing the key text
       ++r.p;
       int node = -1;
-      const int ex = expect[depth - 1];
+      const int ex = expect(depth - 1);
       if (ex >= 0 && key_matches(a.buf, r.p, r.end, a.key_words + a.key_word[ex], a.key_len[ex])) {
         node = ex;
         r.p += a.key_len[ex] + 1;
@@ -481,9 +545,9 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
           ++r.p;
         }
         if (!closed) break;
-        node = lookup(a, stack[depth - 1], h);
+        node = lookup(a, stack(depth - 1), h);
       }
-      if (node >= 0) expect[depth - 1] = a.next_sib[node];
+      if (node >= 0) expect(depth - 1) = a.next_sib[node];
       r.skip_ws();
       if (r.cur() != ':') break;
       ++r.p;
@@ -499,8 +563,9 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs a) {
       if (c == '{' && t == FT_STRUCT) {
         if (depth >= kMaxDepth) { if (!skip_value(r)) break; goto after_value; }
         a.valid[(int64_t)node * n + row] = 1;
-        expect[depth] = a.first_child[node];
-        stack[depth++] = node;
+        expect(depth) = a.first_child[node];
+        stack(depth) = node;
+        ++depth;
         ++r.p;
         continue;
       }
@@ -594,6 +659,8 @@ done:
   if (!ok) {
     for (int k = 0; k < a.nnodes; ++k) a.valid[(int64_t)k * n + row] = 0;
   }
+#undef stack
+#undef expect
 }
 
 // Per-node null counts (one 64-lane ballot per node per wave, one atomic per node per wave) so the host can drop
