@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--ref-rows", type=int, default=100_000_000, help="reference table rows (join flow)")
     ap.add_argument("--pool", type=int, default=3, help="distinct pre-generated batches cycled (pinned source)")
     ap.add_argument("--lz4-chunks", type=int, default=4, help="pinned-lz4: copy/decode pipeline depth per batch")
+    ap.add_argument("--lz4-level", type=int, default=9,
+                    help="pinned-lz4: producer compression level (Kafka compression.lz4.level; 9 is Kafka's default, "
+                         "0 = fast greedy compressor)")
     ap.add_argument("--source", choices=["pinned", "pinned-lz4", "device", "gpu-sim"], default=None,
                     help="pinned: H2D copy of raw bytes every step; pinned-lz4: H2D copy of an LZ4 frame of JSON "
                          "lines, decoded + newline-framed on the GPU; device: bytes already in HBM; gpu-sim: GPU "
@@ -139,7 +142,7 @@ def main():
         for p in range(args.pool):
             buf, offs = generate(prog_nl, E, device, seed=1000 * rank + p + 1, row0=p * E, base_ms=base_ms)
             total = int(offs[-1])
-            frame = lz4.compress_frame(buf[:total].cpu(), lz4.DEFAULT_BLOCK, threads=16)
+            frame = lz4.compress_frame(buf[:total].cpu(), lz4.DEFAULT_BLOCK, threads=16, level=args.lz4_level)
             del buf, offs
             comp_bytes.append(frame.size)
             pool.append(lz4.DeviceFrame.from_frame(frame, lz4.DEFAULT_BLOCK, pin=on_gpu))
@@ -309,6 +312,7 @@ def main():
     if comp_bytes:
         out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)
         out["config"]["lz4_ratio"] = round((sum(sizes) / len(sizes) - 16) / (sum(comp_bytes) / len(comp_bytes)), 2)
+        out["config"]["lz4_level"] = args.lz4_level
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
     if last:

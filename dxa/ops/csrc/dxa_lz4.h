@@ -16,9 +16,13 @@ int64_t compress_block(const uint8_t* src, int64_t n, uint8_t* dst);
 // Decompress one block into dst[cap]; returns the decompressed size or -1 on malformed input / overflow.
 int64_t decompress_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
 uint32_t xxh32(const uint8_t* p, int64_t n, uint32_t seed);
-// Frame: compress with independent blocks of `block_size` (<= 4 MiB) bytes using `threads` workers.
+// High-compression block (hash chains, `depth` candidates per position, lazy matching); same format.
+int64_t compress_block_hc(const uint8_t* src, int64_t n, uint8_t* dst, int depth);
+// Frame: compress with independent blocks of `block_size` (<= 4 MiB) bytes using `threads` workers.  `level`
+// <= 2 is the greedy compressor; L >= 3 is the high-compression mode searching 2^(L-1) candidates (max 4096).
 int64_t frame_bound(int64_t n, int32_t block_size);
-int64_t compress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t block_size, int32_t threads);
+int64_t compress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t block_size, int32_t threads,
+                       int32_t level = 0);
 // Walk a frame's block table.  Fills up to max_blocks entries (may be null to count); returns the block count, or
 // -1 malformed / -2 unsupported (dependent blocks, dictionary).  content_size = -1 when the frame omits it.
 int64_t frame_blocks(const uint8_t* src, int64_t n, int64_t* comp_off, int32_t* comp_len, uint8_t* stored,

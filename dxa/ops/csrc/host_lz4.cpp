@@ -127,6 +127,79 @@ int64_t compress_block(const uint8_t* src, int64_t n, uint8_t* dst) {
   return op - dst;
 }
 
+// High-compression block: hash chains over the block (every position inserted), longest match among up to `depth`
+// candidates, one-step lazy evaluation.  Same output format as compress_block.
+int64_t compress_block_hc(const uint8_t* src, int64_t n, uint8_t* dst, int depth) {
+  uint8_t* op = dst;
+  int64_t anchor = 0;
+  if (n >= kMfLimit + 1) {
+    std::vector<int32_t> head(1u << kHashLog, -1);
+    std::vector<int32_t> chain((size_t)n, -1);
+    const int64_t match_limit = n - kLastLiterals;
+    const int64_t search_limit = n - kMfLimit;
+    int64_t next_insert = 0;
+    auto insert_upto = [&](int64_t pos) {
+      for (; next_insert < pos; ++next_insert) {
+        const uint32_t h = hash4(rd32(src + next_insert));
+        chain[next_insert] = head[h];
+        head[h] = (int32_t)next_insert;
+      }
+    };
+    auto find = [&](int64_t ip, int64_t& best_ref) -> int64_t {
+      insert_upto(ip);
+      const uint32_t seq = rd32(src + ip);
+      int64_t best = 0;
+      int64_t cand = head[hash4(seq)];
+      for (int d = 0; d < depth && cand >= 0 && ip - cand <= 65535; ++d, cand = chain[cand]) {
+        if (rd32(src + cand) != seq) continue;
+        int64_t len = kMinMatch;
+        while (ip + len < match_limit && src[cand + len] == src[ip + len]) ++len;
+        if (len > best) {
+          best = len;
+          best_ref = cand;
+          if (ip + len >= match_limit) break;
+        }
+      }
+      return best;
+    };
+    int64_t ip = 0;
+    while (ip < search_limit) {
+      int64_t ref = -1;
+      int64_t len = find(ip, ref);
+      if (len < kMinMatch) { ++ip; continue; }
+      while (ip + 1 < search_limit) {                  // lazy: a longer match one byte later wins
+        int64_t ref2 = -1;
+        const int64_t len2 = find(ip + 1, ref2);
+        if (len2 <= len) break;
+        ++ip;
+        len = len2;
+        ref = ref2;
+      }
+      int64_t s = ip, r = ref;
+      while (s > anchor && r > 0 && src[s - 1] == src[r - 1]) { --s; --r; ++len; }
+      const int64_t lit = s - anchor;
+      uint8_t* token = op++;
+      const int64_t mlc = len - kMinMatch;
+      *token = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (mlc >= 15 ? 15 : mlc));
+      if (lit >= 15) op = put_len(op, lit - 15);
+      std::memcpy(op, src + anchor, (size_t)lit);
+      op += lit;
+      const int64_t off = s - r;
+      *op++ = (uint8_t)off;
+      *op++ = (uint8_t)(off >> 8);
+      if (mlc >= 15) op = put_len(op, mlc - 15);
+      ip = s + len;
+      anchor = ip;
+    }
+  }
+  const int64_t lit = n - anchor;
+  *op++ = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+  if (lit >= 15) op = put_len(op, lit - 15);
+  if (lit) std::memcpy(op, src + anchor, (size_t)lit);
+  op += lit;
+  return op - dst;
+}
+
 int64_t decompress_block(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) { return decode(src, n, dst, 0, cap); }
 
 uint32_t xxh32(const uint8_t* p, int64_t n, uint32_t seed) {
@@ -158,7 +231,8 @@ int64_t frame_bound(int64_t n, int32_t block_size) {
   return 19 + nb * (4 + block_bound(block_size)) + 4;
 }
 
-int64_t compress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t block_size, int32_t threads) {
+int64_t compress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t block_size, int32_t threads,
+                       int32_t level) {
   if (block_size <= 0 || block_size > 4 * 1024 * 1024) return -1;
   if (cap < frame_bound(n, block_size)) return -1;
   uint8_t* op = dst;
@@ -176,7 +250,9 @@ int64_t compress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap,
     for (int64_t b = b0; b < b1; ++b) {
       const int64_t s = b * block_size;
       const int64_t len = std::min<int64_t>(block_size, n - s);
-      clen[b] = compress_block(src + s, len, tmp.data() + b * block_bound(block_size));
+      uint8_t* out = tmp.data() + b * block_bound(block_size);
+      clen[b] = level <= 2 ? compress_block(src + s, len, out)
+                           : compress_block_hc(src + s, len, out, 1 << std::min(level - 1, 12));
     }
   };
   const int T = std::max(1, std::min<int>(threads, (int)std::min<int64_t>(nb, 64)));
@@ -285,7 +361,11 @@ extern "C" {
 DXA_API int64_t dxa_lz4_frame_bound(int64_t n, int32_t block_size) { return dxa::lz4::frame_bound(n, block_size); }
 DXA_API int64_t dxa_lz4_compress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t block_size,
                                        int32_t threads) {
-  return dxa::lz4::compress_frame(src, n, dst, cap, block_size, threads);
+  return dxa::lz4::compress_frame(src, n, dst, cap, block_size, threads, 0);
+}
+DXA_API int64_t dxa_lz4_compress_frame_level(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap,
+                                             int32_t block_size, int32_t threads, int32_t level) {
+  return dxa::lz4::compress_frame(src, n, dst, cap, block_size, threads, level);
 }
 DXA_API int64_t dxa_lz4_decompress_frame(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
   return dxa::lz4::decompress_frame(src, n, dst, cap);

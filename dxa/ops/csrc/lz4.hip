@@ -418,21 +418,26 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     const uint32_t token = wbyte(X, r);
     int32_t lit = (int32_t)(token >> 4);
     const int32_t mlc = (int32_t)(token & 15);
-    if (lit < 15 && mlc < 15 && r + lit + 3 <= 4 * G && iend - ip >= lit + 3 && cap - op >= lit + mlc + 4) {
-      // ---- fast path.  The match copy is software-pipelined: this sequence's match bytes are loaded now and
-      // stored during the next sequence (after that one's loads are issued), so the load latency overlaps the
-      // next header parse instead of stalling the group.  A source that reaches into the still-pending bytes
-      // flushes them first.
+    // one match-length extension byte (< 255) is also taken on the fast path: high-compression producers emit
+    // many 19..273-byte matches
+    const uint32_t mext = (mlc == 15 && lit < 15 && r + lit + 4 <= 4 * G) ? wbyte(X, r + lit + 3) : 0u;
+    const int32_t fml = mlc + 4 + (int32_t)mext;                      // match length if on the fast path
+    const int32_t fhdr = lit + 3 + (mlc == 15 ? 1 : 0);               // token + literals + offset (+ ext byte)
+    if (lit < 15 && (mlc < 15 || mext < 255) && r + fhdr <= 4 * G && iend - ip >= fhdr && cap - op >= lit + fml) {
+      // ---- fast path.  The match copy is software-pipelined: this sequence's match bytes (up to 32) are loaded
+      // now and stored during the next sequence (after that one's loads are issued), so the load latency
+      // overlaps the next header parse instead of stalling the group.  A source that reaches into the
+      // still-pending bytes flushes them first.  Longer matches are copied directly.
       const uint32_t lv = wbyte(X, r + 1 + gl);
       const int32_t off = (int32_t)(wbyte(X, r + 1 + lit) | (wbyte(X, r + 2 + lit) << 8));
       if (gl < lit) out[op + gl] = (uint8_t)lv;
-      ip += lit + 3;
+      ip += fhdr;
       op += lit;
       if (off == 0 || off > op) { rc = LZ_OFFSET; break; }
-      const int32_t ml = mlc + 4;
+      const int32_t ml = fml;
       const int32_t s0 = op - off;
       const int32_t src_end = s0 + (off < ml ? off : ml);
-      if (pml > 0 && src_end > pdst) {                                 // source overlaps the pending bytes
+      if (pml > 0 && (src_end > pdst || ml > 2 * G)) {                 // source overlaps pending bytes / long copy
         if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
         if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
         pml = 0;
@@ -440,6 +445,19 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       if (src_end > done) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         done = pml > 0 ? pdst : op;
+      }
+      if (ml > 2 * G) {
+        if (off >= ml) {
+          for (int32_t c = 0; c < ml; c += G)
+            if (c + gl < ml) out[op + c + gl] = out[s0 + c + gl];
+        } else {
+          for (int32_t c = 0; c < ml; c += G) {
+            const uint32_t i = (uint32_t)(c + gl);
+            if ((int32_t)i < ml) out[op + i] = out[s0 + (int32_t)(i % (uint32_t)off)];
+          }
+        }
+        op += ml;
+        continue;
       }
       uint32_t v0 = 0, v1 = 0;
       if (off >= ml) {

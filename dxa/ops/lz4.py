@@ -34,6 +34,8 @@ def _host():
         L.dxa_lz4_frame_bound.argtypes = [i64, i32]
         L.dxa_lz4_compress_frame.restype = i64
         L.dxa_lz4_compress_frame.argtypes = [p, i64, p, i64, i32, i32]
+        L.dxa_lz4_compress_frame_level.restype = i64
+        L.dxa_lz4_compress_frame_level.argtypes = [p, i64, p, i64, i32, i32, i32]
         L.dxa_lz4_decompress_frame.restype = i64
         L.dxa_lz4_decompress_frame.argtypes = [p, i64, p, i64]
         L.dxa_lz4_frame_blocks.restype = i64
@@ -61,13 +63,17 @@ def xxh32(data, seed: int = 0) -> int:
     return int(_host().dxa_xxh32(a.ctypes.data, a.size, seed))
 
 
-def compress_frame(data, block_size: int = DEFAULT_BLOCK, threads: Optional[int] = None) -> np.ndarray:
+def compress_frame(data, block_size: int = DEFAULT_BLOCK, threads: Optional[int] = None, level: int = 0
+                   ) -> np.ndarray:
+    """LZ4 frame of ``data``.  ``level`` <= 2: fast greedy compressor; >= 3: high-compression mode (hash chains,
+    2^(level-1) candidates, lazy matching) — the producer-side setting (Kafka ``compression.lz4.level``) that
+    trades compression time for fewer, longer sequences: a smaller frame and a cheaper decode."""
     a = _as_np(data)
     L = _host()
     cap = L.dxa_lz4_frame_bound(a.size, block_size)
     out = np.empty(cap, dtype=np.uint8)
-    m = L.dxa_lz4_compress_frame(a.ctypes.data, a.size, out.ctypes.data, cap, block_size,
-                                 threads or min(16, os.cpu_count() or 4))
+    m = L.dxa_lz4_compress_frame_level(a.ctypes.data, a.size, out.ctypes.data, cap, block_size,
+                                       threads or min(16, os.cpu_count() or 4), level)
     if m < 0:
         raise Lz4Error("lz4 frame compression failed")
     return out[:m]

@@ -91,6 +91,18 @@ def test_frame_roundtrip_and_independent_decoder(block):
         assert f[14] == (lz4.xxh32(f[4:14]) >> 8) & 0xFF
 
 
+@pytest.mark.parametrize("level", [3, 6, 9])
+def test_high_compression_levels_roundtrip(level):
+    """The hash-chain (HC) compressor emits standard LZ4: the independent Python decoder reads it back, and on
+    JSON it needs fewer sequences and bytes than the greedy compressor."""
+    for data in _samples():
+        f = lz4.compress_frame(data, 4096, level=level)
+        assert lz4.decompress_frame(f) == data
+        assert _py_frame_decode(f.tobytes()) == data
+    js = b"".join(_samples(4))
+    assert lz4.compress_frame(js, 16384, level=level).size <= lz4.compress_frame(js, 16384).size
+
+
 def test_block_codec_and_malformed_input():
     data = b"abcdefgh" * 1000 + b"tail-bytes"
     blk = lz4.compress_block(data)

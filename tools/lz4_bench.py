@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--events", type=int, default=2_000_000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--block", type=int, default=16384)
+    ap.add_argument("--level", type=int, default=9, help="producer compression level (0 = fast greedy)")
     a = ap.parse_args()
     from dxa.ops import native, lz4
     from dxa.models import iot
@@ -27,7 +28,7 @@ def main():
     buf, offs = generate(iot.program(newline=True), a.events, dev, seed=1, row0=0, base_ms=1_700_000_000_000)
     total = int(offs[-1])
     host = buf[:total].cpu()
-    frame = lz4.compress_frame(host, a.block, threads=16)
+    frame = lz4.compress_frame(host, a.block, threads=16, level=a.level)
     fr = lz4.DeviceFrame.from_frame(frame, a.block).to(dev)
     out = lz4.decompress_device(fr, check=True)
     torch.cuda.synchronize()
