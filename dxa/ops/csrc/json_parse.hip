@@ -14,6 +14,7 @@
 // Semantics: missing field / JSON null / type mismatch → null for that field; a syntactically malformed record
 // → every field of the row null and row_ok=0 (the reference is "tolerant to mismatched input schema").
 #include "dxa_common.h"
+#include <type_traits>
 
 namespace {
 
@@ -44,6 +45,7 @@ struct ParseArgs {
   const int32_t* key_word;      // [nnodes] offset (in u64 words) of the node's key text
   const int32_t* key_len;       // [nnodes] key length in bytes
   const uint64_t* key_words;    // key texts, zero padded to 8-byte words
+  int32_t nkey_words;
 };
 
 // The same arguments as explicitly global (address space 1) pointers.  Pointers read out of a by-value struct
@@ -71,6 +73,7 @@ struct GArgs {
   const G1 int32_t* key_word;
   const G1 int32_t* key_len;
   const G1 uint64_t* key_words;
+  int32_t nkey_words;
 };
 
 __device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
@@ -94,6 +97,7 @@ __device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
   g.key_word = (const G1 int32_t*)p.key_word;
   g.key_len = (const G1 int32_t*)p.key_len;
   g.key_words = (const G1 uint64_t*)p.key_words;
+  g.nkey_words = p.nkey_words;
   return g;
 }
 
@@ -102,28 +106,104 @@ __constant__ uint64_t kPow10i[9] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 1000
 __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                   1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
+
+// Schema tables (node info, key texts, key lookup table) as seen by the parse loop.  With LDS=true the workgroup
+// first copies them into LDS: every field does ~9 table reads, and as VMEM loads they go through the same per-CU
+// address path the record bytes saturate; from LDS they are broadcast reads.
+#define G3 __attribute__((address_space(3)))
+template <bool LDS>
+struct Tables {
+  typedef typename std::conditional<LDS, const G3 int32_t*, const G1 int32_t*>::type I32P;
+  typedef typename std::conditional<LDS, const G3 uint64_t*, const G1 uint64_t*>::type U64P;
+  I32P node_type, val_slot, len_slot, first_child, next_sib, key_word, key_len, lut_node;
+  U64P key_words, lut_keys;
+  int32_t lut_cap;
+};
+
+__host__ __device__ inline int64_t tables_lds_bytes(int32_t nnodes, int32_t nkw, int32_t lut_cap) {
+  return (int64_t)nkw * 8 + (int64_t)lut_cap * 8 + (int64_t)(8 * nnodes + lut_cap) * 4;
+}
+
+template <bool LDS>
+__device__ __forceinline__ Tables<LDS> load_tables(const GArgs& a);
+
+template <>
+__device__ __forceinline__ Tables<false> load_tables<false>(const GArgs& a) {
+  Tables<false> t;
+  t.node_type = a.node_type; t.val_slot = a.val_slot; t.len_slot = a.len_slot;
+  t.first_child = a.first_child; t.next_sib = a.next_sib; t.key_word = a.key_word; t.key_len = a.key_len;
+  t.lut_node = a.lut_node; t.key_words = a.key_words; t.lut_keys = a.lut_keys; t.lut_cap = a.lut_cap;
+  return t;
+}
+
+extern __shared__ uint64_t dyn_lds[];
+
+template <>
+__device__ __forceinline__ Tables<true> load_tables<true>(const GArgs& a) {
+  G3 uint64_t* u64 = (G3 uint64_t*)dyn_lds;
+  G3 uint64_t* kw = u64;
+  G3 uint64_t* lk = u64 + a.nkey_words;
+  G3 int32_t* i32 = (G3 int32_t*)(lk + a.lut_cap);
+  const int nn = a.nnodes;
+  G3 int32_t* arr[7] = {i32, i32 + nn, i32 + 2 * nn, i32 + 3 * nn, i32 + 4 * nn, i32 + 5 * nn, i32 + 6 * nn};
+  G3 int32_t* ln = i32 + 8 * nn;
+  for (int i = threadIdx.x; i < a.nkey_words; i += blockDim.x) kw[i] = a.key_words[i];
+  for (int i = threadIdx.x; i < a.lut_cap; i += blockDim.x) { lk[i] = a.lut_keys[i]; ln[i] = a.lut_node[i]; }
+  for (int i = threadIdx.x; i < nn; i += blockDim.x) {
+    arr[0][i] = a.node_type[i]; arr[1][i] = a.val_slot[i]; arr[2][i] = a.len_slot[i];
+    arr[3][i] = a.first_child[i]; arr[4][i] = a.next_sib[i]; arr[5][i] = a.key_word[i]; arr[6][i] = a.key_len[i];
+  }
+  __syncthreads();
+  Tables<true> t;
+  t.node_type = arr[0]; t.val_slot = arr[1]; t.len_slot = arr[2]; t.first_child = arr[3]; t.next_sib = arr[4];
+  t.key_word = arr[5]; t.key_len = arr[6]; t.lut_node = ln; t.key_words = kw; t.lut_keys = lk;
+  t.lut_cap = a.lut_cap;
+  return t;
+}
+
 constexpr int kMaxDepth = 8;
 
+// Per-lane 32-byte register window over the lane's record (two global_load_dwordx4 per refill).  Every byte and
+// 8-byte read (SWAR scans, key compares, timestamps) is served from it: lanes read 64 unrelated records, so each
+// load instruction touches 64 cache lines and the per-CU address path, not VALU, bounds the parser — reloading
+// only when the window is exhausted keeps that to ~2 loads per 32 record bytes.
 struct Reader {
   gu8* buf;
   int64_t p, end;
-  uintptr_t wbase;
-  uint64_t wlo, whi;                                      // 16-byte window (one global_load_dwordx4)
+  int64_t wb;                                             // window base offset (16-B aligned in memory), -1: none
+  uint64_t w0, w1, w2, w3;
 
+  __device__ __forceinline__ void fill(int64_t q) {
+    const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(buf + q) & 15);
+    wb = q - o;
+    const G1 uint64_t* w = (const G1 uint64_t*)(buf + wb);  // pointer arithmetic: stays global
+    w0 = w[0];
+    w1 = w[1];
+    w2 = w[2];
+    w3 = w[3];
+  }
+  // word k (0..3) of the window: mask blends, not selects (a select of adjacent fields becomes a dynamically
+  // indexed private array — scratch — in the compiler)
+  __device__ __forceinline__ uint64_t word(uint32_t k) const {
+    const uint64_t m0 = 0ull - (uint64_t)(k & 1u);
+    const uint64_t lo = w0 ^ ((w0 ^ w1) & m0);
+    const uint64_t hi = w2 ^ ((w2 ^ w3) & m0);
+    const uint64_t m1 = 0ull - (uint64_t)((k >> 1) & 1u);
+    return lo ^ ((lo ^ hi) & m1);
+  }
   __device__ __forceinline__ uint32_t at(int64_t q) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(buf + q);
-    const uint32_t o = (uint32_t)(a & 15);
-    if (a - o != wbase) {
-      wbase = a - o;
-      const G1 uint64_t* w = (const G1 uint64_t*)(buf + q - o);   // pointer arithmetic: stays global
-      wlo = w[0];
-      whi = w[1];
-    }
-    // mask blend, not a select: a select of two adjacent fields is turned into a dynamically indexed private
-    // array (scratch) by the compiler
-    const uint64_t m = 0ull - (uint64_t)((o >> 3) & 1u);
-    const uint64_t x = wlo ^ ((wlo ^ whi) & m);
-    return (uint32_t)(x >> ((o & 7u) * 8u)) & 0xffu;
+    if ((uint64_t)(q - wb) >= 32u) fill(q);
+    const uint32_t o = (uint32_t)(q - wb);
+    return (uint32_t)(word(o >> 3) >> ((o & 7u) * 8u)) & 0xffu;
+  }
+  // 8 bytes starting at q (the batch buffer carries >= 16 bytes of tail padding)
+  __device__ __forceinline__ uint64_t load8(int64_t q) {
+    if ((uint64_t)(q - wb) > 24u) fill(q);
+    const uint32_t o = (uint32_t)(q - wb);
+    const uint32_t k = o >> 3, sh = (o & 7u) * 8u;
+    const uint64_t lo = word(k);
+    if (sh == 0) return lo;
+    return (lo >> sh) | (word(k + 1) << (64u - sh));
   }
   __device__ __forceinline__ uint32_t cur() { return p < end ? at(p) : 0u; }
   __device__ __forceinline__ void skip_ws() {
@@ -136,24 +216,14 @@ struct Reader {
 
 __device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
 
-// 8 bytes at any address (two aligned loads + funnel shift); the batch buffer carries 16 bytes of tail padding.
-__device__ __forceinline__ uint64_t load8(const gu8* base, int64_t q) {
-  const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(base + q) & 7);
-  const G1 uint64_t* w = (const G1 uint64_t*)(base + q - o);
-  const uint64_t lo = w[0];
-  const uint32_t sh = o * 8u;
-  if (sh == 0) return lo;
-  const uint64_t hi = w[1];
-  return (lo >> sh) | (hi << (64u - sh));
-}
-
 // Does the key text at q equal the L-byte literal (followed by the closing quote)?
-__device__ __forceinline__ bool key_matches(const gu8* buf, int64_t q, int64_t end, const G1 uint64_t* kw, int L) {
+template <typename KW>
+__device__ __forceinline__ bool key_matches(Reader& r, int64_t q, int64_t end, KW kw, int L) {
   if (q + L >= end) return false;
   int i = 0;
   for (; i + 8 <= L; i += 8)
-    if (load8(buf, q + i) != kw[i >> 3]) return false;
-  const uint64_t tail = load8(buf, q + i);
+    if (r.load8(q + i) != kw[i >> 3]) return false;
+  const uint64_t tail = r.load8(q + i);
   const int rem = L - i;                                   // 0..7 bytes of key, then the quote
   const uint64_t mask = rem == 7 ? ~0ull : ((1ull << (8 * (rem + 1))) - 1);
   const uint64_t want = (rem ? kw[i >> 3] : 0ull) | ((uint64_t)'"' << (8 * rem));
@@ -184,7 +254,7 @@ __device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, b
   s = r.p;
   esc = false;
   while (r.p < r.end) {
-    const uint64_t x = load8(r.buf, r.p);
+    const uint64_t x = r.load8(r.p);
     const uint64_t m = swar_eq(x, 0x2222222222222222ull) | swar_eq(x, 0x5C5C5C5C5C5C5C5Cull);
     if (m == 0) { r.p += 8; continue; }
     r.p += __builtin_ctzll(m) >> 3;
@@ -253,7 +323,7 @@ __device__ __forceinline__ int64_t unescape_inplace(Reader& r, int64_t s, int64_
       default: b[o++] = (uint8_t)n; break;  // \" \\ \/ and unknown
     }
   }
-  r.wbase = 0;  // window may cover rewritten bytes
+  r.wb = -64;  // window may cover rewritten bytes
   return o - s;
 }
 
@@ -263,7 +333,7 @@ __device__ __forceinline__ int64_t unescape_inplace(Reader& r, int64_t s, int64_
 __device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, int& exp10, bool& lost, bool frac) {
   bool any = false;
   while (r.p < r.end) {
-    const uint64_t x = load8(r.buf, r.p);
+    const uint64_t x = r.load8(r.p);
     const uint64_t nm = swar_nondigit(x);
     int k = nm ? (__builtin_ctzll(nm) >> 3) : 8;
     if (k > r.end - r.p) k = (int)(r.end - r.p);
@@ -420,7 +490,8 @@ __device__ __forceinline__ uint64_t hash_escape(Reader& r, uint64_t h) {
   }
 }
 
-__device__ __forceinline__ int lookup(const GArgs& a, int parent, uint64_t name_hash) {
+template <typename T>
+__device__ __forceinline__ int lookup(const T& a, int parent, uint64_t name_hash) {
   uint64_t k = dxa::fmix64(name_hash ^ ((uint64_t)(parent + 1) * dxa::kGold));
   if (k == 0) k = 1;
   const uint32_t mask = (uint32_t)a.lut_cap - 1u;
@@ -435,7 +506,11 @@ __device__ __forceinline__ int lookup(const GArgs& a, int parent, uint64_t name_
 }
 
 // Parse ISO-8601-ish text [s,e): YYYY-MM-DD[(T| )HH:MM[:SS[.ffffff]]][Z|(+|-)HH[:]MM]  → µs since epoch UTC.
-__device__ __forceinline__ bool parse_iso_ts(const gu8* b, int64_t s, int64_t e, int64_t& out, bool date_only_ok) {
+__device__ __forceinline__ bool parse_iso_ts(Reader& rd, int64_t s, int64_t e, int64_t& out, bool date_only_ok) {
+  struct B {
+    Reader& r;
+    __device__ __forceinline__ uint32_t operator[](int64_t i) const { return r.at(i); }
+  } b{rd};
   auto num = [&](int64_t& i, int digits, int& v) -> bool {
     v = 0;
     for (int k = 0; k < digits; ++k) {
@@ -486,8 +561,10 @@ __device__ __forceinline__ bool parse_iso_ts(const gu8* b, int64_t s, int64_t e,
   return true;
 }
 
+template <bool LDS>
 __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
   const GArgs a = to_global(pa);
+  const Tables<LDS> tb = load_tables<LDS>(a);                   // (LDS: whole workgroup, before any early exit)
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= a.n) return;
   const int64_t n = a.n;
@@ -495,8 +572,8 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
   r.buf = a.buf;
   r.p = a.offs[row];
   r.end = a.offs[row + 1];
-  r.wbase = 0;
-  r.wlo = r.whi = 0;
+  r.wb = -64;
+  r.w0 = r.w1 = r.w2 = r.w3 = 0;
 
   // schema-tracked nesting is kept in registers (deeper objects are skipped as unknown values)
   // nesting state in LDS, [level][lane] (consecutive lanes → consecutive banks): dynamically indexed per-lane
@@ -514,7 +591,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
   if (r.cur() != '{') goto done;
   ++r.p;
   stack(0) = 0;  // root node
-  expect(0) = a.first_child[0];
+  expect(0) = tb.first_child[0];
   depth = 1;
   a.valid[row] = 1;  // root struct present
   while (true) {
@@ -531,9 +608,9 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
       ++r.p;
       int node = -1;
       const int ex = expect(depth - 1);
-      if (ex >= 0 && key_matches(a.buf, r.p, r.end, a.key_words + a.key_word[ex], a.key_len[ex])) {
+      if (ex >= 0 && key_matches(r, r.p, r.end, tb.key_words + tb.key_word[ex], tb.key_len[ex])) {
         node = ex;
-        r.p += a.key_len[ex] + 1;
+        r.p += tb.key_len[ex] + 1;
       } else {
         uint64_t h = dxa::kFnvBasis;
         bool closed = false;
@@ -545,9 +622,9 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
           ++r.p;
         }
         if (!closed) break;
-        node = lookup(a, stack(depth - 1), h);
+        node = lookup(tb, stack(depth - 1), h);
       }
-      if (node >= 0) expect(depth - 1) = a.next_sib[node];
+      if (node >= 0) expect(depth - 1) = tb.next_sib[node];
       r.skip_ws();
       if (r.cur() != ':') break;
       ++r.p;
@@ -557,13 +634,13 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
         if (!skip_value(r)) break;
         goto after_value;
       }
-      const int t = a.node_type[node];
-      const int vs = a.val_slot[node];
-      const int ls = a.len_slot[node];
+      const int t = tb.node_type[node];
+      const int vs = tb.val_slot[node];
+      const int ls = tb.len_slot[node];
       if (c == '{' && t == FT_STRUCT) {
         if (depth >= kMaxDepth) { if (!skip_value(r)) break; goto after_value; }
         a.valid[(int64_t)node * n + row] = 1;
-        expect(depth) = a.first_child[node];
+        expect(depth) = tb.first_child[node];
         stack(depth) = node;
         ++depth;
         ++r.p;
@@ -590,7 +667,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
           a.valid[(int64_t)node * n + row] = 1;
         } else if (t == FT_TIMESTAMP || t == FT_DATE) {
           int64_t us;
-          if (parse_iso_ts(a.buf, s, e, us, true)) {
+          if (parse_iso_ts(r, s, e, us, true)) {
             a.vals[(int64_t)vs * n + row] = (t == FT_DATE) ? (us >= 0 ? us / 86400000000ll
                                                                      : -((-us + 86399999999ll) / 86400000000ll))
                                                            : us;
@@ -750,16 +827,20 @@ DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const u
                            const int32_t* val_slot, const int32_t* len_slot, int32_t nnodes, int64_t* vals,
                            int32_t* lens, uint8_t* valid, uint8_t* row_ok, const int32_t* first_child,
                            const int32_t* next_sib, const int32_t* key_word, const int32_t* key_len,
-                           const uint64_t* key_words, void* stream) {
+                           const uint64_t* key_words, int32_t nkey_words, void* stream) {
   if (n <= 0) return 0;
   ParseArgs a{buf, offs, n, lut_keys, lut_node, lut_cap, node_type, val_slot, len_slot, nnodes, vals, lens,
-              valid, row_ok, first_child, next_sib, key_word, key_len, key_words};
+              valid, row_ok, first_child, next_sib, key_word, key_len, key_words, nkey_words};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(valid, 0, (size_t)nnodes * (size_t)n, s);
   if (e != hipSuccess) return (int)e;
   const int block = 256;
   const int64_t grid = (n + block - 1) / block;
-  hipLaunchKernelGGL(json_parse_kernel, dim3((unsigned)grid), dim3(block), 0, s, a);
+  const int64_t tab_bytes = tables_lds_bytes(nnodes, nkey_words, lut_cap);
+  if (tab_bytes <= 24 * 1024)
+    hipLaunchKernelGGL(json_parse_kernel<true>, dim3((unsigned)grid), dim3(block), (size_t)tab_bytes, s, a);
+  else
+    hipLaunchKernelGGL(json_parse_kernel<false>, dim3((unsigned)grid), dim3(block), 0, s, a);
   return (int)hipGetLastError();
 }
 

@@ -221,7 +221,8 @@ def _parse_gpu(buf, offs, n, plan: ParsePlan):
     if n:
         N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
                N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
-               N.ptr(fchild), N.ptr(nsib), N.ptr(kword), N.ptr(klen), N.ptr(kwords), N.stream_handle(buf.device))
+               N.ptr(fchild), N.ptr(nsib), N.ptr(kword), N.ptr(klen), N.ptr(kwords), int(kwords.numel()),
+               N.stream_handle(buf.device))
     nulls = [1] * nn
     if n:
         cnt = torch.empty(nn, dtype=torch.int64, device=buf.device)
