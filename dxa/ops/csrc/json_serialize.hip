@@ -6,6 +6,11 @@
 // Two passes, one lane per row: lengths (no stores) → exclusive scan on the stream → write at exact offsets, so the
 // output is one contiguous blob copied to the host with a single D2H.  Bytes leave through the register-packed
 // 16-B emitter (dxa_emit.h).
+//
+// The column tree is walked by a flat program the host derives from it (one FIELD op per node in preorder, a CLOSE
+// op after each container's children, and for every FIELD the number of ops to jump when the field is omitted):
+// no device recursion (call stacks live in scratch) and comma state is one bit per nesting level in a register.
+// Strings are scanned 8 bytes at a time (SWAR test for bytes needing an escape).
 #include "dxa_common.h"
 #include "dxa_emit.h"
 #include "dxa_ryu.h"
@@ -29,8 +34,8 @@ struct DevNode {
 
 struct SerArgs {
   const DevNode* nodes;
-  const int32_t* top;
-  int32_t ntop;
+  const int32_t* prog;    // 4 ints per op: (code, node, depth, mode | skip << 8)
+  int32_t nprog;
   const uint8_t* text;
   int64_t n;
   int64_t* lens;          // length pass (line length incl. the newline)
@@ -46,10 +51,6 @@ __device__ __forceinline__ bool is_null(const DevNode& nd, int64_t row) {
   return nd.valid != nullptr && nd.valid[row] == 0;
 }
 
-template <bool W>
-__device__ __forceinline__ void put_text(dxa::Emitter<W>& e, const uint8_t* s, int n) {
-  for (int i = 0; i < n; ++i) e.put(s[i]);
-}
 
 template <bool W>
 __device__ void put_u64(dxa::Emitter<W>& e, uint64_t v) {
@@ -112,26 +113,62 @@ __device__ void put_ts(dxa::Emitter<W>& e, int64_t us) {
   e.put('Z'); e.put('"');
 }
 
+#define G1 __attribute__((address_space(1)))
+
+__device__ __forceinline__ uint64_t swar_has(uint64_t x, uint64_t pat) {
+  const uint64_t v = x ^ pat;
+  return (v - 0x0101010101010101ull) & ~v & 0x8080808080808080ull;     // exact for the lowest flagged byte
+}
+
+// 8 bytes at s (aligned loads; an aligned word holding one byte of an allocation is inside it)
+__device__ __forceinline__ uint64_t load8_any(const uint8_t* s) {
+  const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(s) & 7);
+  const G1 uint64_t* w = (const G1 uint64_t*)(s - o);
+  const uint64_t lo = w[0];
+  if (o == 0) return lo;
+  return (lo >> (8 * o)) | (w[1] << (64 - 8 * o));
+}
+
+template <bool W>
+__device__ __forceinline__ void put_escaped(dxa::Emitter<W>& e, uint32_t c) {
+  e.put('\\');
+  switch (c) {
+    case '"': e.put('"'); break;
+    case '\\': e.put('\\'); break;
+    case '\n': e.put('n'); break;
+    case '\r': e.put('r'); break;
+    case '\t': e.put('t'); break;
+    case '\b': e.put('b'); break;
+    case '\f': e.put('f'); break;
+    default: {
+      const uint32_t hi = c >> 4, lo = c & 15;
+      e.put('u'); e.put('0'); e.put('0');
+      e.put((uint8_t)(hi < 10 ? '0' + hi : 'a' + hi - 10));
+      e.put((uint8_t)(lo < 10 ? '0' + lo : 'a' + lo - 10));
+    }
+  }
+}
+
 template <bool W>
 __device__ void put_str(dxa::Emitter<W>& e, const uint8_t* s, int32_t n) {
   e.put('"');
-  for (int32_t i = 0; i < n; ++i) {
-    const uint8_t c = s[i];
-    if (c >= 0x20 && c != '"' && c != '\\') { e.put(c); continue; }
-    e.put('\\');
-    switch (c) {
-      case '"': e.put('"'); break;
-      case '\\': e.put('\\'); break;
-      case '\n': e.put('n'); break;
-      case '\r': e.put('r'); break;
-      case '\t': e.put('t'); break;
-      case '\b': e.put('b'); break;
-      case '\f': e.put('f'); break;
-      default: {
-        const char* hex = "0123456789abcdef";
-        e.put('u'); e.put('0'); e.put('0'); e.put((uint8_t)hex[c >> 4]); e.put((uint8_t)hex[c & 15]);
-      }
+  int32_t i = 0;
+  while (i + 8 <= n) {                                       // 8 bytes per step: escape test by SWAR
+    const uint64_t x = load8_any(s + i);
+    const uint64_t m = ((x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull) |   // < 0x20
+                       swar_has(x, 0x2222222222222222ull) | swar_has(x, 0x5C5C5C5C5C5C5C5Cull);
+    const int j = m ? (int)(__builtin_ctzll(m) >> 3) : 8;
+    for (int t = 0; t < j; ++t) e.put((uint8_t)(x >> (8 * t)));
+    i += j;
+    if (j < 8) {
+      put_escaped(e, (uint32_t)((x >> (8 * j)) & 0xff));
+      ++i;
     }
+  }
+  for (; i < n; ++i) {
+    const uint32_t c = ((const G1 uint8_t*)s)[i];
+    if (c >= 0x20 && c != '"' && c != '\\') e.put((uint8_t)c);
+    else put_escaped(e, c);
   }
   e.put('"');
 }
@@ -139,7 +176,7 @@ __device__ void put_str(dxa::Emitter<W>& e, const uint8_t* s, int32_t n) {
 template <bool W>
 __device__ void put_double(dxa::Emitter<W>& e, double v) {
   // NaN / Infinity are JSON strings in Spark's to_json
-  if (v != v) { put_text(e, (const uint8_t*)"\"NaN\"", 5); return; }
+  if (v != v) { e.put('"'); e.put('N'); e.put('a'); e.put('N'); e.put('"'); return; }
   char buf[32];
   const int n = dxa::ryu::java_double(v, buf, c_ryu_inv, c_ryu_pos);
   const bool inf = buf[n - 1] == 'y';
@@ -148,66 +185,70 @@ __device__ void put_double(dxa::Emitter<W>& e, double v) {
   if (inf) e.put('"');
 }
 
-template <bool W>
-__device__ void put_value(dxa::Emitter<W>& e, const SerArgs& a, const DevNode& nd, int64_t row, int depth);
+enum : int32_t { P_FIELD = 0, P_CLOSE = 1 };
+// FIELD modes: 0 struct member (omitted when null), 1 map member (null written), 2 array element (null written),
+// 3 array element of a filterNull array (omitted when null)
 
 template <bool W>
-__device__ void put_children(dxa::Emitter<W>& e, const SerArgs& a, const DevNode& nd, int64_t row, int depth) {
-  const bool is_array = nd.kind == K_ARRAY;
-  e.put(is_array ? '[' : '{');
-  bool first = true;
-  for (int c = 0; c < nd.nchildren; ++c) {
-    const DevNode& ch = a.nodes[nd.child0 + c];
-    const bool null = is_null(ch, row);
-    if (null && (nd.kind == K_STRUCT || (is_array && nd.drop_nulls))) continue;
-    if (!first) e.put(',');
-    first = false;
-    if (!is_array) {
-      put_text(e, a.text + ch.name_off, ch.name_len);
-      e.put(':');
-    }
-    if (null) put_text(e, (const uint8_t*)"null", 4);
-    else put_value(e, a, ch, row, depth + 1);
-  }
-  e.put(is_array ? ']' : '}');
-}
-
-template <bool W>
-__device__ void put_value(dxa::Emitter<W>& e, const SerArgs& a, const DevNode& nd, int64_t row, int depth) {
-  switch (nd.kind) {
-    case K_I64: put_i64(e, ((const int64_t*)nd.data)[row]); break;
-    case K_F64: put_double(e, ((const double*)nd.data)[row]); break;
-    case K_BOOL:
-      if (((const uint8_t*)nd.data)[row]) put_text(e, (const uint8_t*)"true", 4);
-      else put_text(e, (const uint8_t*)"false", 5);
-      break;
-    case K_STR: put_str(e, nd.arena + nd.starts[row], nd.lens[row]); break;
-    case K_RAW: put_text(e, nd.arena + nd.starts[row], nd.lens[row]); break;
-    case K_TS: put_ts(e, ((const int64_t*)nd.data)[row]); break;
-    case K_DATE: e.put('"'); put_date(e, ((const int64_t*)nd.data)[row]); e.put('"'); break;
-    case K_CONST: put_text(e, a.text + nd.const_off, nd.const_len); break;
-    case K_STRUCT:
-    case K_MAP:
-    case K_ARRAY:
-      if (depth < 16) put_children(e, a, nd, row, depth);
-      break;
-    default: break;
-  }
+__device__ __forceinline__ void put_text(dxa::Emitter<W>& e, const G1 uint8_t* s, int n) {
+  for (int i = 0; i < n; ++i) e.put(s[i]);
 }
 
 template <bool W>
 __device__ int64_t render_row(const SerArgs& a, int64_t row, uint8_t* dst) {
   dxa::Emitter<W> e(dst);
+  const G1 int32_t* prog = (const G1 int32_t*)a.prog;
+  const G1 DevNode* nodes = (const G1 DevNode*)a.nodes;
+  const G1 uint8_t* text = (const G1 uint8_t*)a.text;
   e.put('{');
-  bool first = true;
-  for (int t = 0; t < a.ntop; ++t) {
-    const DevNode& nd = a.nodes[a.top[t]];
-    if (is_null(nd, row)) continue;
-    if (!first) e.put(',');
-    first = false;
-    put_text(e, a.text + nd.name_off, nd.name_len);
-    e.put(':');
-    put_value(e, a, nd, row, 0);
+  uint32_t first = 1u;                                      // bit d: nothing written yet at nesting depth d
+  for (int pc = 0; pc < a.nprog; ++pc) {
+    // four separate loads: copying an int4 (HIP vector class) out of an address-space-1 pointer drops lanes
+    const int code = prog[4 * pc], nidx = prog[4 * pc + 1], depth = prog[4 * pc + 2], mw = prog[4 * pc + 3];
+    if (code == P_CLOSE) {
+      e.put(nodes[nidx].kind == K_ARRAY ? ']' : '}');
+      continue;
+    }
+    const int mode = mw & 0xff;
+    const int skip = mw >> 8;
+    const G1 DevNode& nd = nodes[nidx];
+    const int kind = nd.kind;
+    const bool null = kind == K_NULL || (nd.valid != nullptr && ((const G1 uint8_t*)nd.valid)[row] == 0);
+    if (null && (mode == 0 || mode == 3)) { pc += skip; continue; }
+    if (!((first >> depth) & 1u)) e.put(',');
+    first &= ~(1u << depth);
+    if (mode <= 1) {
+      put_text(e, text + nd.name_off, nd.name_len);
+      e.put(':');
+    }
+    if (null) {
+      e.put('n'); e.put('u'); e.put('l'); e.put('l');
+      pc += skip;
+      continue;
+    }
+    switch (kind) {
+      case K_I64: put_i64(e, ((const G1 int64_t*)nd.data)[row]); break;
+      case K_F64: put_double(e, ((const G1 double*)nd.data)[row]); break;
+      case K_BOOL:
+        if (((const G1 uint8_t*)nd.data)[row]) { e.put('t'); e.put('r'); e.put('u'); e.put('e'); }
+        else { e.put('f'); e.put('a'); e.put('l'); e.put('s'); e.put('e'); }
+        break;
+      case K_STR: put_str(e, nd.arena + ((const G1 int64_t*)nd.starts)[row], ((const G1 int32_t*)nd.lens)[row]); break;
+      case K_RAW:
+        put_text(e, (const G1 uint8_t*)nd.arena + ((const G1 int64_t*)nd.starts)[row],
+                 ((const G1 int32_t*)nd.lens)[row]);
+        break;
+      case K_TS: put_ts(e, ((const G1 int64_t*)nd.data)[row]); break;
+      case K_DATE: e.put('"'); put_date(e, ((const G1 int64_t*)nd.data)[row]); e.put('"'); break;
+      case K_CONST: put_text(e, text + nd.const_off, nd.const_len); break;
+      case K_STRUCT:
+      case K_MAP:
+      case K_ARRAY:
+        e.put(kind == K_ARRAY ? '[' : '{');
+        first |= 1u << (depth + 1);
+        break;
+      default: break;
+    }
   }
   e.put('}');
   e.put('\n');
@@ -243,18 +284,19 @@ const uint64_t h_ryu_pos[2 * DXA_RYU_TABLE_SIZE] = DXA_RYU_POW5_SPLIT_INIT;
 
 DXA_API int dxa_sernode_dev_size() { return (int)sizeof(DevNode); }
 
-DXA_API int dxa_serialize_lengths(const void* nodes, const int32_t* top, int32_t ntop, const uint8_t* text, int64_t n,
+// `prog` / `nprog`: the flat render program (4 ints per op) built by dxa/ops/serialize.py from the node tree.
+DXA_API int dxa_serialize_lengths(const void* nodes, const int32_t* prog, int32_t nprog, const uint8_t* text, int64_t n,
                                   int64_t* lens, void* st) {
   if (n <= 0) return 0;
-  SerArgs a{(const DevNode*)nodes, top, ntop, text, n, lens, nullptr, nullptr};
+  SerArgs a{(const DevNode*)nodes, prog, nprog, text, n, lens, nullptr, nullptr};
   hipLaunchKernelGGL(ser_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, a);
   return (int)hipGetLastError();
 }
 
-DXA_API int dxa_serialize_write(const void* nodes, const int32_t* top, int32_t ntop, const uint8_t* text, int64_t n,
+DXA_API int dxa_serialize_write(const void* nodes, const int32_t* prog, int32_t nprog, const uint8_t* text, int64_t n,
                                 const int64_t* offs, uint8_t* out, void* st) {
   if (n <= 0) return 0;
-  SerArgs a{(const DevNode*)nodes, top, ntop, text, n, nullptr, offs, out};
+  SerArgs a{(const DevNode*)nodes, prog, nprog, text, n, nullptr, offs, out};
   hipLaunchKernelGGL(ser_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, a);
   return (int)hipGetLastError();
 }

@@ -243,6 +243,29 @@ class _DevBuilder:
             return idx
         raise TypeError(f"cannot serialise {col!r}")
 
+    def program(self, top: List[int]) -> List[int]:
+        """Flat render program for json_serialize.hip: preorder FIELD ops (code 0, node, depth, mode | skip << 8) with
+        a CLOSE op (code 1) after each container's children; `skip` = ops to jump when the field is omitted/null.
+        Modes: 0 struct member, 1 map member, 2 array element, 3 filterNull array element."""
+        ops: List[List[int]] = []
+
+        def field(idx: int, depth: int, mode: int):
+            if depth > 30:
+                raise ValueError("JSON nesting deeper than 30 levels")
+            pos = len(ops)
+            ops.append([0, idx, depth, mode])
+            nd = self.nodes[idx]
+            if nd["kind"] in (K_STRUCT, K_MAP, K_ARRAY):
+                cm = {K_STRUCT: 0, K_MAP: 1}.get(nd["kind"], 3 if nd["drop_nulls"] else 2)
+                for j in range(nd["nchildren"]):
+                    field(nd["child0"] + j, depth + 1, cm)
+                ops.append([1, idx, depth, 0])
+            ops[pos][3] = mode | ((len(ops) - pos - 1) << 8)
+
+        for t in top:
+            field(t, 0, 0)
+        return [v for op in ops for v in op]
+
     def device_arrays(self, device):
         arr = (DevNode * max(1, len(self.nodes)))()
         for i, nd in enumerate(self.nodes):
@@ -310,10 +333,12 @@ class Staged:
             b = _DevBuilder()
             top = [b.add(c, nm) for nm, c in zip(self.table.names, self.table.columns)]
             nodes, text = b.device_arrays(dev)
-            top_t = torch.tensor(top, dtype=torch.int32).to(dev)
+            prog = b.program(top)
+            prog_t = torch.tensor(prog or [0], dtype=torch.int32).to(dev)
+            nprog = len(prog) // 4
             st = N.stream_handle(dev)
             lens = torch.empty(max(1, n), dtype=torch.int64, device=dev)
-            N.call("dxa_serialize_lengths", N.ptr(nodes), N.ptr(top_t), len(top), N.ptr(text), n, N.ptr(lens), st)
+            N.call("dxa_serialize_lengths", N.ptr(nodes), N.ptr(prog_t), nprog, N.ptr(text), n, N.ptr(lens), st)
             ends = torch.cumsum(lens[:n], 0)
             offs = ends - lens[:n]
             host_lens = torch.empty(n, dtype=torch.int64, pin_memory=True)
@@ -321,7 +346,7 @@ class Staged:
             side.synchronize()
             total = int(ends[-1].item()) if n else 0
             out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-            N.call("dxa_serialize_write", N.ptr(nodes), N.ptr(top_t), len(top), N.ptr(text), n, N.ptr(offs),
+            N.call("dxa_serialize_write", N.ptr(nodes), N.ptr(prog_t), nprog, N.ptr(text), n, N.ptr(offs),
                    N.ptr(out), st)
             host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
             host.copy_(out[:total], non_blocking=True)
