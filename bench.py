@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--events-per-batch", type=int, default=None, help="events per GPU per micro-batch")
     ap.add_argument("--ref-rows", type=int, default=100_000_000, help="reference table rows (join flow)")
     ap.add_argument("--pool", type=int, default=3, help="distinct pre-generated batches cycled (pinned source)")
+    ap.add_argument("--prefetch", type=int, default=2,
+                    help="batches whose ingest (H2D copy + decode, or generation) is in flight ahead of the one "
+                         "being processed")
     ap.add_argument("--lz4-chunks", type=int, default=4, help="pinned-lz4: copy/decode pipeline depth per batch")
     ap.add_argument("--lz4-level", type=int, default=9,
                     help="pinned-lz4: producer compression level (Kafka compression.lz4.level; 9 is Kafka's default, "
@@ -220,7 +223,7 @@ def main():
             db.record_stream(cur)
             do.record_stream(cur)
         t_s = time.perf_counter()
-        stage(i + 1)
+        stage(i + depth)
         t_p = time.perf_counter()
         m = proc.process_batch(RawBatch(db, do, E), batch_time(i), interval_us)
         if host_trace is not None:
@@ -228,7 +231,9 @@ def main():
         sizes.append(db.shape[0])
         return m
 
-    stage(0)
+    depth = max(1, args.prefetch)
+    for i in range(depth):
+        stage(i)
     for i in range(warmup):
         step(i)
     proc.drain()
@@ -301,7 +306,7 @@ def main():
         "config": {"model": MODEL[flow].format(ref=args.ref_rows), "flow": flow,
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
                    "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,
-                   "source": source, "batch_interval_s": interval_us / 1e6,
+                   "source": source, "ingest_prefetch_batches": depth, "batch_interval_s": interval_us / 1e6,
                    "outputs": "sync" if args.sync_outputs else "pipelined (batch t sinks overlap batch t+1)"},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),

@@ -30,39 +30,37 @@ def decomposable(calls: Dict, ctx) -> bool:
     return True
 
 
-def _partials(call: A.Call, scope, groups: G.Groups, ctx) -> List[Tuple[str, PrimColumn, str]]:
-    """[(partial name suffix, partial column, merge op)] for one aggregate call."""
+def _partials(call: A.Call, scope, ctx) -> List[Tuple[str, Optional[PrimColumn], str, str]]:
+    """[(partial name suffix, input column, aggregate func, merge op)] for one aggregate call; the aggregates of a
+    query are then evaluated together (``G.aggregate_many``)."""
     from .expr import evaluate, predicate_mask
-    n = scope.length
     name = call.name
     if call.star or (name == "count" and not call.args):
-        return [("cnt", G.aggregate(groups, None, "count_star", n), "sum")]
+        return [("cnt", None, "count_star", "sum")]
     arg = materialize(evaluate(call.args[0], scope, ctx))
     if isinstance(arg, ConstColumn):
         arg = arg.materialize()
     if name == "count":
-        return [("cnt", G.aggregate(groups, arg, "count", n), "sum")]
+        return [("cnt", arg, "count", "sum")]
     if name == "count_if":
         m = predicate_mask(arg)
-        return [("cnt", G.aggregate(groups, PrimColumn("long", m.to(torch.int64)), "sum", n), "sum")]
+        return [("cnt", PrimColumn("long", m.to(torch.int64)), "sum", "sum")]
     if name in ("bool_and", "every", "bool_or", "any", "some"):
-        r = G.aggregate(groups, PrimColumn("long", arg.data.to(torch.int64), arg.valid),
-                        "min" if name in ("bool_and", "every") else "max", n)
-        return [("v", r, "min" if name in ("bool_and", "every") else "max")]
+        op = "min" if name in ("bool_and", "every") else "max"
+        return [("v", PrimColumn("long", arg.data.to(torch.int64), arg.valid), op, op)]
     if name in ("first", "first_value", "last", "last_value"):
         f = "first" if name.startswith("first") else "last"
-        return [("v", G.aggregate(groups, arg, f, n), f)]
-    cnt = G.aggregate(groups, arg, "count", n)
+        return [("v", arg, f, f)]
     if name in ("sum", "min", "max"):
-        return [("v", G.aggregate(groups, arg, name, n), name), ("cnt", cnt, "sum")]
+        return [("v", arg, name, name), ("cnt", arg, "count", "sum")]
     if name in ("avg", "mean"):
         x = PrimColumn("double", arg.data.to(torch.float64), arg.valid)
-        return [("s", G.aggregate(groups, x, "sum", n), "sum"), ("cnt", cnt, "sum")]
+        return [("s", x, "sum", "sum"), ("cnt", arg, "count", "sum")]
     # variance family: sum, sum of squares, count
     x = arg.data.to(torch.float64)
-    return [("s", G.aggregate(groups, PrimColumn("double", x, arg.valid), "sum", n), "sum"),
-            ("s2", G.aggregate(groups, PrimColumn("double", x * x, arg.valid), "sum", n), "sum"),
-            ("cnt", cnt, "sum")]
+    return [("s", PrimColumn("double", x, arg.valid), "sum", "sum"),
+            ("s2", PrimColumn("double", x * x, arg.valid), "sum", "sum"),
+            ("cnt", arg, "count", "sum")]
 
 
 def _finish(call: A.Call, merged: Dict[str, PrimColumn]) -> PrimColumn:
@@ -111,14 +109,16 @@ def local_partials(gexprs, keys, aggs: Dict, scope, ctx):
         names.append(nm)
         cols.append(k.take(groups.rep) if groups.ngroups and n else k.take(groups.rep[:0]))
     plan = {}
+    reqs = []
     for ak, call in aggs.items():
-        parts = _partials(call, scope, groups, ctx)
+        parts = _partials(call, scope, ctx)
         plan[ak] = []
-        for suffix, col, op in parts:
+        for suffix, arg, func, op in parts:
             nm = f"__a{len(plan)}_{suffix}"
             plan[ak].append((nm, suffix, op))
             names.append(nm)
-            cols.append(col)
+            reqs.append((arg, func))
+    cols.extend(G.aggregate_many(groups, reqs, n))
     ng_local = groups.ngroups if (gexprs or n) else 0
     if not gexprs and n == 0:
         cols = [c.take(torch.empty(0, dtype=torch.int64, device=dev)) for c in cols]
@@ -147,13 +147,15 @@ def merge_partials(got: Table, plan, key_names: List[str], aggs: Dict, grouped: 
         g2 = _one_group(m, dev)
     ng = g2.ngroups
     out_keys = [got.column(k).take(g2.rep) for k in key_names] if grouped else []
-    finals = {}
-    for ak, call in aggs.items():
-        merged = {}
-        for nm, suffix, op in plan[ak]:
-            c = got.column(nm)
-            merged[suffix] = _empty_merge(c, op, ng, dev) if m == 0 else G.aggregate(g2, c, op, m)
-        finals[ak] = _finish(call, merged)
+    entries = [(ak, nm, suffix, op) for ak in aggs for nm, suffix, op in plan[ak]]
+    if m == 0:
+        vals = [_empty_merge(got.column(nm), op, ng, dev) for _, nm, _, op in entries]
+    else:
+        vals = G.aggregate_many(g2, [(got.column(nm), op) for _, nm, _, op in entries], m)
+    merged_by = {ak: {} for ak in aggs}
+    for (ak, _, suffix, _), v in zip(entries, vals):
+        merged_by[ak][suffix] = v
+    finals = {ak: _finish(call, merged_by[ak]) for ak, call in aggs.items()}
     return out_keys, finals, ng
 
 
@@ -169,10 +171,12 @@ def combine_partials(got: Table, plan, key_names: List[str], grouped: bool) -> T
     for k in key_names:
         names.append(k)
         cols.append(got.column(k).take(g2.rep))
+    reqs = []
     for entries in plan.values():
         for nm, _suffix, op in entries:
             names.append(nm)
-            cols.append(G.aggregate(g2, got.column(nm), op, m))
+            reqs.append((got.column(nm), op))
+    cols.extend(G.aggregate_many(g2, reqs, m))
     t = Table(names, cols, g2.ngroups, dev)
     return t
 

@@ -601,9 +601,7 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
         _collect_aggs(e, ctx, aggs)
     if sel.having is not None:
         _collect_aggs(sel.having, ctx, aggs)
-    subst = {}
-    for k, call in aggs.items():
-        subst[k] = _eval_agg(call, scope, groups, ctx)
+    subst = _eval_aggs(aggs, scope, groups, ctx)
     ng = groups.ngroups
     if n == 0 and not gexprs:
         rep_scope = Scope(scope.names, [ConstColumn(None, c.dtype, 1, dev) for c in scope.cols], scope.quals, 1, dev)
@@ -687,6 +685,32 @@ def _nested_key(col):
     from .serialize import column_json_values
     from .column import strings_from_pylist
     return strings_from_pylist(column_json_values(col), col.device)
+
+
+def _eval_aggs(aggs: Dict, scope: Scope, groups: G.Groups, ctx) -> Dict:
+    """Evaluate a query's aggregate calls.  Plain COUNT / SUM / MIN / MAX / AVG calls are handed to
+    ``G.aggregate_many`` together, so they can share one fused accumulation pass; the rest go one by one."""
+    out = {}
+    batch = []
+    for k, call in aggs.items():
+        name = "avg" if call.name == "mean" else call.name
+        simple = (call.name not in ctx.udafs and not call.distinct and
+                  (call.star or (name == "count" and not call.args) or
+                   (name in ("count", "sum", "min", "max", "avg") and len(call.args) == 1)))
+        if not simple:
+            out[k] = _eval_agg(call, scope, groups, ctx)
+            continue
+        if call.star or not call.args:
+            batch.append((k, None, "count_star"))
+            continue
+        arg = materialize(evaluate(call.args[0], scope, ctx))
+        if isinstance(arg, ConstColumn):
+            arg = arg.materialize()
+        batch.append((k, arg, name))
+    if batch:
+        for (k, _, _), col in zip(batch, G.aggregate_many(groups, [(a, f) for _, a, f in batch], scope.length)):
+            out[k] = col
+    return out
 
 
 def _eval_agg(call: A.Call, scope: Scope, groups: G.Groups, ctx) -> Column:

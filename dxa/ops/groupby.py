@@ -238,3 +238,143 @@ def _host_minmax(groups, col, func, device):
         if b is None or (v < b if func == "min" else v > b):
             best[g] = v
     return column_from_pylist(best, col.dtype, device)
+
+
+# ---- fused aggregation ----------------------------------------------------------------------------------------
+_MA_ADD_U64, _MA_ADD_F64, _MA_MAX = 0, 1, 2
+_MV_COUNT, _MV_I64, _MV_F64, _MV_F64_ORD, _MV_NOT = 0, 1, 2, 3, 4
+_FUSABLE = ("count_star", "count", "sum", "min", "max", "avg", "mean")
+# below this many groups the per-aggregate LDS-privatised kernels win (hot lines would serialise at the memory side)
+FUSED_MIN_GROUPS = 4096
+_MAX_SLOTS = 64
+
+
+def _f64_from_ordered(k: torch.Tensor) -> torch.Tensor:
+    return torch.where(k < 0, k ^ 0x7FFFFFFFFFFFFFFF, k).view(torch.float64)
+
+
+def aggregate_many(groups: Groups, reqs, n: int):
+    """Evaluate several aggregates over the same groups: ``reqs`` is a list of (column or None, func) as for
+    :func:`aggregate`; returns the list of result Columns.
+
+    On the GPU with many groups the simple ones (COUNT, SUM, MIN, MAX, AVG over numeric columns) share one fused
+    pass (``agg_multi_kernel``): one [group][slot] accumulator row, one memory-side atomic request per (row, 8-slot
+    line) instead of one per (row, aggregate); COUNTs over the same validity mask — and the hidden counts of SUM /
+    MIN / MAX / AVG — are computed once.  Everything else goes through :func:`aggregate`."""
+    from ..engine.column import PrimColumn, StrColumn, materialize
+    device = groups.rep.device
+    ng = groups.ngroups
+    if (not _on_gpu(device) or n == 0 or ng < FUSED_MIN_GROUPS or len(reqs) < 2 or
+            n > INT32_MAX):
+        return [aggregate(groups, c, f, n) for c, f in reqs]
+    slots = []                   # (data tensor or None, valid tensor or None, kind, op)
+    keyed = {}
+    keep = []                    # tensors that must outlive the launch (stream-ordered frees make this implicit)
+
+    def slot(key, data, valid, kind, op):
+        s = keyed.get(key)
+        if s is None:
+            s = keyed[key] = len(slots)
+            slots.append((data, valid, kind, op))
+        return s
+
+    def count_slot(valid):
+        return slot(("count", None if valid is None else id(valid)), None, valid, _MV_COUNT, _MA_ADD_F64)
+
+    plan = []
+    for col, func in reqs:
+        if func not in _FUSABLE or len(slots) > _MAX_SLOTS - 3:
+            plan.append(None)
+            continue
+        if func == "count_star":
+            plan.append(("count", count_slot(None), None, None))
+            continue
+        col = materialize(col)
+        if func == "count":
+            plan.append(("count", count_slot(col.valid), None, None))
+            continue
+        if isinstance(col, StrColumn) or not isinstance(col, PrimColumn):
+            plan.append(None)
+            continue
+        data, valid = col.data, col.valid
+        if data.dtype == torch.float32:
+            data = data.to(torch.float64)
+        elif data.dtype != torch.float64:
+            data = data.to(torch.int64)
+        keep.append(data)
+        is_f = data.dtype == torch.float64
+        cnt = count_slot(valid) if valid is not None else None
+        if func in ("avg", "mean"):
+            x = data if is_f else data.to(torch.float64)
+            keep.append(x)
+            s = slot(("sum", id(x), id(valid)), x, valid, _MV_F64, _MA_ADD_F64)
+            plan.append(("avg", s, count_slot(valid), None))
+        elif func == "sum":
+            s = slot(("sum", id(data), id(valid)), data, valid, _MV_F64 if is_f else _MV_I64,
+                     _MA_ADD_F64 if is_f else _MA_ADD_U64)
+            plan.append(("sum", s, cnt, "double" if is_f else "long"))
+        else:
+            kind = (_MV_F64_ORD if is_f else _MV_I64) | (_MV_NOT if func == "min" else 0)
+            s = slot((func, id(data), id(valid)), data, valid, kind, _MA_MAX)
+            plan.append(("f64" if is_f else "i64", s, cnt, col.dtype))
+    if sum(p is not None for p in plan) < 2:
+        return [aggregate(groups, c, f, n) for c, f in reqs]
+    # pack slots into 8-slot lines of one atomic kind each
+    order = []
+    line_ops = []
+    for op in (_MA_ADD_U64, _MA_ADD_F64, _MA_MAX):
+        mine = [i for i, sl in enumerate(slots) if sl[3] == op]
+        for k in range(0, len(mine), 8):
+            chunk = mine[k:k + 8]
+            line_ops.append(op)
+            order.extend(chunk + [None] * (8 - len(chunk)))
+    nlines = len(line_ops)
+    where = {}
+    spec = []
+    for pos, i in enumerate(order):
+        if i is None:
+            spec += [0, 0, -1]                # unused slot of a partly filled line
+            continue
+        where[i] = pos
+        d, v, kind, _ = slots[i]
+        spec += [0 if d is None else d.data_ptr(), 0 if v is None else N.u8(v).data_ptr(), kind]
+    nslots = len(order)
+    while nslots > 0 and order[nslots - 1] is None:
+        nslots -= 1
+    gid = groups.gid if groups.gid.dtype == torch.int32 else groups.gid.to(torch.int32)
+    out = torch.empty((ng, 8 * nlines), dtype=torch.int64, device=device)
+    spec_t = torch.tensor(spec, dtype=torch.int64)
+    ops_t = torch.tensor(line_ops, dtype=torch.int32)
+    N.call("dxa_aggregate_multi", N.ptr(gid), n, ng, nslots, spec_t.data_ptr(), nlines, ops_t.data_ptr(), N.ptr(out),
+           N.stream_handle(device))
+    def col_of(i):
+        v = out[:, where[i]].contiguous()
+        kind = slots[i][2]
+        if kind == _MV_COUNT:
+            return v.view(torch.float64).to(torch.int64)
+        return ~v if kind & _MV_NOT else v
+    res = []
+    for (col, func), p in zip(reqs, plan):
+        if p is None:
+            res.append(aggregate(groups, col, func, n))
+            continue
+        kind, s, c, dt = p
+        if kind == "count":
+            res.append(PrimColumn("long", col_of(s)))
+        elif kind == "avg":
+            cnt_t = col_of(c)
+            tot = col_of(s).view(torch.float64)
+            res.append(PrimColumn("double", tot / cnt_t.clamp(min=1).to(torch.float64), cnt_t > 0))
+        else:
+            v = col_of(s)
+            if kind == "sum":
+                v = v.view(torch.float64) if dt == "double" else v
+                res.append(PrimColumn(dt, v, None if c is None else col_of(c) > 0))
+            else:
+                if kind == "f64":
+                    v = _f64_from_ordered(v)
+                elif dt == "boolean":
+                    v = v.to(torch.bool)
+                res.append(PrimColumn(dt, v, None if c is None else col_of(c) > 0))
+    del keep
+    return res

@@ -109,6 +109,38 @@ def test_groupby_matches_cpu(gpu, ngroups):
                 assert x == y, func
 
 
+@pytest.mark.parametrize("ngroups", [5000, 30000])
+def test_fused_aggregates_match_cpu(gpu, ngroups):
+    """aggregate_many (one fused pass, [group][slot] lines per atomic kind) against the CPU aggregates: nulls,
+    negative / mixed-sign doubles (ordered-bits MIN/MAX), ints, booleans, shared validity masks, >8 slots per kind."""
+    rnd = random.Random(ngroups)
+    n = 60000
+    k = [rnd.randrange(ngroups) for _ in range(n)]
+    v = [None if rnd.random() < 0.03 else rnd.uniform(-1e6, 1e6) * rnd.choice([1, 1e-9]) for _ in range(n)]
+    w = [rnd.choice([-0.5, -3.25, 7.0, 1e300, -1e-300]) for _ in range(n)]
+    iv = [None if rnd.random() < 0.01 else rnd.randint(-2**62, 2**62) for _ in range(n)]
+    bv = [rnd.random() < 0.5 for _ in range(n)]
+    kc = column_from_pylist(k, "long")
+    cols = {"v": column_from_pylist(v, "double"), "w": column_from_pylist(w, "double"),
+            "i": column_from_pylist(iv, "long"), "b": column_from_pylist(bv, "boolean")}
+    reqs = [(None, "count_star")]
+    for nm in ("v", "w", "i"):
+        reqs += [(nm, f) for f in ("sum", "min", "max", "avg", "count")]
+    reqs += [("b", "min"), ("b", "max"), ("v", "sum"), ("w", "max")] + [("w", "sum")] * 9
+    gc = G.group_rows([kc])
+    gg = G.group_rows([kc.to(gpu)])
+    got = G.aggregate_many(gg, [(None if c is None else cols[c].to(gpu), f) for c, f in reqs], n)
+    for (c, f), col in zip(reqs, got):
+        want = G.aggregate(gc, None if c is None else cols[c], f, n).to_pylist()
+        have = col.to_pylist()
+        assert len(want) == len(have) == gc.ngroups
+        for x, y in zip(want, have):
+            if isinstance(x, float):
+                assert y == pytest.approx(x, rel=1e-9, abs=1e-6), (c, f)
+            else:
+                assert x == y, (c, f)
+
+
 @pytest.mark.parametrize("kind", ["inner", "left", "semi", "anti", "full"])
 def test_join_matches_cpu(gpu, kind):
     rnd = random.Random(1)
