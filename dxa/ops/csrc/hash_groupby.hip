@@ -107,6 +107,17 @@ __global__ void verify_i64_kernel(const int64_t* __restrict__ v, const uint8_t* 
   }
 }
 
+// bytes [p, p + avail) (avail <= 8) as one little-endian word, read from the aligned words that overlap them only
+__device__ __forceinline__ uint64_t load_part(const uint8_t* p, int32_t avail) {
+  const uintptr_t x = reinterpret_cast<uintptr_t>(p);
+  const int m = (int)(x & 7);
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(x - m);
+  uint64_t v = q[0] >> (8 * m);
+  if (m && 8 - m < avail) v |= q[1] << (64 - 8 * m);
+  if (avail < 8) v &= (1ull << (8 * avail)) - 1;
+  return v;
+}
+
 __global__ void verify_str_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
                                   const int32_t* __restrict__ lens, const uint8_t* __restrict__ valid,
                                   const int32_t* __restrict__ gid, const int32_t* __restrict__ rep, int64_t n,
@@ -122,8 +133,10 @@ __global__ void verify_str_kernel(const uint8_t* __restrict__ arena, const int64
       else {
         const uint8_t* a = arena + starts[i];
         const uint8_t* b = arena + starts[r];
-        for (int32_t k = 0; k < l; ++k)
-          if (a[k] != b[k]) { diff = true; break; }
+        for (int32_t k = 0; k < l && !diff; k += 8) {
+          const int32_t av = l - k < 8 ? l - k : 8;
+          diff = load_part(a + k, av) != load_part(b + k, av);
+        }
       }
     }
     if (diff) atomicAdd(bad, 1);

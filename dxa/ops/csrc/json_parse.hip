@@ -740,17 +740,28 @@ done:
 #undef expect
 }
 
-// Per-node null counts (one 64-lane ballot per node per wave, one atomic per node per wave) so the host can drop
-// validity masks of columns that turned out complete — every later operator then skips its null handling.
-__global__ __launch_bounds__(256) void null_count_kernel(const uint8_t* __restrict__ valid, int64_t n, int32_t nnodes,
+// Per-node null counts so the host can drop validity masks of columns that turned out complete — every later
+// operator then skips its null handling.  blockIdx.y = node; each lane counts 8 rows from one 8-B word (validity
+// bytes are 0/1: nulls = rows - popcount), a wave sums by shuffles and adds once.
+__global__ __launch_bounds__(256) void null_count_kernel(const uint8_t* __restrict__ valid, int64_t n,
                                                          unsigned long long* __restrict__ nulls) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = row < n;
-  for (int k = 0; k < nnodes; ++k) {
-    const bool isnull = in && valid[(int64_t)k * n + row] == 0;
-    const unsigned long long m = __ballot(isnull);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&nulls[k], (unsigned long long)__popcll(m));
+  const int k = blockIdx.y;
+  const int64_t r0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  unsigned long long cnt = 0;
+  if (r0 < n) {
+    const int32_t avail = n - r0 < 8 ? (int32_t)(n - r0) : 8;
+    const uint8_t* p = valid + (int64_t)k * n + r0;
+    const uintptr_t x = reinterpret_cast<uintptr_t>(p);
+    const int m = (int)(x & 7);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(x - m);
+    uint64_t v = q[0] >> (8 * m);
+    if (m && 8 - m < avail) v |= q[1] << (64 - 8 * m);
+    if (avail < 8) v &= (1ull << (8 * avail)) - 1;
+    cnt = (unsigned long long)(avail - __popcll(v & 0x0101010101010101ull));
   }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&nulls[k], cnt);
 }
 
 // Newline framing: offsets of '\n'-terminated records in a raw byte stream (blob / socket / LZ4-lines sources).
@@ -848,8 +859,9 @@ DXA_API int dxa_null_counts(const uint8_t* valid, int64_t n, int32_t nnodes, uns
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(nulls, 0, sizeof(unsigned long long) * (size_t)nnodes, s);
   if (e != hipSuccess) return (int)e;
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(null_count_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, valid, n, nnodes, nulls);
+  if (n <= 0 || nnodes <= 0) return 0;
+  hipLaunchKernelGGL(null_count_kernel, dim3((unsigned)((n + 2047) / 2048), (unsigned)nnodes), dim3(256), 0, s, valid, n,
+                     nulls);
   return (int)hipGetLastError();
 }
 

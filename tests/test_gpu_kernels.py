@@ -170,6 +170,16 @@ def test_string_ops_match_cpu(gpu):
     ts = strings_from_pylist(["2019-02-28 22:45:00", "2019-02-28T22:45:00Z", "02/28/2019 22:45:00", "bad",
                               "2019-02-28 22:45:00.123", None, "1551394800000", "2019-2-8 1:2:3"], "cpu")
     assert S.to_timestamp(ts).to_pylist() == S.to_timestamp(ts.to(gpu)).to_pylist()
+    # fixed-width fast path (aligned-word reads): every arena alignment, 0-10 fraction digits, near misses
+    forms = ["2019-02-28 22:45:00", "2019-02-28T22:45:00Z", "2019-02-28T22:45:00.5Z", "2019-13-01 00:00:00",
+             "2019-02-28 24:00:00", "2019-02-28X22:45:00", "2019-02-28 22:45:0a", "2019-02-28 22:45:00.",
+             "2019-02-28T22:45:00", "2019-02-28 22:45:00Z", "0001-01-01 00:00:00", "9999-12-31T23:59:59Z"]
+    forms += ["2019-02-28 22:45:00." + "123456789a"[:k] for k in range(1, 11)]
+    vals = []
+    for k, f in enumerate(forms * 8):
+        vals += ["y" * (k % 8), f]
+    ts = strings_from_pylist(vals, "cpu")
+    assert S.to_timestamp(ts).to_pylist() == S.to_timestamp(ts.to(gpu)).to_pylist()
 
 
 def test_full_query_matches_cpu(gpu):
