@@ -41,6 +41,28 @@ class EvalContext:
     device: Any = "cpu"
 
 
+class TakenColumns(list):
+    """``[c.take(idx) for c in cols]`` computed per column on first access: a filtered or grouped scope usually
+    reads a few of its input's columns, so the gathers of the others are never launched."""
+
+    def __init__(self, cols, idx):
+        super().__init__([None] * len(cols))
+        self._src = cols if isinstance(cols, TakenColumns) else list(cols)
+        self._idx = idx
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        v = list.__getitem__(self, i)
+        if v is None:
+            v = self._src[i].take(self._idx)
+            list.__setitem__(self, i, v)
+        return v
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
 class Scope:
     """Columns visible to an expression: (qualifier, name, column) triples over ``length`` rows."""
 

@@ -19,7 +19,8 @@ from ..sql import ast as A
 from ..sql.parser import parse_query
 from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, Table, concat_columns,
                      concat_tables, materialize)
-from .expr import (AGG_FUNCS, EvalContext, EvalError, Scope, cast_column, evaluate, output_name, predicate_mask)
+from .expr import (AGG_FUNCS, EvalContext, EvalError, Scope, TakenColumns, cast_column, evaluate, output_name,
+                   predicate_mask)
 from . import windowfn as W
 from .types import common_type, is_nested
 
@@ -292,7 +293,7 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
             built = catalog.cached_build(ck, lambda: (static[1], J.build_side(rk)))[1]
         li, ri = J.hash_join(lk, rk, kind if kind != "cross" else "inner", built)
     if kind in ("semi", "anti"):
-        out = Scope(left.names, [c.take(li) for c in left.cols], left.quals, int(li.shape[0]), dev)
+        out = Scope(left.names, TakenColumns(left.cols, li), left.quals, int(li.shape[0]), dev)
         out.dist = out_dist
         return out
     cols = []
@@ -307,7 +308,7 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
             m = predicate_mask(evaluate(c, out, ctx))
             pred = m if pred is None else pred & m
         idx = torch.nonzero(pred).flatten()
-        out = Scope(out.names, [c.take(idx) for c in out.cols], out.quals, int(idx.shape[0]), dev)
+        out = Scope(out.names, TakenColumns(out.cols, idx), out.quals, int(idx.shape[0]), dev)
     out.dist = out_dist
     return out
 
@@ -457,7 +458,7 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
             if sel.where is not None:
                 mask = predicate_mask(evaluate(sel.where, scope, ctx))
                 idx = torch.nonzero(mask).flatten()
-                scope = Scope(scope.names, [c.take(idx) for c in scope.cols], scope.quals, int(idx.shape[0]),
+                scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]),
                               scope.device)
             gx = [_resolve_group_expr(g, scope, items) for g in sel.group_by]
             keys = [materialize(evaluate(g, scope, ctx)) for g in gx]
@@ -545,7 +546,7 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     if sel.where is not None:
         mask = predicate_mask(evaluate(sel.where, scope, ctx))
         idx = torch.nonzero(mask).flatten()
-        scope = Scope(scope.names, [c.take(idx) for c in scope.cols], scope.quals, int(idx.shape[0]), scope.device)
+        scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]), scope.device)
         scope.dist = sdist
     items = _expand_items(sel, scope)
     is_agg = bool(sel.group_by) or any(_contains_agg(e, ctx) for e, _ in items) or (
@@ -606,7 +607,7 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
     if n == 0 and not gexprs:
         rep_scope = Scope(scope.names, [ConstColumn(None, c.dtype, 1, dev) for c in scope.cols], scope.quals, 1, dev)
     else:
-        rep_scope = Scope(scope.names, [c.take(groups.rep) for c in scope.cols], scope.quals, ng, dev)
+        rep_scope = Scope(scope.names, TakenColumns(scope.cols, groups.rep), scope.quals, ng, dev)
     m = None
     if sel.having is not None:
         m = predicate_mask(evaluate(sel.having, rep_scope, ctx, subst))
@@ -615,7 +616,7 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
         # window functions see the grouped rows after HAVING (Spark evaluates them last)
         if m is not None:
             keep = torch.nonzero(m).flatten()
-            rep_scope = Scope(rep_scope.names, [c.take(keep) for c in rep_scope.cols], rep_scope.quals,
+            rep_scope = Scope(rep_scope.names, TakenColumns(rep_scope.cols, keep), rep_scope.quals,
                               int(keep.shape[0]), dev)
             subst = {k: c.take(keep) for k, c in subst.items()}
             ng, m = rep_scope.length, None
