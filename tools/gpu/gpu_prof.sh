@@ -1,7 +1,6 @@
 # Kernel-level profiles (kernel trace + stats only) of every bench flow; keeps only the stats CSVs
 set -o pipefail
 mkdir -p gpurun_out/prof
-python -m dxa.ops.build || exit 1
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 for f in groupby join window full; do
