@@ -357,6 +357,10 @@ __global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t
 //     one sequence late (software pipelining), so their load latency overlaps the next header parse.  `done` tracks the output prefix
 //     known complete at the last such wait, so the wait is only taken when a source reaches past it — about
 //     once per `off` bytes (~600 B, one record) for JSON.
+//   * The group width is a template parameter: G = 8 (eight blocks per instruction, a 2-dword window per lane,
+//     4-byte-per-lane match copies) measured 6.07 ms against 4.72 ms for G = 16 on the bench batch (DXA_LZ4_LANES=8
+//     selects it for comparison).
+template <int G>
 __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __restrict__ src,
                                                                const int64_t* __restrict__ comp_off,
                                                                const int32_t* __restrict__ comp_len,
@@ -365,11 +369,15 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
                                                                const int64_t* __restrict__ out_len, int64_t nb,
                                                                uint8_t* __restrict__ dst,
                                                                int32_t* __restrict__ status) {
-  constexpr int G = 16;
+  static_assert(G == 8 || G == 16, "group width");
+  // 64-byte input window = NW dwords per lane; fast-path literals LPL bytes per lane; pipelined matches (<= 32 B)
+  // BPL bytes per lane
+  constexpr int NW = 16 / G, LPL = 16 / G, BPL = 32 / G, LOG_G = G == 8 ? 3 : 4;
+  constexpr int WB = 64, PIPE = 32;
   const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const int gl = (int)(threadIdx.x & (G - 1));
-  const int gbase = (int)((threadIdx.x & 63) & ~(G - 1));             // group's first lane in the wave
-  if (b >= nb) return;                                                 // whole groups exit together
+  const int gbase = (int)((threadIdx.x & 63) & ~(G - 1));
+  if (b >= nb) return;
   const int32_t n = comp_len[b];
   const int64_t cap64 = out_len[b];
   const uint8_t* in = src + comp_off[b];
@@ -384,69 +392,81 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     return;
   }
   const int32_t cap = (int32_t)cap64;
-  // positions are counted from a0 = `in` rounded down to 4 B; frames carry >= 16 readable bytes past a block
   const int32_t shift = (int32_t)(reinterpret_cast<uintptr_t>(in) & 3);
   const uint8_t* a0 = in - shift;
   const int32_t lim = shift + n + 16;
-  auto ld = [&](int32_t w0) -> uint32_t {
-    const int32_t q = w0 + 4 * gl;
-    return (q + 4 <= lim) ? *reinterpret_cast<const uint32_t*>(a0 + q) : 0u;
+  uint32_t X[NW];
+  auto ld = [&](int32_t w0) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int32_t q = w0 + 4 * (gl + G * k);
+      X[k] = (q + 4 <= lim) ? *reinterpret_cast<const uint32_t*>(a0 + q) : 0u;
+    }
   };
-  auto wbyte = [&](uint32_t X, int32_t r) -> uint32_t {               // window byte r (per-lane r allowed)
-    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((gbase + ((r >> 2) & (G - 1))) << 2, (int)X);
+  auto wbyte = [&](int32_t r) -> uint32_t {
+    const int d = (r >> 2) & (G * NW - 1);
+    const int addr = (gbase + (d & (G - 1))) << 2;
+    uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)X[0]);
+    if constexpr (NW == 2) {
+      const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)X[1]);
+      v = (d >> LOG_G) ? v1 : v;
+    }
     return (v >> ((r & 3) * 8)) & 0xffu;
   };
   int32_t xb = 0;
-  uint32_t X = ld(0);
-  auto get = [&](int32_t p) -> uint32_t {                              // general path: byte at position p
-    if (p - xb >= 4 * G) {
+  ld(0);
+  auto get = [&](int32_t p) -> uint32_t {
+    if (p - xb >= WB) {
       xb = p & ~3;
-      X = ld(xb);
+      ld(xb);
     }
-    return wbyte(X, p - xb);
+    return wbyte(p - xb);
   };
   const int32_t iend = shift + n;
   int32_t ip = shift, op = 0, rc = LZ_OK, done = 0;
-  int32_t pdst = 0, pml = 0;                                           // pending (loaded, not yet stored) match
-  uint32_t pv0 = 0, pv1 = 0;
+  int32_t pdst = 0, pml = 0;
+  uint32_t pv[BPL];
+#pragma unroll
+  for (int k = 0; k < BPL; ++k) pv[k] = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < BPL; ++k)
+      if (gl + G * k < pml) out[pdst + G * k + gl] = (uint8_t)pv[k];
+  };
   while (ip < iend) {
-    if (ip - xb > 4 * G - 16) {                                       // keep >= 16 bytes of lookahead
+    if (ip - xb > WB - 16) {
       xb = ip & ~3;
-      X = ld(xb);
+      ld(xb);
     }
     const int32_t r = ip - xb;
-    const uint32_t token = wbyte(X, r);
+    const uint32_t token = wbyte(r);
     int32_t lit = (int32_t)(token >> 4);
     const int32_t mlc = (int32_t)(token & 15);
-    // one match-length extension byte (< 255) is also taken on the fast path: high-compression producers emit
-    // many 19..273-byte matches
-    const uint32_t mext = (mlc == 15 && lit < 15 && r + lit + 4 <= 4 * G) ? wbyte(X, r + lit + 3) : 0u;
-    const int32_t fml = mlc + 4 + (int32_t)mext;                      // match length if on the fast path
-    const int32_t fhdr = lit + 3 + (mlc == 15 ? 1 : 0);               // token + literals + offset (+ ext byte)
-    if (lit < 15 && (mlc < 15 || mext < 255) && r + fhdr <= 4 * G && iend - ip >= fhdr && cap - op >= lit + fml) {
-      // ---- fast path.  The match copy is software-pipelined: this sequence's match bytes (up to 32) are loaded
-      // now and stored during the next sequence (after that one's loads are issued), so the load latency
-      // overlaps the next header parse instead of stalling the group.  A source that reaches into the
-      // still-pending bytes flushes them first.  Longer matches are copied directly.
-      const uint32_t lv = wbyte(X, r + 1 + gl);
-      const int32_t off = (int32_t)(wbyte(X, r + 1 + lit) | (wbyte(X, r + 2 + lit) << 8));
-      if (gl < lit) out[op + gl] = (uint8_t)lv;
+    const uint32_t mext = (mlc == 15 && lit < 15 && r + lit + 4 <= WB) ? wbyte(r + lit + 3) : 0u;
+    const int32_t fml = mlc + 4 + (int32_t)mext;
+    const int32_t fhdr = lit + 3 + (mlc == 15 ? 1 : 0);
+    if (lit < 15 && (mlc < 15 || mext < 255) && r + fhdr <= WB && iend - ip >= fhdr && cap - op >= lit + fml) {
+#pragma unroll
+      for (int k = 0; k < LPL; ++k) {
+        const uint32_t lv = wbyte(r + 1 + G * k + gl);
+        if (gl + G * k < lit) out[op + G * k + gl] = (uint8_t)lv;
+      }
+      const int32_t off = (int32_t)(wbyte(r + 1 + lit) | (wbyte(r + 2 + lit) << 8));
       ip += fhdr;
       op += lit;
       if (off == 0 || off > op) { rc = LZ_OFFSET; break; }
       const int32_t ml = fml;
       const int32_t s0 = op - off;
       const int32_t src_end = s0 + (off < ml ? off : ml);
-      if (pml > 0 && (src_end > pdst || ml > 2 * G)) {                 // source overlaps pending bytes / long copy
-        if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
-        if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
+      if (pml > 0 && (src_end > pdst || ml > PIPE)) {
+        flush();
         pml = 0;
       }
       if (src_end > done) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         done = pml > 0 ? pdst : op;
       }
-      if (ml > 2 * G) {
+      if (ml > PIPE) {
         if (off >= ml) {
           for (int32_t c = 0; c < ml; c += G)
             if (c + gl < ml) out[op + c + gl] = out[s0 + c + gl];
@@ -459,32 +479,28 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
         op += ml;
         continue;
       }
-      uint32_t v0 = 0, v1 = 0;
+      uint32_t v[BPL];
       if (off >= ml) {
-        if (gl < ml) v0 = out[s0 + gl];
-        if (gl + G < ml) v1 = out[s0 + G + gl];
+#pragma unroll
+        for (int k = 0; k < BPL; ++k) v[k] = (gl + G * k < ml) ? out[s0 + G * k + gl] : 0u;
       } else {
         const uint32_t o = (uint32_t)off;
-        if (gl < ml) v0 = out[s0 + (int32_t)((uint32_t)gl % o)];
-        if (gl + G < ml) v1 = out[s0 + (int32_t)((uint32_t)(gl + G) % o)];
+#pragma unroll
+        for (int k = 0; k < BPL; ++k)
+          v[k] = (gl + G * k < ml) ? out[s0 + (int32_t)((uint32_t)(gl + G * k) % o)] : 0u;
       }
-      if (pml > 0) {                                                   // previous sequence's match bytes
-        if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
-        if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
-      }
+      if (pml > 0) flush();
       pdst = op;
       pml = ml;
-      pv0 = v0;
-      pv1 = v1;
+#pragma unroll
+      for (int k = 0; k < BPL; ++k) pv[k] = v[k];
       op += ml;
       continue;
     }
-    if (pml > 0) {                                                     // general path: no pending bytes
-      if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
-      if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
+    if (pml > 0) {
+      flush();
       pml = 0;
     }
-    // ---- general path
     ++ip;
     if (lit == 15) {
       uint32_t e;
@@ -502,7 +518,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       if (c + gl < lit) out[op + c + gl] = a0[ip + c + gl];
     ip += lit;
     op += lit;
-    if (ip >= iend) break;                                             // last sequence: literals only
+    if (ip >= iend) break;
     if (iend - ip < 2) { rc = LZ_TRUNC; break; }
     const int32_t off = (int32_t)(get(ip) | (get(ip + 1) << 8));
     ip += 2;
@@ -536,10 +552,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     }
     op += ml;
   }
-  if (pml > 0) {
-    if (gl < pml) out[pdst + gl] = (uint8_t)pv0;
-    if (gl + G < pml) out[pdst + G + gl] = (uint8_t)pv1;
-  }
+  if (pml > 0) flush();
   if (rc == LZ_OK && op != cap) rc = LZ_SIZE;
   if (gl == 0) status[b] = rc;
 }
@@ -560,12 +573,12 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
                            void* status, void* st) {
   if (nb <= 0) return 0;
   const hipStream_t s = (hipStream_t)st;
-  // DXA_LZ4_LANES selects the decoder for measurements: 16 lanes per block (default), 64 = one wave per block
+  // DXA_LZ4_LANES selects the decoder for measurements: 16 lanes per block (default), 8, 64 = one wave per block
   // with LDS-staged output, 1 = one lane per block
   static const int lanes = [] {
     const char* e = getenv("DXA_LZ4_LANES");
     const int v = e ? atoi(e) : 16;
-    return (v == 1 || v == 16 || v == 64) ? v : 16;
+    return (v == 1 || v == 8 || v == 16 || v == 64) ? v : 16;
   }();
   const uint8_t* s8 = (const uint8_t*)src;
   const int64_t* co = (const int64_t*)comp_off;
@@ -573,10 +586,14 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
   const uint8_t* sd = (const uint8_t*)stored;
   const int64_t* oo = (const int64_t*)out_off;
   const int64_t* ol = (const int64_t*)out_len;
-  if (lanes == 16) {
-    const int64_t threads = nb * 16;
-    hipLaunchKernelGGL(lz4_decode_group_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8, co, cl,
-                       sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status);
+  if (lanes == 8 || lanes == 16) {
+    const int64_t threads = nb * lanes;
+    if (lanes == 8)
+      hipLaunchKernelGGL(lz4_decode_group_kernel<8>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8,
+                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status);
+    else
+      hipLaunchKernelGGL(lz4_decode_group_kernel<16>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8,
+                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status);
     return (int)hipGetLastError();
   }
   const int64_t lb = (max_out + 15) & ~(int64_t)15;         // LDS bytes per wave (16-B aligned slices)
