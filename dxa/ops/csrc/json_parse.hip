@@ -561,8 +561,10 @@ __device__ __forceinline__ bool parse_iso_ts(Reader& rd, int64_t s, int64_t e, i
   return true;
 }
 
+// amdgpu_waves_per_eu(4): the compiler's free choice was 147 VGPRs (3 waves per SIMD); capping at 128 spills 7
+// dwords on cold paths and parses the bench batch in 2.25 ms instead of 2.57 ms (more loads in flight per SIMD).
 template <bool LDS>
-__global__ __launch_bounds__(256) void json_parse_kernel(ParseArgs pa) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void json_parse_kernel(ParseArgs pa) {
   const GArgs a = to_global(pa);
   const Tables<LDS> tb = load_tables<LDS>(a);                   // (LDS: whole workgroup, before any early exit)
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
