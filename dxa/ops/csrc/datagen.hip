@@ -160,7 +160,8 @@ __global__ __launch_bounds__(256) void gen_len_kernel(GenArgs g) {
   g.lens[i] = render<false>(g, i, nullptr);
 }
 
-__global__ __launch_bounds__(256) void gen_write_kernel(GenArgs g) {
+// amdgpu_waves_per_eu(5): 95 VGPRs without spills (the free choice was 102, 4 waves per SIMD).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void gen_write_kernel(GenArgs g) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.n) return;
   render<true>(g, i, g.out + g.offs[i]);
