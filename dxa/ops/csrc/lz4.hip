@@ -360,6 +360,8 @@ __global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t
 //   * The group width is a template parameter: G = 8 (eight blocks per instruction, a 2-dword window per lane,
 //     4-byte-per-lane match copies) measured 6.07 ms against 4.72 ms for G = 16 on the bench batch (DXA_LZ4_LANES=8
 //     selects it for comparison).
+constexpr int kWaitVm0 = 0xF70;                                        // s_waitcnt vmcnt(0) (gfx9 encoding)
+
 template <int G>
 __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __restrict__ src,
                                                                const int64_t* __restrict__ comp_off,
@@ -402,6 +404,11 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       const int32_t q = w0 + 4 * (gl + G * k);
       X[k] = (q + 4 <= lim) ? *reinterpret_cast<const uint32_t*>(a0 + q) : 0u;
     }
+    // wait here, inside the (rare) refill branch, with a wait the compiler can see: otherwise it waits for the
+    // window register where the refill and no-refill paths merge, every sequence (vmcnt retires in order, so that
+    // also drains the pipelined match loads).  Measured neutral on the bench batch (4.72 vs 4.74 ms): the header
+    // chain, not that wait, sets the pace.
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
   };
   auto wbyte = [&](int32_t r) -> uint32_t {
     const int d = (r >> 2) & (G * NW - 1);
@@ -463,7 +470,8 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
         pml = 0;
       }
       if (src_end > done) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        asm volatile("" ::: "memory");
         done = pml > 0 ? pdst : op;
       }
       if (ml > PIPE) {
@@ -538,7 +546,8 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     if (ml > cap - op) { rc = LZ_OVERFLOW; break; }
     const int32_t s0 = op - off;
     if (s0 + (off < ml ? off : ml) > done) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        asm volatile("" ::: "memory");
       done = op;
     }
     if (off >= ml) {
