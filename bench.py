@@ -107,6 +107,10 @@ def main():
         else:
             dist.init_process_group("gloo")                              # CPU rehearsal of the same code path
     on_gpu = device.type == "cuda"
+    numa_cpus = None
+    if on_gpu:
+        from dxa.parallel.affinity import bind_to_device
+        numa_cpus = bind_to_device(local)      # before any pinned buffer: first touch lands on the GPU's socket
 
     from dxa.ops import native
     if on_gpu:
@@ -313,6 +317,7 @@ def main():
         "events_per_sec_per_gpu": value / world,
         "vs_target_1M_events_per_sec_per_gpu": value / world / 1e6,
         "generation_s": round(gen_s, 3),
+        "host_cpus_bound": None if numa_cpus is None else len(numa_cpus),
     }
     if comp_bytes:
         out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)

@@ -32,6 +32,8 @@ def main(argv=None):
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
+        from .parallel.affinity import bind_to_device
+        bind_to_device(local)                  # host threads and pinned staging buffers on the GPU's socket
         from .ops import native
         native.lib()
     else:

@@ -185,3 +185,11 @@ def test_bench_two_ranks_gloo(flow, tmp_path):
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1000 and out["value"] > 0
+
+
+def test_cpulist_parsing_and_cpu_noop():
+    from dxa.parallel.affinity import bind_to_device, parse_cpulist
+    assert parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert parse_cpulist("") == set()
+    if not __import__("torch").cuda.is_available():
+        assert bind_to_device(0) is None          # no GPU: nothing to bind to, affinity untouched
