@@ -788,9 +788,15 @@ __device__ __forceinline__ void nl_masks(const uint8_t* buf, int64_t p, int64_t 
   }
 }
 
+// bit 7 of each byte (nl_bytes) → bit j = byte j
+__device__ __forceinline__ uint32_t nl_pack8(uint64_t m) { return (uint32_t)(((m >> 7) * 0x0102040810204080ull) >> 56); }
+
+// Count pass.  With `bits` it also stores each lane's 16-byte newline mask as 16 bits (1/8 of the input), so the
+// write pass reads the masks instead of the text a second time.
 __global__ __launch_bounds__(256) void count_newlines_kernel(const uint8_t* __restrict__ buf, int64_t len,
                                                              int64_t seg, int64_t nseg,
-                                                             int64_t* __restrict__ counts) {
+                                                             int64_t* __restrict__ counts,
+                                                             uint16_t* __restrict__ bits) {
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nseg) return;                                   // whole waves exit together
@@ -801,15 +807,18 @@ __global__ __launch_bounds__(256) void count_newlines_kernel(const uint8_t* __re
     uint64_t m0, m1;
     nl_masks(buf, p, end, m0, m1);
     c += __popcll(m0) + __popcll(m1);
+    if (bits) bits[p >> 4] = (uint16_t)(nl_pack8(m0) | (nl_pack8(m1) << 8));
   }
   for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o, 64);
   if (lane == 0) counts[s] = c;
 }
 
-__global__ __launch_bounds__(256) void write_newlines_kernel(const uint8_t* __restrict__ buf, int64_t len,
-                                                             int64_t seg, int64_t nseg,
-                                                             const int64_t* __restrict__ base,
-                                                             int64_t* __restrict__ pos, int64_t cap) {
+// Write pass over the packed masks: `pos[k] = position of the k-th newline + delta`.
+__global__ __launch_bounds__(256) void write_newlines_bits_kernel(const uint16_t* __restrict__ bits, int64_t len,
+                                                                  int64_t seg, int64_t nseg,
+                                                                  const int64_t* __restrict__ base,
+                                                                  int64_t* __restrict__ pos, int64_t cap,
+                                                                  int64_t delta) {
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nseg) return;
@@ -818,17 +827,15 @@ __global__ __launch_bounds__(256) void write_newlines_kernel(const uint8_t* __re
   int64_t k = base[s];
   for (int64_t it = beg; it < end; it += 1024) {           // uniform trip count: shuffles see the whole wave
     const int64_t p = it + lane * 16;
-    uint64_t m0, m1;
-    nl_masks(buf, p, end, m0, m1);
-    const uint32_t c = __popcll(m0) + __popcll(m1);
+    uint32_t m = p < end ? bits[p >> 4] : 0u;
+    const uint32_t c = __popc(m);
     uint32_t incl = c;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t v = __shfl_up(incl, o, 64);
       if (lane >= o) incl += v;
     }
     int64_t q = k + (incl - c);
-    while (m0) { const int j = __builtin_ctzll(m0) >> 3; if (q < cap) pos[q] = p + j; ++q; m0 &= m0 - 1; }
-    while (m1) { const int j = __builtin_ctzll(m1) >> 3; if (q < cap) pos[q] = p + 8 + j; ++q; m1 &= m1 - 1; }
+    while (m) { const int j = __builtin_ctz(m); if (q < cap) pos[q] = p + j + delta; ++q; m &= m - 1; }
     k += __shfl(incl, 63, 64);
   }
 }
@@ -867,21 +874,23 @@ DXA_API int dxa_null_counts(const uint8_t* valid, int64_t n, int32_t nnodes, uns
   return (int)hipGetLastError();
 }
 
-DXA_API int dxa_count_newlines(const uint8_t* buf, int64_t len, int64_t seg, int64_t* counts, void* stream) {
+DXA_API int dxa_count_newlines(const uint8_t* buf, int64_t len, int64_t seg, int64_t* counts, uint16_t* bits,
+                               void* stream) {
   if (len <= 0) return 0;
   if (((uintptr_t)buf & 15) || (seg & 1023)) return (int)hipErrorInvalidValue;
   const int64_t nseg = (len + seg - 1) / seg;
   hipLaunchKernelGGL(count_newlines_kernel, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, (hipStream_t)stream, buf,
-                     len, seg, nseg, counts);
+                     len, seg, nseg, counts, bits);
   return (int)hipGetLastError();
 }
 
-DXA_API int dxa_write_newlines(const uint8_t* buf, int64_t len, int64_t seg, const int64_t* base, int64_t* pos,
-                               int64_t cap, void* stream) {
+// `bits` from dxa_count_newlines (same len / seg); writes newline position + delta
+DXA_API int dxa_write_newlines_bits(const uint16_t* bits, int64_t len, int64_t seg, const int64_t* base, int64_t* pos,
+                                    int64_t cap, int64_t delta, void* stream) {
   if (len <= 0) return 0;
-  if (((uintptr_t)buf & 15) || (seg & 1023)) return (int)hipErrorInvalidValue;
+  if (seg & 1023) return (int)hipErrorInvalidValue;
   const int64_t nseg = (len + seg - 1) / seg;
-  hipLaunchKernelGGL(write_newlines_kernel, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, (hipStream_t)stream, buf,
-                     len, seg, nseg, base, pos, cap);
+  hipLaunchKernelGGL(write_newlines_bits_kernel, dim3((unsigned)((nseg + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     bits, len, seg, nseg, base, pos, cap, delta);
   return (int)hipGetLastError();
 }

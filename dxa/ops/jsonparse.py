@@ -172,21 +172,24 @@ def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = No
     if buf.data_ptr() % 16:
         buf = buf.clone()
     counts = torch.empty(max(nseg, 1), dtype=torch.int64, device=dev)
+    # the count pass also keeps a 1-bit-per-byte newline mask, so the write pass reads 1/8 of the text's bytes
+    bits = torch.empty(max((length + 15) // 16, 1), dtype=torch.int16, device=dev)
     st = N.stream_handle(dev)
     if length:
-        N.call("dxa_count_newlines", N.ptr(buf), length, seg, N.ptr(counts), st)
+        N.call("dxa_count_newlines", N.ptr(buf), length, seg, N.ptr(counts), N.ptr(bits), st)
     counts = counts[:nseg]
     base = torch.cumsum(counts, 0) - counts
     total = expected if expected is not None else (int(counts.sum().item()) if nseg else 0)
-    pos = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
-    if length:
-        N.call("dxa_write_newlines", N.ptr(buf), length, seg, N.ptr(base), N.ptr(pos), total, st)
-    pos = pos[:total]
     if expected is not None:
         offs = torch.empty(total + 1, dtype=torch.int64, device=dev)
         offs[:1].zero_()            # a kernel: `offs[0] = 0` is a host-synchronous scalar copy on this stack
-        torch.add(pos, 1, out=offs[1:])
+        if length:                  # record i+1 starts after newline i
+            N.call("dxa_write_newlines_bits", N.ptr(bits), length, seg, N.ptr(base), N.ptr(offs[1:]), total, 1, st)
         return offs
+    pos = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    if length:
+        N.call("dxa_write_newlines_bits", N.ptr(bits), length, seg, N.ptr(base), N.ptr(pos), total, 0, st)
+    pos = pos[:total]
     ends = torch.cat([pos + 1, torch.tensor([length], dtype=torch.int64, device=dev)])
     starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos + 1])
     keep = (ends - starts) > 1  # drop empty lines
