@@ -99,6 +99,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NUMA placement first, from sysfs alone: threads the HIP runtime and RCCL start later inherit the mask, and the
+    # pinned staging buffers are first-touched on the GPU's socket
+    from dxa.parallel.affinity import bind_to_device
+    numa_cpus = bind_to_device(local) if torch.cuda.device_count() > local else None
     device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     if world > 1:
         if device.type == "cuda":
@@ -107,10 +111,6 @@ def main():
         else:
             dist.init_process_group("gloo")                              # CPU rehearsal of the same code path
     on_gpu = device.type == "cuda"
-    numa_cpus = None
-    if on_gpu:
-        from dxa.parallel.affinity import bind_to_device
-        numa_cpus = bind_to_device(local)      # before any pinned buffer: first touch lands on the GPU's socket
 
     from dxa.ops import native
     if on_gpu:
@@ -171,6 +171,7 @@ def main():
         if (on_gpu and source == "pinned-lz4") else None
     staged = {}
     sizes = []
+    framing_checks = []        # device flags: a frame's newline count differed from its producer's record count
 
     def stage(i):
         """Make batch i's raw bytes available in HBM — on a side stream, overlapping batch i-1's processing."""
@@ -192,14 +193,15 @@ def main():
             fr = pool[i % len(pool)]
             if side is None:
                 raw = lz4.decompress_device(fr)
-                staged[i] = (raw, frame_lines_gpu(raw, fr.content_size, expected=E) if on_gpu else
-                             _cpu_lines(raw, fr.content_size), None)
+                offs = (frame_lines_gpu(raw, fr.content_size, expected=E, mismatches=framing_checks) if on_gpu
+                        else _cpu_lines(raw, fr.content_size))
+                staged[i] = (raw, offs, None)
                 return
             # chunked: chunk k's H2D copy overlaps chunk k-1's decode (copy and decode streams)
             raw, _ = ingest.stage(fr)
             ds = ingest.decode_stream
             with torch.cuda.stream(ds):
-                offs = frame_lines_gpu(raw, fr.content_size, expected=E)
+                offs = frame_lines_gpu(raw, fr.content_size, expected=E, mismatches=framing_checks)
                 ev = torch.cuda.Event()
                 ev.record(ds)
             staged[i] = (raw, offs, ev)
@@ -282,6 +284,9 @@ def main():
         dist.all_gather(gathered, lt)
         lat = sorted(float(x) for g in gathered for x in g.tolist())
     lat_sorted = sorted(lat)
+    if framing_checks:
+        from dxa.ops.jsonparse import check_framing
+        check_framing(framing_checks)                      # after the timed region: one host sync
 
     def pct(p):
         if not lat_sorted:

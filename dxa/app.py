@@ -29,11 +29,12 @@ def main(argv=None):
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.device_count() > local:
+        from .parallel.affinity import bind_to_device
+        bind_to_device(local)                  # before the HIP runtime starts threads: they inherit the mask
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
-        from .parallel.affinity import bind_to_device
-        bind_to_device(local)                  # host threads and pinned staging buffers on the GPU's socket
         from .ops import native
         native.lib()
     else:

@@ -18,6 +18,7 @@ from __future__ import annotations
 import copy
 import hashlib
 import json
+import re
 import os
 import threading
 from dataclasses import dataclass, field
@@ -94,6 +95,9 @@ def s300_validate(s: Session):
     g = s.gui
     if not s.flow.get("name"):
         raise ConfigGenerationError("flow name is required")
+    if not re.match(r"^[A-Za-z0-9]+$", str(s.flow["name"])):
+        # names become runtime folder / file names (FlowConfigBuilder.cs:75 keeps only [A-Za-z0-9])
+        raise ConfigGenerationError(f"invalid flow name {s.flow['name']!r}: only letters and digits are allowed")
     inp = g.get("input") or {}
     if inp.get("type", "local").lower() not in INPUT_TYPES:
         raise ConfigGenerationError(f"unsupported input type {inp.get('type')}")

@@ -25,7 +25,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from .sources import Checkpointer, RawBatch, Source, SourceError
+from .sources import Checkpointer, OffsetTrackedSource, RawBatch, Source, SourceError
 
 API_PRODUCE, API_FETCH, API_LIST_OFFSETS, API_METADATA = 0, 1, 2, 3
 API_SASL_HANDSHAKE, API_SASL_AUTH = 17, 36
@@ -380,10 +380,11 @@ class KafkaClient:
         return -1
 
 
-class KafkaSource(Source):
+class KafkaSource(OffsetTrackedSource):
     """Direct Kafka / Event Hubs (Kafka endpoint) stream.  Each rank owns partitions ``i % world == rank``; a batch
-    fetches up to ``max_rate`` records per partition from the committed position; ``commit`` (called after the
-    batch's outputs are written) advances the positions and writes ``offsets.txt``."""
+    fetches up to ``max_rate`` records per partition from the read cursor, which runs ahead of the committed
+    position while the host prefetches; ``commit(bt)`` (called after batch bt's outputs are written) advances the
+    committed positions by exactly that batch's ranges and writes them to ``offsets.txt``."""
     name = "kafka"
 
     def __init__(self, client: KafkaClient, topics: List[str], device, checkpoint_dir: Optional[str] = None,
@@ -394,22 +395,22 @@ class KafkaSource(Source):
         self.device = torch.device(device)
         self.max_rate = max_rate
         self.max_fetches = max_fetches
-        self.ckpt = Checkpointer(checkpoint_dir) if checkpoint_dir else None
+        ckpt = Checkpointer(checkpoint_dir) if checkpoint_dir else None
         meta = client.metadata(topics)
         all_parts = [(t, p) for t in topics for p in meta.get(t, [])]
         self.parts = [tp for i, tp in enumerate(all_parts) if i % world == rank]
-        restored = {} if (self.ckpt is None or flush_existing) else self.ckpt.restore()
-        self.pos: Dict[Tuple[str, int], int] = {}
+        restored = {} if (ckpt is None or flush_existing) else ckpt.restore()
+        pos: Dict[Tuple[str, int], int] = {}
         for t, p in self.parts:
             got = restored.get((t, str(p)))
-            self.pos[(t, p)] = got if got is not None else client.list_offset(t, p, start)
-        self.pending: Dict[Tuple[str, int], Tuple[int, int]] = {}
+            pos[(t, p)] = got if got is not None else client.list_offset(t, p, start)
+        self._init_offsets(pos, ckpt, hub_of=lambda tp: (tp[0], str(tp[1])))
 
     def next_batch(self, batch_time_us: int) -> Optional[RawBatch]:
         vals_list, offs_list = [], []
-        self.pending = {}
+        ranges: Dict[Tuple[str, int], Tuple[int, int]] = {}
         for tp in self.parts:
-            start = self.pos[tp]
+            start = self.fetch_pos[tp]
             cur, got = start, 0
             for _ in range(self.max_fetches):
                 recs, hw = self.client.fetch(tp[0], tp[1], cur)
@@ -428,14 +429,9 @@ class KafkaSource(Source):
                 cur = max(cur, nxt)
                 if cur >= hw or (self.max_rate is not None and got >= self.max_rate):
                     break
-            self.pending[tp] = (start, cur)
+            ranges[tp] = (start, cur)
+        self._record_batch(batch_time_us, ranges)
         return _raw_from_parts(vals_list, offs_list, self.device)
-
-    def commit(self, batch_time_us: int):
-        for tp, (_s, e) in self.pending.items():
-            self.pos[tp] = e
-        if self.ckpt:
-            self.ckpt.write(batch_time_us // 1000, [(t, str(p), s, e) for (t, p), (s, e) in self.pending.items()])
 
     def close(self):
         self.client.close()

@@ -52,6 +52,48 @@ class Source:
         pass
 
 
+class OffsetTrackedSource(Source):
+    """Partitioned source whose reads run ahead of its commits.
+
+    ``StreamingHost(pipeline=True)`` fetches batch t+1 while batch t is still being processed, so the read cursor
+    (``fetch_pos``) and the committed position (``pos``) are distinct: ``next_batch`` advances ``fetch_pos`` at once and
+    records that batch's ``(start, end)`` ranges under its batch time; ``commit(bt)`` pops exactly those ranges and
+    checkpoints them (reference ``EventhubCheckpointer.scala:59-60`` writes one line per partition of the committed
+    batch).  A restart resumes from ``pos`` (the checkpoint), so uncommitted prefetched batches are re-read
+    (at-least-once)."""
+
+    def _init_offsets(self, positions: Dict, ckpt: Optional["Checkpointer"], hub_of=None):
+        self.pos = dict(positions)           # committed
+        self.fetch_pos = dict(positions)     # next record to read
+        self._inflight: "Dict[int, Dict]" = {}
+        self._lock = threading.Lock()
+        self.ckpt = ckpt
+        self._hub_of = hub_of or (lambda key: key)
+
+    def _record_batch(self, batch_time_us: int, ranges: Dict):
+        with self._lock:
+            for k, (_s, e) in ranges.items():
+                self.fetch_pos[k] = e
+            self._inflight[batch_time_us] = ranges
+
+    @property
+    def pending(self) -> Dict:
+        """Ranges of the oldest uncommitted batch (for inspection)."""
+        with self._lock:
+            return dict(self._inflight[min(self._inflight)]) if self._inflight else {}
+
+    def commit(self, batch_time_us: int):
+        with self._lock:
+            ranges = self._inflight.pop(batch_time_us, None)
+            if ranges is None:
+                return
+            for k, (_s, e) in ranges.items():
+                self.pos[k] = max(self.pos.get(k, e), e)
+            if self.ckpt:
+                self.ckpt.write(batch_time_us // 1000,
+                                [(*self._hub_of(k), s, e) for k, (s, e) in ranges.items()])
+
+
 def _to_device_batch(records: Sequence[bytes], device, file_info=None) -> RawBatch:
     buf, offs = frame_records(list(records), device=device, pin=torch.device(device).type == "cuda")
     return RawBatch(buf, offs, len(records), file_info=file_info, source_bytes=int(offs[-1].item()) if records
@@ -205,7 +247,7 @@ class BlobPointerSource(Source):
         return frame_bytes(bytes(blob), self.device, file_info={"inputPath": ";".join(paths)})
 
 
-class PartitionedReplaySource(Source):
+class PartitionedReplaySource(OffsetTrackedSource):
     """Partitioned event log with sequence numbers and reference-format offset checkpoints.
 
     ``partitions``: name → list of event payloads (an in-memory or file-backed log).  ``max_rate`` caps events per
@@ -216,31 +258,26 @@ class PartitionedReplaySource(Source):
                  max_rate: Optional[int] = None, hub: str = "replay", flush_existing: bool = False):
         self.parts = partitions
         self.device = torch.device(device)
-        self.pos = {p: 0 for p in partitions}
-        self.pending: Dict[str, Tuple[int, int]] = {}
         self.max_rate = max_rate
         self.hub = hub
-        self.ckpt = Checkpointer(checkpoint_dir) if checkpoint_dir else None
-        if self.ckpt and not flush_existing:
-            for (name, part), until in self.ckpt.restore().items():
-                if name == hub and part in self.pos:
-                    self.pos[part] = until
+        ckpt = Checkpointer(checkpoint_dir) if checkpoint_dir else None
+        pos = {p: 0 for p in partitions}
+        if ckpt and not flush_existing:
+            for (name, part), until in ckpt.restore().items():
+                if name == hub and part in pos:
+                    pos[part] = until
+        self._init_offsets(pos, ckpt, hub_of=lambda p: (self.hub, p))
 
     def next_batch(self, batch_time_us: int) -> Optional[RawBatch]:
         recs = []
-        self.pending = {}
+        ranges = {}
         for p, log in self.parts.items():
-            start = self.pos[p]
+            start = self.fetch_pos[p]
             end = len(log) if self.max_rate is None else min(len(log), start + self.max_rate)
             recs.extend(log[start:end])
-            self.pending[p] = (start, end)
+            ranges[p] = (start, end)
+        self._record_batch(batch_time_us, ranges)
         return _to_device_batch(recs, self.device)
-
-    def commit(self, batch_time_us: int):
-        for p, (s, e) in self.pending.items():
-            self.pos[p] = e
-        if self.ckpt:
-            self.ckpt.write(batch_time_us // 1000, [(self.hub, p, s, e) for p, (s, e) in self.pending.items()])
 
 
 class Checkpointer:

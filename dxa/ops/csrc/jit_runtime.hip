@@ -56,6 +56,16 @@ DXA_API int dxa_rtc_compile(const char* src, const char* name, const char* arch,
 
 DXA_API void dxa_rtc_free(void* p) { free(p); }
 
+// hipRTC version (major * 1000 + minor): part of the disk cache key of compiled code objects.
+DXA_API int dxa_rtc_version() {
+  int major = 0, minor = 0;
+  if (hiprtcVersion(&major, &minor) != HIPRTC_SUCCESS) return -1;
+  return major * 1000 + minor;
+}
+
+// The fixed compile options of dxa_rtc_compile (before `extra_opt`), for the cache key.
+DXA_API const char* dxa_rtc_options() { return "-O3 -std=c++17"; }
+
 DXA_API int dxa_module_load(const void* image, void** module) {
   return (int)hipModuleLoadData(reinterpret_cast<hipModule_t*>(module), image);
 }

@@ -160,12 +160,17 @@ def frame_records(records: Sequence[bytes], device="cpu", pin: bool = False):
     return buf, o
 
 
-def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = None) -> torch.Tensor:
+def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = None,
+                    mismatches: Optional[list] = None) -> torch.Tensor:
     """Record offsets for '\\n'-delimited data already on the device (newline framing kernels).
 
     With ``expected`` (the producer's record count, e.g. from a batch header) there is no host synchronisation: every
-    record must end with a newline and offsets are ``[0, nl_0 + 1, nl_1 + 1, ...]``.  Without it the count is read
-    back and empty lines are dropped."""
+    record must end with a newline and offsets are ``[0, nl_0 + 1, nl_1 + 1, ...]``.  The count is still verified on
+    the device: if the text holds fewer newlines than ``expected`` the missing offsets are set to ``length`` (empty
+    records, never uninitialised memory), and if it holds more, the extra records are not framed.  Either way a
+    0-d bool device tensor "count differed" is appended to ``mismatches`` when given, for the caller to check at its
+    next synchronisation point (``check_framing``).  Without ``expected`` the count is read back and empty lines are
+    dropped."""
     seg = 1 << 16
     nseg = (length + seg - 1) // seg
     dev = buf.device
@@ -185,6 +190,15 @@ def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = No
         offs[:1].zero_()            # a kernel: `offs[0] = 0` is a host-synchronous scalar copy on this stack
         if length:                  # record i+1 starts after newline i
             N.call("dxa_write_newlines_bits", N.ptr(bits), length, seg, N.ptr(base), N.ptr(offs[1:]), total, 1, st)
+            found = counts.sum()
+            # offsets past the last newline found: empty records at the end of the text
+            offs[1:].masked_fill_(torch.arange(1, total + 1, device=dev) > found, length)
+            if mismatches is not None:
+                mismatches.append(found != total)
+        else:
+            offs[1:].fill_(0)
+            if mismatches is not None:
+                mismatches.append(torch.tensor(total != 0, device=dev))
         return offs
     pos = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
     if length:
@@ -196,6 +210,16 @@ def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = No
     starts, ends = starts[keep], ends[keep]
     # contiguous offsets: record i = [offs[i], offs[i+1]); dropped empty lines only hold whitespace
     return torch.cat([starts, ends[-1:]]) if starts.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
+
+
+def check_framing(mismatches: list):
+    """Raise if any ``frame_lines_gpu(..., expected=..., mismatches=...)`` call saw a record count other than the
+    producer's (one host synchronisation for all of them)."""
+    if mismatches:
+        bad = int(torch.stack([m.reshape(()) for m in mismatches]).sum().item())
+        mismatches.clear()
+        if bad:
+            raise ValueError(f"{bad} framed batch(es) held a different record count than their producer declared")
 
 
 def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan):

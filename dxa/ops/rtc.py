@@ -18,7 +18,7 @@ import subprocess
 import tempfile
 import threading
 from pathlib import Path
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 from . import native as N
 
@@ -45,6 +45,10 @@ def _bind():
     L.dxa_rtc_compile.restype = ctypes.c_int
     L.dxa_rtc_free.argtypes = [p]
     L.dxa_rtc_free.restype = None
+    L.dxa_rtc_version.argtypes = []
+    L.dxa_rtc_version.restype = ctypes.c_int
+    L.dxa_rtc_options.argtypes = []
+    L.dxa_rtc_options.restype = ctypes.c_char_p
     L.dxa_module_load.argtypes = [p, ctypes.POINTER(p)]
     L.dxa_module_load.restype = ctypes.c_int
     L.dxa_module_function.argtypes = [p, ctypes.c_char_p, ctypes.POINTER(p)]
@@ -61,15 +65,30 @@ def cache_dir() -> Path:
     return d
 
 
-def source_digest(src: str) -> str:
-    return hashlib.sha256(f"{ARCH}\0{src}".encode()).hexdigest()[:32]
+_TOOLCHAIN: Optional[str] = None
+# bump when the generated-code ABI (kernel argument layout of dxa/engine/jit.py) changes
+CODEGEN_ABI = 2
+
+
+def toolchain_id() -> str:
+    """hipRTC version + fixed compile options of ``dxa_rtc_compile``: a toolchain upgrade invalidates the cache."""
+    global _TOOLCHAIN
+    if _TOOLCHAIN is None:
+        L = _bind()
+        _TOOLCHAIN = f"hiprtc{L.dxa_rtc_version()}|{L.dxa_rtc_options().decode()}|abi{CODEGEN_ABI}"
+    return _TOOLCHAIN
+
+
+def source_digest(src: str, name: str = "", extra_opts: str = "") -> str:
+    key = f"{ARCH}\0{toolchain_id()}\0{extra_opts}\0{name}\0{src}"
+    return hashlib.sha256(key.encode()).hexdigest()[:32]
 
 
 def compile_code_object(src: str, name: str) -> bytes:
     """hipRTC-compile ``src`` → gfx950 code object bytes (disk-cached by source hash).  Works without a GPU."""
     path = None
     try:
-        path = cache_dir() / f"{source_digest(src)}.co"
+        path = cache_dir() / f"{source_digest(src, name)}.co"
         if path.exists():
             STATS["disk_hits"] += 1
             return path.read_bytes()
@@ -99,7 +118,7 @@ def compile_code_object(src: str, name: str) -> bytes:
 
 def function(src: str, name: str) -> ctypes.c_void_p:
     """Loaded kernel handle for (``src``, ``name``) — compiled and module-loaded once per process."""
-    key = (source_digest(src), name)
+    key = (hashlib.sha256(src.encode()).hexdigest(), name)      # in-process: the toolchain cannot change
     fn = _FUNCS.get(key)
     if fn is not None:
         return fn
@@ -132,7 +151,7 @@ def launch(fn: ctypes.c_void_p, grid: int, block: int, stream: int, args: List[c
 
 def host_compile(src: str) -> ctypes.CDLL:
     """Compile a plain C++ translation unit into a CPU shared object (tests of generated code without a GPU)."""
-    key = source_digest("host\0" + src)
+    key = hashlib.sha256(("host\0" + src).encode()).hexdigest()[:32]
     lib = _HOST.get(key)
     if lib is not None:
         return lib

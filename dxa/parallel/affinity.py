@@ -28,7 +28,62 @@ def parse_cpulist(text: str) -> Set[int]:
     return cpus
 
 
+def _visible_indices() -> Optional[list]:
+    """Physical GPU ordinals exposed to this process (``ROCR_VISIBLE_DEVICES`` applies first, then
+    ``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES`` index into what is left); None = all."""
+    vis = None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None or not v.strip():
+            continue
+        try:
+            ids = [int(x) for x in v.split(",") if x.strip()]
+        except ValueError:               # UUID forms: give up on the sysfs mapping
+            return None
+        vis = ids if vis is None else [vis[i] for i in ids if i < len(vis)]
+    return vis
+
+
+def kfd_pci_path(index: int, topology: str = "/sys/class/kfd/kfd/topology/nodes",
+                 pci_root: str = "/sys/bus/pci/devices") -> Optional[str]:
+    """PCI sysfs folder of HIP device ``index`` from the KFD topology alone (no HIP call, so it can run before the
+    runtime starts any thread): GPU nodes are those with SIMDs, in node order; ``location_id`` packs
+    bus/device/function as ``bus << 8 | dev << 3 | fn``."""
+    try:
+        nodes = sorted((int(n) for n in os.listdir(topology) if n.isdigit()))
+    except OSError:
+        return None
+    gpus = []
+    for n in nodes:
+        props = {}
+        try:
+            with open(os.path.join(topology, str(n), "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0") or 0) > 0:
+            gpus.append(props)
+    vis = _visible_indices()
+    if vis is not None:
+        gpus = [gpus[i] for i in vis if i < len(gpus)]
+    if index >= len(gpus):
+        return None
+    g = gpus[index]
+    try:
+        loc, dom = int(g.get("location_id", "")), int(g.get("domain", "0") or 0)
+    except ValueError:
+        return None
+    bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+    path = os.path.join(pci_root, bdf)
+    return path if os.path.isdir(path) else None
+
+
 def device_pci_path(index: int) -> Optional[str]:
+    path = kfd_pci_path(index)
+    if path is not None:
+        return path
     import torch
     try:
         p = torch.cuda.get_device_properties(index)
@@ -52,8 +107,13 @@ def local_cpus(index: int) -> Optional[Set[int]]:
 
 
 def bind_to_device(index: int) -> Optional[Set[int]]:
-    """Pin this process to the CPUs local to GPU ``index`` (intersected with the CPUs it may use now).  Returns the
-    new CPU set, or None when nothing was changed."""
+    """Pin this process to the CPUs local to GPU ``index`` (intersected with the CPUs it may use now).
+
+    Call it before ``torch.cuda.set_device`` / ``init_process_group``: Linux affinity is per thread and new threads
+    inherit their creator's mask, so binding first places the HIP runtime's and RCCL's helper threads (and the
+    pinned buffers they first-touch) on the GPU's socket.  Threads that already exist are re-bound too (every task
+    of ``/proc/self/task``).  Returns the CPU set the process runs on (also when it already matched), or None when
+    the local CPUs are unknown or binding is disabled (``DXA_NUMA_BIND=0``)."""
     if os.environ.get("DXA_NUMA_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
         return None
     cpus = local_cpus(index)
@@ -61,10 +121,21 @@ def bind_to_device(index: int) -> Optional[Set[int]]:
         return None
     allowed = os.sched_getaffinity(0)
     want = cpus & allowed
-    if not want or want == allowed:
+    if not want:
         return None
+    if want == allowed:
+        return want
     try:
         os.sched_setaffinity(0, want)
     except OSError:
         return None
+    try:
+        tids = [int(t) for t in os.listdir("/proc/self/task")]
+    except OSError:
+        tids = []
+    for tid in tids:
+        try:
+            os.sched_setaffinity(tid, want)
+        except OSError:
+            pass
     return want

@@ -21,9 +21,11 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import threading
 import time
+import uuid
 from typing import Any, Dict, List, Optional
 
 from fastapi import Body, FastAPI, Header, HTTPException, Query, Request
@@ -40,6 +42,28 @@ from .store import DocumentStore
 
 WRITE_ROUTES = {"flow/save", "flow/schedulebatch", "flow/generateconfigs", "flow/startjobs", "flow/restartjobs",
                 "flow/stopjobs", "flow/delete", "job/start", "job/stop", "job/restart", "job/restartallwithretries"}
+
+
+_FLOW_NAME = re.compile(r"^[A-Za-z0-9]+$")
+
+
+def valid_flow_name(display_name: str) -> str:
+    """The reference's ``GenerateValidFlowName`` (FlowConfigBuilder.cs:66-75, EngineEnvironment.cs:165-171): keep
+    ``[A-Za-z0-9]``, lower-case; an empty display name gets a GUID."""
+    if not display_name or not display_name.strip():
+        display_name = uuid.uuid4().hex
+    name = re.sub(r"[^A-Za-z0-9]", "", display_name).lower()
+    if not name:
+        raise ValueError(f"display name '{display_name}' has no alphanumeric characters")
+    return name
+
+
+def check_flow_name(name) -> str:
+    """Flow names become folder and file names (runtime configs, checkpoints, secrets): only ``[A-Za-z0-9]+`` is
+    accepted, so no name can be absolute or climb out of the runtime root."""
+    if not isinstance(name, str) or not _FLOW_NAME.match(name):
+        raise ValueError(f"invalid flow name {name!r}: only letters and digits are allowed")
+    return name
 
 
 def ok(result=None, message=None):
@@ -86,7 +110,7 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
 
     # ---------------------------------------------------------------------------------------------------------------
     def _flow(name: str) -> Dict[str, Any]:
-        f = st.store.get("flows", name)
+        f = st.store.get("flows", check_flow_name(name))
         if f is None:
             raise KeyError(f"flow '{name}' not found")
         return f
@@ -112,8 +136,11 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         flow = body if "gui" in body else {"name": body.get("name"), "gui": body}
         name = flow.get("name") or flow["gui"].get("name")
         if not name:
-            raise ValueError("flow name is required")
-        flow["name"] = name
+            # FlowConfigBuilder.cs:66-75: a new flow's name is its display name reduced to [a-z0-9]
+            name = valid_flow_name(flow["gui"].get("displayName") or flow.get("displayName") or "")
+        flow["name"] = check_flow_name(name)
+        if isinstance(flow.get("gui"), dict) and flow["gui"].get("name"):
+            flow["gui"]["name"] = flow["name"]
         old = st.store.get("flows", name) or {}
         merged = {**old, **flow}
         st.store.upsert("flows", name, merged)
@@ -160,7 +187,7 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
 
     @route("flow/delete")
     def flow_delete(body):
-        name = body if isinstance(body, str) else body.get("name") or body.get("flowName")
+        name = check_flow_name(body if isinstance(body, str) else body.get("name") or body.get("flowName"))
         flow = st.store.get("flows", name) or {}
         for j in flow.get("jobNames", []):
             st.jobs.delete(j)
@@ -168,7 +195,11 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         # DeleteHelper: runtime configs, checkpoints/state and the flow's generated secrets go with it
         import shutil
         from ..config import secrets
-        shutil.rmtree(os.path.join(st.root, "runtime", name), ignore_errors=True)
+        runtime = os.path.realpath(os.path.join(st.root, "runtime"))
+        target = os.path.realpath(os.path.join(runtime, name))
+        if os.path.dirname(target) != runtime:
+            raise ValueError(f"flow runtime folder {target} is outside {runtime}")
+        shutil.rmtree(target, ignore_errors=True)
         secrets.delete_prefix("dxa", f"{name}-")
         return True
 

@@ -82,7 +82,7 @@ def run_parallel(description: str, steps: List[Callable], ctx: Dict[str, Any], i
                  ) -> List[ScenarioResult]:
     def iteration_ctx(i):
         c = dict(ctx)                         # the client is shared; everything an iteration writes is its own
-        c["suffix"] = f"{ctx.get('suffix', '')}-{i}"
+        c["suffix"] = f"{ctx.get('suffix', '')}x{i}"
         return c
     with ThreadPoolExecutor(max_workers=max(1, iterations)) as ex:
         futs = [ex.submit(ScenarioResult(description, steps).run, iteration_ctx(i)) for i in range(iterations)]
@@ -232,7 +232,7 @@ def main(argv=None):
     ap.add_argument("--events", help="sample events file (JSON lines) for schema/LiveQuery steps")
     args = ap.parse_args(argv)
     ctx = {"client": args.url.rstrip("/"), "flow": json.load(open(args.flow, encoding="utf-8-sig")),
-           "suffix": "-" + uuid.uuid4().hex[:6]}
+           "suffix": "x" + uuid.uuid4().hex[:6]}
     if args.events:
         ctx["events"] = [l for l in open(args.events).read().splitlines() if l.strip()]
     steps = [STEPS[s] for s in args.steps.split(",") if s]

@@ -193,3 +193,23 @@ def test_cpulist_parsing_and_cpu_noop():
     assert parse_cpulist("") == set()
     if not __import__("torch").cuda.is_available():
         assert bind_to_device(0) is None          # no GPU: nothing to bind to, affinity untouched
+
+
+def test_kfd_topology_maps_hip_index_to_pci_folder(tmp_path, monkeypatch):
+    """The GPU → PCI mapping comes from the KFD topology alone (usable before the HIP runtime starts)."""
+    from dxa.parallel.affinity import kfd_pci_path
+    topo, pci = tmp_path / "nodes", tmp_path / "pci"
+    # node 0: CPU (no SIMDs); nodes 1, 2: GPUs on buses 0x05 and 0x75 (location_id = bus << 8)
+    for n, simd, loc in ((0, 0, 0), (1, 256, 0x0500), (2, 256, 0x7500)):
+        d = topo / str(n)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simd}\nlocation_id {loc}\ndomain 0\n")
+    for bdf in ("0000:05:00.0", "0000:75:00.0"):
+        (pci / bdf).mkdir(parents=True)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert kfd_pci_path(0, str(topo), str(pci)).endswith("0000:05:00.0")
+    assert kfd_pci_path(1, str(topo), str(pci)).endswith("0000:75:00.0")
+    assert kfd_pci_path(2, str(topo), str(pci)) is None
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert kfd_pci_path(0, str(topo), str(pci)).endswith("0000:75:00.0")

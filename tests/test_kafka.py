@@ -65,17 +65,70 @@ def test_kafka_source_batches_checkpoint_restore(broker, tmp_path):
     assert raw.n == 12                                            # 3 partitions x max_rate 4
     col, ok = parse(raw.buf, raw.offs, ParsePlan(StructType((StructField("p", "long"), StructField("i", "long")))))
     assert sorted(col.child("p").data.tolist()) == [0] * 4 + [1] * 4 + [2] * 4
-    # not committed → the same records again
-    assert src.next_batch(2_000_000).n == 12
+    # the read cursor runs ahead of the commits (prefetch): the next batch is the next 4 per partition
+    raw2 = src.next_batch(2_000_000)
+    assert raw2.n == 12
+    col2, _ = parse(raw2.buf, raw2.offs, ParsePlan(StructType((StructField("p", "long"), StructField("i", "long")))))
+    assert sorted(col2.child("i").data.tolist()) == sorted([4, 1000, 1001, 1002] * 3)
+    src.commit(1_000_000)
+    lines = open(os.path.join(ck, "offsets.txt")).read().splitlines()
+    assert sorted(lines) == ["1000,iot,0,0,4", "1000,iot,1,0,4", "1000,iot,2,0,4"]
     src.commit(2_000_000)
-    assert open(os.path.join(ck, "offsets.txt")).read().splitlines()[0].startswith("2000,iot,")
-    assert src.next_batch(3_000_000).n == 12
-    src.commit(3_000_000)
-    # a restarted source resumes from the checkpoint: 10 - 8 = 2 left per partition
+    lines = open(os.path.join(ck, "offsets.txt")).read().splitlines()
+    assert sorted(lines) == ["2000,iot,0,4,8", "2000,iot,1,4,8", "2000,iot,2,4,8"]
+    assert src.next_batch(3_000_000).n == 6                       # 10 - 8 = 2 left per partition; not committed
+    # a restarted source resumes from the checkpoint: batch 3 was never committed, so it is read again
     src2 = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", ck, max_rate=4)
     assert src2.next_batch(4_000_000).n == 6
     src2.commit(4_000_000)
     assert src2.next_batch(5_000_000).n == 0
+    src2.commit(5_000_000)
+    assert sorted(open(os.path.join(ck, "offsets.txt")).read().splitlines()) == [
+        "5000,iot,0,10,10", "5000,iot,1,10,10", "5000,iot,2,10,10"]
+
+
+class _DeferredProcessor:
+    """Stub processor with pipelined outputs: batch t's completion callback fires while batch t+1 is processed."""
+
+    def __init__(self):
+        self.on_batch_complete = None
+        self.seen = []
+        self._pending = None
+
+    def process_batch(self, raw, bt, interval_us, when=None):
+        from dxa.ops.jsonparse import ParsePlan, parse
+        from dxa.engine.types import StructField, StructType
+        if raw.n:
+            col, _ = parse(raw.buf, raw.offs, ParsePlan(StructType((StructField("p", "long"),
+                                                                    StructField("i", "long")))))
+            self.seen += list(zip(col.child("p").data.tolist(), col.child("i").data.tolist()))
+        if self._pending is not None:
+            self.on_batch_complete(*self._pending)
+        self._pending = (bt, {"n": float(raw.n)})
+        return {}
+
+    def drain(self):
+        if self._pending is not None:
+            self.on_batch_complete(*self._pending)
+            self._pending = None
+
+
+def test_pipelined_host_delivers_every_kafka_record_once(broker, tmp_path):
+    from dxa.engine.host import StreamingHost
+    _produce(broker, 8)
+    ck = str(tmp_path / "ck")
+    src = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", ck, max_rate=3)
+    proc = _DeferredProcessor()
+    host = StreamingHost(proc, src, interval_s=1.0, max_batches=4, realtime=False, pipeline=True)
+    host.run()
+    expected = sorted((p, c * 1000 + i) for p in range(3) for c in range(2) for i in range(4))
+    assert sorted(proc.seen) == expected                          # 24 records, none twice, none skipped
+    assert [m["n"] for m in host.history] == [9.0, 9.0, 6.0, 0.0]
+    # the checkpoint holds the last committed batch's own ranges, and a restart has nothing left to read
+    last = sorted(open(os.path.join(ck, "offsets.txt")).read().splitlines())
+    assert [ln.split(",")[1:] for ln in last] == [["iot", str(p), "8", "8"] for p in range(3)]
+    src2 = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", ck, max_rate=3)
+    assert src2.next_batch(0).n == 0
 
 
 def test_rank_partition_assignment(broker):

@@ -161,6 +161,20 @@ def test_gpu_newline_framing():
     for ln in lines:
         want.append(want[-1] + len(ln) + 1)
     assert offs == want
+    # a producer count that disagrees with the text: missing records are empty (never uninitialised offsets), extra
+    # newlines are not framed, and both are reported through the deferred check
+    from dxa.ops.jsonparse import check_framing
+    checks = []
+    short = frame_lines_gpu(d, len(blob), expected=len(lines) + 5, mismatches=checks).cpu().tolist()
+    assert short == want + [len(blob)] * 5
+    with pytest.raises(ValueError):
+        check_framing(checks)
+    long = frame_lines_gpu(d, len(blob), expected=len(lines) - 3, mismatches=checks).cpu().tolist()
+    assert long == want[:len(lines) - 2]
+    with pytest.raises(ValueError):
+        check_framing(checks)
+    frame_lines_gpu(d, len(blob), expected=len(lines), mismatches=checks)
+    check_framing(checks)
     # counting mode drops empty lines
     offs2 = frame_lines_gpu(d, len(blob)).cpu().tolist()
     recs = [blob[offs2[i]:offs2[i + 1]].strip() for i in range(len(offs2) - 1)]

@@ -166,6 +166,27 @@ def test_flow_crud_and_codegen(client):
     assert client.post("/api/flow/getall", json={}).json()["result"] == []
 
 
+def test_flow_names_cannot_escape_the_runtime_root(client, tmp_path):
+    victim = tmp_path / "victim"
+    victim.mkdir()
+    (victim / "keep.txt").write_text("x")
+    for bad in (str(victim), "../victim", "..", "a/b", "mini.conf", ""):
+        r = client.post("/api/flow/delete", json={"name": bad}).json()
+        assert r["error"] is True, bad
+        f = mini_flow()
+        f["name"] = bad
+        f["gui"]["name"] = bad
+        if bad:
+            assert client.post("/api/flow/save", json=f).json()["error"] is True, bad
+    assert (victim / "keep.txt").exists()
+    # a flow without a name gets its display name reduced to [a-z0-9] (FlowConfigBuilder.cs:66-75)
+    f = mini_flow()
+    f["name"] = ""
+    f["gui"]["name"] = ""
+    f["gui"]["displayName"] = "My IoT / Flow #2"
+    assert client.post("/api/flow/save", json=f).json()["result"]["name"] == "myiotflow2"
+
+
 def test_livequery_kernel(client):
     f = mini_flow()
     client.post("/api/flow/save", json=f)
