@@ -43,6 +43,28 @@ def _run(cmd):
     return r
 
 
+def build_variant(name: str, defines, csrc: Path = CSRC) -> Path:
+    """A/B builds: ``tools/_cmp/libdxa_kernels_<name>.so`` from ``csrc`` with extra ``-D`` defines (loaded by runs
+    with ``DXA_NATIVE_LIB``; tools/gpu/gpu_variants.sh)."""
+    out = HERE.parent.parent / "tools" / "_cmp"
+    out.mkdir(parents=True, exist_ok=True)
+    lib = out / f"libdxa_kernels_{name}.so"
+    flags = [*HIP_FLAGS, *[f"-D{d}" for d in defines]]
+
+    def compile_one(src: Path):
+        obj = out / f"{name}_{src.stem}.o"
+        _run([HIPCC, *flags, "-c", str(src), "-o", str(obj), "-I", str(csrc)])
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(compile_one, sorted(csrc.glob("*.hip"))))
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-lhiprtc", "-o", str(lib)])
+    for o in objs:
+        o.unlink(missing_ok=True)
+    print(f"[dxa.build] built variant {lib}", file=sys.stderr)
+    return lib
+
+
 def build(force: bool = False, verbose: bool = True) -> Path:
     OUT_DIR.mkdir(exist_ok=True)
     hip_srcs = sorted(CSRC.glob("*.hip"))
@@ -77,5 +99,11 @@ def build(force: bool = False, verbose: bool = True) -> Path:
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", help="build tools/_cmp/libdxa_kernels_<VARIANT>.so instead")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for --variant")
+    ap.add_argument("--csrc", default=str(CSRC), help="source folder for --variant")
     args = ap.parse_args()
+    if args.variant:
+        build_variant(args.variant, args.defines, Path(args.csrc))
+        sys.exit(0)
     build(force=args.force)

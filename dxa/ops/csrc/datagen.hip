@@ -33,6 +33,8 @@ struct GenArgs {
   int32_t nops;
   const uint8_t* pool;
   const int32_t* table;   // (off,len) pairs for OP_CHOICE
+  int32_t pool_words;     // pool size in 8-B words (padded)
+  int32_t table_ints;     // table size in int32s
   uint64_t seed;
   int64_t row0;           // global index of the first event (for multi-batch determinism)
   int64_t n;
@@ -47,7 +49,7 @@ __device__ __forceinline__ uint64_t rnd(uint64_t seed, int64_t row, int k) {
   return dxa::fmix64(seed ^ dxa::fmix64((uint64_t)row * dxa::kGold + (uint64_t)k * 0x632BE59BD9B4E019ull));
 }
 
-__device__ void civil(int64_t days, int64_t& y, int& m, int& d) {
+__device__ __forceinline__ void civil(int64_t days, int64_t& y, int& m, int& d) {
   days += 719468;
   const int64_t era = (days >= 0 ? days : days - 146096) / 146097;
   const unsigned doe = (unsigned)(days - era * 146097);
@@ -60,17 +62,32 @@ __device__ void civil(int64_t days, int64_t& y, int& m, int& d) {
   if (m <= 2) ++y;
 }
 
+// little-endian text constants for put_word
+constexpr uint64_t kTrue = 0x65757274ull;          // "true"
+constexpr uint64_t kFalse = 0x65736c6166ull;       // "false"
+constexpr uint64_t kNull = 0x6c6c756eull;          // "null"
+
+// The program tables (ops, literal pool, choice table) as the render loop reads them: staged in LDS by the kernels
+// (uniform reads broadcast from LDS; from global memory the compiler must assume the output stores may alias them
+// and re-issues every read as a vector load).
+struct Tables {
+  const Op* ops;
+  const uint64_t* pool64;   // literal runs and choice strings start 8-B aligned and are zero-padded (datagen.py)
+  const int32_t* table;
+};
+
 template <bool WRITE>
-__device__ int64_t render(const GenArgs& g, int64_t i, uint8_t* dst) {
+__device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int64_t i, uint8_t* dst) {
   dxa::Emitter<WRITE> e(dst);
+  const uint64_t* pool64 = t.pool64;
   const int64_t row = g.row0 + i;
   int skip = 0;
   for (int k = 0; k < g.nops; ++k) {
-    const Op op = g.ops[k];
+    const Op op = t.ops[k];
     if (skip > 0) { --skip; continue; }
     switch (op.code) {
       case OP_LIT:
-        for (int q = 0; q < op.b; ++q) e.put(g.pool[op.a + q]);
+        e.put_text_words(pool64 + (op.a >> 3), op.b);
         break;
       case OP_INT: {
         const uint64_t span = (uint64_t)(op.y - op.x);
@@ -82,25 +99,38 @@ __device__ int64_t render(const GenArgs& g, int64_t i, uint8_t* dst) {
         const double lo = __longlong_as_double(op.x), hi = __longlong_as_double(op.y);
         const double u = (double)(rnd(g.seed, row, k) >> 11) * (1.0 / 9007199254740992.0);
         const double v = lo + u * (hi - lo);
-        int64_t scale = 1;
+        uint64_t scale = 1;
         for (int q = 0; q < op.a; ++q) scale *= 10;
         const int64_t fixed = (int64_t)llround(v * (double)scale);
         const bool neg = fixed < 0;
         const uint64_t af = neg ? (0ull - (uint64_t)fixed) : (uint64_t)fixed;
         if (neg) e.put('-');
-        e.put_u64(af / (uint64_t)scale);
+        // af / scale without a 64-bit software division: a double estimate, corrected by one step either way
+        uint64_t ip;
+        if (af < (1ull << 52)) {
+          ip = (uint64_t)((double)af / (double)scale);
+          if (ip * scale > af) --ip;
+          if ((ip + 1) * scale <= af) ++ip;
+        } else {
+          ip = af / scale;
+        }
+        e.put_u64(ip);
         if (op.a > 0) {
           e.put('.');
-          uint64_t frac = af % (uint64_t)scale;
-          int64_t div = scale / 10;
-          for (int q = 0; q < op.a; ++q) { e.put((uint8_t)('0' + (frac / (uint64_t)div) % 10)); div = div > 1 ? div / 10 : 1; }
+          const uint64_t frac = af - ip * scale;
+          if (op.a <= 8) {
+            e.put_fixed((uint32_t)frac, (uint32_t)op.a);
+          } else {
+            uint64_t div = scale / 10;
+            for (int q = 0; q < op.a; ++q) { e.put((uint8_t)('0' + (frac / div) % 10)); div = div > 1 ? div / 10 : 1; }
+          }
         }
         break;
       }
       case OP_CHOICE: {
         const int idx = (int)(rnd(g.seed, row, k) % (uint64_t)op.b);
-        const int off = g.table[2 * (op.a + idx)], len = g.table[2 * (op.a + idx) + 1];
-        for (int q = 0; q < len; ++q) e.put(g.pool[off + q]);
+        const int off = t.table[2 * (op.a + idx)], len = t.table[2 * (op.a + idx) + 1];
+        e.put_text_words(pool64 + (off >> 3), len);
         break;
       }
       case OP_TS_MS:
@@ -117,7 +147,8 @@ __device__ int64_t render(const GenArgs& g, int64_t i, uint8_t* dst) {
         if (op.a == 0) {
           e.put2(m); e.put('/'); e.put2(d); e.put('/'); e.put_i64(y); e.put(' ');
         } else {
-          e.put_i64(y); e.put('-'); e.put2(m); e.put('-'); e.put2(d); e.put(op.a == 1 ? 'T' : ' ');
+          if (y >= 1000 && y <= 9999) e.put_fixed((uint32_t)y, 4); else e.put_i64(y);
+          e.put('-'); e.put2(m); e.put('-'); e.put2(d); e.put(op.a == 1 ? 'T' : ' ');
         }
         e.put2(hh); e.put(':'); e.put2(mi); e.put(':'); e.put2(ss);
         if (op.a == 1) e.put('Z');
@@ -125,24 +156,28 @@ __device__ int64_t render(const GenArgs& g, int64_t i, uint8_t* dst) {
         break;
       }
       case OP_BOOL:
-        if (rnd(g.seed, row, k) & 1) { e.put('t'); e.put('r'); e.put('u'); e.put('e'); }
-        else { e.put('f'); e.put('a'); e.put('l'); e.put('s'); e.put('e'); }
+        if (rnd(g.seed, row, k) & 1) e.put_word(kTrue, 4);
+        else e.put_word(kFalse, 5);
         break;
       case OP_ALNUM: {
         e.put('"');
         uint64_t r = rnd(g.seed, row, k);
+        uint64_t w = 0;
+        uint32_t nw = 0;
         for (int q = 0; q < op.a; ++q) {
           if ((q & 7) == 7) r = dxa::fmix64(r + q);
           const int c = (int)(r % 62);
           r /= 62;
-          e.put((uint8_t)(c < 10 ? '0' + c : (c < 36 ? 'A' + c - 10 : 'a' + c - 36)));
+          w |= (uint64_t)(c < 10 ? '0' + c : (c < 36 ? 'A' + c - 10 : 'a' + c - 36)) << (8 * nw);
+          if (++nw == 8) { e.put_word(w, 8); w = 0; nw = 0; }
         }
+        if (nw) e.put_word(w, nw);
         e.put('"');
         break;
       }
       case OP_NULLP:
         if ((int)(rnd(g.seed, row, k) % 1000) < op.a) {
-          e.put('n'); e.put('u'); e.put('l'); e.put('l');
+          e.put_word(kNull, 4);
           skip = op.b;
         }
         break;
@@ -154,36 +189,66 @@ __device__ int64_t render(const GenArgs& g, int64_t i, uint8_t* dst) {
   return e.len;
 }
 
-__global__ __launch_bounds__(256) void gen_len_kernel(GenArgs g) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.n) return;
-  g.lens[i] = render<false>(g, i, nullptr);
+// LDS image of the tables: ops (32 B each), pool words, table ints — sizes from the host (lds_bytes)
+__device__ __forceinline__ Tables stage_tables(const GenArgs& g, uint64_t* smem) {
+  const int op_words = g.nops * (int)(sizeof(Op) / 8);
+  const uint64_t* src_ops = reinterpret_cast<const uint64_t*>(g.ops);
+  const uint64_t* src_pool = reinterpret_cast<const uint64_t*>(g.pool);
+  for (int q = threadIdx.x; q < op_words; q += blockDim.x) smem[q] = src_ops[q];
+  uint64_t* pool = smem + op_words;
+  for (int q = threadIdx.x; q < g.pool_words; q += blockDim.x) pool[q] = src_pool[q];
+  int32_t* table = reinterpret_cast<int32_t*>(pool + g.pool_words);
+  for (int q = threadIdx.x; q < g.table_ints; q += blockDim.x) table[q] = g.table[q];
+  __syncthreads();
+  return Tables{reinterpret_cast<const Op*>(smem), pool, table};
 }
 
-// amdgpu_waves_per_eu(5): 95 VGPRs without spills (the free choice was 102, 4 waves per SIMD).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void gen_write_kernel(GenArgs g) {
+__global__ __launch_bounds__(256) void gen_len_kernel(GenArgs g) {
+  extern __shared__ uint64_t smem[];
+  const Tables t = stage_tables(g, smem);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.n) return;
-  render<true>(g, i, g.out + g.offs[i]);
+  g.lens[i] = render<false>(g, t, i, nullptr);
 }
+
+__global__ __launch_bounds__(256) void gen_write_kernel(GenArgs g) {
+  extern __shared__ uint64_t smem[];
+  const Tables t = stage_tables(g, smem);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.n) return;
+  render<true>(g, t, i, g.out + g.offs[i]);
+}
+
+size_t lds_bytes(int32_t nops, int32_t pool_words, int32_t table_ints) {
+  return (size_t)nops * sizeof(Op) + (size_t)pool_words * 8 + (size_t)table_ints * 4;
+}
+
+constexpr size_t kMaxLds = 64 * 1024;
 
 }  // namespace
 
 DXA_API int dxa_datagen_op_size() { return (int)sizeof(Op); }
 
-DXA_API int dxa_datagen_lengths(const void* ops, int32_t nops, const uint8_t* pool, const int32_t* table, uint64_t seed,
-                                int64_t row0, int64_t n, int64_t base_ms, int64_t step_us, int64_t* lens, void* st) {
+DXA_API int dxa_datagen_lengths(const void* ops, int32_t nops, const uint8_t* pool, int32_t pool_words,
+                                const int32_t* table, int32_t table_ints, uint64_t seed, int64_t row0, int64_t n,
+                                int64_t base_ms, int64_t step_us, int64_t* lens, void* st) {
   if (n <= 0) return 0;
-  GenArgs g{(const Op*)ops, nops, pool, table, seed, row0, n, base_ms, step_us, nullptr, nullptr, lens};
-  hipLaunchKernelGGL(gen_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, g);
+  const size_t lds = lds_bytes(nops, pool_words, table_ints);
+  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
+  GenArgs g{(const Op*)ops, nops, pool, table, pool_words, table_ints, seed, row0, n, base_ms, step_us, nullptr,
+            nullptr, lens};
+  hipLaunchKernelGGL(gen_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, g);
   return (int)hipGetLastError();
 }
 
-DXA_API int dxa_datagen_write(const void* ops, int32_t nops, const uint8_t* pool, const int32_t* table, uint64_t seed,
-                              int64_t row0, int64_t n, int64_t base_ms, int64_t step_us, const int64_t* offs,
-                              uint8_t* out, void* st) {
+DXA_API int dxa_datagen_write(const void* ops, int32_t nops, const uint8_t* pool, int32_t pool_words,
+                              const int32_t* table, int32_t table_ints, uint64_t seed, int64_t row0, int64_t n,
+                              int64_t base_ms, int64_t step_us, const int64_t* offs, uint8_t* out, void* st) {
   if (n <= 0) return 0;
-  GenArgs g{(const Op*)ops, nops, pool, table, seed, row0, n, base_ms, step_us, offs, out, nullptr};
-  hipLaunchKernelGGL(gen_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, g);
+  const size_t lds = lds_bytes(nops, pool_words, table_ints);
+  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
+  GenArgs g{(const Op*)ops, nops, pool, table, pool_words, table_ints, seed, row0, n, base_ms, step_us, offs, out,
+            nullptr};
+  hipLaunchKernelGGL(gen_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, g);
   return (int)hipGetLastError();
 }

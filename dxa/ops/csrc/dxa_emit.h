@@ -1,58 +1,196 @@
-// Register-packed byte emitter shared by the device-side text producers (event generator, JSON serializer).
+// Register-packed text emitter shared by the device-side text producers (event generator, JSON serializer).
 #pragma once
 #include "dxa_common.h"
 
+// Full-word stores are ordinary write-back stores by default: a record's 16-B words arrive at one 128-B line over
+// several store instructions, and the L2 merges them into whole-line writes.  Nontemporal stores (DXA_EMIT_NT=1)
+// stream each 16-B piece past the L2 as its own partial-line write: the generator's write pass measured 1.79 ms
+// per 1 M IoT events with them vs 0.77 ms without (tools/gpu/gpu_gen_ab.sh).
+#ifndef DXA_EMIT_NT
+#define DXA_EMIT_NT 0
+#endif
+
 namespace dxa {
 
-// Length pass: counts bytes only.  Write pass: bytes are packed into a 16-byte register word and flushed with one
-// aligned 16-B store (records are contiguous and disjoint, so every aligned word inside a record belongs to exactly
-// one lane); only the unaligned head (< 16 B) and the tail go out as single bytes.  This cuts store instructions
-// ~16x versus byte stores — the write pass was store-issue bound (600-B records, one byte per instruction).
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// Low `n` bytes of w (n in 0..8).
+__device__ __forceinline__ uint64_t low_bytes(uint64_t w, uint32_t n) {
+  return n >= 8 ? w : (w & ((1ull << (8 * n)) - 1ull));
+}
+
+// One lane renders one record into [dst, dst + len).  Records are contiguous and disjoint, so every 16-B aligned
+// word that lies inside a record belongs to that lane alone: the emitter accumulates bytes in a 16-byte register
+// pair (a0, a1) and leaves through one aligned 16-B store per word.  Only the record's first and last partial words
+// (shared with the neighbouring records) go out as naturally aligned 1/2/4/8-B pieces, both in `finish()`: the
+// first word is parked in registers (h0, h1) when it fills, so the per-byte path holds a single store and the
+// piecewise stores are inlined once per kernel, not at every emit site.
+//
+// The unit of input is a word of up to 8 bytes (`put_word`): literal text arrives as 8-B words read from an
+// 8-aligned, zero-padded pool (one load per 8 bytes instead of one byte load per byte), and numbers are formatted
+// into words of digits before they are emitted.  The length pass (WRITE = false) only counts.
 template <bool WRITE>
 struct Emitter {
-  uint8_t* p;
-  int64_t len;
-  int head;            // leading bytes written singly until p + len is 16-B aligned
-  int nacc;            // bytes held in acc
-  uint64_t acc0, acc1;
+  uint8_t* wbase;      // 16-B aligned address of the current word
+  uint8_t* hbase;      // 16-B aligned address of the first word
+  int64_t len;         // bytes emitted so far
+  uint32_t lead;       // bytes of the first word that belong to the previous record (dst & 15)
+  uint32_t nacc;       // bytes of the current word filled (lead included while on the first word)
+  bool first;          // still on the record's first word
+  uint64_t a0, a1;     // current word
+  uint64_t h0, h1;     // the first word, once full (written by finish)
 
-  __device__ __forceinline__ Emitter(uint8_t* dst) : p(dst), len(0), head(0), nacc(0), acc0(0), acc1(0) {
-    if (WRITE) head = (int)((16 - ((uintptr_t)dst & 15)) & 15);
-  }
-  __device__ __forceinline__ void put(uint8_t c) {
+  __device__ __forceinline__ explicit Emitter(uint8_t* dst)
+      : len(0), lead(0), nacc(0), first(true), a0(0), a1(0), h0(0), h1(0) {
     if (WRITE) {
-      if (len < head) {
-        p[len] = c;
+      lead = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
+      wbase = hbase = dst - lead;
+      nacc = lead;
+    } else {
+      wbase = hbase = nullptr;
+    }
+  }
+
+  // bytes [lo, hi) of the word held in (x0, x1), as naturally aligned pieces
+  __device__ __forceinline__ static void store_range(uint8_t* w, uint64_t x0, uint64_t x1, uint32_t lo,
+                                                     uint32_t hi) {
+#pragma unroll 1
+    while (lo < hi) {
+      const uint64_t src = lo < 8 ? x0 : x1;
+      const uint32_t sh = 8 * (lo & 7);
+      if ((lo & 7) == 0 && lo + 8 <= hi) {
+        *reinterpret_cast<uint64_t*>(w + lo) = src;
+        lo += 8;
+      } else if ((lo & 3) == 0 && lo + 4 <= hi) {
+        *reinterpret_cast<uint32_t*>(w + lo) = (uint32_t)(src >> sh);
+        lo += 4;
+      } else if ((lo & 1) == 0 && lo + 2 <= hi) {
+        *reinterpret_cast<uint16_t*>(w + lo) = (uint16_t)(src >> sh);
+        lo += 2;
       } else {
-        if (nacc < 8) acc0 |= (uint64_t)c << (8 * nacc);
-        else acc1 |= (uint64_t)c << (8 * (nacc - 8));
-        if (++nacc == 16) {
-          uint64_t* w = reinterpret_cast<uint64_t*>(p + len - 15);
-          __builtin_nontemporal_store(acc0, w);
-          __builtin_nontemporal_store(acc1, w + 1);
-          acc0 = acc1 = 0;
-          nacc = 0;
-        }
+        w[lo] = (uint8_t)(src >> sh);
+        lo += 1;
       }
     }
-    ++len;
   }
+
+  __device__ __forceinline__ static void store16(uint8_t* w, uint64_t x0, uint64_t x1) {
+    u64x2 v;
+    v.x = x0;
+    v.y = x1;
+#if DXA_EMIT_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(w));
+#else
+    *reinterpret_cast<u64x2*>(w) = v;
+#endif
+  }
+
+  __device__ __forceinline__ void flush_full() {
+    if (first) {
+      h0 = a0;
+      h1 = a1;
+      first = false;
+    } else {
+      store16(wbase, a0, a1);
+    }
+    wbase += 16;
+  }
+
+  // Append the low n bytes of w (n in 0..8; bytes of w above n must be zero).
+  __device__ __forceinline__ void put_word(uint64_t w, uint32_t n) {
+    if (WRITE) {
+      const uint32_t sh = 8 * nacc;       // 0..120
+      uint64_t ov = 0;
+      if (sh < 64) {
+        a0 |= w << sh;
+        if (sh) a1 |= w >> (64 - sh);
+      } else {
+        a1 |= w << (sh - 64);
+        if (sh > 64) ov = w >> (128 - sh);
+      }
+      nacc += n;
+      if (nacc >= 16) {
+        flush_full();
+        a0 = ov;
+        a1 = 0;
+        nacc -= 16;
+      }
+    }
+    len += n;
+  }
+
+  __device__ __forceinline__ void put(uint8_t c) { put_word((uint64_t)c, 1); }
+
+  // Literal text from an 8-B aligned, zero-padded pool (`words` is aligned; bytes past n in the last word are 0).
+  __device__ __forceinline__ void put_text_words(const uint64_t* words, int32_t n) {
+    if (!WRITE) { len += n; return; }
+    int32_t q = 0;
+    for (; q + 8 <= n; q += 8) put_word(words[q >> 3], 8);
+    if (q < n) put_word(words[q >> 3], (uint32_t)(n - q));
+  }
+
   __device__ __forceinline__ void finish() {
     if (WRITE) {
-      uint8_t* q = p + len - nacc;
-      for (int k = 0; k < nacc; ++k) q[k] = (uint8_t)((k < 8 ? acc0 >> (8 * k) : acc1 >> (8 * (k - 8))) & 0xff);
+      if (first) {                       // the record never left its first word
+        if (nacc > lead) store_range(hbase, a0, a1, lead, nacc);
+      } else {
+        if (lead == 0) {
+          store16(hbase, h0, h1);
+        } else {
+          store_range(hbase, h0, h1, lead, 16);
+        }
+        if (nacc) store_range(wbase, a0, a1, 0, nacc);
+      }
     }
   }
-  __device__ __forceinline__ void put_u64(uint64_t v) {
-    char tmp[20];
-    int k = 0;
-    do { tmp[k++] = (char)('0' + v % 10); v /= 10; } while (v);
-    while (k) put((uint8_t)tmp[--k]);
+
+  // ---- numbers --------------------------------------------------------------------------------------------------
+  __device__ __forceinline__ static uint32_t ndigits32(uint32_t x) {
+    return 1u + (x >= 10u) + (x >= 100u) + (x >= 1000u) + (x >= 10000u) + (x >= 100000u) + (x >= 1000000u) +
+           (x >= 10000000u) + (x >= 100000000u) + (x >= 1000000000u);
   }
+
+  // exactly nd (1..8) digits of x (zero-padded)
+  __device__ __forceinline__ void put_fixed(uint32_t x, uint32_t nd) {
+    if (!WRITE) { len += nd; return; }
+    uint64_t w = 0;
+    for (uint32_t i = 0; i < nd; ++i) {        // digit i from the right goes to byte nd-1-i
+      const uint32_t q = x / 10u;
+      w |= (uint64_t)('0' + (x - q * 10u)) << (8 * (nd - 1 - i));
+      x = q;
+    }
+    put_word(w, nd);
+  }
+
+  __device__ __forceinline__ void put_u32(uint32_t x) {
+    if (x < 100000000u) {
+      put_fixed(x, ndigits32(x));
+    } else {
+      const uint32_t hi = x / 100000000u;
+      put_fixed(hi, ndigits32(hi));
+      put_fixed(x - hi * 100000000u, 8);
+    }
+  }
+
+  __device__ __forceinline__ void put_u64(uint64_t v) {
+    if (v <= 0xffffffffull) { put_u32((uint32_t)v); return; }
+    const uint64_t hi = v / 100000000ull;
+    const uint32_t lo = (uint32_t)(v - hi * 100000000ull);
+    if (hi < 100000000ull) {
+      put_fixed((uint32_t)hi, ndigits32((uint32_t)hi));
+    } else {
+      const uint64_t top = hi / 100000000ull;                // < 1845
+      put_fixed((uint32_t)top, ndigits32((uint32_t)top));
+      put_fixed((uint32_t)(hi - top * 100000000ull), 8);
+    }
+    put_fixed(lo, 8);
+  }
+
   __device__ __forceinline__ void put_i64(int64_t v) {
     if (v < 0) { put('-'); put_u64(0ull - (uint64_t)v); } else put_u64((uint64_t)v);
   }
-  __device__ __forceinline__ void put2(int v) { put((uint8_t)('0' + v / 10)); put((uint8_t)('0' + v % 10)); }
+
+  __device__ __forceinline__ void put2(int v) { put_fixed((uint32_t)v, 2); }
 };
 
 }  // namespace dxa

@@ -34,9 +34,11 @@ struct DevNode {
 
 struct SerArgs {
   const DevNode* nodes;
+  int32_t nnodes;
   const int32_t* prog;    // 4 ints per op: (code, node, depth, mode | skip << 8)
   int32_t nprog;
-  const uint8_t* text;
+  const uint8_t* text;    // names and constants, each 8-B aligned and zero-padded (dxa/ops/serialize.py)
+  int32_t text_words;
   int64_t n;
   int64_t* lens;          // length pass (line length incl. the newline)
   const int64_t* offs;    // write pass
@@ -46,31 +48,106 @@ struct SerArgs {
 __constant__ uint64_t c_ryu_inv[2 * DXA_RYU_INV_TABLE_SIZE] = DXA_RYU_POW5_INV_SPLIT_INIT;
 __constant__ uint64_t c_ryu_pos[2 * DXA_RYU_TABLE_SIZE] = DXA_RYU_POW5_SPLIT_INIT;
 
-__device__ __forceinline__ bool is_null(const DevNode& nd, int64_t row) {
-  if (nd.kind == K_NULL) return true;
-  return nd.valid != nullptr && nd.valid[row] == 0;
-}
+#define G1 __attribute__((address_space(1)))
 
+// little-endian text constants for put_word
+constexpr uint64_t kTrue = 0x65757274ull;          // "true"
+constexpr uint64_t kFalse = 0x65736c6166ull;       // "false"
+constexpr uint64_t kNull = 0x6c6c756eull;          // "null"
+constexpr uint64_t kNaN = 0x224e614e22ull;         // "\"NaN\""
+constexpr uint64_t kZeros = 0x3030303030303030ull; // "00000000"
+
+__constant__ uint64_t c_pow10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                                     100000000ull, 1000000000ull, 10000000000ull, 100000000000ull,
+                                     1000000000000ull, 10000000000000ull, 100000000000000ull,
+                                     1000000000000000ull, 10000000000000000ull, 100000000000000000ull,
+                                     1000000000000000000ull, 10000000000000000000ull};
+
+// exactly nd (1..19) digits of x, zero-padded
+template <bool W>
+__device__ __forceinline__ void put_fixed64(dxa::Emitter<W>& e, uint64_t x, uint32_t nd) {
+  if (nd > 16) {
+    const uint64_t hi = x / 10000000000000000ull;
+    e.put_fixed((uint32_t)hi, nd - 16);
+    x -= hi * 10000000000000000ull;
+    nd = 16;
+  }
+  if (nd > 8) {
+    const uint64_t hi = x / 100000000ull;
+    e.put_fixed((uint32_t)hi, nd - 8);
+    e.put_fixed((uint32_t)(x - hi * 100000000ull), 8);
+  } else {
+    e.put_fixed((uint32_t)x, nd);
+  }
+}
 
 template <bool W>
-__device__ void put_u64(dxa::Emitter<W>& e, uint64_t v) {
-  uint64_t p = 1;
-  while (v / p >= 10) p *= 10;
-  for (; p; p /= 10) e.put((uint8_t)('0' + (v / p) % 10));
+__device__ __forceinline__ void put_zeros(dxa::Emitter<W>& e, int k) {
+  for (; k >= 8; k -= 8) e.put_word(kZeros, 8);
+  if (k > 0) e.put_word(dxa::low_bytes(kZeros, (uint32_t)k), (uint32_t)k);
 }
 
+// x / 10^k for k in 1..17 and x < 10^17 without a 64-bit software division: double estimate, then exact correction
+__device__ __forceinline__ uint64_t div_pow10(uint64_t x, int k) {
+  const uint64_t p = c_pow10[k];
+  uint64_t q = (uint64_t)((double)x / (double)p);
+  while (q * p > x) --q;
+  while ((q + 1) * p <= x) ++q;
+  return q;
+}
+
+// Java Double.toString (the text of dxa::ryu::java_double) straight into the emitter: shortest digits from Ryu, then
+// words of digits — no per-character buffer in scratch memory.
 template <bool W>
-__device__ void put_i64(dxa::Emitter<W>& e, int64_t v) {
-  if (v < 0) { e.put('-'); put_u64(e, 0ull - (uint64_t)v); } else put_u64(e, (uint64_t)v);
+__device__ __forceinline__ void put_java_double(dxa::Emitter<W>& e, double v) {
+  if (v != v) { e.put_word(kNaN, 5); return; }                  // Spark's to_json quotes NaN / Infinity
+  uint64_t bits;
+  __builtin_memcpy(&bits, &v, 8);
+  const bool neg = (bits >> 63) != 0;
+  if ((bits & 0x7fffffffffffffffull) == 0x7ff0000000000000ull) {
+    e.put('"');
+    if (neg) e.put('-');
+    e.put_word(0x7974696e69666e49ull, 8);                        // "Infinity"
+    e.put('"');
+    return;
+  }
+  if (neg) e.put('-');
+  if ((bits & 0x7fffffffffffffffull) == 0) { e.put_word(0x302e30ull, 3); return; }   // "0.0"
+  uint64_t d;
+  int32_t ex;
+  dxa::ryu::d2d(v, d, ex, c_ryu_inv, c_ryu_pos);
+  const int len = (int)dxa::ryu::decimal_len(d);
+  const int sci = ex + len - 1;
+  if (sci >= -3 && sci < 7) {
+    const int point = sci + 1;                                   // digits before the decimal point
+    if (point <= 0) {
+      e.put_word(0x2e30ull, 2);                                  // "0."
+      put_zeros(e, -point);
+      put_fixed64(e, d, (uint32_t)len);
+    } else if (point >= len) {
+      put_fixed64(e, d, (uint32_t)len);
+      put_zeros(e, point - len);
+      e.put_word(0x302eull, 2);                                  // ".0"
+    } else {
+      const uint64_t ip = div_pow10(d, len - point);
+      put_fixed64(e, ip, (uint32_t)point);
+      e.put('.');
+      put_fixed64(e, d - ip * c_pow10[len - point], (uint32_t)(len - point));
+    }
+  } else {
+    const uint64_t lead = len > 1 ? div_pow10(d, len - 1) : d;
+    e.put((uint8_t)('0' + lead));
+    e.put('.');
+    if (len > 1) put_fixed64(e, d - lead * c_pow10[len - 1], (uint32_t)(len - 1));
+    else e.put('0');
+    e.put('E');
+    int x = sci;
+    if (x < 0) { e.put('-'); x = -x; }
+    e.put_u32((uint32_t)x);
+  }
 }
 
-template <bool W>
-__device__ __forceinline__ void put2(dxa::Emitter<W>& e, unsigned v) {
-  e.put((uint8_t)('0' + v / 10));
-  e.put((uint8_t)('0' + v % 10));
-}
-
-__device__ void civil(int64_t days, int64_t& y, unsigned& m, unsigned& d) {
+__device__ __forceinline__ void dxa_civil(int64_t days, int64_t& y, unsigned& m, unsigned& d) {
   days += 719468;
   const int64_t era = (days >= 0 ? days : days - 146096) / 146097;
   const unsigned doe = (unsigned)(days - era * 146097);
@@ -84,20 +161,16 @@ __device__ void civil(int64_t days, int64_t& y, unsigned& m, unsigned& d) {
 }
 
 template <bool W>
-__device__ void put_date(dxa::Emitter<W>& e, int64_t days) {
+__device__ __forceinline__ void put_date(dxa::Emitter<W>& e, int64_t days) {
   int64_t y; unsigned m, d;
-  civil(days, y, m, d);
-  if (y >= 0 && y < 10000) {
-    e.put((uint8_t)('0' + y / 1000)); e.put((uint8_t)('0' + y / 100 % 10));
-    e.put((uint8_t)('0' + y / 10 % 10)); e.put((uint8_t)('0' + y % 10));
-  } else {
-    put_i64(e, y);
-  }
-  e.put('-'); put2(e, m); e.put('-'); put2(e, d);
+  dxa_civil(days, y, m, d);
+  if (y >= 0 && y < 10000) e.put_fixed((uint32_t)y, 4);
+  else e.put_i64(y);
+  e.put('-'); e.put2((int)m); e.put('-'); e.put2((int)d);
 }
 
 template <bool W>
-__device__ void put_ts(dxa::Emitter<W>& e, int64_t us) {
+__device__ __forceinline__ void put_ts(dxa::Emitter<W>& e, int64_t us) {
   const int64_t secs = us >= 0 ? us / 1000000 : -((-us + 999999) / 1000000);
   const int64_t frac = us - secs * 1000000;
   const int64_t days = secs >= 0 ? secs / 86400 : -((-secs + 86399) / 86400);
@@ -105,15 +178,11 @@ __device__ void put_ts(dxa::Emitter<W>& e, int64_t us) {
   e.put('"');
   put_date(e, days);
   e.put('T');
-  put2(e, (unsigned)(sod / 3600)); e.put(':'); put2(e, (unsigned)(sod / 60 % 60)); e.put(':');
-  put2(e, (unsigned)(sod % 60));
+  e.put2((int)(sod / 3600)); e.put(':'); e.put2((int)(sod / 60 % 60)); e.put(':'); e.put2((int)(sod % 60));
   e.put('.');
-  const unsigned ms = (unsigned)(frac / 1000);
-  e.put((uint8_t)('0' + ms / 100)); e.put((uint8_t)('0' + ms / 10 % 10)); e.put((uint8_t)('0' + ms % 10));
-  e.put('Z'); e.put('"');
+  e.put_fixed((uint32_t)(frac / 1000), 3);
+  e.put_word(0x225aull, 2);                                      // "Z\""
 }
-
-#define G1 __attribute__((address_space(1)))
 
 __device__ __forceinline__ uint64_t swar_has(uint64_t x, uint64_t pat) {
   const uint64_t v = x ^ pat;
@@ -131,116 +200,121 @@ __device__ __forceinline__ uint64_t load8_any(const uint8_t* s) {
 
 template <bool W>
 __device__ __forceinline__ void put_escaped(dxa::Emitter<W>& e, uint32_t c) {
-  e.put('\\');
+  uint64_t w;
+  uint32_t n = 2;
   switch (c) {
-    case '"': e.put('"'); break;
-    case '\\': e.put('\\'); break;
-    case '\n': e.put('n'); break;
-    case '\r': e.put('r'); break;
-    case '\t': e.put('t'); break;
-    case '\b': e.put('b'); break;
-    case '\f': e.put('f'); break;
+    case '"': w = 0x225cull; break;
+    case '\\': w = 0x5c5cull; break;
+    case '\n': w = 0x6e5cull; break;
+    case '\r': w = 0x725cull; break;
+    case '\t': w = 0x745cull; break;
+    case '\b': w = 0x625cull; break;
+    case '\f': w = 0x665cull; break;
     default: {
       const uint32_t hi = c >> 4, lo = c & 15;
-      e.put('u'); e.put('0'); e.put('0');
-      e.put((uint8_t)(hi < 10 ? '0' + hi : 'a' + hi - 10));
-      e.put((uint8_t)(lo < 10 ? '0' + lo : 'a' + lo - 10));
+      w = 0x3030755cull | ((uint64_t)(hi < 10 ? '0' + hi : 'a' + hi - 10) << 32) |
+          ((uint64_t)(lo < 10 ? '0' + lo : 'a' + lo - 10) << 40);            // \u00XY
+      n = 6;
     }
   }
+  e.put_word(w, n);
 }
 
+// JSON string: 8 bytes per step, SWAR test for bytes that need an escape; clean runs leave as whole words
 template <bool W>
-__device__ void put_str(dxa::Emitter<W>& e, const uint8_t* s, int32_t n) {
+__device__ __forceinline__ void put_str(dxa::Emitter<W>& e, const uint8_t* s, int32_t n) {
   e.put('"');
   int32_t i = 0;
-  while (i + 8 <= n) {                                       // 8 bytes per step: escape test by SWAR
-    const uint64_t x = load8_any(s + i);
+  while (i < n) {
+    uint64_t x = load8_any(s + i);
+    const int32_t avail = n - i < 8 ? n - i : 8;
+    if (avail < 8) x = dxa::low_bytes(x, (uint32_t)avail) | (0x2020202020202020ull << (8 * avail));  // pad: clean
     const uint64_t m = ((x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull) |   // < 0x20
                        swar_has(x, 0x2222222222222222ull) | swar_has(x, 0x5C5C5C5C5C5C5C5Cull);
-    const int j = m ? (int)(__builtin_ctzll(m) >> 3) : 8;
-    for (int t = 0; t < j; ++t) e.put((uint8_t)(x >> (8 * t)));
+    int j = m ? (int)(__builtin_ctzll(m) >> 3) : 8;
+    if (j > avail) j = avail;
+    if (j) e.put_word(dxa::low_bytes(x, (uint32_t)j), (uint32_t)j);
     i += j;
-    if (j < 8) {
+    if (j < avail) {
       put_escaped(e, (uint32_t)((x >> (8 * j)) & 0xff));
       ++i;
     }
   }
-  for (; i < n; ++i) {
-    const uint32_t c = ((const G1 uint8_t*)s)[i];
-    if (c >= 0x20 && c != '"' && c != '\\') e.put((uint8_t)c);
-    else put_escaped(e, c);
-  }
   e.put('"');
 }
 
+// raw (already JSON) text from an arbitrary address
 template <bool W>
-__device__ void put_double(dxa::Emitter<W>& e, double v) {
-  // NaN / Infinity are JSON strings in Spark's to_json
-  if (v != v) { e.put('"'); e.put('N'); e.put('a'); e.put('N'); e.put('"'); return; }
-  char buf[32];
-  const int n = dxa::ryu::java_double(v, buf, c_ryu_inv, c_ryu_pos);
-  const bool inf = buf[n - 1] == 'y';
-  if (inf) e.put('"');
-  for (int i = 0; i < n; ++i) e.put((uint8_t)buf[i]);
-  if (inf) e.put('"');
+__device__ __forceinline__ void put_raw(dxa::Emitter<W>& e, const uint8_t* s, int32_t n) {
+  int32_t i = 0;
+  for (; i + 8 <= n; i += 8) e.put_word(load8_any(s + i), 8);
+  if (i < n) e.put_word(dxa::low_bytes(load8_any(s + i), (uint32_t)(n - i)), (uint32_t)(n - i));
 }
 
 enum : int32_t { P_FIELD = 0, P_CLOSE = 1 };
 // FIELD modes: 0 struct member (omitted when null), 1 map member (null written), 2 array element (null written),
 // 3 array element of a filterNull array (omitted when null)
 
-template <bool W>
-__device__ __forceinline__ void put_text(dxa::Emitter<W>& e, const G1 uint8_t* s, int n) {
-  for (int i = 0; i < n; ++i) e.put(s[i]);
+// The render tables as the row loop reads them: staged in LDS per workgroup (uniform reads broadcast from LDS; from
+// global memory the compiler must assume the output stores may alias them and re-issues every read as a vector load).
+struct Tables {
+  const int32_t* prog;
+  const DevNode* nodes;
+  const uint64_t* text64;
+};
+
+__device__ __forceinline__ Tables stage_tables(const SerArgs& a, uint64_t* smem) {
+  const int node_words = a.nnodes * (int)(sizeof(DevNode) / 8);
+  const int prog_words = (a.nprog * 4 + 1) / 2;
+  const uint64_t* src_nodes = reinterpret_cast<const uint64_t*>(a.nodes);
+  const uint64_t* src_prog = reinterpret_cast<const uint64_t*>(a.prog);
+  const uint64_t* src_text = reinterpret_cast<const uint64_t*>(a.text);
+  for (int q = threadIdx.x; q < node_words; q += blockDim.x) smem[q] = src_nodes[q];
+  uint64_t* prog = smem + node_words;
+  for (int q = threadIdx.x; q < prog_words; q += blockDim.x) prog[q] = src_prog[q];
+  uint64_t* text = prog + prog_words;
+  for (int q = threadIdx.x; q < a.text_words; q += blockDim.x) text[q] = src_text[q];
+  __syncthreads();
+  return Tables{reinterpret_cast<const int32_t*>(prog), reinterpret_cast<const DevNode*>(smem), text};
 }
 
 template <bool W>
-__device__ int64_t render_row(const SerArgs& a, int64_t row, uint8_t* dst) {
+__device__ __forceinline__ int64_t render_row(const SerArgs& a, const Tables& t, int64_t row, uint8_t* dst) {
   dxa::Emitter<W> e(dst);
-  const G1 int32_t* prog = (const G1 int32_t*)a.prog;
-  const G1 DevNode* nodes = (const G1 DevNode*)a.nodes;
-  const G1 uint8_t* text = (const G1 uint8_t*)a.text;
   e.put('{');
   uint32_t first = 1u;                                      // bit d: nothing written yet at nesting depth d
   for (int pc = 0; pc < a.nprog; ++pc) {
-    // four separate loads: copying an int4 (HIP vector class) out of an address-space-1 pointer drops lanes
-    const int code = prog[4 * pc], nidx = prog[4 * pc + 1], depth = prog[4 * pc + 2], mw = prog[4 * pc + 3];
+    const int code = t.prog[4 * pc], nidx = t.prog[4 * pc + 1], depth = t.prog[4 * pc + 2], mw = t.prog[4 * pc + 3];
+    const DevNode& nd = t.nodes[nidx];
+    const int kind = nd.kind;
     if (code == P_CLOSE) {
-      e.put(nodes[nidx].kind == K_ARRAY ? ']' : '}');
+      e.put(kind == K_ARRAY ? ']' : '}');
       continue;
     }
     const int mode = mw & 0xff;
     const int skip = mw >> 8;
-    const G1 DevNode& nd = nodes[nidx];
-    const int kind = nd.kind;
     const bool null = kind == K_NULL || (nd.valid != nullptr && ((const G1 uint8_t*)nd.valid)[row] == 0);
     if (null && (mode == 0 || mode == 3)) { pc += skip; continue; }
     if (!((first >> depth) & 1u)) e.put(',');
     first &= ~(1u << depth);
-    if (mode <= 1) {
-      put_text(e, text + nd.name_off, nd.name_len);
-      e.put(':');
-    }
+    if (mode <= 1) e.put_text_words(t.text64 + (nd.name_off >> 3), nd.name_len);     // "name": (colon included)
     if (null) {
-      e.put('n'); e.put('u'); e.put('l'); e.put('l');
+      e.put_word(kNull, 4);
       pc += skip;
       continue;
     }
     switch (kind) {
-      case K_I64: put_i64(e, ((const G1 int64_t*)nd.data)[row]); break;
-      case K_F64: put_double(e, ((const G1 double*)nd.data)[row]); break;
+      case K_I64: e.put_i64(((const G1 int64_t*)nd.data)[row]); break;
+      case K_F64: put_java_double(e, ((const G1 double*)nd.data)[row]); break;
       case K_BOOL:
-        if (((const G1 uint8_t*)nd.data)[row]) { e.put('t'); e.put('r'); e.put('u'); e.put('e'); }
-        else { e.put('f'); e.put('a'); e.put('l'); e.put('s'); e.put('e'); }
+        if (((const G1 uint8_t*)nd.data)[row]) e.put_word(kTrue, 4);
+        else e.put_word(kFalse, 5);
         break;
       case K_STR: put_str(e, nd.arena + ((const G1 int64_t*)nd.starts)[row], ((const G1 int32_t*)nd.lens)[row]); break;
-      case K_RAW:
-        put_text(e, (const G1 uint8_t*)nd.arena + ((const G1 int64_t*)nd.starts)[row],
-                 ((const G1 int32_t*)nd.lens)[row]);
-        break;
+      case K_RAW: put_raw(e, nd.arena + ((const G1 int64_t*)nd.starts)[row], ((const G1 int32_t*)nd.lens)[row]); break;
       case K_TS: put_ts(e, ((const G1 int64_t*)nd.data)[row]); break;
       case K_DATE: e.put('"'); put_date(e, ((const G1 int64_t*)nd.data)[row]); e.put('"'); break;
-      case K_CONST: put_text(e, text + nd.const_off, nd.const_len); break;
+      case K_CONST: e.put_text_words(t.text64 + (nd.const_off >> 3), nd.const_len); break;
       case K_STRUCT:
       case K_MAP:
       case K_ARRAY:
@@ -250,32 +324,50 @@ __device__ int64_t render_row(const SerArgs& a, int64_t row, uint8_t* dst) {
       default: break;
     }
   }
-  e.put('}');
-  e.put('\n');
+  e.put_word(0x0a7dull, 2);                                 // "}\n"
   e.finish();
   return e.len;
 }
 
 __global__ __launch_bounds__(256) void ser_len_kernel(SerArgs a) {
+  extern __shared__ uint64_t smem[];
+  const Tables t = stage_tables(a, smem);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
-  a.lens[i] = render_row<false>(a, i, nullptr);
+  a.lens[i] = render_row<false>(a, t, i, nullptr);
 }
 
-// amdgpu_waves_per_eu(4): 127 VGPRs instead of 151 (4 waves per SIMD instead of 3), no extra scratch.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ser_write_kernel(SerArgs a) {
+__global__ __launch_bounds__(256) void ser_write_kernel(SerArgs a) {
+  extern __shared__ uint64_t smem[];
+  const Tables t = stage_tables(a, smem);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
-  render_row<true>(a, i, a.out + a.offs[i]);
+  render_row<true>(a, t, i, a.out + a.offs[i]);
 }
 
+size_t ser_lds_bytes(int32_t nnodes, int32_t nprog, int32_t text_words) {
+  return (size_t)nnodes * sizeof(DevNode) + (size_t)((nprog * 4 + 1) / 2) * 8 + (size_t)text_words * 8;
+}
+
+constexpr size_t kMaxLds = 64 * 1024;
+
+// Test entry: Java Double.toString of v[i] into a 32-byte slot — finite values through the serializer's word path
+// (put_java_double), NaN / Infinity unquoted as the host formatter writes them.
 __global__ __launch_bounds__(256) void java_double_kernel(const double* v, int64_t n, uint8_t* out, int32_t* lens) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  char buf[32];
-  const int k = dxa::ryu::java_double(v[i], buf, c_ryu_inv, c_ryu_pos);
-  for (int j = 0; j < k; ++j) out[32 * i + j] = (uint8_t)buf[j];
-  lens[i] = k;
+  const double x = v[i];
+  if (x != x || x - x != 0.0) {
+    char buf[32];
+    const int k = dxa::ryu::java_double(x, buf, c_ryu_inv, c_ryu_pos);
+    for (int j = 0; j < k; ++j) out[32 * i + j] = (uint8_t)buf[j];
+    lens[i] = k;
+    return;
+  }
+  dxa::Emitter<true> e(out + 32 * i);
+  put_java_double(e, x);
+  e.finish();
+  lens[i] = (int32_t)e.len;
 }
 
 const uint64_t h_ryu_inv[2 * DXA_RYU_INV_TABLE_SIZE] = DXA_RYU_POW5_INV_SPLIT_INIT;
@@ -286,19 +378,26 @@ const uint64_t h_ryu_pos[2 * DXA_RYU_TABLE_SIZE] = DXA_RYU_POW5_SPLIT_INIT;
 DXA_API int dxa_sernode_dev_size() { return (int)sizeof(DevNode); }
 
 // `prog` / `nprog`: the flat render program (4 ints per op) built by dxa/ops/serialize.py from the node tree.
-DXA_API int dxa_serialize_lengths(const void* nodes, const int32_t* prog, int32_t nprog, const uint8_t* text, int64_t n,
-                                  int64_t* lens, void* st) {
+// `text` is 8-B aligned with `text_words` words (names / constants 8-B aligned, zero-padded); the tables are staged
+// in LDS, so they must fit in 64 KiB together.
+DXA_API int dxa_serialize_lengths(const void* nodes, int32_t nnodes, const int32_t* prog, int32_t nprog,
+                                  const uint8_t* text, int32_t text_words, int64_t n, int64_t* lens, void* st) {
   if (n <= 0) return 0;
-  SerArgs a{(const DevNode*)nodes, prog, nprog, text, n, lens, nullptr, nullptr};
-  hipLaunchKernelGGL(ser_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, a);
+  const size_t lds = ser_lds_bytes(nnodes, nprog, text_words);
+  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
+  SerArgs a{(const DevNode*)nodes, nnodes, prog, nprog, text, text_words, n, lens, nullptr, nullptr};
+  hipLaunchKernelGGL(ser_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, a);
   return (int)hipGetLastError();
 }
 
-DXA_API int dxa_serialize_write(const void* nodes, const int32_t* prog, int32_t nprog, const uint8_t* text, int64_t n,
-                                const int64_t* offs, uint8_t* out, void* st) {
+DXA_API int dxa_serialize_write(const void* nodes, int32_t nnodes, const int32_t* prog, int32_t nprog,
+                                const uint8_t* text, int32_t text_words, int64_t n, const int64_t* offs, uint8_t* out,
+                                void* st) {
   if (n <= 0) return 0;
-  SerArgs a{(const DevNode*)nodes, prog, nprog, text, n, nullptr, offs, out};
-  hipLaunchKernelGGL(ser_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, a);
+  const size_t lds = ser_lds_bytes(nnodes, nprog, text_words);
+  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
+  SerArgs a{(const DevNode*)nodes, nnodes, prog, nprog, text, text_words, n, nullptr, offs, out};
+  hipLaunchKernelGGL(ser_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, a);
   return (int)hipGetLastError();
 }
 

@@ -30,8 +30,8 @@ _SIGS = {
     "dxa_lz4_block_sizes": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_lz4_decode": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_memcpy_h2d_async": [c_p, c_p, c_i64, c_p],
-    "dxa_serialize_lengths": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p],
-    "dxa_serialize_write": [c_p, c_p, c_i32, c_p, c_i64, c_p, c_p, c_p],
+    "dxa_serialize_lengths": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p],
+    "dxa_serialize_write": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],
     "dxa_java_double_hostcheck": [c_p, c_i64, c_p, c_p],
     "dxa_json_parse": [c_p, c_p, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p,
@@ -63,8 +63,10 @@ _SIGS = {
     "dxa_case_map": [c_p, c_p, c_p, c_i64, c_p, c_p, ctypes.c_int, c_p],
     "dxa_str_to_ts": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
     "dxa_datagen_op_size": [],
-    "dxa_datagen_lengths": [c_p, c_i32, c_p, c_p, ctypes.c_uint64, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
-    "dxa_datagen_write": [c_p, c_i32, c_p, c_p, ctypes.c_uint64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p],
+    "dxa_datagen_lengths": [c_p, c_i32, c_p, c_i32, c_p, c_i32, ctypes.c_uint64, c_i64, c_i64, c_i64, c_i64, c_p,
+                            c_p],
+    "dxa_datagen_write": [c_p, c_i32, c_p, c_i32, c_p, c_i32, ctypes.c_uint64, c_i64, c_i64, c_i64, c_i64, c_p,
+                          c_p, c_p],
 }
 
 # optional symbols (added by later kernels); bound if present

@@ -172,6 +172,8 @@ class _DevBuilder:
         self.keep = []
 
     def _t(self, b: bytes):
+        """Text starts 8-B aligned with zero padding before it: the device emits it as 8-B words."""
+        self.text += b"\0" * (-len(self.text) % 8)
         off = len(self.text)
         self.text += b
         return off, len(b)
@@ -193,7 +195,7 @@ class _DevBuilder:
         idx = len(self.nodes)
         nd = self._blank()
         if name:
-            nd["name"] = self._t(_quoted(name))
+            nd["name"] = self._t(_quoted(name) + b":")
         self.nodes.append(nd)
         if isinstance(col, ConstColumn):
             if col.value is not None:
@@ -273,7 +275,8 @@ class _DevBuilder:
                              nd["name"][1], nd["const"][0], nd["const"][1], nd["data"], nd["valid"], nd["arena"],
                              nd["starts"], nd["lens"])
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device, non_blocking=False)
-        text = torch.frombuffer(bytearray(bytes(self.text) + b"\0"), dtype=torch.uint8).to(device)
+        text = torch.frombuffer(bytearray(bytes(self.text) + b"\0" * (-len(self.text) % 8 + 8)),
+                                dtype=torch.uint8).to(device)
         return raw, text
 
 
@@ -338,7 +341,9 @@ class Staged:
             nprog = len(prog) // 4
             st = N.stream_handle(dev)
             lens = torch.empty(max(1, n), dtype=torch.int64, device=dev)
-            N.call("dxa_serialize_lengths", N.ptr(nodes), N.ptr(prog_t), nprog, N.ptr(text), n, N.ptr(lens), st)
+            nn, tw = len(b.nodes), text.numel() // 8
+            N.call("dxa_serialize_lengths", N.ptr(nodes), nn, N.ptr(prog_t), nprog, N.ptr(text), tw, n, N.ptr(lens),
+                   st)
             ends = torch.cumsum(lens[:n], 0)
             offs = ends - lens[:n]
             host_lens = torch.empty(n, dtype=torch.int64, pin_memory=True)
@@ -346,7 +351,7 @@ class Staged:
             side.synchronize()
             total = int(ends[-1].item()) if n else 0
             out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-            N.call("dxa_serialize_write", N.ptr(nodes), N.ptr(prog_t), nprog, N.ptr(text), n, N.ptr(offs),
+            N.call("dxa_serialize_write", N.ptr(nodes), nn, N.ptr(prog_t), nprog, N.ptr(text), tw, n, N.ptr(offs),
                    N.ptr(out), st)
             host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
             host.copy_(out[:total], non_blocking=True)

@@ -32,10 +32,10 @@ OP_LIT, OP_INT, OP_DBL, OP_CHOICE, OP_TS_MS, OP_TS_STR, OP_BOOL, OP_ALNUM, OP_NU
 
 N.register_sigs({
     "dxa_datagen_op_size": [],
-    "dxa_datagen_lengths": [N.c_p, N.c_i32, N.c_p, N.c_p, ctypes.c_uint64, N.c_i64, N.c_i64, N.c_i64, N.c_i64, N.c_p,
-                            N.c_p],
-    "dxa_datagen_write": [N.c_p, N.c_i32, N.c_p, N.c_p, ctypes.c_uint64, N.c_i64, N.c_i64, N.c_i64, N.c_i64, N.c_p,
-                          N.c_p, N.c_p],
+    "dxa_datagen_lengths": [N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, ctypes.c_uint64, N.c_i64, N.c_i64,
+                            N.c_i64, N.c_i64, N.c_p, N.c_p],
+    "dxa_datagen_write": [N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, ctypes.c_uint64, N.c_i64, N.c_i64, N.c_i64,
+                          N.c_i64, N.c_p, N.c_p, N.c_p],
 })
 
 
@@ -45,6 +45,10 @@ class GenProgram:
     pool: bytearray = field(default_factory=bytearray)
     table: List[Tuple[int, int]] = field(default_factory=list)
 
+    def _align(self):
+        """Text starts 8-B aligned with zero padding before it: the device reads literals as 8-B words."""
+        self.pool += b"\0" * (-len(self.pool) % 8)
+
     def lit(self, s: str | bytes):
         b = s.encode() if isinstance(s, str) else s
         if self.ops and self.ops[-1][0] == OP_LIT and self.ops[-1][1] + self.ops[-1][2] == len(self.pool):
@@ -52,6 +56,7 @@ class GenProgram:
             self.pool += b
             self.ops[-1] = (c, a, ln + len(b), x, y)
             return
+        self._align()
         self.ops.append((OP_LIT, len(self.pool), len(b), 0, 0))
         self.pool += b
 
@@ -59,6 +64,7 @@ class GenProgram:
         start = len(self.table)
         for r in rendered:
             b = r.encode()
+            self._align()
             self.table.append((len(self.pool), len(b)))
             self.pool += b
         self.ops.append((OP_CHOICE, start, len(rendered), 0, 0))
@@ -74,7 +80,8 @@ class GenProgram:
             return cache[key]
         raw = b"".join(struct.pack("<iiiiqq", c, a, b, 0, x, y) for c, a, b, x, y in self.ops)
         ops = torch.frombuffer(bytearray(raw or b"\0" * 32), dtype=torch.uint8).to(device)
-        pool = torch.frombuffer(bytearray(bytes(self.pool) + b"\0" * 16), dtype=torch.uint8).to(device)
+        pad = b"\0" * (-len(self.pool) % 8 + 16)
+        pool = torch.frombuffer(bytearray(bytes(self.pool) + pad), dtype=torch.uint8).to(device)
         tab = torch.tensor([v for p in self.table for v in p] or [0, 0], dtype=torch.int32, device=device)
         cache[key] = (ops, pool, tab)
         self._dev = cache
@@ -231,15 +238,16 @@ def generate(prog: GenProgram, n: int, device, seed: int = 1, row0: int = 0, bas
     ops, pool, tab = prog.device(device)
     st = N.stream_handle(device)
     lens = torch.empty(n, dtype=torch.int64, device=device)
-    N.call("dxa_datagen_lengths", N.ptr(ops), len(prog.ops), N.ptr(pool), N.ptr(tab), seed & (2**64 - 1), row0, n,
-           base_ms, step_us, N.ptr(lens), st)
+    pw, ti = pool.numel() // 8, tab.numel()
+    N.call("dxa_datagen_lengths", N.ptr(ops), len(prog.ops), N.ptr(pool), pw, N.ptr(tab), ti, seed & (2**64 - 1),
+           row0, n, base_ms, step_us, N.ptr(lens), st)
     offs = torch.zeros(n + 1, dtype=torch.int64, device=device)
     torch.cumsum(lens, 0, out=offs[1:])
     total = int(offs[-1].item())
     buf = torch.empty(total + 16, dtype=torch.uint8, device=device)
     buf[total:].zero_()          # the parser's 16-B read window needs zero padding; the rest is fully written
-    N.call("dxa_datagen_write", N.ptr(ops), len(prog.ops), N.ptr(pool), N.ptr(tab), seed & (2**64 - 1), row0, n,
-           base_ms, step_us, N.ptr(offs), N.ptr(buf), st)
+    N.call("dxa_datagen_write", N.ptr(ops), len(prog.ops), N.ptr(pool), pw, N.ptr(tab), ti, seed & (2**64 - 1),
+           row0, n, base_ms, step_us, N.ptr(offs), N.ptr(buf), st)
     return buf, offs
 
 

@@ -304,3 +304,48 @@ def test_json_parse_key_order_speculation(gpu):
     gpu_raw, gpu_ok = parse(bg, og, plan)
     assert torch.equal(cpu_ok.cpu(), gpu_ok.cpu())
     assert cpu_raw.to_pylist() == gpu_raw.to_pylist()
+
+
+def _gen_programs():
+    from dxa.models import iot
+    from dxa.simulate.datagen import compile_simulated, compile_spark
+    spark = schema_from_json(json.dumps({"type": "struct", "fields": [
+        {"name": "id", "type": "long", "nullable": True, "metadata": {"minValue": -5, "maxValue": 10 ** 12}},
+        {"name": "name", "type": "string", "nullable": True, "metadata": {"maxLength": 19}},
+        {"name": "kind", "type": "string", "nullable": False, "metadata": {"allowedValues": ["a", "bb", "a\"c", ""]}},
+        {"name": "v", "type": "double", "nullable": True, "metadata": {"minValue": -1e6, "maxValue": 1e6,
+                                                                        "decimals": 3}},
+        {"name": "w", "type": "double", "nullable": False, "metadata": {"minValue": 0, "maxValue": 1, "decimals": 0}},
+        {"name": "ok", "type": "boolean", "nullable": True, "metadata": {}},
+        {"name": "t", "type": "long", "nullable": False, "metadata": {"useCurrentTimeMillis": True}},
+        {"name": "ts", "type": "string", "nullable": False, "metadata": {"datetimeStringFormat": "MM/dd/yyyy HH:mm:ss"}},
+        {"name": "nested", "type": {"type": "struct", "fields": [
+            {"name": "x", "type": "integer", "nullable": True, "metadata": {}},
+            {"name": "arr", "type": {"type": "array", "elementType": "double", "containsNull": True},
+             "nullable": True, "metadata": {"maxLength": 3}}]}, "nullable": True, "metadata": {}}]}))
+    sim = compile_simulated([
+        {"name": "deviceId", "type": "long", "minRange": 1, "maxRange": 1000},
+        {"name": "temp", "type": "double", "minRange": -40.5, "maxRange": 120.25},
+        {"name": "kind", "type": "string", "valueList": ["DoorLock", "WindowLock", "Heating"]},
+        {"name": "when", "type": "datetime", "datetimeStringFormat": "yyyy-MM-ddTHH:mm:ssZ", "utcAddSeconds": -30},
+        {"name": "const", "type": "string", "value": "fixed"},
+        {"name": "s", "type": "struct", "properties": [
+            {"name": "arr", "type": "array", "minRange": 0, "maxRange": 1, "length": 4, "castAsString": True}]}])
+    return {"iot": iot.program(), "iot_nl": iot.program(newline=True), "spark": compile_spark(spark),
+            "simulated": sim}
+
+
+@pytest.mark.parametrize("name", ["iot", "iot_nl", "spark", "simulated"])
+def test_datagen_matches_cpu(gpu, name):
+    """The GPU event generator renders byte-for-byte what the host reference renders (word-packed emitter: records
+    start at every alignment, so the first/last partial words of each record are exercised)."""
+    from dxa.simulate.datagen import generate, generate_cpu
+    prog = _gen_programs()[name]
+    for seed, row0, n, step in ((1, 0, 2000, 0), (77, 123457, 1531, 997), (2**63 + 5, 10 ** 9, 700, 1000)):
+        base = 1_700_000_000_123
+        gb, go = generate(prog, n, gpu, seed=seed, row0=row0, base_ms=base, step_us=step)
+        cb, co = generate_cpu(prog, n, seed=seed, row0=row0, base_ms=base, step_us=step)
+        assert go.cpu().tolist() == co.tolist()
+        total = int(co[-1])
+        assert bytes(gb[:total].cpu().numpy()) == bytes(cb[:total].numpy())
+        assert not gb[total:].cpu().any()
