@@ -56,14 +56,30 @@ class TimeWindowConf:
 
 
 def _compact_table(t: Table) -> Table:
-    """Detach retained rows from the batch's raw input buffer (string views → own compact arena)."""
-    def comp(c):
+    """Detach retained rows from the batch's raw input buffer (string views → own compact arena); all string leaves
+    are compacted together with one host synchronisation."""
+    from ..ops.strings import compact_many
+    leaves: List[StrColumn] = []
+
+    def collect(c):
         if isinstance(c, StrColumn):
-            return c.compact()
+            leaves.append(c)
+        elif isinstance(c, StructColumn):
+            for k in c.children:
+                collect(k)
+
+    for c in t.columns:
+        collect(c)
+    done = iter(compact_many(leaves))
+
+    def rebuild(c):
+        if isinstance(c, StrColumn):
+            return next(done)
         if isinstance(c, StructColumn):
-            return StructColumn(c.names, [comp(k) for k in c.children], c.length, c.valid, c.is_map, c.dtype, c.device)
+            return StructColumn(c.names, [rebuild(k) for k in c.children], c.length, c.valid, c.is_map, c.dtype,
+                                c.device)
         return c
-    return Table(t.names, [comp(c) for c in t.columns], t.length, t.device)
+    return Table(t.names, [rebuild(c) for c in t.columns], t.length, t.device)
 
 
 @dataclass

@@ -54,6 +54,35 @@ def compact(col):
     return out
 
 
+def compact_many(cols: Sequence) -> list:
+    """``compact`` of several string columns with ONE host synchronisation (all arena sizes are read back together)
+    instead of one per column."""
+    cols = list(cols)
+    if not cols:
+        return []
+    if not _gpu(cols[0].starts) or len(cols) == 1:
+        return [compact(c) for c in cols]
+    device = cols[0].device
+    offs, ends = [], []
+    for c in cols:
+        lens64 = c.lens.to(torch.int64)
+        cs = torch.cumsum(lens64, 0) if c.length else torch.zeros(1, dtype=torch.int64, device=device)
+        offs.append(cs - lens64 if c.length else cs[:0])
+        ends.append(cs[-1:] if c.length else cs)
+    totals = torch.cat(ends).tolist()
+    out = []
+    st = N.stream_handle(device)
+    for c, off, total in zip(cols, offs, totals):
+        dst = _alloc_arena(int(total), device)
+        if c.length and total:
+            N.call("dxa_str_gather", N.ptr(c.arena), N.ptr(c.starts), N.ptr(c.lens), c.length, N.ptr(off), N.ptr(dst),
+                   st)
+        o = type(c)(dst, off, c.lens.clone(), c.valid, c.dtype)
+        o._compact = True
+        out.append(o)
+    return out
+
+
 def concat(cols: Sequence, valid: Optional[torch.Tensor]):
     """Row-concatenate StrColumns (may reference different arenas) into one compact column."""
     device = cols[0].device
