@@ -790,33 +790,25 @@ def _collect(groups: G.Groups, arg, as_set):
 # ---------------------------------------------------------------------------------------------------------------
 
 def _sort_key_tensor(col: Column) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(order key, valid): an int64 tensor whose *unsigned* order is the column's SQL order (dxa.ops.sort — device
+    order-key kernels; strings are dense-ranked on the device)."""
+    from ..ops.sort import column_order_key
     col = materialize(col)
-    if isinstance(col, StrColumn):
-        # rank strings on the host (ORDER BY on strings is not a hot path in DataX flows)
-        vals = col.to_pylist()
-        order = sorted(range(len(vals)), key=lambda i: (vals[i] is None, (vals[i] or "").encode("utf-8")))
-        rank = torch.empty(len(vals), dtype=torch.int64)
-        rank[torch.tensor(order, dtype=torch.int64)] = torch.arange(len(vals), dtype=torch.int64)
-        # equal strings must get equal ranks
-        for k in range(1, len(order)):
-            if vals[order[k]] == vals[order[k - 1]]:
-                rank[order[k]] = rank[order[k - 1]]
-        return rank.to(col.device), col.valid_mask()
-    if isinstance(col, PrimColumn):
-        d = col.data
-        if d.dtype == torch.bool:
-            d = d.to(torch.int64)
-        return d, col.valid_mask()
-    raise QueryError(f"cannot ORDER BY {col.dtype}")
+    if not isinstance(col, (StrColumn, PrimColumn)):
+        raise QueryError(f"cannot ORDER BY {col.dtype}")
+    return column_order_key(col)
 
 
 def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope],
               aliases: Optional[Dict] = None) -> Table:
+    """One stable device radix argsort over all ORDER BY keys (dxa.ops.sort.argsort_words): per item an order key
+    word and, when the column has nulls, a null-placement word above it."""
+    from ..ops.sort import argsort_words, sort_spec_words
     if t.length <= 1:
         return t
     out_scope = Scope.of_table(t)
-    perm = torch.arange(t.length, device=t.device)
-    for it in reversed(items):
+    specs = []
+    for it in items:
         e = it.expr
         if isinstance(e, A.Literal) and e.type in ("int", "long"):
             col = t.columns[e.value - 1]
@@ -831,17 +823,9 @@ def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope
                     raise
                 else:
                     col = evaluate(e, src_scope, ctx)
-        key, valid = _sort_key_tensor(col)
-        key, valid = key[perm], valid[perm]
-        # null slots hold arbitrary bytes (device buffers are not zeroed): give them one key so the stable sort keeps
-        # their order from the previous (more significant) keys
-        key = torch.where(valid, key, torch.zeros_like(key))
+        col = materialize(col)
+        if not isinstance(col, (StrColumn, PrimColumn)):
+            raise QueryError(f"cannot ORDER BY {col.dtype}")
         nulls_first = it.nulls_first if it.nulls_first is not None else it.ascending
-        o = torch.argsort(key, stable=True, descending=not it.ascending)
-        v = valid[o]
-        # move nulls to the requested end, stably
-        nn = torch.nonzero(v).flatten()
-        nl = torch.nonzero(~v).flatten()
-        o = torch.cat([o[nl], o[nn]]) if nulls_first else torch.cat([o[nn], o[nl]])
-        perm = perm[o]
-    return t.take(perm)
+        specs.append((col, it.ascending, nulls_first))
+    return t.take(argsort_words(sort_spec_words(specs)))

@@ -104,20 +104,17 @@ def evaluate_window(wc: A.WindowCall, ev: Callable[[A.Expr], Column], n: int, de
         gid = G.group_rows(keys).gid.to(i64)
     else:
         gid = torch.zeros(n, dtype=i64, device=dev)
+    from ..ops.sort import argsort_words, sort_spec_words
     okeys = []
+    specs = []
     for it in wc.order:
-        okeys.append((it,) + _sort_key(ev(it.expr)))
-    perm = torch.arange(n, device=dev)
-    for it, key, valid in reversed(okeys):
-        k, v = key[perm], valid[perm]
+        col = materialize(ev(it.expr))
+        okeys.append((it,) + _sort_key(col))
         nulls_first = it.nulls_first if it.nulls_first is not None else it.ascending
-        o = torch.argsort(k, stable=True, descending=not it.ascending)
-        vv = v[o]
-        nn = torch.nonzero(vv).flatten()
-        nl = torch.nonzero(~vv).flatten()
-        o = torch.cat([o[nl], o[nn]]) if nulls_first else torch.cat([o[nn], o[nl]])
-        perm = perm[o]
-    perm = perm[torch.argsort(gid[perm], stable=True)]
+        specs.append((col, it.ascending, nulls_first))
+    # one stable device radix argsort: partition id most significant, then the ORDER BY items
+    words = sort_spec_words(specs) + [gid]
+    perm = argsort_words(words)
 
     # -- partition / peer boundaries in sorted order ------------------------------------------------------------
     idx = torch.arange(n, device=dev, dtype=i64)

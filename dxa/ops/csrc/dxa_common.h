@@ -66,7 +66,7 @@ __host__ __device__ __forceinline__ uint64_t fnv1a_step(uint64_t h, uint32_t c) 
 }
 constexpr uint64_t kFnvBasis = 0xcbf29ce484222325ull;
 
-__device__ __forceinline__ int grid_stride_blocks(int64_t n, int block, int cap = 256 * 16) {
+__host__ __device__ __forceinline__ int grid_stride_blocks(int64_t n, int block, int cap = 256 * 16) {
   int64_t b = (n + block - 1) / block;
   if (b < 1) b = 1;
   return (int)(b < cap ? b : cap);

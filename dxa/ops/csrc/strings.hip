@@ -55,6 +55,41 @@ __global__ void str_cmp_lit_kernel(const uint8_t* __restrict__ arena, const int6
   }
 }
 
+// Column-vs-column ordering comparison (op: 2 <, 3 <=, 4 >, 5 >=), byte-wise (UTF-8 code point) order: 8 bytes at
+// a time as big-endian words, then length.
+__device__ __forceinline__ uint64_t be_chunk(const uint8_t* s, int32_t len, int32_t off) {
+  uint64_t v = 0;
+  const int32_t m = len - off < 8 ? len - off : 8;
+  for (int32_t b = 0; b < m; ++b) v |= (uint64_t)s[off + b] << (56 - 8 * b);
+  return v;
+}
+
+__global__ void str_cmp_col_kernel(const uint8_t* __restrict__ aa, const int64_t* __restrict__ as,
+                                   const int32_t* __restrict__ al, const uint8_t* __restrict__ ba,
+                                   const int64_t* __restrict__ bs, const int32_t* __restrict__ bl, int64_t n,
+                                   int32_t op, uint8_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* x = aa + as[i];
+    const uint8_t* y = ba + bs[i];
+    const int32_t lx = al[i], ly = bl[i];
+    const int32_t m = lx < ly ? lx : ly;
+    int c = 0;
+    for (int32_t off = 0; off < m && c == 0; off += 8) {
+      const uint64_t u = be_chunk(x, m, off), v = be_chunk(y, m, off);
+      c = (u > v) - (u < v);
+    }
+    if (c == 0) c = (lx > ly) - (lx < ly);
+    bool r;
+    switch (op) {
+      case 2: r = c < 0; break;
+      case 3: r = c <= 0; break;
+      case 4: r = c > 0; break;
+      default: r = c >= 0; break;
+    }
+    out[i] = r ? 1 : 0;
+  }
+}
+
 // Column-vs-column equality (join residuals, string = string predicates).
 __global__ void str_eq_col_kernel(const uint8_t* __restrict__ aa, const int64_t* __restrict__ as,
                                   const int32_t* __restrict__ al, const uint8_t* __restrict__ ba,
@@ -309,6 +344,15 @@ DXA_API int dxa_str_eq_col(const uint8_t* aa, const int64_t* as, const int32_t* 
   if (n <= 0) return 0;
   hipLaunchKernelGGL(str_eq_col_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, aa, as, al, ba, bs,
                      bl, n, out);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_cmp_col(const uint8_t* aa, const int64_t* as, const int32_t* al, const uint8_t* ba,
+                            const int64_t* bs, const int32_t* bl, int64_t n, int32_t op, uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  if (op < 2 || op > 5) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(str_cmp_col_kernel, dim3(dxa::grid_stride_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, aa, as,
+                     al, ba, bs, bl, n, op, out);
   return (int)hipGetLastError();
 }
 

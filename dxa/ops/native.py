@@ -54,6 +54,7 @@ _SIGS = {
     "dxa_probe_write": [c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, ctypes.c_int, c_p],
     "dxa_str_cmp_lit": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p],
     "dxa_str_eq_col": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
+    "dxa_str_cmp_col": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p],
     "dxa_str_gather": [c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
     "dxa_concat_len": [c_p, c_i32, c_i64, c_p, c_p, c_p],
     "dxa_concat_write": [c_p, c_i32, c_i64, c_p, c_p, c_p, c_p],

@@ -146,10 +146,21 @@ def eq_columns(a, b) -> torch.Tensor:
 
 
 def compare_columns(a, b, op: str) -> torch.Tensor:
-    """General (host-assisted) string column comparison for < <= > >=; equality uses eq_columns."""
+    """Row-wise string column comparison, byte-wise (UTF-8 code point) order; nulls are the caller's (their rows
+    compare as empty strings here)."""
     if op in ("=", "!="):
         eq = eq_columns(a, b)
         return eq if op == "=" else ~eq
+    if _gpu(a.starts):
+        from .sort import _safe_lens
+        n = a.length
+        out = torch.empty(n, dtype=torch.bool, device=a.device)
+        if n:
+            al, bl = _safe_lens(a), _safe_lens(b)
+            N.call("dxa_str_cmp_col", N.ptr(a.arena), N.ptr(a.starts.to(torch.int64).contiguous()), N.ptr(al),
+                   N.ptr(b.arena), N.ptr(b.starts.to(torch.int64).contiguous()), N.ptr(bl), n, _CMP_OPS[op],
+                   N.ptr(out.view(torch.uint8)), N.stream_handle(a.device))
+        return out
     va, vb = _raw_bytes(a), _raw_bytes(b)
     f = {"<": lambda x, y: x < y, "<=": lambda x, y: x <= y, ">": lambda x, y: x > y, ">=": lambda x, y: x >= y}[op]
     return torch.tensor([f(x, y) for x, y in zip(va, vb)], dtype=torch.bool, device=a.device)
