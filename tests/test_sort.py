@@ -96,7 +96,7 @@ def test_gpu_radix_argsort_matches_cpu(n, nwords, small):
             w = torch.randint(0, 7, (n,), generator=g, dtype=torch.int64)
         else:
             w = torch.randint(-(2**63), 2**63 - 1, (n,), generator=g, dtype=torch.int64)
-            w[::5] = w[3]                                   # duplicates: stability matters
+            w[::5] = w[min(3, n - 1)]                       # duplicates: stability matters
         words.append(w)
     want = SO.argsort_words(words)
     got = SO.argsort_words([w.to(dev) for w in words]).cpu()
