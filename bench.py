@@ -75,6 +75,8 @@ def main():
                     help="batches whose ingest (H2D copy + decode, or generation) is in flight ahead of the one "
                          "being processed")
     ap.add_argument("--lz4-chunks", type=int, default=4, help="pinned-lz4: copy/decode pipeline depth per batch")
+    ap.add_argument("--lz4-block", type=int, default=None,
+                    help="pinned-lz4: LZ4 frame block size (default: dxa.ops.lz4.DEFAULT_BLOCK)")
     ap.add_argument("--lz4-level", type=int, default=9,
                     help="pinned-lz4: producer compression level (Kafka compression.lz4.level; 9 is Kafka's default, "
                          "0 = fast greedy compressor)")
@@ -145,14 +147,15 @@ def main():
         from dxa.ops import lz4
         from dxa.ops.jsonparse import frame_lines_gpu
         prog_nl = iot.program(newline=True)
+        lz4_block = args.lz4_block or lz4.DEFAULT_BLOCK
         base_ms = clock0_us // 1000
         for p in range(args.pool):
             buf, offs = generate(prog_nl, E, device, seed=1000 * rank + p + 1, row0=p * E, base_ms=base_ms)
             total = int(offs[-1])
-            frame = lz4.compress_frame(buf[:total].cpu(), lz4.DEFAULT_BLOCK, threads=16, level=args.lz4_level)
+            frame = lz4.compress_frame(buf[:total].cpu(), lz4_block, threads=16, level=args.lz4_level)
             del buf, offs
             comp_bytes.append(frame.size)
-            pool.append(lz4.DeviceFrame.from_frame(frame, lz4.DEFAULT_BLOCK, pin=on_gpu))
+            pool.append(lz4.DeviceFrame.from_frame(frame, lz4_block, pin=on_gpu))
     if source in ("pinned", "device"):
         base_ms = clock0_us // 1000
         for p in range(args.pool):
@@ -328,6 +331,7 @@ def main():
         out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)
         out["config"]["lz4_ratio"] = round((sum(sizes) / len(sizes) - 16) / (sum(comp_bytes) / len(comp_bytes)), 2)
         out["config"]["lz4_level"] = args.lz4_level
+        out["config"]["lz4_block_bytes"] = lz4_block
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
     if last:
