@@ -97,6 +97,61 @@ def _take_valid(valid, idx):
     return None if valid is None else valid[idx]
 
 
+def take_columns(cols: Sequence["Column"], idx: torch.Tensor) -> List["Column"]:
+    """Row gather of several columns with the same index vector.  On the GPU every leaf tensor (data, validity,
+    string starts / lengths, nested validity) moves in one multi-column gather launch (dxa.ops.gather) instead of
+    one indexing kernel per leaf; the CPU path is each column's own ``take``."""
+    cols = list(cols)
+    if idx.device.type != "cuda" or not cols:
+        return [c.take(idx) for c in cols]
+    leaves: List[torch.Tensor] = []
+
+    def plan(c):
+        """Register c's leaf tensors; return a builder taking the gathered leaves (in registration order)."""
+        if isinstance(c, PrimColumn):
+            i = len(leaves)
+            leaves.append(c.data)
+            if c.valid is not None:
+                leaves.append(c.valid)
+            has_v = c.valid is not None
+            return lambda g: PrimColumn(c.dtype, g[i], g[i + 1] if has_v else None)
+        if isinstance(c, StrColumn):
+            i = len(leaves)
+            leaves.extend([c.starts, c.lens])
+            if c.valid is not None:
+                leaves.append(c.valid)
+            has_v = c.valid is not None
+            return lambda g: type(c)(c.arena, g[i], g[i + 1], g[i + 2] if has_v else None, c.dtype)
+        if isinstance(c, StructColumn):
+            i = len(leaves)
+            if c.valid is not None:
+                leaves.append(c.valid)
+            has_v = c.valid is not None
+            kids = [plan(k) for k in c.children]
+            n = int(idx.shape[0])
+            return lambda g: StructColumn(c.names, [b(g) for b in kids], n, g[i] if has_v else None, c.is_map,
+                                          c.dtype, c.device)
+        if isinstance(c, ArrayColumn):
+            i = len(leaves)
+            if c.valid is not None:
+                leaves.append(c.valid)
+            has_v = c.valid is not None
+            els = [plan(e) for e in c.elements]
+            n = int(idx.shape[0])
+            return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device)
+        taken = c.take(idx)                       # constants and other kinds: their own take
+        return lambda g: taken
+
+    builders = [plan(c) for c in cols]
+    if len(leaves) < 2:
+        return [c.take(idx) for c in cols]
+    if any(t.dim() != 1 or t.shape[0] != leaves[0].shape[0] for t in leaves):
+        return [c.take(idx) for c in cols]
+    from ..ops.gather import gather_many
+    g = gather_many(leaves, idx)
+    return [b(g) for b in builders]
+
+
 class PrimColumn(Column):
     def __init__(self, dtype: str, data: torch.Tensor, valid: Optional[torch.Tensor] = None):
         self.dtype = dtype
@@ -275,6 +330,8 @@ class StructColumn(Column):
         return None
 
     def take(self, idx):
+        if idx.device.type == "cuda":
+            return take_columns([self], idx)[0]
         return StructColumn(self.names, [c.take(idx) for c in self.children], int(idx.shape[0]),
                             _take_valid(self.valid, idx), self.is_map, self.dtype, self._device)
 
@@ -321,6 +378,8 @@ class ArrayColumn(Column):
         return self._device
 
     def take(self, idx):
+        if idx.device.type == "cuda":
+            return take_columns([self], idx)[0]
         return ArrayColumn([e.take(idx) for e in self.elements], int(idx.shape[0]), _take_valid(self.valid, idx),
                            self.drop_nulls, self._device)
 
@@ -513,7 +572,7 @@ class Table:
         return StructType(tuple(StructField(n, c.dtype) for n, c in zip(self.names, self.columns)))
 
     def take(self, idx: torch.Tensor) -> "Table":
-        return self._like(self.names, [c.take(idx) for c in self.columns], int(idx.shape[0]))
+        return self._like(self.names, take_columns(self.columns, idx), int(idx.shape[0]))
 
     def filter(self, mask: torch.Tensor) -> "Table":
         idx = torch.nonzero(mask, as_tuple=False).flatten()
