@@ -54,6 +54,21 @@ def compact(col):
     return out
 
 
+def compact_known(col, total: int):
+    """``compact`` when the caller already knows the column's total byte count (no host synchronisation)."""
+    if not _gpu(col.starts):
+        return compact(col)
+    lens64 = col.lens.to(torch.int64)
+    off = torch.cumsum(lens64, 0) - lens64
+    dst = _alloc_arena(total, col.device)
+    if col.length and total:
+        N.call("dxa_str_gather", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), col.length, N.ptr(off),
+               N.ptr(dst), N.stream_handle(col.device))
+    out = type(col)(dst, off, col.lens.clone(), col.valid, col.dtype)
+    out._compact = True
+    return out
+
+
 def compact_many(cols: Sequence) -> list:
     """``compact`` of several string columns with ONE host synchronisation (all arena sizes are read back together)
     instead of one per column."""

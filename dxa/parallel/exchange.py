@@ -126,13 +126,21 @@ def split_by_destination(dest: torch.Tensor, world: int):
 
 
 def shuffle_table(table, dest: torch.Tensor):
-    """Send row i to rank dest[i]; returns the rows this rank receives (in source-rank order)."""
+    """Send row i to rank dest[i]; returns the rows this rank receives (in source-rank order).
+
+    One host synchronisation per exchange: the row count and every string leaf's byte count per destination are
+    computed on the device as one [W, 1 + S] matrix, exchanged with one all-to-all, and read back together with
+    the send side; every later collective (the int64 row matrix, one byte stream per string leaf) has its sizes
+    from that single read-back."""
     from ..engine.column import PrimColumn, StrColumn, Table
+    from ..ops import strings as sops
     W = _w()
     device = table.device
     n = table.length
-    order, counts = split_by_destination(dest.to(torch.int64), W)
+    dest = dest.to(torch.int64)
+    order, counts = split_by_destination(dest, W)
     t = table.take(order)
+    sorted_dest = dest[order]
     leaves: List[_Leaf] = []
     spec: list = []
     for c in t.columns:
@@ -140,7 +148,8 @@ def shuffle_table(table, dest: torch.Tensor):
     # matrix columns
     mats = []
     nvalid = 0
-    for lf in leaves:
+    str_leaves = []
+    for li, lf in enumerate(leaves):
         c = lf.col
         if lf.kind == "prim":
             d = c.data
@@ -153,6 +162,7 @@ def shuffle_table(table, dest: torch.Tensor):
         elif lf.kind == "str":
             lf.mcol = len(mats)
             mats.append(c.lens.to(torch.int64))
+            str_leaves.append(li)
         if c.valid is not None:
             lf.vbit = nvalid
             nvalid += 1
@@ -164,37 +174,35 @@ def shuffle_table(table, dest: torch.Tensor):
             masks[w] |= lf.col.valid.to(torch.int64) << b
     mat_cols = mats + masks
     C = len(mat_cols)
-    recv_counts = _a2a_counts(counts)
-    n_out = int(recv_counts.sum().item())
+    # [W, 1 + S] send sizes: rows, then bytes of each string leaf, per destination (device side)
+    size_cols = [counts]
+    for li in str_leaves:
+        by_dest = torch.zeros(W, dtype=torch.int64, device=device)
+        if n:
+            by_dest.index_add_(0, sorted_dest, mats[leaves[li].mcol])
+        size_cols.append(by_dest)
+    send_sizes = torch.stack(size_cols, 1).contiguous()
+    recv_sizes = _a2a_counts(send_sizes)
+    both = torch.stack([send_sizes, recv_sizes]).tolist()            # the exchange's one host sync
+    send_rows = [r[0] for r in both[0]]
+    recv_rows = [r[0] for r in both[1]]
+    n_out = sum(recv_rows)
     if C:
         send = torch.stack(mat_cols, 1).contiguous() if n else torch.empty((0, C), dtype=torch.int64, device=device)
         recv = torch.empty((n_out, C), dtype=torch.int64, device=device)
-        dist.all_to_all_single(recv, send, recv_counts.tolist(), counts.tolist(), group=_g())
+        dist.all_to_all_single(recv, send, recv_rows, send_rows, group=_g())
     else:
         recv = torch.empty((n_out, 0), dtype=torch.int64, device=device)
-    # string bytes
+    # string bytes: rows are already grouped by destination, so each leaf's packed bytes are too
     str_out = {}
-    cpu_counts = counts.tolist()
-    rc = recv_counts.tolist()
-    bounds = [0]
-    for x in cpu_counts:
-        bounds.append(bounds[-1] + x)
-    rbounds = [0]
-    for x in rc:
-        rbounds.append(rbounds[-1] + x)
-    for li, lf in enumerate(leaves):
-        if lf.kind != "str":
-            continue
-        sc = lf.col.compact()
-        lens64 = sc.lens.to(torch.int64)
-        cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=device), torch.cumsum(lens64, 0)])
-        byte_bounds = cs[torch.tensor(bounds, dtype=torch.int64, device=device)].tolist()
-        send_bytes = [byte_bounds[i + 1] - byte_bounds[i] for i in range(W)]
-        sb = torch.tensor(send_bytes, dtype=torch.int64, device=device)
-        rb = _a2a_counts(sb)
-        total = int(rb.sum().item())
+    for si, li in enumerate(str_leaves):
+        lf = leaves[li]
+        send_bytes = [r[1 + si] for r in both[0]]
+        recv_bytes = [r[1 + si] for r in both[1]]
+        sc = sops.compact_known(lf.col, sum(send_bytes))
+        total = sum(recv_bytes)
         out = torch.zeros(total + 16, dtype=torch.uint8, device=device)
-        dist.all_to_all_single(out[:total], sc.arena[:byte_bounds[-1]].contiguous(), rb.tolist(), send_bytes,
+        dist.all_to_all_single(out[:total], sc.arena[:sum(send_bytes)].contiguous(), recv_bytes, send_bytes,
                                group=_g())
         rlens = recv[:, lf.mcol]
         starts = torch.cumsum(rlens, 0) - rlens
@@ -262,6 +270,6 @@ def rebalance_table(table):
     n = table.length
     counts = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(W)]
     dist.all_gather(counts, torch.tensor([n], dtype=torch.int64, device=device), group=_g())
-    offset = int(sum(int(c.item()) for c in counts[:_RANK]))
+    offset = int(sum(torch.cat(counts).tolist()[:_RANK]))          # one host read-back
     dest = (torch.arange(n, dtype=torch.int64, device=device) + offset) % W
     return shuffle_table(table, dest)

@@ -1,0 +1,66 @@
+"""Count host<->device synchronisations per micro-batch of a bench flow, by source line.
+
+    python tools/sync_audit.py [--flow groupby] [--events 200000] [--batches 3]
+
+Runs the flow's Processor on generated batches with ``torch.cuda.set_sync_debug_mode("warn")`` after one warm-up
+batch and prints, per (file:line in dxa/), how many synchronising calls a batch makes."""
+import argparse
+import collections
+import os
+import sys
+import traceback
+import warnings
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flow", default="groupby")
+    ap.add_argument("--events", type=int, default=200_000)
+    ap.add_argument("--batches", type=int, default=3)
+    a = ap.parse_args()
+    from dxa.engine.processor import Processor, RawBatch
+    from dxa.models import iot
+    from dxa.ops import native
+    from dxa.simulate.datagen import generate
+    native.lib()
+    dev = torch.device("cuda", 0)
+    proc = Processor(iot.flow_settings(workdir="/tmp/dxa_sync_audit", variant=a.flow, ref_rows=1_000_000), dev,
+                     pipeline_outputs=True)
+    if a.flow == "join":
+        proc.reference["RefDevices"] = iot.reference_table(1_000_000, dev)
+    prog = iot.program()
+    t0 = 1_700_000_000_000_000
+    sites = collections.Counter()
+
+    def hook(message, category, filename, lineno, file=None, line=None):
+        st = traceback.extract_stack()[:-1]
+        frames = [f for f in st if "/dxa/" in f.filename]
+        if frames:
+            f = frames[-1]
+            sites[(f.filename.split("/dxa/")[-1], f.lineno, f.name)] += 1
+        else:
+            sites[("<other>", 0, str(message)[:60])] += 1
+
+    for i in range(a.batches + 1):
+        buf, offs = generate(prog, a.events, dev, seed=i + 1, row0=i * a.events, base_ms=t0 // 1000 + i * 1000 - 1000,
+                             step_us=max(1, 1_000_000 // a.events))
+        torch.cuda.synchronize()
+        if i == 1:
+            warnings.showwarning = hook
+            warnings.simplefilter("always")
+            torch.cuda.set_sync_debug_mode("warn")
+        proc.process_batch(RawBatch(buf, offs, a.events), t0 + i * 1_000_000, 1_000_000)
+    torch.cuda.set_sync_debug_mode("default")
+    proc.drain()
+    total = sum(sites.values())
+    print(f"# {a.flow}: {total / a.batches:.1f} synchronising calls per batch")
+    for (f, ln, fn), c in sites.most_common():
+        print(f"{c / a.batches:6.1f}  {f}:{ln}  {fn}")
+
+
+if __name__ == "__main__":
+    main()
