@@ -32,6 +32,7 @@ from fastapi import Body, FastAPI, Header, HTTPException, Query, Request
 from fastapi.responses import HTMLResponse, JSONResponse
 
 from ..flow import configgen
+from ..flow import designer
 from ..sql.codegen import generate_code
 from ..telemetry.metrics import MetricStore
 from .jobs import JobManager
@@ -218,6 +219,24 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         rc = generate_code(body.get("query", ""), rules, body.get("productId", ""))
         return {"code": rc.code, "outputs": rc.outputs, "accumulationTables": rc.accumulation_tables,
                 "timeWindows": rc.time_windows, "metrics": rc.metrics}
+
+    # ---- flow designer model (the reference computes these in the browser: datax-pipeline flowHelpers.js)
+    @route("designer/conditions/sql")
+    def designer_conditions_sql(body):
+        agg = body.get("ruleType") == designer.AGGREGATE_RULE
+        conds = body.get("conditions") or designer.default_group()
+        return {"condition": designer.conditions_to_sql(conds, agg),
+                "error": designer.validate_conditions(conds, body.get("ruleType", designer.SIMPLE_RULE)),
+                "aggs": designer.config_aggregates(agg, conds, body.get("aggs") or []),
+                "pivots": designer.config_pivots(agg, conds, body.get("pivots") or [])}
+
+    @route("designer/flow/toconfig")
+    def designer_to_config(body):
+        return designer.flow_to_config(body.get("flow", body), body.get("query", ""))
+
+    @route("designer/flow/fromconfig")
+    def designer_from_config(body):
+        return designer.config_to_flow(body.get("config", body))
 
     @route("job/getall")
     def job_getall(body):

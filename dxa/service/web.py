@@ -4,7 +4,8 @@ datax-query LiveQuery, datax-jobs, datax-metrics dashboard, datax-home) as one d
 * Flows: list / create / open;
 * Designer tabs: Info, Input (type, mode, connection, schema with *infer from samples*, normalization snippet),
   Reference data, Functions (UDF/UDAF/Azure Function), Query (+ codegen preview + LiveQuery), Rules (tag / alert
-  builder: condition, severity, tag, alert sinks), Outputs (metric, blob/local, event hub, cosmos db, sql, http,
+  rules with the reference's condition builder — nested and/or groups, field / operator / value, aggregates for
+  aggregate rules — turned into SQL by the ``designer/*`` routes, ``dxa.flow.designer``; severity, tag, sinks), Outputs (metric, blob/local, event hub, cosmos db, sql, http,
   file, console), Scale (GPUs), Schedule (batch list) — saved as the Flow JSON the config generator consumes;
 * Jobs: state, start / stop / restart;
 * Metrics: charts of the flow's metric sources (polling ``/api/metrics/get``, the reference's SumWithTimeChart speed =
@@ -69,11 +70,12 @@ OUTPUT T1 TO Metrics;</textarea>
 <div class="row"><button onclick="codegen()">Codegen preview</button><button onclick="newKernel()">New LiveQuery kernel</button>
 <button onclick="execQuery()">Execute selection / all</button><span id="kernel" class="muted"></span></div></section>
 <section id="tab-rules"><h3>Rules</h3><table id="rules"></table>
-<div class="row">id <input id="ru-id" size="8"> type <select id="ru-type"><option>SimpleRule</option>
-<option>AggregateRule</option></select> condition <input id="ru-cond" size="40" placeholder="temperature > 90">
-tag <input id="ru-tag" size="8"> severity <select id="ru-sev"><option>Critical</option><option>Medium</option>
-<option>Low</option></select> alert <input type="checkbox" id="ru-alert"> sinks <input id="ru-sinks" value="Metrics">
-<button onclick="addRule()">add</button></div></section>
+<div class="row">id <input id="ru-id" size="8"> type <select id="ru-type" onchange="condPreview()"><option>SimpleRule</option>
+<option>AggregateRule</option></select> tag <input id="ru-tag" size="8"> severity <select id="ru-sev"><option>Critical</option>
+<option>Medium</option><option>Low</option></select> alert <input type="checkbox" id="ru-alert"> sinks <input id="ru-sinks" value="Metrics"></div>
+<p>Condition builder (groups of conditions; aggregate rules may aggregate a field)</p><div id="cond"></div>
+<div class="row">extra GROUP BY columns <input id="ru-pivots" size="30" placeholder="deviceId,homeId"> condition:
+<code id="ru-sql"></code> <span id="ru-err" class="muted"></span><button onclick="addRule()">add rule</button></div></section>
 <section id="tab-outputs"><h3>Outputs</h3><table id="outs"></table>
 <div class="row">id <input id="o-id" size="10"> type <select id="o-type"><option>metric</option><option>local</option>
 <option>blob</option><option>eventhub</option><option>cosmosdb</option><option>sql</option><option>httppost</option>
@@ -114,8 +116,8 @@ function blankFlow(){return {name:'',gui:{name:'',displayName:'',owner:'',input:
   inputSchemaFile:'',normalizationSnippet:'Raw.*',windowDuration:'1',maxRate:'1000',timestampColumn:'',watermarkValue:'0',
   watermarkUnit:'second'},referenceData:[]},process:{queries:[''],functions:[],jobconfig:{jobNumGpus:'1'}},
   outputs:[{id:'Metrics',type:'metric',properties:{}}],rules:[],batchList:[]}}}
-function newFlow(){flow=blankFlow();fill();show('designer');tab('info')}
-async function openFlow(n){const r=await api('flow/get',{name:n});flow=r.result;fill();show('designer');tab('info')}
+function newFlow(){flow=blankFlow();fill();show('designer');tab('info');renderCond()}
+async function openFlow(n){const r=await api('flow/get',{name:n});flow=r.result;fill();show('designer');tab('info');renderCond()}
 function fill(){const g=flow.gui,i=g.input,p=i.properties;$('fname').textContent=flow.name||'(new flow)';
   $('f-name').value=flow.name||'';$('f-display').value=g.displayName||'';$('f-owner').value=g.owner||'';
   $('i-type').value=i.type||'local';$('i-mode').value=i.mode||'streaming';$('i-conn').value=p.inputEventhubConnection||'';
@@ -139,10 +141,41 @@ function del(kind,k){const g=flow.gui;({ref:g.input.referenceData,fn:g.process.f
 function addRef(){flow.gui.input.referenceData.push({id:$('r-id').value,type:'csv',properties:{path:$('r-path').value,delimiter:$('r-del').value,header:$('r-hdr').value==='true'}});renderLists();}
 function addFunc(){const t=$('fn-type').value,v=$('fn-class').value;flow.gui.process.functions.push({id:$('fn-id').value,type:t,
   properties:t==='azureFunction'?{serviceEndpoint:v,api:'',code:'',methodType:'get',params:[]}:{class:v,path:'',libs:[]}});renderLists();}
-function addRule(){const p={_S_ruleId:$('ru-id').value,_S_ruleType:$('ru-type').value,_S_productId:flow.name,_S_ruleDescription:$('ru-id').value,
-  _S_condition:$('ru-cond').value,_S_tagname:'Tag',_S_tag:$('ru-tag').value,_S_severity:$('ru-sev').value,_S_isAlert:$('ru-alert').checked,
-  _S_alertsinks:$('ru-sinks').value.split(',').filter(x=>x),schemaTableName:'DataXProcessedInput'};
-  flow.gui.rules.push({id:p._S_ruleId,type:'tag',properties:p});renderLists();}
+const OPS=[['equal','='],['notEqual','<>'],['greater','>'],['lessThan','<'],['greaterThanOrEqual','>='],
+  ['lessThanOrEqual','<='],['stringEqual','= text'],['stringNotEqual','<> text'],['contains','contains'],
+  ['notContains','not contains'],['startsWith','starts with'],['endsWith','ends with']];
+const AGGS=['none','MIN','MAX','AVG','SUM','COUNT','DCOUNT'];
+function newCond(){return {type:'condition',conjunction:'and',field:'',operator:'equal',value:'',aggregate:'none'}}
+let ruleConds={type:'group',conjunction:'and',conditions:[newCond()]};
+function sel(opts,v,on){return `<select onchange="${on}">`+opts.map(o=>{const [k,t]=Array.isArray(o)?o:[o,o];
+  return `<option value="${k}" ${k===v?'selected':''}>${t}</option>`}).join('')+'</select>'}
+function nodeAt(path){let n=ruleConds;for(const i of path)n=n.conditions[i];return n}
+function setC(path,k,v){nodeAt(path)[k]=v;condPreview()}
+function addC(path,grp){nodeAt(path).conditions.push(grp?{type:'group',conjunction:'and',conditions:[newCond()]}:newCond());renderCond()}
+function rmC(path){const p=path.slice(0,-1),i=path[path.length-1];nodeAt(p).conditions.splice(i,1);renderCond()}
+function condHtml(g,path){const agg=$('ru-type').value==='AggregateRule';
+  let h='<div style="border-left:3px solid #9ab;padding-left:8px;margin:4px 0">';
+  g.conditions.forEach((c,i)=>{const p=JSON.stringify(path.concat([i]));
+    const conj=i?sel(['and','or'],c.conjunction,`setC(${p},'conjunction',this.value)`):'';
+    if(c.type==='group'){h+=`<div>${conj} group <button onclick='rmC(${p})'>x</button>`+condHtml(c,path.concat([i]))+'</div>';return}
+    h+=`<div class="row">${conj}`+(agg?sel(AGGS,c.aggregate,`setC(${p},'aggregate',this.value)`):'')+
+      `<input size="18" placeholder="field" value="${esc(c.field)}" oninput='setC(${p},"field",this.value)'>`+
+      sel(OPS,c.operator,`setC(${p},'operator',this.value)`)+
+      `<input size="12" placeholder="value" value="${esc(c.value)}" oninput='setC(${p},"value",this.value)'><button onclick='rmC(${p})'>x</button></div>`});
+  const pp=JSON.stringify(path);
+  return h+`<button onclick='addC(${pp},false)'>+ condition</button><button onclick='addC(${pp},true)'>+ group</button></div>`}
+function renderCond(){$('cond').innerHTML=condHtml(ruleConds,[]);condPreview()}
+let condOut={};
+async function condPreview(){const r=await fetch('/api/designer/conditions/sql',{method:'POST',headers:{'Content-Type':'application/json'},
+  body:JSON.stringify({conditions:ruleConds,ruleType:$('ru-type').value,pivots:$('ru-pivots').value.split(',').map(x=>x.trim()).filter(x=>x)})});
+  const j=await r.json();condOut=j.result||{};$('ru-sql').textContent=condOut.condition||'';$('ru-err').textContent=condOut.error||'';}
+async function addRule(){await condPreview();if(condOut.error){$('status').textContent='rule: '+condOut.error;return}
+  const p={_S_ruleId:$('ru-id').value,_S_ruleType:$('ru-type').value,_S_productId:flow.name,_S_ruleDescription:$('ru-id').value,
+  _S_condition:condOut.condition,_S_tagName:'Tag',_S_tag:$('ru-tag').value,_S_severity:$('ru-sev').value,
+  _S_isAlert:$('ru-alert').checked,_S_alertSinks:$('ru-sinks').value.split(',').filter(x=>x),_S_aggs:condOut.aggs||[],
+  _S_pivots:condOut.pivots||[],schemaTableName:'DataXProcessedInput',conditions:JSON.parse(JSON.stringify(ruleConds))};
+  flow.gui.rules.push({id:p._S_ruleId,type:'tag',properties:p});ruleConds={type:'group',conjunction:'and',conditions:[newCond()]};
+  renderLists();renderCond();}
 function addOut(){const t=$('o-type').value,v=$('o-target').value,p={};
   if(t==='local'||t==='blob'){p.folder=v;p.blobPartitionFormat='yyyy/MM/dd/HH';p.format='json';p.compressionType='none'}
   else if(t==='eventhub'||t==='cosmosdb'||t==='sql'){p.connectionString=v}else if(t==='httppost'){p.endpoint=v}
