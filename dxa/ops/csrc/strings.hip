@@ -5,6 +5,7 @@
 // Strings are views (start, len) into a byte arena; producing kernels are two-pass (length, then exclusive scan
 // on the stream, then write), so no kernel ever needs dynamic allocation.
 #include "dxa_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -121,6 +122,52 @@ __global__ void str_gather_kernel(const uint8_t* __restrict__ arena, const int64
     uint8_t* d = dst + dst_off[i];
     const int32_t l = lens[i];
     for (int32_t k = lane; k < l; k += 64) d[k] = s[k];
+  }
+}
+
+// Lane-per-string gather (the default): window panes and exchanges compact millions of short strings (device
+// types, regions, ids: 4-20 B), where a wave per string leaves 60 of 64 lanes idle.  Each lane copies its string
+// with unaligned 8-byte global loads/stores and a 4/2/1-byte tail (stores never touch a neighbour's bytes);
+// strings longer than 128 B are copied afterwards by the whole wave, one at a time (ballot loop).
+// Window flow: 19 gathers of 1 M strings per batch took 730 us with the wave-per-string kernel.
+typedef uint64_t u64u __attribute__((aligned(1)));
+typedef uint32_t u32u __attribute__((aligned(1)));
+typedef uint16_t u16u __attribute__((aligned(1)));
+#define SG1 __attribute__((address_space(1)))
+
+__device__ __forceinline__ void copy_short(const SG1 uint8_t* s, SG1 uint8_t* d, int32_t l) {
+  int32_t k = 0;
+  for (; k + 8 <= l; k += 8) *(SG1 u64u*)(d + k) = *(const SG1 u64u*)(s + k);
+  if (k + 4 <= l) { *(SG1 u32u*)(d + k) = *(const SG1 u32u*)(s + k); k += 4; }
+  if (k + 2 <= l) { *(SG1 u16u*)(d + k) = *(const SG1 u16u*)(s + k); k += 2; }
+  if (k < l) d[k] = s[k];
+}
+
+__global__ __launch_bounds__(256) void str_gather_lane_kernel(const uint8_t* __restrict__ arena,
+                                                              const int64_t* __restrict__ starts,
+                                                              const int32_t* __restrict__ lens, int64_t n,
+                                                              const int64_t* __restrict__ dst_off,
+                                                              uint8_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const SG1 uint8_t* s = nullptr;
+  SG1 uint8_t* d = nullptr;
+  int32_t l = 0;
+  if (i < n) {
+    l = lens[i];
+    s = (const SG1 uint8_t*)arena + starts[i];
+    d = (SG1 uint8_t*)dst + dst_off[i];
+  }
+  const bool lng = l > 128;
+  if (!lng && l > 0) copy_short(s, d, l);
+  uint64_t m = __ballot(lng);
+  const int lane = threadIdx.x & 63;
+  while (m) {
+    const int j = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const SG1 uint8_t* sj = (const SG1 uint8_t*)__shfl((uint64_t)(uintptr_t)s, j);
+    SG1 uint8_t* dj = (SG1 uint8_t*)__shfl((uint64_t)(uintptr_t)d, j);
+    const int32_t lj = __shfl(l, j);
+    for (int32_t k = lane; k < lj; k += 64) dj[k] = sj[k];
   }
 }
 
@@ -359,8 +406,13 @@ DXA_API int dxa_str_cmp_col(const uint8_t* aa, const int64_t* as, const int32_t*
 DXA_API int dxa_str_gather(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
                            const int64_t* dst_off, uint8_t* dst, void* st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(str_gather_kernel, dim3(dxa_blocks(n * 64, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
-                     lens, n, dst_off, dst);
+  static const bool wave_per_string = getenv("DXA_STR_GATHER_WAVE") != nullptr;     // A/B: previous kernel
+  if (wave_per_string)
+    hipLaunchKernelGGL(str_gather_kernel, dim3(dxa_blocks(n * 64, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
+                       lens, n, dst_off, dst);
+  else
+    hipLaunchKernelGGL(str_gather_lane_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st,
+                       arena, starts, lens, n, dst_off, dst);
   return (int)hipGetLastError();
 }
 

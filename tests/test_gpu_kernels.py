@@ -389,3 +389,24 @@ def test_multi_column_take_matches_cpu(gpu):
     b = t_gpu.take(idx.to(gpu)).to_pylist()
     assert json.dumps(a, default=str) == json.dumps(b, default=str)
     assert t_gpu.take(torch.empty(0, dtype=torch.int64, device=gpu)).length == 0
+
+
+def test_string_gather_lengths_and_alignments(gpu):
+    """Compaction (lane-per-string gather with unaligned 8/4/2/1-byte copies; > 128-byte strings by the whole
+    wave) against the CPU gather: every length 0..300, every source alignment, nulls, views in random order."""
+    rnd = random.Random(7)
+    words = []
+    for k in range(2000):
+        L = k % 301 if k % 7 else rnd.choice([0, 1, 7, 8, 9, 129, 300, 1000])
+        words.append("".join(chr(97 + rnd.randint(0, 25)) for _ in range(L)) if rnd.random() > 0.05 else None)
+    c = strings_from_pylist(words, "cpu")
+    # views in shuffled order into the same arena (non-contiguous, unaligned starts)
+    perm = torch.tensor(rnd.sample(range(len(words)), len(words)), dtype=torch.int64)
+    view = c.take(perm)
+    want = [words[i] for i in perm.tolist()]
+    assert S.compact(view).to_pylist() == want
+    gv = c.to(gpu).take(perm.to(gpu))
+    got = S.compact(gv)
+    assert got.to_pylist() == want
+    assert S.compact_known(gv, int(gv.lens.to(torch.int64).sum())).to_pylist() == want
+    assert [x.to_pylist() for x in S.compact_many([gv, gv.take(torch.arange(5, device=gpu))])] == [want, want[:5]]
