@@ -204,8 +204,8 @@ def test_gpu_lz4_wave_decoder_edge_cases():
         else:
             parts.append(parts[rnd.randrange(len(parts))])
     data = b"".join(parts)
-    for block in (1000, 4096, 16384, 40000, 65536, 131072):
-        f = lz4.compress_frame(data, block)
+    for block, level in ((1000, 0), (4096, 0), (16384, 0), (16384, 9), (40000, 9), (65536, 0), (131072, 0)):
+        f = lz4.compress_frame(data, block, level=level)
         for known in (block, None):
             fr = lz4.DeviceFrame.from_frame(f, known).to(dev)
             out = lz4.decompress_device(fr, check=True)
