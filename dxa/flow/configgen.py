@@ -220,7 +220,7 @@ def s500_reference_data(s: Session):
 
 
 def s500_functions(s: Session):
-    udfs, udafs, azf = [], [], []
+    udfs, udafs, azf, hip = [], [], [], []
     for f in s.gui.get("process", {}).get("functions") or []:
         p = dict(f.get("properties") or {})
         t = f.get("type", "").lower()
@@ -229,13 +229,18 @@ def s500_functions(s: Session):
         elif t == "jarudaf":
             udafs.append({"name": f["id"], "class": p.get("class"), "path": p.get("path"),
                           "libs": p.get("libs") or []})
+        elif t == "hipudf":
+            # a HIP __device__ function (dxa.udf.hip): the MI355X form of a jar UDF
+            hip.append({"name": f["id"], "source": p.get("source") or p.get("path"), "entry": p.get("entry") or f["id"],
+                        "returnType": p.get("returnType") or "double", "argTypes": p.get("argTypes") or [],
+                        "nullSafe": str(bool(p.get("nullSafe"))).lower()})
         elif t == "azurefunction":
             azf.append({"name": f["id"], "serviceEndpoint": p.get("serviceEndpoint"), "api": p.get("api"),
                         "code": _secret(s, "azurefunc", p.get("code")), "methodType": p.get("methodType", "get"),
                         "params": p.get("params") or []})
         else:
             raise ConfigGenerationError(f"unsupported function type {f.get('type')}")
-    s.tokens.update(processJarUDFs=udfs, processJarUDAFs=udafs, processAzureFunctions=azf)
+    s.tokens.update(processJarUDFs=udfs, processJarUDAFs=udafs, processAzureFunctions=azf, processHipUDFs=hip)
 
 
 def s500_state_tables(s: Session):
@@ -308,7 +313,7 @@ def s600_job_config(s: Session):
         "metric": ({"httppost": s.metrics_endpoint} if s.metrics_endpoint else
                    {"file": os.path.join(base, "metrics", "batch_metrics.jsonl")}),
         "timestampColumn": t["processTimestampColumn"], "watermark": t["processWatermark"],
-        "jarUDAFs": t["processJarUDAFs"], "jarUDFs": t["processJarUDFs"],
+        "jarUDAFs": t["processJarUDAFs"], "jarUDFs": t["processJarUDFs"], "hipUDFs": t.get("processHipUDFs", []),
         "azureFunctions": t["processAzureFunctions"], "projections": [s.paths["projection"]],
         "timeWindows": t["processTimeWindows"], "transform": s.paths["transform"], "appendEventTags": {},
         "accumulationTables": t["processStateTables"]}

@@ -179,6 +179,9 @@ DEFAULT_SPEC: Dict = {
             "timeWindows": _scoped("timewindow", {"windowDuration": "windowduration"}),
             "jarUDFs": _scoped("jar.udf", _jar()),
             "jarUDAFs": _scoped("jar.udaf", _jar()),
+            "hipUDFs": _scoped("hipudf", {"source": "source", "entry": "entry", "returnType": "returntype",
+                                          "argTypes": {"type": "stringList", "namespace": "argtypes"},
+                                          "nullSafe": "nullsafe"}),
             "accumulationTables": _scoped("statetable", {"schema": "schema", "location": "location"}),
             "azureFunctions": _scoped("azurefunction", {
                 "serviceEndpoint": "serviceendpoint", "api": "api", "code": "code", "methodType": "methodtype",

@@ -18,6 +18,7 @@ import torch
 
 from ..config.settings import SettingDictionary
 from ..engine.types import StructField, StructType
+from ..udf.samples import HEALTH_SCORE_HIP
 
 N_DEVICES = 50
 N_HOMES = 50
@@ -299,7 +300,11 @@ def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Opti
             "datax.job.input.default.referencedata.myDevicesRefdata.path": ref,
             "datax.job.input.default.referencedata.myDevicesRefdata.format": "csv",
             "datax.job.input.default.referencedata.myDevicesRefdata.header": "true",
-            "datax.job.process.jar.udf.healthScore.class": "dxa.udf.samples:HealthScore",
+            # the flow's "Scala UDF" is a HIP device function here (dxa.udf.hip), compiled with hipRTC at startup
+            "datax.job.process.hipudf.healthScore.source": HEALTH_SCORE_HIP,
+            "datax.job.process.hipudf.healthScore.entry": "health_score",
+            "datax.job.process.hipudf.healthScore.returntype": "double",
+            "datax.job.process.hipudf.healthScore.argtypes": "double;long",
             "datax.job.process.statetable.DeviceState.schema":
                 "deviceId long, homeId long, deviceType string, LastSeen timestamp, EventCount long, "
                 "MaxTemperature double",

@@ -3,7 +3,8 @@
 Keys (reference handlers): ``datax.job.process.udf.<name>=<class>`` dynamic UDFs (ExtendedUDFHandler.scala:16-104),
 ``datax.job.process.jar.udf.<name>.class`` / ``jar.udaf.<name>.class`` (JarUDFHandler.scala:14-63),
 ``datax.job.process.azurefunction.<name>.{serviceendpoint,api,code,methodtype,params}`` (AzureFunctionHandler.scala:
-14-65), plus the built-in ``stringToTimestamp`` / ``filterNull`` which the expression engine implements natively.
+14-65), ``datax.job.process.hipudf.<name>.{source,entry,returntype,argtypes,nullsafe}`` (HIP device functions,
+``dxa.udf.hip``), plus the built-in ``stringToTimestamp`` / ``filterNull`` which the expression engine implements natively.
 """
 from __future__ import annotations
 
@@ -63,6 +64,10 @@ def build_udfs(d: S.SettingDictionary, udfs: Dict, udafs: Dict) -> Tuple[Dict, D
         out_udfs[name.lower()] = inst
     for name, sub in d.group_by_sub_namespace(S.PROCESS_PREFIX + "jar.udaf.").items():
         out_udafs[name.lower()] = _instantiate(sub.get_string("class"))
+    # HIP-source device UDFs (the MI355X form of a jar UDF)
+    from .hip import from_settings as hip_udf
+    for name, sub in d.group_by_sub_namespace(S.PROCESS_PREFIX + "hipudf.").items():
+        out_udfs[name.lower()] = hip_udf(name, sub)
     # HTTP functions
     from .http import HttpFunctionUDF
     for name, sub in d.group_by_sub_namespace(S.PROCESS_PREFIX + "azurefunction.").items():

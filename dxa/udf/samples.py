@@ -85,6 +85,23 @@ class HealthScore:
         return PrimColumn("double", 0.7 * bat + 0.3 * sig, valid)
 
 
+HEALTH_SCORE_HIP = r"""
+__device__ __forceinline__ double clamp100(double x) { return x < 0.0 ? 0.0 : (x > 100.0 ? 100.0 : x); }
+__device__ double health_score(double battery, long long rssi) {
+  return 0.7 * clamp100(battery) + 0.3 * clamp100(((double)rssi + 110.0) * (100.0 / 70.0));
+}
+"""
+
+
+class HealthScoreHip:
+    """``HealthScore`` written as a HIP device function (``dxa.udf.hip``): what a Scala UDF jar becomes here."""
+
+    def __new__(cls):
+        from .hip import HipUDF
+        return HipUDF(source=HEALTH_SCORE_HIP, entry="health_score", return_type="double",
+                      arg_types=["double", "long"])
+
+
 REFERENCE_CLASS_MAP = {
     "datax.sample.udf.UdfHelloWorld": UdfHelloWorld,
     "datax.sample.dynamicudf.DynamicUdfHelloWorld": DynamicUdfHelloWorld,
