@@ -220,7 +220,7 @@ def s500_reference_data(s: Session):
 
 
 def s500_functions(s: Session):
-    udfs, udafs, azf, hip = [], [], [], []
+    udfs, udafs, azf, hip, hipa = [], [], [], [], []
     for f in s.gui.get("process", {}).get("functions") or []:
         p = dict(f.get("properties") or {})
         t = f.get("type", "").lower()
@@ -234,13 +234,18 @@ def s500_functions(s: Session):
             hip.append({"name": f["id"], "source": p.get("source") or p.get("path"), "entry": p.get("entry") or f["id"],
                         "returnType": p.get("returnType") or "double", "argTypes": p.get("argTypes") or [],
                         "nullSafe": str(bool(p.get("nullSafe"))).lower()})
+        elif t == "hipudaf":
+            hipa.append({"name": f["id"], "source": p.get("source") or p.get("path"), "prefix": p.get("prefix") or "",
+                         "returnType": p.get("returnType") or "double", "argTypes": p.get("argTypes") or [],
+                         "nullSafe": str(bool(p.get("nullSafe"))).lower()})
         elif t == "azurefunction":
             azf.append({"name": f["id"], "serviceEndpoint": p.get("serviceEndpoint"), "api": p.get("api"),
                         "code": _secret(s, "azurefunc", p.get("code")), "methodType": p.get("methodType", "get"),
                         "params": p.get("params") or []})
         else:
             raise ConfigGenerationError(f"unsupported function type {f.get('type')}")
-    s.tokens.update(processJarUDFs=udfs, processJarUDAFs=udafs, processAzureFunctions=azf, processHipUDFs=hip)
+    s.tokens.update(processJarUDFs=udfs, processJarUDAFs=udafs, processAzureFunctions=azf, processHipUDFs=hip,
+                    processHipUDAFs=hipa)
 
 
 def s500_state_tables(s: Session):
@@ -314,6 +319,7 @@ def s600_job_config(s: Session):
                    {"file": os.path.join(base, "metrics", "batch_metrics.jsonl")}),
         "timestampColumn": t["processTimestampColumn"], "watermark": t["processWatermark"],
         "jarUDAFs": t["processJarUDAFs"], "jarUDFs": t["processJarUDFs"], "hipUDFs": t.get("processHipUDFs", []),
+        "hipUDAFs": t.get("processHipUDAFs", []),
         "azureFunctions": t["processAzureFunctions"], "projections": [s.paths["projection"]],
         "timeWindows": t["processTimeWindows"], "transform": s.paths["transform"], "appendEventTags": {},
         "accumulationTables": t["processStateTables"]}

@@ -182,6 +182,9 @@ DEFAULT_SPEC: Dict = {
             "hipUDFs": _scoped("hipudf", {"source": "source", "entry": "entry", "returnType": "returntype",
                                           "argTypes": {"type": "stringList", "namespace": "argtypes"},
                                           "nullSafe": "nullsafe"}),
+            "hipUDAFs": _scoped("hipudaf", {"source": "source", "prefix": "prefix", "returnType": "returntype",
+                                            "argTypes": {"type": "stringList", "namespace": "argtypes"},
+                                            "nullSafe": "nullsafe"}),
             "accumulationTables": _scoped("statetable", {"schema": "schema", "location": "location"}),
             "azureFunctions": _scoped("azurefunction", {
                 "serviceEndpoint": "serviceendpoint", "api": "api", "code": "code", "methodType": "methodtype",

@@ -176,3 +176,139 @@ def from_settings(name: str, sub) -> HipUDF:
     return HipUDF(source=src, entry=sub.get("entry") or name, return_type=sub.get("returntype") or "double",
                   arg_types=sub.get_string_seq("argtypes") or [],
                   null_safe=(sub.get("nullsafe") or "false").lower() == "true")
+
+
+class HipUDAF:
+    """A user aggregate as HIP device code — the MI355X form of a jar UDAF (Spark ``UserDefinedAggregateFunction``,
+    JarUDFHandler.scala:42-62; sample udaf/UdafLastThreshold.scala:11-56).  The source defines::
+
+        struct State { ... };
+        __device__ void init(State& s);
+        __device__ void update(State& s, T0 a0, T1 a1, ...);      // + one `bool ok_j` per argument when null_safe
+        __device__ RT finish(const State& s, bool& valid);         // set valid = false for a null result
+
+    Rows are ordered by group (stable, so each group sees its rows in input order, as Spark's update order within a
+    partition) and one lane folds one group: init, update per row (rows with a null argument are skipped unless
+    null_safe), finish.  No merge step: a UDAF has no partial state in the distributed GROUP BY, whose rows are
+    shuffled to the key's owner first (dxa.engine.distagg)."""
+    source: str = ""
+    return_type: str = "double"
+    arg_types: Sequence[str] = ()
+    null_safe: bool = False
+    prefix: str = ""                 # names are <prefix>State / <prefix>init / <prefix>update / <prefix>finish
+
+    def __init__(self, source: Optional[str] = None, return_type: Optional[str] = None,
+                 arg_types: Optional[Sequence[str]] = None, null_safe: Optional[bool] = None,
+                 prefix: Optional[str] = None):
+        if source is not None:
+            self.source = source
+        if return_type is not None:
+            self.return_type = return_type
+        if arg_types is not None:
+            self.arg_types = list(arg_types)
+        if null_safe is not None:
+            self.null_safe = null_safe
+        if prefix is not None:
+            self.prefix = prefix
+        self.return_type = _norm_type(self.return_type)
+        self.arg_types = [_norm_type(t) for t in self.arg_types]
+        if self.prefix and not _IDENT.match(self.prefix):
+            raise HipUdfError(f"HIP UDAF prefix {self.prefix!r} is not a C identifier")
+        if not self.source.strip():
+            raise HipUdfError("HIP UDAF source is empty")
+        digest = hashlib.sha256(f"{self.prefix}|{self.return_type}|{self.arg_types}|{self.null_safe}|"
+                                f"{self.source}".encode()).hexdigest()[:12]
+        self.kernel_name = f"dxa_hipudaf_{digest}"
+
+    def render(self, host: bool) -> str:
+        P = self.prefix
+        rt = _TYPES[self.return_type][0]
+        params = ["long long ngroups", "const long long* __restrict__ start", "const long long* __restrict__ order"]
+        for j, t in enumerate(self.arg_types):
+            params.append(f"const {_TYPES[t][0]}* __restrict__ in{j}")
+            params.append(f"const unsigned char* __restrict__ ok{j}")
+        params += [f"{rt}* __restrict__ out", "unsigned char* __restrict__ out_ok"]
+        oks = [f"(ok{j} == nullptr || ok{j}[r])" for j in range(len(self.arg_types))]
+        args = [f"in{j}[r]" for j in range(len(self.arg_types))]
+        if self.null_safe:
+            upd = f"{P}update(s{''.join(', ' + a for a in args)}{''.join(', (bool)' + o for o in oks)});"
+        else:
+            upd = f"if ({' && '.join(oks) or 'true'}) {P}update(s{''.join(', ' + a for a in args)});"
+        body = (f"    {P}State s;\n    {P}init(s);\n"
+                f"    for (long long k = start[g]; k < start[g + 1]; ++k) {{\n"
+                f"      const long long r = order[k];\n      {upd}\n    }}\n"
+                f"    bool valid = true;\n    const {rt} v = ({rt}){P}finish(s, valid);\n"
+                f"    out[g] = valid ? v : ({rt})0;\n    out_ok[g] = valid;\n")
+        if host:
+            return (f"#include <cmath>\n#include <cstdint>\n#define __device__\n#define __forceinline__ inline\n"
+                    f"{self.source}\n"
+                    f"extern \"C\" void {self.kernel_name}({', '.join(params)}) {{\n"
+                    f"  for (long long g = 0; g < ngroups; ++g) {{\n{body}  }}\n}}\n")
+        return (f"#include <hip/hip_runtime.h>\n{self.source}\n"
+                f"extern \"C\" __global__ __launch_bounds__(256) void {self.kernel_name}({', '.join(params)}) {{\n"
+                f"  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;\n"
+                f"  if (g < ngroups) {{\n{body}  }}\n}}\n")
+
+    def aggregate(self, cols, groups, ctx):
+        from ..engine.column import ConstColumn, PrimColumn, materialize
+        from ..ops import rtc
+        if len(cols) != len(self.arg_types):
+            raise HipUdfError(f"UDAF takes {len(self.arg_types)} arguments, got {len(cols)}")
+        device = groups.rep.device
+        ng = int(groups.ngroups)
+        gid = groups.gid.to(torch.int64)
+        order = torch.argsort(gid, stable=True)
+        counts = torch.bincount(gid, minlength=ng) if gid.numel() else torch.zeros(ng, dtype=torch.int64,
+                                                                                   device=device)
+        start = torch.zeros(ng + 1, dtype=torch.int64, device=device)
+        if ng:
+            torch.cumsum(counts, 0, out=start[1:])
+        keep = [order, start]
+        args: List[ctypes._SimpleCData] = [ctypes.c_longlong(ng), ctypes.c_void_p(start.data_ptr()),
+                                           ctypes.c_void_p(order.data_ptr())]
+        for c, t in zip(cols, self.arg_types):
+            c = materialize(c)
+            if isinstance(c, ConstColumn):
+                c = c.materialize()
+            if not isinstance(c, PrimColumn):
+                raise HipUdfError(f"UDAF argument of type {getattr(c, 'dtype', '?')} is not numeric")
+            d = c.data.to(device=device, dtype=_TYPES[t][1]).contiguous()
+            if d.dtype == torch.bool:
+                d = d.view(torch.uint8)
+            keep.append(d)
+            args.append(ctypes.c_void_p(d.data_ptr()))
+            if c.valid is not None:
+                v = c.valid.to(device).contiguous().view(torch.uint8)
+                keep.append(v)
+                args.append(ctypes.c_void_p(v.data_ptr()))
+            else:
+                args.append(ctypes.c_void_p(0))
+        out = torch.empty(max(ng, 1), dtype=_TYPES[self.return_type][1], device=device)
+        out_ok = torch.empty(max(ng, 1), dtype=torch.bool, device=device)
+        args += [ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(out_ok.data_ptr())]
+        if ng:
+            if device.type == "cuda":
+                from ..ops import native as N
+                fn = rtc.function(self.render(host=False), self.kernel_name)
+                rtc.launch(fn, (ng + 255) // 256, 256, N.stream_handle(device), args)
+            else:
+                f = getattr(rtc.host_compile(self.render(host=True)), self.kernel_name)
+                f.restype = None
+                f(*args)
+        sql_type = {"float": "double", "bigint": "long", "integer": "int"}.get(self.return_type, self.return_type)
+        return PrimColumn(sql_type, out[:ng], out_ok[:ng])
+
+
+def udaf_from_settings(name: str, sub) -> HipUDAF:
+    """``datax.job.process.hipudaf.<name>.{source,prefix,returntype,argtypes,nullsafe}`` → HipUDAF."""
+    from ..config.secrets import resolve
+    from ..io import fs
+    src = sub.get("source")
+    if not src:
+        raise HipUdfError(f"hipudaf {name}: 'source' is required")
+    src = resolve(src)
+    if "__device__" not in src:
+        src = fs.read_text(src)
+    return HipUDAF(source=src, return_type=sub.get("returntype") or "double",
+                   arg_types=sub.get_string_seq("argtypes") or [], prefix=sub.get("prefix") or "",
+                   null_safe=(sub.get("nullsafe") or "false").lower() == "true")

@@ -4,7 +4,7 @@ Keys (reference handlers): ``datax.job.process.udf.<name>=<class>`` dynamic UDFs
 ``datax.job.process.jar.udf.<name>.class`` / ``jar.udaf.<name>.class`` (JarUDFHandler.scala:14-63),
 ``datax.job.process.azurefunction.<name>.{serviceendpoint,api,code,methodtype,params}`` (AzureFunctionHandler.scala:
 14-65), ``datax.job.process.hipudf.<name>.{source,entry,returntype,argtypes,nullsafe}`` (HIP device functions,
-``dxa.udf.hip``), plus the built-in ``stringToTimestamp`` / ``filterNull`` which the expression engine implements natively.
+``dxa.udf.hip``), ``datax.job.process.hipudaf.<name>.*`` (HIP device aggregates), plus the built-in ``stringToTimestamp`` / ``filterNull`` which the expression engine implements natively.
 """
 from __future__ import annotations
 
@@ -68,6 +68,9 @@ def build_udfs(d: S.SettingDictionary, udfs: Dict, udafs: Dict) -> Tuple[Dict, D
     from .hip import from_settings as hip_udf
     for name, sub in d.group_by_sub_namespace(S.PROCESS_PREFIX + "hipudf.").items():
         out_udfs[name.lower()] = hip_udf(name, sub)
+    from .hip import udaf_from_settings as hip_udaf
+    for name, sub in d.group_by_sub_namespace(S.PROCESS_PREFIX + "hipudaf.").items():
+        out_udafs[name.lower()] = hip_udaf(name, sub)
     # HTTP functions
     from .http import HttpFunctionUDF
     for name, sub in d.group_by_sub_namespace(S.PROCESS_PREFIX + "azurefunction.").items():

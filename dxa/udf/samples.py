@@ -93,6 +93,25 @@ __device__ double health_score(double battery, long long rssi) {
 """
 
 
+LAST_BY_TIME_HIP = r"""
+// the value at the latest event time of the group (ties: the later row) — UdafLastThreshold.scala:11-56 on numbers
+struct State { long long t; double v; bool any; };
+__device__ void init(State& s) { s.any = false; s.t = 0; s.v = 0.0; }
+__device__ void update(State& s, long long t, double v) {
+  if (!s.any || s.t <= t) { s.t = t; s.v = v; s.any = true; }
+}
+__device__ double finish(const State& s, bool& valid) { valid = s.any; return s.v; }
+"""
+
+
+class LastByTimeHip:
+    """``lastByTime(eventTime, value)``: a HIP device UDAF (``dxa.udf.hip.HipUDAF``)."""
+
+    def __new__(cls):
+        from .hip import HipUDAF
+        return HipUDAF(source=LAST_BY_TIME_HIP, return_type="double", arg_types=["timestamp", "double"])
+
+
 class HealthScoreHip:
     """``HealthScore`` written as a HIP device function (``dxa.udf.hip``): what a Scala UDF jar becomes here."""
 

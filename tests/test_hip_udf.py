@@ -113,3 +113,64 @@ def test_hipudf_flow_function_through_configgen(tmp_path):
     b, s = _cols(50, "cpu", seed=5)
     assert _close(udfs["healthscore"]([b, s], None, 50, torch.device("cpu")).to_pylist(),
                   HealthScore()([b, s], None, 50, torch.device("cpu")).to_pylist())
+
+
+def _last_by_time_reference(keys, ts, vals):
+    best = {}
+    for k, t, v in zip(keys, ts, vals):
+        if t is None or v is None:
+            continue
+        if k not in best or best[k][0] <= t:
+            best[k] = (t, v)
+    return best
+
+
+def _udaf_table(n, device, seed=4):
+    rnd = random.Random(seed)
+    keys = [rnd.randint(0, 40) for _ in range(n)]
+    ts = [None if rnd.random() < 0.05 else rnd.randint(0, 50) for _ in range(n)]     # many ties
+    vals = [None if rnd.random() < 0.05 else rnd.uniform(0, 10) for _ in range(n)]
+    t = Table(["k", "t", "v"], [column_from_pylist(keys, "long", device), column_from_pylist(ts, "timestamp", device),
+                                column_from_pylist(vals, "double", device)], n, torch.device(device))
+    return t, keys, ts, vals
+
+
+def test_hip_udaf_group_by_on_host():
+    from dxa.udf.samples import LastByTimeHip
+    t, keys, ts, vals = _udaf_table(3000, "cpu")
+    cat = Catalog()
+    cat.register("T", t)
+    out = run_sql("SELECT k, lastByTime(t, v) AS lv, COUNT(*) AS n FROM T GROUP BY k", cat,
+                  EvalContext(udafs={"lastbytime": LastByTimeHip()}))
+    best = _last_by_time_reference(keys, ts, vals)
+    got = dict(zip(out.column("k").to_pylist(), out.column("lv").to_pylist()))
+    assert got == {k: (best[k][1] if k in best else None) for k in set(keys)}
+
+
+def test_hipudaf_settings():
+    from dxa.udf.samples import LAST_BY_TIME_HIP
+    d = SettingDictionary({"datax.job.process.hipudaf.lastByTime.source": LAST_BY_TIME_HIP,
+                           "datax.job.process.hipudaf.lastByTime.returntype": "double",
+                           "datax.job.process.hipudaf.lastByTime.argtypes": "timestamp;double"})
+    _, udafs, _ = build_udfs(d, {}, {})
+    t, keys, ts, vals = _udaf_table(400, "cpu", seed=8)
+    cat = Catalog()
+    cat.register("T", t)
+    out = run_sql("SELECT k, lastByTime(t, v) AS lv FROM T GROUP BY k", cat, EvalContext(udafs=udafs))
+    best = _last_by_time_reference(keys, ts, vals)
+    assert dict(zip(out.column("k").to_pylist(), out.column("lv").to_pylist())) == \
+        {k: (best[k][1] if k in best else None) for k in set(keys)}
+
+
+@pytest.mark.gpu
+def test_hip_udaf_on_gpu(gpu):
+    from dxa.udf.samples import LastByTimeHip
+    t, keys, ts, vals = _udaf_table(200_000, gpu, seed=12)
+    cat = Catalog()
+    cat.register("T", t)
+    out = run_sql("SELECT k, lastByTime(t, v) AS lv FROM T GROUP BY k", cat,
+                  EvalContext(udafs={"lastbytime": LastByTimeHip()}))
+    assert out.column("lv").data.is_cuda
+    best = _last_by_time_reference(keys, ts, vals)
+    assert dict(zip(out.column("k").to_pylist(), out.column("lv").to_pylist())) == \
+        {k: (best[k][1] if k in best else None) for k in set(keys)}
