@@ -60,8 +60,11 @@ batch interval (s) <input id="i-window" size="4" value="1"> max rate <input id="
 header <select id="r-hdr"><option>true</option><option>false</option></select><button onclick="addRef()">add</button></div></section>
 <section id="tab-functions"><h3>Functions</h3><table id="funcs"></table>
 <div class="row">id <input id="fn-id"> type <select id="fn-type"><option>jarUDF</option><option>jarUDAF</option>
-<option>azureFunction</option></select> class / endpoint <input id="fn-class" size="40">
-<button onclick="addFunc()">add</button></div></section>
+<option>hipUDF</option><option>hipUDAF</option><option>azureFunction</option></select>
+class / endpoint / HIP entry <input id="fn-class" size="30"> return type <input id="fn-rt" size="8" value="double">
+argument types <input id="fn-args" size="18" placeholder="double,long"><button onclick="addFunc()">add</button></div>
+<p class="muted">hipUDF: a <code>__device__</code> scalar function; hipUDAF: <code>State</code> + init / update / finish
+device functions (compiled for the GPU at job start)</p><textarea id="fn-src" style="height:90px"></textarea></section>
 <section id="tab-query"><h3>Query</h3>
 <textarea id="q-text" style="height:220px">--DataXQuery--
 T1 = SELECT * FROM DataXProcessedInput;
@@ -133,14 +136,18 @@ function collect(){const g=flow.gui,i=g.input,p=i.properties;flow.name=$('f-name
   g.process.jobconfig={...(g.process.jobconfig||{}),jobNumGpus:$('s-gpus').value};return flow;}
 function renderLists(){const g=flow.gui;
   $('refs').innerHTML=(g.input.referenceData||[]).map((r,k)=>`<tr><td>${esc(r.id)}</td><td>${esc(r.properties.path)}</td><td><button onclick="del('ref',${k})">x</button></td></tr>`).join('');
-  $('funcs').innerHTML=(g.process.functions||[]).map((f,k)=>`<tr><td>${esc(f.id)}</td><td>${esc(f.type)}</td><td>${esc(f.properties.class||f.properties.serviceEndpoint)}</td><td><button onclick="del('fn',${k})">x</button></td></tr>`).join('');
+  $('funcs').innerHTML=(g.process.functions||[]).map((f,k)=>`<tr><td>${esc(f.id)}</td><td>${esc(f.type)}</td><td>${esc(f.properties.class||f.properties.serviceEndpoint||f.properties.entry)}</td><td><button onclick="del('fn',${k})">x</button></td></tr>`).join('');
   $('rules').innerHTML=(g.rules||[]).map((r,k)=>{const p=r.properties;return `<tr><td>${esc(p._S_ruleId)}</td><td>${esc(p._S_ruleType)}</td><td>${esc(p._S_condition)}</td><td>${esc(p._S_tag)}</td><td>${esc(p._S_severity)}</td><td>${p._S_isAlert?'alert':''}</td><td><button onclick="del('rule',${k})">x</button></td></tr>`}).join('');
   $('outs').innerHTML=(g.outputs||[]).map((o,k)=>`<tr><td>${esc(o.id)}</td><td>${esc(o.type)}</td><td>${esc(JSON.stringify(o.properties))}</td><td><button onclick="del('out',${k})">x</button></td></tr>`).join('');
   $('sched').innerHTML=(g.batchList||[]).map((b,k)=>`<tr><td>${esc(b.type)}</td><td>${esc(JSON.stringify(b.properties))}</td><td>${b.disabled?'disabled':''}</td><td><button onclick="del('batch',${k})">x</button></td></tr>`).join('');}
 function del(kind,k){const g=flow.gui;({ref:g.input.referenceData,fn:g.process.functions,rule:g.rules,out:g.outputs,batch:g.batchList})[kind].splice(k,1);renderLists();}
 function addRef(){flow.gui.input.referenceData.push({id:$('r-id').value,type:'csv',properties:{path:$('r-path').value,delimiter:$('r-del').value,header:$('r-hdr').value==='true'}});renderLists();}
-function addFunc(){const t=$('fn-type').value,v=$('fn-class').value;flow.gui.process.functions.push({id:$('fn-id').value,type:t,
-  properties:t==='azureFunction'?{serviceEndpoint:v,api:'',code:'',methodType:'get',params:[]}:{class:v,path:'',libs:[]}});renderLists();}
+function addFunc(){const t=$('fn-type').value,v=$('fn-class').value;let p;
+  if(t==='azureFunction')p={serviceEndpoint:v,api:'',code:'',methodType:'get',params:[]};
+  else if(t==='hipUDF'||t==='hipUDAF')p={source:$('fn-src').value,entry:v||$('fn-id').value,returnType:$('fn-rt').value,
+    argTypes:$('fn-args').value.split(',').map(x=>x.trim()).filter(x=>x)};
+  else p={class:v,path:'',libs:[]};
+  flow.gui.process.functions.push({id:$('fn-id').value,type:t,properties:p});renderLists();}
 const OPS=[['equal','='],['notEqual','<>'],['greater','>'],['lessThan','<'],['greaterThanOrEqual','>='],
   ['lessThanOrEqual','<='],['stringEqual','= text'],['stringNotEqual','<> text'],['contains','contains'],
   ['notContains','not contains'],['startsWith','starts with'],['endsWith','ends with']];
