@@ -24,6 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-Wno-unused-result", "-Wno-unused-command-line-argument"]
+LINK_LIBS = ["-lhiprtc", "-lhsa-runtime64"]      # hipRTC (fused expressions, HIP UDFs), ROCr (SDMA copies)
 HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wno-unused-function"]
 
 
@@ -32,7 +33,7 @@ def _digest(paths) -> str:
     for p in sorted(paths):
         h.update(p.name.encode())
         h.update(p.read_bytes())
-    h.update(" ".join(HIP_FLAGS + HOST_FLAGS).encode())
+    h.update(" ".join(HIP_FLAGS + HOST_FLAGS + LINK_LIBS).encode())
     return h.hexdigest()
 
 
@@ -58,7 +59,7 @@ def build_variant(name: str, defines, csrc: Path = CSRC) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(compile_one, sorted(csrc.glob("*.hip"))))
-    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-lhiprtc", "-o", str(lib)])
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), *LINK_LIBS, "-o", str(lib)])
     for o in objs:
         o.unlink(missing_ok=True)
     print(f"[dxa.build] built variant {lib}", file=sys.stderr)
@@ -84,7 +85,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(compile_one, hip_srcs))
-    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-lhiprtc", "-o", str(LIB)])
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), *LINK_LIBS, "-o", str(LIB)])
     if host_srcs:
         _run(["g++", *HOST_FLAGS, "-shared", *map(str, host_srcs), "-I", str(CSRC), "-lz", "-o", str(HOST_LIB)])
     for o in objs:

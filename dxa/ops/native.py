@@ -30,6 +30,7 @@ _SIGS = {
     "dxa_lz4_block_sizes": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_lz4_decode": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_memcpy_h2d_async": [c_p, c_p, c_i64, c_p],
+    "dxa_copy_sdma": [c_p, c_p, c_i64],
     "dxa_serialize_lengths": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p],
     "dxa_serialize_write": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],

@@ -280,6 +280,27 @@ class _DevBuilder:
         return raw, text
 
 
+_SDMA = os.environ.get("DXA_D2H_SDMA", "1") != "0"
+
+
+def d2h(host: torch.Tensor, dev: torch.Tensor, nbytes: int, stream) -> None:
+    """Copy the first ``nbytes`` of ``dev`` into pinned ``host`` and wait.  The producing work must be complete.
+    Runs on an SDMA engine (``dxa_copy_sdma``): a hipMemcpy D2H into pinned memory is a blit kernel that holds CUs
+    for the whole PCIe transfer.  Falls back to the stream copy if the runtime refuses the pointers."""
+    global _SDMA
+    if nbytes <= 0:
+        return
+    if _SDMA:
+        from . import native as N
+        rc = N.lib().dxa_copy_sdma(host.data_ptr(), dev.data_ptr(), nbytes)
+        if rc == 0:
+            return
+        _SDMA = False
+    with torch.cuda.stream(stream):
+        host[:nbytes].copy_(dev[:nbytes], non_blocking=True)
+    stream.synchronize()
+
+
 _side_streams = {}
 _side_lock = threading.Lock()
 
@@ -354,8 +375,8 @@ class Staged:
             N.call("dxa_serialize_write", N.ptr(nodes), nn, N.ptr(prog_t), nprog, N.ptr(text), tw, n, N.ptr(offs),
                    N.ptr(out), st)
             host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
-            host.copy_(out[:total], non_blocking=True)
             side.synchronize()
+            d2h(host, out, total, side)
         self.table = None
         return JsonLines(host.numpy(), host_lens.numpy() - 1)     # the pinned buffer itself, no copy
 

@@ -410,3 +410,13 @@ def test_string_gather_lengths_and_alignments(gpu):
     assert got.to_pylist() == want
     assert S.compact_known(gv, int(gv.lens.to(torch.int64).sum())).to_pylist() == want
     assert [x.to_pylist() for x in S.compact_many([gv, gv.take(torch.arange(5, device=gpu))])] == [want, want[:5]]
+
+
+def test_sdma_device_to_host_copy(gpu):
+    """dxa_copy_sdma (ROCr async copy on a DMA engine) copies a device range into pinned host memory."""
+    from dxa.ops import native as N
+    src = torch.randint(0, 256, (3_000_001,), dtype=torch.uint8, device=gpu)
+    host = torch.empty(3_000_001, dtype=torch.uint8, pin_memory=True)
+    torch.cuda.synchronize()
+    assert N.lib().dxa_copy_sdma(host.data_ptr(), src.data_ptr() + 1, 3_000_000) == 0
+    assert torch.equal(host[:3_000_000], src[1:].cpu())
