@@ -104,12 +104,20 @@ def main():
     # NUMA placement first, from sysfs alone: threads the HIP runtime and RCCL start later inherit the mask, and the
     # pinned staging buffers are first-touched on the GPU's socket
     from dxa.parallel.affinity import bind_to_device
-    numa_cpus = bind_to_device(local) if torch.cuda.device_count() > local else None
-    device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    ndev = torch.cuda.device_count()
+    # DXA_DIST_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing a GPU (collectives staged
+    # through host memory); the default on GPUs is RCCL with one rank per GPU
+    backend = os.environ.get("DXA_DIST_BACKEND") or ("nccl" if ndev else "gloo")
+    dev_index = local % ndev if (ndev and backend == "gloo") else local
+    numa_cpus = bind_to_device(dev_index) if ndev > dev_index else None
+    device = torch.device("cuda", dev_index) if torch.cuda.is_available() else torch.device("cpu")
     if world > 1:
         if device.type == "cuda":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=device)          # RCCL over xGMI
+            torch.cuda.set_device(dev_index)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)      # RCCL over xGMI
+            else:
+                dist.init_process_group("gloo")
         else:
             dist.init_process_group("gloo")                              # CPU rehearsal of the same code path
     on_gpu = device.type == "cuda"
@@ -279,10 +287,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        cdev = device if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        lt = torch.tensor(sorted(lat), dtype=torch.float64, device=device)
+        lt = torch.tensor(sorted(lat), dtype=torch.float64, device=cdev)
         gathered = [torch.empty_like(lt) for _ in range(world)]
         dist.all_gather(gathered, lt)
         lat = sorted(float(x) for g in gathered for x in g.tolist())

@@ -26,21 +26,55 @@ def _w():
     return _WORLD
 
 
+def _staged(t: torch.Tensor) -> bool:
+    """Device tensors over gloo go through host memory: lets a multi-rank run share one GPU (rehearsal of the RCCL
+    path on a single-GPU machine — every kernel on the device, only the collectives on the host)."""
+    return t.is_cuda and dist.get_backend(_g()) == "gloo"
+
+
+def _all_reduce(t: torch.Tensor, op) -> None:
+    if _staged(t):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=_g())
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=_g())
+
+
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> None:
+    if _staged(out):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=_g())
+        out.copy_(h)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=_g())
+
+
+def _all_gather(outs: List[torch.Tensor], t: torch.Tensor) -> None:
+    if _staged(t):
+        hs = [torch.empty(o.shape, dtype=o.dtype) for o in outs]
+        dist.all_gather(hs, t.cpu(), group=_g())
+        for o, h in zip(outs, hs):
+            o.copy_(h)
+    else:
+        dist.all_gather(outs, t, group=_g())
+
+
 def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
     if _w() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_g())
+        _all_reduce(t, dist.ReduceOp.SUM)
     return t
 
 
 def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
     if _w() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_g())
+        _all_reduce(t, dist.ReduceOp.MAX)
     return t
 
 
 def _a2a_counts(counts: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(counts)
-    dist.all_to_all_single(out, counts, group=_g())
+    _a2a(out, counts)
     return out
 
 
@@ -190,7 +224,7 @@ def shuffle_table(table, dest: torch.Tensor):
     if C:
         send = torch.stack(mat_cols, 1).contiguous() if n else torch.empty((0, C), dtype=torch.int64, device=device)
         recv = torch.empty((n_out, C), dtype=torch.int64, device=device)
-        dist.all_to_all_single(recv, send, recv_rows, send_rows, group=_g())
+        _a2a(recv, send, recv_rows, send_rows)
     else:
         recv = torch.empty((n_out, 0), dtype=torch.int64, device=device)
     # string bytes: rows are already grouped by destination, so each leaf's packed bytes are too
@@ -202,8 +236,7 @@ def shuffle_table(table, dest: torch.Tensor):
         sc = sops.compact_known(lf.col, sum(send_bytes))
         total = sum(recv_bytes)
         out = torch.zeros(total + 16, dtype=torch.uint8, device=device)
-        dist.all_to_all_single(out[:total], sc.arena[:sum(send_bytes)].contiguous(), recv_bytes, send_bytes,
-                               group=_g())
+        _a2a(out[:total], sc.arena[:sum(send_bytes)].contiguous(), recv_bytes, send_bytes)
         rlens = recv[:, lf.mcol]
         starts = torch.cumsum(rlens, 0) - rlens
         str_out[li] = (out, starts, rlens.to(torch.int32))
@@ -269,7 +302,7 @@ def rebalance_table(table):
     device = table.device
     n = table.length
     counts = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(W)]
-    dist.all_gather(counts, torch.tensor([n], dtype=torch.int64, device=device), group=_g())
+    _all_gather(counts, torch.tensor([n], dtype=torch.int64, device=device))
     offset = int(sum(torch.cat(counts).tolist()[:_RANK]))          # one host read-back
     dest = (torch.arange(n, dtype=torch.int64, device=device) + offset) % W
     return shuffle_table(table, dest)

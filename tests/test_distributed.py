@@ -41,25 +41,27 @@ def _canon(rows):
     return sorted(out, key=repr)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, device="cpu"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         import torch.distributed as dist
+        if device != "cpu":
+            torch.cuda.set_device(0)       # every rank on the one GPU; collectives staged through gloo
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from dxa import parallel as P
         from dxa.engine.column import Table
         from dxa.engine.expr import EvalContext
         from dxa.engine.query import Catalog, run_sql
         from dxa.engine.types import StructField, StructType
-        P.init(dist.group.WORLD, "cpu")
+        P.init(dist.group.WORLD, device)
         schema = StructType((StructField("k", "long"), StructField("s", "string"), StructField("v", "double")))
         rows = _rows(1, 400)
         rows2 = [{"k": k, "s": "x", "v": 1.0} for k in range(0, 20, 2) for _ in range(2)]
         mine = rows[rank::world]
         mine2 = rows2[rank::world]
-        t = Table.from_pylist(mine, schema)
+        t = Table.from_pylist(mine, schema, device)
         t.dist = P.PARTITIONED
-        t2 = Table.from_pylist(mine2, schema)
+        t2 = Table.from_pylist(mine2, schema, device)
         t2.dist = P.PARTITIONED
         cat = Catalog()
         cat.register("T", t)
@@ -73,12 +75,12 @@ def _worker(rank, world, port, q):
         # paned window aggregation over partitioned panes (partials exchanged, not rows)
         results.append(_window_results(t, P))
         # raw shuffle round trip
-        dest = torch.tensor([i % world for i in range(t.length)], dtype=torch.int64)
+        dest = torch.tensor([i % world for i in range(t.length)], dtype=torch.int64, device=device)
         got = P.shuffle_table(t, dest)
         back = P.allgather_table(got)
         results.append(back.to_pylist())
         # round-robin rebalance of a skewed batch (input repartition): 300 + 100 rows → 200 + 200
-        skew = Table.from_pylist(rows[:300] if rank == 0 else rows[300:], schema)
+        skew = Table.from_pylist(rows[:300] if rank == 0 else rows[300:], schema, device)
         reb = P.rebalance_table(skew)
         results.append((reb.length, P.allgather_table(reb).to_pylist()))
         q.put((rank, results, None))
@@ -102,7 +104,7 @@ def _window_results(t, P):
     views = None
     for b in range(4):
         T = (100 + b) * S
-        ts = PrimColumn("timestamp", torch.full((t.length,), T + 1, dtype=torch.int64))
+        ts = PrimColumn("timestamp", torch.full((t.length,), T + 1, dtype=torch.int64, device=t.device))
         tb = t.with_column("ts", ts)
         tb.dist = t.dist
         views, _ = store.process(tb, T, S)
@@ -125,7 +127,12 @@ def _free_port():
     return p
 
 
-def test_two_rank_queries_match_single_process():
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_two_rank_queries_match_single_process(device):
+    """``cuda``: both ranks on the one GPU of a test box, every kernel on the device and the collectives staged
+    through gloo — the distributed operators' device code on real hardware, short of RCCL itself."""
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
     from dxa.engine.column import Table
     from dxa.engine.expr import EvalContext
     from dxa.engine.query import Catalog, run_sql
@@ -133,7 +140,7 @@ def test_two_rank_queries_match_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, device)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -167,14 +174,21 @@ def test_two_rank_queries_match_single_process():
         assert n_r == 200 and _canon(everything) == _canon(rows)
 
 
-@pytest.mark.parametrize("flow", ["groupby", "window"])
-def test_bench_two_ranks_gloo(flow, tmp_path):
+@pytest.mark.parametrize("flow,device", [("groupby", "cpu"), ("window", "cpu"),
+                                         pytest.param("groupby", "cuda", marks=pytest.mark.gpu)])
+def test_bench_two_ranks_gloo(flow, device, tmp_path):
     """bench.py's multi-rank path (the driver's N-GPU scaling run) rehearsed on CPU: two ranks, gloo, one JSON line
     whose value aggregates both ranks — catches collective mismatches before they reach RCCL."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PYTHONPATH=root)
+    if device == "cuda":
+        if not torch.cuda.is_available():
+            pytest.skip("no GPU")
+        env["DXA_DIST_BACKEND"] = "gloo"          # both ranks share the test box's one GPU
+    else:
+        env["HIP_VISIBLE_DEVICES"] = ""
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                         os.path.join(root, "bench.py"), "--gpus", "2", "--flow", flow, "--events-per-batch", "500",
