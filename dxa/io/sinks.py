@@ -22,7 +22,7 @@ import time
 import uuid
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 from ..config.secrets import resolve
 from ..engine.column import Table
@@ -84,6 +84,13 @@ class Sink:
     write: Callable[[List[str], Table, _dt.datetime, str], int]
     filter_expr: Optional[str] = None
     as_json: bool = True
+    # grouped sinks (blob): rows are split by the string value of ``group_expr`` (a single "main" group without
+    # one) and ``write`` is called once per configured group as write(lines, group, ts, target)
+    groups: Optional[List[str]] = None
+    group_expr: Optional[str] = None
+
+
+DEFAULT_OUTPUT_GROUP = "main"                # BlobSinker.scala:32
 
 
 def _joined(lines):
@@ -105,19 +112,18 @@ def _blob_sink(d, output_name) -> Optional[Sink]:
     fmt = (d.get("format") or "json").lower()
     group_eval = d.get("groupevaluation")
 
-    def write(lines, table, ts, target):
-        total = 0
-        for g, folder in groups.items():
-            folder = blob_folder(resolve(folder), ts, target)
-            data = _joined(lines)
-            suffix = ".json" + (".gz" if compression != "none" else "")
-            path = folder + f"part-{uuid.uuid4().hex[:12]}{suffix}"
-            if len(lines):
-                fs.write_with_timeout(path, data, timeout_s=float(os.environ.get("DATAX_BlobWriterTimeout", 10)),
-                                      gzip_it=compression != "none")
-            total += len(lines)
-        return total
-    return Sink("Blobs", write, group_eval)
+    def write(lines, group, ts, target):
+        """One group's rows into its folder (BlobSinker.sinkDataGroups, :128-157); unknown groups are dropped."""
+        folder = groups.get(group)
+        if folder is None or not len(lines):
+            return 0
+        folder = blob_folder(resolve(folder), ts, target)
+        suffix = ".json" + (".gz" if compression != "none" else "")
+        path = folder + f"part-{uuid.uuid4().hex[:12]}{suffix}"
+        fs.write_with_timeout(path, _joined(lines), timeout_s=float(os.environ.get("DATAX_BlobWriterTimeout", 10)),
+                              gzip_it=compression != "none")
+        return len(lines)
+    return Sink("Blobs", write, groups=sorted(groups), group_expr=group_eval)
 
 
 def _eventhub_sink(d, output_name) -> Optional[Sink]:
@@ -295,6 +301,9 @@ class OutputOperator:
         whole = None
         for s in self.sinks:
             sub = t
+            if s.groups is not None:
+                st.items.append((s, self._split_groups(s, t, ctx, capture)))
+                continue
             if s.filter_expr:
                 from ..engine.expr import EvalContext, Scope, evaluate, predicate_mask
                 from ..sql.parser import parse_expression
@@ -309,6 +318,30 @@ class OutputOperator:
                 payload = _HostRows(t)
             st.items.append((s, payload))
         return st
+
+    @staticmethod
+    def _split_groups(s: Sink, t: Table, ctx, capture) -> Dict[str, Any]:
+        """Rows of a grouped sink by group name: the flag column is a string expression (BlobSinker.scala:175-183,
+        ``rows.groupBy(flagColumn)``); without one every row belongs to "main".  One host read of the distinct group
+        names; each group is a row subset captured for serialization."""
+        if not s.group_expr:
+            return {DEFAULT_OUTPUT_GROUP: capture(t)}
+        from ..engine.column import materialize
+        from ..engine.expr import EvalContext, Scope, evaluate
+        from ..ops import groupby as G
+        from ..sql.parser import parse_expression
+        col = materialize(evaluate(parse_expression(s.group_expr), Scope.of_table(t), ctx or EvalContext()))
+        if hasattr(col, "materialize") and not hasattr(col, "take"):
+            col = col.materialize()
+        groups = G.group_rows([col])
+        names = col.take(groups.rep).to_pylist()
+        out = {}
+        for k, name in enumerate(names):
+            if name is None or str(name) not in s.groups:
+                continue
+            idx = (groups.gid == k).nonzero().flatten()
+            out[str(name)] = capture(t.take(idx))
+        return out
 
     def output(self, table: Table, partition_time: _dt.datetime, ctx=None, target: Optional[str] = None
                ) -> Dict[str, int]:
@@ -338,7 +371,12 @@ class StagedOutput:
         metrics = {f"{SINK_PREFIX}InputEvents": self.n}
         # the key set must not depend on the data: ranks all-reduce the batch metrics as one vector
         for s in self.op.sinks:
-            metrics[f"{SINK_PREFIX}{s.name}_{'Filtered' if s.filter_expr else 'All'}"] = 0
+            if s.groups is not None:             # BlobSinker: <Sink>_Events_<group>, <Sink>_Count_<group> (files)
+                for g in s.groups:
+                    metrics[f"{SINK_PREFIX}{s.name}_Events_{g}"] = 0
+                    metrics[f"{SINK_PREFIX}{s.name}_Count_{g}"] = 0
+            else:
+                metrics[f"{SINK_PREFIX}{s.name}_{'Filtered' if s.filter_expr else 'All'}"] = 0
         if self.n == 0:
             return metrics
         rendered = {}
@@ -353,6 +391,14 @@ class StagedOutput:
 
         def run(item):
             s, payload = item
+            if s.groups is not None:
+                out = {}
+                for g, p in payload.items():
+                    lines, _ = lines_of(p)
+                    cnt = s.write(lines, g, partition_time, target)
+                    out[f"{SINK_PREFIX}{s.name}_Events_{g}"] = cnt
+                    out[f"{SINK_PREFIX}{s.name}_Count_{g}"] = 1 if cnt else 0
+                return out
             lines, rows = lines_of(payload)
             cnt = s.write(lines if lines is not None else [], rows, partition_time, target)
             return {f"{SINK_PREFIX}{s.name}_{'Filtered' if s.filter_expr else 'All'}": cnt}
@@ -361,7 +407,8 @@ class StagedOutput:
             metrics.update(run(self.items[0]))
         else:
             for s, payload in self.items:        # render shared payloads once, before fanning out
-                lines_of(payload)
+                if s.groups is None:
+                    lines_of(payload)
             for r in _sink_pool.map(run, self.items):
                 for k, v in r.items():
                     metrics[k] = metrics.get(k, 0) + v
