@@ -80,10 +80,16 @@ def main():
     ap.add_argument("--lz4-level", type=int, default=9,
                     help="pinned-lz4: producer compression level (Kafka compression.lz4.level; 9 is Kafka's default, "
                          "0 = fast greedy compressor)")
-    ap.add_argument("--source", choices=["pinned", "pinned-lz4", "device", "gpu-sim"], default=None,
+    ap.add_argument("--source", choices=["pinned", "pinned-lz4", "kafka", "device", "gpu-sim"], default=None,
                     help="pinned: H2D copy of raw bytes every step; pinned-lz4: H2D copy of an LZ4 frame of JSON "
-                         "lines, decoded + newline-framed on the GPU; device: bytes already in HBM; gpu-sim: GPU "
+                         "lines, decoded + newline-framed on the GPU; kafka: Kafka v2 record batches (LZ4 codec) as "
+                         "a multi-partition Fetch returns them, planned on the host, decompressed and record-framed "
+                         "on the GPU (the Kafka source's path); device: bytes already in HBM; gpu-sim: GPU "
                          "generator renders each batch")
+    ap.add_argument("--kafka-partitions", type=int, default=16, help="kafka: partitions per fetch (planned in "
+                    "parallel on the host, as per-partition fetch threads would)")
+    ap.add_argument("--kafka-batch-records", type=int, default=26,
+                    help="kafka: records per producer batch (26 SimulatedData events = ~16 KiB, one LZ4 block)")
     ap.add_argument("--profile-stages", action="store_true")
     ap.add_argument("--sync-outputs", action="store_true",
                     help="finish each batch's sink writes before the next batch starts (default: pipelined)")
@@ -151,6 +157,9 @@ def main():
     t_gen = time.perf_counter()
     pool = []
     comp_bytes = []
+    import numpy as np
+    from dxa.ops import lz4
+    lz4_block_k = args.lz4_block or lz4.DEFAULT_BLOCK
     if source == "pinned-lz4":
         from dxa.ops import lz4
         from dxa.ops.jsonparse import frame_lines_gpu
@@ -164,6 +173,30 @@ def main():
             del buf, offs
             comp_bytes.append(frame.size)
             pool.append(lz4.DeviceFrame.from_frame(frame, lz4_block, pin=on_gpu))
+    kafka_parts, kafka_json = [], []
+    if source == "kafka":
+        from dxa.io import kafka as K
+        parts = max(1, args.kafka_partitions)
+        for p in range(args.pool):
+            buf, offs = generate(prog, E, device, seed=1000 * rank + p + 1, row0=p * E, base_ms=clock0_us // 1000)
+            hb, ho = buf.cpu().numpy(), offs.cpu().numpy()
+            del buf, offs
+            cuts = np.linspace(0, E, parts + 1).astype(np.int64)
+            sets = [K.encode_stream(hb, ho[cuts[q]:cuts[q + 1] + 1], args.kafka_batch_records, base_offset=0,
+                                    compression="lz4", level=args.lz4_level, block_size=lz4_block_k,
+                                    threads=16) for q in range(parts)]
+            total = sum(x.size for x in sets)
+            staging = torch.empty(total + 64, dtype=torch.uint8, pin_memory=on_gpu)
+            sn = staging.numpy()
+            bounds, pos = [], 0
+            for x in sets:
+                sn[pos:pos + x.size] = x
+                bounds.append((pos, pos + x.size))
+                pos += x.size
+            comp_bytes.append(total)
+            pool.append(staging)
+            kafka_parts.append(bounds)
+            kafka_json.append(int(ho[-1]))
     if source in ("pinned", "device"):
         base_ms = clock0_us // 1000
         for p in range(args.pool):
@@ -177,15 +210,36 @@ def main():
         torch.cuda.synchronize(device)
     gen_s = time.perf_counter() - t_gen
 
-    side = torch.cuda.Stream(device) if (on_gpu and source in ("pinned", "pinned-lz4", "gpu-sim")) else None
+    side = torch.cuda.Stream(device) if (on_gpu and source in ("pinned", "pinned-lz4", "kafka", "gpu-sim")) else None
     ingest = lz4.ChunkedIngest(device, chunks=args.lz4_chunks, copy_stream=side) \
         if (on_gpu and source == "pinned-lz4") else None
+    kdec = None
+    if source == "kafka":
+        from concurrent.futures import ThreadPoolExecutor
+        from dxa.io import kafka_device as KD
+        planners = ThreadPoolExecutor(max_workers=min(16, max(1, args.kafka_partitions)))
+        if on_gpu:
+            kdec = KD.DeviceRecordDecoder(device, chunks=args.lz4_chunks, copy_stream=side)
     staged = {}
     sizes = []
     framing_checks = []        # device flags: a frame's newline count differed from its producer's record count
 
     def stage(i):
         """Make batch i's raw bytes available in HBM — on a side stream, overlapping batch i-1's processing."""
+        if source == "kafka":
+            staging, bounds = pool[i % len(pool)], kafka_parts[i % len(pool)]
+            sn = staging.numpy()
+            # per-partition plans (headers only), in parallel as per-partition fetch threads would
+            plans = list(planners.map(lambda b: KD.plan_fetch(sn[b[0]:b[1]], 0), bounds))
+            plan = KD.merge([(pl, b[0]) for pl, b in zip(plans, bounds)])
+            if kdec is not None:
+                raw, ev = kdec.decode(staging, plan)
+            else:
+                out, st, en = KD.decode_on_host_like(sn, plan)
+                raw, ev = RawBatch(torch.from_numpy(out), torch.from_numpy(np.append(st, plan.out_bytes)),
+                                   plan.nrec, ends=torch.from_numpy(en)), None
+            staged[i] = (raw, None, ev)
+            return
         if source == "gpu-sim":
             def gen():
                 bt_ms = batch_time(i) // 1000
@@ -234,18 +288,20 @@ def main():
 
     def step(i):
         db, do, ev = staged.pop(i)
+        rb = db if isinstance(db, RawBatch) else RawBatch(db, do, E)
         if ev is not None:
             cur = torch.cuda.current_stream(device)
             cur.wait_event(ev)
-            db.record_stream(cur)
-            do.record_stream(cur)
+            for t in (rb.buf, rb.offs, rb.ends):
+                if t is not None:
+                    t.record_stream(cur)
         t_s = time.perf_counter()
         stage(i + depth)
         t_p = time.perf_counter()
-        m = proc.process_batch(RawBatch(db, do, E), batch_time(i), interval_us)
+        m = proc.process_batch(rb, batch_time(i), interval_us)
         if host_trace is not None:
             host_trace.append((i, round((t_p - t_s) * 1e3, 2), round((time.perf_counter() - t_p) * 1e3, 2)))
-        sizes.append(db.shape[0])
+        sizes.append(kafka_json[i % len(pool)] + 16 if source == "kafka" else rb.buf.shape[0])
         return m
 
     depth = max(1, args.prefetch)
@@ -299,6 +355,8 @@ def main():
     if framing_checks:
         from dxa.ops.jsonparse import check_framing
         check_framing(framing_checks)                      # after the timed region: one host sync
+    if kdec is not None:
+        kdec.check()                                       # every record batch decoded (one host sync)
 
     def pct(p):
         if not lat_sorted:
@@ -323,7 +381,10 @@ def main():
         "dtype": "fp64/int64 columns (no reduced precision)",
         "data": "synthetic (SimulatedData-schema JSON generated on device, random seeds per rank/batch"
                 + ("; delivered as LZ4-framed batches in pinned host memory, decompressed on the GPU in every step)"
-                   if source == "pinned-lz4" else ")"),
+                   if source == "pinned-lz4" else
+                   "; delivered as Kafka v2 record batches with the LZ4 codec in pinned host memory (a "
+                   "multi-partition Fetch), planned on the host, decompressed and record-framed on the GPU in every "
+                   "step)" if source == "kafka" else ")"),
         "config": {"model": MODEL[flow].format(ref=args.ref_rows), "flow": flow,
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
                    "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,
@@ -340,7 +401,10 @@ def main():
         out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)
         out["config"]["lz4_ratio"] = round((sum(sizes) / len(sizes) - 16) / (sum(comp_bytes) / len(comp_bytes)), 2)
         out["config"]["lz4_level"] = args.lz4_level
-        out["config"]["lz4_block_bytes"] = lz4_block
+        out["config"]["lz4_block_bytes"] = lz4_block_k
+    if source == "kafka":
+        out["config"]["kafka_partitions"] = args.kafka_partitions
+        out["config"]["kafka_batch_records"] = args.kafka_batch_records
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
     if last:

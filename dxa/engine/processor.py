@@ -52,6 +52,8 @@ class RawBatch:
     system_properties: Optional[Any] = None   # per-event SystemProperties map column (or None → {})
     file_info: Optional[Dict[str, Any]] = None
     source_bytes: int = 0
+    ends: Optional[torch.Tensor] = None       # int64 [n] record ends when records are not back to back (Kafka
+                                              # values in decompressed record batches); offs[n] = end of the bytes
 
 
 def _read_lines(path: str) -> List[str]:
@@ -162,10 +164,19 @@ class Processor:
         t0 = time.perf_counter()
         buf = raw.buf
         offs = raw.offs
+        ends = raw.ends
         if self.normalizer is not None:
+            if ends is not None:                  # normalizers take back-to-back records: pack the values first
+                from .column import StrColumn
+                starts = offs[:-1]
+                packed = StrColumn(buf, starts, (ends - starts).to(torch.int32)).compact()
+                buf = packed.arena
+                offs = torch.cat([packed.starts, (packed.starts[-1:] + packed.lens[-1:].to(torch.int64))
+                                  if raw.n else torch.zeros(1, dtype=torch.int64, device=buf.device)])
+                ends = None
             buf, offs = self.normalizer(buf, offs)
         with tracing.stage("parse"):
-            raw_col, row_ok = parse(buf, offs, self.parse_plan)
+            raw_col, row_ok = parse(buf, offs, self.parse_plan, ends)
         self._sync()
         self.stage_times["parse"] = time.perf_counter() - t0
         n = raw.n

@@ -54,6 +54,12 @@ def _lib():
         L.dxa_kafka_encode.restype = ctypes.c_void_p
         L.dxa_kafka_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                        ctypes.c_int32, ctypes.c_void_p]
+        L.dxa_kafka_encode_stream.restype = ctypes.c_void_p
+        L.dxa_kafka_encode_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int64] * 4 + \
+            [ctypes.c_int32] * 4 + [ctypes.c_void_p]
+        L.dxa_kafka_encode_lz4.restype = ctypes.c_void_p
+        L.dxa_kafka_encode_lz4.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
         _LIB = L
     return _LIB
 
@@ -65,21 +71,53 @@ def crc32c(data: bytes) -> int:
 CODECS = {"none": 0, "gzip": 1, "lz4": 3}
 
 
-def encode_batch(values: Sequence[bytes], timestamp_ms: Optional[int] = None, compression: str = "none") -> bytes:
-    """One v2 record batch holding ``values`` (null keys); ``compression`` none / gzip / lz4."""
+def encode_batch(values: Sequence[bytes], timestamp_ms: Optional[int] = None, compression: str = "none",
+                 level: int = 1, block_size: int = 64 * 1024) -> bytes:
+    """One v2 record batch holding ``values`` (null keys); ``compression`` none / gzip / lz4 (``level`` and LZ4
+    frame ``block_size`` as Kafka's compression.lz4.level / the producer's block size)."""
     vals = b"".join(values)
     offs = np.zeros(len(values) + 1, dtype=np.int64)
     if values:
         offs[1:] = np.cumsum([len(v) for v in values])
+    return encode_batch_arrays(np.frombuffer(vals, np.uint8), offs, timestamp_ms, compression, level, block_size)
+
+
+def encode_batch_arrays(vals: np.ndarray, offs: np.ndarray, timestamp_ms: Optional[int] = None,
+                        compression: str = "none", level: int = 1, block_size: int = 64 * 1024) -> bytes:
+    """``encode_batch`` over a values buffer + int64 offsets [n+1] (no per-record Python objects)."""
+    vals = np.ascontiguousarray(vals)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    n = int(offs.shape[0]) - 1
     out_len = ctypes.c_int64(0)
     L = _lib()
-    ptr = L.dxa_kafka_encode(vals, offs.ctypes.data, len(values),
-                             int(time.time() * 1000) if timestamp_ms is None else timestamp_ms,
-                             CODECS[compression.lower()], ctypes.byref(out_len))
+    ptr = L.dxa_kafka_encode_lz4(vals.ctypes.data, offs.ctypes.data, n,
+                                 int(time.time() * 1000) if timestamp_ms is None else timestamp_ms,
+                                 CODECS[compression.lower()], level, block_size, ctypes.byref(out_len))
     if not ptr:
         raise KafkaError(f"record batch encode failed ({compression})")
     try:
         return ctypes.string_at(ptr, out_len.value)
+    finally:
+        L.dxa_host_free(ptr)
+
+
+def encode_stream(vals: np.ndarray, offs: np.ndarray, per_batch: int, base_offset: int = 0,
+                  timestamp_ms: Optional[int] = None, compression: str = "lz4", level: int = 9,
+                  block_size: int = 64 * 1024, threads: int = 16) -> np.ndarray:
+    """A producer's record batches of ``per_batch`` records each, back to back as a Fetch response carries them
+    (base offsets from ``base_offset``) → uint8 array.  ``vals`` + int64 ``offs`` [n+1] hold the record values."""
+    vals = np.ascontiguousarray(vals)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    n = int(offs.shape[0]) - 1
+    out_len = ctypes.c_int64(0)
+    L = _lib()
+    ptr = L.dxa_kafka_encode_stream(vals.ctypes.data, offs.ctypes.data, n, per_batch, base_offset,
+                                    int(time.time() * 1000) if timestamp_ms is None else timestamp_ms,
+                                    CODECS[compression.lower()], level, block_size, threads, ctypes.byref(out_len))
+    if not ptr:
+        raise KafkaError(f"record batch stream encode failed ({compression})")
+    try:
+        return np.frombuffer(ctypes.string_at(ptr, out_len.value), dtype=np.uint8).copy()
     finally:
         L.dxa_host_free(ptr)
 
@@ -389,12 +427,15 @@ class KafkaSource(OffsetTrackedSource):
 
     def __init__(self, client: KafkaClient, topics: List[str], device, checkpoint_dir: Optional[str] = None,
                  max_rate: Optional[int] = None, start: int = EARLIEST, flush_existing: bool = False,
-                 rank: int = 0, world: int = 1, max_fetches: int = 64):
+                 rank: int = 0, world: int = 1, max_fetches: int = 64, device_decode: Optional[bool] = None):
         self.client = client
         self.topics = topics
         self.device = torch.device(device)
         self.max_rate = max_rate
         self.max_fetches = max_fetches
+        # record batches decompressed and framed on the GPU (dxa.io.kafka_device); host decoding otherwise
+        self.device_decode = (self.device.type == "cuda") if device_decode is None else device_decode
+        self._decoder = None
         ckpt = Checkpointer(checkpoint_dir) if checkpoint_dir else None
         meta = client.metadata(topics)
         all_parts = [(t, p) for t in topics for p in meta.get(t, [])]
@@ -407,6 +448,59 @@ class KafkaSource(OffsetTrackedSource):
         self._init_offsets(pos, ckpt, hub_of=lambda tp: (tp[0], str(tp[1])))
 
     def next_batch(self, batch_time_us: int) -> Optional[RawBatch]:
+        if self.device_decode:
+            got = self._next_batch_device(batch_time_us)
+            if got is not None:
+                return got
+        return self._next_batch_host(batch_time_us)
+
+    def _next_batch_device(self, batch_time_us: int) -> Optional[RawBatch]:
+        """Fetch, plan batch headers on the host, decode on the GPU.  None (cursor untouched) when a fetched
+        record set needs the host decoder — the batch is then fetched again on the host path."""
+        from . import kafka_device as KD
+        sets, plans = [], []
+        ranges: Dict[Tuple[str, int], Tuple[int, int]] = {}
+        pos = 0
+        for tp in self.parts:
+            start = self.fetch_pos[tp]
+            cur, got = start, 0
+            for _ in range(self.max_fetches):
+                recs, hw = self.client.fetch(tp[0], tp[1], cur)
+                if not recs:
+                    break
+                try:
+                    plan = KD.plan_fetch(recs, cur)
+                except KD.Unsupported:
+                    return None
+                if self.max_rate is not None:
+                    plan = KD.trim(plan, self.max_rate - got)
+                n, nxt = plan.nrec, plan.next_offset
+                if n:
+                    sets.append(recs)
+                    plans.append((plan, pos))
+                    pos += len(recs)
+                got += n
+                cur = max(cur, nxt)
+                if cur >= hw or (self.max_rate is not None and got >= self.max_rate):
+                    break
+            ranges[tp] = (start, cur)
+        staging = torch.empty(pos + 64, dtype=torch.uint8, pin_memory=True)
+        sn = staging.numpy()
+        for recs, (_, at) in zip(sets, plans):
+            sn[at:at + len(recs)] = np.frombuffer(recs, dtype=np.uint8)
+        if self._decoder is None:
+            self._decoder = KD.DeviceRecordDecoder(self.device)
+        raw, done = self._decoder.decode(staging, KD.merge(plans))
+        torch.cuda.current_stream(self.device).wait_event(done)
+        self._record_batch(batch_time_us, ranges)
+        return raw
+
+    def check(self):
+        """Deferred device-decode status check (one host read for all batches decoded since the last call)."""
+        if self._decoder is not None:
+            self._decoder.check()
+
+    def _next_batch_host(self, batch_time_us: int) -> Optional[RawBatch]:
         vals_list, offs_list = [], []
         ranges: Dict[Tuple[str, int], Tuple[int, int]] = {}
         for tp in self.parts:

@@ -1,0 +1,281 @@
+"""Kafka / Event Hubs record batches decoded on the GPU.
+
+The host path (``dxa.io.kafka.decode_records``) decompresses and frames records in C++, which caps a source at a
+few GB/s of JSON per process.  Here the host only walks batch and LZ4-frame headers (``dxa_kafka_plan``: no record
+bytes are touched), the Fetch bytes go to HBM as they arrived from the broker (compressed), and the GPU
+decompresses every LZ4 block (``lz4.hip``, 16 lanes per block, capacity slots because Kafka frames carry no
+content size) and frames the records (``kafka_records.hip``).  The JSON parser then reads each record's value in
+place through per-record [start, end) ranges — the bytes cross PCIe once, compressed, and are never copied on the
+device.
+
+Batches the GPU path does not take (gzip / snappy / zstd codecs, dependent-block LZ4 frames, compacted batches
+with offset gaps) make ``plan_fetch`` raise ``Unsupported``; the source then decodes that fetch on the host.
+CRC-32C is verified on the host when ``verify_crc`` is set (the consumer's ``check.crcs``); the GPU ingest runs
+with it off by default, as a consumer may.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+_PLAN_ERRS = {-2: "message format is not v2", -3: "CRC mismatch", -5: "codec decoded on the host only",
+              -7: "malformed LZ4 frame", -8: "dependent-block LZ4 frame", -9: "offset deltas with gaps"}
+
+
+class Unsupported(Exception):
+    """The fetch needs the host decoder."""
+
+
+_BOUND = False
+
+
+def _lib():
+    global _BOUND
+    from ..ops.serialize import lib
+    L = lib()
+    if not _BOUND:
+        p, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        L.dxa_kafka_plan.argtypes = [p, i64, i64, i32, p, p] + [p] * 11
+        L.dxa_kafka_plan.restype = ctypes.c_int
+        _BOUND = True
+    return L
+
+
+@dataclass
+class FetchPlan:
+    """Host-side plan of one or more Fetch record sets laid out back to back in one staging buffer."""
+    b_count: np.ndarray           # int32 [nbat] records in the batch
+    b_base: np.ndarray            # int64 [nbat] base offset
+    b_skip: np.ndarray            # int32 [nbat] leading records below the fetch offset
+    b_keep: np.ndarray            # int32 [nbat] records emitted after the skipped ones
+    b_first: np.ndarray           # int32 [nbat] first block
+    b_nblk: np.ndarray            # int32 [nbat]
+    b_rec0: np.ndarray            # int64 [nbat] index of the batch's first emitted record
+    k_comp_off: np.ndarray        # int64 [nblk] block payload offset in the staging buffer
+    k_comp_len: np.ndarray        # int32 [nblk]
+    k_stored: np.ndarray          # uint8 [nblk]
+    k_out_off: np.ndarray         # int64 [nblk] output slot
+    k_cap: np.ndarray             # int64 [nblk] slot capacity
+    out_bytes: int
+    next_offset: int
+    nbytes: int = 0               # staging bytes covered
+
+    @property
+    def nbat(self) -> int:
+        return int(self.b_count.shape[0])
+
+    @property
+    def nblk(self) -> int:
+        return int(self.k_comp_off.shape[0])
+
+    @property
+    def nrec(self) -> int:
+        return int(self.b_keep.sum()) if self.nbat else 0
+
+    def last_offsets(self) -> np.ndarray:
+        """Kafka offset of the last emitted record of each batch (for commit ranges)."""
+        return self.b_base + self.b_skip + self.b_keep - 1
+
+
+def plan_fetch(data, min_offset: int, verify_crc: bool = False) -> FetchPlan:
+    """Plan one Fetch record set (bytes / uint8 ndarray) → FetchPlan (offsets relative to ``data``)."""
+    a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    L = _lib()
+    counts = np.zeros(5, dtype=np.int64)
+    nxt = ctypes.c_int64(0)
+    rc = L.dxa_kafka_plan(a.ctypes.data, a.size, min_offset, int(verify_crc), counts.ctypes.data,
+                          ctypes.byref(nxt), *([None] * 11))
+    if rc:
+        raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
+    nbat, nblk = int(counts[0]), int(counts[1])
+    arr = dict(b_count=np.zeros(nbat, np.int32), b_base=np.zeros(nbat, np.int64),
+               b_skip=np.zeros(nbat, np.int32), b_first=np.zeros(nbat, np.int32), b_nblk=np.zeros(nbat, np.int32),
+               b_rec0=np.zeros(nbat, np.int64), k_comp_off=np.zeros(nblk, np.int64),
+               k_comp_len=np.zeros(nblk, np.int32), k_stored=np.zeros(nblk, np.uint8),
+               k_out_off=np.zeros(nblk, np.int64), k_cap=np.zeros(nblk, np.int64))
+    order = ["b_count", "b_base", "b_skip", "b_first", "b_nblk", "b_rec0", "k_comp_off", "k_comp_len", "k_stored",
+             "k_out_off", "k_cap"]
+    rc = L.dxa_kafka_plan(a.ctypes.data, a.size, min_offset, int(verify_crc), counts.ctypes.data,
+                          ctypes.byref(nxt), *[arr[k].ctypes.data for k in order])
+    if rc:
+        raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
+    keep = (arr["b_count"] - arr["b_skip"]).astype(np.int32)
+    return FetchPlan(b_keep=keep, out_bytes=int(counts[3]), next_offset=nxt.value, nbytes=int(a.size), **arr)
+
+
+def merge(plans: Sequence[Tuple[FetchPlan, int]]) -> FetchPlan:
+    """Concatenate plans of record sets staged at the given byte offsets of one buffer."""
+    if not plans:
+        return FetchPlan(*(np.zeros(0, t) for t in (np.int32, np.int64, np.int32, np.int32, np.int32, np.int32,
+                                                      np.int64, np.int64, np.int32, np.uint8, np.int64, np.int64)),
+                         out_bytes=0, next_offset=0)
+    cat = lambda k: np.concatenate([getattr(p, k) for p, _ in plans])  # noqa: E731
+    blk0, out0, rec0 = [], [], []
+    nb = ob = nr = 0
+    for p, _ in plans:
+        blk0.append(nb)
+        out0.append(ob)
+        rec0.append(nr)
+        nb += p.nblk
+        ob += p.out_bytes
+        nr += p.nrec
+    return FetchPlan(
+        b_count=cat("b_count"), b_base=cat("b_base"), b_skip=cat("b_skip"), b_keep=cat("b_keep"),
+        b_first=np.concatenate([p.b_first + b for (p, _), b in zip(plans, blk0)]).astype(np.int32),
+        b_nblk=cat("b_nblk"),
+        b_rec0=np.concatenate([_rec0(p) + r for (p, _), r in zip(plans, rec0)]),
+        k_comp_off=np.concatenate([p.k_comp_off + at for p, at in plans]),
+        k_comp_len=cat("k_comp_len"), k_stored=cat("k_stored"),
+        k_out_off=np.concatenate([p.k_out_off + o for (p, _), o in zip(plans, out0)]),
+        k_cap=cat("k_cap"), out_bytes=ob, next_offset=plans[-1][0].next_offset,
+        nbytes=max(at + p.nbytes for p, at in plans))
+
+
+def _rec0(p: FetchPlan) -> np.ndarray:
+    """Emitted-record index of each batch's first record, from the keep counts (a trim may have changed them)."""
+    if not p.nbat:
+        return np.zeros(0, np.int64)
+    c = np.cumsum(p.b_keep, dtype=np.int64)
+    return c - p.b_keep
+
+
+def trim(p: FetchPlan, max_records: int) -> FetchPlan:
+    """Keep at most ``max_records`` records (a source's maxRate): later batches emit nothing, the batch at the cut
+    emits its first records only.  ``next_offset`` becomes the first offset not emitted."""
+    if p.nrec <= max_records:
+        return p
+    keep = p.b_keep.copy()
+    cum = np.cumsum(keep, dtype=np.int64)
+    cut = int(np.searchsorted(cum, max_records, side="left"))      # first batch reaching the limit
+    before = int(cum[cut - 1]) if cut else 0
+    keep[cut] = max_records - before
+    keep[cut + 1:] = 0
+    q = FetchPlan(**{**p.__dict__, "b_keep": keep.astype(np.int32)})
+    q.b_rec0 = _rec0(q)
+    q.next_offset = int(p.b_base[cut] + p.b_skip[cut] + keep[cut])
+    return q
+
+
+class DeviceRecordDecoder:
+    """Staged Fetch bytes (pinned host) → device RawBatch of record values, on copy + decode streams.
+
+    ``chunks`` splits the H2D copy of the compressed bytes at block boundaries so chunk k's copy overlaps chunk
+    k-1's decode (as ``lz4.ChunkedIngest``)."""
+
+    def __init__(self, device, chunks: int = 4, copy_stream=None, decode_stream=None):
+        self.device = torch.device(device)
+        self.chunks = max(1, chunks)
+        self.copy_stream = copy_stream or torch.cuda.Stream(self.device)
+        self.decode_stream = decode_stream or torch.cuda.Stream(self.device)
+        self.checks: List[torch.Tensor] = []      # per-batch status tensors, checked with check()
+
+    def decode(self, staging: torch.Tensor, plan: FetchPlan):
+        """Returns (RawBatch, done_event).  ``staging`` is a pinned uint8 tensor holding the record sets at the
+        plan's offsets (+32 readable bytes)."""
+        from ..engine.processor import RawBatch
+        from ..ops import native as N
+        dev = self.device
+        n = plan.nrec
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).pin_memory()  # noqa: E731
+        with torch.cuda.stream(self.copy_stream):
+            tabs = [T(x).to(dev, non_blocking=True) for x in (
+                plan.k_comp_off, plan.k_comp_len, plan.k_stored, plan.k_out_off, plan.k_cap, plan.b_count,
+                plan.b_skip, plan.b_keep, plan.b_first, plan.b_nblk, plan.b_rec0)]
+            ddata = torch.empty(plan.nbytes + 32, dtype=torch.uint8, device=dev)
+            tab_ev = torch.cuda.Event()
+            tab_ev.record(self.copy_stream)
+        co, cl, sd, oo, cap, bc, bs, bk, bf, bn, br = tabs
+        with torch.cuda.stream(self.decode_stream):
+            out = torch.empty(plan.out_bytes + 64, dtype=torch.uint8, device=dev)
+            produced = torch.empty(max(1, plan.nblk), dtype=torch.int64, device=dev)
+            bstat = torch.empty(max(1, plan.nblk), dtype=torch.int32, device=dev)
+            offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            ends = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+            rstat = torch.empty(max(1, plan.nbat), dtype=torch.int32, device=dev)
+        self.decode_stream.wait_event(tab_ev)
+        st = self.decode_stream.cuda_stream
+        nb = plan.nblk
+        bounds = np.linspace(0, nb, self.chunks + 1).astype(np.int64)
+        for k in range(self.chunks):
+            b0, b1 = int(bounds[k]), int(bounds[k + 1])
+            if b1 <= b0:
+                continue
+            lo = 0 if k == 0 else int(plan.k_comp_off[b0])
+            hi = plan.nbytes if b1 == nb else int(plan.k_comp_off[b1])
+            N.call("dxa_memcpy_h2d_async", ddata.data_ptr() + lo, staging.data_ptr() + lo, hi - lo,
+                   self.copy_stream.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+            self.decode_stream.wait_event(ev)
+            N.call("dxa_lz4_decode_into", N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
+                   N.ptr(oo[b0:b1]), N.ptr(cap[b0:b1]), b1 - b0, N.ptr(out), N.ptr(produced[b0:b1]),
+                   N.ptr(bstat[b0:b1]), st)
+        with torch.cuda.stream(self.decode_stream):
+            offs[n:].fill_(plan.out_bytes)
+        N.call("dxa_kafka_records", N.ptr(out), plan.nbat, N.ptr(bc), N.ptr(bs), N.ptr(bk), N.ptr(bf), N.ptr(bn),
+               N.ptr(br), N.ptr(oo), N.ptr(cap), N.ptr(produced), N.ptr(bstat), N.ptr(offs), N.ptr(ends),
+               N.ptr(rstat), st)
+        done = torch.cuda.Event()
+        done.record(self.decode_stream)
+        for t in (ddata, produced, bstat, *tabs):
+            t.record_stream(self.decode_stream)
+        self.checks.append(rstat[:plan.nbat])
+        # the pinned bytes must outlive their async copies
+        self._inflight = [(e, b) for e, b in getattr(self, "_inflight", []) if not e.query()] + [(done, staging)]
+        return RawBatch(out, offs, n, ends=ends[:n], source_bytes=plan.nbytes), done
+
+    def check(self):
+        """Raise if any decoded batch failed (one host read of all pending status tensors)."""
+        if not self.checks:
+            return
+        bad = [int((c != 0).sum()) for c in self.checks]
+        self.checks.clear()
+        if any(bad):
+            raise ValueError(f"{sum(bad)} Kafka record batch(es) failed to decode on the device")
+
+
+def decode_on_host_like(staging: np.ndarray, plan: FetchPlan):
+    """CPU reference of ``DeviceRecordDecoder.decode`` (tests): (values buffer, starts, ends)."""
+    from ..ops import lz4
+    out = np.zeros(plan.out_bytes + 64, dtype=np.uint8)
+    starts, ends = [], []
+    for i in range(plan.nbat):
+        f, nb = int(plan.b_first[i]), int(plan.b_nblk[i])
+        p = int(plan.k_out_off[f])
+        end = p
+        for b in range(f, f + nb):                 # a frame's blocks back to back from its first slot
+            src = staging[plan.k_comp_off[b]: plan.k_comp_off[b] + plan.k_comp_len[b]]
+            raw = src.tobytes() if plan.k_stored[b] else lz4.decompress_block(src.tobytes(), int(plan.k_cap[b]))
+            out[end:end + len(raw)] = np.frombuffer(raw, np.uint8)
+            end += len(raw)
+        data = out
+
+        def varint(p):
+            u, s = 0, 0
+            while True:
+                c = int(data[p])
+                p += 1
+                u |= (c & 0x7F) << s
+                s += 7
+                if not c & 0x80:
+                    return (u >> 1) ^ -(u & 1), p
+        skip, keep, count = int(plan.b_skip[i]), int(plan.b_keep[i]), int(plan.b_count[i])
+        for r in range(min(count, skip + keep)):
+            ln, p = varint(p)
+            rec_end = p + ln
+            p += 1
+            _, p = varint(p)
+            _, p = varint(p)
+            kl, p = varint(p)
+            p += max(kl, 0)
+            vl, p = varint(p)
+            if r >= skip:
+                starts.append(p)
+                ends.append(p + max(vl, 0))
+            p = rec_end
+        assert p <= end
+    return out, np.array(starts, np.int64), np.array(ends, np.int64)

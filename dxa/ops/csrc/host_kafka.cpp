@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 #include <zlib.h>
 
@@ -224,9 +225,119 @@ int walk_batches(const uint8_t* data, int64_t len, int64_t min_offset, int64_t m
   return 0;
 }
 
+// ---- device-decode plan -----------------------------------------------------------------------------------------
+// Walks only the record-batch headers and LZ4 frame block headers of a Fetch record set (no record bytes), so the
+// records themselves are decompressed and framed on the GPU (lz4.hip + kafka_records.hip).  Each block gets an
+// output slot: the frame's maximum block size for LZ4 blocks (every block of a frame but the last is full, so a
+// frame's bytes are contiguous from its first slot), its own length for stored data.  Returns 0, or
+// -2 bad magic, -3 CRC, -5 codec the GPU path does not take (gzip / snappy / zstd), -7 malformed LZ4 frame,
+// -8 dependent-block frame, -9 offset deltas that are not 0..count-1 (compacted batch) — the caller decodes such
+// fetches on the host.
+struct Plan {
+  bool write;
+  int32_t* b_count; int64_t* b_base; int32_t* b_skip; int32_t* b_first; int32_t* b_nblk; int64_t* b_rec0;
+  int64_t* k_comp_off; int32_t* k_comp_len; uint8_t* k_stored; int64_t* k_out_off; int64_t* k_cap;
+  int64_t nbat = 0, nblk = 0, nrec = 0, out_bytes = 0;
+  int32_t max_block = 0;
+};
+
+int plan_batches(const uint8_t* data, int64_t len, int64_t min_offset, Plan& pl, int64_t* next_offset,
+                 int verify_crc) {
+  const uint8_t* p = data;
+  const uint8_t* end = data + len;
+  *next_offset = min_offset;
+  while (end - p >= 61) {
+    const int64_t base = be64(p);
+    const int32_t blen = be32(p + 8);
+    if (blen < 49 || end - (p + 12) < blen) break;
+    const uint8_t* b = p + 12;
+    if ((int8_t)b[4] != 2) return -2;
+    const uint32_t crc = (uint32_t)be32(b + 5);
+    const uint8_t* attrs_p = b + 9;
+    const uint8_t* bend = p + 12 + blen;
+    if (verify_crc && crc32c(attrs_p, (size_t)(bend - attrs_p)) != crc) return -3;
+    const int16_t attrs = be16(attrs_p);
+    const int32_t last_delta = be32(attrs_p + 2);
+    const int32_t count = be32(attrs_p + 2 + 4 + 8 + 8 + 8 + 2 + 4);
+    const uint8_t* recs = attrs_p + 2 + 4 + 8 + 8 + 8 + 2 + 4 + 4;
+    const bool control = (attrs >> 5) & 1;
+    if (!control && count > 0 && base + last_delta >= min_offset) {
+      if (last_delta != count - 1) return -9;
+      const int codec = attrs & 7;
+      const int32_t skip = min_offset > base ? (int32_t)(min_offset - base) : 0;
+      const int64_t first = pl.nblk;
+      if (codec == 0) {
+        if (pl.write) {
+          pl.k_comp_off[pl.nblk] = recs - data;
+          pl.k_comp_len[pl.nblk] = (int32_t)(bend - recs);
+          pl.k_stored[pl.nblk] = 1;
+          pl.k_out_off[pl.nblk] = pl.out_bytes;
+          pl.k_cap[pl.nblk] = bend - recs;
+        }
+        pl.out_bytes += bend - recs;
+        ++pl.nblk;
+      } else if (codec == 3) {
+        int64_t content = -1, fend = 0;
+        int32_t mb = 0;
+        const int64_t nb = dxa::lz4::frame_blocks(recs, bend - recs, nullptr, nullptr, nullptr, 0, &content, &mb,
+                                                  &fend);
+        if (nb == -2) return -8;
+        if (nb < 0) return -7;
+        if (pl.write) {
+          dxa::lz4::frame_blocks(recs, bend - recs, pl.k_comp_off + pl.nblk, pl.k_comp_len + pl.nblk,
+                                 pl.k_stored + pl.nblk, nb, &content, &mb, &fend);
+          for (int64_t k = 0; k < nb; ++k) {
+            pl.k_comp_off[pl.nblk + k] += recs - data;
+            pl.k_out_off[pl.nblk + k] = pl.out_bytes + k * (int64_t)mb;
+            pl.k_cap[pl.nblk + k] = mb;
+          }
+        }
+        if (mb > pl.max_block) pl.max_block = mb;
+        pl.out_bytes += nb * (int64_t)mb;
+        pl.nblk += nb;
+      } else {
+        return -5;
+      }
+      if (pl.write) {
+        pl.b_count[pl.nbat] = count;
+        pl.b_base[pl.nbat] = base;
+        pl.b_skip[pl.nbat] = skip;
+        pl.b_first[pl.nbat] = (int32_t)first;
+        pl.b_nblk[pl.nbat] = (int32_t)(pl.nblk - first);
+        pl.b_rec0[pl.nbat] = pl.nrec;
+      }
+      pl.nrec += count - skip;
+      ++pl.nbat;
+    }
+    *next_offset = base + last_delta + 1 > *next_offset ? base + last_delta + 1 : *next_offset;
+    p = bend;
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+// Device-decode plan of a Fetch record set: call with null arrays to size them (counts[0..3] = batches, blocks,
+// records, output bytes; counts[4] = largest block capacity), then again to fill them.
+__attribute__((visibility("default"))) int dxa_kafka_plan(const uint8_t* data, int64_t len, int64_t min_offset,
+                                                         int verify_crc, int64_t* counts, int64_t* next_offset,
+                                                         int32_t* b_count, int64_t* b_base, int32_t* b_skip,
+                                                         int32_t* b_first, int32_t* b_nblk, int64_t* b_rec0,
+                                                         int64_t* k_comp_off, int32_t* k_comp_len, uint8_t* k_stored,
+                                                         int64_t* k_out_off, int64_t* k_cap) {
+  Plan pl{b_count != nullptr, b_count, b_base, b_skip, b_first, b_nblk, b_rec0,
+          k_comp_off, k_comp_len, k_stored, k_out_off, k_cap};
+  const int rc = plan_batches(data, len, min_offset, pl, next_offset, verify_crc);
+  counts[0] = pl.nbat;
+  counts[1] = pl.nblk;
+  counts[2] = pl.nrec;
+  counts[3] = pl.out_bytes;
+  counts[4] = pl.max_block;
+  return rc;
+}
+
 
 __attribute__((visibility("default"))) uint32_t dxa_crc32c(const uint8_t* p, int64_t n) { return crc32c(p, (size_t)n); }
 
@@ -251,10 +362,23 @@ __attribute__((visibility("default"))) int dxa_kafka_extract(const uint8_t* data
   return rc;
 }
 
-// Encode n values (vals + offs[n+1]) as one v2 batch (codec 0 none, 1 gzip, 3 lz4) (baseOffset 0); returns malloc'd bytes.
+// Encode n values (vals + offs[n+1]) as one v2 batch (codec 0 none, 1 gzip, 3 lz4) (baseOffset 0); returns malloc'd
+// bytes.  lz4: one frame of `block_size` blocks at compression `level` (Kafka compression.lz4.level).
+__attribute__((visibility("default"))) uint8_t* dxa_kafka_encode_lz4(const uint8_t* vals, const int64_t* offs,
+                                                                    int64_t n, int64_t timestamp_ms, int32_t codec,
+                                                                    int32_t level, int32_t block_size,
+                                                                    int64_t* out_len);
+
 __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode(const uint8_t* vals, const int64_t* offs, int64_t n,
                                                                 int64_t timestamp_ms, int32_t codec,
                                                                 int64_t* out_len) {
+  return dxa_kafka_encode_lz4(vals, offs, n, timestamp_ms, codec, 1, 64 * 1024, out_len);
+}
+
+__attribute__((visibility("default"))) uint8_t* dxa_kafka_encode_lz4(const uint8_t* vals, const int64_t* offs,
+                                                                    int64_t n, int64_t timestamp_ms, int32_t codec,
+                                                                    int32_t level, int32_t block_size,
+                                                                    int64_t* out_len) {
   std::string recs;
   for (int64_t i = 0; i < n; ++i) {
     std::string r;
@@ -274,9 +398,9 @@ __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode(const uint8_t* 
     if (!gzip_bytes(recs, z)) return nullptr;
     recs.swap(z);
   } else if (codec == 3) {
-    std::string z((size_t)dxa::lz4::frame_bound((int64_t)recs.size(), 64 * 1024), '\0');
+    std::string z((size_t)dxa::lz4::frame_bound((int64_t)recs.size(), block_size), '\0');
     const int64_t m = dxa::lz4::compress_frame((const uint8_t*)recs.data(), (int64_t)recs.size(), (uint8_t*)&z[0],
-                                               (int64_t)z.size(), 64 * 1024, 1);
+                                               (int64_t)z.size(), block_size, 1, level);
     if (m < 0) return nullptr;
     z.resize((size_t)m);
     recs.swap(z);
@@ -304,5 +428,52 @@ __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode(const uint8_t* 
   std::memcpy(p, out.data(), out.size());
   *out_len = (int64_t)out.size();
   return p;
+}
+
+// A producer's stream of record batches as a Fetch response returns them: n values cut into batches of
+// `per_batch` records (the producer's batch.size), each one v2 batch (codec / level / LZ4 block size as above)
+// with broker-assigned base offsets from `base_offset`; `threads` encode batches in parallel.  Returns malloc'd
+// bytes (batches back to back).
+__attribute__((visibility("default"))) uint8_t* dxa_kafka_encode_stream(const uint8_t* vals, const int64_t* offs,
+                                                                       int64_t n, int64_t per_batch,
+                                                                       int64_t base_offset, int64_t timestamp_ms,
+                                                                       int32_t codec, int32_t level,
+                                                                       int32_t block_size, int32_t threads,
+                                                                       int64_t* out_len) {
+  if (per_batch <= 0) return nullptr;
+  const int64_t nbat = (n + per_batch - 1) / per_batch;
+  std::vector<uint8_t*> parts((size_t)nbat, nullptr);
+  std::vector<int64_t> lens((size_t)nbat, 0);
+  const int T = threads > 0 ? threads : 1;
+  std::vector<std::thread> pool;
+  for (int t = 0; t < T; ++t) {
+    pool.emplace_back([&, t]() {
+      for (int64_t b = t; b < nbat; b += T) {
+        const int64_t lo = b * per_batch, hi = lo + per_batch < n ? lo + per_batch : n;
+        parts[(size_t)b] = dxa_kafka_encode_lz4(vals, offs + lo, hi - lo, timestamp_ms, codec, level, block_size,
+                                                &lens[(size_t)b]);
+      }
+    });
+  }
+  for (auto& th : pool) th.join();
+  int64_t total = 0;
+  bool ok = true;
+  for (int64_t b = 0; b < nbat; ++b) {
+    ok = ok && parts[(size_t)b] != nullptr;
+    total += lens[(size_t)b];
+  }
+  uint8_t* out = ok ? (uint8_t*)std::malloc((size_t)(total > 0 ? total : 1)) : nullptr;
+  int64_t pos = 0;
+  for (int64_t b = 0; b < nbat; ++b) {
+    if (out) {
+      std::memcpy(out + pos, parts[(size_t)b], (size_t)lens[(size_t)b]);
+      const int64_t base = base_offset + b * per_batch;
+      for (int k = 0; k < 8; ++k) out[pos + k] = (uint8_t)((uint64_t)base >> (56 - 8 * k));
+      pos += lens[(size_t)b];
+    }
+    std::free(parts[(size_t)b]);
+  }
+  *out_len = total;
+  return out;
 }
 }

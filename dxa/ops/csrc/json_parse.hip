@@ -46,6 +46,8 @@ struct ParseArgs {
   const int32_t* key_len;       // [nnodes] key length in bytes
   const uint64_t* key_words;    // key texts, zero padded to 8-byte words
   int32_t nkey_words;
+  const int64_t* ends;          // [n] record ends when records are not back to back (Kafka values), else null;
+                                // offs[n] is then the end of the bytes
 };
 
 // The same arguments as explicitly global (address space 1) pointers.  Pointers read out of a by-value struct
@@ -74,6 +76,7 @@ struct GArgs {
   const G1 int32_t* key_len;
   const G1 uint64_t* key_words;
   int32_t nkey_words;
+  const G1 int64_t* ends;
 };
 
 __device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
@@ -98,6 +101,7 @@ __device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
   g.key_len = (const G1 int32_t*)p.key_len;
   g.key_words = (const G1 uint64_t*)p.key_words;
   g.nkey_words = p.nkey_words;
+  g.ends = (const G1 int64_t*)p.ends;
   return g;
 }
 
@@ -641,7 +645,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
   Reader r;
   r.buf = a.buf;
   r.p = a.offs[row];
-  r.end = a.offs[row + 1];
+  r.end = a.ends ? a.ends[row] : a.offs[row + 1];
   r.wb = -256;
   r.lim = a.offs[n] + 16;
 #ifdef DXA_PARSE_LDSWIN
@@ -925,11 +929,11 @@ DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const u
                            const int32_t* val_slot, const int32_t* len_slot, int32_t nnodes, int64_t* vals,
                            int32_t* lens, uint8_t* valid, uint8_t* row_ok, const int32_t* first_child,
                            const int32_t* next_sib, const int32_t* key_word, const int32_t* key_len,
-                           const uint64_t* key_words, int32_t nkey_words, void* stream) {
+                           const uint64_t* key_words, int32_t nkey_words, const int64_t* ends, void* stream) {
   if (n <= 0) return 0;
   if (nnodes >= 32767) return (int)hipErrorInvalidValue;   // node ids live in 16-bit LDS nesting slots
   ParseArgs a{buf, offs, n, lut_keys, lut_node, lut_cap, node_type, val_slot, len_slot, nnodes, vals, lens,
-              valid, row_ok, first_child, next_sib, key_word, key_len, key_words, nkey_words};
+              valid, row_ok, first_child, next_sib, key_word, key_len, key_words, nkey_words, ends};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(valid, 0, (size_t)nnodes * (size_t)n, s);
   if (e != hipSuccess) return (int)e;

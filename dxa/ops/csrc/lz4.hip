@@ -370,7 +370,10 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
                                                                const int64_t* __restrict__ out_off,
                                                                const int64_t* __restrict__ out_len, int64_t nb,
                                                                uint8_t* __restrict__ dst,
-                                                               int32_t* __restrict__ status) {
+                                                               int32_t* __restrict__ status,
+                                                               int64_t* __restrict__ produced) {
+  // produced == null: out_len[b] is the exact decompressed size; else it is a capacity and the size is reported
+  // in produced[b] (Kafka frames do not carry their content size)
   static_assert(G == 8 || G == 16, "group width");
   // 64-byte input window = NW dwords per lane; fast-path literals LPL bytes per lane; pipelined matches (<= 32 B)
   // BPL bytes per lane
@@ -385,8 +388,15 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   const uint8_t* in = src + comp_off[b];
   uint8_t* out = dst + out_off[b];
   if (stored[b]) {
+    if (produced ? (n > cap64) : (n != cap64)) {
+      if (gl == 0) status[b] = LZ_SIZE;
+      return;
+    }
     for (int32_t k = gl; k < n; k += G) out[k] = in[k];
-    if (gl == 0) status[b] = (n == cap64) ? LZ_OK : LZ_SIZE;
+    if (gl == 0) {
+      status[b] = LZ_OK;
+      if (produced) produced[b] = n;
+    }
     return;
   }
   if (cap64 > INT32_MAX || cap64 < 0 || n < 0) {
@@ -562,8 +572,11 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     op += ml;
   }
   if (pml > 0) flush();
-  if (rc == LZ_OK && op != cap) rc = LZ_SIZE;
-  if (gl == 0) status[b] = rc;
+  if (rc == LZ_OK && !produced && op != cap) rc = LZ_SIZE;
+  if (gl == 0) {
+    status[b] = rc;
+    if (produced) produced[b] = op;
+  }
 }
 
 }  // namespace
@@ -599,10 +612,10 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
     const int64_t threads = nb * lanes;
     if (lanes == 8)
       hipLaunchKernelGGL(lz4_decode_group_kernel<8>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8,
-                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status);
+                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
     else
       hipLaunchKernelGGL(lz4_decode_group_kernel<16>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8,
-                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status);
+                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
     return (int)hipGetLastError();
   }
   const int64_t lb = (max_out + 15) & ~(int64_t)15;         // LDS bytes per wave (16-B aligned slices)
@@ -621,6 +634,20 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
   }
   hipLaunchKernelGGL(lz4_decode_kernel, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, s, s8, co, cl, sd, oo, ol,
                      nb, (uint8_t*)dst, (int32_t*)status);
+  return (int)hipGetLastError();
+}
+
+// Blocks with a capacity instead of a known size (Kafka LZ4 frames): `cap[b]` bytes reserved at out_off[b], the
+// decompressed size comes back in produced[b].  Always the 16-lane group decoder.
+DXA_API int dxa_lz4_decode_into(const void* src, const void* comp_off, const void* comp_len, const void* stored,
+                                const void* out_off, const void* cap, int64_t nb, void* dst, void* produced,
+                                void* status, void* st) {
+  if (nb <= 0) return 0;
+  const int64_t threads = nb * 16;
+  hipLaunchKernelGGL(lz4_decode_group_kernel<16>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)st, (const uint8_t*)src, (const int64_t*)comp_off, (const int32_t*)comp_len,
+                     (const uint8_t*)stored, (const int64_t*)out_off, (const int64_t*)cap, nb, (uint8_t*)dst,
+                     (int32_t*)status, (int64_t*)produced);
   return (int)hipGetLastError();
 }
 

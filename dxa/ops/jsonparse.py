@@ -222,22 +222,23 @@ def check_framing(mismatches: list):
             raise ValueError(f"{bad} framed batch(es) held a different record count than their producer declared")
 
 
-def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan):
-    """Parse records ``buf[offs[i]:offs[i+1]]`` → (Raw StructColumn, row_ok bool tensor)."""
+def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan, ends: Optional[torch.Tensor] = None):
+    """Parse records ``buf[offs[i]:offs[i+1]]`` (or ``buf[offs[i]:ends[i]]`` when the records are not back to
+    back, e.g. Kafka record values) → (Raw StructColumn, row_ok bool tensor)."""
     n = int(offs.shape[0]) - 1
     device = buf.device
     if device.type == "cuda":
-        return _parse_gpu(buf, offs, n, plan)
-    return _parse_cpu(buf, offs, n, plan)
+        return _parse_gpu(buf, offs, n, plan, ends)
+    return _parse_cpu(buf, offs, n, plan, ends)
 
 
 GPU_MAX_DEPTH = 8      # json_parse.hip kMaxDepth: struct nesting tracked in registers
 
 
-def _parse_gpu(buf, offs, n, plan: ParsePlan):
+def _parse_gpu(buf, offs, n, plan: ParsePlan, ends=None):
     if plan.max_depth >= GPU_MAX_DEPTH:
         # schemas nested deeper than the kernel's register stack parse on the host (same semantics)
-        col, ok = _parse_cpu(buf.cpu(), offs.cpu(), n, plan)
+        col, ok = _parse_cpu(buf.cpu(), offs.cpu(), n, plan, None if ends is None else ends.cpu())
         return col.to(buf.device), ok.to(buf.device)
     lut_k, lut_n, types, vslot, lslot, fchild, nsib, kword, klen, kwords = plan.device_tables(buf.device)
     nn = len(plan.nodes)
@@ -249,7 +250,7 @@ def _parse_gpu(buf, offs, n, plan: ParsePlan):
         N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
                N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
                N.ptr(fchild), N.ptr(nsib), N.ptr(kword), N.ptr(klen), N.ptr(kwords), int(kwords.numel()),
-               N.stream_handle(buf.device))
+               None if ends is None else N.ptr(ends), N.stream_handle(buf.device))
     nulls = [1] * nn
     if n:
         cnt = torch.empty(nn, dtype=torch.int64, device=buf.device)
@@ -360,15 +361,16 @@ def _convert(v, dtype):
     return None
 
 
-def _parse_cpu(buf, offs, n, plan: ParsePlan):
+def _parse_cpu(buf, offs, n, plan: ParsePlan, ends=None):
     from ..engine.column import column_from_pylist, strings_from_pylist, PrimColumn, StructColumn, JsonColumn
     data = buf.cpu().numpy().tobytes()
     o = offs.cpu().tolist()
+    e = ends.cpu().tolist() if ends is not None else o[1:]
     recs = []
     ok = []
     for i in range(n):
         try:
-            d = json.loads(data[o[i]:o[i + 1]].decode("utf-8"))
+            d = json.loads(data[o[i]:e[i]].decode("utf-8"))
             if not isinstance(d, dict):
                 raise ValueError
             recs.append(d)

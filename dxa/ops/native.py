@@ -31,12 +31,14 @@ _SIGS = {
     "dxa_lz4_decode": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_memcpy_h2d_async": [c_p, c_p, c_i64, c_p],
     "dxa_copy_sdma": [c_p, c_p, c_i64],
+    "dxa_lz4_decode_into": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p],
+    "dxa_kafka_records": [c_p, c_i64] + [c_p] * 14,
     "dxa_serialize_lengths": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p],
     "dxa_serialize_write": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],
     "dxa_java_double_hostcheck": [c_p, c_i64, c_p, c_p],
     "dxa_json_parse": [c_p, c_p, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p,
-                       c_p, c_p, c_p, c_p, c_p, c_i32, c_p],
+                       c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p],
     "dxa_count_newlines": [c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_write_newlines_bits": [c_p, c_i64, c_i64, c_p, c_p, c_i64, c_i64, c_p],
     "dxa_null_counts": [c_p, c_i64, c_i32, c_p, c_p],
