@@ -12,10 +12,12 @@ one process per MI355X (BASELINE.json metric "events/sec (node) + p99 latency").
 * ``full``    — codegen'd rules + windowed SQL with a device UDF + reference join + accumulator state (config 5);
 * ``passthrough`` — tag rules on every event and every event written as JSON (config 1's shape at full rate).
 
-Each step is a complete micro-batch exactly as the streaming host runs it.  Sources: ``pinned-lz4`` (default for
-groupby/join/passthrough) — each batch arrives in pinned host memory as an LZ4 frame of newline-delimited JSON events
-(the payload format of an LZ4-compressed Kafka record batch; compressed by the producer, outside the step) and every
-step copies the compressed bytes into HBM, decompresses them on the GPU, frames the records and processes them;
+Each step is a complete micro-batch exactly as the streaming host runs it.  Sources: ``kafka`` (default for
+groupby/join/passthrough) — each batch arrives in pinned host memory as a multi-partition Fetch of Kafka v2 record
+batches with the LZ4 codec (producer batches of ~16 KiB, compression.lz4.level 9; produced outside the step), and
+every step plans the batch headers on the host, copies the compressed bytes into HBM, decompresses and frames the
+records on the GPU and parses the values in place — the Kafka / Event Hubs source's own path
+(``dxa.io.kafka_device``); ``pinned-lz4`` — one LZ4 frame of newline-delimited JSON, newline-framed on the GPU;
 ``pinned`` — the raw JSON bytes are copied into HBM every step (≈2.4x more PCIe bytes); ``gpu-sim`` — the SimulatedData generator renders the next batch on the GPU with event
 times inside that batch's second (needed by the windowed flows, whose windows must see advancing event time; its
 cost is inside the timed step).  Batch times advance one interval per step on a simulated clock.
@@ -39,8 +41,8 @@ sys.path.insert(0, ROOT)
 DEFAULT_EVENTS = {"groupby": 2_000_000, "window": 1_000_000, "join": 2_000_000, "full": 1_000_000,
                   "passthrough": 1_000_000}
 DEFAULT_WARMUP = {"groupby": 5, "window": 305, "join": 3, "full": 305, "passthrough": 3}
-DEFAULT_SOURCE = {"groupby": "pinned-lz4", "window": "gpu-sim", "join": "pinned-lz4", "full": "gpu-sim",
-                  "passthrough": "pinned-lz4"}
+DEFAULT_SOURCE = {"groupby": "kafka", "window": "gpu-sim", "join": "kafka", "full": "gpu-sim",
+                  "passthrough": "kafka"}
 MODEL = {
     "groupby": "SimulatedData IoT flow: 32-col JSON parse + projection + GROUP BY (deviceId, deviceType, homeId) "
                "9 aggregates + alert view + JSON outputs",
@@ -215,9 +217,15 @@ def main():
         if (on_gpu and source == "pinned-lz4") else None
     kdec = None
     if source == "kafka":
-        from concurrent.futures import ThreadPoolExecutor
         from dxa.io import kafka_device as KD
-        planners = ThreadPoolExecutor(max_workers=min(16, max(1, args.kafka_partitions)))
+        from concurrent.futures import ThreadPoolExecutor
+        plan_bufs = KD.PlanBufferPool()
+        planner = ThreadPoolExecutor(max_workers=1)
+        plan_futs = {}
+
+        def make_plan(i):
+            b = kafka_parts[i % len(pool)]
+            return KD.plan_many(pool[i % len(pool)].numpy(), b, [0] * len(b), threads=16, buffer=plan_bufs.get())
         if on_gpu:
             kdec = KD.DeviceRecordDecoder(device, chunks=args.lz4_chunks, copy_stream=side)
     staged = {}
@@ -229,13 +237,17 @@ def main():
         if source == "kafka":
             staging, bounds = pool[i % len(pool)], kafka_parts[i % len(pool)]
             sn = staging.numpy()
-            # per-partition plans (headers only), in parallel as per-partition fetch threads would
-            plans = list(planners.map(lambda b: KD.plan_fetch(sn[b[0]:b[1]], 0), bounds))
-            plan = KD.merge([(pl, b[0]) for pl, b in zip(plans, bounds)])
+            # per-partition plans (headers only), walked in parallel native threads as per-partition fetch threads
+            # would, one batch ahead on a planner thread (the native walk releases the GIL); the merged tables
+            # land in a pinned buffer for one H2D copy
+            fut = plan_futs.pop(i, None) or planner.submit(make_plan, i)
+            plan_futs[i + 1] = planner.submit(make_plan, i + 1)
+            plan = fut.result()
             if kdec is not None:
                 raw, ev = kdec.decode(staging, plan)
             else:
                 out, st, en = KD.decode_on_host_like(sn, plan)
+                plan.buffer.release()
                 raw, ev = RawBatch(torch.from_numpy(out), torch.from_numpy(np.append(st, plan.out_bytes)),
                                    plan.nrec, ends=torch.from_numpy(en)), None
             staged[i] = (raw, None, ev)

@@ -17,13 +17,16 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
 _PLAN_ERRS = {-2: "message format is not v2", -3: "CRC mismatch", -5: "codec decoded on the host only",
               -7: "malformed LZ4 frame", -8: "dependent-block LZ4 frame", -9: "offset deltas with gaps"}
+
+
+TORCH_DT = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64, np.dtype(np.uint8): torch.uint8}
 
 
 class Unsupported(Exception):
@@ -63,6 +66,8 @@ class FetchPlan:
     out_bytes: int
     next_offset: int
     nbytes: int = 0               # staging bytes covered
+    packed: Optional[torch.Tensor] = None      # pinned bytes holding every array above (one H2D copy), if any
+    layout: Optional[list] = None              # [(name, byte offset, count)] of the arrays inside ``packed``
 
     @property
     def nbat(self) -> int:
@@ -105,6 +110,99 @@ def plan_fetch(data, min_offset: int, verify_crc: bool = False) -> FetchPlan:
         raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
     keep = (arr["b_count"] - arr["b_skip"]).astype(np.int32)
     return FetchPlan(b_keep=keep, out_bytes=int(counts[3]), next_offset=nxt.value, nbytes=int(a.size), **arr)
+
+
+_ARRAYS = [("b_count", np.int32, "b"), ("b_base", np.int64, "b"), ("b_skip", np.int32, "b"),
+           ("b_keep", np.int32, "b"), ("b_first", np.int32, "b"), ("b_nblk", np.int32, "b"),
+           ("b_rec0", np.int64, "b"), ("k_comp_off", np.int64, "k"), ("k_comp_len", np.int32, "k"),
+           ("k_stored", np.uint8, "k"), ("k_out_off", np.int64, "k"), ("k_cap", np.int64, "k")]
+
+
+class PlanBuffer:
+    """Reusable pinned buffer the multi-set planner writes its arrays into (no per-step pinned allocation).
+    ``busy`` is the event of the last H2D copy out of it; see ``PlanBufferPool``."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+        self.busy = None
+        self.reserved = False          # handed out by a pool, its plan not yet consumed
+
+    def free(self) -> bool:
+        return not self.reserved and (self.busy is None or self.busy.query())
+
+    def release(self, event=None):
+        """The plan is consumed: the buffer is free once ``event`` (its H2D copy) completes."""
+        self.busy = event
+        self.reserved = False
+
+    def carve(self, nbat: int, nblk: int):
+        layout, pos = [], 0
+        for name, dt, kind in _ARRAYS:
+            cnt = nbat if kind == "b" else nblk
+            layout.append((name, pos, cnt))
+            pos += (cnt * np.dtype(dt).itemsize + 15) // 16 * 16
+        if self.buf is None or self.buf.numel() < pos:
+            self.buf = torch.empty(max(pos, 1) * 5 // 4 + 64, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+        raw = self.buf.numpy()
+        arrs = {name: raw[off:off + cnt * np.dtype(dt).itemsize].view(dt)
+                for (name, off, cnt), (_, dt, _k) in zip(layout, _ARRAYS)}
+        return arrs, layout, pos
+
+
+class PlanBufferPool:
+    """Plan buffers for pipelined ingest: a buffer is reused only once the copy of its previous plan is done."""
+
+    def __init__(self):
+        self.bufs: List[PlanBuffer] = []
+        self._lock = __import__("threading").Lock()
+
+    def get(self) -> PlanBuffer:
+        with self._lock:
+            for b in self.bufs:
+                if b.free():
+                    b.reserved = True
+                    return b
+            b = PlanBuffer()
+            b.reserved = True
+            self.bufs.append(b)
+            return b
+
+
+def plan_many(data: np.ndarray, bounds: Sequence[Tuple[int, int]], min_offsets: Sequence[int],
+              threads: int = 16, buffer: Optional[PlanBuffer] = None) -> FetchPlan:
+    """Plan many record sets of one staging buffer (``data[lo:hi]`` each, one per partition fetch) with the sets
+    walked in parallel native threads; the merged arrays land in ``buffer`` (pinned) for one H2D copy."""
+    L = _lib()
+    if not hasattr(L, "_plan_many_bound"):
+        p, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        L.dxa_kafka_plan_count.argtypes = [p, i64, p, p, p, i32, i32, p, p]
+        L.dxa_kafka_plan_fill.argtypes = [p, i64, p, p, p, i32, p] + [p] * 11
+        L._plan_many_bound = True
+    ns = len(bounds)
+    so = np.array([b[0] for b in bounds], np.int64)
+    sl = np.array([b[1] - b[0] for b in bounds], np.int64)
+    mo = np.array(list(min_offsets), np.int64)
+    counts = np.zeros((ns, 4), np.int64)
+    nxt = np.zeros(ns, np.int64)
+    rc = L.dxa_kafka_plan_count(data.ctypes.data, ns, so.ctypes.data, sl.ctypes.data, mo.ctypes.data, 0, threads,
+                                counts.ctypes.data, nxt.ctypes.data)
+    if rc:
+        raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
+    nbat, nblk = int(counts[:, 0].sum()), int(counts[:, 1].sum())
+    buffer = buffer or PlanBuffer()
+    arrs, layout, used = buffer.carve(nbat, nblk)
+    rc = L.dxa_kafka_plan_fill(data.ctypes.data, ns, so.ctypes.data, sl.ctypes.data, mo.ctypes.data, threads,
+                               counts.ctypes.data, *[arrs[n].ctypes.data for n in
+                                                     ("b_count", "b_base", "b_skip", "b_first", "b_nblk", "b_rec0",
+                                                      "k_comp_off", "k_comp_len", "k_stored", "k_out_off",
+                                                      "k_cap")])
+    if rc:
+        raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
+    np.subtract(arrs["b_count"], arrs["b_skip"], out=arrs["b_keep"])
+    plan = FetchPlan(out_bytes=int(counts[:, 3].sum()), next_offset=int(nxt.max()) if ns else 0,
+                     nbytes=int((so + sl).max()) if ns else 0, packed=buffer.buf[:used], layout=layout, **arrs)
+    plan.buffer = buffer
+    return plan
 
 
 def merge(plans: Sequence[Tuple[FetchPlan, int]]) -> FetchPlan:
@@ -180,14 +278,28 @@ class DeviceRecordDecoder:
         from ..ops import native as N
         dev = self.device
         n = plan.nrec
-        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).pin_memory()  # noqa: E731
+        if plan.packed is None:                      # pack the arrays for one H2D copy
+            if not hasattr(self, "_packs"):
+                self._packs = PlanBufferPool()
+            pb = self._packs.get()
+            plan.buffer = pb
+            arrs, layout, used = pb.carve(plan.nbat, plan.nblk)
+            for name, _dt, _k in _ARRAYS:
+                arrs[name][...] = getattr(plan, name)
+            packed = pb.buf[:used]
+        else:
+            packed, layout = plan.packed, plan.layout
         with torch.cuda.stream(self.copy_stream):
-            tabs = [T(x).to(dev, non_blocking=True) for x in (
-                plan.k_comp_off, plan.k_comp_len, plan.k_stored, plan.k_out_off, plan.k_cap, plan.b_count,
-                plan.b_skip, plan.b_keep, plan.b_first, plan.b_nblk, plan.b_rec0)]
+            dtab = packed.to(dev, non_blocking=True)
             ddata = torch.empty(plan.nbytes + 32, dtype=torch.uint8, device=dev)
             tab_ev = torch.cuda.Event()
             tab_ev.record(self.copy_stream)
+        if getattr(plan, "buffer", None) is not None:
+            plan.buffer.release(tab_ev)
+        views = {name: dtab[off:off + cnt * np.dtype(dt).itemsize].view(TORCH_DT[np.dtype(dt)])
+                 for (name, off, cnt), (_, dt, _k) in zip(layout, _ARRAYS)}
+        tabs = [views[k] for k in ("k_comp_off", "k_comp_len", "k_stored", "k_out_off", "k_cap", "b_count",
+                                   "b_skip", "b_keep", "b_first", "b_nblk", "b_rec0")]
         co, cl, sd, oo, cap, bc, bs, bk, bf, bn, br = tabs
         with torch.cuda.stream(self.decode_stream):
             out = torch.empty(plan.out_bytes + 64, dtype=torch.uint8, device=dev)
@@ -221,11 +333,12 @@ class DeviceRecordDecoder:
                N.ptr(rstat), st)
         done = torch.cuda.Event()
         done.record(self.decode_stream)
-        for t in (ddata, produced, bstat, *tabs):
+        for t in (ddata, produced, bstat, dtab):
             t.record_stream(self.decode_stream)
         self.checks.append(rstat[:plan.nbat])
-        # the pinned bytes must outlive their async copies
-        self._inflight = [(e, b) for e, b in getattr(self, "_inflight", []) if not e.query()] + [(done, staging)]
+        # the pinned bytes (record sets and plan tables) must outlive their async copies
+        self._inflight = [(e, b) for e, b in getattr(self, "_inflight", []) if not e.query()] + \
+            [(done, (staging, packed))]
         return RawBatch(out, offs, n, ends=ends[:n], source_bytes=plan.nbytes), done
 
     def check(self):

@@ -9,6 +9,7 @@
 //   producerId i64 | producerEpoch i16 | baseSequence i32 | count i32 | records…
 // Record: length varint | attributes i8 | timestampDelta varlong | offsetDelta varint | keyLen varint | key |
 //   valueLen varint | value | headerCount varint | headers…   (varints are zig-zag)
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -315,6 +316,18 @@ int plan_batches(const uint8_t* data, int64_t len, int64_t min_offset, Plan& pl,
   return 0;
 }
 
+template <typename F>
+void parallel_sets(int64_t nsets, int threads, F f) {
+  const int T = threads > 0 ? (int)std::min<int64_t>(threads, nsets) : 1;
+  if (T <= 1) {
+    for (int64_t k = 0; k < nsets; ++k) f(k);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int t = 0; t < T; ++t)
+    pool.emplace_back([&, t]() { for (int64_t k = t; k < nsets; k += T) f(k); });
+  for (auto& th : pool) th.join();
+}
 }  // namespace
 
 extern "C" {
@@ -428,6 +441,63 @@ __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode_lz4(const uint8
   std::memcpy(p, out.data(), out.size());
   *out_len = (int64_t)out.size();
   return p;
+}
+
+// Plans of many record sets at once (one per partition fetch), each set on its own worker: the header walk is a
+// chain of cache misses (one batch header every few KiB), so sets are walked in parallel.  count: per set
+// [nbat, nblk, nrec, out_bytes] (set_counts[4*s..]) and next offsets; fill: the sets' plans back to back in the
+// merged arrays (block / output / record indices rebased, block payload offsets relative to `data`).
+
+__attribute__((visibility("default"))) int dxa_kafka_plan_count(const uint8_t* data, int64_t nsets,
+                                                               const int64_t* set_off, const int64_t* set_len,
+                                                               const int64_t* min_off, int verify_crc, int threads,
+                                                               int64_t* set_counts, int64_t* next_off) {
+  std::vector<int> rcs((size_t)nsets, 0);
+  parallel_sets(nsets, threads, [&](int64_t k) {
+    Plan pl{false, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+            nullptr};
+    rcs[(size_t)k] = plan_batches(data + set_off[k], set_len[k], min_off[k], pl, &next_off[k], verify_crc);
+    set_counts[4 * k] = pl.nbat;
+    set_counts[4 * k + 1] = pl.nblk;
+    set_counts[4 * k + 2] = pl.nrec;
+    set_counts[4 * k + 3] = pl.out_bytes;
+  });
+  for (int rc : rcs)
+    if (rc) return rc;
+  return 0;
+}
+
+__attribute__((visibility("default"))) int dxa_kafka_plan_fill(const uint8_t* data, int64_t nsets,
+                                                              const int64_t* set_off, const int64_t* set_len,
+                                                              const int64_t* min_off, int threads,
+                                                              const int64_t* set_counts, int32_t* b_count,
+                                                              int64_t* b_base, int32_t* b_skip, int32_t* b_first,
+                                                              int32_t* b_nblk, int64_t* b_rec0, int64_t* k_comp_off,
+                                                              int32_t* k_comp_len, uint8_t* k_stored,
+                                                              int64_t* k_out_off, int64_t* k_cap) {
+  std::vector<int64_t> base((size_t)(4 * (nsets + 1)), 0);
+  for (int64_t k = 0; k < nsets; ++k)
+    for (int j = 0; j < 4; ++j) base[(size_t)(4 * (k + 1) + j)] = base[(size_t)(4 * k + j)] + set_counts[4 * k + j];
+  std::vector<int> rcs((size_t)nsets, 0);
+  parallel_sets(nsets, threads, [&](int64_t k) {
+    const int64_t b0 = base[(size_t)(4 * k)], k0 = base[(size_t)(4 * k + 1)], r0 = base[(size_t)(4 * k + 2)],
+                  o0 = base[(size_t)(4 * k + 3)];
+    Plan pl{true, b_count + b0, b_base + b0, b_skip + b0, b_first + b0, b_nblk + b0, b_rec0 + b0,
+            k_comp_off + k0, k_comp_len + k0, k_stored + k0, k_out_off + k0, k_cap + k0};
+    int64_t nxt = 0;
+    rcs[(size_t)k] = plan_batches(data + set_off[k], set_len[k], min_off[k], pl, &nxt, 0);
+    for (int64_t i = 0; i < pl.nbat; ++i) {
+      b_first[b0 + i] += (int32_t)k0;
+      b_rec0[b0 + i] += r0;
+    }
+    for (int64_t i = 0; i < pl.nblk; ++i) {
+      k_comp_off[k0 + i] += set_off[k];
+      k_out_off[k0 + i] += o0;
+    }
+  });
+  for (int rc : rcs)
+    if (rc) return rc;
+  return 0;
 }
 
 // A producer's stream of record batches as a Fetch response returns them: n values cut into batches of

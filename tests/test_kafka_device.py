@@ -89,3 +89,19 @@ def test_device_decode_matches_host(gpu):
     pl = ParsePlan(StructType((StructField("id", "long"), StructField("s", "string"))))
     col, ok = parse(raw.buf, raw.offs, pl, raw.ends)
     assert bool(ok.all()) and col.children[0].data.cpu().tolist() == [json.loads(v)["id"] for v in want]
+
+
+def test_plan_many_matches_merged_plans():
+    vals = _values(400, seed=5)
+    sets = [_record_set(vals[:130], 17), _record_set(vals[130:260], 29, "none"), _record_set(vals[260:], 41)]
+    data, bounds = b"", []
+    for x in sets:
+        bounds.append((len(data), len(data) + len(x)))
+        data += x
+    a = np.frombuffer(data, np.uint8)
+    many = KD.plan_many(a, bounds, [3, 0, 0], threads=3)
+    merged = KD.merge([(KD.plan_fetch(a[lo:hi], m), lo) for (lo, hi), m in zip(bounds, [3, 0, 0])])
+    for name, _dt, _k in KD._ARRAYS:
+        assert np.array_equal(getattr(many, name), getattr(merged, name)), name
+    buf, s, e = KD.decode_on_host_like(a, many)
+    assert [buf[x:y].tobytes() for x, y in zip(s, e)] == vals[3:130] + vals[130:]
