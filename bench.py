@@ -316,6 +316,8 @@ def main():
         sizes.append(kafka_json[i % len(pool)] + 16 if source == "kafka" else rb.buf.shape[0])
         return m
 
+    from dxa.utils import settle_gc
+    settle_gc()
     depth = max(1, args.prefetch)
     for i in range(depth):
         stage(i)
@@ -419,6 +421,7 @@ def main():
         out["config"]["kafka_batch_records"] = args.kafka_batch_records
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
+        out["latency_trace_ms"] = [round(x * 1e3, 2) for x in lat]
     if last:
         out["last_batch_outputs"] = {k: v for k, v in last.items() if k.startswith("Output_")}
     if flow == "join":

@@ -97,6 +97,45 @@ def _take_valid(valid, idx):
     return None if valid is None else valid[idx]
 
 
+def _plan_take(c: "Column", idx: torch.Tensor, leaves: List[torch.Tensor]):
+    """Register c's leaf tensors in ``leaves``; return a builder taking the gathered leaves (in registration order).
+    Module-level recursion on purpose: a self-referencing nested function is a reference cycle, and this one would
+    keep every leaf (the batch's raw input arena included) alive until the cyclic collector ran."""
+    if isinstance(c, PrimColumn):
+        i = len(leaves)
+        leaves.append(c.data)
+        if c.valid is not None:
+            leaves.append(c.valid)
+        has_v = c.valid is not None
+        return lambda g: PrimColumn(c.dtype, g[i], g[i + 1] if has_v else None)
+    if isinstance(c, StrColumn):
+        i = len(leaves)
+        leaves.extend([c.starts, c.lens])
+        if c.valid is not None:
+            leaves.append(c.valid)
+        has_v = c.valid is not None
+        return lambda g: type(c)(c.arena, g[i], g[i + 1], g[i + 2] if has_v else None, c.dtype)
+    if isinstance(c, StructColumn):
+        i = len(leaves)
+        if c.valid is not None:
+            leaves.append(c.valid)
+        has_v = c.valid is not None
+        kids = [_plan_take(k, idx, leaves) for k in c.children]
+        n = int(idx.shape[0])
+        return lambda g: StructColumn(c.names, [b(g) for b in kids], n, g[i] if has_v else None, c.is_map,
+                                      c.dtype, c.device)
+    if isinstance(c, ArrayColumn):
+        i = len(leaves)
+        if c.valid is not None:
+            leaves.append(c.valid)
+        has_v = c.valid is not None
+        els = [_plan_take(e, idx, leaves) for e in c.elements]
+        n = int(idx.shape[0])
+        return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device)
+    taken = c.take(idx)                       # constants and other kinds: their own take
+    return lambda g: taken
+
+
 def take_columns(cols: Sequence["Column"], idx: torch.Tensor) -> List["Column"]:
     """Row gather of several columns with the same index vector.  On the GPU every leaf tensor (data, validity,
     string starts / lengths, nested validity) moves in one multi-column gather launch (dxa.ops.gather) instead of
@@ -105,44 +144,7 @@ def take_columns(cols: Sequence["Column"], idx: torch.Tensor) -> List["Column"]:
     if idx.device.type != "cuda" or not cols:
         return [c.take(idx) for c in cols]
     leaves: List[torch.Tensor] = []
-
-    def plan(c):
-        """Register c's leaf tensors; return a builder taking the gathered leaves (in registration order)."""
-        if isinstance(c, PrimColumn):
-            i = len(leaves)
-            leaves.append(c.data)
-            if c.valid is not None:
-                leaves.append(c.valid)
-            has_v = c.valid is not None
-            return lambda g: PrimColumn(c.dtype, g[i], g[i + 1] if has_v else None)
-        if isinstance(c, StrColumn):
-            i = len(leaves)
-            leaves.extend([c.starts, c.lens])
-            if c.valid is not None:
-                leaves.append(c.valid)
-            has_v = c.valid is not None
-            return lambda g: type(c)(c.arena, g[i], g[i + 1], g[i + 2] if has_v else None, c.dtype)
-        if isinstance(c, StructColumn):
-            i = len(leaves)
-            if c.valid is not None:
-                leaves.append(c.valid)
-            has_v = c.valid is not None
-            kids = [plan(k) for k in c.children]
-            n = int(idx.shape[0])
-            return lambda g: StructColumn(c.names, [b(g) for b in kids], n, g[i] if has_v else None, c.is_map,
-                                          c.dtype, c.device)
-        if isinstance(c, ArrayColumn):
-            i = len(leaves)
-            if c.valid is not None:
-                leaves.append(c.valid)
-            has_v = c.valid is not None
-            els = [plan(e) for e in c.elements]
-            n = int(idx.shape[0])
-            return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device)
-        taken = c.take(idx)                       # constants and other kinds: their own take
-        return lambda g: taken
-
-    builders = [plan(c) for c in cols]
+    builders = [_plan_take(c, idx, leaves) for c in cols]
     if len(leaves) < 2:
         return [c.take(idx) for c in cols]
     if any(t.dim() != 1 or t.shape[0] != leaves[0].shape[0] for t in leaves):

@@ -48,6 +48,8 @@ class StreamingHost:
         return (t_us // self.interval_us) * self.interval_us
 
     def run(self):
+        from ..utils import settle_gc
+        settle_gc()
         pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dxa-prefetch") if self.pipeline else None
         next_time = self._batch_time(int(time.time() * 1e6)) + (self.interval_us if self.realtime else 0)
         prefetched = None
@@ -135,6 +137,7 @@ class BlobBatchingHost:
         from ..io.sources import frame_bytes
         results = []
         for p in self.paths:
+            t0 = time.perf_counter()
             files = sorted(glob.glob(str(fs.local_path(p)), recursive=True))
             data = bytearray()
             for f in files:
@@ -144,5 +147,6 @@ class BlobBatchingHost:
             bt = int(self.start.replace(tzinfo=_dt.timezone.utc).timestamp() * 1e6)
             m = self.processor.process_batch(raw, bt, 3600 * 1_000_000)
             m["InputBlobs"] = float(len(files))
+            m["BatchProcessedET"] = time.perf_counter() - t0      # CommonProcessorFactory.scala:509-513
             results.append(m)
         return results

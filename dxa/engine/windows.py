@@ -55,31 +55,34 @@ class TimeWindowConf:
         return TimeWindowConf(wins, True, ts, parse_duration_micros(wm), max(wins.values()), quirk)
 
 
+def _str_leaves(c, out: List[StrColumn]):
+    if isinstance(c, StrColumn):
+        out.append(c)
+    elif isinstance(c, StructColumn):
+        for k in c.children:
+            _str_leaves(k, out)
+
+
+def _rebuild(c, done):
+    if isinstance(c, StrColumn):
+        return next(done)
+    if isinstance(c, StructColumn):
+        return StructColumn(c.names, [_rebuild(k, done) for k in c.children], c.length, c.valid, c.is_map, c.dtype,
+                            c.device)
+    return c
+
+
 def _compact_table(t: Table) -> Table:
     """Detach retained rows from the batch's raw input buffer (string views → own compact arena); all string leaves
-    are compacted together with one host synchronisation."""
+    are compacted together with one host synchronisation.  (Module-level recursion: a self-referencing nested
+    function is a reference cycle, and this one would pin the batch's raw input buffer until the cyclic collector
+    ran.)"""
     from ..ops.strings import compact_many
     leaves: List[StrColumn] = []
-
-    def collect(c):
-        if isinstance(c, StrColumn):
-            leaves.append(c)
-        elif isinstance(c, StructColumn):
-            for k in c.children:
-                collect(k)
-
     for c in t.columns:
-        collect(c)
+        _str_leaves(c, leaves)
     done = iter(compact_many(leaves))
-
-    def rebuild(c):
-        if isinstance(c, StrColumn):
-            return next(done)
-        if isinstance(c, StructColumn):
-            return StructColumn(c.names, [rebuild(k) for k in c.children], c.length, c.valid, c.is_map, c.dtype,
-                                c.device)
-        return c
-    return Table(t.names, [rebuild(c) for c in t.columns], t.length, t.device)
+    return Table(t.names, [_rebuild(c, done) for c in t.columns], t.length, t.device)
 
 
 @dataclass

@@ -250,23 +250,24 @@ class _DevBuilder:
         a CLOSE op (code 1) after each container's children; `skip` = ops to jump when the field is omitted/null.
         Modes: 0 struct member, 1 map member, 2 array element, 3 filterNull array element."""
         ops: List[List[int]] = []
-
-        def field(idx: int, depth: int, mode: int):
-            if depth > 30:
-                raise ValueError("JSON nesting deeper than 30 levels")
-            pos = len(ops)
-            ops.append([0, idx, depth, mode])
-            nd = self.nodes[idx]
-            if nd["kind"] in (K_STRUCT, K_MAP, K_ARRAY):
-                cm = {K_STRUCT: 0, K_MAP: 1}.get(nd["kind"], 3 if nd["drop_nulls"] else 2)
-                for j in range(nd["nchildren"]):
-                    field(nd["child0"] + j, depth + 1, cm)
-                ops.append([1, idx, depth, 0])
-            ops[pos][3] = mode | ((len(ops) - pos - 1) << 8)
-
         for t in top:
-            field(t, 0, 0)
+            self._emit(ops, t, 0, 0)
         return [v for op in ops for v in op]
+
+    def _emit(self, ops: List[List[int]], idx: int, depth: int, mode: int):
+        # a method, not a nested recursive function: that would be a reference cycle pinning this plan (and the
+        # column tensors it keeps alive) until the cyclic collector ran
+        if depth > 30:
+            raise ValueError("JSON nesting deeper than 30 levels")
+        pos = len(ops)
+        ops.append([0, idx, depth, mode])
+        nd = self.nodes[idx]
+        if nd["kind"] in (K_STRUCT, K_MAP, K_ARRAY):
+            cm = {K_STRUCT: 0, K_MAP: 1}.get(nd["kind"], 3 if nd["drop_nulls"] else 2)
+            for j in range(nd["nchildren"]):
+                self._emit(ops, nd["child0"] + j, depth + 1, cm)
+            ops.append([1, idx, depth, 0])
+        ops[pos][3] = mode | ((len(ops) - pos - 1) << 8)
 
     def device_arrays(self, device):
         arr = (DevNode * max(1, len(self.nodes)))()
