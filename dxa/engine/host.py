@@ -81,6 +81,11 @@ class StreamingHost:
                     raise
                 self.batches += 1
                 next_time = bt + self.interval_us
+                if prefetched is not None and prefetched.done() and prefetched.exception() is None:
+                    nxt = prefetched.result()
+                    prep = getattr(self.processor, "prepare", None)
+                    if nxt is not None and prep is not None:
+                        prep(nxt)                            # its parse queues behind this batch's kernels
             self.processor.drain()
         finally:
             self.processor.on_batch_complete = prev_cb

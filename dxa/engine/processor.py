@@ -27,7 +27,7 @@ from .. import parallel as P
 from ..config import settings as S
 from ..config.secrets import resolve
 from ..io import fs
-from ..ops.jsonparse import ParsePlan, parse
+from ..ops.jsonparse import ParsePlan, parse, parse_async
 from ..sql.transform import COMMAND_COMMAND, parse_transform
 from .column import ConstColumn, PrimColumn, StructColumn, Table, concat_tables
 from .expr import EvalContext, EvalError
@@ -54,6 +54,7 @@ class RawBatch:
     source_bytes: int = 0
     ends: Optional[torch.Tensor] = None       # int64 [n] record ends when records are not back to back (Kafka
                                               # values in decompressed record batches); offs[n] = end of the bytes
+    pending: Optional[Any] = None             # jsonparse.PendingParse started by Processor.prepare
 
 
 def _read_lines(path: str) -> List[str]:
@@ -160,6 +161,15 @@ class Processor:
         return keep or None
 
     # ------------------------------------------------------------------------------------------------------------
+    def prepare(self, raw: RawBatch) -> RawBatch:
+        """Queue the batch's JSON parse now, on the current stream (call it right after the previous batch's
+        ``process_batch``).  The parse kernels then run while the host is still planning the previous batch's tail
+        and this batch's start, and ``project`` finds the per-field null counts already on the host instead of
+        waiting for the parse.  A no-op off the GPU and with an input normalizer (which rewrites the bytes first)."""
+        if raw.pending is None and self.normalizer is None and raw.buf.device.type == "cuda":
+            raw.pending = parse_async(raw.buf, raw.offs, self.parse_plan, raw.ends)
+        return raw
+
     def project(self, raw: RawBatch, batch_time_us: int, ctx: EvalContext) -> Table:
         t0 = time.perf_counter()
         buf = raw.buf
@@ -176,7 +186,11 @@ class Processor:
                 ends = None
             buf, offs = self.normalizer(buf, offs)
         with tracing.stage("parse"):
-            raw_col, row_ok = parse(buf, offs, self.parse_plan, ends)
+            if raw.pending is not None and self.normalizer is None:
+                raw_col, row_ok = raw.pending.result()
+                raw.pending = None
+            else:
+                raw_col, row_ok = parse(buf, offs, self.parse_plan, ends)
         self._sync()
         self.stage_times["parse"] = time.perf_counter() - t0
         n = raw.n

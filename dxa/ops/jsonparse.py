@@ -225,39 +225,71 @@ def check_framing(mismatches: list):
 def parse(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan, ends: Optional[torch.Tensor] = None):
     """Parse records ``buf[offs[i]:offs[i+1]]`` (or ``buf[offs[i]:ends[i]]`` when the records are not back to
     back, e.g. Kafka record values) → (Raw StructColumn, row_ok bool tensor)."""
+    return parse_async(buf, offs, plan, ends).result()
+
+
+class PendingParse:
+    """A parse whose kernels are queued: ``result()`` waits only for its per-field null counts (a few bytes copied
+    to pinned memory behind the kernels), then assembles the columns.  ``Processor.prepare`` starts batch t+1's
+    parse while batch t is still being planned, so the wait is normally already over."""
+
+    def __init__(self, done=None, plan=None, arena=None, parts=None, n=0, counts=None, event=None):
+        self._done = done
+        self.plan, self.arena, self.parts, self.n = plan, arena, parts, n
+        self.counts, self.event = counts, event
+
+    def result(self):
+        if self._done is None:
+            if self.event is not None:
+                self.event.synchronize()
+            nulls = self.counts.tolist() if self.counts is not None else [1] * len(self.plan.nodes)
+            vals, lens, valid, row_ok = self.parts
+            self._done = (_assemble(self.plan, self.arena, vals, lens, valid, self.n, nulls), row_ok)
+            self.parts = self.arena = self.counts = self.event = None
+        return self._done
+
+
+def parse_async(buf: torch.Tensor, offs: torch.Tensor, plan: ParsePlan,
+                ends: Optional[torch.Tensor] = None) -> PendingParse:
     n = int(offs.shape[0]) - 1
-    device = buf.device
-    if device.type == "cuda":
-        return _parse_gpu(buf, offs, n, plan, ends)
-    return _parse_cpu(buf, offs, n, plan, ends)
+    if buf.device.type == "cuda" and plan.max_depth < GPU_MAX_DEPTH:
+        return _parse_gpu_async(buf, offs, n, plan, ends)
+    if buf.device.type == "cuda":
+        # schemas nested deeper than the kernel's register stack parse on the host (same semantics)
+        col, ok = _parse_cpu(buf.cpu(), offs.cpu(), n, plan, None if ends is None else ends.cpu())
+        return PendingParse(done=(col.to(buf.device), ok.to(buf.device)))
+    return PendingParse(done=_parse_cpu(buf, offs, n, plan, ends))
 
 
 GPU_MAX_DEPTH = 8      # json_parse.hip kMaxDepth: struct nesting tracked in registers
 
 
 def _parse_gpu(buf, offs, n, plan: ParsePlan, ends=None):
-    if plan.max_depth >= GPU_MAX_DEPTH:
-        # schemas nested deeper than the kernel's register stack parse on the host (same semantics)
-        col, ok = _parse_cpu(buf.cpu(), offs.cpu(), n, plan, None if ends is None else ends.cpu())
-        return col.to(buf.device), ok.to(buf.device)
+    return _parse_gpu_async(buf, offs, n, plan, ends).result()
+
+
+def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
     lut_k, lut_n, types, vslot, lslot, fchild, nsib, kword, klen, kwords = plan.device_tables(buf.device)
     nn = len(plan.nodes)
     vals = torch.empty((max(1, plan.nval), max(n, 1)), dtype=torch.int64, device=buf.device)
     lens = torch.empty((max(1, plan.nlen), max(n, 1)), dtype=torch.int32, device=buf.device)
     valid = torch.empty((nn, max(n, 1)), dtype=torch.uint8, device=buf.device)
     row_ok = torch.empty(max(n, 1), dtype=torch.uint8, device=buf.device)
+    counts = event = None
     if n:
+        st = N.stream_handle(buf.device)
         N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
                N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
                N.ptr(fchild), N.ptr(nsib), N.ptr(kword), N.ptr(klen), N.ptr(kwords), int(kwords.numel()),
-               None if ends is None else N.ptr(ends), N.stream_handle(buf.device))
-    nulls = [1] * nn
-    if n:
+               None if ends is None else N.ptr(ends), st)
         cnt = torch.empty(nn, dtype=torch.int64, device=buf.device)
-        N.call("dxa_null_counts", N.ptr(valid), n, nn, N.ptr(cnt), N.stream_handle(buf.device))
-        nulls = cnt.tolist()   # one tiny D2H per batch
-    vals, lens, valid, row_ok = vals[:, :n], lens[:, :n], valid[:, :n].view(torch.bool), row_ok[:n].view(torch.bool)
-    return _assemble(plan, buf, vals, lens, valid, n, nulls), row_ok
+        N.call("dxa_null_counts", N.ptr(valid), n, nn, N.ptr(cnt), st)
+        counts = torch.empty(nn, dtype=torch.int64, pin_memory=True)
+        counts.copy_(cnt, non_blocking=True)     # a few bytes behind the kernels; read in result()
+        event = torch.cuda.Event()
+        event.record(torch.cuda.current_stream(buf.device))
+    parts = (vals[:, :n], lens[:, :n], valid[:, :n].view(torch.bool), row_ok[:n].view(torch.bool))
+    return PendingParse(plan=plan, arena=buf, parts=parts, n=n, counts=counts, event=event)
 
 
 def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):

@@ -420,3 +420,50 @@ def test_sdma_device_to_host_copy(gpu):
     torch.cuda.synchronize()
     assert N.lib().dxa_copy_sdma(host.data_ptr(), src.data_ptr() + 1, 3_000_000) == 0
     assert torch.equal(host[:3_000_000], src[1:].cpu())
+
+
+def test_parse_ahead_matches_parse(gpu):
+    """jsonparse.parse_async (Processor.prepare's parse-ahead) = parse, including the null-mask decisions."""
+    from dxa.ops.jsonparse import parse_async
+    recs = _records(4000, seed=9)
+    plan = ParsePlan(SCHEMA)
+    bg, og = frame_records(recs, device=gpu)
+    a, ok_a = parse(bg, og, plan)
+    pend = parse_async(bg, og, plan)
+    filler = torch.randn(1 << 22, device=gpu).sort()        # later work on the stream does not disturb the result
+    b, ok_b = pend.result()
+    assert pend.result()[0] is b
+    del filler
+    assert torch.equal(ok_a, ok_b)
+    assert a.to_pylist() == b.to_pylist()
+
+
+@pytest.mark.parametrize("variant", ["groupby", "window"])
+def test_processor_prepare_same_outputs(gpu, variant, tmp_path):
+    """A Processor fed prepared batches (parse queued one batch ahead) produces the same views as one that parses
+    inside process_batch."""
+    from dxa.engine.processor import Processor, RawBatch
+    from dxa.models import iot
+    from dxa.simulate.datagen import generate
+    prog = iot.program()
+    n, t0 = 20000, 1_700_000_000_000_000
+    bufs = [generate(prog, n, gpu, seed=i + 1, row0=i * n, base_ms=t0 // 1000 + i * 1000 - 1000, step_us=50)
+            for i in range(3)]
+    views = []
+    for ahead in (False, True):
+        proc = Processor(iot.flow_settings(workdir=str(tmp_path / f"w{ahead}"), variant=variant), gpu)
+        proc.keep_views = True
+        raws = [RawBatch(b, o, n) for b, o in bufs]
+        got = []
+        for i, rb in enumerate(raws):
+            proc.process_batch(rb, t0 + i * 1_000_000, 1_000_000)
+            if ahead and i + 1 < len(raws):
+                proc.prepare(raws[i + 1])
+                assert raws[i + 1].pending is not None
+            name = "DeviceSummary" if variant == "groupby" else "DeviceWindow"
+            v = proc.last_views[name]
+            rows = sorted(json.dumps(r, sort_keys=True, default=str) for r in zip(*[c.to_pylist() for c in v.columns]))
+            got.append(rows)
+        proc.drain()
+        views.append(got)
+    assert views[0] == views[1]
