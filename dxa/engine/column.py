@@ -177,12 +177,12 @@ class PrimColumn(Column):
     def to_pylist(self):
         vals = self.data.cpu().tolist()
         valid = self.valid.cpu().tolist() if self.valid is not None else None
-        if self.dtype == "timestamp":
-            vals = [ts_to_datetime(v) for v in vals]
-        elif self.dtype == "date":
-            vals = [(EPOCH + _dt.timedelta(days=int(v))).date() for v in vals]
         if valid is not None:
-            vals = [v if ok else None for v, ok in zip(vals, valid)]
+            vals = [v if ok else None for v, ok in zip(vals, valid)]      # values under a null are undefined bytes
+        if self.dtype == "timestamp":
+            vals = [None if v is None else ts_to_datetime(v) for v in vals]
+        elif self.dtype == "date":
+            vals = [None if v is None else (EPOCH + _dt.timedelta(days=int(v))).date() for v in vals]
         return vals
 
     def __repr__(self):

@@ -44,7 +44,8 @@ _SYNC_STAGES = os.environ.get("DXA_SYNC_STAGES") == "1"
 
 @dataclass
 class RawBatch:
-    """One micro-batch of raw event payloads resident on the device."""
+    """One micro-batch of raw event payloads resident on the device.  The JSON parse un-escapes string values in
+    place (json_parse.hip), so a batch's bytes are consumed by its one parse: re-processing needs fresh bytes."""
     buf: torch.Tensor            # uint8, 16-byte padded
     offs: torch.Tensor           # int64 [n+1]
     n: int
