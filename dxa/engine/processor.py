@@ -257,10 +257,13 @@ class Processor:
         t0 = time.perf_counter()
         if self.transform is not None:
             from ..sql.parser import parse_query
-            for cmd in self.transform.commands:
+            live = None if self.keep_views else self._live_statements()
+            for k, cmd in enumerate(self.transform.commands):
                 if cmd.command_type == COMMAND_COMMAND:
                     self._run_command(cmd.text)
                     continue
+                if live is not None and k not in live:
+                    continue                       # a view nothing reads: Spark never evaluates it either
                 q = self._parsed.get(cmd.text)
                 if q is None:
                     q = self._parsed[cmd.text] = parse_query(cmd.text)     # parsed once, reused every batch
@@ -304,6 +307,39 @@ class Processor:
             self._sync()
             self.stage_times["output"] = time.perf_counter() - t1
         return fl.metrics
+
+    def _live_statements(self) -> Optional[set]:
+        """Indices of the transform's query statements whose results can reach an output or a state table.
+        Spark temp views are lazy: the reference registers each statement as ``spark.sql(statement)`` +
+        ``createOrReplaceTempView`` (CommonProcessorFactory.scala:270-288) and only the outputs run actions
+        (:297-305) and state tables write (:258-264), so a view that no output, accumulator or later live statement
+        reads is never computed (the generated ``sa2_*`` copies, a ``Tagged`` view whose only consumers are the per-rule alert
+        views, …), so skipping it changes no output.  Liveness runs backwards over the statements; a statement's
+        reads are over-approximated by every statement name appearing as a word in its text.  ``DXA_DEAD_VIEWS=0``
+        evaluates everything."""
+        if getattr(self, "_live", None) is not None or os.environ.get("DXA_DEAD_VIEWS", "1") == "0":
+            return getattr(self, "_live", None)
+        import re
+        cmds = self.transform.commands
+        names = {c.name.lower() for c in cmds if c.command_type != COMMAND_COMMAND and c.name}
+        needed = {op.name.lower() for op in self.outputs} | {n.lower() for n in self.state_tables}
+        live = set()
+        for k in range(len(cmds) - 1, -1, -1):
+            c = cmds[k]
+            if c.command_type == COMMAND_COMMAND or not c.name:
+                continue
+            nm = c.name.lower()
+            if nm not in needed:
+                continue
+            live.add(k)
+            needed.discard(nm)
+            words = {w.lower() for w in re.findall(r"[A-Za-z_][A-Za-z0-9_]*", c.text)}
+            needed |= (words & names) | ({nm} & words)
+        self._live = live
+        skipped = [c.name for k, c in enumerate(cmds) if c.command_type != COMMAND_COMMAND and k not in live]
+        if skipped:
+            log.info("views no output reads (not evaluated): %s", ", ".join(skipped))
+        return live
 
     def _complete_inflight(self):
         """Finish the in-flight batch: collect sink counts, all-reduce the batch metrics across ranks, persist state
