@@ -528,12 +528,37 @@ def concat_columns(cols: List[Column]) -> Column:
     raise TypeError(f"cannot concat {type(first)}")
 
 
+class LazyColumns(list):
+    """A column list whose entries are produced on first access (``_make(i)``).  Tables and scopes keep such a list
+    as is, so a view whose columns a consumer never reads never pays for them (e.g. ``SELECT * … WHERE`` feeding
+    an alert that only needs the row count).  Iteration and indexing resolve entries; the list's own slots hold
+    ``None`` until then, so list-internal operations (``+``, ``.copy()``) must not be used on it."""
+
+    def _make(self, i):
+        raise NotImplementedError
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        v = list.__getitem__(self, i)
+        if v is None:
+            v = self._make(i)
+            list.__setitem__(self, i, v)
+        return v
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+    def __reversed__(self):
+        return (self[i] for i in range(len(self) - 1, -1, -1))
+
+
 class Table:
     """An ordered set of named columns with a common length (a Spark DataFrame's role in the reference)."""
 
     def __init__(self, names: List[str], columns: List[Column], length: Optional[int] = None, device=None):
         self.names = list(names)
-        self.columns = list(columns)
+        self.columns = columns if isinstance(columns, LazyColumns) else list(columns)
         if length is None:
             length = columns[0].length if columns else 0
         self.length = int(length)
@@ -554,14 +579,11 @@ class Table:
         return self.length
 
     def column(self, name: str) -> Optional[Column]:
-        for n, c in zip(self.names, self.columns):
+        for i, n in enumerate(self.names):          # by index: a lazy column list resolves only the match
             if n == name:
-                return c
-        low = name.lower()
-        for n, c in zip(self.names, self.columns):
-            if n.lower() == low:
-                return c
-        return None
+                return self.columns[i]
+        i = self.index_of(name)
+        return self.columns[i] if i >= 0 else None
 
     def index_of(self, name: str) -> int:
         low = name.lower()

@@ -20,8 +20,8 @@ import torch
 from ..sql import ast as A
 from . import functions as F
 from . import jit as _jit_mod
-from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn,
-                     TORCH_DTYPE, and_valid, column_from_pylist, concat_columns, materialize, strings_from_pylist)
+from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, LazyColumns, PrimColumn, StrColumn,
+                     StructColumn, TORCH_DTYPE, and_valid, column_from_pylist, concat_columns, materialize, strings_from_pylist)
 from .types import (ArrayType, MapType, StructType, common_type, is_integral, is_nested, is_numeric)
 
 AGG_FUNCS = {"count", "sum", "avg", "mean", "min", "max", "first", "last", "first_value", "last_value", "stddev",
@@ -41,26 +41,30 @@ class EvalContext:
     device: Any = "cpu"
 
 
-class TakenColumns(list):
+class TakenColumns(LazyColumns):
     """``[c.take(idx) for c in cols]`` computed per column on first access: a filtered or grouped scope usually
     reads a few of its input's columns, so the gathers of the others are never launched."""
 
     def __init__(self, cols, idx):
         super().__init__([None] * len(cols))
-        self._src = cols if isinstance(cols, TakenColumns) else list(cols)
+        self._src = cols if isinstance(cols, LazyColumns) else list(cols)
         self._idx = idx
 
-    def __getitem__(self, i):
-        if isinstance(i, slice):
-            return [self[j] for j in range(*i.indices(len(self)))]
-        v = list.__getitem__(self, i)
-        if v is None:
-            v = self._src[i].take(self._idx)
-            list.__setitem__(self, i, v)
-        return v
+    def _make(self, i):
+        return self._src[i].take(self._idx)
 
-    def __iter__(self):
-        return (self[i] for i in range(len(self)))
+
+class DeferredColumns(LazyColumns):
+    """A projection's output columns where the bare column references into a lazy scope stay unresolved until
+    read (``entries``: a column, or ``(lazy_list, index)``)."""
+
+    def __init__(self, entries):
+        super().__init__([e if not isinstance(e, tuple) else None for e in entries])
+        self._refs = [e if isinstance(e, tuple) else None for e in entries]
+
+    def _make(self, i):
+        src, j = self._refs[i]
+        return src[j]
 
 
 class Scope:
@@ -75,7 +79,8 @@ class Scope:
 
     @staticmethod
     def of_table(table, qual: Optional[str] = None) -> "Scope":
-        return Scope(list(table.names), list(table.columns), [qual] * len(table.names), table.length, table.device)
+        cols = table.columns if isinstance(table.columns, LazyColumns) else list(table.columns)
+        return Scope(list(table.names), cols, [qual] * len(table.names), table.length, table.device)
 
     def qualifiers(self):
         return {q.lower() for q in self.quals if q}

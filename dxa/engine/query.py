@@ -17,10 +17,10 @@ from .. import parallel as P
 from ..ops.hashing import hash_columns
 from ..sql import ast as A
 from ..sql.parser import parse_query
-from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, Table, concat_columns,
-                     concat_tables, materialize)
-from .expr import (AGG_FUNCS, EvalContext, EvalError, Scope, TakenColumns, cast_column, evaluate, output_name,
-                   predicate_mask)
+from .column import (ArrayColumn, Column, ConstColumn, LazyColumns, PrimColumn, StrColumn, StructColumn, Table,
+                     concat_columns, concat_tables, materialize)
+from .expr import (AGG_FUNCS, DeferredColumns, EvalContext, EvalError, Scope, TakenColumns, cast_column, evaluate,
+                   output_name, predicate_mask)
 from . import windowfn as W
 from .types import common_type, is_nested
 
@@ -560,7 +560,12 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         src = None
     else:
         subst = _window_columns(wcalls, lambda x: evaluate(x, scope, ctx), scope.length, scope.device, {})
-        cols = [evaluate(e, scope, ctx, subst or None) for e, _ in items]
+        if not subst and isinstance(scope.cols, LazyColumns):
+            # bare column references into a filtered scope stay deferred takes: a consumer reading few of them
+            # (an alert view over ``SELECT * … WHERE``) never gathers the rest
+            cols = DeferredColumns([_deferred_ref(e, scope) or evaluate(e, scope, ctx) for e, _ in items])
+        else:
+            cols = [evaluate(e, scope, ctx, subst or None) for e, _ in items]
         out = Table([nm for _, nm in items], cols, scope.length, scope.device)
         out.dist = sdist
         src = scope
@@ -568,6 +573,20 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         out = distinct(out)
         src = None
     return out, (src if want_scope else None)
+
+
+def _deferred_ref(e: A.Expr, scope: Scope):
+    """(scope.cols, index) for a bare, unambiguous column reference (no struct navigation), else None."""
+    if not isinstance(e, A.Ident):
+        return None
+    parts = e.parts
+    if len(parts) == 2 and scope.has_qualifier(parts[0]):
+        hits = scope._find(parts[1], parts[0])
+    elif len(parts) == 1:
+        hits = scope._find(parts[0])
+    else:
+        return None
+    return (scope.cols, hits[0]) if len(hits) == 1 else None
 
 
 def _resolve_group_expr(g: A.Expr, scope: Scope, items) -> A.Expr:

@@ -111,7 +111,9 @@ class HipUDF(VectorUDF):
                     f"{self.source}\n"
                     f"extern \"C\" void {self.kernel_name}({', '.join(params)}) {{\n"
                     f"  for (long long i = 0; i < n; ++i) {{\n    {row}\n  }}\n}}\n")
-        return (f"#include <hip/hip_runtime.h>\n{self.source}\n"
+        # no #include <hip/hip_runtime.h>: hipRTC pre-includes the HIP runtime and device math, and the header
+        # path is not resolvable in every process environment (e.g. under rocprofv3)
+        return (f"{self.source}\n"
                 f"extern \"C\" __global__ __launch_bounds__(256) void {self.kernel_name}({', '.join(params)}) {{\n"
                 f"  const long long stride = (long long)gridDim.x * 256;\n"
                 f"  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {{\n"
@@ -244,7 +246,9 @@ class HipUDAF:
                     f"{self.source}\n"
                     f"extern \"C\" void {self.kernel_name}({', '.join(params)}) {{\n"
                     f"  for (long long g = 0; g < ngroups; ++g) {{\n{body}  }}\n}}\n")
-        return (f"#include <hip/hip_runtime.h>\n{self.source}\n"
+        # no #include <hip/hip_runtime.h>: hipRTC pre-includes the HIP runtime and device math, and the header
+        # path is not resolvable in every process environment (e.g. under rocprofv3)
+        return (f"{self.source}\n"
                 f"extern \"C\" __global__ __launch_bounds__(256) void {self.kernel_name}({', '.join(params)}) {{\n"
                 f"  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;\n"
                 f"  if (g < ngroups) {{\n{body}  }}\n}}\n")
