@@ -171,6 +171,55 @@ __global__ __launch_bounds__(256) void str_gather_lane_kernel(const uint8_t* __r
   }
 }
 
+// Many string gathers in one launch: part p copies its rows [row0_p, row0_{p+1}) of the launch's row space from
+// its own arena into its own destination (dst + dst_off[r]).  Used for row-concatenation (parts share one dst and
+// consecutive offset ranges) and for compacting several columns at once (each its own dst) — one launch instead of
+// one per part.  Descriptors travel in the kernel argument block; a lane finds its part by a short scan of row0.
+constexpr int kMaxStrParts = 32;
+
+struct StrPart {
+  const uint8_t* arena;
+  const int64_t* starts;
+  const int32_t* lens;
+  const int64_t* dst_off;
+  uint8_t* dst;
+  int64_t row0;
+};
+
+struct StrParts {
+  StrPart p[kMaxStrParts];
+  int32_t k;
+  int64_t total;
+};
+
+__global__ __launch_bounds__(256) void str_gather_parts_kernel(const StrParts a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const SG1 uint8_t* s = nullptr;
+  SG1 uint8_t* d = nullptr;
+  int32_t l = 0;
+  if (i < a.total) {
+    int q = 0;
+    for (int t = 1; t < a.k; ++t) q = i >= a.p[t].row0 ? t : q;
+    const StrPart& P = a.p[q];
+    const int64_t r = i - P.row0;
+    l = P.lens[r];
+    s = (const SG1 uint8_t*)P.arena + P.starts[r];
+    d = (SG1 uint8_t*)P.dst + P.dst_off[r];
+  }
+  const bool lng = l > 128;
+  if (!lng && l > 0) copy_short(s, d, l);
+  uint64_t m = __ballot(lng);
+  const int lane = threadIdx.x & 63;
+  while (m) {
+    const int j = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const SG1 uint8_t* sj = (const SG1 uint8_t*)__shfl((uint64_t)(uintptr_t)s, j);
+    SG1 uint8_t* dj = (SG1 uint8_t*)__shfl((uint64_t)(uintptr_t)d, j);
+    const int32_t lj = __shfl(l, j);
+    for (int32_t k = lane; k < lj; k += 64) dj[k] = sj[k];
+  }
+}
+
 // CONCAT(part_0, …, part_{k-1}); each part is either a column view or a literal.  Null in any column part → null.
 struct ConcatPart {
   const uint8_t* arena;
@@ -415,6 +464,29 @@ DXA_API int dxa_str_gather(const uint8_t* arena, const int64_t* starts, const in
                        arena, starts, lens, n, dst_off, dst);
   return (int)hipGetLastError();
 }
+
+// parts: host array of k StrPart descriptors (row0 relative to the first part); launches in groups of kMaxStrParts.
+DXA_API int dxa_str_gather_parts(const void* parts, int32_t k, void* st) {
+  const StrPart* ps = (const StrPart*)parts;
+  for (int32_t g = 0; g < k; g += kMaxStrParts) {
+    const int32_t kk = k - g < kMaxStrParts ? k - g : kMaxStrParts;
+    StrParts a{};
+    const int64_t base = ps[g].row0;
+    for (int32_t j = 0; j < kk; ++j) {
+      a.p[j] = ps[g + j];
+      a.p[j].row0 -= base;
+    }
+    a.k = kk;
+    // the group ends where the next part begins; the caller appends an end sentinel (row0 = total) after part k-1
+    a.total = ps[g + kk].row0 - base;
+    if (a.total <= 0) continue;
+    hipLaunchKernelGGL(str_gather_parts_kernel, dim3((unsigned)((a.total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)st, a);
+  }
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_part_size() { return (int)sizeof(StrPart); }
 
 // parts: device array of ConcatPart (k entries) prepared by the host.
 DXA_API int dxa_concat_len(const void* parts, int32_t k, int64_t n, int64_t* out_len, uint8_t* out_valid, void* st) {

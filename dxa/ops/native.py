@@ -59,6 +59,8 @@ _SIGS = {
     "dxa_str_eq_col": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
     "dxa_str_cmp_col": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p],
     "dxa_str_gather": [c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
+    "dxa_str_gather_parts": [c_p, c_i32, c_p],
+    "dxa_str_part_size": [],
     "dxa_concat_len": [c_p, c_i32, c_i64, c_p, c_p, c_p],
     "dxa_concat_write": [c_p, c_i32, c_i64, c_p, c_p, c_p, c_p],
     "dxa_concat_part_size": [],
@@ -131,7 +133,20 @@ def ptr(t) -> int:
     return t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_handle(device=None) -> int:
+    """The current HIP stream of ``device`` as an integer handle (the raw-stream query skips building a Stream
+    object; a few hundred kernel launches per batch go through here)."""
+    if _RAW_STREAM is not None:
+        idx = getattr(device, "index", None)
+        if idx is None:
+            idx = torch.device(device).index if isinstance(device, (str, int)) and not isinstance(device, bool) \
+                else None
+        if idx is None:
+            idx = torch.cuda.current_device()
+        return _RAW_STREAM(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

@@ -69,6 +69,29 @@ def compact_known(col, total: int):
     return out
 
 
+class _StrPart(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("starts", ctypes.c_void_p), ("lens", ctypes.c_void_p),
+                ("dst_off", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row0", ctypes.c_int64)]
+
+
+def _gather_parts(parts, device) -> None:
+    """One ``dxa_str_gather_parts`` launch (per 32 parts) for many string gathers.  ``parts``: (StrColumn view,
+    destination offsets tensor, destination arena) triples; offsets are per row of the part."""
+    parts = [p for p in parts if p[0].length]
+    if not parts:
+        return
+    if N.lib().dxa_str_part_size() != ctypes.sizeof(_StrPart):
+        raise N.NativeError("StrPart layout mismatch between strings.py and strings.hip")
+    arr = (_StrPart * (len(parts) + 1))()
+    row = 0
+    for j, (c, off, dst) in enumerate(parts):
+        arr[j] = _StrPart(c.arena.data_ptr(), c.starts.data_ptr(), c.lens.data_ptr(), off.data_ptr(),
+                          dst.data_ptr(), row)
+        row += c.length
+    arr[len(parts)].row0 = row                      # end sentinel
+    N.call("dxa_str_gather_parts", ctypes.cast(arr, ctypes.c_void_p), len(parts), N.stream_handle(device))
+
+
 def compact_many(cols: Sequence) -> list:
     """``compact`` of several string columns with ONE host synchronisation (all arena sizes are read back together)
     instead of one per column."""
@@ -85,16 +108,15 @@ def compact_many(cols: Sequence) -> list:
         offs.append(cs - lens64 if c.length else cs[:0])
         ends.append(cs[-1:] if c.length else cs)
     totals = torch.cat(ends).tolist()
-    out = []
-    st = N.stream_handle(device)
+    out, parts = [], []
     for c, off, total in zip(cols, offs, totals):
         dst = _alloc_arena(int(total), device)
         if c.length and total:
-            N.call("dxa_str_gather", N.ptr(c.arena), N.ptr(c.starts), N.ptr(c.lens), c.length, N.ptr(off), N.ptr(dst),
-                   st)
+            parts.append((c, off, dst))
         o = type(c)(dst, off, c.lens.clone(), c.valid, c.dtype)
         o._compact = True
         out.append(o)
+    _gather_parts(parts, device)                   # every column's bytes in one launch
     return out
 
 
@@ -104,21 +126,25 @@ def concat(cols: Sequence, valid: Optional[torch.Tensor]):
     lens = torch.cat([c.lens for c in cols])
     off, total = _offsets(lens)
     dst = _alloc_arena(total, device)
+    if _gpu(cols[0].starts):
+        parts, pos = [], 0
+        for c in cols:
+            if c.length:
+                parts.append((c, off[pos:pos + c.length], dst))
+            pos += c.length
+        _gather_parts(parts, device)                # all parts' bytes in one launch
+        return type(cols[0])(dst, off, lens.to(torch.int32), valid, cols[0].dtype)
     pos = 0
-    for c in cols:
+    for c in cols:                                  # CPU reference path
         n = c.length
         if n:
             o = off[pos:pos + n].contiguous()
-            if _gpu(c.starts):
-                N.call("dxa_str_gather", N.ptr(c.arena), N.ptr(c.starts), N.ptr(c.lens), n, N.ptr(o), N.ptr(dst),
-                       N.stream_handle(device))
-            else:
-                tot = int(c.lens.to(torch.int64).sum().item())
-                if tot:
-                    # destination positions are contiguous from o[0]
-                    srcpos = torch.repeat_interleave(c.starts, c.lens.to(torch.int64)) + (
-                        torch.arange(tot) - torch.repeat_interleave(o - o[0], c.lens.to(torch.int64)))
-                    dst[int(o[0]):int(o[0]) + tot] = c.arena[srcpos]
+            tot = int(c.lens.to(torch.int64).sum().item())
+            if tot:
+                # destination positions are contiguous from o[0]
+                srcpos = torch.repeat_interleave(c.starts, c.lens.to(torch.int64)) + (
+                    torch.arange(tot) - torch.repeat_interleave(o - o[0], c.lens.to(torch.int64)))
+                dst[int(o[0]):int(o[0]) + tot] = c.arena[srcpos]
         pos += n
     return type(cols[0])(dst, off, lens.to(torch.int32), valid, cols[0].dtype)
 

@@ -474,3 +474,32 @@ def test_processor_prepare_same_outputs(gpu, variant, tmp_path):
                     assert b == pytest.approx(a, rel=1e-9)      # float sums: atomic order differs between runs
                 else:
                     assert a == b
+
+
+def test_string_concat_and_compact_many_parts(gpu):
+    """strings.concat / compact_many go through one multi-part gather launch per 32 parts: 45 parts (empty ones,
+    strings longer than the 128-byte lane path, views into shared arenas) against the CPU reference."""
+    rnd = random.Random(11)
+
+    def col(k):
+        vals = [None if rnd.random() < 0.1 else "".join(rnd.choice("abcé\"xyz") for _ in range(rnd.choice(
+            [0, 1, 7, 40, 129, 300]))) for _ in range(k)]
+        return vals
+
+    lists = [col(rnd.choice([0, 1, 5, 60, 300])) for _ in range(45)]
+    cpu_cols = [strings_from_pylist(v, "cpu") for v in lists]
+    gpu_cols = [c.to(gpu) for c in cpu_cols]
+    # views: every other part is a take (starts into a bigger arena, not compact)
+    for i in range(0, 45, 2):
+        if gpu_cols[i].length:
+            idx = torch.arange(gpu_cols[i].length - 1, -1, -1)
+            cpu_cols[i] = cpu_cols[i].take(idx)
+            gpu_cols[i] = gpu_cols[i].take(idx.to(gpu))
+    want = [x for c in cpu_cols for x in c.to_pylist()]
+    nn = sum(c.length for c in gpu_cols)
+    valid = torch.tensor([x is not None for x in want], dtype=torch.bool, device=gpu)
+    got = S.concat(gpu_cols, valid)
+    assert got.to_pylist() == want
+    many = S.compact_many(gpu_cols)
+    assert [c.to_pylist() for c in many] == [c.to_pylist() for c in cpu_cols]
+    assert nn == got.length
