@@ -133,7 +133,8 @@ def ptr(t) -> int:
     return t.data_ptr()
 
 
-_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None) if os.environ.get("DXA_RAW_STREAM", "1") != "0" \
+    else None
 
 
 def stream_handle(device=None) -> int:
