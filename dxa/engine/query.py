@@ -296,11 +296,11 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         out = Scope(left.names, TakenColumns(left.cols, li), left.quals, int(li.shape[0]), dev)
         out.dist = out_dist
         return out
-    cols = []
-    for c in left.cols:
-        cols.append(_take_nullable(c, li))
-    for c in right.cols:
-        cols.append(_take_nullable(c, ri))
+    # which side can carry -1 (no match) is known from the join kind: no per-column host check.  Columns are
+    # gathered on first read (a join feeding a narrow SELECT touches few of them).
+    l_miss, r_miss = kind in ("right", "full"), kind in ("left", "full")
+    cols = _JoinColumns([(left.cols, i, li, l_miss) for i in range(len(left.cols))] +
+                        [(right.cols, i, ri, r_miss) for i in range(len(right.cols))])
     out = Scope(left.names + right.names, cols, left.quals + right.quals, int(li.shape[0]), dev)
     if residual:
         pred = None
@@ -342,14 +342,28 @@ def _coerce_keys(lk, rk):
     return lo, ro
 
 
-def _take_nullable(col: Column, idx: torch.Tensor) -> Column:
-    miss = idx < 0
-    if not bool(miss.any()) if idx.numel() else True:
+def _take_nullable(col: Column, idx: torch.Tensor, may_miss: bool = True) -> Column:
+    """Rows ``idx`` of ``col``; -1 entries (no join partner) become nulls.  No host synchronisation."""
+    if not may_miss:
         return col.take(idx)
-    safe = torch.where(miss, torch.zeros_like(idx), idx)
     if col.length == 0:
         return ConstColumn(None, col.dtype, int(idx.shape[0]), col.device)
+    miss = idx < 0
+    safe = torch.where(miss, torch.zeros_like(idx), idx)
     return col.take(safe).with_valid(~miss)
+
+
+class _JoinColumns(LazyColumns):
+    """A join's output columns, each gathered from its side on first read: entries (side columns, index, row
+    index vector, may hold -1)."""
+
+    def __init__(self, entries):
+        super().__init__([None] * len(entries))
+        self._e = entries
+
+    def _make(self, i):
+        src, j, idx, miss = self._e[i]
+        return _take_nullable(src[j], idx, miss)
 
 
 # ---------------------------------------------------------------------------------------------------------------
