@@ -26,7 +26,8 @@ from .types import (ArrayType, MapType, StructType, common_type, is_integral, is
 
 AGG_FUNCS = {"count", "sum", "avg", "mean", "min", "max", "first", "last", "first_value", "last_value", "stddev",
              "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std", "collect_list", "collect_set",
-             "approx_count_distinct", "count_if", "bool_and", "bool_or", "every", "any", "some"}
+             "approx_count_distinct", "count_if", "bool_and", "bool_or", "every", "any", "some", "percentile",
+             "percentile_approx", "approx_percentile", "median"}
 
 
 class EvalError(Exception):
@@ -39,6 +40,7 @@ class EvalContext:
     udfs: Dict[str, Any] = field(default_factory=dict)   # name → UDF (callable(columns, ctx) → Column)
     udafs: Dict[str, Any] = field(default_factory=dict)
     device: Any = "cpu"
+    catalog: Any = None                   # tables visible to sub-queries (set by query.execute)
 
 
 class TakenColumns(LazyColumns):
@@ -67,6 +69,17 @@ class DeferredColumns(LazyColumns):
         return src[j]
 
 
+class _Prepended(LazyColumns):
+    """``head + rest`` without resolving ``rest`` (a lazy scope stays lazy under lambda bindings)."""
+
+    def __init__(self, head, rest):
+        super().__init__(list(head) + [None] * len(rest))
+        self._k, self._rest = len(head), rest
+
+    def _make(self, i):
+        return self._rest[i - self._k]
+
+
 class Scope:
     """Columns visible to an expression: (qualifier, name, column) triples over ``length`` rows."""
 
@@ -76,6 +89,13 @@ class Scope:
         self.quals = quals
         self.length = int(length)
         self.device = torch.device(device)
+
+    def with_bindings(self, names: List[str], cols: List[Column]) -> "Scope":
+        """This scope plus ``names`` bound to ``cols`` (lambda parameters), which shadow same-named columns."""
+        sc = Scope(list(names) + list(self.names), _Prepended(list(cols), self.cols), [None] * len(names) +
+                   list(self.quals), self.length, self.device)
+        sc.dist = getattr(self, "dist", None)
+        return sc
 
     @staticmethod
     def of_table(table, qual: Optional[str] = None) -> "Scope":
@@ -267,6 +287,10 @@ def evaluate(e: A.Expr, scope: Scope, ctx: EvalContext, subst: Optional[Dict] = 
         return ConstColumn(e.value, t, n, dev)
     if isinstance(e, A.Ident):
         return scope.resolve(e.parts)
+    if isinstance(e, A.SubqueryExpr):
+        return _subquery(e, scope, ctx, subst)
+    if isinstance(e, A.Lambda):
+        raise EvalError("a lambda is only allowed as an argument of a higher-order function")
     if isinstance(e, A.Interval):
         return ConstColumn(e.micros, "interval", n, dev)
     if isinstance(e, A.BinOp):
@@ -869,6 +893,191 @@ def _call(e: A.Call, scope: Scope, ctx: EvalContext, subst):
     return fn(e, scope, ctx, subst)
 
 
+def _subquery(e: A.SubqueryExpr, scope: Scope, ctx: EvalContext, subst) -> Column:
+    """Uncorrelated sub-queries: planned on their own against the statement's catalog."""
+    from . import query as Q
+    from .. import parallel as P
+    n, dev = scope.length, scope.device
+    if ctx.catalog is None:
+        raise EvalError("sub-query outside a query")
+    if e.kind in ("exists", "in"):
+        hit = _correlated_semi(e, scope, ctx, subst)
+        if hit is not None:
+            return bool_col(~hit if e.negated else hit, None)
+    try:
+        t = Q.execute(e.query, ctx.catalog, ctx)
+    except EvalError as err:
+        raise EvalError(f"sub-query failed (only equality-correlated EXISTS / IN sub-queries are supported): "
+                        f"{err}") from err
+    if P.active() and P.dist_of(t) != P.REPLICATED:
+        t = Q._gathered(t)
+    if e.kind == "exists":
+        return ConstColumn(t.length > 0, "boolean", n, dev)
+    if len(t.columns) != 1:
+        raise EvalError(f"sub-query must return one column, got {len(t.columns)}")
+    rc = t.columns[0]
+    if e.kind == "scalar":
+        if t.length > 1:
+            raise EvalError("scalar sub-query returned more than one row")
+        v = rc.to_pylist()[0] if t.length else None
+        return ConstColumn(v, rc.dtype, n, dev)
+    # x [NOT] IN (SELECT c …): a semi-join membership test; SQL three-valued logic for nulls
+    x = evaluate(e.operand, scope, ctx, subst)
+    if isinstance(x, ConstColumn):
+        x = x.materialize()
+    rc = rc.materialize() if isinstance(rc, ConstColumn) else rc
+    from ..ops import join as J
+    from .query import _coerce_keys
+    xs, rs = _coerce_keys([x], [rc])
+    hit = torch.zeros(n, dtype=torch.bool, device=dev)
+    if n and t.length:
+        li, _ = J.hash_join(xs, rs, "semi")
+        hit[li] = True
+    rhs_null = bool((~rc.valid).any()) if (t.length and rc.valid is not None) else False
+    valid = x.valid_mask() & (hit | (not rhs_null)) if (x.valid is not None or rhs_null) else None
+    return bool_col(~hit if e.negated else hit, valid)
+
+
+def _correlated_semi(e: A.SubqueryExpr, scope: Scope, ctx: EvalContext, subst) -> Optional[torch.Tensor]:
+    """Decorrelate ``EXISTS (SELECT … FROM s WHERE s.k = outer.k AND …)`` and the IN form into a semi-join on the
+    equality keys (plus the IN operand / select item).  None when the sub-query is not correlated that way."""
+    from . import query as Q
+    from .. import parallel as P
+    from ..ops import join as J
+    q = e.query
+    body = q.body
+    if q.ctes or not isinstance(body, A.Select) or body.where is None or body.group_by or body.having is not None:
+        return None
+    inner_probe = None
+    outer_keys, inner_keys, rest = [], [], []
+    for c in Q._split_and(body.where):
+        if isinstance(c, A.BinOp) and c.op == "=":
+            if inner_probe is None:
+                inner_probe = Q._relation(body.from_, ctx.catalog, ctx)
+            l_in, r_in = Q._refs_resolvable(c.left, inner_probe), Q._refs_resolvable(c.right, inner_probe)
+            if l_in and not r_in and Q._refs_resolvable(c.right, scope):
+                inner_keys.append(c.left)
+                outer_keys.append(c.right)
+                continue
+            if r_in and not l_in and Q._refs_resolvable(c.left, scope):
+                inner_keys.append(c.right)
+                outer_keys.append(c.left)
+                continue
+        rest.append(c)
+    if not outer_keys:
+        return None
+    inner = inner_probe
+    for c in rest:
+        if not Q._refs_resolvable(c, inner):
+            raise EvalError("correlated sub-query predicates other than equality are not supported")
+    if rest:
+        m = None
+        for c in rest:
+            mc = predicate_mask(evaluate(c, inner, ctx))
+            m = mc if m is None else m & mc
+        idx = torch.nonzero(m).flatten()
+        inner = Scope(inner.names, TakenColumns(inner.cols, idx), inner.quals, int(idx.shape[0]), inner.device)
+    if e.kind == "in":
+        items = Q._expand_items(body, inner)
+        if len(items) != 1:
+            raise EvalError("IN sub-query must return one column")
+        inner_keys.append(items[0][0])
+        outer_keys.append(e.operand)
+    if P.active() and getattr(inner_probe, "dist", P.REPLICATED) != P.REPLICATED:
+        inner = Q._gather_scope(inner)
+    n = scope.length
+    hit = torch.zeros(n, dtype=torch.bool, device=scope.device)
+    if n and inner.length:
+        ok = [materialize(evaluate(k, scope, ctx, subst)) for k in outer_keys]
+        ik = [materialize(evaluate(k, inner, ctx)) for k in inner_keys]
+        ok, ik = Q._coerce_keys(ok, ik)
+        li, _ = J.hash_join(ok, ik, "semi")
+        hit[li] = True
+    return hit
+
+
+def _lambda_arg(e: A.Call, k: int) -> A.Lambda:
+    if len(e.args) <= k or not isinstance(e.args[k], A.Lambda):
+        raise EvalError(f"{e.name}() expects a lambda as argument {k + 1}")
+    return e.args[k]
+
+
+def _hof_elements(e: A.Call, scope, ctx, subst):
+    arr = evaluate(e.args[0], scope, ctx, subst)
+    if not isinstance(arr, ArrayColumn):
+        raise EvalError(f"{e.name}() expects an array")
+    return arr
+
+
+def _slot_present(arr: "ArrayColumn", el) -> torch.Tensor:
+    """Element slot is part of the array (a dropped-null slot is not)."""
+    n = arr.length
+    base = arr.valid_mask() if arr.valid is not None else torch.ones(n, dtype=torch.bool, device=arr.device)
+    if arr.drop_nulls:
+        if isinstance(el, ConstColumn):
+            return base & (el.value is not None)
+        return base & el.valid_mask()
+    return base
+
+
+def _f_transform(e, scope, ctx, subst):
+    """transform(arr, x -> f(x)) / transform(arr, (x, i) -> f(x, i))."""
+    arr = _hof_elements(e, scope, ctx, subst)
+    lam = _lambda_arg(e, 1)
+    out = []
+    for j, el in enumerate(arr.elements):
+        binds = [el] + ([ConstColumn(j, "int", arr.length, arr.device)] if len(lam.params) > 1 else [])
+        v = evaluate(lam.body, scope.with_bindings(list(lam.params[:len(binds)]), binds), ctx, subst)
+        if arr.drop_nulls:                            # keep the slot structure: absent slots stay absent
+            v = v.materialize() if isinstance(v, ConstColumn) else v
+            v = v.with_valid(_slot_present(arr, el))
+        out.append(v)
+    return ArrayColumn(out, arr.length, arr.valid, arr.drop_nulls, arr.device)
+
+
+def _f_array_filter(e, scope, ctx, subst):
+    """filter(arr, x -> pred): slots failing the predicate are dropped."""
+    arr = _hof_elements(e, scope, ctx, subst)
+    lam = _lambda_arg(e, 1)
+    out = []
+    for j, el in enumerate(arr.elements):
+        binds = [el] + ([ConstColumn(j, "int", arr.length, arr.device)] if len(lam.params) > 1 else [])
+        keep = predicate_mask(evaluate(lam.body, scope.with_bindings(list(lam.params[:len(binds)]), binds), ctx,
+                                       subst)) & _slot_present(arr, el)
+        m = el.materialize() if isinstance(el, ConstColumn) else el
+        out.append(m.with_valid(keep))
+    return ArrayColumn(out, arr.length, arr.valid, True, arr.device)
+
+
+def _f_array_exists(kind):
+    def f(e, scope, ctx, subst):
+        arr = _hof_elements(e, scope, ctx, subst)
+        lam = _lambda_arg(e, 1)
+        acc = torch.zeros(arr.length, dtype=torch.bool, device=arr.device) if kind == "exists" else \
+            torch.ones(arr.length, dtype=torch.bool, device=arr.device)
+        for el in arr.elements:
+            p = predicate_mask(evaluate(lam.body, scope.with_bindings([lam.params[0]], [el]), ctx, subst))
+            pres = _slot_present(arr, el)
+            acc = (acc | (p & pres)) if kind == "exists" else (acc & (p | ~pres))
+        return bool_col(acc, arr.valid)
+    return f
+
+
+def _f_array_aggregate(e, scope, ctx, subst):
+    """aggregate(arr, init, (acc, x) -> merge [, acc -> finish])."""
+    arr = _hof_elements(e, scope, ctx, subst)
+    acc = evaluate(e.args[1], scope, ctx, subst)
+    merge = _lambda_arg(e, 2)
+    for el in arr.elements:
+        nxt = evaluate(merge.body, scope.with_bindings(list(merge.params[:2]), [acc, el]), ctx, subst)
+        pres = _slot_present(arr, el)
+        acc = _select_by_conditions([bool_col(pres, None)], [nxt], acc, arr.length, arr.device)
+    if len(e.args) > 3:
+        fin = _lambda_arg(e, 3)
+        acc = evaluate(fin.body, scope.with_bindings([fin.params[0]], [acc]), ctx, subst)
+    return acc.with_valid(arr.valid) if arr.valid is not None else acc
+
+
 def _args(e, scope, ctx, subst):
     return [evaluate(a, scope, ctx, subst) for a in e.args]
 
@@ -1266,6 +1475,8 @@ _FUNCS: Dict[str, Callable] = {
     "uuid": _host_string_fn(lambda *a: str(__import__("uuid").uuid4())),
     "greatest": _f_greatest_least("greatest"), "least": _f_greatest_least("least"),
     "to_json": _f_to_json, "monotonically_increasing_id": _f_monotonic,
+    "transform": _f_transform, "filter": _f_array_filter, "exists": _f_array_exists("exists"),
+    "forall": _f_array_exists("forall"), "aggregate": _f_array_aggregate, "reduce": _f_array_aggregate,
 }
 
 
@@ -1296,3 +1507,6 @@ def output_name(e: A.Expr) -> str:
     if isinstance(e, A.Subscript):
         return output_name(e.index) if e.dot else f"{output_name(e.base)}[{output_name(e.index)}]"
     return type(e).__name__.lower()
+
+
+from . import sqlfuncs as _sqlfuncs  # noqa: E402,F401  (registers the extended built-ins)

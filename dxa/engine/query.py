@@ -48,6 +48,13 @@ class Catalog:
     def names(self):
         return list(self._t)
 
+    def child(self) -> "Catalog":
+        """A scope for WITH: sees every table here; its own registrations stay local."""
+        c = Catalog()
+        c._t = dict(self._t)
+        c._built = self._built
+        return c
+
     def __contains__(self, name):
         return name.lower() in self._t
 
@@ -72,6 +79,19 @@ def _gathered(t: Table) -> Table:
 
 
 def execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
+    if q.ctes:
+        # WITH: each named query sees the catalog plus the CTEs before it
+        catalog = catalog.child()
+        for name, cq in q.ctes:
+            catalog.register(name, execute(cq, catalog, ctx))
+    prev, ctx.catalog = ctx.catalog, catalog
+    try:
+        return _execute(q, catalog, ctx)
+    finally:
+        ctx.catalog = prev
+
+
+def _execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
     out, src_scope = _exec_body(q.body, catalog, ctx, want_scope=bool(q.order_by))
     if (q.order_by or q.limit is not None) and P.active() and P.dist_of(out) != P.REPLICATED:
         # a total order / global LIMIT needs every row: gather (outputs of this shape are small in DataX flows)
@@ -207,7 +227,33 @@ def _relation(src, catalog: Catalog, ctx: EvalContext) -> Scope:
         return sc
     if isinstance(src, A.Join):
         return _join(src, catalog, ctx)
+    if isinstance(src, A.LateralView):
+        from . import generators as GEN
+        if not GEN.is_generator(src.generator):
+            raise QueryError(f"LATERAL VIEW needs a generator function, got {src.generator.name}()")
+        base = _relation(src.source, catalog, ctx)
+        rows, names, cols = GEN.generate(src.generator, base, ctx, src.outer)
+        if src.columns:
+            if len(src.columns) != len(names):
+                raise QueryError(f"LATERAL VIEW {src.generator.name}() produces {len(names)} column(s), "
+                                 f"{len(src.columns)} alias(es) given")
+            names = list(src.columns)
+        out = Scope(base.names + names, _Appended(TakenColumns(base.cols, rows), cols),
+                    base.quals + [src.alias] * len(names), int(rows.shape[0]), base.device)
+        out.dist = getattr(base, "dist", P.REPLICATED)
+        return out
     raise QueryError(f"unsupported FROM item {type(src).__name__}")
+
+
+class _Appended(LazyColumns):
+    """``lazy + tail`` without resolving the lazy part."""
+
+    def __init__(self, lazy, tail):
+        super().__init__([None] * len(lazy) + list(tail))
+        self._lazy = lazy
+
+    def _make(self, i):
+        return self._lazy[i]
 
 
 def _split_and(e: Optional[A.Expr]) -> List[A.Expr]:
@@ -280,8 +326,6 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         li = torch.arange(n_l, device=dev).repeat_interleave(n_r)
         ri = torch.arange(n_r, device=dev).repeat(n_l)
     else:
-        if residual and kind not in ("inner",):
-            raise QueryError("outer joins with non-equi ON conditions are not supported")
         lk = [materialize(evaluate(e, left, ctx)) for e in lkeys]
         rk = [materialize(evaluate(e, right, ctx)) for e in rkeys]
         lk, rk = _coerce_keys(lk, rk)
@@ -291,7 +335,15 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
             # stream–static join: the reference table's hash table is built once and reused every batch
             ck = (static[0], id(static[1]), tuple(e.key() for e in rkeys), tuple(c.dtype for c in rk))
             built = catalog.cached_build(ck, lambda: (static[1], J.build_side(rk)))[1]
-        li, ri = J.hash_join(lk, rk, kind if kind != "cross" else "inner", built)
+        if residual and kind != "inner":
+            # non-equi ON terms of an outer / semi / anti join decide which pairs *match*: filter the equi pairs
+            # first, then add the unmatched rows of the preserved side(s)
+            li, ri = J.hash_join(lk, rk, "inner", built)
+            li, ri = _filter_pairs(left, right, li, ri, residual, ctx)
+            li, ri = _complete_join(li, ri, kind, n_l, n_r, dev)
+            residual = []
+        else:
+            li, ri = J.hash_join(lk, rk, kind if kind != "cross" else "inner", built)
     if kind in ("semi", "anti"):
         out = Scope(left.names, TakenColumns(left.cols, li), left.quals, int(li.shape[0]), dev)
         out.dist = out_dist
@@ -311,6 +363,47 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         out = Scope(out.names, TakenColumns(out.cols, idx), out.quals, int(idx.shape[0]), dev)
     out.dist = out_dist
     return out
+
+
+def _filter_pairs(left: Scope, right: Scope, li, ri, residual, ctx):
+    pairs = Scope(left.names + right.names,
+                  _JoinColumns([(left.cols, i, li, False) for i in range(len(left.cols))] +
+                               [(right.cols, i, ri, False) for i in range(len(right.cols))]),
+                  left.quals + right.quals, int(li.shape[0]), left.device)
+    keep = None
+    for c in residual:
+        m = predicate_mask(evaluate(c, pairs, ctx))
+        keep = m if keep is None else keep & m
+    return li[keep], ri[keep]
+
+
+def _complete_join(li, ri, kind, n_l, n_r, dev):
+    """Matched pairs → the rows of a left / right / full outer, semi or anti join (-1: no partner)."""
+    matched_l = torch.zeros(n_l, dtype=torch.bool, device=dev)
+    if li.numel():
+        matched_l[li] = True
+    if kind in ("semi", "anti"):
+        idx = torch.nonzero(matched_l if kind == "semi" else ~matched_l).flatten()
+        return idx, torch.full_like(idx, -1)
+    parts_l, parts_r = [li], [ri]
+    if kind in ("left", "full"):
+        miss = torch.nonzero(~matched_l).flatten()
+        parts_l.append(miss)
+        parts_r.append(torch.full_like(miss, -1))
+    if kind in ("right", "full"):
+        matched_r = torch.zeros(n_r, dtype=torch.bool, device=dev)
+        if ri.numel():
+            matched_r[ri] = True
+        rmiss = torch.nonzero(~matched_r).flatten()
+        parts_l.append(torch.full_like(rmiss, -1))
+        parts_r.append(rmiss)
+    li, ri = torch.cat(parts_l), torch.cat(parts_r)
+    if kind == "right":
+        order = torch.argsort(ri * (n_l + 1) + torch.where(li >= 0, li, torch.full_like(li, n_l)), stable=True)
+    else:
+        order = torch.argsort(torch.where(li >= 0, li, torch.full_like(li, n_l)) * (n_r + 1) +
+                              torch.where(ri >= 0, ri, torch.full_like(ri, n_r)), stable=True)
+    return li[order], ri[order]
 
 
 def _shuffle_scope(scope: Scope, keys, ref=None) -> Scope:
@@ -563,6 +656,9 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]), scope.device)
         scope.dist = sdist
     items = _expand_items(sel, scope)
+    gen_at = [k for k, (e, _) in enumerate(items) if isinstance(e, A.Call) and e.name in _GENERATOR_NAMES]
+    if gen_at:
+        return _exec_generator_select(sel, items, gen_at, scope, ctx), None
     is_agg = bool(sel.group_by) or any(_contains_agg(e, ctx) for e, _ in items) or (
         sel.having is not None and _contains_agg(sel.having, ctx))
     wcalls = [w for e, _ in items for w in W.window_calls(e)]
@@ -587,6 +683,38 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         out = distinct(out)
         src = None
     return out, (src if want_scope else None)
+
+
+_GENERATOR_NAMES = {"explode", "explode_outer", "posexplode", "posexplode_outer", "inline", "inline_outer",
+                    "stack", "json_tuple"}
+
+
+def _exec_generator_select(sel: A.Select, items, gen_at, scope: Scope, ctx) -> Table:
+    """``SELECT a, explode(arr) AS e FROM …``: the generator's rows replace the input rows; the other items are
+    evaluated over the input rows they came from."""
+    from . import generators as GEN
+    if len(gen_at) > 1:
+        raise QueryError("only one generator is allowed per SELECT clause")
+    if sel.group_by or any(_contains_agg(e, ctx) for e, _ in items):
+        raise QueryError("generators are not supported together with aggregation in one SELECT")
+    k = gen_at[0]
+    call, alias = items[k]
+    rows, names, gcols = GEN.generate(call, scope, ctx)
+    if alias != output_name(call):
+        names = [alias] if len(names) == 1 else names
+    sub = Scope(scope.names, TakenColumns(scope.cols, rows), scope.quals, int(rows.shape[0]), scope.device)
+    sub.dist = getattr(scope, "dist", P.REPLICATED)
+    out_names, out_cols = [], []
+    for j, (e, nm) in enumerate(items):
+        if j == k:
+            out_names += names
+            out_cols += gcols
+        else:
+            out_names.append(nm)
+            out_cols.append(evaluate(e, sub, ctx))
+    out = Table(out_names, out_cols, sub.length, scope.device)
+    out.dist = sub.dist
+    return distinct(out) if sel.distinct else out
 
 
 def _deferred_ref(e: A.Expr, scope: Scope):
@@ -774,6 +902,9 @@ def _eval_agg(call: A.Call, scope: Scope, groups: G.Groups, ctx) -> Column:
         name = "last"
     if name in ("collect_list", "collect_set"):
         return _collect(groups, arg, name == "collect_set")
+    if name in ("percentile", "percentile_approx", "approx_percentile", "median"):
+        p = 0.5 if name == "median" else evaluate(call.args[1], scope, ctx)
+        return _percentile(groups, arg, p, exact=name in ("percentile", "median"))
     if name in ("count_if",):
         m = predicate_mask(arg)
         return G.aggregate(groups, PrimColumn("long", m.to(torch.int64)), "sum", n)
@@ -797,6 +928,53 @@ def _distinct_agg(name, arg, groups: G.Groups, n):
     if name == "count":
         return G.aggregate(owner, vals, "count", int(first_rows.shape[0]))
     return G.aggregate(owner, vals, "sum" if name == "sum" else "avg", int(first_rows.shape[0]))
+
+
+def _percentile(groups: G.Groups, arg, p, exact: bool):
+    """percentile / median (linear interpolation between the two nearest ranks) and percentile_approx (the
+    smallest value whose rank reaches p·count — exact here) per group, from one device sort by (group, value).
+    ``p`` may be a constant or an array of constants (→ array result)."""
+    from .column import ArrayColumn
+    dev = groups.rep.device
+    ng = groups.ngroups
+    if isinstance(p, ArrayColumn):
+        ps = [float(e.value) if isinstance(e, ConstColumn) else float(e.to_pylist()[0]) for e in p.elements]
+        return ArrayColumn([_percentile(groups, arg, ConstColumn(q, "double", 1, dev), exact) for q in ps], ng,
+                           None, False, dev)
+    q = float(p.value if isinstance(p, ConstColumn) else p)
+    if not 0.0 <= q <= 1.0:
+        raise QueryError("percentile must be in [0, 1]")
+    if not isinstance(arg, PrimColumn):
+        arg = cast_column(arg, "double")
+    x = arg.data.to(torch.float64)
+    ok = arg.valid_mask()
+    idx = torch.nonzero(ok).flatten()
+    g = groups.gid.to(torch.int64)[idx]
+    v = x[idx]
+    o = torch.argsort(v, stable=True)
+    o = o[torch.argsort(g[o], stable=True)]
+    g, v = g[o], v[o]
+    cnt = torch.bincount(g, minlength=ng)
+    start = torch.cumsum(cnt, 0) - cnt
+    has = cnt > 0
+    c1 = torch.clamp(cnt - 1, min=0)
+    if exact:
+        pos = q * c1.to(torch.float64)
+        lo = torch.floor(pos).to(torch.int64)
+        hi = torch.clamp(lo + 1, max=c1)
+        fr = pos - lo.to(torch.float64)
+        vl = v[torch.clamp(start + lo, max=max(0, v.numel() - 1))] if v.numel() else torch.zeros(ng, dtype=torch.float64,
+                                                                                                device=dev)
+        vh = v[torch.clamp(start + hi, max=max(0, v.numel() - 1))] if v.numel() else vl
+        r = vl + fr * (vh - vl)
+        return PrimColumn("double", r, has)
+    k = torch.clamp(torch.ceil(q * cnt.to(torch.float64)).to(torch.int64) - 1, min=0)
+    k = torch.minimum(k, c1)
+    r = v[torch.clamp(start + k, max=max(0, v.numel() - 1))] if v.numel() else torch.zeros(ng, dtype=torch.float64,
+                                                                                          device=dev)
+    if arg.dtype in ("int", "long"):
+        return PrimColumn(arg.dtype, r.to(torch.int64), has)
+    return PrimColumn(arg.dtype if arg.dtype in ("double", "float", "decimal") else "double", r, has)
 
 
 def _collect(groups: G.Groups, arg, as_set):

@@ -1,0 +1,850 @@
+"""Spark SQL built-ins beyond the core set in ``expr.py``: math, date formatting / arithmetic, array functions
+(``split`` and friends), hashing / encoding, JSON extraction.
+
+Device-first where it matters for event-rate work: math is tensor arithmetic, ``split`` produces slot views into
+the source arena with two small kernels (strings.hip), ``date_format`` renders fixed-width patterns with one
+kernel and no host synchronisation, ``from_json`` runs the batch JSON parser over the column's bytes.  The
+rarely-hot string digests and encodings are host-assisted (per-row Python), as the engine's other host string
+functions are.
+"""
+from __future__ import annotations
+
+import base64 as _b64
+import datetime as _dt
+import hashlib
+import json
+import math
+import re
+import zlib
+from typing import List, Optional
+
+import torch
+
+from ..sql import ast as A
+from . import functions as F
+from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, column_from_pylist,
+                     materialize, strings_from_pylist)
+from .expr import (EvalError, _args, _host_string_fn, _slot_present, bool_col, cast_column, evaluate,
+                   register_function)
+
+_EPOCH = _dt.datetime(1970, 1, 1)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# math
+# ---------------------------------------------------------------------------------------------------------------
+
+def _num(c: Column, n, dev) -> PrimColumn:
+    c = materialize(c) if isinstance(c, ConstColumn) else c
+    if not isinstance(c, PrimColumn):
+        c = cast_column(c, "double")
+    return c
+
+
+def _and(*valids):
+    out = None
+    for v in valids:
+        if v is not None:
+            out = v if out is None else out & v
+    return out
+
+
+def _binary_double(fn):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        a, b = _args(e, scope, ctx, subst)
+        if isinstance(a, ConstColumn) and isinstance(b, ConstColumn):
+            if a.value is None or b.value is None:
+                return ConstColumn(None, "double", n, dev)
+            r = fn(torch.tensor([float(a.value)], dtype=torch.float64), torch.tensor([float(b.value)],
+                                                                                     dtype=torch.float64))
+            return ConstColumn(float(r[0]), "double", n, dev)
+        a, b = _num(a, n, dev), _num(b, n, dev)
+        return PrimColumn("double", fn(a.data.to(torch.float64), b.data.to(torch.float64)), _and(a.valid, b.valid))
+    return f
+
+
+def _unary_double(fn):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        (a,) = _args(e, scope, ctx, subst)
+        if isinstance(a, ConstColumn):
+            return ConstColumn(None if a.value is None else float(fn(torch.tensor([float(a.value)],
+                                                                                    dtype=torch.float64))[0]),
+                               "double", n, dev)
+        a = _num(a, n, dev)
+        return PrimColumn("double", fn(a.data.to(torch.float64)), a.valid)
+    return f
+
+
+def _f_log(e, scope, ctx, subst):
+    if len(e.args) == 1:
+        return _unary_double(torch.log)(e, scope, ctx, subst)
+    return _binary_double(lambda b, x: torch.log(x) / torch.log(b))(e, scope, ctx, subst)
+
+
+def _f_mod(positive: bool):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        a, b = (_num(c, n, dev) for c in _args(e, scope, ctx, subst))
+        integral = a.dtype in ("int", "long") and b.dtype in ("int", "long")
+        x = a.data if integral else a.data.to(torch.float64)
+        y = b.data if integral else b.data.to(torch.float64)
+        zero = y == 0
+        ys = torch.where(zero, torch.ones_like(y), y)
+        r = torch.fmod(x, ys)                                   # sign of the dividend (Java %)
+        if positive:
+            r = torch.where(r < 0, torch.fmod(r + ys, ys), r)
+        valid = _and(a.valid, b.valid, ~zero)                   # x % 0 is null in Spark
+        return PrimColumn(a.dtype if integral else "double", r, valid)
+    return f
+
+
+def _f_const(v):
+    def f(e, scope, ctx, subst):
+        return ConstColumn(v, "double", scope.length, scope.device)
+    return f
+
+
+def _f_rand(normal: bool):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        g = None
+        if e.args:
+            s = evaluate(e.args[0], scope, ctx, subst)
+            g = torch.Generator(device=dev)
+            g.manual_seed(int(s.value or 0))
+        d = torch.randn(n, dtype=torch.float64, device=dev, generator=g) if normal else \
+            torch.rand(n, dtype=torch.float64, device=dev, generator=g)
+        return PrimColumn("double", d)
+    return f
+
+
+def _f_isnan(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    (a,) = _args(e, scope, ctx, subst)
+    if isinstance(a, ConstColumn):
+        v = a.value
+        return ConstColumn(isinstance(v, float) and math.isnan(v), "boolean", n, dev)
+    a = _num(a, n, dev)
+    return bool_col(torch.isnan(a.data.to(torch.float64)) & a.valid_mask(), None)
+
+
+def _f_nanvl(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    a, b = (_num(c, n, dev) for c in _args(e, scope, ctx, subst))
+    x, y = a.data.to(torch.float64), b.data.to(torch.float64)
+    nan = torch.isnan(x)
+    return PrimColumn("double", torch.where(nan, y, x), torch.where(nan, b.valid_mask(), a.valid_mask())
+                      if (a.valid is not None or b.valid is not None) else None)
+
+
+def _f_cast_to(to):
+    def f(e, scope, ctx, subst):
+        (a,) = _args(e, scope, ctx, subst)
+        return cast_column(a, to)
+    return f
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# dates
+# ---------------------------------------------------------------------------------------------------------------
+
+def _ts(c: Column) -> Column:
+    if c.dtype == "timestamp":
+        return c
+    return cast_column(c, "timestamp")
+
+
+def _days(c: Column) -> Column:
+    """date / timestamp / string → days since epoch (PrimColumn 'date')."""
+    if c.dtype == "date":
+        return c
+    return cast_column(_ts(c), "date")
+
+
+def _f_date_add(sign: int):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        a, k = _args(e, scope, ctx, subst)
+        d = _days(a)
+        if isinstance(d, ConstColumn) and isinstance(k, ConstColumn):
+            return ConstColumn(None if d.value is None or k.value is None else d.value + sign * int(k.value),
+                               "date", n, dev)
+        d, k = materialize(d), _num(k, n, dev)
+        return PrimColumn("date", d.data + sign * k.data.to(torch.int64), _and(d.valid, k.valid))
+    return f
+
+
+def _f_datediff(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    a, b = (materialize(_days(c)) for c in _args(e, scope, ctx, subst))
+    return PrimColumn("int", a.data - b.data, _and(a.valid, b.valid))
+
+
+def _f_add_months(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    a, k = _args(e, scope, ctx, subst)
+    d = materialize(_days(a))
+    k = _num(k, n, dev)
+    y, m, dd = F.civil_from_days(d.data)
+    tot = y * 12 + (m - 1) + k.data.to(torch.int64)
+    ny, nm = F.floor_div(tot, 12), tot % 12 + 1
+    last = _month_len(ny, nm)
+    return PrimColumn("date", F.days_from_civil(ny, nm, torch.minimum(dd, last)), _and(d.valid, k.valid))
+
+
+def _month_len(y, m):
+    nxt_y = torch.where(m == 12, y + 1, y)
+    nxt_m = torch.where(m == 12, torch.ones_like(m), m + 1)
+    return F.days_from_civil(nxt_y, nxt_m, torch.ones_like(m)) - F.days_from_civil(y, m, torch.ones_like(m))
+
+
+def _f_last_day(e, scope, ctx, subst):
+    (a,) = _args(e, scope, ctx, subst)
+    d = materialize(_days(a))
+    y, m, _ = F.civil_from_days(d.data)
+    return PrimColumn("date", F.days_from_civil(y, m, _month_len(y, m)), d.valid)
+
+
+def _f_months_between(e, scope, ctx, subst):
+    args = _args(e, scope, ctx, subst)
+    a, b = (materialize(_ts(c)) for c in args[:2])
+
+    def parts(us):
+        days = F.floor_div(us, F.US_PER_DAY)
+        y, m, d = F.civil_from_days(days)
+        sec = (us - days * F.US_PER_DAY).to(torch.float64) / 1e6
+        return y, m, d, sec, _month_len(y, m)
+    ya, ma, da, sa, la = parts(a.data)
+    yb, mb, db, sb, lb = parts(b.data)
+    months = ((ya - yb) * 12 + (ma - mb)).to(torch.float64)
+    same = (da == db) | ((da == la) & (db == lb))
+    frac = ((da - db).to(torch.float64) * 86400 + (sa - sb)) / (31 * 86400)
+    r = torch.where(same, months, months + frac)
+    r = torch.round(r * 1e8) / 1e8
+    return PrimColumn("double", r, _and(a.valid, b.valid))
+
+
+def _f_weekofyear(e, scope, ctx, subst):
+    (a,) = _args(e, scope, ctx, subst)
+    d = materialize(_days(a))
+    # ISO week: the Thursday of this week decides the year
+    wd = (d.data + 3) % 7                                         # 0 = Monday
+    thu = d.data - wd + 3
+    y, _, _ = F.civil_from_days(thu)
+    jan1 = F.days_from_civil(y, torch.ones_like(y), torch.ones_like(y))
+    return PrimColumn("int", F.floor_div(thu - jan1, 7) + 1, d.valid)
+
+
+def _f_make_date(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    y, m, d = (_num(c, n, dev) for c in _args(e, scope, ctx, subst))
+    yy, mm, ddd = (c.data.to(torch.int64) for c in (y, m, d))
+    ok = (mm >= 1) & (mm <= 12) & (ddd >= 1)
+    mm_s = torch.where(ok, mm, torch.ones_like(mm))
+    ok = ok & (ddd <= _month_len(yy, mm_s))
+    return PrimColumn("date", F.days_from_civil(yy, mm_s, torch.where(ok, ddd, torch.ones_like(ddd))),
+                      _and(y.valid, m.valid, d.valid, ok))
+
+
+_TOKEN = re.compile(r"'([^']|'')*'|([A-Za-z])\2*|.", re.S)
+# fixed-width device codes (strings.hip ts_format_kernel)
+_FIXED = {"yyyy": (1, 4), "yy": (2, 2), "MM": (3, 2), "dd": (4, 2), "HH": (5, 2), "hh": (6, 2), "mm": (7, 2),
+          "ss": (8, 2), "SSS": (9, 3), "SSSSSS": (10, 6), "a": (11, 2), "MMM": (12, 3), "EEE": (13, 3),
+          "DDD": (14, 3)}
+
+
+def _tokens(fmt: str):
+    out = []
+    for m in _TOKEN.finditer(fmt):
+        t = m.group(0)
+        if t.startswith("'"):
+            out.append(("lit", t[1:-1].replace("''", "'") if t != "''" else "'"))
+        elif t[0].isalpha():
+            out.append(("pat", t))
+        else:
+            out.append(("lit", t))
+    return out
+
+
+def compile_pattern(fmt: str):
+    """(ops, literal bytes, width) for a fixed-width Java date pattern, or None (variable-width tokens)."""
+    ops, lits = [], bytearray()
+    width = 0
+    for kind, t in _tokens(fmt):
+        if kind == "lit":
+            b = t.encode("utf-8")
+            if not b:
+                continue
+            if len(b) > 255 or len(lits) + len(b) > 65535:
+                return None
+            ops.append(0 | (len(lits) << 8) | (len(b) << 24))
+            lits += b
+            width += len(b)
+            continue
+        if t not in _FIXED:
+            return None
+        code, w = _FIXED[t]
+        ops.append(code)
+        width += w
+    return ops, bytes(lits), width
+
+
+def _java_format(us: int, fmt: str) -> str:
+    t = _EPOCH + _dt.timedelta(microseconds=us)
+    out = []
+    for kind, tok in _tokens(fmt):
+        if kind == "lit":
+            out.append(tok)
+            continue
+        c, k = tok[0], len(tok)
+        if c == "y":
+            out.append(f"{t.year % 100:02d}" if k == 2 else f"{t.year:0{max(k, 4) if k != 1 else 1}d}")
+        elif c == "M":
+            out.append(t.strftime("%B") if k >= 4 else t.strftime("%b") if k == 3 else f"{t.month:0{k}d}")
+        elif c == "d":
+            out.append(f"{t.day:0{k}d}")
+        elif c == "D":
+            out.append(f"{t.timetuple().tm_yday:0{k}d}")
+        elif c == "H":
+            out.append(f"{t.hour:0{k}d}")
+        elif c == "h":
+            out.append(f"{(t.hour % 12) or 12:0{k}d}")
+        elif c == "m":
+            out.append(f"{t.minute:0{k}d}")
+        elif c == "s":
+            out.append(f"{t.second:0{k}d}")
+        elif c == "S":
+            out.append(f"{t.microsecond:06d}"[:k].ljust(k, "0"))
+        elif c == "a":
+            out.append("AM" if t.hour < 12 else "PM")
+        elif c == "E":
+            out.append(t.strftime("%A") if k >= 4 else t.strftime("%a"))
+        elif c in "XxZ":
+            out.append("Z" if c == "X" else "+0000")
+        elif c == "z":
+            out.append("UTC")
+        else:
+            raise EvalError(f"unsupported date pattern letter {c!r}")
+    return "".join(out)
+
+
+def format_timestamps(ts: Column, fmt: str) -> Column:
+    """Timestamp column → strings in a Java ``SimpleDateFormat`` pattern (UTC)."""
+    n, dev = ts.length, ts.device
+    if isinstance(ts, ConstColumn):
+        return ConstColumn(None if ts.value is None else _java_format(int(ts.value), fmt), "string", n, dev)
+    comp = compile_pattern(fmt) if dev.type == "cuda" else None
+    if comp is not None and n:
+        from ..ops import native as N
+        ops, lits, width = comp
+        opt = torch.tensor(ops or [0], dtype=torch.int32).to(dev, non_blocking=True)
+        lt = torch.frombuffer(bytearray(lits + b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+        arena = torch.empty(n * width + 16, dtype=torch.uint8, device=dev)
+        arena[n * width:].zero_()
+        data = ts.data.to(torch.int64).contiguous()
+        N.call("dxa_ts_format", N.ptr(data), n, N.ptr(opt), len(ops), N.ptr(lt), width, N.ptr(arena),
+               N.stream_handle(dev))
+        starts = torch.arange(n, dtype=torch.int64, device=dev) * width
+        col = StrColumn(arena, starts, torch.full((n,), width, dtype=torch.int32, device=dev), ts.valid)
+        col._keep = (opt, lt)
+        return col
+    vals = ts.data.cpu().tolist()
+    ok = ts.valid.cpu().tolist() if ts.valid is not None else [True] * n
+    return strings_from_pylist([_java_format(int(v), fmt) if k else None for v, k in zip(vals, ok)], dev)
+
+
+def _fmt_arg(e, scope, ctx, subst, k, default):
+    if len(e.args) <= k:
+        return default
+    f = evaluate(e.args[k], scope, ctx, subst)
+    if not isinstance(f, ConstColumn):
+        raise EvalError("date pattern must be a constant")
+    return str(f.value)
+
+
+def _f_date_format(e, scope, ctx, subst):
+    a = evaluate(e.args[0], scope, ctx, subst)
+    return format_timestamps(_ts(a) if a.dtype != "date" else cast_column(a, "timestamp"),
+                             _fmt_arg(e, scope, ctx, subst, 1, "yyyy-MM-dd HH:mm:ss"))
+
+
+def _f_from_unixtime(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    a = _num(evaluate(e.args[0], scope, ctx, subst), n, dev)
+    sec = a.data.to(torch.int64) if a.data.dtype != torch.float64 else a.data.floor().to(torch.int64)
+    return format_timestamps(PrimColumn("timestamp", sec * 1_000_000, a.valid),
+                             _fmt_arg(e, scope, ctx, subst, 1, "yyyy-MM-dd HH:mm:ss"))
+
+
+def _tz_shift(to_utc: bool):
+    """to_utc_timestamp(ts, tz): ts is wall-clock time in tz → UTC.  from_utc_timestamp(ts, tz): UTC → wall clock
+    in tz.  Host-assisted (zone rules from the system tz database)."""
+    def f(e, scope, ctx, subst):
+        a = materialize(_ts(evaluate(e.args[0], scope, ctx, subst)))
+        tz = _fmt_arg(e, scope, ctx, subst, 1, "UTC")
+        from zoneinfo import ZoneInfo
+        z = ZoneInfo(tz)
+        out = []
+        for v in a.data.cpu().tolist():
+            t = _EPOCH + _dt.timedelta(microseconds=int(v))
+            if to_utc:
+                off = t.replace(tzinfo=z).utcoffset()
+            else:
+                off = t.replace(tzinfo=_dt.timezone.utc).astimezone(z).utcoffset()
+            us = int(off.total_seconds() * 1_000_000) if off is not None else 0
+            out.append(int(v) - us if to_utc else int(v) + us)
+        return PrimColumn("timestamp", torch.tensor(out, dtype=torch.int64, device=a.device), a.valid)
+    return f
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# arrays
+# ---------------------------------------------------------------------------------------------------------------
+
+_META = set(".$|()[]{}^?*+\\")
+
+
+def _literal_delim(pat: str) -> Optional[bytes]:
+    """A regex that only matches one fixed string (``','``, ``'\\|'``, ``'::'``) → that string."""
+    out, i = [], 0
+    while i < len(pat):
+        c = pat[i]
+        if c == "\\" and i + 1 < len(pat) and not pat[i + 1].isalnum():
+            out.append(pat[i + 1])
+            i += 2
+            continue
+        if c in _META:
+            return None
+        out.append(c)
+        i += 1
+    s = "".join(out)
+    return s.encode("utf-8") if s else None
+
+
+def array_from_pylist(lists, elem_type, device) -> ArrayColumn:
+    n = len(lists)
+    k = max((len(l) for l in lists if l is not None), default=0)
+    els = [column_from_pylist([l[j] if l is not None and j < len(l) else None for l in lists], elem_type, device)
+           for j in range(max(k, 1))]
+    valid = None if all(l is not None for l in lists) else torch.tensor([l is not None for l in lists],
+                                                                       dtype=torch.bool, device=device)
+    return ArrayColumn(els, n, valid, True, device)
+
+
+def split_strings(col: Column, pattern: str, limit: int = -1) -> ArrayColumn:
+    n, dev = col.length, col.device
+    if not isinstance(col, StrColumn):
+        col = cast_column(col, "string")
+    if isinstance(col, ConstColumn):
+        col = materialize(col)
+    d = _literal_delim(pattern)
+    if col.starts.is_cuda and d is not None and limit <= 0 and n:
+        from ..ops import native as N
+        st = N.stream_handle(dev)
+        dt = torch.frombuffer(bytearray(d), dtype=torch.uint8).to(dev, non_blocking=True)
+        cnt = torch.empty(n, dtype=torch.int32, device=dev)
+        N.call("dxa_str_split_count", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(dt), len(d),
+               N.ptr(cnt), st)
+        K = int(cnt.max().item())                                       # slot count: the one host read
+        ostarts = torch.empty((K, n), dtype=torch.int64, device=dev)
+        olens = torch.empty((K, n), dtype=torch.int32, device=dev)
+        N.call("dxa_str_split_write", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(dt), len(d),
+               K, N.ptr(ostarts), N.ptr(olens), st)
+        row_ok = col.valid
+        els = []
+        for j in range(K):
+            present = olens[j] >= 0
+            v = present if row_ok is None else (present & row_ok)
+            els.append(StrColumn(col.arena, ostarts[j], torch.clamp(olens[j], min=0), v))
+        out = ArrayColumn(els, n, row_ok, True, dev)
+        out._keep = dt
+        return out
+    rx = re.compile(pattern)
+    vals = col.to_pylist()
+    lists = []
+    for v in vals:
+        if v is None:
+            lists.append(None)
+            continue
+        parts = rx.split(v, maxsplit=max(0, limit - 1)) if limit > 0 else rx.split(v)
+        lists.append(parts)
+    return array_from_pylist(lists, "string", dev)
+
+
+def _f_split(e, scope, ctx, subst):
+    a = evaluate(e.args[0], scope, ctx, subst)
+    p = evaluate(e.args[1], scope, ctx, subst)
+    lim = int(evaluate(e.args[2], scope, ctx, subst).value) if len(e.args) > 2 else -1
+    if not isinstance(p, ConstColumn):
+        raise EvalError("split() pattern must be a constant")
+    if isinstance(a, ConstColumn):
+        a = a.materialize()
+    return split_strings(a, str(p.value), lim)
+
+
+def _f_array_contains(e, scope, ctx, subst):
+    from .expr import _compare
+    n, dev = scope.length, scope.device
+    arr, v = _args(e, scope, ctx, subst)
+    if not isinstance(arr, ArrayColumn):
+        raise EvalError("array_contains() expects an array")
+    acc = torch.zeros(n, dtype=torch.bool, device=dev)
+    for el in arr.elements:
+        eq = _compare("=", el, v, n, dev)
+        acc = acc | (eq.data.bool() & eq.valid_mask() & _slot_present(arr, el))
+    return bool_col(acc, arr.valid)
+
+
+def _host_array_fn(fn, elem_type_of=None, scalar_type=None):
+    """Array function evaluated per row on the host: fn(list, *args) → list (array result) or value."""
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        args = _args(e, scope, ctx, subst)
+        arr = args[0]
+        if not isinstance(arr, ArrayColumn):
+            raise EvalError(f"{e.name}() expects an array")
+        lists = arr.to_pylist()
+        extra = [a.to_pylist() if not isinstance(a, ConstColumn) else [a.value] * n for a in args[1:]]
+        out = [None if l is None else fn(l, *[x[i] for x in extra]) for i, l in enumerate(lists)]
+        et = str(arr.elements[0].dtype) if arr.elements else "string"
+        if scalar_type is not None:
+            return column_from_pylist(out, scalar_type if scalar_type != "elem" else et, dev)
+        return array_from_pylist(out, elem_type_of or et, dev)
+    return f
+
+
+def _f_slice(l, start, length):
+    start, length = int(start), int(length)
+    s = start - 1 if start > 0 else len(l) + start
+    return l[max(0, s):max(0, s) + max(0, length)]
+
+
+def _f_sequence(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    args = _args(e, scope, ctx, subst)
+    cols = [a.to_pylist() if not isinstance(a, ConstColumn) else [a.value] * n for a in args]
+    out = []
+    for i in range(n):
+        a, b = cols[0][i], cols[1][i]
+        st = cols[2][i] if len(cols) > 2 else (1 if b >= a else -1)
+        out.append(None if a is None or b is None else list(range(int(a), int(b) + (1 if st > 0 else -1), int(st))))
+    return array_from_pylist(out, "long", dev)
+
+
+def _f_map_part(which):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        (m,) = _args(e, scope, ctx, subst)
+        if not (isinstance(m, StructColumn) and m.is_map):
+            raise EvalError(f"{e.name}() expects a map")
+        if which == "keys":
+            els = [ConstColumn(k, "string", n, dev).materialize().with_valid(c.valid_mask() if c.valid is not None
+                                                                          else None)
+                   for k, c in zip(m.names, m.children)]
+            return ArrayColumn(els, n, m.valid, True, dev)
+        return ArrayColumn(list(m.children), n, m.valid, True, dev)
+    return f
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# hashing / encoding
+# ---------------------------------------------------------------------------------------------------------------
+
+def _sha2(s, bits=256):
+    bits = int(bits)
+    h = {224: hashlib.sha224, 256: hashlib.sha256, 0: hashlib.sha256, 384: hashlib.sha384,
+         512: hashlib.sha512}.get(bits)
+    return None if h is None else h(str(s).encode()).hexdigest()
+
+
+def _hex(v):
+    if isinstance(v, (int, bool)) and not isinstance(v, bool):
+        return format(v & 0xFFFFFFFFFFFFFFFF, "X") if v < 0 else format(v, "X")
+    return str(v).encode().hex().upper()
+
+
+def _initcap(s):
+    return " ".join(w[:1].upper() + w[1:].lower() for w in str(s).split(" "))
+
+
+def _translate(s, frm, to):
+    s, frm, to = str(s), str(frm), str(to)
+    table = {}
+    for i, c in enumerate(frm):
+        if c not in table:
+            table[c] = to[i] if i < len(to) else None
+    return "".join(table.get(c, c) or "" if c in table else c for c in s)
+
+
+# Spark's hash(): Murmur3_x86_32, seed 42 chained through the arguments (HashExpression / Murmur3Hash), with its
+# byte-at-a-time tail for strings (Murmur3_x86_32.hashUnsafeBytes).
+_M32 = 0xFFFFFFFF
+
+
+def _rotl(x, r):
+    return ((x << r) | (x >> (32 - r))) & _M32
+
+
+def _mix_k1(k1):
+    k1 = (k1 * 0xCC9E2D51) & _M32
+    return (_rotl(k1, 15) * 0x1B873593) & _M32
+
+
+def _mix_h1(h1, k1):
+    h1 ^= k1
+    return (_rotl(h1, 13) * 5 + 0xE6546B64) & _M32
+
+
+def _fmix(h1, length):
+    h1 ^= length
+    h1 ^= h1 >> 16
+    h1 = (h1 * 0x85EBCA6B) & _M32
+    h1 ^= h1 >> 13
+    h1 = (h1 * 0xC2B2AE35) & _M32
+    return h1 ^ (h1 >> 16)
+
+
+def _hash_int(v, seed):
+    return _fmix(_mix_h1(seed, _mix_k1(v & _M32)), 4)
+
+
+def _hash_long(v, seed):
+    v &= 0xFFFFFFFFFFFFFFFF
+    h1 = _mix_h1(seed, _mix_k1(v & _M32))
+    return _fmix(_mix_h1(h1, _mix_k1(v >> 32)), 8)
+
+
+def _hash_bytes(b: bytes, seed):
+    h1 = seed
+    aligned = len(b) - len(b) % 4
+    for i in range(0, aligned, 4):
+        h1 = _mix_h1(h1, _mix_k1(int.from_bytes(b[i:i + 4], "little")))
+    for i in range(aligned, len(b)):
+        x = b[i] - 256 if b[i] >= 128 else b[i]                     # Java byte: signed
+        h1 = _mix_h1(h1, _mix_k1(x & _M32))
+    return _fmix(h1, len(b))
+
+
+def spark_hash_value(v, dtype, seed):
+    if v is None:
+        return seed
+    if dtype in ("int", "date") or isinstance(v, bool):
+        return _hash_int(int(v), seed)
+    if dtype in ("long", "timestamp"):
+        return _hash_long(int(v), seed)
+    if dtype in ("double", "float", "decimal"):
+        import struct
+        d = 0.0 if v == 0 else float(v)                                   # -0.0 hashes as 0.0
+        return _hash_long(struct.unpack("<q", struct.pack("<d", d))[0], seed)
+    if isinstance(v, (dict, list)):
+        v = json.dumps(v, separators=(",", ":"))
+    return _hash_bytes(str(v).encode("utf-8"), seed)
+
+
+def _f_hash(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    args = _args(e, scope, ctx, subst)
+    from .column import ts_to_datetime  # noqa: F401  (storage values below, not datetimes)
+    cols = []
+    for a in args:
+        if isinstance(a, ConstColumn):
+            cols.append(([a.value] * n, str(a.dtype)))
+        elif isinstance(a, PrimColumn):
+            vals = a.data.cpu().tolist()
+            ok = a.valid.cpu().tolist() if a.valid is not None else None
+            cols.append(([v if (ok is None or ok[i]) else None for i, v in enumerate(vals)], str(a.dtype)))
+        else:
+            cols.append((a.to_pylist(), str(a.dtype)))
+    out = []
+    for i in range(n):
+        h = 42
+        for vals, dt in cols:
+            h = spark_hash_value(vals[i], dt, h)
+        out.append(h - (1 << 32) if h >= (1 << 31) else h)
+    return column_from_pylist(out, "int", dev)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# JSON
+# ---------------------------------------------------------------------------------------------------------------
+
+_PATH = re.compile(r"\.([^.\[]+)|\[(\d+)\]|\['([^']+)'\]")
+
+
+def _json_path(doc, path: str):
+    if not path.startswith("$"):
+        return None
+    cur = doc
+    for m in _PATH.finditer(path[1:]):
+        key = m.group(1) or m.group(3)
+        if key is not None:
+            if key == "*" or not isinstance(cur, dict) or key not in cur:
+                return None
+            cur = cur[key]
+        else:
+            i = int(m.group(2))
+            if not isinstance(cur, list) or i >= len(cur):
+                return None
+            cur = cur[i]
+    return cur
+
+
+def _get_json_object(s, path):
+    try:
+        v = _json_path(json.loads(s), str(path))
+    except (ValueError, TypeError):
+        return None
+    if v is None:
+        return None
+    if isinstance(v, str):
+        return v
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return json.dumps(v, separators=(",", ":"))
+
+
+def _f_from_json(e, scope, ctx, subst):
+    """from_json(str, schema): the batch JSON parser (device kernel on the GPU) over a private copy of the column's
+    bytes (the parser un-escapes in place)."""
+    from ..ops.jsonparse import ParsePlan, parse
+    from .types import StructType, parse_ddl_schema, schema_from_json
+    n, dev = scope.length, scope.device
+    a = evaluate(e.args[0], scope, ctx, subst)
+    sch = evaluate(e.args[1], scope, ctx, subst)
+    if not isinstance(sch, ConstColumn):
+        raise EvalError("from_json() schema must be a constant")
+    text = str(sch.value).strip()
+    schema = schema_from_json(text) if text.startswith("{") else parse_ddl_schema(text)
+    if not isinstance(schema, StructType):
+        raise EvalError("from_json() supports struct schemas")
+    if isinstance(a, ConstColumn):
+        a = a.materialize()
+    if not isinstance(a, StrColumn):
+        a = cast_column(a, "string")
+    c = a.compact()
+    plan = ParsePlan(schema)
+    ends = c.starts + c.lens.to(torch.int64)
+    offs = torch.cat([c.starts, ends[-1:] if n else torch.zeros(1, dtype=torch.int64, device=dev)])
+    raw, ok = parse(c.arena, offs, plan, ends)
+    valid = ok if a.valid is None else (ok & a.valid)
+    out = raw.with_valid(valid)
+    out._keep = c
+    return out
+
+
+# ---------------------------------------------------------------------------------------------------------------
+
+def _f_window(e, scope, ctx, subst):
+    """window(ts, 'duration'[, 'slide'[, 'start offset']]) → struct<start, end> of the tumbling window holding ts
+    (Spark's event-time window function).  Sliding windows (slide < duration) assign a row to several windows;
+    DataX flows express those with TIMEWINDOW, which this engine evaluates incrementally."""
+    from ..sql.parser import parse_duration_micros
+    n, dev = scope.length, scope.device
+    a = materialize(_ts(evaluate(e.args[0], scope, ctx, subst)))
+
+    def dur(k, default=None):
+        if len(e.args) <= k:
+            return default
+        c = evaluate(e.args[k], scope, ctx, subst)
+        if not isinstance(c, ConstColumn):
+            raise EvalError("window() durations must be constants")
+        return c.value if isinstance(c.value, int) and c.dtype == "interval" else parse_duration_micros(str(c.value))
+    size = dur(1)
+    slide = dur(2, size)
+    off = dur(3, 0)
+    if not size or size <= 0:
+        raise EvalError("window() duration must be positive")
+    if slide != size:
+        raise EvalError("sliding window() (slide < duration) is not supported; use FROM t TIMEWINDOW('…')")
+    start = F.floor_div(a.data - off, size) * size + off
+    return StructColumn(["start", "end"], [PrimColumn("timestamp", start, a.valid),
+                                           PrimColumn("timestamp", start + size, a.valid)], n, a.valid, False, None,
+                        dev)
+
+
+def _register():
+    reg = register_function
+    reg("pow", _binary_double(torch.pow))
+    reg("power", _binary_double(torch.pow))
+    reg("atan2", _binary_double(torch.atan2))
+    reg("hypot", _binary_double(torch.hypot))
+    reg("log", _f_log)
+    reg("log1p", _unary_double(torch.log1p))
+    reg("expm1", _unary_double(torch.expm1))
+    reg("cbrt", _unary_double(lambda x: torch.sign(x) * torch.abs(x).pow(1.0 / 3.0)))
+    reg("degrees", _unary_double(torch.rad2deg))
+    reg("radians", _unary_double(torch.deg2rad))
+    for nm in ("sin", "cos", "tan", "asin", "acos", "atan", "sinh", "cosh", "tanh"):
+        reg(nm, _unary_double(getattr(torch, nm)))
+    reg("cot", _unary_double(lambda x: 1.0 / torch.tan(x)))
+    reg("mod", _f_mod(False))
+    reg("pmod", _f_mod(True))
+    reg("e", _f_const(math.e))
+    reg("pi", _f_const(math.pi))
+    reg("rand", _f_rand(False))
+    reg("random", _f_rand(False))
+    reg("randn", _f_rand(True))
+    reg("isnan", _f_isnan)
+    reg("nanvl", _f_nanvl)
+    reg("factorial", _host_string_fn(lambda x: math.factorial(int(x)) if 0 <= int(x) <= 20 else None, "long"))
+    reg("bin", _host_string_fn(lambda x: format(int(x) & 0xFFFFFFFFFFFFFFFF, "b") if int(x) < 0
+                               else format(int(x), "b")))
+    for nm, to in (("string", "string"), ("int", "int"), ("integer", "int"), ("bigint", "long"), ("long", "long"),
+                   ("double", "double"), ("float", "double"), ("boolean", "boolean"), ("date", "date"),
+                   ("timestamp", "timestamp")):
+        reg(nm, _f_cast_to(to))
+    reg("date_add", _f_date_add(1))
+    reg("dateadd", _f_date_add(1))
+    reg("date_sub", _f_date_add(-1))
+    reg("datediff", _f_datediff)
+    reg("add_months", _f_add_months)
+    reg("last_day", _f_last_day)
+    reg("months_between", _f_months_between)
+    reg("weekofyear", _f_weekofyear)
+    reg("make_date", _f_make_date)
+    reg("date_format", _f_date_format)
+    reg("from_unixtime", _f_from_unixtime)
+    reg("to_utc_timestamp", _tz_shift(True))
+    reg("from_utc_timestamp", _tz_shift(False))
+    reg("split", _f_split)
+    reg("array_contains", _f_array_contains)
+    reg("array_join", _host_array_fn(lambda l, sep, nr=None: str(sep).join(
+        str(x) if x is not None else str(nr) for x in l if x is not None or nr is not None), scalar_type="string"))
+    reg("array_max", _host_array_fn(lambda l: max((x for x in l if x is not None), default=None),
+                                    scalar_type="elem"))
+    reg("array_min", _host_array_fn(lambda l: min((x for x in l if x is not None), default=None),
+                                    scalar_type="elem"))
+    reg("sort_array", _host_array_fn(lambda l, asc=True: sorted(
+        l, key=lambda x: (x is not None, x) if bool(asc) else (x is None, x), reverse=not bool(asc))))
+    reg("array_sort", _host_array_fn(lambda l: sorted((x for x in l if x is not None)) + [x for x in l if x is None]))
+    reg("array_distinct", _host_array_fn(lambda l: list(dict.fromkeys(l))))
+    reg("array_position", _host_array_fn(lambda l, v: next((i + 1 for i, x in enumerate(l) if x == v), 0),
+                                         scalar_type="long"))
+    reg("array_remove", _host_array_fn(lambda l, v: [x for x in l if x != v]))
+    reg("slice", _host_array_fn(_f_slice))
+    reg("sequence", _f_sequence)
+    reg("map_keys", _f_map_part("keys"))
+    reg("map_values", _f_map_part("values"))
+    reg("sha2", _host_string_fn(_sha2))
+    reg("sha", _host_string_fn(lambda s: hashlib.sha1(str(s).encode()).hexdigest()))
+    reg("crc32", _host_string_fn(lambda s: zlib.crc32(str(s).encode()) & 0xFFFFFFFF, "long"))
+    reg("base64", _host_string_fn(lambda s: _b64.b64encode(str(s).encode()).decode()))
+    reg("unbase64", _host_string_fn(lambda s: _b64.b64decode(str(s)).decode("utf-8", errors="replace")))
+    reg("hex", _host_string_fn(_hex))
+    reg("unhex", _host_string_fn(lambda s: bytes.fromhex(str(s)).decode("utf-8", errors="replace")))
+    reg("initcap", _host_string_fn(_initcap))
+    reg("repeat", _host_string_fn(lambda s, k: str(s) * max(0, int(k))))
+    reg("left", _host_string_fn(lambda s, k: str(s)[:max(0, int(k))]))
+    reg("right", _host_string_fn(lambda s, k: str(s)[-int(k):] if int(k) > 0 else ""))
+    reg("translate", _host_string_fn(_translate))
+    reg("ascii", _host_string_fn(lambda s: ord(str(s)[0]) if str(s) else 0, "int"))
+    reg("get_json_object", _host_string_fn(_get_json_object))
+    reg("from_json", _f_from_json)
+    reg("hash", _f_hash)
+    reg("window", _f_window)
+    reg("tumble", _f_window)
+
+
+_register()

@@ -465,6 +465,154 @@ DXA_API int dxa_str_gather(const uint8_t* arena, const int64_t* starts, const in
   return (int)hipGetLastError();
 }
 
+// split(str, literal delimiter) → K slot views into the same arena (no bytes move).  Pass 1 counts each row's
+// parts (delimiters + 1; Spark keeps empty and trailing-empty parts), pass 2 writes slot j's start / length for
+// j < count and length -1 (absent) for the rest.  One lane per row: strings in DataX events are short.
+__device__ __forceinline__ bool delim_at(const uint8_t* p, const uint8_t* d, int32_t dl) {
+  for (int32_t k = 0; k < dl; ++k)
+    if (p[k] != d[k]) return false;
+  return true;
+}
+
+__global__ void str_split_count_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                       const int32_t* __restrict__ lens, int64_t n, const uint8_t* __restrict__ d,
+                                       int32_t dl, int32_t* __restrict__ count) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    int32_t c = 1;
+    for (int32_t k = 0; k + dl <= l;) {
+      if (delim_at(s + k, d, dl)) { ++c; k += dl; } else { ++k; }
+    }
+    count[i] = c;
+  }
+}
+
+__global__ void str_split_write_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                       const int32_t* __restrict__ lens, int64_t n, const uint8_t* __restrict__ d,
+                                       int32_t dl, int32_t K, int64_t* __restrict__ out_starts,
+                                       int32_t* __restrict__ out_lens) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s0 = starts[i];
+    const uint8_t* s = arena + s0;
+    const int32_t l = lens[i];
+    int32_t j = 0, b = 0;
+    for (int32_t k = 0; k + dl <= l && j < K;) {
+      if (delim_at(s + k, d, dl)) {
+        out_starts[(int64_t)j * n + i] = s0 + b;
+        out_lens[(int64_t)j * n + i] = k - b;
+        ++j;
+        k += dl;
+        b = k;
+      } else {
+        ++k;
+      }
+    }
+    if (j < K) {
+      out_starts[(int64_t)j * n + i] = s0 + b;
+      out_lens[(int64_t)j * n + i] = l - b;
+      ++j;
+    }
+    for (; j < K; ++j) {
+      out_starts[(int64_t)j * n + i] = s0;
+      out_lens[(int64_t)j * n + i] = -1;
+    }
+  }
+}
+
+DXA_API int dxa_str_split_count(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                                const uint8_t* d, int32_t dl, int32_t* count, void* st) {
+  if (n <= 0) return 0;
+  if (dl <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(str_split_count_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
+                     lens, n, d, dl, count);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_split_write(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                                const uint8_t* d, int32_t dl, int32_t K, int64_t* out_starts, int32_t* out_lens,
+                                void* st) {
+  if (n <= 0 || K <= 0) return 0;
+  if (dl <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(str_split_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
+                     lens, n, d, dl, K, out_starts, out_lens);
+  return (int)hipGetLastError();
+}
+
+// date_format(ts, pattern) for fixed-width patterns: every row renders to exactly L bytes, so the output arena is
+// n*L with no length pass and no host synchronisation.  Ops (int32): low byte = field code, bits 8.. = argument
+// (literal: offset << 8 | len << 24 into `lits`).  Codes: 0 literal, 1 yyyy, 2 yy, 3 MM, 4 dd, 5 HH, 6 hh, 7 mm,
+// 8 ss, 9 SSS, 10 SSSSSS, 11 a (AM/PM), 12 MMM (Jan…), 13 EEE (Mon…), 14 D (day of year, 3 digits: DDD).
+__device__ __forceinline__ void put_num(uint8_t* o, int64_t v, int w) {
+  for (int k = w - 1; k >= 0; --k) {
+    o[k] = (uint8_t)('0' + (v % 10));
+    v /= 10;
+  }
+}
+
+__global__ void ts_format_kernel(const int64_t* __restrict__ us, int64_t n, const int32_t* __restrict__ ops,
+                                 int32_t nops, const uint8_t* __restrict__ lits, int32_t L, uint8_t* __restrict__ out) {
+  const char* mon = "JanFebMarAprMayJunJulAugSepOctNovDec";
+  const char* dow = "MonTueWedThuFriSatSun";
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = us[i];
+    int64_t days = t >= 0 ? t / 86400000000ll : -((-t + 86400000000ll - 1) / 86400000000ll);
+    const int64_t rem = t - days * 86400000000ll;                    // [0, 1 day) in µs
+    const int64_t hh = rem / 3600000000ll, mi = (rem / 60000000ll) % 60, ss = (rem / 1000000ll) % 60;
+    const int64_t frac = rem % 1000000ll;
+    const int64_t wd = ((days % 7) + 7 + 3) % 7;                     // 0 = Monday (1970-01-01 was a Thursday)
+    // civil from days (Hinnant)
+    const int64_t z = days + 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const int64_t doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    int64_t y = yoe + era * 400;
+    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy + 2) / 153;
+    const int64_t d = doy - (153 * mp + 2) / 5 + 1;
+    const int64_t m = mp < 10 ? mp + 3 : mp - 9;
+    if (m <= 2) ++y;
+    const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+    const int cum[12] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334};
+    const int64_t yday = cum[m - 1] + d + (leap && m > 2 ? 1 : 0);
+    uint8_t* o = out + i * L;
+    for (int32_t k = 0; k < nops; ++k) {
+      const int32_t op = ops[k], code = op & 0xff;
+      switch (code) {
+        case 0: {
+          const int32_t off = (op >> 8) & 0xffff, len = (op >> 24) & 0xff;
+          for (int32_t b = 0; b < len; ++b) o[b] = lits[off + b];
+          o += len;
+          break;
+        }
+        case 1: put_num(o, y < 0 ? 0 : y, 4); o += 4; break;
+        case 2: put_num(o, (y % 100 + 100) % 100, 2); o += 2; break;
+        case 3: put_num(o, m, 2); o += 2; break;
+        case 4: put_num(o, d, 2); o += 2; break;
+        case 5: put_num(o, hh, 2); o += 2; break;
+        case 6: put_num(o, (hh % 12) == 0 ? 12 : hh % 12, 2); o += 2; break;
+        case 7: put_num(o, mi, 2); o += 2; break;
+        case 8: put_num(o, ss, 2); o += 2; break;
+        case 9: put_num(o, frac / 1000, 3); o += 3; break;
+        case 10: put_num(o, frac, 6); o += 6; break;
+        case 11: o[0] = hh < 12 ? 'A' : 'P'; o[1] = 'M'; o += 2; break;
+        case 12: for (int b = 0; b < 3; ++b) o[b] = (uint8_t)mon[(m - 1) * 3 + b]; o += 3; break;
+        case 13: for (int b = 0; b < 3; ++b) o[b] = (uint8_t)dow[wd * 3 + b]; o += 3; break;
+        case 14: put_num(o, yday, 3); o += 3; break;
+        default: break;
+      }
+    }
+  }
+}
+
+DXA_API int dxa_ts_format(const int64_t* us, int64_t n, const int32_t* ops, int32_t nops, const uint8_t* lits,
+                          int32_t L, uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(ts_format_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, us, n, ops, nops,
+                     lits, L, out);
+  return (int)hipGetLastError();
+}
+
 // parts: host array of k StrPart descriptors (row0 relative to the first part); launches in groups of kMaxStrParts.
 DXA_API int dxa_str_gather_parts(const void* parts, int32_t k, void* st) {
   const StrPart* ps = (const StrPart*)parts;

@@ -127,6 +127,14 @@ class ParsePlan:
             else:
                 self.nodes.append(Node(path, parent, f.name, f.dtype, FT.get(f.dtype, FT["string"])))
 
+    def string_val_slots(self, device) -> Optional[torch.Tensor]:
+        """Value-slot rows holding string starts (string and raw-JSON fields), as a device index tensor."""
+        key = ("sslots", str(device))
+        if key not in self._dev:
+            sl = sorted({nd.val_slot for nd in self.nodes[1:] if nd.code in (4, 5)})
+            self._dev[key] = torch.tensor(sl, dtype=torch.int64, device=device) if sl else None
+        return self._dev[key]
+
     def device_tables(self, device):
         key = str(device)
         t = self._dev.get(key)
@@ -272,9 +280,14 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
     lut_k, lut_n, types, vslot, lslot, fchild, nsib, kword, klen, kwords = plan.device_tables(buf.device)
     nn = len(plan.nodes)
     vals = torch.empty((max(1, plan.nval), max(n, 1)), dtype=torch.int64, device=buf.device)
-    lens = torch.empty((max(1, plan.nlen), max(n, 1)), dtype=torch.int32, device=buf.device)
+    # string lengths start at 0: the kernel writes only present fields, and a null string must still be a valid
+    # (empty) view for the kernels that copy / hash / split every row of a column without looking at validity
+    lens = torch.zeros((max(1, plan.nlen), max(n, 1)), dtype=torch.int32, device=buf.device)
     valid = torch.empty((nn, max(n, 1)), dtype=torch.uint8, device=buf.device)
     row_ok = torch.empty(max(n, 1), dtype=torch.uint8, device=buf.device)
+    sslots = plan.string_val_slots(buf.device)
+    if sslots is not None:
+        vals.index_fill_(0, sslots, 0)            # null strings: start 0 (with length 0), never a wild address
     counts = event = None
     if n:
         st = N.stream_handle(buf.device)

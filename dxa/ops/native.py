@@ -60,6 +60,9 @@ _SIGS = {
     "dxa_str_cmp_col": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p],
     "dxa_str_gather": [c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
     "dxa_str_gather_parts": [c_p, c_i32, c_p],
+    "dxa_str_split_count": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_p, c_p],
+    "dxa_ts_format": [c_p, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p],
+    "dxa_str_split_write": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p],
     "dxa_str_part_size": [],
     "dxa_concat_len": [c_p, c_i32, c_i64, c_p, c_p, c_p],
     "dxa_concat_write": [c_p, c_i32, c_i64, c_p, c_p, c_p, c_p],

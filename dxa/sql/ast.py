@@ -275,6 +275,47 @@ class Query:
     body: Any          # Select | SetOp
     order_by: List[OrderItem] = field(default_factory=list)
     limit: Optional[int] = None
+    ctes: List[Tuple[str, "Query"]] = field(default_factory=list)     # WITH name AS (query), …
+
+
+@dataclass(eq=False)
+class SubqueryExpr(Expr):
+    """``(SELECT …)`` as a value (kind ``scalar``), ``EXISTS (SELECT …)`` (``exists``) or ``x [NOT] IN (SELECT …)``
+    (``in``, with ``operand`` = x).  Uncorrelated: the sub-query is planned on its own."""
+    kind: str
+    query: Query
+    operand: Optional[Expr] = None
+    negated: bool = False
+
+    def key(self):
+        return ("subq", self.kind, id(self.query), self.negated,
+                None if self.operand is None else self.operand.key())
+
+    def children(self):
+        return [self.operand] if self.operand is not None else []
+
+
+@dataclass(eq=False)
+class Lambda(Expr):
+    """``x -> expr`` / ``(x, i) -> expr`` argument of a higher-order array function."""
+    params: Tuple[str, ...]
+    body: Expr
+
+    def key(self):
+        return ("lambda", tuple(p.lower() for p in self.params), self.body.key())
+
+    def children(self):
+        return [self.body]
+
+
+@dataclass(eq=False)
+class LateralView:
+    """``FROM src LATERAL VIEW [OUTER] generator(args) alias AS c1[, c2]``."""
+    source: Any
+    generator: Call
+    outer: bool = False
+    alias: Optional[str] = None
+    columns: List[str] = field(default_factory=list)
 
 
 def walk(e: Expr):

@@ -187,8 +187,19 @@ class Parser:
 
     # -- statements ----------------------------------------------------------------------------------------------
     def parse_query(self) -> A.Query:
+        ctes = []
+        if self.is_word("with") and self.peek().kind in ("id", "kw") and not self.is_op("(", tok=self.peek()):
+            self.advance()
+            while True:
+                name = self.ident()
+                self.expect_kw("as")
+                self.expect_op("(")
+                ctes.append((name, self.parse_query()))
+                self.expect_op(")")
+                if not self.accept_op(","):
+                    break
         body = self.parse_set_expr()
-        q = A.Query(body=body)
+        q = A.Query(body=body, ctes=ctes)
         if self.accept_kw("order"):
             self.expect_kw("by")
             q.order_by = self.parse_order_items()
@@ -293,6 +304,23 @@ class Parser:
     def parse_from(self):
         left = self.parse_table_primary()
         while True:
+            if self.is_word("lateral") and self.is_word("view", tok=self.peek()):
+                self.advance()
+                self.advance()
+                outer = self.accept_kw("outer")
+                gen = self.parse_primary()
+                if not isinstance(gen, A.Call):
+                    self.error("LATERAL VIEW expects a generator function call")
+                alias = None
+                if not self.is_kw("as"):
+                    alias = self.ident()
+                cols = []
+                if self.accept_kw("as"):
+                    cols.append(self.ident())
+                    while self.accept_op(","):
+                        cols.append(self.ident())
+                left = A.LateralView(left, gen, outer, alias, cols)
+                continue
             if self.accept_op(","):
                 right = self.parse_table_primary()
                 left = A.Join(left, right, "cross")
@@ -357,7 +385,7 @@ class Parser:
         alias = None
         if self.accept_kw("as"):
             alias = self.ident()
-        elif self.cur.kind == "id":
+        elif self.cur.kind == "id" and not (self.is_word("lateral") and self.is_word("view", tok=self.peek())):
             alias = self.advance().text
         return A.TableRef(name, alias, tw)
 
@@ -396,6 +424,11 @@ class Parser:
                 neg = True
             if self.accept_kw("in"):
                 self.expect_op("(")
+                if self._at_query():
+                    q = self.parse_query()
+                    self.expect_op(")")
+                    e = A.SubqueryExpr("in", q, e, neg)
+                    continue
                 items = [self.parse_expr()]
                 while self.accept_op(","):
                     items.append(self.parse_expr())
@@ -508,11 +541,40 @@ class Parser:
             return A.Literal(s, "string")
         if self.is_op("("):
             self.advance()
-            if self.is_kw("select"):
-                self.error("scalar sub-queries are not supported")
+            if self._at_query():
+                q = self.parse_query()
+                self.expect_op(")")
+                return A.SubqueryExpr("scalar", q)
+            if self.cur.kind == "id" and self.is_op(",", tok=self.peek()):
+                # (x, y) -> body: a multi-parameter lambda
+                save = self.i
+                params = [self.advance().text]
+                while self.accept_op(","):
+                    if self.cur.kind != "id":
+                        break
+                    params.append(self.advance().text)
+                if self.accept_op(")") and self.is_op("-") and self.is_op(">", tok=self.peek()):
+                    self.advance()
+                    self.advance()
+                    return A.Lambda(tuple(params), self.parse_expr())
+                self.i = save
             e = self.parse_expr()
             self.expect_op(")")
             return e
+        if t.kind == "id" and t.text.lower() == "exists" and self.is_op("(", tok=self.peek()):
+            save = self.i
+            self.advance()
+            self.advance()
+            if self._at_query():
+                q = self.parse_query()
+                self.expect_op(")")
+                return A.SubqueryExpr("exists", q)
+            self.i = save
+        if t.kind == "id" and self.is_op("-", tok=self.peek()) and self.is_op(">", tok=self.peek(2)):
+            self.advance()
+            self.advance()
+            self.advance()
+            return A.Lambda((t.text,), self.parse_expr())
         if t.kind == "kw":
             w = t.text.lower()
             if w == "null":
@@ -600,6 +662,9 @@ class Parser:
             args.append(self.parse_expr())
         self.expect_op(")")
         return self._maybe_over(A.Call(low, args, distinct=distinct))
+
+    def _at_query(self) -> bool:
+        return self.is_kw("select") or (self.is_word("with") and self.peek().kind in ("id", "kw"))
 
     def is_word(self, *words, tok=None) -> bool:
         t = tok or self.cur
