@@ -59,15 +59,38 @@ def read_lines(path: str) -> List[str]:
     return read_text(path).splitlines()
 
 
+_GZ_CHUNK = 4 << 20
+_gz_pool: Optional[ThreadPoolExecutor] = None
+_gz_lock = threading.Lock()
+
+
+def _gz_member(chunk, level: int) -> bytes:
+    return gzip.compress(chunk, compresslevel=level, mtime=0)
+
+
+def gzip_parallel(data, level: int = 6, chunk: int = _GZ_CHUNK) -> bytes:
+    """gzip ``data`` as concatenated members compressed in parallel (zlib releases the GIL).  A multi-member gzip
+    file is one valid gzip stream to every reader (RFC 1952 §2.2; ``gzip -d``, Java ``GZIPInputStream``, Hadoop's
+    codec).  Level 6 is ``java.util.zip.GZIPOutputStream``'s default — what the reference's BlobSinker writes."""
+    global _gz_pool
+    mv = memoryview(data) if not isinstance(data, memoryview) else data
+    n = len(mv)
+    if n <= chunk:
+        return _gz_member(mv, level)
+    with _gz_lock:
+        if _gz_pool is None:
+            _gz_pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4), thread_name_prefix="dxa-gz")
+    parts = list(_gz_pool.map(lambda i: _gz_member(mv[i:i + chunk], level), range(0, n, chunk)))
+    return b"".join(parts)
+
+
 def write_atomic(path: str, data: bytes | str, gzip_it: bool = False) -> Path:
     """Write to a temp file in the destination folder, then rename (never leaves a partial file).  A blob PUT is
     atomic on the service side, so remote paths are written in one request."""
     if isinstance(data, str):
         data = data.encode("utf-8")
-    elif isinstance(data, memoryview) and gzip_it:
-        data = bytes(data)
     if gzip_it:
-        data = gzip.compress(data)
+        data = gzip_parallel(data)
     r = _remote(path)
     if r is not None:
         client, container, blob = r

@@ -138,7 +138,7 @@ def _eventhub_sink(d, output_name) -> Optional[Sink]:
         for chunk in _chunks(lines, 200):
             payload = "\n".join(chunk).encode()
             if compression != "none":
-                payload = gzip.compress(payload)
+                payload = fs.gzip_parallel(payload)
             eventhub_send(c, payload, output_name, props)
         return len(lines)
     return Sink("EventHub", write, d.get("filter"))

@@ -61,3 +61,22 @@ def test_filtered_sink_metric_names(tmp_path):
     op, = build_outputs(d)
     m = op.output(Table.from_pylist(ROWS, SCHEMA), dt.datetime(2024, 1, 1))
     assert m["Sink_File_Filtered"] == 2
+
+
+def test_gzip_parallel_is_one_valid_stream():
+    """Blob / Event Hubs payloads are gzip members compressed in parallel and concatenated: one valid gzip
+    stream for any reader."""
+    import gzip
+    import zlib
+    from dxa.io.fs import gzip_parallel
+    data = b"".join(b'{"i":%d,"s":"%s"}\n' % (i, b"x" * (i % 37)) for i in range(300000))
+    z = gzip_parallel(data, chunk=1 << 20)
+    assert gzip.decompress(z) == data
+    d = zlib.decompressobj(16 + zlib.MAX_WBITS)            # a streaming reader that walks member by member
+    out, rest = [], z
+    while rest:
+        out.append(d.decompress(rest))
+        rest = d.unused_data
+        d = zlib.decompressobj(16 + zlib.MAX_WBITS) if rest else d
+    assert b"".join(out) == data
+    assert gzip.decompress(gzip_parallel(b"small")) == b"small"
