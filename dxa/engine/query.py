@@ -533,7 +533,13 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     if not t.panes:
         return None
     proto = t.panes[0].table
-    empty = proto.take(torch.empty(0, dtype=torch.int64, device=proto.device))
+    # a zero-row table of the window's schema (resolves the select list); kept on the store while the schema holds
+    sig = (tuple(proto.names), tuple(str(c.dtype) for c in proto.columns))
+    cached = getattr(t.store, "_empty_proto", None)
+    if cached is None or cached[0] != sig:
+        cached = (sig, proto.take(torch.empty(0, dtype=torch.int64, device=proto.device)))
+        t.store._empty_proto = cached
+    empty = cached[1]
     items = _expand_items(sel, Scope.of_table(empty, alias))
     aggs: Dict = {}
     for e, _ in items:
