@@ -1,0 +1,114 @@
+"""Differential fuzzing of the GPU JSON parser (json_parse.hip) against the CPU reference (Python ``json`` +
+the engine's conversion rules): random records over a schema with every leaf type, nested structs, maps, arrays,
+unknown keys (skipped subtrees), duplicate keys, escapes (incl. surrogate pairs), raw UTF-8, whitespace, wrong
+types, huge numbers and malformed rows.  Raw-JSON texts (maps, arrays, non-string values read as strings) are
+compared as parsed JSON: the device keeps the source text, the reference re-serialises it."""
+import json
+import random
+
+import pytest
+import torch
+
+from dxa.engine.types import schema_from_json
+from dxa.ops.jsonparse import ParsePlan, frame_records, parse
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = schema_from_json(json.dumps({"type": "struct", "fields": [
+    {"name": "a", "type": "long"}, {"name": "b", "type": "double"}, {"name": "c", "type": "string"},
+    {"name": "d", "type": "boolean"}, {"name": "e", "type": "timestamp"}, {"name": "dt", "type": "date"},
+    {"name": "f", "type": {"type": "struct", "fields": [
+        {"name": "g", "type": "long"}, {"name": "h", "type": "string"},
+        {"name": "k", "type": {"type": "struct", "fields": [{"name": "z", "type": "double"}]}}]}},
+    {"name": "m", "type": {"type": "map", "keyType": "string", "valueType": "long", "valueContainsNull": True}},
+    {"name": "arr", "type": {"type": "array", "elementType": "long", "containsNull": True}},
+    {"name": "i", "type": "integer"}]}))
+
+_STRS = ["", "plain", 'q"uote', "back\\slash", "tab\tnl\nret\r", "ctl\x01\x1f", "unié", "日本語", "emoji😀",
+         "slash/", " sep", "a" * 300]
+
+
+def _rand_value(rnd, kind, depth=0):
+    r = rnd.random()
+    if r < 0.06:
+        return None
+    if r < 0.12 and depth < 3:          # wrong type
+        return rnd.choice([{"x": 1}, [1, "a"], "str", 12.5, True, -7])
+    if kind == "long":
+        return rnd.choice([0, 1, -1, 2**62, -2**63, 2**63 - 1, rnd.randint(-10**12, 10**12), 2**64, 3.0])
+    if kind == "int":
+        return rnd.choice([0, 2**31 - 1, -2**31, 2**31, rnd.randint(-1000, 1000)])
+    if kind == "double":
+        return rnd.choice([0.0, -0.0, 1.5, 1e300, -2.5e-300, 123456789.125, rnd.uniform(-1e6, 1e6), 7, -3])
+    if kind == "string":
+        return rnd.choice(_STRS)
+    if kind == "bool":
+        return rnd.random() < 0.5
+    if kind == "ts":
+        return rnd.choice(["2019-02-28T22:45:00Z", "2019-03-01 01:02:03.5", "2020-02-29T12:00:00+05:30",
+                           1551394800, "not a date", "2019-13-01T00:00:00Z"])
+    if kind == "date":
+        return rnd.choice(["2019-02-28", "2020-02-29T10:00:00Z", "bad", "1969-12-31"])
+    if kind == "map":
+        return {f"k{j}": rnd.choice([1, None, -5, 2**40]) for j in range(rnd.randint(0, 3))}
+    if kind == "arr":
+        return [rnd.choice([1, None, 3]) for _ in range(rnd.randint(0, 4))]
+    raise ValueError(kind)
+
+
+def _record(rnd):
+    d = {}
+    fields = [("a", "long"), ("b", "double"), ("c", "string"), ("d", "bool"), ("e", "ts"), ("dt", "date"),
+              ("m", "map"), ("arr", "arr"), ("i", "int")]
+    for k, kind in fields:
+        if rnd.random() < 0.9:
+            d[k] = _rand_value(rnd, kind)
+    if rnd.random() < 0.9:
+        f = {"g": _rand_value(rnd, "long", 1), "h": _rand_value(rnd, "string", 1)}
+        if rnd.random() < 0.7:
+            f["k"] = {"z": _rand_value(rnd, "double", 2)} if rnd.random() < 0.9 else rnd.choice([None, 3, "x"])
+        d["f"] = f if rnd.random() < 0.95 else rnd.choice([None, 5, [1]])
+    if rnd.random() < 0.3:                      # unknown subtrees the parser must skip
+        d["zz_unknown"] = {"deep": [{"x": [1, {"y": "}]\\\"{"}]}, "s": "a,b:c"], "n": -1.5e-3}
+    items = list(d.items())
+    rnd.shuffle(items)
+    s = "{" + ",".join(f"{json.dumps(k)}:{json.dumps(v, ensure_ascii=rnd.random() < 0.5)}" for k, v in items) + "}"
+    if rnd.random() < 0.2:
+        s = s.replace(",", " ,\n ").replace(":", " : ")
+    if rnd.random() < 0.05 and items:            # duplicate key: the last one wins (json / Jackson)
+        k, _ = items[0]
+        s = s[:-1] + ("," if len(s) > 2 else "") + f'{json.dumps(k)}:{json.dumps(_rand_value(rnd, "long"))}' + "}"
+    r = rnd.random()
+    if r < 0.03:
+        s = s[: max(1, len(s) // 2)]             # truncated
+    elif r < 0.04:
+        s = s[:-1] + ",}"                       # trailing comma
+    elif r < 0.05:
+        s = "[" + s + "]"                       # not an object
+    return s.encode("utf-8")
+
+
+def _norm(v):
+    if isinstance(v, str):
+        try:
+            return ("json", json.loads(v))
+        except ValueError:
+            return ("str", v)
+    if isinstance(v, dict):
+        return {k: _norm(x) for k, x in v.items()}
+    if isinstance(v, float) and v != v:
+        return "nan"
+    return v
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_gpu_parser_matches_reference(gpu, seed):
+    rnd = random.Random(seed)
+    recs = [_record(rnd) for _ in range(6000)]
+    plan = ParsePlan(SCHEMA)
+    cpu_raw, cpu_ok = parse(*frame_records(recs), plan)
+    gpu_raw, gpu_ok = parse(*frame_records(recs, device=gpu), plan)
+    assert torch.equal(cpu_ok, gpu_ok.cpu()), [recs[i] for i in torch.nonzero(cpu_ok != gpu_ok.cpu()).flatten()[:3]]
+    a, b = cpu_raw.to_pylist(), gpu_raw.to_pylist()
+    bad = [(i, x, y) for i, (x, y) in enumerate(zip(a, b)) if _norm(x) != _norm(y)]
+    assert not bad, [(recs[i], x, y) for i, x, y in bad[:3]]
