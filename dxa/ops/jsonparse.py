@@ -388,7 +388,9 @@ def _convert(v, dtype):
         if isinstance(v, bool):
             return None
         if isinstance(v, int):
-            return v * 1_000_000
+            if not (-2**63 <= v < 2**63):
+                return None
+            return ((v * 1_000_000 + 2**63) % 2**64) - 2**63      # seconds → µs, wrapping like Spark's long math
         if isinstance(v, str):
             return _iso_to_us(v)
         return None

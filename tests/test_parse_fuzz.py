@@ -69,7 +69,7 @@ def _record(rnd):
             f["k"] = {"z": _rand_value(rnd, "double", 2)} if rnd.random() < 0.9 else rnd.choice([None, 3, "x"])
         d["f"] = f if rnd.random() < 0.95 else rnd.choice([None, 5, [1]])
     if rnd.random() < 0.3:                      # unknown subtrees the parser must skip
-        d["zz_unknown"] = {"deep": [{"x": [1, {"y": "}]\\\"{"}]}, "s": "a,b:c"], "n": -1.5e-3}
+        d["zz_unknown"] = {"deep": [{"x": [1, {"y": '}]\\"{'}]}, "a,b:c"], "n": -1.5e-3}
     items = list(d.items())
     rnd.shuffle(items)
     s = "{" + ",".join(f"{json.dumps(k)}:{json.dumps(v, ensure_ascii=rnd.random() < 0.5)}" for k, v in items) + "}"
