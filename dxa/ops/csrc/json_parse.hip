@@ -309,19 +309,27 @@ __device__ __forceinline__ uint64_t swar_digits(uint64_t x, int k) {
   return ((v & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
 }
 
+// Bytes below 0x20 (unescaped control characters); exact for the lowest flagged byte, like swar_eq.
+__device__ __forceinline__ uint64_t swar_ctl(uint64_t x) {
+  return (x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull;
+}
+
 // Scan a string whose opening quote is at r.p.  On return r.p is past the closing quote.  Eight bytes per step:
-// the first quote or backslash is found with SWAR compares (a string of ~10 chars is one or two steps).
+// the first quote, backslash or control character is found with SWAR compares (a string of ~10 chars is one or
+// two steps).  An unescaped control character makes the record malformed (strict JSON, as Jackson's default).
 __device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, bool& esc) {
   ++r.p;
   s = r.p;
   esc = false;
   while (r.p < r.end) {
     const uint64_t x = r.load8(r.p);
-    const uint64_t m = swar_eq(x, 0x2222222222222222ull) | swar_eq(x, 0x5C5C5C5C5C5C5C5Cull);
+    const uint64_t m = swar_eq(x, 0x2222222222222222ull) | swar_eq(x, 0x5C5C5C5C5C5C5C5Cull) | swar_ctl(x);
     if (m == 0) { r.p += 8; continue; }
     r.p += __builtin_ctzll(m) >> 3;
     if (r.p >= r.end) break;
-    if (((x >> (8 * ((__builtin_ctzll(m) >> 3)))) & 0xff) == '"') { e = r.p; ++r.p; return true; }
+    const uint32_t c = (uint32_t)((x >> (8 * ((__builtin_ctzll(m) >> 3)))) & 0xff);
+    if (c == '"') { e = r.p; ++r.p; return true; }
+    if (c < 0x20u) break;                                 // raw control character inside a string
     esc = true;
     r.p += 2;                                             // backslash + escaped char
   }
@@ -487,28 +495,78 @@ __device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overf
   return true;
 }
 
-// Skip any JSON value at r.p (strings, numbers, literals, nested containers).
+// true / false / null spelled out exactly (r.p at the first letter); advances past it.
+__device__ __forceinline__ bool take_literal(Reader& r, uint32_t c) {
+  const uint64_t x = r.load8(r.p);
+  int L;
+  bool good;
+  if (c == 't') { L = 4; good = (x & 0xffffffffull) == 0x65757274ull; }             // "true"
+  else if (c == 'n') { L = 4; good = (x & 0xffffffffull) == 0x6c6c756eull; }        // "null"
+  else { L = 5; good = (x & 0xffffffffffull) == 0x65736c6166ull; }                   // "false"
+  r.p += L;
+  return good && r.p <= r.end;
+}
+
+// Skip any JSON value at r.p (strings, numbers, literals, nested containers), validating it as strictly as the
+// fields that are parsed: an unknown subtree that is not well-formed JSON makes the record malformed, as it does for
+// a tokenizing parser.  Containers are walked with an explicit state machine; the container kinds of up to 64
+// nesting levels live in one bit mask (deeper input is rejected).
 __device__ __forceinline__ bool skip_value(Reader& r) {
   uint32_t c = r.cur();
   if (c == '"') { int64_t s, e; bool esc; return scan_string(r, s, e, esc); }
-  if (c == '{' || c == '[') {
-    int depth = 0;
-    while (r.p < r.end) {
-      c = r.at(r.p);
-      if (c == '"') { int64_t s, e; bool esc; if (!scan_string(r, s, e, esc)) return false; continue; }
-      if (c == '{' || c == '[') ++depth;
-      else if (c == '}' || c == ']') { if (--depth == 0) { ++r.p; return true; } }
-      ++r.p;
-    }
-    return false;
-  }
   if (c == '-' || is_digit(c)) {
     bool ii, of; int64_t iv; double dv;
     return scan_number(r, ii, of, iv, dv);
   }
-  if (c == 't' || c == 'n') { r.p += 4; return r.p <= r.end; }
-  if (c == 'f') { r.p += 5; return r.p <= r.end; }
-  return false;
+  if (c == 't' || c == 'n' || c == 'f') return take_literal(r, c);
+  if (c != '{' && c != '[') return false;
+  enum { kVal, kValOrClose, kKey, kKeyOrClose, kColon, kSep };
+  uint64_t obj = 0;                                       // bit d: level d is an object
+  int depth = 0, st = kVal;
+  while (true) {
+    r.skip_ws();
+    if (r.p >= r.end) return false;
+    c = r.at(r.p);
+    switch (st) {
+      case kVal:
+      case kValOrClose:
+        if (c == ']' && st == kValOrClose) goto close;
+        if (c == '{' || c == '[') {
+          if (depth == 64) return false;
+          obj = (obj & ~(1ull << depth)) | ((uint64_t)(c == '{') << depth);
+          ++depth;
+          ++r.p;
+          st = c == '{' ? kKeyOrClose : kValOrClose;
+          continue;
+        }
+        if (c == '"') { int64_t s, e; bool esc; if (!scan_string(r, s, e, esc)) return false; }
+        else if (c == '-' || is_digit(c)) { bool ii, of; int64_t iv; double dv; if (!scan_number(r, ii, of, iv, dv)) return false; }
+        else if (c == 't' || c == 'n' || c == 'f') { if (!take_literal(r, c)) return false; }
+        else return false;
+        st = kSep;
+        continue;
+      case kKey:
+      case kKeyOrClose:
+        if (c == '}' && st == kKeyOrClose) goto close;
+        if (c != '"') return false;
+        { int64_t s, e; bool esc; if (!scan_string(r, s, e, esc)) return false; }
+        st = kColon;
+        continue;
+      case kColon:
+        if (c != ':') return false;
+        ++r.p;
+        st = kVal;
+        continue;
+      default:                                            // kSep: ',' or the current container's close
+        if (c == ',') { ++r.p; st = (obj >> (depth - 1)) & 1 ? kKey : kVal; continue; }
+        if (c == ((obj >> (depth - 1)) & 1 ? '}' : ']')) goto close;
+        return false;
+    }
+  close:
+    ++r.p;
+    if (--depth == 0) return true;
+    st = kSep;
+  }
 }
 
 // Hash one escape sequence of a key (r.p at the backslash) as the bytes it decodes to, so "a\u0062" finds "ab".
@@ -666,6 +724,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
 #define expect(i) expect_[(i) * 256]
   int depth = 0;
   bool ok = false;
+  bool comma = false;         // the last token was a member separator
+  uint64_t seen = 0;          // schema nodes (< 64) already assigned in this record
 
   r.skip_ws();
   if (r.cur() != '{') goto done;
@@ -682,11 +742,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
     r.skip_ws();
     uint32_t c = r.cur();
     if (c == '}') {
+      if (comma) break;       // trailing comma: {"a":1,}
       ++r.p;
       if (--depth == 0) { ok = true; break; }
       goto after_value;
     }
     if (c != '"') break;
+    comma = false;
     {
       // ---- key: speculate the expected key first, fall back to hashing the key text
       ++r.p;
@@ -721,6 +783,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
       const int t = tb.node_type[node];
       const int vs = tb.val_slot[node];
       const int ls = tb.len_slot[node];
+      if (node < 64) {                                    // a repeated key: its last occurrence decides (null on a
+        const uint64_t bit = 1ull << node;                // mismatch), as a tokenizing parser's last write would
+        if (seen & bit) a.valid[(int64_t)node * n + row] = 0;
+        seen |= bit;
+      }
       if (c == '{' && t == FT_STRUCT) {
         if (depth >= kMaxDepth) { if (!skip_value(r)) break; goto after_value; }
         a.valid[(int64_t)node * n + row] = 1;
@@ -789,8 +856,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
       if (c == 't' || c == 'f') {
         const int64_t s = r.p;
         const bool v = (c == 't');
-        r.p += v ? 4 : 5;
-        if (r.p > r.end) break;
+        if (!take_literal(r, c)) break;
         if (t == FT_BOOL) {
           a.vals[(int64_t)vs * n + row] = v ? 1 : 0;
           a.valid[(int64_t)node * n + row] = 1;
@@ -802,8 +868,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
         goto after_value;
       }
       if (c == 'n') {
-        r.p += 4;
-        if (r.p > r.end) break;
+        if (!take_literal(r, c)) break;
         goto after_value;
       }
       break;  // unexpected token
@@ -811,9 +876,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
   after_value:
     r.skip_ws();
     c = r.cur();
-    if (c == ',') { ++r.p; continue; }
+    if (c == ',') { ++r.p; comma = true; continue; }
     if (c == '}') continue;  // closes the current object at loop top
     break;
+  }
+  if (ok) {                   // nothing but whitespace may follow the record's object
+    r.skip_ws();
+    ok = r.p >= r.end;
   }
 done:
   a.row_ok[row] = ok ? 1 : 0;
