@@ -15,6 +15,7 @@
 // → every field of the row null and row_ok=0 (the reference is "tolerant to mismatched input schema").
 #include "dxa_common.h"
 #include <type_traits>
+#include "pow10_dd.h"
 
 namespace {
 
@@ -448,6 +449,7 @@ __device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, 
 __device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overflow, int64_t& iv, double& dv) {
   bool neg = false;
   if (r.cur() == '-') { neg = true; ++r.p; }
+  if (r.cur() == '0' && r.p + 1 < r.end && is_digit(r.at(r.p + 1))) return false;    // JSON: no leading zeros
   uint64_t mant = 0;
   int nd = 0, exp10 = 0;
   bool lost = false;
@@ -481,14 +483,19 @@ __device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overf
     iv = neg ? (int64_t)(0ull - mant) : (int64_t)mant;
   }
   double d = (double)mant;
-  if (exp10 != 0) {
-    if (mant < (1ull << 53) && exp10 > 0 && exp10 <= 22) d = d * kPow10[exp10];
+  if (exp10 != 0 || mant >= (1ull << 53)) {
+    if (mant < (1ull << 53) && exp10 > 0 && exp10 <= 22) d = d * kPow10[exp10];           // exact operands
     else if (mant < (1ull << 53) && exp10 < 0 && exp10 >= -22) d = d / kPow10[-exp10];
+    else if (mant == 0) d = 0.0;
+    else if (exp10 > DXA_POW10_DD_MAX) d = __builtin_inf();
+    else if (exp10 < DXA_POW10_DD_MIN) d = 0.0;
     else {
-      int e = exp10;
-      while (e > 22) { d *= 1e22; e -= 22; }
-      while (e < -22) { d /= 1e22; e += 22; }
-      d = e >= 0 ? d * kPow10[e] : d / kPow10[-e];
+      // mantissa (exact as hi + lo) × 10^exp10 (double-double) with one final rounding
+      const double mh = (double)(mant & ~0x7FFull), ml = (double)(mant & 0x7FFull);
+      const double ph = kPow10dd[exp10 - DXA_POW10_DD_MIN][0], pl = kPow10dd[exp10 - DXA_POW10_DD_MIN][1];
+      const double h = mh * ph;
+      const double err = __builtin_fma(mh, ph, -h) + (mh * pl + ml * ph);
+      d = h + err;
     }
   }
   dv = neg ? -d : d;
