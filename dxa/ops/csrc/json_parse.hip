@@ -491,11 +491,13 @@ __device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overf
     else if (exp10 < DXA_POW10_DD_MIN) d = 0.0;
     else {
       // mantissa (exact as hi + lo) × 10^exp10 (double-double) with one final rounding
-      const double mh = (double)(mant & ~0x7FFull), ml = (double)(mant & 0x7FFull);
+      const bool wide = mant >= (1ull << 53);
+      const double mh = (double)(wide ? (mant & ~0x7FFull) : mant), ml = wide ? (double)(mant & 0x7FFull) : 0.0;
       const double ph = kPow10dd[exp10 - DXA_POW10_DD_MIN][0], pl = kPow10dd[exp10 - DXA_POW10_DD_MIN][1];
       const double h = mh * ph;
       const double err = __builtin_fma(mh, ph, -h) + (mh * pl + ml * ph);
       d = h + err;
+      if (exp10 < DXA_POW10_DD_SCALED_BELOW) d = __builtin_ldexp(d, -DXA_POW10_DD_SCALE);   // exact power-of-2 scale
     }
   }
   dv = neg ? -d : d;
