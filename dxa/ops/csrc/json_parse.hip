@@ -332,6 +332,20 @@ __device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, b
     if (c == '"') { e = r.p; ++r.p; return true; }
     if (c < 0x20u) break;                                 // raw control character inside a string
     esc = true;
+    if (r.p + 1 >= r.end) break;
+    const uint32_t n = r.at(r.p + 1);                     // the escaped character must be one JSON defines
+    if (n == 'u') {
+      if (r.p + 6 > r.end) break;
+      bool hex = true;
+      for (int k = 2; k < 6; ++k) {
+        const uint32_t h = r.at(r.p + k);
+        hex &= (h - '0' < 10u) || ((h | 0x20u) - 'a' < 6u);
+      }
+      if (!hex) break;
+      r.p += 6;
+      continue;
+    }
+    if (!(n == '"' || n == '\\' || n == '/' || n == 'b' || n == 'f' || n == 'n' || n == 'r' || n == 't')) break;
     r.p += 2;                                             // backslash + escaped char
   }
   r.p = r.end;

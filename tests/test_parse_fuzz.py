@@ -78,6 +78,11 @@ def _record(rnd):
     if rnd.random() < 0.05 and items:            # duplicate key: the last one wins (json / Jackson)
         k, _ = items[0]
         s = s[:-1] + ("," if len(s) > 2 else "") + f'{json.dumps(k)}:{json.dumps(_rand_value(rnd, "long"))}' + "}"
+    if rnd.random() < 0.03:                       # escapes JSON does not define / malformed \u escapes
+        bad = rnd.choice(['\\x41', '\\u12G4', '\\', '\\U0041'])
+        s = s.replace('"plain"', '"pl' + bad + 'ain"', 1) if b'"plain"' in s.encode() else s
+    if rnd.random() < 0.03:                       # valid \u escapes, upper-case hex
+        s = s.replace('"plain"', '"pl\\u00E9in"', 1)
     r = rnd.random()
     if r < 0.03:
         s = s[: max(1, len(s) // 2)]             # truncated
