@@ -504,7 +504,9 @@ __device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overf
     else if (exp10 > DXA_POW10_DD_MAX) d = __builtin_inf();
     else if (exp10 < DXA_POW10_DD_MIN) d = 0.0;
     else {
-      // mantissa (exact as hi + lo) × 10^exp10 (double-double) with one final rounding
+      // mantissa (exact as hi + lo) × 10^exp10 (double-double) with one final rounding.  No contraction: fusing
+      // h = mh*ph into the final add would count the product's rounding error twice
+#pragma clang fp contract(off)
       const bool wide = mant >= (1ull << 53);
       const double mh = (double)(wide ? (mant & ~0x7FFull) : mant), ml = wide ? (double)(mant & 0x7FFull) : 0.0;
       const double ph = kPow10dd[exp10 - DXA_POW10_DD_MIN][0], pl = kPow10dd[exp10 - DXA_POW10_DD_MIN][1];
