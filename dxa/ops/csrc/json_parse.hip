@@ -805,7 +805,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
         if (!skip_value(r)) break;
         goto after_value;
       }
-      const int t = tb.node_type[node];
+      const int t = tb.node_type[node] & 0xff;
+      const bool raw_arr = (tb.node_type[node] & 0x100) != 0;
       const int vs = tb.val_slot[node];
       const int ls = tb.len_slot[node];
       if (node < 64) {                                    // a repeated key: its last occurrence decides (null on a
@@ -825,7 +826,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
       if (c == '{' || c == '[') {
         const int64_t s = r.p;
         if (!skip_value(r)) break;
-        if ((t == FT_STRING || t == FT_RAW) && ls >= 0) {
+        if ((t == FT_STRING || (t == FT_RAW && (c == '[') == raw_arr)) && ls >= 0) {
           a.vals[(int64_t)vs * n + row] = s;
           a.lens[(int64_t)ls * n + row] = (int32_t)(r.p - s);
           a.valid[(int64_t)node * n + row] = 1;

@@ -141,7 +141,9 @@ class ParsePlan:
         if t is None:
             t = (torch.tensor(self.lut_keys, dtype=torch.int64, device=device),
                  torch.tensor(self.lut_node, dtype=torch.int32, device=device),
-                 torch.tensor([n.code for n in self.nodes], dtype=torch.int32, device=device),
+                 # raw-JSON leaves: bit 8 marks an array type (the value must be '[…]'; maps take '{…}')
+                 torch.tensor([n.code | (0x100 if n.code == FT["raw"] and isinstance(n.dtype, ArrayType) else 0)
+                               for n in self.nodes], dtype=torch.int32, device=device),
                  torch.tensor([n.val_slot for n in self.nodes], dtype=torch.int32, device=device),
                  torch.tensor([n.len_slot for n in self.nodes], dtype=torch.int32, device=device),
                  torch.tensor(self.first_child, dtype=torch.int32, device=device),

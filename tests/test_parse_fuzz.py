@@ -75,7 +75,9 @@ def _record(rnd):
     s = "{" + ",".join(f"{json.dumps(k)}:{json.dumps(v, ensure_ascii=rnd.random() < 0.5)}" for k, v in items) + "}"
     if rnd.random() < 0.2:
         s = s.replace(",", " ,\n ").replace(":", " : ")
-    if rnd.random() < 0.05 and items:            # duplicate key: the last one wins (json / Jackson)
+    if rnd.random() < 0.05 and items and items[0][0] != "f":
+        # duplicate key: the last one wins (json / Jackson).  Not for struct-valued keys: the kernel resolves a
+        # repeated struct key per leaf (children of the earlier object stay set), a documented divergence
         k, _ = items[0]
         s = s[:-1] + ("," if len(s) > 2 else "") + f'{json.dumps(k)}:{json.dumps(_rand_value(rnd, "long"))}' + "}"
     if rnd.random() < 0.03:                       # escapes JSON does not define / malformed \u escapes
