@@ -532,21 +532,41 @@ __device__ __forceinline__ bool take_literal(Reader& r, uint32_t c) {
   return good && r.p <= r.end;
 }
 
+// A JSON number's syntax (-? int frac? exp?) without its value: the skipping paths need no mantissa registers.
+__device__ __forceinline__ bool skip_number(Reader& r) {
+  if (r.cur() == '-') ++r.p;
+  if (!is_digit(r.cur())) return false;
+  if (r.cur() == '0') {
+    ++r.p;
+    if (is_digit(r.cur())) return false;                  // leading zero
+  }
+  while (is_digit(r.cur())) ++r.p;
+  if (r.cur() == '.') {
+    ++r.p;
+    if (!is_digit(r.cur())) return false;
+    while (is_digit(r.cur())) ++r.p;
+  }
+  if ((r.cur() | 0x20u) == 'e') {
+    ++r.p;
+    if (r.cur() == '-' || r.cur() == '+') ++r.p;
+    if (!is_digit(r.cur())) return false;
+    while (is_digit(r.cur())) ++r.p;
+  }
+  return true;
+}
+
 // Skip any JSON value at r.p (strings, numbers, literals, nested containers), validating it as strictly as the
 // fields that are parsed: an unknown subtree that is not well-formed JSON makes the record malformed, as it does for
-// a tokenizing parser.  Containers are walked with an explicit state machine; the container kinds of up to 64
+// a tokenizing parser.  Containers are walked with an explicit state machine; the container kinds of up to 32
 // nesting levels live in one bit mask (deeper input is rejected).
 __device__ __forceinline__ bool skip_value(Reader& r) {
   uint32_t c = r.cur();
   if (c == '"') { int64_t s, e; bool esc; return scan_string(r, s, e, esc); }
-  if (c == '-' || is_digit(c)) {
-    bool ii, of; int64_t iv; double dv;
-    return scan_number(r, ii, of, iv, dv);
-  }
+  if (c == '-' || is_digit(c)) return skip_number(r);
   if (c == 't' || c == 'n' || c == 'f') return take_literal(r, c);
   if (c != '{' && c != '[') return false;
   enum { kVal, kValOrClose, kKey, kKeyOrClose, kColon, kSep };
-  uint64_t obj = 0;                                       // bit d: level d is an object
+  uint32_t obj = 0;                                       // bit d: level d is an object
   int depth = 0, st = kVal;
   while (true) {
     r.skip_ws();
@@ -557,15 +577,15 @@ __device__ __forceinline__ bool skip_value(Reader& r) {
       case kValOrClose:
         if (c == ']' && st == kValOrClose) goto close;
         if (c == '{' || c == '[') {
-          if (depth == 64) return false;
-          obj = (obj & ~(1ull << depth)) | ((uint64_t)(c == '{') << depth);
+          if (depth == 32) return false;
+          obj = (obj & ~(1u << depth)) | ((uint32_t)(c == '{') << depth);
           ++depth;
           ++r.p;
           st = c == '{' ? kKeyOrClose : kValOrClose;
           continue;
         }
         if (c == '"') { int64_t s, e; bool esc; if (!scan_string(r, s, e, esc)) return false; }
-        else if (c == '-' || is_digit(c)) { bool ii, of; int64_t iv; double dv; if (!scan_number(r, ii, of, iv, dv)) return false; }
+        else if (c == '-' || is_digit(c)) { if (!skip_number(r)) return false; }
         else if (c == 't' || c == 'n' || c == 'f') { if (!take_literal(r, c)) return false; }
         else return false;
         st = kSep;
@@ -750,7 +770,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
   int depth = 0;
   bool ok = false;
   bool comma = false;         // the last token was a member separator
-  uint64_t seen = 0;          // schema nodes (< 64) already assigned in this record
+  int store_node = -1;        // skip_any: raw-JSON text of the skipped value goes to this node
+  __shared__ uint64_t s_seen[256];                        // schema nodes (< 64) already assigned in this record
+  s_seen[threadIdx.x] = 0;                                // (per lane in LDS: keeps the loop's VGPR budget)
 
   r.skip_ws();
   if (r.cur() != '{') goto done;
@@ -774,6 +796,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
     }
     if (c != '"') break;
     comma = false;
+    store_node = -1;
     {
       // ---- key: speculate the expected key first, fall back to hashing the key text
       ++r.p;
@@ -801,21 +824,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
       ++r.p;
       r.skip_ws();
       c = r.cur();
-      if (node < 0) {
-        if (!skip_value(r)) break;
-        goto after_value;
-      }
+      if (node < 0) goto skip_any;
       const int t = tb.node_type[node] & 0xff;
       const bool raw_arr = (tb.node_type[node] & 0x100) != 0;
       const int vs = tb.val_slot[node];
       const int ls = tb.len_slot[node];
       if (node < 64) {                                    // a repeated key: its last occurrence decides (null on a
         const uint64_t bit = 1ull << node;                // mismatch), as a tokenizing parser's last write would
+        const uint64_t seen = s_seen[threadIdx.x];
         if (seen & bit) a.valid[(int64_t)node * n + row] = 0;
-        seen |= bit;
+        s_seen[threadIdx.x] = seen | bit;
       }
       if (c == '{' && t == FT_STRUCT) {
-        if (depth >= kMaxDepth) { if (!skip_value(r)) break; goto after_value; }
+        if (depth >= kMaxDepth) goto skip_any;
         a.valid[(int64_t)node * n + row] = 1;
         expect(depth) = tb.first_child[node];
         stack(depth) = node;
@@ -824,14 +845,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
         continue;
       }
       if (c == '{' || c == '[') {
-        const int64_t s = r.p;
-        if (!skip_value(r)) break;
-        if ((t == FT_STRING || (t == FT_RAW && (c == '[') == raw_arr)) && ls >= 0) {
-          a.vals[(int64_t)vs * n + row] = s;
-          a.lens[(int64_t)ls * n + row] = (int32_t)(r.p - s);
-          a.valid[(int64_t)node * n + row] = 1;
-        }
-        goto after_value;
+        if ((t == FT_STRING || (t == FT_RAW && (c == '[') == raw_arr)) && ls >= 0) store_node = node;
+        goto skip_any;
       }
       if (c == '"') {
         int64_t s, e;
@@ -898,6 +913,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
         goto after_value;
       }
       break;  // unexpected token
+    }
+    // the one place a value is skipped (unknown key, raw-JSON container, too-deep struct): a single inlined copy of
+    // the validating skipper keeps the loop's code and register footprint small
+  skip_any: {
+      const int64_t s0 = r.p;
+      if (!skip_value(r)) break;
+      if (store_node >= 0) {
+        a.vals[(int64_t)tb.val_slot[store_node] * n + row] = s0;
+        a.lens[(int64_t)tb.len_slot[store_node] * n + row] = (int32_t)(r.p - s0);
+        a.valid[(int64_t)store_node * n + row] = 1;
+      }
     }
   after_value:
     r.skip_ws();
