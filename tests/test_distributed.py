@@ -25,6 +25,14 @@ QUERIES = [
     "MAX(v) OVER (PARTITION BY k ORDER BY v ROWS BETWEEN 2 PRECEDING AND CURRENT ROW) AS m3 FROM T",
     "SELECT k, v, DENSE_RANK() OVER (ORDER BY k) AS dr, COUNT(*) OVER () AS n FROM T",
     "SELECT k, SUM(v) AS sv, RANK() OVER (ORDER BY k DESC) AS r FROM T GROUP BY k",
+    # the extended SQL surface over partitioned inputs
+    "SELECT k, percentile(v, 0.5) AS p, percentile_approx(v, 0.25) AS pa FROM T GROUP BY k",
+    "WITH w AS (SELECT k, v FROM T WHERE v > 0) SELECT k, COUNT(*) AS c FROM w GROUP BY k",
+    "SELECT k, v FROM T WHERE k IN (SELECT k FROM T2)",
+    "SELECT k, v FROM T t WHERE NOT EXISTS (SELECT 1 FROM T2 b WHERE b.k = t.k)",
+    "SELECT a.k, a.v, b.v AS bv FROM T a LEFT JOIN T2 b ON a.k = b.k AND a.v > 5",
+    "SELECT k, explode(split(s, 'b')) AS part FROM T WHERE s IS NOT NULL",
+    "SELECT (SELECT MAX(v) FROM T) AS m, COUNT(*) AS c FROM T",
 ]
 
 
