@@ -645,7 +645,71 @@ def _lookup(src: A.TableRef, catalog: Catalog):
     return catalog.get(name)
 
 
+def _rewrite_expr(e, fn):
+    """Rebuild an expression tree bottom-up through ``fn(node) -> node | None`` (None: keep, descend)."""
+    import dataclasses
+    r = fn(e)
+    if r is not None:
+        return r
+    if not dataclasses.is_dataclass(e) or not isinstance(e, A.Expr):
+        return e
+    changes = {}
+    for f in dataclasses.fields(e):
+        v = getattr(e, f.name)
+        if isinstance(v, A.Expr):
+            nv = _rewrite_expr(v, fn)
+            if nv is not v:
+                changes[f.name] = nv
+        elif isinstance(v, list) and any(isinstance(x, A.Expr) for x in v):
+            nv = [_rewrite_expr(x, fn) if isinstance(x, A.Expr) else x for x in v]
+            if any(a is not b for a, b in zip(nv, v)):
+                changes[f.name] = nv
+    return dataclasses.replace(e, **changes) if changes else e
+
+
+def _exec_grouping_sets(sel: A.Select, catalog, ctx):
+    """GROUP BY ROLLUP / CUBE / GROUPING SETS: one aggregation per set, UNION ALL.  Group expressions outside the
+    current set read as NULL in the select list and HAVING (not inside aggregates); ``grouping(c)`` /
+    ``grouping_id(…)`` become the set's constant bits (Spark's semantics)."""
+    if any(isinstance(it.expr, A.Star) for it in sel.items):
+        raise QueryError("SELECT * is not supported with ROLLUP / CUBE / GROUPING SETS")
+    all_keys = [g.key() for g in sel.group_by]
+    parts = []
+    for st in sel.grouping_sets:
+        in_set = {g.key() for g in st}
+        rolled = {k for k in all_keys if k not in in_set}
+
+        def fn(node, rolled=rolled):
+            if isinstance(node, A.Call):
+                if node.name in AGG_FUNCS or node.name in ctx.udafs:
+                    return node                                   # aggregates see the real values
+                if node.name == "grouping":
+                    return A.Literal(1 if node.args and node.args[0].key() in rolled else 0, "int")
+                if node.name == "grouping_id":
+                    cols = [a.key() for a in node.args] or all_keys
+                    bits = 0
+                    for k in cols:
+                        bits = (bits << 1) | (1 if k in rolled else 0)
+                    return A.Literal(bits, "long")
+            if isinstance(node, A.Expr) and not isinstance(node, A.Literal) and node.key() in rolled:
+                return A.Literal(None, "null")
+            return None
+        items = [A.SelectItem(_rewrite_expr(it.expr, fn), it.alias or output_name(it.expr)) for it in sel.items]
+        sub = A.Select(items=items, from_=sel.from_, where=sel.where, group_by=list(st),
+                       having=None if sel.having is None else _rewrite_expr(sel.having, fn))
+        if not st and not any(_contains_agg(it.expr, ctx) for it in items):
+            sub.group_by = []
+        out, _ = _exec_select(sub, catalog, ctx)
+        parts.append(out)
+    out = parts[0]
+    for p in parts[1:]:
+        out = _set_op(A.SetOp("union", True, None, None), out, p)
+    return distinct(out) if sel.distinct else out
+
+
 def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
+    if sel.grouping_sets is not None:
+        return _exec_grouping_sets(sel, catalog, ctx), None
     if isinstance(sel.from_, A.TableRef) and not want_scope:
         from .windows import PanedTable
         t = _lookup(sel.from_, catalog)

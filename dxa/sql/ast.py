@@ -260,6 +260,7 @@ class Select:
     group_by: List[Expr] = field(default_factory=list)
     having: Optional[Expr] = None
     distinct: bool = False
+    grouping_sets: Optional[List[List[Expr]]] = None     # ROLLUP / CUBE / GROUPING SETS (subsets of group_by)
 
 
 @dataclass(eq=False)

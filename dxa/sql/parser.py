@@ -272,13 +272,61 @@ class Parser:
             sel.where = self.parse_expr()
         if self.accept_kw("group"):
             self.expect_kw("by")
-            while True:
-                sel.group_by.append(self.parse_expr())
-                if not self.accept_op(","):
-                    break
+            self._parse_group_by(sel)
         if self.accept_kw("having"):
             sel.having = self.parse_expr()
         return sel
+
+    def _parse_group_by(self, sel: A.Select):
+        """GROUP BY e, … [WITH ROLLUP | WITH CUBE] | ROLLUP(…) | CUBE(…) | GROUPING SETS ((…), …)."""
+        def expr_list():
+            self.expect_op("(")
+            out = []
+            if not self.is_op(")"):
+                out.append(self.parse_expr())
+                while self.accept_op(","):
+                    out.append(self.parse_expr())
+            self.expect_op(")")
+            return out
+
+        def uniq(exprs):
+            seen, out = set(), []
+            for e in exprs:
+                if e.key() not in seen:
+                    seen.add(e.key())
+                    out.append(e)
+            return out
+
+        if self.is_word("rollup", "cube") and self.is_op("(", tok=self.peek()):
+            kind = self.advance().text.lower()
+            cols = expr_list()
+            sel.group_by = cols
+            sel.grouping_sets = _rollup(cols) if kind == "rollup" else _cube(cols)
+            return
+        if self.is_word("grouping") and self.is_word("sets", tok=self.peek()):
+            self.advance()
+            self.advance()
+            self.expect_op("(")
+            sets = []
+            while True:
+                if self.is_op("("):
+                    sets.append(expr_list())
+                else:
+                    sets.append([self.parse_expr()])
+                if not self.accept_op(","):
+                    break
+            self.expect_op(")")
+            sel.group_by = uniq([e for st in sets for e in st])
+            sel.grouping_sets = sets
+            return
+        while True:
+            sel.group_by.append(self.parse_expr())
+            if not self.accept_op(","):
+                break
+        if self.is_word("with") and self.is_word("rollup", "cube", tok=self.peek()):
+            self.advance()
+            kind = self.advance().text.lower()
+            sel.grouping_sets = _rollup(sel.group_by) if kind == "rollup" else _cube(sel.group_by)
 
     def parse_select_item(self) -> A.SelectItem:
         if self.is_op("*"):
@@ -724,6 +772,18 @@ class Parser:
         if self.accept_word("following"):
             return ("following", k)
         self.error("expected PRECEDING or FOLLOWING")
+
+
+def _rollup(cols):
+    return [cols[:k] for k in range(len(cols), -1, -1)]
+
+
+def _cube(cols):
+    n = len(cols)
+    sets = []
+    for mask in range((1 << n) - 1, -1, -1):
+        sets.append([c for i, c in enumerate(cols) if mask >> (n - 1 - i) & 1])
+    return sets
 
 
 def _number_literal(text: str) -> A.Literal:

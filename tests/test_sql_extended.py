@@ -155,3 +155,13 @@ def test_extended_functions_gpu_match_cpu(gpu):
                 "SELECT id, percentile_approx(v, 0.5) AS a FROM T GROUP BY id ORDER BY id",
                 "SELECT t.id, r.w FROM T t LEFT JOIN R r ON t.id = r.rid AND r.w > 5 ORDER BY t.id"]:
         assert q(sql, gpu) == q(sql, "cpu"), sql
+
+
+def test_rollup_cube_grouping_sets():
+    rows, _ = q("SELECT id, SUM(v) AS s, grouping_id() AS g FROM T GROUP BY ROLLUP(id) ORDER BY g, id")
+    assert rows == [(1, 1.5, 0), (2, 4.0, 0), (3, 3.25, 0), (None, 8.75, 1)]
+    rows, _ = q("SELECT id, name IS NULL AS nn, COUNT(*) AS c FROM T GROUP BY id, name IS NULL WITH CUBE")
+    assert len(rows) == 3 + 3 + 2 + 1 and (None, None, 4) in rows and (None, False, 3) in rows
+    rows, _ = q("SELECT id, COUNT(*) AS c, grouping(id) AS gi FROM T GROUP BY GROUPING SETS ((id), ()) "
+                "HAVING COUNT(*) > 1 ORDER BY gi")
+    assert rows == [(2, 2, 0), (None, 4, 1)]
