@@ -705,6 +705,43 @@ def _get_json_object(s, path):
     return json.dumps(v, separators=(",", ":"))
 
 
+_SIMPLE_PATH = re.compile(r"^\$((?:\.[A-Za-z_][A-Za-z0-9_]*)+)$")
+
+
+def _f_get_json_object(e, scope, ctx, subst):
+    """get_json_object(json, '$.a.b'): on the GPU a dotted path becomes a one-leaf schema for the batch JSON
+    parser (the leaf read as a string: string values unquoted, anything else as its JSON text, as Spark returns
+    it); array-index paths and host columns take the per-row host path."""
+    a = evaluate(e.args[0], scope, ctx, subst)
+    p = evaluate(e.args[1], scope, ctx, subst)
+    m = _SIMPLE_PATH.match(str(p.value)) if isinstance(p, ConstColumn) and p.value is not None else None
+    if m is None or isinstance(a, ConstColumn) or not a.device.type == "cuda":
+        return _host_string_fn(_get_json_object)(e, scope, ctx, subst)
+    from ..ops.jsonparse import ParsePlan, parse
+    from .types import StructField, StructType
+    keys = m.group(1)[1:].split(".")
+    t = "string"
+    for k in reversed(keys):
+        t = StructType((StructField(k, t),))
+    if not isinstance(a, StrColumn):
+        a = cast_column(a, "string")
+    c = a.compact()                                 # the parser un-escapes in place: parse a private copy
+    n, dev = c.length, c.device
+    ends = c.starts + c.lens.to(torch.int64)
+    offs = torch.cat([c.starts, ends[-1:] if n else torch.zeros(1, dtype=torch.int64, device=dev)])
+    raw, ok = parse(c.arena, offs, ParsePlan(t), ends)
+    col, valid = raw, ok if a.valid is None else (ok & a.valid)
+    for k in keys:
+        if col.valid is not None:
+            valid = valid & col.valid
+        col = col.child(k)
+    if col.valid is not None:
+        valid = valid & col.valid
+    out = StrColumn(col.arena, col.starts, col.lens, valid)
+    out._keep = c
+    return out
+
+
 def _f_from_json(e, scope, ctx, subst):
     """from_json(str, schema): the batch JSON parser (device kernel on the GPU) over a private copy of the column's
     bytes (the parser un-escapes in place)."""
@@ -840,7 +877,7 @@ def _register():
     reg("right", _host_string_fn(lambda s, k: str(s)[-int(k):] if int(k) > 0 else ""))
     reg("translate", _host_string_fn(_translate))
     reg("ascii", _host_string_fn(lambda s: ord(str(s)[0]) if str(s) else 0, "int"))
-    reg("get_json_object", _host_string_fn(_get_json_object))
+    reg("get_json_object", _f_get_json_object)
     reg("from_json", _f_from_json)
     reg("hash", _f_hash)
     reg("window", _f_window)

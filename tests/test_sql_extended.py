@@ -152,6 +152,8 @@ def test_extended_functions_gpu_match_cpu(gpu):
                 "SELECT date_format(ts, 'yyyy-MM-dd HH:mm:ss.SSS') AS a, date_format(ts, 'EEE MMM dd yy hh a DDD') "
                 "AS b FROM T",
                 "SELECT from_json(js, 'x INT, s STRING') AS j FROM T",
+                "SELECT get_json_object(js, '$.x') AS x, get_json_object(js, '$.y') AS y, get_json_object(js, '$.s') "
+                "AS s, get_json_object(js, '$.q.r') AS qr FROM T",
                 "SELECT id, percentile_approx(v, 0.5) AS a FROM T GROUP BY id ORDER BY id",
                 "SELECT t.id, r.w FROM T t LEFT JOIN R r ON t.id = r.rid AND r.w > 5 ORDER BY t.id"]:
         assert q(sql, gpu) == q(sql, "cpu"), sql
