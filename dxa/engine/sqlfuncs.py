@@ -801,6 +801,195 @@ def _f_window(e, scope, ctx, subst):
                         dev)
 
 
+# ---------------------------------------------------------------------------------------------------------------
+# character functions on the GPU (strings.hip): substring / trim / left / right are views into the same arena
+# ---------------------------------------------------------------------------------------------------------------
+
+def spark_substr(s: str, pos: int, length: Optional[int] = None) -> str:
+    """UTF8String.substringSQL: 1-based pos, 0 treated as 1, negative from the end; end computed before the start
+    is clamped."""
+    n = len(s)
+    start = pos - 1 if pos > 0 else (n + pos if pos < 0 else 0)
+    end = n if length is None else start + length
+    start = max(start, 0)
+    if start >= end:
+        return ""
+    return s[start:end]
+
+
+def _gpu_str(c) -> bool:
+    return isinstance(c, StrColumn) and c.starts.is_cuda
+
+
+def _int_arg(c, n, dev):
+    """(per-row int64 tensor or None, constant, validity)."""
+    if isinstance(c, ConstColumn):
+        return None, (None if c.value is None else int(c.value)), None
+    c = _num(c, n, dev)
+    return c.data.to(torch.int64).contiguous(), 0, c.valid
+
+
+def _view(col: StrColumn, starts, lens, valid) -> StrColumn:
+    out = StrColumn(col.arena, starts, lens, valid)
+    return out
+
+
+def _f_substr(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    args = _args(e, scope, ctx, subst)
+    a = args[0]
+    if isinstance(a, ConstColumn) or not _gpu_str(a if isinstance(a, StrColumn) else None):
+        def host(s, p, ln=None):
+            return spark_substr(str(s), int(p), None if ln is None else int(ln))
+        return _host_string_fn(host)(e, scope, ctx, subst)
+    from ..ops import native as N
+    pos_t, pos_c, pos_v = _int_arg(args[1], n, dev)
+    if len(args) > 2:
+        len_t, len_c, len_v = _int_arg(args[2], n, dev)
+    else:
+        len_t, len_c, len_v = None, 2**63 - 1, None
+    if (pos_t is None and pos_c is None) or (len_t is None and len_c is None):
+        return ConstColumn(None, "string", n, dev)
+    os_ = torch.empty(n, dtype=torch.int64, device=dev)
+    ol = torch.empty(n, dtype=torch.int32, device=dev)
+    N.call("dxa_str_substr", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), n, N.ptr(pos_t), pos_c or 0,
+           N.ptr(len_t), len_c if len_c is not None else 0, N.ptr(os_), N.ptr(ol), N.stream_handle(dev))
+    return _view(a, os_, ol, _and(a.valid, pos_v, len_v))
+
+
+def _f_left_right(right: bool):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        a, k = _args(e, scope, ctx, subst)
+        if not isinstance(a, StrColumn) or not _gpu_str(a) or not isinstance(k, ConstColumn):
+            fn = (lambda s, kk: str(s)[-int(kk):] if int(kk) > 0 else "") if right else \
+                (lambda s, kk: str(s)[:max(0, int(kk))])
+            return _host_string_fn(fn)(e, scope, ctx, subst)
+        kk = int(k.value)
+        from ..ops import native as N
+        os_ = torch.empty(n, dtype=torch.int64, device=dev)
+        ol = torch.empty(n, dtype=torch.int32, device=dev)
+        if kk <= 0:
+            return _view(a, a.starts, torch.zeros_like(a.lens), a.valid)
+        pos, ln = (-kk, kk) if right else (1, kk)
+        N.call("dxa_str_substr", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), n, None, pos, None, ln,
+               N.ptr(os_), N.ptr(ol), N.stream_handle(dev))
+        return _view(a, os_, ol, a.valid)
+    return f
+
+
+def _f_trim(mode: int, py):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        args = _args(e, scope, ctx, subst)
+        a = args[0]
+        if len(args) != 1 or not isinstance(a, StrColumn) or not _gpu_str(a):
+            return _host_string_fn(py)(e, scope, ctx, subst)
+        from ..ops import native as N
+        os_ = torch.empty(n, dtype=torch.int64, device=dev)
+        ol = torch.empty(n, dtype=torch.int32, device=dev)
+        N.call("dxa_str_trim", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), n, mode, N.ptr(os_), N.ptr(ol),
+               N.stream_handle(dev))
+        return _view(a, os_, ol, a.valid)
+    return f
+
+
+def _trim_py(chars_mode):
+    def fn(s, t=" "):
+        s, t = str(s), str(t)
+        return s.strip(t) if chars_mode == 3 else s.lstrip(t) if chars_mode == 1 else s.rstrip(t)
+    return fn
+
+
+def _f_char_length(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    (a,) = _args(e, scope, ctx, subst)
+    if isinstance(a, ConstColumn):
+        return ConstColumn(None if a.value is None else len(str(a.value)), "int", n, dev)
+    if not isinstance(a, StrColumn):
+        a = cast_column(a, "string")
+    if not _gpu_str(a):
+        return column_from_pylist([None if v is None else len(v) for v in a.to_pylist()], "int", dev)
+    from ..ops import native as N
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    N.call("dxa_str_numchars", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), n, N.ptr(out), N.stream_handle(dev))
+    return PrimColumn("int", out, a.valid)
+
+
+def _locate_gpu(a: StrColumn, needle: str, start: int, n, dev):
+    from ..ops import native as N
+    b = needle.encode("utf-8")
+    dt = torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    N.call("dxa_str_locate", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), n, N.ptr(dt), len(b), int(start),
+           N.ptr(out), N.stream_handle(dev))
+    r = PrimColumn("int", out, a.valid)
+    r._keep = dt
+    return r
+
+
+def _spark_locate(sub, s, pos=1):
+    pos = int(pos)
+    if pos < 1:
+        return 0
+    sub, s = str(sub), str(s)
+    if sub == "":
+        return 1
+    i = s.find(sub, pos - 1) if pos - 1 <= len(s) else -1
+    return i + 1
+
+
+def _f_instr(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    a, sub = _args(e, scope, ctx, subst)
+    if isinstance(a, StrColumn) and _gpu_str(a) and isinstance(sub, ConstColumn) and sub.value is not None:
+        return _locate_gpu(a, str(sub.value), 1, n, dev)
+    return _host_string_fn(lambda s, x: _spark_locate(x, s, 1), "int")(e, scope, ctx, subst)
+
+
+def _f_locate(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    args = _args(e, scope, ctx, subst)
+    sub, a = args[0], args[1]
+    pos = args[2] if len(args) > 2 else ConstColumn(1, "int", n, dev)
+    if isinstance(a, StrColumn) and _gpu_str(a) and isinstance(sub, ConstColumn) and sub.value is not None and \
+            isinstance(pos, ConstColumn) and pos.value is not None:
+        return _locate_gpu(a, str(sub.value), int(pos.value), n, dev)
+    lists = [x.to_pylist() if not isinstance(x, ConstColumn) else [x.value] * n for x in (sub, a, pos)]
+    out = [None if any(v is None for v in vals) else _spark_locate(*vals) for vals in zip(*lists)]
+    return column_from_pylist(out, "int", dev)
+
+
+def _f_replace(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    args = _args(e, scope, ctx, subst)
+    a = args[0]
+    srch = args[1]
+    rep = args[2] if len(args) > 2 else ConstColumn("", "string", n, dev)
+    if not (isinstance(a, StrColumn) and _gpu_str(a) and isinstance(srch, ConstColumn) and
+            isinstance(rep, ConstColumn) and srch.value is not None and rep.value is not None):
+        return _host_string_fn(lambda s, x, y="": str(s).replace(str(x), str(y)) if str(x) else str(s))(
+            e, scope, ctx, subst)
+    sb, rb = str(srch.value).encode("utf-8"), str(rep.value).encode("utf-8")
+    if not sb:
+        return a
+    from ..ops import native as N
+    from ..ops.strings import _alloc_arena, _offsets
+    st = N.stream_handle(dev)
+    dt = torch.frombuffer(bytearray(sb + b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+    rt = torch.frombuffer(bytearray(rb + b"\0"), dtype=torch.uint8).to(dev, non_blocking=True)
+    lens = torch.empty(n, dtype=torch.int64, device=dev)
+    N.call("dxa_str_replace_len", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), n, N.ptr(dt), len(sb), len(rb),
+           N.ptr(lens), st)
+    off, total = _offsets(lens)
+    dst = _alloc_arena(total, dev)
+    N.call("dxa_str_replace_write", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens), n, N.ptr(dt), len(sb),
+           N.ptr(rt), len(rb), N.ptr(off), N.ptr(dst), st)
+    out = StrColumn(dst, off, lens.to(torch.int32), a.valid)
+    out._keep = (dt, rt)
+    return out
+
+
 def _register():
     reg = register_function
     reg("pow", _binary_double(torch.pow))
@@ -873,8 +1062,20 @@ def _register():
     reg("unhex", _host_string_fn(lambda s: bytes.fromhex(str(s)).decode("utf-8", errors="replace")))
     reg("initcap", _host_string_fn(_initcap))
     reg("repeat", _host_string_fn(lambda s, k: str(s) * max(0, int(k))))
-    reg("left", _host_string_fn(lambda s, k: str(s)[:max(0, int(k))]))
-    reg("right", _host_string_fn(lambda s, k: str(s)[-int(k):] if int(k) > 0 else ""))
+    reg("left", _f_left_right(False))
+    reg("right", _f_left_right(True))
+    reg("substring", _f_substr)
+    reg("substr", _f_substr)
+    reg("trim", _f_trim(3, _trim_py(3)))
+    reg("ltrim", _f_trim(1, _trim_py(1)))
+    reg("rtrim", _f_trim(2, _trim_py(2)))
+    reg("length", _f_char_length)
+    reg("char_length", _f_char_length)
+    reg("character_length", _f_char_length)
+    reg("instr", _f_instr)
+    reg("locate", _f_locate)
+    reg("position", _f_locate)
+    reg("replace", _f_replace)
     reg("translate", _host_string_fn(_translate))
     reg("ascii", _host_string_fn(lambda s: ord(str(s)[0]) if str(s) else 0, "int"))
     reg("get_json_object", _f_get_json_object)

@@ -613,6 +613,193 @@ DXA_API int dxa_ts_format(const int64_t* us, int64_t n, const int32_t* ops, int3
   return (int)hipGetLastError();
 }
 
+// ---- character-level string functions (UTF-8 aware: a character starts at every byte that is not 10xxxxxx) ----
+__device__ __forceinline__ bool utf8_lead(uint8_t b) { return (b & 0xC0) != 0x80; }
+
+// Byte offset of character k (0-based) in s[0, l); l if the string has fewer characters.
+__device__ __forceinline__ int32_t char_to_byte(const uint8_t* s, int32_t l, int64_t k) {
+  if (k <= 0) return 0;
+  int64_t c = -1;
+  for (int32_t i = 0; i < l; ++i) {
+    if (utf8_lead(s[i]) && ++c == k) return i;
+  }
+  return l;
+}
+
+__device__ __forceinline__ int32_t num_chars(const uint8_t* s, int32_t l) {
+  int32_t c = 0;
+  for (int32_t i = 0; i < l; ++i) c += utf8_lead(s[i]);
+  return c;
+}
+
+// substring(str, pos, len) with Spark's UTF8String.substringSQL semantics, as a view (new start / length).
+// len == INT64_MAX: to the end.  pos / len may be per-row (non-null pointer) or constants.
+__global__ void str_substr_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                  const int32_t* __restrict__ lens, int64_t n, const int64_t* __restrict__ pos_col,
+                                  int64_t pos_c, const int64_t* __restrict__ len_col, int64_t len_c,
+                                  int64_t* __restrict__ out_starts, int32_t* __restrict__ out_lens) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    const int64_t pos = pos_col ? pos_col[i] : pos_c;
+    const int64_t length = len_col ? len_col[i] : len_c;
+    int64_t nch = -1;                                      // computed only when needed
+    int64_t start = pos > 0 ? pos - 1 : 0;
+    if (pos < 0) { nch = num_chars(s, l); start = nch + pos; }
+    int64_t end;
+    if (length == INT64_MAX) end = INT64_MAX;
+    else end = start + length;
+    if (start < 0) start = 0;
+    int32_t b0 = 0, b1 = 0;
+    if (start < end) {
+      b0 = char_to_byte(s, l, start);
+      b1 = end == INT64_MAX ? l : char_to_byte(s, l, end);
+      if (b1 < b0) b1 = b0;
+    }
+    out_starts[i] = starts[i] + b0;
+    out_lens[i] = b1 - b0;
+  }
+}
+
+// trim / ltrim / rtrim of ASCII spaces (mode bit 0: left, bit 1: right), as a view.
+__global__ void str_trim_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                const int32_t* __restrict__ lens, int64_t n, int32_t mode,
+                                int64_t* __restrict__ out_starts, int32_t* __restrict__ out_lens) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    int32_t a = 0, b = lens[i];
+    if (mode & 1) while (a < b && s[a] == ' ') ++a;
+    if (mode & 2) while (b > a && s[b - 1] == ' ') --b;
+    out_starts[i] = starts[i] + a;
+    out_lens[i] = b - a;
+  }
+}
+
+__global__ void str_numchars_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                    const int32_t* __restrict__ lens, int64_t n, int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = num_chars(arena + starts[i], lens[i]);
+}
+
+// locate(needle, str, start_char): 1-based character position of the first occurrence at or after character
+// start_char (1-based; < 1 → 0 result), 0 when absent.  instr(str, needle) = locate(needle, str, 1).
+__device__ __forceinline__ int32_t utf8_len(uint8_t b) {
+  return b < 0x80 ? 1 : (b & 0xE0) == 0xC0 ? 2 : (b & 0xF0) == 0xE0 ? 3 : (b & 0xF8) == 0xF0 ? 4 : 1;
+}
+
+// (UTF8String.indexOf(needle, from - 1) + 1, as Spark's StringLocate; an empty needle is found at 1)
+__global__ void str_locate_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                  const int32_t* __restrict__ lens, int64_t n, const uint8_t* __restrict__ d,
+                                  int32_t dl, int64_t from, int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    int64_t r = 0;
+    if (from >= 1) {
+      if (dl == 0) {
+        r = 1;
+      } else {
+        int32_t b = 0;
+        int64_t c = 0;
+        while (b < l && c < from - 1) { b += utf8_len(s[b]); ++c; }
+        while (b + dl <= l) {
+          if (delim_at(s + b, d, dl)) { r = c + 1; break; }
+          b += utf8_len(s[b]);
+          ++c;
+        }
+      }
+    }
+    out[i] = r;
+  }
+}
+
+// replace(str, search, rep) with literal search / replacement: pass 1 writes each row's output length, pass 2
+// (after the host's exclusive scan) writes the bytes.  Non-overlapping, left to right (String.replace).
+__global__ void str_replace_len_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                       const int32_t* __restrict__ lens, int64_t n, const uint8_t* __restrict__ d,
+                                       int32_t dl, int32_t rl, int64_t* __restrict__ out_len) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    int64_t o = 0;
+    for (int32_t k = 0; k < l;) {
+      if (k + dl <= l && delim_at(s + k, d, dl)) { o += rl; k += dl; } else { ++o; ++k; }
+    }
+    out_len[i] = o;
+  }
+}
+
+__global__ void str_replace_write_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                         const int32_t* __restrict__ lens, int64_t n, const uint8_t* __restrict__ d,
+                                         int32_t dl, const uint8_t* __restrict__ rep, int32_t rl,
+                                         const int64_t* __restrict__ off, uint8_t* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    uint8_t* o = dst + off[i];
+    for (int32_t k = 0; k < l;) {
+      if (k + dl <= l && delim_at(s + k, d, dl)) {
+        for (int32_t j = 0; j < rl; ++j) *o++ = rep[j];
+        k += dl;
+      } else {
+        *o++ = s[k++];
+      }
+    }
+  }
+}
+
+DXA_API int dxa_str_substr(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                           const int64_t* pos_col, int64_t pos_c, const int64_t* len_col, int64_t len_c,
+                           int64_t* out_starts, int32_t* out_lens, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_substr_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     n, pos_col, pos_c, len_col, len_c, out_starts, out_lens);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_trim(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n, int32_t mode,
+                         int64_t* out_starts, int32_t* out_lens, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_trim_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens, n,
+                     mode, out_starts, out_lens);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_numchars(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                             int64_t* out, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_numchars_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
+                     lens, n, out);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_locate(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                           const uint8_t* d, int32_t dl, int64_t from, int64_t* out, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_locate_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     n, d, dl, from, out);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_replace_len(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                                const uint8_t* d, int32_t dl, int32_t rl, int64_t* out_len, void* st) {
+  if (n <= 0) return 0;
+  if (dl <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(str_replace_len_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
+                     lens, n, d, dl, rl, out_len);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_str_replace_write(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                                  const uint8_t* d, int32_t dl, const uint8_t* rep, int32_t rl, const int64_t* off,
+                                  uint8_t* dst, void* st) {
+  if (n <= 0) return 0;
+  if (dl <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(str_replace_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
+                     lens, n, d, dl, rep, rl, off, dst);
+  return (int)hipGetLastError();
+}
+
 // parts: host array of k StrPart descriptors (row0 relative to the first part); launches in groups of kMaxStrParts.
 DXA_API int dxa_str_gather_parts(const void* parts, int32_t k, void* st) {
   const StrPart* ps = (const StrPart*)parts;

@@ -167,3 +167,45 @@ def test_rollup_cube_grouping_sets():
     rows, _ = q("SELECT id, COUNT(*) AS c, grouping(id) AS gi FROM T GROUP BY GROUPING SETS ((id), ()) "
                 "HAVING COUNT(*) > 1 ORDER BY gi")
     assert rows == [(2, 2, 0), (None, 4, 1)]
+
+
+def _str_cat(device):
+    t = Table(["s"], [strings_from_pylist(["hello world", "  pad  ", "日本語テキスト", "", None, "aXbXc", "é"], device)])
+    cat = Catalog()
+    cat.register("S", t)
+    return cat
+
+
+STR_QUERIES = [
+    "SELECT substring(s, 2, 3) AS a, substr(s, -3) AS b, substring(s, 0, 2) AS c, substring(s, -9, 3) AS d, "
+    "substring(s, 20) AS e FROM S",
+    "SELECT trim(s) AS a, ltrim(s) AS b, rtrim(s) AS c, left(s, 3) AS d, right(s, 2) AS e, left(s, 0) AS f FROM S",
+    "SELECT length(s) AS a, char_length(s) AS b, instr(s, 'o') AS c, locate('X', s, 3) AS d, locate('', s) AS e, "
+    "instr(s, '語') AS f FROM S",
+    "SELECT replace(s, 'X', '--') AS a, replace(s, 'l') AS b, replace(s, '', 'z') AS c FROM S",
+]
+
+
+def test_character_functions_spark_semantics():
+    rows = [tuple(r) for r in zip(*[c.to_pylist() for c in
+                                    run_sql(STR_QUERIES[0], _str_cat("cpu"), EvalContext()).columns])]
+    assert rows[0] == ("ell", "rld", "he", "llo", "")            # pos 0 reads as 1; -9 on 11 chars → 'llo'
+    assert rows[2] == ("本語テ", "キスト", "日本", "日", "")       # characters, not bytes
+    assert rows[4] == (None,) * 5
+    rows = [tuple(r) for r in zip(*[c.to_pylist() for c in
+                                    run_sql(STR_QUERIES[1], _str_cat("cpu"), EvalContext()).columns])]
+    assert rows[1] == ("pad", "pad  ", "  pad", "  p", "  ", "")
+    rows = [tuple(r) for r in zip(*[c.to_pylist() for c in
+                                    run_sql(STR_QUERIES[2], _str_cat("cpu"), EvalContext()).columns])]
+    assert rows[0] == (11, 11, 5, 0, 1, 0) and rows[2] == (7, 7, 0, 0, 1, 3) and rows[5] == (5, 5, 0, 4, 1, 0)
+    rows = [tuple(r) for r in zip(*[c.to_pylist() for c in
+                                    run_sql(STR_QUERIES[3], _str_cat("cpu"), EvalContext()).columns])]
+    assert rows[5] == ("a--b--c", "aXbXc", "aXbXc") and rows[0][1] == "heo word"
+
+
+@pytest.mark.gpu
+def test_character_functions_gpu_match_cpu(gpu):
+    for sql in STR_QUERIES:
+        cpu = [c.to_pylist() for c in run_sql(sql, _str_cat("cpu"), EvalContext()).columns]
+        dev = [c.to_pylist() for c in run_sql(sql, _str_cat(gpu), EvalContext(device=gpu)).columns]
+        assert cpu == dev, sql
