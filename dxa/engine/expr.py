@@ -1308,7 +1308,18 @@ def _f_concat_ws(e, scope, ctx, subst):
         if i:
             parts.append(sep)
         parts.append(a)
-    # Spark concat_ws skips nulls: host-assisted when any part may be null
+    # Spark concat_ws skips nulls: on the GPU one skip-aware kernel pair; host-assisted elsewhere
+    if dev.type == "cuda" and isinstance(sep, ConstColumn) and sep.value is not None and \
+            not any(isinstance(p, ArrayColumn) for p in args[1:]):
+        from ..ops import strings as S
+        ps = []
+        for p in args[1:]:
+            if isinstance(p, ConstColumn):
+                if p.value is not None:
+                    ps.append(_const_str(p))
+                continue
+            ps.append(p if isinstance(p, StrColumn) else cast_column(p, "string"))
+        return S.concat_ws(_const_str(sep), ps, n, dev)
     if any(not isinstance(p, ConstColumn) and p.valid is not None for p in args[1:]):
         cols = [p.to_pylist() if not isinstance(p, ConstColumn) else [p.value] * n for p in args[1:]]
         s = _const_str(sep)

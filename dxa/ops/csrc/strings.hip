@@ -263,6 +263,57 @@ __global__ void concat_write_kernel(const ConcatPart* __restrict__ parts, int32_
   }
 }
 
+// concat_ws(sep, part_0, …): null parts are skipped and the separator goes between the parts that remain.
+__global__ void concat_ws_len_kernel(const ConcatPart* __restrict__ parts, int32_t k, int64_t n, int32_t sl,
+                                     int64_t* __restrict__ out_len) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t l = 0;
+    int32_t m = 0;
+    for (int32_t p = 0; p < k; ++p) {
+      const ConcatPart& c = parts[p];
+      if (!c.is_lit && c.valid && !c.valid[i]) continue;
+      l += c.is_lit ? c.lit_len : c.lens[i];
+      ++m;
+    }
+    out_len[i] = l + (m > 1 ? (int64_t)(m - 1) * sl : 0);
+  }
+}
+
+__global__ void concat_ws_write_kernel(const ConcatPart* __restrict__ parts, int32_t k, int64_t n,
+                                       const uint8_t* __restrict__ sep, int32_t sl, const int64_t* __restrict__ off,
+                                       uint8_t* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t* d = dst + off[i];
+    bool first = true;
+    for (int32_t p = 0; p < k; ++p) {
+      const ConcatPart& c = parts[p];
+      if (!c.is_lit && c.valid && !c.valid[i]) continue;
+      if (!first)
+        for (int32_t q = 0; q < sl; ++q) *d++ = sep[q];
+      first = false;
+      const uint8_t* s = c.is_lit ? c.lit : c.arena + c.starts[i];
+      const int32_t l = c.is_lit ? c.lit_len : c.lens[i];
+      for (int32_t q = 0; q < l; ++q) d[q] = s[q];
+      d += l;
+    }
+  }
+}
+
+DXA_API int dxa_concat_ws_len(const void* parts, int32_t k, int64_t n, int32_t sl, int64_t* out_len, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(concat_ws_len_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st,
+                     (const ConcatPart*)parts, k, n, sl, out_len);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_concat_ws_write(const void* parts, int32_t k, int64_t n, const uint8_t* sep, int32_t sl,
+                                const int64_t* off, uint8_t* dst, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(concat_ws_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st,
+                     (const ConcatPart*)parts, k, n, sep, sl, off, dst);
+  return (int)hipGetLastError();
+}
+
 __device__ __forceinline__ int i64_digits(int64_t v) {
   uint64_t u = v < 0 ? (0ull - (uint64_t)v) : (uint64_t)v;
   int d = 1;

@@ -272,6 +272,37 @@ def concat_strings(parts: List[Union[str, object]], n: int, device):
     return strings_from_pylist(out, device)
 
 
+def concat_ws(sep: str, parts: List[Union[str, object]], n: int, device):
+    """concat_ws on the device: null column parts are skipped (Spark), the separator joins what remains."""
+    from ..engine.column import StrColumn
+    device = torch.device(device)
+    arr = (_ConcatPart * len(parts))()
+    keep = []
+    for i, p in enumerate(parts):
+        if isinstance(p, str):
+            b = p.encode("utf-8")
+            t = torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8).to(device)
+            keep.append(t)
+            arr[i] = _ConcatPart(0, 0, 0, 0, t.data_ptr(), len(b), 1)
+        else:
+            v = N.u8(p.valid)
+            keep.append(v)
+            arr[i] = _ConcatPart(p.arena.data_ptr(), p.starts.data_ptr(), p.lens.data_ptr(),
+                                 0 if v is None else v.data_ptr(), 0, 0, 0)
+    raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
+    sb = sep.encode("utf-8")
+    st_ = torch.frombuffer(bytearray(sb + b"\0"), dtype=torch.uint8).to(device)
+    lens = torch.empty(n, dtype=torch.int64, device=device)
+    st = N.stream_handle(device)
+    N.call("dxa_concat_ws_len", N.ptr(raw), len(parts), n, len(sb), N.ptr(lens), st)
+    off, total = _offsets(lens)
+    dst = _alloc_arena(total, device)
+    N.call("dxa_concat_ws_write", N.ptr(raw), len(parts), n, N.ptr(st_), len(sb), N.ptr(off), N.ptr(dst), st)
+    col = StrColumn(dst, off, lens.to(torch.int32), None)
+    col._keep = (keep, raw, st_)
+    return col
+
+
 def from_int64(data: torch.Tensor, valid):
     """CAST(long AS STRING)."""
     from ..engine.column import StrColumn, strings_from_pylist

@@ -183,6 +183,7 @@ STR_QUERIES = [
     "SELECT length(s) AS a, char_length(s) AS b, instr(s, 'o') AS c, locate('X', s, 3) AS d, locate('', s) AS e, "
     "instr(s, '語') AS f FROM S",
     "SELECT replace(s, 'X', '--') AS a, replace(s, 'l') AS b, replace(s, '', 'z') AS c FROM S",
+    "SELECT concat_ws('-', s, 'x', s) AS a, concat_ws('', s, NULL, '!') AS b, concat_ws(', ', s) AS c FROM S",
 ]
 
 
@@ -201,6 +202,9 @@ def test_character_functions_spark_semantics():
     rows = [tuple(r) for r in zip(*[c.to_pylist() for c in
                                     run_sql(STR_QUERIES[3], _str_cat("cpu"), EvalContext()).columns])]
     assert rows[5] == ("a--b--c", "aXbXc", "aXbXc") and rows[0][1] == "heo word"
+    rows = [tuple(r) for r in zip(*[c.to_pylist() for c in
+                                    run_sql(STR_QUERIES[4], _str_cat("cpu"), EvalContext()).columns])]
+    assert rows[4] == ("x", "!", "") and rows[5] == ("aXbXc-x-aXbXc", "aXbXc!", "aXbXc")
 
 
 @pytest.mark.gpu
