@@ -775,6 +775,14 @@ def cast_column(col: Column, to: str) -> Column:
         if to == "timestamp":
             from ..ops import strings as S
             return S.to_timestamp(col)
+        if to in ("int", "long", "double", "float", "decimal") and col.starts.is_cuda:
+            from ..ops import native as N
+            mode = {"long": 0, "int": 1}.get(to, 2)
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+            ok = torch.empty(n, dtype=torch.uint8, device=dev)
+            N.call("dxa_str_to_num", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), N.ptr(N.u8(col.valid)),
+                   n, mode, N.ptr(out), N.ptr(ok), N.stream_handle(dev))
+            return PrimColumn(to, out.view(torch.float64) if mode == 2 else out, ok.view(torch.bool))
         vals = col.to_pylist()
         conv = [_cast_value(v, "string", to) for v in vals]
         return column_from_pylist(conv, to, dev)
@@ -821,6 +829,11 @@ def _storage_of(v, dtype):
     return v
 
 
+_CAST_WS = "".join(chr(c) for c in range(33))           # Spark trims bytes <= ' ' before numeric casts
+_INT_STR = re.compile(r"^([+-]?)(\d*)(?:\.(\d*))?$")
+_DBL_STR = re.compile(r"^[+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?$")
+
+
 def _cast_value(v, frm, to):
     if v is None:
         return None
@@ -838,16 +851,28 @@ def _cast_value(v, frm, to):
             return str(v)
         if to in ("int", "long"):
             if isinstance(v, str):
-                s = v.strip()
-                try:
-                    return int(s)
-                except ValueError:
-                    return int(float(s))
+                # Spark (non-ANSI): [+-]digits[.digits] after trimming; the fraction truncates; no exponent
+                m = _INT_STR.match(v.strip(_CAST_WS))
+                if not m or not (m.group(2) or m.group(3)):
+                    return None
+                r = int((m.group(1) or "") + (m.group(2) or "0"))
+                lo, hi = (-2**31, 2**31 - 1) if to == "int" else (-2**63, 2**63 - 1)
+                return r if lo <= r <= hi else None
             if frm == "timestamp":
                 return int(v) // 1_000_000
             return int(v)
         if to in ("double", "float", "decimal"):
-            return float(v.strip()) if isinstance(v, str) else float(v)
+            if isinstance(v, str):
+                t = v.strip(_CAST_WS)
+                low = t.lower()
+                if low in ("inf", "+inf", "infinity", "+infinity"):
+                    return float("inf")
+                if low in ("-inf", "-infinity"):
+                    return float("-inf")
+                if low == "nan":
+                    return float("nan")
+                return float(t) if _DBL_STR.match(t) else None
+            return float(v)
         if to == "boolean":
             if isinstance(v, str):
                 s = v.strip().lower()

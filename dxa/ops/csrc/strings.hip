@@ -5,6 +5,7 @@
 // Strings are views (start, len) into a byte arena; producing kernels are two-pass (length, then exclusive scan
 // on the stream, then write), so no kernel ever needs dynamic allocation.
 #include "dxa_common.h"
+#include "pow10_dd.h"
 #include <stdlib.h>
 
 namespace {
@@ -848,6 +849,110 @@ DXA_API int dxa_str_replace_write(const uint8_t* arena, const int64_t* starts, c
   if (dl <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(str_replace_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
                      lens, n, d, dl, rep, rl, off, dst);
+  return (int)hipGetLastError();
+}
+
+// CAST(string AS BIGINT | INT | DOUBLE) with Spark's non-ANSI semantics: surrounding whitespace (<= ' ') ignored;
+// integers: [+-]digits[.digits] (the fraction truncates; no exponent), out of range → null; doubles: decimal with
+// optional exponent, or inf / infinity / nan (any case, optional sign).  mode 0 long, 1 int, 2 double.
+__device__ __forceinline__ bool ci_eq(const uint8_t* s, int32_t l, const char* w) {
+  int32_t k = 0;
+  for (; w[k]; ++k)
+    if (k >= l || (s[k] | 0x20) != w[k]) return false;
+  return k == l;
+}
+
+__global__ void str_to_num_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                  const int32_t* __restrict__ lens, const uint8_t* __restrict__ valid, int64_t n,
+                                  int32_t mode, int64_t* __restrict__ out, uint8_t* __restrict__ out_ok) {
+  const double kP10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                           1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    out[i] = 0;
+    out_ok[i] = 0;
+    if (valid && !valid[i]) continue;
+    const uint8_t* s = arena + starts[i];
+    int32_t a = 0, b = lens[i];
+    while (a < b && s[a] <= ' ') ++a;
+    while (b > a && s[b - 1] <= ' ') --b;
+    if (a >= b) continue;
+    bool neg = false;
+    int32_t p = a;
+    if (s[p] == '+' || s[p] == '-') { neg = s[p] == '-'; ++p; }
+    if (mode == 2) {
+      const int32_t l = b - p;
+      if (ci_eq(s + p, l, "inf") || ci_eq(s + p, l, "infinity")) {
+        out[i] = __double_as_longlong(neg ? -__builtin_inf() : __builtin_inf());
+        out_ok[i] = 1;
+        continue;
+      }
+      if (ci_eq(s + p, l, "nan") && p == a) {
+        out[i] = __double_as_longlong(__builtin_nan(""));
+        out_ok[i] = 1;
+        continue;
+      }
+    }
+    uint64_t mant = 0;
+    int nd = 0, exp10 = 0, digits = 0;
+    bool lost = false;
+    for (; p < b && s[p] - '0' < 10u; ++p, ++digits) {
+      if (nd < 19) { mant = mant * 10 + (s[p] - '0'); if (mant) ++nd; }
+      else { ++exp10; lost = true; }
+    }
+    int fdigits = 0;
+    if (p < b && s[p] == '.') {
+      ++p;
+      for (; p < b && s[p] - '0' < 10u; ++p, ++fdigits) {
+        if (mode == 2 && nd < 19) { mant = mant * 10 + (s[p] - '0'); if (mant) ++nd; --exp10; }
+      }
+    }
+    if (digits + fdigits == 0) continue;
+    if (mode == 2 && p < b && (s[p] | 0x20) == 'e') {
+      ++p;
+      bool eneg = false;
+      if (p < b && (s[p] == '+' || s[p] == '-')) { eneg = s[p] == '-'; ++p; }
+      int e = 0, ed = 0;
+      for (; p < b && s[p] - '0' < 10u; ++p, ++ed)
+        if (e < 100000) e = e * 10 + (s[p] - '0');
+      if (!ed) continue;
+      exp10 += eneg ? -e : e;
+    }
+    if (p != b) continue;                                 // trailing garbage
+    if (mode == 2) {
+      double d = (double)mant;
+      if (mant == 0) d = 0.0;
+      else if (mant < (1ull << 53) && exp10 >= 0 && exp10 <= 22) d = d * kP10[exp10];
+      else if (mant < (1ull << 53) && exp10 < 0 && exp10 >= -22) d = d / kP10[-exp10];
+      else if (exp10 > DXA_POW10_DD_MAX) d = __builtin_inf();
+      else if (exp10 < DXA_POW10_DD_MIN) d = 0.0;
+      else {
+#pragma clang fp contract(off)
+        const bool wide = mant >= (1ull << 53);
+        const double mh = (double)(wide ? (mant & ~0x7FFull) : mant), ml = wide ? (double)(mant & 0x7FFull) : 0.0;
+        const double ph = kPow10dd[exp10 - DXA_POW10_DD_MIN][0], pl = kPow10dd[exp10 - DXA_POW10_DD_MIN][1];
+        const double h = mh * ph;
+        const double err = __builtin_fma(mh, ph, -h) + (mh * pl + ml * ph);
+        d = h + err;
+        if (exp10 < DXA_POW10_DD_SCALED_BELOW) d = __builtin_ldexp(d, -DXA_POW10_DD_SCALE);
+      }
+      out[i] = __double_as_longlong(neg ? -d : d);
+      out_ok[i] = 1;
+      continue;
+    }
+    if (lost) continue;                                   // more than 19 integer digits
+    const uint64_t lim = mode == 1 ? (neg ? 2147483648ull : 2147483647ull)
+                                   : (neg ? 9223372036854775808ull : 9223372036854775807ull);
+    if (mant > lim) continue;
+    out[i] = neg ? (int64_t)(0ull - mant) : (int64_t)mant;
+    out_ok[i] = 1;
+  }
+}
+
+DXA_API int dxa_str_to_num(const uint8_t* arena, const int64_t* starts, const int32_t* lens, const uint8_t* valid,
+                           int64_t n, int32_t mode, int64_t* out, uint8_t* out_ok, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_to_num_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     valid, n, mode, out, out_ok);
   return (int)hipGetLastError();
 }
 

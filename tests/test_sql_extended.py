@@ -213,3 +213,32 @@ def test_character_functions_gpu_match_cpu(gpu):
         cpu = [c.to_pylist() for c in run_sql(sql, _str_cat("cpu"), EvalContext()).columns]
         dev = [c.to_pylist() for c in run_sql(sql, _str_cat(gpu), EvalContext(device=gpu)).columns]
         assert cpu == dev, sql
+
+
+CAST_VALUES = ["12", " 12 ", "1.9", "-0.5", "1e3", "+7", "", ".", "9223372036854775807", "9223372036854775808",
+               "abc", "2147483648", "-2147483648", "Infinity", "-inf", "NaN", ".5", "5.", "1.5e-300", "\t3\n", None]
+
+
+def _cast_rows(device):
+    t = Table(["s"], [strings_from_pylist(CAST_VALUES, device)])
+    cat = Catalog()
+    cat.register("C", t)
+    out = run_sql("SELECT CAST(s AS BIGINT) AS l, CAST(s AS INT) AS i, CAST(s AS DOUBLE) AS d FROM C", cat,
+                  EvalContext(device=device))
+    return [tuple(r) for r in zip(*[c.to_pylist() for c in out.columns])]
+
+
+def test_string_to_number_casts():
+    rows = _cast_rows("cpu")
+    assert rows[0] == (12, 12, 12.0) and rows[2] == (1, 1, 1.9) and rows[3] == (0, 0, -0.5)
+    assert rows[4] == (None, None, 1000.0) and rows[9][:2] == (None, None) and rows[11] == (2147483648, None,
+                                                                                              2147483648.0)
+    assert rows[13][2] == float("inf") and rows[14][2] == float("-inf") and math.isnan(rows[15][2])
+    assert rows[19] == (3, 3, 3.0) and rows[20] == (None, None, None)
+
+
+@pytest.mark.gpu
+def test_string_to_number_casts_gpu_match_cpu(gpu):
+    def canon(rows):
+        return [tuple("nan" if isinstance(x, float) and x != x else x for x in r) for r in rows]
+    assert canon(_cast_rows(gpu)) == canon(_cast_rows("cpu"))
