@@ -760,6 +760,18 @@ def cast_column(col: Column, to: str) -> Column:
             if col.dtype in ("int", "long"):
                 from ..ops import strings as S
                 return S.from_int64(col.data, col.valid)
+            if col.dtype in ("double", "float", "decimal") and col.data.is_cuda:
+                from ..ops import native as N
+                from ..ops.strings import _alloc_arena, _offsets
+                d = col.data.to(torch.float64).contiguous()
+                v = N.u8(col.valid)
+                st = N.stream_handle(dev)
+                lens = torch.empty(n, dtype=torch.int64, device=dev)
+                N.call("dxa_f64_str_len", N.ptr(d), N.ptr(v), n, N.ptr(lens), st)
+                off, total = _offsets(lens)
+                arena = _alloc_arena(total, dev)
+                N.call("dxa_f64_str_write", N.ptr(d), N.ptr(v), n, N.ptr(off), N.ptr(arena), st)
+                return StrColumn(arena, off, lens.to(torch.int32), col.valid)
             if col.dtype == "boolean":
                 return choose(torch.where(col.data, 0, 1).to(torch.int64),
                               [ConstColumn("true", "string", n, dev), ConstColumn("false", "string", n, dev)],

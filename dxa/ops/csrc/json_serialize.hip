@@ -419,3 +419,38 @@ DXA_API int dxa_java_double_hostcheck(const double* v, int64_t n, uint8_t* out, 
   }
   return 0;
 }
+
+// CAST(double AS STRING): Java Double.toString text (Spark's cast), two passes — lengths, then bytes at the
+// host-scanned offsets.  Invalid rows get length 0.
+namespace {
+__global__ void f64_str_len_kernel(const double* __restrict__ v, const uint8_t* __restrict__ valid, int64_t n,
+                                   int64_t* __restrict__ out_len) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out_len[i] = (valid && !valid[i]) ? 0 : dxa::ryu::java_double(v[i], nullptr, c_ryu_inv, c_ryu_pos);
+}
+
+__global__ void f64_str_write_kernel(const double* __restrict__ v, const uint8_t* __restrict__ valid, int64_t n,
+                                     const int64_t* __restrict__ off, uint8_t* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    char buf[32];
+    const int l = dxa::ryu::java_double(v[i], buf, c_ryu_inv, c_ryu_pos);
+    for (int k = 0; k < l; ++k) dst[off[i] + k] = (uint8_t)buf[k];
+  }
+}
+}  // namespace
+
+DXA_API int dxa_f64_str_len(const double* v, const uint8_t* valid, int64_t n, int64_t* out_len, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(f64_str_len_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, valid, n,
+                     out_len);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_f64_str_write(const double* v, const uint8_t* valid, int64_t n, const int64_t* off, uint8_t* dst,
+                              void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(f64_str_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, valid, n,
+                     off, dst);
+  return (int)hipGetLastError();
+}

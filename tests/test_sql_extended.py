@@ -242,3 +242,18 @@ def test_string_to_number_casts_gpu_match_cpu(gpu):
     def canon(rows):
         return [tuple("nan" if isinstance(x, float) and x != x else x for x in r) for r in rows]
     assert canon(_cast_rows(gpu)) == canon(_cast_rows("cpu"))
+
+
+@pytest.mark.gpu
+def test_double_to_string_cast_gpu_match_cpu(gpu):
+    vals = [0.0, -0.0, 1.0, 0.1, 1e7, 9999999.0, 1e-3, 0.00099, 123456.789, -2.5e-300, 1.7976931348623157e308,
+            5e-324, float("nan"), float("inf"), float("-inf"), None, 100.0, 3.0e10]
+    outs = []
+    for dev in ("cpu", gpu):
+        t = Table(["d"], [column_from_pylist(vals, "double", dev)])
+        cat = Catalog()
+        cat.register("D", t)
+        outs.append(run_sql("SELECT CAST(d AS STRING) AS s, CONCAT('v=', CAST(d AS STRING)) AS c FROM D", cat,
+                            EvalContext(device=dev)).columns[0].to_pylist())
+    assert outs[0] == outs[1]
+    assert outs[0][:4] == ["0.0", "-0.0", "1.0", "0.1"] and outs[0][4] == "1.0E7" and outs[0][15] is None
