@@ -596,6 +596,8 @@ def _like(e: A.Like, scope, ctx, subst):
                 r = S.cmp_literal(v, body, "endswith")
             else:
                 r = S.cmp_literal(v, body, "contains")
+        elif isinstance(v, StrColumn) and v.starts.is_cuda:
+            r = S.like(v, _like_tokens(pat))
         else:
             rx = re.compile(_like_to_regex(pat), re.S)
             r = torch.tensor([s is not None and rx.fullmatch(s) is not None for s in v.to_pylist()],
@@ -606,6 +608,27 @@ def _like(e: A.Like, scope, ctx, subst):
                          device=dev)
     out = bool_col(r, v.valid)
     return evaluate_not(out, n, dev) if e.negated else out
+
+
+def _like_tokens(p: str) -> List[int]:
+    """LIKE pattern → device tokens: literal bytes, 256 for '_', 257 for '%' (escapes resolved)."""
+    out: List[int] = []
+    i = 0
+    while i < len(p):
+        c = p[i]
+        if c == "\\" and i + 1 < len(p):
+            out.extend(p[i + 1].encode("utf-8"))
+            i += 2
+            continue
+        if c == "%":
+            if not out or out[-1] != 257:
+                out.append(257)
+        elif c == "_":
+            out.append(256)
+        else:
+            out.extend(c.encode("utf-8"))
+        i += 1
+    return out
 
 
 def _like_to_regex(p: str) -> str:

@@ -956,6 +956,47 @@ DXA_API int dxa_str_to_num(const uint8_t* arena, const int64_t* starts, const in
   return (int)hipGetLastError();
 }
 
+// General LIKE on the device.  Pattern tokens (int16): 0..255 a literal byte, 256 '_' (one UTF-8 character),
+// 257 '%' (any sequence); escapes are resolved by the host.  Greedy match with one backtrack point (the last '%'):
+// linear in practice, exact for LIKE's two wildcards.
+__global__ void str_like_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                const int32_t* __restrict__ lens, int64_t n, const int16_t* __restrict__ tok,
+                                int32_t m, uint8_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    int32_t si = 0, pi = 0, star_p = -1, star_s = 0;
+    bool ok = true;
+    while (si < l) {
+      const int32_t t = pi < m ? tok[pi] : -1;
+      if (t == 256) { si += utf8_len(s[si]); ++pi; continue; }
+      if (t >= 0 && t < 256 && s[si] == (uint8_t)t) { ++si; ++pi; continue; }
+      if (t == 257) { star_p = pi++; star_s = si; continue; }
+      if (star_p >= 0) {
+        pi = star_p + 1;
+        star_s += utf8_len(s[star_s]);
+        si = star_s;
+        continue;
+      }
+      ok = false;
+      break;
+    }
+    if (ok) {
+      while (pi < m && tok[pi] == 257) ++pi;
+      ok = pi == m && si <= l;
+    }
+    out[i] = ok;
+  }
+}
+
+DXA_API int dxa_str_like(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                         const int16_t* tok, int32_t m, uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(str_like_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     n, tok, m, out);
+  return (int)hipGetLastError();
+}
+
 // parts: host array of k StrPart descriptors (row0 relative to the first part); launches in groups of kMaxStrParts.
 DXA_API int dxa_str_gather_parts(const void* parts, int32_t k, void* st) {
   const StrPart* ps = (const StrPart*)parts;

@@ -180,6 +180,17 @@ def cmp_literal(col, lit: str, op: str) -> torch.Tensor:
     return torch.tensor([f(s) for s in vals], dtype=torch.bool)
 
 
+def like(col, tokens: List[int]) -> torch.Tensor:
+    """General LIKE on the device (tokens from expr._like_tokens) → bool mask."""
+    n = col.length
+    out = torch.empty(n, dtype=torch.bool, device=col.device)
+    if n:
+        tk = torch.tensor(tokens or [0], dtype=torch.int16).to(col.device, non_blocking=True)
+        N.call("dxa_str_like", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(tk), len(tokens),
+               N.ptr(out.view(torch.uint8)), N.stream_handle(col.device))
+    return out
+
+
 def _raw_bytes(col) -> List[bytes]:
     arena = col.arena.cpu().numpy().tobytes()
     return [arena[s:s + l] for s, l in zip(col.starts.cpu().tolist(), col.lens.cpu().tolist())]

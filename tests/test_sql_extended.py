@@ -257,3 +257,21 @@ def test_double_to_string_cast_gpu_match_cpu(gpu):
                             EvalContext(device=dev)).columns[0].to_pylist())
     assert outs[0] == outs[1]
     assert outs[0][:4] == ["0.0", "-0.0", "1.0", "0.1"] and outs[0][4] == "1.0E7" and outs[0][15] is None
+
+
+LIKE_PATTERNS = ["h%o w_rld", "%o%o%", "_", "__", "%", "", "a_b%", "%X_c", "日%ト", "%本_テ%", "%\\%%", "p_d", "%d  "]
+
+
+@pytest.mark.gpu
+def test_general_like_gpu_match_cpu(gpu):
+    vals = ["hello world", "  pad  ", "日本語テキスト", "", None, "aXbXc", "é", "50% off", "pad", "a_b_c"]
+    for pat in LIKE_PATTERNS:
+        outs = []
+        for dev in ("cpu", gpu):
+            t = Table(["s"], [strings_from_pylist(vals, dev)])
+            cat = Catalog()
+            cat.register("L", t)
+            p = pat.replace("'", "''")
+            outs.append(run_sql(f"SELECT s LIKE '{p}' AS m, s NOT LIKE '{p}' AS nm FROM L", cat,
+                                EvalContext(device=dev)).columns[0].to_pylist())
+        assert outs[0] == outs[1], pat
