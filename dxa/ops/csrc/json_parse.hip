@@ -15,7 +15,7 @@
 // → every field of the row null and row_ok=0 (the reference is "tolerant to mismatched input schema").
 #include "dxa_common.h"
 #include <type_traits>
-#include "pow10_dd.h"
+#include "decimal_dd.h"
 
 namespace {
 
@@ -415,7 +415,8 @@ __device__ __forceinline__ int64_t unescape_inplace(Reader& r, int64_t s, int64_
 // Run of decimal digits at r.p, accumulated into (mant, nd, exp10) exactly as a digit-serial loop would: at most
 // 19 significant digits kept (leading zeros are not significant); integer-part digits beyond that raise exp10 and
 // set `lost`; fraction digits beyond it are dropped.  Eight characters per step (SWAR digit test + conversion).
-__device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, int& exp10, bool& lost, bool frac) {
+__device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, int& exp10, bool& lost, bool frac,
+                                            uint64_t& tail, int& nt) {
   bool any = false;
   while (r.p < r.end) {
     const uint64_t x = r.load8(r.p);
@@ -447,9 +448,9 @@ __device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, 
           mant = mant * 10 + (c - '0');
           if (mant) ++nd;
           if (frac) --exp10;
-        } else if (!frac) {
-          ++exp10;
-          lost = true;
+        } else {
+          if (!frac) { ++exp10; lost = true; }
+          if (nt < 19) { tail = tail * 10 + (c - '0'); ++nt; }   // the next 19 digits, for the rounding
         }
       }
       r.p += k;
@@ -464,15 +465,15 @@ __device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overf
   bool neg = false;
   if (r.cur() == '-') { neg = true; ++r.p; }
   if (r.cur() == '0' && r.p + 1 < r.end && is_digit(r.at(r.p + 1))) return false;    // JSON: no leading zeros
-  uint64_t mant = 0;
-  int nd = 0, exp10 = 0;
+  uint64_t mant = 0, tail = 0;
+  int nd = 0, exp10 = 0, nt = 0;
   bool lost = false;
   is_int = true;
-  if (!scan_digits(r, mant, nd, exp10, lost, false)) return false;
+  if (!scan_digits(r, mant, nd, exp10, lost, false, tail, nt)) return false;
   if (r.p < r.end && r.at(r.p) == '.') {
     is_int = false;
     ++r.p;
-    if (!scan_digits(r, mant, nd, exp10, lost, true)) return false;
+    if (!scan_digits(r, mant, nd, exp10, lost, true, tail, nt)) return false;
   }
   if (r.p < r.end && (r.at(r.p) | 0x20u) == 'e') {
     is_int = false;
@@ -497,24 +498,13 @@ __device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overf
     iv = neg ? (int64_t)(0ull - mant) : (int64_t)mant;
   }
   double d = (double)mant;
-  if (exp10 != 0 || mant >= (1ull << 53)) {
-    if (mant < (1ull << 53) && exp10 > 0 && exp10 <= 22) d = d * kPow10[exp10];           // exact operands
-    else if (mant < (1ull << 53) && exp10 < 0 && exp10 >= -22) d = d / kPow10[-exp10];
+  if (exp10 != 0 || mant >= (1ull << 53) || tail != 0) {
+    if (tail == 0 && mant < (1ull << 53) && exp10 > 0 && exp10 <= 22) d = d * kPow10[exp10];   // exact operands
+    else if (tail == 0 && mant < (1ull << 53) && exp10 < 0 && exp10 >= -22) d = d / kPow10[-exp10];
     else if (mant == 0) d = 0.0;
     else if (exp10 > DXA_POW10_DD_MAX) d = __builtin_inf();
     else if (exp10 < DXA_POW10_DD_MIN) d = 0.0;
-    else {
-      // mantissa (exact as hi + lo) × 10^exp10 (double-double) with one final rounding.  No contraction: fusing
-      // h = mh*ph into the final add would count the product's rounding error twice
-#pragma clang fp contract(off)
-      const bool wide = mant >= (1ull << 53);
-      const double mh = (double)(wide ? (mant & ~0x7FFull) : mant), ml = wide ? (double)(mant & 0x7FFull) : 0.0;
-      const double ph = kPow10dd[exp10 - DXA_POW10_DD_MIN][0], pl = kPow10dd[exp10 - DXA_POW10_DD_MIN][1];
-      const double h = mh * ph;
-      const double err = __builtin_fma(mh, ph, -h) + (mh * pl + ml * ph);
-      d = h + err;
-      if (exp10 < DXA_POW10_DD_SCALED_BELOW) d = __builtin_ldexp(d, -DXA_POW10_DD_SCALE);   // exact power-of-2 scale
-    }
+    else d = dxa_decimal_to_double(mant, exp10, tail, nt);
   }
   dv = neg ? -d : d;
   return true;

@@ -5,7 +5,7 @@
 // Strings are views (start, len) into a byte arena; producing kernels are two-pass (length, then exclusive scan
 // on the stream, then write), so no kernel ever needs dynamic allocation.
 #include "dxa_common.h"
-#include "pow10_dd.h"
+#include "decimal_dd.h"
 #include <stdlib.h>
 
 namespace {
@@ -892,18 +892,20 @@ __global__ void str_to_num_kernel(const uint8_t* __restrict__ arena, const int64
         continue;
       }
     }
-    uint64_t mant = 0;
-    int nd = 0, exp10 = 0, digits = 0;
+    uint64_t mant = 0, tail = 0;                          // first 19 significant digits, the next 19
+    int nd = 0, exp10 = 0, digits = 0, nt = 0;
     bool lost = false;
     for (; p < b && s[p] - '0' < 10u; ++p, ++digits) {
       if (nd < 19) { mant = mant * 10 + (s[p] - '0'); if (mant) ++nd; }
-      else { ++exp10; lost = true; }
+      else { ++exp10; lost = true; if (nt < 19) { tail = tail * 10 + (s[p] - '0'); ++nt; } }
     }
     int fdigits = 0;
     if (p < b && s[p] == '.') {
       ++p;
       for (; p < b && s[p] - '0' < 10u; ++p, ++fdigits) {
-        if (mode == 2 && nd < 19) { mant = mant * 10 + (s[p] - '0'); if (mant) ++nd; --exp10; }
+        if (mode != 2) continue;
+        if (nd < 19) { mant = mant * 10 + (s[p] - '0'); if (mant) ++nd; --exp10; }
+        else if (nt < 19) { tail = tail * 10 + (s[p] - '0'); ++nt; }
       }
     }
     if (digits + fdigits == 0) continue;
@@ -921,20 +923,11 @@ __global__ void str_to_num_kernel(const uint8_t* __restrict__ arena, const int64
     if (mode == 2) {
       double d = (double)mant;
       if (mant == 0) d = 0.0;
-      else if (mant < (1ull << 53) && exp10 >= 0 && exp10 <= 22) d = d * kP10[exp10];
-      else if (mant < (1ull << 53) && exp10 < 0 && exp10 >= -22) d = d / kP10[-exp10];
+      else if (tail == 0 && mant < (1ull << 53) && exp10 >= 0 && exp10 <= 22) d = d * kP10[exp10];
+      else if (tail == 0 && mant < (1ull << 53) && exp10 < 0 && exp10 >= -22) d = d / kP10[-exp10];
       else if (exp10 > DXA_POW10_DD_MAX) d = __builtin_inf();
       else if (exp10 < DXA_POW10_DD_MIN) d = 0.0;
-      else {
-#pragma clang fp contract(off)
-        const bool wide = mant >= (1ull << 53);
-        const double mh = (double)(wide ? (mant & ~0x7FFull) : mant), ml = wide ? (double)(mant & 0x7FFull) : 0.0;
-        const double ph = kPow10dd[exp10 - DXA_POW10_DD_MIN][0], pl = kPow10dd[exp10 - DXA_POW10_DD_MIN][1];
-        const double h = mh * ph;
-        const double err = __builtin_fma(mh, ph, -h) + (mh * pl + ml * ph);
-        d = h + err;
-        if (exp10 < DXA_POW10_DD_SCALED_BELOW) d = __builtin_ldexp(d, -DXA_POW10_DD_SCALE);
-      }
+      else d = dxa_decimal_to_double(mant, exp10, tail, nt);
       out[i] = __double_as_longlong(neg ? -d : d);
       out_ok[i] = 1;
       continue;

@@ -137,3 +137,27 @@ def test_gpu_parser_matches_reference(gpu, seed):
             if x != y and not (isinstance(x, float) and isinstance(y, float) and x != x and y != y):
                 bad.append((path, i, x, y))
     assert not bad, [(p, x, y, recs[i]) for p, i, x, y in bad[:4]]
+
+
+def _json_number(rnd):
+    s = rnd.choice(["", "-"]) + rnd.choice(["0"] + [str(rnd.randint(1, 9)) + "".join(
+        rnd.choice("0123456789") for _ in range(rnd.randint(0, 24)))])
+    if rnd.random() < 0.5:
+        s += "." + "".join(rnd.choice("0123456789") for _ in range(rnd.randint(1, 20)))
+    if rnd.random() < 0.5:
+        s += rnd.choice("eE") + rnd.choice(["", "-", "+"]) + str(rnd.randint(0, 420))
+    return s
+
+
+def test_gpu_number_text_matches_reference(gpu):
+    """Decimal text → double / long over long mantissas and exponents past both ends of the double range."""
+    rnd = random.Random(5)
+    recs = [('{"b":%s,"a":%s}' % (_json_number(rnd), _json_number(rnd))).encode() for _ in range(20000)]
+    plan = ParsePlan(SCHEMA)
+    cpu_raw, cpu_ok = parse(*frame_records(recs), plan)
+    gpu_raw, gpu_ok = parse(*frame_records(recs, device=gpu), plan)
+    assert torch.equal(cpu_ok, gpu_ok.cpu())
+    bad = []
+    for (path, a), (_, b) in zip(_leaves(cpu_raw), _leaves(gpu_raw)):
+        bad += [(path, recs[i], x, y) for i, (x, y) in enumerate(zip(a, b)) if x != y]
+    assert not bad, bad[:4]

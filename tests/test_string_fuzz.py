@@ -1,0 +1,134 @@
+"""Differential fuzzing of the device string kernels (strings.hip, json_serialize.hip) against the engine's CPU
+reference: random UTF-8 strings over a small alphabet (so that patterns and needles actually hit) through LIKE,
+substring / left / right / trim, instr / locate, replace, concat_ws, CAST(string AS BIGINT/INT/DOUBLE) and
+CAST(double AS STRING) over random bit patterns.  The CPU side is checked against Python's own semantics first."""
+import math
+import random
+import re
+import struct
+
+import pytest
+
+from dxa.engine.column import Table, column_from_pylist, strings_from_pylist
+from dxa.engine.expr import EvalContext
+from dxa.engine.query import Catalog, run_sql
+
+_ALPHA = ["a", "b", "X", " ", "\t", "é", "日", "%", "_", "\\"]
+N = 400
+
+
+def _rand_str(rnd, k=12):
+    if rnd.random() < 0.05:
+        return None
+    return "".join(rnd.choice(_ALPHA) for _ in range(rnd.randint(0, k)))
+
+
+def _rand_pattern(rnd):
+    out = []
+    for _ in range(rnd.randint(0, 6)):
+        r = rnd.random()
+        out.append("%" if r < 0.25 else "_" if r < 0.4 else "\\%" if r < 0.45 else "\\_" if r < 0.5 else
+                   rnd.choice(["a", "b", "X", " ", "é", "日"]))
+    return "".join(out)
+
+
+def _like_regex(p):
+    rx, i = [], 0
+    while i < len(p):
+        ch = p[i]
+        if ch == "\\" and i + 1 < len(p):
+            rx.append(re.escape(p[i + 1]))
+            i += 2
+            continue
+        rx.append(".*" if ch == "%" else "." if ch == "_" else re.escape(ch))
+        i += 1
+    return re.compile("".join(rx), re.S)
+
+
+def _run(sql, vals, device, dtype="string"):
+    col = strings_from_pylist(vals, device) if dtype == "string" else column_from_pylist(vals, dtype, device)
+    cat = Catalog()
+    cat.register("F", Table(["s"], [col]))
+    return [c.to_pylist() for c in run_sql(sql, cat, EvalContext(device=device)).columns]
+
+
+def _q(s):
+    return s.replace("\\", "\\\\").replace("'", "\\'")
+
+
+def test_like_cpu_matches_regex():
+    rnd = random.Random(7)
+    vals = [_rand_str(rnd) for _ in range(N)]
+    for _ in range(20):
+        pat = _rand_pattern(rnd)
+        got = _run(f"SELECT s LIKE '{_q(pat)}' AS m FROM F", vals, "cpu")[0]
+        rx = _like_regex(pat)
+        assert got == [None if v is None else bool(rx.fullmatch(v)) for v in vals], pat
+
+
+@pytest.mark.gpu
+def test_like_fuzz_gpu_match_cpu(gpu):
+    rnd = random.Random(11)
+    vals = [_rand_str(rnd, 16) for _ in range(N)]
+    for _ in range(60):
+        pat = _rand_pattern(rnd)
+        sql = f"SELECT s LIKE '{_q(pat)}' AS m FROM F"
+        assert _run(sql, vals, gpu) == _run(sql, vals, "cpu"), pat
+
+
+@pytest.mark.gpu
+def test_character_functions_fuzz_gpu_match_cpu(gpu):
+    rnd = random.Random(13)
+    vals = [_rand_str(rnd) for _ in range(N)]
+    for _ in range(25):
+        p, n = rnd.randint(-14, 14), rnd.randint(-2, 14)
+        a, b = rnd.choice(["a", "X", "é", "日", "a ", "", "%_"]), rnd.choice(["", "-", "日本", "zz"])
+        k = rnd.randint(-1, 14)
+        sql = (f"SELECT substring(s, {p}, {n}) AS a, substr(s, {p}) AS b, left(s, {n}) AS c, right(s, {n}) AS d, "
+               f"trim(s) AS e, ltrim(s) AS f, rtrim(s) AS g, length(s) AS h, instr(s, '{a}') AS i, "
+               f"locate('{a}', s, {k}) AS j, replace(s, '{a}', '{b}') AS k, concat_ws('{b}', s, '{a}', s) AS l "
+               f"FROM F")
+        assert _run(sql, vals, gpu) == _run(sql, vals, "cpu"), sql
+
+
+def _rand_num_str(rnd):
+    parts = rnd.choice([["", " ", "\t"], [""]])
+    s = rnd.choice(parts) + rnd.choice(["", "+", "-"])
+    s += "".join(rnd.choice("0123456789") for _ in range(rnd.randint(0, 22)))
+    if rnd.random() < 0.4:
+        s += "." + "".join(rnd.choice("0123456789") for _ in range(rnd.randint(0, 6)))
+    if rnd.random() < 0.2:
+        s += rnd.choice("eE") + rnd.choice(["", "-", "+"]) + str(rnd.randint(0, 400))
+    if rnd.random() < 0.1:
+        s += rnd.choice(["x", " ", "d", "f", "L"])
+    return s
+
+
+@pytest.mark.gpu
+def test_string_to_number_fuzz_gpu_match_cpu(gpu):
+    rnd = random.Random(17)
+    vals = [_rand_num_str(rnd) for _ in range(2 * N)] + ["Infinity", "-Infinity", "NaN", "inf", "nan"]
+    sql = "SELECT CAST(s AS BIGINT) AS l, CAST(s AS INT) AS i, CAST(s AS DOUBLE) AS d FROM F"
+    canon = [[("nan" if isinstance(x, float) and x != x else x) for x in c] for c in _run(sql, vals, "cpu")]
+    got = [[("nan" if isinstance(x, float) and x != x else x) for x in c] for c in _run(sql, vals, gpu)]
+    for a, b, s in zip(zip(*canon), zip(*got), vals):
+        assert a == b, s
+
+
+def test_double_to_string_cpu_round_trips():
+    rnd = random.Random(19)
+    vals = [struct.unpack("<d", struct.pack("<Q", rnd.getrandbits(64)))[0] for _ in range(N)]
+    vals = [v for v in vals if math.isfinite(v)]
+    out = _run("SELECT CAST(s AS STRING) AS t FROM F", vals, "cpu", "double")[0]
+    for v, s in zip(vals, out):
+        assert float(s) == v, (v, s)          # shortest round-trip digits in Java's layout
+
+
+@pytest.mark.gpu
+def test_double_to_string_fuzz_gpu_match_cpu(gpu):
+    rnd = random.Random(23)
+    vals = [struct.unpack("<d", struct.pack("<Q", rnd.getrandbits(64)))[0] for _ in range(4 * N)]
+    vals += [rnd.uniform(-1e8, 1e8) for _ in range(N)] + [float(rnd.randint(-10**9, 10**9)) for _ in range(N)]
+    vals += [10.0 ** e for e in range(-12, 22)] + [None]
+    sql = "SELECT CAST(s AS STRING) AS t FROM F"
+    assert _run(sql, vals, gpu, "double") == _run(sql, vals, "cpu", "double")
