@@ -603,9 +603,19 @@ def _like(e: A.Like, scope, ctx, subst):
             r = torch.tensor([s is not None and rx.fullmatch(s) is not None for s in v.to_pylist()],
                              dtype=torch.bool, device=dev)
     else:
-        rx = re.compile(pat)
-        r = torch.tensor([s is not None and rx.search(s) is not None for s in v.to_pylist()], dtype=torch.bool,
-                         device=dev)
+        from ..ops import regex_dfa
+        dfa = None
+        if isinstance(v, StrColumn) and v.starts.is_cuda:
+            try:
+                dfa = regex_dfa.compile_rlike(pat)
+            except regex_dfa.Unsupported:
+                dfa = None                              # outside the regular subset: host regex
+        if dfa is not None:
+            r = S.rlike(v, dfa)
+        else:
+            rx = re.compile(regex_dfa.java_to_python(pat), re.ASCII)
+            r = torch.tensor([s is not None and rx.search(s) is not None for s in v.to_pylist()], dtype=torch.bool,
+                             device=dev)
     out = bool_col(r, v.valid)
     return evaluate_not(out, n, dev) if e.negated else out
 

@@ -990,6 +990,39 @@ DXA_API int dxa_str_like(const uint8_t* arena, const int64_t* starts, const int3
   return (int)hipGetLastError();
 }
 
+// RLIKE on the device: a byte-level DFA (regex_dfa.py) over symbol classes, run from BOS through the bytes to
+// EOS.  blob = [class of each symbol (258) | next-state table (states × classes)], staged in LDS; a table entry with
+// bit 15 set leads to a terminal state (dead, or accepting — accepting states absorb), so a row stops as soon as
+// its answer is known.
+__global__ void __launch_bounds__(256) str_rlike_kernel(const uint8_t* __restrict__ arena,
+                                                        const int64_t* __restrict__ starts,
+                                                        const int32_t* __restrict__ lens, int64_t n,
+                                                        const int16_t* __restrict__ blob, int32_t words,
+                                                        int32_t ncls, int32_t start, uint8_t* __restrict__ out) {
+  extern __shared__ int16_t dfa_sh[];
+  for (int k = threadIdx.x; k < words; k += blockDim.x) dfa_sh[k] = blob[k];
+  __syncthreads();
+  const int16_t* cls = dfa_sh;
+  const int16_t* tab = dfa_sh + 258;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = arena + starts[i];
+    const int32_t l = lens[i];
+    int32_t e = tab[start * ncls + cls[256]];
+    for (int32_t p = 0; e >= 0 && p < l; ++p) e = tab[e * ncls + cls[s[p]]];
+    if (e >= 0) e = tab[e * ncls + cls[257]];
+    out[i] = e < 0 && (e & 0x7fff) != 0;
+  }
+}
+
+DXA_API int dxa_str_rlike(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                          const int16_t* blob, int32_t words, int32_t ncls, int32_t start, uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  if (words > 258 + 16384 || ncls <= 0 || ncls > 258) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(str_rlike_kernel, dim3(dxa_blocks(n, 256, 1024)), dim3(256), (size_t)words * 2, (hipStream_t)st,
+                     arena, starts, lens, n, blob, words, ncls, start, out);
+  return (int)hipGetLastError();
+}
+
 // parts: host array of k StrPart descriptors (row0 relative to the first part); launches in groups of kMaxStrParts.
 DXA_API int dxa_str_gather_parts(const void* parts, int32_t k, void* st) {
   const StrPart* ps = (const StrPart*)parts;

@@ -191,6 +191,22 @@ def like(col, tokens: List[int]) -> torch.Tensor:
     return out
 
 
+def rlike(col, dfa) -> torch.Tensor:
+    """RLIKE on the device through a regex_dfa.DFA → bool mask."""
+    n = col.length
+    out = torch.empty(n, dtype=torch.bool, device=col.device)
+    if n:
+        blobs = dfa.__dict__.setdefault("_dev", {})
+        blob = blobs.get(col.device)
+        if blob is None:
+            blob = torch.tensor(dfa.classes + [t - 0x10000 if t & 0x8000 else t for t in dfa.table],
+                                dtype=torch.int16).to(col.device)
+            blobs[col.device] = blob
+        N.call("dxa_str_rlike", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(blob),
+               int(blob.numel()), dfa.n_classes, dfa.start, N.ptr(out.view(torch.uint8)), N.stream_handle(col.device))
+    return out
+
+
 def _raw_bytes(col) -> List[bytes]:
     arena = col.arena.cpu().numpy().tobytes()
     return [arena[s:s + l] for s, l in zip(col.starts.cpu().tolist(), col.lens.cpu().tolist())]

@@ -132,3 +132,46 @@ def test_double_to_string_fuzz_gpu_match_cpu(gpu):
     vals += [10.0 ** e for e in range(-12, 22)] + [None]
     sql = "SELECT CAST(s AS STRING) AS t FROM F"
     assert _run(sql, vals, gpu, "double") == _run(sql, vals, "cpu", "double")
+
+
+def _rand_regex(rnd, depth=0):
+    out = []
+    for _ in range(rnd.randint(1, 4)):
+        r = rnd.random()
+        if r < 0.12 and depth < 2:
+            atom = "(" + "|".join(_rand_regex(rnd, depth + 1) for _ in range(rnd.randint(1, 3))) + ")"
+        elif r < 0.22:
+            atom = rnd.choice(["[ab]", "[^a]", "[a-cX]", "[\\d\\s]", "[日é]", "[^ X]"])
+        elif r < 0.32:
+            atom = rnd.choice([".", "\\w", "\\W", "\\s", "\\S", "\\d", "\\D", "\\\\", "\\%", "\\t"])
+        else:
+            atom = rnd.choice(["a", "b", "X", " ", "é", "日", "%", "_"])
+        q = rnd.random()
+        atom += "" if q < 0.6 else rnd.choice(["*", "+", "?", "{2}", "{1,3}", "{0,}", "*?", "+?"])
+        out.append(atom)
+    s = "".join(out)
+    if depth == 0:
+        s = ("^" if rnd.random() < 0.2 else "") + s + ("$" if rnd.random() < 0.2 else "")
+    return s
+
+
+def test_rlike_dfa_matches_host_regex():
+    from dxa.ops.regex_dfa import compile_rlike, java_to_python, run_dfa
+    rnd = random.Random(29)
+    vals = [v for v in (_rand_str(rnd, 10) for _ in range(300)) if v is not None] + ["a\n", "\r", "x "]
+    for _ in range(150):
+        pat = _rand_regex(rnd)
+        dfa = compile_rlike(pat)
+        rx = re.compile(java_to_python(pat), re.ASCII)
+        for v in vals:
+            assert run_dfa(dfa, v.encode()) == (rx.search(v) is not None), (pat, v)
+
+
+@pytest.mark.gpu
+def test_rlike_fuzz_gpu_match_cpu(gpu):
+    rnd = random.Random(31)
+    vals = [_rand_str(rnd, 16) for _ in range(N)]
+    for _ in range(60):
+        pat = _rand_regex(rnd)
+        sql = f"SELECT s RLIKE '{_q(pat)}' AS m, s NOT RLIKE '{_q(pat)}' AS n FROM F"
+        assert _run(sql, vals, gpu) == _run(sql, vals, "cpu"), pat
