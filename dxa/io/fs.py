@@ -84,13 +84,15 @@ def gzip_parallel(data, level: int = 6, chunk: int = _GZ_CHUNK) -> bytes:
     return b"".join(parts)
 
 
-def write_atomic(path: str, data: bytes | str, gzip_it: bool = False) -> Path:
+def write_atomic(path: str, data: bytes | str, gzip_it: bool = False, gzipped: bool = False) -> Path:
     """Write to a temp file in the destination folder, then rename (never leaves a partial file).  A blob PUT is
-    atomic on the service side, so remote paths are written in one request."""
+    atomic on the service side, so remote paths are written in one request.  ``gzipped``: ``data`` is already a
+    gzip stream (e.g. compressed on the GPU by ops/deflate.py)."""
     if isinstance(data, str):
         data = data.encode("utf-8")
-    if gzip_it:
+    if gzip_it and not gzipped:
         data = gzip_parallel(data)
+    gzip_it = gzip_it or gzipped
     r = _remote(path)
     if r is not None:
         client, container, blob = r
@@ -106,8 +108,9 @@ def write_atomic(path: str, data: bytes | str, gzip_it: bool = False) -> Path:
     return p
 
 
-def write_with_timeout(path: str, data: bytes | str, timeout_s: float, gzip_it: bool = False) -> Path:
-    fut = _pool.submit(write_atomic, path, data, gzip_it)
+def write_with_timeout(path: str, data: bytes | str, timeout_s: float, gzip_it: bool = False,
+                       gzipped: bool = False) -> Path:
+    fut = _pool.submit(write_atomic, path, data, gzip_it, gzipped)
     return fut.result(timeout=timeout_s)
 
 

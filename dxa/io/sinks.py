@@ -88,6 +88,9 @@ class Sink:
     # one) and ``write`` is called once per configured group as write(lines, group, ts, target)
     groups: Optional[List[str]] = None
     group_expr: Optional[str] = None
+    # the sink writes gzip files: a device-rendered payload used only by this sink is compressed on the GPU and
+    # crosses PCIe compressed (JsonLines.gz)
+    gzip: bool = False
 
 
 DEFAULT_OUTPUT_GROUP = "main"                # BlobSinker.scala:32
@@ -120,10 +123,14 @@ def _blob_sink(d, output_name) -> Optional[Sink]:
         folder = blob_folder(resolve(folder), ts, target)
         suffix = ".json" + (".gz" if compression != "none" else "")
         path = folder + f"part-{uuid.uuid4().hex[:12]}{suffix}"
-        fs.write_with_timeout(path, _joined(lines), timeout_s=float(os.environ.get("DATAX_BlobWriterTimeout", 10)),
-                              gzip_it=compression != "none")
+        timeout = float(os.environ.get("DATAX_BlobWriterTimeout", 10))
+        gz = getattr(lines, "gz", None) if compression != "none" else None
+        if gz is not None:                   # compressed on the GPU before the D2H (ops/deflate.py)
+            fs.write_with_timeout(path, memoryview(gz), timeout_s=timeout, gzipped=True)
+        else:
+            fs.write_with_timeout(path, _joined(lines), timeout_s=timeout, gzip_it=compression != "none")
         return len(lines)
-    return Sink("Blobs", write, groups=sorted(groups), group_expr=group_eval)
+    return Sink("Blobs", write, groups=sorted(groups), group_expr=group_eval, gzip=compression != "none")
 
 
 def _eventhub_sink(d, output_name) -> Optional[Sink]:
@@ -293,16 +300,16 @@ class OutputOperator:
             return st
         native = native_ser.available()
 
-        def capture(sub):
+        def capture(sub, compress=False):
             if native:
-                return native_ser.stage_table(sub)
+                return native_ser.stage_table(sub, compress=compress)
             return table_to_json_lines(sub)            # pure-Python fallback renders eagerly
 
         whole = None
         for s in self.sinks:
             sub = t
-            if s.groups is not None:
-                st.items.append((s, self._split_groups(s, t, ctx, capture)))
+            if s.groups is not None:                 # per-sink payloads: compressed on the device for gzip blobs
+                st.items.append((s, self._split_groups(s, t, ctx, lambda sub: capture(sub, s.gzip))))
                 continue
             if s.filter_expr:
                 from ..engine.expr import EvalContext, Scope, evaluate, predicate_mask

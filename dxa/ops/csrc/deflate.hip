@@ -1,0 +1,276 @@
+// gzip on the device for blob sinks (the reference's GZipHelper.deflateToBytes, K23 in SURVEY §2.F).
+//
+// The serialized JSON is cut into fixed-size chunks; every chunk becomes one complete gzip member (RFC 1952: a
+// 10-byte header, one final deflate block with the fixed Huffman code, CRC-32, ISIZE), so the members need no
+// coordination and their concatenation is a valid multi-member gzip file (gunzip / zlib with auto-detect / Python's
+// gzip all read it).  One wave owns one chunk, staged in LDS (see gzip_chunks_kernel):
+//   * LZ77 over a 4-byte hash (4096 uint16 heads in LDS), greedy parsing — JSON lines repeat their keys and structure,
+//     which is where deflate's gain comes from;
+//   * the fixed Huffman code (RFC 1951 §3.2.6), token bits placed by a wave prefix sum;
+//   * CRC-32 per lane slice, combined across the wave with the GF(2) multiply of crc32_combine.
+// A second kernel packs the members back to back (exclusive scan of their sizes on the host side).
+// Dynamic Huffman tables would gain more ratio; the fixed code keeps the encoder to one pass, and the output D2H
+// (what this is for: PCIe, not HBM, is the bound) is already cut ~5-6x on the serialized events.
+#include "dxa_common.h"
+
+namespace {
+
+constexpr int kHashBits = 12;
+constexpr int kHashSize = 1 << kHashBits;
+constexpr int kMaxDist = 32768;
+constexpr int kHdr = 12;             // slot layout: [2 pad][10 gzip header][deflate …][crc32][isize]
+
+__device__ __forceinline__ uint32_t rev_bits(uint32_t code, int len) { return __builtin_bitreverse32(code) >> (32 - len); }
+
+// ---- CRC-32 pieces (reflected polynomial 0xEDB88320) ----------------------------------------------------------
+// a·b mod P in the reflected bit order (x^0 is the top bit): the multiply that crc32_combine is built on —
+// crc(A‖B) = (crc(A) · x^(8|B|)) ⊕ crc(B).  Lanes CRC their own slices and the wave combines them in a tree.
+__host__ __device__ constexpr uint32_t mulmodp(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (uint32_t m = 1u << 31; m != 0; m >>= 1) {
+    if (a & m) p ^= b;
+    b = (b & 1) ? ((b >> 1) ^ 0xEDB88320u) : (b >> 1);
+  }
+  return p;
+}
+
+struct X2N {                          // v[k] = x^(2^k) mod P
+  uint32_t v[32];
+  constexpr X2N() : v{} {
+    uint32_t p = 1u << 30;            // x^1
+    for (int k = 0; k < 32; ++k) { v[k] = p; p = mulmodp(p, p); }
+  }
+};
+__constant__ X2N kX2N = X2N();
+
+// x^(8n) mod P
+__device__ __forceinline__ uint32_t x8n(uint32_t n) {
+  uint32_t p = 1u << 31;              // x^0
+  for (int k = 3; n != 0; n >>= 1, ++k)
+    if (n & 1) p = mulmodp(kX2N.v[k & 31], p);
+  return p;
+}
+
+__device__ __forceinline__ uint32_t lds_load4(const uint32_t* w, int32_t p) {
+  const uint32_t a = w[p >> 2], b = w[(p >> 2) + 1];
+  const int sh = (p & 3) * 8;
+  return sh ? ((a >> sh) | (b << (32 - sh))) : a;
+}
+
+// One wave per chunk, everything in LDS: [chunk bytes + pad][hash heads][output word window].
+//   per 64-position group: every lane hashes its position and looks up the newest earlier position with that
+//   hash (heads from earlier groups), extends the match 4 bytes at a time;
+//   the greedy parse walks the group with ballots (a literal run up to the next match start in one step);
+//   token codes are placed with a wave prefix sum of their bit lengths and OR-ed into the word window, whose
+//   complete words go to the chunk's slot after every group.
+constexpr int kWinWords = 72;
+
+__global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restrict__ in, int64_t n_in, int32_t chunk,
+                                                         int64_t n_chunks, uint8_t* __restrict__ slots,
+                                                         int64_t slot_bytes, int32_t* __restrict__ out_len) {
+  extern __shared__ uint32_t gz_sh[];
+  __shared__ uint32_t crc_tab[256];
+  const int lane = threadIdx.x;
+  for (int k = lane; k < 256; k += 64) {
+    uint32_t c = (uint32_t)k;
+    for (int j = 0; j < 8; ++j) c = (c & 1) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
+    crc_tab[k] = c;
+  }
+  uint32_t* dat32 = gz_sh;
+  const uint8_t* dat = (const uint8_t*)gz_sh;
+  uint16_t* head = (uint16_t*)(gz_sh + (chunk >> 2) + 4);     // newest position + 1 per hash (0: none)
+  uint32_t* win = gz_sh + (chunk >> 2) + 4 + kHashSize / 2;
+  const int64_t c = blockIdx.x;
+  const int64_t base = c * chunk;
+  const int32_t L = (int32_t)((n_in - base) < chunk ? (n_in - base) : chunk);
+  const uint8_t* src = in + base;
+  uint8_t* slot = slots + c * slot_bytes;
+  uint32_t* dst = (uint32_t*)(slot + kHdr);
+
+  // stage the chunk (16-byte loads; the chunk start is 16-byte aligned), zero the pad, clear the heads
+  const int32_t L16 = L & ~15;
+  for (int32_t k = lane * 16; k < L16; k += 64 * 16) {
+    const uint4 q = *(const uint4*)(src + k);
+    dat32[(k >> 2) + 0] = q.x; dat32[(k >> 2) + 1] = q.y; dat32[(k >> 2) + 2] = q.z; dat32[(k >> 2) + 3] = q.w;
+  }
+  for (int32_t k = L16 + lane; k < ((L + 3) & ~3) + 16; k += 64) {
+    // the words past L16: assembled from bytes (zero beyond L)
+    if ((k & 3) == 0) {
+      uint32_t w = 0;
+      for (int b = 0; b < 4; ++b) if (k + b < L) w |= (uint32_t)src[k + b] << (8 * b);
+      dat32[k >> 2] = w;
+    }
+  }
+  for (int k = lane; k < kHashSize / 2; k += 64) gz_sh[(chunk >> 2) + 4 + k] = 0;
+  for (int k = lane; k < kWinWords; k += 64) win[k] = 0;
+  if (lane < 10) {
+    const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
+    slot[2 + lane] = hdr[lane];
+  }
+  __syncthreads();
+
+  // CRC-32: 64 slices, then a tree of combines
+  const int32_t S = (chunk + 63) >> 6;
+  const int32_t s0 = lane * S < L ? lane * S : L;
+  const int32_t s1 = s0 + S < L ? s0 + S : L;
+  uint32_t crc = 0xFFFFFFFFu;
+  for (int32_t k = s0; k < s1; ++k) crc = crc_tab[(crc ^ dat[k]) & 0xff] ^ (crc >> 8);
+  crc ^= 0xFFFFFFFFu;
+  if (s1 == s0) crc = 0;
+  uint32_t clen = (uint32_t)(s1 - s0);
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t ocrc = __shfl_down(crc, d, 64), olen = __shfl_down(clen, d, 64);
+    if ((lane & (2 * d - 1)) == 0 && olen != 0) {
+      crc = mulmodp(x8n(olen), crc) ^ ocrc;
+      clen += olen;
+    }
+  }
+  crc = __shfl(crc, 0, 64);
+
+  // LZ77 + fixed-Huffman coding, one 64-position group at a time
+  uint32_t gbit = 3;                  // BFINAL = 1, BTYPE = 01
+  if (lane == 0) win[0] = 3;
+  int32_t wbase = 0;                  // word index of win[0] in the deflate stream
+  int32_t carry = 0;                  // how far the previous group's last match reaches into this group
+  __syncthreads();
+  for (int32_t g = 0; g < L; g += 64) {
+    const int32_t p = g + lane;
+    const bool can = p + 4 <= L;
+    const uint32_t v = lds_load4(dat32, p);
+    const uint32_t h = (v * 2654435761u) >> (32 - kHashBits);
+    int32_t cand = can ? (int32_t)head[h] - 1 : -1;
+    __builtin_amdgcn_wave_barrier();
+    if (can) head[h] = (uint16_t)(p + 1);   // lanes sharing a hash: one of them wins (a candidate, not the newest)
+    // a candidate is only checked for its first 4 bytes here; the full length is measured for the positions the
+    // greedy parse actually takes, by the whole wave at once (64 lanes × 4 bytes = 256 bytes per step)
+    const bool is_m = cand >= 0 && p - cand <= kMaxDist && lds_load4(dat32, cand) == v;
+    const uint64_t mm = __ballot(is_m);
+    const uint64_t live = (L - g) >= 64 ? ~0ull : ((1ull << (L - g)) - 1);
+    uint64_t tok = 0;
+    int32_t len = 0;                  // match length, set on the lanes that start a match token
+    int32_t w = carry;
+    while (w < 64) {
+      const uint64_t from = ~0ull << w;
+      const uint64_t rest = mm & from;
+      if (rest == 0) { tok |= from; w = 64; break; }
+      const int m = __builtin_ctzll(rest);
+      tok |= (from & ~(~0ull << m)) | (1ull << m);
+      const int32_t pm = g + m, cm = __builtin_amdgcn_readlane(cand, m);
+      const int32_t lim = (L - pm) < 258 ? (L - pm) : 258;
+      const int32_t off = 4 + 4 * lane;
+      const uint32_t x = off < lim ? (lds_load4(dat32, cm + off) ^ lds_load4(dat32, pm + off)) : 0u;
+      const uint64_t miss = __ballot(x != 0);
+      int32_t ml = lim;
+      if (miss) {
+        const int k0 = __builtin_ctzll(miss);
+        const int32_t e = 4 + 4 * k0 + (__builtin_ctz(__builtin_amdgcn_readlane(x, k0)) >> 3);
+        ml = e < lim ? e : lim;
+      }
+      if (lane == m) len = ml;
+      w = m + ml;
+    }
+    carry = w - 64;
+    tok &= live;
+    // this lane's code (≤ 31 bits, LSB-first)
+    uint32_t bits = 0, nb = 0;
+    if ((tok >> lane) & 1) {
+      if (len >= 4) {
+        const uint32_t x = (uint32_t)(len - 3);
+        uint32_t sym, eb = 0, ev = 0;
+        if (len == 258) sym = 285;
+        else if (x < 8) sym = 257 + x;
+        else { const int hb = 31 - __builtin_clz(x); eb = hb - 2; sym = 257 + 4 * (hb - 1) + ((x >> eb) & 3); ev = x & ((1u << eb) - 1); }
+        uint32_t cl;
+        if (sym < 280) { bits = rev_bits(sym - 256, 7); cl = 7; }
+        else { bits = rev_bits(0xC0 + (sym - 280), 8); cl = 8; }
+        bits |= ev << cl; nb = cl + eb;
+        const uint32_t y = (uint32_t)(p - cand - 1);
+        uint32_t dc, deb = 0, dev = 0;
+        if (y < 4) dc = y;
+        else { const int hb = 31 - __builtin_clz(y); deb = hb - 1; dc = 2 * hb + ((y >> deb) & 1); dev = y & ((1u << deb) - 1); }
+        bits |= rev_bits(dc, 5) << nb; nb += 5;
+        bits |= dev << nb; nb += deb;
+      } else {
+        const uint32_t b = dat[p];
+        if (b < 144) { bits = rev_bits(0x30 + b, 8); nb = 8; }
+        else { bits = rev_bits(0x190 + (b - 144), 9); nb = 9; }
+      }
+    }
+    // exclusive prefix sum of nb over the wave
+    uint32_t incl = nb;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (nb) {
+      const uint32_t pos = (gbit - (uint32_t)wbase * 32) + incl - nb;
+      const uint32_t wi = pos >> 5, sh = pos & 31;
+      atomicOr(&win[wi], bits << sh);
+      if (sh && sh + nb > 32) atomicOr(&win[wi + 1], bits >> (32 - sh));
+    }
+    gbit += total;
+    __syncthreads();
+    // flush complete words, keep the partial one at win[0]
+    const int32_t nfull = (int32_t)(gbit >> 5) - wbase;
+    for (int k = lane; k < nfull; k += 64) dst[wbase + k] = win[k];
+    const uint32_t keep = win[nfull];
+    __syncthreads();
+    for (int k = lane; k < kWinWords; k += 64) win[k] = k == 0 ? keep : 0;
+    wbase += nfull;
+    __syncthreads();
+  }
+  // end of block (code 256 = 7 zero bits), then the trailer bytes right after the last deflate byte
+  gbit += 7;
+  const uint32_t nbytes = (gbit + 7) >> 3;            // deflate bytes
+  if (lane < 8) {
+    const uint32_t val = lane < 4 ? crc : (uint32_t)L;
+    const uint32_t byte = (val >> (8 * (lane & 3))) & 0xff;
+    const uint32_t at = nbytes - (uint32_t)wbase * 4 + lane;            // byte offset inside the window
+    atomicOr(&win[at >> 2], byte << (8 * (at & 3)));
+  }
+  __syncthreads();
+  const int32_t tail_words = (int32_t)((nbytes + 8 + 3) >> 2) - wbase;
+  for (int k = lane; k < tail_words; k += 64) dst[wbase + k] = win[k];
+  if (lane == 0) out_len[c] = (int32_t)(10 + nbytes + 8);
+}
+
+// member c: slot bytes [2, 2 + out_len[c]) → out[offs[c] …]; one workgroup per member, 16-byte copies where the
+// source and destination alignment allow, bytes otherwise
+__global__ void __launch_bounds__(256) gzip_pack_kernel(const uint8_t* __restrict__ slots, int64_t slot_bytes,
+                                                        const int32_t* __restrict__ out_len,
+                                                        const int64_t* __restrict__ offs, int64_t n_chunks,
+                                                        uint8_t* __restrict__ out) {
+  for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    const uint8_t* s = slots + c * slot_bytes + 2;
+    uint8_t* d = out + offs[c];
+    const int32_t l = out_len[c];
+    for (int32_t k = threadIdx.x; k < l; k += blockDim.x) d[k] = s[k];
+  }
+}
+
+}  // namespace
+
+DXA_API int64_t dxa_gzip_slot_bytes(int32_t chunk) {
+  return ((int64_t)kHdr + ((int64_t)chunk * 9 + 7) / 8 + 32 + 15) & ~(int64_t)15;
+}
+
+DXA_API int dxa_gzip_chunks(const uint8_t* in, int64_t n_in, int32_t chunk, uint8_t* slots, int32_t* out_len,
+                            void* st) {
+  if (n_in <= 0) return 0;
+  if (chunk < 64 || chunk > 32768 || (chunk & 63)) return (int)hipErrorInvalidValue;   // deflate window
+  const int64_t n_chunks = (n_in + chunk - 1) / chunk;
+  const int64_t slot = dxa_gzip_slot_bytes(chunk);
+  const size_t lds = ((size_t)(chunk >> 2) + 4 + kHashSize / 2 + kWinWords) * 4;
+  hipLaunchKernelGGL(gzip_chunks_kernel, dim3((unsigned)n_chunks), dim3(64), lds, (hipStream_t)st, in, n_in, chunk,
+                     n_chunks, slots, slot, out_len);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_gzip_pack(const uint8_t* slots, int32_t chunk, const int32_t* out_len, const int64_t* offs,
+                          int64_t n_chunks, uint8_t* out, void* st) {
+  if (n_chunks <= 0) return 0;
+  hipLaunchKernelGGL(gzip_pack_kernel, dim3(dxa_blocks(n_chunks, 1, 8192)), dim3(256), 0, (hipStream_t)st, slots,
+                     dxa_gzip_slot_bytes(chunk), out_len, offs, n_chunks, out);
+  return (int)hipGetLastError();
+}

@@ -337,10 +337,11 @@ class Staged:
     columns are copied to pinned host memory (async) and rendered by the native host serializer.  ``render`` may
     run on any host thread."""
 
-    def __init__(self, table):
+    def __init__(self, table, compress: bool = False):
         self.n = table.length
         self.event = None
         self.gpu = gpu_serializer_enabled(table.device)
+        self.compress = compress and self.gpu and os.environ.get("DXA_GPU_GZIP", "1") != "0"
         if self.gpu:
             self.table = table
             self.device = table.device
@@ -381,6 +382,16 @@ class Staged:
             out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
             N.call("dxa_serialize_write", N.ptr(nodes), nn, N.ptr(prog_t), nprog, N.ptr(text), tw, n, N.ptr(offs),
                    N.ptr(out), st)
+            if self.compress and total > 1:
+                # gzip of the newline-joined documents (no trailing newline: what a blob sink writes), on the GPU;
+                # only the compressed stream crosses PCIe
+                from .deflate import gzip_device
+                gz = gzip_device(out, total - 1)
+                host = torch.empty(gz.numel(), dtype=torch.uint8, pin_memory=True)
+                side.synchronize()
+                d2h(host, gz, gz.numel(), side)
+                self.table = None
+                return JsonLines(None, host_lens.numpy() - 1, gz=host.numpy())
             host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
             side.synchronize()
             d2h(host, out, total, side)
@@ -419,23 +430,32 @@ class JsonLines:
     ``bytes`` or a uint8 numpy array (e.g. the pinned D2H target of the device serializer — no extra host copy);
     behaves as a read-only sequence of ``str`` (decoded lazily) for sinks that want individual documents."""
 
-    def __init__(self, blob, lens):
+    def __init__(self, blob, lens, gz=None):
+        self.gz = gz                        # gzip of data(), when the device compressed it (then blob may be None)
         self._buf = blob
         self._bytes = blob if isinstance(blob, (bytes, bytearray)) else None
         self.lens = np.asarray(lens, dtype=np.int64)
         self._starts = None
 
+    def _text_buf(self):
+        if self._buf is None:               # compressed-only payload: the text is inflated on first use
+            import gzip as _gzip
+            self._buf = self._bytes = _gzip.decompress(bytes(self.gz)) + b"\n"
+        return self._buf
+
     @property
     def blob(self) -> bytes:
+        self._text_buf()
         if self._bytes is None:
             self._bytes = np.asarray(self._buf).tobytes()
         return self._bytes
 
     def nbytes(self) -> int:
-        return len(self._buf)
+        return len(self._text_buf())
 
     def view(self) -> memoryview:
         """Zero-copy view of the whole newline-terminated buffer."""
+        self._text_buf()
         return memoryview(self._buf if self._bytes is None else self._bytes).cast("B")
 
     def __len__(self):
@@ -479,8 +499,8 @@ class JsonLines:
         return f"JsonLines(n={len(self)}, bytes={self.nbytes()})"
 
 
-def stage_table(table) -> Staged:
-    return Staged(table)
+def stage_table(table, compress: bool = False) -> Staged:
+    return Staged(table, compress)
 
 
 def serialize_table(table, nthreads: Optional[int] = None) -> Tuple[bytes, List[int]]:

@@ -6,6 +6,8 @@ import gzip
 import json
 import os
 
+import pytest
+
 
 from dxa.config.settings import SettingDictionary
 from dxa.engine.column import Table
@@ -80,3 +82,26 @@ def test_gzip_parallel_is_one_valid_stream():
         d = zlib.decompressobj(16 + zlib.MAX_WBITS) if rest else d
     assert b"".join(out) == data
     assert gzip.decompress(gzip_parallel(b"small")) == b"small"
+
+
+@pytest.mark.gpu
+def test_blob_gzip_compressed_on_device(tmp_path, gpu):
+    """A gzip blob sink on a GPU table: the device compresses (ops/deflate.py) and the file inflates to exactly the
+    text the uncompressed path writes."""
+    rows = [{"id": i, "s": f"device-{i % 97}", "v": i * 0.25} for i in range(60000)]
+    schema = StructType((StructField("id", "long"), StructField("s", "string"), StructField("v", "double")))
+    outs = {}
+    for comp in ("gzip", "none"):
+        folder = tmp_path / comp
+        d = SettingDictionary({"datax.job.output.Out.blob.group.main.folder": str(folder) + "/",
+                               "datax.job.output.Out.blob.compressiontype": comp})
+        op, = build_outputs(d)
+        staged = op.stage(Table.from_pylist(rows, schema, gpu))
+        if comp == "gzip":
+            assert staged.items[0][1]["main"].compress
+        m = staged.finish(dt.datetime(2024, 1, 1))
+        assert m["Sink_Blobs_Events_main"] == len(rows)
+        p, = glob.glob(os.path.join(folder, "**", "*.json*"), recursive=True)
+        outs[comp] = gzip.open(p).read() if comp == "gzip" else open(p, "rb").read()
+    assert outs["gzip"] == outs["none"]
+    assert [json.loads(l)["id"] for l in outs["gzip"].splitlines()] == list(range(60000))
