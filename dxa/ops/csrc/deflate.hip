@@ -4,7 +4,7 @@
 // 10-byte header, one final deflate block with the fixed Huffman code, CRC-32, ISIZE), so the members need no
 // coordination and their concatenation is a valid multi-member gzip file (gunzip / zlib with auto-detect / Python's
 // gzip all read it).  One wave owns one chunk, staged in LDS (see gzip_chunks_kernel):
-//   * LZ77 over a 4-byte hash (4096 uint16 heads in LDS), greedy parsing — JSON lines repeat their keys and structure,
+//   * LZ77 over a 4-byte hash (2048 uint16 heads in LDS), greedy parsing — JSON lines repeat their keys and structure,
 //     which is where deflate's gain comes from;
 //   * the fixed Huffman code (RFC 1951 §3.2.6), token bits placed by a wave prefix sum;
 //   * CRC-32 per lane slice, combined across the wave with the GF(2) multiply of crc32_combine.
@@ -15,7 +15,7 @@
 
 namespace {
 
-constexpr int kHashBits = 12;
+constexpr int kHashBits = 11;
 constexpr int kHashSize = 1 << kHashBits;
 constexpr int kMaxDist = 32768;
 constexpr int kHdr = 12;             // slot layout: [2 pad][10 gzip header][deflate …][crc32][isize]
@@ -51,6 +51,19 @@ __device__ __forceinline__ uint32_t x8n(uint32_t n) {
   return p;
 }
 
+struct CrcPow {
+  int32_t slice;                      // bytes per lane slice (a multiple of 4, an odd number of words)
+  uint32_t x[6];                      // x^(8·slice·2^l) mod P
+};
+
+uint32_t host_x8n(uint64_t n) {
+  constexpr X2N t{};
+  uint32_t p = 1u << 31;
+  for (int k = 3; n != 0; n >>= 1, ++k)
+    if (n & 1) p = mulmodp(t.v[k & 31], p);
+  return p;
+}
+
 __device__ __forceinline__ uint32_t lds_load4(const uint32_t* w, int32_t p) {
   const uint32_t a = w[p >> 2], b = w[(p >> 2) + 1];
   const int sh = (p & 3) * 8;
@@ -63,11 +76,12 @@ __device__ __forceinline__ uint32_t lds_load4(const uint32_t* w, int32_t p) {
 //   the greedy parse walks the group with ballots (a literal run up to the next match start in one step);
 //   token codes are placed with a wave prefix sum of their bit lengths and OR-ed into the word window, whose
 //   complete words go to the chunk's slot after every group.
-constexpr int kWinWords = 72;
+constexpr int kRing = 128;            // output word ring (a group writes ≤ 63 words)
 
 __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restrict__ in, int64_t n_in, int32_t chunk,
                                                          int64_t n_chunks, uint8_t* __restrict__ slots,
-                                                         int64_t slot_bytes, int32_t* __restrict__ out_len) {
+                                                         int64_t slot_bytes, int32_t* __restrict__ out_len,
+                                                         CrcPow pw) {
   extern __shared__ uint32_t gz_sh[];
   __shared__ uint32_t crc_tab[256];
   const int lane = threadIdx.x;
@@ -102,26 +116,36 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
     }
   }
   for (int k = lane; k < kHashSize / 2; k += 64) gz_sh[(chunk >> 2) + 4 + k] = 0;
-  for (int k = lane; k < kWinWords; k += 64) win[k] = 0;
+  for (int k = lane; k < kRing; k += 64) win[k] = 0;
   if (lane < 10) {
     const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
     slot[2 + lane] = hdr[lane];
   }
   __syncthreads();
 
-  // CRC-32: 64 slices, then a tree of combines
-  const int32_t S = (chunk + 63) >> 6;
+  // CRC-32: 64 slices (an odd number of words each, so the lanes' word reads fall in distinct LDS banks), then a
+  // tree of combines; the x^(8·len) multipliers of full slices come precomputed from the host
+  const int32_t S = pw.slice;
   const int32_t s0 = lane * S < L ? lane * S : L;
   const int32_t s1 = s0 + S < L ? s0 + S : L;
   uint32_t crc = 0xFFFFFFFFu;
-  for (int32_t k = s0; k < s1; ++k) crc = crc_tab[(crc ^ dat[k]) & 0xff] ^ (crc >> 8);
+  int32_t k = s0;
+  for (; k + 4 <= s1; k += 4) {
+    const uint32_t w = dat32[k >> 2];
+    crc = crc_tab[(crc ^ w) & 0xff] ^ (crc >> 8);
+    crc = crc_tab[(crc ^ (w >> 8)) & 0xff] ^ (crc >> 8);
+    crc = crc_tab[(crc ^ (w >> 16)) & 0xff] ^ (crc >> 8);
+    crc = crc_tab[(crc ^ (w >> 24)) & 0xff] ^ (crc >> 8);
+  }
+  for (; k < s1; ++k) crc = crc_tab[(crc ^ dat[k]) & 0xff] ^ (crc >> 8);
   crc ^= 0xFFFFFFFFu;
   if (s1 == s0) crc = 0;
   uint32_t clen = (uint32_t)(s1 - s0);
-  for (int d = 1; d < 64; d <<= 1) {
+  for (int l = 0; l < 6; ++l) {
+    const int d = 1 << l;
     const uint32_t ocrc = __shfl_down(crc, d, 64), olen = __shfl_down(clen, d, 64);
     if ((lane & (2 * d - 1)) == 0 && olen != 0) {
-      crc = mulmodp(x8n(olen), crc) ^ ocrc;
+      crc = mulmodp(olen == (uint32_t)(S << l) ? pw.x[l] : x8n(olen), crc) ^ ocrc;
       clen += olen;
     }
   }
@@ -130,7 +154,7 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
   // LZ77 + fixed-Huffman coding, one 64-position group at a time
   uint32_t gbit = 3;                  // BFINAL = 1, BTYPE = 01
   if (lane == 0) win[0] = 3;
-  int32_t wbase = 0;                  // word index of win[0] in the deflate stream
+  int32_t wbase = 0;                  // first deflate word not yet flushed to the slot
   int32_t carry = 0;                  // how far the previous group's last match reaches into this group
   __syncthreads();
   for (int32_t g = 0; g < L; g += 64) {
@@ -191,34 +215,36 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
         bits |= rev_bits(dc, 5) << nb; nb += 5;
         bits |= dev << nb; nb += deb;
       } else {
-        const uint32_t b = dat[p];
+        const uint32_t b = v & 0xff;
         if (b < 144) { bits = rev_bits(0x30 + b, 8); nb = 8; }
         else { bits = rev_bits(0x190 + (b - 144), 9); nb = 9; }
       }
     }
-    // exclusive prefix sum of nb over the wave
-    uint32_t incl = nb;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += o;
+    // exclusive prefix sum of the code lengths (≤ 31: five bit planes, ballots + mbcnt, no LDS round trips)
+    uint32_t excl = 0, total = 0;
+    for (int bp = 0; bp < 5; ++bp) {
+      const uint64_t m = __ballot((nb >> bp) & 1);
+      excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bp;
+      total += (uint32_t)__builtin_popcountll(m) << bp;
     }
-    const uint32_t total = __shfl(incl, 63, 64);
     if (nb) {
-      const uint32_t pos = (gbit - (uint32_t)wbase * 32) + incl - nb;
+      const uint32_t pos = gbit + excl;
       const uint32_t wi = pos >> 5, sh = pos & 31;
-      atomicOr(&win[wi], bits << sh);
-      if (sh && sh + nb > 32) atomicOr(&win[wi + 1], bits >> (32 - sh));
+      atomicOr(&win[wi & (kRing - 1)], bits << sh);
+      if (sh && sh + nb > 32) atomicOr(&win[(wi + 1) & (kRing - 1)], bits >> (32 - sh));
     }
     gbit += total;
-    __syncthreads();
-    // flush complete words, keep the partial one at win[0]
+    // flush the words this group completed (ring slots are zeroed as they leave; a wave's LDS operations complete
+    // in order, so no barrier is needed between the ORs above and these reads)
+    __builtin_amdgcn_wave_barrier();
     const int32_t nfull = (int32_t)(gbit >> 5) - wbase;
-    for (int k = lane; k < nfull; k += 64) dst[wbase + k] = win[k];
-    const uint32_t keep = win[nfull];
-    __syncthreads();
-    for (int k = lane; k < kWinWords; k += 64) win[k] = k == 0 ? keep : 0;
+    for (int k = lane; k < nfull; k += 64) {
+      const int idx = (wbase + k) & (kRing - 1);
+      dst[wbase + k] = win[idx];
+      win[idx] = 0;
+    }
     wbase += nfull;
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
   }
   // end of block (code 256 = 7 zero bits), then the trailer bytes right after the last deflate byte
   gbit += 7;
@@ -226,12 +252,12 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
   if (lane < 8) {
     const uint32_t val = lane < 4 ? crc : (uint32_t)L;
     const uint32_t byte = (val >> (8 * (lane & 3))) & 0xff;
-    const uint32_t at = nbytes - (uint32_t)wbase * 4 + lane;            // byte offset inside the window
-    atomicOr(&win[at >> 2], byte << (8 * (at & 3)));
+    const uint32_t at = nbytes + lane;                                  // byte offset in the deflate stream
+    atomicOr(&win[(at >> 2) & (kRing - 1)], byte << (8 * (at & 3)));
   }
   __syncthreads();
-  const int32_t tail_words = (int32_t)((nbytes + 8 + 3) >> 2) - wbase;
-  for (int k = lane; k < tail_words; k += 64) dst[wbase + k] = win[k];
+  const int32_t end_words = (int32_t)((nbytes + 8 + 3) >> 2);
+  for (int k = wbase + lane; k < end_words; k += 64) dst[k] = win[k & (kRing - 1)];
   if (lane == 0) out_len[c] = (int32_t)(10 + nbytes + 8);
 }
 
@@ -261,9 +287,14 @@ DXA_API int dxa_gzip_chunks(const uint8_t* in, int64_t n_in, int32_t chunk, uint
   if (chunk < 64 || chunk > 32768 || (chunk & 63)) return (int)hipErrorInvalidValue;   // deflate window
   const int64_t n_chunks = (n_in + chunk - 1) / chunk;
   const int64_t slot = dxa_gzip_slot_bytes(chunk);
-  const size_t lds = ((size_t)(chunk >> 2) + 4 + kHashSize / 2 + kWinWords) * 4;
+  const size_t lds = ((size_t)(chunk >> 2) + 4 + kHashSize / 2 + kRing) * 4;
+  CrcPow pw{};
+  int32_t words = ((chunk + 63) / 64 + 3) / 4;
+  if ((words & 1) == 0) ++words;
+  pw.slice = words * 4;
+  for (int l = 0; l < 6; ++l) pw.x[l] = host_x8n((uint64_t)pw.slice << l);
   hipLaunchKernelGGL(gzip_chunks_kernel, dim3((unsigned)n_chunks), dim3(64), lds, (hipStream_t)st, in, n_in, chunk,
-                     n_chunks, slots, slot, out_len);
+                     n_chunks, slots, slot, out_len, pw);
   return (int)hipGetLastError();
 }
 
