@@ -92,6 +92,8 @@ def main():
                     "parallel on the host, as per-partition fetch threads would)")
     ap.add_argument("--kafka-batch-records", type=int, default=26,
                     help="kafka: records per producer batch (26 SimulatedData events = ~16 KiB, one LZ4 block)")
+    ap.add_argument("--sink", choices=["null", "blob"], default="null",
+                    help="output sink: null (rendered JSON lands in host memory) or blob (gzip files under /tmp)")
     ap.add_argument("--profile-stages", action="store_true")
     ap.add_argument("--sync-outputs", action="store_true",
                     help="finish each batch's sink writes before the next batch starts (default: pipelined)")
@@ -141,7 +143,7 @@ def main():
     if world > 1:
         parallel.init(dist.group.WORLD, device)
 
-    proc = Processor(iot.flow_settings(workdir=f"/tmp/dxa_bench_{flow}_{rank}", variant=flow,
+    proc = Processor(iot.flow_settings(workdir=f"/tmp/dxa_bench_{flow}_{rank}", variant=flow, sink=args.sink,
                                        ref_rows=args.ref_rows), device, pipeline_outputs=not args.sync_outputs)
     t_ref = time.perf_counter()
     if flow == "join":
@@ -422,7 +424,8 @@ def main():
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
                    "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,
                    "source": source, "ingest_prefetch_batches": depth, "batch_interval_s": interval_us / 1e6,
-                   "outputs": "sync" if args.sync_outputs else "pipelined (batch t sinks overlap batch t+1)"},
+                   "outputs": "sync" if args.sync_outputs else "pipelined (batch t sinks overlap batch t+1)",
+                   "sink": args.sink},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),
         "events_per_sec_per_gpu": value / world,

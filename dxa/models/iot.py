@@ -318,6 +318,9 @@ def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Opti
         })
     for o in dict.fromkeys(outputs):
         d[f"datax.job.output.{o}.{sink}.enabled"] = "true"
+        if sink == "blob":                    # gzip JSON files under the work dir (BlobSinker's layout)
+            d[f"datax.job.output.{o}.blob.group.main.folder"] = os.path.join(workdir, "out", o) + "/"
+            d[f"datax.job.output.{o}.blob.compressiontype"] = "gzip"
     with open(paths["schema"], "w") as f:
         f.write(schema_to_json(iot_spark_schema()))
     with open(paths["projection"], "w") as f:
