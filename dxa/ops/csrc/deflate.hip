@@ -70,14 +70,213 @@ __device__ __forceinline__ uint32_t lds_load4(const uint32_t* w, int32_t p) {
   return sh ? ((a >> sh) | (b << (32 - sh))) : a;
 }
 
+// deflate length / distance symbols (RFC 1951 §3.2.5): symbol, extra-bit count, extra-bit value
+__device__ __forceinline__ void len_sym(int32_t len, uint32_t& sym, uint32_t& eb, uint32_t& ev) {
+  const uint32_t x = (uint32_t)(len - 3);
+  eb = 0; ev = 0;
+  if (len == 258) sym = 285;
+  else if (x < 8) sym = 257 + x;
+  else { const int hb = 31 - __builtin_clz(x); eb = hb - 2; sym = 257 + 4 * (hb - 1) + ((x >> eb) & 3); ev = x & ((1u << eb) - 1); }
+}
+__device__ __forceinline__ void dist_sym(int32_t dist, uint32_t& dc, uint32_t& eb, uint32_t& ev) {
+  const uint32_t y = (uint32_t)(dist - 1);
+  eb = 0; ev = 0;
+  if (y < 4) dc = y;
+  else { const int hb = 31 - __builtin_clz(y); eb = hb - 1; dc = 2 * hb + ((y >> eb) & 1); ev = y & ((1u << eb) - 1); }
+}
+
+// fixed Huffman literal/length code (RFC 1951 §3.2.6): bit-reversed code | length << 16
+__device__ __forceinline__ uint32_t fixed_code(uint32_t sym) {
+  if (sym < 144) return rev_bits(0x30 + sym, 8) | (8u << 16);
+  if (sym < 256) return rev_bits(0x190 + (sym - 144), 9) | (9u << 16);
+  if (sym < 280) return rev_bits(sym - 256, 7) | (7u << 16);
+  return rev_bits(0xC0 + (sym - 280), 8) | (8u << 16);
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+constexpr int kRing = 128;            // output word ring (one emit round writes ≤ 97 words)
+constexpr int kNLL = 286, kND = 30, kDOff = 288, kNSym = 320;   // LL alphabet at 0 (288 slots: the fixed code
+                                                                // defines 286/287), distances at kDOff
+
+struct Out {                          // the chunk's deflate bit stream: LDS word ring → slot words
+  uint32_t* win;
+  uint32_t* dst;
+  uint32_t gbit = 0;                  // bits emitted
+  int32_t wbase = 0;                  // first word not yet flushed
+
+  __device__ __forceinline__ void place(uint32_t v, uint32_t n, uint32_t pos) {
+    if (!n) return;
+    const uint32_t wi = pos >> 5, sh = pos & 31;
+    atomicOr(&win[wi & (kRing - 1)], v << sh);
+    if (sh && sh + n > 32) atomicOr(&win[(wi + 1) & (kRing - 1)], v >> (32 - sh));
+  }
+  // every lane appends (a: na bits, then b: nb bits), lanes in order; na, nb ≤ 28.  Offsets by a prefix sum over
+  // six bit planes of na + nb (ballots + mbcnt); complete words leave for the slot (a wave's LDS operations
+  // complete in order, so the ORs are visible to the flush reads without a barrier)
+  __device__ __forceinline__ void emit(uint32_t a, uint32_t na, uint32_t b, uint32_t nb, int lane) {
+    const uint32_t n = na + nb;
+    uint32_t excl = 0, total = 0;
+    for (int bp = 0; bp < 6; ++bp) {
+      const uint64_t m = __ballot((n >> bp) & 1);
+      excl += lanes_below(m) << bp;
+      total += (uint32_t)__builtin_popcountll(m) << bp;
+    }
+    place(a, na, gbit + excl);
+    place(b, nb, gbit + excl + na);
+    gbit += total;
+    __builtin_amdgcn_wave_barrier();
+    const int32_t nfull = (int32_t)(gbit >> 5) - wbase;
+    for (int k = lane; k < nfull; k += 64) {
+      const int idx = (wbase + k) & (kRing - 1);
+      dst[wbase + k] = win[idx];
+      win[idx] = 0;
+    }
+    wbase += nfull;
+    __builtin_amdgcn_wave_barrier();
+  }
+};
+
+// One 64-position group of the greedy LZ77 parse (identical in both passes): every lane hashes its position and
+// looks up the newest earlier position with that hash (heads from earlier groups); a candidate is checked for its
+// first 4 bytes; the walk takes a literal run up to the next match start in one step and measures that match with
+// the whole wave (64 lanes × 4 bytes = 256 bytes per step).  Returns this lane's token: 0 none, 1 literal, 2 match.
+__device__ __forceinline__ int parse_group(const uint32_t* dat32, uint16_t* head, int32_t L, int32_t g,
+                                           int32_t& carry, int lane, uint32_t& lit, int32_t& len, int32_t& dist) {
+  const int32_t p = g + lane;
+  const bool can = p + 4 <= L;
+  const uint32_t v = lds_load4(dat32, p);
+  const uint32_t h = (v * 2654435761u) >> (32 - kHashBits);
+  const int32_t cand = can ? (int32_t)head[h] - 1 : -1;
+  __builtin_amdgcn_wave_barrier();
+  if (can) head[h] = (uint16_t)(p + 1);     // lanes sharing a hash: one of them wins (a candidate, not the newest)
+  const bool is_m = cand >= 0 && p - cand <= kMaxDist && lds_load4(dat32, cand) == v;
+  const uint64_t mm = __ballot(is_m);
+  const uint64_t live = (L - g) >= 64 ? ~0ull : ((1ull << (L - g)) - 1);
+  uint64_t tok = 0;
+  len = 0;
+  int32_t w = carry;
+  while (w < 64) {
+    const uint64_t from = ~0ull << w;
+    const uint64_t rest = mm & from;
+    if (rest == 0) { tok |= from; w = 64; break; }
+    const int m = __builtin_ctzll(rest);
+    tok |= (from & ~(~0ull << m)) | (1ull << m);
+    const int32_t pm = g + m, cm = __builtin_amdgcn_readlane(cand, m);
+    const int32_t lim = (L - pm) < 258 ? (L - pm) : 258;
+    const int32_t off = 4 + 4 * lane;
+    const uint32_t x = off < lim ? (lds_load4(dat32, cm + off) ^ lds_load4(dat32, pm + off)) : 0u;
+    const uint64_t miss = __ballot(x != 0);
+    int32_t ml = lim;
+    if (miss) {
+      const int k0 = __builtin_ctzll(miss);
+      const int32_t e = 4 + 4 * k0 + (__builtin_ctz(__builtin_amdgcn_readlane(x, k0)) >> 3);
+      ml = e < lim ? e : lim;
+    }
+    if (lane == m) len = ml;
+    w = m + ml;
+  }
+  carry = w - 64;
+  tok &= live;
+  lit = v & 0xff;
+  dist = p - cand;
+  if (!((tok >> lane) & 1)) return 0;
+  return len >= 4 ? 2 : 1;
+}
+
+// Code lengths for n symbols from their counts, limited to 15 bits, as a complete prefix code (what inflate
+// accepts; a single used symbol gets length 1 — the one incomplete code it allows).  Shannon lengths
+// ceil(log2(total/f)), then an over-full Kraft sum is repaired by lengthening the longest codes below 15, and the
+// slack is filled by shortening the longest codes (the slack is always a multiple of their Kraft weight).
+// Returns the Kraft sum in units of 2^-15.
+__device__ uint32_t build_lengths(const uint32_t* hist, uint32_t* lens, int n, int lane) {
+  uint32_t tot = 0;
+  for (int i = lane; i < n; i += 64) tot += hist[i];
+  tot = wave_sum(tot);
+  uint32_t kr = 0;
+  for (int i = lane; i < n; i += 64) {
+    const uint32_t f = hist[i];
+    uint32_t l = 0;
+    if (f) {
+      const float r = __log2f((float)tot / (float)f);
+      l = (uint32_t)ceilf(r);
+      l = l < 1 ? 1 : (l > 15 ? 15 : l);
+      kr += 1u << (15 - l);
+    }
+    lens[i] = l;
+  }
+  uint32_t K = wave_sum(kr);
+  for (int l = 14; l >= 1 && K > 32768u; --l) {
+    const uint32_t need = (K - 32768u + (1u << (14 - l)) - 1) >> (14 - l);
+    uint32_t seen = 0;
+    for (int r = 0; r < n && seen < need; r += 64) {
+      const int i = r + lane;
+      const bool at = i < n && lens[i] == (uint32_t)l;
+      const uint64_t m = __ballot(at);
+      if (at && seen + lanes_below(m) < need) lens[i] = l + 1;
+      seen += (uint32_t)__builtin_popcountll(m);
+    }
+    K -= (seen < need ? seen : need) << (14 - l);
+  }
+  for (int l = 15; l >= 2 && K < 32768u; --l) {
+    const uint32_t need = (32768u - K) >> (15 - l);
+    uint32_t seen = 0;
+    for (int r = 0; r < n && seen < need; r += 64) {
+      const int i = r + lane;
+      const bool at = i < n && lens[i] == (uint32_t)l;
+      const uint64_t m = __ballot(at);
+      if (at && seen + lanes_below(m) < need) lens[i] = l - 1;
+      seen += (uint32_t)__builtin_popcountll(m);
+    }
+    K += (seen < need ? seen : need) << (15 - l);
+  }
+  __builtin_amdgcn_wave_barrier();
+  return K;
+}
+
+// Canonical codes (RFC 1951 §3.2.2) for n lengths → tab[i] = bit-reversed code | length << 16.  nc: 16 LDS words.
+__device__ void assign_codes(const uint32_t* lens, uint32_t* tab, int n, uint32_t* nc, int lane) {
+  uint32_t cnt = 0;                   // lane l (1..15) counts the codes of length l
+  for (int i = 0; i < n; ++i) cnt += (lane >= 1 && lane <= 15 && lens[i] == (uint32_t)lane) ? 1u : 0u;
+  // next_code[l] = (next_code[l-1] + count[l-1]) << 1
+  uint32_t code = 0;
+  for (int l = 1; l <= 15; ++l) {
+    const uint32_t prev = __shfl(cnt, l - 1, 64);
+    code = (code + (l >= 2 ? prev : 0u)) << 1;
+    if (lane == l) nc[l] = code;
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int r = 0; r < n; r += 64) {
+    const int i = r + lane;
+    const uint32_t l = i < n ? lens[i] : 0u;
+    uint32_t c = 0;
+    for (int ll = 1; ll <= 15; ++ll) {
+      const uint64_t m = __ballot(l == (uint32_t)ll);
+      if (!m) continue;
+      if (l == (uint32_t)ll) c = nc[ll] + lanes_below(m);
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) nc[ll] += (uint32_t)__builtin_popcountll(m);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (i < n) tab[i] = l ? (rev_bits(c, (int)l) | (l << 16)) : 0u;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // One wave per chunk, everything in LDS: [chunk bytes + pad][hash heads][output word window].
 //   per 64-position group: every lane hashes its position and looks up the newest earlier position with that
 //   hash (heads from earlier groups), extends the match 4 bytes at a time;
 //   the greedy parse walks the group with ballots (a literal run up to the next match start in one step);
 //   token codes are placed with a wave prefix sum of their bit lengths and OR-ed into the word window, whose
 //   complete words go to the chunk's slot after every group.
-constexpr int kRing = 128;            // output word ring (a group writes ≤ 63 words)
 
+template <bool kDyn>
 __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restrict__ in, int64_t n_in, int32_t chunk,
                                                          int64_t n_chunks, uint8_t* __restrict__ slots,
                                                          int64_t slot_bytes, int32_t* __restrict__ out_len,
@@ -151,104 +350,117 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
   }
   crc = __shfl(crc, 0, 64);
 
-  // LZ77 + fixed-Huffman coding, one 64-position group at a time
-  uint32_t gbit = 3;                  // BFINAL = 1, BTYPE = 01
-  if (lane == 0) win[0] = 3;
-  int32_t wbase = 0;                  // first deflate word not yet flushed to the slot
+  uint32_t* hist = win + kRing;       // [kNSym] counts: LL at 0, D at kDOff (dynamic only)
+  uint32_t* lens = hist + kNSym;      // [kNSym] code lengths
+  uint32_t* tab = lens + kNSym;       // [kNSym] codes
+  uint32_t* nc = tab + kNSym;         // [16]
+  bool use_dyn = false;
+  uint32_t nll = 257, ndist = 1;
   int32_t carry = 0;                  // how far the previous group's last match reaches into this group
-  __syncthreads();
-  for (int32_t g = 0; g < L; g += 64) {
-    const int32_t p = g + lane;
-    const bool can = p + 4 <= L;
-    const uint32_t v = lds_load4(dat32, p);
-    const uint32_t h = (v * 2654435761u) >> (32 - kHashBits);
-    int32_t cand = can ? (int32_t)head[h] - 1 : -1;
-    __builtin_amdgcn_wave_barrier();
-    if (can) head[h] = (uint16_t)(p + 1);   // lanes sharing a hash: one of them wins (a candidate, not the newest)
-    // a candidate is only checked for its first 4 bytes here; the full length is measured for the positions the
-    // greedy parse actually takes, by the whole wave at once (64 lanes × 4 bytes = 256 bytes per step)
-    const bool is_m = cand >= 0 && p - cand <= kMaxDist && lds_load4(dat32, cand) == v;
-    const uint64_t mm = __ballot(is_m);
-    const uint64_t live = (L - g) >= 64 ? ~0ull : ((1ull << (L - g)) - 1);
-    uint64_t tok = 0;
-    int32_t len = 0;                  // match length, set on the lanes that start a match token
-    int32_t w = carry;
-    while (w < 64) {
-      const uint64_t from = ~0ull << w;
-      const uint64_t rest = mm & from;
-      if (rest == 0) { tok |= from; w = 64; break; }
-      const int m = __builtin_ctzll(rest);
-      tok |= (from & ~(~0ull << m)) | (1ull << m);
-      const int32_t pm = g + m, cm = __builtin_amdgcn_readlane(cand, m);
-      const int32_t lim = (L - pm) < 258 ? (L - pm) : 258;
-      const int32_t off = 4 + 4 * lane;
-      const uint32_t x = off < lim ? (lds_load4(dat32, cm + off) ^ lds_load4(dat32, pm + off)) : 0u;
-      const uint64_t miss = __ballot(x != 0);
-      int32_t ml = lim;
-      if (miss) {
-        const int k0 = __builtin_ctzll(miss);
-        const int32_t e = 4 + 4 * k0 + (__builtin_ctz(__builtin_amdgcn_readlane(x, k0)) >> 3);
-        ml = e < lim ? e : lim;
-      }
-      if (lane == m) len = ml;
-      w = m + ml;
-    }
-    carry = w - 64;
-    tok &= live;
-    // this lane's code (≤ 31 bits, LSB-first)
-    uint32_t bits = 0, nb = 0;
-    if ((tok >> lane) & 1) {
-      if (len >= 4) {
-        const uint32_t x = (uint32_t)(len - 3);
-        uint32_t sym, eb = 0, ev = 0;
-        if (len == 258) sym = 285;
-        else if (x < 8) sym = 257 + x;
-        else { const int hb = 31 - __builtin_clz(x); eb = hb - 2; sym = 257 + 4 * (hb - 1) + ((x >> eb) & 3); ev = x & ((1u << eb) - 1); }
-        uint32_t cl;
-        if (sym < 280) { bits = rev_bits(sym - 256, 7); cl = 7; }
-        else { bits = rev_bits(0xC0 + (sym - 280), 8); cl = 8; }
-        bits |= ev << cl; nb = cl + eb;
-        const uint32_t y = (uint32_t)(p - cand - 1);
-        uint32_t dc, deb = 0, dev = 0;
-        if (y < 4) dc = y;
-        else { const int hb = 31 - __builtin_clz(y); deb = hb - 1; dc = 2 * hb + ((y >> deb) & 1); dev = y & ((1u << deb) - 1); }
-        bits |= rev_bits(dc, 5) << nb; nb += 5;
-        bits |= dev << nb; nb += deb;
-      } else {
-        const uint32_t b = v & 0xff;
-        if (b < 144) { bits = rev_bits(0x30 + b, 8); nb = 8; }
-        else { bits = rev_bits(0x190 + (b - 144), 9); nb = 9; }
+  if constexpr (kDyn) {
+    // pass 1: parse, count symbols
+    for (int k = lane; k < kNSym; k += 64) hist[k] = 0;
+    __syncthreads();
+    for (int32_t g = 0; g < L; g += 64) {
+      uint32_t lit; int32_t len, dist;
+      const int t = parse_group(dat32, head, L, g, carry, lane, lit, len, dist);
+      if (t == 1) {
+        atomicAdd(&hist[lit], 1u);
+      } else if (t == 2) {
+        uint32_t sym, eb, ev, dc, deb, dev;
+        len_sym(len, sym, eb, ev);
+        dist_sym(dist, dc, deb, dev);
+        atomicAdd(&hist[sym], 1u);
+        atomicAdd(&hist[kDOff + dc], 1u);
       }
     }
-    // exclusive prefix sum of the code lengths (≤ 31: five bit planes, ballots + mbcnt, no LDS round trips)
-    uint32_t excl = 0, total = 0;
-    for (int bp = 0; bp < 5; ++bp) {
-      const uint64_t m = __ballot((nb >> bp) & 1);
-      excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bp;
-      total += (uint32_t)__builtin_popcountll(m) << bp;
-    }
-    if (nb) {
-      const uint32_t pos = gbit + excl;
-      const uint32_t wi = pos >> 5, sh = pos & 31;
-      atomicOr(&win[wi & (kRing - 1)], bits << sh);
-      if (sh && sh + nb > 32) atomicOr(&win[(wi + 1) & (kRing - 1)], bits >> (32 - sh));
-    }
-    gbit += total;
-    // flush the words this group completed (ring slots are zeroed as they leave; a wave's LDS operations complete
-    // in order, so no barrier is needed between the ORs above and these reads)
+    if (lane == 0) hist[256] += 1;      // end of block
+    for (int k = lane; k < kHashSize / 2; k += 64) gz_sh[(chunk >> 2) + 4 + k] = 0;
+    __syncthreads();
+
+    // dynamic code lengths; the block is written with them only when that (header included) beats the fixed code
+    // (the extra bits of lengths and distances are the same either way)
+    for (int k = lane; k < kNSym; k += 64) lens[k] = 0;
     __builtin_amdgcn_wave_barrier();
-    const int32_t nfull = (int32_t)(gbit >> 5) - wbase;
-    for (int k = lane; k < nfull; k += 64) {
-      const int idx = (wbase + k) & (kRing - 1);
-      dst[wbase + k] = win[idx];
-      win[idx] = 0;
+    const uint32_t k_ll = build_lengths(hist, lens, kNLL, lane);
+    const uint32_t k_d = build_lengths(hist + kDOff, lens + kDOff, kND, lane);
+    const uint64_t used_d = __ballot(lane < kND && lens[kDOff + lane] != 0);
+    if (used_d == 0 && lane == 0) lens[kDOff] = 1;                         // no match: one (unused) distance code
+    const bool single_d = __builtin_popcountll(used_d) <= 1;
+    uint32_t hi_ll = 0;
+    for (int i = lane; i < kNLL; i += 64) if (lens[i]) hi_ll = i;
+    for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(hi_ll, d, 64); hi_ll = o > hi_ll ? o : hi_ll; }
+    nll = hi_ll + 1 < 257 ? 257 : hi_ll + 1;
+    ndist = used_d ? 64 - __builtin_clzll(used_d) : 1;
+    uint32_t dyn = 0, fix = 0;
+    for (int i = lane; i < kNSym; i += 64) {
+      const uint32_t f = hist[i];
+      const uint32_t fl = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < kDOff ? 8 : 5;
+      dyn += f * lens[i];
+      fix += f * fl;
     }
-    wbase += nfull;
-    __builtin_amdgcn_wave_barrier();
+    dyn = wave_sum(dyn) + 17 + 57 + 4 * (nll + ndist);
+    fix = wave_sum(fix);
+    use_dyn = k_ll == 32768u && (k_d == 32768u || single_d) && dyn < fix;
+    __syncthreads();
+    if (!use_dyn)
+      for (int i = lane; i < kNSym; i += 64)
+        lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < kDOff ? 8 : (i < kDOff + kND ? 5 : 0);
+    __syncthreads();
+    assign_codes(lens, tab, kDOff, nc, lane);
+    for (int k = lane; k < 16; k += 64) nc[k] = 0;
+    __syncthreads();
+    assign_codes(lens + kDOff, tab + kDOff, kND, nc, lane);
+    __syncthreads();
+
+
   }
-  // end of block (code 256 = 7 zero bits), then the trailer bytes right after the last deflate byte
-  gbit += 7;
-  const uint32_t nbytes = (gbit + 7) >> 3;            // deflate bytes
+  Out o;
+  o.win = win;
+  o.dst = dst;
+  if (use_dyn) {
+    // BFINAL, BTYPE = 10, HLIT, HDIST, HCLEN = 15 (all 19 code-length code lengths follow); the code-length code
+    // gives symbols 0..15 four bits each (complete) and RLE symbols 16-18 none
+    constexpr uint8_t kOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    uint32_t a = 0, na = 0;
+    if (lane == 0) { a = 1u | (2u << 1) | ((nll - 257) << 3) | ((ndist - 1) << 8) | (15u << 13); na = 17; }
+    else if (lane <= 19) { a = kOrder[lane - 1] <= 15 ? 4u : 0u; na = 3; }
+    o.emit(a, na, 0, 0, lane);
+    for (uint32_t r = 0; r < nll + ndist; r += 64) {
+      const uint32_t i = r + lane;
+      uint32_t v = 0, nv = 0;
+      if (i < nll + ndist) { v = rev_bits(i < nll ? lens[i] : lens[kDOff + (i - nll)], 4); nv = 4; }
+      o.emit(v, nv, 0, 0, lane);
+    }
+  } else {
+    o.emit(lane == 0 ? 3u : 0u, lane == 0 ? 3u : 0u, 0, 0, lane);      // BFINAL, BTYPE = 01
+  }
+
+  // pass 2: the same parse, coded
+  carry = 0;
+  for (int32_t g = 0; g < L; g += 64) {
+    uint32_t lit; int32_t len, dist;
+    const int t = parse_group(dat32, head, L, g, carry, lane, lit, len, dist);
+    uint32_t a = 0, na = 0, b = 0, nb = 0;
+    if (t == 1) {
+      const uint32_t e = kDyn ? tab[lit] : fixed_code(lit);
+      a = e & 0xffff; na = e >> 16;
+    } else if (t == 2) {
+      uint32_t sym, eb, ev, dc, deb, dev;
+      len_sym(len, sym, eb, ev);
+      dist_sym(dist, dc, deb, dev);
+      const uint32_t e = kDyn ? tab[sym] : fixed_code(sym), e2 = kDyn ? tab[kDOff + dc] : (rev_bits(dc, 5) | (5u << 16));
+      a = (e & 0xffff) | (ev << (e >> 16)); na = (e >> 16) + eb;
+      b = (e2 & 0xffff) | (dev << (e2 >> 16)); nb = (e2 >> 16) + deb;
+    }
+    o.emit(a, na, b, nb, lane);
+  }
+  {
+    const uint32_t e = kDyn ? tab[256] : fixed_code(256);               // end of block
+    o.emit(lane == 0 ? (e & 0xffff) : 0u, lane == 0 ? (e >> 16) : 0u, 0, 0, lane);
+  }
+  // the trailer bytes right after the last deflate byte
+  const uint32_t nbytes = (o.gbit + 7) >> 3;          // deflate bytes
   if (lane < 8) {
     const uint32_t val = lane < 4 ? crc : (uint32_t)L;
     const uint32_t byte = (val >> (8 * (lane & 3))) & 0xff;
@@ -257,7 +469,7 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
   }
   __syncthreads();
   const int32_t end_words = (int32_t)((nbytes + 8 + 3) >> 2);
-  for (int k = wbase + lane; k < end_words; k += 64) dst[k] = win[k & (kRing - 1)];
+  for (int k = o.wbase + lane; k < end_words; k += 64) dst[k] = win[k & (kRing - 1)];
   if (lane == 0) out_len[c] = (int32_t)(10 + nbytes + 8);
 }
 
@@ -282,19 +494,23 @@ DXA_API int64_t dxa_gzip_slot_bytes(int32_t chunk) {
 }
 
 DXA_API int dxa_gzip_chunks(const uint8_t* in, int64_t n_in, int32_t chunk, uint8_t* slots, int32_t* out_len,
-                            void* st) {
+                            int32_t dynamic, void* st) {
   if (n_in <= 0) return 0;
   if (chunk < 64 || chunk > 32768 || (chunk & 63)) return (int)hipErrorInvalidValue;   // deflate window
   const int64_t n_chunks = (n_in + chunk - 1) / chunk;
   const int64_t slot = dxa_gzip_slot_bytes(chunk);
-  const size_t lds = ((size_t)(chunk >> 2) + 4 + kHashSize / 2 + kRing) * 4;
+  const size_t lds = ((size_t)(chunk >> 2) + 4 + kHashSize / 2 + kRing + (dynamic ? 3 * kNSym + 16 : 0)) * 4;
   CrcPow pw{};
   int32_t words = ((chunk + 63) / 64 + 3) / 4;
   if ((words & 1) == 0) ++words;
   pw.slice = words * 4;
   for (int l = 0; l < 6; ++l) pw.x[l] = host_x8n((uint64_t)pw.slice << l);
-  hipLaunchKernelGGL(gzip_chunks_kernel, dim3((unsigned)n_chunks), dim3(64), lds, (hipStream_t)st, in, n_in, chunk,
-                     n_chunks, slots, slot, out_len, pw);
+  if (dynamic)
+    hipLaunchKernelGGL(gzip_chunks_kernel<true>, dim3((unsigned)n_chunks), dim3(64), lds, (hipStream_t)st, in, n_in,
+                       chunk, n_chunks, slots, slot, out_len, pw);
+  else
+    hipLaunchKernelGGL(gzip_chunks_kernel<false>, dim3((unsigned)n_chunks), dim3(64), lds, (hipStream_t)st, in, n_in,
+                       chunk, n_chunks, slots, slot, out_len, pw);
   return (int)hipGetLastError();
 }
 

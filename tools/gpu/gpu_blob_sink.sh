@@ -12,3 +12,7 @@ DXA_GPU_GZIP=0 timeout -k 10 300 python bench.py --flow passthrough --sink blob 
 du -sh /tmp/dxa_bench_passthrough_0/out
 rm -rf /tmp/dxa_bench_passthrough_0/out
 summ gpurun_out/pt_blob_host.log
+DXA_GZIP_DYNAMIC=1 timeout -k 10 300 python bench.py --flow passthrough --sink blob --steps 10 > gpurun_out/pt_blob_dyn.log 2>&1 || { tail -20 gpurun_out/pt_blob_dyn.log; exit 1; }
+du -sh /tmp/dxa_bench_passthrough_0/out
+rm -rf /tmp/dxa_bench_passthrough_0/out
+summ gpurun_out/pt_blob_dyn.log
