@@ -559,6 +559,31 @@ def _sha2(s, bits=256):
     return None if h is None else h(str(s).encode()).hexdigest()
 
 
+def _sha2_kind(args):
+    b = args[1] if len(args) > 1 else None
+    if b is None or not isinstance(b, ConstColumn) or b.value is None:
+        return None
+    return {0: 2, 256: 2, 224: 3}.get(int(b.value))          # 384 / 512: host
+
+
+def _f_digest(kind, host, out_type="string"):
+    """md5 / sha1 / sha2 / crc32 / hex / base64: device kernels (ops/csrc/digest.hip) for device string columns,
+    the host function otherwise (constants, numeric hex, sha2 384/512)."""
+    def f(e, scope, ctx, subst):
+        args = _args(e, scope, ctx, subst)
+        a = args[0] if args else None
+        k = kind(args) if callable(kind) else kind
+        if k is not None and _gpu_str(a):
+            from ..ops import strings as S
+            if k == "crc32":
+                return PrimColumn("long", S.crc32(a), a.valid)
+            if k in ("hex", "base64"):
+                return S.encode(a, 0 if k == "hex" else 1)
+            return S.digest(a, k)
+        return _host_string_fn(host, out_type)(e, scope, ctx, subst)
+    return f
+
+
 def _hex(v):
     if isinstance(v, (int, bool)) and not isinstance(v, bool):
         return format(v & 0xFFFFFFFFFFFFFFFF, "X") if v < 0 else format(v, "X")
@@ -1053,12 +1078,14 @@ def _register():
     reg("sequence", _f_sequence)
     reg("map_keys", _f_map_part("keys"))
     reg("map_values", _f_map_part("values"))
-    reg("sha2", _host_string_fn(_sha2))
-    reg("sha", _host_string_fn(lambda s: hashlib.sha1(str(s).encode()).hexdigest()))
-    reg("crc32", _host_string_fn(lambda s: zlib.crc32(str(s).encode()) & 0xFFFFFFFF, "long"))
-    reg("base64", _host_string_fn(lambda s: _b64.b64encode(str(s).encode()).decode()))
+    reg("sha2", _f_digest(_sha2_kind, _sha2))
+    reg("sha", _f_digest(1, lambda s: hashlib.sha1(str(s).encode()).hexdigest()))
+    reg("sha1", _f_digest(1, lambda s: hashlib.sha1(str(s).encode()).hexdigest()))
+    reg("md5", _f_digest(0, lambda s: hashlib.md5(str(s).encode()).hexdigest()))
+    reg("crc32", _f_digest("crc32", lambda s: zlib.crc32(str(s).encode()) & 0xFFFFFFFF, "long"))
+    reg("base64", _f_digest("base64", lambda s: _b64.b64encode(str(s).encode()).decode()))
     reg("unbase64", _host_string_fn(lambda s: _b64.b64decode(str(s)).decode("utf-8", errors="replace")))
-    reg("hex", _host_string_fn(_hex))
+    reg("hex", _f_digest("hex", _hex))
     reg("unhex", _host_string_fn(lambda s: bytes.fromhex(str(s)).decode("utf-8", errors="replace")))
     reg("initcap", _host_string_fn(_initcap))
     reg("repeat", _host_string_fn(lambda s, k: str(s) * max(0, int(k))))

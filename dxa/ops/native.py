@@ -66,6 +66,9 @@ _SIGS = {
     "dxa_str_rlike": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_i32, c_p, c_p],
     "dxa_gzip_chunks": [c_p, c_i64, c_i32, c_p, c_p, c_i32, c_p],
     "dxa_gzip_pack": [c_p, c_i32, c_p, c_p, c_i64, c_p, c_p],
+    "dxa_str_digest": [c_p, c_p, c_p, c_i64, c_i32, c_p, c_p],
+    "dxa_str_crc32": [c_p, c_p, c_p, c_i64, c_p, c_p],
+    "dxa_str_encode": [c_p, c_p, c_p, c_i64, c_i32, c_p, c_p, c_p],
     "dxa_f64_str_len": [c_p, c_p, c_i64, c_p, c_p],
     "dxa_f64_str_write": [c_p, c_p, c_i64, c_p, c_p, c_p],
     "dxa_str_to_num": [c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p, c_p],

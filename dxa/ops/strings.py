@@ -207,6 +207,45 @@ def rlike(col, dfa) -> torch.Tensor:
     return out
 
 
+_DIGEST_WIDTH = {0: 32, 1: 40, 2: 64, 3: 56}
+
+
+def digest(col, kind: int):
+    """md5 (0) / sha1 (1) / sha256 (2) / sha224 (3) of every row on the device → lower-case hex StrColumn."""
+    from ..engine.column import StrColumn
+    n, w = col.length, _DIGEST_WIDTH[kind]
+    dev = col.device
+    out = _alloc_arena(n * w, dev)
+    if n:
+        N.call("dxa_str_digest", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, kind, N.ptr(out),
+               N.stream_handle(dev))
+    starts = torch.arange(n, dtype=torch.int64, device=dev) * w
+    return StrColumn(out, starts, torch.full((n,), w, dtype=torch.int32, device=dev), col.valid)
+
+
+def crc32(col) -> torch.Tensor:
+    """CRC-32 of every row's bytes on the device → int64 tensor."""
+    out = torch.empty(col.length, dtype=torch.int64, device=col.device)
+    if col.length:
+        N.call("dxa_str_crc32", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), col.length, N.ptr(out),
+               N.stream_handle(col.device))
+    return out
+
+
+def encode(col, mode: int):
+    """hex (0: upper-case, 2 chars per byte) / base64 (1: padded) of every row on the device → StrColumn."""
+    from ..engine.column import StrColumn
+    n, dev = col.length, col.device
+    l64 = col.lens.to(torch.int64)
+    out_lens = l64 * 2 if mode == 0 else (l64 + 2) // 3 * 4
+    off, total = _offsets(out_lens)
+    out = _alloc_arena(total, dev)
+    if n:
+        N.call("dxa_str_encode", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, mode, N.ptr(off),
+               N.ptr(out), N.stream_handle(dev))
+    return StrColumn(out, off, out_lens.to(torch.int32), col.valid)
+
+
 def _raw_bytes(col) -> List[bytes]:
     arena = col.arena.cpu().numpy().tobytes()
     return [arena[s:s + l] for s, l in zip(col.starts.cpu().tolist(), col.lens.cpu().tolist())]

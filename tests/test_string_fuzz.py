@@ -175,3 +175,30 @@ def test_rlike_fuzz_gpu_match_cpu(gpu):
         pat = _rand_regex(rnd)
         sql = f"SELECT s RLIKE '{_q(pat)}' AS m, s NOT RLIKE '{_q(pat)}' AS n FROM F"
         assert _run(sql, vals, gpu) == _run(sql, vals, "cpu"), pat
+
+
+def test_digest_functions_cpu_reference():
+    import base64
+    import hashlib
+    import zlib
+    vals = ["", "abc", "日本語", None]
+    out = _run("SELECT md5(s) AS a, sha1(s) AS b, sha2(s, 256) AS c, sha2(s, 224) AS d, crc32(s) AS e, hex(s) AS f, "
+               "base64(s) AS g FROM F", vals, "cpu")
+    for i, v in enumerate(vals):
+        if v is None:
+            assert all(c[i] is None for c in out)
+            continue
+        b = v.encode()
+        assert [c[i] for c in out] == [hashlib.md5(b).hexdigest(), hashlib.sha1(b).hexdigest(),
+                                       hashlib.sha256(b).hexdigest(), hashlib.sha224(b).hexdigest(),
+                                       zlib.crc32(b), b.hex().upper(), base64.b64encode(b).decode()]
+
+
+@pytest.mark.gpu
+def test_digest_functions_gpu_match_cpu(gpu):
+    rnd = random.Random(37)
+    vals = [_rand_str(rnd, 40) for _ in range(N)]
+    vals += ["x" * k for k in (0, 1, 54, 55, 56, 57, 63, 64, 65, 119, 120, 1000)] + ["é" * 28, "日" * 40]
+    sql = ("SELECT md5(s) AS a, sha1(s) AS b, sha2(s, 256) AS c, sha2(s, 224) AS d, sha2(s, 0) AS e, crc32(s) AS f, "
+           "hex(s) AS g, base64(s) AS h, sha2(s, 512) AS i FROM F")
+    assert _run(sql, vals, gpu) == _run(sql, vals, "cpu")
