@@ -559,6 +559,75 @@ def _sha2(s, bits=256):
     return None if h is None else h(str(s).encode()).hexdigest()
 
 
+def _java_regex(p):
+    from ..ops.regex_dfa import java_to_python
+    return re.compile(java_to_python(str(p)), re.ASCII)
+
+
+def _host_regexp_extract(s, p, g=1):
+    m = _java_regex(p).search(str(s))
+    return (m.group(int(g)) or "") if m else ""
+
+
+def _host_regexp_replace(s, p, r):
+    """Java Matcher.replaceAll: after an empty match the next search starts one character later (Python's re.sub
+    would retry the same position for a non-empty match, which Java does not)."""
+    from ..ops.regex_vm import replacement_tokens
+    rx = _java_regex(p)
+    toks = replacement_tokens(str(r), rx.groups)
+    s = str(s)
+
+    def expand(m):
+        out = bytearray()
+        for t in toks:
+            if t >= 0:
+                out.append(t)
+            else:
+                out += (m.group(-1 - t) or "").encode("utf-8")
+        return out.decode("utf-8")
+    out, pos, last = [], 0, 0
+    while pos <= len(s):
+        m = rx.search(s, pos)
+        if m is None:
+            break
+        out.append(s[last:m.start()])
+        out.append(expand(m))
+        last = m.end()
+        pos = m.end() if m.end() > m.start() else m.end() + 1
+    out.append(s[last:])
+    return "".join(out)
+
+
+def _f_regexp(kind):
+    """regexp_extract / regexp_replace: the backtracking program on the device (ops/regex_vm.py) for device string
+    columns with a constant pattern; rows over the kernel's budget and everything else go to the host regex (Java
+    syntax read the Java way)."""
+    host = _host_regexp_extract if kind == "extract" else _host_regexp_replace
+
+    def f(e, scope, ctx, subst):
+        args = _args(e, scope, ctx, subst)
+        a = args[0] if args else None
+        consts = all(isinstance(x, ConstColumn) and x.value is not None for x in args[1:])
+        if _gpu_str(a) and consts and len(args) >= 2:
+            from ..ops import regex_vm, strings as S
+            try:
+                prog = regex_vm.compile_vm(str(args[1].value))
+                if kind == "extract":
+                    g = int(args[2].value) if len(args) > 2 else 1
+                    if not 0 <= g <= min(prog.ngroups, regex_vm.MAX_GROUPS):
+                        raise regex_vm.Unsupported("group index")
+                    out, bad = S.regex_extract(a, prog, g)
+                else:
+                    toks = regex_vm.replacement_tokens(str(args[2].value) if len(args) > 2 else "", prog.ngroups)
+                    out, bad = S.regex_replace(a, prog, toks)
+                if not bool(bad.any()):
+                    return out
+            except regex_vm.Unsupported:
+                pass
+        return _host_string_fn(host)(e, scope, ctx, subst)
+    return f
+
+
 def _sha2_kind(args):
     b = args[1] if len(args) > 1 else None
     if b is None or not isinstance(b, ConstColumn) or b.value is None:
@@ -1078,6 +1147,8 @@ def _register():
     reg("sequence", _f_sequence)
     reg("map_keys", _f_map_part("keys"))
     reg("map_values", _f_map_part("values"))
+    reg("regexp_extract", _f_regexp("extract"))
+    reg("regexp_replace", _f_regexp("replace"))
     reg("sha2", _f_digest(_sha2_kind, _sha2))
     reg("sha", _f_digest(1, lambda s: hashlib.sha1(str(s).encode()).hexdigest()))
     reg("sha1", _f_digest(1, lambda s: hashlib.sha1(str(s).encode()).hexdigest()))

@@ -990,6 +990,150 @@ DXA_API int dxa_str_like(const uint8_t* arena, const int64_t* starts, const int3
   return (int)hipGetLastError();
 }
 
+// regexp_extract / regexp_replace: a backtracking program (regex_vm.py) per row, Java's match choice (leftmost
+// start; SPLIT x,y tries x first).  Backtrack stack and step budget are bounded; a row that exceeds either gets
+// status 1 and the host recomputes the column.
+constexpr int kRxStack = 64;
+constexpr int kRxBudget = 1 << 16;
+constexpr int kRxCaps = 32;                // 2 × (9 groups + 1) captures, then loop position registers
+
+struct RxArgs {
+  const uint8_t* arena; const int64_t* starts; const int32_t* lens; int64_t n;
+  const int4* prog; const uint32_t* sets;
+  int32_t mode;                       // 0 extract group, 1 replace: lengths, 2 replace: write
+  int32_t group;
+  const int32_t* rep; int32_t nrep;   // replacement tokens: byte, or -1-k for group k
+  int64_t* out_start; int32_t* out_len; const int64_t* out_off; uint8_t* out; uint8_t* status;
+};
+
+__device__ __forceinline__ bool rx_bit(const uint32_t* sets, int k, uint32_t c) {
+  return (sets[k * 8 + (c >> 5)] >> (c & 31)) & 1;
+}
+
+// 1 matched (cap filled), 0 no match from this start, -1 over budget
+__device__ int rx_match_at(const RxArgs& a, const uint8_t* s, int32_t len, int32_t start, int32_t* cap, int& steps) {
+  int32_t stk[3 * kRxStack];          // (kind << 24 | pc or capture slot, sp or old value) + spare
+  int top = 0;
+  for (int k = 0; k < kRxCaps; ++k) cap[k] = -1;
+  stk[0] = 0; stk[1] = start; top = 1;
+  while (top > 0) {
+    --top;
+    const int32_t tag = stk[2 * top];
+    if (tag < 0) { cap[-1 - tag] = stk[2 * top + 1]; continue; }            // restore a capture
+    int32_t pc = tag, sp = stk[2 * top + 1];
+    while (true) {
+      if (++steps > kRxBudget) return -1;
+      const int4 in = a.prog[pc];
+      bool ok = true;
+      switch (in.x) {
+        case 0:                                   // CHAR
+          ok = sp < len && s[sp] == (uint8_t)in.y; sp += ok; ++pc; break;
+        case 1:                                   // SET
+          ok = sp < len && s[sp] < 128 && rx_bit(a.sets, in.y, s[sp]); sp += ok; ++pc; break;
+        case 2: {                                 // ANY: one code point, not a line terminator
+          if (sp >= len) { ok = false; break; }
+          const uint8_t c = s[sp];
+          const int32_t u = utf8_len(c);
+          if (c == '\n' || c == '\r') ok = false;
+          else if (c == 0xC2 && sp + 1 < len && s[sp + 1] == 0x85) ok = false;
+          else if (c == 0xE2 && sp + 2 < len && s[sp + 1] == 0x80 && (s[sp + 2] == 0xA8 || s[sp + 2] == 0xA9)) ok = false;
+          sp += (sp + u <= len) ? u : len - sp; ++pc; break;
+        }
+        case 3: {                                 // NOTSET: one code point outside an ASCII set
+          if (sp >= len) { ok = false; break; }
+          const uint8_t c = s[sp];
+          if (c < 128) { ok = !rx_bit(a.sets, in.y, c); sp += 1; }
+          else { const int32_t u = utf8_len(c); sp += (sp + u <= len) ? u : len - sp; }
+          ++pc; break;
+        }
+        case 4:                                   // SPLIT: try a, remember b
+          if (top >= kRxStack) return -1;
+          stk[2 * top] = in.z; stk[2 * top + 1] = sp; ++top; pc = in.y; break;
+        case 5: pc = in.y; break;                 // JMP
+        case 6:                                   // SAVE
+          if (top >= kRxStack) return -1;
+          stk[2 * top] = -1 - in.y; stk[2 * top + 1] = cap[in.y]; ++top;
+          cap[in.y] = sp; ++pc; break;
+        case 7: ok = sp == 0; ++pc; break;        // BOL
+        case 8: ok = sp == len || (sp == len - 1 && s[sp] == '\n'); ++pc; break;       // EOL
+        case 10: pc = sp == cap[in.y] ? in.w : in.z; break;                          // LOOP: no progress → leave
+        case 9: return 1;                         // MATCH
+        default: return -1;
+      }
+      if (!ok) break;
+    }
+  }
+  return 0;
+}
+
+// leftmost match starting at or after `from` (code-point boundaries): 1 found, 0 none, -1 over budget
+__device__ int rx_find(const RxArgs& a, const uint8_t* s, int32_t len, int32_t from, int32_t* cap, int& steps) {
+  for (int32_t st = from; st <= len; ++st) {
+    if (st < len && (s[st] & 0xC0) == 0x80) continue;                    // inside a code point
+    const int r = rx_match_at(a, s, len, st, cap, steps);
+    if (r != 0) return r;
+  }
+  return 0;
+}
+
+__global__ void __launch_bounds__(256) str_regex_kernel(RxArgs a) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = a.arena + a.starts[i];
+    const int32_t len = a.lens[i];
+    int32_t cap[kRxCaps];
+    int steps = 0;
+    uint8_t bad = 0;
+    if (a.mode == 0) {
+      const int r = rx_find(a, s, len, 0, cap, steps);
+      int32_t b = 0, e = 0;
+      if (r == 1 && cap[2 * a.group] >= 0 && cap[2 * a.group + 1] >= 0) { b = cap[2 * a.group]; e = cap[2 * a.group + 1]; }
+      bad = r < 0;
+      a.out_start[i] = a.starts[i] + b;
+      a.out_len[i] = e - b;
+    } else {
+      uint8_t* o = a.mode == 2 ? a.out + a.out_off[i] : nullptr;
+      int64_t olen = 0;
+      int32_t pos = 0, last = 0;
+      while (pos <= len) {
+        const int r = rx_find(a, s, len, pos, cap, steps);
+        if (r < 0) { bad = 1; break; }
+        if (r == 0) break;
+        const int32_t ms = cap[0], me = cap[1];
+        if (o) for (int32_t k = last; k < ms; ++k) o[olen + k - last] = s[k];
+        olen += ms - last;
+        for (int32_t t = 0; t < a.nrep; ++t) {
+          const int32_t tk = a.rep[t];
+          if (tk >= 0) { if (o) o[olen] = (uint8_t)tk; ++olen; continue; }
+          const int32_t g = -1 - tk, gb = cap[2 * g], ge = cap[2 * g + 1];
+          if (gb < 0 || ge < 0) continue;
+          if (o) for (int32_t k = gb; k < ge; ++k) o[olen + k - gb] = s[k];
+          olen += ge - gb;
+        }
+        last = me;
+        pos = me > ms ? me : me + (me < len ? utf8_len(s[me]) : 1);
+      }
+      if (!bad) {
+        if (o) for (int32_t k = last; k < len; ++k) o[olen + k - last] = s[k];
+        olen += len - last;
+      }
+      if (a.mode == 1) a.out_len[i] = bad ? 0 : (int32_t)olen;
+    }
+    a.status[i] = bad;
+  }
+}
+
+DXA_API int dxa_str_regex(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                          const int32_t* prog, const int32_t* sets, int32_t mode, int32_t group, const int32_t* rep,
+                          int32_t nrep, int64_t* out_start, int32_t* out_len, const int64_t* out_off, uint8_t* out,
+                          uint8_t* status, void* st) {
+  if (n <= 0) return 0;
+  if (mode < 0 || mode > 2 || group < 0 || group > 9) return (int)hipErrorInvalidValue;
+  RxArgs a{arena, starts, lens, n, (const int4*)prog, (const uint32_t*)sets, mode, group, rep, nrep,
+           out_start, out_len, out_off, out, status};
+  hipLaunchKernelGGL(str_regex_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, a);
+  return (int)hipGetLastError();
+}
+
 // RLIKE on the device: a byte-level DFA (regex_dfa.py) over symbol classes, run from BOS through the bytes to
 // EOS.  blob = [class of each symbol (258) | next-state table (states × classes)], staged in LDS; a table entry with
 // bit 15 set leads to a terminal state (dead, or accepting — accepting states absorb), so a row stops as soon as

@@ -35,7 +35,8 @@ _CONT = frozenset(range(0x80, 0xC0))
 
 
 # ---- AST ------------------------------------------------------------------------------------------------------
-# ("seq", [nodes]) ("alt", [nodes]) ("rep", node, lo, hi|None) ("set", frozenset bytes) ("bytes", b"...")
+# ("seq", [nodes]) ("alt", [nodes]) ("rep", node, lo, hi|None, lazy) ("set", frozenset bytes) ("bytes", b"...")
+# ("group", index, node) a capturing group (the DFA reads it as its node)
 # ("any",) one code point except line terminators; ("notset", frozenset ascii) any code point outside an ASCII
 # set (incl. every multi-byte one); ("bos",) ("eos",)
 
@@ -43,6 +44,7 @@ _CONT = frozenset(range(0x80, 0xC0))
 class _Parser:
     def __init__(self, p: str):
         self.p, self.i = p, 0
+        self.groups = 0
 
     def peek(self):
         return self.p[self.i] if self.i < len(self.p) else None
@@ -77,23 +79,24 @@ class _Parser:
             c = self.peek()
             if c == "*":
                 self.take()
-                atom = ("rep", atom, 0, None)
+                atom = ("rep", atom, 0, None, False)
             elif c == "+":
                 self.take()
-                atom = ("rep", atom, 1, None)
+                atom = ("rep", atom, 1, None, False)
             elif c == "?":
                 self.take()
-                atom = ("rep", atom, 0, 1)
+                atom = ("rep", atom, 0, 1, False)
             elif c == "{" and self._is_counted():
                 lo, hi = self._counted()
-                atom = ("rep", atom, lo, hi)
+                atom = ("rep", atom, lo, hi, False)
             else:
                 return atom
             if atom[0] == "rep" and atom[1][0] in ("bos", "eos"):
                 raise Unsupported("quantified anchor")
             nxt = self.peek()
-            if nxt == "?":                  # lazy: same language
+            if nxt == "?":                  # lazy: the same language (the DFA), another match choice (the VM)
                 self.take()
+                atom = atom[:4] + (True,)
             elif nxt == "+":
                 raise Unsupported("possessive quantifier")
 
@@ -118,16 +121,21 @@ class _Parser:
     def atom(self):
         c = self.take()
         if c == "(":
+            capture = True
             if self.peek() == "?":
                 self.take()
                 if self.peek() != ":":
                     raise Unsupported("group construct (?" + (self.peek() or ""))
                 self.take()
+                capture = False
+            if capture:
+                self.groups += 1
+                idx = self.groups
             node = self.alt()
             if self.peek() != ")":
                 raise Unsupported("unclosed group")
             self.take()
-            return node
+            return ("group", idx, node) if capture else node
         if c == ".":
             return ("any",)
         if c == "^":
@@ -311,8 +319,10 @@ class _NFA:
                 self.eps[s].append(a)
                 self.eps[b].append(e)
             return s, e
+        if k == "group":
+            return self.build(node[2])
         if k == "rep":
-            _, sub, lo, hi = node
+            _, sub, lo, hi, _lazy = node
             s = e = self.state()
             for _ in range(lo):
                 a, b = self.build(sub)

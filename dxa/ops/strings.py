@@ -246,6 +246,50 @@ def encode(col, mode: int):
     return StrColumn(out, off, out_lens.to(torch.int32), col.valid)
 
 
+def _vm_tensors(prog, device):
+    cache = prog.__dict__.setdefault("_dev", {})
+    t = cache.get(device)
+    if t is None:
+        t = cache[device] = (torch.tensor(prog.code, dtype=torch.int32).to(device),
+                             torch.tensor(prog.sets, dtype=torch.int32).to(device))
+    return t
+
+
+def regex_extract(col, prog, group: int):
+    """regexp_extract on the device: views into the source arena (no copy).  Returns (StrColumn, fallback mask)
+    — rows whose match exceeded the kernel's backtracking budget are flagged for the host."""
+    from ..engine.column import StrColumn
+    n, dev = col.length, col.device
+    code, sets = _vm_tensors(prog, dev)
+    starts = torch.empty(n, dtype=torch.int64, device=dev)
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    if n:
+        N.call("dxa_str_regex", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(code), N.ptr(sets),
+               0, group, 0, 0, N.ptr(starts), N.ptr(lens), 0, 0, N.ptr(status), N.stream_handle(dev))
+    return StrColumn(col.arena, starts, lens, col.valid), status.bool()
+
+
+def regex_replace(col, prog, tokens: List[int]):
+    """regexp_replace on the device (length pass, scan, write pass) → (StrColumn, fallback mask)."""
+    from ..engine.column import StrColumn
+    n, dev = col.length, col.device
+    code, sets = _vm_tensors(prog, dev)
+    rep = torch.tensor(tokens or [0], dtype=torch.int32).to(dev)
+    lens = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    st = N.stream_handle(dev)
+    args = (N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(code), N.ptr(sets))
+    if n:
+        N.call("dxa_str_regex", *args, 1, 0, N.ptr(rep), len(tokens), 0, N.ptr(lens), 0, 0, N.ptr(status), st)
+    off, total = _offsets(lens)
+    out = _alloc_arena(total, dev)
+    if n and total:
+        N.call("dxa_str_regex", *args, 2, 0, N.ptr(rep), len(tokens), 0, 0, N.ptr(off), N.ptr(out), N.ptr(status),
+               st)
+    return StrColumn(out, off, lens, col.valid), status.bool()
+
+
 def _raw_bytes(col) -> List[bytes]:
     arena = col.arena.cpu().numpy().tobytes()
     return [arena[s:s + l] for s, l in zip(col.starts.cpu().tolist(), col.lens.cpu().tolist())]

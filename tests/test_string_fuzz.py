@@ -202,3 +202,32 @@ def test_digest_functions_gpu_match_cpu(gpu):
     sql = ("SELECT md5(s) AS a, sha1(s) AS b, sha2(s, 256) AS c, sha2(s, 224) AS d, sha2(s, 0) AS e, crc32(s) AS f, "
            "hex(s) AS g, base64(s) AS h, sha2(s, 512) AS i FROM F")
     assert _run(sql, vals, gpu) == _run(sql, vals, "cpu")
+
+
+def test_regexp_host_java_semantics():
+    vals = ["key=abc;x=1", "no", "a\r", "baaac", None]
+    out = _run("SELECT regexp_extract(s, 'key=(\\\\w*)', 1) AS a, regexp_replace(s, 'a*', '-') AS b, "
+               "regexp_extract(s, 'a.', 0) AS c, regexp_replace(s, '(a)(a)?', '[$2$1]') AS d FROM F", vals, "cpu")
+    assert out[0] == ["abc", "", "", "", None]
+    assert out[1][3] == "-b--c-"                       # Java's empty-match stepping
+    assert out[2][2] == ""                             # '.' does not take \r (Java)
+    assert out[3][3] == "b[aa][a]c"
+
+
+@pytest.mark.gpu
+def test_regexp_fuzz_gpu_match_cpu(gpu):
+    from dxa.ops import regex_vm, strings as S
+    from dxa.engine.column import strings_from_pylist
+    rnd = random.Random(41)
+    vals = [_rand_str(rnd, 16) for _ in range(N)]
+    col = strings_from_pylist(vals, gpu)
+    for _ in range(60):
+        pat = _rand_regex(rnd)
+        prog = regex_vm.compile_vm(pat)
+        g = rnd.randint(0, min(prog.ngroups, 9))
+        rep = rnd.choice(["", "#", "<$0>", "[$1]" if prog.ngroups >= 1 else "x", "\\$"])
+        sql = (f"SELECT regexp_extract(s, '{_q(pat)}', {g}) AS a, regexp_replace(s, '{_q(pat)}', '{_q(rep)}') AS b "
+               f"FROM F")
+        assert _run(sql, vals, gpu) == _run(sql, vals, "cpu"), (pat, g, rep)
+        _, bad = S.regex_extract(col, prog, g)
+        assert not bool(bad.any()), pat                  # the device path itself produced the answer

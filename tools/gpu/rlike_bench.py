@@ -29,3 +29,21 @@ for pat in ["door (open|closed)", "^home.*alert$", "\\d{2} temp", "[^a-z ]", "(d
     assert m[:200000].cpu().tolist() == ref, pat
     print(f"{pat!r:34} states={dfa.n_states:4} classes={dfa.n_classes:3}  device {dt * 1e3:7.3f} ms "
           f"({len(vals) / dt / 1e9:6.2f} G rows/s)  host re {hdt * 1e3:8.1f} ms  hits={int(m.sum())}")
+
+# regexp_extract / regexp_replace through the backtracking program (regex_vm.py)
+from dxa.ops import regex_vm  # noqa: E402
+
+for pat, g, rep in [("(door|home) (\\w+)", 2, "<$1>"), ("(\\d+) temp", 1, "#"), ("a.*?e", 0, "")]:
+    prog = regex_vm.compile_vm(pat)
+    for what in ("extract", "replace"):
+        fn = (lambda: S.regex_extract(col, prog, g)) if what == "extract" else \
+            (lambda: S.regex_replace(col, prog, regex_vm.replacement_tokens(rep, prog.ngroups)))
+        out, bad = fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(5):
+            out, bad = fn()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / 5
+        print(f"regexp_{what} {pat!r:26} device {dt * 1e3:7.2f} ms ({len(vals) / dt / 1e9:5.2f} G rows/s) "
+              f"fallback rows {int(bad.sum())}")
