@@ -1004,6 +1004,8 @@ struct RxArgs {
   int32_t group;
   const int32_t* rep; int32_t nrep;   // replacement tokens: byte, or -1-k for group k
   int64_t* out_start; int32_t* out_len; const int64_t* out_off; uint8_t* out; uint8_t* status;
+  const uint8_t* hit;                 // optional RLIKE prefilter (the DFA): rows without a match skip the search
+  int32_t nprog, nsets;
 };
 
 __device__ __forceinline__ bool rx_bit(const uint32_t* sets, int k, uint32_t c) {
@@ -1076,15 +1078,27 @@ __device__ int rx_find(const RxArgs& a, const uint8_t* s, int32_t len, int32_t f
   return 0;
 }
 
+constexpr int kRxLdsInts = 4096;      // program + bitmaps staged in LDS when they fit (16 KB)
+
 __global__ void __launch_bounds__(256) str_regex_kernel(RxArgs a) {
+  __shared__ int32_t rx_sh[kRxLdsInts];
+  const int words = a.nprog * 4 + a.nsets * 8;
+  if (words <= kRxLdsInts) {
+    for (int k = threadIdx.x; k < a.nprog * 4; k += blockDim.x) rx_sh[k] = ((const int32_t*)a.prog)[k];
+    for (int k = threadIdx.x; k < a.nsets * 8; k += blockDim.x) rx_sh[a.nprog * 4 + k] = (int32_t)a.sets[k];
+    __syncthreads();
+    a.prog = (const int4*)rx_sh;
+    a.sets = (const uint32_t*)(rx_sh + a.nprog * 4);
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint8_t* s = a.arena + a.starts[i];
     const int32_t len = a.lens[i];
     int32_t cap[kRxCaps];
     int steps = 0;
     uint8_t bad = 0;
+    const bool skip = a.hit != nullptr && !a.hit[i];
     if (a.mode == 0) {
-      const int r = rx_find(a, s, len, 0, cap, steps);
+      const int r = skip ? 0 : rx_find(a, s, len, 0, cap, steps);
       int32_t b = 0, e = 0;
       if (r == 1 && cap[2 * a.group] >= 0 && cap[2 * a.group + 1] >= 0) { b = cap[2 * a.group]; e = cap[2 * a.group + 1]; }
       bad = r < 0;
@@ -1094,7 +1108,7 @@ __global__ void __launch_bounds__(256) str_regex_kernel(RxArgs a) {
       uint8_t* o = a.mode == 2 ? a.out + a.out_off[i] : nullptr;
       int64_t olen = 0;
       int32_t pos = 0, last = 0;
-      while (pos <= len) {
+      while (!skip && pos <= len) {
         const int r = rx_find(a, s, len, pos, cap, steps);
         if (r < 0) { bad = 1; break; }
         if (r == 0) break;
@@ -1123,13 +1137,13 @@ __global__ void __launch_bounds__(256) str_regex_kernel(RxArgs a) {
 }
 
 DXA_API int dxa_str_regex(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
-                          const int32_t* prog, const int32_t* sets, int32_t mode, int32_t group, const int32_t* rep,
-                          int32_t nrep, int64_t* out_start, int32_t* out_len, const int64_t* out_off, uint8_t* out,
-                          uint8_t* status, void* st) {
+                          const int32_t* prog, int32_t nprog, const int32_t* sets, int32_t nsets, int32_t mode,
+                          int32_t group, const int32_t* rep, int32_t nrep, int64_t* out_start, int32_t* out_len,
+                          const int64_t* out_off, uint8_t* out, uint8_t* status, const uint8_t* hit, void* st) {
   if (n <= 0) return 0;
   if (mode < 0 || mode > 2 || group < 0 || group > 9) return (int)hipErrorInvalidValue;
   RxArgs a{arena, starts, lens, n, (const int4*)prog, (const uint32_t*)sets, mode, group, rep, nrep,
-           out_start, out_len, out_off, out, status};
+           out_start, out_len, out_off, out, status, hit, nprog, nsets};
   hipLaunchKernelGGL(str_regex_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, a);
   return (int)hipGetLastError();
 }

@@ -64,7 +64,8 @@ _SIGS = {
     "dxa_ts_format": [c_p, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p],
     "dxa_str_like": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_p, c_p],
     "dxa_str_rlike": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_i32, c_p, c_p],
-    "dxa_str_regex": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_p],
+    "dxa_str_regex": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p,
+                      c_p, c_p],
     "dxa_gzip_chunks": [c_p, c_i64, c_i32, c_p, c_p, c_i32, c_p],
     "dxa_gzip_pack": [c_p, c_i32, c_p, c_p, c_i64, c_p, c_p],
     "dxa_str_digest": [c_p, c_p, c_p, c_i64, c_i32, c_p, c_p],

@@ -34,6 +34,7 @@ class Program:
     sets: List[int] = field(default_factory=list)       # 8 uint32 words per bitmap
     ngroups: int = 0
     loops: int = 0
+    pattern: str = ""
 
     def emit(self, op, a=0, b=0, c=0) -> int:
         if len(self.code) // 4 >= MAX_PROG:
@@ -159,7 +160,7 @@ def compile_vm(pattern: str) -> Program:
         return hit
     parser = _Parser(pattern)
     ast = parser.parse()
-    prog = Program(ngroups=parser.groups)
+    prog = Program(ngroups=parser.groups, pattern=pattern)
     prog.emit(SAVE, 0)
     _gen(prog, ast)
     prog.emit(SAVE, 1)

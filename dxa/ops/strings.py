@@ -246,6 +246,19 @@ def encode(col, mode: int):
     return StrColumn(out, off, out_lens.to(torch.int32), col.valid)
 
 
+def _prefilter(col, prog):
+    """RLIKE mask from the pattern's DFA (rows that cannot match skip the backtracking search), or None."""
+    from . import regex_dfa
+    pat = getattr(prog, "pattern", None)
+    if pat is None:
+        return None
+    try:
+        dfa = regex_dfa.compile_rlike(pat)
+    except regex_dfa.Unsupported:
+        return None
+    return rlike(col, dfa)
+
+
 def _vm_tensors(prog, device):
     cache = prog.__dict__.setdefault("_dev", {})
     t = cache.get(device)
@@ -265,8 +278,10 @@ def regex_extract(col, prog, group: int):
     lens = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     if n:
-        N.call("dxa_str_regex", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(code), N.ptr(sets),
-               0, group, 0, 0, N.ptr(starts), N.ptr(lens), 0, 0, N.ptr(status), N.stream_handle(dev))
+        hit = _prefilter(col, prog)
+        N.call("dxa_str_regex", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(code),
+               code.numel() // 4, N.ptr(sets), sets.numel() // 8, 0, group, 0, 0, N.ptr(starts), N.ptr(lens), 0, 0,
+               N.ptr(status), N.ptr(hit), N.stream_handle(dev))
     return StrColumn(col.arena, starts, lens, col.valid), status.bool()
 
 
@@ -279,14 +294,17 @@ def regex_replace(col, prog, tokens: List[int]):
     lens = torch.zeros(n, dtype=torch.int32, device=dev)
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     st = N.stream_handle(dev)
-    args = (N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(code), N.ptr(sets))
+    args = (N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(code), code.numel() // 4, N.ptr(sets),
+            sets.numel() // 8)
+    hit = _prefilter(col, prog) if n else None
     if n:
-        N.call("dxa_str_regex", *args, 1, 0, N.ptr(rep), len(tokens), 0, N.ptr(lens), 0, 0, N.ptr(status), st)
+        N.call("dxa_str_regex", *args, 1, 0, N.ptr(rep), len(tokens), 0, N.ptr(lens), 0, 0, N.ptr(status),
+               N.ptr(hit), st)
     off, total = _offsets(lens)
     out = _alloc_arena(total, dev)
     if n and total:
         N.call("dxa_str_regex", *args, 2, 0, N.ptr(rep), len(tokens), 0, 0, N.ptr(off), N.ptr(out), N.ptr(status),
-               st)
+               N.ptr(hit), st)
     return StrColumn(out, off, lens, col.valid), status.bool()
 
 
