@@ -47,3 +47,27 @@ for pat, g, rep in [("(door|home) (\\w+)", 2, "<$1>"), ("(\\d+) temp", 1, "#"), 
         dt = (time.perf_counter() - t) / 5
         print(f"regexp_{what} {pat!r:26} device {dt * 1e3:7.2f} ms ({len(vals) / dt / 1e9:5.2f} G rows/s) "
               f"fallback rows {int(bad.sum())}")
+
+# md5 / sha1 / sha256 / sha224 / crc32 (one lane per row), checked against hashlib / zlib on a sample
+import hashlib  # noqa: E402
+import zlib  # noqa: E402
+
+
+for kind, name in [(0, "md5"), (1, "sha1"), (2, "sha256"), (3, "sha224"), (4, "crc32")]:
+    fn = (lambda: S.crc32(col)) if kind == 4 else (lambda: S.digest(col, kind))
+    out = fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(10):
+        out = fn()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / 10
+    sample = vals[:2000]
+    if kind == 4:
+        assert out[:2000].cpu().tolist() == [zlib.crc32(v.encode()) for v in sample], name
+    else:
+        h = getattr(hashlib, name)
+        got = out.to_pylist()[:2000]
+        assert got == [h(v.encode()).hexdigest() for v in sample], name
+    print(f"{name:8} device {dt * 1e3:7.3f} ms ({len(vals) / dt / 1e9:5.2f} G rows/s, "
+          f"{int(col.lens.sum()) / dt / 1e9:6.1f} GB/s of input)")
