@@ -355,6 +355,8 @@ class Processor:
             t_done = max(t_done, t_end)
             for k, v in res.items():
                 metrics[f"Output_{name}_{k}"] = float(v)
+        for st in self.state_tables.values():
+            st.flush()                 # this rank's standby part is durable before the all-reduce (= the barrier)
         if P.active():
             # batch metrics are job-wide: one all-reduce of the count vector (timings stay per-rank)
             keys = sorted(metrics)

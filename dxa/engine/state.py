@@ -5,21 +5,30 @@ Reference: DataProcessing/datax-host/src/main/scala/datax/handler/StateTableHand
 the standby copy and flips; the flip is persisted after the batch's outputs (CommonProcessorFactory.scala:318-320).
 
 Here the active copy is a device-resident columnar table (queried straight from HBM every batch); the standby copy
-is written to ``<location>/<A|B>/part-0.parquet`` (pyarrow) and ``metadata.info`` is rewritten atomically after
+is written to ``<location>/<A|B>/part-<rank>.parquet`` (pyarrow) and ``metadata.info`` is rewritten atomically after
 outputs, so a restarted engine resumes from the last committed accumulator state.
+
+Multi-GPU (SURVEY §2.G X10 — Spark writes the state table as one Parquet part per partition): every rank keeps and
+persists ITS share of the table, as the query produced it — a ``GROUP BY`` result lives on the key's owner rank
+(``hashed``), a global aggregate is identical everywhere (``replicated``).  The distribution tag survives the
+overwrite, so the next batch's ``UNION ALL <state> … GROUP BY`` treats the state rows as rank-local rows again rather
+than as a replicated copy (which ``_set_op`` would keep on rank 0 only).  ``metadata.info`` is flipped once per batch
+by rank 0, after every rank's part is durable (the batch-metrics all-reduce in ``Processor._complete_inflight`` is
+the barrier), and records ``parts`` (the world size that wrote the copy) and ``dist``.  On restart with the same
+world size each rank reads its own part; with a different one, rank r reads parts ``p ≡ r (mod W)`` and the table
+is tagged ``partitioned`` (the next GROUP BY re-shuffles it by key hash).
 """
 from __future__ import annotations
 
-from typing import Dict, Optional
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List
 
 import torch
 
+from .. import parallel as P
 from ..io import fs
-from .column import Table
+from .column import Table, concat_tables
 from .types import StructType, parse_ddl_schema
-
-
-from concurrent.futures import ThreadPoolExecutor
 
 _writer = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dxa-state")
 
@@ -31,70 +40,119 @@ class StateTable:
         self.location = location.rstrip("/") + "/"
         self.device = torch.device(device)
         self.meta_file = self.location + "metadata.info"
+        self.rank, self.world = P.rank(), P.world()
         self.params = self._read_meta()
         self.modified = False
+        self._pending = None
         self.active: Table = self._load(self.params["active"])
 
+    # ---- metadata ------------------------------------------------------------------------------------------------
     def _read_meta(self) -> Dict[str, str]:
         if fs.exists(self.meta_file):
             out = {}
             for line in fs.read_lines(self.meta_file):
+                if not line.strip():
+                    continue
                 pos = line.find("=")
                 if pos <= 0:
                     raise ValueError(f"Invalid content in '{self.meta_file}': '{line}'")
                 out[line[:pos]] = line[pos + 1:]
+            if "active" not in out or "standby" not in out:
+                raise ValueError(f"'{self.meta_file}' names no active/standby copy")
             return out
         return {"active": "A", "standby": "B"}
 
-    def _path(self, suffix: str) -> str:
-        return self.location + suffix + "/part-0.parquet"
+    @property
+    def dist(self) -> str:
+        """Distribution of the active copy across ranks (``replicated`` on a single rank)."""
+        return P.dist_of(self.active) if P.active() else P.REPLICATED
 
-    def _load(self, suffix: str) -> Table:
-        p = self._path(suffix)
+    def _path(self, suffix: str, part: int) -> str:
+        return f"{self.location}{suffix}/part-{part}.parquet"
+
+    # ---- load ----------------------------------------------------------------------------------------------------
+    def _read_part(self, suffix: str, part: int):
+        p = self._path(suffix, part)
         if not fs.exists(p):
-            return Table.empty(self.schema, self.device)
+            return None
         import pyarrow.parquet as pq
         from ..io.arrow import table_from_arrow
         return table_from_arrow(pq.read_table(str(fs.local_path(p))), self.schema, self.device)
 
+    def _load(self, suffix: str) -> Table:
+        parts_written = int(self.params.get("parts", "1"))
+        dist = self.params.get("dist", P.REPLICATED if parts_written == 1 else P.PARTITIONED)
+        if not P.active():
+            # one rank owns everything: a replicated copy is any one part, a partitioned one is all parts
+            mine = [0] if dist == P.REPLICATED else list(range(parts_written))
+            tag = P.REPLICATED
+        elif dist == P.REPLICATED:
+            mine, tag = [0], P.REPLICATED
+        else:
+            mine = [p for p in range(parts_written) if p % self.world == self.rank]
+            # same world: the rows are exactly the ones this rank produced (HASHED stays valid but nothing downstream
+            # distinguishes it from PARTITIONED); a different world: any key may now sit on any rank
+            tag = P.PARTITIONED
+        tables: List[Table] = [t for t in (self._read_part(suffix, p) for p in mine) if t is not None]
+        t = concat_tables(tables) if tables else Table.empty(self.schema, self.device)
+        if len(tables) > 1:
+            t = Table(t.names, t.columns, t.length, t.device)
+        t.dist = tag if P.active() else P.REPLICATED
+        if P.active() and not tables and dist != P.REPLICATED:
+            t.dist = P.PARTITIONED       # an empty share of a partitioned table
+        return t
+
+    # ---- update --------------------------------------------------------------------------------------------------
     def overwrite(self, t: Table):
-        """INSERT OVERWRITE standby + flip (returns the new active table).  The standby Parquet copy is written by
+        """INSERT OVERWRITE standby + flip (returns the new active table).  The standby Parquet part is written by
         a background writer from pinned host buffers; ``persist`` (after the batch's outputs) waits for it before
         it flips ``metadata.info``, so the metadata never names a partially written copy."""
         from ..io.arrow import to_host_async
+        dist = P.dist_of(t)
         t = _conform(t, self.schema)
+        t.dist = dist if P.active() else P.REPLICATED
         self._wait_write()
-        host, ev = to_host_async(t)
-        self._pending = _writer.submit(self._write, self.params["standby"], host, ev)
-        self.params = {"active": self.params["standby"], "standby": self.params["active"]}
-        self.modified = not self.modified
+        if P.active() and dist == P.REPLICATED and self.rank != 0:
+            self._pending = None          # replicated result: rank 0's part-0 is the copy
+        else:
+            host, ev = to_host_async(t)
+            self._pending = _writer.submit(self._write, self.params["standby"], self.rank, host, ev)
+        self.params = {"active": self.params["standby"], "standby": self.params["active"],
+                       "parts": str(self.world), "dist": t.dist}
+        self.modified = True
         self.active = t
         return t
 
     def _wait_write(self):
-        p = getattr(self, "_pending", None)
+        p = self._pending
         if p is not None:
             self._pending = None
             p.result()
 
-    def _write(self, suffix: str, t: Table, event=None):
+    def _write(self, suffix: str, part: int, t: Table, event=None):
         import pyarrow.parquet as pq
         from ..io.arrow import table_to_arrow
         if event is not None:
             event.synchronize()
-        p = fs.local_path(self._path(suffix))
+        p = fs.local_path(self._path(suffix, part))
         p.parent.mkdir(parents=True, exist_ok=True)
-        tmp = p.with_suffix(".tmp")
+        tmp = p.with_name(p.name + ".tmp")
         # uncompressed, no dictionary pages or statistics: the standby copy is rewritten every batch and read back
         # only on restart (2 ms instead of 6.7 ms for a 10 K-row state table; still a Parquet file Spark can read)
         pq.write_table(table_to_arrow(t, self.schema), str(tmp), compression="none", use_dictionary=False,
                        write_statistics=False)
         tmp.replace(p)
 
+    def flush(self):
+        """Make this rank's standby part durable (call on every rank before the barrier that precedes ``persist``)."""
+        self._wait_write()
+
     def persist(self):
+        """Flip ``metadata.info`` (rank 0 only; every rank's part must already be durable — see ``flush``)."""
         self._wait_write()
         if self.modified:
-            fs.write_atomic(self.meta_file, "\n".join(f"{k}={v}" for k, v in self.params.items()))
+            if self.rank == 0:
+                fs.write_atomic(self.meta_file, "\n".join(f"{k}={v}" for k, v in self.params.items()))
             self.modified = False
 
 

@@ -182,8 +182,10 @@ def test_two_rank_queries_match_single_process(device):
         assert n_r == 200 and _canon(everything) == _canon(rows)
 
 
-@pytest.mark.parametrize("flow,device", [("groupby", "cpu"), ("window", "cpu"),
-                                         pytest.param("groupby", "cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("flow,device", [("groupby", "cpu"), ("window", "cpu"), ("full", "cpu"), ("join", "cpu"),
+                                         pytest.param("groupby", "cuda", marks=pytest.mark.gpu),
+                                         pytest.param("full", "cuda", marks=pytest.mark.gpu),
+                                         pytest.param("join", "cuda", marks=pytest.mark.gpu)])
 def test_bench_two_ranks_gloo(flow, device, tmp_path):
     """bench.py's multi-rank path (the driver's N-GPU scaling run) rehearsed on CPU: two ranks, gloo, one JSON line
     whose value aggregates both ranks — catches collective mismatches before they reach RCCL."""
@@ -200,7 +202,7 @@ def test_bench_two_ranks_gloo(flow, device, tmp_path):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                         os.path.join(root, "bench.py"), "--gpus", "2", "--flow", flow, "--events-per-batch", "500",
-                        "--steps", "2", "--warmup", "3"], capture_output=True, text=True, env=env, timeout=600,
+                        "--steps", "2", "--warmup", "3", "--ref-rows", "5000"], capture_output=True, text=True, env=env, timeout=600,
                        cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
