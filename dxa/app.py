@@ -48,21 +48,23 @@ def main(argv=None):
     from .engine.processor import Processor
     from .io.sources import build_source
     from .telemetry.metrics import MetricStore
+    from .telemetry import appinsights
+    appinsights.configure(d)
     proc = Processor(d, device, metric_store=MetricStore.default())
     app = (args.get("app") or "").lower() or None
     if app == "batch":
         from .config.secrets import resolve
         from .service.scheduler import _parse_time
         blobs = list(d.group_by_sub_namespace(S.INPUT_PREFIX + "blob.").values())
-        first = blobs[0] if blobs else None
-
-        def pick(key, conf_key, default=None):
-            return args.get(key) or (first.get(conf_key) if first is not None else None) or default
-        start = _parse_time(pick("processStartTime", "processstarttime"))
-        end = _parse_time(pick("processEndTime", "processendtime"))
-        inc = _dt.timedelta(minutes=float(pick("partitionIncrement", "partitionincrement", 60)))
-        paths = [resolve(sub.get_string("path")) for sub in blobs]
-        res = BlobBatchingHost(proc, device, paths, start, end, inc).run()
+        # per input blob: its own path template, time range and partition increment (BatchBlobInputSetting.scala:
+        # 18-48); ``processStartTime=`` / ``processEndTime=`` / ``partitionIncrement=`` arguments override all
+        specs = []
+        for sub in blobs:
+            s0 = _parse_time(args.get("processStartTime") or sub.get("processstarttime"))
+            s1 = _parse_time(args.get("processEndTime") or sub.get("processendtime"))
+            step = _dt.timedelta(minutes=float(args.get("partitionIncrement") or sub.get("partitionincrement") or 60))
+            specs.append((resolve(sub.get_string("path")), s0, s1, step))
+        res = BlobBatchingHost(proc, device, [], blobs=specs).run()
         print(json.dumps({"batches": len(res)}), flush=True)
         return 0
     src = build_source(d, device, app)

@@ -18,7 +18,7 @@ import signal
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List, Optional, Tuple
 
 from ..io import fs
 from .processor import Processor, RawBatch
@@ -55,6 +55,8 @@ class StreamingHost:
         prefetched = None
         prev_cb = self.processor.on_batch_complete
         self.processor.on_batch_complete = self._completed
+        from ..telemetry.appinsights import track_event, track_exception
+        kind = "localstreaming" if getattr(self.source, "name", "") == "local" else "streaming"
         try:
             while not self._stop.is_set():
                 if self.max_batches is not None and self.batches >= self.max_batches:
@@ -73,12 +75,18 @@ class StreamingHost:
                     prefetched = pool.submit(self.source.next_batch, nbt)
                 if raw is None:
                     break
+                bt_str = _fmt_batch_time(bt)
+                track_event(f"{kind}/batch/begin", {"batchTime": bt_str})
                 try:
                     self.processor.process_batch(raw, bt, self.interval_us, _dt.datetime.utcfromtimestamp(bt / 1e6))
-                except Exception:
+                except Exception as e:
+                    # EventHubStreamingFactory.scala:100-106: the exception with the batch's per-partition start
+                    # sequence numbers as measurements, then fail the job
+                    track_exception("StreamingHost", bt_str, e, {"batchTime": bt_str}, self._offset_measures(bt))
                     log.exception("batch failed; stopping the job (restart resumes from the last checkpoint)")
                     time.sleep(1.0)
                     raise
+                track_event(f"{kind}/batch/end", {"batchTime": bt_str})
                 self.batches += 1
                 next_time = bt + self.interval_us
                 if prefetched is not None and prefetched.done() and prefetched.exception() is None:
@@ -94,12 +102,30 @@ class StreamingHost:
             self.source.close()
         return self.history
 
+    def _offset_measures(self, bt: int) -> Dict[str, float]:
+        ranges = getattr(self.source, "_inflight", {}).get(bt, {}) if hasattr(self.source, "_inflight") else {}
+        hub_of = getattr(self.source, "_hub_of", lambda k: (str(k), ""))
+        out = {}
+        for k, (s, _e) in ranges.items():
+            name, part = hub_of(k)
+            out[f"{name}-{part}-fromSeqNo"] = float(s)
+        return out
+
     def _completed(self, bt: int, metrics: Dict[str, float]):
-        """A batch's outputs are written: only now are its source offsets committed (at-least-once)."""
+        """A batch's outputs are written: only now are its source offsets committed (at-least-once) — after the
+        source confirms the batch decoded cleanly (device-side decoders report errors asynchronously)."""
+        verify = getattr(self.source, "verify", None)
+        if verify is not None:
+            verify(bt)
         self.source.commit(bt)
         self.history.append(metrics)
         if self.on_batch:
             self.on_batch(bt, metrics)
+
+
+def _fmt_batch_time(bt_us: int) -> str:
+    """Spark ``Time.toString``: ``<ms> ms``."""
+    return f"{bt_us // 1000} ms"
 
 
 _TOKEN = re.compile(r"\{([^}]+)\}")
@@ -115,6 +141,16 @@ def _java_fmt_to_strftime(fmt: str) -> str:
 def expand_path_template(template: str, start: _dt.datetime, end: _dt.datetime,
                          increment: _dt.timedelta) -> List[str]:
     """``wasbs://c@a/{yyyy-MM-dd}/{HH}/*.json`` → one path per time partition in [start, end]."""
+    return [p for p, _t in expand_path_prefixes(template, start, end, increment)]
+
+
+def expand_path_prefixes(template: str, start: _dt.datetime, end: _dt.datetime,
+                         increment: _dt.timedelta) -> List[Tuple[str, _dt.datetime]]:
+    """(path, partition time) per distinct time partition of ``template`` in [start, end], stepping by
+    ``increment`` (BlobBatchingHost.getInputBlobPathPrefixes, BlobBatchingHost.scala:28-53).  A template without a
+    ``{…}`` date pattern is one path stamped now, as the reference."""
+    if not _TOKEN.search(template):
+        return [(template, _dt.datetime.utcnow())]
     out = []
     t = start
     seen = set()
@@ -122,36 +158,58 @@ def expand_path_template(template: str, start: _dt.datetime, end: _dt.datetime,
         p = _TOKEN.sub(lambda m: t.strftime(_java_fmt_to_strftime(m.group(1))), template)
         if p not in seen:
             seen.add(p)
-            out.append(p)
+            out.append((p, t))
         t += increment
     return out
 
 
 class BlobBatchingHost:
-    """Batch mode: process the files of every time partition in a window as one batch per partition."""
+    """Batch mode (BatchApp → BlobBatchingHost.runBatchApp, BlobBatchingHost.scala:68-105): expand every input
+    blob's path template over its time range, list the files under every partition prefix (``fs.list_matching`` —
+    local folders, globs and ``wasbs://`` containers alike), and process ALL of them as ONE batch stamped with the
+    earliest partition time and a 1-hour interval.
 
-    def __init__(self, processor: Processor, device, path_templates: List[str], start: _dt.datetime,
-                 end: _dt.datetime, increment: _dt.timedelta):
+    With W ranks each file is read by exactly one rank (``fs.owned_by_rank``), as Spark spreads ``makeRDD(files)``
+    over executors; the batch's metrics are all-reduced by the processor, so ``InputBlobs`` counts every file once.
+    ``blobs``: (path template, start, end, partition increment) per configured input blob."""
+
+    def __init__(self, processor: Processor, device, path_templates: List[str], start: _dt.datetime = None,
+                 end: _dt.datetime = None, increment: _dt.timedelta = None,
+                 blobs: Optional[List[Tuple[str, _dt.datetime, _dt.datetime, _dt.timedelta]]] = None):
         self.processor = processor
         self.device = device
-        self.paths = [p for tpl in path_templates for p in expand_path_template(tpl, start, end, increment)]
-        self.start = start
+        specs = list(blobs or []) + [(tpl, start, end, increment) for tpl in path_templates]
+        self.prefixes = [pt for tpl, s, e, inc in specs for pt in expand_path_prefixes(tpl, s, e, inc)]
+        self.paths = [p for p, _t in self.prefixes]
+
+    def list_files(self) -> List[str]:
+        seen, out = set(), []
+        for p, _t in self.prefixes:
+            for f in fs.list_matching(p):
+                if f not in seen:
+                    seen.add(f)
+                    out.append(f)
+        return out
 
     def run(self) -> List[Dict[str, float]]:
-        import glob
+        from .. import parallel as P
         from ..io.sources import frame_bytes
-        results = []
-        for p in self.paths:
-            t0 = time.perf_counter()
-            files = sorted(glob.glob(str(fs.local_path(p)), recursive=True))
-            data = bytearray()
-            for f in files:
-                b = fs.read_bytes(f)
+        from ..telemetry.appinsights import track_event
+        track_event("batch/app/begin")
+        t0 = time.perf_counter()
+        files = self.list_files()
+        mine = fs.owned_by_rank(files, P.rank(), P.world())
+        data = bytearray()
+        for f in mine:
+            b = fs.read_bytes(f)
+            if b:
                 data += b if b.endswith(b"\n") else b + b"\n"
-            raw = frame_bytes(bytes(data), self.device, file_info={"inputPath": p})
-            bt = int(self.start.replace(tzinfo=_dt.timezone.utc).timestamp() * 1e6)
-            m = self.processor.process_batch(raw, bt, 3600 * 1_000_000)
-            m["InputBlobs"] = float(len(files))
-            m["BatchProcessedET"] = time.perf_counter() - t0      # CommonProcessorFactory.scala:509-513
-            results.append(m)
-        return results
+        raw = frame_bytes(bytes(data), self.device, file_info={"inputPath": ";".join(mine)} if mine else None)
+        t_min = min((t for _p, t in self.prefixes), default=_dt.datetime.utcnow())
+        bt = int(t_min.replace(tzinfo=_dt.timezone.utc).timestamp() * 1e6)
+        m = self.processor.process_batch(raw, bt, 3600 * 1_000_000)
+        m = self.processor.drain() or m
+        m["InputBlobs"] = float(len(files))
+        m["BatchProcessedET"] = time.perf_counter() - t0      # CommonProcessorFactory.scala:509-513
+        track_event("batch/end", properties=None, measurements=m)
+        return [m]

@@ -56,6 +56,8 @@ class RawBatch:
     ends: Optional[torch.Tensor] = None       # int64 [n] record ends when records are not back to back (Kafka
                                               # values in decompressed record batches); offs[n] = end of the bytes
     pending: Optional[Any] = None             # jsonparse.PendingParse started by Processor.prepare
+    status: Optional[Any] = None              # source-side decode status (kafka_device.DecodeStatus), checked by
+                                              # the source before the batch's offsets are committed
 
 
 def _read_lines(path: str) -> List[str]:
@@ -428,7 +430,7 @@ class Processor:
             except Exception:  # noqa: BLE001
                 self._inflight = None
             from ..telemetry.appinsights import track_exception
-            track_exception("ProcessDataFrame", batch_time_us)
+            track_exception("ProcessDataFrame", _fmt_ts(batch_time_us))
             raise
 
 

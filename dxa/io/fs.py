@@ -139,6 +139,63 @@ def list_files(path: str, recursive: bool = False) -> List[str]:
     return sorted(str(x) for x in it if x.is_file())
 
 
+_GLOB = re.compile(r"[*?\[]")
+
+
+def list_matching(path: str) -> List[str]:
+    """Files under ``path`` (HadoopClient.listFiles: a folder is listed recursively, HadoopClient.scala:470-479), or
+    matching it when it holds glob characters (``*``, ``?``, ``[…]``; ``**`` crosses folders) — local and remote
+    (``wasbs://``) alike, through ``list_files``."""
+    m = _GLOB.search(path)
+    if m is None:
+        r = _remote(path)
+        if r is None and local_path(path).is_file():
+            return [str(local_path(path))]
+        return list_files(path, recursive=True)
+    base = path[: path.rfind("/", 0, m.start()) + 1]
+    names = list_files(base, recursive=True) if base else []
+    rx = glob_regex(str(local_path(path)) if _remote(path) is None else path)
+    return sorted(n for n in names if rx.fullmatch(n))
+
+
+def glob_regex(pattern: str):
+    """``*`` / ``?`` stay inside one folder, ``**`` (and ``**/``) crosses folders, ``[…]`` is a character class."""
+    out, i = [], 0
+    while i < len(pattern):
+        ch = pattern[i]
+        if pattern.startswith("**/", i):
+            out.append("(?:.*/)?")
+            i += 3
+        elif pattern.startswith("**", i):
+            out.append(".*")
+            i += 2
+        elif ch == "*":
+            out.append("[^/]*")
+            i += 1
+        elif ch == "?":
+            out.append("[^/]")
+            i += 1
+        elif ch == "[" and "]" in pattern[i + 1:]:
+            j = pattern.index("]", i + 1)
+            body = pattern[i + 1:j]
+            out.append("[" + ("^" + body[1:] if body.startswith("!") else body) + "]")
+            i = j + 1
+        else:
+            out.append(re.escape(ch))
+            i += 1
+    return re.compile("".join(out))
+
+
+def owned_by_rank(items: List[str], rank: int, world: int) -> List[str]:
+    """The share of ``items`` (file paths, partition names) one rank reads: a stable hash of the name modulo the
+    world size, so every rank agrees without communicating and a file is read by exactly one rank (SURVEY §2.G X11:
+    source partition → rank)."""
+    if world <= 1:
+        return list(items)
+    import zlib
+    return [x for x in items if zlib.crc32(x.encode("utf-8")) % world == rank]
+
+
 def delete(path: str):
     r = _remote(path)
     if r is not None:

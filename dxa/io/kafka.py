@@ -427,8 +427,11 @@ class KafkaSource(OffsetTrackedSource):
 
     def __init__(self, client: KafkaClient, topics: List[str], device, checkpoint_dir: Optional[str] = None,
                  max_rate: Optional[int] = None, start: int = EARLIEST, flush_existing: bool = False,
-                 rank: int = 0, world: int = 1, max_fetches: int = 64, device_decode: Optional[bool] = None):
+                 rank: int = 0, world: int = 1, max_fetches: int = 64, device_decode: Optional[bool] = None,
+                 verify_crc: bool = True):
         self.client = client
+        self.verify_crc = verify_crc          # consumer check.crcs (default true)
+        self._status: Dict[int, object] = {}
         self.topics = topics
         self.device = torch.device(device)
         self.max_rate = max_rate
@@ -436,7 +439,7 @@ class KafkaSource(OffsetTrackedSource):
         # record batches decompressed and framed on the GPU (dxa.io.kafka_device); host decoding otherwise
         self.device_decode = (self.device.type == "cuda") if device_decode is None else device_decode
         self._decoder = None
-        ckpt = Checkpointer(checkpoint_dir) if checkpoint_dir else None
+        ckpt = Checkpointer(checkpoint_dir, rank, world) if checkpoint_dir else None
         meta = client.metadata(topics)
         all_parts = [(t, p) for t in topics for p in meta.get(t, [])]
         self.parts = [tp for i, tp in enumerate(all_parts) if i % world == rank]
@@ -469,7 +472,7 @@ class KafkaSource(OffsetTrackedSource):
                 if not recs:
                     break
                 try:
-                    plan = KD.plan_fetch(recs, cur)
+                    plan = KD.plan_fetch(recs, cur, self.verify_crc)
                 except KD.Unsupported:
                     return None
                 if self.max_rate is not None:
@@ -489,16 +492,40 @@ class KafkaSource(OffsetTrackedSource):
         for recs, (_, at) in zip(sets, plans):
             sn[at:at + len(recs)] = np.frombuffer(recs, dtype=np.uint8)
         if self._decoder is None:
-            self._decoder = KD.DeviceRecordDecoder(self.device)
+            self._decoder = KD.DeviceRecordDecoder(self.device, track=False)
         raw, done = self._decoder.decode(staging, KD.merge(plans))
-        torch.cuda.current_stream(self.device).wait_event(done)
+        cur_stream = torch.cuda.current_stream(self.device)
+        cur_stream.wait_event(done)
+        # the batch's tensors were allocated on the decode stream but are read on the consumer's stream (parse,
+        # string views, outputs): without record_stream the caching allocator could hand their memory to the next
+        # decode while this batch's kernels still read it
+        for t in (raw.buf, raw.offs, raw.ends):
+            if t is not None:
+                t.record_stream(cur_stream)
         self._record_batch(batch_time_us, ranges)
+        with self._lock:
+            self._status[batch_time_us] = raw.status
         return raw
 
+    def verify(self, batch_time_us: int):
+        """Raise ``DecodeError`` if batch ``batch_time_us`` failed to decode on the device.  The streaming host calls
+        this before ``commit`` — a corrupt batch fails the job without committing its offsets (the host decoder
+        raises ``KafkaError`` for the same data); the status was copied to pinned memory behind the decode, so this
+        reads one word."""
+        with self._lock:
+            st = self._status.pop(batch_time_us, None)
+        if st is not None and st.failed():
+            from .kafka_device import DecodeError
+            raise DecodeError(f"Kafka batch {batch_time_us}: record batches failed to decode on the device")
+
     def check(self):
-        """Deferred device-decode status check (one host read for all batches decoded since the last call)."""
-        if self._decoder is not None:
-            self._decoder.check()
+        """Check every decoded batch not yet verified (tests, shutdown)."""
+        with self._lock:
+            pending, self._status = self._status, {}
+        bad = [bt for bt, st in pending.items() if st is not None and st.failed()]
+        if bad:
+            from .kafka_device import DecodeError
+            raise DecodeError(f"Kafka batches {bad}: record batches failed to decode on the device")
 
     def _next_batch_host(self, batch_time_us: int) -> Optional[RawBatch]:
         vals_list, offs_list = [], []
@@ -510,7 +537,7 @@ class KafkaSource(OffsetTrackedSource):
                 recs, hw = self.client.fetch(tp[0], tp[1], cur)
                 if not recs:
                     break
-                vals, offs, recoffs, nxt = decode_records(recs, cur, pad=0)
+                vals, offs, recoffs, nxt = decode_records(recs, cur, pad=0, verify_crc=self.verify_crc)
                 n = len(recoffs)
                 if self.max_rate is not None and got + n > self.max_rate:
                     n = self.max_rate - got
@@ -571,5 +598,6 @@ def build_kafka_source(inp, device, kind: str, rank: int = 0, world: int = 1) ->
         ckpt = inp.get("kafka.checkpointdir")
         rate = inp.get("kafka.maxrate")
         flush = (inp.get("kafka.flushexistingcheckpoints") or "false").lower() == "true"
+    crcs = (inp.get(f"{kind}.checkcrcs") or "true").lower() != "false"
     return KafkaSource(client, topics, device, ckpt, int(rate) if rate else None,
-                       flush_existing=flush, rank=rank, world=world)
+                       flush_existing=flush, rank=rank, world=world, verify_crc=crcs)

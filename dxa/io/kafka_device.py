@@ -86,7 +86,7 @@ class FetchPlan:
         return self.b_base + self.b_skip + self.b_keep - 1
 
 
-def plan_fetch(data, min_offset: int, verify_crc: bool = False) -> FetchPlan:
+def plan_fetch(data, min_offset: int, verify_crc: bool = True) -> FetchPlan:
     """Plan one Fetch record set (bytes / uint8 ndarray) → FetchPlan (offsets relative to ``data``)."""
     a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     L = _lib()
@@ -169,9 +169,11 @@ class PlanBufferPool:
 
 
 def plan_many(data: np.ndarray, bounds: Sequence[Tuple[int, int]], min_offsets: Sequence[int],
-              threads: int = 16, buffer: Optional[PlanBuffer] = None) -> FetchPlan:
+              threads: int = 16, buffer: Optional[PlanBuffer] = None, verify_crc: bool = True) -> FetchPlan:
     """Plan many record sets of one staging buffer (``data[lo:hi]`` each, one per partition fetch) with the sets
-    walked in parallel native threads; the merged arrays land in ``buffer`` (pinned) for one H2D copy."""
+    walked in parallel native threads; the merged arrays land in ``buffer`` (pinned) for one H2D copy.
+    ``verify_crc`` checks every record batch's CRC-32C on the host (the consumer's ``check.crcs``, default true;
+    SSE4.2 ``crc32`` in host_kafka.cpp)."""
     L = _lib()
     if not hasattr(L, "_plan_many_bound"):
         p, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
@@ -184,7 +186,8 @@ def plan_many(data: np.ndarray, bounds: Sequence[Tuple[int, int]], min_offsets: 
     mo = np.array(list(min_offsets), np.int64)
     counts = np.zeros((ns, 4), np.int64)
     nxt = np.zeros(ns, np.int64)
-    rc = L.dxa_kafka_plan_count(data.ctypes.data, ns, so.ctypes.data, sl.ctypes.data, mo.ctypes.data, 0, threads,
+    rc = L.dxa_kafka_plan_count(data.ctypes.data, ns, so.ctypes.data, sl.ctypes.data, mo.ctypes.data,
+                                int(verify_crc), threads,
                                 counts.ctypes.data, nxt.ctypes.data)
     if rc:
         raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
@@ -264,12 +267,15 @@ class DeviceRecordDecoder:
     ``chunks`` splits the H2D copy of the compressed bytes at block boundaries so chunk k's copy overlaps chunk
     k-1's decode (as ``lz4.ChunkedIngest``)."""
 
-    def __init__(self, device, chunks: int = 4, copy_stream=None, decode_stream=None):
+    def __init__(self, device, chunks: int = 4, copy_stream=None, decode_stream=None, track: bool = True):
         self.device = torch.device(device)
         self.chunks = max(1, chunks)
         self.copy_stream = copy_stream or torch.cuda.Stream(self.device)
         self.decode_stream = decode_stream or torch.cuda.Stream(self.device)
-        self.checks: List[torch.Tensor] = []      # per-batch status tensors, checked with check()
+        # per-batch DecodeStatus objects, drained by check(); ``track=False``: the caller checks each batch's
+        # ``RawBatch.status`` itself (KafkaSource.verify) and nothing accumulates here
+        self.track = track
+        self.checks: List["DecodeStatus"] = []
 
     def decode(self, staging: torch.Tensor, plan: FetchPlan):
         """Returns (RawBatch, done_event).  ``staging`` is a pinned uint8 tensor holding the record sets at the
@@ -331,24 +337,48 @@ class DeviceRecordDecoder:
         N.call("dxa_kafka_records", N.ptr(out), plan.nbat, N.ptr(bc), N.ptr(bs), N.ptr(bk), N.ptr(bf), N.ptr(bn),
                N.ptr(br), N.ptr(oo), N.ptr(cap), N.ptr(produced), N.ptr(bstat), N.ptr(offs), N.ptr(ends),
                N.ptr(rstat), st)
+        with torch.cuda.stream(self.decode_stream):
+            status = DecodeStatus((rstat[:plan.nbat] != 0).sum(), self.decode_stream)
         done = torch.cuda.Event()
         done.record(self.decode_stream)
         for t in (ddata, produced, bstat, dtab):
             t.record_stream(self.decode_stream)
-        self.checks.append(rstat[:plan.nbat])
+        if self.track:
+            self.checks.append(status)
         # the pinned bytes (record sets and plan tables) must outlive their async copies
         self._inflight = [(e, b) for e, b in getattr(self, "_inflight", []) if not e.query()] + \
             [(done, (staging, packed))]
-        return RawBatch(out, offs, n, ends=ends[:n], source_bytes=plan.nbytes), done
+        return RawBatch(out, offs, n, ends=ends[:n], source_bytes=plan.nbytes, status=status), done
 
     def check(self):
-        """Raise if any decoded batch failed (one host read of all pending status tensors)."""
-        if not self.checks:
-            return
-        bad = [int((c != 0).sum()) for c in self.checks]
-        self.checks.clear()
-        if any(bad):
-            raise ValueError(f"{sum(bad)} Kafka record batch(es) failed to decode on the device")
+        """Raise if any decoded batch failed (reads the pending batches' status words, already copied to pinned
+        host memory behind their decodes)."""
+        pending, self.checks = self.checks, []
+        bad = sum(s.failed() for s in pending)
+        if bad:
+            raise DecodeError(f"{bad} Kafka record batch(es) failed to decode on the device")
+
+
+class DecodeError(ValueError):
+    pass
+
+
+class DecodeStatus:
+    """Number of record batches of one fetch that failed to decode (corrupt LZ4 block, record framing past the
+    batch), copied device → pinned host on the decode stream right behind the decode, so reading it later costs
+    no device synchronisation beyond that batch's own decode."""
+
+    __slots__ = ("host", "event")
+
+    def __init__(self, bad: torch.Tensor, stream):
+        self.host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+        self.host.copy_(bad.reshape(1), non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(stream)
+
+    def failed(self) -> int:
+        self.event.synchronize()
+        return int(self.host[0])
 
 
 def decode_on_host_like(staging: np.ndarray, plan: FetchPlan):

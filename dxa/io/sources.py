@@ -101,23 +101,34 @@ def _to_device_batch(records: Sequence[bytes], device, file_info=None) -> RawBat
 
 
 class LocalGeneratorSource(Source):
-    """Synthetic events from a SimulatedData/DataGenerator schema, rendered on the device."""
+    """Synthetic events from a SimulatedData/DataGenerator schema, rendered on the device.
+
+    ``events_per_batch`` is the JOB's rate, as the reference's single local receiver (LocalStreamingSource.scala:
+    31-37): with W ranks, rank r renders rows ``[row + off_r, row + off_r + n_r)`` of the same counter-based stream
+    (``n_r`` = its share), so the W ranks together produce exactly the events one rank would, never duplicates."""
     name = "local"
 
-    def __init__(self, schema, events_per_batch: int, device, seed: int = 1, simulated: bool = False):
+    def __init__(self, schema, events_per_batch: int, device, seed: int = 1, simulated: bool = False,
+                 rank: Optional[int] = None, world: Optional[int] = None):
+        from .. import parallel as P
         from ..simulate.datagen import compile_simulated, compile_spark
         self.prog = compile_simulated(schema) if simulated else compile_spark(schema)
         self.n = int(events_per_batch)
         self.device = torch.device(device)
         self.seed = seed
         self.row = 0
+        self.rank = P.rank() if rank is None else rank
+        self.world = P.world() if world is None else world
+        base, extra = divmod(self.n, self.world)
+        self.n_mine = base + (1 if self.rank < extra else 0)
+        self.offset = self.rank * base + min(self.rank, extra)
 
     def next_batch(self, batch_time_us: int) -> Optional[RawBatch]:
         from ..simulate.datagen import generate
-        buf, offs = generate(self.prog, self.n, self.device, seed=self.seed, row0=self.row,
+        buf, offs = generate(self.prog, self.n_mine, self.device, seed=self.seed, row0=self.row + self.offset,
                              base_ms=batch_time_us // 1000, step_us=0)
         self.row += self.n
-        return RawBatch(buf, offs, self.n)
+        return RawBatch(buf, offs, self.n_mine)
 
 
 class QueueSource(Source):
@@ -150,9 +161,13 @@ class SocketSource(QueueSource):
     """TCP listener: each connection streams newline-delimited JSON events."""
     name = "socket"
 
-    def __init__(self, device, host: str = "127.0.0.1", port: int = 9999):
+    def __init__(self, device, host: str = "127.0.0.1", port: int = 9999, rank: Optional[int] = None):
+        """With W ranks each rank is one receiver: rank r listens on ``port + r`` (port 0: any free port), so
+        producers spread their connections over the ranks the way Spark spreads receivers over executors."""
+        from .. import parallel as P
         super().__init__(device)
-        self.sock = socket.create_server((host, port))
+        rank = P.rank() if rank is None else rank
+        self.sock = socket.create_server((host, port + rank if port else 0))
         self.port = self.sock.getsockname()[1]
         self._stop = False
         threading.Thread(target=self._accept, daemon=True).start()
@@ -178,19 +193,24 @@ class SocketSource(QueueSource):
 
 
 class FileSource(Source):
-    """New files appearing under a folder (glob pattern), newline-delimited JSON (gzip-aware).  Each batch takes the
-    files not yet processed; framing runs on the device."""
+    """New files appearing under a folder or glob pattern (local or ``wasbs://``), newline-delimited JSON
+    (gzip-aware).  Each batch takes the files not yet processed; framing runs on the device.  With W ranks a file is
+    read by exactly one rank (``fs.owned_by_rank``: stable hash of its path), as Spark spreads input files over
+    executors."""
     name = "file"
 
-    def __init__(self, pattern: str, device, max_files_per_batch: int = 1000):
+    def __init__(self, pattern: str, device, max_files_per_batch: int = 1000, rank: Optional[int] = None,
+                 world: Optional[int] = None):
+        from .. import parallel as P
         self.pattern = pattern
         self.device = torch.device(device)
         self.seen = set()
         self.max_files = max_files_per_batch
+        self.rank = P.rank() if rank is None else rank
+        self.world = P.world() if world is None else world
 
     def _list(self) -> List[str]:
-        import glob
-        return sorted(p for p in glob.glob(str(fs.local_path(self.pattern)), recursive=True) if os.path.isfile(p))
+        return fs.owned_by_rank(fs.list_matching(self.pattern), self.rank, self.world)
 
     def next_batch(self, batch_time_us: int) -> Optional[RawBatch]:
         files = [p for p in self._list() if p not in self.seen][: self.max_files]
@@ -256,12 +276,17 @@ class PartitionedReplaySource(OffsetTrackedSource):
 
     def __init__(self, partitions: Dict[str, Sequence[bytes]], device, checkpoint_dir: Optional[str] = None,
                  max_rate: Optional[int] = None, hub: str = "replay", flush_existing: bool = False):
-        self.parts = partitions
         self.device = torch.device(device)
         self.max_rate = max_rate
         self.hub = hub
+        from .. import parallel as P
+        # partition → rank: rank r reads the partitions at positions ≡ r (mod W) of the sorted partition list, and
+        # checkpoints them in its own offsets file
+        names = sorted(partitions)
+        mine = [p for i, p in enumerate(names) if i % P.world() == P.rank()]
+        self.parts = {p: partitions[p] for p in mine}
         ckpt = Checkpointer(checkpoint_dir) if checkpoint_dir else None
-        pos = {p: 0 for p in partitions}
+        pos = {p: 0 for p in self.parts}
         if ckpt and not flush_existing:
             for (name, part), until in ckpt.restore().items():
                 if name == hub and part in pos:
@@ -281,10 +306,21 @@ class PartitionedReplaySource(OffsetTrackedSource):
 
 
 class Checkpointer:
-    """``offsets.txt`` (+ ``.old`` backup) — the reference's EventhubCheckpointer format."""
+    """``offsets.txt`` (+ ``.old`` backup) — the reference's EventhubCheckpointer format
+    (``batchTimeMs,ehName,partition,fromSeq,untilSeq``, EventhubCheckpointer.scala:16-73).
 
-    def __init__(self, folder: str):
-        self.path = os.path.join(str(fs.local_path(folder)), "offsets.txt")
+    With W ranks every rank owns a disjoint set of partitions and writes its own file, ``<folder>/rank-<r>/
+    offsets.txt`` (ranks never overwrite each other's lines); ``restore`` reads the single-rank file and every
+    rank's file and keeps, per (hub, partition), the line of the latest batch — so a restart at any world size finds
+    every partition's committed position, whichever rank wrote it."""
+
+    def __init__(self, folder: str, rank: Optional[int] = None, world: Optional[int] = None):
+        from .. import parallel as P
+        rank = P.rank() if rank is None else rank
+        world = P.world() if world is None else world
+        self.root = str(fs.local_path(folder))
+        sub = self.root if world <= 1 else os.path.join(self.root, f"rank-{rank}")
+        self.path = os.path.join(sub, "offsets.txt")
 
     def write(self, batch_ms: int, ranges):
         os.makedirs(os.path.dirname(self.path), exist_ok=True)
@@ -293,17 +329,30 @@ class Checkpointer:
         lines = [f"{batch_ms},{name},{part},{s},{e}" for name, part, s, e in ranges]
         fs.write_atomic(self.path, "\n".join(lines) + "\n")
 
-    def restore(self) -> Dict[Tuple[str, str], int]:
-        path = self.path if os.path.exists(self.path) else (self.path + ".old" if os.path.exists(
-            self.path + ".old") else None)
-        if path is None:
-            return {}
-        out = {}
-        for line in open(path):
-            parts = line.strip().split(",")
-            if len(parts) == 5:
-                out[(parts[1], parts[2])] = int(parts[4])
+    def _files(self) -> List[str]:
+        out = []
+        cands = [os.path.join(self.root, "offsets.txt")]
+        if os.path.isdir(self.root):
+            cands += [os.path.join(self.root, d, "offsets.txt") for d in sorted(os.listdir(self.root))
+                      if d.startswith("rank-")]
+        for c in cands:
+            if os.path.exists(c):
+                out.append(c)
+            elif os.path.exists(c + ".old"):
+                out.append(c + ".old")
         return out
+
+    def restore(self) -> Dict[Tuple[str, str], int]:
+        best: Dict[Tuple[str, str], Tuple[int, int]] = {}
+        for path in self._files():
+            for line in open(path):
+                parts = line.strip().split(",")
+                if len(parts) != 5:
+                    continue
+                key, ms, until = (parts[1], parts[2]), int(parts[0]), int(parts[4])
+                if key not in best or ms >= best[key][0]:
+                    best[key] = (ms, until)
+        return {k: v[1] for k, v in best.items()}
 
 
 def build_source(settings, device, kind: Optional[str] = None) -> Source:

@@ -23,10 +23,9 @@
 namespace {
 
 uint32_t g_crc_table[8][256];
-bool g_crc_init = false;
 
-void crc_init() {
-  if (g_crc_init) return;
+// table for the portable path, built once (thread-safe static init)
+bool crc_init() {
   for (uint32_t i = 0; i < 256; ++i) {
     uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
@@ -34,12 +33,12 @@ void crc_init() {
   }
   for (uint32_t i = 0; i < 256; ++i)
     for (int t = 1; t < 8; ++t) g_crc_table[t][i] = (g_crc_table[t - 1][i] >> 8) ^ g_crc_table[0][g_crc_table[t - 1][i] & 0xff];
-  g_crc_init = true;
+  return true;
 }
 
-uint32_t crc32c(const uint8_t* p, size_t n) {
-  crc_init();
-  uint32_t c = 0xFFFFFFFFu;
+uint32_t crc32c_sw(const uint8_t* p, size_t n, uint32_t c) {
+  static const bool init = crc_init();
+  (void)init;
   while (n >= 8) {
     uint64_t w;
     std::memcpy(&w, p, 8);
@@ -51,7 +50,37 @@ uint32_t crc32c(const uint8_t* p, size_t n) {
     n -= 8;
   }
   while (n--) c = (c >> 8) ^ g_crc_table[0][(c ^ *p++) & 0xff];
-  return c ^ 0xFFFFFFFFu;
+  return c;
+}
+
+#if defined(__x86_64__)
+// SSE4.2 crc32 computes exactly CRC-32C (Castagnoli): one 8-byte step per instruction, ~8 GB/s per core against
+// ~2.5 GB/s for the slice-by-8 table path (Kafka's check.crcs covers every record batch a fetch returns)
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(const uint8_t* p, size_t n, uint32_t c) {
+  uint64_t c64 = c;
+  while (n && ((uintptr_t)p & 7)) { c64 = __builtin_ia32_crc32qi((uint32_t)c64, *p++); --n; }
+  while (n >= 32) {
+    uint64_t w0, w1, w2, w3;
+    std::memcpy(&w0, p, 8); std::memcpy(&w1, p + 8, 8); std::memcpy(&w2, p + 16, 8); std::memcpy(&w3, p + 24, 8);
+    c64 = __builtin_ia32_crc32di(c64, w0);
+    c64 = __builtin_ia32_crc32di(c64, w1);
+    c64 = __builtin_ia32_crc32di(c64, w2);
+    c64 = __builtin_ia32_crc32di(c64, w3);
+    p += 32;
+    n -= 32;
+  }
+  while (n >= 8) { uint64_t w; std::memcpy(&w, p, 8); c64 = __builtin_ia32_crc32di(c64, w); p += 8; n -= 8; }
+  while (n--) c64 = __builtin_ia32_crc32qi((uint32_t)c64, *p++);
+  return (uint32_t)c64;
+}
+const bool g_has_sse42 = __builtin_cpu_supports("sse4.2");
+#endif
+
+uint32_t crc32c(const uint8_t* p, size_t n) {
+#if defined(__x86_64__)
+  if (g_has_sse42) return crc32c_hw(p, n, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+#endif
+  return crc32c_sw(p, n, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
 }
 
 inline int64_t be64(const uint8_t* p) {
