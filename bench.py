@@ -236,6 +236,7 @@ def main():
 
     def stage(i):
         """Make batch i's raw bytes available in HBM — on a side stream, overlapping batch i-1's processing."""
+        arrival[i] = time.perf_counter()
         if source == "kafka":
             staging, bounds = pool[i % len(pool)], kafka_parts[i % len(pool)]
             sn = staging.numpy()
@@ -297,8 +298,21 @@ def main():
         staged[i] = (db, do, ev)
 
     lat = []
+    # Latency-Batch (CommonProcessorFactory.scala:373: completion wall time − batch time).  The bench runs the stream
+    # saturated, so a batch's time is the wall-clock moment it closes and starts arriving — when stage(i) begins its
+    # ingest (``prefetch`` steps before it is processed) — and it completes when its last sink write finishes.  (The
+    # simulated clock passed to process_batch only drives event times / windows.)
+    arrival = {}
+    lat_batch = []
+
+    def on_complete(bt, m):
+        lat.append(m["Latency-Process"])
+        i = (bt - clock0_us) // interval_us
+        t_arr = arrival.pop(i, None)
+        if t_arr is not None:
+            lat_batch.append(proc.last_done_perf - t_arr)
     host_trace = [] if os.environ.get("DXA_BENCH_HOST_TRACE") else None
-    proc.on_batch_complete = lambda bt, m: lat.append(m["Latency-Process"])
+    proc.on_batch_complete = on_complete
 
     ready = {}
     parse_ahead = on_gpu and os.environ.get("DXA_PARSE_AHEAD", "1") != "0"
@@ -342,6 +356,7 @@ def main():
     if world > 1:
         dist.barrier()
     lat.clear()
+    lat_batch.clear()
     sizes.clear()
     prof = None
     if args.torch_profile:
@@ -382,22 +397,27 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        lt = torch.tensor(sorted(lat), dtype=torch.float64, device=cdev)
-        gathered = [torch.empty_like(lt) for _ in range(world)]
-        dist.all_gather(gathered, lt)
-        lat = sorted(float(x) for g in gathered for x in g.tolist())
+        def gather_all(xs):
+            lt = torch.tensor(sorted(xs), dtype=torch.float64, device=cdev)
+            gathered = [torch.empty_like(lt) for _ in range(world)]
+            dist.all_gather(gathered, lt)
+            return sorted(float(x) for g in gathered for x in g.tolist())
+        lat = gather_all(lat)
+        lat_batch = gather_all(lat_batch) if len(lat_batch) == args.steps else lat_batch
     lat_sorted = sorted(lat)
+    latb_sorted = sorted(lat_batch)
     if framing_checks:
         from dxa.ops.jsonparse import check_framing
         check_framing(framing_checks)                      # after the timed region: one host sync
     if kdec is not None:
         kdec.check()                                       # every record batch decoded (one host sync)
 
-    def pct(p):
-        if not lat_sorted:
+    def pct(p, xs=None):
+        xs = lat_sorted if xs is None else xs
+        if not xs:
             return None
-        k = min(len(lat_sorted) - 1, max(0, int(round(p / 100.0 * (len(lat_sorted) - 1)))))
-        return lat_sorted[k] * 1000.0
+        k = min(len(xs) - 1, max(0, int(round(p / 100.0 * (len(xs) - 1)))))
+        return xs[k] * 1000.0
 
     total_events = E * world * args.steps
     value = total_events / elapsed
@@ -428,6 +448,8 @@ def main():
                    "sink": args.sink},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),
+        "p50_latency_batch_ms": pct(50, latb_sorted),
+        "p99_latency_batch_ms": pct(99, latb_sorted),
         "events_per_sec_per_gpu": value / world,
         "vs_target_1M_events_per_sec_per_gpu": value / world / 1e6,
         "generation_s": round(gen_s, 3),

@@ -372,6 +372,7 @@ class Processor:
         # where the completion was observed)
         metrics["Latency-Process"] = t_done - fl.t0
         metrics["Latency-Batch"] = (time.time() * 1e6 - fl.batch_time_us) / 1e6
+        self.last_done_perf = t_done            # perf_counter() when the batch's last sink write finished
         if P.rank() == 0:
             self.metric_logger.send_batch_metrics(metrics, fl.batch_time_us // 1000)
         self.last_metrics = metrics

@@ -6,9 +6,10 @@ columns, ``to_json(struct(*))``, ``Sink_InputEvents`` / ``Sink_<S>_All|Filtered`
 EventHubStreamPoster.scala (200-event chunks, newline-joined), HttpPoster.scala (200-event JSON arrays),
 CosmosDBSinker.scala, SqlSinker.scala.
 
-Sinks available on a single node without cloud services: blob → local/mounted folder; eventhub → a local spool
-folder per hub (or an http(s) endpoint); httppost → real HTTP; cosmosdb → JSON document folder per
-database/collection; sql → SQLite (``sqlite:///path``); plus ``file``, ``console``, ``memory`` and ``null``.
+Cloud targets are real clients (Blob / Event Hubs / Cosmos DB REST, SQL Server over TDS — ``dxa.io.tds``).  The
+single-node stand-ins are opt-in only: blob → local/mounted folder; eventhub → a local spool folder per hub;
+cosmosdb ``local:`` → JSON document folder per database/collection; sql ``sqlite:///path`` or ``local:`` → SQLite;
+plus ``file``, ``console``, ``memory`` and ``null``.  A connection string that is neither fails at job start.
 """
 from __future__ import annotations
 
@@ -165,26 +166,37 @@ def _http_sink(d, output_name) -> Optional[Sink]:
     return Sink("HttpPost", write, d.get("filter"))
 
 
+def _local_scheme(conn: str) -> Optional[str]:
+    """``local:`` / ``local:<sub folder>`` — an explicit request for the single-node stand-in of a cloud sink."""
+    return conn[len("local:"):].strip("/") if conn.lower().startswith("local:") else None
+
+
 def _cosmos_sink(d, output_name) -> Optional[Sink]:
-    conn = d.get("connectionstring")
-    if not conn:
+    conn_ref = d.get("connectionstring")
+    if not conn_ref:
         return None
     db = d.get("database") or "db"
     coll = d.get("collection") or output_name
+    from . import azure
+    conn = resolve(conn_ref)
+    local = _local_scheme(conn)
+    if local is None and not azure.is_cosmos_connection(conn):
+        # a production string that does not parse must not silently turn into local files
+        raise ValueError(f"output '{output_name}': cosmosdb.connectionstring is neither a Cosmos DB connection "
+                         "string (AccountEndpoint=…;AccountKey=…) nor an explicit 'local:' target")
 
     def write(lines, table, ts, target):
-        from . import azure
-        c = resolve(conn)
-        if azure.is_cosmos_connection(c):
+        if local is None:
             # document upserts through the REST API (CosmosDBSinker's upsert mode)
-            client = azure.CosmosClient(c)
+            client = azure.CosmosClient(conn)
             for line in lines:
                 doc = json.loads(line)
                 doc.setdefault("id", str(uuid.uuid4()))
                 client.upsert(db, coll, doc)
             return len(lines)
         root = os.environ.get("DXA_FS_ROOT", ".dxa_fs")
-        folder = os.path.join(root, "cosmosdb", db, coll)
+        folder = os.path.join(root, "cosmosdb", local, db, coll) if local else os.path.join(root, "cosmosdb", db,
+                                                                                            coll)
         os.makedirs(folder, exist_ok=True)
         for line in lines:
             doc = json.loads(line)
@@ -194,18 +206,63 @@ def _cosmos_sink(d, output_name) -> Optional[Sink]:
     return Sink("CosmosDB", write, d.get("filter"))
 
 
+def _opt(d, key):
+    """Setting lookup tolerant of the reference's camelCase keys (``trustServerCertificate``)."""
+    v = d.get(key)
+    if v is None:
+        low = key.lower()
+        for k, val in d.items():
+            if k.lower() == low:
+                return val
+    return v
+
+
 def _sql_sink(d, output_name) -> Optional[Sink]:
-    conn = d.get("connectionstring")
-    if not conn:
+    """SqlSinker (SqlSinker.scala:19-107): SQL Server / Azure SQL over TDS (``jdbc:sqlserver://…`` or ADO.NET
+    strings; ``usebulkinsert`` → bulk load), SQLite for ``sqlite:///path``, a local SQLite file for ``local:``.
+    Anything else fails at job start."""
+    conn_ref = d.get("connectionstring")
+    if not conn_ref:
         return None
     table_name = d.get("table") or output_name
+    conn = resolve(conn_ref)
     lock = threading.Lock()
+    from . import tds
+    if tds.is_sqlserver_connection(conn) or (_opt(d, "url") and tds.is_sqlserver_connection(resolve(_opt(d, "url")))):
+        def sec(key):
+            v = _opt(d, key)
+            return resolve(v) if v else None
+        writer = tds.SqlServerWriter(
+            conn, table_name, write_mode=d.get("writemode") or "append", url=sec("url"),
+            database=_opt(d, "databasename"), user=sec("user"), password=sec("password"),
+            encrypt=_opt(d, "encrypt"), trust_server_certificate=_opt(d, "trustServerCertificate"),
+            host_name_in_certificate=_opt(d, "hostNameInCertificate"),
+            connect_timeout=float(d.get("connectiontimeout") or 30), query_timeout=float(d.get("querytimeout") or 30),
+            bulk=(d.get("usebulkinsert") or "false").lower() == "true",
+            bulk_batch=int(d.get("bulkcopybatchsize") or 2000),
+            table_lock=(d.get("usebulkcopytablelock") or "false").lower() == "true")
+
+        def write_tds(lines, table, ts, target):
+            if table.length == 0:
+                return 0
+            cols = table.names
+            types = [c.dtype for c in table.columns]
+            rows = [[json.dumps(v, default=str) if isinstance(v, (dict, list)) else v for v in
+                     (r[c] for c in cols)] for r in table.to_pylist()]
+            with lock:
+                return writer.write(cols, types, rows)
+        return Sink("SqlSink", write_tds, d.get("filter"), as_json=False)
+    local = _local_scheme(conn)
+    if conn.startswith("sqlite:///"):
+        path = conn[len("sqlite:///"):]
+    elif local is not None:
+        path = os.path.join(os.environ.get("DXA_FS_ROOT", ".dxa_fs"), "sql", (local or "sql") + ".db")
+    else:
+        raise ValueError(f"output '{output_name}': sql.connectionstring is not a SQL Server connection string "
+                         "(jdbc:sqlserver://… or Server=…), a sqlite:/// path or an explicit 'local:' target")
 
     def write(lines, table, ts, target):
         import sqlite3
-        c = resolve(conn)
-        path = c[len("sqlite:///"):] if c.startswith("sqlite:///") else os.path.join(
-            os.environ.get("DXA_FS_ROOT", ".dxa_fs"), "sql.db")
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         rows = table.to_pylist()
         if not rows:

@@ -12,7 +12,9 @@ from dxa.sql.codegen import generate_code, loads_lenient
 from dxa.sql.parser import tokenize
 from dxa.sql.transform import parse_transform
 
-FIX = "/root/reference/Services/DataX.Flow/DataX.Flow.CodegenRules.Tests"
+from tests.fixtures import ref_path
+
+FIX = ref_path("Services/DataX.Flow/DataX.Flow.CodegenRules.Tests")
 CASES = [
     # (user code file or literal, rules, expected, product, custom templates?)
     ("usercode.txt", "Rules.json", "cgen.txt", "P1", True),

@@ -10,7 +10,9 @@ import re
 
 import pytest
 
-CFG = "/root/reference/Services/DataX.Config/DataX.Config.Test/Resource"
+from tests.fixtures import ref_path
+
+CFG = ref_path("Services/DataX.Config/DataX.Config.Test/Resource")
 pytestmark = pytest.mark.skipif(not os.path.isdir(CFG), reason="reference fixtures not mounted")
 
 ENV_SPECIFIC = re.compile(r"(checkpointdir|blobschemafile|process\.projection|process\.transform|\.location$|"

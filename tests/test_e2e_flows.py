@@ -10,8 +10,10 @@ import sys
 
 import pytest
 
-SAMPLES = "/root/reference/DeploymentLocal/sample"
-DEVICES = "/root/reference/DeploymentCloud/Deployment.DataX/Samples/usercontent/devices.csv"
+from tests.fixtures import ref_path
+
+SAMPLES = ref_path("DeploymentLocal/sample")
+DEVICES = ref_path("DeploymentCloud/Deployment.DataX/Samples/usercontent/devices.csv")
 pytestmark = pytest.mark.skipif(not os.path.isdir(SAMPLES), reason="reference samples not mounted")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 

@@ -208,3 +208,67 @@ def test_kafka_source_device_decode_matches_host(broker, tmp_path, compression):
         got[mode] = (rows, sorted(open(os.path.join(tmp_path / mode, "offsets.txt")).read().splitlines()))
     assert got["device"] == got["host"]
     assert [len(r) for r in got["device"][0]] == [210, 210, 30]
+
+
+@pytest.mark.gpu
+def test_kafka_device_batches_survive_next_decode(broker, tmp_path):
+    """A batch's device buffers are recorded on the consumer stream: work queued on it behind a long kernel still
+    reads batch 1's bytes after the batch is dropped and batch 2 decodes (the caching allocator must not hand batch
+    1's memory to batch 2's decode stream)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = K.KafkaClient(f"127.0.0.1:{broker.port}")
+    for p in range(3):
+        c.produce("iot", p, [json.dumps({"p": p, "i": i, "pad": "x" * (i % 50)}).encode() for i in range(400)],
+                  compression="lz4")
+    src = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cuda:0", max_rate=200,
+                        device_decode=True)
+    raw1 = src.next_batch(1_000_000)
+    torch.cuda.synchronize()
+    want = raw1.buf.cpu().clone()
+    torch.cuda._sleep(200_000_000)                 # the consumer stream is busy for a while ...
+    late = raw1.buf.clone()                        # ... so this copy of batch 1 runs after batch 2's decode
+    del raw1
+    raw2 = src.next_batch(2_000_000)
+    torch.cuda.synchronize()
+    assert torch.equal(late.cpu(), want)
+    assert raw2.n == 600
+    src.verify(1_000_000)
+    src.verify(2_000_000)
+
+
+@pytest.mark.gpu
+def test_kafka_device_decode_failure_is_reported(broker):
+    """A corrupt LZ4 block that passes the host plan fails on the device; ``verify`` (called by the streaming host
+    before commit) raises instead of committing malformed rows."""
+    import torch
+    from dxa.io import kafka_device as KD
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    vals = [json.dumps({"i": i, "s": "abc" * 20}).encode() for i in range(200)]
+    rs = bytearray(K.encode_batch(vals, 1, "lz4", level=9))
+    plan = KD.plan_fetch(bytes(rs), 0, verify_crc=False)
+    # point the first block's first match far before the output start: the decoder must flag it
+    off = int(plan.k_comp_off[0])
+    stored = bool(plan.k_stored[0])
+    if stored:
+        pytest.skip("first block stored uncompressed")
+    tok = rs[off]
+    lit = tok >> 4
+    p = off + 1
+    if lit == 15:
+        while rs[p] == 255:
+            p += 1
+        lit += rs[p]
+        p += 1
+    p += lit
+    rs[p:p + 2] = (0xFFFF).to_bytes(2, "little")
+    staging = torch.zeros(len(rs) + 64, dtype=torch.uint8).pin_memory()
+    staging[:len(rs)] = torch.frombuffer(bytearray(rs), dtype=torch.uint8)
+    dec = KD.DeviceRecordDecoder(torch.device("cuda:0"))
+    raw, ev = dec.decode(staging, plan)
+    torch.cuda.current_stream().wait_event(ev)
+    assert raw.status.failed() > 0
+    with pytest.raises(KD.DecodeError):
+        dec.check()

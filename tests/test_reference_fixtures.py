@@ -16,8 +16,9 @@ import time
 import pytest
 import torch
 
-REF = "/root/reference"
-CFG = os.path.join(REF, "Services/DataX.Config/DataX.Config.Test/Resource")
+from tests.fixtures import ref_path
+
+CFG = ref_path("Services/DataX.Config/DataX.Config.Test/Resource")
 need_ref = pytest.mark.skipif(not os.path.isdir(CFG), reason="reference fixtures not mounted")
 
 

@@ -12,9 +12,10 @@ from dxa.service import scheduler as S
 from dxa.service.metrics_ingestor import generate_row, ingest_lines
 from dxa.telemetry.metrics import MetricStore
 
-REF = "/root/reference"
-SAMPLE = os.path.join(REF, "DeploymentLocal/sample/HomeAutomationLocal.json")
-BATCH = os.path.join(REF, "Services/DataX.Config/DataX.Config.Test/Resource/batchFlow.json")
+from tests.fixtures import ref_path
+
+SAMPLE = ref_path("DeploymentLocal/sample/HomeAutomationLocal.json")
+BATCH = ref_path("Services/DataX.Config/DataX.Config.Test/Resource/batchFlow.json")
 
 SCHEMA = json.dumps({"type": "struct", "fields": [
     {"name": "deviceId", "type": "long", "nullable": True, "metadata": {}},

@@ -7,7 +7,9 @@ import pytest
 
 from dxa.simulate.simulated_data import DataGen, DotNetRandom, SimulatedDataService, dotnet_g15, file_output
 
-D = "/root/reference/Services/DataX.SimulatedData/DataX.SimulatedData.DataGenServiceTest"
+from tests.fixtures import ref_path
+
+D = ref_path("Services/DataX.SimulatedData/DataX.SimulatedData.DataGenServiceTest")
 need_ref = pytest.mark.skipif(not os.path.isdir(D), reason="reference fixtures not mounted")
 
 
