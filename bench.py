@@ -438,8 +438,8 @@ def main():
                 + ("; delivered as LZ4-framed batches in pinned host memory, decompressed on the GPU in every step)"
                    if source == "pinned-lz4" else
                    "; delivered as Kafka v2 record batches with the LZ4 codec in pinned host memory (a "
-                   "multi-partition Fetch), planned on the host, decompressed and record-framed on the GPU in every "
-                   "step)" if source == "kafka" else ")"),
+                   "multi-partition Fetch), planned on the host, CRC-32C-verified (check.crcs), decompressed and "
+                   "record-framed on the GPU in every step)" if source == "kafka" else ")"),
         "config": {"model": MODEL[flow].format(ref=args.ref_rows), "flow": flow,
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
                    "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,

@@ -472,7 +472,7 @@ class KafkaSource(OffsetTrackedSource):
                 if not recs:
                     break
                 try:
-                    plan = KD.plan_fetch(recs, cur, self.verify_crc)
+                    plan = KD.plan_fetch(recs, cur)                # CRCs are checked on the device
                 except KD.Unsupported:
                     return None
                 if self.max_rate is not None:
@@ -492,7 +492,7 @@ class KafkaSource(OffsetTrackedSource):
         for recs, (_, at) in zip(sets, plans):
             sn[at:at + len(recs)] = np.frombuffer(recs, dtype=np.uint8)
         if self._decoder is None:
-            self._decoder = KD.DeviceRecordDecoder(self.device, track=False)
+            self._decoder = KD.DeviceRecordDecoder(self.device, track=False, verify_crc=self.verify_crc)
         raw, done = self._decoder.decode(staging, KD.merge(plans))
         cur_stream = torch.cuda.current_stream(self.device)
         cur_stream.wait_event(done)

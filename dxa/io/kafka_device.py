@@ -10,8 +10,10 @@ device.
 
 Batches the GPU path does not take (gzip / snappy / zstd codecs, dependent-block LZ4 frames, compacted batches
 with offset gaps) make ``plan_fetch`` raise ``Unsupported``; the source then decodes that fetch on the host.
-CRC-32C is verified on the host when ``verify_crc`` is set (the consumer's ``check.crcs``); the GPU ingest runs
-with it off by default, as a consumer may.
+CRC-32C (the consumer's ``check.crcs``, on by default) is verified on the GPU over the compressed bytes already in
+HBM (``kafka_crc_kernel``: one wave per batch, 64 segment CRCs combined in GF(2)), so the host planner reads only
+headers; a mismatch fails the batch's status like a decode error.  ``plan_*(verify_crc=True)`` checks on the host
+instead (the host decoder's path).
 """
 from __future__ import annotations
 
@@ -42,7 +44,7 @@ def _lib():
     L = lib()
     if not _BOUND:
         p, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
-        L.dxa_kafka_plan.argtypes = [p, i64, i64, i32, p, p] + [p] * 11
+        L.dxa_kafka_plan.argtypes = [p, i64, i64, i32, p, p] + [p] * 14
         L.dxa_kafka_plan.restype = ctypes.c_int
         _BOUND = True
     return L
@@ -68,6 +70,15 @@ class FetchPlan:
     nbytes: int = 0               # staging bytes covered
     packed: Optional[torch.Tensor] = None      # pinned bytes holding every array above (one H2D copy), if any
     layout: Optional[list] = None              # [(name, byte offset, count)] of the arrays inside ``packed``
+    b_crc_off: Optional[np.ndarray] = None     # int64 [nbat] CRC-covered range start (attributes) in the staging
+    b_crc_len: Optional[np.ndarray] = None     # int32 [nbat] CRC-covered length
+    b_crc: Optional[np.ndarray] = None         # int32 [nbat] stored CRC-32C (bits)
+
+    def __post_init__(self):
+        n = int(self.b_count.shape[0])
+        for name, dt in (("b_crc_off", np.int64), ("b_crc_len", np.int32), ("b_crc", np.int32)):
+            if getattr(self, name) is None:
+                setattr(self, name, np.zeros(n, dt))
 
     @property
     def nbat(self) -> int:
@@ -86,14 +97,15 @@ class FetchPlan:
         return self.b_base + self.b_skip + self.b_keep - 1
 
 
-def plan_fetch(data, min_offset: int, verify_crc: bool = True) -> FetchPlan:
-    """Plan one Fetch record set (bytes / uint8 ndarray) → FetchPlan (offsets relative to ``data``)."""
+def plan_fetch(data, min_offset: int, verify_crc: bool = False) -> FetchPlan:
+    """Plan one Fetch record set (bytes / uint8 ndarray) → FetchPlan (offsets relative to ``data``).
+    ``verify_crc``: check CRCs here on the host (the default leaves them to the device decode)."""
     a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     L = _lib()
     counts = np.zeros(5, dtype=np.int64)
     nxt = ctypes.c_int64(0)
     rc = L.dxa_kafka_plan(a.ctypes.data, a.size, min_offset, int(verify_crc), counts.ctypes.data,
-                          ctypes.byref(nxt), *([None] * 11))
+                          ctypes.byref(nxt), *([None] * 14))
     if rc:
         raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
     nbat, nblk = int(counts[0]), int(counts[1])
@@ -101,9 +113,10 @@ def plan_fetch(data, min_offset: int, verify_crc: bool = True) -> FetchPlan:
                b_skip=np.zeros(nbat, np.int32), b_first=np.zeros(nbat, np.int32), b_nblk=np.zeros(nbat, np.int32),
                b_rec0=np.zeros(nbat, np.int64), k_comp_off=np.zeros(nblk, np.int64),
                k_comp_len=np.zeros(nblk, np.int32), k_stored=np.zeros(nblk, np.uint8),
-               k_out_off=np.zeros(nblk, np.int64), k_cap=np.zeros(nblk, np.int64))
+               k_out_off=np.zeros(nblk, np.int64), k_cap=np.zeros(nblk, np.int64),
+               b_crc_off=np.zeros(nbat, np.int64), b_crc_len=np.zeros(nbat, np.int32), b_crc=np.zeros(nbat, np.int32))
     order = ["b_count", "b_base", "b_skip", "b_first", "b_nblk", "b_rec0", "k_comp_off", "k_comp_len", "k_stored",
-             "k_out_off", "k_cap"]
+             "k_out_off", "k_cap", "b_crc_off", "b_crc_len", "b_crc"]
     rc = L.dxa_kafka_plan(a.ctypes.data, a.size, min_offset, int(verify_crc), counts.ctypes.data,
                           ctypes.byref(nxt), *[arr[k].ctypes.data for k in order])
     if rc:
@@ -115,7 +128,8 @@ def plan_fetch(data, min_offset: int, verify_crc: bool = True) -> FetchPlan:
 _ARRAYS = [("b_count", np.int32, "b"), ("b_base", np.int64, "b"), ("b_skip", np.int32, "b"),
            ("b_keep", np.int32, "b"), ("b_first", np.int32, "b"), ("b_nblk", np.int32, "b"),
            ("b_rec0", np.int64, "b"), ("k_comp_off", np.int64, "k"), ("k_comp_len", np.int32, "k"),
-           ("k_stored", np.uint8, "k"), ("k_out_off", np.int64, "k"), ("k_cap", np.int64, "k")]
+           ("k_stored", np.uint8, "k"), ("k_out_off", np.int64, "k"), ("k_cap", np.int64, "k"),
+           ("b_crc_off", np.int64, "b"), ("b_crc_len", np.int32, "b"), ("b_crc", np.int32, "b")]
 
 
 class PlanBuffer:
@@ -169,16 +183,16 @@ class PlanBufferPool:
 
 
 def plan_many(data: np.ndarray, bounds: Sequence[Tuple[int, int]], min_offsets: Sequence[int],
-              threads: int = 16, buffer: Optional[PlanBuffer] = None, verify_crc: bool = True) -> FetchPlan:
+              threads: int = 16, buffer: Optional[PlanBuffer] = None, verify_crc: bool = False) -> FetchPlan:
     """Plan many record sets of one staging buffer (``data[lo:hi]`` each, one per partition fetch) with the sets
     walked in parallel native threads; the merged arrays land in ``buffer`` (pinned) for one H2D copy.
-    ``verify_crc`` checks every record batch's CRC-32C on the host (the consumer's ``check.crcs``, default true;
-    SSE4.2 ``crc32`` in host_kafka.cpp)."""
+    ``verify_crc`` checks every record batch's CRC-32C here on the host (SSE4.2 ``crc32`` in host_kafka.cpp);
+    by default the device decode verifies them (``DeviceRecordDecoder(verify_crc=True)``)."""
     L = _lib()
     if not hasattr(L, "_plan_many_bound"):
         p, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         L.dxa_kafka_plan_count.argtypes = [p, i64, p, p, p, i32, i32, p, p]
-        L.dxa_kafka_plan_fill.argtypes = [p, i64, p, p, p, i32, p] + [p] * 11
+        L.dxa_kafka_plan_fill.argtypes = [p, i64, p, p, p, i32, p] + [p] * 14
         L._plan_many_bound = True
     ns = len(bounds)
     so = np.array([b[0] for b in bounds], np.int64)
@@ -198,7 +212,7 @@ def plan_many(data: np.ndarray, bounds: Sequence[Tuple[int, int]], min_offsets: 
                                counts.ctypes.data, *[arrs[n].ctypes.data for n in
                                                      ("b_count", "b_base", "b_skip", "b_first", "b_nblk", "b_rec0",
                                                       "k_comp_off", "k_comp_len", "k_stored", "k_out_off",
-                                                      "k_cap")])
+                                                      "k_cap", "b_crc_off", "b_crc_len", "b_crc")])
     if rc:
         raise Unsupported(_PLAN_ERRS.get(rc, f"plan error {rc}"))
     np.subtract(arrs["b_count"], arrs["b_skip"], out=arrs["b_keep"])
@@ -233,7 +247,9 @@ def merge(plans: Sequence[Tuple[FetchPlan, int]]) -> FetchPlan:
         k_comp_len=cat("k_comp_len"), k_stored=cat("k_stored"),
         k_out_off=np.concatenate([p.k_out_off + o for (p, _), o in zip(plans, out0)]),
         k_cap=cat("k_cap"), out_bytes=ob, next_offset=plans[-1][0].next_offset,
-        nbytes=max(at + p.nbytes for p, at in plans))
+        nbytes=max(at + p.nbytes for p, at in plans),
+        b_crc_off=np.concatenate([p.b_crc_off + at for p, at in plans]), b_crc_len=cat("b_crc_len"),
+        b_crc=cat("b_crc"))
 
 
 def _rec0(p: FetchPlan) -> np.ndarray:
@@ -267,8 +283,10 @@ class DeviceRecordDecoder:
     ``chunks`` splits the H2D copy of the compressed bytes at block boundaries so chunk k's copy overlaps chunk
     k-1's decode (as ``lz4.ChunkedIngest``)."""
 
-    def __init__(self, device, chunks: int = 4, copy_stream=None, decode_stream=None, track: bool = True):
+    def __init__(self, device, chunks: int = 4, copy_stream=None, decode_stream=None, track: bool = True,
+                 verify_crc: bool = True):
         self.device = torch.device(device)
+        self.verify_crc = verify_crc          # CRC-32C of every batch on the device (check.crcs)
         self.chunks = max(1, chunks)
         self.copy_stream = copy_stream or torch.cuda.Stream(self.device)
         self.decode_stream = decode_stream or torch.cuda.Stream(self.device)
@@ -306,6 +324,7 @@ class DeviceRecordDecoder:
                  for (name, off, cnt), (_, dt, _k) in zip(layout, _ARRAYS)}
         tabs = [views[k] for k in ("k_comp_off", "k_comp_len", "k_stored", "k_out_off", "k_cap", "b_count",
                                    "b_skip", "b_keep", "b_first", "b_nblk", "b_rec0")]
+        crc_tabs = [views[k] for k in ("b_crc_off", "b_crc_len", "b_crc")]
         co, cl, sd, oo, cap, bc, bs, bk, bf, bn, br = tabs
         with torch.cuda.stream(self.decode_stream):
             out = torch.empty(plan.out_bytes + 64, dtype=torch.uint8, device=dev)
@@ -337,6 +356,8 @@ class DeviceRecordDecoder:
         N.call("dxa_kafka_records", N.ptr(out), plan.nbat, N.ptr(bc), N.ptr(bs), N.ptr(bk), N.ptr(bf), N.ptr(bn),
                N.ptr(br), N.ptr(oo), N.ptr(cap), N.ptr(produced), N.ptr(bstat), N.ptr(offs), N.ptr(ends),
                N.ptr(rstat), st)
+        if self.verify_crc:
+            N.call("dxa_kafka_crc", N.ptr(ddata), plan.nbat, *[N.ptr(t) for t in crc_tabs], N.ptr(rstat), st)
         with torch.cuda.stream(self.decode_stream):
             status = DecodeStatus((rstat[:plan.nbat] != 0).sum(), self.decode_stream)
         done = torch.cuda.Event()
@@ -381,12 +402,65 @@ class DecodeStatus:
         return int(self.host[0])
 
 
-def decode_on_host_like(staging: np.ndarray, plan: FetchPlan):
-    """CPU reference of ``DeviceRecordDecoder.decode`` (tests): (values buffer, starts, ends)."""
+_CRC_POLY = 0x82F63B78
+
+
+def _multmodp(a: int, b: int) -> int:
+    p = 0
+    m = 1 << 31
+    while m:
+        if a & m:
+            p ^= b
+        b = (b >> 1) ^ _CRC_POLY if b & 1 else b >> 1
+        m >>= 1
+    return p
+
+
+def _x2n_table():
+    t, p = [], 1 << 30
+    for _ in range(32):
+        t.append(p)
+        p = _multmodp(p, p)
+    return t
+
+
+_X2N = _x2n_table()
+
+
+def crc32c_segmented(data: bytes, lanes: int = 64) -> int:
+    """CPU mirror of ``kafka_crc_kernel``: per-lane segment CRCs (8-byte multiple segments) combined as
+    Σ x^(8·after_l)·crc_l in GF(2)[x]/P — equal to the serial CRC-32C of ``data``."""
+    from .kafka import crc32c
+    n = len(data)
+    seg = (((n + lanes - 1) // lanes) + 7) // 8 * 8
+    total = 0
+    for lane in range(lanes):
+        lo, hi = min(lane * seg, n), min(lane * seg + seg, n)
+        if hi <= lo:
+            continue
+        c = crc32c(data[lo:hi])
+        after, k, sc = n - hi, 3, 1 << 31
+        while after:
+            if after & 1:
+                sc = _multmodp(_X2N[k & 31], sc)
+            after >>= 1
+            k += 1
+        total ^= _multmodp(sc, c) if c else 0
+    return total
+
+
+def decode_on_host_like(staging: np.ndarray, plan: FetchPlan, verify_crc: bool = False):
+    """CPU reference of ``DeviceRecordDecoder.decode`` (tests): (values buffer, starts, ends).  ``verify_crc``
+    raises on a batch whose CRC-32C does not match (the device's status 7)."""
     from ..ops import lz4
     out = np.zeros(plan.out_bytes + 64, dtype=np.uint8)
     starts, ends = [], []
     for i in range(plan.nbat):
+        if verify_crc:
+            lo = int(plan.b_crc_off[i])
+            got = crc32c_segmented(staging[lo:lo + int(plan.b_crc_len[i])].tobytes())
+            if got != int(plan.b_crc[i]) & 0xFFFFFFFF:
+                raise DecodeError(f"batch {i}: CRC-32C mismatch")
         f, nb = int(plan.b_first[i]), int(plan.b_nblk[i])
         p = int(plan.k_out_off[f])
         end = p

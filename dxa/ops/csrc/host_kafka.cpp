@@ -267,6 +267,9 @@ struct Plan {
   bool write;
   int32_t* b_count; int64_t* b_base; int32_t* b_skip; int32_t* b_first; int32_t* b_nblk; int64_t* b_rec0;
   int64_t* k_comp_off; int32_t* k_comp_len; uint8_t* k_stored; int64_t* k_out_off; int64_t* k_cap;
+  // per batch: the CRC-covered range (attributes .. end, offset from the set start) and the stored CRC-32C, for the
+  // device-side check (kafka_crc_kernel); optional
+  int64_t* b_crc_off = nullptr; int32_t* b_crc_len = nullptr; int32_t* b_crc = nullptr;
   int64_t nbat = 0, nblk = 0, nrec = 0, out_bytes = 0;
   int32_t max_block = 0;
 };
@@ -335,6 +338,11 @@ int plan_batches(const uint8_t* data, int64_t len, int64_t min_offset, Plan& pl,
         pl.b_first[pl.nbat] = (int32_t)first;
         pl.b_nblk[pl.nbat] = (int32_t)(pl.nblk - first);
         pl.b_rec0[pl.nbat] = pl.nrec;
+        if (pl.b_crc_off) {
+          pl.b_crc_off[pl.nbat] = attrs_p - data;
+          pl.b_crc_len[pl.nbat] = (int32_t)(bend - attrs_p);
+          pl.b_crc[pl.nbat] = (int32_t)crc;
+        }
       }
       pl.nrec += count - skip;
       ++pl.nbat;
@@ -368,9 +376,10 @@ __attribute__((visibility("default"))) int dxa_kafka_plan(const uint8_t* data, i
                                                          int32_t* b_count, int64_t* b_base, int32_t* b_skip,
                                                          int32_t* b_first, int32_t* b_nblk, int64_t* b_rec0,
                                                          int64_t* k_comp_off, int32_t* k_comp_len, uint8_t* k_stored,
-                                                         int64_t* k_out_off, int64_t* k_cap) {
+                                                         int64_t* k_out_off, int64_t* k_cap, int64_t* b_crc_off,
+                                                         int32_t* b_crc_len, int32_t* b_crc) {
   Plan pl{b_count != nullptr, b_count, b_base, b_skip, b_first, b_nblk, b_rec0,
-          k_comp_off, k_comp_len, k_stored, k_out_off, k_cap};
+          k_comp_off, k_comp_len, k_stored, k_out_off, k_cap, b_crc_off, b_crc_len, b_crc};
   const int rc = plan_batches(data, len, min_offset, pl, next_offset, verify_crc);
   counts[0] = pl.nbat;
   counts[1] = pl.nblk;
@@ -503,7 +512,8 @@ __attribute__((visibility("default"))) int dxa_kafka_plan_fill(const uint8_t* da
                                                               int64_t* b_base, int32_t* b_skip, int32_t* b_first,
                                                               int32_t* b_nblk, int64_t* b_rec0, int64_t* k_comp_off,
                                                               int32_t* k_comp_len, uint8_t* k_stored,
-                                                              int64_t* k_out_off, int64_t* k_cap) {
+                                                              int64_t* k_out_off, int64_t* k_cap, int64_t* b_crc_off,
+                                                              int32_t* b_crc_len, int32_t* b_crc) {
   std::vector<int64_t> base((size_t)(4 * (nsets + 1)), 0);
   for (int64_t k = 0; k < nsets; ++k)
     for (int j = 0; j < 4; ++j) base[(size_t)(4 * (k + 1) + j)] = base[(size_t)(4 * k + j)] + set_counts[4 * k + j];
@@ -512,12 +522,14 @@ __attribute__((visibility("default"))) int dxa_kafka_plan_fill(const uint8_t* da
     const int64_t b0 = base[(size_t)(4 * k)], k0 = base[(size_t)(4 * k + 1)], r0 = base[(size_t)(4 * k + 2)],
                   o0 = base[(size_t)(4 * k + 3)];
     Plan pl{true, b_count + b0, b_base + b0, b_skip + b0, b_first + b0, b_nblk + b0, b_rec0 + b0,
-            k_comp_off + k0, k_comp_len + k0, k_stored + k0, k_out_off + k0, k_cap + k0};
+            k_comp_off + k0, k_comp_len + k0, k_stored + k0, k_out_off + k0, k_cap + k0,
+            b_crc_off ? b_crc_off + b0 : nullptr, b_crc_len ? b_crc_len + b0 : nullptr, b_crc ? b_crc + b0 : nullptr};
     int64_t nxt = 0;
     rcs[(size_t)k] = plan_batches(data + set_off[k], set_len[k], min_off[k], pl, &nxt, 0);
     for (int64_t i = 0; i < pl.nbat; ++i) {
       b_first[b0 + i] += (int32_t)k0;
       b_rec0[b0 + i] += r0;
+      if (b_crc_off) b_crc_off[b0 + i] += set_off[k];
     }
     for (int64_t i = 0; i < pl.nblk; ++i) {
       k_comp_off[k0 + i] += set_off[k];

@@ -136,6 +136,82 @@ __global__ __launch_bounds__(256) void kafka_records_kernel(
   bstatus[i] = rc;
 }
 
+
+// ---- CRC-32C of every record batch, on the device (the consumer's check.crcs) -------------------------------------
+// The CRC covers a batch from its attributes field to its end (~16 KiB for a 16 KiB producer batch), in the
+// compressed bytes already in HBM, so the host planner touches no record bytes at all (host CRC would read every
+// fetched byte once more from host memory — ~55 GB/s per GPU at the groupby rate, on top of the DMA's own reads).
+// One wave per batch: lane l takes the contiguous segment [l*seg, (l+1)*seg) and runs slice-by-8 table CRC over it
+// (tables in LDS); the 64 finalized segment CRCs are combined as crc(AB) = x^(8|B|)·crc(A) ⊕ crc(B) in GF(2)[x]/P
+// (reflected, zlib's multmodp/x2nmodp with the Castagnoli polynomial), i.e. each lane scales its CRC by
+// x^(8·bytes after its segment) and the wave XOR-reduces.  A mismatch sets the batch's status to 7.
+constexpr uint32_t kCrcPoly = 0x82F63B78u;
+
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 1
+  for (uint32_t m = 1u << 31; m; m >>= 1) {
+    if (a & m) p ^= b;
+    b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(256) void kafka_crc_kernel(const uint8_t* __restrict__ data, int64_t nbat,
+                                                        const int64_t* __restrict__ b_off,
+                                                        const int32_t* __restrict__ b_len,
+                                                        const int32_t* __restrict__ b_want,
+                                                        int32_t* __restrict__ bstatus) {
+  __shared__ uint32_t tab[8][256];
+  __shared__ uint32_t x2n[32];
+  const int tid = threadIdx.x;
+  {
+    uint32_t c = (uint32_t)tid;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+    tab[0][tid] = c;
+    for (int t = 1; t < 8; ++t) {
+      // tab[t][i] = (tab[t-1][i] >> 8) ^ tab[0][tab[t-1][i] & 0xff]: needs all of tab[0] first
+      __syncthreads();
+      tab[t][tid] = (tab[t - 1][tid] >> 8) ^ tab[0][tab[t - 1][tid] & 0xff];
+    }
+    if (tid < 32) {                                   // x^(2^k) mod P, reflected (x^1 = bit 30)
+      uint32_t p = 1u << 30;
+      for (int k = 0; k < tid; ++k) p = multmodp(p, p);
+      x2n[tid] = p;
+    }
+    __syncthreads();
+  }
+  const int lane = tid & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6); i < nbat; i += waves) {
+    const int64_t n = b_len[i];
+    const uint8_t* base = data + b_off[i];
+    const int64_t seg = (((n + 63) >> 6) + 7) & ~(int64_t)7;
+    const int64_t lo = lane * seg < n ? lane * seg : n;
+    const int64_t hi = lo + seg < n ? lo + seg : n;
+    uint32_t c = 0xFFFFFFFFu;
+    const uint8_t* q = base + lo;
+    const uint8_t* e = base + hi;
+    while (q < e && ((uintptr_t)q & 7)) c = (c >> 8) ^ tab[0][(c ^ *q++) & 0xff];
+    for (; q + 8 <= e; q += 8) {
+      const uint2 w = *reinterpret_cast<const uint2*>(q);
+      const uint32_t lo32 = w.x ^ c, hi32 = w.y;
+      c = tab[7][lo32 & 0xff] ^ tab[6][(lo32 >> 8) & 0xff] ^ tab[5][(lo32 >> 16) & 0xff] ^ tab[4][lo32 >> 24] ^
+          tab[3][hi32 & 0xff] ^ tab[2][(hi32 >> 8) & 0xff] ^ tab[1][(hi32 >> 16) & 0xff] ^ tab[0][hi32 >> 24];
+    }
+    while (q < e) c = (c >> 8) ^ tab[0][(c ^ *q++) & 0xff];
+    uint32_t crc = (hi > lo) ? ~c : 0u;               // CRC-32C of an empty segment is 0
+    // scale by x^(8 * bytes after this segment)
+    uint64_t after = (uint64_t)(n - hi);
+    uint32_t sc = 1u << 31;                            // x^0
+    for (int k = 3; after; after >>= 1, ++k)
+      if (after & 1) sc = multmodp(x2n[k & 31], sc);
+    uint32_t term = crc ? multmodp(sc, crc) : 0u;
+    for (int off = 32; off; off >>= 1) term ^= (uint32_t)__shfl_xor((int)term, off, 64);
+    if (lane == 0 && term != (uint32_t)b_want[i]) bstatus[i] = 7;
+  }
+}
+
 }  // namespace
 
 DXA_API int dxa_kafka_records(const uint8_t* buf, int64_t nbat, const int32_t* b_count, const int32_t* b_skip,
@@ -151,5 +227,16 @@ DXA_API int dxa_kafka_records(const uint8_t* buf, int64_t nbat, const int32_t* b
   hipLaunchKernelGGL(kafka_records_kernel, dim3((unsigned)((nbat + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      buf, nbat, b_count, b_skip, b_keep, b_first, b_nblk, b_rec0, k_out_off, k_cap, produced,
                      blk_status, starts, ends, bstatus);
+  return (int)hipGetLastError();
+}
+
+// Verify every planned batch's CRC-32C (after dxa_kafka_records on the same stream: a mismatch overrides the
+// batch's framing status with 7).
+DXA_API int dxa_kafka_crc(const uint8_t* data, int64_t nbat, const int64_t* b_off, const int32_t* b_len,
+                          const int32_t* b_want, int32_t* bstatus, void* stream) {
+  if (nbat <= 0) return 0;
+  const int64_t blocks = (nbat + 3) / 4;
+  hipLaunchKernelGGL(kafka_crc_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                     (hipStream_t)stream, data, nbat, b_off, b_len, b_want, bstatus);
   return (int)hipGetLastError();
 }

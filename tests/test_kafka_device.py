@@ -105,3 +105,51 @@ def test_plan_many_matches_merged_plans():
         assert np.array_equal(getattr(many, name), getattr(merged, name)), name
     buf, s, e = KD.decode_on_host_like(a, many)
     assert [buf[x:y].tobytes() for x, y in zip(s, e)] == vals[3:130] + vals[130:]
+
+
+def test_plan_carries_crc_ranges_and_segmented_crc_matches():
+    """The plan records each batch's CRC-covered range and stored CRC; the device's segmented combine
+    (mirrored on the CPU) reproduces the serial CRC-32C for every length, and a flipped byte fails the check."""
+    import random as R
+    for n in list(range(0, 70)) + [127, 128, 129, 511, 4095, 16384, 16391]:
+        b = bytes(R.Random(n).getrandbits(8) for _ in range(n))
+        assert KD.crc32c_segmented(b) == K.crc32c(b), n
+    vals = _values(200, seed=9)
+    rs = _record_set(vals, 37, "lz4") + _record_set(vals[:20], 20, "none", base=200)
+    plan = KD.plan_fetch(rs, 0)
+    a = np.frombuffer(rs, np.uint8)
+    for i in range(plan.nbat):
+        lo, ln = int(plan.b_crc_off[i]), int(plan.b_crc_len[i])
+        assert K.crc32c(rs[lo:lo + ln]) == int(plan.b_crc[i]) & 0xFFFFFFFF
+    buf, s, e = KD.decode_on_host_like(a, plan, verify_crc=True)
+    assert [buf[x:y].tobytes() for x, y in zip(s, e)] == vals + vals[:20]
+    bad = bytearray(rs)
+    bad[int(plan.b_crc_off[-1]) + 200] ^= 0x01            # inside the stored (codec none) batch's records
+    with pytest.raises(KD.DecodeError):
+        KD.decode_on_host_like(np.frombuffer(bytes(bad), np.uint8), KD.plan_fetch(bytes(bad), 0), verify_crc=True)
+    with pytest.raises(KD.Unsupported):
+        KD.plan_fetch(bytes(bad), 0, verify_crc=True)     # the host check catches it too
+    # offsets survive plan_many's set shifting
+    many = KD.plan_many(np.frombuffer(rs + rs, np.uint8), [(0, len(rs)), (len(rs), 2 * len(rs))], [0, 0], threads=2)
+    assert np.array_equal(many.b_crc_off[plan.nbat:], plan.b_crc_off + len(rs))
+
+
+@pytest.mark.gpu
+def test_device_crc_flags_corrupt_batch(gpu):
+    vals = _values(400, seed=11)
+    rs = bytearray(_record_set(vals, 50, "lz4") + _record_set(vals[:30], 30, "none", base=400))
+    plan = KD.plan_fetch(bytes(rs), 0)
+    staging = torch.zeros(len(rs) + 64, dtype=torch.uint8).pin_memory()
+    staging[:len(rs)] = torch.frombuffer(bytearray(rs), dtype=torch.uint8)
+    dec = KD.DeviceRecordDecoder(gpu)
+    raw, ev = dec.decode(staging, plan)
+    torch.cuda.current_stream(gpu).wait_event(ev)
+    assert raw.status.failed() == 0
+    dec.check()
+    rs[int(plan.b_crc_off[-1]) + 100] ^= 0x20                # corrupt a value byte of the stored batch
+    staging[:len(rs)] = torch.frombuffer(bytearray(rs), dtype=torch.uint8)
+    raw, ev = dec.decode(staging, KD.plan_fetch(bytes(rs), 0))
+    torch.cuda.current_stream(gpu).wait_event(ev)
+    assert raw.status.failed() == 1                          # framing is intact: only the CRC catches it
+    with pytest.raises(KD.DecodeError):
+        dec.check()
