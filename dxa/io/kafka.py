@@ -370,6 +370,14 @@ class KafkaClient:
         return self._conn(self.brokers[nid])
 
     def list_offset(self, topic: str, partition: int, when: int = LATEST) -> int:
+        """EARLIEST (-2), LATEST (-1), or a timestamp in ms → the first offset whose record timestamp is at or after
+        it (the end of the log when there is none: the broker answers -1)."""
+        off = self._list_offset(topic, partition, when)
+        if off < 0 and when >= 0:
+            return self._list_offset(topic, partition, LATEST)
+        return off
+
+    def _list_offset(self, topic: str, partition: int, when: int) -> int:
         body = _W().i32(-1).array([topic], lambda w, t: w.str(t).array(
             [partition], lambda w2, p: w2.i32(p).i64(when))).b
         r = self._leader(topic, partition).request(API_LIST_OFFSETS, 1, bytes(body))
@@ -403,8 +411,8 @@ class KafkaClient:
         return b"", offset
 
     def produce(self, topic: str, partition: int, values: Sequence[bytes], acks: int = 1,
-                compression: str = "none") -> int:
-        batch = encode_batch(values, compression=compression)
+                compression: str = "none", timestamp_ms: Optional[int] = None) -> int:
+        batch = encode_batch(values, timestamp_ms, compression=compression)
         body = _W().str(None).i16(acks).i32(30000).array(
             [topic], lambda w, t: w.str(t).array([partition], lambda w2, p: w2.i32(p).bytes(batch))).b
         r = self._leader(topic, partition).request(API_PRODUCE, 3, bytes(body))
@@ -577,6 +585,23 @@ def _raw_from_parts(vals_list, offs_list, device) -> RawBatch:
     return RawBatch(tb, to, n, source_bytes=total)
 
 
+def start_position(start_enqueue_time: Optional[str], auto_offset_reset: Optional[str] = None,
+                   now_ms: Optional[int] = None) -> int:
+    """The reference's starting position (EventHubStreamingFactory.scala:47-64; KafkaInputSetting.scala:91):
+    ``startenqueuetime`` unset → ``autooffsetreset`` (default "latest": end of stream); 0 → start of stream;
+    < 0 → now + that many seconds; > 0 → that epoch second.  Returns EARLIEST / LATEST or a timestamp in ms, which
+    ``KafkaClient.list_offset`` resolves per partition (ListOffsets by timestamp: the first record at or after it)."""
+    import time as _time
+    if start_enqueue_time not in (None, ""):
+        v = int(str(start_enqueue_time).strip())
+        if v == 0:
+            return EARLIEST
+        if v < 0:
+            return (int(_time.time() * 1000) if now_ms is None else now_ms) + v * 1000
+        return v * 1000
+    return EARLIEST if (auto_offset_reset or "latest").strip().lower() == "earliest" else LATEST
+
+
 def build_kafka_source(inp, device, kind: str, rank: int = 0, world: int = 1) -> KafkaSource:
     """From ``datax.job.input.default.{kafka|eventhub}.*`` settings."""
     from ..config.secrets import resolve
@@ -599,5 +624,6 @@ def build_kafka_source(inp, device, kind: str, rank: int = 0, world: int = 1) ->
         rate = inp.get("kafka.maxrate")
         flush = (inp.get("kafka.flushexistingcheckpoints") or "false").lower() == "true"
     crcs = (inp.get(f"{kind}.checkcrcs") or "true").lower() != "false"
-    return KafkaSource(client, topics, device, ckpt, int(rate) if rate else None,
+    start = start_position(inp.get(f"{kind}.startenqueuetime"), inp.get(f"{kind}.autooffsetreset"))
+    return KafkaSource(client, topics, device, ckpt, int(rate) if rate else None, start=start,
                        flush_existing=flush, rank=rank, world=world, verify_crc=crcs)

@@ -287,6 +287,9 @@ class DeviceRecordDecoder:
                  verify_crc: bool = True):
         self.device = torch.device(device)
         self.verify_crc = verify_crc          # CRC-32C of every batch on the device (check.crcs)
+        # the CRC check runs on its own stream, concurrently with the LZ4 decode (which is latency-bound and leaves
+        # CUs idle); only the batch's status waits for it, never the consumer of the decoded records
+        self.crc_stream = torch.cuda.Stream(self.device) if verify_crc else None
         self.chunks = max(1, chunks)
         self.copy_stream = copy_stream or torch.cuda.Stream(self.device)
         self.decode_stream = decode_stream or torch.cuda.Stream(self.device)
@@ -337,16 +340,20 @@ class DeviceRecordDecoder:
         st = self.decode_stream.cuda_stream
         nb = plan.nblk
         bounds = np.linspace(0, nb, self.chunks + 1).astype(np.int64)
-        for k in range(self.chunks):
+        ev_last = tab_ev
+        copied = 0                 # staging bytes already sent: chunks are contiguous from byte 0 (the batch headers
+        for k in range(self.chunks):       # between blocks travel too — the device CRC check reads them)
             b0, b1 = int(bounds[k]), int(bounds[k + 1])
             if b1 <= b0:
                 continue
-            lo = 0 if k == 0 else int(plan.k_comp_off[b0])
+            lo = copied
             hi = plan.nbytes if b1 == nb else int(plan.k_comp_off[b1])
+            copied = hi
             N.call("dxa_memcpy_h2d_async", ddata.data_ptr() + lo, staging.data_ptr() + lo, hi - lo,
                    self.copy_stream.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
+            ev_last = ev
             self.decode_stream.wait_event(ev)
             N.call("dxa_lz4_decode_into", N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
                    N.ptr(oo[b0:b1]), N.ptr(cap[b0:b1]), b1 - b0, N.ptr(out), N.ptr(produced[b0:b1]),
@@ -356,19 +363,31 @@ class DeviceRecordDecoder:
         N.call("dxa_kafka_records", N.ptr(out), plan.nbat, N.ptr(bc), N.ptr(bs), N.ptr(bk), N.ptr(bf), N.ptr(bn),
                N.ptr(br), N.ptr(oo), N.ptr(cap), N.ptr(produced), N.ptr(bstat), N.ptr(offs), N.ptr(ends),
                N.ptr(rstat), st)
-        if self.verify_crc:
-            N.call("dxa_kafka_crc", N.ptr(ddata), plan.nbat, *[N.ptr(t) for t in crc_tabs], N.ptr(rstat), st)
-        with torch.cuda.stream(self.decode_stream):
-            status = DecodeStatus((rstat[:plan.nbat] != 0).sum(), self.decode_stream)
         done = torch.cuda.Event()
         done.record(self.decode_stream)
+        if self.verify_crc:
+            cs = self.crc_stream
+            cs.wait_event(ev_last)                       # every staging byte is in HBM
+            with torch.cuda.stream(cs):
+                cstat = torch.empty(max(1, plan.nbat), dtype=torch.int32, device=dev)
+            N.call("dxa_kafka_crc", N.ptr(ddata), plan.nbat, *[N.ptr(t) for t in crc_tabs], N.ptr(cstat),
+                   cs.cuda_stream)
+            cs.wait_event(done)
+            with torch.cuda.stream(cs):
+                bad = (rstat[:plan.nbat] != 0).sum() + (cstat[:plan.nbat] != 0).sum()
+                status = DecodeStatus(bad, cs)
+            for t in (ddata, dtab, rstat):
+                t.record_stream(cs)
+        else:
+            with torch.cuda.stream(self.decode_stream):
+                status = DecodeStatus((rstat[:plan.nbat] != 0).sum(), self.decode_stream)
         for t in (ddata, produced, bstat, dtab):
             t.record_stream(self.decode_stream)
         if self.track:
             self.checks.append(status)
         # the pinned bytes (record sets and plan tables) must outlive their async copies
         self._inflight = [(e, b) for e, b in getattr(self, "_inflight", []) if not e.query()] + \
-            [(done, (staging, packed))]
+            [(status.event if self.verify_crc else done, (staging, packed))]
         return RawBatch(out, offs, n, ends=ends[:n], source_bytes=plan.nbytes, status=status), done
 
     def check(self):

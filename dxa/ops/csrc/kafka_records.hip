@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256) void kafka_records_kernel(
 // One wave per batch: lane l takes the contiguous segment [l*seg, (l+1)*seg) and runs slice-by-8 table CRC over it
 // (tables in LDS); the 64 finalized segment CRCs are combined as crc(AB) = x^(8|B|)·crc(A) ⊕ crc(B) in GF(2)[x]/P
 // (reflected, zlib's multmodp/x2nmodp with the Castagnoli polynomial), i.e. each lane scales its CRC by
-// x^(8·bytes after its segment) and the wave XOR-reduces.  A mismatch sets the batch's status to 7.
+// x^(8·bytes after its segment) and the wave XOR-reduces.  Writes 7 (mismatch) or 0 per batch into its own status
+// array, so the check runs on a side stream concurrently with the LZ4 decode and record framing.
 constexpr uint32_t kCrcPoly = 0x82F63B78u;
 
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void kafka_crc_kernel(const uint8_t* __restric
       if (after & 1) sc = multmodp(x2n[k & 31], sc);
     uint32_t term = crc ? multmodp(sc, crc) : 0u;
     for (int off = 32; off; off >>= 1) term ^= (uint32_t)__shfl_xor((int)term, off, 64);
-    if (lane == 0 && term != (uint32_t)b_want[i]) bstatus[i] = 7;
+    if (lane == 0) bstatus[i] = term != (uint32_t)b_want[i] ? 7 : 0;
   }
 }
 
@@ -230,8 +231,7 @@ DXA_API int dxa_kafka_records(const uint8_t* buf, int64_t nbat, const int32_t* b
   return (int)hipGetLastError();
 }
 
-// Verify every planned batch's CRC-32C (after dxa_kafka_records on the same stream: a mismatch overrides the
-// batch's framing status with 7).
+// Verify every planned batch's CRC-32C: cstatus[i] = 7 on a mismatch, 0 otherwise.
 DXA_API int dxa_kafka_crc(const uint8_t* data, int64_t nbat, const int64_t* b_off, const int32_t* b_len,
                           const int32_t* b_want, int32_t* bstatus, void* stream) {
   if (nbat <= 0) return 0;

@@ -87,7 +87,11 @@ class FakeBroker:
             out += struct.pack(">i", n)
             for _ in range(n):
                 p, ts = r.i32(), r.i64()
-                off = 0 if ts == -2 else self.next[(t, p)]
+                if ts >= 0:                                   # by timestamp: first batch whose max timestamp >= ts
+                    off = next((base for base, _last, raw in self.logs[(t, p)]
+                                if struct.unpack_from(">q", raw, 35)[0] >= ts), -1)
+                else:
+                    off = 0 if ts == -2 else self.next[(t, p)]
                 out += struct.pack(">ihqq", p, 0, -1, off)
             return bytes(out), authed
         if api == 1:

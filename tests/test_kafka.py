@@ -172,8 +172,11 @@ def test_build_source_from_settings(broker, tmp_path):
     d = SettingDictionary({"datax.job.input.default.kafka.bootstrapservers": f"127.0.0.1:{broker.port}",
                            "datax.job.input.default.kafka.topics": "iot",
                            "datax.job.input.default.kafka.checkpointdir": str(tmp_path / "k")})
-    src = build_source(d, "cpu")
-    assert isinstance(src, K.KafkaSource) and src.next_batch(0).n == 6
+    src = build_source(d, "cpu")                  # auto.offset.reset defaults to latest, as the reference
+    assert isinstance(src, K.KafkaSource) and src.next_batch(0).n == 0
+    d = SettingDictionary(dict(d.dict, **{"datax.job.input.default.kafka.autooffsetreset": "earliest",
+                                          "datax.job.input.default.kafka.checkpointdir": str(tmp_path / "k2")}))
+    assert build_source(d, "cpu").next_batch(0).n == 6
 
 
 @pytest.mark.gpu
@@ -272,3 +275,20 @@ def test_kafka_device_decode_failure_is_reported(broker):
     assert raw.status.failed() > 0
     with pytest.raises(KD.DecodeError):
         dec.check()
+
+
+def test_start_position_from_enqueue_time(broker):
+    """startenqueuetime (EventHubStreamingFactory.scala:47-64): 0 → start, >0 → epoch seconds, <0 → now-relative,
+    unset → autooffsetreset (latest by default); resolved with ListOffsets by timestamp."""
+    assert K.start_position("0") == K.EARLIEST and K.start_position(None) == K.LATEST
+    assert K.start_position(None, "earliest") == K.EARLIEST
+    assert K.start_position("1700000000") == 1_700_000_000_000
+    assert K.start_position("-60", now_ms=10_000_000) == 10_000_000 - 60_000
+    c = K.KafkaClient(f"127.0.0.1:{broker.port}")
+    for k, ts in enumerate((1_000_000, 2_000_000, 3_000_000)):
+        c.produce("iot", 0, [json.dumps({"k": k, "i": i}).encode() for i in range(5)], timestamp_ms=ts)
+    assert c.list_offset("iot", 0, 2_000_000) == 5
+    assert c.list_offset("iot", 0, 2_500_000) == 10
+    assert c.list_offset("iot", 0, 9_000_000) == 15            # past the end: the log end
+    src = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", start=K.start_position("2000"))
+    assert src.fetch_pos[("iot", 0)] == 5 and src.next_batch(0).n == 10
