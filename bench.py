@@ -92,8 +92,9 @@ def main():
                     "parallel on the host, as per-partition fetch threads would)")
     ap.add_argument("--kafka-batch-records", type=int, default=26,
                     help="kafka: records per producer batch (26 SimulatedData events = ~16 KiB, one LZ4 block)")
-    ap.add_argument("--no-crc", action="store_true",
-                    help="kafka: skip the CRC-32C check of record batches (consumer check.crcs=false)")
+    ap.add_argument("--crc", choices=["host", "device", "off"], default="host",
+                    help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): host planner "
+                         "threads (default), the GPU (kafka_crc_kernel), or not at all")
     ap.add_argument("--sink", choices=["null", "blob"], default="null",
                     help="output sink: null (rendered JSON lands in host memory) or blob (gzip files under /tmp)")
     ap.add_argument("--profile-stages", action="store_true")
@@ -229,10 +230,11 @@ def main():
 
         def make_plan(i):
             b = kafka_parts[i % len(pool)]
-            return KD.plan_many(pool[i % len(pool)].numpy(), b, [0] * len(b), threads=16, buffer=plan_bufs.get())
+            return KD.plan_many(pool[i % len(pool)].numpy(), b, [0] * len(b), threads=16, buffer=plan_bufs.get(),
+                                verify_crc=args.crc == "host")
         if on_gpu:
             kdec = KD.DeviceRecordDecoder(device, chunks=args.lz4_chunks, copy_stream=side,
-                                          verify_crc=not args.no_crc)
+                                          verify_crc=args.crc == "device")
     staged = {}
     sizes = []
     framing_checks = []        # device flags: a frame's newline count differed from its producer's record count
@@ -442,7 +444,8 @@ def main():
                    if source == "pinned-lz4" else
                    "; delivered as Kafka v2 record batches with the LZ4 codec in pinned host memory (a "
                    "multi-partition Fetch), planned on the host, "
-                   + ("CRC-32C-verified (check.crcs), " if not args.no_crc else "") +
+                   + ({"host": "CRC-32C-verified on the host (check.crcs), ",
+                       "device": "CRC-32C-verified on the GPU (check.crcs), "}.get(args.crc, "")) +
                    "decompressed and record-framed on the GPU in every step)" if source == "kafka" else ")"),
         "config": {"model": MODEL[flow].format(ref=args.ref_rows), "flow": flow,
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
@@ -467,7 +470,7 @@ def main():
     if source == "kafka":
         out["config"]["kafka_partitions"] = args.kafka_partitions
         out["config"]["kafka_batch_records"] = args.kafka_batch_records
-        out["config"]["check_crcs"] = not args.no_crc
+        out["config"]["check_crcs"] = args.crc
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
         out["latency_trace_ms"] = [round(x * 1e3, 2) for x in lat]

@@ -436,9 +436,12 @@ class KafkaSource(OffsetTrackedSource):
     def __init__(self, client: KafkaClient, topics: List[str], device, checkpoint_dir: Optional[str] = None,
                  max_rate: Optional[int] = None, start: int = EARLIEST, flush_existing: bool = False,
                  rank: int = 0, world: int = 1, max_fetches: int = 64, device_decode: Optional[bool] = None,
-                 verify_crc: bool = True):
+                 check_crcs="host"):
         self.client = client
-        self.verify_crc = verify_crc          # consumer check.crcs (default true)
+        # consumer check.crcs: "host" (default; the planner / host decoder checks), "device" (kafka_crc_kernel on
+        # the GPU ingest path), or off (False / "false")
+        self.check_crcs = {True: "host", False: "off", "true": "host", "false": "off"}.get(check_crcs, check_crcs)
+        self.verify_crc = self.check_crcs != "off"
         self._status: Dict[int, object] = {}
         self.topics = topics
         self.device = torch.device(device)
@@ -480,7 +483,7 @@ class KafkaSource(OffsetTrackedSource):
                 if not recs:
                     break
                 try:
-                    plan = KD.plan_fetch(recs, cur)                # CRCs are checked on the device
+                    plan = KD.plan_fetch(recs, cur, self.check_crcs == "host")
                 except KD.Unsupported:
                     return None
                 if self.max_rate is not None:
@@ -500,7 +503,8 @@ class KafkaSource(OffsetTrackedSource):
         for recs, (_, at) in zip(sets, plans):
             sn[at:at + len(recs)] = np.frombuffer(recs, dtype=np.uint8)
         if self._decoder is None:
-            self._decoder = KD.DeviceRecordDecoder(self.device, track=False, verify_crc=self.verify_crc)
+            self._decoder = KD.DeviceRecordDecoder(self.device, track=False,
+                                                   verify_crc=self.check_crcs == "device")
         raw, done = self._decoder.decode(staging, KD.merge(plans))
         cur_stream = torch.cuda.current_stream(self.device)
         cur_stream.wait_event(done)
@@ -623,7 +627,7 @@ def build_kafka_source(inp, device, kind: str, rank: int = 0, world: int = 1) ->
         ckpt = inp.get("kafka.checkpointdir")
         rate = inp.get("kafka.maxrate")
         flush = (inp.get("kafka.flushexistingcheckpoints") or "false").lower() == "true"
-    crcs = (inp.get(f"{kind}.checkcrcs") or "true").lower() != "false"
+    crcs = (inp.get(f"{kind}.checkcrcs") or "true").lower()          # true (host) | device | false
     start = start_position(inp.get(f"{kind}.startenqueuetime"), inp.get(f"{kind}.autooffsetreset"))
     return KafkaSource(client, topics, device, ckpt, int(rate) if rate else None, start=start,
-                       flush_existing=flush, rank=rank, world=world, verify_crc=crcs)
+                       flush_existing=flush, rank=rank, world=world, check_crcs=crcs)

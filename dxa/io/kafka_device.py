@@ -10,10 +10,12 @@ device.
 
 Batches the GPU path does not take (gzip / snappy / zstd codecs, dependent-block LZ4 frames, compacted batches
 with offset gaps) make ``plan_fetch`` raise ``Unsupported``; the source then decodes that fetch on the host.
-CRC-32C (the consumer's ``check.crcs``, on by default) is verified on the GPU over the compressed bytes already in
-HBM (``kafka_crc_kernel``: one wave per batch, 64 segment CRCs combined in GF(2)), so the host planner reads only
-headers; a mismatch fails the batch's status like a decode error.  ``plan_*(verify_crc=True)`` checks on the host
-instead (the host decoder's path).
+CRC-32C (the consumer's ``check.crcs``, on by default) is verified by the host planner (SSE4.2 ``crc32``, ~8 GB/s
+per planner thread) or, with ``DeviceRecordDecoder(verify_crc=True)``, on the GPU over the compressed bytes already
+in HBM (``kafka_crc_kernel``: one wave per batch, lane-interleaved words combined in GF(2)).  Measured on MI355X
+(profiles/crc/README.md): the GPU check takes ~0.6 ms per 441 MB batch but steals LDS and CU time from the LZ4
+decode, which is the pipeline's critical path, costing ~20 % of the groupby rate, while the host check is free at
+one GPU — so the host is the default and the device check is the option for CPU-starved hosts.
 """
 from __future__ import annotations
 
@@ -97,9 +99,9 @@ class FetchPlan:
         return self.b_base + self.b_skip + self.b_keep - 1
 
 
-def plan_fetch(data, min_offset: int, verify_crc: bool = False) -> FetchPlan:
+def plan_fetch(data, min_offset: int, verify_crc: bool = True) -> FetchPlan:
     """Plan one Fetch record set (bytes / uint8 ndarray) → FetchPlan (offsets relative to ``data``).
-    ``verify_crc``: check CRCs here on the host (the default leaves them to the device decode)."""
+    ``verify_crc``: check every batch's CRC-32C here on the host (False: left to the device, or not checked)."""
     a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     L = _lib()
     counts = np.zeros(5, dtype=np.int64)
@@ -183,11 +185,11 @@ class PlanBufferPool:
 
 
 def plan_many(data: np.ndarray, bounds: Sequence[Tuple[int, int]], min_offsets: Sequence[int],
-              threads: int = 16, buffer: Optional[PlanBuffer] = None, verify_crc: bool = False) -> FetchPlan:
+              threads: int = 16, buffer: Optional[PlanBuffer] = None, verify_crc: bool = True) -> FetchPlan:
     """Plan many record sets of one staging buffer (``data[lo:hi]`` each, one per partition fetch) with the sets
     walked in parallel native threads; the merged arrays land in ``buffer`` (pinned) for one H2D copy.
-    ``verify_crc`` checks every record batch's CRC-32C here on the host (SSE4.2 ``crc32`` in host_kafka.cpp);
-    by default the device decode verifies them (``DeviceRecordDecoder(verify_crc=True)``)."""
+    ``verify_crc`` checks every record batch's CRC-32C here on the host (SSE4.2 ``crc32`` in host_kafka.cpp, in the
+    planner threads); False leaves it to the device decode (``DeviceRecordDecoder(verify_crc=True)``) or skips it."""
     L = _lib()
     if not hasattr(L, "_plan_many_bound"):
         p, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
@@ -284,7 +286,7 @@ class DeviceRecordDecoder:
     k-1's decode (as ``lz4.ChunkedIngest``)."""
 
     def __init__(self, device, chunks: int = 4, copy_stream=None, decode_stream=None, track: bool = True,
-                 verify_crc: bool = True):
+                 verify_crc: bool = False):
         self.device = torch.device(device)
         self.verify_crc = verify_crc          # CRC-32C of every batch on the device (check.crcs)
         # the CRC check runs on its own stream, concurrently with the LZ4 decode (which is latency-bound and leaves
@@ -446,26 +448,58 @@ def _x2n_table():
 _X2N = _x2n_table()
 
 
-def crc32c_segmented(data: bytes, lanes: int = 64) -> int:
-    """CPU mirror of ``kafka_crc_kernel``: per-lane segment CRCs (8-byte multiple segments) combined as
-    Σ x^(8·after_l)·crc_l in GF(2)[x]/P — equal to the serial CRC-32C of ``data``."""
-    from .kafka import crc32c
+def _raw_crc(reg: int, data: bytes) -> int:
+    for byte in data:
+        reg ^= byte
+        for _ in range(8):
+            reg = (reg >> 1) ^ _CRC_POLY if reg & 1 else reg >> 1
+    return reg
+
+
+def _x8n(n: int) -> int:
+    p, sq = 1 << 31, 1 << 30
+    for _ in range(3):
+        sq = _multmodp(sq, sq)
+    while n:
+        if n & 1:
+            p = _multmodp(sq, p)
+        sq = _multmodp(sq, sq)
+        n >>= 1
+    return p
+
+
+def crc32c_segmented(data: bytes, base_align: int = 0) -> int:
+    """CPU mirror of ``kafka_crc_kernel``: 512-B rows right-aligned on the 8-B boundary at or below the end (the data
+    starts ``base_align`` bytes past an 8-B boundary), lane l accumulating the 8-B word at l*8 of every row with the
+    zero-init register (acc = T8(acc ^ w), then ·x^(8·504) between rows), the init folded into the first 4 bytes,
+    bytes before the start as zeros, lane results scaled by x^(64·(63-l)) and XORed, the tail folded serially —
+    equal to the serial CRC-32C of ``data`` (≥ 4 bytes)."""
     n = len(data)
-    seg = (((n + lanes - 1) // lanes) + 7) // 8 * 8
+    e = base_align + n                         # positions relative to the 8-B aligned origin
+    E = e - (e & 7)
+    if E - base_align < 8:                     # tiny: all serial
+        return ~_raw_crc(0xFFFFFFFF, data) & 0xFFFFFFFF
+    nrow = (E - base_align + 511) // 512
+    r0 = E - nrow * 512
+    msg = bytearray(data)
+    for q in range(min(4, n)):
+        msg[q] ^= 0xFF
+
+    def byte_at(pos):
+        q = pos - base_align
+        return msg[q] if 0 <= q < n else 0
     total = 0
-    for lane in range(lanes):
-        lo, hi = min(lane * seg, n), min(lane * seg + seg, n)
-        if hi <= lo:
-            continue
-        c = crc32c(data[lo:hi])
-        after, k, sc = n - hi, 3, 1 << 31
-        while after:
-            if after & 1:
-                sc = _multmodp(_X2N[k & 31], sc)
-            after >>= 1
-            k += 1
-        total ^= _multmodp(sc, c) if c else 0
-    return total
+    for lane in range(64):
+        acc = 0
+        for r in range(nrow):
+            a = r0 + r * 512 + lane * 8
+            acc = _raw_crc(acc, bytes(byte_at(a + k) for k in range(8)))
+            if r + 1 < nrow:
+                acc = _multmodp(_x8n(504), acc)
+        if acc:
+            total ^= _multmodp(_x8n((63 - lane) * 8), acc)
+    reg = _raw_crc(total, bytes(msg[E - base_align:]))
+    return ~reg & 0xFFFFFFFF
 
 
 def decode_on_host_like(staging: np.ndarray, plan: FetchPlan, verify_crc: bool = False):
@@ -477,7 +511,7 @@ def decode_on_host_like(staging: np.ndarray, plan: FetchPlan, verify_crc: bool =
     for i in range(plan.nbat):
         if verify_crc:
             lo = int(plan.b_crc_off[i])
-            got = crc32c_segmented(staging[lo:lo + int(plan.b_crc_len[i])].tobytes())
+            got = crc32c_segmented(staging[lo:lo + int(plan.b_crc_len[i])].tobytes(), lo & 7)
             if got != int(plan.b_crc[i]) & 0xFFFFFFFF:
                 raise DecodeError(f"batch {i}: CRC-32C mismatch")
         f, nb = int(plan.b_first[i]), int(plan.b_nblk[i])

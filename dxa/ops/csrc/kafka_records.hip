@@ -138,14 +138,19 @@ __global__ __launch_bounds__(256) void kafka_records_kernel(
 
 
 // ---- CRC-32C of every record batch, on the device (the consumer's check.crcs) -------------------------------------
-// The CRC covers a batch from its attributes field to its end (~16 KiB for a 16 KiB producer batch), in the
-// compressed bytes already in HBM, so the host planner touches no record bytes at all (host CRC would read every
-// fetched byte once more from host memory — ~55 GB/s per GPU at the groupby rate, on top of the DMA's own reads).
-// One wave per batch: lane l takes the contiguous segment [l*seg, (l+1)*seg) and runs slice-by-8 table CRC over it
-// (tables in LDS); the 64 finalized segment CRCs are combined as crc(AB) = x^(8|B|)·crc(A) ⊕ crc(B) in GF(2)[x]/P
-// (reflected, zlib's multmodp/x2nmodp with the Castagnoli polynomial), i.e. each lane scales its CRC by
-// x^(8·bytes after its segment) and the wave XOR-reduces.  Writes 7 (mismatch) or 0 per batch into its own status
-// array, so the check runs on a side stream concurrently with the LZ4 decode and record framing.
+// The CRC covers a batch from its attributes field to its end (~16 KiB for a 16 KiB producer batch), over the
+// compressed bytes already in HBM, so the host planner touches no record bytes (a host CRC would read every fetched
+// byte once more from host memory — ~55 GB/s per GPU at the groupby rate, on top of the DMA's own reads).
+//
+// One wave per batch, lane-interleaved: the bytes are cut into 512-B rows right-aligned on the 8-B boundary at or
+// below the batch end, and lane l owns the 8-B word at l*8 of every row — one coalesced 512-B load per row.  The
+// zero-init ("raw") CRC register is linear in the message, so each lane accumulates its words as if every other
+// byte were zero: acc = T8(acc ^ w) (slice-by-8: "process 8 bytes") then acc = acc·x^(8·504) (the 504 zero bytes
+// of the other lanes, a 4-table constant multiply).  After the last row lane l is still (63-l)·8 bytes from the
+// end: acc·x^(64·(63-l)) (per-lane constant, precomputed), XOR-reduced over the wave.  The 0xFFFFFFFF init is
+// folded into the message (XOR into its first 4 bytes); bytes before the batch start load as zero (no effect on a
+// zero-init register); lane 0 finishes the < 8-B tail serially and inverts.  LDS holds only the tables (12 KiB), so
+// the check shares CUs with the LZ4 decode it runs beside (side stream).  Writes 7 (mismatch) or 0 per batch.
 constexpr uint32_t kCrcPoly = 0x82F63B78u;
 
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
@@ -158,58 +163,74 @@ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
   return p;
 }
 
+// x^(8n) mod P (reflected) by square-and-multiply from x^1
+__device__ uint32_t x8n(uint64_t n) {
+  uint32_t p = 1u << 31, sq = 1u << 30;         // x^0, x^1
+  for (int q = 0; q < 3; ++q) sq = multmodp(sq, sq);
+  for (; n; n >>= 1) {
+    if (n & 1) p = multmodp(sq, p);
+    sq = multmodp(sq, sq);
+  }
+  return p;
+}
+
 __global__ __launch_bounds__(256) void kafka_crc_kernel(const uint8_t* __restrict__ data, int64_t nbat,
                                                         const int64_t* __restrict__ b_off,
                                                         const int32_t* __restrict__ b_len,
                                                         const int32_t* __restrict__ b_want,
                                                         int32_t* __restrict__ bstatus) {
-  __shared__ uint32_t tab[8][256];
-  __shared__ uint32_t x2n[32];
-  const int tid = threadIdx.x;
+  __shared__ uint32_t t8[8][256];          // slice-by-8
+  __shared__ uint32_t m504[4][256];        // multiply by x^(8*504)
+  const int tid = threadIdx.x, lane = tid & 63;
   {
     uint32_t c = (uint32_t)tid;
     for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
-    tab[0][tid] = c;
+    t8[0][tid] = c;
+    const uint32_t k504 = x8n(504);
+    for (int j = 0; j < 4; ++j) m504[j][tid] = multmodp(k504, (uint32_t)tid << (8 * j));
     for (int t = 1; t < 8; ++t) {
-      // tab[t][i] = (tab[t-1][i] >> 8) ^ tab[0][tab[t-1][i] & 0xff]: needs all of tab[0] first
       __syncthreads();
-      tab[t][tid] = (tab[t - 1][tid] >> 8) ^ tab[0][tab[t - 1][tid] & 0xff];
-    }
-    if (tid < 32) {                                   // x^(2^k) mod P, reflected (x^1 = bit 30)
-      uint32_t p = 1u << 30;
-      for (int k = 0; k < tid; ++k) p = multmodp(p, p);
-      x2n[tid] = p;
+      t8[t][tid] = (t8[t - 1][tid] >> 8) ^ t8[0][t8[t - 1][tid] & 0xff];
     }
     __syncthreads();
   }
-  const int lane = tid & 63;
+  const uint32_t kend = x8n((uint64_t)(63 - lane) * 8);   // this lane's distance to the end of a row
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6); i < nbat; i += waves) {
-    const int64_t n = b_len[i];
-    const uint8_t* base = data + b_off[i];
-    const int64_t seg = (((n + 63) >> 6) + 7) & ~(int64_t)7;
-    const int64_t lo = lane * seg < n ? lane * seg : n;
-    const int64_t hi = lo + seg < n ? lo + seg : n;
-    uint32_t c = 0xFFFFFFFFu;
-    const uint8_t* q = base + lo;
-    const uint8_t* e = base + hi;
-    while (q < e && ((uintptr_t)q & 7)) c = (c >> 8) ^ tab[0][(c ^ *q++) & 0xff];
-    for (; q + 8 <= e; q += 8) {
-      const uint2 w = *reinterpret_cast<const uint2*>(q);
-      const uint32_t lo32 = w.x ^ c, hi32 = w.y;
-      c = tab[7][lo32 & 0xff] ^ tab[6][(lo32 >> 8) & 0xff] ^ tab[5][(lo32 >> 16) & 0xff] ^ tab[4][lo32 >> 24] ^
-          tab[3][hi32 & 0xff] ^ tab[2][(hi32 >> 8) & 0xff] ^ tab[1][(hi32 >> 16) & 0xff] ^ tab[0][hi32 >> 24];
+    const int64_t s = b_off[i], e = s + b_len[i];
+    int64_t E = e - (int64_t)(reinterpret_cast<uintptr_t>(data + e) & 7);          // 8-B aligned end
+    if (E - s < 8) E = s;                                      // tiny batch: all serial (init not folded)
+    const int64_t nrow = (E - s + 511) / 512;
+    const int64_t r0 = E - nrow * 512;                         // 8-B aligned; row 0 may start before s
+    uint32_t acc = 0;
+    for (int64_t r = 0; r < nrow; ++r) {
+      const int64_t a = r0 + r * 512 + lane * 8;
+      uint64_t w = 0;
+      if (a + 8 > s) {
+        w = *reinterpret_cast<const uint64_t*>(data + a);
+        if (a < s + 4) {                                       // zero bytes before s, XOR the init into s..s+3
+          const int64_t lo = s - a;                            // may be negative
+          const uint64_t keep = lo > 0 ? (~0ull << (8 * lo)) : ~0ull;
+          const int64_t x0 = lo > 0 ? lo : 0, x1 = lo + 4 < 8 ? lo + 4 : 8;
+          uint64_t inv = 0;
+          for (int64_t q = x0; q < x1; ++q) inv |= 0xffull << (8 * q);
+          w = (w & keep) ^ inv;
+        }
+      }
+      acc = (uint32_t)(acc ^ (uint32_t)w);
+      const uint32_t hi = (uint32_t)(w >> 32);
+      acc = t8[7][acc & 0xff] ^ t8[6][(acc >> 8) & 0xff] ^ t8[5][(acc >> 16) & 0xff] ^ t8[4][acc >> 24] ^
+            t8[3][hi & 0xff] ^ t8[2][(hi >> 8) & 0xff] ^ t8[1][(hi >> 16) & 0xff] ^ t8[0][hi >> 24];
+      if (r + 1 < nrow)
+        acc = m504[0][acc & 0xff] ^ m504[1][(acc >> 8) & 0xff] ^ m504[2][(acc >> 16) & 0xff] ^ m504[3][acc >> 24];
     }
-    while (q < e) c = (c >> 8) ^ tab[0][(c ^ *q++) & 0xff];
-    uint32_t crc = (hi > lo) ? ~c : 0u;               // CRC-32C of an empty segment is 0
-    // scale by x^(8 * bytes after this segment)
-    uint64_t after = (uint64_t)(n - hi);
-    uint32_t sc = 1u << 31;                            // x^0
-    for (int k = 3; after; after >>= 1, ++k)
-      if (after & 1) sc = multmodp(x2n[k & 31], sc);
-    uint32_t term = crc ? multmodp(sc, crc) : 0u;
+    uint32_t term = acc ? multmodp(kend, acc) : 0u;
     for (int off = 32; off; off >>= 1) term ^= (uint32_t)__shfl_xor((int)term, off, 64);
-    if (lane == 0) bstatus[i] = term != (uint32_t)b_want[i] ? 7 : 0;
+    if (lane == 0) {
+      uint32_t c = E > s ? term : 0xFFFFFFFFu;                 // raw register after [s, E); continue the tail
+      for (int64_t p = E; p < e; ++p) c = (c >> 8) ^ t8[0][(c ^ data[p]) & 0xff];
+      bstatus[i] = ~c != (uint32_t)b_want[i] ? 7 : 0;
+    }
   }
 }
 
@@ -235,8 +256,9 @@ DXA_API int dxa_kafka_records(const uint8_t* buf, int64_t nbat, const int32_t* b
 DXA_API int dxa_kafka_crc(const uint8_t* data, int64_t nbat, const int64_t* b_off, const int32_t* b_len,
                           const int32_t* b_want, int32_t* bstatus, void* stream) {
   if (nbat <= 0) return 0;
+  // grid-strided over the batches, 4 waves (one batch each) per workgroup; tables built once per workgroup
   const int64_t blocks = (nbat + 3) / 4;
-  hipLaunchKernelGGL(kafka_crc_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+  hipLaunchKernelGGL(kafka_crc_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0,
                      (hipStream_t)stream, data, nbat, b_off, b_len, b_want, bstatus);
   return (int)hipGetLastError();
 }

@@ -198,7 +198,8 @@ def test_kafka_source_device_decode_matches_host(broker, tmp_path, compression):
     got = {}
     for mode in ("device", "host"):
         src = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cuda:0", str(tmp_path / mode),
-                            max_rate=70, device_decode=(mode == "device"))
+                            max_rate=70, device_decode=(mode == "device"),
+                            check_crcs="device" if mode == "device" else "host")
         rows = []
         for bt in (1, 2, 3):
             raw = src.next_batch(bt * 1_000_000)

@@ -1,6 +1,8 @@
 # groupby bench with / without the device CRC check (A/B, twice each), and a kernel-stats profile
 set -o pipefail
 mkdir -p gpurun_out/crc
+timeout -k 10 300 python -u -m pytest tests/test_kafka_device.py tests/test_kafka.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/crc/tests.log 2>&1 || { tail -30 gpurun_out/crc/tests.log; exit 1; }
+tail -1 gpurun_out/crc/tests.log
 R=$GRAFT_REPO_ROOT
 for rep in 1 2; do
   for v in crc nocrc; do
