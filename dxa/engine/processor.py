@@ -131,15 +131,22 @@ class Processor:
 
     # ------------------------------------------------------------------------------------------------------------
     def _load_reference_data(self) -> Dict[str, Table]:
+        """``datax.job.input.default.referencedata.<name>.{path,format,delimiter,header}`` (ReferenceDataHandler.scala:
+        42-60) → resident device tables; ``schema`` (DDL) types columns at load (an extension: Spark reads strings).
+        Load statistics land in ``reference_stats``."""
         out = {}
+        self.reference_stats: Dict[str, Dict[str, float]] = {}
         for name, sub in self.settings.group_by_sub_namespace(S.INPUT_PREFIX + "referencedata.").items():
             fmt = (sub.get("format") or "csv").lower()
             path = resolve(sub.get_string("path"))
             if fmt not in ("csv", "tsv"):
                 raise ValueError(f"unsupported reference data format {fmt}")
             from ..io.refdata import load_csv
+            stats: Dict[str, float] = {}
             out[name] = load_csv(path, sub.get("delimiter") or ("\t" if fmt == "tsv" else ","),
-                                 (sub.get("header") or "true").lower() == "true", self.device)
+                                 (sub.get("header") or "true").lower() == "true", self.device,
+                                 schema=sub.get("schema"), stats=stats)
+            self.reference_stats[name] = stats
         return out
 
     def _needed_raw_paths(self):

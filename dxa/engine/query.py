@@ -329,14 +329,23 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         ri = torch.arange(n_r, device=dev).repeat(n_l)
     else:
         lk = [materialize(evaluate(e, left, ctx)) for e in lkeys]
-        rk = [materialize(evaluate(e, right, ctx)) for e in rkeys]
-        lk, rk = _coerce_keys(lk, rk)
         built = None
         static = _static_table(j.right, catalog)
         if static is not None and kind in ("inner", "left", "semi", "anti") and rdist == P.REPLICATED:
-            # stream–static join: the reference table's hash table is built once and reused every batch
-            ck = (static[0], id(static[1]), tuple(e.key() for e in rkeys), tuple(c.dtype for c in rk))
-            built = catalog.cached_build(ck, lambda: (static[1], J.build_side(rk)))[1]
+            # stream–static join: the reference table's keys are evaluated and coerced, and its hash table built,
+            # ONCE — every later batch only evaluates and coerces its own (stream) side
+            ck = (static[0], id(static[1]), tuple(e.key() for e in rkeys), tuple(c.dtype for c in lk))
+
+            def build():
+                rk0 = [materialize(evaluate(e, right, ctx)) for e in rkeys]
+                types = [_join_key_type(a.dtype, b.dtype) for a, b in zip(lk, rk0)]
+                rk1 = [b if b.dtype == t else cast_column(b, t) for b, t in zip(rk0, types)]
+                return static[1], types, rk1, J.build_side(rk1)
+            _t, types, rk, built = catalog.cached_build(ck, build)
+            lk = [a if a.dtype == t else cast_column(a, t) for a, t in zip(lk, types)]
+        else:
+            rk = [materialize(evaluate(e, right, ctx)) for e in rkeys]
+            lk, rk = _coerce_keys(lk, rk)
         if residual and kind != "inner":
             # non-equi ON terms of an outer / semi / anti join decide which pairs *match*: filter the equi pairs
             # first, then add the unmatched rows of the preserved side(s)
@@ -425,11 +434,22 @@ def _gather_scope(scope: Scope) -> Scope:
     return out
 
 
+def _join_key_type(a, b):
+    """Type both sides of an equi-join key are compared in.  Spark 2.4's PromoteStrings casts a string compared with
+    a numeric / boolean value to the other side's type (so ``3 = '003'`` holds); otherwise the widest common type."""
+    if a != b:
+        if a == "string" and b in ("long", "int", "double", "boolean", "decimal"):
+            return "double" if b == "decimal" else b
+        if b == "string" and a in ("long", "int", "double", "boolean", "decimal"):
+            return "double" if a == "decimal" else a
+    return common_type(a, b)
+
+
 def _coerce_keys(lk, rk):
     lo, ro = [], []
     for a, b in zip(lk, rk):
         if a.dtype != b.dtype:
-            t = common_type(a.dtype, b.dtype)
+            t = _join_key_type(a.dtype, b.dtype)
             a = cast_column(a, t) if a.dtype != t else a
             b = cast_column(b, t) if b.dtype != t else b
         lo.append(a)

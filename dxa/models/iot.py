@@ -265,6 +265,15 @@ def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Opti
     paths = {"schema": os.path.join(workdir, "inputschema.json"),
              "projection": os.path.join(workdir, "projection.txt"),
              "transform": os.path.join(workdir, f"{name}-combined.txt")}
+    if variant == "join":
+        # the 100M-row reference table goes through the real referencedata path: a CSV file, loaded on the device
+        # (rank 0 reads, RCCL broadcast, line framing + tokenizer kernels); written once per size
+        ref_csv = os.path.join(os.path.dirname(workdir.rstrip("/")) or workdir, f"dxa_refdevices_{ref_rows}.csv")
+        extra = dict(extra or {})
+        extra.setdefault("datax.job.input.default.referencedata.RefDevices.path", ref_csv)
+        extra.setdefault("datax.job.input.default.referencedata.RefDevices.format", "csv")
+        extra.setdefault("datax.job.input.default.referencedata.RefDevices.header", "true")
+        extra.setdefault("datax.job.input.default.referencedata.RefDevices.schema", REF_SCHEMA)
     outputs = {"groupby": ["DeviceSummary", "HotDeviceAlerts"], "window": ["DeviceWindow", "HotDeviceAlerts"],
                "join": ["ZoneSummary"], "full": ["DeviceNamed", "DeviceState"], "passthrough": ["Tagged"]}[variant]
     d = {
@@ -330,6 +339,56 @@ def flow_settings(workdir: Optional[str] = None, sink: str = "null", extra: Opti
     if extra:
         d.update(extra)
     return SettingDictionary(d)
+
+
+REF_SCHEMA = "refKey long, zone long, tier string"
+_TIERS = (b"bronze", b"silver", b"gold", b"platinum")
+
+
+def write_reference_csv(path: str, n_rows: int, device) -> int:
+    """The device-registry reference data as a CSV file (``refKey,zone,tier`` with a header): the same rows as
+    ``reference_table`` (shuffled keys 0..n-1, zone = hash % 1000, one of 4 tiers), rendered on the device in one
+    pass and written once.  Returns the file size."""
+    device = torch.device(device)
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    keys = torch.randperm(n_rows, generator=g).to(device) if n_rows <= 4_000_000 else _device_perm(n_rows, device)
+    zone = (keys * 2654435761) % 1000
+    tier = keys % 4
+
+    def digits(x, width):
+        d = torch.empty((x.shape[0], width), dtype=torch.uint8, device=device)
+        v = x.clone()
+        for k in range(width - 1, -1, -1):
+            d[:, k] = (v % 10).to(torch.uint8) + 48
+            v //= 10
+        nd = torch.ones_like(x)
+        t = x // 10
+        for _ in range(width - 1):
+            nd += (t > 0).to(nd.dtype)
+            t //= 10
+        keep = torch.arange(width, device=device).unsqueeze(0) >= (width - nd).unsqueeze(1)
+        return d, keep
+    kd, kk = digits(keys, max(1, len(str(max(n_rows - 1, 0)))))
+    zd, zk = digits(zone, 3)
+    tw = max(len(t) for t in _TIERS)
+    tab = torch.zeros((4, tw), dtype=torch.uint8)
+    tmask = torch.zeros((4, tw), dtype=torch.bool)
+    for i, t in enumerate(_TIERS):
+        tab[i, :len(t)] = torch.tensor(list(t), dtype=torch.uint8)
+        tmask[i, :len(t)] = True
+    td, tk = tab.to(device)[tier], tmask.to(device)[tier]
+    n = keys.shape[0]
+    comma = torch.full((n, 1), 44, dtype=torch.uint8, device=device)
+    nl = torch.full((n, 1), 10, dtype=torch.uint8, device=device)
+    ones = torch.ones((n, 1), dtype=torch.bool, device=device)
+    body = torch.cat([kd, comma, zd, comma, td, nl], 1)
+    keep = torch.cat([kk, ones, zk, ones, tk, ones], 1)
+    data = body[keep].cpu().numpy()
+    del body, keep, kd, kk, zd, zk, td, tk
+    with open(path, "wb") as f:
+        f.write(b"refKey,zone,tier\n")
+        data.tofile(f)
+    return 17 + int(data.size)
 
 
 def reference_table(n_rows: int, device):

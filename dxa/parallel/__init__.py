@@ -71,5 +71,5 @@ def set_dist(table, d: str):
     return table
 
 
-from .exchange import (all_reduce_sum, allgather_table, broadcast_table, rebalance_table,  # noqa: E402
-                       shuffle_table, split_by_destination)
+from .exchange import (all_reduce_sum, allgather_table, broadcast_bytes, broadcast_table,  # noqa: E402
+                       broadcast_tensor, rebalance_table, shuffle_table, split_by_destination)

@@ -264,6 +264,45 @@ def shuffle_table(table, dest: torch.Tensor):
     return out
 
 
+def _broadcast(t: torch.Tensor, src: int) -> None:
+    if _staged(t):
+        h = t.cpu()
+        dist.broadcast(h, src=src, group=_g())
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src=src, group=_g())
+
+
+def broadcast_bytes(data: bytes, src: int = 0) -> bytes:
+    """``data`` from rank ``src`` on every rank: one broadcast of the length, one of the bytes (a device buffer over
+    RCCL when the ranks own GPUs — xGMI moves it; host memory over gloo)."""
+    from . import _DEVICE, _RANK
+    dev = _DEVICE if (_DEVICE is not None and dist.get_backend(_g()) != "gloo") else torch.device("cpu")
+    n = torch.tensor([len(data) if _RANK == src else 0], dtype=torch.int64, device=dev)
+    _broadcast(n, src)
+    size = int(n.item())
+    if _RANK == src:
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if size else \
+            torch.empty(0, dtype=torch.uint8, device=dev)
+    else:
+        buf = torch.empty(size, dtype=torch.uint8, device=dev)
+    if size:
+        _broadcast(buf, src)
+    return data if _RANK == src else buf.cpu().numpy().tobytes()
+
+
+def broadcast_tensor(t: Optional[torch.Tensor], src: int = 0, dtype=torch.uint8, device=None) -> torch.Tensor:
+    """A 1-D tensor from rank ``src`` on every rank (others pass None): length, then data — two collectives."""
+    from . import _RANK
+    dev = torch.device(device) if device is not None else (t.device if t is not None else torch.device("cpu"))
+    n = torch.tensor([t.numel() if _RANK == src else 0], dtype=torch.int64, device=dev)
+    _broadcast(n, src)
+    out = t.contiguous() if _RANK == src else torch.empty(int(n.item()), dtype=dtype, device=dev)
+    if out.numel():
+        _broadcast(out, src)
+    return out
+
+
 def allgather_table(table):
     """Every rank receives the concatenation of all ranks' rows (rank order)."""
     from ..engine.column import Table
@@ -276,18 +315,106 @@ def allgather_table(table):
     return shuffle_table(table.take(idx), dest)
 
 
+def _pack(table):
+    """Flatten a table for a collective: (spec, leaves, [n, C] int64 matrix, {leaf: compacted string bytes})."""
+    from ..ops import strings as sops
+    device = table.device
+    n = table.length
+    leaves: List[_Leaf] = []
+    spec: list = []
+    for c in table.columns:
+        _flatten(c, leaves, spec)
+    mats, nvalid = [], 0
+    strs = {}
+    for li, lf in enumerate(leaves):
+        c = lf.col
+        if lf.kind == "prim":
+            d = c.data
+            d = d.view(torch.int64) if d.dtype == torch.float64 else (d if d.dtype == torch.int64 else d.to(torch.int64))
+            lf.mcol = len(mats)
+            mats.append(d)
+        elif lf.kind == "str":
+            lf.mcol = len(mats)
+            mats.append(c.lens.to(torch.int64))
+            total = int(c.lens.to(torch.int64).sum().item()) if n else 0
+            strs[li] = sops.compact_known(c, total).arena[:total].contiguous() if n else \
+                torch.empty(0, dtype=torch.uint8, device=device)
+        if c.valid is not None:
+            lf.vbit = nvalid
+            nvalid += 1
+    masks = [torch.zeros(n, dtype=torch.int64, device=device) for _ in range((nvalid + 62) // 63)]
+    for lf in leaves:
+        if lf.vbit >= 0:
+            w, b = divmod(lf.vbit, 63)
+            masks[w] |= lf.col.valid.to(torch.int64) << b
+    cols = mats + masks
+    mat = torch.stack(cols, 1).contiguous() if (cols and n) else torch.empty((n, len(cols)), dtype=torch.int64,
+                                                                              device=device)
+    return spec, leaves, mat, strs, len(mats)
+
+
+def _leaf_meta(leaves):
+    """Picklable per-leaf layout (what a receiver needs to rebuild columns it has never seen)."""
+    return [(lf.kind, lf.dtype, lf.mcol, lf.vbit, lf.torch_dtype,
+             type(lf.col) if lf.kind == "str" else None, getattr(lf.col, "dtype", None)) for lf in leaves]
+
+
+def _unpack(table_names, spec, meta, mat, strs, nmats, device):
+    from ..engine.column import PrimColumn, Table
+    n = int(mat.shape[0])
+    out = {}
+    for li, (kind, dtype, mcol, vbit, tdt, scls, cdt) in enumerate(meta):
+        valid = None
+        if vbit >= 0:
+            w, b = divmod(vbit, 63)
+            valid = ((mat[:, nmats + w] >> b) & 1).to(torch.bool)
+        if kind == "prim":
+            d = mat[:, mcol].contiguous()
+            if tdt == torch.float64:
+                d = d.view(torch.float64)
+            elif tdt == torch.bool:
+                d = d.to(torch.bool)
+            elif tdt is not None and tdt != torch.int64:
+                d = d.to(tdt)
+            out[li] = PrimColumn(dtype, d, valid)
+        elif kind == "str":
+            lens = mat[:, mcol]
+            starts = torch.cumsum(lens, 0) - lens
+            arena = torch.zeros(int(strs[li].shape[0]) + 16, dtype=torch.uint8, device=device)
+            arena[:strs[li].shape[0]] = strs[li]
+            out[li] = scls(arena, starts, lens.to(torch.int32), valid, cdt)
+        else:
+            out[li] = valid
+    return Table(table_names, [_rebuild(sp, out, n, device) for sp in spec], n, device)
+
+
 def broadcast_table(table, src: int = 0):
+    """Rank ``src``'s table on every rank (the others pass any table with the same column names, e.g. empty): the
+    layout travels as one small object broadcast, the data as one broadcast of the packed [rows × C] int64 matrix
+    plus one per string leaf's bytes — the source sends each byte once (ncclBroadcast's pipelined ring/tree over
+    xGMI), never W copies."""
     from . import _RANK
     W = _w()
     if W <= 1:
         return table
+    device = table.device
     if _RANK == src:
-        n = table.length
-        idx = torch.arange(n, device=table.device).repeat(W)
-        dest = torch.arange(W, device=table.device).repeat_interleave(n)
-        return shuffle_table(table.take(idx), dest)
-    empty = table.take(torch.empty(0, dtype=torch.int64, device=table.device))
-    return shuffle_table(empty, torch.empty(0, dtype=torch.int64, device=table.device))
+        spec, leaves, mat, strs, nmats = _pack(table)
+        layout = [spec, _leaf_meta(leaves), nmats, int(mat.shape[0]), int(mat.shape[1]), sorted(strs)]
+    else:
+        layout, mat, strs = [None] * 6, None, {}
+    obj = [layout]
+    dist.broadcast_object_list(obj, src=src, group=_g())
+    spec, meta, nmats, rows, C, str_ids = obj[0]
+    flat = broadcast_tensor(mat.reshape(-1) if _RANK == src else None, src, torch.int64, device)
+    mat = flat.reshape(rows, C)
+    got = {li: broadcast_tensor(strs[li] if _RANK == src else None, src, torch.uint8, device) for li in str_ids}
+    out = _unpack(table.names, spec, meta, mat, got, nmats, device)
+    out.dist = P_REPLICATED
+    return out
+
+
+P_REPLICATED = "replicated"
 
 
 def rebalance_table(table):

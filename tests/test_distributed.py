@@ -237,3 +237,46 @@ def test_kfd_topology_maps_hip_index_to_pci_folder(tmp_path, monkeypatch):
     assert kfd_pci_path(2, str(topo), str(pci)) is None
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
     assert kfd_pci_path(0, str(topo), str(pci)).endswith("0000:75:00.0")
+
+
+def _bcast_worker(rank, world, port, q, path):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from dxa import parallel as P
+        from dxa.engine.column import Table
+        from dxa.engine.types import StructField, StructType
+        from dxa.io.refdata import load_csv
+        P.init(dist.group.WORLD, "cpu")
+        schema = StructType((StructField("k", "long"), StructField("s", "string"), StructField("v", "double")))
+        rows = _rows(3, 50) if rank == 0 else []
+        t = P.broadcast_table(Table.from_pylist(rows, schema))
+        ref = load_csv(path, ",", True, "cpu")
+        q.put((rank, (t.to_pylist(), ref.to_pylist()), None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_broadcast_table_and_reference_data(tmp_path):
+    """Rank 0's table / reference file reaches every rank through broadcasts (no per-rank file reads)."""
+    path = tmp_path / "ref.csv"
+    path.write_text('id,name\n1,"a,b"\n2,\n')
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q, str(path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, r, err = q.get(timeout=240)
+        assert err is None, err
+        res[rank] = r
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert _canon(res[r][0]) == _canon(_rows(3, 50))
+        assert res[r][1] == [{"id": "1", "name": "a,b"}, {"id": "2", "name": None}]
