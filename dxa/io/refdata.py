@@ -81,6 +81,8 @@ def load_csv(path: str, delimiter: str = ",", header: bool = True, device="cpu",
     device = torch.device(device)
     t0 = time.perf_counter()
     data = read_shared(path, device)
+    if data.startswith(b"\xef\xbb\xbf"):                   # UTF-8 BOM (files saved by Excel / .NET)
+        data = data[3:]
     t_read = time.perf_counter() - t0
     if device.type == "cuda":
         table = _load_device(data, delimiter, header, device, quote, escape)
