@@ -345,15 +345,22 @@ REF_SCHEMA = "refKey long, zone long, tier string"
 _TIERS = (b"bronze", b"silver", b"gold", b"platinum")
 
 
-def write_reference_csv(path: str, n_rows: int, device) -> int:
+def write_reference_csv(path: str, n_rows: int, device, chunk: int = 1 << 23) -> int:
     """The device-registry reference data as a CSV file (``refKey,zone,tier`` with a header): the same rows as
-    ``reference_table`` (shuffled keys 0..n-1, zone = hash % 1000, one of 4 tiers), rendered on the device in one
-    pass and written once.  Returns the file size."""
+    ``reference_table`` (shuffled keys 0..n-1, zone = hash % 1000, one of 4 tiers), rendered on the device 8 M rows
+    at a time and written once.  Returns the file size."""
     device = torch.device(device)
     g = torch.Generator(device="cpu").manual_seed(1234)
-    keys = torch.randperm(n_rows, generator=g).to(device) if n_rows <= 4_000_000 else _device_perm(n_rows, device)
-    zone = (keys * 2654435761) % 1000
-    tier = keys % 4
+    keys_all = torch.randperm(n_rows, generator=g).to(device) if n_rows <= 4_000_000 else \
+        _device_perm(n_rows, device)
+    kw = max(1, len(str(max(n_rows - 1, 0))))
+    tw = max(len(t) for t in _TIERS)
+    tab = torch.zeros((4, tw), dtype=torch.uint8)
+    tmask = torch.zeros((4, tw), dtype=torch.bool)
+    for i, t in enumerate(_TIERS):
+        tab[i, :len(t)] = torch.tensor(list(t), dtype=torch.uint8)
+        tmask[i, :len(t)] = True
+    tab, tmask = tab.to(device), tmask.to(device)
 
     def digits(x, width):
         d = torch.empty((x.shape[0], width), dtype=torch.uint8, device=device)
@@ -368,27 +375,26 @@ def write_reference_csv(path: str, n_rows: int, device) -> int:
             t //= 10
         keep = torch.arange(width, device=device).unsqueeze(0) >= (width - nd).unsqueeze(1)
         return d, keep
-    kd, kk = digits(keys, max(1, len(str(max(n_rows - 1, 0)))))
-    zd, zk = digits(zone, 3)
-    tw = max(len(t) for t in _TIERS)
-    tab = torch.zeros((4, tw), dtype=torch.uint8)
-    tmask = torch.zeros((4, tw), dtype=torch.bool)
-    for i, t in enumerate(_TIERS):
-        tab[i, :len(t)] = torch.tensor(list(t), dtype=torch.uint8)
-        tmask[i, :len(t)] = True
-    td, tk = tab.to(device)[tier], tmask.to(device)[tier]
-    n = keys.shape[0]
-    comma = torch.full((n, 1), 44, dtype=torch.uint8, device=device)
-    nl = torch.full((n, 1), 10, dtype=torch.uint8, device=device)
-    ones = torch.ones((n, 1), dtype=torch.bool, device=device)
-    body = torch.cat([kd, comma, zd, comma, td, nl], 1)
-    keep = torch.cat([kk, ones, zk, ones, tk, ones], 1)
-    data = body[keep].cpu().numpy()
-    del body, keep, kd, kk, zd, zk, td, tk
+    size = 0
     with open(path, "wb") as f:
-        f.write(b"refKey,zone,tier\n")
-        data.tofile(f)
-    return 17 + int(data.size)
+        head = b"refKey,zone,tier\n"
+        f.write(head)
+        size += len(head)
+        for lo in range(0, n_rows, chunk):
+            keys = keys_all[lo:lo + chunk]
+            n = keys.shape[0]
+            zone, tier = (keys * 2654435761) % 1000, keys % 4
+            kd, kk = digits(keys, kw)
+            zd, zk = digits(zone, 3)
+            comma = torch.full((n, 1), 44, dtype=torch.uint8, device=device)
+            nl = torch.full((n, 1), 10, dtype=torch.uint8, device=device)
+            ones = torch.ones((n, 1), dtype=torch.bool, device=device)
+            body = torch.cat([kd, comma, zd, comma, tab[tier], nl], 1)
+            keep = torch.cat([kk, ones, zk, ones, tmask[tier], ones], 1)
+            data = body[keep].cpu().numpy()
+            data.tofile(f)
+            size += int(data.size)
+    return size
 
 
 def reference_table(n_rows: int, device):

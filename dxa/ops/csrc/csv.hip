@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void csv_tokenize_kernel(uint8_t* __restrict__
         if (c == escape && escape != quote && q + 1 < end) {
           const uint32_t nx = w.at(q + 1);
           if (nx == quote || nx == escape) {
-            if (out != q) buf[out] = (uint8_t)nx;
+            buf[out] = (uint8_t)nx;
             rewrite = true;
             ++out;
             q += 2;
