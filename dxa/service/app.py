@@ -323,9 +323,31 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         return st.kernels.get(body["kernelId"]).execute(body.get("query", ""))
 
     # -- schema inference / samples ----------------------------------------------------------------------------------
+    def _sample(body) -> Optional[List[str]]:
+        """Sample the flow's configured input (``inputType`` / ``inputMode`` of the InteractiveQueryObject) for
+        ``seconds``, save the sample file (SchemaGenerator.SaveSample) and keep the raw events for LiveQuery."""
+        from .sampler import SampleError, sample_input, save_sample
+        if not (body.get("inputType") or (body.get("inputMode") or "").lower() == "batching"):
+            return None
+        try:
+            sampled = sample_input(body)
+        except SampleError as e:
+            raise HTTPException(status_code=400, detail=str(e))
+        if not sampled:
+            raise HTTPException(status_code=400, detail="Can't capture any data from the data source.")
+        name = body.get("name") or body.get("displayName") or "flow"
+        save_sample(os.path.join(st.root, "samples"), name, body.get("userName") or "", sampled)
+        return [e["Raw"] for e in sampled]
+
     @route("inputdata/inferschema")
     def infer(body):
-        events = body.get("events") or st.samples.get(body.get("name"), [])
+        """SchemaInferenceManager.GetInputSchema: sample the configured input (or take posted ``events``), union-merge
+        the JSON shapes into a Spark StructType."""
+        events = body.get("events")
+        if not events:
+            events = _sample(body)
+        if not events:
+            events = st.samples.get(body.get("name"), [])
         if not events and body.get("name") in st.queues:
             events = st.queues[body.get("name")][:1000]
         res = infer_schema(events)
@@ -335,7 +357,8 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
 
     @route("inputdata/refreshsample")
     def refresh_sample(body):
-        st.samples[body["name"]] = [e if isinstance(e, str) else json.dumps(e) for e in body.get("events") or []]
+        events = body.get("events") or _sample(body) or []
+        st.samples[body["name"]] = [e if isinstance(e, str) else json.dumps(e) for e in events]
         return len(st.samples[body["name"]])
 
     @route("inputdata/refreshsampleandkernel")
