@@ -128,6 +128,7 @@ class Processor:
         self._inflight: Optional[_InFlight] = None
         self.completed: List = []
         self.on_batch_complete = None
+        self.clock: Callable[[], float] = time.time     # current_timestamp() of a batch (tests pin it)
 
     # ------------------------------------------------------------------------------------------------------------
     def _load_reference_data(self) -> Dict[str, Table]:
@@ -421,7 +422,7 @@ class Processor:
         ``Latency-Process`` measured to output completion) arrive through ``on_batch_complete`` / ``completed``
         when the next batch (or ``drain()``) completes it."""
         t0 = time.perf_counter()
-        ctx = EvalContext(now_us=int(time.time() * 1e6), udfs=self.udfs, udafs=self.udafs, device=self.device)
+        ctx = EvalContext(now_us=int(self.clock() * 1e6), udfs=self.udfs, udafs=self.udafs, device=self.device)
         for refresh in self.udf_refreshers:
             refresh(batch_time_us)
         try:

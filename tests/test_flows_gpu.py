@@ -49,6 +49,7 @@ def _run(variant, device, batches, workdir):
     proc = Processor(_settings(variant, workdir), device)
     per_batch = []
     for bt, buf, offs in batches:
+        proc.clock = lambda bt=bt: bt / 1e6 + 0.25         # current_timestamp() (alert EventTime) pinned per batch
         raw = RawBatch(buf.clone().to(device), offs.clone().to(device), N_EVENTS)
         proc.process_batch(raw, bt, INTERVAL_US)
         proc.drain()
@@ -56,16 +57,6 @@ def _run(variant, device, batches, workdir):
         sinks.MEMORY_SINKS.clear()
     state = {n: st.active.to_pylist() for n, st in proc.state_tables.items()}
     return per_batch, state
-
-
-def _norm(v):
-    if isinstance(v, float):
-        return ("f", v)
-    if isinstance(v, dict):
-        return {k: _norm(x) for k, x in v.items()}
-    if isinstance(v, list):
-        return [_norm(x) for x in v]
-    return v
 
 
 def _key(row):
