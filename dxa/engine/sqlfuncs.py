@@ -722,24 +722,78 @@ def _hash_bytes(b: bytes, seed):
 
 
 def spark_hash_value(v, dtype, seed):
+    """One argument of Spark's hash() (Murmur3Hash, HashExpression): int/date/boolean → hashInt, long/timestamp →
+    hashLong, float → hashInt(floatToIntBits), double → hashLong(doubleToLongBits) (-0.0 as 0.0, NaN canonical),
+    decimal → hashLong(unscaled) for ≤ 18 digits else the unscaled BigInteger's two's-complement bytes.  Decimal
+    precision/scale are not tracked by this engine: the scale is the value's shortest exact decimal form."""
+    import math
+    import struct
     if v is None:
         return seed
     if dtype in ("int", "date") or isinstance(v, bool):
         return _hash_int(int(v), seed)
     if dtype in ("long", "timestamp"):
         return _hash_long(int(v), seed)
-    if dtype in ("double", "float", "decimal"):
-        import struct
+    if dtype == "float":
+        f = struct.unpack("<f", struct.pack("<f", float(v)))[0]
+        bits = 0x7FC00000 if math.isnan(f) else struct.unpack("<I", struct.pack("<f", 0.0 if f == 0 else f))[0]
+        return _hash_int(bits, seed)
+    if dtype == "double":
         d = 0.0 if v == 0 else float(v)                                   # -0.0 hashes as 0.0
-        return _hash_long(struct.unpack("<q", struct.pack("<d", d))[0], seed)
+        bits = 0x7FF8000000000000 if math.isnan(d) else struct.unpack("<Q", struct.pack("<d", d))[0]
+        return _hash_long(bits, seed)
+    if dtype == "decimal":
+        from decimal import Decimal
+        sign, digits, exp = Decimal(repr(float(v))).normalize().as_tuple()
+        unscaled = int("".join(map(str, digits)) or "0") * (10 ** exp if exp > 0 else 1) * (-1 if sign else 1)
+        if abs(unscaled) < 10 ** 18:
+            return _hash_long(unscaled, seed)
+        nbytes = (unscaled.bit_length() + 8) // 8
+        return _hash_bytes(unscaled.to_bytes(nbytes, "big", signed=True), seed)
     if isinstance(v, (dict, list)):
         v = json.dumps(v, separators=(",", ":"))
     return _hash_bytes(str(v).encode("utf-8"), seed)
 
 
+_HASH_KIND = {"int": 0, "date": 0, "long": 1, "timestamp": 1, "double": 2, "float": 3, "boolean": 4}
+
+
+def _hash_device(args, n, dev):
+    """hash() on the device (spark_hash.hip): one launch per argument folding into an int32 per-row state; None
+    when an argument type needs the host path (decimal, nested)."""
+    from ..ops import native as N
+    from .column import StrColumn, materialize
+    cols = []
+    for a in args:
+        a = materialize(a) if isinstance(a, ConstColumn) else a
+        if isinstance(a, StrColumn):
+            cols.append(("s", a))
+        elif isinstance(a, PrimColumn) and str(a.dtype) in _HASH_KIND:
+            cols.append(("p", a))
+        else:
+            return None
+    h = torch.full((n,), 42, dtype=torch.int32, device=dev)
+    st = N.stream_handle(dev)
+    for kind, a in cols:
+        v = None if a.valid is None else N.u8(a.valid.contiguous())
+        if kind == "s":
+            N.call("dxa_spark_hash_str", N.ptr(a.arena), N.ptr(a.starts), N.ptr(a.lens.contiguous()),
+                   N.ptr(v) if v is not None else None, n, N.ptr(h), st)
+        else:
+            d = a.data.contiguous()
+            d = d.view(torch.uint8) if d.dtype == torch.bool else d
+            N.call("dxa_spark_hash_fixed", N.ptr(d), _HASH_KIND[str(a.dtype)], N.ptr(v) if v is not None else None,
+                   n, N.ptr(h), st)
+    return PrimColumn("int", h.to(torch.int64))
+
+
 def _f_hash(e, scope, ctx, subst):
     n, dev = scope.length, scope.device
     args = _args(e, scope, ctx, subst)
+    if dev.type == "cuda":
+        out = _hash_device(args, n, dev)
+        if out is not None:
+            return out
     from .column import ts_to_datetime  # noqa: F401  (storage values below, not datetimes)
     cols = []
     for a in args:

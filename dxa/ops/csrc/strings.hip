@@ -1057,7 +1057,15 @@ __device__ int rx_match_at(const RxArgs& a, const uint8_t* s, int32_t len, int32
           stk[2 * top] = -1 - in.y; stk[2 * top + 1] = cap[in.y]; ++top;
           cap[in.y] = sp; ++pc; break;
         case 7: ok = sp == 0; ++pc; break;        // BOL
-        case 8: ok = sp == len || (sp == len - 1 && s[sp] == '\n'); ++pc; break;       // EOL
+        case 8: {                                 // EOL: Java $ (Pattern.Dollar) — end, or before a final
+          const int64_t r = len - sp;             // \r\n, \n (not after \r), \r, U+0085, U+2028, U+2029
+          ok = r == 0 ||
+               (r == 1 && (s[sp] == '\n' ? !(sp > 0 && s[sp - 1] == '\r') : s[sp] == '\r')) ||
+               (r == 2 && ((s[sp] == '\r' && s[sp + 1] == '\n') || (s[sp] == 0xC2 && s[sp + 1] == 0x85))) ||
+               (r == 3 && s[sp] == 0xE2 && s[sp + 1] == 0x80 && (s[sp + 2] == 0xA8 || s[sp + 2] == 0xA9));
+          ++pc;
+          break;
+        }
         case 10: pc = sp == cap[in.y] ? in.w : in.z; break;                          // LOOP: no progress → leave
         case 9: return 1;                         // MATCH
         default: return -1;

@@ -35,6 +35,8 @@ _SIGS = {
     "dxa_kafka_records": [c_p, c_i64] + [c_p] * 14,
     "dxa_kafka_crc": [c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
     "dxa_csv_tokenize": [c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p],
+    "dxa_spark_hash_fixed": [c_p, c_i32, c_p, c_i64, c_p, c_p],
+    "dxa_spark_hash_str": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
     "dxa_serialize_lengths": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p],
     "dxa_serialize_write": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],

@@ -41,6 +41,10 @@ _CONT = frozenset(range(0x80, 0xC0))
 # set (incl. every multi-byte one); ("bos",) ("eos",)
 
 
+def _ends_with_cr(node) -> bool:
+    return (node[0] == "set" and node[1] == frozenset([13])) or (node[0] == "bytes" and node[1].endswith(b"\r"))
+
+
 class _Parser:
     def __init__(self, p: str):
         self.p, self.i = p, 0
@@ -70,7 +74,10 @@ class _Parser:
     def seq(self):
         items = []
         while self.peek() is not None and self.peek() not in "|)":
-            items.append(self.quantified())
+            q = self.quantified()
+            if q == ("eos",) and items and _ends_with_cr(items[-1]):
+                q = ("eos", True)          # a literal \r before $: a final \n there is half of \r\n
+            items.append(q)
         return ("seq", items)
 
     def quantified(self):
@@ -293,12 +300,20 @@ class _NFA:
         if k == "bos":
             return self.chain([frozenset([BOS])])
         if k == "eos":
+            # Java's $ without MULTILINE (Pattern.Dollar): end of input, or before a final line terminator —
+            # \r\n, \n, \r, U+0085 (C2 85), U+2028 / U+2029 (E2 80 A8/A9).  A final \n right after a \r is the
+            # second half of \r\n, where $ does not match: when the pattern puts a literal \r just before the $,
+            # the lone-\n alternative is left out (the lookbehind an NFA cannot express in general)
             s, e = self.state(), self.state()
-            a, b = self.chain([frozenset([EOS])])
-            c, d = self.chain([frozenset([10]), frozenset([EOS])])
-            self.eps[s] += [a, c]
-            self.eps[b].append(e)
-            self.eps[d].append(e)
+            terms = [[], [frozenset([13]), frozenset([10])], [frozenset([13])], [frozenset([0xC2]), frozenset([0x85])],
+                     [frozenset([0xE2]), frozenset([0x80]), frozenset([0xA8])],
+                     [frozenset([0xE2]), frozenset([0x80]), frozenset([0xA9])]]
+            if not node[1:] or not node[1]:
+                terms.append([frozenset([10])])
+            for t in terms:
+                a, b = self.chain(t + [frozenset([EOS])])
+                self.eps[s].append(a)
+                self.eps[b].append(e)
             return s, e
         if k in ("any", "notset"):
             s, e = self.state(), self.state()
@@ -472,6 +487,12 @@ def java_to_python(pattern: str) -> str:
                 continue
         elif c == ".":
             out.append(r"[^\n\r\u0085\u2028\u2029]")
+            i += 1
+            continue
+        elif c == "$":
+            # Java's $ (no MULTILINE): end of input, or before a final line terminator — \r\n, \n (not right
+            # after a \r), \r, U+0085, U+2028, U+2029 (Pattern.Dollar); Python's $ knows only a final \n
+            out.append(r"(?:(?=\r\n\Z)|(?<!\r)(?=\n\Z)|(?=[\r\u0085\u2028\u2029]\Z)|\Z)")
             i += 1
             continue
         out.append(c)

@@ -231,3 +231,31 @@ def test_regexp_fuzz_gpu_match_cpu(gpu):
         assert _run(sql, vals, gpu) == _run(sql, vals, "cpu"), (pat, g, rep)
         _, bad = S.regex_extract(col, prog, g)
         assert not bool(bad.any()), pat                  # the device path itself produced the answer
+
+
+# Java's $ without MULTILINE (Pattern.Dollar): end of input, or before a final \r\n, \n (not right after \r), \r,
+# U+0085, U+2028, U+2029.  Expected values are Java's.
+DOLLAR_CASES = [
+    ("a$", "a", True), ("a$", "a\n", True), ("a$", "a\r", True), ("a$", "a\r\n", True), ("a$", "a ", True),
+    ("a$", "a ", True), ("a$", "a\u0085", True), ("a$", "a\n\n", False), ("a$", "a\r\r", False),
+    ("a$", "ab", False), ("a\r$", "a\r\n", False), ("a\r$", "a\r", True), ("^x.*$", "xyz\r\n", True),
+    ("b$", "ab c", False),
+]
+
+
+@pytest.mark.parametrize("pattern,value,want", DOLLAR_CASES)
+def test_java_dollar_terminators_host_and_dfa(pattern, value, want):
+    import re
+    from dxa.ops.regex_dfa import compile_rlike, java_to_python, run_dfa
+    assert bool(re.search(java_to_python(pattern), value, re.ASCII)) == want
+    assert run_dfa(compile_rlike(pattern), value.encode("utf-8")) == want
+
+
+@pytest.mark.gpu
+def test_java_dollar_terminators_gpu(gpu):
+    """The same $ cases through the device RLIKE (DFA kernel) and regexp_extract (VM, its EOL opcode)."""
+    for pattern, value, want in DOLLAR_CASES:
+        sql = f"SELECT s RLIKE '{_q(pattern)}' AS m, regexp_extract(s, '({_q(pattern)})', 1) AS x FROM F"
+        got = _run(sql, [value], gpu)
+        assert got == _run(sql, [value], "cpu"), (pattern, value)
+        assert bool(got[0][0]) == want, (pattern, value, got)
