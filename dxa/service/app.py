@@ -13,7 +13,9 @@ website's metrics API, in one process:
 
 Every response is ``{"error": bool, "message": str|null, "result": …}`` (Services/DataX.Contract/Result/ApiResult.cs).
 Routes are served both at ``/api/<route>`` and behind the gateway shape ``/api/{application}/{service}/<route>``;
-write routes require the Writer role when ``DXA_AUTH=1`` (roles from ``X-DXA-Roles``; DataXAuthConstants.cs).
+every route is authenticated by ``dxa.service.auth`` (Azure AD / JWT bearer tokens with the DataXReader /
+DataXWriter app roles, a trusted gateway's roles header, or loopback-only onebox mode; DataXAuthConstants.cs,
+RolesCheck.cs) and write routes require the Writer role.
 
     python -m dxa.service.app --port 5000 --root ./.dxa
 """
@@ -41,8 +43,15 @@ from .schema_inference import infer_schema
 from .sqlanalyzer import analyze
 from .store import DocumentStore
 
+# routes needing the Writer role: FlowManagementController's mutations, and — as in the reference, whose
+# SchemaInferenceController / InteractiveQueryController / LiveDataController are [DataXWriter] — schema inference
+# and every LiveQuery kernel route
 WRITE_ROUTES = {"flow/save", "flow/schedulebatch", "flow/generateconfigs", "flow/startjobs", "flow/restartjobs",
-                "flow/stopjobs", "flow/delete", "job/start", "job/stop", "job/restart", "job/restartallwithretries"}
+                "flow/stopjobs", "flow/delete", "job/start", "job/stop", "job/restart", "job/restartallwithretries",
+                "job/syncall", "job/syncbynames", "inputdata/inferschema", "inputdata/refreshsample",
+                "inputdata/refreshsampleandkernel", "kernel", "kernel/refresh", "kernel/deleteList", "kernel/delete",
+                "kernels/delete", "kernels/deleteall", "kernel/sampleinputfromquery", "kernel/executequery",
+                "ingest"}
 
 
 _FLOW_NAME = re.compile(r"^[A-Za-z0-9]+$")
@@ -101,13 +110,18 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
     st = ServiceState(root, device, metrics_endpoint)
     app.state.dxa = st
 
-    def authorize(route: str, roles: Optional[str]):
-        if os.environ.get("DXA_AUTH") != "1":
-            return
-        have = {r.strip().lower() for r in (roles or "").split(",") if r.strip()}
-        need = "writer" if route in WRITE_ROUTES else "reader"
-        if need not in have and "writer" not in have:
-            raise HTTPException(status_code=403, detail=f"{need} role required")
+    from .auth import AuthError, Authenticator
+    authn = Authenticator()
+    app.state.auth = authn
+
+    def authorize(route: str, roles: Optional[str], authorization: Optional[str] = None,
+                  client_host: Optional[str] = None):
+        """Reader / Writer role check (dxa.service.auth: JWT bearer tokens, trusted gateway header, or local
+        onebox only)."""
+        try:
+            return authn.check(route in WRITE_ROUTES, authorization, roles, client_host)
+        except AuthError as e:
+            raise HTTPException(status_code=e.status, detail=str(e))
 
     # ---------------------------------------------------------------------------------------------------------------
     def _flow(name: str) -> Dict[str, Any]:
@@ -368,8 +382,8 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
             st.kernels.get(body["kernelId"]).refresh(st.samples[body["name"]])
         return body.get("kernelId")
 
-    def dispatch(route_name: str, body, roles):
-        authorize(route_name, roles)
+    def dispatch(route_name: str, body, roles, authorization=None, client_host=None):
+        authorize(route_name, roles, authorization, client_host)
         fn = handlers.get(route_name)
         if fn is None:
             raise HTTPException(status_code=404, detail=f"unknown route {route_name}")
@@ -398,7 +412,9 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         return ok(ingest_lines(st.metrics, request_body.splitlines()))
 
     @app.post("/api/ingest/{flow}")
-    def ingest(flow: str, events: List[Any] = Body(...)):
+    def ingest(flow: str, request: Request, events: List[Any] = Body(...),
+               x_dxa_roles: Optional[str] = Header(None), authorization: Optional[str] = Header(None)):
+        authorize("ingest", x_dxa_roles, authorization, request.client.host if request.client else None)
         q = st.queues.setdefault(flow, [])
         q.extend(e if isinstance(e, str) else json.dumps(e) for e in events)
         del q[:-100_000]
@@ -428,15 +444,17 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
             return raw.decode()
 
     @app.api_route("/api/{path:path}", methods=["GET", "POST"])
-    async def generic(path: str, request: Request, x_dxa_roles: Optional[str] = Header(None)):
+    async def generic(path: str, request: Request, x_dxa_roles: Optional[str] = Header(None),
+                      authorization: Optional[str] = Header(None)):
         parts = path.strip("/").split("/")
         body = await _body(request)
         if request.method == "GET" and body is None:
             body = dict(request.query_params) or None
+        host = request.client.host if request.client else None
         for k in range(len(parts)):
             cand = "/".join(parts[k:])
             if cand in handlers:
-                return JSONResponse(dispatch(cand, body, x_dxa_roles))
+                return JSONResponse(dispatch(cand, body, x_dxa_roles, authorization, host))
         raise HTTPException(status_code=404, detail=f"unknown route {path}")
 
     return app

@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# the service tests drive the app through starlette's TestClient (not a loopback peer); auth itself is covered by
+# tests/test_auth.py, which sets its own mode
+os.environ.setdefault("DXA_AUTH", "off")
 
 
 def pytest_configure(config):

@@ -237,9 +237,15 @@ def test_infer_schema_and_metrics(client):
     assert client.get("/").status_code == 200
 
 
-def test_auth_roles(client, monkeypatch):
-    monkeypatch.setenv("DXA_AUTH", "1")
-    assert client.post("/api/flow/save", json=mini_flow()).status_code == 403
+def test_auth_roles(tmp_path, monkeypatch):
+    """Behind a trusted gateway (DXA_AUTH=gateway): roles from X-DXA-Roles (bearer tokens: tests/test_auth.py)."""
+    from fastapi.testclient import TestClient
+    from dxa.service.app import create_app
+    monkeypatch.setenv("DXA_AUTH", "gateway")
+    monkeypatch.setenv("DXA_SUPERVISE", "0")
+    client = TestClient(create_app(str(tmp_path / "svc")))
+    assert client.post("/api/flow/save", json=mini_flow()).status_code == 401
+    assert client.post("/api/flow/save", json=mini_flow(), headers={"X-DXA-Roles": "Reader"}).status_code == 403
     assert client.post("/api/flow/save", json=mini_flow(), headers={"X-DXA-Roles": "Writer"}).status_code == 200
     assert client.post("/api/flow/getall", json={}, headers={"X-DXA-Roles": "Reader"}).status_code == 200
 
