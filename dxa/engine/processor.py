@@ -58,6 +58,9 @@ class RawBatch:
     pending: Optional[Any] = None             # jsonparse.PendingParse started by Processor.prepare
     status: Optional[Any] = None              # source-side decode status (kafka_device.DecodeStatus), checked by
                                               # the source before the batch's offsets are committed
+    file_rows: Optional[List[Tuple[Dict[str, str], int]]] = None   # per-file FileInternal + its row count, in row
+                                              # order (blob-pointer batches: the FileInfo column varies per row)
+    source_metrics: Optional[Dict[str, float]] = None   # e.g. InputBlobs / Latency-Blobs, merged into the batch's
 
 
 def _read_lines(path: str) -> List[str]:
@@ -216,11 +219,26 @@ class Processor:
             pp["InputTime"] = str(raw.file_info.get("fileTime", ""))
             pp["Partition"] = str(raw.file_info.get("outputFileName", ""))
         names = ["Raw", "Properties", "SystemProperties", f"{S.NAME_PREFIX}Properties"]
-        cols = [raw_col, props, sysprops, ConstColumn(pp, empty_map, n, dev)]
         internal = f"__{S.NAME_PREFIX}_"
-        if raw.file_info:
+        targets = {i.get("target") for i, _c in raw.file_rows or []} or {(raw.file_info or {}).get("target")}
+        self._batch_target = next(iter(targets)) if len(targets) == 1 else None      # ${target} of blob outputs
+        self._source_metrics = dict(raw.source_metrics or {})
+        if raw.file_rows:
+            # one FileInternal per file: per-row map columns gathered from a k-row table (k = files)
+            from .column import column_from_pylist
+            infos = [dict(i) for i, _c in raw.file_rows]
+            idx = torch.repeat_interleave(torch.arange(len(infos), device=dev),
+                                          torch.tensor([c for _i, c in raw.file_rows], device=dev))
+            pps = [dict(pp, InputTime=str(i.get("fileTime", "")), Partition=str(i.get("outputFileName", "")))
+                   for i in infos]
+            cols = [raw_col, props, sysprops, column_from_pylist(pps, empty_map, dev).take(idx)]
             names.append(f"{internal}FileInfo")
-            cols.append(ConstColumn(dict(raw.file_info), empty_map, n, dev))
+            cols.append(column_from_pylist(infos, empty_map, dev).take(idx))
+        else:
+            cols = [raw_col, props, sysprops, ConstColumn(pp, empty_map, n, dev)]
+            if raw.file_info:
+                names.append(f"{internal}FileInfo")
+                cols.append(ConstColumn(dict(raw.file_info), empty_map, n, dev))
         table = Table(names, cols, n, dev)
         if self.pre_projection is not None:
             table = self.pre_projection(table, ctx)
@@ -249,6 +267,7 @@ class Processor:
         cat._built = getattr(self, "_ref_built", {})
         self._ref_built = cat._built
         metrics["Input_Normalized_Events_Count"] = projected.length
+        metrics.update(getattr(self, "_source_metrics", None) or {})
         part = P.PARTITIONED if P.active() else P.REPLICATED
         projected.dist = part
         if self.window_store is not None:
@@ -304,7 +323,8 @@ class Processor:
             staged.append((op.name, op.stage(t, ctx)))
         self._complete_inflight()
         from ..io.sinks import _pool
-        fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(_timed, st.finish, partition_time))
+        target = getattr(self, "_batch_target", None)
+        fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(_timed, st.finish, partition_time, target))
                                                  for name, st in staged], t_start)
         fl.t_staged = time.perf_counter()
         fl.stages = dict(self.stage_times)

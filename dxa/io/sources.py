@@ -17,6 +17,7 @@ error at job start (the conf keys are still generated and parsed).
 """
 from __future__ import annotations
 
+import datetime as _dt
 import gzip
 import json
 import os
@@ -236,15 +237,77 @@ def frame_bytes(data: bytes, device, file_info=None) -> RawBatch:
     return _to_device_batch(recs, device, file_info)
 
 
+_SA_REGEX = r"wasbs?://[\w-]+@([\w\d]+)\.blob\.core\.windows\.net/.*"
+
+
+def _java_time_pattern(fmt: str) -> str:
+    out = fmt
+    for j, p in (("yyyy", "%Y"), ("MM", "%m"), ("dd", "%d"), ("HH", "%H"), ("mm", "%M"), ("ss", "%S"),
+                 ("SSS", "%f")):
+        out = out.replace(j, p)
+    return out.replace("'", "")
+
+
 class BlobPointerSource(Source):
-    """Events of the form ``{"BlobPath": "<path>"}`` (reference BlobPointerInput.scala:28-36): the pointed-to files
-    are read and their lines become the batch."""
+    """Events of the form ``{"BlobPath": "<path>"}`` (BlobPointerInput.scala:28-162): each pointed-to blob's lines
+    become rows of the batch, with a per-row ``FileInternal`` (input path, file time, output file name, target,
+    rule index prefix).
+
+    With ``datax.job.input.default.source.<id>.target`` sources configured, a path is in scope only when the source
+    id extracted by ``sourceidregex`` (default: the storage account of a ``wasbs://`` URL) names one of them; its
+    file time comes from ``filetimeregex`` (group 1; ``filetimeformat`` or ``yyyy-MM-dd HH:mm:ss`` after '_'→':'
+    and 'T'→' '), its output file name from ``blobpathregex`` (groups joined by '-'); out-of-scope paths are dropped
+    (BlobPointerInput.filterPathGroups).  Without sources, every path (optionally filtered by ``path_regex``) is
+    read.  Per batch: ``InputBlobs`` and ``Latency-Blobs`` (now − earliest file time)."""
     name = "blobpointer"
 
-    def __init__(self, inner: Source, device, path_regex: Optional[str] = None):
+    def __init__(self, inner: Source, device, path_regex: Optional[str] = None, settings=None):
         self.inner = inner
         self.device = torch.device(device)
         self.rx = re.compile(path_regex) if path_regex else None
+        self.sources: Dict[str, Dict[str, Optional[str]]] = {}
+        self.source_id_rx = re.compile(_SA_REGEX)
+        self.blob_path_rx = self.file_time_rx = None
+        self.file_time_fmt = None
+        if settings is not None:
+            from ..config import settings as S
+            inp = settings.sub_dictionary(S.INPUT_PREFIX)
+            for sid, sub in inp.group_by_sub_namespace("source.").items():
+                self.sources[sid] = {"target": sub.get("target"), "catalogprefix": sub.get("catalogprefix")}
+            if inp.get("sourceidregex"):
+                self.source_id_rx = re.compile(inp.get("sourceidregex"))
+            if inp.get("blobpathregex"):
+                self.blob_path_rx = re.compile(inp.get("blobpathregex"))
+            if inp.get("filetimeregex"):
+                self.file_time_rx = re.compile(inp.get("filetimeregex"))
+            self.file_time_fmt = inp.get("filetimeformat")
+        self.last_metrics: Dict[str, float] = {}
+
+    def file_internal(self, path: str) -> Optional[Dict[str, str]]:
+        """FileInternal of one path, or None when it is out of scope."""
+        if not self.sources:
+            return {"inputPath": path}
+        m = self.source_id_rx.search(path)
+        src = self.sources.get(m.group(1)) if m else None
+        if src is None:
+            return None
+        info = {"inputPath": path, "target": src.get("target") or "", "ruleIndexPrefix": src.get("catalogprefix") or ""}
+        if self.file_time_rx is not None:
+            t = self.file_time_rx.search(path)
+            if t:
+                try:
+                    txt = t.group(1)
+                    ts = (_dt.datetime.strptime(txt, _java_time_pattern(self.file_time_fmt)) if self.file_time_fmt
+                          else _dt.datetime.fromisoformat(txt.replace("_", ":").replace("T", " ")))
+                    info["fileTime"] = ts.strftime("%Y-%m-%d %H:%M:%S")
+                except ValueError:
+                    log_warn(f"cannot parse the file time of {path}")
+        if self.blob_path_rx is not None:
+            m2 = self.blob_path_rx.search(path)
+            if m2 is None:
+                raise SourceError(f"blobpathregex does not match blob path '{path}'")
+            info["outputFileName"] = "-".join(g or "" for g in m2.groups())
+        return info
 
     def next_batch(self, batch_time_us: int) -> Optional[RawBatch]:
         b = self.inner.next_batch(batch_time_us)
@@ -252,19 +315,47 @@ class BlobPointerSource(Source):
             return b
         data = b.buf.cpu().numpy().tobytes()
         offs = b.offs.cpu().tolist()
-        paths = []
+        ends = b.ends.cpu().tolist() if b.ends is not None else None
+        files: List[Tuple[str, Dict[str, str]]] = []
+        seen = set()
+        dropped = 0
         for i in range(b.n):
             try:
-                p = json.loads(data[offs[i]:offs[i + 1]])["BlobPath"]
+                p = json.loads(data[offs[i]:(ends[i] if ends else offs[i + 1])])["BlobPath"]
             except Exception:  # noqa: BLE001
                 continue
-            if self.rx is None or self.rx.search(p):
-                paths.append(p)
+            if (self.rx is not None and not self.rx.search(p)) or p in seen:
+                continue
+            seen.add(p)
+            info = self.file_internal(p)
+            if info is None:
+                dropped += 1
+                continue
+            files.append((p, info))
+        if dropped:
+            log_warn(f"Found out-of-scope paths count={dropped}")
         blob = bytearray()
-        for p in paths:
+        rows: List[Tuple[Dict[str, str], int]] = []
+        for p, info in files:
             x = fs.read_bytes(p)
-            blob += x if x.endswith(b"\n") else x + b"\n"
-        return frame_bytes(bytes(blob), self.device, file_info={"inputPath": ";".join(paths)})
+            if x and not x.endswith(b"\n"):
+                x += b"\n"
+            blob += x
+            rows.append((info, sum(1 for line in x.split(b"\n")[:-1] if len(line) >= 1)))
+        times = [_dt.datetime.fromisoformat(i["fileTime"]) for i, _ in rows if i.get("fileTime")]
+        self.last_metrics = {"InputBlobs": float(len(files))}
+        if times:
+            self.last_metrics["Latency-Blobs"] = (_dt.datetime.utcnow() - min(times)).total_seconds()
+        raw = frame_bytes(bytes(blob), self.device, file_info={"inputPath": ";".join(p for p, _ in files)})
+        if rows and sum(r for _i, r in rows) == raw.n:
+            raw.file_rows = rows
+        raw.source_metrics = dict(self.last_metrics)
+        return raw
+
+
+def log_warn(msg: str):
+    import logging
+    logging.getLogger("dxa.sources").warning(msg)
 
 
 class PartitionedReplaySource(OffsetTrackedSource):
@@ -389,6 +480,11 @@ def build_source(settings, device, kind: Optional[str] = None) -> Source:
         return SocketSource(device, inp.get("socket.host") or "127.0.0.1", int(inp.get("socket.port") or 9999))
     if kind == "queue":
         return QueueSource(device)
+    if kind in ("blob", "blobpointer"):
+        # BlobStreamingApp: the stream carries {"BlobPath": …} pointer events (BlobPointerInput.scala)
+        inner_kind = "eventhub" if inp.get("eventhub.connectionstring") else (
+            "kafka" if (inp.get("kafka.bootstrapservers") or inp.get("kafka.topics")) else "queue")
+        return BlobPointerSource(build_source(settings, device, inner_kind), device, settings=settings)
     if kind in ("kafka", "eventhub", "kafkaeventhub", "iothub"):
         from .. import parallel as P
         from .kafka import build_kafka_source
