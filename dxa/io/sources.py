@@ -89,7 +89,8 @@ class OffsetTrackedSource(Source):
             if ranges is None:
                 return
             for k, (_s, e) in ranges.items():
-                self.pos[k] = max(self.pos.get(k, e), e)
+                prev = self.pos.get(k)
+                self.pos[k] = e if prev is None else max(prev, e)
             if self.ckpt:
                 self.ckpt.write(batch_time_us // 1000,
                                 [(*self._hub_of(k), s, e) for k, (s, e) in ranges.items()])
@@ -460,7 +461,7 @@ def build_source(settings, device, kind: Optional[str] = None) -> Source:
         elif inp.get("socket.port"):
             kind = "socket"
         elif inp.get("eventhub.connectionstring"):
-            kind = "eventhub"
+            kind = "eventhub"                # AMQP unless eventhub.protocol=kafka (the Kafka endpoint)
         elif inp.get("kafka.bootstrapservers") or inp.get("kafka.topics"):
             kind = "kafka"
         else:
@@ -485,9 +486,14 @@ def build_source(settings, device, kind: Optional[str] = None) -> Source:
         inner_kind = "eventhub" if inp.get("eventhub.connectionstring") else (
             "kafka" if (inp.get("kafka.bootstrapservers") or inp.get("kafka.topics")) else "queue")
         return BlobPointerSource(build_source(settings, device, inner_kind), device, settings=settings)
+    if kind in ("eventhub", "iothub") and (inp.get("eventhub.protocol") or "amqp").lower() == "amqp":
+        # the direct AMQP stream (EventHubStreamingFactory); IoT Hub's built-in endpoint is Event Hub-compatible
+        from .. import parallel as P
+        from .eventhub import build_eventhub_source
+        return build_eventhub_source(inp, device, P.rank(), P.world())
     if kind in ("kafka", "eventhub", "kafkaeventhub", "iothub"):
         from .. import parallel as P
         from .kafka import build_kafka_source
-        return build_kafka_source(inp, device, "eventhub" if kind in ("eventhub", "iothub") else "kafka",
-                                  P.rank(), P.world())
+        return build_kafka_source(inp, device, "eventhub" if kind in ("eventhub", "iothub", "kafkaeventhub")
+                                  else "kafka", P.rank(), P.world())
     raise SourceError(f"unknown input kind '{kind}'")

@@ -68,6 +68,27 @@ def sample_kafka(servers: str, topics: List[str], seconds: float, sasl=None, use
         client.close()
 
 
+def sample_eventhub_amqp(conn: str, hub: Optional[str], seconds: float,
+                         max_events: int = 100_000) -> List[Dict[str, Any]]:
+    """Events arriving on every partition of the hub during ``seconds`` (AMQP receiver at the end of the stream)."""
+    from ..io.eventhub import LATEST, EventHubSource
+    src = EventHubSource(conn, "cpu", start=LATEST, rank=0, world=1, hub=hub, wait_s=0.2)
+    out: List[Dict[str, Any]] = []
+    try:
+        deadline = time.monotonic() + seconds
+        while time.monotonic() < deadline and len(out) < max_events:
+            src.conn.pump(min(0.2, max(0.01, deadline - time.monotonic())))
+            for p, link in src.links.items():
+                for m in link.drain():
+                    ann = {str(k): str(v) for k, v in m["annotations"].items()}
+                    out.append(_event_raw(m["body"].decode("utf-8", "replace"),
+                                          {str(k): str(v) for k, v in (m["app"] or {}).items()},
+                                          dict(ann, **{"x-opt-partition-id": p})))
+        return out
+    finally:
+        src.close()
+
+
 def sample_blobs(paths: List[str], max_docs: int = MAX_BLOB_DOCS) -> List[Dict[str, Any]]:
     """The newest documents (lines of the most recently modified files) under each batch input path; ``{…}`` date
     tokens in a path match any folder name."""
@@ -128,6 +149,8 @@ def sample_input(q: Dict[str, Any], seconds: Optional[int] = None) -> List[Dict[
         names = [t.strip() for t in (q.get("eventhubNames") or "").split(",") if t.strip()]
         if kind == "kafka":
             return sample_kafka(conn, names, secs)
+        if kind in ("events", "eventhub", "iothub"):          # EventhubMessageBus: AMQP from the end
+            return sample_eventhub_amqp(conn, names[0] if names else None, secs)
         es = K.eventhub_kafka_settings(conn)
         topics = [es["topic"]] if es.get("topic") else names
         return sample_kafka(es["bootstrap"], topics, secs, sasl=es["sasl"], use_ssl=True)
