@@ -31,7 +31,7 @@ import uuid
 from typing import Any, Dict, List, Optional
 
 from fastapi import Body, FastAPI, Header, HTTPException, Query, Request
-from fastapi.responses import HTMLResponse, JSONResponse
+from fastapi.responses import JSONResponse
 
 from ..flow import configgen
 from ..flow import designer
@@ -149,6 +149,8 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
     @route("flow/save")
     def flow_save(body):
         flow = body if "gui" in body else {"name": body.get("name"), "gui": body}
+        if "gui" not in body and body.get("displayName"):
+            flow["displayName"] = body["displayName"]
         name = flow.get("name") or flow["gui"].get("name")
         if not name:
             # FlowConfigBuilder.cs:66-75: a new flow's name is its display name reduced to [a-z0-9]
@@ -420,10 +422,10 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
         del q[:-100_000]
         return ok(len(events))
 
-    @app.get("/", response_class=HTMLResponse)
-    def home():
-        from .web import INDEX_HTML
-        return INDEX_HTML
+    # the website: page routes, /dist packages, web-composition / user / functionenabled / freshness (website.py);
+    # registered before the generic /api/{path} route below so its /api/* routes win
+    from .website import mount_website
+    mount_website(app, st, authn)
 
     # node-side Livy-compatible batch API (remote job submission: job_clients.LivyClient)
     from .job_clients import batch_routes

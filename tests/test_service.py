@@ -416,19 +416,4 @@ def test_designer_shaped_flow_generates_and_runs(client, tmp_path):
     lines = [json.loads(l) for f in files for l in open(f).read().splitlines() if l.strip()]
     assert len(lines) == 50 and all("Rules" in r for r in lines)
     page = client.get("/").text
-    assert "Designer" in page and "inferSchema" in page
-
-
-def test_console_javascript_parses():
-    import re
-    import shutil
-    import subprocess
-    from dxa.service.web import INDEX_HTML
-    node = shutil.which("node") or shutil.which("nodejs")
-    if node is None:
-        pytest.skip("node not available")
-    js = re.search(r"<script>(.*)</script>", INDEX_HTML, re.S).group(1)
-    r = subprocess.run([node, "--check", "-"], input=js, capture_output=True, text=True)
-    if "--check" in r.stderr and "-" in r.stderr:
-        pytest.skip("node --check from stdin unsupported")
-    assert r.returncode == 0, r.stderr
+    assert "/dist/app.js" in page
