@@ -92,6 +92,10 @@ def main():
                     "parallel on the host, as per-partition fetch threads would)")
     ap.add_argument("--kafka-batch-records", type=int, default=26,
                     help="kafka: records per producer batch (26 SimulatedData events = ~16 KiB, one LZ4 block)")
+    ap.add_argument("--kafka-batch-size", type=int, default=None, metavar="BYTES",
+                    help="kafka: size record batches as a Java producer with batch.size=BYTES does (the estimated "
+                         "compressed size fills batch.size; dxa.io.kafka.records_per_batch) instead of a fixed "
+                         "--kafka-batch-records")
     ap.add_argument("--crc", choices=["host", "device", "off"], default="host",
                     help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): host planner "
                          "threads (default), the GPU (kafka_crc_kernel), or not at all")
@@ -201,6 +205,10 @@ def main():
             hb, ho = buf.cpu().numpy(), offs.cpu().numpy()
             del buf, offs
             cuts = np.linspace(0, E, parts + 1).astype(np.int64)
+            if args.kafka_batch_size and p == 0:
+                # batch.size semantics of the Java producer: records per batch from the learned compression ratio
+                args.kafka_batch_records, _r = K.records_per_batch(hb, ho, args.kafka_batch_size,
+                                                                   level=args.lz4_level, block_size=lz4_block_k)
             sets = [K.encode_stream(hb, ho[cuts[q]:cuts[q + 1] + 1], args.kafka_batch_records, base_offset=0,
                                     compression="lz4", level=args.lz4_level, block_size=lz4_block_k,
                                     threads=16) for q in range(parts)]
@@ -482,6 +490,8 @@ def main():
     if source == "kafka":
         out["config"]["kafka_partitions"] = args.kafka_partitions
         out["config"]["kafka_batch_records"] = args.kafka_batch_records
+        if args.kafka_batch_size:
+            out["config"]["kafka_batch_size"] = args.kafka_batch_size
         out["config"]["check_crcs"] = args.crc
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)

@@ -122,6 +122,29 @@ def encode_stream(vals: np.ndarray, offs: np.ndarray, per_batch: int, base_offse
         L.dxa_host_free(ptr)
 
 
+KAFKA_BATCH_SIZE = 16384          # producer batch.size default (bytes)
+_RATIO_FACTOR = 1.05               # CompressionRatioEstimator.COMPRESSION_RATIO_ESTIMATION_FACTOR
+
+
+def records_per_batch(vals: np.ndarray, offs: np.ndarray, batch_size: int = KAFKA_BATCH_SIZE,
+                      compression: str = "lz4", level: int = 9, block_size: int = 64 * 1024,
+                      rounds: int = 4, sample: int = 20000) -> Tuple[int, float]:
+    """How many records a Java producer puts in one record batch: the accumulator closes a batch when its *estimated
+    compressed* size would pass ``batch.size`` (MemoryRecordsBuilder.hasRoomFor: uncompressed bytes × the topic's
+    learned compression ratio × 1.05).  The ratio estimate starts at 1.0 and converges to the observed one, so the
+    fixed point is iterated on a sample of the records → (records per batch, compressed/uncompressed ratio)."""
+    n = int(offs.shape[0]) - 1
+    m = min(n, sample)
+    avg = float(offs[m] - offs[0]) / max(1, m)
+    ratio = 1.0
+    per = 1
+    for _ in range(rounds):
+        per = max(1, int(batch_size / (avg * ratio * _RATIO_FACTOR)))
+        enc = encode_stream(vals, offs[:m + 1], per, compression=compression, level=level, block_size=block_size)
+        ratio = enc.nbytes / float(offs[m] - offs[0])
+    return per, ratio
+
+
 _ERRS = {-2: "unsupported message format (magic != 2)", -3: "CRC mismatch", -4: "gzip decode failed",
          -5: "unsupported compression codec (snappy/zstd)", -6: "lz4 decode failed"}
 

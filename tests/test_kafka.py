@@ -293,3 +293,19 @@ def test_start_position_from_enqueue_time(broker):
     assert c.list_offset("iot", 0, 9_000_000) == 15            # past the end: the log end
     src = K.KafkaSource(K.KafkaClient(f"127.0.0.1:{broker.port}"), ["iot"], "cpu", start=K.start_position("2000"))
     assert src.fetch_pos[("iot", 0)] == 5 and src.next_batch(0).n == 10
+
+
+def test_records_per_batch_follows_the_producer_estimator():
+    """batch.size bounds a batch's estimated *compressed* size (MemoryRecordsBuilder.hasRoomFor): with LZ4 on
+    SimulatedData JSON (~3.3x) a 16 KiB batch holds ~84 records, not 16 KiB / 608 B = 26."""
+    from dxa.io import kafka as K
+    from dxa.models import iot
+    from dxa.simulate.datagen import generate
+    buf, offs = generate(iot.program(), 20000, torch.device("cpu"), seed=3, row0=0, base_ms=1_700_000_000_000)
+    per, ratio = K.records_per_batch(buf.numpy(), offs.numpy(), sample=8000)
+    avg = float(offs[-1]) / 20000
+    assert 0.25 < ratio < 0.4
+    # the fixed point: the estimated compressed batch fills batch.size
+    assert abs(per * avg * ratio * 1.05 - K.KAFKA_BATCH_SIZE) < avg * ratio * 1.05 * 2
+    per_none, ratio_none = K.records_per_batch(buf.numpy(), offs.numpy(), compression="none", sample=8000)
+    assert ratio_none > 1.0 and per_none < 27
