@@ -362,7 +362,7 @@ __global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t
 //     selects it for comparison).
 constexpr int kWaitVm0 = 0xF70;                                        // s_waitcnt vmcnt(0) (gfx9 encoding)
 
-template <int G>
+template <int G, int R>
 __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __restrict__ src,
                                                                const int64_t* __restrict__ comp_off,
                                                                const int32_t* __restrict__ comp_len,
@@ -375,10 +375,18 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   // produced == null: out_len[b] is the exact decompressed size; else it is a capacity and the size is reported
   // in produced[b] (Kafka frames do not carry their content size)
   static_assert(G == 8 || G == 16, "group width");
+  static_assert(R == 0 || (R >= 64 && (R & (R - 1)) == 0), "ring size: 0 or a power of two >= 64");
   // 64-byte input window = NW dwords per lane; fast-path literals LPL bytes per lane; pipelined matches (<= 32 B)
   // BPL bytes per lane
   constexpr int NW = 16 / G, LPL = 16 / G, BPL = 32 / G, LOG_G = G == 8 ? 3 : 4;
   constexpr int WB = 64, PIPE = 32;
+  // History ring: the block's last R output bytes in LDS.  A match with off + len <= R reads its source there
+  // (LDS latency) instead of from the output in HBM, which put a global round trip on the sequence chain for
+  // every match (the load, or the vmcnt wait that makes the group's own earlier stores visible).  JSON matches are
+  // mostly a record apart (~600 B), so a 2 KiB ring serves nearly all of them; farther ones take the global path.
+  constexpr int RS = R > 0 ? R : 1;
+  __shared__ uint8_t ring_all[R > 0 ? (256 / G) * R : 1];
+  uint8_t* ring = ring_all + (R > 0 ? (int)(threadIdx.x / G) * R : 0);
   const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const int gl = (int)(threadIdx.x & (G - 1));
   const int gbase = (int)((threadIdx.x & 63) & ~(G - 1));
@@ -387,6 +395,16 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   const int64_t cap64 = out_len[b];
   const uint8_t* in = src + comp_off[b];
   uint8_t* out = dst + out_off[b];
+  // every output byte goes to HBM and (with a ring) to the block's history ring
+  auto put = [&](int32_t pos, uint8_t v) {
+    out[pos] = v;
+    if constexpr (R > 0) ring[pos & (RS - 1)] = v;
+  };
+  // an earlier output byte at distance <= R from the write position: from the ring
+  auto hist = [&](int32_t pos) -> uint32_t {
+    if constexpr (R > 0) return ring[pos & (RS - 1)];
+    return out[pos];
+  };
   if (stored[b]) {
     if (produced ? (n > cap64) : (n != cap64)) {
       if (gl == 0) status[b] = LZ_SIZE;
@@ -448,7 +466,16 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   auto flush = [&]() {
 #pragma unroll
     for (int k = 0; k < BPL; ++k)
-      if (gl + G * k < pml) out[pdst + G * k + gl] = (uint8_t)pv[k];
+      if (gl + G * k < pml) put(pdst + G * k + gl, (uint8_t)pv[k]);
+  };
+  // make the group's own earlier HBM stores visible before a match reads its source from HBM (only matches that
+  // reach past the ring, or every match without one)
+  auto sync_src = [&](int32_t src_end, int32_t now) {
+    if (src_end > done) {
+      __builtin_amdgcn_s_waitcnt(kWaitVm0);
+      asm volatile("" ::: "memory");
+      done = now;
+    }
   };
   while (ip < iend) {
     if (ip - xb > WB - 16) {
@@ -466,7 +493,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
 #pragma unroll
       for (int k = 0; k < LPL; ++k) {
         const uint32_t lv = wbyte(r + 1 + G * k + gl);
-        if (gl + G * k < lit) out[op + G * k + gl] = (uint8_t)lv;
+        if (gl + G * k < lit) put(op + G * k + gl, (uint8_t)lv);
       }
       const int32_t off = (int32_t)(wbyte(r + 1 + lit) | (wbyte(r + 2 + lit) << 8));
       ip += fhdr;
@@ -475,23 +502,18 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       const int32_t ml = fml;
       const int32_t s0 = op - off;
       const int32_t src_end = s0 + (off < ml ? off : ml);
+      const bool near = R > 0 && off + ml <= R;   // source and destination both inside the ring
       if (pml > 0 && (src_end > pdst || ml > PIPE)) {
         flush();
         pml = 0;
       }
-      if (src_end > done) {
-        __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        asm volatile("" ::: "memory");
-        done = pml > 0 ? pdst : op;
-      }
+      if (!near) sync_src(src_end, pml > 0 ? pdst : op);
       if (ml > PIPE) {
-        if (off >= ml) {
-          for (int32_t c = 0; c < ml; c += G)
-            if (c + gl < ml) out[op + c + gl] = out[s0 + c + gl];
-        } else {
-          for (int32_t c = 0; c < ml; c += G) {
-            const uint32_t i = (uint32_t)(c + gl);
-            if ((int32_t)i < ml) out[op + i] = out[s0 + (int32_t)(i % (uint32_t)off)];
+        for (int32_t c = 0; c < ml; c += G) {
+          const int32_t i = c + gl;
+          if (i < ml) {
+            const int32_t sp = s0 + (off >= ml ? i : (int32_t)((uint32_t)i % (uint32_t)off));
+            put(op + i, (uint8_t)(near ? hist(sp) : out[sp]));
           }
         }
         op += ml;
@@ -500,12 +522,15 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       uint32_t v[BPL];
       if (off >= ml) {
 #pragma unroll
-        for (int k = 0; k < BPL; ++k) v[k] = (gl + G * k < ml) ? out[s0 + G * k + gl] : 0u;
+        for (int k = 0; k < BPL; ++k)
+          v[k] = (gl + G * k < ml) ? (near ? hist(s0 + G * k + gl) : (uint32_t)out[s0 + G * k + gl]) : 0u;
       } else {
         const uint32_t o = (uint32_t)off;
 #pragma unroll
-        for (int k = 0; k < BPL; ++k)
-          v[k] = (gl + G * k < ml) ? out[s0 + (int32_t)((uint32_t)(gl + G * k) % o)] : 0u;
+        for (int k = 0; k < BPL; ++k) {
+          const int32_t sp = s0 + (int32_t)((uint32_t)(gl + G * k) % o);
+          v[k] = (gl + G * k < ml) ? (near ? hist(sp) : (uint32_t)out[sp]) : 0u;
+        }
       }
       if (pml > 0) flush();
       pdst = op;
@@ -533,7 +558,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     if (lit > iend - ip) { rc = LZ_TRUNC; break; }
     if (lit > cap - op) { rc = LZ_OVERFLOW; break; }
     for (int32_t c = 0; c < lit; c += G)
-      if (c + gl < lit) out[op + c + gl] = a0[ip + c + gl];
+      if (c + gl < lit) put(op + c + gl, a0[ip + c + gl]);
     ip += lit;
     op += lit;
     if (ip >= iend) break;
@@ -555,18 +580,13 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     ml += 4;
     if (ml > cap - op) { rc = LZ_OVERFLOW; break; }
     const int32_t s0 = op - off;
-    if (s0 + (off < ml ? off : ml) > done) {
-      __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        asm volatile("" ::: "memory");
-      done = op;
-    }
-    if (off >= ml) {
-      for (int32_t c = 0; c < ml; c += G)
-        if (c + gl < ml) out[op + c + gl] = out[s0 + c + gl];
-    } else {
-      for (int32_t c = 0; c < ml; c += G) {
-        const uint32_t i = (uint32_t)(c + gl);
-        if ((int32_t)i < ml) out[op + i] = out[s0 + (int32_t)(i % (uint32_t)off)];
+    const bool near = R > 0 && off + ml <= R;   // source and destination both inside the ring
+    if (!near) sync_src(s0 + (off < ml ? off : ml), op);
+    for (int32_t c = 0; c < ml; c += G) {
+      const int32_t i = c + gl;
+      if (i < ml) {
+        const int32_t sp = s0 + (off >= ml ? i : (int32_t)((uint32_t)i % (uint32_t)off));
+        put(op + i, (uint8_t)(near ? hist(sp) : out[sp]));
       }
     }
     op += ml;
@@ -590,18 +610,64 @@ DXA_API int dxa_lz4_block_sizes(const void* src, const void* comp_off, const voi
   return (int)hipGetLastError();
 }
 
-DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* comp_len, const void* stored,
-                           const void* out_off, const void* out_len, int64_t nb, int64_t max_out, void* dst,
-                           void* status, void* st) {
-  if (nb <= 0) return 0;
-  const hipStream_t s = (hipStream_t)st;
-  // DXA_LZ4_LANES selects the decoder for measurements: 16 lanes per block (default), 8, 64 = one wave per block
-  // with LDS-staged output, 1 = one lane per block
+// DXA_LZ4_LANES selects the decoder for measurements: 16 lanes per block (default), 8, 64 = one wave per block
+// with LDS-staged output, 1 = one lane per block
+static int lz4_lanes() {
   static const int lanes = [] {
     const char* e = getenv("DXA_LZ4_LANES");
     const int v = e ? atoi(e) : 16;
     return (v == 1 || v == 8 || v == 16 || v == 64) ? v : 16;
   }();
+  return lanes;
+}
+
+// DXA_LZ4_RING: history-ring bytes per block for the group decoder (0 = match sources from HBM, the default;
+// 1024 / 2048 / 4096 for measurements).  Measured on the groupby batch (2 M events, 26-record batches): ring 0
+// 8.13 ms/step, 1024 8.71, 2048 12.61 (LDS byte stores and the occupancy the ring costs outweigh the HBM round
+// trips it saves); 84-record / 51 KB blocks: 18.7 / 20.8 / 22.8 ms — the chain there is latency-bound on too few
+// waves, which the chunk count (kafka_device.DeviceRecordDecoder) addresses instead.
+static int lz4_ring() {
+  static const int ring = [] {
+    const char* e = getenv("DXA_LZ4_RING");
+    const int v = e ? atoi(e) : 0;
+    return (v == 0 || v == 1024 || v == 2048 || v == 4096) ? v : 0;
+  }();
+  return ring;
+}
+
+// launch the G-lane group decoder with the configured ring (LDS per 256-thread workgroup = 256 / G * ring)
+template <int G>
+static void launch_group(int64_t nb, hipStream_t s, const uint8_t* src, const int64_t* co, const int32_t* cl,
+                         const uint8_t* sd, const int64_t* oo, const int64_t* ol, uint8_t* dst, int32_t* status,
+                         int64_t* produced) {
+  const dim3 grid((unsigned)((nb * G + 255) / 256));
+  int ring = lz4_ring();
+  if (G == 8 && ring > 2048) ring = 2048;                 // 32 blocks per workgroup: keep LDS <= 64 KiB
+  switch (ring) {
+    case 0:
+      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 0>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb, dst,
+                         status, produced);
+      break;
+    case 1024:
+      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 1024>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb,
+                         dst, status, produced);
+      break;
+    case 4096:
+      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 4096>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb,
+                         dst, status, produced);
+      break;
+    default:
+      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 2048>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb,
+                         dst, status, produced);
+  }
+}
+
+DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* comp_len, const void* stored,
+                           const void* out_off, const void* out_len, int64_t nb, int64_t max_out, void* dst,
+                           void* status, void* st) {
+  if (nb <= 0) return 0;
+  const hipStream_t s = (hipStream_t)st;
+  const int lanes = lz4_lanes();
   const uint8_t* s8 = (const uint8_t*)src;
   const int64_t* co = (const int64_t*)comp_off;
   const int32_t* cl = (const int32_t*)comp_len;
@@ -609,13 +675,10 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
   const int64_t* oo = (const int64_t*)out_off;
   const int64_t* ol = (const int64_t*)out_len;
   if (lanes == 8 || lanes == 16) {
-    const int64_t threads = nb * lanes;
     if (lanes == 8)
-      hipLaunchKernelGGL(lz4_decode_group_kernel<8>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8,
-                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
+      launch_group<8>(nb, s, s8, co, cl, sd, oo, ol, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
     else
-      hipLaunchKernelGGL(lz4_decode_group_kernel<16>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, s8,
-                         co, cl, sd, oo, ol, nb, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
+      launch_group<16>(nb, s, s8, co, cl, sd, oo, ol, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
     return (int)hipGetLastError();
   }
   const int64_t lb = (max_out + 15) & ~(int64_t)15;         // LDS bytes per wave (16-B aligned slices)
@@ -638,16 +701,22 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
 }
 
 // Blocks with a capacity instead of a known size (Kafka LZ4 frames): `cap[b]` bytes reserved at out_off[b], the
-// decompressed size comes back in produced[b].  Always the 16-lane group decoder.
+// decompressed size comes back in produced[b].  The group decoder, 16 lanes per block (8 with DXA_LZ4_LANES=8).
 DXA_API int dxa_lz4_decode_into(const void* src, const void* comp_off, const void* comp_len, const void* stored,
                                 const void* out_off, const void* cap, int64_t nb, void* dst, void* produced,
                                 void* status, void* st) {
   if (nb <= 0) return 0;
-  const int64_t threads = nb * 16;
-  hipLaunchKernelGGL(lz4_decode_group_kernel<16>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)st, (const uint8_t*)src, (const int64_t*)comp_off, (const int32_t*)comp_len,
-                     (const uint8_t*)stored, (const int64_t*)out_off, (const int64_t*)cap, nb, (uint8_t*)dst,
-                     (int32_t*)status, (int64_t*)produced);
+  const hipStream_t s = (hipStream_t)st;
+  const uint8_t* s8 = (const uint8_t*)src;
+  const int64_t* co = (const int64_t*)comp_off;
+  const int32_t* cl = (const int32_t*)comp_len;
+  const uint8_t* sd = (const uint8_t*)stored;
+  const int64_t* oo = (const int64_t*)out_off;
+  const int64_t* cp = (const int64_t*)cap;
+  if (lz4_lanes() == 8)
+    launch_group<8>(nb, s, s8, co, cl, sd, oo, cp, (uint8_t*)dst, (int32_t*)status, (int64_t*)produced);
+  else
+    launch_group<16>(nb, s, s8, co, cl, sd, oo, cp, (uint8_t*)dst, (int32_t*)status, (int64_t*)produced);
   return (int)hipGetLastError();
 }
 
