@@ -144,7 +144,7 @@ def main():
         native.lib()
     from dxa.engine.processor import Processor, RawBatch
     from dxa.models import iot
-    from dxa.simulate.datagen import generate
+    from dxa.simulate.datagen import generate, generate_begin, generate_finish
     from dxa import parallel
 
     if world > 1:
@@ -256,6 +256,7 @@ def main():
             kdec = KD.DeviceRecordDecoder(device, chunks=args.lz4_chunks, copy_stream=side,
                                           verify_crc=args.crc == "device")
     staged = {}
+    gen_pending = {}           # gpu-sim: batches whose length pass is queued (datagen.generate_begin)
     sizes = []
     framing_checks = []        # device flags: a frame's newline count differed from its producer's record count
 
@@ -281,15 +282,18 @@ def main():
             staged[i] = (raw, None, ev)
             return
         if source == "gpu-sim":
-            def gen():
-                bt_ms = batch_time(i) // 1000
-                return generate(prog, E, device, seed=7919 * rank + i + 1, row0=i * E, base_ms=bt_ms - 1000,
-                                step_us=max(1, interval_us // E))
+            def gen_args(j):
+                return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=batch_time(j) // 1000 - 1000,
+                            step_us=max(1, interval_us // E))
             if side is None:
-                staged[i] = gen() + (None,)
+                staged[i] = generate(prog, E, device, **gen_args(i)) + (None,)
                 return
             with torch.cuda.stream(side):
-                db, do = gen()
+                # batch i's length pass was queued one stage earlier, so its size is already known here; queue
+                # batch i+1's now (the host never waits on a length pass stuck behind the compute stream's kernels)
+                pend = gen_pending.pop(i, None) or generate_begin(prog, E, device, **gen_args(i))
+                gen_pending[i + 1] = generate_begin(prog, E, device, **gen_args(i + 1))
+                db, do = generate_finish(pend)
                 ev = torch.cuda.Event()
                 ev.record(side)
             staged[i] = (db, do, ev)

@@ -7,6 +7,8 @@ over device columns with the dxa kernels (hash group-by / hash join / string ops
 """
 from __future__ import annotations
 
+import functools
+
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -68,8 +70,14 @@ class Catalog:
         return b
 
 
+@functools.lru_cache(maxsize=256)
+def _parse_cached(sql: str):
+    return parse_query(sql)          # ASTs are not mutated by execution (Processor reuses its parsed transform too)
+
+
 def run_sql(sql: str, catalog: Catalog, ctx: EvalContext) -> Table:
-    return execute(parse_query(sql), catalog, ctx)
+    """Parse (cached per SQL text: the projection step re-runs the same statement every batch) and execute."""
+    return execute(_parse_cached(sql), catalog, ctx)
 
 
 def _gathered(t: Table) -> Table:

@@ -235,6 +235,30 @@ def generate(prog: GenProgram, n: int, device, seed: int = 1, row0: int = 0, bas
     base_ms = int(time.time() * 1000) if base_ms is None else base_ms
     if device.type != "cuda":
         return generate_cpu(prog, n, seed, row0, base_ms, step_us)
+    return generate_finish(generate_begin(prog, n, device, seed, row0, base_ms, step_us))
+
+
+@dataclass
+class PendingGen:
+    """A device generation whose length pass is queued (``generate_begin``); ``generate_finish`` reads the total
+    size, allocates and renders.  Splitting the two lets a source queue batch t+1's length pass one step before it
+    needs the bytes, so reading the size never waits behind the kernels running on the GPU."""
+    prog: "GenProgram"
+    n: int
+    device: torch.device
+    seed: int
+    row0: int
+    base_ms: int
+    step_us: int
+    offs: torch.Tensor
+    total: torch.Tensor                  # offs[-1] copied to pinned host memory
+    ready: Any                           # torch.cuda.Event after that copy
+
+
+def generate_begin(prog: GenProgram, n: int, device, seed: int = 1, row0: int = 0, base_ms: Optional[int] = None,
+                   step_us: int = 0) -> PendingGen:
+    device = torch.device(device)
+    base_ms = int(time.time() * 1000) if base_ms is None else base_ms
     ops, pool, tab = prog.device(device)
     st = N.stream_handle(device)
     lens = torch.empty(n, dtype=torch.int64, device=device)
@@ -243,12 +267,25 @@ def generate(prog: GenProgram, n: int, device, seed: int = 1, row0: int = 0, bas
            row0, n, base_ms, step_us, N.ptr(lens), st)
     offs = torch.zeros(n + 1, dtype=torch.int64, device=device)
     torch.cumsum(lens, 0, out=offs[1:])
-    total = int(offs[-1].item())
-    buf = torch.empty(total + 16, dtype=torch.uint8, device=device)
+    total = torch.empty(1, dtype=torch.int64, pin_memory=True)
+    total.copy_(offs[-1:], non_blocking=True)
+    ready = torch.cuda.Event()
+    ready.record(torch.cuda.current_stream(device))
+    lens.record_stream(torch.cuda.current_stream(device))
+    return PendingGen(prog, n, device, seed, row0, base_ms, step_us, offs, total, ready)
+
+
+def generate_finish(p: PendingGen) -> Tuple[torch.Tensor, torch.Tensor]:
+    p.ready.synchronize()
+    total = int(p.total[0])
+    ops, pool, tab = p.prog.device(p.device)
+    pw, ti = pool.numel() // 8, tab.numel()
+    buf = torch.empty(total + 16, dtype=torch.uint8, device=p.device)
     buf[total:].zero_()          # the parser's 16-B read window needs zero padding; the rest is fully written
-    N.call("dxa_datagen_write", N.ptr(ops), len(prog.ops), N.ptr(pool), pw, N.ptr(tab), ti, seed & (2**64 - 1),
-           row0, n, base_ms, step_us, N.ptr(offs), N.ptr(buf), st)
-    return buf, offs
+    N.call("dxa_datagen_write", N.ptr(ops), len(p.prog.ops), N.ptr(pool), pw, N.ptr(tab), ti,
+           p.seed & (2**64 - 1), p.row0, p.n, p.base_ms, p.step_us, N.ptr(p.offs), N.ptr(buf),
+           N.stream_handle(p.device))
+    return buf, p.offs
 
 
 M64 = (1 << 64) - 1
