@@ -93,10 +93,24 @@ class Processor:
             self.transform = parse_transform(_read_lines(tpath))
         self.windows = TimeWindowConf.from_settings(d)
         self.window_store = WindowStore(self.windows) if self.windows.enabled else None
-        self.state_tables = create_state_tables(d, self.device)
-        # ---- extensions
+        # ---- independent initialisers run concurrently, as the reference's init futures on an 8-thread pool
+        # (CommonProcessorFactory.scala:43-44,58-73): UDF builds (hipRTC compiles of HIP UDFs, plugin imports) and
+        # sink construction (connections, logins) overlap each other and the state-table restore and reference-data
+        # load, which stay on this thread in this order (at N ranks both run collectives — a restart's key
+        # reshuffle, the reference broadcast — whose order must match on every rank).  The first failure is
+        # re-raised (the reference's failFast).
+        from concurrent.futures import ThreadPoolExecutor
         from ..udf.registry import build_udfs
-        self.udfs, self.udafs, self.udf_refreshers = build_udfs(d, udfs or {}, udafs or {})
+        from ..io.sinks import build_outputs
+        init_pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dxa-init")
+        f_udfs = init_pool.submit(build_udfs, d, udfs or {}, udafs or {})
+        f_outputs = init_pool.submit(build_outputs, d)
+        try:
+            self.state_tables = create_state_tables(d, self.device)
+            self.udfs, self.udafs, self.udf_refreshers = f_udfs.result()
+        except BaseException:
+            init_pool.shutdown(wait=True, cancel_futures=True)
+            raise
         from ..udf.registry import _instantiate
         if normalizer is None and d.get(S.PROCESS_PREFIX + "inputnormalizer"):
             normalizer = _instantiate(d.get(S.PROCESS_PREFIX + "inputnormalizer"))          # InputNormalizerHandler
@@ -109,11 +123,13 @@ class Processor:
         self.pre_projection = pre_projection
         self.append_props = {k: v for k, v in d.sub_dictionary(S.PROCESS_PREFIX + "appendproperty.").items()}
         # ---- reference data (resident across batches: stream–static joins build their hash tables once)
-        self.reference: Dict[str, Table] = self._load_reference_data()
-        # ---- outputs + metrics
-        from ..io.sinks import build_outputs
+        try:
+            self.reference: Dict[str, Table] = self._load_reference_data()
+            # ---- outputs + metrics
+            self.outputs = f_outputs.result()
+        finally:
+            init_pool.shutdown(wait=True)
         from ..telemetry.metrics import MetricLogger
-        self.outputs = build_outputs(d)
         self.metric_logger = MetricLogger.from_settings(d, metric_store)
         self.parse_plan = ParsePlan(self.raw_schema, self._needed_raw_paths() if parse_prune else None)
         # input rebalance across ranks (reference: datax.job.input.default.eventhub.repartition → rdd.repartition)
