@@ -360,9 +360,12 @@ __global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t
 //   * The group width is a template parameter: G = 8 (eight blocks per instruction, a 2-dword window per lane,
 //     4-byte-per-lane match copies) measured 6.07 ms against 4.72 ms for G = 16 on the bench batch (DXA_LZ4_LANES=8
 //     selects it for comparison).
+//   * Measured and dropped (profiles/kafka_batching/README.md): an LDS history ring for match sources (the byte
+//     stores to LDS and the occupancy it costs outweigh the HBM round trips it saves: 8.13 -> 8.71 / 12.61 ms per
+//     groupby step with a 1 / 2 KiB ring) and branch-free masked stores (below).
 constexpr int kWaitVm0 = 0xF70;                                        // s_waitcnt vmcnt(0) (gfx9 encoding)
 
-template <int G, int R>
+template <int G>
 __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __restrict__ src,
                                                                const int64_t* __restrict__ comp_off,
                                                                const int32_t* __restrict__ comp_len,
@@ -375,18 +378,10 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   // produced == null: out_len[b] is the exact decompressed size; else it is a capacity and the size is reported
   // in produced[b] (Kafka frames do not carry their content size)
   static_assert(G == 8 || G == 16, "group width");
-  static_assert(R == 0 || (R >= 64 && (R & (R - 1)) == 0), "ring size: 0 or a power of two >= 64");
   // 64-byte input window = NW dwords per lane; fast-path literals LPL bytes per lane; pipelined matches (<= 32 B)
   // BPL bytes per lane
   constexpr int NW = 16 / G, LPL = 16 / G, BPL = 32 / G, LOG_G = G == 8 ? 3 : 4;
   constexpr int WB = 64, PIPE = 32;
-  // History ring: the block's last R output bytes in LDS.  A match with off + len <= R reads its source there
-  // (LDS latency) instead of from the output in HBM, which put a global round trip on the sequence chain for
-  // every match (the load, or the vmcnt wait that makes the group's own earlier stores visible).  JSON matches are
-  // mostly a record apart (~600 B), so a 2 KiB ring serves nearly all of them; farther ones take the global path.
-  constexpr int RS = R > 0 ? R : 1;
-  __shared__ uint8_t ring_all[R > 0 ? (256 / G) * R : 1];
-  uint8_t* ring = ring_all + (R > 0 ? (int)(threadIdx.x / G) * R : 0);
   const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const int gl = (int)(threadIdx.x & (G - 1));
   const int gbase = (int)((threadIdx.x & 63) & ~(G - 1));
@@ -395,16 +390,13 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   const int64_t cap64 = out_len[b];
   const uint8_t* in = src + comp_off[b];
   uint8_t* out = dst + out_off[b];
-  // every output byte goes to HBM and (with a ring) to the block's history ring
-  auto put = [&](int32_t pos, uint8_t v) {
-    out[pos] = v;
-    if constexpr (R > 0) ring[pos & (RS - 1)] = v;
+  // predicated byte stores / loads: the exec-mask branch around each skips the memory instruction when no lane of
+  // the wave needs it (a branch-free variant storing masked-off lanes to a dump buffer measured 4.77 -> 5.84 ms on
+  // 16 KiB blocks and 6.90 -> 8.48 ms on 64 KiB blocks: the extra stores cost more than the branches)
+  auto put = [&](bool on, int32_t pos, uint32_t v) {
+    if (on) out[pos] = (uint8_t)v;
   };
-  // an earlier output byte at distance <= R from the write position: from the ring
-  auto hist = [&](int32_t pos) -> uint32_t {
-    if constexpr (R > 0) return ring[pos & (RS - 1)];
-    return out[pos];
-  };
+  auto fetch = [&](bool on, int32_t pos) -> uint32_t { return on ? (uint32_t)out[pos] : 0u; };
   if (stored[b]) {
     if (produced ? (n > cap64) : (n != cap64)) {
       if (gl == 0) status[b] = LZ_SIZE;
@@ -465,17 +457,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   for (int k = 0; k < BPL; ++k) pv[k] = 0;
   auto flush = [&]() {
 #pragma unroll
-    for (int k = 0; k < BPL; ++k)
-      if (gl + G * k < pml) put(pdst + G * k + gl, (uint8_t)pv[k]);
-  };
-  // make the group's own earlier HBM stores visible before a match reads its source from HBM (only matches that
-  // reach past the ring, or every match without one)
-  auto sync_src = [&](int32_t src_end, int32_t now) {
-    if (src_end > done) {
-      __builtin_amdgcn_s_waitcnt(kWaitVm0);
-      asm volatile("" ::: "memory");
-      done = now;
-    }
+    for (int k = 0; k < BPL; ++k) put(gl + G * k < pml, pdst + G * k + gl, pv[k]);
   };
   while (ip < iend) {
     if (ip - xb > WB - 16) {
@@ -486,14 +468,15 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     const uint32_t token = wbyte(r);
     int32_t lit = (int32_t)(token >> 4);
     const int32_t mlc = (int32_t)(token & 15);
-    const uint32_t mext = (mlc == 15 && lit < 15 && r + lit + 4 <= WB) ? wbyte(r + lit + 3) : 0u;
+    const bool has_ext = mlc == 15 && lit < 15 && r + lit + 4 <= WB;
+    const uint32_t mext = has_ext ? wbyte(r + lit + 3) : 0u;
     const int32_t fml = mlc + 4 + (int32_t)mext;
     const int32_t fhdr = lit + 3 + (mlc == 15 ? 1 : 0);
     if (lit < 15 && (mlc < 15 || mext < 255) && r + fhdr <= WB && iend - ip >= fhdr && cap - op >= lit + fml) {
 #pragma unroll
       for (int k = 0; k < LPL; ++k) {
         const uint32_t lv = wbyte(r + 1 + G * k + gl);
-        if (gl + G * k < lit) put(op + G * k + gl, (uint8_t)lv);
+        put(gl + G * k < lit, op + G * k + gl, lv);
       }
       const int32_t off = (int32_t)(wbyte(r + 1 + lit) | (wbyte(r + 2 + lit) << 8));
       ip += fhdr;
@@ -502,18 +485,23 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       const int32_t ml = fml;
       const int32_t s0 = op - off;
       const int32_t src_end = s0 + (off < ml ? off : ml);
-      const bool near = R > 0 && off + ml <= R;   // source and destination both inside the ring
       if (pml > 0 && (src_end > pdst || ml > PIPE)) {
         flush();
         pml = 0;
       }
-      if (!near) sync_src(src_end, pml > 0 ? pdst : op);
+      if (src_end > done) {
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        asm volatile("" ::: "memory");
+        done = pml > 0 ? pdst : op;
+      }
       if (ml > PIPE) {
-        for (int32_t c = 0; c < ml; c += G) {
-          const int32_t i = c + gl;
-          if (i < ml) {
-            const int32_t sp = s0 + (off >= ml ? i : (int32_t)((uint32_t)i % (uint32_t)off));
-            put(op + i, (uint8_t)(near ? hist(sp) : out[sp]));
+        if (off >= ml) {
+          for (int32_t c = 0; c < ml; c += G)
+            if (c + gl < ml) out[op + c + gl] = out[s0 + c + gl];
+        } else {
+          for (int32_t c = 0; c < ml; c += G) {
+            const uint32_t i = (uint32_t)(c + gl);
+            if ((int32_t)i < ml) out[op + i] = out[s0 + (int32_t)(i % (uint32_t)off)];
           }
         }
         op += ml;
@@ -522,15 +510,11 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
       uint32_t v[BPL];
       if (off >= ml) {
 #pragma unroll
-        for (int k = 0; k < BPL; ++k)
-          v[k] = (gl + G * k < ml) ? (near ? hist(s0 + G * k + gl) : (uint32_t)out[s0 + G * k + gl]) : 0u;
+        for (int k = 0; k < BPL; ++k) v[k] = fetch(gl + G * k < ml, s0 + G * k + gl);
       } else {
         const uint32_t o = (uint32_t)off;
 #pragma unroll
-        for (int k = 0; k < BPL; ++k) {
-          const int32_t sp = s0 + (int32_t)((uint32_t)(gl + G * k) % o);
-          v[k] = (gl + G * k < ml) ? (near ? hist(sp) : (uint32_t)out[sp]) : 0u;
-        }
+        for (int k = 0; k < BPL; ++k) v[k] = fetch(gl + G * k < ml, s0 + (int32_t)((uint32_t)(gl + G * k) % o));
       }
       if (pml > 0) flush();
       pdst = op;
@@ -558,7 +542,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     if (lit > iend - ip) { rc = LZ_TRUNC; break; }
     if (lit > cap - op) { rc = LZ_OVERFLOW; break; }
     for (int32_t c = 0; c < lit; c += G)
-      if (c + gl < lit) put(op + c + gl, a0[ip + c + gl]);
+      if (c + gl < lit) out[op + c + gl] = a0[ip + c + gl];
     ip += lit;
     op += lit;
     if (ip >= iend) break;
@@ -580,13 +564,18 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     ml += 4;
     if (ml > cap - op) { rc = LZ_OVERFLOW; break; }
     const int32_t s0 = op - off;
-    const bool near = R > 0 && off + ml <= R;   // source and destination both inside the ring
-    if (!near) sync_src(s0 + (off < ml ? off : ml), op);
-    for (int32_t c = 0; c < ml; c += G) {
-      const int32_t i = c + gl;
-      if (i < ml) {
-        const int32_t sp = s0 + (off >= ml ? i : (int32_t)((uint32_t)i % (uint32_t)off));
-        put(op + i, (uint8_t)(near ? hist(sp) : out[sp]));
+    if (s0 + (off < ml ? off : ml) > done) {
+      __builtin_amdgcn_s_waitcnt(kWaitVm0);
+      asm volatile("" ::: "memory");
+      done = op;
+    }
+    if (off >= ml) {
+      for (int32_t c = 0; c < ml; c += G)
+        if (c + gl < ml) out[op + c + gl] = out[s0 + c + gl];
+    } else {
+      for (int32_t c = 0; c < ml; c += G) {
+        const uint32_t i = (uint32_t)(c + gl);
+        if ((int32_t)i < ml) out[op + i] = out[s0 + (int32_t)(i % (uint32_t)off)];
       }
     }
     op += ml;
@@ -621,45 +610,15 @@ static int lz4_lanes() {
   return lanes;
 }
 
-// DXA_LZ4_RING: history-ring bytes per block for the group decoder (0 = match sources from HBM, the default;
-// 1024 / 2048 / 4096 for measurements).  Measured on the groupby batch (2 M events, 26-record batches): ring 0
-// 8.13 ms/step, 1024 8.71, 2048 12.61 (LDS byte stores and the occupancy the ring costs outweigh the HBM round
-// trips it saves); 84-record / 51 KB blocks: 18.7 / 20.8 / 22.8 ms — the chain there is latency-bound on too few
-// waves, which the chunk count (kafka_device.DeviceRecordDecoder) addresses instead.
-static int lz4_ring() {
-  static const int ring = [] {
-    const char* e = getenv("DXA_LZ4_RING");
-    const int v = e ? atoi(e) : 0;
-    return (v == 0 || v == 1024 || v == 2048 || v == 4096) ? v : 0;
-  }();
-  return ring;
-}
-
-// launch the G-lane group decoder with the configured ring (LDS per 256-thread workgroup = 256 / G * ring)
+// launch the G-lane group decoder (one block per G lanes)
 template <int G>
-static void launch_group(int64_t nb, hipStream_t s, const uint8_t* src, const int64_t* co, const int32_t* cl,
-                         const uint8_t* sd, const int64_t* oo, const int64_t* ol, uint8_t* dst, int32_t* status,
-                         int64_t* produced) {
+static int launch_group(int64_t nb, hipStream_t s, const uint8_t* src, const int64_t* co, const int32_t* cl,
+                        const uint8_t* sd, const int64_t* oo, const int64_t* ol, uint8_t* dst, int32_t* status,
+                        int64_t* produced) {
   const dim3 grid((unsigned)((nb * G + 255) / 256));
-  int ring = lz4_ring();
-  if (G == 8 && ring > 2048) ring = 2048;                 // 32 blocks per workgroup: keep LDS <= 64 KiB
-  switch (ring) {
-    case 0:
-      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 0>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb, dst,
-                         status, produced);
-      break;
-    case 1024:
-      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 1024>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb,
-                         dst, status, produced);
-      break;
-    case 4096:
-      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 4096>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb,
-                         dst, status, produced);
-      break;
-    default:
-      hipLaunchKernelGGL((lz4_decode_group_kernel<G, 2048>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb,
-                         dst, status, produced);
-  }
+  hipLaunchKernelGGL((lz4_decode_group_kernel<G>), grid, dim3(256), 0, s, src, co, cl, sd, oo, ol, nb, dst, status,
+                     produced);
+  return (int)hipGetLastError();
 }
 
 DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* comp_len, const void* stored,
