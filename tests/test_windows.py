@@ -42,16 +42,20 @@ def _canon(t):
     return sorted(out)
 
 
-@pytest.mark.parametrize("quirk,block", [(True, 16), (False, 16), (False, 2), (True, 3)])
-def test_paned_aggregate_matches_materialized(quirk, block, monkeypatch):
+@pytest.mark.parametrize("quirk,block,win,nb", [(True, 16, 5, 12), (False, 16, 5, 12), (False, 2, 5, 12),
+                                                (True, 3, 5, 12), (False, 4, 23, 60), (True, 5, 31, 70)])
+def test_paned_aggregate_matches_materialized(quirk, block, win, nb, monkeypatch):
+    """Paned answers (per-pane partials; complete blocks combined into one table, the oldest block's suffix
+    combinations, the newest block's running combination) equal the materialized window, batch after batch, through
+    block completions and evictions."""
     import numpy as np
     import dxa.engine.query as Q
     monkeypatch.setattr(Q, "BLOCK", block)
     rng = np.random.default_rng(7)
-    conf = TimeWindowConf({"W": 5 * S}, True, "ts", 2 * S, 5 * S, quirk)
+    conf = TimeWindowConf({"W": win * S}, True, "ts", 2 * S, win * S, quirk)
     store = WindowStore(conf)
     ctx = EvalContext(now_us=0)
-    for b in range(12):
+    for b in range(nb):
         T = (100 + b) * S
         views, _ = store.process(batch(rng, T, 200, 3 * S), T, S)
         assert isinstance(views["W"], PanedTable)
@@ -66,8 +70,11 @@ def test_paned_aggregate_matches_materialized(quirk, block, monkeypatch):
             assert _canon(paned) == _canon(ref), (b, q)
     # fully-inside panes were answered from cached partials (and pre-combined blocks when blocks are small)
     assert any(p.partials for p in store.past.values())
-    if block <= 3:
+    if block <= 3 or win > 2 * block:
         assert store.blocks
+    if win > 2 * block:
+        kinds = {k[0] for k in store.blocks if isinstance(k[0], str)}
+        assert {"mid", "part", "sfx"} <= kinds
 
 
 def test_window_ranges_and_eviction():
