@@ -614,90 +614,34 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
         state["meta"] = cached[1:]
         return cached[0]
 
-    # Sliding-window combination (a two-stack scheme at block granularity, for non-invertible MIN / MAX): panes are
-    # grouped in blocks of BLOCK consecutive batches.  A batch merges three pre-combined partial tables instead of
-    # every pane's: all complete in-window blocks ("mid", rebuilt only when the set of complete blocks changes), the
-    # partly evicted oldest block (its suffix combinations are built once, when its first pane leaves, so each
-    # later batch reuses one) and the growing newest block (previous combination + the new pane).  Entries live in
-    # ``store.blocks`` keyed by the pane keys they cover, and are dropped as soon as one of those panes is evicted.
+    # complete blocks of BLOCK consecutive in-window panes are pre-combined once and reused until a member is
+    # evicted, so a 300-pane window merges ~20 block partials + the loose panes at its edges instead of 300 tables.
+    # (Measured and dropped, profiles/window_merge/: combining all complete blocks into one table was within noise;
+    # additionally keeping the newest block's running combination and the oldest block's suffix combinations cost
+    # more — a group-by pass per batch plus bursts — than the concat it saves.)
     store = t.store
     span = BLOCK * max(1, store.interval_us)
     parts = []
     by_block: Dict[int, list] = {}
-
-    def combine(tables):
-        pl, kn, _ = state["meta"]
-        return tables[0] if len(tables) == 1 else D.combine_partials(concat_tables(tables), pl, kn, bool(sel.group_by))
-
-    def cached(key, members, build):
-        ent = store.blocks.get(key)
-        if ent is None or ent[0] != members:
-            tab = build()
-            ent = (members, tab, state["meta"])
-            store.blocks[key] = ent
-        state.setdefault("meta", ent[2])
-        return ent[1]
-
-    def block_table(bid, panes):
-        members = tuple(p.key for p in panes)
-
-        def build():
-            run = store.blocks.get(("part", fp, bid))          # the block's running combination while it grew
-            if run is not None and run[0] == members[:len(run[0])]:
-                state.setdefault("meta", run[2])
-                return combine([run[1]] + [pane_partial(p, True) for p in panes[len(run[0]):]])
-            return combine([pane_partial(p, True) for p in panes])
-        return cached((fp, bid), members, build)
-
-    def suffixes(bid, panes):
-        """The combination of panes[j:] for every j, built right to left; returns the whole one."""
-        acc = None
-        for j in range(len(panes) - 1, -1, -1):
-            key = ("sfx", fp, tuple(p.key for p in panes[j:]))
-            ent = store.blocks.get(key)
-            if ent is None:
-                pp = pane_partial(panes[j], True)
-                acc = pp if acc is None else combine([pp, acc])
-                store.blocks[key] = (key[2], acc, state["meta"])
-            else:
-                state.setdefault("meta", ent[2])
-                acc = ent[1]
-        return acc
-
     try:
         for pane, full in t.pieces():
             if full and cacheable and store.interval_us:
                 by_block.setdefault(pane.key // span, []).append(pane)
             else:
                 parts.append(pane_partial(pane, full))
-        for b in by_block:
-            by_block[b].sort(key=lambda p: p.key)
-        complete = sorted(b for b, ps in by_block.items() if len(ps) == BLOCK)
-        if complete:
-            members = tuple(p.key for b in complete for p in by_block[b])
-            parts.append(cached(("mid", fp), members,
-                                lambda: combine([block_table(b, by_block[b]) for b in complete])))
-        for bid in sorted(b for b, ps in by_block.items() if len(ps) < BLOCK):
-            ps = by_block[bid]
-            members = tuple(p.key for p in ps)
-            run = store.blocks.get(("part", fp, bid))
-            if run is not None and run[0] == members:
-                state.setdefault("meta", run[2])
-                parts.append(run[1])
-                continue
-            sfx = store.blocks.get(("sfx", fp, members))
-            if sfx is not None:                                 # the oldest block, one more pane evicted
-                state.setdefault("meta", sfx[2])
-                tab = sfx[1]
-            elif run is not None and members[:len(run[0])] == run[0]:
-                state.setdefault("meta", run[2])                # the newest block grew
-                tab = combine([run[1]] + [pane_partial(p, True) for p in ps[len(run[0]):]])
-            elif bid != max(by_block):
-                tab = suffixes(bid, ps)    # an older block only loses panes at the front from now on
+        for bid, panes in by_block.items():
+            if len(panes) == BLOCK:
+                members = tuple(sorted(p.key for p in panes))
+                ent = store.blocks.get((fp, bid))
+                if ent is None or ent[0] != members:
+                    ps = [pane_partial(p, True) for p in panes]
+                    pl, kn, _ = state["meta"]
+                    ent = (members, D.combine_partials(concat_tables(ps), pl, kn, bool(sel.group_by)), state["meta"])
+                    store.blocks[(fp, bid)] = ent
+                state.setdefault("meta", ent[2])
+                parts.append(ent[1])
             else:
-                tab = combine([pane_partial(p, True) for p in ps])
-            store.blocks[("part", fp, bid)] = (members, tab, state["meta"])
-            parts.append(tab)
+                parts.extend(pane_partial(p, True) for p in panes)
         if "meta" not in state:
             # nothing of this rank's window is in range: still produce (empty) partials, so every rank runs the
             # same exchange — the choice of plan must not depend on a rank's data
