@@ -91,6 +91,27 @@ def test_device_decode_matches_host(gpu):
     assert bool(ok.all()) and col.children[0].data.cpu().tolist() == [json.loads(v)["id"] for v in want]
 
 
+@pytest.mark.gpu
+def test_device_decode_launch_sizing(gpu):
+    """Java-producer-sized batches (90 records, one 64 KiB-frame LZ4 block each): the decode is split into at most
+    nblocks / min_blocks_per_chunk launches; one launch and four launches give the host decoder's records."""
+    vals = _values(6000, seed=13)
+    rs = _record_set(vals, 90, "lz4", 9, 65536)
+    plan = KD.plan_fetch(rs, 0)
+    staging = torch.zeros(len(rs) + 64, dtype=torch.uint8).pin_memory()
+    staging[:len(rs)] = torch.frombuffer(bytearray(rs), dtype=torch.uint8)
+    dec = KD.DeviceRecordDecoder(gpu, chunks=4)
+    assert dec.min_blocks_per_chunk >= 64
+    for mb in (1, 10 ** 9):                       # 4 launches / 1 launch
+        dec.min_blocks_per_chunk = mb
+        raw, ev = dec.decode(staging, KD.plan_fetch(rs, 0))
+        torch.cuda.current_stream(gpu).wait_event(ev)
+        dec.check()
+        buf = raw.buf.cpu().numpy()
+        s, e = raw.offs[:-1].cpu().tolist(), raw.ends.cpu().tolist()
+        assert raw.n == plan.nrec == 6000 and [buf[x:y].tobytes() for x, y in zip(s, e)] == vals
+
+
 def test_plan_many_matches_merged_plans():
     vals = _values(400, seed=5)
     sets = [_record_set(vals[:130], 17), _record_set(vals[130:260], 29, "none"), _record_set(vals[260:], 41)]
