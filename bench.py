@@ -96,6 +96,9 @@ def main():
                     help="kafka: size record batches as a Java producer with batch.size=BYTES does (the estimated "
                          "compressed size fills batch.size; dxa.io.kafka.records_per_batch) instead of a fixed "
                          "--kafka-batch-records")
+    ap.add_argument("--kafka-codec", choices=["lz4", "gzip"], default="lz4",
+                    help="kafka: record batch compression codec (gzip = the Event Hubs Kafka endpoint's codec; "
+                         "inflated on the GPU by inflate.hip)")
     ap.add_argument("--crc", choices=["host", "device", "off"], default="host",
                     help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): host planner "
                          "threads (default), the GPU (kafka_crc_kernel), or not at all")
@@ -208,9 +211,10 @@ def main():
             if args.kafka_batch_size and p == 0:
                 # batch.size semantics of the Java producer: records per batch from the learned compression ratio
                 args.kafka_batch_records, _r = K.records_per_batch(hb, ho, args.kafka_batch_size,
+                                                                   compression=args.kafka_codec,
                                                                    level=args.lz4_level, block_size=lz4_block_k)
             sets = [K.encode_stream(hb, ho[cuts[q]:cuts[q + 1] + 1], args.kafka_batch_records, base_offset=0,
-                                    compression="lz4", level=args.lz4_level, block_size=lz4_block_k,
+                                    compression=args.kafka_codec, level=args.lz4_level, block_size=lz4_block_k,
                                     threads=16) for q in range(parts)]
             total = sum(x.size for x in sets)
             staging = torch.empty(total + 64, dtype=torch.uint8, pin_memory=on_gpu)
@@ -466,7 +470,7 @@ def main():
         "data": "synthetic (SimulatedData-schema JSON generated on device, random seeds per rank/batch"
                 + ("; delivered as LZ4-framed batches in pinned host memory, decompressed on the GPU in every step)"
                    if source == "pinned-lz4" else
-                   "; delivered as Kafka v2 record batches with the LZ4 codec in pinned host memory (a "
+                   f"; delivered as Kafka v2 record batches with the {args.kafka_codec.upper()} codec in pinned host memory (a "
                    "multi-partition Fetch), planned on the host, "
                    + ({"host": "CRC-32C-verified on the host (check.crcs), ",
                        "device": "CRC-32C-verified on the GPU (check.crcs), "}.get(args.crc, "")) +
@@ -497,6 +501,7 @@ def main():
         if args.kafka_batch_size:
             out["config"]["kafka_batch_size"] = args.kafka_batch_size
         out["config"]["check_crcs"] = args.crc
+        out["config"]["kafka_codec"] = args.kafka_codec
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
         out["latency_trace_ms"] = [round(x * 1e3, 2) for x in lat]

@@ -8,8 +8,10 @@ content size) and frames the records (``kafka_records.hip``).  The JSON parser t
 place through per-record [start, end) ranges — the bytes cross PCIe once, compressed, and are never copied on the
 device.
 
-Batches the GPU path does not take (gzip / snappy / zstd codecs, dependent-block LZ4 frames, compacted batches
-with offset gaps) make ``plan_fetch`` raise ``Unsupported``; the source then decodes that fetch on the host.
+gzip batches (codec 1, the Event Hubs Kafka endpoint's codec) are inflated on the GPU too (``inflate.hip``: the
+planner strips the gzip header and takes the size from the ISIZE trailer).  Batches the GPU path does not take
+(snappy / zstd codecs, dependent-block LZ4 frames, compacted batches with offset gaps) make ``plan_fetch`` raise
+``Unsupported``; the source then decodes that fetch on the host.
 CRC-32C (the consumer's ``check.crcs``, on by default) is verified by the host planner (SSE4.2 ``crc32``, ~8 GB/s
 per planner thread) or, with ``DeviceRecordDecoder(verify_crc=True)``, on the GPU over the compressed bytes already
 in HBM (``kafka_crc_kernel``: one wave per batch, lane-interleaved words combined in GF(2)).  Measured on MI355X
@@ -348,6 +350,7 @@ class DeviceRecordDecoder:
         st = self.decode_stream.cuda_stream
         nb = plan.nblk
         chunks = max(1, min(self.chunks, nb // max(1, self.min_blocks_per_chunk)))
+        has_gzip = bool(nb) and bool((plan.k_stored[:nb] == 2).any())
         bounds = np.linspace(0, nb, chunks + 1).astype(np.int64)
         ev_last = tab_ev
         copied = 0                 # staging bytes already sent: chunks are contiguous from byte 0 (the batch headers
@@ -367,6 +370,10 @@ class DeviceRecordDecoder:
             N.call("dxa_lz4_decode_into", N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
                    N.ptr(oo[b0:b1]), N.ptr(cap[b0:b1]), b1 - b0, N.ptr(out), N.ptr(produced[b0:b1]),
                    N.ptr(bstat[b0:b1]), st)
+            if has_gzip:                   # gzip batches (kind 2) of the chunk: inflate.hip
+                N.call("dxa_inflate_into", N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
+                       N.ptr(oo[b0:b1]), N.ptr(cap[b0:b1]), b1 - b0, N.ptr(out), N.ptr(produced[b0:b1]),
+                       N.ptr(bstat[b0:b1]), st)
         with torch.cuda.stream(self.decode_stream):
             offs[n:].fill_(plan.out_bytes)
         N.call("dxa_kafka_records", N.ptr(out), plan.nbat, N.ptr(bc), N.ptr(bs), N.ptr(bk), N.ptr(bf), N.ptr(bn),
@@ -526,7 +533,12 @@ def decode_on_host_like(staging: np.ndarray, plan: FetchPlan, verify_crc: bool =
         end = p
         for b in range(f, f + nb):                 # a frame's blocks back to back from its first slot
             src = staging[plan.k_comp_off[b]: plan.k_comp_off[b] + plan.k_comp_len[b]]
-            raw = src.tobytes() if plan.k_stored[b] else lz4.decompress_block(src.tobytes(), int(plan.k_cap[b]))
+            kind = int(plan.k_stored[b])
+            if kind == 2:                          # deflate data of a gzip member (header / trailer stripped)
+                import zlib
+                raw = zlib.decompressobj(-15).decompress(src.tobytes())
+            else:
+                raw = src.tobytes() if kind else lz4.decompress_block(src.tobytes(), int(plan.k_cap[b]))
             out[end:end + len(raw)] = np.frombuffer(raw, np.uint8)
             end += len(raw)
         data = out

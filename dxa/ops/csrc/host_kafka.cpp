@@ -259,8 +259,9 @@ int walk_batches(const uint8_t* data, int64_t len, int64_t min_offset, int64_t m
 // Walks only the record-batch headers and LZ4 frame block headers of a Fetch record set (no record bytes), so the
 // records themselves are decompressed and framed on the GPU (lz4.hip + kafka_records.hip).  Each block gets an
 // output slot: the frame's maximum block size for LZ4 blocks (every block of a frame but the last is full, so a
-// frame's bytes are contiguous from its first slot), its own length for stored data.  Returns 0, or
-// -2 bad magic, -3 CRC, -5 codec the GPU path does not take (gzip / snappy / zstd), -7 malformed LZ4 frame,
+// frame's bytes are contiguous from its first slot), its own length for stored data, the gzip trailer's ISIZE for
+// a gzip member (kind 2: inflated by inflate.hip).  Returns 0, or
+// -2 bad magic, -3 CRC, -5 codec the GPU path does not take (snappy / zstd, odd gzip headers), -7 malformed LZ4 frame,
 // -8 dependent-block frame, -9 offset deltas that are not 0..count-1 (compacted batch) — the caller decodes such
 // fetches on the host.
 struct Plan {
@@ -273,6 +274,28 @@ struct Plan {
   int64_t nbat = 0, nblk = 0, nrec = 0, out_bytes = 0;
   int32_t max_block = 0;
 };
+
+// Length of a gzip member header (RFC 1952 2.3: ID1 ID2 CM FLG MTIME XFL OS, then FEXTRA / FNAME / FCOMMENT /
+// FHCRC as flagged), or -1 when it is not a deflate gzip header.
+int64_t gzip_header_len(const uint8_t* p, int64_t n) {
+  if (n < 10 || p[0] != 0x1f || p[1] != 0x8b || p[2] != 8) return -1;
+  const uint8_t flg = p[3];
+  if (flg & 0xe0) return -1;                         // reserved bits
+  int64_t k = 10;
+  if (flg & 4) {                                     // FEXTRA
+    if (k + 2 > n) return -1;
+    k += 2 + ((int64_t)p[k] | ((int64_t)p[k + 1] << 8));
+  }
+  for (int f : {8, 16}) {                            // FNAME, FCOMMENT: zero-terminated
+    if (flg & f) {
+      while (k < n && p[k]) ++k;
+      if (k >= n) return -1;
+      ++k;
+    }
+  }
+  if (flg & 2) k += 2;                               // FHCRC
+  return k <= n ? k : -1;
+}
 
 int plan_batches(const uint8_t* data, int64_t len, int64_t min_offset, Plan& pl, int64_t* next_offset,
                  int verify_crc) {
@@ -328,6 +351,24 @@ int plan_batches(const uint8_t* data, int64_t len, int64_t min_offset, Plan& pl,
         if (mb > pl.max_block) pl.max_block = mb;
         pl.out_bytes += nb * (int64_t)mb;
         pl.nblk += nb;
+      } else if (codec == 1) {
+        // gzip (Java GZIPOutputStream: one member): the device inflates the deflate data between the header and
+        // the 8-byte trailer, whose ISIZE is the exact decompressed size (inflate.hip)
+        const int64_t hdr = gzip_header_len(recs, bend - recs);
+        if (hdr < 0 || bend - recs < hdr + 8) return -5;
+        const uint8_t* t = bend - 4;
+        const int64_t isize = (int64_t)t[0] | ((int64_t)t[1] << 8) | ((int64_t)t[2] << 16) | ((int64_t)t[3] << 24);
+        if (isize > INT32_MAX) return -5;
+        if (pl.write) {
+          pl.k_comp_off[pl.nblk] = recs + hdr - data;
+          pl.k_comp_len[pl.nblk] = (int32_t)(bend - 8 - (recs + hdr));
+          pl.k_stored[pl.nblk] = 2;
+          pl.k_out_off[pl.nblk] = pl.out_bytes;
+          pl.k_cap[pl.nblk] = isize;
+        }
+        if (isize > pl.max_block) pl.max_block = (int32_t)isize;
+        pl.out_bytes += isize;
+        ++pl.nblk;
       } else {
         return -5;
       }

@@ -386,6 +386,8 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
   const int gl = (int)(threadIdx.x & (G - 1));
   const int gbase = (int)((threadIdx.x & 63) & ~(G - 1));
   if (b >= nb) return;
+  const uint8_t kd = stored[b];            // 0 LZ4 block, 1 stored bytes, 2 deflate (inflate.hip's, skipped here)
+  if (kd > 1) return;
   const int32_t n = comp_len[b];
   const int64_t cap64 = out_len[b];
   const uint8_t* in = src + comp_off[b];
@@ -397,7 +399,7 @@ __global__ __launch_bounds__(256) void lz4_decode_group_kernel(const uint8_t* __
     if (on) out[pos] = (uint8_t)v;
   };
   auto fetch = [&](bool on, int32_t pos) -> uint32_t { return on ? (uint32_t)out[pos] : 0u; };
-  if (stored[b]) {
+  if (kd) {
     if (produced ? (n > cap64) : (n != cap64)) {
       if (gl == 0) status[b] = LZ_SIZE;
       return;

@@ -33,7 +33,7 @@ def _record_set(vals, per_batch, compression="lz4", level=9, block=16384, base=0
 
 
 @pytest.mark.parametrize("compression,level,block", [("lz4", 9, 16384), ("lz4", 1, 65536), ("lz4", 9, 4096),
-                                                     ("none", 0, 0)])
+                                                     ("none", 0, 0), ("gzip", 6, 0)])
 def test_plan_matches_host_decoder(compression, level, block):
     vals = _values(500, seed=1)
     rs = _record_set(vals, 37, compression, level, block or 65536)
@@ -63,9 +63,31 @@ def test_merge_and_trim():
 
 
 def test_unsupported_codec_falls_back():
-    rs = _record_set(_values(20), 10, "gzip")
+    """snappy / zstd batches (codecs 2 / 4) are decoded on the host: the planner refuses them."""
+    rs = bytearray(_record_set(_values(20), 20, "none"))
+    attrs = 12 + 9                                    # baseOffset, batchLength, leaderEpoch, magic, crc
+    rs[attrs + 1] = (rs[attrs + 1] & ~7) | 4          # compression codec = zstd
+    rs[12 + 5:12 + 9] = K.crc32c(bytes(rs[attrs:])).to_bytes(4, "big")
     with pytest.raises(KD.Unsupported):
-        KD.plan_fetch(rs, 0)
+        KD.plan_fetch(bytes(rs), 0)
+
+
+def test_gzip_plan_strips_header_and_reads_isize():
+    """gzip batches become one kind-2 block: the deflate data between the member header and the trailer, with the
+    trailer's ISIZE as the exact output size (inflated on the device by inflate.hip)."""
+    import zlib
+    vals = _values(300, seed=21)
+    rs = _record_set(vals, 70, "gzip") + _record_set(vals[:5], 5, "lz4", base=300)
+    plan = KD.plan_fetch(rs, 0)
+    kinds = plan.k_stored[:plan.nblk].tolist()
+    assert kinds.count(2) == 5 and 0 in kinds
+    for b in range(plan.nblk):
+        if kinds[b] == 2:
+            lo, n = int(plan.k_comp_off[b]), int(plan.k_comp_len[b])
+            raw = zlib.decompressobj(-15).decompress(rs[lo:lo + n])
+            assert len(raw) == int(plan.k_cap[b])
+    buf, s, e = KD.decode_on_host_like(np.frombuffer(rs, np.uint8), plan)
+    assert [buf[x:y].tobytes() for x, y in zip(s, e)] == vals + vals[:5]
 
 
 @pytest.mark.gpu
@@ -110,6 +132,45 @@ def test_device_decode_launch_sizing(gpu):
         buf = raw.buf.cpu().numpy()
         s, e = raw.offs[:-1].cpu().tolist(), raw.ends.cpu().tolist()
         assert raw.n == plan.nrec == 6000 and [buf[x:y].tobytes() for x, y in zip(s, e)] == vals
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level", [1, 6, 9])
+def test_device_inflate_matches_host(gpu, level):
+    """gzip record batches inflated on the GPU (inflate.hip) next to LZ4 and uncompressed batches in one fetch: fixed
+    and dynamic Huffman blocks, stored blocks (incompressible values), long matches and RLE runs."""
+    import zlib
+    rnd = random.Random(level)
+    vals = _values(2500, seed=30 + level)
+    vals += [bytes(rnd.getrandbits(8) for _ in range(rnd.choice([1, 100, 3000]))) for _ in range(40)]   # stored
+    vals += [b"a" * rnd.choice([3, 258, 1000, 40000]) for _ in range(20)]                                # RLE
+    vals += [b'{"x":1}'] * 50                                                                           # fixed codes
+    enc = lambda vs, per, codec, base: _record_set(vs, per, codec, level, 16384, base)               # noqa: E731
+    rs = (enc(vals[:1500], 60, "gzip", 0) + enc(vals[1500:2000], 40, "lz4", 1500) +
+          enc(vals[2000:2100], 25, "none", 2000) + enc(vals[2100:], 1, "gzip", 2100))
+    plan = KD.plan_fetch(rs, 0)
+    assert (plan.k_stored[:plan.nblk] == 2).sum() > 30
+    staging = torch.zeros(len(rs) + 64, dtype=torch.uint8).pin_memory()
+    staging[:len(rs)] = torch.frombuffer(bytearray(rs), dtype=torch.uint8)
+    dec = KD.DeviceRecordDecoder(gpu, chunks=2)
+    raw, ev = dec.decode(staging, plan)
+    torch.cuda.current_stream(gpu).wait_event(ev)
+    dec.check()
+    buf = raw.buf.cpu().numpy()
+    s, e = raw.offs[:-1].cpu().tolist(), raw.ends.cpu().tolist()
+    assert raw.n == len(vals) and [buf[x:y].tobytes() for x, y in zip(s, e)] == vals
+    # a corrupted deflate stream is reported (nonzero status), never read or written out of range
+    bad = bytearray(rs)
+    b0 = int(np.nonzero(plan.k_stored[:plan.nblk] == 2)[0][0])
+    lo = int(plan.k_comp_off[b0])
+    for k in range(lo + 5, lo + 40):
+        bad[k] ^= 0x5a
+    plan2 = KD.plan_fetch(bytes(bad), 0, verify_crc=False)
+    staging[:len(bad)] = torch.frombuffer(bad, dtype=torch.uint8)
+    raw2, ev2 = dec.decode(staging, plan2)
+    torch.cuda.current_stream(gpu).wait_event(ev2)
+    with pytest.raises(KD.DecodeError):
+        dec.check()
 
 
 def test_plan_many_matches_merged_plans():
