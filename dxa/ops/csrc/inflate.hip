@@ -27,7 +27,8 @@ constexpr int LBITS = 9;                // literal/length fast-table bits
 constexpr int DBITS = 8;                // distance fast-table bits
 constexpr int kWaitVm0 = 0xF70;         // s_waitcnt vmcnt(0) (gfx9 encoding)
 
-enum : int32_t { IF_OK = 0, IF_TRUNC = 1, IF_DIST = 2, IF_OVERFLOW = 3, IF_SIZE = 4, IF_CODE = 5, IF_BLOCK = 6 };
+// nonzero status = where the member failed (IF_CODE + n: which code check)
+enum : int32_t { IF_OK = 0, IF_TRUNC = 1, IF_DIST = 2, IF_OVERFLOW = 3, IF_SIZE = 4, IF_CODE = 10, IF_BLOCK = 6 };
 
 struct Tables {
   uint16_t lfast[1 << LBITS];
@@ -39,7 +40,7 @@ struct Tables {
   uint8_t lens[320];                     // code lengths of the block being built (literal/length then distance)
   uint8_t clens[20];                     // code-length code lengths
   uint16_t csorted[19];
-  uint16_t ccount[8];
+  uint16_t ccount[16];                   // build_table writes a count for every length 0..15
 };
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -52,13 +53,25 @@ __constant__ uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t c, int n) { return __builtin_bitreverse32(c) >> (32 - n); }
 
+// The 16 lanes of a member hand data to each other through the group's LDS tables (lane 0 writes a code length,
+// every lane reads it).  LDS operations of one wave execute in order, but without a fence the compiler may keep or
+// move LDS values across the hand-off as if no other lane wrote them — this makes every earlier LDS write of the
+// wave visible to every later LDS read (measured: without it, ~1 in 5000 members built its tables from stale LDS).
+__device__ __forceinline__ void lane_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Canonical Huffman tables from code lengths: count per length, symbols sorted by (length, symbol) and (fast != null)
 // a `bits`-bit direct table.  Returns false for an over-subscribed set.  All IG lanes call it; lane gl fills every
 // IG-th replica of a short code.
 __device__ bool build_table(const uint8_t* lens, int n, uint16_t* count, uint16_t* sorted, uint16_t* fast, int bits,
                             int maxlen, int gl) {
+  lane_sync();                               // the lengths were written by other lanes of the group
   if (fast) {
     for (int i = gl; i < (1 << bits); i += IG) fast[i] = 0;
+    lane_sync();
   }
   uint16_t cnt[16];
   for (int l = 0; l < 16; ++l) cnt[l] = 0;
@@ -94,6 +107,7 @@ __device__ bool build_table(const uint8_t* lens, int n, uint16_t* count, uint16_
       for (int k = gl; k < (1 << (bits - l)); k += IG) fast[r | ((uint32_t)k << l)] = e;
     }
   }
+  lane_sync();                               // tables complete before any lane decodes with them
   return true;
 }
 
@@ -216,11 +230,11 @@ __global__ __launch_bounds__(WG) void inflate_group_kernel(const uint8_t* __rest
       if (gl == 0) {
         for (int i = 0; i < 19; ++i) T.clens[i] = (uint8_t)cl[i];
       }
-      if (!build_table(T.clens, 19, T.ccount, T.csorted, nullptr, 0, 7, gl)) { rc = IF_CODE; break; }
+      if (!build_table(T.clens, 19, T.ccount, T.csorted, nullptr, 0, 7, gl)) { rc = IF_CODE + 0; break; }
       int i = 0;
       while (i < nlit + ndist) {
         const int sym = slow(T.ccount, T.csorted, 7);
-        if (sym < 0) { rc = IF_CODE; break; }
+        if (sym < 0) { rc = IF_CODE + 1; break; }
         if (sym < 16) {
           if (gl == 0) T.lens[i] = (uint8_t)sym;
           ++i;
@@ -228,7 +242,8 @@ __global__ __launch_bounds__(WG) void inflate_group_kernel(const uint8_t* __rest
         }
         int rep, val = 0;
         if (sym == 16) {
-          if (i == 0) { rc = IF_CODE; break; }
+          if (i == 0) { rc = IF_CODE + 2; break; }
+          lane_sync();
           val = T.lens[i - 1];
           rep = 3 + (int)bits(2);
         } else if (sym == 17) {
@@ -236,23 +251,24 @@ __global__ __launch_bounds__(WG) void inflate_group_kernel(const uint8_t* __rest
         } else {
           rep = 11 + (int)bits(7);
         }
-        if (i + rep > nlit + ndist) { rc = IF_CODE; break; }
+        if (i + rep > nlit + ndist) { rc = IF_CODE + 3; break; }
         for (int k = gl; k < rep; k += IG) T.lens[i + k] = (uint8_t)val;
         i += rep;
       }
       if (rc != IF_OK) break;
-      if (T.lens[256] == 0) { rc = IF_CODE; break; }   // no end-of-block code
+      lane_sync();
+      if (T.lens[256] == 0) { rc = IF_CODE + 4; break; }   // no end-of-block code
     }
     if (!build_table(T.lens, nlit, T.lcount, T.lsorted, T.lfast, LBITS, 15, gl) ||
         !build_table(T.lens + nlit, ndist, T.dcount, T.dsorted, T.dfast, DBITS, 15, gl)) {
-      rc = IF_CODE;
+      rc = IF_CODE + 5;
       break;
     }
     // ---- symbols
     for (;;) {
       if ((int64_t)ip * 8 - bc > (int64_t)lim * 8) { rc = IF_TRUNC; break; }
       const int sym = decode(T.lfast, LBITS, T.lcount, T.lsorted);
-      if (sym < 0) { rc = IF_CODE; break; }
+      if (sym < 0) { rc = IF_CODE + 6; break; }
       if (sym < 256) {
         if (op >= cap) { rc = IF_OVERFLOW; break; }
         if (gl == 0) out[op] = (uint8_t)sym;
@@ -261,10 +277,10 @@ __global__ __launch_bounds__(WG) void inflate_group_kernel(const uint8_t* __rest
       }
       if (sym == 256) break;
       const int li = sym - 257;
-      if (li >= 29) { rc = IF_CODE; break; }
+      if (li >= 29) { rc = IF_CODE + 7; break; }
       const int32_t len = kLenBase[li] + (int32_t)bits(kLenExtra[li]);
       const int ds = decode(T.dfast, DBITS, T.dcount, T.dsorted);
-      if (ds < 0 || ds >= 30) { rc = IF_CODE; break; }
+      if (ds < 0 || ds >= 30) { rc = IF_CODE + 8; break; }
       const int32_t dist = kDistBase[ds] + (int32_t)bits(kDistExtra[ds]);
       if (dist > op) { rc = IF_DIST; break; }
       if (len > cap - op) { rc = IF_OVERFLOW; break; }
