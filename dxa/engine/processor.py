@@ -13,6 +13,7 @@ datax/processor/CommonProcessorFactory.scala:42-660) re-designed for one MI355X 
 """
 from __future__ import annotations
 
+import copy
 import datetime as _dt
 import json
 import logging
@@ -301,29 +302,31 @@ class Processor:
         views: Dict[str, Table] = {}
         t0 = time.perf_counter()
         if self.transform is not None:
-            from ..sql.parser import parse_query
             live = None if self.keep_views else self._live_statements()
-            for k, cmd in enumerate(self.transform.commands):
-                if cmd.command_type == COMMAND_COMMAND:
-                    self._run_command(cmd.text)
-                    continue
-                if live is not None and k not in live:
-                    continue                       # a view nothing reads: Spark never evaluates it either
-                q = self._parsed.get(cmd.text)
-                if q is None:
-                    q = self._parsed[cmd.text] = parse_query(cmd.text)     # parsed once, reused every batch
-                ts = time.perf_counter() if _SYNC_STAGES else 0.0
-                with tracing.stage(f"sql:{cmd.name}"):
-                    result = execute(q, cat, ctx)
-                if _SYNC_STAGES:
-                    self._sync()
-                    self.stage_times[f"sql:{cmd.name}"] = time.perf_counter() - ts
-                st = self.state_tables.get(cmd.name)
-                if st is not None:
-                    self._complete_inflight()      # the previous batch's state flip must be durable first
-                    result = st.overwrite(result)
-                cat.register(cmd.name, result)
-                views[cmd.name] = result
+            cmds = self.transform.commands
+            for step in self._view_schedule(live):
+                if len(step) > 1:
+                    # independent views: each on a side HIP stream, forked from and joined back to this stream
+                    results = self._run_concurrent([cmds[k] for k in step], cat, ctx)
+                else:
+                    cmd = cmds[step[0]]
+                    if cmd.command_type == COMMAND_COMMAND:
+                        self._run_command(cmd.text)
+                        continue
+                    ts = time.perf_counter() if _SYNC_STAGES else 0.0
+                    with tracing.stage(f"sql:{cmd.name}"):
+                        results = [execute(self._query(cmd), cat, ctx)]
+                    if _SYNC_STAGES:
+                        self._sync()
+                        self.stage_times[f"sql:{cmd.name}"] = time.perf_counter() - ts
+                for k, result in zip(step, results):
+                    cmd = cmds[k]
+                    st = self.state_tables.get(cmd.name)
+                    if st is not None:
+                        self._complete_inflight()      # the previous batch's state flip must be durable first
+                        result = st.overwrite(result)
+                    cat.register(cmd.name, result)
+                    views[cmd.name] = result
         self._sync()
         self.stage_times["transform"] = time.perf_counter() - t0
         # outputs: device half staged here (filters + async D2H into pinned memory), host half (JSON rendering +
@@ -353,6 +356,122 @@ class Processor:
             self._sync()
             self.stage_times["output"] = time.perf_counter() - t1
         return fl.metrics
+
+    def _query(self, cmd):
+        q = self._parsed.get(cmd.text)
+        if q is None:
+            from ..sql.parser import parse_query
+            q = self._parsed[cmd.text] = parse_query(cmd.text)         # parsed once, reused every batch
+        return q
+
+    def _concurrent_views(self) -> bool:
+        """Run independent views concurrently (``datax.job.process.concurrentviews``, env ``DXA_VIEW_STREAMS``)?
+        Only on the GPU and at world size 1: views at N ranks issue RCCL collectives (key shuffles, broadcasts),
+        whose order must match on every rank, so there they stay in statement order."""
+        env = os.environ.get("DXA_VIEW_STREAMS")
+        on = env != "0" if env is not None else \
+            self.settings.get_bool(S.PROCESS_PREFIX + "concurrentviews", False)
+        return on and self.device.type == "cuda" and not P.active()
+
+    def _view_schedule(self, live: Optional[set]) -> List[List[int]]:
+        """The transform's statements as steps; a step of several statements runs them concurrently.
+
+        Sequential mode: one statement per step, in text order.  Concurrent mode (the reference runs outputs and
+        init work in parallel futures, CommonProcessorFactory.scala:43-73,114-117; here independent *views* also
+        overlap, each on its own HIP stream): a statement's level is one more than the levels of the earlier
+        statements whose names it reads (read-after-write) and of the earlier statements that read its own name
+        (write-after-read: a statement that reads an accumulator's previous state runs before the accumulator is
+        overwritten).  Steps run level by level; the views of a level run together, and accumulator (state-table)
+        statements — whose overwrite completes the in-flight batch — run alone after them.  Commands (SET, CREATE
+        TABLE) keep their place ahead of everything (they produce no view)."""
+        key = ("sched", None if live is None else tuple(sorted(live)), self._concurrent_views())
+        if getattr(self, "_sched", (None,))[0] == key:
+            return self._sched[1]
+        cmds = self.transform.commands
+        if not key[2]:
+            steps = [[k] for k, c in enumerate(cmds)
+                     if c.command_type == COMMAND_COMMAND or live is None or k in live]
+            self._sched = (key, steps)
+            return steps
+        import re
+        level: Dict[str, int] = {}
+        reads: List[Tuple[int, set]] = []
+        lv: Dict[int, int] = {}
+        commands = []
+        for k, c in enumerate(cmds):
+            if c.command_type == COMMAND_COMMAND:
+                commands.append(k)
+                continue
+            if live is not None and k not in live:
+                continue
+            nm = c.name.lower()
+            words = {w.lower() for w in re.findall(r"[A-Za-z_][A-Za-z0-9_]*", c.text)}
+            lk = 0
+            for w in words:
+                if w in level and w != nm:
+                    lk = max(lk, level[w] + 1)
+            for j, wj in reads:
+                if nm in wj:
+                    lk = max(lk, lv[j] + 1)
+            if nm in level:                       # a redefinition: after the earlier definition
+                lk = max(lk, level[nm] + 1)
+            lv[k] = lk
+            level[nm] = lk
+            reads.append((k, words))
+        steps = [[k] for k in commands]
+        for L in sorted(set(lv.values())):
+            ks = [k for k in sorted(lv) if lv[k] == L]
+            plain = [k for k in ks if cmds[k].name not in self.state_tables]
+            if plain:
+                steps.append(plain)
+            steps += [[k] for k in ks if cmds[k].name in self.state_tables]
+        self._sched = (key, steps)
+        return steps
+
+    def _run_concurrent(self, cmds, cat, ctx) -> List[Table]:
+        """Fork-join of independent views: each statement runs on a worker thread with its own HIP stream.  The
+        side streams first wait for this stream (the views' inputs), and this stream waits for every side stream
+        before any result is used; so blocks a side stream allocates are reused only behind those waits.  The
+        host threads overlap one view's Python planning with another's synchronising reads (the GIL is released
+        while a thread waits on the device)."""
+        dev = self.device
+        main = torch.cuda.current_stream(dev)
+        if getattr(self, "_view_pool", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._view_pool = ThreadPoolExecutor(max_workers=4, thread_name_prefix="dxa-view")
+            self._view_streams = [torch.cuda.Stream(dev) for _ in range(4)]
+        fork = torch.cuda.Event()
+        fork.record(main)
+        times = self.stage_times
+
+        def run(slot, cmd):
+            s = self._view_streams[slot % len(self._view_streams)]
+            torch.cuda.set_device(dev)
+            s.wait_event(fork)
+            with torch.cuda.stream(s):
+                ts = time.perf_counter()
+                with tracing.stage(f"sql:{cmd.name}"):
+                    # a context per branch: execute() swaps ctx.catalog for WITH / sub-query scopes
+                    out = execute(self._query(cmd), cat, copy.copy(ctx))
+                if _SYNC_STAGES:
+                    s.synchronize()
+                    times[f"sql:{cmd.name}"] = time.perf_counter() - ts
+            return out
+
+        for cmd in cmds:
+            self._query(cmd)                      # parse on this thread (the cache is a plain dict)
+        futures = [self._view_pool.submit(run, i, cmd) for i, cmd in enumerate(cmds)]
+        results, err = [], None
+        for f in futures:
+            try:
+                results.append(f.result())
+            except BaseException as e:  # noqa: BLE001 — join every branch before re-raising
+                err = err or e
+        for s in self._view_streams[:len(cmds)]:
+            main.wait_stream(s)
+        if err is not None:
+            raise err
+        return results
 
     def _live_statements(self) -> Optional[set]:
         """Indices of the transform's query statements whose results can reach an output or a state table.

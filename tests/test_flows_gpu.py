@@ -118,3 +118,25 @@ def test_flow_outputs_gpu_match_cpu(gpu, variant, tmp_path):
         _close(sorted(state_gpu[name], key=_key), sorted(state_cpu[name], key=_key), f"state.{name}")
     if variant in ("full",):
         assert state_gpu["DeviceState"], "accumulator never updated"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["full", "window"])
+def test_concurrent_views_match_sequential(gpu, variant, tmp_path, monkeypatch):
+    """Independent views on side HIP streams (DXA_VIEW_STREAMS=1) give the same outputs and accumulator as the
+    statement-order run on one stream; the schedule really has a concurrent step."""
+    import time
+    from dxa.engine.processor import Processor
+    clock0 = (int(time.time()) - 3600) * 1_000_000
+    batches = _batches(gpu, clock0)
+    monkeypatch.setenv("DXA_VIEW_STREAMS", "1")
+    p = Processor(_settings(variant, tmp_path / "probe"), gpu)
+    steps = p._view_schedule(p._live_statements())
+    if variant == "full":
+        assert any(len(s) > 1 for s in steps), steps
+    got_c, state_c = _run(variant, gpu, batches, tmp_path / "conc" / "w")
+    monkeypatch.setenv("DXA_VIEW_STREAMS", "0")
+    got_s, state_s = _run(variant, gpu, batches, tmp_path / "seq" / "w")
+    _compare_outputs(got_c, got_s)
+    for name in state_c:
+        _close(sorted(state_c[name], key=_key), sorted(state_s[name], key=_key), f"state.{name}")
