@@ -203,8 +203,22 @@ class WindowStore:
         c = self.conf
         E = batch_time_us - c.watermark_us
         S = E - c.max_window_us
-        kept = self._range(projected, E, None)
-        kept = _compact_table(kept)
+        cur = None
+        if projected.length:
+            # one host read for the common case (every event valid and not late): the batch's pane statistics and
+            # the late-event check come back together; otherwise filter, then take the kept rows' statistics
+            ts, ok = self._ts(projected)
+            big = torch.iinfo(torch.int64).max
+            lo_, hi_, nok, nkeep = torch.stack([torch.where(ok, ts, torch.full_like(ts, big)).min(),
+                                                torch.where(ok, ts, torch.full_like(ts, -big)).max(),
+                                                ok.sum(), (ok & (ts >= E)).sum()]).tolist()
+            if int(nkeep) == projected.length:
+                kept = _compact_table(projected)
+                cur = Pane(batch_time_us, kept, int(lo_), int(hi_), True)
+            else:
+                kept = _compact_table(projected.filter(ok & (ts >= E)))
+        else:
+            kept = _compact_table(projected)
         kept.dist = projected.dist
         cut = batch_time_us - (c.watermark_us + c.max_window_us)
         for t in [t for t in self.past if t <= cut]:
@@ -214,7 +228,8 @@ class WindowStore:
             live = set(self.past)
             for k in [k for k, ent in self.blocks.items() if not live.issuperset(ent[0])]:
                 del self.blocks[k]
-        cur = self._pane(batch_time_us, kept)
+        if cur is None:
+            cur = self._pane(batch_time_us, kept)
         if len(self.past) > 1 or (not c.legacy_union_quirk and self.past):
             panes = [cur] + list(self.past.values())
         else:
