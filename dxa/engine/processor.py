@@ -366,12 +366,11 @@ class Processor:
 
     def _concurrent_views(self) -> bool:
         """Run independent views concurrently (``datax.job.process.concurrentviews``, env ``DXA_VIEW_STREAMS``)?
-        Only on the GPU and at world size 1: views at N ranks issue RCCL collectives (key shuffles, broadcasts),
-        whose order must match on every rank, so there they stay in statement order."""
+        On the GPU each branch gets a side HIP stream; on the CPU only a thread.  At N ranks each branch slot also
+        gets its own communicator (``parallel.branch_groups``)."""
         env = os.environ.get("DXA_VIEW_STREAMS")
-        on = env != "0" if env is not None else \
+        return env != "0" if env is not None else \
             self.settings.get_bool(S.PROCESS_PREFIX + "concurrentviews", False)
-        return on and self.device.type == "cuda" and not P.active()
 
     def _view_schedule(self, live: Optional[set]) -> List[List[int]]:
         """The transform's statements as steps; a step of several statements runs them concurrently.
@@ -433,42 +432,58 @@ class Processor:
         side streams first wait for this stream (the views' inputs), and this stream waits for every side stream
         before any result is used; so blocks a side stream allocates are reused only behind those waits.  The
         host threads overlap one view's Python planning with another's synchronising reads (the GIL is released
-        while a thread waits on the device)."""
+        while a thread waits on the device).  At N ranks branch ``i`` issues its collectives (key shuffles,
+        broadcasts) on communicator ``i``, so every communicator sees the same sequence on every rank."""
         dev = self.device
-        main = torch.cuda.current_stream(dev)
+        cuda = dev.type == "cuda"
+        nslots = 4
         if getattr(self, "_view_pool", None) is None:
             from concurrent.futures import ThreadPoolExecutor
-            self._view_pool = ThreadPoolExecutor(max_workers=4, thread_name_prefix="dxa-view")
-            self._view_streams = [torch.cuda.Stream(dev) for _ in range(4)]
-        fork = torch.cuda.Event()
-        fork.record(main)
+            self._view_pool = ThreadPoolExecutor(max_workers=nslots, thread_name_prefix="dxa-view")
+            self._view_streams = [torch.cuda.Stream(dev) for _ in range(nslots)] if cuda else []
+        groups = P.branch_groups(nslots) if P.active() else [None] * nslots
+        main = torch.cuda.current_stream(dev) if cuda else None
+        fork = None
+        if cuda:
+            fork = torch.cuda.Event()
+            fork.record(main)
         times = self.stage_times
 
         def run(slot, cmd):
-            s = self._view_streams[slot % len(self._view_streams)]
-            torch.cuda.set_device(dev)
-            s.wait_event(fork)
-            with torch.cuda.stream(s):
+            import contextlib
+            s = self._view_streams[slot] if cuda else None
+            with contextlib.ExitStack() as es:
+                if cuda:
+                    torch.cuda.set_device(dev)
+                    s.wait_event(fork)
+                    es.enter_context(torch.cuda.stream(s))
+                if groups[slot] is not None:
+                    es.enter_context(P.use_branch(groups[slot]))
                 ts = time.perf_counter()
                 with tracing.stage(f"sql:{cmd.name}"):
                     # a context per branch: execute() swaps ctx.catalog for WITH / sub-query scopes
                     out = execute(self._query(cmd), cat, copy.copy(ctx))
-                if _SYNC_STAGES:
+                if _SYNC_STAGES and cuda:
                     s.synchronize()
                     times[f"sql:{cmd.name}"] = time.perf_counter() - ts
             return out
 
         for cmd in cmds:
             self._query(cmd)                      # parse on this thread (the cache is a plain dict)
-        futures = [self._view_pool.submit(run, i, cmd) for i, cmd in enumerate(cmds)]
         results, err = [], None
-        for f in futures:
-            try:
-                results.append(f.result())
-            except BaseException as e:  # noqa: BLE001 — join every branch before re-raising
-                err = err or e
-        for s in self._view_streams[:len(cmds)]:
-            main.wait_stream(s)
+        for base in range(0, len(cmds), nslots):  # at most one branch per slot (stream, communicator) at a time
+            chunk = cmds[base:base + nslots]
+            futures = [self._view_pool.submit(run, i, cmd) for i, cmd in enumerate(chunk)]
+            for f in futures:
+                try:
+                    results.append(f.result())
+                except BaseException as e:  # noqa: BLE001 — join every branch before re-raising
+                    err = err or e
+            if err is not None:
+                break
+        if cuda:
+            for s in self._view_streams[:len(cmds)]:
+                main.wait_stream(s)
         if err is not None:
             raise err
         return results

@@ -17,6 +17,7 @@ tests run the same code over gloo.
 """
 from __future__ import annotations
 
+import threading
 from typing import List, Optional, Tuple
 
 import torch
@@ -25,6 +26,8 @@ _GROUP = None
 _WORLD = 1
 _RANK = 0
 _DEVICE = None
+_TLS = threading.local()          # per-thread communicator override (concurrent views)
+_BRANCH_GROUPS: List = []
 
 PARTITIONED = "partitioned"
 HASHED = "hashed"
@@ -43,6 +46,42 @@ def init(group=None, device=None):
 def shutdown():
     global _GROUP, _WORLD, _RANK
     _GROUP, _WORLD, _RANK = None, 1, 0
+    _BRANCH_GROUPS.clear()
+
+
+def group():
+    """The communicator of this thread's collectives: the job's group, or the branch group a concurrent view
+    runs on (``use_branch``)."""
+    g = getattr(_TLS, "group", None)
+    return g if g is not None else _GROUP
+
+
+def branch_groups(n: int) -> List:
+    """``n`` extra communicators over the job's ranks, created once, in the same order on every rank (a
+    collective).  Concurrent views run branch ``i`` of a level on group ``i``: each group sees its branch's
+    collectives in program order on every rank, so branches on different threads cannot interleave one
+    communicator's operations differently across ranks.  With RCCL each group is its own communicator (own
+    channels over xGMI), so the branches' exchanges also overlap on the links."""
+    import torch.distributed as dist
+    ranks = list(range(_WORLD))
+    while len(_BRANCH_GROUPS) < n:
+        _BRANCH_GROUPS.append(dist.new_group(ranks=ranks, backend=dist.get_backend(_GROUP)))
+    return _BRANCH_GROUPS[:n]
+
+
+class use_branch:
+    """``with use_branch(g):`` — collectives issued by this thread go to ``g``."""
+
+    def __init__(self, g):
+        self.g = g
+
+    def __enter__(self):
+        self.prev = getattr(_TLS, "group", None)
+        _TLS.group = self.g
+        return self.g
+
+    def __exit__(self, *exc):
+        _TLS.group = self.prev
 
 
 def active() -> bool:

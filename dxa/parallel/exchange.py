@@ -17,8 +17,8 @@ import torch.distributed as dist
 
 
 def _g():
-    from . import _GROUP
-    return _GROUP
+    from . import group
+    return group()
 
 
 def _w():

@@ -15,9 +15,9 @@ def _names(p, steps):
     return [[cmds[k].name for k in s] for s in steps]
 
 
-def test_sequential_off_gpu(tmp_path):
+def test_sequential_by_default(tmp_path):
     p = _proc(tmp_path, "full")
-    assert not p._concurrent_views()                  # CPU: statement order
+    assert not p._concurrent_views()                  # default: statement order
     steps = p._view_schedule(p._live_statements())
     assert all(len(s) == 1 for s in steps)
     assert [k for s in steps for k in s] == sorted(k for s in steps for k in s)
