@@ -364,13 +364,18 @@ class Processor:
             q = self._parsed[cmd.text] = parse_query(cmd.text)         # parsed once, reused every batch
         return q
 
-    def _concurrent_views(self) -> bool:
-        """Run independent views concurrently (``datax.job.process.concurrentviews``, env ``DXA_VIEW_STREAMS``)?
-        On the GPU each branch gets a side HIP stream; on the CPU only a thread.  At N ranks each branch slot also
-        gets its own communicator (``parallel.branch_groups``)."""
+    def _concurrent_views(self) -> Optional[str]:
+        """How independent views run (``datax.job.process.concurrentviews``, env ``DXA_VIEW_STREAMS``):
+        ``None`` — one after another on the batch stream; ``"streams"`` — one after another on this thread, each on
+        its own side HIP stream (a view's synchronising reads wait only for its own kernels, and its kernels overlap
+        the next view's planning); ``"threads"`` — a worker thread per view as well (each thread's collectives on
+        its own communicator at N ranks).  ``true`` selects ``streams``."""
         env = os.environ.get("DXA_VIEW_STREAMS")
-        return env != "0" if env is not None else \
-            self.settings.get_bool(S.PROCESS_PREFIX + "concurrentviews", False)
+        v = (env if env is not None else self.settings.get(S.PROCESS_PREFIX + "concurrentviews") or "false")
+        v = v.strip().lower()
+        if v in ("0", "false", "off", "no", ""):
+            return None
+        return "threads" if v == "threads" else "streams"
 
     def _view_schedule(self, live: Optional[set]) -> List[List[int]]:
         """The transform's statements as steps; a step of several statements runs them concurrently.
@@ -428,20 +433,23 @@ class Processor:
         return steps
 
     def _run_concurrent(self, cmds, cat, ctx) -> List[Table]:
-        """Fork-join of independent views: each statement runs on a worker thread with its own HIP stream.  The
-        side streams first wait for this stream (the views' inputs), and this stream waits for every side stream
-        before any result is used; so blocks a side stream allocates are reused only behind those waits.  The
-        host threads overlap one view's Python planning with another's synchronising reads (the GIL is released
-        while a thread waits on the device).  At N ranks branch ``i`` issues its collectives (key shuffles,
-        broadcasts) on communicator ``i``, so every communicator sees the same sequence on every rank."""
+        """Fork-join of independent views: each statement runs on its own side HIP stream (``threads`` mode: on a
+        worker thread too).  The side streams first wait for this stream (the views' inputs), and this stream waits
+        for every side stream before any result is used; so blocks a side stream allocates are reused only behind
+        those waits.  Worker threads overlap one view's Python planning with another's synchronising reads (the GIL
+        is released while a thread waits on the device) — measured slower than ``streams`` on the full flow
+        (profiles/view_streams), as every PyTorch call hands the GIL over.  At N ranks branch ``i`` of a threaded
+        level issues its collectives (key shuffles, broadcasts) on communicator ``i``, so every communicator sees
+        the same sequence on every rank."""
         dev = self.device
         cuda = dev.type == "cuda"
         nslots = 4
+        threads = self._concurrent_views() == "threads"
         if getattr(self, "_view_pool", None) is None:
             from concurrent.futures import ThreadPoolExecutor
             self._view_pool = ThreadPoolExecutor(max_workers=nslots, thread_name_prefix="dxa-view")
             self._view_streams = [torch.cuda.Stream(dev) for _ in range(nslots)] if cuda else []
-        groups = P.branch_groups(nslots) if P.active() else [None] * nslots
+        groups = P.branch_groups(nslots) if P.active() and threads else [None] * nslots
         main = torch.cuda.current_stream(dev) if cuda else None
         fork = None
         if cuda:
@@ -471,6 +479,14 @@ class Processor:
         for cmd in cmds:
             self._query(cmd)                      # parse on this thread (the cache is a plain dict)
         results, err = [], None
+        if not threads:
+            try:
+                results = [run(i % nslots, cmd) for i, cmd in enumerate(cmds)]
+            finally:
+                if cuda:
+                    for s in self._view_streams[:len(cmds)]:
+                        main.wait_stream(s)
+            return results
         for base in range(0, len(cmds), nslots):  # at most one branch per slot (stream, communicator) at a time
             chunk = cmds[base:base + nslots]
             futures = [self._view_pool.submit(run, i, cmd) for i, cmd in enumerate(chunk)]

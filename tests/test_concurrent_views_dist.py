@@ -74,7 +74,7 @@ def _run(rank, world, work, batches):
 def _worker(rank, world, port, work, batches, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                          DXA_VIEW_STREAMS="1")
+                          DXA_VIEW_STREAMS="threads")
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from dxa import parallel as P

@@ -121,15 +121,16 @@ def test_flow_outputs_gpu_match_cpu(gpu, variant, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["streams", "threads"])
 @pytest.mark.parametrize("variant", ["full", "window"])
-def test_concurrent_views_match_sequential(gpu, variant, tmp_path, monkeypatch):
-    """Independent views on side HIP streams (DXA_VIEW_STREAMS=1) give the same outputs and accumulator as the
-    statement-order run on one stream; the schedule really has a concurrent step."""
+def test_concurrent_views_match_sequential(gpu, variant, mode, tmp_path, monkeypatch):
+    """Independent views on side HIP streams (DXA_VIEW_STREAMS=streams / threads) give the same outputs and
+    accumulator as the statement-order run on one stream; the schedule really has a concurrent step."""
     import time
     from dxa.engine.processor import Processor
     clock0 = (int(time.time()) - 3600) * 1_000_000
     batches = _batches(gpu, clock0)
-    monkeypatch.setenv("DXA_VIEW_STREAMS", "1")
+    monkeypatch.setenv("DXA_VIEW_STREAMS", mode)
     p = Processor(_settings(variant, tmp_path / "probe"), gpu)
     steps = p._view_schedule(p._live_statements())
     if variant == "full":
