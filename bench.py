@@ -30,6 +30,7 @@ With N>1 ranks, per-GPU work is fixed (weak scaling); GROUP BYs are two-phase ov
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -147,7 +148,7 @@ def main():
         native.lib()
     from dxa.engine.processor import Processor, RawBatch
     from dxa.models import iot
-    from dxa.simulate.datagen import generate, generate_begin, generate_finish
+    from dxa.simulate.datagen import generate, generate_begin, generate_finish, generate_slotted
     from dxa import parallel
 
     if world > 1:
@@ -289,6 +290,17 @@ def main():
             def gen_args(j):
                 return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=batch_time(j) // 1000 - 1000,
                             step_us=max(1, interval_us // E))
+            if os.environ.get("DXA_GEN_SLOTTED", "1") != "0":
+                # one render launch per batch into fixed-size slots (no length pass, scan or host size read)
+                ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
+                with ctx:
+                    db, do, de = generate_slotted(prog, E, device, **gen_args(i))
+                    ev = None
+                    if side is not None:
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                staged[i] = (RawBatch(db, do, E, ends=de), None, ev)
+                return
             if side is None:
                 staged[i] = generate(prog, E, device, **gen_args(i)) + (None,)
                 return

@@ -43,6 +43,8 @@ struct GenArgs {
   const int64_t* offs;    // write pass: [n+1]
   uint8_t* out;           // write pass
   int64_t* lens;          // length pass
+  int64_t stride;         // slotted pass: bytes per event slot (16-B multiple, >= the program's length bound)
+  int64_t* ends;          // slotted pass: [n] record ends (offs [n+1] are the slot starts)
 };
 
 __device__ __forceinline__ uint64_t rnd(uint64_t seed, int64_t row, int k) {
@@ -219,6 +221,21 @@ __global__ __launch_bounds__(256) void gen_write_kernel(GenArgs g) {
   render<true>(g, t, i, g.out + g.offs[i]);
 }
 
+// One pass, no length pass or scan: event i renders into its own 16-B aligned slot [i*stride, i*stride+len) (the
+// host bounds every op's text, so len <= stride) and publishes its slot start and record end.  The parser takes
+// (offs, ends) records with gaps as it does for Kafka values, so the batch needs no host read of its total size.
+__global__ __launch_bounds__(256) void gen_slot_kernel(GenArgs g) {
+  extern __shared__ uint64_t smem[];
+  const Tables t = stage_tables(g, smem);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.n) return;
+  const int64_t start = i * g.stride;
+  const int64_t len = render<true>(g, t, i, g.out + start);
+  const_cast<int64_t*>(g.offs)[i] = start;
+  g.ends[i] = start + (len <= g.stride ? len : 0);     // an over-long record (a bound bug) becomes an empty row
+  if (i == g.n - 1) const_cast<int64_t*>(g.offs)[g.n] = g.n * g.stride;
+}
+
 size_t lds_bytes(int32_t nops, int32_t pool_words, int32_t table_ints) {
   return (size_t)nops * sizeof(Op) + (size_t)pool_words * 8 + (size_t)table_ints * 4;
 }
@@ -236,7 +253,7 @@ DXA_API int dxa_datagen_lengths(const void* ops, int32_t nops, const uint8_t* po
   const size_t lds = lds_bytes(nops, pool_words, table_ints);
   if (lds > kMaxLds) return (int)hipErrorInvalidValue;
   GenArgs g{(const Op*)ops, nops, pool, table, pool_words, table_ints, seed, row0, n, base_ms, step_us, nullptr,
-            nullptr, lens};
+            nullptr, lens, 0, nullptr};
   hipLaunchKernelGGL(gen_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, g);
   return (int)hipGetLastError();
 }
@@ -248,7 +265,21 @@ DXA_API int dxa_datagen_write(const void* ops, int32_t nops, const uint8_t* pool
   const size_t lds = lds_bytes(nops, pool_words, table_ints);
   if (lds > kMaxLds) return (int)hipErrorInvalidValue;
   GenArgs g{(const Op*)ops, nops, pool, table, pool_words, table_ints, seed, row0, n, base_ms, step_us, offs, out,
-            nullptr};
+            nullptr, 0, nullptr};
   hipLaunchKernelGGL(gen_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, g);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_datagen_slotted(const void* ops, int32_t nops, const uint8_t* pool, int32_t pool_words,
+                                const int32_t* table, int32_t table_ints, uint64_t seed, int64_t row0, int64_t n,
+                                int64_t base_ms, int64_t step_us, int64_t stride, int64_t* offs, int64_t* ends,
+                                uint8_t* out, void* st) {
+  if (n <= 0) return 0;
+  if (stride <= 0 || (stride & 15)) return (int)hipErrorInvalidValue;
+  const size_t lds = lds_bytes(nops, pool_words, table_ints);
+  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
+  GenArgs g{(const Op*)ops, nops, pool, table, pool_words, table_ints, seed, row0, n, base_ms, step_us, offs, out,
+            nullptr, stride, ends};
+  hipLaunchKernelGGL(gen_slot_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, g);
   return (int)hipGetLastError();
 }

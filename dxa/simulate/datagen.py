@@ -36,6 +36,8 @@ N.register_sigs({
                             N.c_i64, N.c_i64, N.c_p, N.c_p],
     "dxa_datagen_write": [N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, ctypes.c_uint64, N.c_i64, N.c_i64, N.c_i64,
                           N.c_i64, N.c_p, N.c_p, N.c_p],
+    "dxa_datagen_slotted": [N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, ctypes.c_uint64, N.c_i64, N.c_i64,
+                            N.c_i64, N.c_i64, N.c_i64, N.c_p, N.c_p, N.c_p, N.c_p],
 })
 
 
@@ -71,6 +73,36 @@ class GenProgram:
 
     def op(self, code, a=0, b=0, x=0, y=0):
         self.ops.append((code, a, b, x, y))
+
+    def max_len(self) -> int:
+        """Upper bound of one rendered event's length: every op at its longest text (a NULLP op may only shorten
+        the ops it skips, so it adds its own 4 bytes).  Sizes the slots of ``generate_slotted``."""
+        import math
+        total = 0
+        for code, a, b, x, y in self.ops:
+            if code == OP_LIT:
+                total += b
+            elif code == OP_INT:
+                total += max(len(str(x)), len(str(y))) if x <= y else 21
+            elif code == OP_DBL:
+                lo = struct.unpack("<d", struct.pack("<q", x))[0]
+                hi = struct.unpack("<d", struct.pack("<q", y))[0]
+                m = max(abs(lo), abs(hi))
+                ip = len(str(int(m) + 1)) if math.isfinite(m) and m < 1e18 else 20
+                total += 1 + ip + 1 + a                 # sign, integer part (+1 for rounding up), '.', decimals
+            elif code == OP_CHOICE:
+                total += max((ln for _, ln in self.table[a:a + b]), default=0)
+            elif code == OP_TS_MS:
+                total += 20
+            elif code == OP_TS_STR:
+                total += 40
+            elif code == OP_BOOL:
+                total += 5
+            elif code == OP_ALNUM:
+                total += a + 2
+            elif code == OP_NULLP:
+                total += 4
+        return total
 
     # -- device upload --------------------------------------------------------------------------------------------
     def device(self, device):
@@ -286,6 +318,33 @@ def generate_finish(p: PendingGen) -> Tuple[torch.Tensor, torch.Tensor]:
            p.seed & (2**64 - 1), p.row0, p.n, p.base_ms, p.step_us, N.ptr(p.offs), N.ptr(buf),
            N.stream_handle(p.device))
     return buf, p.offs
+
+
+def generate_slotted(prog: GenProgram, n: int, device, seed: int = 1, row0: int = 0,
+                     base_ms: Optional[int] = None, step_us: int = 0):
+    """Render n events in ONE device pass → (buf, offs [n+1], ends [n]): event i lands in its own 16-B aligned slot
+    of ``prog.max_len()`` bytes (rounded up), so there is no length pass, no scan and no host read of the total size
+    before the render — the whole generation is one launch queued on the current stream.  Records have gaps between
+    them, which the parser takes as it does Kafka values (``RawBatch.ends``).  Bytes are identical to ``generate``'s
+    records.  On the CPU this is ``generate_cpu`` with ends = offs[1:]."""
+    device = torch.device(device)
+    base_ms = int(time.time() * 1000) if base_ms is None else base_ms
+    if device.type != "cuda":
+        buf, offs = generate_cpu(prog, n, seed, row0, base_ms, step_us)
+        return buf, offs, offs[1:].clone()
+    stride = max(16, (prog.max_len() + 15) // 16 * 16)
+    ops, pool, tab = prog.device(device)
+    buf = torch.empty(n * stride + 16, dtype=torch.uint8, device=device)
+    buf[n * stride:].zero_()     # the parser's read window past the last slot
+    offs = torch.empty(n + 1, dtype=torch.int64, device=device)
+    ends = torch.empty(max(n, 1), dtype=torch.int64, device=device)[:n]
+    if n == 0:
+        offs.zero_()
+        return buf, offs, ends
+    N.call("dxa_datagen_slotted", N.ptr(ops), len(prog.ops), N.ptr(pool), pool.numel() // 8, N.ptr(tab), tab.numel(),
+           seed & (2**64 - 1), row0, n, base_ms, step_us, stride, N.ptr(offs), N.ptr(ends), N.ptr(buf),
+           N.stream_handle(device))
+    return buf, offs, ends
 
 
 M64 = (1 << 64) - 1

@@ -351,6 +351,27 @@ def test_datagen_matches_cpu(gpu, name):
         assert not gb[total:].cpu().any()
 
 
+@pytest.mark.parametrize("name", ["iot", "spark", "simulated"])
+def test_datagen_slotted_matches_cpu(gpu, name):
+    """The one-pass slotted generator (fixed-size 16-B aligned slots, no length pass) renders the host reference's
+    records byte for byte; slot starts and record ends describe them, and the JSON parser reads the gapped batch to
+    the same columns as the packed one."""
+    from dxa.simulate.datagen import generate_cpu, generate_slotted
+    prog = _gen_programs()[name]
+    for seed, row0, n, step in ((1, 0, 2000, 0), (2**63 + 5, 10 ** 9, 700, 1000)):
+        base = 1_700_000_000_123
+        gb, go, ge = generate_slotted(prog, n, gpu, seed=seed, row0=row0, base_ms=base, step_us=step)
+        cb, co = generate_cpu(prog, n, seed=seed, row0=row0, base_ms=base, step_us=step)
+        go, ge, gbh = go.cpu().tolist(), ge.cpu().tolist(), bytes(gb.cpu().numpy())
+        stride = go[1] - go[0]
+        assert stride % 16 == 0 and stride >= prog.max_len()
+        cbh, co = bytes(cb.numpy()), co.tolist()
+        for i in range(n):
+            assert go[i] == i * stride
+            assert gbh[go[i]:ge[i]] == cbh[co[i]:co[i + 1]], i
+        assert go[n] == n * stride and not any(gbh[n * stride:])
+
+
 def test_order_by_and_string_ordering_match_cpu(gpu):
     """ORDER BY over strings (device dense ranks), doubles with NaN/-0.0, nulls first/last, DESC — one device radix
     argsort — and string < / >= predicates (device compare kernel) give the CPU engine's rows in the same order."""

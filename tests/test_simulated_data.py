@@ -96,3 +96,25 @@ def test_gpu_program_path_on_cpu():
     svc = SimulatedDataService([_schema()], [], period_s=0, gpu=True, device="cpu", emit_rules=False)
     evs = [json.loads(e) for e in svc.events_for_tick(0)]
     assert len(evs) == 5 and all(1 <= e["d"]["id"] < 4 and e["d"]["kind"] in ("a", "b") for e in evs)
+
+
+def test_program_length_bound_covers_rendered_events():
+    """``GenProgram.max_len`` (the slot size of the one-pass generator) bounds every rendered event, including
+    nullable Spark fields, arrays, alphanumerics and extreme seeds."""
+    from dxa.models import iot
+    from dxa.simulate.datagen import compile_spark, generate_cpu
+    from dxa.engine.types import from_json_obj
+    spark = from_json_obj({"type": "struct", "fields": [
+        {"name": "a", "type": "long", "nullable": True, "metadata": {"minValue": -5, "maxValue": 10 ** 12}},
+        {"name": "d", "type": "double", "nullable": True, "metadata": {"minValue": -999.5, "maxValue": 999.5}},
+        {"name": "s", "type": "string", "nullable": False, "metadata": {"maxLength": 13}},
+        {"name": "t", "type": "string", "nullable": True, "metadata": {"datetimeStringFormat": "MM/dd/yyyy HH:mm:ss"}},
+        {"name": "b", "type": "boolean", "nullable": True, "metadata": {}},
+        {"name": "arr", "type": {"type": "array", "elementType": "double", "containsNull": True}, "nullable": True,
+         "metadata": {"maxLength": 3}}]})
+    for prog in (iot.program(), compile_spark(spark)):
+        bound = prog.max_len()
+        for seed in (1, 2**63 + 5):
+            _, offs = generate_cpu(prog, 3000, seed=seed, row0=10 ** 9, base_ms=1_700_000_000_123, step_us=997)
+            lens = (offs[1:] - offs[:-1])
+            assert int(lens.max()) <= bound
