@@ -290,8 +290,9 @@ def main():
             def gen_args(j):
                 return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=batch_time(j) // 1000 - 1000,
                             step_us=max(1, interval_us // E))
-            if os.environ.get("DXA_GEN_SLOTTED", "1") != "0":
-                # one render launch per batch into fixed-size slots (no length pass, scan or host size read)
+            if os.environ.get("DXA_GEN_SLOTTED", "0") == "1":
+                # one render launch per batch into fixed-size slots (no length pass, scan or host size read); off by
+                # default: measured within run-to-run noise of the two-pass path (profiles/gen_slot)
                 ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
                 with ctx:
                     db, do, de = generate_slotted(prog, E, device, **gen_args(i))
