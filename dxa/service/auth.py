@@ -9,7 +9,9 @@ Modes (``DXA_AUTH``):
   ``aad:<tenant>`` for Azure AD's published keys) or HS256 with ``DXA_AUTH_HS256_SECRET``; ``exp`` / ``nbf`` (5 min
   skew), ``aud`` (``DXA_AUTH_AUDIENCE``) and ``iss`` (``DXA_AUTH_ISSUER``) are checked; the ``roles`` claim must hold
   the Reader role (read routes) or the Writer role (writes; Writer implies Reader), unless ``oid.tid`` is in
-  ``DXA_AUTH_CLIENT_WHITELIST``;
+  ``DXA_AUTH_CLIENT_WHITELIST``.  With JWKS keys an audience is required (a tenant's signing keys also sign tokens
+  issued for every other application in it; ``DXA_AUTH_ANY_AUDIENCE=1`` opts out), and only the configured role
+  names count (RolesCheck.cs:20-21);
 * ``local`` (the default with no key source: the onebox) — requests from the loopback interface pass, anything else
   gets 401 (RolesCheck.EnsureWriter(request, isLocal));
 * ``gateway`` — behind a trusted gateway that already authenticated the caller: roles come from ``X-DXA-Roles``
@@ -80,10 +82,11 @@ def rsa_sign_sha256(n: int, d: int, message: bytes) -> bytes:
 class KeySet:
     """RS256 public keys by ``kid`` from a JWKS document (file, URL, or ``aad:<tenant>``), refreshed hourly."""
 
-    def __init__(self, source: str, ttl_s: float = 3600.0):
+    def __init__(self, source: str, ttl_s: float = 3600.0, min_refresh_s: float = 60.0):
         self.source = source
         self.ttl = ttl_s
-        self._keys: Dict[Optional[str], Tuple[int, int]] = {}
+        self.min_refresh = min_refresh_s      # an unknown ``kid`` re-reads the key set at most this often (a forged
+        self._keys: Dict[Optional[str], Tuple[int, int]] = {}   # kid per request must not become a fetch per request)
         self._at = 0.0
         self._lock = threading.Lock()
 
@@ -100,7 +103,9 @@ class KeySet:
 
     def get(self, kid: Optional[str]) -> Tuple[int, int]:
         with self._lock:
-            if not self._keys or time.time() - self._at > self.ttl or (kid is not None and kid not in self._keys):
+            age = time.time() - self._at
+            if (not self._keys or age > self.ttl
+                    or (kid is not None and kid not in self._keys and age > self.min_refresh)):
                 doc = self._fetch()
                 keys = {}
                 for k in doc.get("keys", []):
@@ -170,6 +175,10 @@ class Authenticator:
         self.whitelist = {x.strip() for x in (env.get("DXA_AUTH_CLIENT_WHITELIST") or "").split(",") if x.strip()}
         if self.mode == "jwt" and not (self.keys or self.secret):
             raise ValueError("DXA_AUTH=jwt needs DXA_AUTH_JWKS or DXA_AUTH_HS256_SECRET")
+        if self.mode == "jwt" and self.keys is not None and not self.audience \
+                and env.get("DXA_AUTH_ANY_AUDIENCE") != "1":
+            raise ValueError("DXA_AUTH_JWKS needs DXA_AUTH_AUDIENCE (the application's id URI): the key set also "
+                             "signs tokens issued to other applications (DXA_AUTH_ANY_AUDIENCE=1 to accept any)")
 
     @staticmethod
     def _is_local(client_host: Optional[str]) -> bool:
@@ -197,8 +206,8 @@ class Authenticator:
         roles = claims.get("roles") or []
         roles = [roles] if isinstance(roles, str) else list(roles)
         low = {r.lower() for r in roles}
-        writer = WRITER_ROLE.lower() in low or "writer" in low
-        reader = writer or READER_ROLE.lower() in low or "reader" in low
+        writer = WRITER_ROLE.lower() in low
+        reader = writer or READER_ROLE.lower() in low
         who = f"{claims.get('oid', '')}.{claims.get('tid', '')}"
         if who in self.whitelist:
             return claims

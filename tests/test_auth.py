@@ -100,3 +100,29 @@ def test_hs256_whitelist_and_local_mode():
     with pytest.raises(A.AuthError) as e:
         local.check(False, None, None, "10.1.2.3")
     assert e.value.status == 401
+
+
+def test_jwks_requires_audience_and_exact_roles(rsa_key, tmp_path):
+    """A tenant's JWKS also signs other applications' tokens: JWKS mode refuses to run without an audience, and only
+    the configured role names (DataXReader / DataXWriter) grant access — a generic "Writer" role does not."""
+    n, d, jwks = rsa_key
+    with pytest.raises(ValueError):
+        A.Authenticator({"DXA_AUTH_JWKS": jwks})
+    assert A.Authenticator({"DXA_AUTH_JWKS": jwks, "DXA_AUTH_ANY_AUDIENCE": "1"}).mode == "jwt"
+    a = A.Authenticator({"DXA_AUTH_HS256_SECRET": "k"})
+    with pytest.raises(A.AuthError) as e:
+        a.check(True, "Bearer " + A.make_token(_claims(["Writer"]), secret=b"k"), None, "10.0.0.1")
+    assert e.value.status == 403
+
+
+def test_unknown_kid_does_not_refetch_per_request(rsa_key):
+    n, d, jwks = rsa_key
+    ks = A.KeySet(jwks)
+    calls = []
+    real = ks._fetch
+    ks._fetch = lambda: calls.append(1) or real()
+    ks.get("k1")
+    for _ in range(5):
+        with pytest.raises(A.AuthError):
+            ks.get("forged-kid")
+    assert len(calls) == 1

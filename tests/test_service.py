@@ -245,9 +245,9 @@ def test_auth_roles(tmp_path, monkeypatch):
     monkeypatch.setenv("DXA_SUPERVISE", "0")
     client = TestClient(create_app(str(tmp_path / "svc")))
     assert client.post("/api/flow/save", json=mini_flow()).status_code == 401
-    assert client.post("/api/flow/save", json=mini_flow(), headers={"X-DXA-Roles": "Reader"}).status_code == 403
-    assert client.post("/api/flow/save", json=mini_flow(), headers={"X-DXA-Roles": "Writer"}).status_code == 200
-    assert client.post("/api/flow/getall", json={}, headers={"X-DXA-Roles": "Reader"}).status_code == 200
+    assert client.post("/api/flow/save", json=mini_flow(), headers={"X-DXA-Roles": "DataXReader"}).status_code == 403
+    assert client.post("/api/flow/save", json=mini_flow(), headers={"X-DXA-Roles": "DataXWriter"}).status_code == 200
+    assert client.post("/api/flow/getall", json={}, headers={"X-DXA-Roles": "DataXReader"}).status_code == 200
 
 
 @pytest.mark.timeout(300)
