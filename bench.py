@@ -246,16 +246,21 @@ def main():
     ingest = lz4.ChunkedIngest(device, chunks=args.lz4_chunks, copy_stream=side) \
         if (on_gpu and source == "pinned-lz4") else None
     kdec = None
+    plan_threads = None
     if source == "kafka":
         from dxa.io import kafka_device as KD
         from concurrent.futures import ThreadPoolExecutor
         plan_bufs = KD.PlanBufferPool()
+        # planner threads: this rank's share of the CPUs its socket's ranks are bound to (16 on a 1-GPU run)
+        from dxa.parallel.affinity import host_threads
+        plan_threads = host_threads(dev_index, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         planner = ThreadPoolExecutor(max_workers=1)
         plan_futs = {}
 
         def make_plan(i):
             b = kafka_parts[i % len(pool)]
-            return KD.plan_many(pool[i % len(pool)].numpy(), b, [0] * len(b), threads=16, buffer=plan_bufs.get(),
+            return KD.plan_many(pool[i % len(pool)].numpy(), b, [0] * len(b), threads=plan_threads,
+                                buffer=plan_bufs.get(),
                                 verify_crc=args.crc == "host")
         if on_gpu:
             kdec = KD.DeviceRecordDecoder(device, chunks=args.lz4_chunks, copy_stream=side,
@@ -502,6 +507,7 @@ def main():
         "vs_target_1M_events_per_sec_per_gpu": value / world / 1e6,
         "generation_s": round(gen_s, 3),
         "host_cpus_bound": None if numa_cpus is None else len(numa_cpus),
+        "host_plan_threads": plan_threads,
     }
     if comp_bytes:
         out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)

@@ -139,3 +139,22 @@ def bind_to_device(index: int) -> Optional[Set[int]]:
         except OSError:
             pass
     return want
+
+
+def host_threads(index: int, local_world: int = 1, cap: int = 16, floor: int = 2) -> int:
+    """Worker threads one rank should start for host-side batch work (Kafka batch planning, CRC checks).
+
+    Ranks whose GPUs share a socket are bound to the same CPU set (``bind_to_device``), so each takes its share:
+    ``len(cpus) // ranks on that set``, clamped to [floor, cap].  With 8 ranks on a 2-socket node, 4 ranks per socket
+    each start cpus/4 planner threads instead of all of them starting ``cap`` and oversubscribing the socket."""
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = os.cpu_count() or floor
+    mine = local_cpus(index)
+    share = 1
+    if mine and local_world > 1:
+        share = sum(1 for j in range(local_world) if local_cpus(j) == mine) or 1
+    elif local_world > 1:
+        share = local_world
+    return max(floor, min(cap, cpus // share))

@@ -283,3 +283,17 @@ def test_broadcast_table_and_reference_data(tmp_path):
     for r in (0, 1):
         assert _canon(res[r][0]) == _canon(_rows(3, 50))
         assert res[r][1] == [{"id": "1", "name": "a,b"}, {"id": "2", "name": None}]
+
+
+def test_host_threads_share_the_socket(monkeypatch):
+    """Co-located ranks bound to one socket split its CPUs for host-side batch work."""
+    from dxa.parallel import affinity as AF
+    monkeypatch.setattr(AF.os, "sched_getaffinity", lambda pid: set(range(64)))
+    monkeypatch.setattr(AF, "local_cpus", lambda j: set(range(64)) if j < 4 else set(range(64, 128)))
+    assert AF.host_threads(0, 1) == 16
+    assert AF.host_threads(0, 8) == 16            # 4 ranks on 64 CPUs
+    assert AF.host_threads(5, 8, cap=32) == 16
+    monkeypatch.setattr(AF.os, "sched_getaffinity", lambda pid: set(range(16)))
+    assert AF.host_threads(0, 8) == 4
+    monkeypatch.setattr(AF, "local_cpus", lambda j: None)
+    assert AF.host_threads(0, 8) == 2
