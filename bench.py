@@ -131,6 +131,10 @@ def main():
     backend = os.environ.get("DXA_DIST_BACKEND") or ("nccl" if ndev else "gloo")
     dev_index = local % ndev if (ndev and backend == "gloo") else local
     numa_cpus = bind_to_device(dev_index) if ndev > dev_index else None
+    # host worker threads (producer-side compression before the timed region, Kafka batch planning inside it): this
+    # rank's share of the CPUs its socket's ranks are bound to — 16 on a 1-GPU run
+    from dxa.parallel.affinity import host_threads
+    host_thr = host_threads(dev_index, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     device = torch.device("cuda", dev_index) if torch.cuda.is_available() else torch.device("cpu")
     if world > 1:
         if device.type == "cuda":
@@ -196,7 +200,7 @@ def main():
         for p in range(args.pool):
             buf, offs = generate(prog_nl, E, device, seed=1000 * rank + p + 1, row0=p * E, base_ms=base_ms)
             total = int(offs[-1])
-            frame = lz4.compress_frame(buf[:total].cpu(), lz4_block, threads=16, level=args.lz4_level)
+            frame = lz4.compress_frame(buf[:total].cpu(), lz4_block, threads=host_thr, level=args.lz4_level)
             del buf, offs
             comp_bytes.append(frame.size)
             pool.append(lz4.DeviceFrame.from_frame(frame, lz4_block, pin=on_gpu))
@@ -216,7 +220,7 @@ def main():
                                                                    level=args.lz4_level, block_size=lz4_block_k)
             sets = [K.encode_stream(hb, ho[cuts[q]:cuts[q + 1] + 1], args.kafka_batch_records, base_offset=0,
                                     compression=args.kafka_codec, level=args.lz4_level, block_size=lz4_block_k,
-                                    threads=16) for q in range(parts)]
+                                    threads=host_thr) for q in range(parts)]
             total = sum(x.size for x in sets)
             staging = torch.empty(total + 64, dtype=torch.uint8, pin_memory=on_gpu)
             sn = staging.numpy()
@@ -251,9 +255,7 @@ def main():
         from dxa.io import kafka_device as KD
         from concurrent.futures import ThreadPoolExecutor
         plan_bufs = KD.PlanBufferPool()
-        # planner threads: this rank's share of the CPUs its socket's ranks are bound to (16 on a 1-GPU run)
-        from dxa.parallel.affinity import host_threads
-        plan_threads = host_threads(dev_index, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        plan_threads = host_thr
         planner = ThreadPoolExecutor(max_workers=1)
         plan_futs = {}
 
