@@ -988,7 +988,7 @@ def _eval_agg(call: A.Call, scope: Scope, groups: G.Groups, ctx) -> Column:
     if call.star or (name == "count" and not call.args):
         return G.aggregate(groups, None, "count_star", n)
     if name == "count" and len(call.args) > 1:
-        raise QueryError("count with multiple arguments is not supported")
+        return _count_tuple([materialize(evaluate(a, scope, ctx)) for a in call.args], groups, n, call.distinct)
     arg = materialize(evaluate(call.args[0], scope, ctx))
     if isinstance(arg, ConstColumn):
         arg = arg.materialize()
@@ -1019,6 +1019,25 @@ def _eval_agg(call: A.Call, scope: Scope, groups: G.Groups, ctx) -> Column:
     if name == "mean":
         name = "avg"
     return G.aggregate(groups, arg, name, n)
+
+
+def _count_tuple(args, groups: G.Groups, n, distinct: bool):
+    """count(a, b, …) — rows whose arguments are all non-null — and count(DISTINCT a, b, …), the distinct such
+    tuples per group (Spark's Count over several children)."""
+    args = [a.materialize() if isinstance(a, ConstColumn) else a for a in args]
+    ok = args[0].valid_mask()
+    for a in args[1:]:
+        ok = ok & a.valid_mask()
+    if not distinct:
+        return G.aggregate(groups, PrimColumn("long", torch.zeros(n, dtype=torch.int64, device=ok.device), ok),
+                           "count", n)
+    gcol = PrimColumn("long", groups.gid.to(torch.int64))
+    sub = G.group_rows([gcol] + args)
+    first = sub.rep
+    owner = G.Groups(groups.gid[first], groups.ngroups, groups.rep)
+    m = int(first.shape[0])
+    return G.aggregate(owner, PrimColumn("long", torch.zeros(m, dtype=torch.int64, device=ok.device), ok[first]),
+                       "count", m)
 
 
 def _distinct_agg(name, arg, groups: G.Groups, n):

@@ -275,3 +275,11 @@ def test_general_like_gpu_match_cpu(gpu):
             outs.append(run_sql(f"SELECT s LIKE '{p}' AS m, s NOT LIKE '{p}' AS nm FROM L", cat,
                                 EvalContext(device=dev)).columns[0].to_pylist())
         assert outs[0] == outs[1], pat
+
+
+def test_count_of_several_arguments():
+    """count(a, b) counts rows whose arguments are all non-null; count(DISTINCT a, b) the distinct such tuples."""
+    assert q("SELECT count(id, v) AS c, count(name, v) AS d FROM T")[0] == [(3, 2)]
+    assert q("SELECT count(DISTINCT id, name) AS c FROM T")[0] == [(3,)]
+    rows, _ = q("SELECT id, count(name, v) AS c, count(DISTINCT name, id) AS d FROM T GROUP BY id ORDER BY id")
+    assert rows == [(1, 1, 1), (2, 1, 2), (3, 0, 0)]
