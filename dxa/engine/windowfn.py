@@ -140,13 +140,57 @@ def evaluate_window(wc: A.WindowCall, ev: Callable[[A.Expr], Column], n: int, de
     size = pend - pstart + 1
     pos = idx - pstart
 
-    res = _compute(name, wc, ev, perm, idx, pstart, pend, peer_new, peer_start, peer_end, size, pos, n, dev)
+    rkey = _range_key(wc, okeys, specs, perm) if _has_range_offsets(wc) else None
+    res = _compute(name, wc, ev, perm, idx, pstart, pend, peer_new, peer_start, peer_end, size, pos, n, dev, rkey)
     inv = torch.empty_like(perm)
     inv[perm] = idx
     return res.take(inv)
 
 
-def _frame(wc, idx, pstart, pend, peer_start, peer_end):
+def _has_range_offsets(wc) -> bool:
+    return wc.frame is not None and wc.frame[0] == "range" and any(
+        b[0] in ("preceding", "following") for b in wc.frame[1:])
+
+
+def _range_key(wc, okeys, specs, perm):
+    """The ORDER BY value of every row in sorted order, made ascending (DESC keys negated) with nulls mapped to the
+    end of the range they sort to, for RANGE frames with value offsets (Spark: one numeric / date / timestamp
+    ORDER BY expression; timestamp offsets are INTERVALs, in microseconds here)."""
+    if len(wc.order) != 1:
+        raise WindowError("a RANGE frame with value offsets needs exactly one ORDER BY expression")
+    col, asc, nulls_first = specs[0]
+    if not isinstance(col, PrimColumn) or col.dtype in ("string", "boolean"):
+        raise WindowError("a RANGE frame with value offsets needs a numeric, date or timestamp ORDER BY")
+    x = col.data[perm]
+    valid = col.valid_mask()[perm]
+    x = x.to(torch.float64) if x.is_floating_point() else x.to(torch.int64)
+    if not asc:
+        x = -x
+    if x.is_floating_point():
+        lo, hi = float("-inf"), float("inf")
+    else:
+        info = torch.iinfo(torch.int64)
+        lo, hi = info.min, info.max
+    x = torch.where(valid, x, torch.full_like(x, lo if nulls_first else hi))
+    return x, valid
+
+
+def _bound_search(key, lo, hi, v, strict: bool):
+    """First index j in [lo, hi+1) with key[j] >= v (``strict``: key[j] > v), per row — a vectorised binary search
+    inside every row's partition (key ascending within it)."""
+    n = key.shape[0]
+    L, R = lo.clone(), hi + 1
+    for _ in range(max(1, int(n).bit_length() + 1)):
+        active = L < R
+        mid = (L + R) // 2
+        km = key[mid.clamp(0, n - 1)]
+        right = active & ((km <= v) if strict else (km < v))
+        L = torch.where(right, mid + 1, L)
+        R = torch.where(active & ~right, mid, R)
+    return L
+
+
+def _frame(wc, idx, pstart, pend, peer_start, peer_end, rkey=None):
     if wc.frame is None:
         if wc.order:
             return pstart, peer_end         # RANGE BETWEEN UNBOUNDED PRECEDING AND CURRENT ROW
@@ -164,7 +208,19 @@ def _frame(wc, idx, pstart, pend, peer_start, peer_end):
                 return peer_start if is_start else peer_end
             return idx
         if kind == "range":
-            raise WindowError("RANGE frames with value offsets are not supported; use ROWS")
+            key, valid = rkey
+            off = -k if t == "preceding" else k
+            if key.is_floating_point():
+                v = key + float(off)
+            else:
+                if isinstance(off, float):
+                    raise WindowError("an integral RANGE ORDER BY needs integral offsets")
+                v = key + int(off)
+            pos = (_bound_search(key, pstart, pend, v, strict=False) if is_start
+                   else _bound_search(key, pstart, pend, v, strict=True) - 1)
+            return torch.where(valid, pos, peer_start if is_start else peer_end)   # a null key: its peers
+        if isinstance(k, float):
+            raise WindowError("ROWS frame offsets must be integers")
         return idx - k if t == "preceding" else idx + k
 
     a = torch.maximum(bound(lo, True), pstart)
@@ -172,7 +228,7 @@ def _frame(wc, idx, pstart, pend, peer_start, peer_end):
     return a, b
 
 
-def _compute(name, wc, ev, perm, idx, pstart, pend, peer_new, peer_start, peer_end, size, pos, n, dev):
+def _compute(name, wc, ev, perm, idx, pstart, pend, peer_new, peer_start, peer_end, size, pos, n, dev, rkey=None):
     from .expr import _select_by_conditions
     from .query import _take_nullable
     args = wc.func.args
@@ -225,7 +281,7 @@ def _compute(name, wc, ev, perm, idx, pstart, pend, peer_new, peer_start, peer_e
         if isinstance(x, ConstColumn):
             x = x.materialize()
         x = x.take(perm)
-    a, b = _frame(wc, idx, pstart, pend, peer_start, peer_end)
+    a, b = _frame(wc, idx, pstart, pend, peer_start, peer_end, rkey)
     nonempty = a <= b
 
     if name in VALUE:

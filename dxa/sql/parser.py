@@ -763,10 +763,19 @@ class Parser:
             if not self.accept_word("row"):
                 self.error("expected ROW")
             return ("current", 0)
-        t = self.advance()
-        if t.kind != "num":
-            self.error("expected a frame offset")
-        k = int(t.text.rstrip("lL"))
+        if self.is_word("interval"):              # RANGE offsets over timestamps: INTERVAL '5' MINUTES → micros
+            self.advance()
+            if self.cur.kind == "str":
+                k = parse_duration_micros(self.advance().text)
+            else:
+                n = self.advance()
+                k = parse_duration_micros(f"{n.text} {self.ident()}")
+        else:
+            t = self.advance()
+            if t.kind != "num":
+                self.error("expected a frame offset")
+            txt = t.text.rstrip("lLdD")
+            k = float(txt) if any(c in txt for c in ".eE") else int(txt)
         if self.accept_word("preceding"):
             return ("preceding", k)
         if self.accept_word("following"):

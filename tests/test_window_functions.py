@@ -172,7 +172,8 @@ def test_window_functions_gpu_match_cpu():
              "v": None if rnd.random() < 0.1 else float(rnd.randint(-500, 500))} for i in range(20000)]
     sql = ("SELECT id, row_number() OVER (PARTITION BY k ORDER BY t, id) AS rn, rank() OVER (PARTITION BY k ORDER BY t) "
            "AS rk, sum(v) OVER (PARTITION BY k ORDER BY t) AS run, min(v) OVER (PARTITION BY k ORDER BY id ROWS "
-           "BETWEEN 3 PRECEDING AND 2 FOLLOWING) AS mn, lag(v, 2) OVER (PARTITION BY k ORDER BY id) AS lg FROM T "
+           "BETWEEN 3 PRECEDING AND 2 FOLLOWING) AS mn, lag(v, 2) OVER (PARTITION BY k ORDER BY id) AS lg, "
+           "max(v) OVER (PARTITION BY k ORDER BY t DESC RANGE BETWEEN 4 PRECEDING AND 1 FOLLOWING) AS rg FROM T "
            "ORDER BY id")
     out = {}
     for dev in ("cpu", "cuda"):
@@ -180,3 +181,61 @@ def test_window_functions_gpu_match_cpu():
         c.register("T", Table.from_pylist(rows, SCHEMA, dev))
         out[dev] = [json.loads(l) for l in table_to_json_lines(run_sql(sql, c, EvalContext(now_us=0)))]
     assert out["cpu"] == out["cuda"]
+
+
+def _brute_range(rows, lo, hi, desc=False, func="sum"):
+    """RANGE BETWEEN lo AND hi (offsets, None = unbounded) over ORDER BY t per k, in Spark's terms: rows are placed
+    on the ordering axis (s·t, nulls at -inf for ASC NULLS FIRST / +inf for DESC NULLS LAST); an unbounded side
+    reaches the partition's end, an offset side is the current row's position + offset (a null row's own position)."""
+    inf = float("inf")
+    s = -1 if desc else 1
+
+    def ov(x):
+        return (inf if desc else -inf) if x["t"] is None else s * x["t"]
+    out = {}
+    for r in rows:
+        peers = [x for x in rows if x["k"] == r["k"]]
+        c = ov(r)
+        lower = -inf if lo is None else (c if r["t"] is None else c + lo)
+        upper = inf if hi is None else (c if r["t"] is None else c + hi)
+        frame = [x for x in peers if lower <= ov(x) <= upper]
+        vals = [x["v"] for x in frame if x["v"] is not None]
+        if func == "sum":
+            out[r["id"]] = sum(vals) if vals else None
+        elif func == "count":
+            out[r["id"]] = len(vals)
+        else:
+            out[r["id"]] = max(vals) if vals else None
+    return out
+
+
+@pytest.mark.parametrize("desc", [False, True])
+def test_range_frames_with_value_offsets(desc):
+    """RANGE frames with numeric offsets (Spark: one ORDER BY expression; frame = rows whose ORDER BY value lies
+    within [v - lo, v + hi]; a null key's frame is its null peers) against a row-by-row reference."""
+    rnd = random.Random(5)
+    rows = [{"id": i, "k": rnd.choice(["a", "b", None]), "t": None if rnd.random() < 0.1 else rnd.randint(0, 40),
+             "v": None if rnd.random() < 0.1 else float(rnd.randint(-5, 9))} for i in range(300)]
+    cat = _cat(rows)
+    d = " DESC" if desc else ""
+    for lo_sql, hi_sql, lo, hi in (("5 PRECEDING", "CURRENT ROW", -5, 0), ("3 PRECEDING", "2 FOLLOWING", -3, 2),
+                                   ("UNBOUNDED PRECEDING", "4 PRECEDING", None, -4),
+                                   ("2 FOLLOWING", "UNBOUNDED FOLLOWING", 2, None)):
+        for func in ("sum", "count", "max"):
+            got = q(cat, f"SELECT id, {func}(v) OVER (PARTITION BY k ORDER BY t{d} RANGE BETWEEN {lo_sql} AND "
+                         f"{hi_sql}) AS x FROM T")
+            want = _brute_range(rows, lo, hi, desc, func)
+            assert {g["id"]: g.get("x") for g in got} == want, (lo_sql, hi_sql, func)
+
+
+def test_range_interval_offsets_over_timestamps():
+    from dxa.engine.column import column_from_pylist
+    c = Catalog()
+    h = 3_600_000_000
+    c.register("E", Table(["ts", "x"], [column_from_pylist([0, h // 2, h, 3 * h, 3 * h + 1], "timestamp"),
+                                        column_from_pylist([1, 2, 3, 4, 5], "long")]))
+    got = q(c, "SELECT x, sum(x) OVER (ORDER BY ts RANGE BETWEEN INTERVAL 1 HOUR PRECEDING AND CURRENT ROW) AS s "
+               "FROM E")
+    assert [(g["x"], g["s"]) for g in got] == [(1, 1), (2, 3), (3, 6), (4, 4), (5, 9)]
+    with pytest.raises(Exception):
+        q(c, "SELECT sum(x) OVER (ORDER BY ts, x RANGE BETWEEN 1 PRECEDING AND CURRENT ROW) AS s FROM E")
