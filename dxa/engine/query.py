@@ -758,6 +758,7 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         idx = torch.nonzero(mask).flatten()
         scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]), scope.device)
         scope.dist = sdist
+    sel, scope = _sliding_windows(sel, scope, ctx)
     items = _expand_items(sel, scope)
     gen_at = [k for k, (e, _) in enumerate(items) if isinstance(e, A.Call) and e.name in _GENERATOR_NAMES]
     if gen_at:
@@ -786,6 +787,47 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         out = distinct(out)
         src = None
     return out, (src if want_scope else None)
+
+
+_WINDOW_COL = "__dxa_window"
+
+
+def _sliding_windows(sel: A.Select, scope: Scope, ctx):
+    """Spark's TimeWindowing for sliding ``window(ts, dur, slide)`` (slide < dur): each row is repeated once per
+    window holding its timestamp (after WHERE, before grouping), and every occurrence of that window call in the
+    SELECT list, GROUP BY and HAVING reads the expanded rows' window struct.  One distinct sliding window per
+    SELECT, as in Spark."""
+    from . import sqlfuncs as SF
+    exprs = [it.expr for it in sel.items] + list(sel.group_by) + ([sel.having] if sel.having is not None else [])
+    found = {}
+    for e in exprs:
+        for node in A.walk(e):
+            if isinstance(node, A.Call) and node.name == "window" and len(node.args) >= 3:
+                size, slide, _ = SF.window_params(node, scope, ctx)
+                if slide != size:
+                    found.setdefault(node.key(), node)
+    if not found:
+        return sel, scope
+    if len(found) > 1:
+        raise QueryError("only one distinct sliding window() is allowed per SELECT")
+    key, call = next(iter(found.items()))
+    rows, wcol = SF.sliding_windows(call, scope, ctx)
+    sdist = getattr(scope, "dist", P.REPLICATED)
+    base = Scope(scope.names, TakenColumns(scope.cols, rows), scope.quals, int(rows.shape[0]), scope.device)
+    out = base.with_bindings([_WINDOW_COL], [wcol])
+    out.dist = sdist
+    ref = A.Ident((_WINDOW_COL,))
+
+    def sub(node):
+        return ref if isinstance(node, A.Call) and node.name == "window" and node.key() == key else None
+    import dataclasses
+    sel2 = dataclasses.replace(
+        sel, items=[dataclasses.replace(it, expr=A.replace(it.expr, sub),
+                                        alias=it.alias or ("window" if sub(it.expr) is not None else None))
+                    for it in sel.items],
+        group_by=[A.replace(g, sub) for g in sel.group_by],
+        having=None if sel.having is None else A.replace(sel.having, sub))
+    return sel2, out
 
 
 _GENERATOR_NAMES = {"explode", "explode_outer", "posexplode", "posexplode_outer", "inline", "inline_outer",

@@ -942,11 +942,56 @@ def _f_window(e, scope, ctx, subst):
     if not size or size <= 0:
         raise EvalError("window() duration must be positive")
     if slide != size:
-        raise EvalError("sliding window() (slide < duration) is not supported; use FROM t TIMEWINDOW('…')")
+        raise EvalError("sliding window() is expanded by the SELECT it appears in (query._sliding_windows)")
     start = F.floor_div(a.data - off, size) * size + off
     return StructColumn(["start", "end"], [PrimColumn("timestamp", start, a.valid),
                                            PrimColumn("timestamp", start + size, a.valid)], n, a.valid, False, None,
                         dev)
+
+
+def window_params(e, scope, ctx):
+    """(duration, slide, start offset) in microseconds of a ``window(ts, dur[, slide[, start]])`` call."""
+    from ..sql.parser import parse_duration_micros
+
+    def dur(k, default=None):
+        if len(e.args) <= k:
+            return default
+        c = evaluate(e.args[k], scope, ctx)
+        if not isinstance(c, ConstColumn):
+            raise EvalError("window() durations must be constants")
+        return c.value if isinstance(c.value, int) and c.dtype == "interval" else parse_duration_micros(str(c.value))
+    size = dur(1)
+    slide = dur(2, size)
+    off = dur(3, 0)
+    if not size or size <= 0 or not slide or slide <= 0:
+        raise EvalError("window() duration and slide must be positive")
+    if slide > size:
+        raise EvalError("window() slide must not exceed the duration")
+    return size, slide, off
+
+
+def sliding_windows(e, scope, ctx):
+    """Rows of a sliding ``window(ts, dur, slide[, start])`` expansion (Spark's TimeWindowing: every window
+    [s, s + dur) with s ≡ start (mod slide) that holds ts; rows with a null ts produce none) →
+    (input row of every output row, struct<start, end> column), in input-row order with windows latest-start
+    first, as Spark's expansion emits them."""
+    size, slide, off = window_params(e, scope, ctx)
+    a = materialize(_ts(evaluate(e.args[0], scope, ctx)))
+    n, dev = scope.length, scope.device
+    k = -(-size // slide)
+    ok = a.valid_mask()
+    last = a.data - torch.remainder(a.data - off, slide)
+    picks = []
+    for j in range(k):
+        st = last - j * slide
+        m = ok & (a.data < st + size)
+        picks.append(torch.nonzero(m).flatten() * k + j)
+    code = torch.sort(torch.cat(picks)).values
+    rows, j = code // k, code % k
+    start = last[rows] - j * slide
+    m = int(rows.shape[0])
+    return rows, StructColumn(["start", "end"], [PrimColumn("timestamp", start), PrimColumn("timestamp", start + size)],
+                              m, None, False, None, dev)
 
 
 # ---------------------------------------------------------------------------------------------------------------

@@ -324,3 +324,28 @@ def walk(e: Expr):
     yield e
     for c in e.children():
         yield from walk(c)
+
+
+def replace(e, fn):
+    """Copy of expression ``e`` with every node for which ``fn(node)`` returns an Expr replaced by it (pre-order: a
+    replaced node's subtree is not visited).  Fields holding expressions or lists of them are rebuilt; other fields
+    are shared."""
+    import dataclasses
+    if not isinstance(e, Expr):
+        return e
+    r = fn(e)
+    if r is not None:
+        return r
+    if not dataclasses.is_dataclass(e):
+        return e
+    changes = {}
+    for f in dataclasses.fields(e):
+        v = getattr(e, f.name)
+        if isinstance(v, Expr):
+            nv = replace(v, fn)
+        elif isinstance(v, list) and any(isinstance(x, Expr) for x in v):
+            nv = [replace(x, fn) for x in v]
+        else:
+            continue
+        changes[f.name] = nv
+    return dataclasses.replace(e, **changes) if changes else e

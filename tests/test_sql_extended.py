@@ -283,3 +283,23 @@ def test_count_of_several_arguments():
     assert q("SELECT count(DISTINCT id, name) AS c FROM T")[0] == [(3,)]
     rows, _ = q("SELECT id, count(name, v) AS c, count(DISTINCT name, id) AS d FROM T GROUP BY id ORDER BY id")
     assert rows == [(1, 1, 1), (2, 1, 2), (3, 0, 0)]
+
+
+def test_sliding_window_function():
+    """window(ts, dur, slide): every window [s, s + dur) with s a multiple of the slide that holds ts (Spark's
+    TimeWindowing expansion), usable in GROUP BY; a tumbling window() stays one row per input row."""
+    m = 60_000_000
+    cat = Catalog()
+    cat.register("E", Table(["ts", "x"], [column_from_pylist([0, 4 * m, 5 * m, 12 * m, None], "timestamp"),
+                                          column_from_pylist([1, 2, 3, 4, 5], "long")]))
+    ctx = EvalContext(now_us=0)
+    out = run_sql("SELECT window(ts, '10 minutes', '5 minutes') AS w, count(*) AS c, sum(x) AS s FROM E "
+                  "GROUP BY window(ts, '10 minutes', '5 minutes') ORDER BY w.start", cat, ctx)
+    rows = [tuple(r) for r in zip(*[c.to_pylist() for c in out.columns])]
+    starts = [r[0]["start"] if isinstance(r[0], dict) else r[0][0] for r in rows]
+    as_min = [int((s - dt.datetime(1970, 1, 1)).total_seconds() // 60) if isinstance(s, dt.datetime) else s // m
+              for s in starts]
+    assert as_min == [-5, 0, 5, 10]
+    assert [(r[1], r[2]) for r in rows] == [(2, 3), (3, 6), (2, 7), (1, 4)]
+    out = run_sql("SELECT x, window(ts, '10 minutes', '5 minutes') FROM E WHERE x < 3", cat, ctx)
+    assert out.names == ["x", "window"] and out.columns[0].to_pylist() == [1, 1, 2, 2]
