@@ -332,9 +332,24 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         n_l, n_r = left.length, right.length
     if kind == "cross" or (not lkeys):
         if kind not in ("cross", "inner"):
-            raise QueryError(f"{kind} join without equi-join keys is not supported")
-        li = torch.arange(n_l, device=dev).repeat_interleave(n_r)
-        ri = torch.arange(n_r, device=dev).repeat(n_l)
+            # outer / semi / anti join on non-equi terms only (Spark's broadcast nested-loop join): the pairs
+            # that satisfy ON, in left-row chunks of at most 2^26 pairs, then the preserved side's unmatched rows
+            lis, ris = [], []
+            step = max(1, (1 << 26) // max(1, n_r))
+            for s0 in range(0, n_l, step):
+                s1 = min(n_l, s0 + step)
+                cl = torch.arange(s0, s1, device=dev).repeat_interleave(n_r)
+                cr = torch.arange(n_r, device=dev).repeat(s1 - s0)
+                if residual:
+                    cl, cr = _filter_pairs(left, right, cl, cr, residual, ctx)
+                lis.append(cl)
+                ris.append(cr)
+            e = torch.zeros(0, dtype=torch.int64, device=dev)
+            li, ri = _complete_join(torch.cat(lis) if lis else e, torch.cat(ris) if ris else e, kind, n_l, n_r, dev)
+            residual = []
+        else:
+            li = torch.arange(n_l, device=dev).repeat_interleave(n_r)
+            ri = torch.arange(n_r, device=dev).repeat(n_l)
     else:
         lk = [materialize(evaluate(e, left, ctx)) for e in lkeys]
         built = None

@@ -303,3 +303,15 @@ def test_sliding_window_function():
     assert [(r[1], r[2]) for r in rows] == [(2, 3), (3, 6), (2, 7), (1, 4)]
     out = run_sql("SELECT x, window(ts, '10 minutes', '5 minutes') FROM E WHERE x < 3", cat, ctx)
     assert out.names == ["x", "window"] and out.columns[0].to_pylist() == [1, 1, 2, 2]
+
+
+def test_outer_joins_on_non_equi_terms_only():
+    """LEFT / RIGHT / FULL / SEMI / ANTI joins whose ON has no equality key (a nested-loop join in Spark)."""
+    assert q("SELECT t.id, r.rid FROM T t LEFT JOIN R r ON r.w > t.v * 2 ORDER BY t.id, r.rid")[0] == \
+        [(1, 2), (1, 5), (2, None), (2, 2), (3, 2), (3, 5)]
+    assert q("SELECT r.rid, t.id FROM T t RIGHT JOIN R r ON t.v > r.w ORDER BY r.rid, t.id")[0] == \
+        [(2, None), (3, 1), (3, 2), (3, 3), (5, None)]
+    assert q("SELECT id FROM T t LEFT SEMI JOIN R r ON r.w < t.v ORDER BY id")[0] == [(1,), (2,), (3,)]
+    assert q("SELECT id FROM T t LEFT ANTI JOIN R r ON r.w < t.v")[0] == [(2,)]
+    rows = q("SELECT t.id, r.rid FROM T t FULL JOIN R r ON t.v > 100 ORDER BY t.id, r.rid")[0]
+    assert len(rows) == 7 and sum(1 for a, b in rows if a is None) == 3
