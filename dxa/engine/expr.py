@@ -27,7 +27,8 @@ from .types import (ArrayType, MapType, StructType, common_type, is_integral, is
 AGG_FUNCS = {"count", "sum", "avg", "mean", "min", "max", "first", "last", "first_value", "last_value", "stddev",
              "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std", "collect_list", "collect_set",
              "approx_count_distinct", "count_if", "bool_and", "bool_or", "every", "any", "some", "percentile",
-             "percentile_approx", "approx_percentile", "median"}
+             "percentile_approx", "approx_percentile", "median", "corr", "covar_pop", "covar_samp", "kurtosis",
+             "skewness", "max_by", "min_by"}
 
 
 class EvalError(Exception):

@@ -1046,6 +1046,12 @@ def _eval_agg(call: A.Call, scope: Scope, groups: G.Groups, ctx) -> Column:
         return G.aggregate(groups, None, "count_star", n)
     if name == "count" and len(call.args) > 1:
         return _count_tuple([materialize(evaluate(a, scope, ctx)) for a in call.args], groups, n, call.distinct)
+    if name in ("corr", "covar_pop", "covar_samp", "kurtosis", "skewness", "max_by", "min_by"):
+        args = [materialize(evaluate(a, scope, ctx)) for a in call.args]
+        args = [a.materialize() if isinstance(a, ConstColumn) else a for a in args]
+        if name in ("max_by", "min_by"):
+            return _arg_extreme(args, groups, n, name == "max_by")
+        return _moments(name, args, groups)
     arg = materialize(evaluate(call.args[0], scope, ctx))
     if isinstance(arg, ConstColumn):
         arg = arg.materialize()
@@ -1076,6 +1082,72 @@ def _eval_agg(call: A.Call, scope: Scope, groups: G.Groups, ctx) -> Column:
     if name == "mean":
         name = "avg"
     return G.aggregate(groups, arg, name, n)
+
+
+def _moments(name, args, groups: G.Groups):
+    """corr / covar_pop / covar_samp (two arguments) and skewness / kurtosis (one) per group, from two device passes
+    (group means, then centred co-moments with index_add): Spark's Corr / Covariance / CentralMomentAgg results —
+    null for an empty group, NaN where Spark divides by zero (corr of a constant, covar_samp of one row), kurtosis
+    as excess kurtosis."""
+    ng = groups.ngroups
+    xs = [cast_column(a, "double") if a.dtype != "double" else a for a in args]
+    ok = xs[0].valid_mask()
+    for a in xs[1:]:
+        ok = ok & a.valid_mask()
+    idx = torch.nonzero(ok).flatten()
+    gid = groups.gid.to(torch.int64)[idx]
+    vals = [a.data.to(torch.float64)[idx] for a in xs]
+    dev = gid.device
+    f64 = torch.float64
+
+    def gsum(v):
+        return torch.zeros(ng, dtype=f64, device=dev).index_add_(0, gid, v)
+    cnt = gsum(torch.ones_like(vals[0]))
+    safe = cnt.clamp(min=1)
+    d = [v - (gsum(v) / safe)[gid] for v in vals]
+    has = cnt > 0
+    nan = torch.full_like(cnt, float("nan"))
+    if name in ("corr", "covar_pop", "covar_samp"):
+        if len(d) != 2:
+            raise QueryError(f"{name} takes two arguments")
+        cxy = gsum(d[0] * d[1])
+        if name == "covar_pop":
+            return PrimColumn("double", cxy / safe, has)
+        if name == "covar_samp":
+            return PrimColumn("double", torch.where(cnt > 1, cxy / (cnt - 1).clamp(min=1), nan), has)
+        den = torch.sqrt(gsum(d[0] * d[0]) * gsum(d[1] * d[1]))
+        return PrimColumn("double", torch.where(den > 0, cxy / torch.where(den > 0, den, torch.ones_like(den)), nan),
+                          has)
+    m2, m = gsum(d[0] * d[0]), cnt
+    if name == "skewness":
+        m3 = gsum(d[0] ** 3)
+        r = torch.sqrt(m) * m3 / torch.where(m2 > 0, m2, torch.ones_like(m2)) ** 1.5
+    else:
+        m4 = gsum(d[0] ** 4)
+        r = m * m4 / torch.where(m2 > 0, m2 * m2, torch.ones_like(m2)) - 3.0
+    return PrimColumn("double", torch.where(m2 > 0, r, nan), has)
+
+
+def _arg_extreme(args, groups: G.Groups, n, is_max: bool):
+    """max_by(x, y) / min_by(x, y): x of the row with the largest / smallest non-null y per group (one device
+    sort by (group, y); ties keep the first row in input order)."""
+    if len(args) != 2:
+        raise QueryError("max_by / min_by take two arguments")
+    x, y = args
+    from ..ops.sort import argsort_words, sort_spec_words
+    ok = y.valid_mask()
+    idx = torch.nonzero(ok).flatten()
+    gid = groups.gid.to(torch.int64)[idx]
+    ysub = y.take(idx)
+    perm = argsort_words(sort_spec_words([(ysub, not is_max, False)]) + [gid])
+    sg = gid[perm]
+    first = torch.ones_like(sg, dtype=torch.bool)
+    first[1:] = sg[1:] != sg[:-1]
+    rows = idx[perm[first]]
+    owner = sg[first]
+    pick = torch.full((groups.ngroups,), -1, dtype=torch.int64, device=gid.device)
+    pick[owner] = rows
+    return _take_nullable(x, pick)
 
 
 def _count_tuple(args, groups: G.Groups, n, distinct: bool):

@@ -1283,3 +1283,238 @@ def _register():
 
 
 _register()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# more Spark built-ins: bit ops, rint, width_bucket, next_day, typeof, spark_partition_id, timestamp_seconds and
+# host-assisted text functions (format_number, conv, soundex, levenshtein, substring_index, format_string, …)
+# ---------------------------------------------------------------------------------------------------------------
+
+def _f_shift(kind):
+    def f(e, scope, ctx, subst):
+        n, dev = scope.length, scope.device
+        a, k = _args(e, scope, ctx, subst)
+        a, k = materialize(_num(a, n, dev)), materialize(_num(k, n, dev))
+        x = a.data.to(torch.int64)
+        s = (k.data.to(torch.int64) & 63)
+        if kind == "left":
+            r = torch.bitwise_left_shift(x, s)
+        elif kind == "right":
+            r = torch.bitwise_right_shift(x, s)
+        else:                                   # unsigned: logical shift of the 64-bit pattern
+            r = torch.where(s == 0, x, torch.bitwise_right_shift(x, s) & ((1 << (64 - s)) - 1))
+        return PrimColumn("long", r, _and(a.valid, k.valid))
+    return f
+
+
+def _f_bit_count(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    (a,) = _args(e, scope, ctx, subst)
+    a = materialize(_num(a, n, dev))
+    x = a.data.to(torch.int64)
+    c = torch.zeros_like(x)
+    for b in range(64):
+        c += (torch.bitwise_right_shift(x, b) & 1)
+    return PrimColumn("int", c.to(torch.int32), a.valid)
+
+
+def _f_rint(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    (a,) = _args(e, scope, ctx, subst)
+    a = materialize(_num(a, n, dev))
+    return PrimColumn("double", torch.round(a.data.to(torch.float64)), a.valid)    # round half to even
+
+
+def _f_width_bucket(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    v, lo, hi, k = (materialize(_num(c, n, dev)) for c in _args(e, scope, ctx, subst))
+    x, a, b = (c.data.to(torch.float64) for c in (v, lo, hi))
+    nb = k.data.to(torch.int64)
+    asc = a < b
+    frac = torch.where(asc, (x - a) / (b - a), (a - x) / (a - b))
+    inner = torch.floor(frac * nb.to(torch.float64)).to(torch.int64) + 1
+    r = torch.where(frac < 0, torch.zeros_like(inner), torch.where(frac >= 1, nb + 1, inner))
+    ok = _and(_and(v.valid, lo.valid), _and(hi.valid, k.valid))
+    good = (nb > 0) & (a != b) & torch.isfinite(x)
+    ok = good if ok is None else ok & good
+    return PrimColumn("long", r, ok)
+
+
+_DOW = {"mo": 0, "mon": 0, "monday": 0, "tu": 1, "tue": 1, "tuesday": 1, "we": 2, "wed": 2, "wednesday": 2,
+        "th": 3, "thu": 3, "thursday": 3, "fr": 4, "fri": 4, "friday": 4, "sa": 5, "sat": 5, "saturday": 5,
+        "su": 6, "sun": 6, "sunday": 6}
+
+
+def _f_next_day(e, scope, ctx, subst):
+    """next_day(date, 'Mon'): the first date later than ``date`` falling on that weekday (null for a bad name)."""
+    n, dev = scope.length, scope.device
+    a, w = _args(e, scope, ctx, subst)
+    if not isinstance(w, ConstColumn):
+        raise EvalError("next_day() day-of-week must be a constant")
+    tgt = _DOW.get(str(w.value or "").strip().lower())
+    d = materialize(_days(a))
+    if tgt is None:
+        return ConstColumn(None, "date", n, dev)
+    cur = torch.remainder(d.data.to(torch.int64) + 3, 7)          # 1970-01-01 was a Thursday (Mon = 0)
+    step = torch.remainder(tgt - cur + 6, 7) + 1
+    return PrimColumn("date", d.data.to(torch.int64) + step, d.valid)
+
+
+def _f_typeof(e, scope, ctx, subst):
+    (a,) = _args(e, scope, ctx, subst)
+    t = {"long": "bigint", "int": "int", "double": "double", "string": "string", "boolean": "boolean",
+         "timestamp": "timestamp", "date": "date"}.get(str(a.dtype), str(a.dtype))
+    return ConstColumn(t, "string", scope.length, scope.device)
+
+
+def _f_partition_id(e, scope, ctx, subst):
+    from .. import parallel as P
+    return ConstColumn(P.rank() if P.active() else 0, "int", scope.length, scope.device)
+
+
+def _f_timestamp_seconds(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    (a,) = _args(e, scope, ctx, subst)
+    a = materialize(_num(a, n, dev))
+    x = a.data
+    us = torch.round(x.to(torch.float64) * 1e6).to(torch.int64) if x.is_floating_point() else x.to(torch.int64) * \
+        1_000_000
+    return PrimColumn("timestamp", us, a.valid)
+
+
+def _format_number(x, d):
+    if isinstance(d, str):
+        raise ValueError("format patterns are not supported")
+    d = int(d)
+    if d < 0:
+        return None
+    from decimal import ROUND_HALF_EVEN, Decimal
+    q = Decimal(repr(float(x))).quantize(Decimal(1).scaleb(-d), rounding=ROUND_HALF_EVEN)
+    return f"{q:,.{d}f}"
+
+
+_DIGITS = "0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ"
+
+
+def _conv(s, fb, tb):
+    """conv(num, from_base, to_base): Spark/Hive NumberConverter — unsigned 64-bit unless to_base < 0."""
+    fb, tb = int(fb), int(tb)
+    if not (2 <= abs(fb) <= 36 and 2 <= abs(tb) <= 36):
+        return None
+    t = str(s).strip().upper()
+    neg = t.startswith("-")
+    t = t[1:] if neg else t
+    v = 0
+    for ch in t:
+        k = _DIGITS.find(ch)
+        if k < 0 or k >= abs(fb):
+            break
+        v = v * abs(fb) + k
+    v &= (1 << 64) - 1
+    if neg:
+        v = (-v) & ((1 << 64) - 1)
+    out_neg = False
+    if tb < 0 and v >= 1 << 63:
+        v = (1 << 64) - v
+        out_neg = True
+    b = abs(tb)
+    digits = ""
+    while True:
+        digits = _DIGITS[v % b] + digits
+        v //= b
+        if not v:
+            break
+    return ("-" if out_neg else "") + digits
+
+
+def _soundex(s):
+    s = str(s)
+    if not s or not s[0].isalpha():
+        return s
+    codes = {**dict.fromkeys("BFPV", "1"), **dict.fromkeys("CGJKQSXZ", "2"), **dict.fromkeys("DT", "3"), "L": "4",
+             **dict.fromkeys("MN", "5"), "R": "6"}
+    up = s.upper()
+    out, last = up[0], codes.get(up[0], "")
+    for ch in up[1:]:
+        c = codes.get(ch, "")
+        if c and c != last:
+            out += c
+            if len(out) == 4:
+                break
+        if ch not in "HW":
+            last = c
+    return out.ljust(4, "0")
+
+
+def _levenshtein(a, b):
+    a, b = str(a), str(b)
+    prev = list(range(len(b) + 1))
+    for i, ca in enumerate(a, 1):
+        cur = [i]
+        for j, cb in enumerate(b, 1):
+            cur.append(min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (ca != cb)))
+        prev = cur
+    return prev[-1]
+
+
+def _substring_index(s, delim, count):
+    s, delim, count = str(s), str(delim), int(count)
+    if not delim or count == 0:
+        return ""
+    parts = s.split(delim)
+    return delim.join(parts[:count]) if count > 0 else delim.join(parts[count:])
+
+
+def _java_format(fmt, *args):
+    """format_string / printf: Java Formatter specs mapped onto Python's % formatting (%s %d %f %e %x %o %c %b %%,
+    flags and widths)."""
+    import re as _re
+    out, it = [], iter(args)
+
+    def conv(m):
+        spec, flags, width, prec, c = m.group(0), m.group(1) or "", m.group(2) or "", m.group(3) or "", m.group(4)
+        if c == "%":
+            return "%"
+        if c == "n":
+            return "\n"
+        v = next(it, None)
+        if c in "bB":
+            return str(v is not None and v is not False).lower()
+        if v is None:
+            return "null"
+        pf = flags.replace(",", "")
+        body = f"%{pf}{width}{prec}{'s' if c in 'sS' else c.lower() if c in 'xXeEgG' else c}"
+        r = body % (int(v) if c in "dxXoc" else float(v) if c in "feEgG" else v)
+        if "," in flags and c in "df":
+            r = f"{(int(v) if c == 'd' else float(v)):,{prec}{'d' if c == 'd' else 'f'}}".rjust(int(width or 0))
+        return r.upper() if c in "SXEG" else r
+    return _re.sub(r"%([-#+ 0,(]*)(\d+)?(\.\d+)?([a-zA-Z%])", conv, str(fmt))
+
+
+def _register_more():
+    reg = register_function
+    reg("shiftleft", _f_shift("left"))
+    reg("shiftright", _f_shift("right"))
+    reg("shiftrightunsigned", _f_shift("unsigned"))
+    reg("bit_count", _f_bit_count)
+    reg("rint", _f_rint)
+    reg("width_bucket", _f_width_bucket)
+    reg("next_day", _f_next_day)
+    reg("typeof", _f_typeof)
+    reg("spark_partition_id", _f_partition_id)
+    reg("timestamp_seconds", _f_timestamp_seconds)
+    reg("input_file_name", lambda e, scope, ctx, subst: ConstColumn("", "string", scope.length, scope.device))
+    reg("format_number", _host_string_fn(_format_number))
+    reg("conv", _host_string_fn(_conv))
+    reg("soundex", _host_string_fn(_soundex))
+    reg("levenshtein", _host_string_fn(_levenshtein, "int"))
+    reg("substring_index", _host_string_fn(_substring_index))
+    reg("char", _host_string_fn(lambda x: chr(int(x) % 256) if int(x) >= 0 else ""))
+    reg("chr", _host_string_fn(lambda x: chr(int(x) % 256) if int(x) >= 0 else ""))
+    reg("octet_length", _host_string_fn(lambda s: len(str(s).encode("utf-8")), "int"))
+    reg("bit_length", _host_string_fn(lambda s: 8 * len(str(s).encode("utf-8")), "int"))
+    reg("format_string", _host_string_fn(_java_format))
+    reg("printf", _host_string_fn(_java_format))
+
+
+_register_more()

@@ -315,3 +315,52 @@ def test_outer_joins_on_non_equi_terms_only():
     assert q("SELECT id FROM T t LEFT ANTI JOIN R r ON r.w < t.v")[0] == [(2,)]
     rows = q("SELECT t.id, r.rid FROM T t FULL JOIN R r ON t.v > 100 ORDER BY t.id, r.rid")[0]
     assert len(rows) == 7 and sum(1 for a, b in rows if a is None) == 3
+
+
+def test_statistical_aggregates_and_max_by():
+    """corr / covar_pop / covar_samp / skewness / kurtosis (Spark's central-moment aggregates) and max_by / min_by,
+    per group, against numpy."""
+    import numpy as np
+    rnd = np.random.default_rng(3)
+    n = 500
+    k = rnd.integers(0, 4, n)
+    x = rnd.normal(size=n)
+    y = 2 * x + rnd.normal(size=n)
+    cat = Catalog()
+    cat.register("S", Table(["k", "x", "y"], [column_from_pylist(k.tolist(), "long", "cpu"),
+                                             column_from_pylist(x.tolist(), "double", "cpu"),
+                                             column_from_pylist(y.tolist(), "double", "cpu")]))
+    out = run_sql("SELECT k, corr(x, y) AS c, covar_pop(x, y) AS cp, covar_samp(x, y) AS cs, skewness(x) AS sk, "
+                  "kurtosis(x) AS ku, max_by(x, y) AS mb, min_by(y, x) AS nb FROM S GROUP BY k ORDER BY k", cat,
+                  EvalContext(now_us=0))
+    got = list(zip(*[c.to_pylist() for c in out.columns]))
+    for g in range(4):
+        m = k == g
+        xs, ys = x[m], y[m]
+        dx, dy = xs - xs.mean(), ys - ys.mean()
+        want = (g, np.corrcoef(xs, ys)[0, 1], (dx * dy).mean(), (dx * dy).sum() / (m.sum() - 1),
+                np.sqrt(m.sum()) * (dx ** 3).sum() / ((dx ** 2).sum() ** 1.5),
+                m.sum() * (dx ** 4).sum() / ((dx ** 2).sum() ** 2) - 3, xs[np.argmax(ys)], ys[np.argmin(xs)])
+        assert got[g][0] == g
+        assert np.allclose(got[g][1:], want[1:], rtol=1e-9, atol=1e-12)
+
+
+def test_more_spark_builtins():
+    """Spark's values for the bit / math / date / text built-ins added here (Hive/Spark documentation examples)."""
+    one = "FROM T WHERE id = 1"
+    assert q(f"SELECT shiftleft(2, 1), shiftright(-8, 1), shiftrightunsigned(-1, 60), bit_count(7) {one}")[0] == \
+        [(4, -4, 15, 3)]
+    assert q(f"SELECT rint(2.5), rint(3.5), width_bucket(5.3, 0.2, 10.6, 5), width_bucket(-1.0, 0.0, 10.0, 5) "
+             f"{one}")[0] == [(2.0, 4.0, 3, 0)]
+    # 2015-01-14 is a Wednesday: next Tuesday 2015-01-20, next Wednesday one week on
+    rows = q(f"SELECT next_day(to_date('2015-01-14'), 'TU'), next_day(to_date('2015-01-14'), 'Wed') {one}")[0]
+    assert [str(v)[:10] for v in rows[0]] == ["2015-01-20", "2015-01-21"]
+    assert q(f"SELECT format_number(12332.123456, 4), format_number(-0.5, 0), conv('100', 2, 10), "
+             f"conv(-10, 16, -10), conv('ff', 16, 2) {one}")[0] == \
+        [("12,332.1235", "-0", "4", "-16", "11111111")]
+    assert q(f"SELECT soundex('Miller'), levenshtein('kitten', 'sitting'), substring_index('www.apache.org', '.', 2), "
+             f"substring_index('www.apache.org', '.', -2), chr(65), octet_length('é') {one}")[0] == \
+        [("M460", 3, "www.apache", "apache.org", "A", 2)]
+    assert q(f"SELECT format_string('Hello World %d %s', 100, 'days'), printf('%5.2f|%-4s|%x', 3.14159, 'ab', 255) "
+             f"{one}")[0] == [("Hello World 100 days", " 3.14|ab  |ff")]
+    assert q(f"SELECT typeof(id), typeof(v), spark_partition_id() {one}")[0] == [("bigint", "double", 0)]
