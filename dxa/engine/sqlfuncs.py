@@ -1465,7 +1465,7 @@ def _substring_index(s, delim, count):
     return delim.join(parts[:count]) if count > 0 else delim.join(parts[count:])
 
 
-def _java_format(fmt, *args):
+def _java_printf(fmt, *args):
     """format_string / printf: Java Formatter specs mapped onto Python's % formatting (%s %d %f %e %x %o %c %b %%,
     flags and widths)."""
     import re as _re
@@ -1491,6 +1491,15 @@ def _java_format(fmt, *args):
     return _re.sub(r"%([-#+ 0,(]*)(\d+)?(\.\d+)?([a-zA-Z%])", conv, str(fmt))
 
 
+def _overlay(s, rep, pos, ln=None):
+    """overlay(input, replace, pos[, len]): Spark's Overlay — input[:pos-1] + replace + input[pos-1+len:], len
+    defaulting to the replacement's length."""
+    s, rep, pos = str(s), str(rep), int(pos)
+    ln = len(rep) if ln is None or int(ln) < 0 else int(ln)
+    start = max(pos - 1, 0)
+    return s[:start] + rep + s[start + ln:]
+
+
 def _register_more():
     reg = register_function
     reg("shiftleft", _f_shift("left"))
@@ -1513,8 +1522,9 @@ def _register_more():
     reg("chr", _host_string_fn(lambda x: chr(int(x) % 256) if int(x) >= 0 else ""))
     reg("octet_length", _host_string_fn(lambda s: len(str(s).encode("utf-8")), "int"))
     reg("bit_length", _host_string_fn(lambda s: 8 * len(str(s).encode("utf-8")), "int"))
-    reg("format_string", _host_string_fn(_java_format))
-    reg("printf", _host_string_fn(_java_format))
+    reg("overlay", _host_string_fn(_overlay))
+    reg("format_string", _host_string_fn(_java_printf))
+    reg("printf", _host_string_fn(_java_printf))
 
 
 _register_more()

@@ -122,6 +122,14 @@ def parse_duration_micros(text: str) -> int:
     return total
 
 
+_EXTRACT_FIELDS = {"year": "year", "years": "year", "yr": "year", "quarter": "quarter", "qtr": "quarter",
+                   "month": "month", "months": "month", "mon": "month", "week": "weekofyear", "weeks": "weekofyear",
+                   "day": "dayofmonth", "days": "dayofmonth", "d": "dayofmonth", "dayofweek": "dayofweek",
+                   "dow": "dayofweek", "doy": "dayofyear", "dayofyear": "dayofyear", "hour": "hour", "hours": "hour",
+                   "h": "hour", "minute": "minute", "minutes": "minute", "min": "minute", "second": "second",
+                   "seconds": "second", "s": "second"}
+
+
 class Parser:
     def __init__(self, sql: str):
         self.sql = sql
@@ -704,6 +712,40 @@ class Parser:
             self.advance()
             self.advance()
             return self._maybe_over(A.Call(low, [], star=True))
+        if low == "extract" and self.peek().kind in ("id", "kw") and self.is_word("from", tok=self.peek()):
+            # EXTRACT(field FROM source) → the field's function (Spark's Extract)
+            field = self.advance().text.lower()
+            self.advance()
+            src = self.parse_expr()
+            self.expect_op(")")
+            fn = _EXTRACT_FIELDS.get(field)
+            if fn is None:
+                self.error(f"unknown EXTRACT field {field!r}")
+            return A.Call(fn, [src])
+        if low == "position":
+            # POSITION(substr IN str) → locate(substr, str); the comma form falls through
+            save = self.i
+            sub = self.parse_bitor()
+            if self.accept_kw("in"):
+                src = self.parse_expr()
+                self.expect_op(")")
+                return A.Call("locate", [sub, src])
+            self.i = save
+        if low == "overlay":
+            # OVERLAY(input PLACING replace FROM pos [FOR len])
+            save = self.i
+            inp = self.parse_expr()
+            if self.accept_word("placing"):
+                rep = self.parse_expr()
+                if not self.accept_kw("from"):
+                    self.error("expected FROM in OVERLAY")
+                pos = self.parse_expr()
+                args = [inp, rep, pos]
+                if self.accept_word("for"):
+                    args.append(self.parse_expr())
+                self.expect_op(")")
+                return A.Call("overlay", args)
+            self.i = save
         distinct = self.accept_kw("distinct")
         args = [self.parse_expr()]
         while self.accept_op(","):

@@ -364,3 +364,12 @@ def test_more_spark_builtins():
     assert q(f"SELECT format_string('Hello World %d %s', 100, 'days'), printf('%5.2f|%-4s|%x', 3.14159, 'ab', 255) "
              f"{one}")[0] == [("Hello World 100 days", " 3.14|ab  |ff")]
     assert q(f"SELECT typeof(id), typeof(v), spark_partition_id() {one}")[0] == [("bigint", "double", 0)]
+
+
+def test_extract_position_overlay_syntax():
+    one = "FROM T WHERE id = 1"
+    # T0 = 2019-02-28 23:00:00 UTC (a Thursday: dayofweek 5)
+    assert q(f"SELECT extract(YEAR FROM ts), extract(month FROM ts), extract(DAY FROM ts), extract(hour FROM ts), "
+             f"extract(dow FROM ts), extract(quarter FROM ts) {one}")[0] == [(2019, 2, 28, 23, 5, 1)]
+    assert q(f"SELECT position('b' IN name), position('b', name), overlay('Spark SQL' PLACING '_' FROM 6), "
+             f"overlay('Spark SQL' PLACING 'CORE' FROM 7 FOR 0) {one}")[0] == [(3, 3, "Spark_SQL", "Spark CORESQL")]
