@@ -373,3 +373,20 @@ def test_extract_position_overlay_syntax():
              f"extract(dow FROM ts), extract(quarter FROM ts) {one}")[0] == [(2019, 2, 28, 23, 5, 1)]
     assert q(f"SELECT position('b' IN name), position('b', name), overlay('Spark SQL' PLACING '_' FROM 6), "
              f"overlay('Spark SQL' PLACING 'CORE' FROM 7 FOR 0) {one}")[0] == [(3, 3, "Spark_SQL", "Spark CORESQL")]
+
+
+@pytest.mark.gpu
+def test_round3_sql_additions_gpu_match_cpu(gpu):
+    """count(a, b), non-equi outer joins, sliding window(), moments / max_by, bit and text built-ins, EXTRACT: the
+    device run gives the CPU run's rows."""
+    for sql in ["SELECT id, count(name, v) AS c, count(DISTINCT name, id) AS d FROM T GROUP BY id ORDER BY id",
+                "SELECT t.id, r.rid FROM T t LEFT JOIN R r ON r.w > t.v * 2 ORDER BY t.id, r.rid",
+                "SELECT id FROM T t LEFT ANTI JOIN R r ON r.w < t.v ORDER BY id",
+                "SELECT window(ts, '2 hours', '1 hour').start AS s, count(*) AS c FROM T "
+                "GROUP BY window(ts, '2 hours', '1 hour') ORDER BY s",
+                "SELECT id, covar_pop(v, id) AS cp, max_by(name, v) AS mb, min_by(v, id) AS nb FROM T GROUP BY id "
+                "ORDER BY id",
+                "SELECT shiftleft(id, 3) AS a, bit_count(id) AS b, width_bucket(v, 0, 5, 5) AS w, "
+                "next_day(to_date(ts), 'Mon') AS nd, extract(hour FROM ts) AS h, substring_index(name, ',', 1) AS si "
+                "FROM T ORDER BY id, v"]:
+        assert q(sql, gpu) == q(sql, "cpu"), sql
