@@ -1500,6 +1500,38 @@ def _overlay(s, rep, pos, ln=None):
     return s[:start] + rep + s[start + ln:]
 
 
+def _arrays_overlap(l, m):
+    if m is None:
+        return None
+    a = {x for x in l if x is not None}
+    if any(x in a for x in m if x is not None):
+        return True
+    return None if (l and m and (None in l or None in m)) else False
+
+
+def _dedup(xs):
+    out, seen, null = [], set(), False
+    for x in xs:
+        if x is None:
+            if not null:
+                out.append(None)
+                null = True
+        elif x not in seen:
+            seen.add(x)
+            out.append(x)
+    return out
+
+
+def _f_flatten(e, scope, ctx, subst):
+    (arr,) = _args(e, scope, ctx, subst)
+    if not isinstance(arr, ArrayColumn) or not arr.elements or not isinstance(arr.elements[0], ArrayColumn):
+        raise EvalError("flatten() expects an array of arrays")
+    inner = arr.elements[0]
+    et = str(inner.elements[0].dtype) if inner.elements else "string"
+    out = [None if l is None or any(x is None for x in l) else [y for x in l for y in x] for l in arr.to_pylist()]
+    return array_from_pylist(out, et, scope.device)
+
+
 def _register_more():
     reg = register_function
     reg("shiftleft", _f_shift("left"))
@@ -1523,6 +1555,11 @@ def _register_more():
     reg("octet_length", _host_string_fn(lambda s: len(str(s).encode("utf-8")), "int"))
     reg("bit_length", _host_string_fn(lambda s: 8 * len(str(s).encode("utf-8")), "int"))
     reg("overlay", _host_string_fn(_overlay))
+    reg("arrays_overlap", _host_array_fn(_arrays_overlap, scalar_type="boolean"))
+    reg("array_union", _host_array_fn(lambda l, m: None if m is None else _dedup(list(l) + list(m))))
+    reg("array_intersect", _host_array_fn(lambda l, m: None if m is None else _dedup([x for x in l if x in m])))
+    reg("array_except", _host_array_fn(lambda l, m: None if m is None else _dedup([x for x in l if x not in m])))
+    reg("flatten", _f_flatten)
     reg("format_string", _host_string_fn(_java_printf))
     reg("printf", _host_string_fn(_java_printf))
 

@@ -390,3 +390,11 @@ def test_round3_sql_additions_gpu_match_cpu(gpu):
                 "next_day(to_date(ts), 'Mon') AS nd, extract(hour FROM ts) AS h, substring_index(name, ',', 1) AS si "
                 "FROM T ORDER BY id, v"]:
         assert q(sql, gpu) == q(sql, "cpu"), sql
+
+
+def test_array_set_functions_and_flatten():
+    one = "FROM T WHERE id = 1"
+    assert q(f"SELECT flatten(array(array(1), array(2, 3))), arrays_overlap(array(1, 2), array(2)), "
+             f"arrays_overlap(array(1), array(3)), array_union(array(1, 2, 2), array(2, 3)), "
+             f"array_intersect(array(1, 2), array(2, 3)), array_except(array(1, 2), array(2, 3)) {one}")[0] == \
+        [([1, 2, 3], True, False, [1, 2, 3], [2], [1])]
