@@ -1532,6 +1532,26 @@ def _f_flatten(e, scope, ctx, subst):
     return array_from_pylist(out, et, scope.device)
 
 
+def _json_ddl(v) -> str:
+    """Spark's JsonInferSchema type of one JSON value, as schema_of_json prints it (fields sorted by name)."""
+    if isinstance(v, bool):
+        return "boolean"
+    if isinstance(v, int):
+        return "bigint"
+    if isinstance(v, float):
+        return "double"
+    if isinstance(v, dict):
+        return "struct<" + ",".join(f"{k}:{_json_ddl(x)}" for k, x in sorted(v.items())) + ">"
+    if isinstance(v, list):
+        kinds = {_json_ddl(x) for x in v if x is not None}
+        if not kinds:
+            return "array<string>"
+        if kinds <= {"bigint", "double"}:
+            return "array<double>" if "double" in kinds else "array<bigint>"
+        return f"array<{kinds.pop()}>" if len(kinds) == 1 else "array<string>"
+    return "string"
+
+
 def _register_more():
     reg = register_function
     reg("shiftleft", _f_shift("left"))
@@ -1560,6 +1580,7 @@ def _register_more():
     reg("array_intersect", _host_array_fn(lambda l, m: None if m is None else _dedup([x for x in l if x in m])))
     reg("array_except", _host_array_fn(lambda l, m: None if m is None else _dedup([x for x in l if x not in m])))
     reg("flatten", _f_flatten)
+    reg("schema_of_json", _host_string_fn(lambda t: _json_ddl(json.loads(str(t)))))
     reg("format_string", _host_string_fn(_java_printf))
     reg("printf", _host_string_fn(_java_printf))
 

@@ -398,3 +398,8 @@ def test_array_set_functions_and_flatten():
              f"arrays_overlap(array(1), array(3)), array_union(array(1, 2, 2), array(2, 3)), "
              f"array_intersect(array(1, 2), array(2, 3)), array_except(array(1, 2), array(2, 3)) {one}")[0] == \
         [([1, 2, 3], True, False, [1, 2, 3], [2], [1])]
+
+
+def test_schema_of_json():
+    assert q("SELECT schema_of_json('[{\"col\":0}]') AS a, schema_of_json('{\"b\":1.5,\"a\":[1,2],\"c\":\"x\"}') AS b "
+             "FROM T WHERE id = 1")[0] == [("array<struct<col:bigint>>", "struct<a:array<bigint>,b:double,c:string>")]
