@@ -856,7 +856,21 @@ def _exec_generator_select(sel: A.Select, items, gen_at, scope: Scope, ctx) -> T
     if len(gen_at) > 1:
         raise QueryError("only one generator is allowed per SELECT clause")
     if sel.group_by or any(_contains_agg(e, ctx) for e, _ in items):
-        raise QueryError("generators are not supported together with aggregation in one SELECT")
+        # Spark's ExtractGenerator over an Aggregate: aggregate first (the generator's arguments become hidden
+        # aggregate outputs, e.g. explode(collect_list(v))), then generate over the aggregated rows
+        import dataclasses
+        k = gen_at[0]
+        call, alias = items[k]
+        hidden = [f"__dxa_gen{i}" for i in range(len(call.args))]
+        others = [(e, nm) for j, (e, nm) in enumerate(items) if j != k]
+        agg = _aggregate(sel, others + list(zip(call.args, hidden)), scope, ctx)
+        ascope = Scope.of_table(agg)
+        ascope.dist = getattr(agg, "dist", P.REPLICATED)
+        gcall = A.Call(call.name, [A.Ident((h,)) for h in hidden], call.distinct, call.star)
+        items2 = [(A.Ident((nm,)), nm) for e, nm in others]
+        items2.insert(k, (gcall, alias))
+        plain = dataclasses.replace(sel, group_by=[], having=None, grouping_sets=None)
+        return _exec_generator_select(plain, items2, [k], ascope, ctx)
     k = gen_at[0]
     call, alias = items[k]
     rows, names, gcols = GEN.generate(call, scope, ctx)
@@ -1243,6 +1257,10 @@ def _collect(groups: G.Groups, arg, as_set):
             continue
         out[g].append(v)
     from .types import ArrayType
+    if isinstance(arg, (PrimColumn, StrColumn)) and isinstance(arg.dtype, str):
+        # a real array column (fixed slots): explode, size, array functions and JSON output all take it
+        from .sqlfuncs import array_from_pylist
+        return array_from_pylist(out, arg.dtype, groups.rep.device)
     return strings_from_pylist([json.dumps([json_value(x, arg.dtype) for x in o], separators=(",", ":"))
                                 for o in out], groups.rep.device, ArrayType(arg.dtype))
 

@@ -403,3 +403,11 @@ def test_array_set_functions_and_flatten():
 def test_schema_of_json():
     assert q("SELECT schema_of_json('[{\"col\":0}]') AS a, schema_of_json('{\"b\":1.5,\"a\":[1,2],\"c\":\"x\"}') AS b "
              "FROM T WHERE id = 1")[0] == [("array<struct<col:bigint>>", "struct<a:array<bigint>,b:double,c:string>")]
+
+
+def test_generator_over_aggregate():
+    """SELECT k, explode(collect_list(v)) … GROUP BY k: aggregate first, then generate (Spark's ExtractGenerator)."""
+    rows, names = q("SELECT id, explode(collect_list(v)) AS x FROM T GROUP BY id ORDER BY id, x")
+    assert names == ["id", "x"] and rows == [(1, 1.5), (2, 4.0), (3, 3.25)]
+    rows, _ = q("SELECT id, posexplode(collect_list(id)) FROM T GROUP BY id HAVING count(*) > 1")
+    assert rows == [(2, 0, 2), (2, 1, 2)]
