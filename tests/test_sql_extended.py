@@ -386,6 +386,8 @@ def test_round3_sql_additions_gpu_match_cpu(gpu):
                 "GROUP BY window(ts, '2 hours', '1 hour') ORDER BY s",
                 "SELECT id, covar_pop(v, id) AS cp, max_by(name, v) AS mb, min_by(v, id) AS nb FROM T GROUP BY id "
                 "ORDER BY id",
+                "SELECT id, explode(collect_list(v)) AS x FROM T GROUP BY id ORDER BY id, x",
+                "SELECT flatten(array(array(id), array(id, 2))) AS f, array_union(array(id), array(2)) AS u FROM T",
                 "SELECT shiftleft(id, 3) AS a, bit_count(id) AS b, width_bucket(v, 0, 5, 5) AS w, "
                 "next_day(to_date(ts), 'Mon') AS nd, extract(hour FROM ts) AS h, substring_index(name, ',', 1) AS si "
                 "FROM T ORDER BY id, v"]:
