@@ -232,7 +232,9 @@ __global__ __launch_bounds__(256) void gen_slot_kernel(GenArgs g) {
   const int64_t start = i * g.stride;
   const int64_t len = render<true>(g, t, i, g.out + start);
   const_cast<int64_t*>(g.offs)[i] = start;
-  g.ends[i] = start + (len <= g.stride ? len : 0);     // an over-long record (a bound bug) becomes an empty row
+  // len <= stride by construction (GenProgram.max_len bounds every op's text); were the bound ever wrong, the row
+  // is published empty so the parser reports it malformed instead of reading into the next slot
+  g.ends[i] = start + (len <= g.stride ? len : 0);
   if (i == g.n - 1) const_cast<int64_t*>(g.offs)[g.n] = g.n * g.stride;
 }
 
