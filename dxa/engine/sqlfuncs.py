@@ -1552,6 +1552,33 @@ def _json_ddl(v) -> str:
     return "string"
 
 
+def _f_zip_with(e, scope, ctx, subst):
+    """zip_with(a, b, (x, y) -> f): element-wise over the longer array's length, the shorter side padded with nulls
+    (Spark's ZipWith).  Fixed-length arrays only: a slot-compacted (variable-length) array cannot hold the null
+    elements the padding produces."""
+    from .expr import _lambda_arg
+    a = evaluate(e.args[0], scope, ctx, subst)
+    b = evaluate(e.args[1], scope, ctx, subst)
+    if not (isinstance(a, ArrayColumn) and isinstance(b, ArrayColumn)):
+        raise EvalError("zip_with() expects two arrays")
+    if a.drop_nulls or b.drop_nulls:
+        raise EvalError("zip_with() over variable-length arrays is not supported")
+    lam = _lambda_arg(e, 2)
+    if len(lam.params) != 2:
+        raise EvalError("zip_with() takes a two-argument lambda")
+    n, dev = scope.length, scope.device
+
+    def slot(arr, j):
+        if j < len(arr.elements):
+            return arr.elements[j]
+        t = str(arr.elements[0].dtype) if arr.elements else "string"
+        return ConstColumn(None, t, n, dev)
+    out = [evaluate(lam.body, scope.with_bindings(list(lam.params), [slot(a, j), slot(b, j)]), ctx, subst)
+           for j in range(max(len(a.elements), len(b.elements)))]
+    valid = a.valid if b.valid is None else (b.valid if a.valid is None else a.valid & b.valid)
+    return ArrayColumn(out, n, valid, False, dev)
+
+
 def _register_more():
     reg = register_function
     reg("shiftleft", _f_shift("left"))
@@ -1580,6 +1607,7 @@ def _register_more():
     reg("array_intersect", _host_array_fn(lambda l, m: None if m is None else _dedup([x for x in l if x in m])))
     reg("array_except", _host_array_fn(lambda l, m: None if m is None else _dedup([x for x in l if x not in m])))
     reg("flatten", _f_flatten)
+    reg("zip_with", _f_zip_with)
     reg("schema_of_json", _host_string_fn(lambda t: _json_ddl(json.loads(str(t)))))
     reg("format_string", _host_string_fn(_java_printf))
     reg("printf", _host_string_fn(_java_printf))

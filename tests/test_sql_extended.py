@@ -413,3 +413,9 @@ def test_generator_over_aggregate():
     assert names == ["id", "x"] and rows == [(1, 1.5), (2, 4.0), (3, 3.25)]
     rows, _ = q("SELECT id, posexplode(collect_list(id)) FROM T GROUP BY id HAVING count(*) > 1")
     assert rows == [(2, 0, 2), (2, 1, 2)]
+
+
+def test_zip_with():
+    assert q("SELECT zip_with(array(1, 2), array(3, 4, 5), (x, y) -> x + y) AS z, "
+             "zip_with(array('a', 'b'), array('c', 'd'), (x, y) -> concat(x, y)) AS c FROM T WHERE id = 1")[0] == \
+        [([4, 6, None], ["ac", "bd"])]
