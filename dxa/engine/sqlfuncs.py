@@ -1579,6 +1579,22 @@ def _f_zip_with(e, scope, ctx, subst):
     return ArrayColumn(out, n, valid, False, dev)
 
 
+def _f_map_from_arrays(e, scope, ctx, subst):
+    """map_from_arrays(keys, values) with a constant key array (this engine's maps have constant keys): the map
+    whose key i holds element i of ``values``."""
+    from .expr import _const_str
+    ks = evaluate(e.args[0], scope, ctx, subst)
+    vs = evaluate(e.args[1], scope, ctx, subst)
+    if not (isinstance(ks, ArrayColumn) and all(isinstance(k, ConstColumn) for k in ks.elements)):
+        raise EvalError("map_from_arrays() needs a constant key array")
+    if not isinstance(vs, ArrayColumn) or len(vs.elements) != len(ks.elements) or vs.drop_nulls:
+        raise EvalError("map_from_arrays() needs a fixed-length value array of the keys' length")
+    names = [_const_str(k) for k in ks.elements]
+    if len(set(names)) != len(names):
+        raise EvalError("map_from_arrays(): duplicate map keys")
+    return StructColumn(names, list(vs.elements), scope.length, vs.valid, True, None, scope.device)
+
+
 def _register_more():
     reg = register_function
     reg("shiftleft", _f_shift("left"))
@@ -1608,6 +1624,7 @@ def _register_more():
     reg("array_except", _host_array_fn(lambda l, m: None if m is None else _dedup([x for x in l if x not in m])))
     reg("flatten", _f_flatten)
     reg("zip_with", _f_zip_with)
+    reg("map_from_arrays", _f_map_from_arrays)
     reg("schema_of_json", _host_string_fn(lambda t: _json_ddl(json.loads(str(t)))))
     reg("format_string", _host_string_fn(_java_printf))
     reg("printf", _host_string_fn(_java_printf))

@@ -419,3 +419,8 @@ def test_zip_with():
     assert q("SELECT zip_with(array(1, 2), array(3, 4, 5), (x, y) -> x + y) AS z, "
              "zip_with(array('a', 'b'), array('c', 'd'), (x, y) -> concat(x, y)) AS c FROM T WHERE id = 1")[0] == \
         [([4, 6, None], ["ac", "bd"])]
+
+
+def test_map_from_arrays_constant_keys():
+    assert q("SELECT map_from_arrays(array('a', 'b'), array(id, 2)) AS m FROM T WHERE id = 1")[0] == \
+        [({"a": 1, "b": 2},)]
