@@ -40,6 +40,9 @@ class StreamingHost:
         self._stop = threading.Event()
         self.batches = 0
         self.history: List[Dict[str, float]] = []
+        declare = getattr(processor, "declare_source_metrics", None)
+        if declare is not None:
+            declare(getattr(source, "metric_names", ()))
 
     def stop(self):
         self._stop.set()

@@ -58,7 +58,8 @@ class RawBatch:
                                               # values in decompressed record batches); offs[n] = end of the bytes
     pending: Optional[Any] = None             # jsonparse.PendingParse started by Processor.prepare
     status: Optional[Any] = None              # source-side decode status (kafka_device.DecodeStatus), checked by
-                                              # the source before the batch's offsets are committed
+                                              # process_batch before the transform (no row of a corrupt batch
+                                              # reaches a sink or an accumulator)
     file_rows: Optional[List[Tuple[Dict[str, str], int]]] = None   # per-file FileInternal + its row count, in row
                                               # order (blob-pointer batches: the FileInfo column varies per row)
     source_metrics: Optional[Dict[str, float]] = None   # e.g. InputBlobs / Latency-Blobs, merged into the batch's
@@ -148,6 +149,7 @@ class Processor:
         self._inflight: Optional[_InFlight] = None
         self.completed: List = []
         self.on_batch_complete = None
+        self.source_metric_names: Tuple[str, ...] = ()
         self.clock: Callable[[], float] = time.time     # current_timestamp() of a batch (tests pin it)
 
     # ------------------------------------------------------------------------------------------------------------
@@ -284,7 +286,7 @@ class Processor:
         cat._built = getattr(self, "_ref_built", {})
         self._ref_built = cat._built
         metrics["Input_Normalized_Events_Count"] = projected.length
-        metrics.update(getattr(self, "_source_metrics", None) or {})
+        metrics.update(self._batch_source_metrics())
         part = P.PARTITIONED if P.active() else P.REPLICATED
         projected.dist = part
         if self.window_store is not None:
@@ -356,6 +358,24 @@ class Processor:
             self._sync()
             self.stage_times["output"] = time.perf_counter() - t1
         return fl.metrics
+
+    def declare_source_metrics(self, names) -> None:
+        """The metric names the source may attach to a batch (``Source.metric_names``).  Every batch carries all of
+        them — zero, or ``-inf`` for a latency (dropped after the reduction when no rank measured it) — so the key
+        set every rank all-reduces does not depend on its data: an empty batch or a batch without file times on one
+        rank still matches the others."""
+        self.source_metric_names = tuple(names or ())
+
+    def _batch_source_metrics(self) -> Dict[str, float]:
+        got = dict(getattr(self, "_source_metrics", None) or {})
+        declared = getattr(self, "source_metric_names", ())
+        out = {k: (float("-inf") if P.is_max_metric(k) else 0.0) for k in declared}
+        undeclared = sorted(set(got) - set(declared))
+        if undeclared and P.active():
+            raise EvalError(f"source metrics {undeclared} were not declared (Source.metric_names): at N ranks the "
+                            f"batch metric key set must not depend on the data")
+        out.update(got)
+        return out
 
     def _query(self, cmd):
         q = self._parsed.get(cmd.text)
@@ -553,14 +573,17 @@ class Processor:
                 metrics[f"Output_{name}_{k}"] = float(v)
         for st in self.state_tables.values():
             st.flush()                 # this rank's standby part is durable before the all-reduce (= the barrier)
-        if P.active():
-            # batch metrics are job-wide: one all-reduce of the count vector (timings stay per-rank)
-            keys = sorted(metrics)
-            vec = torch.tensor([float(metrics[k]) for k in keys], dtype=torch.float64, device=self.device)
-            P.all_reduce_sum(vec)
-            metrics.update(zip(keys, vec.tolist()))
+        # batch metrics are job-wide: counts summed, latencies maxed over ranks, key sets checked first (timings
+        # stay per-rank)
+        metrics = fl.metrics = P.reduce_metrics(metrics, self.device)
+        flipped = False
         for st in self.state_tables.values():
+            flipped |= st.modified
             st.persist()
+        if flipped and P.active():
+            # rank 0 flipped metadata.info just now: no rank may overwrite the copy the old metadata named (its next
+            # standby) before that flip is on disk — the next batch's standby writes are ordered after this point
+            P.order_point(self.device)
         metrics.update(tracing.stage_metrics(fl.stages))          # per-rank stage timings (not all-reduced)
         # processing latency = batch start → its last sink write finished (measured where the write finished, not
         # where the completion was observed)
@@ -614,6 +637,12 @@ class Processor:
         try:
             _maybe_inject_fault(self.batches)
             projected = self.project(raw, batch_time_us, ctx)
+            # a device-side decode failure (corrupt LZ4 block, bad CRC) must stop the batch before any of its rows
+            # reach an accumulator or a sink — the host decoder raises at the same point (before processing).  The
+            # status word sits in pinned memory behind the decode, which the parse above already waited for
+            check = getattr(raw.status, "raise_if_failed", None)
+            if check is not None:
+                check(f"batch {batch_time_us}")
             metrics = self.route(projected, batch_time_us, interval_us, ctx,
                                  partition_time or _dt.datetime.utcnow(), t0)
             self.batches += 1

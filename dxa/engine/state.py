@@ -148,7 +148,9 @@ class StateTable:
         self._wait_write()
 
     def persist(self):
-        """Flip ``metadata.info`` (rank 0 only; every rank's part must already be durable — see ``flush``)."""
+        """Flip ``metadata.info`` (rank 0 only; every rank's part must already be durable — see ``flush``).  At N
+        ranks the processor follows the flips with ``parallel.order_point``: the next batch's standby writes (into
+        the copy the previous metadata named active) are ordered after rank 0's flip."""
         self._wait_write()
         if self.modified:
             if self.rank == 0:

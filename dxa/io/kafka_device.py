@@ -436,6 +436,12 @@ class DecodeStatus:
         self.event.synchronize()
         return int(self.host[0])
 
+    def raise_if_failed(self, what: str = "batch"):
+        """Called by the processor before a batch's rows reach a state table or a sink."""
+        bad = self.failed()
+        if bad:
+            raise DecodeError(f"{what}: {bad} Kafka record batch(es) failed to decode on the device")
+
 
 _CRC_POLY = 0x82F63B78
 

@@ -42,6 +42,9 @@ class SourceError(Exception):
 
 class Source:
     name = "source"
+    # metric names this source may attach to a batch (RawBatch.source_metrics); the processor zero-fills the absent
+    # ones so every rank all-reduces the same key set
+    metric_names: Tuple[str, ...] = ()
 
     def next_batch(self, batch_time_us: int) -> Optional[RawBatch]:
         raise NotImplementedError
@@ -261,6 +264,7 @@ class BlobPointerSource(Source):
     (BlobPointerInput.filterPathGroups).  Without sources, every path (optionally filtered by ``path_regex``) is
     read.  Per batch: ``InputBlobs`` and ``Latency-Blobs`` (now − earliest file time)."""
     name = "blobpointer"
+    metric_names = ("InputBlobs", "Latency-Blobs")
 
     def __init__(self, inner: Source, device, path_regex: Optional[str] = None, settings=None):
         self.inner = inner

@@ -445,8 +445,10 @@ class TdsClient:
         string, timestamp."""
         specs = [_bulk_type(t) for _n, t in columns]
         hints = " WITH (TABLOCK)" if table_lock else ""
-        self.execute(f"INSERT BULK {quote_ident(table)} (" +
-                     ", ".join(f"{quote_ident(n)} {s[0]}" for (n, _t), s in zip(columns, specs)) + ")" + hints)
+        # the rows are encoded BEFORE the INSERT BULK statement goes out: a value the bulk format cannot carry
+        # (a string over 4000 characters) raises here, while the connection is still idle — once INSERT BULK is
+        # acknowledged the server accepts nothing but the BulkLoadBCP message, so a fallback to INSERT must start
+        # from an idle connection
         msg = bytearray(b"\x81") + struct.pack("<H", len(columns))
         for (name, _t), spec in zip(columns, specs):
             msg += struct.pack("<IH", 0, 0x0009) + spec[1]
@@ -457,6 +459,8 @@ class TdsClient:
             for v, spec in zip(row, specs):
                 msg += spec[2](v)
         msg += b"\xfd" + struct.pack("<HHQ", 0, 0, 0)
+        self.execute(f"INSERT BULK {quote_ident(table)} (" +
+                     ", ".join(f"{quote_ident(n)} {s[0]}" for (n, _t), s in zip(columns, specs)) + ")" + hints)
         self.ch.send(_packet(PT_BULK, bytes(msg), self.packet_size))
         _t, reply = self.ch.read_message()
         r = parse_reply(reply)

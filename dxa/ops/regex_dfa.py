@@ -14,6 +14,7 @@ the host regex.  The DFA is built over byte equivalence classes and kept ≤ 16 
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass
 from typing import Dict, FrozenSet, List, Optional, Tuple
 
@@ -459,16 +460,61 @@ def run_dfa(dfa: DFA, data: bytes) -> bool:
     return bool(dfa.accept[st])
 
 
+_INLINE_FLAGS = re.compile(r"\(\?([idmsuxU]*)(?:-([idmsuxU]*))?([:)])")
+_LT_ALL = "\\n\\r\\u0085\\u2028\\u2029"
+
+
 def java_to_python(pattern: str) -> str:
-    """Host-regex form of a Java pattern for the cases ``re`` reads differently: ``.`` does not take \\r or the
-    Unicode line terminators.  (Use with ``re.ASCII`` so that ``\\d\\w\\s`` are ASCII as in Java.)"""
+    """Host-regex form of a Java pattern for the cases ``re`` reads differently (use with ``re.ASCII`` so that
+    ``\\d\\w\\s`` are ASCII as in Java):
+
+    * ``.`` takes no line terminator (\\n \\r U+0085 U+2028 U+2029) — any character under ``(?s)`` (DOTALL);
+    * ``$`` is end of input or before a FINAL line terminator; under ``(?m)`` (MULTILINE) before ANY line terminator
+      (never between \\r and \\n) or at the end (java.util.regex.Pattern.Dollar);
+    * ``^`` under ``(?m)`` is the start, or after any line terminator except at the end of input (Pattern.Caret);
+    * ``(?d)`` (UNIX_LINES) makes \\n the only line terminator for all three.
+
+    Inline flags apply from where they appear to the end of the enclosing group, or inside ``(?flags:…)``; the
+    ``m``/``s``/``d`` semantics are compiled into the output here, so those letters (and ``u``/``U``) are removed
+    from the flag groups Python sees."""
     out, i, in_cls = [], 0, False
+    flags = set()
+    stack = []
     while i < len(pattern):
         c = pattern[i]
         if c == "\\" and i + 1 < len(pattern):
             out.append(pattern[i:i + 2])
             i += 2
             continue
+        if not in_cls and c == "(":
+            m = _INLINE_FLAGS.match(pattern, i)
+            if m:
+                on, off, end = set(m.group(1)), set(m.group(2) or ""), m.group(3)
+                new = (flags | on) - off
+                keep_on = "".join(f for f in m.group(1) if f in "ix")
+                keep_off = "".join(f for f in (m.group(2) or "") if f in "ix")
+                grp = keep_on + ("-" + keep_off if keep_off else "")
+                if end == ":":
+                    stack.append(flags)
+                    flags = new
+                    out.append(f"(?{grp}:" if grp else "(?:")
+                else:
+                    flags = new
+                    if grp:
+                        out.append(f"(?{grp})")
+                i = m.end()
+                continue
+            stack.append(set(flags))
+            out.append(c)
+            i += 1
+            continue
+        if not in_cls and c == ")":
+            if stack:
+                flags = stack.pop()
+            out.append(c)
+            i += 1
+            continue
+        lt = "\\n" if "d" in flags else _LT_ALL
         if in_cls:
             if c == "]":
                 in_cls = False
@@ -486,13 +532,26 @@ def java_to_python(pattern: str) -> str:
                 i += 2
                 continue
         elif c == ".":
-            out.append(r"[^\n\r\u0085\u2028\u2029]")
+            out.append(r"[\s\S]" if "s" in flags else f"[^{lt}]")
             i += 1
             continue
         elif c == "$":
-            # Java's $ (no MULTILINE): end of input, or before a final line terminator — \r\n, \n (not right
-            # after a \r), \r, U+0085, U+2028, U+2029 (Pattern.Dollar); Python's $ knows only a final \n
-            out.append(r"(?:(?=\r\n\Z)|(?<!\r)(?=\n\Z)|(?=[\r\u0085\u2028\u2029]\Z)|\Z)")
+            if "d" in flags:
+                out.append(r"(?=\n)" if "m" in flags else r"(?:(?=\n\Z)|\Z)")
+            elif "m" in flags:
+                # MULTILINE: before any line terminator (before the \r of \r\n, never between them), or the end
+                out.append(r"(?:(?=[\r\u0085\u2028\u2029])|(?<!\r)(?=\n)|\Z)")
+            else:
+                # end of input, or before a final line terminator — \r\n, \n (not right after a \r), \r, U+0085,
+                # U+2028, U+2029 (Pattern.Dollar); Python's $ knows only a final \n
+                out.append(r"(?:(?=\r\n\Z)|(?<!\r)(?=\n\Z)|(?=[\r\u0085\u2028\u2029]\Z)|\Z)")
+            i += 1
+            continue
+        elif c == "^" and "m" in flags:
+            if "d" in flags:
+                out.append(r"(?:\A|(?<=\n)(?!\Z))")
+            else:
+                out.append(r"(?:\A|(?<=[\n\u0085\u2028\u2029])(?!\Z)|(?<=\r)(?!\n)(?!\Z))")
             i += 1
             continue
         out.append(c)

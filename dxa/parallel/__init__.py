@@ -10,7 +10,8 @@ The reference scales by data-partition parallelism with Spark hash exchanges und
   packed [rows × cols] int64 matrix (+ one for string bytes) routed by ``hash(keys) % world`` → merge on the owner.
   Only partials cross xGMI (kilobytes per batch for the IoT flow), so the exchange is latency-, not link-bound;
 * joins of two partitioned inputs shuffle both sides by join-key hash; partitioned ⨝ replicated joins are local;
-* batch metrics are summed with one all-reduce; rank 0 emits them.
+* batch metrics have a rank-independent key set (checked by digest before any value moves); counts are summed and
+  latencies maxed over ranks; rank 0 emits them.
 
 ``init`` is a no-op for world size 1, which keeps the single-GPU path free of collectives.  Multi-process CPU
 tests run the same code over gloo.
@@ -110,5 +111,6 @@ def set_dist(table, d: str):
     return table
 
 
-from .exchange import (all_reduce_sum, allgather_table, broadcast_bytes, broadcast_table,  # noqa: E402
-                       broadcast_tensor, rebalance_table, shuffle_table, split_by_destination)
+from .exchange import (MetricKeysMismatch, all_reduce_sum, allgather_table, broadcast_bytes,  # noqa: E402
+                       broadcast_table, broadcast_tensor, is_max_metric, order_point, rebalance_table, reduce_metrics,
+                       shuffle_table, split_by_destination)

@@ -72,6 +72,71 @@ def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+class MetricKeysMismatch(RuntimeError):
+    """Ranks entered the batch-metrics reduction with different key sets."""
+
+
+def is_max_metric(name: str) -> bool:
+    """Metrics whose job-wide value is the maximum over ranks: latencies (``Latency-Blobs`` is measured from the
+    earliest blob time of the whole batch, CommonProcessorFactory.scala:573-576 — the largest per-rank latency)."""
+    return name.startswith("Latency-")
+
+
+def _keys_digest(keys: List[str]) -> int:
+    import hashlib
+    h = hashlib.blake2b("\n".join(keys).encode("utf-8"), digest_size=8).digest()
+    return int.from_bytes(h, "little") & ((1 << 52) - 1)       # exact in a float64
+
+
+def reduce_metrics(metrics: dict, device) -> dict:
+    """Job-wide batch metrics: counts summed, latencies maxed over ranks (``is_max_metric``).
+
+    The values travel as vectors ordered by sorted key, so every rank must hold the same key set.  That is checked
+    first with one 4-element MAX all-reduce of (digest, −digest, count, −count) of the key list: a mismatch shows on
+    every rank (the largest digest differs from some rank's own, the smallest from another's) and raises
+    ``MetricKeysMismatch`` instead of handing RCCL mismatched buffers (a hang or a silent mis-sum).  Then one SUM and
+    one MAX all-reduce, read back with one host sync.  A MAX metric holding ``-inf`` on every rank (declared but
+    not measured anywhere, e.g. ``Latency-Blobs`` of a batch without file times) is dropped, as the reference omits
+    it."""
+    if _w() <= 1:
+        return {k: v for k, v in metrics.items() if not (is_max_metric(k) and v == float("-inf"))}
+    keys = sorted(metrics)
+    d = _keys_digest(keys)
+    chk = torch.tensor([d, -d, len(keys), -len(keys)], dtype=torch.float64, device=device)
+    _all_reduce(chk, dist.ReduceOp.MAX)
+    got = chk.tolist()
+    if got != [float(d), float(-d), float(len(keys)), float(-len(keys))]:
+        from . import rank
+        raise MetricKeysMismatch(f"rank {rank()}: batch metric keys differ across ranks ({len(keys)} keys here: "
+                                 f"{keys})")
+    skeys = [k for k in keys if not is_max_metric(k)]
+    mkeys = [k for k in keys if is_max_metric(k)]
+    vs = torch.tensor([float(metrics[k]) for k in skeys], dtype=torch.float64, device=device)
+    vm = torch.tensor([float(metrics[k]) for k in mkeys], dtype=torch.float64, device=device)
+    if skeys:
+        _all_reduce(vs, dist.ReduceOp.SUM)
+    if mkeys:
+        _all_reduce(vm, dist.ReduceOp.MAX)
+    out = dict(metrics)
+    vals = torch.cat([vs, vm]).tolist()
+    for k, v in zip(skeys + mkeys, vals):
+        if is_max_metric(k) and v == float("-inf"):
+            out.pop(k, None)
+        else:
+            out[k] = v
+    return out
+
+
+def order_point(device) -> None:
+    """A point every rank's later stream work is ordered after: one 1-element all-reduce on the current stream.
+    Over RCCL it does not block the host — work queued after it on this stream (and host threads waiting on events
+    recorded after it) cannot run before every rank has issued it, i.e. before every rank's host got here; over gloo
+    it is a host barrier."""
+    if _w() > 1:
+        t = torch.zeros(1, dtype=torch.float32, device=device)
+        _all_reduce(t, dist.ReduceOp.SUM)
+
+
 def _a2a_counts(counts: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(counts)
     _a2a(out, counts)

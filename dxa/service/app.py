@@ -51,7 +51,7 @@ WRITE_ROUTES = {"flow/save", "flow/schedulebatch", "flow/generateconfigs", "flow
                 "job/syncall", "job/syncbynames", "inputdata/inferschema", "inputdata/refreshsample",
                 "inputdata/refreshsampleandkernel", "kernel", "kernel/refresh", "kernel/deleteList", "kernel/delete",
                 "kernels/delete", "kernels/deleteall", "kernel/sampleinputfromquery", "kernel/executequery",
-                "ingest"}
+                "ingest", "metrics/ingest"}
 
 
 _FLOW_NAME = re.compile(r"^[A-Za-z0-9]+$")
@@ -397,19 +397,28 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
             return err(f"{type(e).__name__}: {e}")
 
     # -- metrics -------------------------------------------------------------------------------------------------
+    def _client(request: Request) -> Optional[str]:
+        return request.client.host if request.client else None
+
     @app.get("/api/metrics/get")
-    def metrics_get(m: str, s: float = 0, e: float = 1e18):
+    def metrics_get(request: Request, m: str, s: float = 0, e: float = 1e18,
+                    x_dxa_roles: Optional[str] = Header(None), authorization: Optional[str] = Header(None)):
+        authorize("metrics/get", x_dxa_roles, authorization, _client(request))
         rows = st.metrics.zrangebyscore(m, s, e)
         return [json.loads(v) for _, v in rows]
 
     @app.post("/api/data/upload")
-    def data_upload(items: List[Dict[str, Any]] = Body(...)):
+    def data_upload(request: Request, items: List[Dict[str, Any]] = Body(...),
+                    x_dxa_roles: Optional[str] = Header(None), authorization: Optional[str] = Header(None)):
+        authorize("metrics/ingest", x_dxa_roles, authorization, _client(request))
         from .metrics_ingestor import ingest_items
         ingest_items(st.metrics, items, st.local_cache)
         return "done"
 
     @app.post("/api/metrics/ingest")
-    def metrics_ingest(request_body: str = Body(..., media_type="text/plain")):
+    def metrics_ingest(request: Request, request_body: str = Body(..., media_type="text/plain"),
+                       x_dxa_roles: Optional[str] = Header(None), authorization: Optional[str] = Header(None)):
+        authorize("metrics/ingest", x_dxa_roles, authorization, _client(request))
         from .metrics_ingestor import ingest_lines
         return ok(ingest_lines(st.metrics, request_body.splitlines()))
 
@@ -429,7 +438,7 @@ def create_app(root: str = ".dxa", device: str = "cpu", metrics_endpoint: Option
 
     # node-side Livy-compatible batch API (remote job submission: job_clients.LivyClient)
     from .job_clients import batch_routes
-    batch_routes(app, st.jobs)
+    batch_routes(app, st.jobs, authn)
 
     @app.get("/api/health")
     def health():

@@ -14,12 +14,14 @@ from __future__ import annotations
 
 import base64
 import json
+import os
 import re
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
 import requests
+from fastapi import Header, Request
 
 from .jobs import ERROR, IDLE, RUNNING, STARTING, SUCCESS
 
@@ -286,31 +288,63 @@ class BatchRegistry:
         return {"msg": "deleted"}
 
 
-def batch_routes(app, jobs):
-    """Mount ``/batches`` (Livy batch protocol) on a FastAPI app, backed by ``jobs``."""
+def batch_routes(app, jobs, authn=None, env: Optional[Dict[str, str]] = None):
+    """Mount ``/batches`` (Livy batch protocol) on a FastAPI app, backed by ``jobs``.
+
+    Submission and deletion start and stop engine processes with caller-chosen ``conf`` and ``env.*`` variables,
+    so they need the Writer role and listing needs Reader — through ``authn`` (``dxa.service.auth``: bearer JWT,
+    gateway roles header, or loopback-only onebox), or HTTP Basic credentials matching ``DXA_BATCHES_BASIC``
+    (``user:password``; what ``LivyClient`` sends, from the job's ``livy://`` connection string)."""
+    import hmac
     from fastapi import Body, HTTPException
     reg = BatchRegistry(jobs)
     app.state.batches = reg
+    basic = (env if env is not None else os.environ).get("DXA_BATCHES_BASIC")
+
+    def check(request: Request, need_writer: bool, authorization: Optional[str], roles: Optional[str]):
+        if basic and authorization and authorization.lower().startswith("basic "):
+            try:
+                given = base64.b64decode(authorization[6:].strip()).decode("utf-8")
+            except (ValueError, UnicodeDecodeError):
+                given = ""
+            if hmac.compare_digest(given.encode(), basic.encode()):
+                return
+            raise HTTPException(status_code=401, detail="invalid credentials")
+        if authn is None:
+            return
+        from .auth import AuthError
+        try:
+            authn.check(need_writer, authorization, roles, request.client.host if request.client else None)
+        except AuthError as e:
+            raise HTTPException(status_code=e.status, detail=str(e))
 
     @app.post("/batches")
-    def batches_submit(body: Dict[str, Any] = Body(...)):
+    def batches_submit(request: Request, body: Dict[str, Any] = Body(...),
+                       authorization: Optional[str] = Header(None), x_dxa_roles: Optional[str] = Header(None)):
+        check(request, True, authorization, x_dxa_roles)
         try:
             return reg.submit(body)
         except (ValueError, KeyError) as e:
             raise HTTPException(status_code=400, detail=str(e))
 
     @app.get("/batches")
-    def batches_list():
+    def batches_list(request: Request, authorization: Optional[str] = Header(None),
+                     x_dxa_roles: Optional[str] = Header(None)):
+        check(request, False, authorization, x_dxa_roles)
         return reg.list()
 
     @app.get("/batches/{bid}")
-    def batches_get(bid: int):
+    def batches_get(bid: int, request: Request, authorization: Optional[str] = Header(None),
+                    x_dxa_roles: Optional[str] = Header(None)):
+        check(request, False, authorization, x_dxa_roles)
         if bid not in reg.names:
             raise HTTPException(status_code=404, detail=f"batch {bid} not found")
         return reg.get(bid)
 
     @app.delete("/batches/{bid}")
-    def batches_delete(bid: int):
+    def batches_delete(bid: int, request: Request, authorization: Optional[str] = Header(None),
+                       x_dxa_roles: Optional[str] = Header(None)):
+        check(request, True, authorization, x_dxa_roles)
         if bid not in reg.names:
             raise HTTPException(status_code=404, detail=f"batch {bid} not found")
         return reg.delete(bid)

@@ -134,7 +134,9 @@ def mount_website(app: FastAPI, st, authn, onebox: Optional[bool] = None):
         return enabled_functions(comp, ident["isWriter"], bool(onebox))
 
     @app.get("/api/metrics/{name}/freshness")
-    def freshness(name: str):
-        """metricService.js:93 — the newest point of a metric (the dashboard's data-freshness box)."""
+    def freshness(name: str, request: Request, authorization: Optional[str] = Header(None),
+                  x_dxa_roles: Optional[str] = Header(None)):
+        """metricService.js:93 — the newest point of a metric (the dashboard's data-freshness box).  Reader role."""
+        _identity(request, authorization, x_dxa_roles)
         rows = st.metrics.zrangebyscore(name, float("-inf"), float("inf"))
         return [json.loads(v) for _, v in rows[-1:]]

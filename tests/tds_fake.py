@@ -73,6 +73,7 @@ class FakeSqlServer:
         self.tables = {}
         self.statements = []
         self.logins = []
+        self.protocol_errors = []
         self.sock = socket.create_server(("127.0.0.1", 0))
         self.port = self.sock.getsockname()[1]
         self._stop = False
@@ -116,6 +117,11 @@ class FakeSqlServer:
             bulk_target = None
             while True:
                 t, msg = ch.read_message()
+                if t != T.PT_BULK and bulk_target is not None:
+                    # after INSERT BULK the server expects the BulkLoadBCP message and nothing else: a real SQL
+                    # Server fails the request and drops the connection
+                    self.protocol_errors.append(f"packet type {t} after INSERT BULK")
+                    return
                 if t == T.PT_SQLBATCH:
                     hdr = struct.unpack("<I", msg[:4])[0]
                     sql = msg[hdr:].decode("utf-16-le")

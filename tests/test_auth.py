@@ -126,3 +126,44 @@ def test_unknown_kid_does_not_refetch_per_request(rsa_key):
         with pytest.raises(A.AuthError):
             ks.get("forged-kid")
     assert len(calls) == 1
+
+
+def test_metrics_upload_and_batches_routes_need_roles(tmp_path, monkeypatch):
+    """Every route of the app is authenticated: the metrics reads (Reader), metric ingestion and the Livy-style
+    ``/batches`` job submission (Writer) answer 401 without a token; ``/batches`` also takes the Basic credentials
+    of ``DXA_BATCHES_BASIC`` (what a fleet's LivyClient sends)."""
+    import base64
+    from dxa.service.app import create_app
+    monkeypatch.setenv("DXA_AUTH", "jwt")
+    monkeypatch.setenv("DXA_AUTH_HS256_SECRET", "k3y")
+    monkeypatch.setenv("DXA_SUPERVISE", "0")
+    monkeypatch.setenv("DXA_BATCHES_BASIC", "fleet:pw")
+    client = TestClient(create_app(str(tmp_path / "svc")))
+
+    def tok(roles):
+        return {"Authorization": "Bearer " + A.make_token(_claims(roles, aud=None, iss=None), "HS256",
+                                                           secret=b"k3y")}
+    reader, writer = tok(["DataXReader"]), tok(["DataXWriter"])
+    item = [{"app": "DATAX-x", "met": "m1", "val": 3}]
+    # no token: 401 everywhere
+    assert client.get("/api/metrics/get", params={"m": "DATAX-x:m1"}).status_code == 401
+    assert client.get("/api/metrics/DATAX-x:m1/freshness").status_code == 401
+    assert client.post("/api/data/upload", json=item).status_code == 401
+    assert client.post("/api/metrics/ingest", content='{"app":"p","met":"m","val":2}',
+                       headers={"Content-Type": "text/plain"}).status_code == 401
+    assert client.post("/batches", json={"file": "x", "args": []}).status_code == 401
+    assert client.get("/batches").status_code == 401
+    assert client.get("/batches/1").status_code == 401
+    assert client.delete("/batches/1").status_code == 401
+    # readers read, writers write
+    assert client.post("/api/data/upload", json=item, headers=reader).status_code == 403
+    assert client.post("/api/data/upload", json=item, headers=writer).json() == "done"
+    assert client.get("/api/metrics/get", params={"m": "DATAX-x:m1"}, headers=reader).json()[0]["val"] == 3
+    assert client.get("/api/metrics/DATAX-x:m1/freshness", headers=reader).status_code == 200
+    assert client.post("/batches", json={"file": "x"}, headers=reader).status_code == 403
+    assert client.get("/batches", headers=reader).json()["total"] == 0
+    # Livy Basic credentials
+    basic = {"Authorization": "Basic " + base64.b64encode(b"fleet:pw").decode()}
+    bad = {"Authorization": "Basic " + base64.b64encode(b"fleet:nope").decode()}
+    assert client.get("/batches", headers=basic).status_code == 200
+    assert client.get("/batches", headers=bad).status_code == 401

@@ -259,3 +259,20 @@ def test_java_dollar_terminators_gpu(gpu):
         got = _run(sql, [value], gpu)
         assert got == _run(sql, [value], "cpu"), (pattern, value)
         assert bool(got[0][0]) == want, (pattern, value, got)
+
+
+@pytest.mark.parametrize("pattern,value,want", [
+    ("(?m)^b$", "a\nb\nc", True), ("^b$", "a\nb\nc", False),           # MULTILINE: every line end / start
+    ("(?m)a$", "a\r\nb", True), ("(?m)a\r$", "a\r\nb", False),          # never between \r and \n
+    ("(?m)^c", "a c", True), ("(?m)^$", "a\n", False),             # ^ not after a final terminator
+    ("(?s)a.b", "a\nb", True), ("a.b", "a\nb", False),                   # DOTALL
+    ("(?d)a.b", "a\rb", True), ("a.b", "a\rb", False),                   # UNIX_LINES: \n only
+    ("(?d)a$", "a\r", False), ("a$", "a\r", True),
+    ("(?m:^b)|zz", "a\nb", True), ("(?m:x)|^b", "a\nb", False),          # scoped flags end with their group
+    ("(?i)ABC", "xabc", True)])
+def test_java_inline_flags_host(pattern, value, want):
+    """Java's MULTILINE / DOTALL / UNIX_LINES inline flags on the host regex path (java.util.regex.Pattern's Caret,
+    Dollar and Dot), which Python's ``re`` reads differently."""
+    import re
+    from dxa.ops.regex_dfa import java_to_python
+    assert bool(re.search(java_to_python(pattern), value, re.ASCII)) == want

@@ -119,3 +119,25 @@ def test_unparseable_connection_strings_fail_at_start():
         _cosmos_sink(SettingDictionary({"connectionstring": "mongodb://x"}), "o")
     assert _sink("local:") is not None and _sink("sqlite:////tmp/x.db") is not None
     assert _cosmos_sink(SettingDictionary({"connectionstring": "local:"}), "o") is not None
+
+
+def test_bulk_falls_back_to_insert_for_long_strings():
+    """A chunk holding a string over 4000 characters cannot travel as a bulk-load nvarchar(4000): the writer finds
+    it while encoding, before INSERT BULK is sent, and INSERTs that chunk on the idle connection (the fake, like a
+    real server, drops a connection that sends anything but the BulkLoadBCP message after INSERT BULK)."""
+    from dxa.engine.column import Table
+    from dxa.engine.types import StructField, StructType
+    srv = FakeSqlServer(encryption="none")
+    try:
+        s = _sink(f"jdbc:sqlserver://127.0.0.1:{srv.port};database=iot;user=sa;password=p@ss;",
+                  usebulkinsert="true", bulkcopybatchsize="2")
+        schema = StructType((StructField("deviceId", "long"), StructField("name", "string")))
+        rows = [{"deviceId": i, "name": ("x" * 5000) if i == 2 else f"d{i}"} for i in range(5)]
+        assert s.write(None, Table.from_pylist(rows, schema), None, None) == 5
+        assert not srv.protocol_errors
+        got = sorted(srv.tables["dbo.Devices"]["rows"])
+        assert [r[0] for r in got] == [0, 1, 2, 3, 4] and len(got[2][1]) == 5000
+        assert sum(q.startswith("INSERT BULK") for q in srv.statements) == 2           # chunks {0,1} and {4}
+        assert sum(q.startswith("INSERT INTO") for q in srv.statements) == 1           # chunk {2,3}
+    finally:
+        srv.close()
