@@ -81,6 +81,11 @@ class _Prepended(LazyColumns):
         return self._rest[i - self._k]
 
 
+class HiddenQual(str):
+    """The qualifier of a column reachable only qualified: the per-side key copies of a USING / NATURAL join, whose
+    unqualified name resolves to the join's merged key column (and ``SELECT *`` lists that one only)."""
+
+
 class Scope:
     """Columns visible to an expression: (qualifier, name, column) triples over ``length`` rows."""
 
@@ -110,6 +115,9 @@ class Scope:
         low = name.lower()
         out = [i for i, n in enumerate(self.names) if n.lower() == low and
                (qual is None or (self.quals[i] or "").lower() == qual.lower())]
+        if qual is None:
+            vis = [i for i in out if not isinstance(self.quals[i], HiddenQual)]
+            out = vis or out
         exact = [i for i in out if self.names[i] == name]
         return exact or out
 

@@ -21,8 +21,8 @@ from ..sql import ast as A
 from ..sql.parser import parse_query
 from .column import (ArrayColumn, Column, ConstColumn, LazyColumns, PrimColumn, StrColumn, StructColumn, Table,
                      concat_columns, concat_tables, materialize)
-from .expr import (AGG_FUNCS, DeferredColumns, EvalContext, EvalError, Scope, TakenColumns, cast_column, evaluate,
-                   output_name, predicate_mask)
+from .expr import (AGG_FUNCS, DeferredColumns, EvalContext, EvalError, HiddenQual, Scope, TakenColumns, cast_column,
+                   evaluate, output_name, predicate_mask)
 from . import windowfn as W
 from .types import common_type, is_nested
 
@@ -100,7 +100,10 @@ def execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
 
 
 def _execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
-    out, src_scope = _exec_body(q.body, catalog, ctx, want_scope=bool(q.order_by))
+    out, src_scope = _exec_body(q.body, catalog, ctx, want_scope=bool(q.order_by or q.sort_by))
+    if q.distribute_by or q.sort_by:
+        out = _distribute_sort(q, out, src_scope, ctx)
+        src_scope = None
     if (q.order_by or q.limit is not None) and P.active() and P.dist_of(out) != P.REPLICATED:
         # a total order / global LIMIT needs every row: gather (outputs of this shape are small in DataX flows)
         out = _gathered(out)
@@ -115,6 +118,38 @@ def _execute(q: A.Query, catalog: Catalog, ctx: EvalContext) -> Table:
         out = _order_by(out, q.order_by, ctx, src_scope, aliases)
     if q.limit is not None:
         out = out.slice(0, q.limit)
+    return out
+
+
+def _distribute_sort(q: A.Query, out: Table, src_scope, ctx) -> Table:
+    """``DISTRIBUTE BY`` / ``SORT BY`` / ``CLUSTER BY`` (Spark's RepartitionByExpression + a per-partition sort):
+    at N ranks the rows move to the owner of their key hash (one all-to-all) and each rank sorts its own share; on
+    one rank the only partition is the whole result, so SORT BY orders it all and DISTRIBUTE BY moves nothing."""
+    aliases = {}
+    if isinstance(q.body, A.Select):
+        for it in q.body.items:
+            if not isinstance(it.expr, A.Star):
+                aliases.setdefault(it.expr.key(), it.alias or output_name(it.expr))
+    if q.distribute_by and P.active() and P.dist_of(out) != P.REPLICATED and out.length >= 0:
+        sc = Scope.of_table(out)
+        keys = []
+        for e in q.distribute_by:
+            try:
+                keys.append(materialize(evaluate(e, sc, ctx)))
+            except EvalError:
+                named = aliases.get(e.key())
+                if named is None or out.column(named) is None:
+                    raise
+                keys.append(materialize(out.column(named)))
+        keys = [k if not isinstance(k, (StructColumn, ArrayColumn)) else _nested_key(k) for k in keys]
+        dest = P.owner_of(hash_columns(keys)) if out.length else torch.empty(0, dtype=torch.int64, device=out.device)
+        out = P.shuffle_table(out, dest)
+        out.dist = P.HASHED
+        src_scope = None
+    if q.sort_by:
+        dist = P.dist_of(out)
+        out = _order_by(out, q.sort_by, ctx, src_scope, aliases)
+        out.dist = dist
     return out
 
 
@@ -227,14 +262,20 @@ def _relation(src, catalog: Catalog, ctx: EvalContext) -> Scope:
         t = catalog.get(name)
         if t is None:
             raise QueryError(f"table or view not found: {name}")
+        if src.sample:
+            t = _sample(t, src.sample)
         sc = Scope.of_table(t, src.alias or src.name.split(".")[-1])
         sc.dist = P.dist_of(t)
         return sc
     if isinstance(src, A.SubqueryRef):
         t = execute(src.query, catalog, ctx)
+        if src.sample:
+            t = _sample(t, src.sample)
         sc = Scope.of_table(t, src.alias)
         sc.dist = P.dist_of(t)
         return sc
+    if isinstance(src, A.Pivot):
+        return _pivot(src, catalog, ctx)
     if isinstance(src, A.Join):
         return _join(src, catalog, ctx)
     if isinstance(src, A.LateralView):
@@ -253,6 +294,122 @@ def _relation(src, catalog: Catalog, ctx: EvalContext) -> Scope:
         out.dist = getattr(base, "dist", P.REPLICATED)
         return out
     raise QueryError(f"unsupported FROM item {type(src).__name__}")
+
+
+_SAMPLE_SEED = 0x5DEECE66D
+
+
+def _sample(t: Table, spec) -> Table:
+    """``TABLESAMPLE``: ``("rows", n)`` keeps the first n rows (Spark plans it as a LIMIT — global, so a partitioned
+    input is gathered first); ``("fraction", f)`` keeps each row with probability f, decided by a hash of the row's
+    position and a fixed seed, so the same input gives the same sample on every run (Spark's Bernoulli sampler
+    draws a fresh seed per query; here repeatability wins — rank r hashes its own positions salted with r)."""
+    kind, v = spec
+    dist = P.dist_of(t)
+    if kind == "rows":
+        if P.active() and dist != P.REPLICATED:
+            t = _gathered(t)
+            dist = P.REPLICATED
+        out = t.slice(0, min(int(v), t.length))
+        out.dist = dist
+        return out
+    if v >= 1.0 or t.length == 0:
+        return t
+    pos = torch.arange(t.length, dtype=torch.int64, device=t.device)
+    salt = (_SAMPLE_SEED + 0x9E3779B97F4A7C15 * (P.rank() + 1)) & 0x7FFFFFFFFFFFFFFF
+    h = pos * -7046029254386353131 + salt
+    h = h ^ ((h >> 31) & 0x1FFFFFFFF)
+    h = h * -4658895280553007687
+    h = h ^ ((h >> 29) & 0x7FFFFFFFF)
+    u = (h & ((1 << 53) - 1)).to(torch.float64) / float(1 << 53)
+    out = t.take(torch.nonzero(u < v).flatten())
+    out.dist = dist
+    return out
+
+
+def _pivot(pv: A.Pivot, catalog, ctx) -> Scope:
+    """``PIVOT (agg [AS a], … FOR cols IN (values))`` as Spark 2.4's ResolvePivot: GROUP BY every source column
+    that neither an aggregate nor a pivot column reads; per (value, aggregate) one column holding the aggregate
+    over the rows whose pivot columns equal the value (``agg(IF(cols = value, arg, NULL))`` — COUNT(*) counts the
+    matching rows); columns are named by the value (its alias, else its string form) when there is one aggregate,
+    else ``<value>_<aggregate alias or SQL text>``."""
+    base = _relation(pv.source, catalog, ctx)
+    simple = isinstance(pv.source, (A.TableRef, A.SubqueryRef))
+    qual = (pv.source.alias or (pv.source.name.split(".")[-1] if isinstance(pv.source, A.TableRef) else None)) \
+        if simple else None
+
+    def unq(e):
+        # a join's columns are flattened below: references keep their column name only
+        return A.replace(e, lambda n: A.Ident((n.parts[-1],)) if isinstance(n, A.Ident) and not simple else None)
+    aggs = [(unq(a), al) for a, al in pv.aggs]
+    cols = [unq(c) for c in pv.columns]
+    used = set()
+    for e in [a for a, _ in aggs] + cols:
+        for node in A.walk(e):
+            if isinstance(node, A.Ident):
+                used.add(node.parts[-1].lower() if (len(node.parts) > 1 and qual and
+                                                    node.parts[0].lower() == qual.lower()) else node.parts[0].lower())
+    for a, _ in aggs:
+        if not _contains_agg(a, ctx):
+            raise QueryError(f"PIVOT expects aggregate expressions, got {output_name(a)}")
+    visible = [i for i, q in enumerate(base.quals) if not isinstance(q, HiddenQual)]
+    group = [base.names[i] for i in visible if base.names[i].lower() not in used]
+    tmp = f"__dxa_pivot_{id(pv)}"
+    t = Table([base.names[i] for i in visible], [base.cols[i] for i in visible], base.length, base.device)
+    t.dist = getattr(base, "dist", P.REPLICATED)
+    cat = catalog.child()
+    cat.register(tmp, t)
+
+    def value_name(vs, alias):
+        if alias:
+            return alias
+        strs = []
+        for v in vs:
+            if not isinstance(v, A.Literal):
+                raise QueryError("PIVOT values must be literals")
+            strs.append("null" if v.value is None else
+                        ("true" if v.value is True else "false" if v.value is False else str(v.value)))
+        return strs[0] if len(strs) == 1 else "[" + ",".join(strs) + "]"
+
+    def cond(vs):
+        c = None
+        for col, v in zip(cols, vs):
+            term = A.IsNull(col) if isinstance(v, A.Literal) and v.value is None else A.BinOp("=", col, v)
+            c = term if c is None else A.BinOp("and", c, term)
+        return c
+
+    def masked(agg, cnd):
+        def sub(node):
+            if isinstance(node, A.Call) and (node.name in AGG_FUNCS or node.name in ctx.udafs):
+                if node.star:
+                    return A.Call(node.name, [A.Call("if", [cnd, A.Literal(1, "int"), A.Literal(None, "null")])],
+                                  node.distinct)
+                return A.Call(node.name, [A.Call("if", [cnd, x, A.Literal(None, "null")]) for x in node.args[:1]]
+                              + list(node.args[1:]), node.distinct)
+            return None
+        return A.replace(agg, sub)
+    def guarded(agg, cnd):
+        # Spark 2.4 pivots numeric / boolean aggregates in two phases (GROUP BY groups + pivot column, then
+        # PivotFirst): a group without rows for a value gets NULL there — also for COUNT, which the one-phase
+        # rewrite alone would give as 0.  Collections keep the one-phase result (an empty array).
+        m = masked(agg, cnd)
+        if any(isinstance(n, A.Call) and n.name in ("collect_list", "collect_set") for n in A.walk(agg)):
+            return m
+        hits = A.Call("count", [A.Call("if", [cnd, A.Literal(1, "int"), A.Literal(None, "null")])])
+        return A.Call("if", [A.BinOp(">", hits, A.Literal(0, "int")), m, A.Literal(None, "null")])
+    items = [A.SelectItem(A.Ident((g,)), g) for g in group]
+    single = len(aggs) == 1
+    for vs, valias in pv.values:
+        vname = value_name(vs, valias)
+        c = cond(vs)
+        for a, aalias in aggs:
+            name = vname if single else f"{vname}_{aalias or output_name(a)}"
+            items.append(A.SelectItem(guarded(a, c), name))
+    sel = A.Select(items=items, from_=A.TableRef(tmp, qual), group_by=[A.Ident((g,)) for g in group])
+    out, _ = _exec_select(sel, cat, ctx)
+    sc = Scope.of_table(out, pv.alias)
+    sc.dist = P.dist_of(out)
+    return sc
 
 
 class _Appended(LazyColumns):
@@ -290,16 +447,117 @@ def _static_table(src, catalog):
     return None
 
 
+def _rel_names(rel) -> set:
+    """Names a hint can use for a relation: its alias, or its table name."""
+    if isinstance(rel, A.TableRef):
+        return {(rel.alias or rel.name.split(".")[-1]).lower(), rel.name.lower()}
+    if isinstance(rel, (A.SubqueryRef, A.Pivot)) and rel.alias:
+        return {rel.alias.lower()}
+    return set()
+
+
 def _join(j: A.Join, catalog, ctx) -> Scope:
+    out = _join_rows(j, catalog, ctx)
+    using = getattr(out, "_using", None)
+    if not using:
+        return out
+    return _merge_using(out, using, j.kind, ctx)
+
+
+def _merge_using(out: Scope, using, kind: str, ctx) -> Scope:
+    """A USING / NATURAL join's output: the key columns once, first (left's value; right's for RIGHT JOIN;
+    ``coalesce(left, right)`` for FULL), then the remaining left and right columns (Spark's
+    ``Join(..., UsingJoin)`` projection).  The per-side copies stay reachable qualified (``a.k``)."""
+    keys = using
+    names, cols, quals = [], [], []
+    for nm, li, ri in keys:
+        lc, rc = out.cols[li], out.cols[ri]
+        if kind == "right":
+            c = rc
+        elif kind == "full":
+            tmp = Scope(["__l", "__r"], [lc, rc], [None, None], out.length, out.device)
+            c = evaluate(A.Call("coalesce", [A.Ident(("__l",)), A.Ident(("__r",))]), tmp, ctx)
+        else:
+            c = lc
+        names.append(nm)
+        cols.append(c)
+        quals.append(None)
+    key_idx = {i for _n, li, ri in keys for i in (li, ri)}
+    merged = Scope(names + list(out.names), _Prefixed(cols, out.cols),
+                   quals + [HiddenQual(q or "") if i in key_idx else q for i, q in enumerate(out.quals)],
+                   out.length, out.device)
+    merged.dist = getattr(out, "dist", P.REPLICATED)
+    return merged
+
+
+class _Prefixed(LazyColumns):
+    """``head + tail`` where ``tail`` (a join's lazily gathered columns) stays unresolved until read."""
+
+    def __init__(self, head, tail):
+        super().__init__(list(head) + [None] * len(tail))
+        self._n = len(head)
+        self._tail = tail
+
+    def _make(self, i):
+        return self._tail[i - self._n]
+
+
+class _ColRef(A.Expr):
+    """A join key given by column position in its side's scope (USING / NATURAL keys)."""
+
+    def __init__(self, idx: int):
+        self.idx = idx
+
+    def key(self):
+        return ("colref", self.idx)
+
+    def children(self):
+        return []
+
+
+def _visible_index(scope: Scope, name: str) -> Optional[int]:
+    low = name.lower()
+    hits = [i for i, (n, q) in enumerate(zip(scope.names, scope.quals))
+            if n.lower() == low and not isinstance(q, HiddenQual)]
+    if len(hits) > 1:
+        raise QueryError(f"USING column '{name}' is ambiguous on one side of the join")
+    return hits[0] if hits else None
+
+
+def _key_col(e, scope: Scope, ctx) -> Column:
+    if isinstance(e, _ColRef):
+        return materialize(scope.cols[e.idx])
+    return materialize(evaluate(e, scope, ctx))
+
+
+def _join_rows(j: A.Join, catalog, ctx) -> Scope:
     left = _relation(j.left, catalog, ctx)
     right = _relation(j.right, catalog, ctx)
     n_l, n_r = left.length, right.length
     dev = left.device
     lkeys, rkeys, residual = [], [], []
-    if j.using:
-        for nm in j.using:
-            lkeys.append(A.Ident((nm,)))
-            rkeys.append(A.Ident((nm,)))
+    using = list(j.using or [])
+    if j.natural:
+        lvis = [n for n, q in zip(left.names, left.quals) if not isinstance(q, HiddenQual)]
+        rvis = {n.lower() for n, q in zip(right.names, right.quals) if not isinstance(q, HiddenQual)}
+        seen = set()
+        for n in lvis:
+            if n.lower() in rvis and n.lower() not in seen:
+                seen.add(n.lower())
+                using.append(n)
+        if not using:
+            j = A.Join(j.left, j.right, "cross" if j.kind == "inner" else j.kind, None, None,
+                       broadcast=j.broadcast)
+    using_idx = []
+    for nm in using:
+        li = _visible_index(left, nm)
+        ri = _visible_index(right, nm)
+        if li is None or ri is None:
+            raise QueryError(f"USING column '{nm}' cannot be resolved on the "
+                             f"{'left' if li is None else 'right'} side of the join")
+        using_idx.append((left.names[li], li, len(left.names) + ri))
+        lkeys.append(_ColRef(li))
+        rkeys.append(_ColRef(ri))
     for c in _split_and(j.on):
         if isinstance(c, A.BinOp) and c.op == "=":
             if _refs_resolvable(c.left, left) and _refs_resolvable(c.right, right) and not \
@@ -316,11 +574,21 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
     kind = j.kind
     ldist, rdist = getattr(left, "dist", P.REPLICATED), getattr(right, "dist", P.REPLICATED)
     out_dist = P.REPLICATED
+    bc = j.broadcast or set()
+    if P.active() and ldist != P.REPLICATED and rdist != P.REPLICATED and bc:
+        # /*+ BROADCAST(x) */: replicate the named side (all-gather) instead of co-partitioning both by key hash —
+        # the build side then need not be shuffled every batch (Spark's broadcast hash join)
+        if (_rel_names(j.right) & bc) and kind in ("inner", "left", "semi", "anti", "cross"):
+            right = _gather_scope(right)
+            rdist = P.REPLICATED
+        elif (_rel_names(j.left) & bc) and kind in ("inner", "right", "cross"):
+            left = _gather_scope(left)
+            ldist = P.REPLICATED
     if P.active() and (ldist != P.REPLICATED or rdist != P.REPLICATED):
         if ldist != P.REPLICATED and rdist != P.REPLICATED and lkeys:
             # co-partition both sides by the join-key hash (Spark's shuffle hash join)
-            left = _shuffle_scope(left, [materialize(evaluate(e, left, ctx)) for e in lkeys])
-            right = _shuffle_scope(right, [materialize(evaluate(e, right, ctx)) for e in rkeys], ref=left)
+            left = _shuffle_scope(left, [_key_col(e, left, ctx) for e in lkeys])
+            right = _shuffle_scope(right, [_key_col(e, right, ctx) for e in rkeys], ref=left)
             out_dist = P.HASHED
         elif ldist != P.REPLICATED and kind in ("inner", "left", "semi", "anti", "cross"):
             out_dist = ldist            # partitioned ⨝ replicated: rank-local
@@ -351,7 +619,7 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
             li = torch.arange(n_l, device=dev).repeat_interleave(n_r)
             ri = torch.arange(n_r, device=dev).repeat(n_l)
     else:
-        lk = [materialize(evaluate(e, left, ctx)) for e in lkeys]
+        lk = [_key_col(e, left, ctx) for e in lkeys]
         built = None
         static = _static_table(j.right, catalog)
         if static is not None and kind in ("inner", "left", "semi", "anti") and rdist == P.REPLICATED:
@@ -360,14 +628,14 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
             ck = (static[0], id(static[1]), tuple(e.key() for e in rkeys), tuple(c.dtype for c in lk))
 
             def build():
-                rk0 = [materialize(evaluate(e, right, ctx)) for e in rkeys]
+                rk0 = [_key_col(e, right, ctx) for e in rkeys]
                 types = [_join_key_type(a.dtype, b.dtype) for a, b in zip(lk, rk0)]
                 rk1 = [b if b.dtype == t else cast_column(b, t) for b, t in zip(rk0, types)]
                 return static[1], types, rk1, J.build_side(rk1)
             _t, types, rk, built = catalog.cached_build(ck, build)
             lk = [a if a.dtype == t else cast_column(a, t) for a, t in zip(lk, types)]
         else:
-            rk = [materialize(evaluate(e, right, ctx)) for e in rkeys]
+            rk = [_key_col(e, right, ctx) for e in rkeys]
             lk, rk = _coerce_keys(lk, rk)
         if residual and kind != "inner":
             # non-equi ON terms of an outer / semi / anti join decide which pairs *match*: filter the equi pairs
@@ -396,6 +664,7 @@ def _join(j: A.Join, catalog, ctx) -> Scope:
         idx = torch.nonzero(pred).flatten()
         out = Scope(out.names, TakenColumns(out.cols, idx), out.quals, int(idx.shape[0]), dev)
     out.dist = out_dist
+    out._using = using_idx            # USING / NATURAL keys: (name, left index, right index in the joined scope)
     return out
 
 
@@ -530,6 +799,8 @@ def _expand_items(sel: A.Select, scope: Scope) -> List[Tuple[A.Expr, str]]:
         if isinstance(e, A.Star):
             if not e.qualifier:
                 for nm, q in zip(scope.names, scope.quals):
+                    if isinstance(q, HiddenQual):
+                        continue              # a USING join's per-side key copy: the merged key is listed instead
                     items.append((A.Ident(((q,) if q and _dup(scope, nm) else ()) + (nm,)), nm))
                 continue
             q = e.qualifier
@@ -550,7 +821,7 @@ def _expand_items(sel: A.Select, scope: Scope) -> List[Tuple[A.Expr, str]]:
 
 def _dup(scope: Scope, nm: str) -> bool:
     low = nm.lower()
-    return sum(1 for n in scope.names if n.lower() == low) > 1
+    return sum(1 for n, q in zip(scope.names, scope.quals) if n.lower() == low and not isinstance(q, HiddenQual)) > 1
 
 
 NONDETERMINISTIC = {"rand", "random", "randn", "uuid", "now", "current_timestamp", "current_date",

@@ -228,12 +228,14 @@ class TableRef:
     name: str
     alias: Optional[str] = None
     timewindow: Optional[str] = None   # DataX extension: FROM t TIMEWINDOW('5 minutes')
+    sample: Optional[tuple] = None     # TABLESAMPLE: ("fraction", f) | ("rows", n)
 
 
 @dataclass(eq=False)
 class SubqueryRef:
     query: "Query"
     alias: Optional[str] = None
+    sample: Optional[tuple] = None
 
 
 @dataclass(eq=False)
@@ -243,6 +245,19 @@ class Join:
     kind: str          # 'inner' | 'left' | 'right' | 'full' | 'cross' | 'semi' | 'anti'
     on: Optional[Expr] = None
     using: Optional[List[str]] = None
+    natural: bool = False              # NATURAL JOIN: USING every column name both sides share
+    broadcast: Optional[set] = None    # relation names/aliases a BROADCAST hint names (lower case)
+
+
+@dataclass(eq=False)
+class Pivot:
+    """``FROM src PIVOT (aggs FOR cols IN (values))``: group by every column of ``src`` that no aggregate and no
+    pivot column reads, one output column per (value, aggregate)."""
+    source: Any
+    aggs: List[Tuple[Expr, Optional[str]]]
+    columns: List[Expr]
+    values: List[Tuple[List[Expr], Optional[str]]]
+    alias: Optional[str] = None
 
 
 @dataclass(eq=False)
@@ -261,6 +276,7 @@ class Select:
     having: Optional[Expr] = None
     distinct: bool = False
     grouping_sets: Optional[List[List[Expr]]] = None     # ROLLUP / CUBE / GROUPING SETS (subsets of group_by)
+    hints: List[Tuple[str, List[str]]] = field(default_factory=list)    # /*+ NAME(args) */
 
 
 @dataclass(eq=False)
@@ -277,6 +293,8 @@ class Query:
     order_by: List[OrderItem] = field(default_factory=list)
     limit: Optional[int] = None
     ctes: List[Tuple[str, "Query"]] = field(default_factory=list)     # WITH name AS (query), …
+    distribute_by: List[Expr] = field(default_factory=list)           # DISTRIBUTE BY / CLUSTER BY keys
+    sort_by: List["OrderItem"] = field(default_factory=list)          # SORT BY (within each rank's partition)
 
 
 @dataclass(eq=False)

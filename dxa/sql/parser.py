@@ -28,13 +28,14 @@ KEYWORDS = {
 }
 
 _TOKEN_RE = re.compile(r"""
-    (?P<ws>\s+|--[^\n]*) |
+    (?P<hint>/\*\+.*?\*/) |
+    (?P<ws>\s+|--[^\n]*|/\*.*?\*/) |
     (?P<num>(?:\d+\.\d*|\.\d+|\d+)(?:[eE][+-]?\d+)?[LlDdSsYy]?(?:BD)?) |
     (?P<str>'(?:[^'\\]|\\.|'')*'|"(?:[^"\\]|\\.|"")*") |
     (?P<bq>`(?:[^`]|``)*`) |
     (?P<id>[A-Za-z_][A-Za-z0-9_$]*) |
     (?P<op><=>|<>|!=|==|<=|>=|\|\||&&|[-+*/%=<>(),.;\[\]~&|^!:])
-""", re.VERBOSE)
+""", re.VERBOSE | re.DOTALL)
 
 
 class Tok:
@@ -86,6 +87,8 @@ def tokenize(sql: str) -> List[Tok]:
             toks.append(Tok("id", text[1:-1].replace("``", "`"), pos))
         elif kind == "str":
             toks.append(Tok("str", _unquote(text), pos))
+        elif kind == "hint":
+            toks.append(Tok("hint", text[3:-2], pos))
         else:
             toks.append(Tok(kind, text, pos))
         pos = m.end()
@@ -211,12 +214,51 @@ class Parser:
         if self.accept_kw("order"):
             self.expect_kw("by")
             q.order_by = self.parse_order_items()
+        if self.is_word("cluster") and self.is_kw("by", tok=self.peek()):
+            self.advance()
+            self.advance()
+            q.distribute_by = self._expr_list()
+            q.sort_by = [A.OrderItem(e) for e in q.distribute_by]
+        else:
+            if self.is_word("distribute") and self.is_kw("by", tok=self.peek()):
+                self.advance()
+                self.advance()
+                q.distribute_by = self._expr_list()
+            if self.is_word("sort") and self.is_kw("by", tok=self.peek()):
+                self.advance()
+                self.advance()
+                q.sort_by = self.parse_order_items()
+        if (q.distribute_by or q.sort_by) and q.order_by:
+            self.error("ORDER BY cannot be combined with SORT BY / DISTRIBUTE BY / CLUSTER BY")
         if self.accept_kw("limit"):
             t = self.advance()
             if t.kind != "num":
                 self.error("expected LIMIT count")
             q.limit = int(t.text)
         return q
+
+    def _expr_list(self):
+        out = [self.parse_expr()]
+        while self.accept_op(","):
+            out.append(self.parse_expr())
+        return out
+
+    def _alias_word_ok(self) -> bool:
+        """An identifier right after a relation is its alias — unless it opens a clause that Spark does not reserve
+        (NATURAL JOIN, PIVOT (…), TABLESAMPLE (…), DISTRIBUTE/SORT/CLUSTER BY, LATERAL VIEW)."""
+        t, n = self.cur, self.peek()
+        if t.kind != "id":
+            return False
+        w = t.text.lower()
+        if w == "natural" and (self.is_kw("join", "inner", "left", "right", "full", tok=n)):
+            return False
+        if w in ("pivot", "tablesample") and self.is_op("(", tok=n):
+            return False
+        if w in ("distribute", "sort", "cluster") and self.is_kw("by", tok=n):
+            return False
+        if w == "lateral" and self.is_word("view", tok=n):
+            return False
+        return True
 
     def parse_order_items(self):
         items = []
@@ -265,6 +307,9 @@ class Parser:
 
     def parse_select(self) -> A.Select:
         self.expect_kw("select")
+        hints = []
+        while self.cur.kind == "hint":
+            hints += _parse_hints(self.advance().text)
         distinct = self.accept_kw("distinct")
         if not distinct:
             self.accept_kw("all")
@@ -273,9 +318,12 @@ class Parser:
             items.append(self.parse_select_item())
             if not self.accept_op(","):
                 break
-        sel = A.Select(items=items, distinct=distinct)
+        sel = A.Select(items=items, distinct=distinct, hints=hints)
         if self.accept_kw("from"):
             sel.from_ = self.parse_from()
+            bc = {a.lower() for name, args in hints if name in _BROADCAST_HINTS for a in args}
+            if bc:
+                _mark_broadcast(sel.from_, bc)
         if self.accept_kw("where"):
             sel.where = self.parse_expr()
         if self.accept_kw("group"):
@@ -383,6 +431,10 @@ class Parser:
                 continue
             kind = None
             save = self.i
+            natural = False
+            if self.is_word("natural") and self.is_kw("join", "inner", "left", "right", "full", tok=self.peek()):
+                self.advance()
+                natural = True
             if self.accept_kw("join"):
                 kind = "inner"
             elif self.accept_kw("inner"):
@@ -403,10 +455,18 @@ class Parser:
                 self.expect_kw("join")
             if kind is None:
                 self.i = save
+                if self.is_word("pivot") and self.is_op("(", tok=self.peek()):
+                    left = self.parse_pivot(left)
+                    continue
                 return left
+            if natural and kind in ("semi", "anti", "cross"):
+                self.error(f"NATURAL {kind.upper()} JOIN is not supported")
             right = self.parse_table_primary()
             on = None
             using = None
+            if natural:
+                left = A.Join(left, right, kind, None, None, natural=True)
+                continue
             if self.accept_kw("on"):
                 on = self.parse_expr()
             elif self.accept_kw("using"):
@@ -421,12 +481,13 @@ class Parser:
         if self.accept_op("("):
             q = self.parse_query()
             self.expect_op(")")
+            sample = self.parse_sample()
             alias = None
             if self.accept_kw("as"):
                 alias = self.ident()
-            elif self.cur.kind == "id":
+            elif self._alias_word_ok():
                 alias = self.advance().text
-            return A.SubqueryRef(q, alias)
+            return A.SubqueryRef(q, alias, sample)
         name = self.ident()
         while self.accept_op("."):
             name += "." + self.ident()
@@ -438,12 +499,101 @@ class Parser:
                 self.error("TIMEWINDOW expects a string literal")
             tw = t.text
             self.expect_op(")")
+        sample = self.parse_sample()
         alias = None
         if self.accept_kw("as"):
             alias = self.ident()
-        elif self.cur.kind == "id" and not (self.is_word("lateral") and self.is_word("view", tok=self.peek())):
+        elif self._alias_word_ok():
             alias = self.advance().text
-        return A.TableRef(name, alias, tw)
+        return A.TableRef(name, alias, tw, sample)
+
+    def parse_sample(self):
+        """``TABLESAMPLE (x PERCENT | n ROWS | BUCKET x OUT OF y)`` → ("fraction", f) | ("rows", n)."""
+        if not (self.is_word("tablesample") and self.is_op("(", tok=self.peek())):
+            return None
+        self.advance()
+        self.advance()
+        if self.is_word("bucket"):
+            self.advance()
+            x = self._sample_number()
+            if not (self.accept_word("out") and self.accept_word("of")):
+                self.error("expected OUT OF")
+            y = self._sample_number()
+            if y <= 0 or x <= 0 or x > y:
+                self.error("TABLESAMPLE BUCKET x OUT OF y needs 0 < x <= y")
+            out = ("fraction", x / y)
+        else:
+            v = self._sample_number()
+            if self.accept_word("percent"):
+                if not 0 <= v <= 100:
+                    self.error("TABLESAMPLE percentage must be between 0 and 100")
+                out = ("fraction", v / 100.0)
+            elif self.accept_word("rows"):
+                if v < 0 or v != int(v):
+                    self.error("TABLESAMPLE row count must be a non-negative integer")
+                out = ("rows", int(v))
+            else:
+                self.error("expected PERCENT or ROWS")
+        self.expect_op(")")
+        return out
+
+    def _sample_number(self) -> float:
+        t = self.advance()
+        if t.kind != "num":
+            self.error("expected a number")
+        return float(t.text.rstrip("LlDdSsYy"))
+
+    def parse_pivot(self, source):
+        """``PIVOT (agg [AS a], … FOR col | (c1, c2) IN (v [AS x], (v1, v2) [AS x], …)) [alias]``
+        (Spark 2.4 pivotClause; applies to the FROM clause's relation)."""
+        self.advance()
+        self.expect_op("(")
+        aggs = []
+        while True:
+            e = self.parse_expr()
+            alias = None
+            if self.accept_kw("as"):
+                alias = self.ident()
+            elif self.cur.kind == "id" and not self.is_word("for"):
+                alias = self.advance().text
+            aggs.append((e, alias))
+            if not self.accept_op(","):
+                break
+        if not self.accept_word("for"):
+            self.error("expected FOR")
+        if self.accept_op("("):
+            cols = self._expr_list()
+            self.expect_op(")")
+        else:
+            cols = [self.parse_postfix()]
+        self.expect_kw("in")
+        self.expect_op("(")
+        values = []
+        while True:
+            if self.is_op("(") and len(cols) > 1:
+                self.advance()
+                vs = self._expr_list()
+                self.expect_op(")")
+            else:
+                vs = [self.parse_expr()]
+            if len(vs) != len(cols):
+                self.error(f"PIVOT value has {len(vs)} parts for {len(cols)} column(s)")
+            alias = None
+            if self.accept_kw("as"):
+                alias = self.ident()
+            elif self.cur.kind == "id":
+                alias = self.advance().text
+            values.append((vs, alias))
+            if not self.accept_op(","):
+                break
+        self.expect_op(")")
+        self.expect_op(")")
+        alias = None
+        if self.accept_kw("as"):
+            alias = self.ident()
+        elif self._alias_word_ok():
+            alias = self.advance().text
+        return A.Pivot(source, aggs, cols, values, alias)
 
     # -- expressions ---------------------------------------------------------------------------------------------
     def parse_expr(self) -> A.Expr:
@@ -823,6 +973,38 @@ class Parser:
         if self.accept_word("following"):
             return ("following", k)
         self.error("expected PRECEDING or FOLLOWING")
+
+
+_BROADCAST_HINTS = ("broadcast", "broadcastjoin", "mapjoin")
+_KNOWN_HINTS = _BROADCAST_HINTS + ("merge", "shuffle_merge", "mergejoin", "shuffle_hash", "shuffle_replicate_nl",
+                                   "coalesce", "repartition", "repartition_by_range")
+_HINT_RE = re.compile(r"\s*([A-Za-z_][A-Za-z0-9_]*)\s*(?:\(([^)]*)\))?\s*,?")
+
+
+def _parse_hints(text: str):
+    """``/*+ BROADCAST(a, b) COALESCE(3) */`` → [("broadcast", ["a", "b"]), ("coalesce", ["3"])].  Join-strategy
+    hints steer the distributed join (BROADCAST replicates the named relation instead of co-partitioning both
+    sides); the others are accepted and ignored, as Spark ignores hints it cannot apply; an unparsable hint body is
+    ignored with it (Spark logs a warning)."""
+    out, pos = [], 0
+    text = text.strip()
+    while pos < len(text):
+        m = _HINT_RE.match(text, pos)
+        if not m or m.end() == pos:
+            return out
+        args = [a.strip().strip("`") for a in (m.group(2) or "").split(",") if a.strip()]
+        out.append((m.group(1).lower(), args))
+        pos = m.end()
+    return out
+
+
+def _mark_broadcast(rel, names):
+    if isinstance(rel, A.Join):
+        rel.broadcast = set(names) | set(getattr(rel, "broadcast", ()) or ())
+        _mark_broadcast(rel.left, names)
+        _mark_broadcast(rel.right, names)
+    elif isinstance(rel, (A.LateralView, A.Pivot)):
+        _mark_broadcast(rel.source, names)
 
 
 def _rollup(cols):
