@@ -535,6 +535,7 @@ def main():
                                  "read_s": round(st.get("read_s", 0.0), 3), "load_s": round(st.get("total_s", 0.0), 3),
                                  "gb_per_s": round(st["bytes"] / st["total_s"] / 1e9, 2) if st.get("total_s") else None,
                                  "csv_written_s": ref_write_s,
+                                 "host_staged_on_this_rank": st.get("host_staged"),
                                  "path": "referencedata CSV: rank-0 read + broadcast, device line framing + tokenizer "
                                          "(csv.hip), schema cast on device"}
     if flow in ("window", "full") and proc.window_store is not None:

@@ -4,9 +4,10 @@ with the given delimiter and header options and no schema inference, so every co
 joins cast as needed.
 
 MI355X path (``load_csv`` on a GPU):
-* rank 0 reads the file once (local, mounted or ``wasbs://``; gzip-aware) and, with several ranks, broadcasts the
-  raw bytes over RCCL — ONE collective of the compact text, never W copies of parsed columns (SURVEY §2.G X3);
-* every rank copies the bytes to HBM, frames lines with the newline kernels and tokenizes one line per lane
+* rank 0 reads the file once (local, mounted or ``wasbs://``; gzip-aware), copies the bytes to HBM and, with
+  several ranks, broadcasts that device buffer over RCCL — ONE collective of the compact text, never W copies of
+  parsed columns, and the receivers' copies land straight in HBM (no host staging on ranks > 0; SURVEY §2.G X3);
+* every rank frames lines with the newline kernels and tokenizes one line per lane
   (``csv.hip``): each cell is a [start, len) view into the resident byte arena, so a 100 M-row table is one pass over
   its bytes and stays in HBM for the life of the job (sized for 288 GB); joins against it reuse one cached hash
   table (``Catalog.cached_build``).
@@ -76,24 +77,49 @@ def read_shared(path: str, device) -> bytes:
     return P.broadcast_bytes(data, src=0)
 
 
+def read_shared_device(path: str, device) -> Tuple[torch.Tensor, int, bool]:
+    """The file's bytes in HBM on every rank → (buffer with 64 zero bytes of padding, length, host_staged).  Rank 0
+    reads the file and copies it to the device once; other ranks receive the RCCL broadcast straight into their own
+    HBM (``host_staged`` is False there: the payload never touched their host memory)."""
+    from .. import parallel as P
+    if P.active():
+        data = fs.read_bytes(path) if P.rank() == 0 else None
+        buf, length = P.broadcast_device_bytes(data, 0, device)
+        return buf, length, P.rank() == 0
+    data = fs.read_bytes(path)
+    length = len(data)
+    host = torch.empty(length + 64, dtype=torch.uint8, pin_memory=True)
+    host[length:].zero_()
+    if length:
+        host[:length] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    buf = host.to(device, non_blocking=True)
+    buf.record_stream(torch.cuda.current_stream(device))
+    return buf, length, True
+
+
 def load_csv(path: str, delimiter: str = ",", header: bool = True, device="cpu", schema: Optional[str] = None,
              quote: str = '"', escape: str = "\\", stats: Optional[dict] = None) -> Table:
     device = torch.device(device)
     t0 = time.perf_counter()
-    data = read_shared(path, device)
-    if data.startswith(b"\xef\xbb\xbf"):                   # UTF-8 BOM (files saved by Excel / .NET)
-        data = data[3:]
-    t_read = time.perf_counter() - t0
+    staged = True
     if device.type == "cuda":
-        table = _load_device(data, delimiter, header, device, quote, escape)
+        buf, length, staged = read_shared_device(path, device)
+        t_read = time.perf_counter() - t0
+        table = _load_device(buf, length, delimiter, header, device, quote, escape)
     else:
+        data = read_shared(path, device)
+        if data.startswith(b"\xef\xbb\xbf"):               # UTF-8 BOM (files saved by Excel / .NET)
+            data = data[3:]
+        length = len(data)
+        t_read = time.perf_counter() - t0
         table = _load_host(data.decode("utf-8"), delimiter, header, device, quote, escape)
     if schema:
         table = _apply_schema(table, schema)
     if stats is not None:
         if device.type == "cuda":
             torch.cuda.synchronize(device)
-        stats.update(bytes=len(data), rows=table.length, read_s=t_read, total_s=time.perf_counter() - t0)
+        stats.update(bytes=length, rows=table.length, read_s=t_read, total_s=time.perf_counter() - t0,
+                     host_staged=staged)
     return table
 
 
@@ -115,11 +141,27 @@ def _load_host(text: str, delimiter, header, device, quote, escape) -> Table:
     return Table(names, cols, len(rows), device)
 
 
-def _load_device(data: bytes, delimiter, header, device, quote, escape) -> Table:
+def _head(buf: torch.Tensor, length: int, need_newline: bool = True) -> bytes:
+    """The first bytes of a device buffer, up to and including the first non-empty line (a small D2H read)."""
+    k = min(length, 1 << 16)
+    while True:
+        head = buf[:k].cpu().numpy().tobytes()
+        if k >= length or any(l.strip(b"\r") for l in head.split(b"\n")[:-1]):
+            return head
+        k = min(length, k * 4)
+
+
+def _load_device(buf: torch.Tensor, length: int, delimiter, header, device, quote, escape) -> Table:
+    """CSV bytes already in HBM (``buf``: ``length`` bytes + ≥ 64 zero bytes) → device string table."""
     from ..ops import native as N
     from ..ops.jsonparse import frame_lines_gpu
     if len(delimiter) != 1 or len(quote) != 1 or len(escape) != 1:
         raise ValueError("CSV delimiter, quote and escape must be single characters")
+    data = _head(buf, length)
+    if data.startswith(b"\xef\xbb\xbf"):                   # UTF-8 BOM (files saved by Excel / .NET): re-base the
+        nb = torch.zeros(length - 3 + 64, dtype=torch.uint8, device=device)   # bytes (kernels want an aligned start)
+        nb[:length - 3] = buf[3:length]
+        buf, length, data = nb, length - 3, data[3:]
     # header / column count from the first non-empty line (host: a few bytes)
     first_end = 0
     first = ""
@@ -135,12 +177,6 @@ def _load_device(data: bytes, delimiter, header, device, quote, escape) -> Table
     names = _header_names(first, delimiter, quote, escape) if header else \
         [f"_c{i}" for i in range(len(tokenize_line(first, delimiter, quote, escape)))]
     ncols = len(names)
-    length = len(data)
-    host = torch.empty(length + 64, dtype=torch.uint8, pin_memory=True)
-    host[length:].zero_()
-    if length:
-        host[:length] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
-    buf = host.to(device, non_blocking=True)
     offs = frame_lines_gpu(buf, length)                 # non-empty lines (one host read of the line count)
     if header:
         offs = offs[1:]                                 # the first non-empty line is the header

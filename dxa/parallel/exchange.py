@@ -144,79 +144,8 @@ def _a2a_counts(counts: torch.Tensor) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------------------------------------------
-# flatten / rebuild
+# table collectives (wire format: dxa.parallel.packing)
 # ---------------------------------------------------------------------------------------------------------------
-
-class _Leaf:
-    __slots__ = ("kind", "dtype", "col", "mcol", "vbit", "value", "torch_dtype")
-
-    def __init__(self, kind, dtype, col=None, value=None):
-        self.kind, self.dtype, self.col, self.value = kind, dtype, col, value
-        self.mcol = -1
-        self.vbit = -1
-        self.torch_dtype = None
-
-
-def _flatten(col, leaves: List[_Leaf], spec: list):
-    """Walk a column tree; record leaves (data-bearing) and a rebuild spec."""
-    from ..engine.column import ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn
-    if isinstance(col, ConstColumn):
-        spec.append(("const", col.value, col.dtype))
-        return
-    if isinstance(col, StructColumn):
-        has_valid = col.valid is not None
-        vleaf = None
-        if has_valid:
-            vleaf = len(leaves)
-            leaves.append(_Leaf("valid_only", "boolean", col))
-        sub = []
-        for c in col.children:
-            _flatten(c, leaves, sub)
-        spec.append(("struct", col.names, col.is_map, col.dtype, vleaf, sub))
-        return
-    if isinstance(col, ArrayColumn):
-        has_valid = col.valid is not None
-        vleaf = None
-        if has_valid:
-            vleaf = len(leaves)
-            leaves.append(_Leaf("valid_only", "boolean", col))
-        sub = []
-        for c in col.elements:
-            _flatten(c, leaves, sub)
-        spec.append(("array", col.drop_nulls, vleaf, sub))
-        return
-    if isinstance(col, StrColumn):
-        spec.append(("str", len(leaves), type(col), col.dtype))
-        leaves.append(_Leaf("str", col.dtype, col))
-        return
-    if isinstance(col, PrimColumn):
-        spec.append(("prim", len(leaves), col.dtype))
-        lf = _Leaf("prim", col.dtype, col)
-        lf.torch_dtype = col.data.dtype
-        leaves.append(lf)
-        return
-    raise TypeError(f"cannot exchange column {col!r}")
-
-
-def _rebuild(spec_item, leaves_out, n, device):
-    from ..engine.column import ArrayColumn, ConstColumn, PrimColumn, StrColumn, StructColumn
-    kind = spec_item[0]
-    if kind == "const":
-        return ConstColumn(spec_item[1], spec_item[2], n, device)
-    if kind == "prim" or kind == "str":
-        return leaves_out[spec_item[1]]
-    if kind == "struct":
-        _, names, is_map, dtype, vleaf, sub = spec_item
-        kids = [_rebuild(s, leaves_out, n, device) for s in sub]
-        valid = leaves_out[vleaf] if vleaf is not None else None
-        return StructColumn(names, kids, n, valid, is_map, dtype, device)
-    if kind == "array":
-        _, drop, vleaf, sub = spec_item
-        els = [_rebuild(s, leaves_out, n, device) for s in sub]
-        valid = leaves_out[vleaf] if vleaf is not None else None
-        return ArrayColumn(els, n, valid, drop, device)
-    raise ValueError(kind)
-
 
 def split_by_destination(dest: torch.Tensor, world: int):
     order = torch.argsort(dest, stable=True)
@@ -224,108 +153,63 @@ def split_by_destination(dest: torch.Tensor, world: int):
     return order, counts
 
 
+def _force_torch() -> bool:
+    import os
+    return os.environ.get("DXA_XCHG_TORCH") == "1"
+
+
 def shuffle_table(table, dest: torch.Tensor):
     """Send row i to rank dest[i]; returns the rows this rank receives (in source-rank order).
 
-    One host synchronisation per exchange: the row count and every string leaf's byte count per destination are
-    computed on the device as one [W, 1 + S] matrix, exchanged with one all-to-all, and read back together with
-    the send side; every later collective (the int64 row matrix, one byte stream per string leaf) has its sizes
-    from that single read-back."""
-    from ..engine.column import PrimColumn, StrColumn, Table
-    from ..ops import strings as sops
+    Device path (``exchange.hip``): plan (histogram + scan: the [W × (1+S)] send sizes) → one all-to-all of the
+    sizes and ONE host read-back of sent and received sizes → scatter (matrix + string arenas, destination-ordered)
+    → one all-to-all of the matrix and one per string leaf → one unpack launch.  Three kernel launches on the send
+    side and one on the receive side, however many columns the table has.  ``DXA_XCHG_TORCH=1`` runs the torch
+    reference implementation of the same wire format."""
+    from . import packing as PK
     W = _w()
     device = table.device
-    n = table.length
-    dest = dest.to(torch.int64)
-    order, counts = split_by_destination(dest, W)
-    t = table.take(order)
-    sorted_dest = dest[order]
-    leaves: List[_Leaf] = []
-    spec: list = []
-    for c in t.columns:
-        _flatten(c, leaves, spec)
-    # matrix columns
-    mats = []
-    nvalid = 0
-    str_leaves = []
-    for li, lf in enumerate(leaves):
-        c = lf.col
-        if lf.kind == "prim":
-            d = c.data
-            if d.dtype == torch.float64:
-                d = d.view(torch.int64)
-            elif d.dtype != torch.int64:
-                d = d.to(torch.int64)
-            lf.mcol = len(mats)
-            mats.append(d)
-        elif lf.kind == "str":
-            lf.mcol = len(mats)
-            mats.append(c.lens.to(torch.int64))
-            str_leaves.append(li)
-        if c.valid is not None:
-            lf.vbit = nvalid
-            nvalid += 1
-    nmask = (nvalid + 62) // 63
-    masks = [torch.zeros(n, dtype=torch.int64, device=device) for _ in range(nmask)]
-    for lf in leaves:
-        if lf.vbit >= 0:
-            w, b = divmod(lf.vbit, 63)
-            masks[w] |= lf.col.valid.to(torch.int64) << b
-    mat_cols = mats + masks
-    C = len(mat_cols)
-    # [W, 1 + S] send sizes: rows, then bytes of each string leaf, per destination (device side)
-    size_cols = [counts]
-    for li in str_leaves:
-        by_dest = torch.zeros(W, dtype=torch.int64, device=device)
-        if n:
-            by_dest.index_add_(0, sorted_dest, mats[leaves[li].mcol])
-        size_cols.append(by_dest)
-    send_sizes = torch.stack(size_cols, 1).contiguous()
-    recv_sizes = _a2a_counts(send_sizes)
-    both = torch.stack([send_sizes, recv_sizes]).tolist()            # the exchange's one host sync
+    lay = PK.Layout(table)
+    sizes, state = PK.plan(lay, dest.to(torch.int64), W, _force_torch())
+    # the per-leaf "has validity" flags ride along with the sizes: every rank ORs what it receives, so all ranks
+    # agree on the matrix layout without another collective
+    flags = torch.tensor(lay.flags(), dtype=torch.int64, device=device).expand(W, -1)
+    ext = torch.cat([sizes, flags], 1).contiguous()
+    recv_sizes = _a2a_counts(ext)
+    both = torch.stack([ext, recv_sizes]).tolist()              # the exchange's one host sync
+    lay.assign_flags(_or_rows([r[1 + lay.S:] for r in both[1]]))
     send_rows = [r[0] for r in both[0]]
     recv_rows = [r[0] for r in both[1]]
+    send_bytes = [[r[1 + s] for r in both[0]] for s in range(lay.S)]
+    recv_bytes = [[r[1 + s] for r in both[1]] for s in range(lay.S)]
+    mat, arenas = PK.scatter(lay, state, send_rows, send_bytes)
     n_out = sum(recv_rows)
-    if C:
-        send = torch.stack(mat_cols, 1).contiguous() if n else torch.empty((0, C), dtype=torch.int64, device=device)
-        recv = torch.empty((n_out, C), dtype=torch.int64, device=device)
-        _a2a(recv, send, recv_rows, send_rows)
-    else:
-        recv = torch.empty((n_out, 0), dtype=torch.int64, device=device)
-    # string bytes: rows are already grouped by destination, so each leaf's packed bytes are too
-    str_out = {}
-    for si, li in enumerate(str_leaves):
-        lf = leaves[li]
-        send_bytes = [r[1 + si] for r in both[0]]
-        recv_bytes = [r[1 + si] for r in both[1]]
-        sc = sops.compact_known(lf.col, sum(send_bytes))
-        total = sum(recv_bytes)
-        out = torch.zeros(total + 16, dtype=torch.uint8, device=device)
-        _a2a(out[:total], sc.arena[:sum(send_bytes)].contiguous(), recv_bytes, send_bytes)
-        rlens = recv[:, lf.mcol]
-        starts = torch.cumsum(rlens, 0) - rlens
-        str_out[li] = (out, starts, rlens.to(torch.int32))
-    # rebuild leaves
-    leaves_out = {}
-    for li, lf in enumerate(leaves):
-        valid = None
-        if lf.vbit >= 0:
-            w, b = divmod(lf.vbit, 63)
-            valid = ((recv[:, len(mats) + w] >> b) & 1).to(torch.bool)
-        if lf.kind == "prim":
-            d = recv[:, lf.mcol].contiguous()
-            if lf.torch_dtype == torch.float64:
-                d = d.view(torch.float64)
-            elif lf.torch_dtype == torch.bool:
-                d = d.to(torch.bool)
-            leaves_out[li] = PrimColumn(lf.dtype, d, valid)
-        elif lf.kind == "str":
-            arena, starts, lens = str_out[li]
-            leaves_out[li] = type(lf.col)(arena, starts, lens, valid, lf.col.dtype)
-        else:   # valid_only
-            leaves_out[li] = valid if valid is not None else None
-    cols = [_rebuild(s, leaves_out, n_out, device) for s in spec]
-    out = Table(t.names, cols, n_out, device)
+    recv = torch.empty((n_out, lay.C), dtype=torch.int64, device=device)
+    if lay.C:
+        _a2a(recv, mat, recv_rows, send_rows)
+    rarenas = []
+    for si in range(lay.S):
+        total = sum(recv_bytes[si])
+        out = torch.zeros(total + 16, dtype=torch.uint8, device=device)      # +16: string kernels over-read
+        _a2a(out[:total], arenas[si][:sum(send_bytes[si])], recv_bytes[si], send_bytes[si])
+        rarenas.append(out)
+    row_prefix = _prefix(recv_rows)
+    byte_base = [_prefix(recv_bytes[si])[:W] for si in range(lay.S)]
+    return PK.unpack(lay.names, lay.spec, lay.meta(), recv, rarenas, row_prefix, row_prefix[:W], byte_base, n_out,
+                     device, _force_torch())
+
+
+def _or_rows(rows):
+    out = [0] * len(rows[0])
+    for r in rows:
+        out = [a | int(b) for a, b in zip(out, r)]
+    return out
+
+
+def _prefix(xs):
+    out = [0]
+    for x in xs:
+        out.append(out[-1] + int(x))
     return out
 
 
@@ -338,22 +222,83 @@ def _broadcast(t: torch.Tensor, src: int) -> None:
         dist.broadcast(t, src=src, group=_g())
 
 
+def _all_gather_into(out: torch.Tensor, t: torch.Tensor) -> None:
+    """``out`` = the ranks' equal-size ``t`` concatenated in rank order — ``all_gather_into_tensor`` over RCCL
+    (one output buffer, no per-rank copies); a list all-gather over gloo."""
+    W = _w()
+    if not _staged(t) and dist.get_backend(_g()) != "gloo":
+        dist.all_gather_into_tensor(out, t.contiguous(), group=_g())
+        return
+    parts = [torch.empty(t.shape, dtype=t.dtype) for _ in range(W)]
+    dist.all_gather(parts, t.cpu(), group=_g())
+    out.copy_(torch.cat(parts).to(out.device))
+
+
 def broadcast_bytes(data: bytes, src: int = 0) -> bytes:
-    """``data`` from rank ``src`` on every rank: one broadcast of the length, one of the bytes (a device buffer over
-    RCCL when the ranks own GPUs — xGMI moves it; host memory over gloo)."""
-    from . import _DEVICE, _RANK
-    dev = _DEVICE if (_DEVICE is not None and dist.get_backend(_g()) != "gloo") else torch.device("cpu")
-    n = torch.tensor([len(data) if _RANK == src else 0], dtype=torch.int64, device=dev)
+    """``data`` from rank ``src`` on every rank, as host bytes (small payloads: configuration, layouts).  Bulk
+    payloads that end on the device use ``broadcast_device_bytes``."""
+    from . import _RANK
+    n = torch.tensor([len(data) if _RANK == src else 0], dtype=torch.int64)
+    dist.broadcast(n, src=src, group=_gloo_or_default())
+    size = int(n.item())
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8) if (_RANK == src and size) else \
+        torch.empty(size, dtype=torch.uint8)
+    if size:
+        dist.broadcast(buf, src=src, group=_gloo_or_default())
+    return data if _RANK == src else buf.numpy().tobytes()
+
+
+def _gloo_or_default():
+    """Host-tensor broadcasts need a gloo communicator; with RCCL as the job's backend they go through a device
+    buffer instead (``broadcast_device_bytes``)."""
+    g = _g()
+    return g if dist.get_backend(g) == "gloo" else _host_group()
+
+
+_HOST_GROUP = None
+
+
+def _host_group():
+    global _HOST_GROUP
+    if _HOST_GROUP is None:
+        _HOST_GROUP = dist.new_group(backend="gloo")
+    return _HOST_GROUP
+
+
+def broadcast_device_bytes(data: Optional[bytes], src: int, device, pad: int = 64) -> Tuple[torch.Tensor, int]:
+    """A byte payload from rank ``src`` as a device buffer on every rank → (buffer of length + ``pad`` zeroed
+    bytes, length).  The source copies its bytes to the device once (pinned staging) and the RCCL broadcast moves
+    them over xGMI straight into every receiver's HBM: receivers never stage the payload in host memory (SURVEY
+    §2.G X3 — a 100 M-row reference table's CSV crosses each receiver's PCIe link zero times).  Over gloo (CPU
+    ranks) the buffer is a host tensor."""
+    from . import _RANK
+    device = torch.device(device)
+    n = torch.tensor([len(data) if _RANK == src else 0], dtype=torch.int64, device=device)
     _broadcast(n, src)
     size = int(n.item())
     if _RANK == src:
-        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if size else \
-            torch.empty(0, dtype=torch.uint8, device=dev)
+        if device.type == "cuda":
+            host = torch.empty(size + pad, dtype=torch.uint8, pin_memory=True)
+            host[size:].zero_()
+            if size:
+                host[:size] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            buf = host.to(device, non_blocking=True)
+            buf.record_stream(torch.cuda.current_stream(device))
+        else:
+            buf = torch.zeros(size + pad, dtype=torch.uint8)
+            if size:
+                buf[:size] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
     else:
-        buf = torch.empty(size, dtype=torch.uint8, device=dev)
+        buf = torch.zeros(size + pad, dtype=torch.uint8, device=device)
     if size:
-        _broadcast(buf, src)
-    return data if _RANK == src else buf.cpu().numpy().tobytes()
+        _broadcast(buf[:size], src) if not _staged(buf) else _broadcast_staged_slice(buf, size, src)
+    return buf, size
+
+
+def _broadcast_staged_slice(buf, size, src):
+    h = buf[:size].cpu()
+    dist.broadcast(h, src=src, group=_g())
+    buf[:size].copy_(h)
 
 
 def broadcast_tensor(t: Optional[torch.Tensor], src: int = 0, dtype=torch.uint8, device=None) -> torch.Tensor:
@@ -369,88 +314,52 @@ def broadcast_tensor(t: Optional[torch.Tensor], src: int = 0, dtype=torch.uint8,
 
 
 def allgather_table(table):
-    """Every rank receives the concatenation of all ranks' rows (rank order)."""
+    """Every rank receives the concatenation of all ranks' rows (rank order).
+
+    The table is packed once (identity order), the per-rank sizes are all-gathered (the one host read-back), and
+    the matrix and every string arena travel with one ``all_gather_into_tensor`` each, padded to the largest
+    rank's share: the receive buffer is W × the largest share — the result's size for balanced ranks — and no rank
+    ever materialises W copies of its own rows.  One unpack launch reads the padded buffers in place (strings stay
+    views into the gathered arenas)."""
+    from . import packing as PK
     from ..engine.column import Table
     W = _w()
     if W <= 1:
         return table
-    n = table.length
-    idx = torch.arange(n, device=table.device).repeat(W)
-    dest = torch.arange(W, device=table.device).repeat_interleave(n)
-    return shuffle_table(table.take(idx), dest)
-
-
-def _pack(table):
-    """Flatten a table for a collective: (spec, leaves, [n, C] int64 matrix, {leaf: compacted string bytes})."""
-    from ..ops import strings as sops
     device = table.device
-    n = table.length
-    leaves: List[_Leaf] = []
-    spec: list = []
-    for c in table.columns:
-        _flatten(c, leaves, spec)
-    mats, nvalid = [], 0
-    strs = {}
-    for li, lf in enumerate(leaves):
-        c = lf.col
-        if lf.kind == "prim":
-            d = c.data
-            d = d.view(torch.int64) if d.dtype == torch.float64 else (d if d.dtype == torch.int64 else d.to(torch.int64))
-            lf.mcol = len(mats)
-            mats.append(d)
-        elif lf.kind == "str":
-            lf.mcol = len(mats)
-            mats.append(c.lens.to(torch.int64))
-            total = int(c.lens.to(torch.int64).sum().item()) if n else 0
-            strs[li] = sops.compact_known(c, total).arena[:total].contiguous() if n else \
-                torch.empty(0, dtype=torch.uint8, device=device)
-        if c.valid is not None:
-            lf.vbit = nvalid
-            nvalid += 1
-    masks = [torch.zeros(n, dtype=torch.int64, device=device) for _ in range((nvalid + 62) // 63)]
-    for lf in leaves:
-        if lf.vbit >= 0:
-            w, b = divmod(lf.vbit, 63)
-            masks[w] |= lf.col.valid.to(torch.int64) << b
-    cols = mats + masks
-    mat = torch.stack(cols, 1).contiguous() if (cols and n) else torch.empty((n, len(cols)), dtype=torch.int64,
-                                                                              device=device)
-    return spec, leaves, mat, strs, len(mats)
+    lay = PK.Layout(table)
+    sizes, state = PK.plan(lay, None, 1, _force_torch())          # [1, 1+S]: rows, bytes per string leaf
+    flags = torch.tensor([lay.flags()], dtype=torch.int64, device=device)
+    ext = torch.cat([sizes.reshape(1, -1), flags], 1).contiguous()
+    allsz = torch.empty((W, ext.shape[1]), dtype=torch.int64, device=device)
+    _all_gather_into(allsz, ext)
+    got = allsz.tolist()                                           # the one host sync
+    lay.assign_flags(_or_rows([r[1 + lay.S:] for r in got]))      # the ranks' agreed validity layout
+    rows = [r[0] for r in got]
+    bts = [[r[1 + s] for r in got] for s in range(lay.S)]
+    maxr = max(rows)
+    maxb = [max(bts[s]) for s in range(lay.S)]
+    me = _rank()
+    mat, arenas = PK.scatter(lay, state, [lay.n], [[bts[s][me]] for s in range(lay.S)], rows_alloc=maxr,
+                             bytes_alloc=maxb)
+    n_out = sum(rows)
+    gm = torch.empty((W * maxr, lay.C), dtype=torch.int64, device=device)
+    if lay.C and maxr:
+        _all_gather_into(gm, mat[:maxr])
+    gar = []
+    for s in range(lay.S):
+        ga = torch.zeros(W * maxb[s] + 16, dtype=torch.uint8, device=device)
+        if maxb[s]:
+            _all_gather_into(ga[:W * maxb[s]], arenas[s][:maxb[s]])
+        gar.append(ga)
+    out = PK.unpack(lay.names, lay.spec, lay.meta(), gm, gar, _prefix(rows), [k * maxr for k in range(W)],
+                    [[k * maxb[s] for k in range(W)] for s in range(lay.S)], n_out, device, _force_torch())
+    return Table(out.names, out.columns, out.length, device)
 
 
-def _leaf_meta(leaves):
-    """Picklable per-leaf layout (what a receiver needs to rebuild columns it has never seen)."""
-    return [(lf.kind, lf.dtype, lf.mcol, lf.vbit, lf.torch_dtype,
-             type(lf.col) if lf.kind == "str" else None, getattr(lf.col, "dtype", None)) for lf in leaves]
-
-
-def _unpack(table_names, spec, meta, mat, strs, nmats, device):
-    from ..engine.column import PrimColumn, Table
-    n = int(mat.shape[0])
-    out = {}
-    for li, (kind, dtype, mcol, vbit, tdt, scls, cdt) in enumerate(meta):
-        valid = None
-        if vbit >= 0:
-            w, b = divmod(vbit, 63)
-            valid = ((mat[:, nmats + w] >> b) & 1).to(torch.bool)
-        if kind == "prim":
-            d = mat[:, mcol].contiguous()
-            if tdt == torch.float64:
-                d = d.view(torch.float64)
-            elif tdt == torch.bool:
-                d = d.to(torch.bool)
-            elif tdt is not None and tdt != torch.int64:
-                d = d.to(tdt)
-            out[li] = PrimColumn(dtype, d, valid)
-        elif kind == "str":
-            lens = mat[:, mcol]
-            starts = torch.cumsum(lens, 0) - lens
-            arena = torch.zeros(int(strs[li].shape[0]) + 16, dtype=torch.uint8, device=device)
-            arena[:strs[li].shape[0]] = strs[li]
-            out[li] = scls(arena, starts, lens.to(torch.int32), valid, cdt)
-        else:
-            out[li] = valid
-    return Table(table_names, [_rebuild(sp, out, n, device) for sp in spec], n, device)
+def _rank():
+    from . import _RANK
+    return _RANK
 
 
 def broadcast_table(table, src: int = 0):
@@ -458,23 +367,40 @@ def broadcast_table(table, src: int = 0):
     layout travels as one small object broadcast, the data as one broadcast of the packed [rows × C] int64 matrix
     plus one per string leaf's bytes — the source sends each byte once (ncclBroadcast's pipelined ring/tree over
     xGMI), never W copies."""
+    from . import packing as PK
     from . import _RANK
     W = _w()
     if W <= 1:
         return table
     device = table.device
     if _RANK == src:
-        spec, leaves, mat, strs, nmats = _pack(table)
-        layout = [spec, _leaf_meta(leaves), nmats, int(mat.shape[0]), int(mat.shape[1]), sorted(strs)]
+        lay = PK.Layout(table)
+        sizes, state = PK.plan(lay, None, 1, _force_torch())
+        szl = sizes.tolist()[0]
+        mat, arenas = PK.scatter(lay, state, [lay.n], [[szl[1 + s]] for s in range(lay.S)])
+        layout = [lay.spec, lay.meta(), lay.n, lay.C, [int(szl[1 + s]) for s in range(lay.S)]]
     else:
-        layout, mat, strs = [None] * 6, None, {}
+        layout, mat, arenas = None, None, None
     obj = [layout]
     dist.broadcast_object_list(obj, src=src, group=_g())
-    spec, meta, nmats, rows, C, str_ids = obj[0]
-    flat = broadcast_tensor(mat.reshape(-1) if _RANK == src else None, src, torch.int64, device)
-    mat = flat.reshape(rows, C)
-    got = {li: broadcast_tensor(strs[li] if _RANK == src else None, src, torch.uint8, device) for li in str_ids}
-    out = _unpack(table.names, spec, meta, mat, got, nmats, device)
+    spec, meta, rows, C, nbytes = obj[0]
+    if _RANK != src:
+        mat = torch.empty((rows, C), dtype=torch.int64, device=device)
+    if rows and C:
+        _broadcast(mat, src)
+    got = []
+    for s, nb in enumerate(nbytes):
+        buf = torch.zeros(nb + 16, dtype=torch.uint8, device=device)
+        if _RANK == src and nb:
+            buf[:nb] = arenas[s][:nb]
+        if nb:
+            if _staged(buf):
+                _broadcast_staged_slice(buf, nb, src)
+            else:
+                _broadcast(buf[:nb], src)
+        got.append(buf)
+    out = PK.unpack(table.names, spec, meta, mat, got, [0, rows], [0], [[0] for _ in nbytes], rows, device,
+                    _force_torch())
     out.dist = P_REPLICATED
     return out
 

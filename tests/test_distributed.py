@@ -251,35 +251,45 @@ def test_kfd_topology_maps_hip_index_to_pci_folder(tmp_path, monkeypatch):
     assert kfd_pci_path(0, str(topo), str(pci)).endswith("0000:75:00.0")
 
 
-def _bcast_worker(rank, world, port, q, path):
+def _bcast_worker(rank, world, port, q, path, device="cpu"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         import torch.distributed as dist
+        if device != "cpu":
+            torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from dxa import parallel as P
         from dxa.engine.column import Table
         from dxa.engine.types import StructField, StructType
         from dxa.io.refdata import load_csv
-        P.init(dist.group.WORLD, "cpu")
+        P.init(dist.group.WORLD, device)
         schema = StructType((StructField("k", "long"), StructField("s", "string"), StructField("v", "double")))
         rows = _rows(3, 50) if rank == 0 else []
-        t = P.broadcast_table(Table.from_pylist(rows, schema))
-        ref = load_csv(path, ",", True, "cpu")
-        q.put((rank, (t.to_pylist(), ref.to_pylist()), None))
+        t = P.broadcast_table(Table.from_pylist(rows, schema, device))
+        st = {}
+        ref = load_csv(path, ",", True, device, stats=st)
+        # on a GPU only rank 0 stages the file in host memory; the others receive it straight into HBM
+        assert device == "cpu" or st["host_staged"] == (rank == 0), st
+        ag = P.allgather_table(Table.from_pylist(rows if rank == 0 else _rows(4, 7), schema, device))
+        q.put((rank, (t.to_pylist(), ref.to_pylist(), ag.to_pylist()), None))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:
         q.put((rank, None, traceback.format_exc()))
 
 
-def test_broadcast_table_and_reference_data(tmp_path):
-    """Rank 0's table / reference file reaches every rank through broadcasts (no per-rank file reads)."""
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_broadcast_table_and_reference_data(tmp_path, device):
+    """Rank 0's table / reference file reaches every rank through broadcasts (no per-rank file reads); an
+    all-gather of uneven shares (50 and 7 rows) gives every rank both, in rank order."""
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
     path = tmp_path / "ref.csv"
     path.write_text('id,name\n1,"a,b"\n2,\n')
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q, str(path))) for r in range(2)]
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q, str(path), device)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -292,6 +302,8 @@ def test_broadcast_table_and_reference_data(tmp_path):
     for r in (0, 1):
         assert _canon(res[r][0]) == _canon(_rows(3, 50))
         assert res[r][1] == [{"id": "1", "name": "a,b"}, {"id": "2", "name": None}]
+        assert res[r][2] == res[0][2] and _canon(res[r][2]) == _canon(_rows(3, 50) + _rows(4, 7))
+        assert [x["k"] for x in res[r][2]] == [x["k"] for x in _rows(3, 50) + _rows(4, 7)]     # rank order
 
 
 def test_host_threads_share_the_socket(monkeypatch):

@@ -165,10 +165,15 @@ def _rows_equal(got, want, path):
     _close(got, want, path)
 
 
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("variant", ["groupby", "window", "join", "full", "passthrough"])
-def test_flow_two_ranks_match_one(variant, tmp_path):
+def test_flow_two_ranks_match_one(variant, device, tmp_path):
+    """``cuda``: both ranks on the test box's one GPU (every kernel, incl. the exchange pack / unpack kernels, on
+    the device; the collectives staged through gloo)."""
     import time
     from dxa import parallel as P
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
     shared1, shared2 = str(tmp_path / "one_shared"), str(tmp_path / "two_shared")     # state dirs differ per run
     for s in (shared1, shared2):
         os.makedirs(s, exist_ok=True)
@@ -177,8 +182,8 @@ def test_flow_two_ranks_match_one(variant, tmp_path):
     clock0 = (int(time.time()) - 3600) * 1_000_000
     batches = _batches(clock0)
     P.shutdown()
-    one = _run(variant, 0, 1, str(tmp_path / "one" / "w"), shared1, batches)
-    two = _spawn_flow(variant, tmp_path, shared2, batches)
+    one = _run(variant, 0, 1, str(tmp_path / "one" / "w"), shared1, batches, device)
+    two = _spawn_flow(variant, tmp_path, shared2, batches, device)
     rows_seen = 0
     for b in range(N_BATCHES):
         lines1, state1, m1 = one[b]
@@ -204,12 +209,12 @@ def test_flow_two_ranks_match_one(variant, tmp_path):
         assert k0 and k1 and not (k0 & k1)
 
 
-def _spawn_flow(variant, tmp_path, shared, batches):
+def _spawn_flow(variant, tmp_path, shared, batches, device="cpu"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q, variant, str(tmp_path / f"two{r}" / "w"), shared,
-                                               batches, "cpu")) for r in range(2)]
+                                               batches, device)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
