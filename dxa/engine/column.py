@@ -420,13 +420,13 @@ def strings_from_pylist(values: Sequence[Optional[str]], device, dtype="string")
         starts[i] = acc
         acc += l
     blob = b"".join(enc)
-    arena = torch.frombuffer(bytearray(blob + b"\0" * 16), dtype=torch.uint8).to(device)
+    arena = _h2d(blob + b"\0" * 16, torch.uint8, device)
     valid = None
     if any(v is None for v in values):
-        valid = torch.tensor([v is not None for v in values], dtype=torch.bool, device=device)
+        valid = _h2d([v is not None for v in values], torch.bool, device)
     cls = JsonColumn if dtype != "string" else StrColumn
-    return cls(arena, torch.tensor(starts, dtype=torch.int64, device=device),
-               torch.tensor(lens, dtype=torch.int32, device=device), valid, dtype)
+    return cls(arena, _h2d(starts, torch.int64, device),
+               _h2d(lens, torch.int32, device), valid, dtype)
 
 
 def _py_to_storage(v, dtype):
@@ -457,7 +457,7 @@ def column_from_pylist(values: Sequence[Any], dtype: Any, device="cpu") -> Colum
                     for f in dtype.fields]
         valid = None
         if any(v is None for v in values):
-            valid = torch.tensor([v is not None for v in values], dtype=torch.bool, device=device)
+            valid = _h2d([v is not None for v in values], torch.bool, device)
         return StructColumn(names, children, n, valid, False, dtype, device)
     if isinstance(dtype, (MapType, ArrayType)):
         return strings_from_pylist([None if v is None else json.dumps(v, separators=(",", ":")) for v in values],
@@ -465,10 +465,10 @@ def column_from_pylist(values: Sequence[Any], dtype: Any, device="cpu") -> Colum
     if dtype == "null":
         return ConstColumn(None, "null", n, device)
     tdt = TORCH_DTYPE[dtype]
-    data = torch.tensor([_py_to_storage(v, dtype) for v in values], dtype=tdt, device=device)
+    data = _h2d([_py_to_storage(v, dtype) for v in values], tdt, device)
     valid = None
     if any(v is None or (isinstance(v, float) and dtype == "null") for v in values):
-        valid = torch.tensor([v is not None for v in values], dtype=torch.bool, device=device)
+        valid = _h2d([v is not None for v in values], torch.bool, device)
     return PrimColumn(dtype, data, valid)
 
 
@@ -657,3 +657,8 @@ def concat_tables(tables: List[Table]) -> Table:
             parts.append(c)
         cols.append(concat_columns(parts))
     return Table(names, cols, sum(t.length for t in tables), tables[0].device)
+
+
+def _h2d(data, dtype, device):
+    from ..ops.native import h2d
+    return h2d(data, dtype, device)

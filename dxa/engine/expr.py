@@ -675,8 +675,8 @@ def choose(branch: torch.Tensor, options: List[Column], n, dev) -> Column:
         if dtype == "null":
             return ConstColumn(None, "null", n, dev)
         tdt = TORCH_DTYPE.get(dtype, torch.float64)
-        table = torch.tensor([0 if v is None else v for v in vals], dtype=tdt, device=dev)
-        ok = torch.tensor([v is not None for v in vals], dtype=torch.bool, device=dev)
+        table = _h2d([0 if v is None else v for v in vals], tdt, dev)
+        ok = _h2d([v is not None for v in vals], torch.bool, dev)
         b = branch.to(torch.int64)
         okb = ok[b]
         return PrimColumn(dtype, table[b], None if bool(okb.all()) else okb)
@@ -1600,3 +1600,8 @@ def output_name(e: A.Expr) -> str:
 
 
 from . import sqlfuncs as _sqlfuncs  # noqa: E402,F401  (registers the extended built-ins)
+
+
+def _h2d(data, dtype, device):
+    from ..ops.native import h2d
+    return h2d(data, dtype, device)

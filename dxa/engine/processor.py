@@ -247,7 +247,7 @@ class Processor:
             from .column import column_from_pylist
             infos = [dict(i) for i, _c in raw.file_rows]
             idx = torch.repeat_interleave(torch.arange(len(infos), device=dev),
-                                          torch.tensor([c for _i, c in raw.file_rows], device=dev))
+                                          _h2d([c for _i, c in raw.file_rows], torch.int64, dev))
             pps = [dict(pp, InputTime=str(i.get("fileTime", "")), Partition=str(i.get("outputFileName", "")))
                    for i in infos]
             cols = [raw_col, props, sysprops, column_from_pylist(pps, empty_map, dev).take(idx)]
@@ -696,3 +696,8 @@ class _InFlight:
 def _fmt_ts(us: int) -> str:
     t = _dt.datetime(1970, 1, 1) + _dt.timedelta(microseconds=int(us))
     return t.strftime("%Y-%m-%d %H:%M:%S.") + f"{t.microsecond // 1000:03d}"
+
+
+def _h2d(data, dtype, device):
+    from ..ops.native import h2d
+    return h2d(data, dtype, device)

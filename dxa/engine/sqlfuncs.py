@@ -395,7 +395,7 @@ def _tz_shift(to_utc: bool):
                 off = t.replace(tzinfo=_dt.timezone.utc).astimezone(z).utcoffset()
             us = int(off.total_seconds() * 1_000_000) if off is not None else 0
             out.append(int(v) - us if to_utc else int(v) + us)
-        return PrimColumn("timestamp", torch.tensor(out, dtype=torch.int64, device=a.device), a.valid)
+        return PrimColumn("timestamp", _h2d(out, torch.int64, a.device), a.valid)
     return f
 
 
@@ -1631,3 +1631,106 @@ def _register_more():
 
 
 _register_more()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# device paths of the string built-ins (dxa/ops/strfuncs.py, csrc/strfuncs.hip)
+# ---------------------------------------------------------------------------------------------------------------
+
+def _const_arg(args, i, default=None):
+    if i >= len(args):
+        return True, default
+    a = args[i]
+    return (isinstance(a, ConstColumn), a.value if isinstance(a, ConstColumn) else None)
+
+
+def _dev_str(c):
+    """``c`` as a device StrColumn with contiguous int64 starts / int32 lens (or None if it is not one)."""
+    if not _gpu_str(c):
+        return None
+    st = c.starts if (c.starts.dtype == torch.int64 and c.starts.is_contiguous()) else \
+        c.starts.to(torch.int64).contiguous()
+    ln = c.lens if (c.lens.dtype == torch.int32 and c.lens.is_contiguous()) else c.lens.to(torch.int32).contiguous()
+    if st is c.starts and ln is c.lens:
+        return c
+    return type(c)(c.arena, st, ln, c.valid, c.dtype)
+
+
+def _device_string_fn(name, device_fn, host_fn, out_type="string"):
+    """``device_fn(col, *const_args)`` on a device string column with constant (non-null) extra arguments; a None
+    result (rows the kernel does not handle) or any other argument shape → the host function."""
+    host = _host_string_fn(host_fn, out_type)
+
+    def f(e, scope, ctx, subst):
+        args = _args(e, scope, ctx, subst)
+        a = _dev_str(args[0]) if args else None
+        if a is not None and all(isinstance(x, ConstColumn) and x.value is not None for x in args[1:]):
+            out = device_fn(a, *[x.value for x in args[1:]])
+            if out is not None:
+                return out
+        return host(e, scope, ctx, subst)
+    f.__name__ = f"_f_{name}"
+    return f
+
+
+def _lpad_host(s, l, p=" "):
+    s, l, p = str(s), int(l), str(p)
+    if l <= 0:
+        return ""
+    if len(s) >= l or not p:
+        return s[:l]
+    fill = l - len(s)
+    return (p * (fill // len(p) + 1))[:fill] + s
+
+
+def _rpad_host(s, l, p=" "):
+    s, l, p = str(s), int(l), str(p)
+    if l <= 0:
+        return ""
+    if len(s) >= l or not p:
+        return s[:l]
+    fill = l - len(s)
+    return s + (p * (fill // len(p) + 1))[:fill]
+
+
+def _ascii_host(s):
+    b = str(s).encode("utf-8")
+    return (b[0] - 256 if b[0] >= 128 else b[0]) if b else 0
+
+
+def _levenshtein_fn(e, scope, ctx, subst):
+    args = _args(e, scope, ctx, subst)
+    if len(args) == 2 and any(_gpu_str(x) for x in args):
+        cols = [materialize(x) if isinstance(x, ConstColumn) and x.value is not None else x for x in args]
+        a, b = (_dev_str(c) for c in cols)
+        if a is not None and b is not None and a.length == b.length:
+            from ..ops import strfuncs as SF
+            out = SF.levenshtein(a, b)
+            if out is not None:
+                return out
+    return _host_string_fn(_levenshtein, "int")(e, scope, ctx, subst)
+
+
+def _register_device_strings():
+    from ..ops import strfuncs as SF
+    reg = register_function
+    reg("lpad", _device_string_fn("lpad", lambda c, l, p=" ": SF.pad(c, int(l), str(p), True), _lpad_host))
+    reg("rpad", _device_string_fn("rpad", lambda c, l, p=" ": SF.pad(c, int(l), str(p), False), _rpad_host))
+    reg("reverse", _device_string_fn("reverse", SF.reverse, lambda s: str(s)[::-1]))
+    reg("repeat", _device_string_fn("repeat", lambda c, k: SF.repeat(c, int(k)),
+                                    lambda s, k: str(s) * max(0, int(k))))
+    reg("translate", _device_string_fn("translate", lambda c, m, r: SF.translate(c, str(m), str(r)), _translate))
+    reg("initcap", _device_string_fn("initcap", SF.initcap, _initcap))
+    reg("ascii", _device_string_fn("ascii", SF.ascii_code, _ascii_host, "int"))
+    reg("substring_index", _device_string_fn("substring_index",
+                                             lambda c, d, k: SF.substring_index(c, str(d), int(k)),
+                                             _substring_index))
+    reg("levenshtein", _levenshtein_fn)
+
+
+_register_device_strings()
+
+
+def _h2d(data, dtype, device):
+    from ..ops.native import h2d
+    return h2d(data, dtype, device)

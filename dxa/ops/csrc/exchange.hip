@@ -339,9 +339,8 @@ DXA_API int dxa_xchg_limits(int32_t* out) {
 // Phase 1 (before the size exchange): histograms + scan → hist bases, sizes.
 DXA_API int dxa_xchg_plan(const void* args, void* stream) {
   const PackArgs& a = *(const PackArgs*)args;
-  if (a.n > 0) {
-    hipLaunchKernelGGL(xchg_hist_kernel, dim3(a.nblocks), dim3(kThreads), 0, (hipStream_t)stream, a);
-  }
+  // also for n == 0: the (single) block writes the zero histogram the scan reads
+  hipLaunchKernelGGL(xchg_hist_kernel, dim3(a.nblocks), dim3(kThreads), 0, (hipStream_t)stream, a);
   hipLaunchKernelGGL(xchg_scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

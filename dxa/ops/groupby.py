@@ -115,8 +115,8 @@ def _exact_groups(keys, device) -> Groups:
             rep.append(i)
         gid.append(g)
     dt = torch.int32 if _on_gpu(device) else torch.int64
-    return Groups(torch.tensor(gid, dtype=dt, device=device), len(rep),
-                  torch.tensor(rep, dtype=torch.int64, device=device))
+    return Groups(N.h2d(gid, dt, device), len(rep),
+                  N.h2d(rep, torch.int64, device))
 
 
 _OPS = {"sum": 0, "min": 1, "max": 2, "count": 3}

@@ -208,13 +208,13 @@ def frame_lines_gpu(buf: torch.Tensor, length: int, expected: Optional[int] = No
         else:
             offs[1:].fill_(0)
             if mismatches is not None:
-                mismatches.append(torch.tensor(total != 0, device=dev))
+                mismatches.append(torch.full((), bool(total != 0), dtype=torch.bool, device=dev))
         return offs
     pos = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
     if length:
         N.call("dxa_write_newlines_bits", N.ptr(bits), length, seg, N.ptr(base), N.ptr(pos), total, 0, st)
     pos = pos[:total]
-    ends = torch.cat([pos + 1, torch.tensor([length], dtype=torch.int64, device=dev)])
+    ends = torch.cat([pos + 1, N.h2d([length], torch.int64, dev)])
     starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos + 1])
     keep = (ends - starts) > 1  # drop empty lines
     starts, ends = starts[keep], ends[keep]

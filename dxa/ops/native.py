@@ -201,3 +201,27 @@ def u8(mask):
     if mask is None:
         return None
     return mask.view(torch.uint8) if mask.dtype == torch.bool else mask
+
+
+def h2d(data, dtype=None, device="cpu") -> torch.Tensor:
+    """Host data (list, bytes or CPU tensor) as a tensor on ``device`` WITHOUT stalling the host.
+
+    On ROCm a blocking host→device copy from pageable memory — ``tensor.to(cuda)``, ``torch.tensor(list,
+    device=cuda)`` — returns only after the stream has drained (``tools/gpu/h2d_sync_probe.py``: a 64-byte upload
+    behind a 20 ms kernel blocks the host 20 ms), which serialises host planning with device work.  Here the bytes go
+    through a pinned staging block from torch's caching host allocator (reused only after the copy ran) and a
+    non-blocking copy on the current stream."""
+    dev = torch.device(device)
+    if isinstance(data, torch.Tensor):
+        h = data
+    elif isinstance(data, (bytes, bytearray, memoryview)):
+        h = torch.frombuffer(bytearray(data), dtype=torch.uint8) if len(data) else torch.empty(0, dtype=torch.uint8)
+        if dtype is not None and dtype != torch.uint8:
+            h = h.view(dtype)
+    else:
+        h = torch.tensor(data, dtype=dtype)
+    if dev.type != "cuda":
+        return h.to(dev)
+    if h.numel() == 0:
+        return torch.empty(h.shape, dtype=h.dtype, device=dev)
+    return h.pin_memory().to(dev, non_blocking=True)

@@ -275,9 +275,9 @@ class _DevBuilder:
             arr[i] = DevNode(nd["kind"], nd["nchildren"], nd["child0"], nd["drop_nulls"], nd["name"][0],
                              nd["name"][1], nd["const"][0], nd["const"][1], nd["data"], nd["valid"], nd["arena"],
                              nd["starts"], nd["lens"])
-        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device, non_blocking=False)
-        text = torch.frombuffer(bytearray(bytes(self.text) + b"\0" * (-len(self.text) % 8 + 8)),
-                                dtype=torch.uint8).to(device)
+        from . import native as N
+        raw = N.h2d(bytes(arr), torch.uint8, device)
+        text = N.h2d(bytes(self.text) + b"\0" * (-len(self.text) % 8 + 8), torch.uint8, device)
         return raw, text
 
 
@@ -366,7 +366,7 @@ class Staged:
             top = [b.add(c, nm) for nm, c in zip(self.table.names, self.table.columns)]
             nodes, text = b.device_arrays(dev)
             prog = b.program(top)
-            prog_t = torch.tensor(prog or [0], dtype=torch.int32).to(dev)
+            prog_t = N.h2d(prog or [0], torch.int32, dev)
             nprog = len(prog) // 4
             st = N.stream_handle(dev)
             lens = torch.empty(max(1, n), dtype=torch.int64, device=dev)

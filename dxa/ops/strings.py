@@ -263,8 +263,7 @@ def _vm_tensors(prog, device):
     cache = prog.__dict__.setdefault("_dev", {})
     t = cache.get(device)
     if t is None:
-        t = cache[device] = (torch.tensor(prog.code, dtype=torch.int32).to(device),
-                             torch.tensor(prog.sets, dtype=torch.int32).to(device))
+        t = cache[device] = (N.h2d(prog.code, torch.int32, device), N.h2d(prog.sets, torch.int32, device))
     return t
 
 
@@ -290,7 +289,7 @@ def regex_replace(col, prog, tokens: List[int]):
     from ..engine.column import StrColumn
     n, dev = col.length, col.device
     code, sets = _vm_tensors(prog, dev)
-    rep = torch.tensor(tokens or [0], dtype=torch.int32).to(dev)
+    rep = N.h2d(tokens or [0], torch.int32, dev)
     lens = torch.zeros(n, dtype=torch.int32, device=dev)
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     st = N.stream_handle(dev)
@@ -342,7 +341,7 @@ def compare_columns(a, b, op: str) -> torch.Tensor:
         return out
     va, vb = _raw_bytes(a), _raw_bytes(b)
     f = {"<": lambda x, y: x < y, "<=": lambda x, y: x <= y, ">": lambda x, y: x > y, ">=": lambda x, y: x >= y}[op]
-    return torch.tensor([f(x, y) for x, y in zip(va, vb)], dtype=torch.bool, device=a.device)
+    return N.h2d([f(x, y) for x, y in zip(va, vb)], torch.bool, a.device)
 
 
 class _ConcatPart(ctypes.Structure):
@@ -362,7 +361,7 @@ def concat_strings(parts: List[Union[str, object]], n: int, device):
         for i, p in enumerate(parts):
             if isinstance(p, str):
                 b = p.encode("utf-8")
-                t = torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8).to(device)
+                t = N.h2d(b + b"\0", torch.uint8, device)
                 keep.append(t)
                 arr[i] = _ConcatPart(0, 0, 0, 0, t.data_ptr(), len(b), 1)
             else:
@@ -370,7 +369,7 @@ def concat_strings(parts: List[Union[str, object]], n: int, device):
                 keep.append(v)
                 arr[i] = _ConcatPart(p.arena.data_ptr(), p.starts.data_ptr(), p.lens.data_ptr(),
                                      0 if v is None else v.data_ptr(), 0, 0, 0)
-        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
+        raw = N.h2d(bytes(arr), torch.uint8, device)
         lens = torch.empty(n, dtype=torch.int64, device=device)
         ok = torch.empty(n, dtype=torch.bool, device=device)
         st = N.stream_handle(device)
@@ -409,7 +408,7 @@ def concat_ws(sep: str, parts: List[Union[str, object]], n: int, device):
     for i, p in enumerate(parts):
         if isinstance(p, str):
             b = p.encode("utf-8")
-            t = torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8).to(device)
+            t = N.h2d(b + b"\0", torch.uint8, device)
             keep.append(t)
             arr[i] = _ConcatPart(0, 0, 0, 0, t.data_ptr(), len(b), 1)
         else:
@@ -417,9 +416,9 @@ def concat_ws(sep: str, parts: List[Union[str, object]], n: int, device):
             keep.append(v)
             arr[i] = _ConcatPart(p.arena.data_ptr(), p.starts.data_ptr(), p.lens.data_ptr(),
                                  0 if v is None else v.data_ptr(), 0, 0, 0)
-    raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
+    raw = N.h2d(bytes(arr), torch.uint8, device)
     sb = sep.encode("utf-8")
-    st_ = torch.frombuffer(bytearray(sb + b"\0"), dtype=torch.uint8).to(device)
+    st_ = N.h2d(sb + b"\0", torch.uint8, device)
     lens = torch.empty(n, dtype=torch.int64, device=device)
     st = N.stream_handle(device)
     N.call("dxa_concat_ws_len", N.ptr(raw), len(parts), n, len(sb), N.ptr(lens), st)

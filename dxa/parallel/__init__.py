@@ -112,5 +112,6 @@ def set_dist(table, d: str):
 
 
 from .exchange import (MetricKeysMismatch, all_reduce_sum, allgather_table, broadcast_bytes,  # noqa: E402
+                       broadcast_device_bytes,
                        broadcast_table, broadcast_tensor, is_max_metric, order_point, rebalance_table, reduce_metrics,
                        shuffle_table, split_by_destination)

@@ -173,7 +173,7 @@ def shuffle_table(table, dest: torch.Tensor):
     sizes, state = PK.plan(lay, dest.to(torch.int64), W, _force_torch())
     # the per-leaf "has validity" flags ride along with the sizes: every rank ORs what it receives, so all ranks
     # agree on the matrix layout without another collective
-    flags = torch.tensor(lay.flags(), dtype=torch.int64, device=device).expand(W, -1)
+    flags = _h2d(lay.flags(), torch.int64, device).expand(W, -1)
     ext = torch.cat([sizes, flags], 1).contiguous()
     recv_sizes = _a2a_counts(ext)
     both = torch.stack([ext, recv_sizes]).tolist()              # the exchange's one host sync
@@ -329,7 +329,7 @@ def allgather_table(table):
     device = table.device
     lay = PK.Layout(table)
     sizes, state = PK.plan(lay, None, 1, _force_torch())          # [1, 1+S]: rows, bytes per string leaf
-    flags = torch.tensor([lay.flags()], dtype=torch.int64, device=device)
+    flags = _h2d([lay.flags()], torch.int64, device)
     ext = torch.cat([sizes.reshape(1, -1), flags], 1).contiguous()
     allsz = torch.empty((W, ext.shape[1]), dtype=torch.int64, device=device)
     _all_gather_into(allsz, ext)
@@ -424,3 +424,8 @@ def rebalance_table(table):
     offset = int(sum(torch.cat(counts).tolist()[:_RANK]))          # one host read-back
     dest = (torch.arange(n, dtype=torch.int64, device=device) + offset) % W
     return shuffle_table(table, dest)
+
+
+def _h2d(data, dtype, device):
+    from ..ops.native import h2d
+    return h2d(data, dtype, device)

@@ -199,7 +199,7 @@ def scatter_torch(lay: Layout, state, send_rows: List[int], send_bytes: List[Lis
         cols.append(lens)
         lens_c = lens.clamp(min=0)
         excl = torch.cumsum(lens_c, 0) - lens_c
-        by = torch.tensor(send_bytes[lf.sidx], dtype=torch.int64, device=dev)
+        by = _h2d(send_bytes[lf.sidx], torch.int64, dev)
         dstart = torch.cumsum(by, 0) - by
         offs_cols.append(excl - dstart[sdest] if n else excl)
         total = int(sum(send_bytes[lf.sidx]))
@@ -230,9 +230,9 @@ def unpack_torch(names, spec, meta, mat, arenas, row_prefix, src_base, byte_base
     nprim = sum(1 for m in meta if m[0] == "prim")
     dev = device
     r = torch.arange(n_out, dtype=torch.int64, device=dev)
-    rp = torch.tensor(row_prefix, dtype=torch.int64, device=dev)
+    rp = _h2d(row_prefix, torch.int64, dev)
     k = (torch.searchsorted(rp[1:W], r, right=True) if W > 1 else torch.zeros_like(r))
-    src = torch.tensor(src_base, dtype=torch.int64, device=dev)[k] + r - rp[k]
+    src = _h2d(src_base, torch.int64, dev)[k] + r - rp[k]
     rows = mat[src] if n_out else torch.empty((0, mat.shape[1]), dtype=torch.int64, device=dev)
     mask0 = nprim + 2 * nstr
     out = {}
@@ -251,7 +251,7 @@ def unpack_torch(names, spec, meta, mat, arenas, row_prefix, src_base, byte_base
                 d = d.to(tdt)
             out[li] = PrimColumn(dtype, d, valid)
         elif kind == "str":
-            bb = torch.tensor(byte_base[sidx], dtype=torch.int64, device=dev)[k]
+            bb = _h2d(byte_base[sidx], torch.int64, dev)[k]
             starts = bb + rows[:, nprim + nstr + sidx]
             out[li] = stype(arenas[sidx], starts, rows[:, mcol].to(torch.int32), valid, cdt)
         else:
@@ -510,3 +510,8 @@ def unpack(names, spec, meta, mat, arenas, row_prefix, src_base, byte_base, n_ou
     if not force_torch and torch.device(device).type == "cuda" and len(meta) <= _limits()[4]:
         return unpack_device(names, spec, meta, mat, arenas, row_prefix, src_base, byte_base, n_out, device)
     return unpack_torch(names, spec, meta, mat, arenas, row_prefix, src_base, byte_base, n_out, device)
+
+
+def _h2d(data, dtype, device):
+    from ..ops.native import h2d
+    return h2d(data, dtype, device)

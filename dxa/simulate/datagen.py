@@ -111,10 +111,10 @@ class GenProgram:
         if key in cache:
             return cache[key]
         raw = b"".join(struct.pack("<iiiiqq", c, a, b, 0, x, y) for c, a, b, x, y in self.ops)
-        ops = torch.frombuffer(bytearray(raw or b"\0" * 32), dtype=torch.uint8).to(device)
+        ops = N.h2d(raw or b"\0" * 32, torch.uint8, device)
         pad = b"\0" * (-len(self.pool) % 8 + 16)
-        pool = torch.frombuffer(bytearray(bytes(self.pool) + pad), dtype=torch.uint8).to(device)
-        tab = torch.tensor([v for p in self.table for v in p] or [0, 0], dtype=torch.int32, device=device)
+        pool = N.h2d(bytes(self.pool) + pad, torch.uint8, device)
+        tab = N.h2d([v for p in self.table for v in p] or [0, 0], torch.int32, device)
         cache[key] = (ops, pool, tab)
         self._dev = cache
         return cache[key]

@@ -7,3 +7,5 @@ for f in full window; do
   timeout -k 10 300 python tools/host_profile.py --flow $f > gpurun_out/r4b/hprof_$f.txt 2>gpurun_out/r4b/hprof_$f.err || { tail -20 gpurun_out/r4b/hprof_$f.err; exit 1; }
   echo "$f profiled"
 done
+timeout -k 10 120 python tools/gpu/h2d_sync_probe.py > gpurun_out/r4b/h2d_probe.txt 2>&1 || { tail -20 gpurun_out/r4b/h2d_probe.txt; exit 1; }
+cat gpurun_out/r4b/h2d_probe.txt
