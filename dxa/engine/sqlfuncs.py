@@ -497,6 +497,10 @@ def _f_array_contains(e, scope, ctx, subst):
     return bool_col(acc, arr.valid)
 
 
+def _nan_key(x):
+    return (isinstance(x, float) and x != x, x if not (isinstance(x, float) and x != x) else 0.0)
+
+
 def _host_array_fn(fn, elem_type_of=None, scalar_type=None):
     """Array function evaluated per row on the host: fn(list, *args) → list (array result) or value."""
     def f(e, scope, ctx, subst):
@@ -1231,13 +1235,16 @@ def _register():
     reg("array_contains", _f_array_contains)
     reg("array_join", _host_array_fn(lambda l, sep, nr=None: str(sep).join(
         str(x) if x is not None else str(nr) for x in l if x is not None or nr is not None), scalar_type="string"))
-    reg("array_max", _host_array_fn(lambda l: max((x for x in l if x is not None), default=None),
+    # Spark orders NaN above every other double
+    reg("array_max", _host_array_fn(lambda l: max((x for x in l if x is not None), default=None, key=_nan_key),
                                     scalar_type="elem"))
-    reg("array_min", _host_array_fn(lambda l: min((x for x in l if x is not None), default=None),
+    reg("array_min", _host_array_fn(lambda l: min((x for x in l if x is not None), default=None, key=_nan_key),
                                     scalar_type="elem"))
-    reg("sort_array", _host_array_fn(lambda l, asc=True: sorted(
-        l, key=lambda x: (x is not None, x) if bool(asc) else (x is None, x), reverse=not bool(asc))))
-    reg("array_sort", _host_array_fn(lambda l: sorted((x for x in l if x is not None)) + [x for x in l if x is None]))
+    reg("sort_array", _host_array_fn(lambda l, asc=True: (
+        [x for x in l if x is None] + sorted((x for x in l if x is not None), key=_nan_key)) if bool(asc) else
+        (sorted((x for x in l if x is not None), key=_nan_key, reverse=True) + [x for x in l if x is None])))
+    reg("array_sort", _host_array_fn(lambda l: sorted((x for x in l if x is not None), key=_nan_key) +
+                                     [x for x in l if x is None]))
     reg("array_distinct", _host_array_fn(lambda l: list(dict.fromkeys(l))))
     reg("array_position", _host_array_fn(lambda l, v: next((i + 1 for i, x in enumerate(l) if x == v), 0),
                                          scalar_type="long"))
@@ -1711,9 +1718,52 @@ def _levenshtein_fn(e, scope, ctx, subst):
     return _host_string_fn(_levenshtein, "int")(e, scope, ctx, subst)
 
 
+def _octets(mult):
+    """octet_length / bit_length: byte counts of the UTF-8 text (the lengths column itself on the device)."""
+    host = _host_string_fn(lambda s: mult * len(str(s).encode("utf-8")), "int")
+
+    def f(e, scope, ctx, subst):
+        args = _args(e, scope, ctx, subst)
+        if len(args) == 1 and isinstance(args[0], StrColumn):
+            return PrimColumn("int", args[0].lens.to(torch.int32) * mult, args[0].valid)
+        return host(e, scope, ctx, subst)
+    return f
+
+
+_CHR_TABLE = None
+
+
+def _f_chr(e, scope, ctx, subst):
+    """chr(n) / char(n): the character n mod 256 (Latin-1 code point, UTF-8 encoded); '' for n < 0 — a view into
+    a 256-entry table arena, no per-row host work."""
+    global _CHR_TABLE
+    (a,) = _args(e, scope, ctx, subst)
+    if isinstance(a, ConstColumn) or not isinstance(a, PrimColumn):
+        return _host_string_fn(lambda x: chr(int(x) % 256) if int(x) >= 0 else "")(e, scope, ctx, subst)
+    dev = a.device
+    if _CHR_TABLE is None or _CHR_TABLE[0].device != dev:
+        enc = [chr(c).encode("utf-8") for c in range(256)]
+        starts, pos = [], 0
+        for b in enc:
+            starts.append(pos)
+            pos += len(b)
+        from ..ops.native import h2d
+        _CHR_TABLE = (h2d(b"".join(enc) + b"\0" * 16, torch.uint8, dev), h2d(starts, torch.int64, dev),
+                      h2d([len(b) for b in enc], torch.int32, dev))
+    arena, st, ln = _CHR_TABLE
+    x = a.data.to(torch.int64)
+    code = torch.remainder(x, 256)
+    neg = x < 0
+    return StrColumn(arena, st[code], torch.where(neg, torch.zeros_like(ln[code]), ln[code]), a.valid)
+
+
 def _register_device_strings():
     from ..ops import strfuncs as SF
     reg = register_function
+    reg("octet_length", _octets(1))
+    reg("bit_length", _octets(8))
+    reg("chr", _f_chr)
+    reg("char", _f_chr)
     reg("lpad", _device_string_fn("lpad", lambda c, l, p=" ": SF.pad(c, int(l), str(p), True), _lpad_host))
     reg("rpad", _device_string_fn("rpad", lambda c, l, p=" ": SF.pad(c, int(l), str(p), False), _rpad_host))
     reg("reverse", _device_string_fn("reverse", SF.reverse, lambda s: str(s)[::-1]))
@@ -1734,3 +1784,8 @@ _register_device_strings()
 def _h2d(data, dtype, device):
     from ..ops.native import h2d
     return h2d(data, dtype, device)
+
+
+# array built-ins as slot-matrix tensor operations (dxa/engine/arrayfuncs.py registers itself on import, with the
+# row-wise functions above as its fallback)
+from . import arrayfuncs  # noqa: E402,F401

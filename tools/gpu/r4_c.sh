@@ -1,7 +1,7 @@
 # Round 4: device string built-ins + non-blocking uploads; window/full/groupby benches
 set -o pipefail
 mkdir -p gpurun_out/r4c
-timeout -k 10 600 python -u -m pytest tests/test_strfuncs.py tests/test_packing.py -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r4c/tests.log 2>&1 || { tail -60 gpurun_out/r4c/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_strfuncs.py tests/test_arrayfuncs.py tests/test_packing.py -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r4c/tests.log 2>&1 || { tail -60 gpurun_out/r4c/tests.log; exit 1; }
 tail -1 gpurun_out/r4c/tests.log
 for f in window full groupby; do
   timeout -k 10 300 python bench.py --flow $f --steps 30 > gpurun_out/r4c/bench_$f.log 2>&1 || { tail -20 gpurun_out/r4c/bench_$f.log; exit 1; }
