@@ -18,6 +18,7 @@ import datetime as _dt
 import json
 import logging
 import os
+import re
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -183,7 +184,7 @@ class Processor:
             return None
         if any(re.search(r"\bRaw\s*\.\s*\*", t) for t in texts):
             # Raw.* expands every field into the projected table: keep all leaves unless SQL proves otherwise
-            return None
+            return self._raw_paths_read_by_sql(texts)
         keep = set()
         for t in texts:
             for m in re.finditer(r"\bRaw((?:\s*\.\s*[A-Za-z_`][A-Za-z0-9_`]*)+)", t):
@@ -191,6 +192,58 @@ class Processor:
                 keep.add(parts)
             if re.search(r"\bRaw\b(?!\s*\.)", t):
                 return None
+        return keep or None
+
+    def _raw_paths_read_by_sql(self, projection_texts) -> Optional[set]:
+        """Column pruning through ``Raw.*``: the Raw leaves any live transform statement can read.
+
+        With ``Raw.*`` every JSON field becomes a column of ``DataXProcessedInput`` — but when no live statement
+        selects ``*`` (nor any output / hook sees the projected table whole), the only columns that can reach an
+        output are the ones statements name.  Every identifier of the live statements and projection lines is
+        matched against the raw schema's paths (at any offset, so ``Raw.a.b``, ``a.b`` and ``t.a.b`` all name
+        ``a.b``; a struct named whole keeps its subtree); the parser then extracts only those fields and windows
+        retain only those columns.  Over-keeping is harmless; anything the analysis cannot see keeps everything."""
+        if self.transform is None or self.pre_projection is not None or self.normalizer is not None:
+            return None
+        from ..sql import ast as A
+        from ..sql.parser import parse_expression, parse_query
+        base = f"{S.NAME_PREFIX}ProcessedInput".lower()
+        if any(op.name.lower().startswith(base) for op in self.outputs):
+            return None
+        live = self._live_statements()
+        idents = []
+        for k, c in enumerate(self.transform.commands):
+            if c.command_type == COMMAND_COMMAND or (live is not None and k not in live):
+                continue
+            try:
+                q = parse_query(c.text)
+            except Exception:  # noqa: BLE001 — statements the parser rejects fail later, loudly
+                return None
+            nodes = list(_ast_nodes(q))
+            if any(isinstance(n, A.Star) for n in nodes):
+                return None
+            idents += [n.parts for n in nodes if isinstance(n, A.Ident)]
+        for t in projection_texts:
+            if re.match(r"^\s*Raw\s*\.\s*\*\s*$", t):
+                continue
+            try:
+                e = parse_expression(re.sub(r"\s+AS\s+`?[A-Za-z_][A-Za-z0-9_]*`?\s*$", "", t, flags=re.I))
+            except Exception:  # noqa: BLE001
+                return None
+            idents += [n.parts for n in A.walk(e) if isinstance(n, A.Ident)]
+        tree = _schema_tree(self.raw_schema)
+        keep = set()
+        for parts in idents:
+            low = [p.lower() for p in parts]
+            for i in range(len(low)):
+                node, path = tree, ()
+                for p in low[i:]:
+                    if node is None or p not in node:
+                        break
+                    name, node = node[p]
+                    path += (name,)
+                if path:
+                    keep.add(path)
         return keep or None
 
     # ------------------------------------------------------------------------------------------------------------
@@ -701,3 +754,30 @@ def _fmt_ts(us: int) -> str:
 def _h2d(data, dtype, device):
     from ..ops.native import h2d
     return h2d(data, dtype, device)
+
+
+def _schema_tree(st: StructType):
+    """lower-case field name → (field name, subtree or None) for a struct schema."""
+    out = {}
+    for f in st.fields:
+        out[f.name.lower()] = (f.name, _schema_tree(f.dtype) if isinstance(f.dtype, StructType) else None)
+    return out
+
+
+def _ast_nodes(obj):
+    """Every AST node (expressions, select items, relations) reachable from a parsed query."""
+    from dataclasses import fields, is_dataclass
+    stack = [obj]
+    seen = set()
+    while stack:
+        o = stack.pop()
+        if id(o) in seen:
+            continue
+        seen.add(id(o))
+        if isinstance(o, (list, tuple)):
+            stack.extend(o)
+            continue
+        if is_dataclass(o):
+            yield o
+            for f in fields(o):
+                stack.append(getattr(o, f.name))
