@@ -197,22 +197,30 @@ class Processor:
     def _raw_paths_read_by_sql(self, projection_texts) -> Optional[set]:
         """Column pruning through ``Raw.*``: the Raw leaves any live transform statement can read.
 
-        With ``Raw.*`` every JSON field becomes a column of ``DataXProcessedInput`` — but when no live statement
-        selects ``*`` (nor any output / hook sees the projected table whole), the only columns that can reach an
-        output are the ones statements name.  Every identifier of the live statements and projection lines is
-        matched against the raw schema's paths (at any offset, so ``Raw.a.b``, ``a.b`` and ``t.a.b`` all name
-        ``a.b``; a struct named whole keeps its subtree); the parser then extracts only those fields and windows
-        retain only those columns.  Over-keeping is harmless; anything the analysis cannot see keeps everything."""
+        With ``Raw.*`` every JSON field becomes a column of ``DataXProcessedInput``, but only the columns some
+        consumer reads can reach an output.  Demand runs backwards over the live statements: an output or an
+        accumulator needs all of its view; a statement needs, from every relation it reads, the identifiers it
+        names — plus, where it selects ``*``, whatever its own consumers need (so an alert view ``SELECT *, … FROM
+        DataXProcessedInput WHERE …`` read only by ``SELECT DISTINCT <constants> FROM it`` adds nothing).  The
+        demand on the input views is matched against the raw schema's paths (at any offset: ``Raw.a.b``, ``a.b``,
+        ``t.a.b`` all name ``a.b``; a struct named whole keeps its subtree); the parser then extracts only those
+        fields and windows retain only those columns.  Over-keeping is harmless; anything the analysis cannot see
+        (``*`` reaching an output, hooks, unparsable text) keeps everything."""
         if self.transform is None or self.pre_projection is not None or self.normalizer is not None:
             return None
         from ..sql import ast as A
         from ..sql.parser import parse_expression, parse_query
         base = f"{S.NAME_PREFIX}ProcessedInput".lower()
-        if any(op.name.lower().startswith(base) for op in self.outputs):
-            return None
+        ALL = None
+        demand: Dict[str, Optional[set]] = {}
+        for op in self.outputs:
+            demand[op.name.lower()] = ALL
+        for n in self.state_tables:
+            demand[n.lower()] = ALL
         live = self._live_statements()
-        idents = []
-        for k, c in enumerate(self.transform.commands):
+        cmds = self.transform.commands
+        for k in range(len(cmds) - 1, -1, -1):
+            c = cmds[k]
             if c.command_type == COMMAND_COMMAND or (live is not None and k not in live):
                 continue
             try:
@@ -220,9 +228,21 @@ class Processor:
             except Exception:  # noqa: BLE001 — statements the parser rejects fail later, loudly
                 return None
             nodes = list(_ast_nodes(q))
-            if any(isinstance(n, A.Star) for n in nodes):
-                return None
-            idents += [n.parts for n in nodes if isinstance(n, A.Ident)]
+            own = demand.get(c.name.lower(), set())
+            ids = {tuple(p.lower() for p in n.parts) for n in nodes if isinstance(n, A.Ident)}
+            star = any(isinstance(n, A.Star) for n in nodes)
+            need = ALL if (star and own is ALL) else (ids | (own if star else set()))
+            for r in {n.name.lower() for n in nodes if isinstance(n, A.TableRef)}:
+                if r == c.name.lower():
+                    continue
+                cur = demand.get(r, set())
+                demand[r] = ALL if (cur is ALL or need is ALL) else cur | need
+        idents = []
+        for name, d in demand.items():
+            if name == base or name.startswith(base + "_") or name in {w.lower() for w in self.windows.windows}:
+                if d is ALL:
+                    return None
+                idents += list(d)
         for t in projection_texts:
             if re.match(r"^\s*Raw\s*\.\s*\*\s*$", t):
                 continue

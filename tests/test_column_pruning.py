@@ -34,7 +34,7 @@ def _run(variant, prune, tmp_path):
 
 
 def test_pruned_outputs_equal_unpruned(tmp_path):
-    for variant in ("groupby", "window"):
+    for variant in ("groupby", "window", "full"):
         p1, a = _run(variant, True, tmp_path)
         p0, b = _run(variant, False, tmp_path)
         assert a == b, variant
