@@ -175,6 +175,9 @@ class PrimColumn(Column):
         return PrimColumn(self.dtype, self.data.to(device), None if self.valid is None else self.valid.to(device))
 
     def to_pylist(self):
+        from .decimal import is_decimal, to_python
+        if is_decimal(self.dtype):
+            return to_python(self)
         vals = self.data.cpu().tolist()
         valid = self.valid.cpu().tolist() if self.valid is not None else None
         if valid is not None:
@@ -289,6 +292,9 @@ class ConstColumn(Column):
 
 
 def _const_prim(value, dtype, n, device):
+    from .decimal import const_column, is_decimal
+    if is_decimal(dtype):
+        return const_column(value, dtype, n, device)
     tdt = TORCH_DTYPE.get(dtype, torch.float64)
     if value is None:
         return PrimColumn(dtype, torch.zeros(n, dtype=tdt, device=device), torch.zeros(n, dtype=torch.bool,
@@ -464,6 +470,9 @@ def column_from_pylist(values: Sequence[Any], dtype: Any, device="cpu") -> Colum
                                    device, dtype)
     if dtype == "null":
         return ConstColumn(None, "null", n, device)
+    from .decimal import from_python, is_decimal
+    if is_decimal(dtype):
+        return from_python(values, dtype, device)
     tdt = TORCH_DTYPE[dtype]
     data = _h2d([_py_to_storage(v, dtype) for v in values], tdt, device)
     valid = None

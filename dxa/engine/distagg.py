@@ -16,7 +16,9 @@ from .. import parallel as P
 from ..ops import groupby as G
 from ..ops.hashing import hash_columns
 from ..sql import ast as A
+from . import decimal as Dec
 from .column import ConstColumn, PrimColumn, Table, materialize
+from .decimal import is_decimal
 
 DECOMPOSABLE = {"count", "sum", "min", "max", "avg", "mean", "first", "last", "first_value", "last_value",
                 "stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std", "count_if",
@@ -51,6 +53,14 @@ def _partials(call: A.Call, scope, ctx) -> List[Tuple[str, Optional[PrimColumn],
     if name in ("first", "first_value", "last", "last_value"):
         f = "first" if name.startswith("first") else "last"
         return [("v", arg, f, f)]
+    if is_decimal(arg.dtype):
+        t = arg.dtype
+        if name == "sum":          # partial sums are already of SUM's result type; merging keeps that type
+            return [("v", arg, "sum", "sum_keep"), ("cnt", arg, "count", "sum")]
+        if name in ("avg", "mean"):  # exact: decimal sum + count, divided once at the end (HALF_UP)
+            return [(f"davg_{t.precision}_{t.scale}", arg, "sum", "sum_keep"), ("cnt", arg, "count", "sum")]
+        if name not in ("min", "max"):
+            arg = Dec.to_double(arg)
     if name in ("sum", "min", "max"):
         return [("v", arg, name, name), ("cnt", arg, "count", "sum")]
     if name in ("avg", "mean"):
@@ -72,6 +82,10 @@ def _finish(call: A.Call, merged: Dict[str, PrimColumn]) -> PrimColumn:
         if "cnt" in merged:
             return v.with_valid(merged["cnt"].data > 0)
         return v
+    davg = next((k for k in merged if k.startswith("davg_")), None)
+    if davg is not None:
+        _, p, sc = davg.split("_")
+        return Dec.avg_from_sum(merged[davg], merged["cnt"], Dec.DecimalType(int(p), int(sc)))
     if set(merged) == {"cnt"}:
         c = merged["cnt"]
         return PrimColumn("long", c.data, None)
@@ -190,6 +204,8 @@ def distributed_aggregate(gexprs, keys, aggs: Dict, scope, ctx):
 
 
 def _empty_merge(c, op, ng, dev):
+    if is_decimal(c.dtype):
+        return Dec.const_column(0 if op in ("sum", "sum_keep") else None, c.dtype, ng, dev)
     if op == "sum":
         return PrimColumn(c.dtype, torch.zeros(ng, dtype=c.data.dtype if hasattr(c, "data") else torch.int64,
                                                device=dev))

@@ -9,6 +9,7 @@ integral ``%`` keeps the dividend's sign, WHERE treats null as false.
 """
 from __future__ import annotations
 
+import contextvars
 import json
 import math
 import re
@@ -23,6 +24,8 @@ from . import jit as _jit_mod
 from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, LazyColumns, PrimColumn, StrColumn,
                      StructColumn, TORCH_DTYPE, and_valid, column_from_pylist, concat_columns, materialize, strings_from_pylist)
 from .types import (ArrayType, MapType, StructType, common_type, is_integral, is_nested, is_numeric)
+from . import decimal as D
+from .decimal import is_decimal
 
 AGG_FUNCS = {"count", "sum", "avg", "mean", "min", "max", "first", "last", "first_value", "last_value", "stddev",
              "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std", "collect_list", "collect_set",
@@ -276,10 +279,27 @@ def _coerce_const_for(col_other: Column, const: ConstColumn) -> ConstColumn:
 # evaluator
 # ---------------------------------------------------------------------------------------------------------------
 
+# Built-ins that take decimal(p,s) arguments as they are; every other function sees its decimal arguments as
+# doubles (Spark's implicit cast for functions typed on DoubleType: ImplicitTypeCasts) — see _call / evaluate.
+_DECIMAL_AWARE = frozenset({"coalesce", "if", "nvl", "ifnull", "nullif", "nvl2", "to_json", "named_struct", "struct",
+                            "array", "map", "concat", "concat_ws", "isnull", "isnotnull", "string", "abs",
+                            "negative", "positive"})
+
+_DEMOTE: "contextvars.ContextVar" = contextvars.ContextVar("dxa_decimal_demote", default=None)
+
+
 def evaluate(e: A.Expr, scope: Scope, ctx: EvalContext, subst: Optional[Dict] = None, _jit: bool = True) -> Column:
     """Evaluate ``e`` over every row of ``scope``.  ``subst`` maps expression keys to precomputed columns
     (aggregate results).  Scalar operator trees over large device batches run as one generated kernel
     (``jit.py``); ``_jit=False`` evaluates this node with tensor ops (its children may still fuse)."""
+    r = _evaluate_node(e, scope, ctx, subst, _jit)
+    dem = _DEMOTE.get()
+    if dem is not None and id(e) in dem and is_decimal(r.dtype):
+        return _dec_to_double(r)
+    return r
+
+
+def _evaluate_node(e: A.Expr, scope: Scope, ctx: EvalContext, subst: Optional[Dict], _jit: bool) -> Column:
     if subst:
         k = e.key()
         if k in subst:
@@ -313,6 +333,8 @@ def evaluate(e: A.Expr, scope: Scope, ctx: EvalContext, subst: Optional[Dict] = 
         if e.op == "-":
             if isinstance(v, ConstColumn):
                 return ConstColumn(None if v.value is None else -v.value, v.dtype, n, dev)
+            if is_decimal(v.dtype):
+                return D.negate(v)
             return PrimColumn(v.dtype, -v.data, v.valid)
         if e.op == "~":
             if isinstance(v, ConstColumn):
@@ -396,9 +418,62 @@ def _logic(op: str, a: Column, b: Column, n, dev) -> Column:
     return bool_col(t, t | f)
 
 
+def _dec_operands(a: Column, b: Column):
+    """Spark DecimalPrecision coercion for a binary operator with a decimal side: ('double', a, b) when the other
+    side is fractional (or a string / anything non-integral), else ('decimal', a, b) with integral sides widened to
+    decimal(10,0) / decimal(20,0)."""
+    other = b if is_decimal(a.dtype) else a
+    if not (is_decimal(other.dtype) or other.dtype in ("int", "long", "null")):
+        return "double", _dec_to_double(a), _dec_to_double(b)
+    return "decimal", _to_dec(a), _to_dec(b)
+
+
+def _dec_to_double(c: Column) -> Column:
+    if not is_decimal(c.dtype):
+        return c
+    if isinstance(c, ConstColumn):
+        return ConstColumn(None if c.value is None else float(c.value), "double", c.length, c.device)
+    return D.to_double(c)
+
+
+def _to_dec(c: Column) -> Column:
+    if is_decimal(c.dtype) or c.dtype == "null":
+        return c
+    if isinstance(c, ConstColumn):
+        # Spark 2.4 DecimalPrecision (literalPickMinimumPrecision): an integral literal next to a decimal takes the
+        # tightest decimal(digits, 0) — DecimalType.fromLiteral
+        t = D.DecimalType(max(1, len(str(abs(int(c.value))))), 0) if c.value is not None else D.of_integral(c.dtype)
+        return ConstColumn(D.quantize(c.value, t), t, c.length, c.device)
+    t = D.of_integral(c.dtype)
+    return D.from_integral(c, t)
+
+
+def _dec_arith(op: str, a: Column, b: Column, n, dev) -> Column:
+    kind, a, b = _dec_operands(a, b)
+    if kind == "double":
+        return _arith(op, a, b, n, dev)
+    if op not in ("+", "-", "*", "/", "%"):
+        if op == "div":
+            return _arith(op, cast_column(a, "long") if not isinstance(a, ConstColumn) else
+                          ConstColumn(D.scalar_to(a.value, a.dtype, "long"), "long", n, dev),
+                          cast_column(b, "long") if not isinstance(b, ConstColumn) else
+                          ConstColumn(D.scalar_to(b.value, b.dtype, "long"), "long", n, dev), n, dev)
+        raise EvalError(f"cannot apply {op} to {a.dtype} and {b.dtype}")
+    at = a.dtype if is_decimal(a.dtype) else b.dtype
+    bt = b.dtype if is_decimal(b.dtype) else a.dtype
+    rt = D.result_type(op, at, bt)
+    if (isinstance(a, ConstColumn) and a.value is None) or (isinstance(b, ConstColumn) and b.value is None):
+        return ConstColumn(None, rt, n, dev)
+    if _all_const(a, b):
+        return ConstColumn(D.scalar_op(op, a.value, b.value, rt), rt, n, dev)
+    return D.arith(op, as_prim(a), as_prim(b), at, bt)
+
+
 def _arith(op: str, a: Column, b: Column, n, dev) -> Column:
     if a.dtype == "timestamp" or b.dtype == "timestamp":
         return _ts_arith(op, a, b, n, dev)
+    if is_decimal(a.dtype) or is_decimal(b.dtype):
+        return _dec_arith(op, a, b, n, dev)
     rt = common_type(a.dtype if a.dtype != "interval" else "long", b.dtype if b.dtype != "interval" else "long")
     if op == "/":
         rt = "double"
@@ -502,6 +577,10 @@ def _compare(op: str, a: Column, b: Column, n, dev) -> Column:
         a = _coerce_const_for(b, a)
     if (isinstance(a, ConstColumn) and a.value is None) or (isinstance(b, ConstColumn) and b.value is None):
         return ConstColumn(None, "boolean", n, dev)
+    if is_decimal(a.dtype) or is_decimal(b.dtype):
+        kind, a, b = _dec_operands(a, b)
+        if kind == "decimal" and not _all_const(a, b):
+            return bool_col(D.compare_lanes(op, as_prim(a), as_prim(b), a.dtype, b.dtype), _result_valid(a, b))
     if _all_const(a, b):
         x, y = a.value, b.value
         try:
@@ -666,6 +745,10 @@ def _like_to_regex(p: str) -> str:
 
 def choose(branch: torch.Tensor, options: List[Column], n, dev) -> Column:
     """Row-wise selection: result[i] = options[branch[i]][i] (branch == len(options) → null)."""
+    if any(is_decimal(o.dtype) for o in options):
+        target = _unify_type(options)
+        if is_decimal(target):
+            return _choose_decimal(branch, options, target, n, dev)
     if all(isinstance(o, ConstColumn) for o in options):
         vals = [o.value for o in options] + [None]
         dtype = next((o.dtype for o in options if o.value is not None), options[0].dtype)
@@ -711,6 +794,22 @@ def choose(branch: torch.Tensor, options: List[Column], n, dev) -> Column:
                           for o in opts])
     idx = branch.to(torch.int64) * n + torch.arange(n, device=dev)
     return big.take(idx)
+
+
+def _choose_decimal(branch, options, target, n, dev):
+    opts = []
+    for o in options + [ConstColumn(None, target, n, dev)]:
+        if isinstance(o, ConstColumn):
+            o = ConstColumn(None if o.value is None else _cast_value(o.value, o.dtype, target), target, n, dev)
+            o = o.materialize()
+        elif o.dtype != target:
+            o = cast_column(o, target)
+        opts.append(o)
+    b = branch.to(torch.int64)
+    data = torch.stack([o.data for o in opts])
+    idx = b.view(1, n, 1).expand(1, n, 2) if data.dim() == 3 else b.view(1, n)
+    valid = torch.stack([o.valid_mask() for o in opts]).gather(0, b.view(1, n)).squeeze(0)
+    return PrimColumn(target, data.gather(0, idx).squeeze(0), None if bool(valid.all()) else valid)
 
 
 def _unify_type(cols):
@@ -777,6 +876,8 @@ def _concat(parts: List[Column], n, dev):
 
 def _const_str(c: ConstColumn) -> str:
     v = c.value
+    if is_decimal(c.dtype):
+        return D.render(v, c.dtype.scale)
     if isinstance(v, bool):
         return "true" if v else "false"
     if isinstance(v, float):
@@ -797,6 +898,10 @@ def cast_column(col: Column, to: str) -> Column:
         return col
     if isinstance(col, ConstColumn):
         return ConstColumn(_cast_value(col.value, col.dtype, to), to, n, dev)
+    if is_decimal(to) or is_decimal(col.dtype):
+        r = _cast_decimal(col, to)
+        if r is not None:
+            return r
     if to == "string":
         if isinstance(col, PrimColumn):
             if col.dtype in ("int", "long"):
@@ -873,6 +978,36 @@ def cast_column(col: Column, to: str) -> Column:
     raise EvalError(f"cannot cast {col.dtype} to {to}")
 
 
+def _cast_decimal(col: Column, to) -> Optional[Column]:
+    """Casts into and out of decimal(p,s) (Spark Cast: HALF_UP to the scale, NULL on overflow; decimal → integral
+    truncates toward zero)."""
+    n, dev = col.length, col.device
+    if is_decimal(to):
+        if is_decimal(col.dtype):
+            return D.change_type(col, to)
+        if col.dtype in ("int", "long", "boolean") and isinstance(col, PrimColumn):
+            return D.from_integral(col, to)
+        if col.dtype in ("double", "float") and isinstance(col, PrimColumn):
+            return D.from_double(col, to)
+        if col.dtype == "timestamp" and isinstance(col, PrimColumn):
+            return D.from_double(PrimColumn("double", col.data.to(torch.float64) / 1e6, col.valid), to)
+        if col.dtype == "string" and isinstance(col, StrColumn):
+            return D.from_text(col, to)
+        raise EvalError(f"cannot cast {col.dtype} to {to}")
+    if to in ("int", "long"):
+        return D.to_integral(col, to)
+    if to in ("double", "float"):
+        return D.to_double(col)
+    if to == "boolean":
+        return D.to_boolean(col)
+    if to == "string":
+        return D.to_text_column(col)
+    if to == "timestamp":
+        d = D.to_double(col)
+        return PrimColumn("timestamp", (d.data * 1e6).to(torch.int64), d.valid)
+    return None
+
+
 def _storage_of(v, dtype):
     from .column import datetime_to_us
     import datetime as dt
@@ -891,6 +1026,14 @@ _DBL_STR = re.compile(r"^[+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?$")
 def _cast_value(v, frm, to):
     if v is None:
         return None
+    if is_decimal(to):
+        if frm == "timestamp":
+            v = v / 1e6
+        return D.cast_scalar(v, frm, to)
+    if is_decimal(frm):
+        if to == "timestamp":
+            return int(float(v) * 1_000_000)
+        return D.scalar_to(v, frm, to)
     try:
         if to == "string":
             if isinstance(v, bool):
@@ -969,7 +1112,11 @@ def _call(e: A.Call, scope: Scope, ctx: EvalContext, subst):
     fn = _FUNCS.get(name)
     if fn is None:
         raise EvalError(f"undefined function {name}()")
-    return fn(e, scope, ctx, subst)
+    tok = _DEMOTE.set(None if name in _DECIMAL_AWARE else frozenset(id(a) for a in e.args))
+    try:
+        return fn(e, scope, ctx, subst)
+    finally:
+        _DEMOTE.reset(tok)
 
 
 def _subquery(e: A.SubqueryExpr, scope: Scope, ctx: EvalContext, subst) -> Column:
@@ -1249,6 +1396,15 @@ def _f_size(e, scope, ctx, subst):
     return column_from_pylist([-1 if v is None else len(v) for v in vals], "int", dev)
 
 
+def _f_abs(e, scope, ctx, subst):
+    (a,) = _args(e, scope, ctx, subst)
+    if is_decimal(a.dtype):
+        if isinstance(a, ConstColumn):
+            return ConstColumn(None if a.value is None else abs(a.value), a.dtype, a.length, a.device)
+        return D.absolute(a)
+    return _ABS_NUM(e, scope, ctx, subst)
+
+
 def _unary_num(fn, out_type=None):
     def f(e, scope, ctx, subst):
         n, dev = scope.length, scope.device
@@ -1270,6 +1426,9 @@ def _unary_num(fn, out_type=None):
             r = r.to(torch.int64)
         return PrimColumn(rt, r, a.valid)
     return f
+
+
+_ABS_NUM = _unary_num(torch.abs)
 
 
 def _f_round(e, scope, ctx, subst):
@@ -1531,7 +1690,7 @@ _FUNCS: Dict[str, Callable] = {
     "nullif": _f_nullif, "nvl2": _f_nvl2, "isnull": _f_isnull(False), "isnotnull": _f_isnull(True),
     "map": _f_map, "struct": _f_struct, "named_struct": _f_named_struct, "array": _f_array,
     "filternull": _f_filternull, "size": _f_size, "cardinality": _f_size, "element_at": _f_element_at,
-    "abs": _unary_num(torch.abs), "floor": _unary_num(torch.floor, "long"), "ceil": _unary_num(torch.ceil, "long"),
+    "abs": _f_abs, "floor": _unary_num(torch.floor, "long"), "ceil": _unary_num(torch.ceil, "long"),
     "ceiling": _unary_num(torch.ceil, "long"), "sqrt": _unary_num(torch.sqrt, "double"),
     "exp": _unary_num(torch.exp, "double"), "ln": _unary_num(torch.log, "double"),
     "log10": _unary_num(torch.log10, "double"), "log2": _unary_num(torch.log2, "double"),

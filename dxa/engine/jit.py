@@ -30,6 +30,7 @@ import torch
 
 from ..sql import ast as A
 from .column import Column, ConstColumn, PrimColumn
+from .decimal import is_decimal
 from .types import common_type
 
 NUMERIC = {"int", "long", "double", "float", "decimal"}
@@ -107,6 +108,10 @@ class _Gen:
                 return R("true" if col.value else "false", "true", "boolean", False, const=col, col=col)
             if dt in NUMERIC | INTEGRAL_STORAGE:
                 return R(_lit(col.value, dt), "true", dt, False, const=col, col=col)
+            if is_decimal(dt):
+                # a decimal literal fuses only next to a double (Spark compares / computes that pair in double):
+                # see _decimal_pair
+                return R(_lit(float(col.value), "double"), "true", dt, False, const=col, col=col)
             if dt == "string":
                 return R("0", "true", "string", False, const=col, col=col)      # only usable after coercion
             raise NotFusible(dt)
@@ -236,13 +241,30 @@ class _Gen:
                 raise NotFusible("string literal vs computed value")
         return a, b
 
+    @staticmethod
+    def _decimal_pair(a: R, b: R) -> Tuple[R, R]:
+        """decimal literal ⊕ double operand → both double (Spark DecimalPrecision: a double side wins); any other
+        decimal operand stays on the tensor evaluator (exact 64/128-bit lanes)."""
+        if not (is_decimal(a.dtype) or is_decimal(b.dtype)):
+            return a, b
+        out = []
+        for x, y in ((a, b), (b, a)):
+            if is_decimal(x.dtype) and x.const is not None and y.dtype in FRACTIONAL:
+                x = R(x.val, x.ok, "double", x.nullable, const=ConstColumn(float(x.const.value), "double",
+                                                                           x.const.length, x.const.device))
+            out.append(x)
+        a, b = out
+        if is_decimal(a.dtype) or is_decimal(b.dtype):
+            raise NotFusible("decimal")
+        return a, b
+
     def compare(self, op: str, a: R, b: R) -> R:
         if op == "<=>":
             eq = self.compare("=", a, b)
             self.nops += 1
             return R(self.tmp("bool", f"(({a.ok}) && ({b.ok}) && ({eq.ok}) && {eq.val}) || (!({a.ok}) && !({b.ok}))"),
                      "true", "boolean", False)
-        a, b = self._coerce(a, b)
+        a, b = self._decimal_pair(*self._coerce(a, b))
         okinds = NUMERIC | INTEGRAL_STORAGE | {"boolean", "null"}
         if a.dtype not in okinds or b.dtype not in okinds:
             raise NotFusible("compare types")
@@ -270,6 +292,7 @@ class _Gen:
         return self.tmp("bool", f"{a.ok} && {b.ok}")
 
     def arith(self, op: str, a: R, b: R) -> R:
+        a, b = self._decimal_pair(a, b)
         kinds = NUMERIC | {"null"}
         if a.dtype not in kinds or b.dtype not in kinds:
             raise NotFusible("arith types")           # timestamps, booleans, strings: tensor evaluator

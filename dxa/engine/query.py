@@ -587,8 +587,11 @@ def _join_rows(j: A.Join, catalog, ctx) -> Scope:
     if P.active() and (ldist != P.REPLICATED or rdist != P.REPLICATED):
         if ldist != P.REPLICATED and rdist != P.REPLICATED and lkeys:
             # co-partition both sides by the join-key hash (Spark's shuffle hash join)
-            left = _shuffle_scope(left, [_key_col(e, left, ctx) for e in lkeys])
-            right = _shuffle_scope(right, [_key_col(e, right, ctx) for e in rkeys], ref=left)
+            # (keys in the type both sides compare in, so equal keys hash alike: 3 vs 3.0, decimal(10,2) vs
+            # decimal(38,4))
+            lk0, rk0 = _coerce_keys([_key_col(e, left, ctx) for e in lkeys], [_key_col(e, right, ctx) for e in rkeys])
+            left = _shuffle_scope(left, lk0)
+            right = _shuffle_scope(right, rk0, ref=left)
             out_dist = P.HASHED
         elif ldist != P.REPLICATED and kind in ("inner", "left", "semi", "anti", "cross"):
             out_dist = ldist            # partitioned ⨝ replicated: rank-local

@@ -12,6 +12,7 @@ import json
 from typing import Any, List, Optional
 
 from . import functions as F
+from .decimal import is_decimal, render, to_text_values
 from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn, Table,
                      datetime_to_us)
 from .types import ArrayType, MapType, StructType
@@ -48,6 +49,8 @@ def _frag_values(col: Column) -> List[Optional[str]]:
                 for s, l, ok in zip(col.starts.cpu().tolist(), col.lens.cpu().tolist(), valid)]
     if isinstance(col, StrColumn):
         return [None if v is None else _jstr(v) for v in col.to_pylist()]
+    if isinstance(col, PrimColumn) and is_decimal(col.dtype):
+        return to_text_values(col)
     if isinstance(col, PrimColumn):
         valid = col.valid.cpu().tolist() if col.valid is not None else [True] * n
         data = col.data.cpu().tolist()
@@ -112,6 +115,8 @@ def _scalar_text(v, dtype, raw=True) -> str:
         return '"' + F.format_timestamp_us(v) + '"'
     if dtype == "date":
         return '"' + (_dt.date(1970, 1, 1) + _dt.timedelta(days=int(v))).isoformat() + '"'
+    if is_decimal(dtype):
+        return render(v, dtype.scale)
     if isinstance(v, float) or dtype in ("double", "float", "decimal"):
         return _double_text(float(v))
     if isinstance(v, int):

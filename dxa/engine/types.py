@@ -75,7 +75,12 @@ def type_str(t) -> str:
 
 
 def is_numeric(t) -> bool:
-    return isinstance(t, str) and t in NUMERIC
+    return isinstance(t, str) and (t in NUMERIC or _is_dec(t))
+
+
+def _is_dec(t) -> bool:
+    from .decimal import is_decimal
+    return is_decimal(t)
 
 
 def is_integral(t) -> bool:
@@ -95,7 +100,8 @@ def from_json_obj(o) -> Any:
     if isinstance(o, str):
         t = _SPARK_NAMES.get(o.lower(), o.lower())
         if t.startswith("decimal"):
-            return "decimal"
+            from .decimal import parse_decimal_type
+            return parse_decimal_type(t)
         if t not in SCALAR_TYPES:
             raise ValueError(f"unsupported data type {o!r}")
         return t
@@ -184,8 +190,9 @@ def _ddl_type(ty: str):
     if low.startswith("struct<"):
         inner = ty.strip()[7:-1]
         return parse_ddl_schema(inner.replace(":", " "))
-    if low.startswith("decimal"):
-        return "decimal"
+    if low.startswith(("decimal", "numeric", "dec(")) or low == "dec":
+        from .decimal import parse_decimal_type
+        return parse_decimal_type(low)
     return from_json_obj(low)
 
 
@@ -198,6 +205,8 @@ def common_type(a, b):
     if b == "null":
         return a
     if is_numeric(a) and is_numeric(b):
+        if _is_dec(a) or _is_dec(b):
+            return _wider_decimal(a, b)
         if a in FRACTIONAL or b in FRACTIONAL:
             return "double"
         return "long"
@@ -206,3 +215,15 @@ def common_type(a, b):
     if "string" in (a, b) and not is_nested(a) and not is_nested(b):
         return "string"
     return a
+
+
+def _wider_decimal(a, b):
+    """Spark DecimalPrecision.widerDecimalType / findTightestCommonType: a double or float wins; integers take
+    part as decimal(10,0) / decimal(20,0)."""
+    from .decimal import DecimalType, bounded, is_decimal, of_integral
+    if a in ("double", "float") or b in ("double", "float"):
+        return "double"
+    da = a if is_decimal(a) else of_integral(a)
+    db = b if is_decimal(b) else of_integral(b)
+    s = max(da.scale, db.scale)
+    return bounded(max(da.precision - da.scale, db.precision - db.scale) + s, s)

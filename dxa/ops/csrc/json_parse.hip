@@ -21,7 +21,7 @@ namespace {
 
 enum : int32_t {
   FT_STRUCT = 0, FT_BOOL = 1, FT_LONG = 2, FT_DOUBLE = 3, FT_STRING = 4, FT_RAW = 5,
-  FT_TIMESTAMP = 6, FT_INT = 7, FT_DATE = 8,
+  FT_TIMESTAMP = 6, FT_INT = 7, FT_DATE = 8, FT_DECIMAL = 9,   // FT_DECIMAL: the number token's text (decimal.hip)
 };
 
 struct ParseArgs {
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
             a.vals[(int64_t)vs * n + row] = iv * 1000000ll;
             a.valid[(int64_t)node * n + row] = 1;
           }
-        } else if (t == FT_STRING) {
+        } else if (t == FT_STRING || t == FT_DECIMAL) {
           a.vals[(int64_t)vs * n + row] = s;
           a.lens[(int64_t)ls * n + row] = (int32_t)(r.p - s);
           a.valid[(int64_t)node * n + row] = 1;

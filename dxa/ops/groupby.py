@@ -15,6 +15,8 @@ from typing import List, Optional
 import torch
 
 from . import native as N
+from ..engine.decimal import (aggregate as decimal_aggregate, is_decimal, key_parts as decimal_key_parts,
+                              to_double as decimal_to_double)
 from .hashing import hash_columns
 
 INT32_MAX = 2**31 - 1
@@ -48,6 +50,8 @@ def group_rows(keys: List) -> Groups:
         return Groups(torch.zeros(n, dtype=torch.int64, device=device), 1,
                       torch.zeros(1, dtype=torch.int64, device=device))
     keys = [materialize(k) for k in keys]
+    if any(is_decimal(k.dtype) for k in keys):
+        keys = [p for k in keys for p in (decimal_key_parts(k) if is_decimal(k.dtype) else [k])]
     h = hash_columns(keys)
     if _on_gpu(device):
         st = N.stream_handle(device)
@@ -168,6 +172,12 @@ def aggregate(groups: Groups, col, func: str, n: int):
         return PrimColumn("long", _agg_raw(groups, None, None, "count", n, device))
     col = materialize(col)
     valid = col.valid
+    if is_decimal(col.dtype) and func not in ("count", "first", "last"):
+        r = decimal_aggregate(groups, col, func, n)
+        if r is not None:
+            return r
+        col = decimal_to_double(col)               # variance / stddev: over doubles, as Spark casts them
+        valid = col.valid
     if n == 0 and func != "count":
         # only the global aggregate has a group with no rows: every aggregate but COUNT is NULL there (Spark)
         rdt = {"avg": "double", "stddev": "double", "stddev_samp": "double", "stddev_pop": "double",
@@ -293,7 +303,7 @@ def aggregate_many(groups: Groups, reqs, n: int):
         if func == "count":
             plan.append(("count", count_slot(col.valid), None, None))
             continue
-        if isinstance(col, StrColumn) or not isinstance(col, PrimColumn):
+        if isinstance(col, StrColumn) or not isinstance(col, PrimColumn) or is_decimal(col.dtype):
             plan.append(None)
             continue
         data, valid = col.data, col.valid

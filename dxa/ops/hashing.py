@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from . import native as N
+from ..engine.decimal import is_decimal, key_parts as decimal_key_parts
 
 SEED = np.uint64(0x5bd1e9955bd1e995)
 GOLD = np.uint64(0x9E3779B97F4A7C15)
@@ -87,6 +88,8 @@ def hash_columns(cols: List) -> torch.Tensor:
     """64-bit row hash over one or more key columns → int64 tensor (bit pattern of the uint64 hash)."""
     from ..engine.column import PrimColumn, StrColumn, materialize
     assert cols
+    if any(is_decimal(c.dtype) for c in cols):
+        cols = [p for c in cols for p in (decimal_key_parts(materialize(c)) if is_decimal(c.dtype) else [c])]
     n = cols[0].length
     device = cols[0].device
     if torch.device(device).type == "cuda":

@@ -16,6 +16,7 @@ import torch
 from . import native as N
 from .groupby import _next_pow2, _on_gpu
 from .hashing import hash_columns
+from ..engine.decimal import is_decimal, key_parts as decimal_key_parts
 
 
 @dataclass
@@ -38,7 +39,16 @@ def _any_null(cols) -> Optional[torch.Tensor]:
     return m
 
 
+def _flat_keys(keys: List) -> List:
+    """Wide decimal keys compare / hash as their two 64-bit words (dxa/engine/decimal.py key_parts)."""
+    if not any(is_decimal(k.dtype) for k in keys):
+        return keys
+    from ..engine.column import materialize
+    return [p for k in keys for p in (decimal_key_parts(materialize(k)) if is_decimal(k.dtype) else [k])]
+
+
 def build_side(keys: List) -> BuiltSide:
+    keys = _flat_keys(keys)
     n = keys[0].length
     device = keys[0].device
     h = hash_columns(keys) if n else torch.empty(0, dtype=torch.int64, device=device)
@@ -73,6 +83,7 @@ def build_side(keys: List) -> BuiltSide:
 
 def probe(built: BuiltSide, keys: List, outer: bool) -> Tuple[torch.Tensor, torch.Tensor]:
     """Candidate pairs by hash.  outer=True emits (i, -1) for probe rows without candidates."""
+    keys = _flat_keys(keys)
     n = keys[0].length
     device = keys[0].device
     if n == 0:
@@ -129,6 +140,7 @@ def probe(built: BuiltSide, keys: List, outer: bool) -> Tuple[torch.Tensor, torc
 
 def keys_equal(lcols: List, rcols: List, li: torch.Tensor, ri: torch.Tensor) -> torch.Tensor:
     """Exact key equality of candidate pairs (ri == -1 rows are reported unequal)."""
+    lcols, rcols = _flat_keys(lcols), _flat_keys(rcols)
     from ..engine.column import StrColumn, PrimColumn, materialize
     device = li.device
     ok = torch.ones(li.shape[0], dtype=torch.bool, device=device)

@@ -16,10 +16,14 @@ import numpy as np
 import torch
 
 from . import native as N
+from decimal import Decimal as _Decimal
+
+from ..engine.decimal import from_text as decimal_from_text, is_decimal, quantize as decimal_quantize
 from ..engine.types import ArrayType, MapType, StructField, StructType
 
 FT = {"struct": 0, "boolean": 1, "long": 2, "double": 3, "float": 3, "decimal": 3, "string": 4, "raw": 5,
-      "timestamp": 6, "int": 7, "date": 8}
+      "timestamp": 6, "int": 7, "date": 8, "decimal_exact": 9}
+FT_DECIMAL = 9          # decimal(p,s): the kernel keeps the number token's text; decimal.hip converts it exactly
 
 FNV_BASIS = 0xcbf29ce484222325
 FNV_PRIME = 0x100000001b3
@@ -69,7 +73,7 @@ class ParsePlan:
             if nd.code != 0:
                 nd.val_slot = nv
                 nv += 1
-                if nd.code in (4, 5):
+                if nd.code in (4, 5, FT_DECIMAL):
                     nd.len_slot = nl
                     nl += 1
         self.nval, self.nlen = nv, nl
@@ -125,13 +129,14 @@ class ParsePlan:
             elif isinstance(f.dtype, (MapType, ArrayType)):
                 self.nodes.append(Node(path, parent, f.name, f.dtype, FT["raw"]))
             else:
-                self.nodes.append(Node(path, parent, f.name, f.dtype, FT.get(f.dtype, FT["string"])))
+                code = FT_DECIMAL if is_decimal(f.dtype) else FT.get(f.dtype, FT["string"])
+                self.nodes.append(Node(path, parent, f.name, f.dtype, code))
 
     def string_val_slots(self, device) -> Optional[torch.Tensor]:
         """Value-slot rows holding string starts (string and raw-JSON fields), as a device index tensor."""
         key = ("sslots", str(device))
         if key not in self._dev:
-            sl = sorted({nd.val_slot for nd in self.nodes[1:] if nd.code in (4, 5)})
+            sl = sorted({nd.val_slot for nd in self.nodes[1:] if nd.code in (4, 5, FT_DECIMAL)})
             self._dev[key] = torch.tensor(sl, dtype=torch.int64, device=device) if sl else None
         return self._dev[key]
 
@@ -323,6 +328,8 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
             cols[idx] = StrColumn(arena, raw, lens[nd.len_slot], v)
         elif nd.code == FT["raw"]:
             cols[idx] = JsonColumn(arena, raw, lens[nd.len_slot], v, nd.dtype)
+        elif nd.code == FT_DECIMAL:
+            cols[idx] = decimal_from_text(StrColumn(arena, raw, lens[nd.len_slot], v), nd.dtype, trim=False)
         elif nd.code == FT["double"]:
             cols[idx] = PrimColumn(nd.dtype if nd.dtype in ("double", "float", "decimal") else "double",
                                    raw.view(torch.float64), v)
@@ -364,6 +371,17 @@ def _iso_to_us(s: str) -> Optional[int]:
     return us
 
 
+def _floats(v):
+    """JSON fractions were parsed as exact decimals; everything but decimal fields sees them as doubles."""
+    if isinstance(v, _Decimal):
+        return float(v)
+    if isinstance(v, dict):
+        return {k: _floats(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_floats(x) for x in v]
+    return v
+
+
 def _convert(v, dtype):
     """Python JSON value → storage value for a leaf, or None (null / mismatch)."""
     if v is None:
@@ -376,10 +394,17 @@ def _convert(v, dtype):
         if not (-2**63 <= v < 2**63):
             return None
         return v
+    if is_decimal(dtype):
+        if isinstance(v, bool) or not isinstance(v, (int, _Decimal)):
+            return None
+        return decimal_quantize(v, dtype)
     if dtype in ("double", "float", "decimal"):
-        if isinstance(v, bool) or not isinstance(v, (int, float)):
+        if isinstance(v, bool) or not isinstance(v, (int, float, _Decimal)):
             return None
         return float(v)
+    if dtype == "string" and isinstance(v, _Decimal):
+        return str(v)                                  # the number token's own text
+    v = _floats(v)
     if dtype == "boolean":
         return v if isinstance(v, bool) else None
     if dtype == "string":
@@ -419,7 +444,7 @@ def _parse_cpu(buf, offs, n, plan: ParsePlan, ends=None):
     ok = []
     for i in range(n):
         try:
-            d = json.loads(data[o[i]:e[i]].decode("utf-8"))
+            d = json.loads(data[o[i]:e[i]].decode("utf-8"), parse_float=_Decimal)
             if not isinstance(d, dict):
                 raise ValueError
             recs.append(d)
@@ -443,6 +468,8 @@ def _parse_cpu(buf, offs, n, plan: ParsePlan, ends=None):
                 conv = [_convert(v, nd.dtype) for v in vals]
                 if nd.code == FT["raw"]:
                     col = strings_from_pylist(conv, "cpu", nd.dtype)
+                elif is_decimal(nd.dtype):
+                    col = column_from_pylist(conv, nd.dtype, "cpu")
                 elif nd.dtype in ("float", "decimal"):
                     col = column_from_pylist(conv, "double", "cpu")
                     col.dtype = nd.dtype

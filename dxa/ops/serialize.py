@@ -89,6 +89,7 @@ class _Builder:
     def add(self, col, name: Optional[str]) -> int:
         from ..engine.column import (ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn)
         from ..engine.serialize import _scalar_text
+        from ..engine.decimal import is_decimal, to_text_column as decimal_text
         idx = len(self.nodes)
         nd = {"kind": K_NULL, "nchildren": 0, "child0": 0, "drop_nulls": 0, "name": _quoted(name) if name else b"",
               "data": 0, "valid": 0, "arena": 0, "starts": 0, "lens": 0, "const": b""}
@@ -100,6 +101,8 @@ class _Builder:
                 nd["kind"] = K_CONST
                 nd["const"] = _scalar_text(col.value, col.dtype).encode("utf-8")
             return idx
+        if isinstance(col, PrimColumn) and is_decimal(col.dtype):
+            col = decimal_text(col, raw=True)       # exact digits at the column's scale, a raw JSON number
         nd["valid"] = self._host(col.valid.view(torch.uint8) if col.valid is not None else None)
         if isinstance(col, StrColumn):
             nd["kind"] = K_RAW if isinstance(col, JsonColumn) else K_STR
@@ -192,6 +195,7 @@ class _DevBuilder:
     def add(self, col, name: Optional[str]) -> int:
         from ..engine.column import (ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn)
         from ..engine.serialize import _scalar_text
+        from ..engine.decimal import is_decimal, to_text_column as decimal_text
         idx = len(self.nodes)
         nd = self._blank()
         if name:
@@ -202,6 +206,8 @@ class _DevBuilder:
                 nd["kind"] = K_CONST
                 nd["const"] = self._t(_scalar_text(col.value, col.dtype).encode("utf-8"))
             return idx
+        if isinstance(col, PrimColumn) and is_decimal(col.dtype):
+            col = decimal_text(col, raw=True)       # exact digits at the column's scale, a raw JSON number
         if col.valid is not None:
             nd["valid"] = self._dev(col.valid.view(torch.uint8) if col.valid.dtype == torch.bool else col.valid)
         if isinstance(col, StrColumn):

@@ -226,6 +226,12 @@ def column_order_key(col, descending: bool = False):
     from ..engine.column import PrimColumn, StrColumn
     if isinstance(col, StrColumn):
         key = order_key(string_ranks(col), "int", descending)
+    elif isinstance(col, PrimColumn) and col.data.dim() == 2:
+        # wide decimal(p > 18): dense ranks of the signed 128-bit values — (hi, lo ^ sign) sorts lexicographically
+        # as signed words in exactly the 128-bit order
+        hl = torch.stack([col.data[:, 1], col.data[:, 0] ^ (-(1 << 63))], 1)
+        ranks = torch.unique(hl, dim=0, return_inverse=True)[1].to(torch.int64)
+        key = order_key(ranks, "int", descending)
     elif isinstance(col, PrimColumn):
         kind = "float" if col.data.dtype in (torch.float64, torch.float32) else "int"
         key = order_key(col.data, kind, descending)

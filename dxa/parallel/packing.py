@@ -71,6 +71,16 @@ def flatten(col, leaves: List[Leaf], spec: list):
         lf.str_type = type(col)
         leaves.append(lf)
         return
+    if isinstance(col, PrimColumn) and col.data.dim() == 2:
+        # a wide decimal(p > 18, s): its (lo, hi) words travel as two int64 leaves
+        lo = PrimColumn("long", col.data[:, 0].contiguous(), col.valid)
+        hi = PrimColumn("long", col.data[:, 1].contiguous(), None)
+        spec.append(("wide", len(leaves), len(leaves) + 1, col.dtype))
+        for part in (lo, hi):
+            lf = Leaf("prim", "long", part)
+            lf.torch_dtype = torch.int64
+            leaves.append(lf)
+        return
     if isinstance(col, PrimColumn):
         spec.append(("prim", len(leaves)))
         lf = Leaf("prim", col.dtype, col)
@@ -87,6 +97,10 @@ def rebuild(spec_item, leaves_out, n, device):
         return ConstColumn(spec_item[1], spec_item[2], n, device)
     if kind in ("prim", "str"):
         return leaves_out[spec_item[1]]
+    if kind == "wide":
+        from ..engine.column import PrimColumn
+        lo, hi = leaves_out[spec_item[1]], leaves_out[spec_item[2]]
+        return PrimColumn(spec_item[3], torch.stack([lo.data, hi.data], 1), lo.valid)
     if kind == "struct":
         _, names, is_map, dtype, vleaf, sub = spec_item
         kids = [rebuild(s, leaves_out, n, device) for s in sub]

@@ -710,7 +710,8 @@ class Parser:
         if self.is_op("-"):
             self.advance()
             operand = self.parse_unary()
-            if isinstance(operand, A.Literal) and operand.type in ("long", "int", "double", "decimal"):
+            if isinstance(operand, A.Literal) and (operand.type in ("long", "int", "double")
+                                                   or str(operand.type).startswith("decimal(")):
                 return A.Literal(-operand.value, operand.type)
             return A.UnaryOp("-", operand)
         if self.accept_op("+"):
@@ -823,6 +824,7 @@ class Parser:
 
     def parse_type_name(self) -> str:
         name = self.ident().lower()
+        args = []
         if self.accept_op("("):
             depth = 1
             while depth:
@@ -833,6 +835,14 @@ class Parser:
                     depth += 1
                 elif self.is_op(")", tok=t):
                     depth -= 1
+                elif depth == 1 and t.kind == "num":
+                    args.append(t.text)
+        if name in ("decimal", "numeric", "dec"):
+            from ..engine.decimal import DecimalType
+            try:
+                return DecimalType(*(int(a) for a in args[:2])) if args else DecimalType(10, 0)
+            except ValueError:
+                self.error(f"invalid decimal type {name}({', '.join(args)})")
         return {"integer": "int", "bigint": "long", "smallint": "int", "tinyint": "int", "real": "float",
                 "varchar": "string", "char": "string", "text": "string", "bool": "boolean",
                 "numeric": "decimal", "dec": "decimal"}.get(name, name)
@@ -1022,14 +1032,25 @@ def _cube(cols):
 def _number_literal(text: str) -> A.Literal:
     up = text.upper()
     if up.endswith("BD"):
-        return A.Literal(float(text[:-2]), "double")
+        from ..engine.decimal import literal_type
+        import decimal as _pd
+        t = literal_type(text[:-2])
+        if t is None:
+            raise SqlError(f"decimal literal {text} exceeds 38 digits")
+        return A.Literal(_pd.Decimal(text[:-2]), t)
     suffix = up[-1]
     if suffix in "LSY":
         return A.Literal(int(text[:-1]), "long")
     if suffix == "D":
         return A.Literal(float(text[:-1]), "double")
-    if any(c in text for c in ".eE"):
+    if "e" in text.lower():
         return A.Literal(float(text), "double")
+    if "." in text:
+        # Spark: an unsuffixed fractional literal is an exact decimal of its own digits (over 38 digits: double)
+        from ..engine.decimal import literal_type
+        import decimal as _pd
+        t = literal_type(text)
+        return A.Literal(_pd.Decimal(text), t) if t is not None else A.Literal(float(text), "double")
     v = int(text)
     return A.Literal(v, "int" if -2**31 <= v < 2**31 else "long")
 
