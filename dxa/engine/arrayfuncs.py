@@ -87,32 +87,20 @@ def _str_eq(a, b, S):
 
 
 def _build(els: List, order: torch.Tensor, keep: torch.Tensor, row_valid, drop_nulls=True) -> ArrayColumn:
-    """Output slots: slot j of row r is input slot ``order[r, j]`` when ``keep[r, j]`` (kept slots first)."""
+    """Output slots: slot j of row r is input slot ``order[r, j]`` when ``keep[r, j]`` (kept slots first).  The
+    element stacks are built once and gathered for every output slot together ([n, K] → [K, n] rows)."""
     n = order.shape[0]
     dev = order.device
     K = order.shape[1]
-    out = []
-    for j in range(K):
-        idx = order[:, j]
-        kj = keep[:, j]
-        out.append(_pick(els, idx, kj))
-    if not out:
+    if not K or not els:
         return ArrayColumn([], n, row_valid, True, dev)
-    return ArrayColumn(out, n, row_valid, drop_nulls, dev)
-
-
-def _pick(els, idx, keep):
-    """Per row r: els[idx[r]][r], valid where ``keep`` (and the picked element is non-null)."""
     e0 = els[0]
+    val = torch.stack([e.valid_mask() for e in els], 1).gather(1, order) & keep
+    val_t = val.t().contiguous()
     if isinstance(e0, PrimColumn):
-        data = torch.stack([e.data for e in els], 1)
-        val = torch.stack([e.valid_mask() for e in els], 1)
-        d = data.gather(1, idx.unsqueeze(1)).squeeze(1)
-        v = val.gather(1, idx.unsqueeze(1)).squeeze(1) & keep
-        return PrimColumn(e0.dtype, d, v)
-    starts = torch.stack([e.starts.to(torch.int64) for e in els], 1)
-    lens = torch.stack([e.lens.to(torch.int32) for e in els], 1)
-    val = torch.stack([e.valid_mask() for e in els], 1)
+        data_t = torch.stack([e.data for e in els], 1).gather(1, order).t().contiguous()
+        out = [PrimColumn(e0.dtype, data_t[j], val_t[j]) for j in range(K)]
+        return ArrayColumn(out, n, row_valid, drop_nulls, dev)
     arena = e0.arena
     if len({id(e.arena) for e in els}) != 1:
         # slots over different arenas: one compact arena holding every slot's bytes (slot k, row r at k*n + r)
@@ -120,10 +108,13 @@ def _pick(els, idx, keep):
         cat = S.concat(els, None)
         starts = cat.starts.view(len(els), e0.length).t()
         arena = cat.arena
-    s = starts.gather(1, idx.unsqueeze(1)).squeeze(1)
-    ln = lens.gather(1, idx.unsqueeze(1)).squeeze(1)
-    v = val.gather(1, idx.unsqueeze(1)).squeeze(1) & keep
-    return type(e0)(arena, s, ln, v, e0.dtype)
+    else:
+        starts = torch.stack([e.starts.to(torch.int64) for e in els], 1)
+    lens = torch.stack([e.lens.to(torch.int32) for e in els], 1)
+    st_t = starts.gather(1, order).t().contiguous()
+    ln_t = lens.gather(1, order).t().contiguous()
+    out = [type(e0)(arena, st_t[j], ln_t[j], val_t[j], e0.dtype) for j in range(K)]
+    return ArrayColumn(out, n, row_valid, drop_nulls, dev)
 
 
 def _compact(keep: torch.Tensor) -> torch.Tensor:
@@ -134,14 +125,14 @@ def _compact(keep: torch.Tensor) -> torch.Tensor:
 
 
 def _first_occurrence(eq: torch.Tensor, present: torch.Tensor, nonnull: torch.Tensor) -> torch.Tensor:
-    """keep[r, i]: present slot i has no equal present slot before it (null equals null)."""
+    """keep[r, i]: present slot i has no equal present slot before it (null equals null).  Slots are classed
+    0 absent / 1 null / 2 value: two slots are the same when their classes agree and they are null or equal."""
     n, K = present.shape
-    both_null = (~nonnull & present).unsqueeze(2) & (~nonnull & present).unsqueeze(1)
-    same = (eq & nonnull.unsqueeze(2) & nonnull.unsqueeze(1)) | both_null
-    same = same & present.unsqueeze(2) & present.unsqueeze(1)
+    cls = present.to(torch.int8) + nonnull.to(torch.int8)
+    c = cls.unsqueeze(2)
     earlier = torch.ones((K, K), dtype=torch.bool, device=present.device).tril(-1)      # j < i
-    dup = (same & earlier.unsqueeze(0)).any(2)
-    return present & ~dup
+    same = (c == cls.unsqueeze(1)) & (eq | (c == 1)) & earlier
+    return present & ~same.any(2)
 
 
 def _row_valid(arr):

@@ -520,9 +520,17 @@ def _host_array_fn(fn, elem_type_of=None, scalar_type=None):
 
 
 def _f_slice(l, start, length):
+    # Spark 2.4 Slice: a negative start counts from the end; a start index before the first element (or past the
+    # last) gives an empty array, not a clipped one
     start, length = int(start), int(length)
+    if start == 0:
+        raise EvalError("slice: SQL array indices start at 1")
+    if length < 0:
+        raise EvalError("slice: length must be greater than or equal to 0")
     s = start - 1 if start > 0 else len(l) + start
-    return l[max(0, s):max(0, s) + max(0, length)]
+    if s < 0 or s >= len(l):
+        return []
+    return l[s:s + length]
 
 
 def _f_sequence(e, scope, ctx, subst):
@@ -1261,9 +1269,9 @@ def _register():
     reg("md5", _f_digest(0, lambda s: hashlib.md5(str(s).encode()).hexdigest()))
     reg("crc32", _f_digest("crc32", lambda s: zlib.crc32(str(s).encode()) & 0xFFFFFFFF, "long"))
     reg("base64", _f_digest("base64", lambda s: _b64.b64encode(str(s).encode()).decode()))
-    reg("unbase64", _host_string_fn(lambda s: _b64.b64decode(str(s)).decode("utf-8", errors="replace")))
+    reg("unbase64", _host_string_fn(lambda s: _unbase64(s)))
     reg("hex", _f_digest("hex", _hex))
-    reg("unhex", _host_string_fn(lambda s: bytes.fromhex(str(s)).decode("utf-8", errors="replace")))
+    reg("unhex", _host_string_fn(lambda s: _unhex(s)))
     reg("initcap", _host_string_fn(_initcap))
     reg("repeat", _host_string_fn(lambda s, k: str(s) * max(0, int(k))))
     reg("left", _f_left_right(False))
@@ -1390,13 +1398,17 @@ def _f_timestamp_seconds(e, scope, ctx, subst):
 
 
 def _format_number(x, d):
+    """java.text.DecimalFormat("#,##0.00…", HALF_EVEN) over the value's shortest digits (Spark FormatNumber)."""
     if isinstance(d, str):
         raise ValueError("format patterns are not supported")
     d = int(d)
     if d < 0:
         return None
     from decimal import ROUND_HALF_EVEN, Decimal
-    q = Decimal(repr(float(x))).quantize(Decimal(1).scaleb(-d), rounding=ROUND_HALF_EVEN)
+    if isinstance(x, float) and (x != x or x in (float("inf"), float("-inf"))):
+        return "\ufffd" if x != x else ("-\u221e" if x < 0 else "\u221e")      # Java 8 DecimalFormatSymbols
+    v = Decimal(x) if isinstance(x, int) and not isinstance(x, bool) else Decimal(repr(float(x)))
+    q = v.quantize(Decimal(1).scaleb(-d), rounding=ROUND_HALF_EVEN)
     return f"{q:,.{d}f}"
 
 
@@ -1404,26 +1416,34 @@ _DIGITS = "0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ"
 
 
 def _conv(s, fb, tb):
-    """conv(num, from_base, to_base): Spark/Hive NumberConverter — unsigned 64-bit unless to_base < 0."""
+    """conv(num, from_base, to_base): Spark 2.4 NumberConverter.convert — the space-trimmed digits up to the first
+    invalid one as an unsigned 64-bit value (saturating at 2^64 - 1), negated for a leading '-' unless to_base < 0,
+    which prints a signed value instead."""
     fb, tb = int(fb), int(tb)
-    if not (2 <= abs(fb) <= 36 and 2 <= abs(tb) <= 36):
+    if not (2 <= fb <= 36 and 2 <= abs(tb) <= 36):
         return None
-    t = str(s).strip().upper()
+    t = str(s).strip(" ")
+    if not t:
+        return None
     neg = t.startswith("-")
     t = t[1:] if neg else t
+    if len(t.encode("utf-8")) > 64:
+        return None
+    M = (1 << 64) - 1
     v = 0
     for ch in t:
-        k = _DIGITS.find(ch)
-        if k < 0 or k >= abs(fb):
+        k = _DIGITS.find(ch.upper()) if ch.isascii() else -1
+        if k < 0 or k >= fb:
             break
-        v = v * abs(fb) + k
-    v &= (1 << 64) - 1
-    if neg:
-        v = (-v) & ((1 << 64) - 1)
-    out_neg = False
+        v = v * fb + k
+        if v > M:
+            v = M
+            break
+    if neg and tb > 0:
+        v = M if v >= 1 << 63 else (-v) & M
     if tb < 0 and v >= 1 << 63:
-        v = (1 << 64) - v
-        out_neg = True
+        v = (-v) & M
+        neg = True
     b = abs(tb)
     digits = ""
     while True:
@@ -1431,16 +1451,16 @@ def _conv(s, fb, tb):
         v //= b
         if not v:
             break
-    return ("-" if out_neg else "") + digits
+    return ("-" if neg and tb < 0 else "") + digits
 
 
 def _soundex(s):
     s = str(s)
-    if not s or not s[0].isalpha():
+    if not s or not ("a" <= s[0] <= "z" or "A" <= s[0] <= "Z"):      # UTF8String.soundex: ASCII letters only
         return s
     codes = {**dict.fromkeys("BFPV", "1"), **dict.fromkeys("CGJKQSXZ", "2"), **dict.fromkeys("DT", "3"), "L": "4",
              **dict.fromkeys("MN", "5"), "R": "6"}
-    up = s.upper()
+    up = "".join(c.upper() if c.isascii() else "\0" for c in s)
     out, last = up[0], codes.get(up[0], "")
     for ch in up[1:]:
         c = codes.get(ch, "")
@@ -1496,6 +1516,57 @@ def _java_printf(fmt, *args):
             r = f"{(int(v) if c == 'd' else float(v)):,{prec}{'d' if c == 'd' else 'f'}}".rjust(int(width or 0))
         return r.upper() if c in "SXEG" else r
     return _re.sub(r"%([-#+ 0,(]*)(\d+)?(\.\d+)?([a-zA-Z%])", conv, str(fmt))
+
+
+def _unhex(s):
+    """Spark Hex.unhex: an odd length pads a leading '0'; any non-hex character → NULL (BINARY shown as text)."""
+    t = str(s)
+    if len(t) % 2:
+        t = "0" + t
+    try:
+        if not all(c in "0123456789abcdefABCDEF" for c in t):
+            return None
+        return bytes.fromhex(t).decode("utf-8", errors="replace")
+    except ValueError:
+        return None
+
+
+_B64 = {c: i for i, c in enumerate("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/")}
+_B64.update({"-": 62, "_": 63})
+
+
+def _unbase64(s):
+    """commons-codec Base64.decodeBase64 (Spark UnBase64): lenient — characters outside the (standard or URL-safe)
+    alphabet are skipped, '=' ends the data, a trailing 2- / 3-symbol group gives 1 / 2 bytes."""
+    acc, m, out = 0, 0, bytearray()
+    for c in str(s):
+        if c == "=":
+            break
+        v = _B64.get(c)
+        if v is None:
+            continue
+        acc = (acc << 6) | v
+        m += 1
+        if m == 4:
+            out += bytes(((acc >> 16) & 255, (acc >> 8) & 255, acc & 255))
+            acc, m = 0, 0
+    if m >= 2:
+        out.append((acc >> (4 if m == 2 else 10)) & 255)
+        if m == 3:
+            out.append((acc >> 2) & 255)
+    return bytes(out).decode("utf-8", errors="replace")
+
+
+def _split_part(s, d, k):
+    """split_part(str, delim, n): the n-th field (from the end when n < 0); out of range → ''; an empty delimiter
+    makes the whole string the only field; n = 0 is an error."""
+    s, d, k = str(s), str(d), int(k)
+    if k == 0:
+        raise EvalError("split_part: the field index must not be 0")
+    parts = s.split(d) if d else [s]
+    if abs(k) > len(parts):
+        return ""
+    return parts[k - 1] if k > 0 else parts[k]
 
 
 def _overlay(s, rep, pos, ln=None):
@@ -1776,6 +1847,80 @@ def _register_device_strings():
                                              lambda c, d, k: SF.substring_index(c, str(d), int(k)),
                                              _substring_index))
     reg("levenshtein", _levenshtein_fn)
+    reg("format_number", _f_format_number)
+    reg("conv", _device_string_fn("conv", _conv_device, _conv))
+    reg("bin", _f_bin)
+    reg("soundex", _device_string_fn("soundex", SF.soundex, _soundex))
+    reg("unhex", _device_string_fn("unhex", lambda c: SF.decode(c, 0), _unhex))
+    reg("unbase64", _device_string_fn("unbase64", lambda c: SF.decode(c, 1), _unbase64))
+    reg("split_part", _device_string_fn("split_part", lambda c, d, k: SF.split_part(c, str(d), int(k))
+                                        if int(k) != 0 else None, _split_part))
+    reg("factorial", _f_factorial)
+    reg("overlay", _f_overlay)
+
+
+def _conv_device(col, fb, tb):
+    from ..ops import strfuncs as SF
+    fb, tb = int(fb), int(tb)
+    if not (2 <= fb <= 36 and 2 <= abs(tb) <= 36):
+        return None                                  # the host path yields the NULLs
+    return SF.conv(col, fb, tb)
+
+
+def _f_format_number(e, scope, ctx, subst):
+    args = _args(e, scope, ctx, subst)
+    x = args[0] if args else None
+    if (len(args) == 2 and isinstance(x, PrimColumn) and x.data.is_cuda and x.dtype in ("int", "long", "double", "float")
+            and isinstance(args[1], ConstColumn) and isinstance(args[1].value, int)):
+        from ..ops import strfuncs as SF
+        out = SF.format_number(x, int(args[1].value))
+        if out is not None:
+            return out
+    return _host_string_fn(_format_number)(e, scope, ctx, subst)
+
+
+def _f_bin(e, scope, ctx, subst):
+    (x,) = _args(e, scope, ctx, subst)
+    if isinstance(x, PrimColumn) and x.data.is_cuda and x.dtype in ("int", "long", "double", "float"):
+        from ..ops import strfuncs as SF
+        if x.data.dtype == torch.float64:             # Spark casts to bigint (truncation)
+            x = cast_column(x, "long")
+        return SF.bin_text(x)
+    return _host_string_fn(lambda v: format(int(v) & 0xFFFFFFFFFFFFFFFF, "b"))(e, scope, ctx, subst)
+
+
+_FACT = [math.factorial(i) for i in range(21)]
+
+
+def _f_factorial(e, scope, ctx, subst):
+    (x,) = _args(e, scope, ctx, subst)
+    n, dev = scope.length, scope.device
+    if isinstance(x, ConstColumn):
+        v = None if x.value is None else int(x.value)
+        return ConstColumn(_FACT[v] if v is not None and 0 <= v <= 20 else None, "long", n, dev)
+    k = x.data.to(torch.int64) if x.data.dtype != torch.float64 else x.data.trunc().to(torch.int64)
+    ok = (k >= 0) & (k <= 20)
+    table = _h2d(_FACT, torch.int64, dev)
+    out = table[torch.where(ok, k, torch.zeros_like(k))]
+    return PrimColumn("long", out, ok if x.valid is None else ok & x.valid)
+
+
+def _f_overlay(e, scope, ctx, subst):
+    """overlay(input, replace, pos[, len]) = substring(input, 1, pos - 1) || replace || substring(input, pos + len)
+    (Spark's Overlay over substringSQL; len < 0 or absent → the replacement's length) — evaluated through the
+    device substring / concat paths."""
+    if len(e.args) not in (3, 4):
+        raise EvalError("overlay expects 3 or 4 arguments")
+    s, r, pos = e.args[:3]
+    rlen = A.Call("char_length", [r])
+    if len(e.args) == 4:
+        ln = e.args[3]
+        ln = A.Call("if", [A.BinOp(">=", ln, A.Literal(0, "int")), ln, rlen])
+    else:
+        ln = rlen
+    head = A.Call("substring", [s, A.Literal(1, "int"), A.BinOp("-", pos, A.Literal(1, "int"))])
+    tail = A.Call("substring", [s, A.BinOp("+", pos, ln)])
+    return evaluate(A.Call("concat", [head, r, tail]), scope, ctx, subst)
 
 
 _register_device_strings()

@@ -163,3 +163,105 @@ def levenshtein(a, b) -> Optional[object]:
     if int(bad.item()):
         return None
     return PrimColumn("int", out, and_valid(a.valid, b.valid))
+
+
+# ---- number ↔ text and codecs (dxa/ops/csrc/strconv.hip) ----------------------------------------------------------
+
+N.register_sigs({
+    "dxa_format_number": [c_p, c_i32, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p],
+    "dxa_conv": [c_p, c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p],
+    "dxa_bin": [c_p, c_i64, c_p, c_p, c_p, c_p],
+    "dxa_soundex": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
+    "dxa_str_decode": [c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p],
+    "dxa_split_part": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i64, c_p, c_p, c_p],
+})
+FMT_SLOT, CONV_SLOT = 64, 66
+
+
+def _slots(n, width, dev):
+    return (torch.empty(n * width + 16, dtype=torch.uint8, device=dev),
+            torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int32, device=dev))
+
+
+def format_number(col, d: int):
+    """format_number(x, d) over a device double / integral column; None when a row needs the host (|x| ≥ 10^18,
+    NaN / ±Inf) — one 4-byte flag read."""
+    from ..engine.column import StrColumn
+    dev, n = col.device, col.length
+    if d < 0 or d > 38:
+        return None
+    f64 = col.data.dtype in (torch.float64, torch.float32)
+    data = col.data.to(torch.float64 if f64 else torch.int64).contiguous()
+    arena, starts, lens = _slots(n, FMT_SLOT, dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    N.call("dxa_format_number", N.ptr(data), 1 if f64 else 0, N.ptr(N.u8(col.valid)), n, int(d), N.ptr(arena),
+           N.ptr(starts), N.ptr(lens), N.ptr(bad), N.stream_handle(dev))
+    if int(bad.item()):
+        return None
+    return StrColumn(arena, starts, lens, col.valid)
+
+
+def conv(col, from_base: int, to_base: int):
+    from ..engine.column import StrColumn
+    dev, n = col.device, col.length
+    out, starts, lens = _slots(n, CONV_SLOT, dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    N.call("dxa_conv", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), N.ptr(N.u8(col.valid)), n,
+           int(from_base), int(to_base), N.ptr(out), N.ptr(starts), N.ptr(lens), N.ptr(ok), _st(col))
+    return StrColumn(out, starts, lens, ok.view(torch.bool))
+
+
+def bin_text(col):
+    from ..engine.column import StrColumn
+    dev, n = col.device, col.length
+    out, starts, lens = _slots(n, CONV_SLOT, dev)
+    N.call("dxa_bin", N.ptr(col.data.to(torch.int64).contiguous()), n, N.ptr(out), N.ptr(starts), N.ptr(lens),
+           N.stream_handle(dev))
+    return StrColumn(out, starts, lens, col.valid)
+
+
+def soundex(col):
+    """None when some row's first byte is not an ASCII letter (Spark returns those inputs unchanged)."""
+    from ..engine.column import StrColumn
+    dev, n = col.device, col.length
+    out, starts, lens = _slots(n, 4, dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    N.call("dxa_soundex", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), N.ptr(N.u8(col.valid)), n,
+           N.ptr(out), N.ptr(starts), N.ptr(lens), N.ptr(bad), _st(col))
+    if int(bad.item()):
+        return None
+    return StrColumn(out, starts, lens, col.valid)
+
+
+def decode(col, mode: int):
+    """unhex (mode 0) / unbase64 (mode 1); None when an output is not ASCII (the host decodes those bytes with
+    replacement characters)."""
+    from ..engine.column import StrColumn
+    dev, n = col.device, col.length
+    lens = torch.empty(n, dtype=torch.int64, device=dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    args = (N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), N.ptr(N.u8(col.valid)), n, mode)
+    N.call("dxa_str_decode", *args, None, None, N.ptr(lens), N.ptr(ok), N.ptr(bad), _st(col))
+    off, total = _offsets(lens)                      # the one host read (with the flag behind it)
+    if int(bad.item()):
+        return None
+    dst = _alloc_arena(total, dev)
+    N.call("dxa_str_decode", *args, N.ptr(off), N.ptr(dst), N.ptr(lens), N.ptr(ok), N.ptr(bad), _st(col))
+    return StrColumn(dst, off, lens.to(torch.int32), ok.view(torch.bool))
+
+
+def split_part(col, delim: str, k: int):
+    from ..engine.column import StrColumn
+    if k == 0:
+        raise ValueError("split_part: the field index must not be 0")
+    dev, n = col.device, col.length
+    db = delim.encode("utf-8")
+    dl = upload(db, torch.uint8, dev)
+    st = torch.empty(n, dtype=torch.int64, device=dev)
+    ln = torch.empty(n, dtype=torch.int32, device=dev)
+    N.call("dxa_split_part", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n, N.ptr(dl), len(db), int(k),
+           N.ptr(st), N.ptr(ln), _st(col))
+    out = StrColumn(col.arena, st, ln, col.valid)
+    out._keep = dl
+    return out

@@ -1,5 +1,6 @@
-"""Device string built-ins (dxa/ops/csrc/strfuncs.hip): lpad / rpad / reverse / repeat / translate / initcap / ascii /
-substring_index / levenshtein.  CPU: Spark 2.4's documented results (UTF8String semantics, hand-computed); GPU: the
+"""Device string built-ins (dxa/ops/csrc/strfuncs.hip, strconv.hip): lpad / rpad / reverse / repeat / translate /
+initcap / ascii / substring_index / levenshtein / format_number / conv / bin / soundex / unhex / unbase64 / split_part
+/ factorial / overlay.  CPU: Spark 2.4's documented results (UTF8String semantics, hand-computed); GPU: the
 device path over 1 M rows matches the CPU evaluator and runs in < 10 ms per function (user SQL runs in Spark's
 codegen on the executors, CommonProcessorFactory.scala:257-275 — no per-row host work here either)."""
 import random
@@ -42,6 +43,34 @@ def test_spark_semantics_cpu():
     assert _q("SELECT ascii(s) a FROM T", [{"s": "é", "t": None}])[0]["a"] == -61
 
 
+def test_number_text_and_codecs_cpu():
+    """format_number / conv / bin / soundex / unhex / unbase64 / split_part / factorial / overlay against Spark's
+    documented results (DecimalFormat HALF_EVEN, NumberConverter, UTF8String.soundex, Hex.unhex, commons-codec
+    Base64, the Spark docs' overlay examples)."""
+    one = [{"s": "x", "t": None}]
+    q = lambda e: _q(f"SELECT {e} AS r FROM T", one)[0]["r"]
+    assert q("format_number(1234567.891, 2)") == "1,234,567.89"
+    assert q("format_number(-0.005, 2)") == "-0.00" and q("format_number(2.5, 0)") == "2"
+    assert q("format_number(3.5, 0)") == "4" and q("format_number(12345, 1)") == "12,345.0"
+    assert q("format_number(1.0, -1)") is None
+    assert q("conv('ff', 16, 10)") == "255" and q("conv('-ff', 16, 10)") == "18446744073709551361"
+    assert q("conv('-ff', 16, -10)") == "-255" and q("conv(' 100 ', 2, 10)") == "4"
+    assert q("conv('zz', 36, 16)") == "50F" and q("conv('12', 40, 10)") is None
+    assert q("conv('ffffffffffffffffff', 16, 10)") == "18446744073709551615"          # saturates
+    assert q("conv('12x4', 10, 16)") == "C"                                             # stops at 'x'
+    assert q("bin(13)") == "1101" and q("bin(-1)") == "1" * 64
+    assert [q(f"soundex('{w}')") for w in ("Robert", "Tymczak", "Pfister", "Ashcraft", "", "1abc")] == \
+        ["R163", "T522", "P236", "A261", "", "1abc"]
+    assert q("unhex('414243')") == "ABC" and q("unhex('F')") == "\x0f" and q("unhex('GG')") is None
+    assert q("unbase64('QUJD')") == "ABC" and q("unbase64('QUJ')") == "AB" and q("unbase64('Q U\nJD')") == "ABC"
+    assert [q(f"split_part('a,b,,c', ',', {k})") for k in (2, -1, 3, 5)] == ["b", "c", "", ""]
+    assert q("factorial(5)") == 120 and q("factorial(21)") is None and q("factorial(-1)") is None
+    assert q("overlay('Spark SQL', '_', 6)") == "Spark_SQL"
+    assert q("overlay('Spark SQL', 'CORE', 7)") == "Spark CORE"
+    assert q("overlay('Spark SQL', 'ANSI ', 7, 0)") == "Spark ANSI SQL"
+    assert q("overlay('Spark SQL', 'tructured', 2, 4)") == "Structured SQL"
+
+
 def _rand_rows(n, seed=5):
     rnd = random.Random(seed)
     alpha = "abcdefghij ABCDEF.,-"
@@ -59,6 +88,11 @@ GPU_FUNCS = [
     ("repeat(s, 3)", "repeat"), ("translate(s, 'abc.', 'XY')", "translate"), ("initcap(t)", "initcap"),
     ("ascii(s)", "ascii"), ("substring_index(s, '.', 1)", "substring_index"),
     ("substring_index(s, '.', -1)", "substring_index_neg"), ("levenshtein(t, s)", "levenshtein"),
+    ("format_number(length(t) * 1234.5678, 2)", "format_number"), ("format_number(length(s), 0)", "format_number_int"),
+    ("conv(t, 16, 10)", "conv"), ("conv(t, 16, -2)", "conv_neg"), ("bin(length(t) - 9)", "bin"),
+    ("soundex(concat('a', t))", "soundex"), ("unhex(t)", "unhex"), ("unbase64(base64(t))", "unbase64"),
+    ("split_part(s, '.', 2)", "split_part"), ("split_part(s, ' ', -1)", "split_part_neg"),
+    ("factorial(length(t) - 3)", "factorial"), ("overlay(t, 'XY', 3)", "overlay"),
 ]
 
 
