@@ -1047,6 +1047,7 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         idx = torch.nonzero(mask).flatten()
         scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]), scope.device)
         scope.dist = sdist
+    sel = _window_column_refs(sel, scope)
     sel, scope = _sliding_windows(sel, scope, ctx)
     items = _expand_items(sel, scope)
     gen_at = [k for k, (e, _) in enumerate(items) if isinstance(e, A.Call) and e.name in _GENERATOR_NAMES]
@@ -1079,6 +1080,28 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
 
 
 _WINDOW_COL = "__dxa_window"
+
+
+def _window_column_refs(sel: A.Select, scope: Scope) -> A.Select:
+    """Spark's TimeWindowing names the grouped ``window(...)`` struct ``window``: with ``GROUP BY window(ts, …)``
+    the SELECT list and HAVING may say ``window`` / ``window.start`` / ``window.end`` (when the input has no column of
+    that name)."""
+    calls = [g for g in sel.group_by if isinstance(g, A.Call) and g.name == "window"]
+    if len(calls) != 1 or scope._find("window"):
+        return sel
+    call = calls[0]
+
+    def sub(node):
+        if isinstance(node, A.Ident) and node.parts[0].lower() == "window":
+            e = call
+            for part in node.parts[1:]:
+                e = A.Subscript(e, A.Literal(part, "string"), dot=True)
+            return e
+        return None
+    import dataclasses
+    return dataclasses.replace(
+        sel, items=[dataclasses.replace(it, expr=A.replace(it.expr, sub)) for it in sel.items],
+        having=None if sel.having is None else A.replace(sel.having, sub))
 
 
 def _sliding_windows(sel: A.Select, scope: Scope, ctx):
