@@ -24,6 +24,7 @@ constexpr int kMaxW = 64;                  // ranks
 constexpr int kMaxCols = 64;               // prim data columns
 constexpr int kMaxValid = 64;              // validity bits
 constexpr int kMaxStr = 8;                 // string leaves
+constexpr int kMaxExtra = 4;               // extra words per send-size row
 
 // kinds of a prim column (element width)
 enum : int32_t { K8 = 0, K4 = 1, K1 = 2, K2 = 3 };
@@ -60,6 +61,9 @@ struct PackArgs {
   XCol cols[kMaxCols];
   XValid valids[kMaxValid];
   XStr strs[kMaxStr];
+  int32_t sizes_stride;  // row stride of `sizes` (>= 1 + nstr)
+  int32_t nextra;        // words written after the sizes of every destination row (the layout's validity flags,
+  int64_t extra[kMaxExtra];  //   which ride with the send sizes through the size all-to-all)
 };
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -115,7 +119,9 @@ __global__ __launch_bounds__(1024) void xchg_scan_kernel(const PackArgs a) {
     for (int d = threadIdx.x; d < a.W; d += blockDim.x) {
       int64_t t = 0;
       for (int b = 0; b < a.nblocks; ++b) t += h[(int64_t)d * a.nblocks + b];
-      a.sizes[(int64_t)d * S1 + s] = t;
+      a.sizes[(int64_t)d * a.sizes_stride + s] = t;
+      if (s == 0)
+        for (int x = 0; x < a.nextra; ++x) a.sizes[(int64_t)d * a.sizes_stride + S1 + x] = a.extra[x];
     }
     // chunked scan: each thread owns a contiguous run of ceil(m / threads) entries
     const int64_t per = (m + blockDim.x - 1) / blockDim.x;
@@ -333,6 +339,7 @@ DXA_API int dxa_xchg_limits(int32_t* out) {
   out[5] = kRows;
   out[6] = (int32_t)sizeof(PackArgs);
   out[7] = (int32_t)sizeof(UnpackArgs);
+  out[8] = kMaxExtra;
   return 0;
 }
 

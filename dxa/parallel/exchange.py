@@ -170,11 +170,9 @@ def shuffle_table(table, dest: torch.Tensor):
     W = _w()
     device = table.device
     lay = PK.Layout(table)
-    sizes, state = PK.plan(lay, dest.to(torch.int64), W, _force_torch())
-    # the per-leaf "has validity" flags ride along with the sizes: every rank ORs what it receives, so all ranks
-    # agree on the matrix layout without another collective
-    flags = _h2d(lay.flags(), torch.int64, device).expand(W, -1)
-    ext = torch.cat([sizes, flags], 1).contiguous()
+    # the per-leaf "has validity" flags ride along with the sizes (written by the plan's scan kernel): every rank
+    # ORs what it receives, so all ranks agree on the matrix layout without another collective
+    ext, state = PK.plan(lay, dest.to(torch.int64), W, _force_torch(), extra=lay.flags())
     recv_sizes = _a2a_counts(ext)
     both = torch.stack([ext, recv_sizes]).tolist()              # the exchange's one host sync
     lay.assign_flags(_or_rows([r[1 + lay.S:] for r in both[1]]))
@@ -328,9 +326,8 @@ def allgather_table(table):
         return table
     device = table.device
     lay = PK.Layout(table)
-    sizes, state = PK.plan(lay, None, 1, _force_torch())          # [1, 1+S]: rows, bytes per string leaf
-    flags = _h2d([lay.flags()], torch.int64, device)
-    ext = torch.cat([sizes.reshape(1, -1), flags], 1).contiguous()
+    # [1, 1+S+F]: rows, bytes per string leaf, then the validity flags
+    ext, state = PK.plan(lay, None, 1, _force_torch(), extra=lay.flags())
     allsz = torch.empty((W, ext.shape[1]), dtype=torch.int64, device=device)
     _all_gather_into(allsz, ext)
     got = allsz.tolist()                                           # the one host sync

@@ -287,7 +287,7 @@ def _limits():
         N.register_sigs({"dxa_xchg_limits": [ctypes.c_void_p], "dxa_xchg_plan": [ctypes.c_void_p, ctypes.c_void_p],
                          "dxa_xchg_scatter": [ctypes.c_void_p, ctypes.c_void_p],
                          "dxa_xchg_unpack": [ctypes.c_void_p, ctypes.c_void_p]})
-        arr = (ctypes.c_int32 * 8)()
+        arr = (ctypes.c_int32 * 9)()
         N.call("dxa_xchg_limits", ctypes.cast(arr, ctypes.c_void_p))
         _LIMITS = list(arr)
     return _LIMITS
@@ -314,7 +314,8 @@ def _pack_args_type(L):
                     ("nblocks", ctypes.c_int32), ("ncols", ctypes.c_int32), ("nvalid", ctypes.c_int32),
                     ("nstr", ctypes.c_int32), ("C", ctypes.c_int32), ("hist", ctypes.c_void_p),
                     ("sizes", ctypes.c_void_p), ("mat", ctypes.c_void_p), ("cols", _XCol * maxc),
-                    ("valids", _XValid * maxv), ("strs", _XStr * maxs)]
+                    ("valids", _XValid * maxv), ("strs", _XStr * maxs), ("sizes_stride", ctypes.c_int32),
+                    ("nextra", ctypes.c_int32), ("extra", ctypes.c_int64 * L[8])]
     return PackArgs
 
 
@@ -353,7 +354,7 @@ class DevicePlan:
         self.args, self.keep, self.hist = args, keep, hist
 
 
-def plan_device(lay: Layout, dest: Optional[torch.Tensor], W: int):
+def plan_device(lay: Layout, dest: Optional[torch.Tensor], W: int, extra=()):
     from ..ops import native as N
     L = _limits()
     n, dev = lay.n, lay.device
@@ -381,8 +382,11 @@ def plan_device(lay: Layout, dest: Optional[torch.Tensor], W: int):
         keep += [st, ln, c.arena]
         a.strs[lf.sidx] = _XStr(c.arena.data_ptr(), st.data_ptr(), ln.data_ptr(), 0)
     hist = torch.empty((1 + lay.S) * W * a.nblocks, dtype=torch.int64, device=dev)
-    sizes = torch.empty((W, 1 + lay.S), dtype=torch.int64, device=dev)
+    sizes = torch.empty((W, 1 + lay.S + len(extra)), dtype=torch.int64, device=dev)
     a.hist, a.sizes = hist.data_ptr(), sizes.data_ptr()
+    a.sizes_stride, a.nextra = sizes.shape[1], len(extra)
+    for i, x in enumerate(extra):
+        a.extra[i] = int(x)
     N.call("dxa_xchg_plan", ctypes.byref(a), N.stream_handle(dev))
     return sizes, DevicePlan(a, keep, hist)
 
@@ -496,11 +500,16 @@ def unpack_device(names, spec, meta, mat, arenas, row_prefix, src_base, byte_bas
 # dispatch
 # ---------------------------------------------------------------------------------------------------------------
 
-def plan(lay: Layout, dest: Optional[torch.Tensor], W: int, force_torch: bool = False):
-    if not force_torch and device_ok(lay, W):
-        sizes, st = plan_device(lay, dest, W)
+def plan(lay: Layout, dest: Optional[torch.Tensor], W: int, force_torch: bool = False, extra=()):
+    """Send sizes [W, 1+S (+ len(extra))]: rows and bytes per string leaf for every destination, then ``extra``
+    words repeated on every row (the device path writes them from its scan kernel: no upload, no concatenation)."""
+    if not force_torch and device_ok(lay, W) and len(extra) <= _limits()[8]:
+        sizes, st = plan_device(lay, dest, W, extra)
         return sizes, ("device", st)
     sizes, st = plan_torch(lay, dest, W)
+    if extra:
+        x = _h2d(list(extra), torch.int64, sizes.device).expand(W, -1)
+        sizes = torch.cat([sizes, x], 1).contiguous()
     return sizes, ("torch", st)
 
 

@@ -146,3 +146,27 @@ def test_exchange_launch_count(gpu):
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
     kernels = [n for n in names if "xchg" in n]
     assert len(kernels) == 3, names
+
+
+@pytest.mark.gpu
+def test_send_side_is_three_launches():
+    """The shuffle's send side — partition histogram, scan (with the validity flags written into the size rows) and
+    the scatter into the packed matrix + string arenas — is three kernel launches whatever the table's width."""
+    from launch_count import count_launches
+    from dxa.engine.column import PrimColumn, strings_from_pylist
+    dev = torch.device("cuda")
+    n = 100_000
+    cols = [PrimColumn("long", torch.arange(n, device=dev) * k) for k in range(12)]
+    cols.append(PrimColumn("double", torch.rand(n, dtype=torch.float64, device=dev), torch.rand(n, device=dev) > 0.1))
+    cols.append(strings_from_pylist([f"s{i % 977}" for i in range(n)], dev))
+    t = Table([f"c{i}" for i in range(len(cols))], cols, n, dev)
+    dest = torch.randint(0, 8, (n,), device=dev)
+    torch.cuda.synchronize()
+    lay = PK.Layout(t)
+    with count_launches() as log:
+        ext, state = PK.plan(lay, dest, 8, extra=lay.flags())
+    sz = ext.tolist()                                       # the exchange's one host read-back
+    with count_launches() as log2:
+        PK.scatter(lay, state, [r[0] for r in sz], [[r[1 + s] for r in sz] for s in range(lay.S)])
+    # dxa_xchg_plan = histogram + scan kernels
+    assert log == ["dxa_xchg_plan"] and log2 == ["dxa_xchg_scatter"], (log, log2)
