@@ -6,9 +6,10 @@
 //     no length pass, no scan, no host read;
 //   * unhex / unbase64 outputs are at most the input length: a length pass, a scan, a write pass;
 //   * split_part is a view (start, length) into the input arena.
-// Rows a kernel does not reproduce exactly flag `bad` (format_number beyond 10^18 or NaN / ±Inf, codec output that
-// is not ASCII — the host path decodes it with replacement characters, soundex inputs returned unchanged); the
-// caller then evaluates the column on the host (the CPU evaluator, the differential tests' oracle).
+// Decoded bytes that are not UTF-8 become U+FFFD per maximal ill-formed subpart (utf8_clean, Python's
+// errors="replace"), as the host path renders them.  Rows a kernel does not reproduce exactly flag `bad`
+// (format_number beyond 10^18 or NaN / ±Inf, soundex inputs Spark returns unchanged); the caller then evaluates
+// the column on the host (the CPU evaluator, the differential tests' oracle).
 #include "dxa_common.h"
 #include "dxa_ryu.h"
 
@@ -320,7 +321,7 @@ __global__ void decode_kernel(const uint8_t* __restrict__ arena, const int64_t* 
     if (!write) {
       out_len[i] = ok ? p : 0;
       ovalid[i] = ok ? 1 : 0;
-      if (ok && !ascii) atomicAdd(bad, 1);
+      (void)ascii;
     }
   }
 }
@@ -378,7 +379,78 @@ __global__ void split_part_kernel(const uint8_t* __restrict__ arena, const int64
   }
 }
 
+// UTF-8 validation with Python's errors="replace" (the Unicode "maximal subpart" policy): a well-formed sequence is
+// copied, every maximal ill-formed subpart becomes U+FFFD (EF BF BD).  Returns the byte length of the clean text.
+__device__ int64_t utf8_clean(const uint8_t* s, int32_t l, uint8_t* o, bool& changed) {
+  int64_t p = 0;
+  int32_t k = 0;
+  while (k < l) {
+    const uint8_t c = s[k];
+    if (c < 0x80) {
+      if (o) o[p] = c;
+      ++p;
+      ++k;
+      continue;
+    }
+    int need;
+    uint8_t lo = 0x80, hi = 0xBF;                          // bounds of the first continuation byte
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) { need = 2; lo = 0xA0; }
+    else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+    else if (c == 0xED) { need = 2; hi = 0x9F; }
+    else if (c == 0xF0) { need = 3; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) { need = 3; hi = 0x8F; }
+    else need = -1;
+    int got = 0;
+    if (need > 0) {
+      while (got < need && k + 1 + got < l) {
+        const uint8_t b = s[k + 1 + got];
+        const uint8_t blo = got == 0 ? lo : 0x80, bhi = got == 0 ? hi : 0xBF;
+        if (b < blo || b > bhi) break;
+        ++got;
+      }
+    }
+    if (need > 0 && got == need) {
+      for (int z = 0; z <= need; ++z) {
+        if (o) o[p] = s[k + z];
+        ++p;
+      }
+      k += need + 1;
+    } else {
+      if (o) { o[p] = 0xEF; o[p + 1] = 0xBF; o[p + 2] = 0xBD; }
+      p += 3;
+      k += 1 + got;
+      changed = true;
+    }
+  }
+  return p;
+}
+
+// pass 1 (dst == nullptr): clean lengths + the count of rows that change; pass 2: write at off[i]
+__global__ void utf8_clean_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                  const int32_t* __restrict__ lens, int64_t n, const int64_t* __restrict__ off,
+                                  uint8_t* __restrict__ dst, int64_t* __restrict__ out_len,
+                                  int32_t* __restrict__ changed_rows) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    bool changed = false;
+    const int64_t L = utf8_clean(arena + starts[i], lens[i], dst ? dst + off[i] : nullptr, changed);
+    if (!dst) {
+      out_len[i] = L;
+      if (changed) atomicAdd(changed_rows, 1);
+    }
+  }
+}
+
 }  // namespace
+
+DXA_API int dxa_utf8_clean(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
+                           const int64_t* off, uint8_t* dst, int64_t* out_len, int32_t* changed_rows, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(utf8_clean_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, arena, starts, lens,
+                     n, off, dst, out_len, changed_rows);
+  return (int)hipGetLastError();
+}
 
 DXA_API int dxa_fmt_slot_bytes() { return kFmtSlot; }
 DXA_API int dxa_conv_slot_bytes() { return kConvSlot; }

@@ -174,6 +174,7 @@ N.register_sigs({
     "dxa_soundex": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
     "dxa_str_decode": [c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_p],
     "dxa_split_part": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i64, c_p, c_p, c_p],
+    "dxa_utf8_clean": [c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
 })
 FMT_SLOT, CONV_SLOT = 64, 66
 
@@ -234,8 +235,7 @@ def soundex(col):
 
 
 def decode(col, mode: int):
-    """unhex (mode 0) / unbase64 (mode 1); None when an output is not ASCII (the host decodes those bytes with
-    replacement characters)."""
+    """unhex (mode 0) / unbase64 (mode 1): the decoded bytes as text (ill-formed UTF-8 → U+FFFD, utf8_clean)."""
     from ..engine.column import StrColumn
     dev, n = col.device, col.length
     lens = torch.empty(n, dtype=torch.int64, device=dev)
@@ -243,12 +243,31 @@ def decode(col, mode: int):
     bad = torch.zeros(1, dtype=torch.int32, device=dev)
     args = (N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), N.ptr(N.u8(col.valid)), n, mode)
     N.call("dxa_str_decode", *args, None, None, N.ptr(lens), N.ptr(ok), N.ptr(bad), _st(col))
-    off, total = _offsets(lens)                      # the one host read (with the flag behind it)
-    if int(bad.item()):
-        return None
+    off, total = _offsets(lens)
     dst = _alloc_arena(total, dev)
     N.call("dxa_str_decode", *args, N.ptr(off), N.ptr(dst), N.ptr(lens), N.ptr(ok), N.ptr(bad), _st(col))
-    return StrColumn(dst, off, lens.to(torch.int32), ok.view(torch.bool))
+    return utf8_clean(StrColumn(dst, off, lens.to(torch.int32), ok.view(torch.bool)))
+
+
+def utf8_clean(col):
+    """Bytes → text as Python's ``bytes.decode("utf-8", errors="replace")`` renders them: the column itself when it is
+    already well-formed UTF-8 (one read of the changed-row count), else a rewritten copy."""
+    from ..engine.column import StrColumn
+    dev, n = col.device, col.length
+    if n == 0:
+        return col
+    lens = torch.empty(n, dtype=torch.int64, device=dev)
+    changed = torch.zeros(1, dtype=torch.int32, device=dev)
+    a = (N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), n)
+    N.call("dxa_utf8_clean", *a, None, None, N.ptr(lens), N.ptr(changed), _st(col))
+    cs = torch.cumsum(lens, 0)
+    total, nchanged = torch.stack([cs[-1], changed[0].to(torch.int64)]).tolist()
+    if not nchanged:
+        return col
+    off = cs - lens
+    dst = _alloc_arena(int(total), dev)
+    N.call("dxa_utf8_clean", *a, N.ptr(off), N.ptr(dst), None, None, _st(col))
+    return StrColumn(dst, off, lens.to(torch.int32), col.valid)
 
 
 def split_part(col, delim: str, k: int):
