@@ -546,6 +546,15 @@ class LazyColumns(list):
     def _make(self, i):
         raise NotImplementedError
 
+    def prefetch(self, idxs) -> None:
+        """Resolve several entries together (subclasses batch their gathers into one launch); the default resolves
+        them one by one."""
+        for i in idxs:
+            self[i]
+
+    def _unresolved(self, idxs):
+        return [i for i in dict.fromkeys(idxs) if 0 <= i < len(self) and list.__getitem__(self, i) is None]
+
     def __getitem__(self, i):
         if isinstance(i, slice):
             return [self[j] for j in range(*i.indices(len(self)))]
@@ -556,6 +565,7 @@ class LazyColumns(list):
         return v
 
     def __iter__(self):
+        self.prefetch(range(len(self)))            # every entry will be read: resolve them together
         return (self[i] for i in range(len(self)))
 
     def __reversed__(self):

@@ -22,7 +22,8 @@ from ..sql import ast as A
 from . import functions as F
 from . import jit as _jit_mod
 from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, LazyColumns, PrimColumn, StrColumn,
-                     StructColumn, TORCH_DTYPE, and_valid, column_from_pylist, concat_columns, materialize, strings_from_pylist)
+                     StructColumn, TORCH_DTYPE, and_valid, column_from_pylist, concat_columns, materialize, strings_from_pylist,
+                     take_columns)
 from .types import (ArrayType, MapType, StructType, common_type, is_integral, is_nested, is_numeric)
 from . import decimal as D
 from .decimal import is_decimal
@@ -59,6 +60,15 @@ class TakenColumns(LazyColumns):
     def _make(self, i):
         return self._src[i].take(self._idx)
 
+    def prefetch(self, idxs) -> None:
+        todo = self._unresolved(idxs)
+        if not todo:
+            return
+        if isinstance(self._src, LazyColumns):
+            self._src.prefetch(todo)
+        for i, c in zip(todo, take_columns([self._src[i] for i in todo], self._idx)):
+            list.__setitem__(self, i, c)
+
 
 class DeferredColumns(LazyColumns):
     """A projection's output columns where the bare column references into a lazy scope stay unresolved until
@@ -71,6 +81,16 @@ class DeferredColumns(LazyColumns):
     def _make(self, i):
         src, j = self._refs[i]
         return src[j]
+
+    def prefetch(self, idxs) -> None:
+        todo = self._unresolved(idxs)
+        by_src = {}
+        for i in todo:
+            src, j = self._refs[i]
+            by_src.setdefault(id(src), (src, []))[1].append(j)
+        for src, js in by_src.values():
+            if isinstance(src, LazyColumns):
+                src.prefetch(js)
 
 
 class _Prepended(LazyColumns):
@@ -126,6 +146,32 @@ class Scope:
 
     def has_qualifier(self, q: str) -> bool:
         return q.lower() in self.qualifiers()
+
+    def index_of(self, parts: Tuple[str, ...]) -> Optional[int]:
+        """The column a reference reads (as ``resolve`` picks it), without materialising anything."""
+        if len(parts) >= 2 and self.has_qualifier(parts[0]):
+            hits = self._find(parts[1], parts[0])
+            if hits:
+                return hits[0]
+        hits = self._find(parts[0])
+        return hits[0] if hits else None
+
+    def prefetch(self, exprs) -> None:
+        """Gather together every column the expressions read from a lazy (filtered / joined) scope: one multi-column
+        gather launch instead of a take per column as each is first touched."""
+        if not isinstance(self.cols, LazyColumns):
+            return
+        idx = []
+        for e in exprs:
+            if e is None:
+                continue
+            for node in A.walk(e):
+                if isinstance(node, A.Ident):
+                    k = self.index_of(node.parts)
+                    if k is not None:
+                        idx.append(k)
+        if len(idx) > 1:
+            self.cols.prefetch(idx)
 
     def try_resolve(self, parts: Tuple[str, ...]) -> Optional[Column]:
         try:

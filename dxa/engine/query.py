@@ -20,7 +20,7 @@ from ..ops.hashing import hash_columns
 from ..sql import ast as A
 from ..sql.parser import parse_query
 from .column import (ArrayColumn, Column, ConstColumn, LazyColumns, PrimColumn, StrColumn, StructColumn, Table,
-                     concat_columns, concat_tables, materialize)
+                     concat_columns, concat_tables, materialize, take_columns)
 from .expr import (AGG_FUNCS, DeferredColumns, EvalContext, EvalError, HiddenQual, Scope, TakenColumns, cast_column,
                    evaluate, output_name, predicate_mask)
 from . import windowfn as W
@@ -775,6 +775,27 @@ class _JoinColumns(LazyColumns):
         src, j, idx, miss = self._e[i]
         return _take_nullable(src[j], idx, miss)
 
+    def prefetch(self, idxs) -> None:
+        """The requested columns of each join side in one multi-column gather; -1 (no partner) rows become nulls
+        through one shared mask."""
+        groups = {}
+        for i in self._unresolved(idxs):
+            src, j, idx, miss = self._e[i]
+            groups.setdefault((id(src), id(idx), miss), (src, idx, miss, []))[3].append(i)
+        for src, idx, miss, ii in groups.values():
+            cols = [src[self._e[i][1]] for i in ii]
+            if len(ii) < 2 or any(c.length == 0 for c in cols):
+                continue                              # single columns / empty sides: resolved on access
+            if miss:
+                gone = idx < 0
+                taken = take_columns(cols, torch.where(gone, torch.zeros_like(idx), idx))
+                keep = ~gone
+                taken = [c.with_valid(keep) for c in taken]
+            else:
+                taken = take_columns(cols, idx)
+            for i, c in zip(ii, taken):
+                list.__setitem__(self, i, c)
+
 
 # ---------------------------------------------------------------------------------------------------------------
 # SELECT
@@ -1043,10 +1064,14 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     scope = _relation(sel.from_, catalog, ctx)
     sdist = getattr(scope, "dist", P.REPLICATED)
     if sel.where is not None:
+        scope.prefetch([sel.where])
         mask = predicate_mask(evaluate(sel.where, scope, ctx))
         idx = torch.nonzero(mask).flatten()
         scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]), scope.device)
         scope.dist = sdist
+    # the columns the statement reads (bare output references excepted: they stay deferred) in one gather
+    scope.prefetch([it.expr for it in sel.items if not isinstance(it.expr, (A.Ident, A.Star))] +
+                   list(sel.group_by) + [sel.having])
     sel = _window_column_refs(sel, scope)
     sel, scope = _sliding_windows(sel, scope, ctx)
     items = _expand_items(sel, scope)

@@ -117,36 +117,62 @@ def table_from_arrow(at, schema: StructType, device) -> Table:
     return Table([f.name for f in schema.fields], cols, at.num_rows, device)
 
 
-def _pinned_copy(t: torch.Tensor, keep: list) -> torch.Tensor:
-    src = t.detach().contiguous()
-    h = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
-    h.copy_(src, non_blocking=True)
-    keep.append(src)
-    return h
-
-
 def to_host_async(t: Table):
     """Start copying a device table to pinned host memory on the current stream → (host Table, event or None).
-    The host table may only be read after ``event.synchronize()``."""
-    from ..engine.column import StructColumn, ArrayColumn, column_from_pylist
+    The host table may only be read after ``event.synchronize()``.
+
+    Every leaf buffer (data, validity, string arena / starts / lengths) is packed into one device staging buffer by
+    one concatenation launch (widest elements first, so every host view stays aligned) and crosses PCIe as ONE
+    copy, instead of a copy per buffer."""
+    from ..engine.column import column_from_pylist
     if t.device.type != "cuda":
         return t, None
-    keep: list = []
-    cols = []
+    leaves: list = []                       # device tensors to ship
+
+    def leaf(x):
+        leaves.append(x.detach().contiguous())
+        return len(leaves) - 1
+
+    plan = []
     for c in t.columns:
         c = materialize(c)
         if isinstance(c, StrColumn):
             cc = c.compact()
-            cols.append(type(cc)(_pinned_copy(cc.arena, keep), _pinned_copy(cc.starts, keep),
-                                 _pinned_copy(cc.lens, keep),
-                                 None if cc.valid is None else _pinned_copy(cc.valid, keep), cc.dtype))
+            plan.append(("str", type(cc), cc.dtype, leaf(cc.arena), leaf(cc.starts), leaf(cc.lens),
+                         None if cc.valid is None else leaf(cc.valid)))
         elif isinstance(c, PrimColumn):
-            cols.append(PrimColumn(c.dtype, _pinned_copy(c.data, keep),
-                                   None if c.valid is None else _pinned_copy(c.valid, keep)))
+            plan.append(("prim", c.dtype, leaf(c.data), None if c.valid is None else leaf(c.valid)))
         else:                                   # nested: synchronous Python round trip (rare)
-            cols.append(column_from_pylist(c.to_pylist(), c.dtype, "cpu"))
+            plan.append(("host", column_from_pylist(c.to_pylist(), c.dtype, "cpu")))
+    order = sorted(range(len(leaves)), key=lambda i: -leaves[i].element_size())
+    offs, pos = {}, 0
+    for i in order:
+        offs[i] = pos
+        pos += leaves[i].numel() * leaves[i].element_size()
+    host_buf = torch.empty(max(pos, 1), dtype=torch.uint8, pin_memory=True)
+    keep: list = []
+    if pos:
+        staged = torch.cat([leaves[i].view(torch.uint8).reshape(-1) for i in order])
+        host_buf[:pos].copy_(staged, non_blocking=True)
+        keep.append(staged)
+
+    def view(i):
+        x = leaves[i]
+        nb = x.numel() * x.element_size()
+        return host_buf[offs[i]:offs[i] + nb].view(x.dtype).view(x.shape)
+
+    cols = []
+    for p in plan:
+        if p[0] == "str":
+            _, typ, dt, a, st, ln, v = p
+            cols.append(typ(view(a), view(st), view(ln), None if v is None else view(v), dt))
+        elif p[0] == "prim":
+            _, dt, d, v = p
+            cols.append(PrimColumn(dt, view(d), None if v is None else view(v)))
+        else:
+            cols.append(p[1])
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(t.device))
     host = Table(list(t.names), cols, t.length, "cpu")
-    host._keep = keep
+    host._keep = keep + [host_buf]
     return host, ev

@@ -57,6 +57,78 @@ __global__ void hash_str_kernel(const uint8_t* __restrict__ arena, const int64_t
   }
 }
 
+// Several key columns in ONE launch: the per-column hashes above, combined in column order exactly as the
+// one-launch-per-column sequence combines them (so both paths give the same bits), and the matching equality check
+// against each row's group representative.
+constexpr int kMaxKeyCols = 16;
+enum : int32_t { KC_I64 = 0, KC_F64 = 1, KC_STR = 2 };
+
+struct KeyCol {
+  const void* data;        // int64 / double values, or the string arena
+  const int64_t* starts;
+  const int32_t* lens;
+  const uint8_t* valid;
+  int32_t kind;
+  int32_t pad;
+};
+
+struct KeyCols {
+  KeyCol c[kMaxKeyCols];
+  int32_t ncols;
+  int64_t n;
+};
+
+__device__ __forceinline__ uint64_t key_hash(const KeyCol& k, int64_t i) {
+  if (k.valid && !k.valid[i]) return dxa::kNullHash;
+  if (k.kind == KC_STR) return dxa::hash_bytes((const uint8_t*)k.data + k.starts[i], k.lens[i]);
+  if (k.kind == KC_F64) {
+    double d = ((const double*)k.data)[i];
+    if (d == 0.0) d = 0.0;
+    uint64_t bits = (uint64_t)__double_as_longlong(d);
+    if (d != d) bits = 0x7ff8000000000000ull;
+    return dxa::hash_i64(bits);
+  }
+  return dxa::hash_i64((uint64_t)((const int64_t*)k.data)[i]);
+}
+
+__global__ void hash_multi_kernel(const KeyCols a, uint64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = key_hash(a.c[0], i);
+    for (int j = 1; j < a.ncols; ++j) h = dxa::hash_combine(h, key_hash(a.c[j], i));
+    out[i] = h;
+  }
+}
+
+__device__ __forceinline__ uint64_t load_part(const uint8_t* p, int32_t avail);
+
+__global__ void verify_multi_kernel(const KeyCols a, const int32_t* __restrict__ gid, const int32_t* __restrict__ rep,
+                                    int32_t* __restrict__ bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = rep[gid[i]];
+    bool diff = false;
+    for (int j = 0; j < a.ncols && !diff; ++j) {
+      const KeyCol& k = a.c[j];
+      const bool vi = k.valid ? k.valid[i] != 0 : true;
+      const bool vr = k.valid ? k.valid[r] != 0 : true;
+      diff = vi != vr;
+      if (diff || !vi) continue;
+      if (k.kind == KC_STR) {
+        const int32_t l = k.lens[i];
+        if (l != k.lens[r]) { diff = true; continue; }
+        const uint8_t* x = (const uint8_t*)k.data + k.starts[i];
+        const uint8_t* y = (const uint8_t*)k.data + k.starts[r];
+        for (int32_t q = 0; q < l && !diff; q += 8) {
+          const int32_t av = l - q < 8 ? l - q : 8;
+          diff = load_part(x + q, av) != load_part(y + q, av);
+        }
+      } else {
+        diff = ((const int64_t*)k.data)[i] != ((const int64_t*)k.data)[r];     // bit equality (as verify_i64)
+      }
+    }
+    if (diff) atomicAdd(bad, 1);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // group-by: insert / number / gather
 // ------------------------------------------------------------------------------------------------------------
@@ -499,6 +571,87 @@ DXA_API int dxa_aggregate_multi(const int32_t* gid, int64_t n, int32_t ngroups, 
   const int64_t cells = (int64_t)ngroups * nlines * 8;
   hipLaunchKernelGGL(agg_multi_init_kernel, dim3(dxa_blocks(cells, 256)), dim3(256), 0, s, a, ngroups);
   if (n > 0) hipLaunchKernelGGL(agg_multi_kernel, dim3(dxa_blocks(n * 8, 256, 8192)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+// Finishing pass of the fused aggregates: every requested aggregate's output column from the [group][slot]
+// accumulator rows in ONE launch — counts (held as doubles) to int64, NOT-ed minima back, ordered doubles back to
+// doubles, AVG = sum / count, and the "group saw a non-null input" validity — instead of a slice/convert/compare
+// chain per aggregate.  dst_data [nreq][ngroups] (int64 or double bits), dst_valid [nreq][ngroups].
+constexpr int kMaxFinish = 64;
+enum : int { F_COUNT = 0, F_I64 = 1, F_F64 = 2, F_AVG = 3, F_F64_ORD = 4, F_NOT = 8 };
+
+struct FinishArgs {
+  const long long* acc;
+  int32_t ngroups;
+  int32_t stride;
+  int32_t nreq;
+  int32_t kind[kMaxFinish];
+  int32_t pos[kMaxFinish];
+  int32_t cnt[kMaxFinish];     // slot of the request's count (-1: none)
+  long long* dst;
+  uint8_t* valid;
+};
+
+__global__ __launch_bounds__(256) void agg_finish_kernel(FinishArgs a) {
+  const int64_t total = (int64_t)a.ngroups * a.nreq;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t / a.ngroups);
+    const int64_t g = t - (int64_t)r * a.ngroups;
+    const long long* row = a.acc + g * a.stride;
+    const int k = a.kind[r];
+    long long v = row[a.pos[r]];
+    if (k & F_NOT) v = ~v;
+    const double c = a.cnt[r] >= 0 ? __longlong_as_double(row[a.cnt[r]]) : 1.0;
+    long long o;
+    switch (k & 7) {
+      case F_COUNT: o = (long long)__longlong_as_double(v); break;
+      case F_AVG: o = __double_as_longlong(__longlong_as_double(v) / (c > 1.0 ? c : 1.0)); break;
+      case F_F64_ORD: o = v < 0 ? (v ^ 0x7fffffffffffffffll) : v; break;
+      default: o = v; break;
+    }
+    a.dst[t] = o;
+    a.valid[t] = c > 0.0 ? 1 : 0;
+  }
+}
+
+DXA_API int dxa_aggregate_finish(const void* acc, int32_t ngroups, int32_t stride, int32_t nreq, const int32_t* spec,
+                                 void* dst, uint8_t* valid, void* st) {
+  if (ngroups <= 0 || nreq <= 0) return 0;
+  if (nreq > kMaxFinish) return 1;
+  FinishArgs a{};
+  a.acc = (const long long*)acc;
+  a.ngroups = ngroups;
+  a.stride = stride;
+  a.nreq = nreq;
+  for (int r = 0; r < nreq; ++r) {
+    a.kind[r] = spec[3 * r];
+    a.pos[r] = spec[3 * r + 1];
+    a.cnt[r] = spec[3 * r + 2];
+  }
+  a.dst = (long long*)dst;
+  a.valid = valid;
+  const int64_t total = (int64_t)ngroups * nreq;
+  hipLaunchKernelGGL(agg_finish_kernel, dim3(dxa_blocks(total, 256)), dim3(256), 0, (hipStream_t)st, a);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_key_cols_size() { return (int)sizeof(KeyCols); }
+
+DXA_API int dxa_hash_multi(const void* args, uint64_t* out, void* st) {
+  const KeyCols& a = *(const KeyCols*)args;
+  if (a.n <= 0) return 0;
+  if (a.ncols <= 0 || a.ncols > kMaxKeyCols) return 1;
+  hipLaunchKernelGGL(hash_multi_kernel, dim3(dxa_blocks(a.n, 256)), dim3(256), 0, (hipStream_t)st, a, out);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_verify_multi(const void* args, const int32_t* gid, const int32_t* rep, int32_t* bad, void* st) {
+  const KeyCols& a = *(const KeyCols*)args;
+  if (a.n <= 0) return 0;
+  if (a.ncols <= 0 || a.ncols > kMaxKeyCols) return 1;
+  hipLaunchKernelGGL(verify_multi_kernel, dim3(dxa_blocks(a.n, 256)), dim3(256), 0, (hipStream_t)st, a, gid, rep,
+                     bad);
   return (int)hipGetLastError();
 }
 

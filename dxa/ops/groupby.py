@@ -8,6 +8,7 @@ grouping instead of merging distinct keys.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass
 from typing import List, Optional
@@ -17,7 +18,7 @@ import torch
 from . import native as N
 from ..engine.decimal import (aggregate as decimal_aggregate, is_decimal, key_parts as decimal_key_parts,
                               to_double as decimal_to_double)
-from .hashing import hash_columns
+from .hashing import MAX_KEY_COLS, hash_columns, key_cols
 
 INT32_MAX = 2**31 - 1
 
@@ -66,7 +67,10 @@ def group_rows(keys: List) -> Groups:
         N.call("dxa_group_ids", N.ptr(table), cap, N.ptr(slot), n, N.ptr(gid_of_slot), N.ptr(scal), N.ptr(gid),
                N.ptr(rep), st)
         bad_ptr = scal.data_ptr() + 4
-        for k in keys:
+        kc = key_cols(keys) if 2 <= len(keys) <= MAX_KEY_COLS else None
+        if kc is not None:
+            N.call("dxa_verify_multi", ctypes.byref(kc), N.ptr(gid), N.ptr(rep), bad_ptr, st)   # all keys, one launch
+        for k in ([] if kc is not None else keys):
             if isinstance(k, StrColumn):
                 N.call("dxa_verify_str", N.ptr(k.arena), N.ptr(k.starts), N.ptr(k.lens), N.ptr(N.u8(k.valid)),
                        N.ptr(gid), N.ptr(rep), n, bad_ptr, st)
@@ -253,6 +257,7 @@ def _host_minmax(groups, col, func, device):
 # ---- fused aggregation ----------------------------------------------------------------------------------------
 _MA_ADD_U64, _MA_ADD_F64, _MA_MAX = 0, 1, 2
 _MV_COUNT, _MV_I64, _MV_F64, _MV_F64_ORD, _MV_NOT = 0, 1, 2, 3, 4
+_F_COUNT, _F_I64, _F_F64, _F_AVG, _F_F64_ORD, _F_NOT = 0, 1, 2, 3, 4, 8       # hash_groupby.hip agg_finish_kernel
 _FUSABLE = ("count_star", "count", "sum", "min", "max", "avg", "mean")
 # below this many groups the per-aggregate LDS-privatised kernels win (hot lines would serialise at the memory side)
 FUSED_MIN_GROUPS = 4096
@@ -293,7 +298,7 @@ def aggregate_many(groups: Groups, reqs, n: int):
 
     plan = []
     for col, func in reqs:
-        if func not in _FUSABLE or len(slots) > _MAX_SLOTS - 3:
+        if func not in _FUSABLE or len(slots) > _MAX_SLOTS - 3 or sum(q is not None for q in plan) >= 64:
             plan.append(None)
             continue
         if func == "count_star":
@@ -357,34 +362,49 @@ def aggregate_many(groups: Groups, reqs, n: int):
     ops_t = torch.tensor(line_ops, dtype=torch.int32)
     N.call("dxa_aggregate_multi", N.ptr(gid), n, ng, nslots, spec_t.data_ptr(), nlines, ops_t.data_ptr(), N.ptr(out),
            N.stream_handle(device))
-    def col_of(i):
-        v = out[:, where[i]].contiguous()
-        kind = slots[i][2]
-        if kind == _MV_COUNT:
-            return v.view(torch.float64).to(torch.int64)
-        return ~v if kind & _MV_NOT else v
+    # one finishing launch for every fused request: output data [R][ng] + validity [R][ng]
+    fin, fin_of = [], {}
+    for ri, p in enumerate(plan):
+        if p is None:
+            continue
+        kind, s, c, dt = p
+        skind = slots[s][2]
+        if kind == "count":
+            k, cnt = _F_COUNT, -1
+        elif kind == "avg":
+            k, cnt = _F_AVG, where[c]
+        elif kind == "sum":
+            k, cnt = (_F_F64 if dt == "double" else _F_I64), (-1 if c is None else where[c])
+        else:
+            k = (_F_F64_ORD if kind == "f64" else _F_I64) | (_F_NOT if skind & _MV_NOT else 0)
+            cnt = -1 if c is None else where[c]
+        fin_of[ri] = len(fin)
+        fin.append((k, where[s], cnt))
+    dst = torch.empty((len(fin), ng), dtype=torch.int64, device=device)
+    dvalid = torch.empty((len(fin), ng), dtype=torch.uint8, device=device)
+    fspec = torch.tensor([x for f in fin for x in f], dtype=torch.int32)
+    N.call("dxa_aggregate_finish", N.ptr(out), ng, 8 * nlines, len(fin), fspec.data_ptr(), N.ptr(dst), N.ptr(dvalid),
+           N.stream_handle(device))
     res = []
-    for (col, func), p in zip(reqs, plan):
+    for ri, ((col, func), p) in enumerate(zip(reqs, plan)):
         if p is None:
             res.append(aggregate(groups, col, func, n))
             continue
         kind, s, c, dt = p
+        j = fin_of[ri]
+        v = dst[j]
+        ok = dvalid[j].view(torch.bool)
         if kind == "count":
-            res.append(PrimColumn("long", col_of(s)))
+            res.append(PrimColumn("long", v))
         elif kind == "avg":
-            cnt_t = col_of(c)
-            tot = col_of(s).view(torch.float64)
-            res.append(PrimColumn("double", tot / cnt_t.clamp(min=1).to(torch.float64), cnt_t > 0))
+            res.append(PrimColumn("double", v.view(torch.float64), ok))
+        elif kind == "sum":
+            res.append(PrimColumn(dt, v.view(torch.float64) if dt == "double" else v, None if c is None else ok))
         else:
-            v = col_of(s)
-            if kind == "sum":
-                v = v.view(torch.float64) if dt == "double" else v
-                res.append(PrimColumn(dt, v, None if c is None else col_of(c) > 0))
-            else:
-                if kind == "f64":
-                    v = _f64_from_ordered(v)
-                elif dt == "boolean":
-                    v = v.to(torch.bool)
-                res.append(PrimColumn(dt, v, None if c is None else col_of(c) > 0))
+            if kind == "f64":
+                v = v.view(torch.float64)
+            elif dt == "boolean":
+                v = v.to(torch.bool)
+            res.append(PrimColumn(dt, v, None if c is None else ok))
     del keep
     return res

@@ -5,6 +5,7 @@ functions so GPU results can be differential-tested against it.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List
 
 import numpy as np
@@ -84,6 +85,57 @@ def _col_hash_np(col) -> np.ndarray:
     return out
 
 
+MAX_KEY_COLS = 16
+_KC_I64, _KC_F64, _KC_STR = 0, 1, 2
+
+
+class _KeyCol(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("starts", ctypes.c_void_p), ("lens", ctypes.c_void_p),
+                ("valid", ctypes.c_void_p), ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class _KeyCols(ctypes.Structure):
+    _fields_ = [("c", _KeyCol * MAX_KEY_COLS), ("ncols", ctypes.c_int32), ("n", ctypes.c_int64)]
+
+
+N.register_sigs({"dxa_key_cols_size": [], "dxa_hash_multi": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+                 "dxa_verify_multi": [ctypes.c_void_p] * 5})
+
+
+def key_cols(cols):
+    """By-value descriptor of materialised device key columns for the fused hash / verify kernels (None when a
+    column is not a plain string / 8-byte column).  The descriptor keeps the tensors it points at alive."""
+    from ..engine.column import PrimColumn, StrColumn
+    if N.lib().dxa_key_cols_size() != ctypes.sizeof(_KeyCols):
+        raise N.NativeError("KeyCols layout mismatch between hashing.py and hash_groupby.hip")
+    a = _KeyCols()
+    keep = []
+    for j, c in enumerate(cols):
+        v = N.u8(c.valid)
+        if v is not None:
+            v = v.contiguous()
+            keep.append(v)
+        if isinstance(c, StrColumn):
+            st, ln = c.starts, c.lens
+            if st.dtype != torch.int64 or ln.dtype != torch.int32:
+                return None
+            a.c[j] = _KeyCol(c.arena.data_ptr(), st.data_ptr(), ln.data_ptr(), 0 if v is None else v.data_ptr(),
+                             _KC_STR, 0)
+        elif isinstance(c, PrimColumn) and c.data.dim() == 1:
+            d = c.data
+            kind = _KC_F64 if d.dtype == torch.float64 else _KC_I64
+            if d.dtype not in (torch.float64, torch.int64):
+                d = d.to(torch.int64)
+            d = d.contiguous()
+            keep.append(d)
+            a.c[j] = _KeyCol(d.data_ptr(), None, None, 0 if v is None else v.data_ptr(), kind, 0)
+        else:
+            return None
+    a.ncols, a.n = len(cols), cols[0].length
+    a._keep = keep
+    return a
+
+
 def hash_columns(cols: List) -> torch.Tensor:
     """64-bit row hash over one or more key columns → int64 tensor (bit pattern of the uint64 hash)."""
     from ..engine.column import PrimColumn, StrColumn, materialize
@@ -97,6 +149,11 @@ def hash_columns(cols: List) -> torch.Tensor:
         if n == 0:
             return out
         st = N.stream_handle(device)
+        if 2 <= len(cols) <= MAX_KEY_COLS:
+            kc = key_cols([materialize(c) for c in cols])
+            if kc is not None:
+                N.call("dxa_hash_multi", ctypes.byref(kc), N.ptr(out), st)     # every key column, one launch
+                return out
         for j, c in enumerate(cols):
             c = materialize(c)
             comb = 1 if j else 0
