@@ -668,14 +668,28 @@ def concat_tables(tables: List[Table]) -> Table:
     if len(tables) == 1:
         return tables[0]
     names = tables[0].names
+    device = tables[0].device
+    batched = torch.device(device).type == "cuda"
+    segs = []
     cols = []
     for i, n in enumerate(names):
         parts = []
         for t in tables:
             c = t.column(n) if t.names[i].lower() != n.lower() else t.columns[i]
             parts.append(c)
+        if batched and all(isinstance(c, PrimColumn) for c in parts):
+            from ..ops.copybatch import concat_prims
+            got = concat_prims(parts, device)
+            if got is not None:
+                data, valid, sg = got
+                segs.extend(sg)
+                cols.append(PrimColumn(parts[0].dtype, data, valid))
+                continue
         cols.append(concat_columns(parts))
-    return Table(names, cols, sum(t.length for t in tables), tables[0].device)
+    if segs:
+        from ..ops.copybatch import copy_batch
+        copy_batch(segs, device)                    # every fixed-width column of every table: one launch
+    return Table(names, cols, sum(t.length for t in tables), device)
 
 
 def _h2d(data, dtype, device):

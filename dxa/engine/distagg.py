@@ -8,6 +8,7 @@ still one exchange, just a bigger one.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -102,6 +103,60 @@ def _finish(call: A.Call, merged: Dict[str, PrimColumn]) -> PrimColumn:
     return PrimColumn("double", out, c > (0 if pop else 1))
 
 
+class _PFReq(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("valid", ctypes.c_void_p), ("cnt", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("out_valid", ctypes.c_void_p), ("kind", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
+class _PFArgs(ctypes.Structure):
+    _fields_ = [("r", _PFReq * 32), ("nreq", ctypes.c_int32), ("n", ctypes.c_int64)]
+
+
+def _finish_all(aggs: Dict, merged_by: Dict, ng: int, dev) -> Dict:
+    """Every aggregate's final column; on the GPU the SUM / MIN / MAX validity and the AVG division of all of them
+    run in one launch (``dxa_partial_finish``) instead of a compare / divide chain per aggregate."""
+    out = {}
+    reqs = []
+    for ak, call in aggs.items():
+        m = merged_by[ak]
+        simple = ("v" in m and "cnt" in m and call.name not in ("bool_and", "every", "bool_or", "any", "some")
+                  and len(m) == 2)
+        avg = call.name in ("avg", "mean") and set(m) == {"s", "cnt"}
+        if dev.type == "cuda" and ng and (simple or avg) and len(reqs) < 32:
+            v = m["v"] if simple else m["s"]
+            c = m["cnt"]
+            if v.data.dim() == 1 and v.data.element_size() == 8 and c.data.dtype == torch.int64:
+                reqs.append((ak, call, simple, v, c))
+                continue
+        out[ak] = _finish(call, m)
+    if reqs:
+        from ..ops import native as N
+        if N.lib().dxa_partial_finish_size() != ctypes.sizeof(_PFArgs):
+            raise N.NativeError("PartialFinishArgs layout mismatch between distagg.py and hash_groupby.hip")
+        a = _PFArgs()
+        keep = []
+        valid_all = torch.empty((len(reqs), ng), dtype=torch.uint8, device=dev)
+        avg_out = torch.empty((sum(1 for r in reqs if not r[2]), ng), dtype=torch.float64, device=dev)
+        k_avg = 0
+        for j, (ak, call, simple, v, c) in enumerate(reqs):
+            d = v.data.contiguous()
+            cc = c.data.contiguous()
+            vv = N.u8(v.valid) if simple else None             # AVG: NULL exactly when the count is 0
+            keep += [d, cc] + ([vv] if vv is not None else [])
+            o = avg_out[k_avg] if not simple else None
+            a.r[j] = _PFReq(d.data_ptr(), 0 if vv is None else vv.data_ptr(), cc.data_ptr(),
+                            0 if o is None else o.data_ptr(), valid_all[j].data_ptr(), 0 if simple else 1, 0)
+            if simple:
+                out[ak] = PrimColumn(v.dtype, v.data, valid_all[j].view(torch.bool))
+            else:
+                out[ak] = PrimColumn("double", avg_out[k_avg], valid_all[j].view(torch.bool))
+                k_avg += 1
+        a.nreq, a.n = len(reqs), ng
+        N.call("dxa_partial_finish", ctypes.byref(a), N.stream_handle(dev))
+    return {ak: out[ak] for ak in aggs}
+
+
 def _one_group(n, dev):
     return G.Groups(torch.zeros(n, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
                     torch.zeros(1, dtype=torch.int64, device=dev))
@@ -169,7 +224,7 @@ def merge_partials(got: Table, plan, key_names: List[str], aggs: Dict, grouped: 
     merged_by = {ak: {} for ak in aggs}
     for (ak, _, suffix, _), v in zip(entries, vals):
         merged_by[ak][suffix] = v
-    finals = {ak: _finish(call, merged_by[ak]) for ak, call in aggs.items()}
+    finals = _finish_all(aggs, merged_by, ng, dev)
     return out_keys, finals, ng
 
 

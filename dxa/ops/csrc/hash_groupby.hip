@@ -655,6 +655,49 @@ DXA_API int dxa_verify_multi(const void* args, const int32_t* gid, const int32_t
   return (int)hipGetLastError();
 }
 
+// Final step of merged partial aggregates (distributed / windowed GROUP BY, engine/distagg.py) for many aggregates
+// in ONE launch: SUM / MIN / MAX keep their merged data and become NULL where no input row was non-null
+// (valid = own validity & count > 0); AVG = sum / max(count, 1) with the same validity.
+constexpr int kMaxPartialFinish = 32;
+struct PartialFinishReq {
+  const long long* data;     // merged value (int64 or double bits)
+  const uint8_t* valid;      // its validity (null: all valid)
+  const long long* cnt;      // merged count
+  long long* out;            // AVG result (double bits); unused for kind 0
+  uint8_t* out_valid;
+  int32_t kind;              // 0 value-by-count, 1 average
+  int32_t pad;
+};
+struct PartialFinishArgs {
+  PartialFinishReq r[kMaxPartialFinish];
+  int32_t nreq;
+  int64_t n;
+};
+
+__global__ __launch_bounds__(256) void partial_finish_kernel(PartialFinishArgs a) {
+  const int64_t total = a.n * a.nreq;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t / a.n);
+    const int64_t i = t - (int64_t)q * a.n;
+    const PartialFinishReq& r = a.r[q];
+    const long long c = r.cnt[i];
+    const bool ok = c > 0 && (r.valid == nullptr || r.valid[i] != 0);
+    if (r.kind == 1)
+      r.out[i] = __double_as_longlong(__longlong_as_double(r.data[i]) / (double)(c > 1 ? c : 1));
+    r.out_valid[i] = ok ? 1 : 0;
+  }
+}
+
+DXA_API int dxa_partial_finish_size() { return (int)sizeof(PartialFinishArgs); }
+
+DXA_API int dxa_partial_finish(const void* args, void* st) {
+  const PartialFinishArgs& a = *(const PartialFinishArgs*)args;
+  if (a.n <= 0 || a.nreq <= 0) return 0;
+  if (a.nreq > kMaxPartialFinish) return 1;
+  hipLaunchKernelGGL(partial_finish_kernel, dim3(dxa_blocks(a.n * a.nreq, 256)), dim3(256), 0, (hipStream_t)st, a);
+  return (int)hipGetLastError();
+}
+
 DXA_API int dxa_slot_count(const int32_t* slot_of_row, int64_t n, int32_t* cnt, void* st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(slot_count_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, slot_of_row, n, cnt);

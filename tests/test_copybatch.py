@@ -1,0 +1,60 @@
+"""Batched device copies (dxa/ops/csrc/copy_batch.hip) and the one-launch table concatenation built on them,
+against torch.cat of the same tensors."""
+import pytest
+import torch
+
+from dxa.engine.column import PrimColumn, Table, concat_tables, strings_from_pylist
+
+
+@pytest.mark.gpu
+def test_copy_batch_segments_and_fills():
+    from dxa.ops.copybatch import copy_batch
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(3)
+    srcs = [torch.randint(0, 255, (n,), generator=g, dtype=torch.uint8).to(dev) for n in (1, 7, 16, 33, 70_000,
+                                                                                          200_003)]
+    total = sum(s.numel() for s in srcs) + 5 + 64
+    dst = torch.zeros(total, dtype=torch.uint8, device=dev)
+    segs, pos, want = [], 0, []
+    for s in srcs:
+        segs.append((s, 0, dst, pos, s.numel(), 0))
+        want.append(s.cpu())
+        pos += s.numel()
+    segs.append((None, 0, dst, pos, 5, 0xAB))            # a fill
+    want.append(torch.full((5,), 0xAB, dtype=torch.uint8))
+    pos += 5
+    segs.append((srcs[4], 3, dst, pos, 64, 0))            # an unaligned slice
+    want.append(srcs[4][3:67].cpu())
+    copy_batch(segs, dev)
+    assert torch.equal(dst.cpu(), torch.cat(want))
+
+
+@pytest.mark.gpu
+def test_concat_tables_one_launch_matches_cat():
+    from launch_count import count_launches
+    dev = torch.device("cuda")
+    tabs = []
+    for k, n in enumerate((3, 0, 1000, 17, 4096)):
+        a = PrimColumn("long", torch.arange(n, device=dev) * (k + 1))
+        b = PrimColumn("double", torch.rand(n, dtype=torch.float64, device=dev),
+                       None if k % 2 else torch.rand(n, device=dev) > 0.3)
+        c = PrimColumn("boolean", torch.rand(n, device=dev) > 0.5)
+        w = PrimColumn("decimal(38,2)", torch.randint(-99, 99, (n, 2), device=dev))
+        tabs.append(Table(["a", "b", "c", "w"], [a, b, c, w], n, dev))
+    with count_launches() as log:
+        out = concat_tables(tabs)
+    assert log.count("dxa_copy_batch") == 1 and not any(x.startswith("cat") for x in log), log
+    for j, nm in enumerate(["a", "b", "c", "w"]):
+        want = torch.cat([t.columns[j].data for t in tabs])
+        assert torch.equal(out.columns[j].data, want), nm
+    vb = torch.cat([t.columns[1].valid_mask() for t in tabs])
+    assert torch.equal(out.columns[1].valid, vb)
+    assert out.columns[0].valid is None and out.length == sum(t.length for t in tabs)
+
+
+def test_concat_tables_cpu_strings_and_prims():
+    t1 = Table(["s", "x"], [strings_from_pylist(["a", None], "cpu"), PrimColumn("long", torch.tensor([1, 2]))], 2, "cpu")
+    t2 = Table(["s", "x"], [strings_from_pylist(["bb"], "cpu"), PrimColumn("long", torch.tensor([3]),
+                                                                     torch.tensor([False]))], 1)
+    out = concat_tables([t1, t2])
+    assert out.columns[0].to_pylist() == ["a", None, "bb"] and out.columns[1].to_pylist() == [1, 2, None]

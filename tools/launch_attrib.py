@@ -23,12 +23,18 @@ CPU_MODE = "--device" in sys.argv and "cpu" in sys.argv
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+DEPTH = int(os.environ.get("ATTRIB_DEPTH", "1"))
+
+
 def _site(skip_native=False):
+    out = []
     for fr in reversed(traceback.extract_stack()[:-2]):
         f = fr.filename
         if "/dxa/" in f and not f.endswith("launch_attrib.py") and not (skip_native and f.endswith("native.py")):
-            return f"{os.path.relpath(f, ROOT)}:{fr.lineno} {fr.name}"
-    return "<other>"
+            out.append(f"{os.path.relpath(f, ROOT).replace('dxa/', '')}:{fr.lineno} {fr.name}")
+            if len(out) >= DEPTH:
+                break
+    return " < ".join(out) if out else "<other>"
 
 
 # ATen ops that only make views / allocate: no kernel launch
