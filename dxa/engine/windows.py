@@ -157,6 +157,31 @@ class PanedTable(Table):
         return t
 
 
+_TS_SCRATCH: Dict = {}
+
+
+def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int) -> List[int]:
+    """[min, max, count] of the valid timestamps and the count of valid ones >= E — one reduction launch and one
+    4-word read on the GPU (reduce_stats.hip), tensor ops on the CPU."""
+    if ts.is_cuda and ts.numel():
+        from ..ops import native as N
+        dev = ts.device
+        scratch = _TS_SCRATCH.get(dev)
+        if scratch is None:
+            N.register_sigs({"dxa_ts_stats_scratch_bytes": [],
+                             "dxa_ts_stats": [N.c_p, N.c_p, N.c_i64, N.c_i64, N.c_p, N.c_p, N.c_p]})
+            scratch = _TS_SCRATCH[dev] = torch.zeros(N.lib().dxa_ts_stats_scratch_bytes(), dtype=torch.uint8,
+                                                     device=dev)
+        out = torch.empty(4, dtype=torch.int64, device=dev)
+        N.call("dxa_ts_stats", N.ptr(ts.contiguous()), N.ptr(N.u8(ok.contiguous())), ts.numel(), int(E),
+               N.ptr(scratch), N.ptr(out), N.stream_handle(dev))
+        return out.tolist()
+    big = torch.iinfo(torch.int64).max
+    return torch.stack([torch.where(ok, ts, torch.full_like(ts, big)).min(),
+                        torch.where(ok, ts, torch.full_like(ts, -big)).max(),
+                        ok.sum(), (ok & (ts >= E)).sum()]).tolist()
+
+
 class WindowStore:
     def __init__(self, conf: TimeWindowConf):
         self.conf = conf
@@ -192,10 +217,7 @@ class WindowStore:
         if t.length == 0:
             return Pane(key, t, 0, -1, True)
         ts, ok = self._ts(t)
-        big = torch.iinfo(torch.int64).max
-        stats = torch.stack([torch.where(ok, ts, torch.full_like(ts, big)).min(),
-                             torch.where(ok, ts, torch.full_like(ts, -big)).max(),
-                             ok.sum()]).tolist()
+        stats = _ts_stats(ts, ok, 0)
         return Pane(key, t, int(stats[0]), int(stats[1]), int(stats[2]) == t.length)
 
     def process(self, projected: Table, batch_time_us: int, interval_us: int):
@@ -208,10 +230,7 @@ class WindowStore:
             # one host read for the common case (every event valid and not late): the batch's pane statistics and
             # the late-event check come back together; otherwise filter, then take the kept rows' statistics
             ts, ok = self._ts(projected)
-            big = torch.iinfo(torch.int64).max
-            lo_, hi_, nok, nkeep = torch.stack([torch.where(ok, ts, torch.full_like(ts, big)).min(),
-                                                torch.where(ok, ts, torch.full_like(ts, -big)).max(),
-                                                ok.sum(), (ok & (ts >= E)).sum()]).tolist()
+            lo_, hi_, nok, nkeep = _ts_stats(ts, ok, E)
             if int(nkeep) == projected.length:
                 kept = _compact_table(projected)
                 cur = Pane(batch_time_us, kept, int(lo_), int(hi_), True)

@@ -1,0 +1,104 @@
+// Event-time statistics of a batch in ONE launch (engine/windows.py: a window pane's time span and the late-event
+// check): min and max of the valid timestamps, the valid count and the count of valid timestamps >= E.  A
+// grid-stride pass reduces per workgroup (wave shuffles + LDS), and the last workgroup to finish (a ticket counter
+// that it resets to zero for the next launch) folds the per-workgroup partials — no zero-fill launch, no second
+// kernel.  The caller reads the 4 results back with one copy.
+#include "dxa_common.h"
+
+namespace {
+
+constexpr int kBlocks = 256;
+constexpr int kThreads = 256;
+
+struct Stat {
+  long long mn, mx, cnt, keep;
+};
+
+__device__ __forceinline__ Stat combine(Stat a, Stat b) {
+  Stat r;
+  r.mn = a.mn < b.mn ? a.mn : b.mn;
+  r.mx = a.mx > b.mx ? a.mx : b.mx;
+  r.cnt = a.cnt + b.cnt;
+  r.keep = a.keep + b.keep;
+  return r;
+}
+
+__device__ __forceinline__ Stat wave_reduce(Stat s) {
+  for (int o = 32; o > 0; o >>= 1) {
+    Stat t;
+    t.mn = __shfl_down(s.mn, o, 64);
+    t.mx = __shfl_down(s.mx, o, 64);
+    t.cnt = __shfl_down(s.cnt, o, 64);
+    t.keep = __shfl_down(s.keep, o, 64);
+    s = combine(s, t);
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(kThreads) void ts_stats_kernel(const int64_t* __restrict__ ts,
+                                                            const uint8_t* __restrict__ valid, int64_t n,
+                                                            int64_t E, long long* __restrict__ part,
+                                                            unsigned int* __restrict__ ticket,
+                                                            long long* __restrict__ out) {
+  const long long BIG = 0x7fffffffffffffffll;
+  Stat s{BIG, -BIG, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    const long long t = ts[i];
+    s.mn = t < s.mn ? t : s.mn;
+    s.mx = t > s.mx ? t : s.mx;
+    s.cnt += 1;
+    s.keep += t >= E ? 1 : 0;
+  }
+  s = wave_reduce(s);
+  __shared__ Stat w[kThreads / 64];
+  __shared__ bool last;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) w[wid] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Stat b = w[0];
+    for (int k = 1; k < (int)(blockDim.x / 64); ++k) b = combine(b, w[k]);
+    long long* p = part + 4 * blockIdx.x;
+    p[0] = b.mn;
+    p[1] = b.mx;
+    p[2] = b.cnt;
+    p[3] = b.keep;
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (threadIdx.x == 0) {
+    Stat r{BIG, -BIG, 0, 0};
+    for (unsigned b = 0; b < gridDim.x; ++b) {
+      const volatile long long* p = part + 4 * b;
+      Stat x{p[0], p[1], p[2], p[3]};
+      r = combine(r, x);
+    }
+    out[0] = r.mn;
+    out[1] = r.mx;
+    out[2] = r.cnt;
+    out[3] = r.keep;
+    atomicExch(ticket, 0u);                                // ready for the next launch (stream-ordered)
+  }
+}
+
+}  // namespace
+
+DXA_API int dxa_ts_stats_scratch_bytes() { return kBlocks * 4 * 8 + 64; }
+
+// scratch: dxa_ts_stats_scratch_bytes() bytes, zero-initialised once by the caller and reused launch after launch
+// on one stream.  out: [4] int64 = min, max, valid count, count(valid & ts >= E).
+DXA_API int dxa_ts_stats(const int64_t* ts, const uint8_t* valid, int64_t n, int64_t E, void* scratch,
+                         long long* out, void* st) {
+  long long* part = (long long*)scratch;
+  unsigned int* ticket = (unsigned int*)((char*)scratch + kBlocks * 4 * 8);
+  int64_t blocks = (n + kThreads - 1) / kThreads;
+  if (blocks > kBlocks) blocks = kBlocks;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(ts_stats_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)st, ts, valid, n, E,
+                     part, ticket, out);
+  return (int)hipGetLastError();
+}
