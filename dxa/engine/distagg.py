@@ -126,7 +126,8 @@ def _finish_all(aggs: Dict, merged_by: Dict, ng: int, dev) -> Dict:
         if dev.type == "cuda" and ng and (simple or avg) and len(reqs) < 32:
             v = m["v"] if simple else m["s"]
             c = m["cnt"]
-            if v.data.dim() == 1 and v.data.element_size() == 8 and c.data.dtype == torch.int64:
+            if (isinstance(v, PrimColumn) and isinstance(c, PrimColumn) and v.data.dim() == 1
+                    and v.data.element_size() == 8 and c.data.dtype == torch.int64):
                 reqs.append((ak, call, simple, v, c))
                 continue
         out[ak] = _finish(call, m)

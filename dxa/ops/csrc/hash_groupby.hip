@@ -698,6 +698,58 @@ DXA_API int dxa_partial_finish(const void* args, void* st) {
   return (int)hipGetLastError();
 }
 
+// Group ids in first-occurrence order (the CPU reference's numbering): the groups' representative rows (their
+// first row) are sorted in one workgroup — a bitonic sort of (row << 32 | group) keys in LDS, up to kRenumberMax
+// groups — giving each group its rank, then one pass rewrites the row → group map.  Replaces an argsort and four
+// indexing launches.
+constexpr int kRenumberMax = 4096;
+
+__global__ __launch_bounds__(1024) void renumber_sort_kernel(const int32_t* __restrict__ rep, int32_t ng,
+                                                             int32_t* __restrict__ inv, int64_t* __restrict__ rep_out) {
+  __shared__ unsigned long long k[kRenumberMax];
+  int m = 1;
+  while (m < ng) m <<= 1;
+  for (int i = threadIdx.x; i < m; i += blockDim.x)
+    k[i] = i < ng ? (((unsigned long long)(uint32_t)rep[i]) << 32) | (uint32_t)i : ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= m; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const unsigned long long a = k[i], b = k[j];
+          if ((a > b) == up) { k[i] = b; k[j] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int p = threadIdx.x; p < ng; p += blockDim.x) {
+    const unsigned long long v = k[p];
+    inv[(int32_t)(v & 0xffffffffu)] = p;
+    rep_out[p] = (int64_t)(v >> 32);
+  }
+}
+
+__global__ void renumber_rows_kernel(int32_t* __restrict__ gid, int64_t n, const int32_t* __restrict__ inv) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    gid[i] = inv[gid[i]];
+}
+
+DXA_API int dxa_group_renumber_max() { return kRenumberMax; }
+
+// gid: [n] int32 rewritten in place; rep: [ng] int32 first rows; inv: [ng] int32 scratch; rep_out: [ng] int64
+DXA_API int dxa_group_renumber(int32_t* gid, int64_t n, const int32_t* rep, int32_t ng, int32_t* inv,
+                               int64_t* rep_out, void* st) {
+  if (ng <= 0) return 0;
+  if (ng > kRenumberMax) return 1;
+  hipStream_t s = (hipStream_t)st;
+  hipLaunchKernelGGL(renumber_sort_kernel, dim3(1), dim3(1024), 0, s, rep, ng, inv, rep_out);
+  if (n > 0) hipLaunchKernelGGL(renumber_rows_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, s, gid, n, inv);
+  return (int)hipGetLastError();
+}
+
 DXA_API int dxa_slot_count(const int32_t* slot_of_row, int64_t n, int32_t* cnt, void* st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(slot_count_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, slot_of_row, n, cnt);

@@ -82,6 +82,11 @@ def group_rows(keys: List) -> Groups:
         ng, bad = scal.tolist()
         if bad:
             return _exact_groups(keys, device)
+        if 0 < ng <= _RENUMBER_MAX:
+            inv = torch.empty(ng, dtype=torch.int32, device=device)
+            rep_out = torch.empty(ng, dtype=torch.int64, device=device)
+            N.call("dxa_group_renumber", N.ptr(gid), n, N.ptr(rep), ng, N.ptr(inv), N.ptr(rep_out), st)
+            return Groups(gid, ng, rep_out)
         rep = rep[:ng].to(torch.int64)
         order = torch.argsort(rep)
         inv = torch.empty(ng, dtype=torch.int32, device=device)
@@ -256,6 +261,7 @@ def _host_minmax(groups, col, func, device):
 
 # ---- fused aggregation ----------------------------------------------------------------------------------------
 _MA_ADD_U64, _MA_ADD_F64, _MA_MAX = 0, 1, 2
+_RENUMBER_MAX = 4096          # hash_groupby.hip kRenumberMax: one-workgroup bitonic renumbering
 _MV_COUNT, _MV_I64, _MV_F64, _MV_F64_ORD, _MV_NOT = 0, 1, 2, 3, 4
 _F_COUNT, _F_I64, _F_F64, _F_AVG, _F_F64_ORD, _F_NOT = 0, 1, 2, 3, 4, 8       # hash_groupby.hip agg_finish_kernel
 _FUSABLE = ("count_star", "count", "sum", "min", "max", "avg", "mean")

@@ -10,5 +10,5 @@ for f in window full; do
   ATTRIB_DEPTH=3 timeout -k 10 400 python tools/launch_attrib.py --flow $f --batches 6 --top 80 > gpurun_out/r4j/attrib_$f.txt 2>&1 || { tail -20 gpurun_out/r4j/attrib_$f.txt; exit 1; }
   head -3 gpurun_out/r4j/attrib_$f.txt | tail -1
 done
-timeout -k 10 900 python -u -m pytest tests/test_copybatch.py tests/test_packing.py tests/test_strfuncs.py tests/test_decimal.py tests/test_flows_gpu.py tests/test_distributed.py tests/test_jit.py -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r4j/tests.log 2>&1 || { grep -E "PASS|FAIL|Error" gpurun_out/r4j/tests.log | tail -30; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_window_stats.py tests/test_copybatch.py tests/test_packing.py tests/test_strfuncs.py tests/test_decimal.py tests/test_flows_gpu.py tests/test_distributed.py tests/test_jit.py -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/r4j/tests.log 2>&1 || { grep -E "PASS|FAIL|Error" gpurun_out/r4j/tests.log | tail -30; exit 1; }
 tail -1 gpurun_out/r4j/tests.log
