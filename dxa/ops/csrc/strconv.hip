@@ -263,6 +263,9 @@ __global__ void decode_kernel(const uint8_t* __restrict__ arena, const int64_t* 
       if (!write) { out_len[i] = 0; ovalid[i] = 0; }
       continue;
     }
+    // a row the length pass rejected owns no output bytes: decoding its valid prefix would write into the next
+    // row's slot
+    if (write && !ovalid[i]) continue;
     const uint8_t* s = arena + starts[i];
     const int32_t l = lens[i];
     uint8_t* o = write ? dst + off[i] : nullptr;
