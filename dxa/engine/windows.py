@@ -158,12 +158,13 @@ class PanedTable(Table):
 
 
 _TS_SCRATCH: Dict = {}
+_TS_KERNEL = __import__("os").environ.get("DXA_TS_STATS_KERNEL", "1") != "0"          # A/B switch
 
 
 def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int) -> List[int]:
     """[min, max, count] of the valid timestamps and the count of valid ones >= E — one reduction launch and one
     4-word read on the GPU (reduce_stats.hip), tensor ops on the CPU."""
-    if ts.is_cuda and ts.numel():
+    if ts.is_cuda and ts.numel() and _TS_KERNEL:
         from ..ops import native as N
         dev = ts.device
         scratch = _TS_SCRATCH.get(dev)

@@ -82,7 +82,7 @@ def group_rows(keys: List) -> Groups:
         ng, bad = scal.tolist()
         if bad:
             return _exact_groups(keys, device)
-        if 0 < ng <= _RENUMBER_MAX:
+        if 0 < ng <= _RENUMBER_MAX and _RENUMBER_KERNEL:
             inv = torch.empty(ng, dtype=torch.int32, device=device)
             rep_out = torch.empty(ng, dtype=torch.int64, device=device)
             N.call("dxa_group_renumber", N.ptr(gid), n, N.ptr(rep), ng, N.ptr(inv), N.ptr(rep_out), st)
@@ -262,6 +262,7 @@ def _host_minmax(groups, col, func, device):
 # ---- fused aggregation ----------------------------------------------------------------------------------------
 _MA_ADD_U64, _MA_ADD_F64, _MA_MAX = 0, 1, 2
 _RENUMBER_MAX = 4096          # hash_groupby.hip kRenumberMax: one-workgroup bitonic renumbering
+_RENUMBER_KERNEL = __import__("os").environ.get("DXA_RENUMBER_KERNEL", "1") != "0"        # A/B switch
 _MV_COUNT, _MV_I64, _MV_F64, _MV_F64_ORD, _MV_NOT = 0, 1, 2, 3, 4
 _F_COUNT, _F_I64, _F_F64, _F_AVG, _F_F64_ORD, _F_NOT = 0, 1, 2, 3, 4, 8       # hash_groupby.hip agg_finish_kernel
 _FUSABLE = ("count_star", "count", "sum", "min", "max", "avg", "mean")
