@@ -340,6 +340,23 @@ __global__ void i64_write_kernel(const int64_t* __restrict__ v, int64_t n, const
   }
 }
 
+// CAST(long AS STRING) into fixed 24-byte slots (an int64 prints in at most 20 bytes): one launch, no length pass,
+// no scan and no host read of the total size.
+__global__ void i64_slot_kernel(const int64_t* __restrict__ v, int64_t n, uint8_t* __restrict__ dst,
+                                int64_t* __restrict__ starts, int32_t* __restrict__ lens) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = v[i];
+    const int nd = i64_digits(x);
+    uint8_t* d = dst + i * 24;
+    uint64_t u = x < 0 ? (0ull - (uint64_t)x) : (uint64_t)x;
+    int p = nd - 1;
+    do { d[p--] = (uint8_t)('0' + u % 10); u /= 10; } while (u);
+    if (x < 0) d[0] = '-';
+    starts[i] = i * 24;
+    lens[i] = nd;
+  }
+}
+
 // mode 0: lower, 1: upper (ASCII; bytes ≥ 0x80 untouched, matching Spark for ASCII data)
 __global__ void case_map_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
                                 const int32_t* __restrict__ lens, int64_t n, const int64_t* __restrict__ off,
@@ -1239,6 +1256,13 @@ DXA_API int dxa_i64_to_str_len(const int64_t* v, int64_t n, int64_t* out_len, vo
 DXA_API int dxa_i64_to_str_write(const int64_t* v, int64_t n, const int64_t* off, uint8_t* dst, void* st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(i64_write_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, n, off, dst);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_i64_to_str_slots(const int64_t* v, int64_t n, uint8_t* dst, int64_t* starts, int32_t* lens, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(i64_slot_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, v, n, dst, starts,
+                     lens);
   return (int)hipGetLastError();
 }
 

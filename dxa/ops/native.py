@@ -98,6 +98,7 @@ _SIGS = {
     "dxa_concat_part_size": [],
     "dxa_i64_to_str_len": [c_p, c_i64, c_p, c_p],
     "dxa_i64_to_str_write": [c_p, c_i64, c_p, c_p, c_p],
+    "dxa_i64_to_str_slots": [c_p, c_i64, c_p, c_p, c_p, c_p],
     "dxa_case_map": [c_p, c_p, c_p, c_i64, c_p, c_p, ctypes.c_int, c_p],
     "dxa_str_to_ts": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
     "dxa_datagen_op_size": [],

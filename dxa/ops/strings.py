@@ -374,8 +374,14 @@ def concat_strings(parts: List[Union[str, object]], n: int, device):
         ok = torch.empty(n, dtype=torch.bool, device=device)
         st = N.stream_handle(device)
         N.call("dxa_concat_len", N.ptr(raw), len(parts), n, N.ptr(lens), N.ptr(ok.view(torch.uint8)), st)
-        off, total = _offsets(lens)
-        dst = _alloc_arena(total, device)
+        bound = _concat_bound(parts, n)
+        if bound is not None:
+            # every part has a known per-row maximum (literals, fixed-slot conversions): allocate that, no host read
+            off = torch.cumsum(lens, 0) - lens if n else lens
+            dst = _alloc_arena(bound, device)
+        else:
+            off, total = _offsets(lens)
+            dst = _alloc_arena(total, device)
         N.call("dxa_concat_write", N.ptr(raw), len(parts), n, N.ptr(off), N.ptr(ok.view(torch.uint8)), N.ptr(dst), st)
         valid = None if all(isinstance(p, str) or p.valid is None for p in parts) else ok
         col = StrColumn(dst, off, lens.to(torch.int32), valid)
@@ -397,6 +403,20 @@ def concat_strings(parts: List[Union[str, object]], n: int, device):
         out.append(None if null else "".join(s))
     from ..engine.column import strings_from_pylist
     return strings_from_pylist(out, device)
+
+
+def _concat_bound(parts, n: int):
+    """Upper bound of a CONCAT's total bytes when every column part carries ``_max_len`` (bytes per row)."""
+    tot = 0
+    for p in parts:
+        if isinstance(p, str):
+            tot += len(p.encode("utf-8"))
+        else:
+            m = getattr(p, "_max_len", None)
+            if m is None:
+                return None
+            tot += m
+    return tot * n
 
 
 def concat_ws(sep: str, parts: List[Union[str, object]], n: int, device):
@@ -435,13 +455,16 @@ def from_int64(data: torch.Tensor, valid):
     from ..engine.column import StrColumn, strings_from_pylist
     n = data.shape[0]
     if _gpu(data):
-        st = N.stream_handle(data.device)
-        lens = torch.empty(n, dtype=torch.int64, device=data.device)
-        N.call("dxa_i64_to_str_len", N.ptr(data), n, N.ptr(lens), st)
-        off, total = _offsets(lens)
-        dst = _alloc_arena(total, data.device)
-        N.call("dxa_i64_to_str_write", N.ptr(data), n, N.ptr(off), N.ptr(dst), st)
-        return StrColumn(dst, off, lens.to(torch.int32), valid)
+        # fixed 24-byte slots: one launch, no host read (a compact copy is made only if the column is retained)
+        dev = data.device
+        dst = torch.empty(n * 24 + 16, dtype=torch.uint8, device=dev)
+        starts = torch.empty(n, dtype=torch.int64, device=dev)
+        lens = torch.empty(n, dtype=torch.int32, device=dev)
+        N.call("dxa_i64_to_str_slots", N.ptr(data.to(torch.int64).contiguous()), n, N.ptr(dst), N.ptr(starts),
+               N.ptr(lens), N.stream_handle(dev))
+        out = StrColumn(dst, starts, lens, valid)
+        out._max_len = 20
+        return out
     vals = data.tolist()
     v = valid.tolist() if valid is not None else [True] * n
     return strings_from_pylist([str(x) if ok else None for x, ok in zip(vals, v)], data.device)

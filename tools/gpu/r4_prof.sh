@@ -8,7 +8,3 @@ for f in window full; do
 done
 FLOWS="full window" bash tools/gpu/gpu_host_profile.sh || exit 1
 FLOWS="window full passthrough groupby join" bash tools/gpu/gpu_prof.sh || exit 1
-for F in full window passthrough; do
-  FLOW=$F timeout -k 10 900 bash tools/gpu/gpu_pmc.sh || exit 1
-  echo "pmc $F done"
-done

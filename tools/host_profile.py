@@ -22,13 +22,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--device", default="cuda")
     a = ap.parse_args()
     from dxa.engine.processor import Processor, RawBatch
     from dxa.models import iot
     from dxa.ops import native
     from dxa.simulate.datagen import generate
     native.lib()
-    dev = torch.device("cuda", 0)
+    dev = torch.device(a.device)
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     proc = Processor(iot.flow_settings(workdir=f"/tmp/dxa_hprof_{a.flow}", variant=a.flow, ref_rows=1_000_000), dev)
     if a.flow in ("join", "full"):
         proc.reference["RefDevices"] = iot.reference_table(1_000_000, dev)
@@ -38,17 +40,17 @@ def main():
     for i in range(a.warmup + a.batches):
         bufs.append(generate(prog, a.events, dev, seed=i + 1, row0=i * a.events,
                              base_ms=t0 // 1000 + i * 1000 - 1000, step_us=max(1, 1_000_000 // a.events)))
-    torch.cuda.synchronize()
+    sync()
     for i in range(a.warmup):
         proc.process_batch(RawBatch(bufs[i][0], bufs[i][1], a.events), t0 + i * 1_000_000, 1_000_000)
     proc.drain()
-    torch.cuda.synchronize()
+    sync()
     pr = cProfile.Profile()
     pr.enable()
     for i in range(a.warmup, a.warmup + a.batches):
         proc.process_batch(RawBatch(bufs[i][0], bufs[i][1], a.events), t0 + i * 1_000_000, 1_000_000)
     proc.drain()
-    torch.cuda.synchronize()
+    sync()
     pr.disable()
     for key in ("tottime", "cumulative"):
         s = io.StringIO()

@@ -55,6 +55,7 @@ class Counter(TorchDispatchMode):
         self.ops = collections.Counter()
         self.names = collections.Counter()
         self.syncs = collections.Counter()
+        self.by_name_site = collections.Counter()
         self.on = False
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
@@ -69,6 +70,7 @@ class Counter(TorchDispatchMode):
                     site = _site()
                     self.ops[site] += 1
                     self.names[name] += 1
+                    self.by_name_site[(name, site)] += 1
                 if "_local_scalar_dense" in name or ("copy" in name and torch.is_tensor(out) and not out.is_cuda):
                     self.syncs[site or _site()] += 1
         return out
@@ -136,6 +138,9 @@ def main():
     print("\n== ATen ops by name (per batch)")
     for s, c in cnt.names.most_common(40):
         print(f"{c / nb:7.1f}  {s}")
+    print("\n== (op, site) pairs (per batch)")
+    for (nm, st), c in cnt.by_name_site.most_common(50):
+        print(f"{c / nb:7.1f}  {nm:28s} {st}")
     print("\n== host syncs by site (per batch)")
     for s, c in cnt.syncs.most_common(40):
         print(f"{c / nb:7.1f}  {s}")
