@@ -151,6 +151,44 @@ __global__ void table_insert_kernel(const uint64_t* __restrict__ h, int64_t n, u
   }
 }
 
+// Insert + number + gather in ONE pass: the lane whose CAS claims an empty slot takes the next group id from a
+// counter and publishes it in gid_of_slot (pre-filled with -1); lanes that find the key already present wait for
+// that id.  The claim and the publication come before any lane of the wave waits (straight-line code, then a
+// reconvergent spin), so a waiting lane only ever waits on another wave.  Ids come out in claim order; the host
+// renumbers them by first row (dxa_group_renumber).  Replaces the table_number scan over every slot of the table.
+__global__ void group_build_kernel(const uint64_t* __restrict__ h, int64_t n, uint64_t* __restrict__ keys,
+                                   int64_t cap_mask, int32_t* __restrict__ gid_of_slot, int32_t* __restrict__ counter,
+                                   int32_t* __restrict__ gid, int32_t* __restrict__ rep) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = dxa::fix_key(h[i]);
+    int64_t s = (int64_t)(fmix64(k) & (uint64_t)cap_mask);
+    bool claimed = false;
+    while (true) {
+      const uint64_t cur = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == k) break;
+      if (cur == dxa::kEmpty) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&keys[s], (unsigned long long)dxa::kEmpty,
+                                        (unsigned long long)k);
+        if (prev == dxa::kEmpty) { claimed = true; break; }
+        if (prev == k) break;
+      }
+      s = (s + 1) & cap_mask;
+    }
+    int32_t g = -1;
+    if (claimed) {
+      g = atomicAdd(counter, 1);
+      __hip_atomic_store(&gid_of_slot[s], g, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!claimed) {
+      do {
+        g = __hip_atomic_load(&gid_of_slot[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      } while (g < 0);
+    }
+    gid[i] = g;
+    atomicMin(&rep[g], (int32_t)i);
+  }
+}
+
 __global__ void table_number_kernel(const uint64_t* __restrict__ keys, int64_t cap, int32_t* __restrict__ gid_of_slot,
                                     int32_t* __restrict__ counter) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (int64_t)gridDim.x * blockDim.x) {
@@ -514,6 +552,15 @@ DXA_API int dxa_group_ids(const uint64_t* keys, int64_t cap, const int32_t* slot
   if (n > 0)
     hipLaunchKernelGGL(group_gather_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, s, slot_of_row, gid_of_slot, n,
                        gid, rep);
+  return (int)hipGetLastError();
+}
+
+// keys: [cap] filled with 0xFF; gid_of_slot: [cap] filled with -1; counter: [1] zeroed; rep: [n] INT32_MAX
+DXA_API int dxa_group_build(const uint64_t* h, int64_t n, uint64_t* keys, int64_t cap, int32_t* gid_of_slot,
+                            int32_t* counter, int32_t* gid, int32_t* rep, void* st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(group_build_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, h, n, keys, cap - 1,
+                     gid_of_slot, counter, gid, rep);
   return (int)hipGetLastError();
 }
 

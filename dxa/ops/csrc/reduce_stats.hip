@@ -70,17 +70,27 @@ __global__ __launch_bounds__(kThreads) void ts_stats_kernel(const int64_t* __res
   __syncthreads();
   if (!last) return;
   __threadfence();
+  // the last workgroup folds the partials in parallel: one partial per thread, then the same wave / LDS reduction
+  Stat r{BIG, -BIG, 0, 0};
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+    const long long* p = part + 4 * b;
+    Stat x{__hip_atomic_load(&p[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+           __hip_atomic_load(&p[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+           __hip_atomic_load(&p[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+           __hip_atomic_load(&p[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+    r = combine(r, x);
+  }
+  r = wave_reduce(r);
+  __syncthreads();                                         // w[] is reused
+  if (lane == 0) w[wid] = r;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    Stat r{BIG, -BIG, 0, 0};
-    for (unsigned b = 0; b < gridDim.x; ++b) {
-      const volatile long long* p = part + 4 * b;
-      Stat x{p[0], p[1], p[2], p[3]};
-      r = combine(r, x);
-    }
-    out[0] = r.mn;
-    out[1] = r.mx;
-    out[2] = r.cnt;
-    out[3] = r.keep;
+    Stat b = w[0];
+    for (int k = 1; k < (int)(blockDim.x / 64); ++k) b = combine(b, w[k]);
+    out[0] = b.mn;
+    out[1] = b.mx;
+    out[2] = b.cnt;
+    out[3] = b.keep;
     atomicExch(ticket, 0u);                                // ready for the next launch (stream-ordered)
   }
 }

@@ -58,13 +58,12 @@ def group_rows(keys: List) -> Groups:
         st = N.stream_handle(device)
         cap = _next_pow2(2 * n)
         table = torch.full((cap,), -1, dtype=torch.int64, device=device)
-        slot = torch.empty(n, dtype=torch.int32, device=device)
-        N.call("dxa_table_insert", N.ptr(h), n, N.ptr(table), cap, N.ptr(slot), st)
-        gid_of_slot = torch.empty(cap, dtype=torch.int32, device=device)
+        gid_of_slot = torch.full((cap,), -1, dtype=torch.int32, device=device)
         scal = torch.zeros(2, dtype=torch.int32, device=device)   # [ngroups, bad]
         gid = torch.empty(n, dtype=torch.int32, device=device)
         rep = torch.full((n,), INT32_MAX, dtype=torch.int32, device=device)
-        N.call("dxa_group_ids", N.ptr(table), cap, N.ptr(slot), n, N.ptr(gid_of_slot), N.ptr(scal), N.ptr(gid),
+        # insert, number and gather in one pass (no scan over the table's slots)
+        N.call("dxa_group_build", N.ptr(h), n, N.ptr(table), cap, N.ptr(gid_of_slot), N.ptr(scal), N.ptr(gid),
                N.ptr(rep), st)
         bad_ptr = scal.data_ptr() + 4
         kc = key_cols(keys) if 2 <= len(keys) <= MAX_KEY_COLS else None

@@ -93,6 +93,8 @@ GPU_FUNCS = [
     ("soundex(concat('a', t))", "soundex"), ("unhex(t)", "unhex"), ("unbase64(base64(t))", "unbase64"),
     ("split_part(s, '.', 2)", "split_part"), ("split_part(s, ' ', -1)", "split_part_neg"),
     ("factorial(length(t) - 3)", "factorial"), ("overlay(t, 'XY', 3)", "overlay"),
+    ("concat('device ', length(t) * 1000003 - 7, ' home ', -length(s))", "concat_int_slots"),
+    ("concat(t, CAST(length(t) AS STRING))", "concat_mixed"),
 ]
 
 

@@ -3,7 +3,7 @@ set -o pipefail
 F=${FLOW:-groupby}
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/pmc_$F
-python -m dxa.ops.build || exit 1
+# (extensions are built in-tree before the call; nothing is compiled on the box)
 cd /tmp && export TMPDIR=/tmp
 rocprofv3 -L > $R/gpurun_out/counters_list.txt 2>&1 || true
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
