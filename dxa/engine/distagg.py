@@ -18,7 +18,7 @@ from ..ops import groupby as G
 from ..ops.hashing import hash_columns
 from ..sql import ast as A
 from . import decimal as Dec
-from .column import ConstColumn, PrimColumn, Table, materialize
+from .column import ConstColumn, PrimColumn, Table, materialize, take_columns
 from .decimal import is_decimal
 
 DECOMPOSABLE = {"count", "sum", "min", "max", "avg", "mean", "first", "last", "first_value", "last_value",
@@ -177,7 +177,7 @@ def local_partials(gexprs, keys, aggs: Dict, scope, ctx):
         nm = f"__k{i}"
         key_names.append(nm)
         names.append(nm)
-        cols.append(k.take(groups.rep) if groups.ngroups and n else k.take(groups.rep[:0]))
+    cols.extend(take_columns(list(keys), groups.rep if groups.ngroups and n else groups.rep[:0]))
     plan = {}
     reqs = []
     for ak, call in aggs.items():
@@ -216,7 +216,7 @@ def merge_partials(got: Table, plan, key_names: List[str], aggs: Dict, grouped: 
     else:
         g2 = _one_group(m, dev)
     ng = g2.ngroups
-    out_keys = [got.column(k).take(g2.rep) for k in key_names] if grouped else []
+    out_keys = take_columns([got.column(k) for k in key_names], g2.rep) if grouped else []
     entries = [(ak, nm, suffix, op) for ak in aggs for nm, suffix, op in plan[ak]]
     if m == 0:
         vals = [_empty_merge(got.column(nm), op, ng, dev) for _, nm, _, op in entries]

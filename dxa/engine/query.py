@@ -1069,8 +1069,8 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         idx = torch.nonzero(mask).flatten()
         scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]), scope.device)
         scope.dist = sdist
-    # the columns the statement reads (bare output references excepted: they stay deferred) in one gather
-    scope.prefetch([it.expr for it in sel.items if not isinstance(it.expr, (A.Ident, A.Star))] +
+    # the columns the statement reads in one gather (a SELECT * stays deferred: its consumer may read few columns)
+    scope.prefetch([it.expr for it in sel.items if not isinstance(it.expr, A.Star)] +
                    list(sel.group_by) + [sel.having])
     sel = _window_column_refs(sel, scope)
     sel, scope = _sliding_windows(sel, scope, ctx)

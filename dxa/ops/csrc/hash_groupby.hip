@@ -129,6 +129,36 @@ __global__ void verify_multi_kernel(const KeyCols a, const int32_t* __restrict__
   }
 }
 
+// Join candidate pairs: out[j] = (ri[j] >= 0) and every key column of left row li[j] equals right row ri[j] (SQL
+// equality: a NULL on either side never matches; doubles compare as numbers).  One launch for all key columns.
+__global__ void pairs_equal_kernel(const KeyCols L, const KeyCols R, const int64_t* __restrict__ li,
+                                   const int64_t* __restrict__ ri, int64_t m, uint8_t* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = li[j], b = ri[j];
+    bool eq = b >= 0;
+    for (int c = 0; c < L.ncols && eq; ++c) {
+      const KeyCol& x = L.c[c];
+      const KeyCol& y = R.c[c];
+      if ((x.valid && !x.valid[a]) || (y.valid && !y.valid[b])) { eq = false; break; }
+      if (x.kind == KC_STR) {
+        const int32_t l = x.lens[a];
+        if (l != y.lens[b]) { eq = false; break; }
+        const uint8_t* p = (const uint8_t*)x.data + x.starts[a];
+        const uint8_t* q = (const uint8_t*)y.data + y.starts[b];
+        for (int32_t k = 0; k < l && eq; k += 8) {
+          const int32_t av = l - k < 8 ? l - k : 8;
+          eq = load_part(p + k, av) == load_part(q + k, av);
+        }
+      } else if (x.kind == KC_F64) {
+        eq = ((const double*)x.data)[a] == ((const double*)y.data)[b];
+      } else {
+        eq = ((const int64_t*)x.data)[a] == ((const int64_t*)y.data)[b];
+      }
+    }
+    out[j] = eq ? 1 : 0;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // group-by: insert / number / gather
 // ------------------------------------------------------------------------------------------------------------
@@ -690,6 +720,19 @@ DXA_API int dxa_hash_multi(const void* args, uint64_t* out, void* st) {
   if (a.n <= 0) return 0;
   if (a.ncols <= 0 || a.ncols > kMaxKeyCols) return 1;
   hipLaunchKernelGGL(hash_multi_kernel, dim3(dxa_blocks(a.n, 256)), dim3(256), 0, (hipStream_t)st, a, out);
+  return (int)hipGetLastError();
+}
+
+DXA_API int dxa_pairs_equal(const void* left, const void* right, const int64_t* li, const int64_t* ri, int64_t m,
+                            uint8_t* out, void* st) {
+  const KeyCols& L = *(const KeyCols*)left;
+  const KeyCols& R = *(const KeyCols*)right;
+  if (m <= 0) return 0;
+  if (L.ncols <= 0 || L.ncols > kMaxKeyCols || L.ncols != R.ncols) return 1;
+  for (int c = 0; c < L.ncols; ++c)
+    if (L.c[c].kind != R.c[c].kind) return 1;
+  hipLaunchKernelGGL(pairs_equal_kernel, dim3(dxa_blocks(m, 256)), dim3(256), 0, (hipStream_t)st, L, R, li, ri, m,
+                     out);
   return (int)hipGetLastError();
 }
 

@@ -99,7 +99,8 @@ class _KeyCols(ctypes.Structure):
 
 
 N.register_sigs({"dxa_key_cols_size": [], "dxa_hash_multi": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
-                 "dxa_verify_multi": [ctypes.c_void_p] * 5})
+                 "dxa_verify_multi": [ctypes.c_void_p] * 5,
+                 "dxa_pairs_equal": [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]})
 
 
 def key_cols(cols):

@@ -8,6 +8,7 @@ A reference table that stays resident across batches (stream–static join) keep
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -15,7 +16,7 @@ import torch
 
 from . import native as N
 from .groupby import _next_pow2, _on_gpu
-from .hashing import hash_columns
+from .hashing import MAX_KEY_COLS, hash_columns, key_cols
 from ..engine.decimal import is_decimal, key_parts as decimal_key_parts
 
 
@@ -143,6 +144,16 @@ def keys_equal(lcols: List, rcols: List, li: torch.Tensor, ri: torch.Tensor) -> 
     lcols, rcols = _flat_keys(lcols), _flat_keys(rcols)
     from ..engine.column import StrColumn, PrimColumn, materialize
     device = li.device
+    if device.type == "cuda" and len(lcols) <= MAX_KEY_COLS:
+        L = key_cols([materialize(c) for c in lcols])
+        R = key_cols([materialize(c) for c in rcols])
+        if L is not None and R is not None and all(L.c[j].kind == R.c[j].kind for j in range(len(lcols))):
+            m = int(li.shape[0])
+            out = torch.empty(m, dtype=torch.uint8, device=device)
+            if m:
+                N.call("dxa_pairs_equal", ctypes.byref(L), ctypes.byref(R), N.ptr(li.to(torch.int64).contiguous()),
+                       N.ptr(ri.to(torch.int64).contiguous()), m, N.ptr(out), N.stream_handle(device))
+            return out.view(torch.bool)
     ok = torch.ones(li.shape[0], dtype=torch.bool, device=device)
     has = ri >= 0
     rsafe = torch.where(has, ri, torch.zeros_like(ri))
