@@ -169,7 +169,7 @@ def local_partials(gexprs, keys, aggs: Dict, scope, ctx):
     contributes no row."""
     dev = scope.device
     n = scope.length
-    groups = G.group_rows(keys) if gexprs else _one_group(n, dev)
+    groups = G.group_rows(keys, ordered=False) if gexprs else _one_group(n, dev)     # partials: order unseen
     names: List[str] = []
     cols = []
     key_names = []

@@ -38,7 +38,10 @@ def _on_gpu(device) -> bool:
     return torch.device(device).type == "cuda"
 
 
-def group_rows(keys: List) -> Groups:
+def group_rows(keys: List, ordered: bool = True) -> Groups:
+    """Group ids of the rows.  ``ordered``: ids follow the groups' first rows (the CPU reference's numbering, and
+    the order of a GROUP BY's output); intermediate groupings whose order is never seen (partial aggregates that are
+    merged later) pass False and keep the device's claim order."""
     from ..engine.column import materialize, PrimColumn, StrColumn, ConstColumn
     n = keys[0].length
     device = keys[0].device
@@ -81,6 +84,8 @@ def group_rows(keys: List) -> Groups:
         ng, bad = scal.tolist()
         if bad:
             return _exact_groups(keys, device)
+        if not ordered:
+            return Groups(gid, ng, rep[:ng].to(torch.int64))
         if 0 < ng <= _RENUMBER_MAX and _RENUMBER_KERNEL:
             inv = torch.empty(ng, dtype=torch.int32, device=device)
             rep_out = torch.empty(ng, dtype=torch.int64, device=device)
