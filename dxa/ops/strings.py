@@ -103,27 +103,30 @@ def _gather_parts(parts, device) -> None:
 
 
 def compact_many(cols: Sequence) -> list:
-    """``compact`` of several string columns with ONE host synchronisation (all arena sizes are read back together)
-    instead of one per column."""
+    """``compact`` of several string columns with ONE host synchronisation and one scan: every column's bytes are
+    packed into one shared arena (column k's rows after column k-1's), offsets from a single scan over all the
+    lengths, the bytes moved by one multi-part gather launch."""
     cols = list(cols)
     if not cols:
         return []
     if not _gpu(cols[0].starts) or len(cols) == 1:
         return [compact(c) for c in cols]
     device = cols[0].device
-    offs, ends = [], []
+    total_rows = sum(c.length for c in cols)
+    if total_rows == 0:
+        return [compact(c) for c in cols]
+    lens_all = torch.cat([c.lens for c in cols])
+    cs = torch.cumsum(lens_all, 0, dtype=torch.int64)
+    ex = cs - lens_all
+    total = int(cs[-1].item())
+    dst = _alloc_arena(total, device)
+    out, parts, r = [], [], 0
     for c in cols:
-        lens64 = c.lens.to(torch.int64)
-        cs = torch.cumsum(lens64, 0) if c.length else torch.zeros(1, dtype=torch.int64, device=device)
-        offs.append(cs - lens64 if c.length else cs[:0])
-        ends.append(cs[-1:] if c.length else cs)
-    totals = torch.cat(ends).tolist()
-    out, parts = [], []
-    for c, off, total in zip(cols, offs, totals):
-        dst = _alloc_arena(int(total), device)
-        if c.length and total:
+        off = ex[r:r + c.length]
+        r += c.length
+        if c.length:
             parts.append((c, off, dst))
-        o = type(c)(dst, off, c.lens.clone(), c.valid, c.dtype)
+        o = type(c)(dst, off, c.lens, c.valid, c.dtype)
         o._compact = True
         out.append(o)
     _gather_parts(parts, device)                   # every column's bytes in one launch
@@ -355,21 +358,7 @@ def concat_strings(parts: List[Union[str, object]], n: int, device):
     from ..engine.column import StrColumn, and_valid
     device = torch.device(device)
     if device.type == "cuda":
-        lits = []
-        arr = (_ConcatPart * len(parts))()
-        keep = []
-        for i, p in enumerate(parts):
-            if isinstance(p, str):
-                b = p.encode("utf-8")
-                t = N.h2d(b + b"\0", torch.uint8, device)
-                keep.append(t)
-                arr[i] = _ConcatPart(0, 0, 0, 0, t.data_ptr(), len(b), 1)
-            else:
-                v = N.u8(p.valid)
-                keep.append(v)
-                arr[i] = _ConcatPart(p.arena.data_ptr(), p.starts.data_ptr(), p.lens.data_ptr(),
-                                     0 if v is None else v.data_ptr(), 0, 0, 0)
-        raw = N.h2d(bytes(arr), torch.uint8, device)
+        arr, keep, raw = _concat_parts(parts, device)
         lens = torch.empty(n, dtype=torch.int64, device=device)
         ok = torch.empty(n, dtype=torch.bool, device=device)
         st = N.stream_handle(device)
@@ -405,6 +394,38 @@ def concat_strings(parts: List[Union[str, object]], n: int, device):
     return strings_from_pylist(out, device)
 
 
+def _concat_parts(parts, device):
+    """The part descriptors and every literal's bytes in ONE device buffer (one upload): descriptors first, then the
+    literals, whose device addresses are known once the buffer is allocated."""
+    arr = (_ConcatPart * len(parts))()
+    head = ctypes.sizeof(arr)
+    lits, pos = [], head
+    for p in parts:
+        if isinstance(p, str):
+            b = p.encode("utf-8") + b"\0"
+            lits.append((pos, b))
+            pos += len(b)
+    raw = torch.empty(pos, dtype=torch.uint8, device=device)
+    base = raw.data_ptr()
+    keep = []
+    li = 0
+    for i, p in enumerate(parts):
+        if isinstance(p, str):
+            off, b = lits[li]
+            li += 1
+            arr[i] = _ConcatPart(0, 0, 0, 0, base + off, len(b) - 1, 1)
+        else:
+            v = N.u8(p.valid)
+            keep.append(v)
+            arr[i] = _ConcatPart(p.arena.data_ptr(), p.starts.data_ptr(), p.lens.data_ptr(),
+                                 0 if v is None else v.data_ptr(), 0, 0, 0)
+    blob = bytearray(bytes(arr))
+    for off, b in lits:
+        blob += b
+    raw.copy_(torch.frombuffer(blob, dtype=torch.uint8).pin_memory(), non_blocking=True)
+    return arr, keep, raw
+
+
 def _concat_bound(parts, n: int):
     """Upper bound of a CONCAT's total bytes when every column part carries ``_max_len`` (bytes per row)."""
     tot = 0
@@ -423,20 +444,7 @@ def concat_ws(sep: str, parts: List[Union[str, object]], n: int, device):
     """concat_ws on the device: null column parts are skipped (Spark), the separator joins what remains."""
     from ..engine.column import StrColumn
     device = torch.device(device)
-    arr = (_ConcatPart * len(parts))()
-    keep = []
-    for i, p in enumerate(parts):
-        if isinstance(p, str):
-            b = p.encode("utf-8")
-            t = N.h2d(b + b"\0", torch.uint8, device)
-            keep.append(t)
-            arr[i] = _ConcatPart(0, 0, 0, 0, t.data_ptr(), len(b), 1)
-        else:
-            v = N.u8(p.valid)
-            keep.append(v)
-            arr[i] = _ConcatPart(p.arena.data_ptr(), p.starts.data_ptr(), p.lens.data_ptr(),
-                                 0 if v is None else v.data_ptr(), 0, 0, 0)
-    raw = N.h2d(bytes(arr), torch.uint8, device)
+    arr, keep, raw = _concat_parts(parts, device)
     sb = sep.encode("utf-8")
     st_ = N.h2d(sb + b"\0", torch.uint8, device)
     lens = torch.empty(n, dtype=torch.int64, device=device)
