@@ -672,6 +672,7 @@ def concat_tables(tables: List[Table]) -> Table:
     batched = torch.device(device).type == "cuda"
     segs = []
     cols = []
+    str_groups = []                                 # (output position, parts) of the string columns
     for i, n in enumerate(names):
         parts = []
         for t in tables:
@@ -685,10 +686,23 @@ def concat_tables(tables: List[Table]) -> Table:
                 segs.extend(sg)
                 cols.append(PrimColumn(parts[0].dtype, data, valid))
                 continue
+        if (batched and all(isinstance(c, StrColumn) and not isinstance(c, JsonColumn) for c in parts)
+                and len({type(c) for c in parts}) == 1):
+            str_groups.append((len(cols), parts))
+            cols.append(None)
+            continue
         cols.append(concat_columns(parts))
+    if str_groups:
+        from ..ops.copybatch import valid_segments
+        from ..ops.strings import concat_multi
+        got = concat_multi([p for _, p in str_groups])
+        for (at, parts), (arena, starts, lens) in zip(str_groups, got):
+            valid, sg = valid_segments(parts, device)
+            segs.extend(sg)
+            cols[at] = type(parts[0])(arena, starts, lens, valid, parts[0].dtype)
     if segs:
         from ..ops.copybatch import copy_batch
-        copy_batch(segs, device)                    # every fixed-width column of every table: one launch
+        copy_batch(segs, device)                    # every fixed-width leaf of every table: one launch
     return Table(names, cols, sum(t.length for t in tables), device)
 
 

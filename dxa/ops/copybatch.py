@@ -64,3 +64,21 @@ def concat_prims(parts: Sequence, device):
                 segs.append((None, 0, valid, r, n, 1))
         r += n
     return data, valid, segs
+
+
+def valid_segments(parts: Sequence, device):
+    """Concatenated validity of columns (None when none has nulls) as copy / fill segments."""
+    if not any(p.valid is not None for p in parts):
+        return None, []
+    total = sum(p.length for p in parts)
+    valid = torch.empty(total, dtype=torch.bool, device=device)
+    segs, r = [], 0
+    for p in parts:
+        n = p.length
+        if p.valid is not None:
+            v = p.valid if p.valid.is_contiguous() else p.valid.contiguous()
+            segs.append((v, 0, valid, r, n, 0))
+        else:
+            segs.append((None, 0, valid, r, n, 1))
+        r += n
+    return valid, segs

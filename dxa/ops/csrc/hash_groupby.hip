@@ -827,15 +827,76 @@ __global__ void renumber_rows_kernel(int32_t* __restrict__ gid, int64_t n, const
     gid[i] = inv[gid[i]];
 }
 
+// Any number of groups over at most kBitmapRows rows: a group's rank is the number of first rows before its own,
+// read off a bitmap of first rows held in LDS (64 KiB) and the word-wise exclusive popcount sums (32 KiB).
+constexpr int kBitmapWords = 8192;
+constexpr int64_t kBitmapRows = (int64_t)kBitmapWords * 64;
+
+__global__ __launch_bounds__(1024) void renumber_bitmap_kernel(const int32_t* __restrict__ rep, int32_t ng,
+                                                               int32_t* __restrict__ inv,
+                                                               int64_t* __restrict__ rep_out) {
+  __shared__ unsigned long long bits[kBitmapWords];
+  __shared__ uint32_t pre[kBitmapWords];
+  __shared__ uint32_t wsum[16];
+  const int t = threadIdx.x;
+  for (int w = t; w < kBitmapWords; w += blockDim.x) bits[w] = 0ull;
+  __syncthreads();
+  for (int g = t; g < ng; g += blockDim.x) {
+    const uint32_t r = (uint32_t)rep[g];
+    atomicOr(&bits[r >> 6], 1ull << (r & 63));
+  }
+  __syncthreads();
+  // exclusive scan of the words' popcounts: 8 consecutive words per thread, then a block scan of the thread sums
+  constexpr int kPer = kBitmapWords / 1024;
+  uint32_t local = 0;
+  for (int k = 0; k < kPer; ++k) local += (uint32_t)__popcll(bits[t * kPer + k]);
+  const int lane = t & 63, wid = t >> 6;
+  uint32_t incl = local;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (int k = 0; k < (int)(blockDim.x / 64); ++k) {
+      const uint32_t v = wsum[k];
+      wsum[k] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  uint32_t run = wsum[wid] + incl - local;
+  for (int k = 0; k < kPer; ++k) {
+    pre[t * kPer + k] = run;
+    run += (uint32_t)__popcll(bits[t * kPer + k]);
+  }
+  __syncthreads();
+  for (int g = t; g < ng; g += blockDim.x) {
+    const uint32_t r = (uint32_t)rep[g];
+    const uint32_t w = r >> 6;
+    const unsigned long long below = (r & 63) ? (bits[w] & ((1ull << (r & 63)) - 1ull)) : 0ull;
+    const int32_t rank = (int32_t)(pre[w] + (uint32_t)__popcll(below));
+    inv[g] = rank;
+    rep_out[rank] = (int64_t)r;
+  }
+}
+
 DXA_API int dxa_group_renumber_max() { return kRenumberMax; }
+DXA_API int64_t dxa_group_renumber_bitmap_rows() { return kBitmapRows; }
 
 // gid: [n] int32 rewritten in place; rep: [ng] int32 first rows; inv: [ng] int32 scratch; rep_out: [ng] int64
 DXA_API int dxa_group_renumber(int32_t* gid, int64_t n, const int32_t* rep, int32_t ng, int32_t* inv,
                                int64_t* rep_out, void* st) {
   if (ng <= 0) return 0;
-  if (ng > kRenumberMax) return 1;
   hipStream_t s = (hipStream_t)st;
-  hipLaunchKernelGGL(renumber_sort_kernel, dim3(1), dim3(1024), 0, s, rep, ng, inv, rep_out);
+  if (n <= kBitmapRows)
+    hipLaunchKernelGGL(renumber_bitmap_kernel, dim3(1), dim3(1024), 0, s, rep, ng, inv, rep_out);
+  else if (ng <= kRenumberMax)
+    hipLaunchKernelGGL(renumber_sort_kernel, dim3(1), dim3(1024), 0, s, rep, ng, inv, rep_out);
+  else
+    return 1;
   if (n > 0) hipLaunchKernelGGL(renumber_rows_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, s, gid, n, inv);
   return (int)hipGetLastError();
 }

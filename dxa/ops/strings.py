@@ -133,6 +133,31 @@ def compact_many(cols: Sequence) -> list:
     return out
 
 
+def concat_multi(groups: Sequence[Sequence]):
+    """Several row-concatenations of device StrColumns at once (a table concatenation's string columns): one length
+    concatenation, one scan, one host read and one multi-part gather for all of them; the outputs share one arena.
+    Returns [(arena, starts, lens)] per group (validity is the caller's)."""
+    device = groups[0][0].device
+    flat = [c for g in groups for c in g]
+    lens_all = torch.cat([c.lens.to(torch.int32) for c in flat])
+    if lens_all.numel() == 0:
+        return [(_alloc_arena(0, device), torch.zeros(0, dtype=torch.int64, device=device),
+                 torch.zeros(0, dtype=torch.int32, device=device)) for _ in groups]
+    cs = torch.cumsum(lens_all, 0, dtype=torch.int64)
+    ex = cs - lens_all
+    dst = _alloc_arena(int(cs[-1].item()), device)
+    out, parts, pos = [], [], 0
+    for g in groups:
+        n = sum(c.length for c in g)
+        for c in g:
+            if c.length:
+                parts.append((c, ex[pos:pos + c.length], dst))
+            pos += c.length
+        out.append((dst, ex[pos - n:pos], lens_all[pos - n:pos]))
+    _gather_parts(parts, device)                    # every part of every column in one launch
+    return out
+
+
 def concat(cols: Sequence, valid: Optional[torch.Tensor]):
     """Row-concatenate StrColumns (may reference different arenas) into one compact column."""
     device = cols[0].device

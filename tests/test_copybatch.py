@@ -58,3 +58,20 @@ def test_concat_tables_cpu_strings_and_prims():
                                                                      torch.tensor([False]))], 1)
     out = concat_tables([t1, t2])
     assert out.columns[0].to_pylist() == ["a", None, "bb"] and out.columns[1].to_pylist() == [1, 2, None]
+
+
+@pytest.mark.gpu
+def test_concat_tables_with_strings_matches_cpu():
+    dev = torch.device("cuda")
+    rows = [[("a", 1), (None, 2), ("héllo", 3)], [], [("x" * 40, 4)], [("", None), ("zz", 6)]]
+    tabs_g, tabs_c = [], []
+    for r in rows:
+        s = [x[0] for x in r]
+        v = [x[1] for x in r]
+        from dxa.engine.column import column_from_pylist
+        for dev_, out in ((dev, tabs_g), ("cpu", tabs_c)):
+            out.append(Table(["s", "v"], [strings_from_pylist(s, dev_), column_from_pylist(v, "long", dev_)],
+                             len(r), dev_))
+    g, c = concat_tables(tabs_g), concat_tables(tabs_c)
+    assert g.columns[0].to_pylist() == c.columns[0].to_pylist() == ["a", None, "héllo", "x" * 40, "", "zz"]
+    assert g.columns[1].to_pylist() == c.columns[1].to_pylist()
