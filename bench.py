@@ -423,6 +423,8 @@ def main():
         import cProfile
         cprof = cProfile.Profile()
         cprof.enable()
+    from dxa.ops import serialize as _ser0
+    ser_stats0 = dict(_ser0.STATS)
     t0 = time.perf_counter()
     last = None
     for i in range(warmup, warmup + args.steps):
@@ -542,6 +544,14 @@ def main():
         out["window_panes"] = len(proc.window_store.past)
         out["window_retained_rows"] = proc.window_store.retained_rows()
     if on_gpu:
+        from dxa.ops import serialize as _ser
+        rs = {k: v - ser_stats0.get(k, 0) for k, v in _ser.STATS.items()}
+        if rs["d2h_bytes"]:
+            # rendered output text crossing PCIe (sinks' D2H), per timed step; d2h_s is the copies' wall time
+            out["output_d2h"] = {"mb_per_step": round(rs["d2h_bytes"] / args.steps / 1e6, 1),
+                                 "ms_per_step": round(rs["d2h_s"] / args.steps * 1e3, 2),
+                                 "gb_per_s": round(rs["d2h_bytes"] / rs["d2h_s"] / 1e9, 2) if rs["d2h_s"] else None,
+                                 "render_launch_pairs_per_step": round(rs["launch_pairs"] / args.steps, 2)}
         out["max_hbm_allocated_gb"] = round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
     if args.profile_stages:
         out["stage_s"] = {k: round(v, 5) for k, v in proc.stage_times.items()}

@@ -415,6 +415,8 @@ class Processor:
             if P.active() and P.dist_of(t) == P.REPLICATED and P.rank() != 0:
                 t = t.slice(0, 0)      # replicated results are written once, by rank 0
             staged.append((op.name, op.stage(t, ctx)))
+        from ..ops.serialize import link_render_groups
+        link_render_groups([p for _, st in staged for p in st.payloads()])    # one render launch pair per batch
         self._complete_inflight()
         from ..io.sinks import _pool
         target = getattr(self, "_batch_target", None)

@@ -430,6 +430,13 @@ class StagedOutput:
         self.n = n
         self.items: List = []
 
+    def payloads(self) -> List[Any]:
+        """Every captured payload (a grouped sink contributes one per group)."""
+        out = []
+        for _, p in self.items:
+            out.extend(p.values() if isinstance(p, dict) else [p])
+        return out
+
     def finish(self, partition_time: _dt.datetime, target: Optional[str] = None) -> Dict[str, int]:
         """Host-side half: render JSON (waits only for this output's D2H copies) and write every sink."""
         metrics = {f"{SINK_PREFIX}InputEvents": self.n}

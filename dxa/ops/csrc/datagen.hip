@@ -79,8 +79,9 @@ struct Tables {
 };
 
 template <bool WRITE>
-__device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int64_t i, uint8_t* dst) {
-  dxa::Emitter<WRITE> e(dst);
+__device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int64_t i, uint8_t* dst,
+                                          uint8_t* stage = nullptr) {
+  dxa::Emitter<WRITE> e(dst, stage);
   const uint64_t* pool64 = t.pool64;
   const int64_t row = g.row0 + i;
   int skip = 0;
@@ -191,6 +192,10 @@ __device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int
   return e.len;
 }
 
+__host__ __device__ __forceinline__ size_t lds_bytes_dev(int32_t nops, int32_t pool_words, int32_t table_ints) {
+  return (size_t)nops * sizeof(Op) + (size_t)pool_words * 8 + (size_t)table_ints * 4;
+}
+
 // LDS image of the tables: ops (32 B each), pool words, table ints — sizes from the host (lds_bytes)
 __device__ __forceinline__ Tables stage_tables(const GenArgs& g, uint64_t* smem) {
   const int op_words = g.nops * (int)(sizeof(Op) / 8);
@@ -213,12 +218,18 @@ __global__ __launch_bounds__(256) void gen_len_kernel(GenArgs g) {
   g.lens[i] = render<false>(g, t, i, nullptr);
 }
 
+// the lane's 64-B emitter staging slot, after the tables (lds_bytes, 16-B aligned)
+__device__ __forceinline__ uint8_t* stage_slot(const GenArgs& g, uint64_t* smem) {
+  const size_t tables = (lds_bytes_dev(g.nops, g.pool_words, g.table_ints) + 15) & ~(size_t)15;
+  return reinterpret_cast<uint8_t*>(smem) + tables + (size_t)threadIdx.x * dxa::kEmitStageBytes;
+}
+
 __global__ __launch_bounds__(256) void gen_write_kernel(GenArgs g) {
   extern __shared__ uint64_t smem[];
   const Tables t = stage_tables(g, smem);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.n) return;
-  render<true>(g, t, i, g.out + g.offs[i]);
+  render<true>(g, t, i, g.out + g.offs[i], stage_slot(g, smem));
 }
 
 // One pass, no length pass or scan: event i renders into its own 16-B aligned slot [i*stride, i*stride+len) (the
@@ -238,8 +249,12 @@ __global__ __launch_bounds__(256) void gen_slot_kernel(GenArgs g) {
   if (i == g.n - 1) const_cast<int64_t*>(g.offs)[g.n] = g.n * g.stride;
 }
 
-size_t lds_bytes(int32_t nops, int32_t pool_words, int32_t table_ints) {
-  return (size_t)nops * sizeof(Op) + (size_t)pool_words * 8 + (size_t)table_ints * 4;
+size_t lds_bytes(int32_t nops, int32_t pool_words, int32_t table_ints) { return lds_bytes_dev(nops, pool_words, table_ints); }
+
+// the write pass adds the emitters' staging slots (DXA_EMIT_STAGE)
+size_t write_lds_bytes(int32_t nops, int32_t pool_words, int32_t table_ints) {
+  return DXA_EMIT_STAGE ? ((lds_bytes(nops, pool_words, table_ints) + 15) & ~(size_t)15) + 256 * dxa::kEmitStageBytes
+                        : lds_bytes(nops, pool_words, table_ints);
 }
 
 constexpr size_t kMaxLds = 64 * 1024;
@@ -268,7 +283,8 @@ DXA_API int dxa_datagen_write(const void* ops, int32_t nops, const uint8_t* pool
   if (lds > kMaxLds) return (int)hipErrorInvalidValue;
   GenArgs g{(const Op*)ops, nops, pool, table, pool_words, table_ints, seed, row0, n, base_ms, step_us, offs, out,
             nullptr, 0, nullptr};
-  hipLaunchKernelGGL(gen_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, g);
+  hipLaunchKernelGGL(gen_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                     write_lds_bytes(nops, pool_words, table_ints), (hipStream_t)st, g);
   return (int)hipGetLastError();
 }
 

@@ -9,8 +9,21 @@
 #ifndef DXA_EMIT_NT
 #define DXA_EMIT_NT 0
 #endif
+// Staged 64-B segments (DXA_EMIT_STAGE=1, an Emitter given an LDS slot): with ~64 K lanes per XCD each filling its
+// own line, half-written lines are evicted from the L2 and written back as partial-sector requests — PMC WRITE_SIZE
+// of the generator's write pass is 1.70 GB for 0.61 GB of text (2.8x), the serializer's 1.54 GB for 0.66 GB.  With
+// a slot, a lane's full words wait in LDS (64 B per lane, kEmitStageBytes) until their 64-B segment is complete and
+// leave as four back-to-back 16-B stores: measured on MI355X (profiles/pmc/passthrough_r4.md) that cuts the write
+// traffic to 0.72 / 0.75 GB, but the kernels do not get faster (gen_write 559 vs 544 us, ser_write 1134 vs 1043 us:
+// they are issue-bound, and the staging costs VGPRs — 71 -> 82 and 95 -> 103, one wave per SIMD less).  Off by
+// default; the variant build keeps it measurable.
+#ifndef DXA_EMIT_STAGE
+#define DXA_EMIT_STAGE 0
+#endif
 
 namespace dxa {
+
+constexpr int kEmitStageBytes = 64;     // LDS per lane for a staged Emitter
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
@@ -39,9 +52,15 @@ struct Emitter {
   bool first;          // still on the record's first word
   uint64_t a0, a1;     // current word
   uint64_t h0, h1;     // the first word, once full (written by finish)
+  uint8_t* stg;        // this lane's 64-B LDS staging slot, or null (direct 16-B stores)
+  uint32_t swz;        // slot swizzle (lane & 3): spreads the lanes' 16-B LDS writes over the banks
 
   __device__ __forceinline__ explicit Emitter(uint8_t* dst)
-      : len(0), lead(0), nacc(0), first(true), a0(0), a1(0), h0(0), h1(0) {
+      : Emitter(dst, nullptr) {}
+
+  __device__ __forceinline__ Emitter(uint8_t* dst, uint8_t* stage)
+      : len(0), lead(0), nacc(0), first(true), a0(0), a1(0), h0(0), h1(0), stg(DXA_EMIT_STAGE ? stage : nullptr),
+        swz(threadIdx.x & 3u) {
     if (WRITE) {
       lead = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
       wbase = hbase = dst - lead;
@@ -85,11 +104,37 @@ struct Emitter {
 #endif
   }
 
+  __device__ __forceinline__ u64x2 staged(uint32_t slot) const {
+    return *reinterpret_cast<const u64x2*>(stg + 16 * (slot ^ swz));
+  }
+
+  // the staged words in slots [0, nslots) of the segment holding wbase that lie past the record's first word
+  __device__ __forceinline__ void flush_segment(uint32_t nslots) {
+    uint8_t* seg = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(wbase) & ~(uintptr_t)63);
+    for (uint32_t j = 0; j < 3; ++j) {
+      if (j < nslots && seg + 16 * j > hbase) {
+        const u64x2 v = staged(j);
+        store16(seg + 16 * j, v.x, v.y);
+      }
+    }
+  }
+
   __device__ __forceinline__ void flush_full() {
     if (first) {
       h0 = a0;
       h1 = a1;
       first = false;
+    } else if (stg != nullptr) {
+      const uint32_t slot = (uint32_t)(reinterpret_cast<uintptr_t>(wbase) >> 4) & 3u;
+      if (slot == 3) {                   // segment complete: slots 0..2 from LDS, slot 3 from registers
+        flush_segment(3);
+        store16(wbase, a0, a1);
+      } else {
+        u64x2 v;
+        v.x = a0;
+        v.y = a1;
+        *reinterpret_cast<u64x2*>(stg + 16 * (slot ^ swz)) = v;
+      }
     } else {
       store16(wbase, a0, a1);
     }
@@ -134,6 +179,7 @@ struct Emitter {
       if (first) {                       // the record never left its first word
         if (nacc > lead) store_range(hbase, a0, a1, lead, nacc);
       } else {
+        if (stg != nullptr) flush_segment((uint32_t)(reinterpret_cast<uintptr_t>(wbase) >> 4) & 3u);  // staged words
         if (lead == 0) {
           store16(hbase, h0, h1);
         } else {

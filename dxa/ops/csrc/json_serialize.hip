@@ -5,7 +5,8 @@
 //
 // Two passes, one lane per row: lengths (no stores) → exclusive scan on the stream → write at exact offsets, so the
 // output is one contiguous blob copied to the host with a single D2H.  Bytes leave through the register-packed
-// 16-B emitter (dxa_emit.h).
+// 16-B emitter (dxa_emit.h).  Every output table of a batch renders in the same launch pair (one segment each):
+// one upload of the tables, one scan, one D2H of the lengths and one of the text per batch, not per output.
 //
 // The column tree is walked by a flat program the host derives from it (one FIELD op per node in preorder, a CLOSE
 // op after each container's children, and for every FIELD the number of ops to jump when the field is omitted):
@@ -32,6 +33,19 @@ struct DevNode {
   const int32_t* lens;
 };
 
+// Several tables render in one launch pair: segment s owns rows [row[s], row[s+1]) of the output, render ops
+// [pc[s], pc[s+1]) of the shared program and workgroups [block[s], block[s+1]) (a workgroup never straddles two
+// segments, so the program a wave walks is uniform).  Row indices into a segment's columns are local to it.
+constexpr int kMaxSeg = 16;
+
+struct SerSegs {
+  int32_t nseg;
+  int32_t pad;
+  int64_t row[kMaxSeg + 1];
+  int32_t pc[kMaxSeg + 1];
+  int32_t block[kMaxSeg + 1];
+};
+
 struct SerArgs {
   const DevNode* nodes;
   int32_t nnodes;
@@ -39,10 +53,11 @@ struct SerArgs {
   int32_t nprog;
   const uint8_t* text;    // names and constants, each 8-B aligned and zero-padded (dxa/ops/serialize.py)
   int32_t text_words;
-  int64_t n;
   int64_t* lens;          // length pass (line length incl. the newline)
-  const int64_t* offs;    // write pass
+  const int64_t* ends;    // write pass: inclusive scan of lens (line i starts at ends[i] - lens[i])
   uint8_t* out;
+  int32_t stage_off;      // write pass: LDS offset of the emitters' 64-B staging slots (0: direct stores)
+  SerSegs seg;
 };
 
 __constant__ uint64_t c_ryu_inv[2 * DXA_RYU_INV_TABLE_SIZE] = DXA_RYU_POW5_INV_SPLIT_INIT;
@@ -279,11 +294,12 @@ __device__ __forceinline__ Tables stage_tables(const SerArgs& a, uint64_t* smem)
 }
 
 template <bool W>
-__device__ __forceinline__ int64_t render_row(const SerArgs& a, const Tables& t, int64_t row, uint8_t* dst) {
-  dxa::Emitter<W> e(dst);
+__device__ __forceinline__ int64_t render_row(const Tables& t, int pc0, int pc1, int64_t row, uint8_t* dst,
+                                              uint8_t* stage = nullptr) {
+  dxa::Emitter<W> e(dst, stage);
   e.put('{');
   uint32_t first = 1u;                                      // bit d: nothing written yet at nesting depth d
-  for (int pc = 0; pc < a.nprog; ++pc) {
+  for (int pc = pc0; pc < pc1; ++pc) {
     const int code = t.prog[4 * pc], nidx = t.prog[4 * pc + 1], depth = t.prog[4 * pc + 2], mw = t.prog[4 * pc + 3];
     const DevNode& nd = t.nodes[nidx];
     const int kind = nd.kind;
@@ -329,20 +345,34 @@ __device__ __forceinline__ int64_t render_row(const SerArgs& a, const Tables& t,
   return e.len;
 }
 
+// (segment, local row, global row) of this lane; false past the end of its segment
+__device__ __forceinline__ bool seg_row(const SerSegs& g, int& s, int64_t& local, int64_t& row) {
+  const int b = (int)blockIdx.x;
+  s = 0;
+  while (s + 1 < g.nseg && b >= g.block[s + 1]) ++s;      // uniform: at most kMaxSeg scalar compares
+  local = (int64_t)(b - g.block[s]) * blockDim.x + threadIdx.x;
+  row = g.row[s] + local;
+  return row < g.row[s + 1];
+}
+
 __global__ __launch_bounds__(256) void ser_len_kernel(SerArgs a) {
   extern __shared__ uint64_t smem[];
   const Tables t = stage_tables(a, smem);
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  a.lens[i] = render_row<false>(a, t, i, nullptr);
+  int s;
+  int64_t local, row;
+  if (!seg_row(a.seg, s, local, row)) return;
+  a.lens[row] = render_row<false>(t, a.seg.pc[s], a.seg.pc[s + 1], local, nullptr);
 }
 
 __global__ __launch_bounds__(256) void ser_write_kernel(SerArgs a) {
   extern __shared__ uint64_t smem[];
   const Tables t = stage_tables(a, smem);
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  render_row<true>(a, t, i, a.out + a.offs[i]);
+  int s;
+  int64_t local, row;
+  if (!seg_row(a.seg, s, local, row)) return;
+  uint8_t* stage = a.stage_off ? reinterpret_cast<uint8_t*>(smem) + a.stage_off + threadIdx.x * dxa::kEmitStageBytes
+                               : nullptr;
+  render_row<true>(t, a.seg.pc[s], a.seg.pc[s + 1], local, a.out + (a.ends[row] - a.lens[row]), stage);
 }
 
 size_t ser_lds_bytes(int32_t nnodes, int32_t nprog, int32_t text_words) {
@@ -377,27 +407,41 @@ const uint64_t h_ryu_pos[2 * DXA_RYU_TABLE_SIZE] = DXA_RYU_POW5_SPLIT_INIT;
 
 DXA_API int dxa_sernode_dev_size() { return (int)sizeof(DevNode); }
 
-// `prog` / `nprog`: the flat render program (4 ints per op) built by dxa/ops/serialize.py from the node tree.
-// `text` is 8-B aligned with `text_words` words (names / constants 8-B aligned, zero-padded); the tables are staged
-// in LDS, so they must fit in 64 KiB together.
-DXA_API int dxa_serialize_lengths(const void* nodes, int32_t nnodes, const int32_t* prog, int32_t nprog,
-                                  const uint8_t* text, int32_t text_words, int64_t n, int64_t* lens, void* st) {
-  if (n <= 0) return 0;
-  const size_t lds = ser_lds_bytes(nnodes, nprog, text_words);
-  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
-  SerArgs a{(const DevNode*)nodes, nnodes, prog, nprog, text, text_words, n, lens, nullptr, nullptr};
-  hipLaunchKernelGGL(ser_len_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, a);
-  return (int)hipGetLastError();
-}
+DXA_API int dxa_sersegs_size() { return (int)sizeof(SerSegs); }
+DXA_API int dxa_sersegs_max() { return kMaxSeg; }
 
-DXA_API int dxa_serialize_write(const void* nodes, int32_t nnodes, const int32_t* prog, int32_t nprog,
-                                const uint8_t* text, int32_t text_words, int64_t n, const int64_t* offs, uint8_t* out,
-                                void* st) {
-  if (n <= 0) return 0;
+// One pass of the serializer over every segment.  `tables` holds the node array (nnodes DevNode), then the flat
+// render program (nprog ops of 4 ints, padded to 8 B), then the text pool (text_words 8-B words; names / constants
+// 8-B aligned and zero-padded) — one upload per batch, built by dxa/ops/serialize.py.  `segs` is a host SerSegs with
+// nseg, row[0..nseg] and pc[0..nseg] filled; the workgroup ranges are derived here.  The tables are staged in LDS,
+// so they must fit in 64 KiB together.  write == 0: line lengths into `lens`; write == 1: lines into `out` at
+// ends[i] - lens[i].
+DXA_API int dxa_serialize_rows(int32_t write, const void* tables, int32_t nnodes, int32_t nprog, int32_t text_words,
+                               const void* segs, int64_t* lens, const int64_t* ends, uint8_t* out, void* st) {
+  SerSegs g = *(const SerSegs*)segs;
+  if (g.nseg <= 0 || g.nseg > kMaxSeg) return (int)hipErrorInvalidValue;
+  int64_t blocks = 0;
+  for (int s = 0; s < g.nseg; ++s) {
+    if (g.row[s + 1] < g.row[s] || g.pc[s + 1] < g.pc[s] || g.pc[s + 1] > nprog) return (int)hipErrorInvalidValue;
+    g.block[s] = (int32_t)blocks;
+    blocks += (g.row[s + 1] - g.row[s] + 255) / 256;
+  }
+  g.block[g.nseg] = (int32_t)blocks;
+  if (blocks == 0) return 0;
+  if (blocks > 0x7fffffff) return (int)hipErrorInvalidValue;
   const size_t lds = ser_lds_bytes(nnodes, nprog, text_words);
   if (lds > kMaxLds) return (int)hipErrorInvalidValue;
-  SerArgs a{(const DevNode*)nodes, nnodes, prog, nprog, text, text_words, n, nullptr, offs, out};
-  hipLaunchKernelGGL(ser_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), lds, (hipStream_t)st, a);
+  const uint8_t* base = (const uint8_t*)tables;
+  const size_t prog_off = (size_t)nnodes * sizeof(DevNode);
+  const size_t text_off = prog_off + (size_t)((nprog * 4 + 1) / 2) * 8;
+  const size_t stage_off = (lds + 15) & ~(size_t)15;
+  const bool stage = write && DXA_EMIT_STAGE && stage_off + 256 * dxa::kEmitStageBytes <= kMaxLds;
+  SerArgs a{(const DevNode*)base, nnodes, (const int32_t*)(base + prog_off), nprog, base + text_off, text_words,
+            lens, ends, out, stage ? (int32_t)stage_off : 0, g};
+  if (write)
+    hipLaunchKernelGGL(ser_write_kernel, dim3((unsigned)blocks), dim3(256),
+                       stage ? stage_off + 256 * dxa::kEmitStageBytes : lds, (hipStream_t)st, a);
+  else hipLaunchKernelGGL(ser_len_kernel, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)st, a);
   return (int)hipGetLastError();
 }
 

@@ -38,8 +38,7 @@ _SIGS = {
     "dxa_csv_tokenize": [c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p],
     "dxa_spark_hash_fixed": [c_p, c_i32, c_p, c_i64, c_p, c_p],
     "dxa_spark_hash_str": [c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
-    "dxa_serialize_lengths": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p],
-    "dxa_serialize_write": [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p, c_p],
+    "dxa_serialize_rows": [c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p],
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],
     "dxa_java_double_hostcheck": [c_p, c_i64, c_p, c_p],
     "dxa_json_parse": [c_p, c_p, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p,

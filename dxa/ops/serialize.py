@@ -275,16 +275,139 @@ class _DevBuilder:
             ops.append([1, idx, depth, 0])
         ops[pos][3] = mode | ((len(ops) - pos - 1) << 8)
 
-    def device_arrays(self, device):
+    def tables_blob(self, prog: List[int]) -> bytes:
+        """Node array, render program (padded to 8 B) and text pool as ONE buffer, the layout dxa_serialize_rows
+        expects: a single upload per rendered batch."""
         arr = (DevNode * max(1, len(self.nodes)))()
         for i, nd in enumerate(self.nodes):
             arr[i] = DevNode(nd["kind"], nd["nchildren"], nd["child0"], nd["drop_nulls"], nd["name"][0],
                              nd["name"][1], nd["const"][0], nd["const"][1], nd["data"], nd["valid"], nd["arena"],
                              nd["starts"], nd["lens"])
-        from . import native as N
-        raw = N.h2d(bytes(arr), torch.uint8, device)
-        text = N.h2d(bytes(self.text) + b"\0" * (-len(self.text) % 8 + 8), torch.uint8, device)
-        return raw, text
+        p = (ctypes.c_int32 * max(2, len(prog) + len(prog) % 2))(*prog)
+        text = bytes(self.text) + b"\0" * (-len(self.text) % 8 + 8)
+        return bytes(arr)[:ctypes.sizeof(DevNode) * len(self.nodes)] + bytes(p)[:((len(prog) * 4 + 7) // 8) * 8] + text
+
+
+class _SerSegs(ctypes.Structure):
+    _fields_ = [("nseg", ctypes.c_int32), ("pad", ctypes.c_int32), ("row", ctypes.c_int64 * 17),
+                ("pc", ctypes.c_int32 * 17), ("block", ctypes.c_int32 * 17)]
+
+
+MAX_SEGMENTS = 16
+_LDS_LIMIT = 64 * 1024
+STATS = {"rendered_bytes": 0, "d2h_bytes": 0, "d2h_s": 0.0, "launch_pairs": 0}
+
+
+def _render_members(members: List["Staged"]) -> None:
+    """Render every GPU-staged table of ``members`` with ONE length launch, one scan, one write launch, one upload
+    of the render tables and one D2H each for the lengths and the text (a segment per table); each member's
+    ``JsonLines`` is a slice of the shared pinned blob.  A gzip member is rendered alone (its compressed stream is
+    what crosses PCIe)."""
+    from . import native as N
+    dev = members[0].device
+    side = _side_stream(dev)
+    with torch.cuda.stream(side):
+        for m in members:
+            side.wait_event(m.event)
+        b = _DevBuilder()
+        progs = []
+        for m in members:
+            top = [b.add(c, nm) for nm, c in zip(m.table.names, m.table.columns)]
+            progs.append(b.program(top))
+        prog = [v for p in progs for v in p]
+        nprog = len(prog) // 4
+        blob = b.tables_blob(prog)
+        tw = (len(blob) - ctypes.sizeof(DevNode) * len(b.nodes) - ((len(prog) * 4 + 7) // 8) * 8) // 8
+        segs = _SerSegs()
+        segs.nseg = len(members)
+        r = pc = 0
+        for k, m in enumerate(members):
+            segs.row[k], segs.pc[k] = r, pc
+            r += m.n
+            pc += len(progs[k]) // 4
+        segs.row[len(members)], segs.pc[len(members)] = r, pc
+        n = r
+        lens_h = torch.empty(n, dtype=torch.int64, pin_memory=True)
+        if n:
+            tables = N.h2d(blob, torch.uint8, dev)
+            st = N.stream_handle(dev)
+            lens = torch.empty(n, dtype=torch.int64, device=dev)
+            N.call("dxa_serialize_rows", 0, N.ptr(tables), len(b.nodes), nprog, tw, ctypes.addressof(segs), N.ptr(lens),
+                   None, None, st)
+            ends = torch.cumsum(lens, 0)
+            lens_h.copy_(lens, non_blocking=True)
+            side.synchronize()
+        lens_np = lens_h.numpy()
+        total = int(lens_np.sum())
+        STATS["rendered_bytes"] += total
+        STATS["launch_pairs"] += 1
+        if n:
+            out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+            N.call("dxa_serialize_rows", 1, N.ptr(tables), len(b.nodes), nprog, tw, ctypes.addressof(segs), N.ptr(lens),
+                   N.ptr(ends), N.ptr(out), st)
+        if len(members) == 1 and members[0].compress and total > 1:
+            # gzip of the newline-joined documents (no trailing newline: what a blob sink writes), on the GPU;
+            # only the compressed stream crosses PCIe
+            from .deflate import gzip_device
+            gz = gzip_device(out, total - 1)
+            host = torch.empty(gz.numel(), dtype=torch.uint8, pin_memory=True)
+            side.synchronize()
+            d2h(host, gz, gz.numel(), side)
+            members[0]._done(JsonLines(None, lens_np - 1, gz=host.numpy()))
+            return
+        host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        side.synchronize()
+        d2h(host, out if n else host, total, side)
+    blob_np = host.numpy()                              # the pinned buffer itself, no copy
+    r = off = 0
+    for m in members:
+        ln = lens_np[r:r + m.n]
+        size = int(ln.sum())
+        m._done(JsonLines(blob_np[off:off + size], ln - 1))
+        r += m.n
+        off += size
+
+
+class RenderGroup:
+    """GPU-staged tables of one batch (every output's payloads) rendered together by whichever sink thread asks
+    first (``_render_members``); the others wait on the lock and take their slice."""
+
+    def __init__(self, members: List["Staged"]):
+        self.members = members
+        self.lock = threading.Lock()
+
+    def ensure(self) -> None:
+        with self.lock:
+            if any(m._result is None for m in self.members):
+                _render_members(self.members)
+
+
+def link_render_groups(staged: List["Staged"]) -> None:
+    """Group the GPU-staged, uncompressed, non-empty tables of a batch (same device, at most MAX_SEGMENTS per group,
+    render tables within the 64 KiB the kernels stage in LDS) so each group renders with one launch pair."""
+    seen, by_dev = set(), {}
+    for s in staged:
+        if not isinstance(s, Staged) or not s.gpu or s.compress or s.n == 0 or id(s) in seen or s.group is not None:
+            continue
+        seen.add(id(s))
+        by_dev.setdefault(s.device, []).append(s)
+    for ms in by_dev.values():
+        cur, size = [], 0
+        for m in ms:
+            est = m.lds_estimate()
+            if cur and (len(cur) == MAX_SEGMENTS or size + est > _LDS_LIMIT):
+                _close_group(cur)
+                cur, size = [], 0
+            cur.append(m)
+            size += est
+        _close_group(cur)
+
+
+def _close_group(ms: List["Staged"]) -> None:
+    if len(ms) > 1:
+        g = RenderGroup(ms)
+        for m in ms:
+            m.group = g
 
 
 _SDMA = os.environ.get("DXA_D2H_SDMA", "1") != "0"
@@ -297,15 +420,21 @@ def d2h(host: torch.Tensor, dev: torch.Tensor, nbytes: int, stream) -> None:
     global _SDMA
     if nbytes <= 0:
         return
-    if _SDMA:
-        from . import native as N
-        rc = N.lib().dxa_copy_sdma(host.data_ptr(), dev.data_ptr(), nbytes)
-        if rc == 0:
-            return
-        _SDMA = False
-    with torch.cuda.stream(stream):
-        host[:nbytes].copy_(dev[:nbytes], non_blocking=True)
-    stream.synchronize()
+    import time
+    t0 = time.perf_counter()
+    try:
+        if _SDMA:
+            from . import native as N
+            rc = N.lib().dxa_copy_sdma(host.data_ptr(), dev.data_ptr(), nbytes)
+            if rc == 0:
+                return
+            _SDMA = False
+        with torch.cuda.stream(stream):
+            host[:nbytes].copy_(dev[:nbytes], non_blocking=True)
+        stream.synchronize()
+    finally:
+        STATS["d2h_bytes"] += nbytes
+        STATS["d2h_s"] += time.perf_counter() - t0
 
 
 _side_streams = {}
@@ -348,6 +477,8 @@ class Staged:
         self.event = None
         self.gpu = gpu_serializer_enabled(table.device)
         self.compress = compress and self.gpu and os.environ.get("DXA_GPU_GZIP", "1") != "0"
+        self.group = None
+        self._result = None
         if self.gpu:
             self.table = table
             self.device = table.device
@@ -361,48 +492,27 @@ class Staged:
             self.event = torch.cuda.Event()
             self.event.record(torch.cuda.current_stream(table.device))
 
-    def _render_gpu(self) -> "JsonLines":
-        from . import native as N
-        dev = self.device
-        n = self.n
-        side = _side_stream(dev)
-        with torch.cuda.stream(side):
-            side.wait_event(self.event)
-            b = _DevBuilder()
-            top = [b.add(c, nm) for nm, c in zip(self.table.names, self.table.columns)]
-            nodes, text = b.device_arrays(dev)
-            prog = b.program(top)
-            prog_t = N.h2d(prog or [0], torch.int32, dev)
-            nprog = len(prog) // 4
-            st = N.stream_handle(dev)
-            lens = torch.empty(max(1, n), dtype=torch.int64, device=dev)
-            nn, tw = len(b.nodes), text.numel() // 8
-            N.call("dxa_serialize_lengths", N.ptr(nodes), nn, N.ptr(prog_t), nprog, N.ptr(text), tw, n, N.ptr(lens),
-                   st)
-            ends = torch.cumsum(lens[:n], 0)
-            offs = ends - lens[:n]
-            host_lens = torch.empty(n, dtype=torch.int64, pin_memory=True)
-            host_lens.copy_(lens[:n], non_blocking=True)
-            side.synchronize()
-            total = int(ends[-1].item()) if n else 0
-            out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-            N.call("dxa_serialize_write", N.ptr(nodes), nn, N.ptr(prog_t), nprog, N.ptr(text), tw, n, N.ptr(offs),
-                   N.ptr(out), st)
-            if self.compress and total > 1:
-                # gzip of the newline-joined documents (no trailing newline: what a blob sink writes), on the GPU;
-                # only the compressed stream crosses PCIe
-                from .deflate import gzip_device
-                gz = gzip_device(out, total - 1)
-                host = torch.empty(gz.numel(), dtype=torch.uint8, pin_memory=True)
-                side.synchronize()
-                d2h(host, gz, gz.numel(), side)
-                self.table = None
-                return JsonLines(None, host_lens.numpy() - 1, gz=host.numpy())
-            host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
-            side.synchronize()
-            d2h(host, out, total, side)
+    def _done(self, jl: "JsonLines") -> None:
+        self._result = jl
         self.table = None
-        return JsonLines(host.numpy(), host_lens.numpy() - 1)     # the pinned buffer itself, no copy
+
+    def lds_estimate(self) -> int:
+        """Upper bound of this table's share of the render tables (nodes + program + names) in LDS."""
+        def walk(c, name):
+            kids = getattr(c, "children", None) or getattr(c, "elements", None) or []
+            names = getattr(c, "names", None) or [None] * len(kids)
+            const = len(str(getattr(c, "value", "") or "")) if type(c).__name__ == "ConstColumn" else 0
+            return (ctypes.sizeof(DevNode) + 32 + len(name or "") + 16 + const +
+                    sum(walk(k, nm) for nm, k in zip(names, kids)))
+        return sum(walk(c, nm) for nm, c in zip(self.table.names, self.table.columns))
+
+    def _render_gpu(self) -> "JsonLines":
+        if self._result is None:
+            if self.group is not None:
+                self.group.ensure()
+            else:
+                _render_members([self])
+        return self._result
 
     def render(self, nthreads: Optional[int] = None) -> "JsonLines":
         if self.gpu:

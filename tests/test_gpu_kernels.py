@@ -249,6 +249,26 @@ def test_gpu_serializer_matches_host(gpu, monkeypatch):
     assert dev.lens.tolist() == host.lens.tolist()
 
 
+def test_gpu_serializer_render_group_matches_host(gpu):
+    """Several output tables of a batch (different schemas and row counts, one of 300 rows so a workgroup would
+    straddle segments if the kernel did not pad them) render in one launch pair; each slice equals the table's own
+    host rendering."""
+    from dxa.ops import serialize as ser
+    t = _serializer_table("cpu")
+    parts = [t, t.take(torch.arange(0, 300)), Table(["s", "l"], [t.columns[2], t.columns[0]], t.length),
+             t.take(torch.arange(1000, 1257))]
+    hosts = [ser.Staged(p).render() for p in parts]
+    staged = [ser.Staged(p.to(gpu)) for p in parts]
+    ser.link_render_groups(staged)
+    assert staged[0].group is not None and all(s.group is staged[0].group for s in staged)
+    before = ser.STATS["launch_pairs"]
+    for k in (2, 0, 3, 1):                               # any member may trigger the render
+        dev = staged[k].render()
+        assert dev.blob == hosts[k].blob, k
+        assert dev.lens.tolist() == hosts[k].lens.tolist()
+    assert ser.STATS["launch_pairs"] == before + 1
+
+
 def test_gpu_java_double_matches_host(gpu):
     import ctypes
     import numpy as np
