@@ -369,6 +369,10 @@ def main():
 
     ready = {}
     parse_ahead = on_gpu and os.environ.get("DXA_PARSE_AHEAD", "1") != "0"
+    # parse-ahead on its own stream, queued BEFORE the previous batch's process_batch so the parse overlaps that
+    # batch's query kernels (DXA_PARSE_STREAM=0: behind them on the compute stream, after process_batch)
+    parse_stream = torch.cuda.Stream(device) if parse_ahead and os.environ.get("DXA_PARSE_STREAM", "1") != "0" \
+        else None
 
     def take(i):
         db, do, ev = staged.pop(i)
@@ -381,15 +385,32 @@ def main():
                     t.record_stream(cur)
         return rb
 
+    def take_to(i, stream):
+        """Batch i for a parse on ``stream``: ordered after its ingest there; its bytes are also read later on the
+        compute stream (string columns view them), so both streams hold them."""
+        db, do, ev = staged.pop(i)
+        rb = db if isinstance(db, RawBatch) else RawBatch(db, do, E)
+        if ev is not None:
+            stream.wait_event(ev)
+        cur = torch.cuda.current_stream(device)
+        for t in (rb.buf, rb.offs, rb.ends):
+            if t is not None:
+                t.record_stream(stream)
+                t.record_stream(cur)
+        return rb
+
     def step(i):
         rb = ready.pop(i, None) or take(i)
         t_s = time.perf_counter()
         stage(i + depth)
         t_p = time.perf_counter()
+        # parse-ahead (Processor.prepare).  Never across the warm-up → timed boundary or past the last timed batch,
+        # so every timed batch parses inside the timed region
+        ahead = parse_ahead and i + 1 in staged and i + 1 != warmup and i + 1 < warmup + args.steps
+        if ahead and parse_stream is not None:
+            ready[i + 1] = proc.prepare(take_to(i + 1, parse_stream), stream=parse_stream)
         m = proc.process_batch(rb, batch_time(i), interval_us)
-        # parse-ahead (Processor.prepare): queue batch i+1's parse behind batch i's kernels.  Never across the
-        # warm-up → timed boundary or past the last timed batch, so every timed batch parses inside the timed region
-        if parse_ahead and i + 1 in staged and i + 1 != warmup and i + 1 < warmup + args.steps:
+        if ahead and parse_stream is None:          # behind batch i's kernels on the compute stream
             ready[i + 1] = proc.prepare(take(i + 1))
         if host_trace is not None:
             host_trace.append((i, round((t_p - t_s) * 1e3, 2), round((time.perf_counter() - t_p) * 1e3, 2)))
@@ -425,6 +446,7 @@ def main():
         cprof.enable()
     from dxa.ops import serialize as _ser0
     ser_stats0 = dict(_ser0.STATS)
+    host0 = dict(getattr(proc, "host_acc", {}))
     t0 = time.perf_counter()
     last = None
     for i in range(warmup, warmup + args.steps):
@@ -555,6 +577,8 @@ def main():
         out["max_hbm_allocated_gb"] = round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
     if args.profile_stages:
         out["stage_s"] = {k: round(v, 5) for k, v in proc.stage_times.items()}
+        out["host_ms_per_step"] = {k: round((v - host0.get(k, 0.0)) / args.steps * 1e3, 3)
+                                   for k, v in getattr(proc, "host_acc", {}).items()}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -13,6 +13,7 @@ datax/processor/CommonProcessorFactory.scala:42-660) re-designed for one MI355X 
 """
 from __future__ import annotations
 
+import collections
 import copy
 import datetime as _dt
 import json
@@ -143,6 +144,9 @@ class Processor:
         self.last_views: Dict[str, Table] = {}
         self.keep_views = False
         self.stage_times: Dict[str, float] = {}
+        # host wall time per phase / statement, summed over batches (no device syncs): where the planning thread
+        # spends a batch (bench.py --profile-stages prints it per step)
+        self.host_acc: Dict[str, float] = collections.defaultdict(float)
         self._parsed: Dict[str, object] = {}
         # output pipelining: batch t's sink work overlaps batch t+1's device work (at most one batch in flight)
         self.pipeline_outputs = pipeline_outputs if pipeline_outputs is not None else \
@@ -267,13 +271,22 @@ class Processor:
         return keep or None
 
     # ------------------------------------------------------------------------------------------------------------
-    def prepare(self, raw: RawBatch) -> RawBatch:
-        """Queue the batch's JSON parse now, on the current stream (call it right after the previous batch's
-        ``process_batch``).  The parse kernels then run while the host is still planning the previous batch's tail
-        and this batch's start, and ``project`` finds the per-field null counts already on the host instead of
-        waiting for the parse.  A no-op off the GPU and with an input normalizer (which rewrites the bytes first)."""
+    def prepare(self, raw: RawBatch, stream=None) -> RawBatch:
+        """Queue the batch's JSON parse now, so that ``project`` finds the per-field null counts already on the
+        host instead of waiting for the parse.  A no-op off the GPU and with an input normalizer (which rewrites
+        the bytes first).
+
+        ``stream=None``: on the current stream (call it right after the previous batch's ``process_batch``; the
+        parse then runs behind that batch's kernels).  A side ``stream`` (its own parse stream, already ordered after
+        the batch's ingest): call it BEFORE the previous batch's ``process_batch`` — the parse then overlaps that
+        batch's query kernels, which leave most of the chip idle (profiles/round4: the ``full`` flow's kernels keep
+        the GPU busy ~35 % of the step), and ``project`` no longer waits a whole parse per batch."""
         if raw.pending is None and self.normalizer is None and raw.buf.device.type == "cuda":
-            raw.pending = parse_async(raw.buf, raw.offs, self.parse_plan, raw.ends)
+            if stream is None:
+                raw.pending = parse_async(raw.buf, raw.offs, self.parse_plan, raw.ends)
+            else:
+                with torch.cuda.stream(stream):
+                    raw.pending = parse_async(raw.buf, raw.offs, self.parse_plan, raw.ends)
         return raw
 
     def project(self, raw: RawBatch, batch_time_us: int, ctx: EvalContext) -> Table:
@@ -363,8 +376,10 @@ class Processor:
         part = P.PARTITIONED if P.active() else P.REPLICATED
         projected.dist = part
         if self.window_store is not None:
+            tw = time.perf_counter()
             with tracing.stage("windows", self.stage_times):
                 views, cnt = self.window_store.process(projected, batch_time_us, interval_us)
+            self.host_acc["windows"] += time.perf_counter() - tw
             for k, v in views.items():
                 v.dist = part
                 cat.register(k, v)
@@ -388,9 +403,10 @@ class Processor:
                     if cmd.command_type == COMMAND_COMMAND:
                         self._run_command(cmd.text)
                         continue
-                    ts = time.perf_counter() if _SYNC_STAGES else 0.0
+                    ts = time.perf_counter()
                     with tracing.stage(f"sql:{cmd.name}"):
                         results = [execute(self._query(cmd), cat, ctx)]
+                    self.host_acc[f"sql:{cmd.name}"] += time.perf_counter() - ts
                     if _SYNC_STAGES:
                         self._sync()
                         self.stage_times[f"sql:{cmd.name}"] = time.perf_counter() - ts
@@ -398,8 +414,9 @@ class Processor:
                     cmd = cmds[k]
                     st = self.state_tables.get(cmd.name)
                     if st is not None:
-                        self._complete_inflight()      # the previous batch's state flip must be durable first
-                        result = st.overwrite(result)
+                        # the device-side state moves on now; the standby write waits for the previous batch's
+                        # flip (StateTable.release in _complete_inflight), not this batch
+                        result = st.overwrite(result, tag=batch_time_us)
                     cat.register(cmd.name, result)
                     views[cmd.name] = result
         self._sync()
@@ -417,7 +434,10 @@ class Processor:
             staged.append((op.name, op.stage(t, ctx)))
         from ..ops.serialize import link_render_groups
         link_render_groups([p for _, st in staged for p in st.payloads()])    # one render launch pair per batch
+        t2 = time.perf_counter()
+        self.host_acc["outputs:stage"] += t2 - t1
         self._complete_inflight()
+        self.host_acc["outputs:complete_previous"] += time.perf_counter() - t2
         from ..io.sinks import _pool
         target = getattr(self, "_batch_target", None)
         fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(_timed, st.finish, partition_time, target))
@@ -647,18 +667,19 @@ class Processor:
             for k, v in res.items():
                 metrics[f"Output_{name}_{k}"] = float(v)
         for st in self.state_tables.values():
-            st.flush()                 # this rank's standby part is durable before the all-reduce (= the barrier)
+            st.flush(fl.batch_time_us)  # this rank's standby part is durable before the all-reduce (= the barrier)
         # batch metrics are job-wide: counts summed, latencies maxed over ranks, key sets checked first (timings
         # stay per-rank)
         metrics = fl.metrics = P.reduce_metrics(metrics, self.device)
         flipped = False
         for st in self.state_tables.values():
-            flipped |= st.modified
-            st.persist()
+            flipped |= st.persist(fl.batch_time_us)
         if flipped and P.active():
             # rank 0 flipped metadata.info just now: no rank may overwrite the copy the old metadata named (its next
             # standby) before that flip is on disk — the next batch's standby writes are ordered after this point
             P.order_point(self.device)
+        for st in self.state_tables.values():
+            st.release()               # the next batch's deferred standby writes may start
         metrics.update(tracing.stage_metrics(fl.stages))          # per-rank stage timings (not all-reduced)
         # processing latency = batch start → its last sink write finished (measured where the write finished, not
         # where the completion was observed)
@@ -711,15 +732,19 @@ class Processor:
             refresh(batch_time_us)
         try:
             _maybe_inject_fault(self.batches)
+            tp = time.perf_counter()
             projected = self.project(raw, batch_time_us, ctx)
+            self.host_acc["project"] += time.perf_counter() - tp
             # a device-side decode failure (corrupt LZ4 block, bad CRC) must stop the batch before any of its rows
             # reach an accumulator or a sink — the host decoder raises at the same point (before processing).  The
             # status word sits in pinned memory behind the decode, which the parse above already waited for
             check = getattr(raw.status, "raise_if_failed", None)
             if check is not None:
                 check(f"batch {batch_time_us}")
+            tr = time.perf_counter()
             metrics = self.route(projected, batch_time_us, interval_us, ctx,
                                  partition_time or _dt.datetime.utcnow(), t0)
+            self.host_acc["route"] += time.perf_counter() - tr
             self.batches += 1
             return metrics
         except Exception:

@@ -21,7 +21,7 @@ is tagged ``partitioned`` (the next GROUP BY re-shuffles it by key hash).
 from __future__ import annotations
 
 from concurrent.futures import ThreadPoolExecutor
-from typing import Dict, List
+from typing import Any, Callable, Dict, List, Optional
 
 import torch
 
@@ -33,6 +33,24 @@ from .types import StructType, parse_ddl_schema
 _writer = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dxa-state")
 
 
+class _Write:
+    """One batch's overwrite of a state table: the standby-part write (submitted, or deferred until the previous
+    batch's flip is released) and the metadata that batch's ``persist`` flips to."""
+
+    def __init__(self, tag, params: Dict[str, str]):
+        self.tag = tag
+        self.params = params
+        self.fut = None
+        self.job: Optional[Callable[[], Any]] = None
+        self.persisted = False
+
+    def wait(self):
+        if self.job is not None:            # never released: nothing may still reference its copy
+            self.fut, self.job = _writer.submit(self.job), None
+        if self.fut is not None:
+            self.fut.result()
+
+
 class StateTable:
     def __init__(self, name: str, schema: StructType, location: str, device):
         self.name = name
@@ -42,8 +60,7 @@ class StateTable:
         self.meta_file = self.location + "metadata.info"
         self.rank, self.world = P.rank(), P.world()
         self.params = self._read_meta()
-        self.modified = False
-        self._pending = None
+        self._writes: List[_Write] = []      # overwrites not yet released, oldest first
         self.active: Table = self._load(self.params["active"])
 
     # ---- metadata ------------------------------------------------------------------------------------------------
@@ -103,31 +120,45 @@ class StateTable:
         return t
 
     # ---- update --------------------------------------------------------------------------------------------------
-    def overwrite(self, t: Table):
-        """INSERT OVERWRITE standby + flip (returns the new active table).  The standby Parquet part is written by
-        a background writer from pinned host buffers; ``persist`` (after the batch's outputs) waits for it before
-        it flips ``metadata.info``, so the metadata never names a partially written copy."""
+    def overwrite(self, t: Table, tag=None):
+        """INSERT OVERWRITE standby + flip (returns the new active table).  The device work (conform, one packed
+        D2H) starts here; the standby Parquet part is written by a background writer from the pinned host copy.
+        ``persist(tag)`` (after the batch's outputs) waits for that write before it flips ``metadata.info``, so the
+        metadata never names a partially written copy.
+
+        The next batch may overwrite before this one is persisted (outputs are pipelined): its write goes to the
+        copy the on-disk metadata still names active, so it is deferred until ``release`` of this batch's flip —
+        the batch itself (the device-side state) does not wait."""
         from ..io.arrow import to_host_async
         dist = P.dist_of(t)
         t = _conform(t, self.schema)
         t.dist = dist if P.active() else P.REPLICATED
-        self._wait_write()
-        if P.active() and dist == P.REPLICATED and self.rank != 0:
-            self._pending = None          # replicated result: rank 0's part-0 is the copy
-        else:
+        job = None
+        if not (P.active() and dist == P.REPLICATED and self.rank != 0):   # replicated: rank 0's part-0 is the copy
             host, ev = to_host_async(t)
-            self._pending = _writer.submit(self._write, self.params["standby"], self.rank, host, ev)
+            suffix, rank = self.params["standby"], self.rank
+            job = lambda: self._write(suffix, rank, host, ev)             # noqa: E731
         self.params = {"active": self.params["standby"], "standby": self.params["active"],
                        "parts": str(self.world), "dist": t.dist}
-        self.modified = True
+        w = _Write(tag, dict(self.params))
+        if job is not None:
+            if self._writes:
+                w.job = job
+            else:
+                w.fut = _writer.submit(job)
+        self._writes.append(w)
         self.active = t
         return t
 
-    def _wait_write(self):
-        p = self._pending
-        if p is not None:
-            self._pending = None
-            p.result()
+    @property
+    def modified(self) -> bool:
+        return any(not w.persisted for w in self._writes)
+
+    def _entry(self, tag) -> Optional[_Write]:
+        for w in self._writes:
+            if not w.persisted and (tag is None or w.tag == tag):
+                return w
+        return None
 
     def _write(self, suffix: str, part: int, t: Table, event=None):
         import pyarrow.parquet as pq
@@ -143,19 +174,35 @@ class StateTable:
                        write_statistics=False)
         tmp.replace(p)
 
-    def flush(self):
-        """Make this rank's standby part durable (call on every rank before the barrier that precedes ``persist``)."""
-        self._wait_write()
+    def flush(self, tag=None):
+        """Make this rank's standby part of batch ``tag`` durable (call on every rank before the barrier that
+        precedes ``persist``)."""
+        w = self._entry(tag)
+        if w is not None:
+            w.wait()
 
-    def persist(self):
-        """Flip ``metadata.info`` (rank 0 only; every rank's part must already be durable — see ``flush``).  At N
-        ranks the processor follows the flips with ``parallel.order_point``: the next batch's standby writes (into
-        the copy the previous metadata named active) are ordered after rank 0's flip."""
-        self._wait_write()
-        if self.modified:
-            if self.rank == 0:
-                fs.write_atomic(self.meta_file, "\n".join(f"{k}={v}" for k, v in self.params.items()))
-            self.modified = False
+    def persist(self, tag=None) -> bool:
+        """Flip ``metadata.info`` to batch ``tag``'s copy (rank 0 only; every rank's part must already be durable —
+        see ``flush``).  At N ranks the processor follows the flips with ``parallel.order_point`` and then
+        ``release``: the next batch's standby write (into the copy the previous metadata named active) starts only
+        after rank 0's flip.  Returns whether there was a flip."""
+        w = self._entry(tag)
+        if w is None:
+            return False
+        w.wait()
+        if self.rank == 0:
+            fs.write_atomic(self.meta_file, "\n".join(f"{k}={v}" for k, v in w.params.items()))
+        w.persisted = True
+        return True
+
+    def release(self) -> None:
+        """The persisted flips are ordered (after ``order_point`` at N ranks): drop them and start the next
+        batch's deferred standby write."""
+        while self._writes and self._writes[0].persisted:
+            self._writes.pop(0)
+        if self._writes and self._writes[0].job is not None:
+            w = self._writes[0]
+            w.fut, w.job = _writer.submit(w.job), None
 
 
 def _conform(t: Table, schema: StructType) -> Table:

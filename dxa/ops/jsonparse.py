@@ -248,10 +248,10 @@ class PendingParse:
     to pinned memory behind the kernels), then assembles the columns.  ``Processor.prepare`` starts batch t+1's
     parse while batch t is still being planned, so the wait is normally already over."""
 
-    def __init__(self, done=None, plan=None, arena=None, parts=None, n=0, counts=None, event=None):
+    def __init__(self, done=None, plan=None, arena=None, parts=None, n=0, counts=None, event=None, stream=None):
         self._done = done
         self.plan, self.arena, self.parts, self.n = plan, arena, parts, n
-        self.counts, self.event = counts, event
+        self.counts, self.event, self.stream = counts, event, stream
 
     def result(self):
         if self._done is None:
@@ -259,8 +259,16 @@ class PendingParse:
                 self.event.synchronize()
             nulls = self.counts.tolist() if self.counts is not None else [1] * len(self.plan.nodes)
             vals, lens, valid, row_ok = self.parts
+            if self.stream is not None and self.arena is not None:
+                cur = torch.cuda.current_stream(self.arena.device)
+                if cur != self.stream:
+                    # parsed on a side stream (Processor.prepare): the host already waited for it, so the consumer
+                    # stream needs no device wait, but the caching allocator must not hand these blocks back to the
+                    # parse stream while the consumer's kernels may still read them
+                    for t in (vals, lens, valid, row_ok, self.arena):
+                        t.record_stream(cur)
             self._done = (_assemble(self.plan, self.arena, vals, lens, valid, self.n, nulls), row_ok)
-            self.parts = self.arena = self.counts = self.event = None
+            self.parts = self.arena = self.counts = self.event = self.stream = None
         return self._done
 
 
@@ -309,7 +317,8 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
         event = torch.cuda.Event()
         event.record(torch.cuda.current_stream(buf.device))
     parts = (vals[:, :n], lens[:, :n], valid[:, :n].view(torch.bool), row_ok[:n].view(torch.bool))
-    return PendingParse(plan=plan, arena=buf, parts=parts, n=n, counts=counts, event=event)
+    return PendingParse(plan=plan, arena=buf, parts=parts, n=n, counts=counts, event=event,
+                        stream=torch.cuda.current_stream(buf.device))
 
 
 def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):

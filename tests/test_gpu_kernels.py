@@ -492,14 +492,19 @@ def test_processor_prepare_same_outputs(gpu, variant, tmp_path):
     bufs = [generate(prog, n, gpu, seed=i + 1, row0=i * n, base_ms=t0 // 1000 + i * 1000 - 1000, step_us=50)
             for i in range(3)]
     views = []
-    for ahead in (False, True):
+    side = torch.cuda.Stream(gpu)
+    for ahead in (False, True, "side"):
         proc = Processor(iot.flow_settings(workdir=str(tmp_path / f"w{ahead}"), variant=variant), gpu)
         proc.keep_views = True
         raws = [RawBatch(b.clone(), o, n) for b, o in bufs]      # a parse consumes its bytes (in-place unescape)
+        side.wait_stream(torch.cuda.current_stream(gpu))
         got = []
         for i, rb in enumerate(raws):
+            if ahead == "side" and i + 1 < len(raws):
+                proc.prepare(raws[i + 1], stream=side)           # overlaps batch i's query kernels
+                assert raws[i + 1].pending is not None
             proc.process_batch(rb, t0 + i * 1_000_000, 1_000_000)
-            if ahead and i + 1 < len(raws):
+            if ahead is True and i + 1 < len(raws):
                 proc.prepare(raws[i + 1])
                 assert raws[i + 1].pending is not None
             name = "DeviceSummary" if variant == "groupby" else "DeviceWindow"
@@ -507,7 +512,7 @@ def test_processor_prepare_same_outputs(gpu, variant, tmp_path):
             got.append(sorted(zip(*[c.to_pylist() for c in v.columns]), key=lambda r: tuple(map(str, r[:3]))))
         proc.drain()
         views.append(got)
-    for x, y in zip(*views):                                # per batch
+    for x, y in [(a, b) for v in views[1:] for a, b in zip(views[0], v)]:    # per batch, vs parse-in-process
         assert len(x) == len(y)
         for rx, ry in zip(x, y):
             for a, b in zip(rx, ry):

@@ -157,3 +157,38 @@ def test_state_restart_resumes(tmp_path, w_before, w_after):
     _run_world(w_before, str(tmp_path / "a"), state, [0, 1])
     after = _run_world(w_after, str(tmp_path / "b"), state, [2])
     assert _union(after, 0) == _expected([0, 1, 2])
+
+
+def test_pipelined_overwrite_defers_standby_write_until_previous_flip(tmp_path):
+    """Batch t+1 overwrites the state before batch t is persisted (outputs pipelined): its standby write must wait
+    for t's flip + release (it targets the copy t's on-disk metadata still names active), while the device-side
+    state moves on at once."""
+    import os
+    from dxa.engine.column import column_from_pylist, Table
+    from dxa.engine.state import StateTable
+    from dxa.engine.types import parse_ddl_schema
+    loc = str(tmp_path / "st")
+    st = StateTable("S", parse_ddl_schema("k long, v long"), loc, "cpu")
+
+    def tab(v):
+        return Table(["k", "v"], [column_from_pylist([1], "long"), column_from_pylist([v], "long")], 1)
+
+    def meta():
+        return dict(line.split("=", 1) for line in open(os.path.join(loc, "metadata.info")).read().split())
+
+    st.overwrite(tab(10), tag=1)              # batch 1 → copy B
+    st.overwrite(tab(20), tag=2)              # batch 2 → copy A, deferred (batch 1 not flipped yet)
+    assert st.active.columns[1].to_pylist() == [20]
+    assert st._writes[1].job is not None and st._writes[1].fut is None
+    st.flush(1)
+    assert st.persist(1)
+    assert meta()["active"] == "B"
+    assert not os.path.exists(os.path.join(loc, "A", "part-0.parquet"))   # batch 2 has not touched A yet
+    st.release()
+    st.flush(2)
+    assert os.path.exists(os.path.join(loc, "A", "part-0.parquet"))
+    assert st.persist(2)
+    st.release()
+    assert meta()["active"] == "A" and not st.modified
+    again = StateTable("S", parse_ddl_schema("k long, v long"), loc, "cpu")
+    assert again.active.columns[1].to_pylist() == [20]
