@@ -670,39 +670,39 @@ def concat_tables(tables: List[Table]) -> Table:
     names = tables[0].names
     device = tables[0].device
     batched = torch.device(device).type == "cuda"
-    segs = []
+    segs = None
+    if batched:
+        from ..ops.copybatch import Segments, concat_prims, valid_segments
+        segs = Segments()
+    same = all(t.names == names for t in tables)      # the usual case: one schema, no per-column name lookups
     cols = []
     str_groups = []                                 # (output position, parts) of the string columns
     for i, n in enumerate(names):
-        parts = []
-        for t in tables:
-            c = t.column(n) if t.names[i].lower() != n.lower() else t.columns[i]
-            parts.append(c)
-        if batched and all(isinstance(c, PrimColumn) for c in parts):
-            from ..ops.copybatch import concat_prims
-            got = concat_prims(parts, device)
-            if got is not None:
-                data, valid, sg = got
-                segs.extend(sg)
-                cols.append(PrimColumn(parts[0].dtype, data, valid))
+        if same:
+            parts = [t.columns[i] for t in tables]
+        else:
+            parts = [t.column(n) if t.names[i].lower() != n.lower() else t.columns[i] for t in tables]
+        kinds = {type(c) for c in parts}
+        if batched and len(kinds) == 1:
+            kind = next(iter(kinds))
+            if kind is PrimColumn:
+                got = concat_prims(parts, device, segs)
+                if got is not None:
+                    cols.append(PrimColumn(parts[0].dtype, got[0], got[1]))
+                    continue
+            elif kind is StrColumn:
+                str_groups.append((len(cols), parts))
+                cols.append(None)
                 continue
-        if (batched and all(isinstance(c, StrColumn) and not isinstance(c, JsonColumn) for c in parts)
-                and len({type(c) for c in parts}) == 1):
-            str_groups.append((len(cols), parts))
-            cols.append(None)
-            continue
         cols.append(concat_columns(parts))
     if str_groups:
-        from ..ops.copybatch import valid_segments
         from ..ops.strings import concat_multi
         got = concat_multi([p for _, p in str_groups])
         for (at, parts), (arena, starts, lens) in zip(str_groups, got):
-            valid, sg = valid_segments(parts, device)
-            segs.extend(sg)
+            valid, _ = valid_segments(parts, device, segs)
             cols[at] = type(parts[0])(arena, starts, lens, valid, parts[0].dtype)
     if segs:
-        from ..ops.copybatch import copy_batch
-        copy_batch(segs, device)                    # every fixed-width leaf of every table: one launch
+        segs.launch(device)                         # every fixed-width leaf of every table: one launch
     return Table(names, cols, sum(t.length for t in tables), device)
 
 

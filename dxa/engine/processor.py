@@ -416,7 +416,8 @@ class Processor:
                     if st is not None:
                         # the device-side state moves on now; the standby write waits for the previous batch's
                         # flip (StateTable.release in _complete_inflight), not this batch
-                        result = st.overwrite(result, tag=batch_time_us)
+                        with tracing.host_section("state:overwrite"):
+                            result = st.overwrite(result, tag=batch_time_us)
                     cat.register(cmd.name, result)
                     views[cmd.name] = result
         self._sync()

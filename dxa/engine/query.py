@@ -19,6 +19,7 @@ from .. import parallel as P
 from ..ops.hashing import hash_columns
 from ..sql import ast as A
 from ..sql.parser import parse_query
+from ..telemetry.tracing import host_section
 from .column import (ArrayColumn, Column, ConstColumn, LazyColumns, PrimColumn, StrColumn, StructColumn, Table,
                      concat_columns, concat_tables, materialize, take_columns)
 from .expr import (AGG_FUNCS, DeferredColumns, EvalContext, EvalError, HiddenQual, Scope, TakenColumns, cast_column,
@@ -203,7 +204,8 @@ def _set_op(op: A.SetOp, left: Table, right: Table) -> Table:
         right = _gathered(right) if rd != P.REPLICATED else right
         ld = rd = P.REPLICATED
     if op.op == "union":
-        out = concat_tables([left, right])
+        with host_section("setop:concat"):
+            out = concat_tables([left, right])
         out.dist = P.REPLICATED if (ld == P.REPLICATED and rd == P.REPLICATED) else P.PARTITIONED
         return out if op.all else distinct(out)
     # INTERSECT / EXCEPT (distinct semantics)
@@ -933,6 +935,8 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     span = BLOCK * max(1, store.interval_us)
     parts = []
     by_block: Dict[int, list] = {}
+    sec = host_section("paned:partials")
+    sec.__enter__()
     try:
         for pane, full in t.pieces():
             if full and cacheable and store.interval_us:
@@ -958,15 +962,19 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
             parts.append(pane_partial(_EmptyPane(empty), False))
     except _NotPaned:
         return None
+    finally:
+        sec.__exit__(None, None, None)
     plan, key_names, gexprs = state["meta"]
     parts = [p for p in parts if p.length] or parts[:1]
     dev = proto.device
     grouped = bool(sel.group_by)
-    got = concat_tables(parts)
+    with host_section("paned:concat"):
+        got = _concat_panes(parts, store, fp)
     tag = P.REPLICATED
     if P.active() and t.dist != P.REPLICATED:
         got, tag = D.exchange_partials(got, key_names, grouped)
-    out_keys, finals, ng = D.merge_partials(got, plan, key_names, aggs, grouped)
+    with host_section("paned:merge"):
+        out_keys, finals, ng = D.merge_partials(got, plan, key_names, aggs, grouped)
     subst = dict(finals)
     for g, k in zip(gexprs, out_keys):
         subst[g.key()] = k
@@ -977,6 +985,52 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
         out = out.filter(predicate_mask(evaluate(sel.having, escope, ctx, subst)))
     out.dist = tag if grouped else P.REPLICATED
     return out
+
+
+def _row_view(t: Table, a: int, b: int) -> Optional[Table]:
+    """Rows [a, b) of a table of flat columns as views (no copy, no launch); None for other column kinds."""
+    cols = []
+    for c in t.columns:
+        v = None if c.valid is None else c.valid[a:b]
+        if type(c) is PrimColumn:
+            cols.append(PrimColumn(c.dtype, c.data[a:b], v))
+        elif type(c) is StrColumn:
+            cols.append(StrColumn(c.arena, c.starts[a:b], c.lens[a:b], v, c.dtype))
+        else:
+            return None
+    return Table(t.names, cols, b - a, t.device)
+
+
+def _concat_panes(parts: List[Table], store, fp) -> Table:
+    """``concat_tables(parts)`` for a window's partial tables, reusing last batch's concatenation: from one batch
+    to the next only the edges change (the clipped oldest panes, the newest pane), so the run of parts that ended
+    last batch's list and reappears here is taken as ONE row view of last batch's result instead of ~30 tables
+    (a block completing or expiring breaks the run: then everything is concatenated afresh).  The cache holds the
+    parts themselves, so no id is reused while it is alive."""
+    cache = getattr(store, "concat_cache", None)
+    if cache is None:
+        cache = store.concat_cache = {}
+    hit = cache.get(fp)
+    pieces = parts
+    if hit is not None and len(parts) >= 4:
+        cparts, coffs, ctab = hit
+        pos = {id(p): k for k, p in enumerate(cparts)}
+        a = next((k for k, p in enumerate(parts) if id(p) in pos), None)
+        if a is not None:
+            j = pos[id(parts[a])]
+            m = 0
+            while a + m < len(parts) and j + m < len(cparts) and parts[a + m] is cparts[j + m]:
+                m += 1
+            if j + m == len(cparts) and m >= 3:
+                mid = _row_view(ctab, coffs[j], coffs[j + m])
+                if mid is not None:
+                    pieces = parts[:a] + [mid] + parts[a + m:]
+    got = concat_tables(pieces)
+    offs = [0]
+    for p in parts:
+        offs.append(offs[-1] + p.length)
+    cache[fp] = (list(parts), offs, got)
+    return got
 
 
 def _lookup(src: A.TableRef, catalog: Catalog):
@@ -1249,7 +1303,8 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
     if P.active() and getattr(scope, "dist", P.REPLICATED) != P.REPLICATED:
         return _aggregate_distributed(sel, items, scope, ctx, gexprs, keys)
     if gexprs:
-        groups = G.group_rows(keys)
+        with host_section("aggregate:group_rows"):
+            groups = G.group_rows(keys)
     else:
         # global aggregate: one group, even over zero rows
         groups = G.Groups(torch.zeros(n, dtype=torch.int32 if dev.type == "cuda" else torch.int64, device=dev), 1,
@@ -1259,7 +1314,8 @@ def _aggregate(sel: A.Select, items, scope: Scope, ctx) -> Table:
         _collect_aggs(e, ctx, aggs)
     if sel.having is not None:
         _collect_aggs(sel.having, ctx, aggs)
-    subst = _eval_aggs(aggs, scope, groups, ctx)
+    with host_section("aggregate:aggs"):
+        subst = _eval_aggs(aggs, scope, groups, ctx)
     ng = groups.ngroups
     if n == 0 and not gexprs:
         rep_scope = Scope(scope.names, [ConstColumn(None, c.dtype, 1, dev) for c in scope.cols], scope.quals, 1, dev)

@@ -23,6 +23,7 @@ import torch
 
 from .column import PrimColumn, StrColumn, StructColumn, Table, concat_tables, ConstColumn
 from .expr import EvalError
+from ..telemetry.tracing import host_section
 
 PROCESS_PREFIX_KEY = "timewindow."
 
@@ -230,10 +231,12 @@ class WindowStore:
         if projected.length:
             # one host read for the common case (every event valid and not late): the batch's pane statistics and
             # the late-event check come back together; otherwise filter, then take the kept rows' statistics
-            ts, ok = self._ts(projected)
-            lo_, hi_, nok, nkeep = _ts_stats(ts, ok, E)
+            with host_section("windows:stats"):
+                ts, ok = self._ts(projected)
+                lo_, hi_, nok, nkeep = _ts_stats(ts, ok, E)
             if int(nkeep) == projected.length:
-                kept = _compact_table(projected)
+                with host_section("windows:compact"):
+                    kept = _compact_table(projected)
                 cur = Pane(batch_time_us, kept, int(lo_), int(hi_), True)
             else:
                 kept = _compact_table(projected.filter(ok & (ts >= E)))

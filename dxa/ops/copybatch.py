@@ -19,66 +19,122 @@ _CHUNK = None
 Segment = Tuple[Optional[torch.Tensor], int, torch.Tensor, int, int, int]
 
 
-def copy_batch(segments: Sequence[Segment], device) -> None:
+def _chunk_size() -> int:
     global _CHUNK
     if _CHUNK is None:
         if N.lib().dxa_copy_chunk_size() != 32:
             raise N.NativeError("CopyChunk layout mismatch between copybatch.py and copy_batch.hip")
         _CHUNK = int(N.lib().dxa_copy_chunk_bytes())
-    rows: List[Tuple[int, int, int, int]] = []
-    for src, so, dst, do, nb, fill in segments:
-        if nb <= 0:
-            continue
-        sp = 0 if src is None else src.data_ptr() + so
-        dp = dst.data_ptr() + do
-        for k in range(0, nb, _CHUNK):
-            rows.append((0 if src is None else sp + k, dp + k, min(_CHUNK, nb - k), fill))
-    if not rows:
-        return
-    tab = torch.from_numpy(np.array(rows, dtype=np.uint64).view(np.int64)).pin_memory()
-    dtab = tab.to(device, non_blocking=True)
-    N.call("dxa_copy_batch", N.ptr(dtab), len(rows), N.stream_handle(device))
+    return _CHUNK
 
 
-def concat_prims(parts: Sequence, device):
-    """Row-concatenation of 1-D / [n, 2] PrimColumns of one storage dtype → (data, valid or None), all segments in
-    one launch (None when the parts do not share a storage layout)."""
+class Segments:
+    """Copy / fill segments accumulated as flat arrays (source pointer or 0 for a fill, destination pointer, bytes,
+    fill byte): a table concatenation appends one array block per column instead of a Python tuple per part."""
+
+    def __init__(self):
+        self.src: List[np.ndarray] = []
+        self.dst: List[np.ndarray] = []
+        self.nb: List[np.ndarray] = []
+        self.fill: List[np.ndarray] = []
+        self.keep: List[torch.Tensor] = []        # temporaries the segments read (alive until the launch is queued)
+
+    def add(self, src, dst, nb, fill=0) -> None:
+        nb = np.asarray(nb, dtype=np.int64)
+        k = nb.shape[0] if nb.ndim else 1
+        nb = nb.reshape(k)
+        self.src.append(np.broadcast_to(np.asarray(src, dtype=np.int64), (k,)))
+        self.dst.append(np.broadcast_to(np.asarray(dst, dtype=np.int64), (k,)))
+        self.nb.append(nb)
+        self.fill.append(np.broadcast_to(np.asarray(fill, dtype=np.int64), (k,)))
+
+    def extend(self, segments: Sequence[Segment]) -> None:
+        for src, so, dst, do, nb, fill in segments:
+            self.add(0 if src is None else src.data_ptr() + so, dst.data_ptr() + do, nb, fill)
+
+    def __bool__(self):
+        return bool(self.nb)
+
+    def launch(self, device) -> None:
+        if not self.nb:
+            return
+        chunk = _chunk_size()
+        src, dst = np.concatenate(self.src), np.concatenate(self.dst)
+        nb, fill = np.concatenate(self.nb), np.concatenate(self.fill)
+        keep = nb > 0
+        if not keep.all():
+            src, dst, nb, fill = src[keep], dst[keep], nb[keep], fill[keep]
+        if nb.size == 0:
+            return
+        per = (nb + chunk - 1) // chunk                      # chunks per segment (one workgroup each)
+        if (per == 1).all():
+            rows = np.stack([src, dst, nb, fill], axis=1)
+        else:
+            seg = np.repeat(np.arange(nb.size), per)
+            k = np.arange(seg.size) - np.repeat(np.cumsum(per) - per, per)
+            off = k * chunk
+            rows = np.stack([np.where(src[seg] != 0, src[seg] + off, 0), dst[seg] + off,
+                             np.minimum(chunk, nb[seg] - off), fill[seg]], axis=1)
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        tab = torch.from_numpy(rows).pin_memory()
+        dtab = tab.to(device, non_blocking=True)
+        N.call("dxa_copy_batch", N.ptr(dtab), int(rows.shape[0]), N.stream_handle(device))
+        self.keep.clear()                           # freed after the launch: reuse is ordered behind it
+
+
+def copy_batch(segments, device) -> None:
+    """Run segments — a ``Segments`` or a sequence of (src tensor | None, src offset, dst tensor, dst offset, bytes,
+    fill) — as one launch."""
+    if not isinstance(segments, Segments):
+        sg = Segments()
+        sg.extend(segments)
+        segments = sg
+    segments.launch(device)
+
+
+def concat_prims(parts: Sequence, device, segs: Optional[Segments] = None):
+    """Row-concatenation of 1-D / [n, 2] PrimColumns of one storage dtype → (data, valid or None, segments), every
+    part's bytes as one block of segment arrays (None when the parts do not share a storage layout)."""
     d0 = parts[0].data
-    if any(p.data.dtype != d0.dtype or p.data.dim() != d0.dim() or p.data.shape[1:] != d0.shape[1:]
-           or not p.data.is_contiguous() for p in parts):
-        return None
-    total = sum(p.length for p in parts)
-    data = torch.empty((total,) + tuple(d0.shape[1:]), dtype=d0.dtype, device=device)
-    row_bytes = d0.element_size() * (d0.shape[1] if d0.dim() == 2 else 1)
-    any_null = any(p.valid is not None for p in parts)
-    valid = torch.empty(total, dtype=torch.bool, device=device) if any_null else None
-    segs, r = [], 0
-    for p in parts:
-        n = p.length
-        segs.append((p.data, 0, data, r * row_bytes, n * row_bytes, 0))
-        if any_null:
-            if p.valid is not None:
-                v = p.valid if p.valid.is_contiguous() else p.valid.contiguous()
-                segs.append((v, 0, valid, r, n, 0))
-            else:
-                segs.append((None, 0, valid, r, n, 1))
-        r += n
+    dt, dim, tail = d0.dtype, d0.dim(), d0.shape[1:]
+    lens = np.empty(len(parts), dtype=np.int64)
+    ptrs = np.empty(len(parts), dtype=np.int64)
+    any_null = False
+    for k, p in enumerate(parts):
+        d = p.data
+        if d.dtype != dt or d.dim() != dim or d.shape[1:] != tail or not d.is_contiguous():
+            return None
+        lens[k] = p.length
+        ptrs[k] = d.data_ptr()
+        any_null = any_null or p.valid is not None
+    total = int(lens.sum())
+    data = torch.empty((total,) + tuple(tail), dtype=dt, device=device)
+    row_bytes = d0.element_size() * (d0.shape[1] if dim == 2 else 1)
+    segs = Segments() if segs is None else segs
+    starts = np.cumsum(lens) - lens
+    segs.add(ptrs, data.data_ptr() + starts * row_bytes, lens * row_bytes)
+    valid = _valid_into(parts, lens, starts, total, device, segs) if any_null else None
     return data, valid, segs
 
 
-def valid_segments(parts: Sequence, device):
-    """Concatenated validity of columns (None when none has nulls) as copy / fill segments."""
-    if not any(p.valid is not None for p in parts):
-        return None, []
-    total = sum(p.length for p in parts)
+def _valid_into(parts, lens, starts, total, device, segs: Segments):
     valid = torch.empty(total, dtype=torch.bool, device=device)
-    segs, r = [], 0
-    for p in parts:
-        n = p.length
+    vp = np.zeros(len(parts), dtype=np.int64)
+    for k, p in enumerate(parts):
         if p.valid is not None:
             v = p.valid if p.valid.is_contiguous() else p.valid.contiguous()
-            segs.append((v, 0, valid, r, n, 0))
-        else:
-            segs.append((None, 0, valid, r, n, 1))
-        r += n
-    return valid, segs
+            vp[k] = v.data_ptr()
+            if v is not p.valid:
+                segs.keep.append(v)                  # a contiguous copy must outlive the launch
+    segs.add(vp, valid.data_ptr() + starts, lens, np.where(vp == 0, 1, 0))
+    return valid
+
+
+def valid_segments(parts: Sequence, device, segs: Optional[Segments] = None):
+    """Concatenated validity of columns (None when none has nulls) as copy / fill segments."""
+    segs = Segments() if segs is None else segs
+    if not any(p.valid is not None for p in parts):
+        return None, segs
+    lens = np.fromiter((p.length for p in parts), dtype=np.int64, count=len(parts))
+    starts = np.cumsum(lens) - lens
+    return _valid_into(parts, lens, starts, int(lens.sum()), device, segs), segs

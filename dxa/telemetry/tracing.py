@@ -10,6 +10,7 @@
 """
 from __future__ import annotations
 
+import collections
 import logging
 import os
 import time
@@ -55,6 +56,63 @@ def stage(name: str, times: Optional[Dict[str, float]] = None):
             rf.__exit__(None, None, None)
         if _nvtx is not None:
             _nvtx.range_pop()
+
+
+# host-time sections inside a statement (DXA_HOST_TIMERS=1; bench.py --profile-stages prints them per step)
+HOST_ACC: Dict[str, float] = collections.defaultdict(float)
+_HOST_TIMERS = os.environ.get("DXA_HOST_TIMERS") == "1"
+
+
+class _Section:
+    __slots__ = ("name", "t0")
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        HOST_ACC[self.name] += time.perf_counter() - self.t0
+
+
+class _NoSection:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_SECTION = _NoSection()
+
+
+def host_section(name: str):
+    """Accumulate this block's host wall time under ``name`` (no-op unless DXA_HOST_TIMERS=1)."""
+    return _Section(name) if _HOST_TIMERS else _NO_SECTION
+
+
+def time_host_syncs() -> None:
+    """DXA_HOST_TIMERS=1: also accumulate the host time spent blocked in ``.item()`` / ``.tolist()`` /
+    ``Event.synchronize`` / ``Stream.synchronize`` (device waits) under ``sync:<name>``."""
+    if not _HOST_TIMERS:
+        return
+    import torch
+
+    def wrap(owner, attr, key):
+        fn = getattr(owner, attr)
+
+        def timed(*a, **k):
+            t0 = time.perf_counter()
+            try:
+                return fn(*a, **k)
+            finally:
+                HOST_ACC[key] += time.perf_counter() - t0
+        setattr(owner, attr, timed)
+    wrap(torch.Tensor, "item", "sync:item")
+    wrap(torch.Tensor, "tolist", "sync:tolist")
+    wrap(torch.cuda.Event, "synchronize", "sync:event")
+    wrap(torch.cuda.Stream, "synchronize", "sync:stream")
 
 
 def stage_metrics(times: Dict[str, float]) -> Dict[str, float]:

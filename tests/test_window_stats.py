@@ -27,3 +27,31 @@ def test_gpu_matches_reference():
         E = int(ts[0])
         for _ in range(2):
             assert _ts_stats(ts.cuda(), ok.cuda(), E) == _ref(ts, ok, E), n
+
+
+def test_concat_panes_reuses_last_run_and_matches_concat():
+    """_concat_panes over a sliding list of partial tables (oldest dropped, newest appended, a fresh clipped part in
+    front) equals concat_tables of the same list, batch after batch, while reusing the previous result."""
+    import types
+    from dxa.engine.column import Table, column_from_pylist, concat_tables, strings_from_pylist
+    from dxa.engine.query import _concat_panes
+
+    def part(k):
+        n = 3 + k % 4
+        return Table(["k", "s", "v"], [column_from_pylist([k * 10 + i for i in range(n)], "long"),
+                                      strings_from_pylist([f"s{k}-{i}" if i % 3 else None for i in range(n)], "cpu"),
+                                      column_from_pylist([None if i == 1 else float(k + i) for i in range(n)],
+                                                         "double")], n)
+    store = types.SimpleNamespace()
+    panes = [part(k) for k in range(12)]
+    for b in range(8):
+        clipped = part(100 + b)                                # recomputed every batch
+        parts = [clipped] + panes[b:b + 8]
+        got = _concat_panes(parts, store, "fp")
+        want = concat_tables(parts)
+        assert got.length == want.length
+        for x, y in zip(got.columns, want.columns):
+            assert x.to_pylist() == y.to_pylist()
+        if b:
+            # the previous batch's panes[b:b+7] were reused as one view of its result
+            assert store.concat_cache["fp"][0][1] is panes[b]

@@ -1,0 +1,7 @@
+# Round 4: host-time sections of the full / window flows (DXA_HOST_TIMERS=1: sections + device-wait time)
+set -o pipefail
+mkdir -p gpurun_out/r4t
+for f in full window; do
+DXA_HOST_TIMERS=1 timeout -k 10 300 python bench.py --flow $f --steps 100 --profile-stages > gpurun_out/r4t/$f.log 2>&1 || { tail -20 gpurun_out/r4t/$f.log; exit 1; }
+grep metric gpurun_out/r4t/$f.log | python -c "import sys,json; d=json.loads(sys.stdin.readline()); print('$f', round(d['value']/1e6,2), 'M ev/s', round(d['ms_per_step'],2)); print('  ', d.get('host_ms_per_step')); print('  ', d.get('host_sections_ms_per_step'))"
+done
