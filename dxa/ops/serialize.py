@@ -306,7 +306,7 @@ def _render_members(members: List["Staged"]) -> None:
     from . import native as N
     dev = members[0].device
     side = _side_stream(dev)
-    with torch.cuda.stream(side):
+    with torch.inference_mode(), torch.cuda.stream(side):
         for m in members:
             side.wait_event(m.event)
         b = _DevBuilder()
