@@ -585,6 +585,35 @@ DXA_API int dxa_group_ids(const uint64_t* keys, int64_t cap, const int32_t* slot
   return (int)hipGetLastError();
 }
 
+namespace {
+// The group table's initial state, one launch instead of three fills and a memset: keys all-ones (empty), no
+// group per slot, counters zero, rep "no row yet".
+__global__ __launch_bounds__(256) void group_init_kernel(uint64_t* keys, int64_t cap, int32_t* gid_of_slot,
+                                                         int32_t* counter, int32_t* rep, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = i0; i < cap; i += stride) {
+    keys[i] = ~0ull;
+    gid_of_slot[i] = -1;
+  }
+  for (int64_t i = i0; i < n; i += stride) rep[i] = 0x7fffffff;
+  if (i0 < 2) counter[i0] = 0;
+}
+}  // namespace
+
+// dxa_group_build on uninitialised buffers: initialise (one launch), then build.  counter: [2] (ngroups, bad).
+DXA_API int dxa_group_build_init(const uint64_t* h, int64_t n, uint64_t* keys, int64_t cap, int32_t* gid_of_slot,
+                                 int32_t* counter, int32_t* gid, int32_t* rep, void* st) {
+  if (n <= 0) return 0;
+  const int64_t work = cap > n ? cap : n;
+  const int64_t blocks = (work + 255) / 256;
+  hipLaunchKernelGGL(group_init_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     (hipStream_t)st, keys, cap, gid_of_slot, counter, rep, n);
+  hipLaunchKernelGGL(group_build_kernel, dim3(dxa_blocks(n, 256)), dim3(256), 0, (hipStream_t)st, h, n, keys, cap - 1,
+                     gid_of_slot, counter, gid, rep);
+  return (int)hipGetLastError();
+}
+
 // keys: [cap] filled with 0xFF; gid_of_slot: [cap] filled with -1; counter: [1] zeroed; rep: [n] INT32_MAX
 DXA_API int dxa_group_build(const uint64_t* h, int64_t n, uint64_t* keys, int64_t cap, int32_t* gid_of_slot,
                             int32_t* counter, int32_t* gid, int32_t* rep, void* st) {

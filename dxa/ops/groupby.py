@@ -60,13 +60,17 @@ def group_rows(keys: List, ordered: bool = True) -> Groups:
     if _on_gpu(device):
         st = N.stream_handle(device)
         cap = _next_pow2(2 * n)
-        table = torch.full((cap,), -1, dtype=torch.int64, device=device)
-        gid_of_slot = torch.full((cap,), -1, dtype=torch.int32, device=device)
-        scal = torch.zeros(2, dtype=torch.int32, device=device)   # [ngroups, bad]
-        gid = torch.empty(n, dtype=torch.int32, device=device)
-        rep = torch.full((n,), INT32_MAX, dtype=torch.int32, device=device)
-        # insert, number and gather in one pass (no scan over the table's slots)
-        N.call("dxa_group_build", N.ptr(h), n, N.ptr(table), cap, N.ptr(gid_of_slot), N.ptr(scal), N.ptr(gid),
+        # one allocation, initialised by the build call's own init launch: [table int64 cap | gid_of_slot int32 cap
+        # | rep int32 n | gid int32 n | scal int32 2 (ngroups, bad)]
+        ws = torch.empty(cap + (cap + 2 * n + 2 + 1) // 2, dtype=torch.int64, device=device)
+        table = ws[:cap]
+        i32 = ws[cap:].view(torch.int32)
+        gid_of_slot = i32[:cap]
+        rep = i32[cap:cap + n]
+        gid = i32[cap + n:cap + 2 * n]
+        scal = i32[cap + 2 * n:cap + 2 * n + 2]
+        # initialise, then insert, number and gather in one pass (no scan over the table's slots)
+        N.call("dxa_group_build_init", N.ptr(h), n, N.ptr(table), cap, N.ptr(gid_of_slot), N.ptr(scal), N.ptr(gid),
                N.ptr(rep), st)
         bad_ptr = scal.data_ptr() + 4
         kc = key_cols(keys) if 2 <= len(keys) <= MAX_KEY_COLS else None

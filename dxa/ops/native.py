@@ -60,6 +60,7 @@ _SIGS = {
     "dxa_partial_finish": [c_p, c_p],
     "dxa_group_renumber": [c_p, c_i64, c_p, c_i32, c_p, c_p, c_p],
     "dxa_group_build": [c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
+    "dxa_group_build_init": [c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
     "dxa_slot_count": [c_p, c_i64, c_p, c_p],
     "dxa_slot_scatter": [c_p, c_i64, c_p, c_p, c_p, c_p],
     "dxa_probe_count": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, ctypes.c_int, c_p],
