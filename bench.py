@@ -158,8 +158,12 @@ def main():
     if world > 1:
         parallel.init(dist.group.WORLD, device)
 
+    # passthrough is bound by the D2H of its rendered JSON: two batches' outputs in flight overlap one batch's copy
+    # with the next one's rendering (profiles/round4/output_depth/: 64.5 -> 71.8 M ev/s); the other flows keep one
+    # (no gain measured, lower latency).  DXA_OUTPUT_DEPTH overrides.
+    depth_extra = {"datax.job.process.outputdepth": "2"} if flow == "passthrough" else None
     settings = iot.flow_settings(workdir=f"/tmp/dxa_bench_{flow}_{rank}", variant=flow, sink=args.sink,
-                                 ref_rows=args.ref_rows)
+                                 ref_rows=args.ref_rows, extra=depth_extra)
     ref_write_s = None
     if flow == "join":
         # config 4's reference table is a real CSV read through datax.job.input.default.referencedata.* (rank 0
@@ -534,7 +538,9 @@ def main():
                    "global_batch": E * world, "seq_len": None, "parallelism": f"dp{world}",
                    "events_per_gpu_per_batch": E, "avg_event_bytes": round(avg_bytes, 1) if avg_bytes else None,
                    "source": source, "ingest_prefetch_batches": depth, "batch_interval_s": interval_us / 1e6,
-                   "outputs": "sync" if args.sync_outputs else "pipelined (batch t sinks overlap batch t+1)",
+                   "outputs": "sync" if args.sync_outputs else (
+                       "pipelined (batch t sinks overlap batch t+1)" if proc.output_depth == 1 else
+                       f"pipelined, {proc.output_depth} batches' outputs in flight"),
                    "sink": args.sink},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),

@@ -152,7 +152,14 @@ class Processor:
         # output pipelining: batch t's sink work overlaps batch t+1's device work (at most one batch in flight)
         self.pipeline_outputs = pipeline_outputs if pipeline_outputs is not None else \
             d.get_bool(S.PROCESS_PREFIX + "pipelineoutputs", False)
-        self._inflight: Optional[_InFlight] = None
+        # batches whose outputs may be in flight at once (datax.job.process.outputdepth, env DXA_OUTPUT_DEPTH): 1 =
+        # batch t's sinks overlap batch t+1's processing only.  2 also overlaps batch t's D2H / sink writes with
+        # batch t+1's rendering — for flows bound by the output copy (every event re-serialised); batches still
+        # complete (metrics, state flips, offset commits) in order, but sinks of consecutive batches may finish
+        # out of order
+        depth = os.environ.get("DXA_OUTPUT_DEPTH") or d.get_or_else(S.PROCESS_PREFIX + "outputdepth", "1") or "1"
+        self.output_depth = max(1, int(depth))
+        self._inflights: "collections.deque[_InFlight]" = collections.deque()
         self.completed: List = []
         self.on_batch_complete = None
         self.source_metric_names: Tuple[str, ...] = ()
@@ -442,7 +449,8 @@ class Processor:
         link_render_groups([p for _, st in staged for p in st.payloads()])    # one render launch pair per batch
         t2 = time.perf_counter()
         self.host_acc["outputs:stage"] += t2 - t1
-        self._complete_inflight()
+        while len(self._inflights) >= self.output_depth:
+            self._complete_inflight()
         self.host_acc["outputs:complete_previous"] += time.perf_counter() - t2
         from ..io.sinks import _pool
         target = getattr(self, "_batch_target", None)
@@ -450,12 +458,13 @@ class Processor:
                                                  for name, st in staged], t_start)
         fl.t_staged = time.perf_counter()
         fl.stages = dict(self.stage_times)
-        self._inflight = fl
+        self._inflights.append(fl)
         self.stage_times["output_stage"] = time.perf_counter() - t1
         if self.keep_views:
             self.last_views = {**{k: cat.get(k) for k in cat.names()}, **views}
         if not self.pipeline_outputs:
-            self._complete_inflight()
+            while self._inflights:
+                self._complete_inflight()
             self._sync()
             self.stage_times["output"] = time.perf_counter() - t1
         return fl.metrics
@@ -661,10 +670,9 @@ class Processor:
     def _complete_inflight(self):
         """Finish the in-flight batch: collect sink counts, all-reduce the batch metrics across ranks, persist state
         tables (after outputs, as the reference), stamp latencies, emit metrics and fire ``on_batch_complete``."""
-        fl = self._inflight
-        if fl is None:
+        if not self._inflights:
             return None
-        self._inflight = None
+        fl = self._inflights.popleft()
         metrics = fl.metrics
         t_done = fl.t_staged
         for name, f in fl.futures:
@@ -703,7 +711,9 @@ class Processor:
 
     def drain(self) -> Optional[Dict[str, float]]:
         """Complete the in-flight batch (pipelined mode); returns its metrics."""
-        m = self._complete_inflight()
+        m = None
+        while self._inflights:
+            m = self._complete_inflight()
         self._sync()
         return m
 
@@ -765,9 +775,10 @@ class Processor:
         except Exception:
             log.exception("batch %s failed", batch_time_us)
             try:
-                self._complete_inflight()       # the previous batch still gets its outputs and metrics
+                while self._inflights:
+                    self._complete_inflight()   # the previous batches still get their outputs and metrics
             except Exception:  # noqa: BLE001
-                self._inflight = None
+                self._inflights.clear()
             from ..telemetry.appinsights import track_exception
             track_exception("ProcessDataFrame", _fmt_ts(batch_time_us))
             raise
