@@ -5,7 +5,8 @@ syncs (``_local_scalar_dense`` = .item()/.tolist(), D2H copies) are counted sepa
     python tools/launch_attrib.py --flow full --batches 8 [--events 1000000] > attrib.txt
 
 Runs the bench's gpu-sim batches through the Processor like tests/test_flows_gpu.py; the first two batches are warmup
-(not counted)."""
+(not counted).  Run it with DXA_INFERENCE_MODE=0: under torch.inference_mode the dispatch mode sees composite ops
+before they decompose (``to.dtype`` no-ops, ``item``), which miscounts launches and syncs."""
 from __future__ import annotations
 
 import argparse
