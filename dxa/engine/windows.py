@@ -73,17 +73,31 @@ def _rebuild(c, done):
     return c
 
 
-def _compact_table(t: Table) -> Table:
+def _compact_table(t: Table, known=None) -> Table:
     """Detach retained rows from the batch's raw input buffer (string views → own compact arena); all string leaves
-    are compacted together with one host synchronisation.  (Module-level recursion: a self-referencing nested
+    are compacted together with one host synchronisation — none when ``known`` = (leaves' concatenated lengths,
+    their total) was already read with the pane statistics.  (Module-level recursion: a self-referencing nested
     function is a reference cycle, and this one would pin the batch's raw input buffer until the cyclic collector
     ran.)"""
     from ..ops.strings import compact_many
     leaves: List[StrColumn] = []
     for c in t.columns:
         _str_leaves(c, leaves)
-    done = iter(compact_many(leaves))
+    if known is not None:
+        done = iter(compact_many(leaves, lens_all=known[0], total=known[1]))
+    else:
+        done = iter(compact_many(leaves))
     return Table(t.names, [_rebuild(c, done) for c in t.columns], t.length, t.device)
+
+
+def _str_lens_all(t: Table):
+    """The string leaves' lengths concatenated (device, int32) — None when the table has no string leaf."""
+    leaves: List[StrColumn] = []
+    for c in t.columns:
+        _str_leaves(c, leaves)
+    if len(leaves) < 2 or not leaves[0].lens.is_cuda:
+        return None
+    return torch.cat([c.lens for c in leaves])
 
 
 @dataclass
@@ -162,9 +176,10 @@ _TS_SCRATCH: Dict = {}
 _TS_KERNEL = __import__("os").environ.get("DXA_TS_STATS_KERNEL", "1") != "0"          # A/B switch
 
 
-def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int) -> List[int]:
+def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int, lens_all: Optional[torch.Tensor] = None) -> List[int]:
     """[min, max, count] of the valid timestamps and the count of valid ones >= E — one reduction launch and one
-    4-word read on the GPU (reduce_stats.hip), tensor ops on the CPU."""
+    4-word read on the GPU (reduce_stats.hip), tensor ops on the CPU.  With ``lens_all`` (the pane's string lengths)
+    a fifth word, their sum, comes back in the same read: the pane's compaction then needs no read of its own."""
     if ts.is_cuda and ts.numel() and _TS_KERNEL:
         from ..ops import native as N
         dev = ts.device
@@ -174,14 +189,18 @@ def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int) -> List[int]:
                              "dxa_ts_stats": [N.c_p, N.c_p, N.c_i64, N.c_i64, N.c_p, N.c_p, N.c_p]})
             scratch = _TS_SCRATCH[dev] = torch.zeros(N.lib().dxa_ts_stats_scratch_bytes(), dtype=torch.uint8,
                                                      device=dev)
-        out = torch.empty(4, dtype=torch.int64, device=dev)
+        out = torch.empty(4 if lens_all is None else 5, dtype=torch.int64, device=dev)
         N.call("dxa_ts_stats", N.ptr(ts.contiguous()), N.ptr(N.u8(ok.contiguous())), ts.numel(), int(E),
                N.ptr(scratch), N.ptr(out), N.stream_handle(dev))
+        if lens_all is not None:
+            torch.sum(lens_all, 0, dtype=torch.int64, out=out[4])
         return out.tolist()
     big = torch.iinfo(torch.int64).max
-    return torch.stack([torch.where(ok, ts, torch.full_like(ts, big)).min(),
-                        torch.where(ok, ts, torch.full_like(ts, -big)).max(),
-                        ok.sum(), (ok & (ts >= E)).sum()]).tolist()
+    vals = [torch.where(ok, ts, torch.full_like(ts, big)).min(), torch.where(ok, ts, torch.full_like(ts, -big)).max(),
+            ok.sum(), (ok & (ts >= E)).sum()]
+    if lens_all is not None:
+        vals.append(lens_all.sum(dtype=torch.int64).to(ts.device))
+    return torch.stack(vals).tolist()
 
 
 class WindowStore:
@@ -233,10 +252,12 @@ class WindowStore:
             # the late-event check come back together; otherwise filter, then take the kept rows' statistics
             with host_section("windows:stats"):
                 ts, ok = self._ts(projected)
-                lo_, hi_, nok, nkeep = _ts_stats(ts, ok, E)
+                lens_all = _str_lens_all(projected)
+                got = _ts_stats(ts, ok, E, lens_all)
+                lo_, hi_, nok, nkeep = got[:4]
             if int(nkeep) == projected.length:
                 with host_section("windows:compact"):
-                    kept = _compact_table(projected)
+                    kept = _compact_table(projected, None if lens_all is None else (lens_all, int(got[4])))
                 cur = Pane(batch_time_us, kept, int(lo_), int(hi_), True)
             else:
                 kept = _compact_table(projected.filter(ok & (ts >= E)))

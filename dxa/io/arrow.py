@@ -137,7 +137,11 @@ def to_host_async(t: Table):
     for c in t.columns:
         c = materialize(c)
         if isinstance(c, StrColumn):
-            cc = c.compact()
+            # a small arena crosses as it is (the host side packs the strings when it builds Arrow): no device
+            # compaction, whose size read would stall the batch thread; a view into a large buffer (a batch's raw
+            # input) is compacted first so only its rows' bytes cross PCIe
+            small = c.arena.numel() <= max(1 << 20, 512 * c.length)
+            cc = c if small else c.compact()
             plan.append(("str", type(cc), cc.dtype, leaf(cc.arena), leaf(cc.starts), leaf(cc.lens),
                          None if cc.valid is None else leaf(cc.valid)))
         elif isinstance(c, PrimColumn):

@@ -102,10 +102,11 @@ def _gather_parts(parts, device) -> None:
     N.call("dxa_str_gather_parts", ctypes.cast(arr, ctypes.c_void_p), len(parts), N.stream_handle(device))
 
 
-def compact_many(cols: Sequence) -> list:
+def compact_many(cols: Sequence, lens_all: Optional[torch.Tensor] = None, total: Optional[int] = None) -> list:
     """``compact`` of several string columns with ONE host synchronisation and one scan: every column's bytes are
     packed into one shared arena (column k's rows after column k-1's), offsets from a single scan over all the
-    lengths, the bytes moved by one multi-part gather launch."""
+    lengths, the bytes moved by one multi-part gather launch.  ``lens_all`` / ``total``: the columns' lengths
+    already concatenated and their sum already read (then no synchronisation here)."""
     cols = list(cols)
     if not cols:
         return []
@@ -115,10 +116,12 @@ def compact_many(cols: Sequence) -> list:
     total_rows = sum(c.length for c in cols)
     if total_rows == 0:
         return [compact(c) for c in cols]
-    lens_all = torch.cat([c.lens for c in cols])
+    if lens_all is None:
+        lens_all = torch.cat([c.lens for c in cols])
     cs = torch.cumsum(lens_all, 0, dtype=torch.int64)
     ex = cs - lens_all
-    total = int(cs[-1].item())
+    if total is None:
+        total = int(cs[-1].item())
     dst = _alloc_arena(total, device)
     out, parts, r = [], [], 0
     for c in cols:
