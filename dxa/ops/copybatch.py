@@ -66,20 +66,25 @@ class Segments:
             src, dst, nb, fill = src[keep], dst[keep], nb[keep], fill[keep]
         if nb.size == 0:
             return
-        per = (nb + chunk - 1) // chunk                      # chunks per segment (one workgroup each)
-        if (per == 1).all():
-            rows = np.stack([src, dst, nb, fill], axis=1)
-        else:
-            seg = np.repeat(np.arange(nb.size), per)
-            k = np.arange(seg.size) - np.repeat(np.cumsum(per) - per, per)
-            off = k * chunk
-            rows = np.stack([np.where(src[seg] != 0, src[seg] + off, 0), dst[seg] + off,
-                             np.minimum(chunk, nb[seg] - off), fill[seg]], axis=1)
-        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        rows = chunk_rows(src, dst, nb, fill, chunk)
         tab = torch.from_numpy(rows).pin_memory()
         dtab = tab.to(device, non_blocking=True)
         N.call("dxa_copy_batch", N.ptr(dtab), int(rows.shape[0]), N.stream_handle(device))
         self.keep.clear()                           # freed after the launch: reuse is ordered behind it
+
+
+def chunk_rows(src: np.ndarray, dst: np.ndarray, nb: np.ndarray, fill: np.ndarray, chunk: int) -> np.ndarray:
+    """Segments (all ``nb > 0``) split into rows of at most ``chunk`` bytes — (src | 0, dst, bytes, fill) int64, one
+    workgroup's work each (copy_batch.hip CopyChunk)."""
+    per = (nb + chunk - 1) // chunk
+    if (per == 1).all():
+        rows = np.stack([src, dst, nb, fill], axis=1)
+    else:
+        seg = np.repeat(np.arange(nb.size), per)
+        off = (np.arange(seg.size) - np.repeat(np.cumsum(per) - per, per)) * chunk
+        rows = np.stack([np.where(src[seg] != 0, src[seg] + off, 0), dst[seg] + off,
+                         np.minimum(chunk, nb[seg] - off), fill[seg]], axis=1)
+    return np.ascontiguousarray(rows, dtype=np.int64)
 
 
 def copy_batch(segments, device) -> None:

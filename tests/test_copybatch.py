@@ -75,3 +75,26 @@ def test_concat_tables_with_strings_matches_cpu():
     g, c = concat_tables(tabs_g), concat_tables(tabs_c)
     assert g.columns[0].to_pylist() == c.columns[0].to_pylist() == ["a", None, "héllo", "x" * 40, "", "zz"]
     assert g.columns[1].to_pylist() == c.columns[1].to_pylist()
+
+
+def test_chunk_rows_split_segments_cpu():
+    """Chunking of copy / fill segments into per-workgroup rows (host side of copy_batch): every byte of every
+    segment covered exactly once, fills keep a null source, no row over the chunk size."""
+    import numpy as np
+    from dxa.ops.copybatch import chunk_rows
+    src = np.array([1000, 0, 5000, 9000], dtype=np.int64)
+    dst = np.array([100000, 200000, 300000, 400000], dtype=np.int64)
+    nb = np.array([10, 25, 7, 16], dtype=np.int64)
+    fill = np.array([0, 1, 0, 0], dtype=np.int64)
+    rows = chunk_rows(src, dst, nb, fill, 8)
+    assert (rows[:, 2] <= 8).all() and (rows[:, 2] > 0).all()
+    for k in range(4):
+        mine = rows[(rows[:, 1] >= dst[k]) & (rows[:, 1] < dst[k] + nb[k])]
+        assert mine[:, 2].sum() == nb[k]
+        assert sorted(mine[:, 1] - dst[k]) == list(range(0, nb[k], 8))
+        if src[k] == 0:
+            assert (mine[:, 0] == 0).all() and (mine[:, 3] == 1).all()
+        else:
+            assert (mine[:, 0] - src[k] == mine[:, 1] - dst[k]).all()
+    one = chunk_rows(src, dst, nb, fill, 64)
+    assert one.shape == (4, 4) and (one[:, 2] == nb).all()
