@@ -95,7 +95,7 @@ def _str_lens_all(t: Table):
     leaves: List[StrColumn] = []
     for c in t.columns:
         _str_leaves(c, leaves)
-    if len(leaves) < 2 or not leaves[0].lens.is_cuda:
+    if len(leaves) < 2:
         return None
     return torch.cat([c.lens for c in leaves])
 
