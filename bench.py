@@ -65,6 +65,54 @@ def _cpu_lines(raw, length):
     return torch.cat([torch.zeros(1, dtype=torch.int64), nl + 1])
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """``--gpus N`` without a launcher: start N rank processes of this script (one per GPU, the environment
+    ``torch.distributed.run`` would give them) and wait for all of them.  Runs before anything touches the GPU — no
+    ``import torch`` in this process — and never execs: the children are subprocesses, rank 0's JSON line reaches
+    stdout through the inherited descriptor, and the parent exits non-zero when any rank fails (the survivors are
+    stopped then, so a dead rank cannot leave the others blocked in a collective).  The reference scales the same
+    way, one partition per executor task (EventHubStreamingFactory.scala:86, StreamingHost.scala:68-69)."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def forward(sig, _frame):                 # a signal to the launcher (a time limit) reaches every rank
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(sig)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.1)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +163,11 @@ def main():
     warmup = DEFAULT_WARMUP[flow] if args.warmup is None else args.warmup
     E = args.events_per_batch or DEFAULT_EVENTS[flow]
     source = args.source or DEFAULT_SOURCE[flow]
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            sys.exit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}")
+    elif args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -146,6 +199,8 @@ def main():
         else:
             dist.init_process_group("gloo")                              # CPU rehearsal of the same code path
     on_gpu = device.type == "cuda"
+    if os.environ.get("DXA_BENCH_FAIL_RANK") == str(rank):        # fault injection (tests): this rank dies
+        raise SystemExit(f"bench.py: rank {rank} failing on request (DXA_BENCH_FAIL_RANK)")
 
     from dxa.ops import native
     if on_gpu:

@@ -64,6 +64,8 @@ struct PackArgs {
   int32_t sizes_stride;  // row stride of `sizes` (>= 1 + nstr)
   int32_t nextra;        // words written after the sizes of every destination row (the layout's validity flags,
   int64_t extra[kMaxExtra];  //   which ride with the send sizes through the size all-to-all)
+  int32_t coalesce;      // 1: every leaf's bytes go to ONE arena (strs[*].dst equal), destination-major —
+  int32_t pad1;          //   [d0: leaf 0 | leaf 1 | …][d1: …] — so one byte all-to-all moves every string leaf
 };
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -158,6 +160,7 @@ __global__ __launch_bounds__(kThreads) void xchg_scatter_kernel(const PackArgs a
   __shared__ int64_t run[1 + kMaxStr][kMaxW];
   __shared__ int64_t blk[1 + kMaxStr][kMaxW];      // this block's base per (s, d)
   __shared__ int64_t dstart[1 + kMaxStr][kMaxW];   // destination block start per (s, d)
+  __shared__ int64_t shift[kMaxStr][kMaxW];        // leaf arena position → coalesced arena position per (s, d)
   const int S1 = 1 + a.nstr;
   const int W = a.W;
   const int wave = threadIdx.x >> 6;
@@ -168,6 +171,18 @@ __global__ __launch_bounds__(kThreads) void xchg_scatter_kernel(const PackArgs a
     run[s][d] = 0;
     blk[s][d] = a.hist[(int64_t)s * m + (int64_t)d * a.nblocks + blockIdx.x];
     dstart[s][d] = a.hist[(int64_t)s * m + (int64_t)d * a.nblocks];
+    if (s > 0) {
+      // coalesced: leaf s of destination d starts after every earlier destination's bytes (all leaves) and the
+      // earlier leaves' bytes of d; the sizes matrix [W][sizes_stride] holds the per-(d, leaf) byte counts
+      int64_t pos = 0;
+      if (a.coalesce) {
+        for (int e = 0; e < d; ++e)
+          for (int q = 0; q < a.nstr; ++q) pos += a.sizes[(int64_t)e * a.sizes_stride + 1 + q];
+        for (int q = 0; q < s - 1; ++q) pos += a.sizes[(int64_t)d * a.sizes_stride + 1 + q];
+        pos -= dstart[s][d];
+      }
+      shift[s - 1][d] = pos;
+    }
   }
   const int64_t base = (int64_t)blockIdx.x * kRows;
   const int nmask_base = a.ncols + 2 * a.nstr;
@@ -256,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void xchg_scatter_kernel(const PackArgs a
         const int64_t off = blk[1 + s][d] + pre_b[s] + boff[s];      // absolute in this leaf's send arena
         row[a.ncols + s] = (int64_t)st.lens[i];
         row[a.ncols + a.nstr + s] = off - dstart[1 + s][d];           // relative to the destination's bytes
-        if (len[s] > 0) copy_bytes(st.arena + st.starts[i], st.dst + off, len[s]);
+        if (len[s] > 0) copy_bytes(st.arena + st.starts[i], st.dst + off + shift[s][d], len[s]);
       }
       const int nmask = a.C - nmask_base;
       for (int w = 0; w < nmask; ++w) {

@@ -42,6 +42,21 @@ def init(group=None, device=None):
     _WORLD = dist.get_world_size(_GROUP)
     _RANK = dist.get_rank(_GROUP)
     _DEVICE = torch.device(device) if device is not None else None
+    # the host-side (gloo) communicator for small host-byte broadcasts under RCCL: created HERE, on every rank of
+    # the job's group at the same point (new_group is itself a collective — created lazily by one rank's reference
+    # data refresh it would deadlock the others)
+    from . import exchange as X
+    X._HOST_GROUP = None
+    if _WORLD > 1 and dist.get_backend(_GROUP) != "gloo":
+        X._HOST_GROUP = dist.new_group(ranks=_group_ranks(_GROUP), backend="gloo")
+
+
+def _group_ranks(g):
+    import torch.distributed as dist
+    try:
+        return dist.get_process_group_ranks(g)
+    except Exception:                                  # the default group
+        return list(range(dist.get_world_size()))
 
 
 def shutdown():

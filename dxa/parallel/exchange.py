@@ -3,8 +3,8 @@
 A table is flattened into (a) one [rows × C] int64 matrix — every fixed-width leaf becomes one column (doubles
 bit-cast, booleans widened), every string leaf contributes its byte lengths, validity travels as 63-bit masks — and
 (b) one byte stream per string leaf.  Rows are stably sorted by destination so each destination's block is
-contiguous; a single ``all_to_all_single`` moves the matrix (plus one per string leaf and one tiny one for the
-counts).  Sized for xGMI: all blocks of a rank leave in one collective, so the 7 links are driven concurrently and the
+contiguous; a single ``all_to_all_single`` moves the matrix, one more moves the bytes of every string leaf (one
+destination-major buffer), and one tiny one the counts — three collectives per exchange whatever the column count.  Sized for xGMI: all blocks of a rank leave in one collective, so the 7 links are driven concurrently and the
 per-call latency is paid once per exchange, not per column.
 """
 from __future__ import annotations
@@ -163,7 +163,8 @@ def shuffle_table(table, dest: torch.Tensor):
 
     Device path (``exchange.hip``): plan (histogram + scan: the [W × (1+S)] send sizes) → one all-to-all of the
     sizes and ONE host read-back of sent and received sizes → scatter (matrix + string arenas, destination-ordered)
-    → one all-to-all of the matrix and one per string leaf → one unpack launch.  Three kernel launches on the send
+    → one all-to-all of the matrix and ONE of every string leaf's bytes (coalesced, destination-major) → one
+    unpack launch.  Three kernel launches on the send
     side and one on the receive side, however many columns the table has.  ``DXA_XCHG_TORCH=1`` runs the torch
     reference implementation of the same wire format."""
     from . import packing as PK
@@ -180,19 +181,21 @@ def shuffle_table(table, dest: torch.Tensor):
     recv_rows = [r[0] for r in both[1]]
     send_bytes = [[r[1 + s] for r in both[0]] for s in range(lay.S)]
     recv_bytes = [[r[1 + s] for r in both[1]] for s in range(lay.S)]
-    mat, arenas = PK.scatter(lay, state, send_rows, send_bytes)
+    mat, arenas = PK.scatter(lay, state, send_rows, send_bytes, coalesce=True)
     n_out = sum(recv_rows)
     recv = torch.empty((n_out, lay.C), dtype=torch.int64, device=device)
     if lay.C:
         _a2a(recv, mat, recv_rows, send_rows)
-    rarenas = []
-    for si in range(lay.S):
-        total = sum(recv_bytes[si])
+    rarenas, byte_base = [], []
+    if lay.S:
+        # every string leaf in ONE byte all-to-all: destination-major blocks [leaf 0 | leaf 1 | …] per rank
+        send_split, _ = PK.coalesced_bytes(send_bytes)
+        recv_split, byte_base = PK.coalesced_bytes(recv_bytes)
+        total = sum(recv_split)
         out = torch.zeros(total + 16, dtype=torch.uint8, device=device)      # +16: string kernels over-read
-        _a2a(out[:total], arenas[si][:sum(send_bytes[si])], recv_bytes[si], send_bytes[si])
-        rarenas.append(out)
+        _a2a(out[:total], arenas[0][:sum(send_split)], recv_split, send_split)
+        rarenas = [out] * lay.S
     row_prefix = _prefix(recv_rows)
-    byte_base = [_prefix(recv_bytes[si])[:W] for si in range(lay.S)]
     return PK.unpack(lay.names, lay.spec, lay.meta(), recv, rarenas, row_prefix, row_prefix[:W], byte_base, n_out,
                      device, _force_torch())
 
@@ -211,13 +214,21 @@ def _prefix(xs):
     return out
 
 
+def _gsrc(src: int, g=None) -> int:
+    """torch.distributed takes a broadcast's source as a GLOBAL rank; ``src`` is a rank of the communicator."""
+    g = _g() if g is None else g
+    if g is None or g == dist.group.WORLD:
+        return src
+    return dist.get_global_rank(g, src)
+
+
 def _broadcast(t: torch.Tensor, src: int) -> None:
     if _staged(t):
         h = t.cpu()
-        dist.broadcast(h, src=src, group=_g())
+        dist.broadcast(h, src=_gsrc(src), group=_g())
         t.copy_(h)
     else:
-        dist.broadcast(t, src=src, group=_g())
+        dist.broadcast(t, src=_gsrc(src), group=_g())
 
 
 def _all_gather_into(out: torch.Tensor, t: torch.Tensor) -> None:
@@ -233,34 +244,33 @@ def _all_gather_into(out: torch.Tensor, t: torch.Tensor) -> None:
 
 
 def broadcast_bytes(data: bytes, src: int = 0) -> bytes:
-    """``data`` from rank ``src`` on every rank, as host bytes (small payloads: configuration, layouts).  Bulk
-    payloads that end on the device use ``broadcast_device_bytes``."""
+    """``data`` from rank ``src`` (a rank of the job's group) on every rank, as host bytes (small payloads:
+    configuration, layouts).  Bulk payloads that end on the device use ``broadcast_device_bytes``."""
     from . import _RANK
+    g = _gloo_or_default()
+    gsrc = _gsrc(src, g)
     n = torch.tensor([len(data) if _RANK == src else 0], dtype=torch.int64)
-    dist.broadcast(n, src=src, group=_gloo_or_default())
+    dist.broadcast(n, src=gsrc, group=g)
     size = int(n.item())
     buf = torch.frombuffer(bytearray(data), dtype=torch.uint8) if (_RANK == src and size) else \
         torch.empty(size, dtype=torch.uint8)
     if size:
-        dist.broadcast(buf, src=src, group=_gloo_or_default())
+        dist.broadcast(buf, src=gsrc, group=g)
     return data if _RANK == src else buf.numpy().tobytes()
 
 
 def _gloo_or_default():
-    """Host-tensor broadcasts need a gloo communicator; with RCCL as the job's backend they go through a device
-    buffer instead (``broadcast_device_bytes``)."""
+    """Host-tensor broadcasts need a gloo communicator; with RCCL as the job's backend that is the host group
+    ``parallel.init`` created on every rank (same ranks as the job's group)."""
     g = _g()
-    return g if dist.get_backend(g) == "gloo" else _host_group()
+    if dist.get_backend(g) == "gloo":
+        return g
+    if _HOST_GROUP is None:
+        raise RuntimeError("broadcast_bytes under RCCL needs parallel.init() (it creates the host group)")
+    return _HOST_GROUP
 
 
 _HOST_GROUP = None
-
-
-def _host_group():
-    global _HOST_GROUP
-    if _HOST_GROUP is None:
-        _HOST_GROUP = dist.new_group(backend="gloo")
-    return _HOST_GROUP
 
 
 def broadcast_device_bytes(data: Optional[bytes], src: int, device, pad: int = 64) -> Tuple[torch.Tensor, int]:
@@ -295,7 +305,7 @@ def broadcast_device_bytes(data: Optional[bytes], src: int, device, pad: int = 6
 
 def _broadcast_staged_slice(buf, size, src):
     h = buf[:size].cpu()
-    dist.broadcast(h, src=src, group=_g())
+    dist.broadcast(h, src=_gsrc(src), group=_g())
     buf[:size].copy_(h)
 
 
@@ -315,8 +325,8 @@ def allgather_table(table):
     """Every rank receives the concatenation of all ranks' rows (rank order).
 
     The table is packed once (identity order), the per-rank sizes are all-gathered (the one host read-back), and
-    the matrix and every string arena travel with one ``all_gather_into_tensor`` each, padded to the largest
-    rank's share: the receive buffer is W × the largest share — the result's size for balanced ranks — and no rank
+    the matrix and the string bytes (every leaf in one buffer) travel with one ``all_gather_into_tensor`` each,
+    padded to the largest rank's share: the receive buffer is W × the largest share — the result's size for balanced ranks — and no rank
     ever materialises W copies of its own rows.  One unpack launch reads the padded buffers in place (strings stay
     views into the gathered arenas)."""
     from . import packing as PK
@@ -335,22 +345,30 @@ def allgather_table(table):
     rows = [r[0] for r in got]
     bts = [[r[1 + s] for r in got] for s in range(lay.S)]
     maxr = max(rows)
-    maxb = [max(bts[s]) for s in range(lay.S)]
     me = _rank()
+    # every string leaf's bytes in one buffer per rank ([leaf 0 | leaf 1 | …]), padded to the largest rank's total:
+    # one all-gather moves them all
+    tot = [sum(bts[s][k] for s in range(lay.S)) for k in range(W)]
+    maxb = max(tot) if lay.S else 0
     mat, arenas = PK.scatter(lay, state, [lay.n], [[bts[s][me]] for s in range(lay.S)], rows_alloc=maxr,
-                             bytes_alloc=maxb)
+                             bytes_alloc=[maxb], coalesce=True)
     n_out = sum(rows)
     gm = torch.empty((W * maxr, lay.C), dtype=torch.int64, device=device)
     if lay.C and maxr:
         _all_gather_into(gm, mat[:maxr])
-    gar = []
-    for s in range(lay.S):
-        ga = torch.zeros(W * maxb[s] + 16, dtype=torch.uint8, device=device)
-        if maxb[s]:
-            _all_gather_into(ga[:W * maxb[s]], arenas[s][:maxb[s]])
-        gar.append(ga)
+    gar, byte_base = [], [[0] * W for _ in range(lay.S)]
+    if lay.S:
+        ga = torch.zeros(W * maxb + 16, dtype=torch.uint8, device=device)
+        if maxb:
+            _all_gather_into(ga[:W * maxb], arenas[0][:maxb])
+        gar = [ga] * lay.S
+        for k in range(W):
+            pos = k * maxb
+            for s in range(lay.S):
+                byte_base[s][k] = pos
+                pos += bts[s][k]
     out = PK.unpack(lay.names, lay.spec, lay.meta(), gm, gar, _prefix(rows), [k * maxr for k in range(W)],
-                    [[k * maxb[s] for k in range(W)] for s in range(lay.S)], n_out, device, _force_torch())
+                    byte_base, n_out, device, _force_torch())
     return Table(out.names, out.columns, out.length, device)
 
 
@@ -362,7 +380,7 @@ def _rank():
 def broadcast_table(table, src: int = 0):
     """Rank ``src``'s table on every rank (the others pass any table with the same column names, e.g. empty): the
     layout travels as one small object broadcast, the data as one broadcast of the packed [rows × C] int64 matrix
-    plus one per string leaf's bytes — the source sends each byte once (ncclBroadcast's pipelined ring/tree over
+    plus one of every string leaf's bytes — the source sends each byte once (ncclBroadcast's pipelined ring/tree over
     xGMI), never W copies."""
     from . import packing as PK
     from . import _RANK
@@ -374,30 +392,30 @@ def broadcast_table(table, src: int = 0):
         lay = PK.Layout(table)
         sizes, state = PK.plan(lay, None, 1, _force_torch())
         szl = sizes.tolist()[0]
-        mat, arenas = PK.scatter(lay, state, [lay.n], [[szl[1 + s]] for s in range(lay.S)])
+        mat, arenas = PK.scatter(lay, state, [lay.n], [[szl[1 + s]] for s in range(lay.S)], coalesce=True)
         layout = [lay.spec, lay.meta(), lay.n, lay.C, [int(szl[1 + s]) for s in range(lay.S)]]
     else:
         layout, mat, arenas = None, None, None
     obj = [layout]
-    dist.broadcast_object_list(obj, src=src, group=_g())
+    dist.broadcast_object_list(obj, src=_gsrc(src), group=_g())
     spec, meta, rows, C, nbytes = obj[0]
     if _RANK != src:
         mat = torch.empty((rows, C), dtype=torch.int64, device=device)
     if rows and C:
         _broadcast(mat, src)
-    got = []
-    for s, nb in enumerate(nbytes):
-        buf = torch.zeros(nb + 16, dtype=torch.uint8, device=device)
-        if _RANK == src and nb:
-            buf[:nb] = arenas[s][:nb]
-        if nb:
-            if _staged(buf):
-                _broadcast_staged_slice(buf, nb, src)
-            else:
-                _broadcast(buf[:nb], src)
-        got.append(buf)
-    out = PK.unpack(table.names, spec, meta, mat, got, [0, rows], [0], [[0] for _ in nbytes], rows, device,
-                    _force_torch())
+    # every string leaf's bytes in one broadcast ([leaf 0 | leaf 1 | …])
+    nb = sum(nbytes)
+    buf = torch.zeros(nb + 16, dtype=torch.uint8, device=device)
+    if _RANK == src and nb:
+        buf[:nb] = arenas[0][:nb]
+    if nb:
+        if _staged(buf):
+            _broadcast_staged_slice(buf, nb, src)
+        else:
+            _broadcast(buf[:nb], src)
+    got = [buf] * len(nbytes)
+    out = PK.unpack(table.names, spec, meta, mat, got, [0, rows], [0], [[sum(nbytes[:s])] for s in range(len(nbytes))],
+                    rows, device, _force_torch())
     out.dist = P_REPLICATED
     return out
 

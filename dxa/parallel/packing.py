@@ -315,7 +315,8 @@ def _pack_args_type(L):
                     ("nstr", ctypes.c_int32), ("C", ctypes.c_int32), ("hist", ctypes.c_void_p),
                     ("sizes", ctypes.c_void_p), ("mat", ctypes.c_void_p), ("cols", _XCol * maxc),
                     ("valids", _XValid * maxv), ("strs", _XStr * maxs), ("sizes_stride", ctypes.c_int32),
-                    ("nextra", ctypes.c_int32), ("extra", ctypes.c_int64 * L[8])]
+                    ("nextra", ctypes.c_int32), ("extra", ctypes.c_int64 * L[8]), ("coalesce", ctypes.c_int32),
+                    ("pad1", ctypes.c_int32)]
     return PackArgs
 
 
@@ -384,6 +385,7 @@ def plan_device(lay: Layout, dest: Optional[torch.Tensor], W: int, extra=()):
     hist = torch.empty((1 + lay.S) * W * a.nblocks, dtype=torch.int64, device=dev)
     sizes = torch.empty((W, 1 + lay.S + len(extra)), dtype=torch.int64, device=dev)
     a.hist, a.sizes = hist.data_ptr(), sizes.data_ptr()
+    keep.append(sizes)                 # the scatter kernel reads it again (coalesced string bytes)
     a.sizes_stride, a.nextra = sizes.shape[1], len(extra)
     for i, x in enumerate(extra):
         a.extra[i] = int(x)
@@ -392,8 +394,11 @@ def plan_device(lay: Layout, dest: Optional[torch.Tensor], W: int, extra=()):
 
 
 def scatter_device(lay: Layout, plan: DevicePlan, send_rows: List[int], send_bytes: List[List[int]],
-                   rows_alloc: Optional[int] = None, bytes_alloc: Optional[List[int]] = None):
-    """Send matrix + arenas; ``rows_alloc`` / ``bytes_alloc`` over-allocate (padding for all-gathers)."""
+                   rows_alloc: Optional[int] = None, bytes_alloc: Optional[List[int]] = None,
+                   coalesce: bool = False):
+    """Send matrix + arenas; ``rows_alloc`` / ``bytes_alloc`` over-allocate (padding for all-gathers).  With
+    ``coalesce`` the arenas are ONE buffer, destination-major (``coalesced_bytes``), and ``bytes_alloc`` is its
+    one-element capacity."""
     from ..ops import native as N
     a = plan.args
     n, dev = lay.n, lay.device
@@ -416,6 +421,17 @@ def scatter_device(lay: Layout, plan: DevicePlan, send_rows: List[int], send_byt
     mat = torch.empty((R, lay.C), dtype=torch.int64, device=dev)
     if R > n:
         mat[n:].zero_()
+    a.mat = mat.data_ptr()
+    if coalesce:
+        total = sum(int(x) for b in send_bytes for x in b)
+        cap = max(total, (bytes_alloc or [0])[0])
+        ar = torch.empty(cap + 16, dtype=torch.uint8, device=dev)
+        for lf in lay.strs:
+            a.strs[lf.sidx].dst = ar.data_ptr()
+        a.coalesce = 1
+        N.call("dxa_xchg_scatter", ctypes.byref(a), N.stream_handle(dev))
+        a.coalesce = 0
+        return mat, [ar[:cap]]
     arenas = []
     for lf in lay.strs:
         total = int(sum(send_bytes[lf.sidx]))
@@ -423,7 +439,6 @@ def scatter_device(lay: Layout, plan: DevicePlan, send_rows: List[int], send_byt
         ar = torch.empty(cap + 16, dtype=torch.uint8, device=dev)
         arenas.append(ar)
         a.strs[lf.sidx].dst = ar.data_ptr()
-    a.mat = mat.data_ptr()
     N.call("dxa_xchg_scatter", ctypes.byref(a), N.stream_handle(dev))
     return mat, [ar[:max(int(sum(send_bytes[lf.sidx])), (bytes_alloc or [0] * lay.S)[lf.sidx])]
                  for ar, lf in zip(arenas, lay.strs)]
@@ -513,14 +528,45 @@ def plan(lay: Layout, dest: Optional[torch.Tensor], W: int, force_torch: bool = 
     return sizes, ("torch", st)
 
 
-def scatter(lay: Layout, state, send_rows, send_bytes, rows_alloc=None, bytes_alloc=None):
+def coalesced_bytes(sizes: List[List[int]]) -> Tuple[List[int], List[List[int]]]:
+    """Layout of ONE destination-major byte buffer holding every string leaf: ``sizes[s][d]`` bytes of leaf s for
+    rank d are at ``[d0: leaf 0 | leaf 1 | …][d1: …]`` → (bytes per rank, start of leaf s's block of rank d).
+    Used for both sides of a collective: send splits / leaf bases, or received sizes per source rank."""
+    S = len(sizes)
+    W = len(sizes[0]) if S else 0
+    per_rank, base, pos = [], [[0] * W for _ in range(S)], 0
+    for d in range(W):
+        start = pos
+        for s in range(S):
+            base[s][d] = pos
+            pos += int(sizes[s][d])
+        per_rank.append(pos - start)
+    return per_rank, base
+
+
+def scatter(lay: Layout, state, send_rows, send_bytes, rows_alloc=None, bytes_alloc=None, coalesce=False):
+    """Send matrix and string bytes.  ``coalesce``: the bytes as ONE buffer laid out by ``coalesced_bytes`` (one
+    collective moves every string leaf); ``bytes_alloc`` is then ``[capacity]``."""
     kind, st = state
     if kind == "device":
-        return scatter_device(lay, st, send_rows, send_bytes, rows_alloc, bytes_alloc)
+        return scatter_device(lay, st, send_rows, send_bytes, rows_alloc, bytes_alloc, coalesce)
     mat, arenas = scatter_torch(lay, st, send_rows, send_bytes)
     if rows_alloc and rows_alloc > mat.shape[0]:
         mat = torch.cat([mat, torch.zeros((rows_alloc - mat.shape[0], lay.C), dtype=torch.int64,
                                           device=mat.device)])
+    if coalesce:
+        dev = lay.device
+        parts = []
+        W = len(send_rows)
+        for d in range(W):
+            for s in range(lay.S):
+                lo = sum(int(x) for x in send_bytes[s][:d])
+                parts.append(arenas[s][lo:lo + int(send_bytes[s][d])])
+        buf = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=dev)
+        cap = (bytes_alloc or [0])[0]
+        if cap > buf.shape[0]:
+            buf = torch.cat([buf, torch.zeros(cap - buf.shape[0], dtype=torch.uint8, device=dev)])
+        return mat, [buf]
     if bytes_alloc:
         arenas = [torch.cat([ar, torch.zeros(bytes_alloc[j] - ar.shape[0], dtype=torch.uint8, device=ar.device)])
                   if bytes_alloc[j] > ar.shape[0] else ar for j, ar in enumerate(arenas)]

@@ -202,12 +202,17 @@ def test_bench_two_ranks_gloo(flow, device, tmp_path):
         env["DXA_DIST_BACKEND"] = "gloo"          # both ranks share the test box's one GPU
     else:
         env["HIP_VISIBLE_DEVICES"] = ""
+    bench_args = [os.path.join(root, "bench.py"), "--gpus", "2", "--flow", flow, "--events-per-batch", "500",
+                  "--steps", "2", "--warmup", "3", "--ref-rows", "5000"]
     for _attempt in range(3):         # the free port can be taken by a parallel test between probe and bind
-        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                            os.path.join(root, "bench.py"), "--gpus", "2", "--flow", flow, "--events-per-batch",
-                            "500", "--steps", "2", "--warmup", "3", "--ref-rows", "5000"], capture_output=True,
-                           text=True, env=env, timeout=600, cwd=str(tmp_path))
+        if device == "cuda":
+            # bench.py starts its own ranks for --gpus N (no launcher): the driver's plain `bench.py --gpus N`
+            r = subprocess.run([sys.executable] + bench_args, capture_output=True, text=True,
+                               env=dict(env, MASTER_PORT=str(_free_port())), timeout=600, cwd=str(tmp_path))
+        else:
+            r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + bench_args,
+                               capture_output=True, text=True, env=env, timeout=600, cwd=str(tmp_path))
         err = r.stderr.lower()
         if r.returncode == 0 or not any(m in err for m in ("address already in use", "eaddrinuse",
                                                            "failed to listen", "connection refused")):
@@ -223,6 +228,56 @@ def test_bench_two_ranks_gloo(flow, device, tmp_path):
     assert outs and all(v >= 0 for v in outs.values())
     if flow == "passthrough":
         assert outs["Output_Tagged_Sink_InputEvents"] == 1000
+    # the value is the job's events over the MAX-over-ranks elapsed time
+    assert out["value"] == pytest.approx(1000 * 2 / (out["ms_per_step"] * 2 / 1e3), rel=1e-9)
+
+
+@pytest.mark.parametrize("n", [3, 4])
+def test_bench_launches_its_own_ranks(n, tmp_path):
+    """``python bench.py --gpus N`` with no launcher starts N rank processes itself (subprocesses, before any GPU
+    call) and prints ONE job-wide line with ``n_gpus`` N: the driver's scaling run must not silently measure one
+    rank.  Passthrough tags and writes every event, so its job-wide sink count is exactly N x events."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, HIP_VISIBLE_DEVICES="", MASTER_PORT=str(_free_port()))
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--flow", "passthrough",
+                        "--events-per-batch", "300", "--steps", "2", "--warmup", "2"], capture_output=True, text=True,
+                       env=env, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["config"]["parallelism"] == f"dp{n}"
+    assert out["config"]["global_batch"] == 300 * n
+    assert out["last_batch_outputs"]["Output_Tagged_Sink_InputEvents"] == 300 * n
+
+
+def test_bench_rejects_world_size_mismatch(tmp_path):
+    """A launcher's WORLD_SIZE that disagrees with --gpus fails loudly instead of reporting the wrong n_gpus."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, HIP_VISIBLE_DEVICES="", WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, env=env, timeout=120, cwd=str(tmp_path))
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_failing_rank_fails_the_job(tmp_path):
+    """One rank dying makes the self-launched job exit non-zero (the survivors are stopped, not left hanging)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, HIP_VISIBLE_DEVICES="", MASTER_PORT=str(_free_port()),
+               DXA_BENCH_FAIL_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--flow", "passthrough",
+                        "--events-per-batch", "100", "--steps", "1", "--warmup", "1"], capture_output=True,
+                       text=True, env=env, timeout=300, cwd=str(tmp_path))
+    assert r.returncode != 0
+    assert "exited with" in r.stderr and "failing on request" in r.stderr
 
 
 def test_cpulist_parsing_and_cpu_noop():

@@ -61,6 +61,17 @@ def _raw(records, device):
     return RawBatch(buf.to(device), offs.to(device), len(records))
 
 
+EMPTY_BATCH = 2          # the batch in which the last rank's share is empty
+
+
+def _share(records, rank, world, b):
+    """Rank ``rank``'s records of batch ``b``: every world-th event (as world source partitions would hold them),
+    except that in batch EMPTY_BATCH the last rank receives nothing (an idle partition) and the others split it."""
+    if world > 1 and b == EMPTY_BATCH:
+        return [] if rank == world - 1 else records[rank::world - 1]
+    return records[rank::world]
+
+
 def _run(variant, rank, world, workdir, shared, batches, device="cpu"):
     """This rank's share of every batch through a Processor: per batch (sink lines by output, state rows, metrics)."""
     from dxa.engine.processor import Processor
@@ -68,9 +79,9 @@ def _run(variant, rank, world, workdir, shared, batches, device="cpu"):
     sinks.MEMORY_SINKS.clear()
     proc = Processor(_settings(variant, workdir, shared), device)
     out = []
-    for bt, records in batches:
+    for b, (bt, records) in enumerate(batches):
         proc.clock = lambda bt=bt: bt / 1e6 + 0.25         # current_timestamp() (alert EventTime) pinned per batch
-        m = proc.process_batch(_raw(records[rank::world], device), bt, INTERVAL_US)
+        m = proc.process_batch(_raw(_share(records, rank, world, b), device), bt, INTERVAL_US)
         m = proc.drain() or m
         lines = {k: list(v) for k, v in sinks.MEMORY_SINKS.items()}
         sinks.MEMORY_SINKS.clear()
@@ -165,11 +176,14 @@ def _rows_equal(got, want, path):
     _close(got, want, path)
 
 
-@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("world,device", [(2, "cpu"), (3, "cpu"), (4, "cpu"),
+                                          pytest.param(2, "cuda", marks=pytest.mark.gpu),
+                                          pytest.param(3, "cuda", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("variant", ["groupby", "window", "join", "full", "passthrough"])
-def test_flow_two_ranks_match_one(variant, device, tmp_path):
-    """``cuda``: both ranks on the test box's one GPU (every kernel, incl. the exchange pack / unpack kernels, on
-    the device; the collectives staged through gloo)."""
+def test_flow_ranks_match_one(variant, world, device, tmp_path):
+    """W ranks (2, 3 — a world that is not a power of two, so ``owner_of``'s modulo is uneven — and 4), the last
+    one idle in one batch, against the one-rank run.  ``cuda``: every rank on the test box's one GPU (every kernel,
+    incl. the exchange pack / unpack kernels, on the device; the collectives staged through gloo)."""
     import time
     from dxa import parallel as P
     if device == "cuda" and not torch.cuda.is_available():
@@ -183,20 +197,21 @@ def test_flow_two_ranks_match_one(variant, device, tmp_path):
     batches = _batches(clock0)
     P.shutdown()
     one = _run(variant, 0, 1, str(tmp_path / "one" / "w"), shared1, batches, device)
-    two = _spawn_flow(variant, tmp_path, shared2, batches, device)
+    two = _spawn_flow(variant, tmp_path, shared2, batches, device, world)
+    ranks = range(world)
     rows_seen = 0
     for b in range(N_BATCHES):
         lines1, state1, m1 = one[b]
-        names = set(lines1) | set(two[0][b][0]) | set(two[1][b][0])
+        names = set(lines1).union(*(set(two[r][b][0]) for r in ranks))
         for name in sorted(names):
             want = [json.loads(l) for l in lines1.get(name, [])]
-            got = [json.loads(l) for r in (0, 1) for l in two[r][b][0].get(name, [])]
+            got = [json.loads(l) for r in ranks for l in two[r][b][0].get(name, [])]
             _rows_equal(got, want, f"batch{b}.{name}")
             rows_seen += len(want)
         for name in state1:
-            _rows_equal(two[0][b][1][name] + two[1][b][1][name], state1[name], f"batch{b}.state.{name}")
+            _rows_equal([x for r in ranks for x in two[r][b][1][name]], state1[name], f"batch{b}.state.{name}")
         # the job-wide metrics (all-reduced) equal the one-rank metrics on every rank
-        for r in (0, 1):
+        for r in ranks:
             assert two[r][b][2].keys() == m1.keys(), (b, r, sorted(set(two[r][b][2]) ^ set(m1)))
             for k in m1:
                 assert two[r][b][2][k] == pytest.approx(m1[k]), (b, r, k)
@@ -204,17 +219,17 @@ def test_flow_two_ranks_match_one(variant, device, tmp_path):
     if variant == "full":
         assert one[-1][1]["DeviceState"], "accumulator never updated"
         # accumulator rows live on exactly one rank each
-        k0 = {(r["deviceId"], r["homeId"], r["deviceType"]) for r in two[0][-1][1]["DeviceState"]}
-        k1 = {(r["deviceId"], r["homeId"], r["deviceType"]) for r in two[1][-1][1]["DeviceState"]}
-        assert k0 and k1 and not (k0 & k1)
+        ks = [{(x["deviceId"], x["homeId"], x["deviceType"]) for x in two[r][-1][1]["DeviceState"]} for r in ranks]
+        assert all(ks)
+        assert sum(len(k) for k in ks) == len(set().union(*ks))
 
 
-def _spawn_flow(variant, tmp_path, shared, batches, device="cpu"):
+def _spawn_flow(variant, tmp_path, shared, batches, device="cpu", world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, variant, str(tmp_path / f"two{r}" / "w"), shared,
-                                               batches, device)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, variant, str(tmp_path / f"two{r}" / "w"), shared,
+                                               batches, device)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
