@@ -86,6 +86,60 @@ def test_torch_pack_roundtrip_cpu():
     _check_roundtrip(rows, dest, outs)
 
 
+def _coalesced(t, dest, force_torch):
+    """Coalesced pack (every string leaf in one destination-major buffer) → per-destination unpack, with the
+    receive-side byte bases computed by ``coalesced_bytes`` exactly as ``shuffle_table`` does."""
+    lay = PK.Layout(t)
+    sizes, state = PK.plan(lay, dest, W, force_torch)
+    sz = sizes.tolist()
+    send_rows = [r[0] for r in sz]
+    send_bytes = [[r[1 + s] for r in sz] for s in range(lay.S)]
+    mat, (buf,) = PK.scatter(lay, state, send_rows, send_bytes, coalesce=True)
+    per_rank, base = PK.coalesced_bytes(send_bytes)
+    assert sum(per_rank) <= buf.shape[0]
+    outs, r0 = [], 0
+    for d in range(W):
+        rows = send_rows[d]
+        lo = sum(per_rank[:d])
+        piece = torch.zeros(per_rank[d] + 16, dtype=torch.uint8, device=t.device)
+        piece[:per_rank[d]] = buf[lo:lo + per_rank[d]]
+        outs.append(PK.unpack(lay.names, lay.spec, lay.meta(), mat[r0:r0 + rows], [piece] * lay.S, [0, rows], [0],
+                              [[base[s][d] - lo] for s in range(lay.S)], rows, t.device, force_torch))
+        r0 += rows
+    return buf[:sum(per_rank)], outs
+
+
+def test_coalesced_bytes_layout():
+    per_rank, base = PK.coalesced_bytes([[3, 0, 5], [1, 2, 0]])       # 2 leaves x 3 ranks
+    assert per_rank == [4, 2, 5]
+    assert base == [[0, 4, 6], [3, 4, 11]]
+
+
+def test_torch_coalesced_roundtrip_cpu():
+    rows = _rows(2000)
+    t = Table.from_pylist(rows, SCHEMA)
+    dest = [random.Random(5).randrange(W) for _ in rows]
+    dest[:50] = [1] * 50
+    dest = [d if d != 3 else 4 for d in dest]            # destination 3 receives nothing
+    _buf, outs = _coalesced(t, torch.tensor(dest), True)
+    _check_roundtrip(rows, dest, outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 777, 20000])
+def test_device_coalesced_pack_matches_torch(gpu, n):
+    rows = _rows(n, seed=9)
+    rnd = random.Random(13)
+    dest = [rnd.randrange(W) for _ in rows]
+    t = Table.from_pylist(rows, SCHEMA, gpu)
+    dt = torch.tensor(dest, dtype=torch.int64, device=gpu)
+    buf_d, outs_d = _coalesced(t, dt, False)
+    buf_t, outs_t = _coalesced(t, dt, True)
+    assert torch.equal(buf_d.cpu(), buf_t.cpu())
+    _check_roundtrip(rows, dest, outs_d)
+    _check_roundtrip(rows, dest, outs_t)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [0, 1, 777, 20000])
 def test_device_pack_matches_torch(gpu, n):
