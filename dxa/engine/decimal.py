@@ -212,6 +212,49 @@ def mul_pow10(h, l, k: int):
     return torch.where(neg, nh, ah), torch.where(neg, nl, al), ovf
 
 
+def div_pow10_round(h, l, k: int, half_even: bool):
+    """signed 128 / 10^k rounded HALF_UP (``half_even`` False) or HALF_EVEN (ties to the even quotient), exact: the
+    digits below the last dropped one only matter for the tie test, so their remainders are OR-ed."""
+    if k <= 0:
+        return h, l
+    if not half_even:
+        return div_pow10_half_up(h, l, k)
+    ah, al, neg = abs128(h, l)
+    sticky = torch.zeros_like(neg)
+    remaining = k - 1
+    while remaining > 0:
+        step = min(remaining, 9)
+        ah, al, r = divmod_small_u(ah, al, 10 ** step)
+        sticky |= r != 0
+        remaining -= step
+    ah, al, last = divmod_small_u(ah, al, 10)
+    up = (last > 5) | ((last == 5) & (sticky | ((al & 1) == 1)))
+    ah, al = add128(ah, al, torch.zeros_like(ah), up.to(torch.int64))
+    nh, nl = neg128(ah, al)
+    return torch.where(neg, nh, ah), torch.where(neg, nl, al)
+
+
+def round_column(col, digits: int, half_even: bool):
+    """round / bround of decimal(p, s) to ``digits`` places: Spark 2.4's RoundBase keeps decimal(p, min(s, digits))
+    (a larger digit count keeps the scale); the value is rounded HALF_UP / HALF_EVEN and is NULL when it no longer
+    fits p digits (Decimal.toPrecision).  Negative digits round left of the point; the result scale is then 0."""
+    t: DecimalType = col.dtype
+    new_scale = max(0, min(t.scale, digits))
+    h, l = lanes(col.data)
+    drop = t.scale - digits
+    if drop > 0:
+        h, l = div_pow10_round(h, l, drop, half_even)          # value · 10^digits, an integer
+        # back to the result scale: digits < 0 multiplies the dropped places back in
+        h, l, ovf = mul_pow10(h, l, new_scale - digits)
+    else:
+        ovf = torch.zeros_like(h, dtype=torch.bool)
+    rt = DecimalType(t.precision, new_scale)
+    ok = fits(h, l, rt.precision) & ~ovf
+    valid = ok if col.valid is None else col.valid & ok
+    from .column import PrimColumn
+    return PrimColumn(rt, pack(h, l, rt), valid)
+
+
 def div_pow10_half_up(h, l, k: int):
     """signed 128 / 10^k rounded HALF_UP (away from zero at .5), exact."""
     if k <= 0:
@@ -230,6 +273,24 @@ def div_pow10_half_up(h, l, k: int):
     ah, al = add128(ah, al, torch.zeros_like(ah), up.to(torch.int64))
     nh, nl = neg128(ah, al)
     return torch.where(neg, nh, ah), torch.where(neg, nl, al)
+
+
+def div_u_vec_half_up(h, l, d: torch.Tensor):
+    """signed 128 / d per element (0 < d < 2^31, an int64 tensor), rounded HALF_UP, exact: long division over
+    four 32-bit limbs, then +1 on the magnitude when 2·remainder ≥ d."""
+    ah, al, neg = abs128(h, l)
+    x = _limbs(ah, al)
+    rem = torch.zeros_like(al)
+    q = [None] * 4
+    for i in (3, 2, 1, 0):
+        cur = (rem << 32) | x[i]                   # rem < d < 2^31 → cur < 2^63
+        q[i] = cur // d
+        rem = cur - q[i] * d
+    qh, ql = _from_limbs(*q)
+    up = (2 * rem >= d).to(torch.int64)
+    qh, ql = add128(qh, ql, torch.zeros_like(qh), up)
+    nh, nl = neg128(qh, ql)
+    return torch.where(neg, nh, qh), torch.where(neg, nl, ql)
 
 
 def pow10_128(k: int, like: torch.Tensor):

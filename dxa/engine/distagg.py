@@ -67,11 +67,9 @@ def _partials(call: A.Call, scope, ctx) -> List[Tuple[str, Optional[PrimColumn],
     if name in ("avg", "mean"):
         x = PrimColumn("double", arg.data.to(torch.float64), arg.valid)
         return [("s", x, "sum", "sum"), ("cnt", arg, "count", "sum")]
-    # variance family: sum, sum of squares, count
-    x = arg.data.to(torch.float64)
-    return [("s", PrimColumn("double", x, arg.valid), "sum", "sum"),
-            ("s2", PrimColumn("double", x * x, arg.valid), "sum", "sum"),
-            ("cnt", arg, "count", "sum")]
+    # variance family: (count, sum, centred M2) per partial group — merged with Chan's formula (``_chan_merge``)
+    x = PrimColumn("double", arg.data.to(torch.float64), arg.valid)
+    return [("s", x, "sum", "sum"), ("m2", x, "m2", "m2"), ("cnt", arg, "count", "sum")]
 
 
 def _finish(call: A.Call, merged: Dict[str, PrimColumn]) -> PrimColumn:
@@ -94,13 +92,13 @@ def _finish(call: A.Call, merged: Dict[str, PrimColumn]) -> PrimColumn:
     s = merged["s"].data
     if name in ("avg", "mean"):
         return PrimColumn("double", s / c.clamp(min=1), c > 0)
-    s2 = merged["s2"].data
-    mean = s / c.clamp(min=1)
-    m2 = (s2 - c * mean * mean).clamp(min=0)
+    m2 = merged["m2"].data
     pop = name.endswith("_pop")
     var = m2 / (c if pop else (c - 1)).clamp(min=1)
     out = var.sqrt() if name.startswith("std") else var
-    return PrimColumn("double", out, c > (0 if pop else 1))
+    if not pop:                # Spark 2.4 CentralMomentAgg: NaN for one row, null for none
+        out = torch.where(c == 1, torch.full_like(out, float("nan")), out)
+    return PrimColumn("double", out, c > 0)
 
 
 class _PFReq(ctypes.Structure):
@@ -221,7 +219,8 @@ def merge_partials(got: Table, plan, key_names: List[str], aggs: Dict, grouped: 
     if m == 0:
         vals = [_empty_merge(got.column(nm), op, ng, dev) for _, nm, _, op in entries]
     else:
-        vals = G.aggregate_many(g2, [(got.column(nm), op) for _, nm, _, op in entries], m)
+        vals = G.aggregate_many(g2, [(got.column(nm), _merge_op(op)) for _, nm, _, op in entries], m)
+        vals = _chan_merge(g2, got, entries, vals, m)
     merged_by = {ak: {} for ak in aggs}
     for (ak, _, suffix, _), v in zip(entries, vals):
         merged_by[ak][suffix] = v
@@ -242,13 +241,46 @@ def combine_partials(got: Table, plan, key_names: List[str], grouped: bool) -> T
         names.append(k)
         cols.append(got.column(k).take(g2.rep))
     reqs = []
-    for entries in plan.values():
-        for nm, _suffix, op in entries:
+    ents = []
+    for ak, entries in plan.items():
+        for nm, suffix, op in entries:
             names.append(nm)
-            reqs.append((got.column(nm), op))
-    cols.extend(G.aggregate_many(g2, reqs, m))
+            reqs.append((got.column(nm), _merge_op(op)))
+            ents.append((ak, nm, suffix, op))
+    cols.extend(_chan_merge(g2, got, ents, G.aggregate_many(g2, reqs, m), m))
     t = Table(names, cols, g2.ngroups, dev)
     return t
+
+
+def _merge_op(op: str) -> str:
+    return "sum" if op == "m2" else op
+
+
+def _chan_merge(g2, got: Table, entries, vals, m: int):
+    """Complete the M2 merges of the variance family: the partial M2s were summed; Chan et al.'s pairwise update
+    adds Σ n_i (mean_i − mean)² over the partials of each merged group (mean = Σ s_i / Σ n_i), which is exact
+    algebra for any number of partials and keeps every term centred."""
+    by_agg = {}
+    for j, (ak, nm, suffix, _op) in enumerate(entries):
+        by_agg.setdefault(ak, {})[suffix] = (j, nm)
+    gid = g2.gid.to(torch.int64)
+    for ak, parts in by_agg.items():
+        if "m2" not in parts:
+            continue
+        jm, _ = parts["m2"]
+        js, ns = parts["s"]
+        jc, nc = parts["cnt"]
+        n_i = got.column(nc).data.to(torch.float64)
+        s_i = got.column(ns).data.to(torch.float64)
+        n = vals[jc].data.to(torch.float64)
+        mean = vals[js].data.to(torch.float64) / n.clamp(min=1)
+        mean_i = s_i / n_i.clamp(min=1)
+        d = mean_i - mean[gid]
+        corr = G.aggregate(g2, PrimColumn("double", torch.where(n_i > 0, n_i * d * d, torch.zeros_like(d))), "sum",
+                           m)
+        mv = vals[jm]
+        vals[jm] = PrimColumn("double", mv.data + corr.data, mv.valid)
+    return vals
 
 
 def distributed_aggregate(gexprs, keys, aggs: Dict, scope, ctx):

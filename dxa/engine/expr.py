@@ -327,7 +327,8 @@ def _coerce_const_for(col_other: Column, const: ConstColumn) -> ConstColumn:
 
 # Built-ins that take decimal(p,s) arguments as they are; every other function sees its decimal arguments as
 # doubles (Spark's implicit cast for functions typed on DoubleType: ImplicitTypeCasts) — see _call / evaluate.
-_DECIMAL_AWARE = frozenset({"coalesce", "if", "nvl", "ifnull", "nullif", "nvl2", "to_json", "named_struct", "struct",
+_DECIMAL_AWARE = frozenset({"round", "bround", "hash",
+                            "coalesce", "if", "nvl", "ifnull", "nullif", "nvl2", "to_json", "named_struct", "struct",
                             "array", "map", "concat", "concat_ws", "isnull", "isnotnull", "string", "abs",
                             "negative", "positive"})
 
@@ -1478,17 +1479,51 @@ _ABS_NUM = _unary_num(torch.abs)
 
 
 def _f_round(e, scope, ctx, subst):
+    """round (HALF_UP) / bround (HALF_EVEN) — Spark 2.4's RoundBase:
+
+    * decimal(p, s) → decimal(p, min(s, d)), exact (``decimal.round_column``);
+    * double / float → ``BigDecimal(x).setScale(d, mode).toDouble``, where Scala's ``BigDecimal(x)`` is the shortest
+      decimal that reads back as x (``Double.toString``).  So ``round(1.005, 2)`` on a double is 1.01, not the 1.0 that
+      scaling the binary value gives.  On the device: t = (2f+1) / (2·10^d) is the double nearest to the tie point
+      f + ½ above f = ⌊|x|·10^d⌋ (one correctly rounded division of exact operands).  x above t rounds up, below
+      rounds down, and x == t is the tie, decided by the mode.  A double equal to the tie's nearest double has the
+      tie as its shortest form except at 16-17 significant digits;
+    * int / long: unchanged for d ≥ 0, rounded to 10^-d otherwise."""
     n, dev = scope.length, scope.device
     a = evaluate(e.args[0], scope, ctx, subst)
     digits = int(evaluate(e.args[1], scope, ctx, subst).value) if len(e.args) > 1 else 0
+    half_even = e.name == "bround"
     if isinstance(a, ConstColumn):
         a = a.materialize()
-    if a.dtype in ("int", "long"):
-        return a
-    scale = 10.0 ** digits
-    x = a.data * scale
-    r = torch.sign(x) * torch.floor(torch.abs(x) + 0.5) / scale    # HALF_UP like Spark
-    return PrimColumn("double", r, a.valid)
+    if is_decimal(a.dtype):
+        return D.round_column(a, digits, half_even)
+    if a.dtype in ("int", "long", "short", "byte"):
+        if digits >= 0:
+            return a
+        m = 10 ** (-digits)
+        x = a.data.to(torch.int64)
+        q, r = torch.div(x.abs(), m, rounding_mode="floor"), x.abs() % m
+        up = (2 * r > m) | ((2 * r == m) & (~torch.tensor(half_even, device=x.device) | (q % 2 == 1)))
+        res = torch.sign(x) * (q + up.to(torch.int64)) * m
+        return PrimColumn(a.dtype, res.to(a.data.dtype), a.valid)
+    x = a.data.to(torch.float64)
+    ax = x.abs()
+    if digits >= 0:
+        sc = 10.0 ** digits
+        f = torch.floor(ax * sc)
+        t = (2 * f + 1) / (2 * sc)
+    else:
+        sc = 10.0 ** (-digits)
+        f = torch.floor(ax / sc)
+        t = (2 * f + 1) * sc / 2
+    tie_up = (torch.remainder(f, 2) == 1) if half_even else torch.ones_like(ax, dtype=torch.bool)
+    r = f + ((ax > t) | ((ax == t) & tie_up)).to(torch.float64)
+    res = torch.sign(x) * (r / sc if digits >= 0 else r * sc)
+    res = torch.where(torch.isfinite(x), res, x)                  # NaN / ±Infinity pass through
+    rt = "float" if a.dtype == "float" else "double"
+    if rt == "float":
+        res = res.to(a.data.dtype)
+    return PrimColumn(rt, res, a.valid)
 
 
 def _f_ts_part(part):

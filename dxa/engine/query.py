@@ -734,11 +734,13 @@ def _gather_scope(scope: Scope) -> Scope:
 def _join_key_type(a, b):
     """Type both sides of an equi-join key are compared in.  Spark 2.4's PromoteStrings casts a string compared with
     a numeric / boolean value to the other side's type (so ``3 = '003'`` holds); otherwise the widest common type."""
+    from .decimal import is_decimal
     if a != b:
-        if a == "string" and b in ("long", "int", "double", "boolean", "decimal"):
-            return "double" if b == "decimal" else b
-        if b == "string" and a in ("long", "int", "double", "boolean", "decimal"):
-            return "double" if a == "decimal" else a
+        # string vs decimal: double (findCommonTypeForBinaryComparison, SPARK-22469)
+        if a == "string" and (b in ("long", "int", "double", "boolean") or is_decimal(b)):
+            return "double" if is_decimal(b) else b
+        if b == "string" and (a in ("long", "int", "double", "boolean") or is_decimal(a)):
+            return "double" if is_decimal(a) else a
     return common_type(a, b)
 
 
@@ -1589,12 +1591,16 @@ def _percentile(groups: G.Groups, arg, p, exact: bool):
         raise QueryError("percentile must be in [0, 1]")
     if not isinstance(arg, PrimColumn):
         arg = cast_column(arg, "double")
-    x = arg.data.to(torch.float64)
+    from .decimal import is_decimal, to_double
+    dec = is_decimal(arg.dtype)
+    # decimals: the exact percentile interpolates their double values (Spark's Percentile result is a double); the
+    # approximate one returns an input VALUE, so it keeps the decimal type (ApproximatePercentile's dataType)
+    x = to_double(arg).data if dec else arg.data.to(torch.float64)
     ok = arg.valid_mask()
     idx = torch.nonzero(ok).flatten()
     g = groups.gid.to(torch.int64)[idx]
     v = x[idx]
-    o = torch.argsort(v, stable=True)
+    o = torch.argsort(arg.data[idx] if (dec and arg.dtype.narrow) else v, stable=True)
     o = o[torch.argsort(g[o], stable=True)]
     g, v = g[o], v[o]
     cnt = torch.bincount(g, minlength=ng)
@@ -1613,11 +1619,15 @@ def _percentile(groups: G.Groups, arg, p, exact: bool):
         return PrimColumn("double", r, has)
     k = torch.clamp(torch.ceil(q * cnt.to(torch.float64)).to(torch.int64) - 1, min=0)
     k = torch.minimum(k, c1)
+    if dec:
+        at = idx[o][torch.clamp(start + k, max=max(0, v.numel() - 1))] if v.numel() else \
+            torch.zeros(ng, dtype=torch.int64, device=dev)
+        return _take_nullable(arg, torch.where(has, at, torch.full_like(at, -1)))
     r = v[torch.clamp(start + k, max=max(0, v.numel() - 1))] if v.numel() else torch.zeros(ng, dtype=torch.float64,
                                                                                           device=dev)
     if arg.dtype in ("int", "long"):
         return PrimColumn(arg.dtype, r.to(torch.int64), has)
-    return PrimColumn(arg.dtype if arg.dtype in ("double", "float", "decimal") else "double", r, has)
+    return PrimColumn(arg.dtype if arg.dtype in ("double", "float") else "double", r, has)
 
 
 def _collect(groups: G.Groups, arg, as_set):

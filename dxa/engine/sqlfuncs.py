@@ -736,8 +736,8 @@ def _hash_bytes(b: bytes, seed):
 def spark_hash_value(v, dtype, seed):
     """One argument of Spark's hash() (Murmur3Hash, HashExpression): int/date/boolean → hashInt, long/timestamp →
     hashLong, float → hashInt(floatToIntBits), double → hashLong(doubleToLongBits) (-0.0 as 0.0, NaN canonical),
-    decimal → hashLong(unscaled) for ≤ 18 digits else the unscaled BigInteger's two's-complement bytes.  Decimal
-    precision/scale are not tracked by this engine: the scale is the value's shortest exact decimal form."""
+    decimal(p, s) → hashLong(unscaled) for p ≤ 18 else the unscaled BigInteger's two's-complement bytes (the
+    column's precision decides, not the value's)."""
     import math
     import struct
     if v is None:
@@ -754,17 +754,29 @@ def spark_hash_value(v, dtype, seed):
         d = 0.0 if v == 0 else float(v)                                   # -0.0 hashes as 0.0
         bits = 0x7FF8000000000000 if math.isnan(d) else struct.unpack("<Q", struct.pack("<d", d))[0]
         return _hash_long(bits, seed)
-    if dtype == "decimal":
-        from decimal import Decimal
-        sign, digits, exp = Decimal(repr(float(v))).normalize().as_tuple()
-        unscaled = int("".join(map(str, digits)) or "0") * (10 ** exp if exp > 0 else 1) * (-1 if sign else 1)
-        if abs(unscaled) < 10 ** 18:
+    from .decimal import is_decimal
+    if is_decimal(dtype):
+        # the column's unscaled integer: storage int (narrow), [lo, hi] words (wide), or a Python Decimal (literals)
+        if isinstance(v, list):
+            lo, hi = int(v[0]), int(v[1])
+            unscaled = (hi << 64) | (lo & ((1 << 64) - 1))
+        elif isinstance(v, int):
+            unscaled = v
+        else:
+            from decimal import Decimal
+            unscaled = int(Decimal(str(v)).scaleb(dtype.scale))
+        if dtype.precision <= 18:                                   # DecimalType.MAX_LONG_DIGITS
             return _hash_long(unscaled, seed)
-        nbytes = (unscaled.bit_length() + 8) // 8
+        nbytes = (unscaled.bit_length() + 8) // 8                  # BigInteger.toByteArray: minimal two's complement
         return _hash_bytes(unscaled.to_bytes(nbytes, "big", signed=True), seed)
     if isinstance(v, (dict, list)):
         v = json.dumps(v, separators=(",", ":"))
     return _hash_bytes(str(v).encode("utf-8"), seed)
+
+
+def _is_dec(t):
+    from .decimal import is_decimal
+    return is_decimal(t)
 
 
 _HASH_KIND = {"int": 0, "date": 0, "long": 1, "timestamp": 1, "double": 2, "float": 3, "boolean": 4}
@@ -782,6 +794,8 @@ def _hash_device(args, n, dev):
             cols.append(("s", a))
         elif isinstance(a, PrimColumn) and str(a.dtype) in _HASH_KIND:
             cols.append(("p", a))
+        elif isinstance(a, PrimColumn) and _is_dec(a.dtype) and a.dtype.narrow:
+            cols.append(("p", PrimColumn("long", a.data, a.valid)))    # hashLong(unscaled): the storage word
         else:
             return None
     h = torch.full((n,), 42, dtype=torch.int32, device=dev)
@@ -810,11 +824,12 @@ def _f_hash(e, scope, ctx, subst):
     cols = []
     for a in args:
         if isinstance(a, ConstColumn):
-            cols.append(([a.value] * n, str(a.dtype)))
+            cols.append(([a.value] * n, a.dtype if _is_dec(a.dtype) else str(a.dtype)))
         elif isinstance(a, PrimColumn):
             vals = a.data.cpu().tolist()
             ok = a.valid.cpu().tolist() if a.valid is not None else None
-            cols.append(([v if (ok is None or ok[i]) else None for i, v in enumerate(vals)], str(a.dtype)))
+            cols.append(([v if (ok is None or ok[i]) else None for i, v in enumerate(vals)],
+                         a.dtype if _is_dec(a.dtype) else str(a.dtype)))
         else:
             cols.append((a.to_pylist(), str(a.dtype)))
     out = []

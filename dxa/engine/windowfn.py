@@ -8,8 +8,9 @@ every statement to ``spark.sql``); here each window call is evaluated column-at-
 2. in sorted order, partition / peer boundaries become flag vectors and ``cummax``/``cummin`` scans give every row its
    partition start/end and peer-group start/end — no per-partition loops;
 3. ranking functions are arithmetic on those positions; ``lag``/``lead``/``first_value``/``last_value``/
-   ``nth_value`` are gathers; aggregates over a frame ``[a, b]`` use prefix sums (count/sum/avg) and a sparse table
-   (min/max, O(n log n) build, O(1) query), so running, sliding and whole-partition frames cost the same;
+   ``nth_value`` are gathers; aggregates over a frame ``[a, b]`` use prefix sums for counts and integer / decimal
+   sums (exact: int64 and 32-bit decimal limbs), power-of-two block sums for double sums (no prefix differences,
+   which cancel catastrophically) and a sparse table for min/max (O(n log n) build, O(1) query);
 4. the result is scattered back to input row order.
 
 Distributed scopes are re-partitioned by the PARTITION BY keys (RCCL all-to-all) before evaluation, or gathered when
@@ -314,13 +315,23 @@ def _compute(name, wc, ev, perm, idx, pstart, pend, peer_new, peer_start, peer_e
     if name == "count":
         return PrimColumn("long", cnt)
     has = cnt > 0
+    from .decimal import is_decimal
+    if is_decimal(x.dtype):
+        return _decimal_frame_agg(name, x, valid, a, b, nonempty, cnt, has, n, dev)
     data = x.data
     if data.dtype == torch.bool:
         data = data.to(torch.int64)
     if name in ("sum", "avg"):
         integral = x.dtype in _INT_TYPES and not data.is_floating_point()
-        acc = data.to(torch.int64 if integral else torch.float64)
-        s = frame_sum(torch.cumsum(torch.where(valid, acc, torch.zeros_like(acc)), 0))
+        if integral:
+            # int64 prefix differences are exact (two's complement wraps, as Spark's long sum does)
+            s = frame_sum(torch.cumsum(torch.where(valid, data.to(torch.int64), torch.zeros_like(data,
+                                                                                                dtype=torch.int64)),
+                                       0))
+        else:
+            s = _float_frame_sum(torch.where(valid, data.to(torch.float64), torch.zeros_like(data,
+                                                                                              dtype=torch.float64)),
+                                 a, b, nonempty)
         if name == "sum":
             return PrimColumn("long" if integral else "double", s, has)
         return PrimColumn("double", s.to(torch.float64) / cnt.clamp(min=1).to(torch.float64), has)
@@ -332,3 +343,108 @@ def _compute(name, wc, ev, perm, idx, pstart, pend, peer_new, peer_start, peer_e
         fill = info.min if is_max else info.max
     masked = torch.where(valid, data, torch.full_like(data, fill))
     return PrimColumn(x.dtype, _minmax_frame(masked, a, b, is_max), has)
+
+
+def _float_frame_sum(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, nonempty: torch.Tensor) -> torch.Tensor:
+    """Σ x[a[i] .. b[i]] for doubles WITHOUT prefix-sum differences (those cancel catastrophically: a 2-row frame
+    over values of 1.6e12 inherits the rounding of a prefix of 3e17).  Every frame is cut into aligned power-of-two
+    blocks by the bits of its length, lowest bit first: level k holds the sums of the 2^k-row runs starting at every
+    row (one add of level k-1 per level), so a frame sum adds at most log2(len) block sums — each the sum of values
+    inside the frame only, and exact Spark order for frames of one or two rows.  Memory stays O(n): one level at a
+    time."""
+    n = x.shape[0]
+    length = torch.where(nonempty, b - a + 1, torch.zeros_like(a))
+    acc = torch.zeros_like(x)
+    if n == 0:
+        return acc
+    maxlen = int(length.max())                                     # one host read (the level count)
+    pos = a.clamp(0, n - 1)
+    level = x
+    k = 0
+    while (1 << k) <= maxlen:
+        take = ((length >> k) & 1).to(torch.bool)
+        acc = acc + torch.where(take, level[pos], torch.zeros_like(acc))
+        pos = torch.where(take, (pos + (1 << k)).clamp(max=n - 1), pos)
+        step = 1 << k
+        if (step << 1) <= maxlen:
+            nxt = level.clone()
+            nxt[: n - step] = level[: n - step] + level[step:]
+            level = nxt
+        k += 1
+    return acc
+
+
+def _decimal_frame_agg(name, x, valid, a, b, nonempty, cnt, has, n, dev):
+    """Framed SUM / AVG / MIN / MAX over decimal(p, s) with Spark's result types: SUM → decimal(p+10, s), AVG →
+    decimal(p+4, s+4) rounded HALF_UP, MIN / MAX → the input type.  Sums are exact: the unscaled 128-bit values are
+    split into 32-bit limbs whose int64 prefix sums cannot overflow below 2^31 rows, so frame differences of those
+    prefixes are exact; the limbs are then carried back together (as ``decimal.group_sum`` does per group)."""
+    from . import decimal as D
+    t = x.dtype
+    h, l = D.lanes(x.data)
+    if name in ("min", "max"):
+        is_max = name == "max"
+        if t.narrow:
+            info = torch.iinfo(torch.int64)
+            fill = info.min if is_max else info.max
+            masked = torch.where(valid, x.data, torch.full_like(x.data, fill))
+            return PrimColumn(t, _minmax_frame(masked, a, b, is_max), has)
+        at = _argbest_frame(h, l ^ D.SIGN, valid, a, b, is_max)
+        return PrimColumn(t, x.data[at], has)
+    z = torch.zeros_like(l)
+    h = torch.where(valid, h, z)
+    l = torch.where(valid, l, z)
+    parts = D._limbs(h, l)[:3] + [h >> 32]                   # three unsigned limbs + the signed top limb
+    zero = torch.zeros(1, dtype=torch.int64, device=dev)
+    sums = []
+    for p in parts:
+        pz = torch.cat([zero, torch.cumsum(p, 0)])
+        d = pz[(b + 1).clamp(0, n)] - pz[a.clamp(0, n)]
+        sums.append(torch.where(nonempty, d, torch.zeros_like(d)))
+    c = torch.zeros_like(sums[0])
+    out = []
+    for k in range(3):
+        v = sums[k] + c
+        out.append(v & D.MASK32)
+        c = v >> 32
+    hi = (out[2] & D.MASK32) | ((sums[3] + c) << 32)
+    lo = (out[0] & D.MASK32) | ((out[1] & D.MASK32) << 32)
+    if name == "sum":
+        ts = D.result_sum(t)
+        return D.column(ts, hi, lo, has & D.fits(hi, lo, ts.precision))
+    ta = D.result_avg(t)
+    hh, ll, ovf = D.mul_pow10(hi, lo, ta.scale - t.scale)
+    hh, ll = D.div_u_vec_half_up(hh, ll, cnt.clamp(min=1))
+    return D.column(ta, hh, ll, has & ~ovf & D.fits(hh, ll, ta.precision))
+
+
+def _argbest_frame(kh: torch.Tensor, kl: torch.Tensor, valid, a, b, is_max: bool) -> torch.Tensor:
+    """Row index of the max / min (kh, kl) key (lexicographic, signed) inside every frame: a sparse table of
+    row indices (wide decimals, whose order key is two words)."""
+    n = kh.shape[0]
+    big = torch.iinfo(torch.int64)
+    fill = big.min if is_max else big.max
+    kh = torch.where(valid, kh, torch.full_like(kh, fill))
+    kl = torch.where(valid, kl, torch.full_like(kl, fill))
+
+    def better(i, j):                               # index of the better of rows i, j (ties: the earlier)
+        gt = (kh[j] > kh[i]) | ((kh[j] == kh[i]) & (kl[j] > kl[i]))
+        lt = (kh[j] < kh[i]) | ((kh[j] == kh[i]) & (kl[j] < kl[i]))
+        return torch.where(gt if is_max else lt, j, i)
+    idx = torch.arange(n, device=kh.device)
+    levels = [idx]
+    k = 1
+    while 2 * k <= n:
+        prev = levels[-1]
+        nxt = prev.clone()
+        nxt[: n - k] = better(prev[: n - k], prev[k:])
+        levels.append(nxt)
+        k *= 2
+    table = torch.stack(levels)
+    length = (b - a + 1).clamp(min=1)
+    lvl = torch.floor(torch.log2(length.to(torch.float64))).to(torch.int64).clamp(max=len(levels) - 1)
+    lvl = torch.where((1 << lvl) > length, lvl - 1, lvl)
+    span = 1 << lvl
+    ai = a.clamp(0, n - 1)
+    bi = (b - span + 1).clamp(0, n - 1)
+    return better(table[lvl, ai], table[lvl, bi])

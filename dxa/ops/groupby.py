@@ -236,20 +236,33 @@ def aggregate(groups: Groups, col, func: str, n: int):
         s = _agg_raw(groups, data.to(torch.float64) if data.dtype != torch.float64 else data, valid, "sum", n, device)
         c = cnt if cnt is not None else _agg_raw(groups, None, None, "count", n, device)
         return PrimColumn("double", s / c.clamp(min=1).to(torch.float64), c > 0)
-    if func in ("stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std"):
-        x = data.to(torch.float64)
-        s = _agg_raw(groups, x, valid, "sum", n, device)
-        s2 = _agg_raw(groups, x * x, valid, "sum", n, device)
+    if func == "m2":
+        # Σ (x − mean)² per group: the partial state of the variance family (Chan merge in engine/distagg.py)
         c = (cnt if cnt is not None else _agg_raw(groups, None, None, "count", n, device)).to(torch.float64)
-        mean = s / c.clamp(min=1)
-        m2 = (s2 - c * mean * mean).clamp(min=0)
+        return PrimColumn("double", _central_m2(groups, data.to(torch.float64), valid, c, n, device),
+                          None if cnt is None else cnt > 0)
+    if func in ("stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop", "std"):
+        c = (cnt if cnt is not None else _agg_raw(groups, None, None, "count", n, device)).to(torch.float64)
+        m2 = _central_m2(groups, data.to(torch.float64), valid, c, n, device)
         pop = func.endswith("_pop")
         denom = c if pop else (c - 1)
         var = m2 / denom.clamp(min=1)
         out = var.sqrt() if func.startswith("std") else var
-        ok = c > (0 if pop else 1)
-        return PrimColumn("double", out, ok)
+        if not pop:            # Spark 2.4: the sample statistics of ONE row are NaN (null only for no rows)
+            out = torch.where(c == 1, torch.full_like(out, float("nan")), out)
+        return PrimColumn("double", out, c > 0)
     raise ValueError(f"unsupported aggregate {func}")
+
+
+def _central_m2(groups, x, valid, c, n, device):
+    """Σ (x − mean_g)² per group in two passes (group means, then centred squares): no Σx² − n·mean² cancellation —
+    the values 1e9 + {1, 2, 3} have variance 1, which the one-pass form loses entirely.  Spark's CentralMomentAgg
+    keeps (n, mean, M2) per partition for the same reason."""
+    s = _agg_raw(groups, x, valid, "sum", n, device)
+    mean = s / c.clamp(min=1)
+    gid = groups.gid.to(torch.int64)
+    d = x - mean[gid]
+    return _agg_raw(groups, d * d, valid, "sum", n, device)
 
 
 def _host_minmax(groups, col, func, device):
