@@ -129,9 +129,14 @@ def _plan_take(c: "Column", idx: torch.Tensor, leaves: List[torch.Tensor]):
         if c.valid is not None:
             leaves.append(c.valid)
         has_v = c.valid is not None
+        ip = len(leaves)
+        if c.present is not None:
+            leaves.append(c.present)
+        has_p = c.present is not None
         els = [_plan_take(e, idx, leaves) for e in c.elements]
         n = int(idx.shape[0])
-        return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device)
+        return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device,
+                                     present=g[ip] if has_p else None)
     taken = c.take(idx)                       # constants and other kinds: their own take
     return lambda g: taken
 
@@ -371,11 +376,17 @@ class StructColumn(Column):
 
 
 class ArrayColumn(Column):
-    def __init__(self, elements: List[Column], length: int, valid=None, drop_nulls=False, device=None):
+    """K element slots per row.  A row's array is its PRESENT slots, left to right: every slot, unless
+    ``drop_nulls`` (null slots are absent) or a ``present`` mask [rows × K] says otherwise — arrays of different
+    lengths in one column (``IF(c, array(1), array(2, 3))``, unions) keep their own lengths that way."""
+
+    def __init__(self, elements: List[Column], length: int, valid=None, drop_nulls=False, device=None,
+                 present: Optional[torch.Tensor] = None):
         self.elements = list(elements)
         self.length = int(length)
         self.valid = valid
         self.drop_nulls = drop_nulls
+        self.present = present
         self._device = torch.device(device) if device is not None else (
             elements[0].device if elements else torch.device("cpu"))
         et = elements[0].dtype if elements else "null"
@@ -385,26 +396,54 @@ class ArrayColumn(Column):
     def device(self):
         return self._device
 
+    def canonical(self) -> Optional["ArrayColumn"]:
+        """The same arrays without a ``present`` mask: absent slots become null slots of a ``drop_nulls`` array —
+        exact unless a present slot holds a real null element (then None: the caller renders on the host)."""
+        if self.present is None:
+            return self
+        els = []
+        for j, e in enumerate(self.elements):
+            e = materialize(e)
+            p = self.present[:, j]
+            if not self.drop_nulls and bool((p & ~e.valid_mask()).any()):
+                return None
+            els.append(e.with_valid(p))
+        return ArrayColumn(els, self.length, self.valid, True, self._device)
+
+    def slot_present(self, j: int) -> Optional[torch.Tensor]:
+        """Presence of slot j per row from the ``present`` mask (None: every row has it)."""
+        return None if self.present is None else self.present[:, j]
+
     def take(self, idx):
         if idx.device.type == "cuda":
             return take_columns([self], idx)[0]
         return ArrayColumn([e.take(idx) for e in self.elements], int(idx.shape[0]), _take_valid(self.valid, idx),
-                           self.drop_nulls, self._device)
+                           self.drop_nulls, self._device,
+                           present=None if self.present is None else self.present[idx])
 
     def with_valid(self, extra):
-        return ArrayColumn(self.elements, self.length, and_valid(self.valid, extra), self.drop_nulls, self._device)
+        return ArrayColumn(self.elements, self.length, and_valid(self.valid, extra), self.drop_nulls, self._device,
+                           present=self.present)
 
     def to(self, device):
         return ArrayColumn([e.to(device) for e in self.elements], self.length,
-                           None if self.valid is None else self.valid.to(device), self.drop_nulls, device)
+                           None if self.valid is None else self.valid.to(device), self.drop_nulls, device,
+                           present=None if self.present is None else self.present.to(device))
 
     def to_pylist(self):
         els = [e.to_pylist() for e in self.elements]
         valid = self.valid.cpu().tolist() if self.valid is not None else [True] * self.length
+        pres = self.present.cpu().tolist() if self.present is not None else None
         out = []
         for i in range(self.length):
             if not valid[i]:
                 out.append(None)
+                continue
+            if pres is not None:
+                row = [col[i] for j, col in enumerate(els) if pres[i][j]]
+                if self.drop_nulls:
+                    row = [v for v in row if v is not None]
+                out.append(row)
                 continue
             row = [col[i] for col in els]
             if self.drop_nulls:
@@ -489,6 +528,17 @@ def materialize(col: Column) -> Column:
     return col.materialize() if isinstance(col, ConstColumn) else col
 
 
+def _null_like(col, n: int):
+    """An all-null column shaped like array / struct column ``col`` (same element / field layout)."""
+    dev = col.device
+    none = torch.zeros(n, dtype=torch.bool, device=dev)
+    if isinstance(col, ArrayColumn):
+        return ArrayColumn([], n, none, col.drop_nulls, dev, present=torch.zeros((n, 0), dtype=torch.bool,
+                                                                                     device=dev))
+    return StructColumn(col.names, [ConstColumn(None, c.dtype, n, dev) for c in col.children], n, none, col.is_map,
+                        col.dtype, dev)
+
+
 def concat_columns(cols: List[Column]) -> Column:
     """Row-wise concatenation (UNION ALL, window unions).  Types must already agree."""
     cols = [c for c in cols]
@@ -498,6 +548,12 @@ def concat_columns(cols: List[Column]) -> Column:
     device = cols[0].device
     if all(isinstance(c, ConstColumn) for c in cols) and len({(repr(c.value), str(c.dtype)) for c in cols}) == 1:
         return ConstColumn(cols[0].value, cols[0].dtype, n, device)
+    shaped = next((c for c in cols if isinstance(c, (ArrayColumn, StructColumn))), None)
+    if shaped is not None:
+        # a NULL literal next to arrays / structs (IF(c, array(1), NULL), a CASE's missing ELSE): an all-null
+        # column of the same shape, not a JSON text column
+        cols = [_null_like(shaped, c.length) if (isinstance(c, ConstColumn) and c.value is None) else c
+                for c in cols]
     cols = [materialize(c) for c in cols]
     any_null = any(c.valid is not None for c in cols)
     valid = torch.cat([c.valid_mask() for c in cols]) if any_null else None
@@ -524,6 +580,7 @@ def concat_columns(cols: List[Column]) -> Column:
         return StructColumn(names, children, n, valid, first.is_map, first.dtype, device)
     if isinstance(first, ArrayColumn):
         k = max(len(c.elements) for c in cols)
+        et = next((c.elements[0].dtype for c in cols if c.elements), "null")
         elements = []
         for j in range(k):
             parts = []
@@ -531,9 +588,21 @@ def concat_columns(cols: List[Column]) -> Column:
                 if j < len(c.elements):
                     parts.append(c.elements[j])
                 else:
-                    parts.append(ConstColumn(None, first.elements[0].dtype, c.length, device))
+                    parts.append(ConstColumn(None, et, c.length, device))
             elements.append(concat_columns(parts))
-        return ArrayColumn(elements, n, valid, first.drop_nulls, device)
+        present = None
+        if any(len(c.elements) != k or c.present is not None for c in cols):
+            # a shorter array's missing slots are absent, not null elements
+            pm = []
+            for c in cols:
+                p = torch.zeros((c.length, k), dtype=torch.bool, device=device)
+                if c.present is not None:
+                    p[:, :len(c.elements)] = c.present
+                else:
+                    p[:, :len(c.elements)] = True
+                pm.append(p)
+            present = torch.cat(pm)
+        return ArrayColumn(elements, n, valid, first.drop_nulls, device, present=present)
     raise TypeError(f"cannot concat {type(first)}")
 
 

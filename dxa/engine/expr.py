@@ -1286,6 +1286,10 @@ def _slot_present(arr: "ArrayColumn", el) -> torch.Tensor:
     """Element slot is part of the array (a dropped-null slot is not)."""
     n = arr.length
     base = arr.valid_mask() if arr.valid is not None else torch.ones(n, dtype=torch.bool, device=arr.device)
+    if arr.present is not None:
+        j = next((j for j, x in enumerate(arr.elements) if x is el), None)
+        if j is not None:
+            base = base & arr.present[:, j]
     if arr.drop_nulls:
         if isinstance(el, ConstColumn):
             return base & (el.value is not None)
@@ -1429,16 +1433,19 @@ def _f_filternull(e, scope, ctx, subst):
 
 
 def _f_size(e, scope, ctx, subst):
+    """size / cardinality: the number of present slots; Spark 2.4 (spark.sql.legacy.sizeOfNull) gives -1 for a NULL
+    array or map."""
     n, dev = scope.length, scope.device
     (a,) = _args(e, scope, ctx, subst)
     if isinstance(a, ArrayColumn):
-        if a.drop_nulls:
-            cnt = torch.zeros(n, dtype=torch.int64, device=dev)
-            for el in a.elements:
-                cnt += as_prim(el).valid_mask().to(torch.int64) if not isinstance(el, ConstColumn) else (
-                    0 if el.value is None else 1)
-            return PrimColumn("int", cnt, a.valid)
-        return PrimColumn("int", torch.full((n,), len(a.elements), dtype=torch.int64, device=dev), a.valid)
+        cnt = torch.zeros(n, dtype=torch.int64, device=dev)
+        ones = torch.ones(n, dtype=torch.bool, device=dev)
+        for el in a.elements:
+            p = _slot_present(ArrayColumn(a.elements, n, None, a.drop_nulls, dev, present=a.present), el)
+            cnt += (p if isinstance(p, torch.Tensor) else ones & bool(p)).to(torch.int64)
+        if a.valid is not None:
+            cnt = torch.where(a.valid, cnt, torch.full_like(cnt, -1))
+        return PrimColumn("int", cnt)
     vals = a.to_pylist()
     return column_from_pylist([-1 if v is None else len(v) for v in vals], "int", dev)
 
@@ -1815,8 +1822,67 @@ def register_function(name: str, fn: Callable):
     _FUNCS[name.lower()] = fn
 
 
+_SQL_TYPE = {"long": "BIGINT", "bigint": "BIGINT", "int": "INT", "integer": "INT", "short": "SMALLINT",
+             "smallint": "SMALLINT", "byte": "TINYINT", "tinyint": "TINYINT", "string": "STRING",
+             "double": "DOUBLE", "float": "FLOAT", "boolean": "BOOLEAN", "timestamp": "TIMESTAMP", "date": "DATE",
+             "binary": "BINARY"}
+# functions whose Spark expression prints under another name (FunctionRegistry aliases → the class's prettyName)
+_PRETTY_FN = {"ucase": "upper", "lcase": "lower", "substr": "substring", "mean": "avg", "std": "stddev_samp",
+              "stddev": "stddev_samp", "variance": "var_samp", "char_length": "length", "character_length": "length",
+              "power": "pow", "ceiling": "ceil", "approx_percentile": "percentile_approx", "first_value": "first",
+              "last_value": "last", "some": "bool_or", "any": "bool_or", "every": "bool_and", "sign": "signum",
+              "random": "rand", "day": "dayofmonth", "now": "current_timestamp"}
+_RANKING_FNS = {"row_number", "rank", "dense_rank", "percent_rank", "cume_dist", "ntile"}
+
+
+def _type_sql(t) -> str:
+    if is_decimal(t):
+        return f"DECIMAL({t.precision},{t.scale})"
+    return _SQL_TYPE.get(str(t).lower(), str(t).upper())
+
+
+def _frame_bound_sql(b) -> str:
+    kind, k = b
+    return {"unbounded_preceding": "UNBOUNDED PRECEDING", "unbounded_following": "UNBOUNDED FOLLOWING",
+            "current": "CURRENT ROW"}.get(kind) or f"{k} {'PRECEDING' if kind == 'preceding' else 'FOLLOWING'}"
+
+
+def _window_sql(w: A.WindowCall) -> str:
+    """Spark's WindowSpecDefinition.sql after ResolveWindowFrame: PARTITION BY, ORDER BY with explicit direction and
+    null order, and the resolved frame (ranking / offset functions have their own ROWS frame)."""
+    parts = []
+    if w.partition:
+        parts.append("PARTITION BY " + ", ".join(output_name(p) for p in w.partition))
+    if w.order:
+        items = []
+        for o in w.order:
+            nf = o.nulls_first if o.nulls_first is not None else o.ascending
+            items.append(f"{output_name(o.expr)} {'ASC' if o.ascending else 'DESC'} "
+                         f"NULLS {'FIRST' if nf else 'LAST'}")
+        parts.append("ORDER BY " + ", ".join(items))
+    name = w.func.name
+    if name in _RANKING_FNS:
+        parts.append("ROWS BETWEEN UNBOUNDED PRECEDING AND CURRENT ROW")
+    elif name in ("lag", "lead"):
+        k = output_name(w.func.args[1]) if len(w.func.args) > 1 else "1"
+        k = f"-{k}" if name == "lag" else k
+        bound = f"{k} {'PRECEDING' if name == 'lag' else 'FOLLOWING'}"
+        parts.append(f"ROWS BETWEEN {bound} AND {bound}")
+    elif w.frame is not None:
+        kind, lo, hi = w.frame
+        parts.append(f"{kind.upper()} BETWEEN {_frame_bound_sql(lo)} AND {_frame_bound_sql(hi)}")
+    elif w.order:
+        parts.append("RANGE BETWEEN UNBOUNDED PRECEDING AND CURRENT ROW")
+    else:
+        parts.append("ROWS BETWEEN UNBOUNDED PRECEDING AND UNBOUNDED FOLLOWING")
+    return "(" + " ".join(parts) + ")"
+
+
 def output_name(e: A.Expr) -> str:
-    """Spark-like auto-generated column name for an un-aliased select expression."""
+    """Spark 2.4's auto-generated name of an un-aliased select expression: ``toPrettySQL`` — the expression's
+    ``sql`` with literals and attributes printed bare (``usePrettyExpression``).  LIKE / RLIKE print infix, BETWEEN
+    is the conjunction the parser builds, CASE / IS NULL / NOT / unary minus use their ``sql`` forms, window calls
+    carry their resolved frame, aliased functions their canonical names."""
     if isinstance(e, A.Ident):
         return e.parts[-1]
     if isinstance(e, A.Literal):
@@ -1824,18 +1890,60 @@ def output_name(e: A.Expr) -> str:
             return "NULL"
         if isinstance(e.value, bool):
             return "true" if e.value else "false"
+        if e.type == "date":
+            return f"DATE '{e.value}'"
+        if e.type == "timestamp":
+            return f"TIMESTAMP('{e.value}')"
+        if isinstance(e.value, float):
+            return F.java_double_str(e.value)
         return str(e.value)
+    if isinstance(e, A.WindowCall):
+        return f"{output_name(e.func)} OVER {_window_sql(e)}"
     if isinstance(e, A.Call):
+        name = _PRETTY_FN.get(e.name, e.name)
         if e.star:
-            return f"{e.name}(1)" if e.name == "count" else f"{e.name}(*)"
+            return f"{name}(1)" if e.name == "count" else f"{name}(*)"
         inner = ", ".join(output_name(a) for a in e.args)
-        return f"{e.name}({'DISTINCT ' if e.distinct else ''}{inner})"
+        return f"{name}({'DISTINCT ' if e.distinct else ''}{inner})"
     if isinstance(e, A.Cast):
-        return f"CAST({output_name(e.operand)} AS {e.to.upper()})"
+        return f"CAST({output_name(e.operand)} AS {_type_sql(e.to)})"
     if isinstance(e, A.BinOp):
-        return f"({output_name(e.left)} {e.op.upper() if e.op in ('and', 'or') else e.op} {output_name(e.right)})"
+        op = e.op.upper() if e.op in ("and", "or", "div") else e.op
+        op = "=" if op == "==" else ("NOT (" if False else op)
+        if e.op in ("!=", "<>"):
+            return f"(NOT ({output_name(e.left)} = {output_name(e.right)}))"
+        return f"({output_name(e.left)} {op} {output_name(e.right)})"
+    if isinstance(e, A.UnaryOp):
+        if e.op == "not":
+            return f"(NOT {output_name(e.operand)})"
+        if e.op == "~":
+            return f"~{output_name(e.operand)}"
+        return f"({e.op} {output_name(e.operand)})"
+    if isinstance(e, A.IsNull):
+        return f"({output_name(e.operand)} IS {'NOT ' if e.negated else ''}NULL)"
+    if isinstance(e, A.Like):
+        r = f"{output_name(e.operand)} {'RLIKE' if e.regex else 'LIKE'} {output_name(e.pattern)}"
+        return f"(NOT {r})" if e.negated else r
+    if isinstance(e, A.Between):
+        v = output_name(e.operand)
+        r = f"(({v} >= {output_name(e.low)}) AND ({v} <= {output_name(e.high)}))"
+        return f"(NOT {r})" if e.negated else r
+    if isinstance(e, A.InList):
+        r = f"({output_name(e.operand)} IN ({', '.join(output_name(x) for x in e.items)}))"
+        return f"(NOT {r})" if e.negated else r
+    if isinstance(e, A.Case):
+        whens = e.whens
+        if e.operand is not None:
+            op = output_name(e.operand)
+            cases = "".join(f" WHEN ({op} = {output_name(c)}) THEN {output_name(v)}" for c, v in whens)
+        else:
+            cases = "".join(f" WHEN {output_name(c)} THEN {output_name(v)}" for c, v in whens)
+        els = f" ELSE {output_name(e.default)}" if e.default is not None else ""
+        return f"CASE{cases}{els} END"
     if isinstance(e, A.Subscript):
         return output_name(e.index) if e.dot else f"{output_name(e.base)}[{output_name(e.index)}]"
+    if isinstance(e, A.SubqueryExpr):
+        return "scalarsubquery()" if e.kind == "scalar" else e.kind
     return type(e).__name__.lower()
 
 

@@ -820,10 +820,60 @@ def _collect_aggs(e: A.Expr, ctx, out: Dict):
         _collect_aggs(c, ctx, out)
 
 
+def _star_columns(st: A.Star, scope: Scope) -> List[Tuple[A.Expr, str]]:
+    """(expression, name) of every column a ``*`` / ``q.*`` stands for in ``scope``."""
+    out = []
+    if not st.qualifier:
+        for nm, q in zip(scope.names, scope.quals):
+            if isinstance(q, HiddenQual):
+                continue              # a USING join's per-side key copy: the merged key is listed instead
+            out.append((A.Ident(((q,) if q and _dup(scope, nm) else ()) + (nm,)), nm))
+        return out
+    q = st.qualifier
+    if len(q) == 1 and scope.has_qualifier(q[0]):
+        for nm, qq in zip(scope.names, scope.quals):
+            if (qq or "").lower() == q[0].lower():
+                out.append((A.Ident((qq, nm)), nm))
+        return out
+    col = scope.resolve(q)
+    if isinstance(col, StructColumn):
+        return [(A.Ident(q + (nm,)), nm) for nm in col.names]
+    raise QueryError(f"cannot expand {'.'.join(q)}.*")
+
+
+def _expand_call_stars(e: A.Expr, scope: Scope) -> A.Expr:
+    """``struct(*)``, ``to_json(struct(t.*))``, ``hash(*)``, ``concat_ws(',', *)``: a star argument of a function
+    (not COUNT(*)) stands for every column it names, in order (Spark's ResolveReferences expands
+    ``UnresolvedStar`` inside function arguments the same way)."""
+    def fn(node):
+        if not isinstance(node, A.Call):
+            return None
+        if not (node.star and node.name != "count") and not any(isinstance(a, A.Star) for a in node.args):
+            return None
+        args = []
+        if node.star and node.name != "count":
+            args += [x for x, _ in _star_columns(A.Star(()), scope)]
+        for a in node.args:
+            if isinstance(a, A.Star):
+                args += [x for x, _ in _star_columns(a, scope)]
+            else:
+                args.append(_expand_call_stars(a, scope))
+        return A.Call(node.name, args, distinct=node.distinct)
+    return A.replace(e, fn)
+
+
+def _has_call_star(e: A.Expr) -> bool:
+    return any(isinstance(x, A.Call) and ((x.star and x.name != "count") or any(isinstance(a, A.Star) for a in x.args))
+               for x in A.walk(e))
+
+
 def _expand_items(sel: A.Select, scope: Scope) -> List[Tuple[A.Expr, str]]:
     items = []
     for it in sel.items:
         e = it.expr
+        if not isinstance(e, A.Star) and _has_call_star(e):
+            items.append((_expand_call_stars(e, scope), it.alias or output_name(e)))
+            continue
         if isinstance(e, A.Star):
             if not e.qualifier:
                 for nm, q in zip(scope.names, scope.quals):

@@ -87,12 +87,13 @@ def _frag_values(col: Column) -> List[Optional[str]]:
     if isinstance(col, ArrayColumn):
         els = [_frag_values(e) for e in col.elements]
         valid = col.valid.cpu().tolist() if col.valid is not None else [True] * n
+        pres = col.present.cpu().tolist() if col.present is not None else None
         out = []
         for i in range(n):
             if not valid[i]:
                 out.append(None)
                 continue
-            parts = [e[i] for e in els]
+            parts = [e[i] for j, e in enumerate(els) if pres is None or pres[i][j]]
             if col.drop_nulls:
                 parts = [p for p in parts if p is not None]
             else:

@@ -493,6 +493,8 @@ def _f_array_contains(e, scope, ctx, subst):
     acc = torch.zeros(n, dtype=torch.bool, device=dev)
     for el in arr.elements:
         eq = _compare("=", el, v, n, dev)
+        if isinstance(eq, ConstColumn):          # a literal array against a literal value
+            eq = eq.materialize()
         acc = acc | (eq.data.bool() & eq.valid_mask() & _slot_present(arr, el))
     return bool_col(acc, arr.valid)
 

@@ -90,6 +90,7 @@ class _Builder:
         from ..engine.column import (ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn)
         from ..engine.serialize import _scalar_text
         from ..engine.decimal import is_decimal, to_text_column as decimal_text
+        col = _canon_array(col)
         idx = len(self.nodes)
         nd = {"kind": K_NULL, "nchildren": 0, "child0": 0, "drop_nulls": 0, "name": _quoted(name) if name else b"",
               "data": 0, "valid": 0, "arena": 0, "starts": 0, "lens": 0, "const": b""}
@@ -157,6 +158,20 @@ class _Builder:
         raise TypeError(f"cannot serialise {col!r}")
 
 
+def _canon_array(col):
+    """Arrays with a per-row ``present`` mask as the serializer's node kinds express them: a drop-nulls array, or —
+    when a present slot holds a real null — the rows rendered on the host as raw JSON text."""
+    from ..engine.column import ArrayColumn, JsonColumn, column_from_pylist
+    if not isinstance(col, ArrayColumn) or col.present is None:
+        return col
+    canon = col.canonical()
+    if canon is not None:
+        return canon
+    from ..engine.serialize import _frag_values
+    sc = column_from_pylist(_frag_values(col), "string", col.device)
+    return JsonColumn(sc.arena, sc.starts, sc.lens, sc.valid, "string")
+
+
 class DevNode(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("nchildren", ctypes.c_int32), ("child0", ctypes.c_int32),
                 ("drop_nulls", ctypes.c_int32), ("name_off", ctypes.c_int32), ("name_len", ctypes.c_int32),
@@ -196,6 +211,7 @@ class _DevBuilder:
         from ..engine.column import (ArrayColumn, ConstColumn, JsonColumn, PrimColumn, StrColumn, StructColumn)
         from ..engine.serialize import _scalar_text
         from ..engine.decimal import is_decimal, to_text_column as decimal_text
+        col = _canon_array(col)
         idx = len(self.nodes)
         nd = self._blank()
         if name:

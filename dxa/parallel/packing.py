@@ -41,6 +41,14 @@ class Leaf:
         self.str_type = None
 
 
+class _Presence:
+    """A slot-presence mask in the shape of a validity-only leaf."""
+    dtype = "boolean"
+
+    def __init__(self, mask):
+        self.valid = mask
+
+
 def flatten(col, leaves: List[Leaf], spec: list):
     """Walk a column tree; record data-bearing leaves and a rebuild spec."""
     from ..engine.column import ArrayColumn, ConstColumn, PrimColumn, StrColumn, StructColumn
@@ -60,10 +68,15 @@ def flatten(col, leaves: List[Leaf], spec: list):
     if isinstance(col, ArrayColumn):
         vleaf = len(leaves)
         leaves.append(Leaf("valid_only", "boolean", col))
+        # one presence leaf per slot, on every rank (a rank without a ``present`` mask sends all-ones)
+        pleaves = []
+        for j in range(len(col.elements)):
+            pleaves.append(len(leaves))
+            leaves.append(Leaf("valid_only", "boolean", _Presence(col.slot_present(j))))
         sub = []
         for c in col.elements:
             flatten(c, leaves, sub)
-        spec.append(("array", col.drop_nulls, vleaf, sub))
+        spec.append(("array", col.drop_nulls, vleaf, sub, pleaves))
         return
     if isinstance(col, StrColumn):
         spec.append(("str", len(leaves)))
@@ -106,9 +119,14 @@ def rebuild(spec_item, leaves_out, n, device):
         kids = [rebuild(s, leaves_out, n, device) for s in sub]
         return StructColumn(names, kids, n, leaves_out[vleaf] if vleaf is not None else None, is_map, dtype, device)
     if kind == "array":
-        _, drop, vleaf, sub = spec_item
+        _, drop, vleaf, sub, pleaves = spec_item
         els = [rebuild(s, leaves_out, n, device) for s in sub]
-        return ArrayColumn(els, n, leaves_out[vleaf] if vleaf is not None else None, drop, device)
+        pm = [leaves_out.get(p) for p in pleaves]
+        present = None
+        if any(p is not None for p in pm):
+            ones = torch.ones(n, dtype=torch.bool, device=device)
+            present = torch.stack([ones if p is None else p for p in pm], 1)
+        return ArrayColumn(els, n, leaves_out[vleaf] if vleaf is not None else None, drop, device, present=present)
     raise ValueError(kind)
 
 

@@ -907,11 +907,28 @@ class Parser:
                 return A.Call("overlay", args)
             self.i = save
         distinct = self.accept_kw("distinct")
-        args = [self.parse_expr()]
+        args = [self._parse_call_arg()]
         while self.accept_op(","):
-            args.append(self.parse_expr())
+            args.append(self._parse_call_arg())
         self.expect_op(")")
         return self._maybe_over(A.Call(low, args, distinct=distinct))
+
+    def _parse_call_arg(self):
+        """A function argument; ``*`` and ``q.*`` (e.g. ``struct(*)``, ``to_json(struct(t.*))``) become Star nodes
+        that the select list expands to the columns they name."""
+        if self.is_op("*") and (self.is_op(",", tok=self.peek()) or self.is_op(")", tok=self.peek())):
+            self.advance()
+            return A.Star(())
+        save = self.i
+        quals = []
+        while self.cur.kind in ("id", "qid") and self.is_op(".", tok=self.peek()):
+            quals.append(self.advance().text)
+            self.advance()
+            if self.is_op("*"):
+                self.advance()
+                return A.Star(tuple(quals))
+        self.i = save
+        return self.parse_expr()
 
     def _at_query(self) -> bool:
         return self.is_kw("select") or (self.is_word("with") and self.peek().kind in ("id", "kw"))

@@ -33,6 +33,9 @@ QUERIES = [
     "SELECT a.k, a.v, b.v AS bv FROM T a LEFT JOIN T2 b ON a.k = b.k AND a.v > 5",
     "SELECT k, explode(split(s, 'b')) AS part FROM T WHERE s IS NOT NULL",
     "SELECT (SELECT MAX(v) FROM T) AS m, COUNT(*) AS c FROM T",
+    # the variance family's (n, mean, M2) partials merged with Chan's formula: with a 1e6 offset the one-pass
+    # Σx² − n·mean² form loses the 6th decimal
+    "SELECT k, STDDEV(v + 1e6) AS sd, VAR_POP(v - 1e6) AS vp FROM T GROUP BY k",
 ]
 
 
@@ -45,7 +48,8 @@ def _rows(seed, n):
 def _canon(rows):
     out = []
     for r in rows:
-        out.append(tuple((k, round(v, 6) if isinstance(v, float) else v) for k, v in sorted(r.items())))
+        out.append(tuple((k, ("nan" if v != v else round(v, 6)) if isinstance(v, float) else v)
+                         for k, v in sorted(r.items())))
     return sorted(out, key=repr)
 
 

@@ -28,9 +28,34 @@ def test_float_and_decimal_rules():
     assert spark_hash_value(1.5, "float", 42) == _hash_int(struct.unpack("<I", struct.pack("<f", 1.5))[0], 42)
     assert spark_hash_value(-0.0, "float", 42) == spark_hash_value(0.0, "float", 42)
     assert spark_hash_value(float("nan"), "double", 42) == _hash_long(0x7FF8000000000000, 42)
-    # decimal: the unscaled value (12.34 → 1234)
-    assert spark_hash_value(12.34, "decimal", 42) == _hash_long(1234, 42)
-    assert spark_hash_value(7.0, "decimal", 42) == _hash_long(7, 42)
+    # decimal(p, s): hashLong of the unscaled value AT THE COLUMN'S SCALE for p <= 18 (12.34 as decimal(10,2) →
+    # 1234; 7 as decimal(10,2) → 700), the BigInteger's bytes above that
+    from decimal import Decimal
+    from dxa.engine.decimal import DecimalType
+    from dxa.engine.sqlfuncs import _hash_bytes
+    assert spark_hash_value(1234, DecimalType(10, 2), 42) == _hash_long(1234, 42)
+    assert spark_hash_value(Decimal("7"), DecimalType(10, 2), 42) == _hash_long(700, 42)
+    assert spark_hash_value(Decimal("1.25"), DecimalType(10, 2), 42) == 1910520950       # hashLong(125, 42)
+    assert spark_hash_value([125, 0], DecimalType(20, 2), 42) == _hash_bytes(bytes([125]), 42)
+    assert spark_hash_value([-1, -1], DecimalType(20, 2), 42) == _hash_bytes(bytes([0xFF]), 42)   # -1
+
+
+def test_decimal_hash_in_sql():
+    from dxa.engine.column import Table
+    from dxa.engine.expr import EvalContext
+    from dxa.engine.query import Catalog, run_sql
+    from dxa.engine.types import StructField, StructType
+    cat = Catalog()
+    cat.register("T", Table.from_pylist([{"k": 1}], StructType((StructField("k", "long"),))))
+    out = run_sql("SELECT hash(CAST(1.25 AS DECIMAL(10,2))) AS h, hash(CAST(k AS DECIMAL(10,2))) AS h2 FROM T", cat,
+                  EvalContext()).to_pylist()
+    assert out == [{"h": 1910520950, "h2": _hl(100)}]
+
+
+def _hl(v):
+    from dxa.engine.sqlfuncs import _hash_long
+    r = _hash_long(v, 42)
+    return r - (1 << 32) if r >= (1 << 31) else r
 
 
 @pytest.mark.gpu
