@@ -255,6 +255,11 @@ class Processor:
                 if d is ALL:
                     return None
                 idents += list(d)
+        # columns the job's settings name rather than its SQL: the window timestamp column (WindowStore reads it
+        # from every batch, TimeWindowHandler.scala:41-67) must survive pruning even when no statement names it
+        ts_col = getattr(self.windows, "timestamp_column", None)
+        if ts_col:
+            idents.append(tuple(p.strip().strip("`") for p in str(ts_col).split(".")))
         for t in projection_texts:
             if re.match(r"^\s*Raw\s*\.\s*\*\s*$", t):
                 continue

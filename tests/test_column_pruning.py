@@ -50,3 +50,51 @@ def test_pruned_outputs_equal_unpruned(tmp_path):
 def test_star_keeps_every_field(tmp_path):
     p, _ = _run("passthrough", True, tmp_path)
     assert p.parse_plan.keep is None
+
+
+def test_window_timestamp_column_survives_pruning(tmp_path):
+    """``Raw.*`` projection, windowed SQL that never names the timestamp column: the column the settings name
+    (datax.job.process.timestampcolumn) is still parsed, so the window store can bucket the rows."""
+    from dxa.config.settings import SettingDictionary
+    from dxa.engine.processor import Processor
+    from dxa.io import sinks
+    from dxa.ops.jsonparse import frame_records
+    from dxa.engine.processor import RawBatch
+    schema = {"type": "struct", "fields": [
+        {"name": "id", "type": "long", "nullable": True, "metadata": {}},
+        {"name": "ts", "type": "timestamp", "nullable": True, "metadata": {}},
+        {"name": "v", "type": "double", "nullable": True, "metadata": {}},
+        {"name": "junk", "type": "string", "nullable": True, "metadata": {}}]}
+    (tmp_path / "s.json").write_text(json.dumps(schema))
+    (tmp_path / "p.txt").write_text("Raw.*\n")
+    (tmp_path / "t.txt").write_text("--DataXQuery--\nW = SELECT id, SUM(v) AS sv, COUNT(*) AS c "
+                                    "FROM DataXProcessedInput_3seconds GROUP BY id\n")
+    d = SettingDictionary({
+        "datax.job.name": "tsprune", "datax.job.input.default.blobschemafile": str(tmp_path / "s.json"),
+        "datax.job.process.projection": str(tmp_path / "p.txt"),
+        "datax.job.process.transform": str(tmp_path / "t.txt"),
+        "datax.job.process.timewindow.DataXProcessedInput_3seconds.windowduration": "3 seconds",
+        "datax.job.process.watermark": "1 second", "datax.job.process.timestampcolumn": "ts",
+        "datax.job.process.pipelineoutputs": "false", "datax.job.output.W.memory.enabled": "true"})
+    def run(prune):
+        proc = Processor(d, "cpu", parse_prune=prune)
+        sinks.MEMORY_SINKS.clear()
+        t0 = 1_700_000_000
+        got = []
+        for b in range(3):
+            bt = (t0 + b) * 1_000_000
+            recs = [json.dumps({"id": i % 2, "ts": f"2023-11-14T22:13:{19 + b:02d}.{500 + i:03d}Z", "v": 1.0,
+                                "junk": "x"}).encode() for i in range(4)]
+            buf, offs = frame_records(recs)
+            proc.clock = lambda bt=bt: bt / 1e6
+            proc.process_batch(RawBatch(buf, offs, len(recs)), bt, 1_000_000)
+            proc.drain()
+            got.append(sorted(json.loads(l)["c"] for l in sinks.MEMORY_SINKS.get("W", [])))
+            sinks.MEMORY_SINKS.clear()
+        return proc, got
+    proc, got = run(True)
+    assert proc.parse_plan.keep is not None
+    leaves = {p[-1] for p in proc.parse_plan.keep}
+    assert "ts" in leaves and "junk" not in leaves
+    _, want = run(False)
+    assert got == want and got[-1] and got[-1][0] >= 4     # the window holds more than one batch of rows
