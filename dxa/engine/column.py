@@ -290,6 +290,8 @@ class ConstColumn(Column):
         v = self.value
         if self.dtype == "timestamp" and v is not None:
             v = ts_to_datetime(v)
+        elif self.dtype == "date" and isinstance(v, int) and not isinstance(v, bool):
+            v = (EPOCH + _dt.timedelta(days=v)).date()
         return [v] * self.length
 
     def __repr__(self):

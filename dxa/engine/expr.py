@@ -327,7 +327,7 @@ def _coerce_const_for(col_other: Column, const: ConstColumn) -> ConstColumn:
 
 # Built-ins that take decimal(p,s) arguments as they are; every other function sees its decimal arguments as
 # doubles (Spark's implicit cast for functions typed on DoubleType: ImplicitTypeCasts) — see _call / evaluate.
-_DECIMAL_AWARE = frozenset({"round", "bround", "hash",
+_DECIMAL_AWARE = frozenset({"round", "bround", "hash", "typeof",
                             "coalesce", "if", "nvl", "ifnull", "nullif", "nvl2", "to_json", "named_struct", "struct",
                             "array", "map", "concat", "concat_ws", "isnull", "isnotnull", "string", "abs",
                             "negative", "positive"})
@@ -1906,6 +1906,9 @@ def output_name(e: A.Expr) -> str:
         inner = ", ".join(output_name(a) for a in e.args)
         return f"{name}({'DISTINCT ' if e.distinct else ''}{inner})"
     if isinstance(e, A.Cast):
+        if e.typed_literal:            # Literal.sql of a timestamp / date value
+            v = output_name(e.operand)
+            return f"TIMESTAMP('{v}')" if str(e.to).lower() == "timestamp" else f"DATE '{v}'"
         return f"CAST({output_name(e.operand)} AS {_type_sql(e.to)})"
     if isinstance(e, A.BinOp):
         op = e.op.upper() if e.op in ("and", "or", "div") else e.op

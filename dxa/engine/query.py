@@ -1742,7 +1742,7 @@ def _order_by(t: Table, items: List[A.OrderItem], ctx, src_scope: Optional[Scope
                 else:
                     col = evaluate(e, src_scope, ctx)
         col = materialize(col)
-        if not isinstance(col, (StrColumn, PrimColumn)):
+        if not isinstance(col, (StrColumn, PrimColumn, StructColumn)):
             raise QueryError(f"cannot ORDER BY {col.dtype}")
         nulls_first = it.nulls_first if it.nulls_first is not None else it.ascending
         specs.append((col, it.ascending, nulls_first))

@@ -378,14 +378,47 @@ def _f_from_unixtime(e, scope, ctx, subst):
                              _fmt_arg(e, scope, ctx, subst, 1, "yyyy-MM-dd HH:mm:ss"))
 
 
+# java.time.ZoneId.SHORT_IDS, which java.util.TimeZone.getTimeZone (Spark 2.4's DateTimeUtils.getTimeZone) honours;
+# EST / MST / HST are fixed offsets there
+_JAVA_SHORT_IDS = {
+    "ACT": "Australia/Darwin", "AET": "Australia/Sydney", "AGT": "America/Argentina/Buenos_Aires",
+    "ART": "Africa/Cairo", "AST": "America/Anchorage", "BET": "America/Sao_Paulo", "BST": "Asia/Dhaka",
+    "CAT": "Africa/Harare", "CNT": "America/St_Johns", "CST": "America/Chicago", "CTT": "Asia/Shanghai",
+    "EAT": "Africa/Addis_Ababa", "ECT": "Europe/Paris", "IET": "America/Indiana/Indianapolis",
+    "IST": "Asia/Kolkata", "JST": "Asia/Tokyo", "MIT": "Pacific/Apia", "NET": "Asia/Yerevan",
+    "NST": "Pacific/Auckland", "PLT": "Asia/Karachi", "PNT": "America/Phoenix", "PRT": "America/Puerto_Rico",
+    "PST": "America/Los_Angeles", "SST": "Pacific/Guadalcanal", "VST": "Asia/Ho_Chi_Minh"}
+_JAVA_FIXED = {"EST": -5 * 60, "MST": -7 * 60, "HST": -10 * 60}
+_GMT_OFFSET = re.compile(r"^(?:GMT|UTC)([+-])(\d{1,2})(?::?(\d{2}))?$")
+
+
+def java_time_zone(tz: str):
+    """tzinfo for a zone id as java.util.TimeZone.getTimeZone reads it: region ids, the legacy three-letter ids
+    (``PST``, ``CTT``, … via ZoneId.SHORT_IDS; ``EST`` / ``MST`` / ``HST`` fixed), ``GMT+8`` / ``GMT-08:00``
+    custom offsets, and — like Java — GMT for an id it does not know."""
+    from zoneinfo import ZoneInfo
+    t = str(tz).strip()
+    if t in _JAVA_FIXED:
+        return _dt.timezone(_dt.timedelta(minutes=_JAVA_FIXED[t]))
+    if t in _JAVA_SHORT_IDS:
+        return ZoneInfo(_JAVA_SHORT_IDS[t])
+    m = _GMT_OFFSET.match(t)
+    if m:
+        mins = int(m.group(2)) * 60 + int(m.group(3) or 0)
+        return _dt.timezone(_dt.timedelta(minutes=-mins if m.group(1) == "-" else mins))
+    try:
+        return ZoneInfo(t)
+    except Exception:  # noqa: BLE001 — unknown ids are GMT in Java
+        return _dt.timezone.utc
+
+
 def _tz_shift(to_utc: bool):
     """to_utc_timestamp(ts, tz): ts is wall-clock time in tz → UTC.  from_utc_timestamp(ts, tz): UTC → wall clock
     in tz.  Host-assisted (zone rules from the system tz database)."""
     def f(e, scope, ctx, subst):
         a = materialize(_ts(evaluate(e.args[0], scope, ctx, subst)))
         tz = _fmt_arg(e, scope, ctx, subst, 1, "UTC")
-        from zoneinfo import ZoneInfo
-        z = ZoneInfo(tz)
+        z = java_time_zone(tz)
         out = []
         for v in a.data.cpu().tolist():
             t = _EPOCH + _dt.timedelta(microseconds=int(v))
@@ -430,7 +463,12 @@ def array_from_pylist(lists, elem_type, device) -> ArrayColumn:
            for j in range(max(k, 1))]
     valid = None if all(l is not None for l in lists) else torch.tensor([l is not None for l in lists],
                                                                        dtype=torch.bool, device=device)
-    return ArrayColumn(els, n, valid, True, device)
+    if all(len(l) == k for l in lists if l is not None) and k:
+        return ArrayColumn(els, n, valid, False, device)
+    # rows of different lengths: a presence mask keeps real null elements (drop_nulls would lose them)
+    present = torch.tensor([[l is not None and j < len(l) for j in range(max(k, 1))] for l in lists],
+                           dtype=torch.bool, device=device).reshape(n, max(k, 1))
+    return ArrayColumn(els, n, valid, False, device, present=present)
 
 
 def split_strings(col: Column, pattern: str, limit: int = -1) -> ArrayColumn:
@@ -1951,3 +1989,279 @@ def _h2d(data, dtype, device):
 # array built-ins as slot-matrix tensor operations (dxa/engine/arrayfuncs.py registers itself on import, with the
 # row-wise functions above as its fallback)
 from . import arrayfuncs  # noqa: E402,F401
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Spark 2.4 built-ins: str_to_map, map_concat, array_repeat, encode / decode, sentences, xpath_*, assert_true
+# ---------------------------------------------------------------------------------------------------------------
+
+def _const_str(c):
+    from .expr import _const_str as cs
+    return cs(c)
+
+
+def _raw_rows(col) -> list:
+    """Row bytes of a string / binary column (None for null), without a UTF-8 decode."""
+    col = materialize(col)
+    if isinstance(col, ConstColumn):
+        v = col.value
+        return [None if v is None else (v if isinstance(v, bytes) else str(v).encode("utf-8"))] * col.length
+    if not isinstance(col, StrColumn):
+        return [None if v is None else str(v).encode("utf-8") for v in col.to_pylist()]
+    arena = col.arena.cpu().numpy().tobytes()
+    st, ln = col.starts.cpu().tolist(), col.lens.cpu().tolist()
+    ok = col.valid.cpu().tolist() if col.valid is not None else [True] * col.length
+    return [arena[s:s + l] if o else None for s, l, o in zip(st, ln, ok)]
+
+
+def _binary_column(values, device):
+    sc = strings_from_pylist(values, device)
+    return StrColumn(sc.arena, sc.starts, sc.lens, sc.valid, "binary")
+
+
+# java.nio charset names Spark's Encode / Decode accept (StringUtils: US-ASCII, ISO-8859-1, UTF-8, UTF-16BE,
+# UTF-16LE, UTF-16); Java's UTF-16 encoder writes a big-endian byte-order mark
+_CHARSETS = {"us-ascii": "ascii", "iso-8859-1": "latin-1", "utf-8": "utf-8", "utf-16be": "utf-16-be",
+             "utf-16le": "utf-16-le", "utf-16": "utf-16"}
+
+
+def _charset(name) -> str:
+    cs = _CHARSETS.get(str(name).strip().lower())
+    if cs is None:
+        raise EvalError(f"unsupported charset {name!r} (US-ASCII, ISO-8859-1, UTF-8, UTF-16BE, UTF-16LE, UTF-16)")
+    return cs
+
+
+def _f_encode(e, scope, ctx, subst):
+    s, cs = _args(e, scope, ctx, subst)
+    py = _charset(_const_str(cs))
+    out = []
+    for v in (s.to_pylist() if not isinstance(s, ConstColumn) else [s.value] * scope.length):
+        if v is None:
+            out.append(None)
+        elif py == "utf-16":
+            out.append(b"\xfe\xff" + str(v).encode("utf-16-be"))
+        else:
+            out.append(str(v).encode(py, errors="replace").replace(b"\\ufffd", b"?"))
+    return _binary_column(out, scope.device)
+
+
+def _f_decode(e, scope, ctx, subst):
+    b, cs = _args(e, scope, ctx, subst)
+    py = _charset(_const_str(cs))
+    out = []
+    for v in _raw_rows(b):
+        if v is None:
+            out.append(None)
+        elif py == "utf-16":
+            if v[:2] == b"\xff\xfe":
+                out.append(v[2:].decode("utf-16-le", errors="replace"))
+            else:
+                out.append((v[2:] if v[:2] == b"\xfe\xff" else v).decode("utf-16-be", errors="replace"))
+        else:
+            out.append(v.decode(py, errors="replace"))
+    return column_from_pylist(out, "string", scope.device)
+
+
+def _f_str_to_map(e, scope, ctx, subst):
+    """str_to_map(text[, pairDelim = ',', keyValueDelim = ':']): delimiters are regexes (StringToMap splits
+    with String.split); a pair without the key/value delimiter maps to NULL.  This engine's maps have the batch's
+    keys as fields (in first-appearance order); a key a row lacks is absent there."""
+    n, dev = scope.length, scope.device
+    args = _args(e, scope, ctx, subst)
+    pd = _const_str(args[1]) if len(args) > 1 else ","
+    kd = _const_str(args[2]) if len(args) > 2 else ":"
+    texts = args[0].to_pylist() if not isinstance(args[0], ConstColumn) else [args[0].value] * n
+    rows, keys = [], {}
+    for t in texts:
+        if t is None:
+            rows.append(None)
+            continue
+        m = {}
+        for pair in re.split(pd, str(t)):
+            kv = re.split(kd, pair, maxsplit=1)
+            k = kv[0]
+            if k not in m:
+                m[k] = kv[1] if len(kv) > 1 else None
+            keys.setdefault(k, None)
+        rows.append(m)
+    names = list(keys)
+    cols = [column_from_pylist([None if r is None else r.get(k) for r in rows], "string", dev) for k in names]
+    valid = None if all(r is not None for r in rows) else torch.tensor([r is not None for r in rows],
+                                                                      dtype=torch.bool, device=dev)
+    return StructColumn(names, cols, n, valid, True, None, dev)
+
+
+def _f_map_concat(e, scope, ctx, subst):
+    """map_concat(m1, m2, …): the union of the maps' keys; a key in several maps takes the later map's value
+    where that map has it.  NULL when any argument is NULL (Spark 2.4 MapConcat)."""
+    n, dev = scope.length, scope.device
+    ms = [materialize(m) for m in _args(e, scope, ctx, subst)]
+    for m in ms:
+        if not (isinstance(m, StructColumn) and m.is_map):
+            raise EvalError("map_concat() expects maps")
+    names, cols = [], {}
+    for m in ms:
+        for k, c in zip(m.names, m.children):
+            c = materialize(c)
+            if k not in cols:
+                names.append(k)
+                cols[k] = c
+            else:
+                from .expr import _select_by_conditions
+                cols[k] = _select_by_conditions([PrimColumn("boolean", c.valid_mask())], [c], cols[k], n, dev)
+    valid = None
+    for m in ms:
+        if m.valid is not None:
+            valid = m.valid if valid is None else valid & m.valid
+    return StructColumn(names, [cols[k] for k in names], n, valid, True, None, dev)
+
+
+def _f_array_repeat(e, scope, ctx, subst):
+    """array_repeat(element, count): ``count`` copies (a NULL count → NULL, a negative one → empty)."""
+    n, dev = scope.length, scope.device
+    x, c = _args(e, scope, ctx, subst)
+    if isinstance(c, ConstColumn):
+        if c.value is None:
+            return ConstColumn(None, "null", n, dev)
+        k = max(0, int(c.value))
+        return ArrayColumn([x] * k, n, None, False, dev) if k else \
+            ArrayColumn([], n, None, False, dev, present=torch.zeros((n, 0), dtype=torch.bool, device=dev))
+    cnt = materialize(c)
+    cd = cnt.data.to(torch.int64).clamp(min=0)
+    k = int(cd.max()) if n else 0                                 # slot count: one host read
+    j = torch.arange(max(k, 0), device=dev)
+    present = j.unsqueeze(0) < cd.unsqueeze(1)
+    return ArrayColumn([x] * k, n, cnt.valid, False, dev, present=present)
+
+
+_SENT_END = re.compile(r"(?<=[.!?])\s+")
+_WORD = re.compile(r"[\w']+", re.UNICODE)
+
+
+def _sentences(text):
+    """Sentences → words, as Spark's Sentences does with java.text.BreakIterator (sentence then word instances,
+    punctuation dropped)."""
+    out = []
+    for sent in _SENT_END.split(str(text).strip()):
+        words = [w.strip("'") for w in _WORD.findall(sent)]
+        words = [w for w in words if w]
+        if words:
+            out.append(words)
+    return out
+
+
+def _f_sentences(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    a = _args(e, scope, ctx, subst)[0]
+    texts = a.to_pylist() if not isinstance(a, ConstColumn) else [a.value] * n
+    rows = [None if t is None else _sentences(t) for t in texts]
+    k = max((len(r) for r in rows if r is not None), default=0)
+    outer = [array_from_pylist([r[j] if r is not None and j < len(r) else [] for r in rows], "string", dev)
+             for j in range(k)]
+    present = torch.tensor([[r is not None and j < len(r) for j in range(k)] for r in rows],
+                           dtype=torch.bool, device=dev).reshape(n, k)
+    valid = None if all(r is not None for r in rows) else torch.tensor([r is not None for r in rows],
+                                                                      dtype=torch.bool, device=dev)
+    return ArrayColumn(outer, n, valid, False, dev, present=present)
+
+
+def _xpath_eval(xml, path):
+    """The XPath subset Spark's xpath_* examples use: location paths from the document (``a/b``, ``/a/b``,
+    ``//b``, ``a/b/@attr``, ``a/b/text()``) and ``sum(…)`` / ``count(…)`` over them → ('nodes', [text]) or
+    ('number', v).  (Spark runs javax.xml.xpath; full XPath 1.0 is out of scope here.)"""
+    import xml.etree.ElementTree as ET
+    p = str(path).strip()
+    m = re.match(r"^(sum|count)\((.*)\)$", p)
+    if m:
+        kind, vals = _xpath_eval(xml, m.group(2))
+        if m.group(1) == "count":
+            return "number", float(len(vals))
+        tot = 0.0
+        for v in vals:
+            try:
+                tot += float(v)
+            except ValueError:
+                return "number", float("nan")
+        return "number", tot
+    root = ET.fromstring(str(xml))
+    attr = text = False
+    if p.endswith("/text()"):
+        p, text = p[:-7], True
+    am = re.match(r"^(.*)/@([\w:-]+)$", p)
+    if am:
+        p, attr = am.group(1), am.group(2)
+    if p.startswith("//"):
+        nodes = ([root] if root.tag == p[2:].split("/")[0] and "/" not in p[2:] else []) + root.findall(".//" + p[2:])
+    else:
+        steps = [s for s in p.lstrip("/").split("/") if s]
+        if not steps or steps[0] not in (root.tag, "*"):
+            nodes = []
+        elif len(steps) == 1:
+            nodes = [root]
+        else:
+            nodes = root.findall("/".join(steps[1:]))
+    if attr:
+        return "nodes", [n.get(attr) for n in nodes if n.get(attr) is not None]
+    if text:
+        return "nodes", [n.text for n in nodes if n.text is not None]
+    return "nodes", ["".join(n.itertext()) for n in nodes]
+
+
+def _xpath_scalar(kind):
+    def fn(xml, path):
+        k, v = _xpath_eval(xml, path)
+        if kind == "string":
+            return (v[0] if v else "") if k == "nodes" else F.java_double_str(v)
+        if kind == "boolean":
+            return bool(v) if k == "nodes" else v != 0
+        num = v if k == "number" else (float(v[0]) if v else float("nan"))
+        if kind in ("int", "long", "short"):
+            return 0 if num != num else int(num)
+        return num
+    return fn
+
+
+def _f_xpath(e, scope, ctx, subst):
+    n, dev = scope.length, scope.device
+    x, p = _args(e, scope, ctx, subst)
+    xs = x.to_pylist() if not isinstance(x, ConstColumn) else [x.value] * n
+    path = _const_str(p)
+    rows = [None if v is None else _xpath_eval(v, path)[1] for v in xs]
+    return array_from_pylist(rows, "string", dev)
+
+
+def _f_assert_true(e, scope, ctx, subst):
+    """assert_true(cond): NULL when every row's condition holds; otherwise the query fails (Spark's AssertTrue:
+    "'<cond>' is not true!")."""
+    from .expr import output_name
+    (c,) = _args(e, scope, ctx, subst)
+    c = materialize(c)
+    ok = c.data.bool() & c.valid_mask() if not isinstance(c, ConstColumn) else None
+    bad = (not c.value) if isinstance(c, ConstColumn) else bool((~ok).any())
+    if bad:
+        raise EvalError(f"'{output_name(e.args[0])}' is not true!")
+    return ConstColumn(None, "null", scope.length, scope.device)
+
+
+def _register_spark24_more():
+    reg = register_function
+    reg("encode", _f_encode)
+    reg("decode", _f_decode)
+    reg("str_to_map", _f_str_to_map)
+    reg("map_concat", _f_map_concat)
+    reg("array_repeat", _f_array_repeat)
+    reg("sentences", _f_sentences)
+    reg("xpath", _f_xpath)
+    reg("xpath_string", _host_string_fn(_xpath_scalar("string")))
+    reg("xpath_boolean", _host_string_fn(_xpath_scalar("boolean"), "boolean"))
+    reg("xpath_int", _host_string_fn(_xpath_scalar("int"), "int"))
+    reg("xpath_short", _host_string_fn(_xpath_scalar("short"), "int"))
+    reg("xpath_long", _host_string_fn(_xpath_scalar("long"), "long"))
+    reg("xpath_double", _host_string_fn(_xpath_scalar("double"), "double"))
+    reg("xpath_number", _host_string_fn(_xpath_scalar("double"), "double"))
+    reg("xpath_float", _host_string_fn(_xpath_scalar("double"), "double"))
+    reg("assert_true", _f_assert_true)
+
+
+_register_spark24_more()

@@ -243,11 +243,31 @@ def column_order_key(col, descending: bool = False):
     return key, valid
 
 
+def _expand_struct_specs(specs):
+    """A struct sort key is its fields, left to right (Spark's struct ordering): the struct's own null placement
+    first (a flag column that is null where the struct is), then every field — nested structs recursively — with
+    the struct's direction and ascending-nulls-first field ordering (reversed as a whole for DESC)."""
+    from ..engine.column import ConstColumn, PrimColumn, StructColumn
+    out = []
+    for col, ascending, nulls_first in specs:
+        if isinstance(col, ConstColumn):
+            col = col.materialize()
+        if not isinstance(col, StructColumn):
+            out.append((col, ascending, nulls_first))
+            continue
+        if col.valid is not None:
+            out.append((PrimColumn("int", torch.zeros(col.length, dtype=torch.int64, device=col.valid.device),
+                                   col.valid), ascending, nulls_first))
+        out += _expand_struct_specs([(c, ascending, ascending) for c in col.children])
+    return out
+
+
 def sort_spec_words(specs) -> List[torch.Tensor]:
     """``specs``: [(column, ascending, nulls_first)] most significant first → key words, least significant first:
-    every item contributes its order key and, above it, a null-placement flag word."""
+    every item contributes its order key and, above it, a null-placement flag word.  Struct columns order by their
+    fields (``_expand_struct_specs``)."""
     words: List[torch.Tensor] = []
-    for col, ascending, nulls_first in reversed(list(specs)):
+    for col, ascending, nulls_first in reversed(_expand_struct_specs(list(specs))):
         key, valid = column_order_key(col, not ascending)
         words.append(key)
         if col.valid is not None:

@@ -73,6 +73,7 @@ class WindowCall(Expr):
     partition: List[Expr] = field(default_factory=list)
     order: List["OrderItem"] = field(default_factory=list)
     frame: Optional[tuple] = None
+    ref: Optional[str] = None          # ``OVER w``: a window the query's WINDOW clause names (resolved by the parser)
 
     def key(self):
         return ("over", self.func.key(), tuple(p.key() for p in self.partition),
@@ -183,6 +184,7 @@ class Case(Expr):
 class Cast(Expr):
     operand: Expr
     to: str
+    typed_literal: bool = False        # ``TIMESTAMP '…'`` / ``DATE '…'``: a literal of that type (Spark's typed literal)
 
     def key(self):
         return ("cast", self.to, self.operand.key())

@@ -258,6 +258,8 @@ class Parser:
             return False
         if w == "lateral" and self.is_word("view", tok=n):
             return False
+        if w == "window" and n.kind in ("id", "kw") and self.is_kw("as", tok=self.peek(2)):
+            return False                 # WINDOW w AS (…) after the FROM clause
         return True
 
     def parse_order_items(self):
@@ -292,11 +294,13 @@ class Parser:
         return left
 
     def parse_set_term(self):
+        if self.is_word("values") and (self.is_op("(", tok=self.peek()) or self.peek().kind in ("num", "str")):
+            return self._parse_values().body
         if self.is_op("("):
             # parenthesised query
             save = self.i
             self.advance()
-            if self.is_kw("select") or self.is_op("("):
+            if self.is_kw("select") or self.is_op("(") or self.is_word("values"):
                 q = self.parse_query()
                 self.expect_op(")")
                 if q.order_by or q.limit is not None:
@@ -331,7 +335,40 @@ class Parser:
             self._parse_group_by(sel)
         if self.accept_kw("having"):
             sel.having = self.parse_expr()
+        if self.is_word("window") and self.peek().kind in ("id", "kw"):
+            self._parse_window_clause(sel)
         return sel
+
+    def _parse_window_clause(self, sel: A.Select):
+        """``WINDOW w AS (PARTITION BY … ORDER BY … frame), w2 AS w`` → every ``OVER w`` of the select list,
+        HAVING and ORDER BY takes that specification."""
+        self.advance()
+        defs = {}
+        while True:
+            name = self.ident().lower()
+            self.expect_kw("as")
+            if self.accept_op("("):
+                defs[name] = self._window_spec()
+            else:
+                other = self.ident().lower()
+                if other not in defs:
+                    self.error(f"window {other} is not defined")
+                defs[name] = defs[other]
+            if not self.accept_op(","):
+                break
+
+        def fill(node):
+            if isinstance(node, A.WindowCall) and node.ref is not None:
+                spec = defs.get(node.ref.lower())
+                if spec is None:
+                    self.error(f"window {node.ref} is not defined")
+                part, order, frame = spec
+                return A.WindowCall(A.replace(node.func, fill), list(part), list(order), frame)
+            return None
+        sel.items = [A.SelectItem(A.replace(it.expr, fill), it.alias) for it in sel.items]
+        if sel.having is not None:
+            sel.having = A.replace(sel.having, fill)
+        self._window_defs = defs
 
     def _parse_group_by(self, sel: A.Select):
         """GROUP BY e, … [WITH ROLLUP | WITH CUBE] | ROLLUP(…) | CUBE(…) | GROUPING SETS ((…), …)."""
@@ -379,6 +416,23 @@ class Parser:
             sel.group_by.append(self.parse_expr())
             if not self.accept_op(","):
                 break
+        if self.is_word("grouping") and self.is_word("sets", tok=self.peek()):
+            # GROUP BY a, b GROUPING SETS ((a), (b), ()) — Spark 2.4's form: the list names the grouping columns
+            self.advance()
+            self.advance()
+            self.expect_op("(")
+            sets = []
+            while True:
+                if self.is_op("("):
+                    sets.append(expr_list())
+                else:
+                    sets.append([self.parse_expr()])
+                if not self.accept_op(","):
+                    break
+            self.expect_op(")")
+            sel.group_by = uniq(sel.group_by + [e for st in sets for e in st])
+            sel.grouping_sets = sets
+            return
         if self.is_word("with") and self.is_word("rollup", "cube", tok=self.peek()):
             self.advance()
             kind = self.advance().text.lower()
@@ -477,7 +531,63 @@ class Parser:
                 self.expect_op(")")
             left = A.Join(left, right, kind, on, using)
 
+    def _parse_values(self) -> A.Query:
+        """``VALUES (1, 'a'), (2, 'b')`` / ``VALUES 1, 2`` (Spark's inline table) → a UNION ALL of one-row SELECTs
+        named col1, col2, … (balanced, so a long list stays shallow); the set operation widens each column to the
+        rows' common type as Spark's inline-table resolution does."""
+        self.advance()                                   # VALUES
+        rows = []
+        while True:
+            if self.is_op("(") and not self._at_query_after_paren():
+                self.advance()
+                row = [self.parse_expr()]
+                while self.accept_op(","):
+                    row.append(self.parse_expr())
+                self.expect_op(")")
+            else:
+                row = [self.parse_expr()]
+            rows.append(row)
+            if not self.accept_op(","):
+                break
+        width = len(rows[0])
+        if any(len(r) != width for r in rows):
+            self.error("VALUES rows must have the same number of columns")
+        names = [f"col{i + 1}" for i in range(width)]
+        sels = [A.Select(items=[A.SelectItem(e, nm) for e, nm in zip(r, names)]) for r in rows]
+
+        def tree(lo, hi):
+            if hi - lo == 1:
+                return sels[lo]
+            mid = (lo + hi) // 2
+            return A.SetOp("union", True, tree(lo, mid), tree(mid, hi))
+        return A.Query(tree(0, len(sels)))
+
+    def _at_query_after_paren(self) -> bool:
+        t = self.peek()
+        return t.kind in ("id", "kw") and t.text.lower() in ("select", "with", "values")
+
+    def _rename_columns(self, q: A.Query, alias, names):
+        """``… AS t(x, y)``: the relation's columns renamed positionally (a projection over it)."""
+        inner = A.SubqueryRef(q, "__v")
+        items = [A.SelectItem(A.Ident(("__v", f"col{i + 1}")), nm) for i, nm in enumerate(names)]
+        return A.SubqueryRef(A.Query(A.Select(items=items, from_=inner)), alias)
+
     def parse_table_primary(self):
+        if self.is_word("values") and (self.is_op("(", tok=self.peek()) or self.peek().kind in ("num", "str")):
+            q = self._parse_values()
+            alias, cols = None, []
+            if self.accept_kw("as"):
+                alias = self.ident()
+            elif self._alias_word_ok():
+                alias = self.advance().text
+            if alias is not None and self.accept_op("("):
+                cols.append(self.ident())
+                while self.accept_op(","):
+                    cols.append(self.ident())
+                self.expect_op(")")
+            if cols:
+                return self._rename_columns(q, alias, cols)
+            return A.SubqueryRef(q, alias)
         if self.accept_op("("):
             q = self.parse_query()
             self.expect_op(")")
@@ -811,6 +921,10 @@ class Parser:
                 pass  # function named like a keyword
             elif w not in ("first", "last", "timewindow", "div", "regexp", "semi", "anti", "nulls"):
                 self.error(f"unexpected keyword {t.text}")
+        if t.kind in ("id", "kw") and t.text.lower() in ("timestamp", "date") and self.peek().kind == "str":
+            # typed literal: TIMESTAMP '2020-01-01 00:00:00', DATE '2020-01-01'
+            ty = self.advance().text.lower()
+            return A.Cast(A.Literal(self.advance().text, "string"), ty, typed_literal=True)
         if t.kind in ("id", "kw"):
             name = self.advance().text
             if self.is_op("("):
@@ -944,11 +1058,20 @@ class Parser:
         return False
 
     def _maybe_over(self, call):
-        """``call OVER (PARTITION BY ... ORDER BY ... frame)`` (Spark window functions)."""
+        """``call OVER (PARTITION BY ... ORDER BY ... frame)`` (Spark window functions); ``call OVER w`` names a
+        window of the query's WINDOW clause."""
+        if self.is_word("over") and self.peek().kind in ("id", "kw") and not self.is_op("(", tok=self.peek()):
+            self.advance()
+            return A.WindowCall(call, ref=self.ident())
         if not (self.is_word("over") and self.is_op("(", tok=self.peek())):
             return call
         self.advance()
         self.expect_op("(")
+        part, order, frame = self._window_spec()
+        return A.WindowCall(call, part, order, frame)
+
+    def _window_spec(self):
+        """The inside of ``( … )`` of a window: (partition, order, frame); consumes the closing parenthesis."""
         part, order, frame = [], [], None
         if self.accept_word("partition"):
             self.expect_kw("by")
@@ -969,7 +1092,7 @@ class Parser:
                 lo, hi = self._frame_bound(), ("current", 0)
             frame = (kind, lo, hi)
         self.expect_op(")")
-        return A.WindowCall(call, part, order, frame)
+        return part, order, frame
 
     def _frame_bound(self):
         if self.accept_word("unbounded"):
