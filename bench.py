@@ -145,9 +145,11 @@ def main():
                     help="kafka: size record batches as a Java producer with batch.size=BYTES does (the estimated "
                          "compressed size fills batch.size; dxa.io.kafka.records_per_batch) instead of a fixed "
                          "--kafka-batch-records")
-    ap.add_argument("--kafka-codec", choices=["lz4", "gzip"], default="lz4",
-                    help="kafka: record batch compression codec (gzip = the Event Hubs Kafka endpoint's codec; "
-                         "inflated on the GPU by inflate.hip)")
+    ap.add_argument("--kafka-codec", choices=["lz4", "gzip", "snappy", "zstd"], default="lz4",
+                    help="kafka: record batch compression codec, decoded on the GPU (lz4.hip; gzip = the Event Hubs "
+                         "Kafka endpoint's codec, inflate.hip; snappy = snappy-java's xerial stream, snappy.hip; "
+                         "zstd = zstd-jni's frames, zstd.hip)")
+    ap.add_argument("--zstd-level", type=int, default=3, help="kafka zstd: producer compression.zstd.level")
     ap.add_argument("--crc", choices=["host", "device", "off"], default="host",
                     help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): host planner "
                          "threads (default), the GPU (kafka_crc_kernel), or not at all")
@@ -274,11 +276,12 @@ def main():
             cuts = np.linspace(0, E, parts + 1).astype(np.int64)
             if args.kafka_batch_size and p == 0:
                 # batch.size semantics of the Java producer: records per batch from the learned compression ratio
-                args.kafka_batch_records, _r = K.records_per_batch(hb, ho, args.kafka_batch_size,
-                                                                   compression=args.kafka_codec,
-                                                                   level=args.lz4_level, block_size=lz4_block_k)
+                args.kafka_batch_records, _r = K.records_per_batch(
+                    hb, ho, args.kafka_batch_size, compression=args.kafka_codec,
+                    level=args.zstd_level if args.kafka_codec == "zstd" else args.lz4_level, block_size=lz4_block_k)
+            clevel = args.zstd_level if args.kafka_codec == "zstd" else args.lz4_level
             sets = [K.encode_stream(hb, ho[cuts[q]:cuts[q + 1] + 1], args.kafka_batch_records, base_offset=0,
-                                    compression=args.kafka_codec, level=args.lz4_level, block_size=lz4_block_k,
+                                    compression=args.kafka_codec, level=clevel, block_size=lz4_block_k,
                                     threads=host_thr) for q in range(parts)]
             total = sum(x.size for x in sets)
             staging = torch.empty(total + 64, dtype=torch.uint8, pin_memory=on_gpu)
@@ -609,7 +612,8 @@ def main():
     }
     if comp_bytes:
         out["config"]["ingest_bytes_per_event"] = round(sum(comp_bytes) / len(comp_bytes) / E, 1)
-        out["config"]["lz4_ratio"] = round((sum(sizes) / len(sizes) - 16) / (sum(comp_bytes) / len(comp_bytes)), 2)
+        out["config"]["compression_ratio"] = round((sum(sizes) / len(sizes) - 16) / (sum(comp_bytes) / len(comp_bytes)),
+                                                   2)
         out["config"]["lz4_level"] = args.lz4_level
         out["config"]["lz4_block_bytes"] = lz4_block_k
     if source == "kafka":
@@ -619,6 +623,8 @@ def main():
             out["config"]["kafka_batch_size"] = args.kafka_batch_size
         out["config"]["check_crcs"] = args.crc
         out["config"]["kafka_codec"] = args.kafka_codec
+        if args.kafka_codec == "zstd":
+            out["config"]["zstd_level"] = args.zstd_level
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
         out["latency_trace_ms"] = [round(x * 1e3, 2) for x in lat]

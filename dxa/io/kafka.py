@@ -64,17 +64,83 @@ def _lib():
     return _LIB
 
 
+def _codec_fns():
+    L = _lib()
+    if not hasattr(L, "_codecs_bound"):
+        p, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        for name, args in (("dxa_snappy_compress", [p, i64, p, i64, i32]), ("dxa_snappy_decompress", [p, i64, p, i64]),
+                           ("dxa_snappy_length", [p, i64]), ("dxa_zstd_decompress", [p, i64, p, i64]),
+                           ("dxa_zstd_bound", [p, i64]), ("dxa_zstd_compress", [p, i64, p, i64, i32, i32]),
+                           ("dxa_zstd_compress_bound", [i64])):
+            f = getattr(L, name)
+            f.argtypes, f.restype = args, i64
+        L._codecs_bound = True
+    return L
+
+
+def snappy_compress(data: bytes, xerial: bool = True) -> bytes:
+    """snappy-java's xerial stream (what Java producers write) or one raw block."""
+    L = _codec_fns()
+    cap = 256 + len(data) * 2
+    out = ctypes.create_string_buffer(cap)
+    n = L.dxa_snappy_compress(data, len(data), out, cap, int(xerial))
+    if n < 0:
+        raise KafkaError("snappy compress failed")
+    return out.raw[:n]
+
+
+def snappy_decompress(data: bytes) -> bytes:
+    """xerial stream or raw block → bytes (the host decoder of codec 2)."""
+    L = _codec_fns()
+    m = L.dxa_snappy_length(data, len(data))
+    if m < 0:
+        raise KafkaError("malformed snappy payload")
+    out = ctypes.create_string_buffer(max(1, m))
+    if L.dxa_snappy_decompress(data, len(data), out, m) != m:
+        raise KafkaError("malformed snappy payload")
+    return out.raw[:m]
+
+
+def zstd_compress(data: bytes, level: int = 3, content_size: bool = False,
+                  checksum: bool = False) -> bytes:
+    """One zstd frame from the system libzstd (the producer side: Kafka's zstd-jni stream omits the content size)."""
+    L = _codec_fns()
+    cap = L.dxa_zstd_compress_bound(len(data))
+    if cap < 0:
+        raise KafkaError("libzstd is not installed")
+    out = ctypes.create_string_buffer(cap)
+    n = L.dxa_zstd_compress(data, len(data), out, cap, level, int(content_size) | (int(checksum) << 1))
+    if n < 0:
+        raise KafkaError("zstd compress failed")
+    return out.raw[:n]
+
+
+def zstd_decompress(data: bytes) -> bytes:
+    """Frames → bytes with this package's decoder (host_zstd.cpp, RFC 8878; no libzstd involved)."""
+    L = _codec_fns()
+    bound = L.dxa_zstd_bound(data, len(data))
+    if bound < 0:
+        raise KafkaError("malformed zstd frame")
+    out = ctypes.create_string_buffer(max(1, bound))
+    m = L.dxa_zstd_decompress(data, len(data), out, bound)
+    if m < 0:
+        raise KafkaError(f"malformed zstd frame (error {m})")
+    return out.raw[:m]
+
+
 def crc32c(data: bytes) -> int:
     return int(_lib().dxa_crc32c(data, len(data)))
 
 
-CODECS = {"none": 0, "gzip": 1, "lz4": 3}
+CODECS = {"none": 0, "gzip": 1, "snappy": 2, "lz4": 3, "zstd": 4}
+ZSTD_DEFAULT_LEVEL = 3            # Kafka's compression.zstd.level default (zstd's own default)
 
 
 def encode_batch(values: Sequence[bytes], timestamp_ms: Optional[int] = None, compression: str = "none",
                  level: int = 1, block_size: int = 64 * 1024) -> bytes:
-    """One v2 record batch holding ``values`` (null keys); ``compression`` none / gzip / lz4 (``level`` and LZ4
-    frame ``block_size`` as Kafka's compression.lz4.level / the producer's block size)."""
+    """One v2 record batch holding ``values`` (null keys); ``compression`` none / gzip / snappy / lz4 / zstd
+    (``level``: Kafka's compression.lz4.level or compression.zstd.level; ``block_size``: the LZ4 frame block size).
+    snappy is snappy-java's xerial stream (what the Java producer writes); zstd needs the system libzstd."""
     vals = b"".join(values)
     offs = np.zeros(len(values) + 1, dtype=np.int64)
     if values:
@@ -146,7 +212,7 @@ def records_per_batch(vals: np.ndarray, offs: np.ndarray, batch_size: int = KAFK
 
 
 _ERRS = {-2: "unsupported message format (magic != 2)", -3: "CRC mismatch", -4: "gzip decode failed",
-         -5: "unsupported compression codec (snappy/zstd)", -6: "lz4 decode failed"}
+         -5: "unsupported compression codec", -6: "record batch decompression failed (lz4 / snappy / zstd)"}
 
 
 def decode_records(record_set: bytes, min_offset: int, pad: int = 16, verify_crc: bool = True

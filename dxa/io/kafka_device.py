@@ -9,9 +9,12 @@ place through per-record [start, end) ranges — the bytes cross PCIe once, comp
 device.
 
 gzip batches (codec 1, the Event Hubs Kafka endpoint's codec) are inflated on the GPU too (``inflate.hip``: the
-planner strips the gzip header and takes the size from the ISIZE trailer).  Batches the GPU path does not take
-(snappy / zstd codecs, dependent-block LZ4 frames, compacted batches with offset gaps) make ``plan_fetch`` raise
-``Unsupported``; the source then decodes that fetch on the host.
+planner strips the gzip header and takes the size from the ISIZE trailer), snappy batches (codec 2: snappy-java's
+xerial stream split into its raw blocks, exact sizes from their preambles) by ``snappy.hip`` and zstd batches
+(codec 4: one frame per batch, a capacity slot of blocks x block maximum, size reported by the kernel) by
+``zstd.hip``.  Batches the GPU path does not take (dependent-block LZ4 frames, zstd dictionaries, compacted
+batches with offset gaps) make ``plan_fetch`` raise ``Unsupported``; the source then decodes that fetch on the
+host.
 CRC-32C (the consumer's ``check.crcs``, on by default) is verified by the host planner (SSE4.2 ``crc32``, ~8 GB/s
 per planner thread) or, with ``DeviceRecordDecoder(verify_crc=True)``, on the GPU over the compressed bytes already
 in HBM (``kafka_crc_kernel``: one wave per batch, lane-interleaved words combined in GF(2)).  Measured on MI355X
@@ -350,7 +353,8 @@ class DeviceRecordDecoder:
         st = self.decode_stream.cuda_stream
         nb = plan.nblk
         chunks = max(1, min(self.chunks, nb // max(1, self.min_blocks_per_chunk)))
-        has_gzip = bool(nb) and bool((plan.k_stored[:nb] == 2).any())
+        kinds = set(np.unique(plan.k_stored[:nb]).tolist()) if nb else set()
+        has_gzip, has_snappy, has_zstd = 2 in kinds, 3 in kinds, 4 in kinds
         bounds = np.linspace(0, nb, chunks + 1).astype(np.int64)
         ev_last = tab_ev
         copied = 0                 # staging bytes already sent: chunks are contiguous from byte 0 (the batch headers
@@ -370,10 +374,14 @@ class DeviceRecordDecoder:
             N.call("dxa_lz4_decode_into", N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
                    N.ptr(oo[b0:b1]), N.ptr(cap[b0:b1]), b1 - b0, N.ptr(out), N.ptr(produced[b0:b1]),
                    N.ptr(bstat[b0:b1]), st)
-            if has_gzip:                   # gzip batches (kind 2) of the chunk: inflate.hip
-                N.call("dxa_inflate_into", N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
-                       N.ptr(oo[b0:b1]), N.ptr(cap[b0:b1]), b1 - b0, N.ptr(out), N.ptr(produced[b0:b1]),
-                       N.ptr(bstat[b0:b1]), st)
+            # the other codecs' entries of the chunk: gzip members (kind 2, inflate.hip), snappy raw blocks
+            # (kind 3, snappy.hip), zstd frames (kind 4, zstd.hip); each kernel skips the kinds it does not own
+            for present, entry in ((has_gzip, "dxa_inflate_into"), (has_snappy, "dxa_snappy_decode_into"),
+                                   (has_zstd, "dxa_zstd_decode_into")):
+                if present:
+                    N.call(entry, N.ptr(ddata), N.ptr(co[b0:b1]), N.ptr(cl[b0:b1]), N.ptr(sd[b0:b1]),
+                           N.ptr(oo[b0:b1]), N.ptr(cap[b0:b1]), b1 - b0, N.ptr(out), N.ptr(produced[b0:b1]),
+                           N.ptr(bstat[b0:b1]), st)
         with torch.cuda.stream(self.decode_stream):
             offs[n:].fill_(plan.out_bytes)
         N.call("dxa_kafka_records", N.ptr(out), plan.nbat, N.ptr(bc), N.ptr(bs), N.ptr(bk), N.ptr(bf), N.ptr(bn),
@@ -543,6 +551,12 @@ def decode_on_host_like(staging: np.ndarray, plan: FetchPlan, verify_crc: bool =
             if kind == 2:                          # deflate data of a gzip member (header / trailer stripped)
                 import zlib
                 raw = zlib.decompressobj(-15).decompress(src.tobytes())
+            elif kind == 3:                        # a snappy raw block
+                from .kafka import snappy_decompress
+                raw = snappy_decompress(src.tobytes())
+            elif kind == 4:                        # a zstd frame
+                from .kafka import zstd_decompress
+                raw = zstd_decompress(src.tobytes())
             else:
                 raw = src.tobytes() if kind else lz4.decompress_block(src.tobytes(), int(plan.k_cap[b]))
             out[end:end + len(raw)] = np.frombuffer(raw, np.uint8)

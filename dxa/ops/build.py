@@ -87,7 +87,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
         objs = list(ex.map(compile_one, hip_srcs))
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), *LINK_LIBS, "-o", str(LIB)])
     if host_srcs:
-        _run(["g++", *HOST_FLAGS, "-shared", *map(str, host_srcs), "-I", str(CSRC), "-lz", "-o", str(HOST_LIB)])
+        _run(["g++", *HOST_FLAGS, "-shared", *map(str, host_srcs), "-I", str(CSRC), "-lz", "-ldl", "-o", str(HOST_LIB)])
     for o in objs:
         o.unlink(missing_ok=True)
     stamp.write_text(digest)

@@ -19,6 +19,8 @@
 #include <zlib.h>
 
 #include "dxa_lz4.h"
+#include "dxa_snappy.h"
+#include "dxa_zstd.h"
 
 namespace {
 
@@ -244,8 +246,26 @@ int walk_batches(const uint8_t* data, int64_t len, int64_t min_offset, int64_t m
         if (!lz4_unframe(recs, (size_t)(bend - recs), raw)) return -6;
         rc = walk_records((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + raw.size(), count, base,
                           min_offset, s);
+      } else if (codec == 2) {
+        // snappy: snappy-java's xerial stream (Java producers) or one raw block (librdkafka)
+        const int64_t m = dxa::snappy::payload_length(recs, bend - recs);
+        if (m < 0) return -6;
+        std::string raw((size_t)m, '\0');
+        if (dxa::snappy::decompress_payload(recs, bend - recs, (uint8_t*)&raw[0], m) != m) return -6;
+        rc = walk_records((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + raw.size(), count, base,
+                          min_offset, s);
+      } else if (codec == 4) {
+        // zstd: one frame (zstd-jni's ZstdOutputStream; no content size, so decode into a bound-sized buffer)
+        const int64_t bound = dxa::zstd::decompressed_bound(recs, bend - recs);
+        if (bound < 0) return -6;
+        std::string raw((size_t)bound, '\0');
+        const int64_t m = dxa::zstd::decompress(recs, bend - recs, (uint8_t*)&raw[0], bound);
+        if (m < 0) return -6;
+        raw.resize((size_t)m);
+        rc = walk_records((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + raw.size(), count, base,
+                          min_offset, s);
       } else {
-        return -5;                                     // snappy / zstd: not built in
+        return -5;                                     // unknown codec
       }
       if (rc) return rc;
     }
@@ -369,6 +389,60 @@ int plan_batches(const uint8_t* data, int64_t len, int64_t min_offset, Plan& pl,
         if (isize > pl.max_block) pl.max_block = (int32_t)isize;
         pl.out_bytes += isize;
         ++pl.nblk;
+      } else if (codec == 2) {
+        // snappy: every xerial chunk (or the one raw block) is an independent raw block with its exact size in
+        // its varint preamble — kind 3, decoded by snappy.hip
+        if (dxa::snappy::is_xerial(recs, bend - recs)) {
+          const int64_t nc = dxa::snappy::xerial_chunks(recs, bend - recs, nullptr, nullptr, nullptr, 0);
+          if (nc < 0) return -7;
+          std::vector<int64_t> co((size_t)nc), ol((size_t)nc);
+          std::vector<int32_t> cl((size_t)nc);
+          dxa::snappy::xerial_chunks(recs, bend - recs, co.data(), cl.data(), ol.data(), nc);
+          for (int64_t k = 0; k < nc; ++k) {
+            if (pl.write) {
+              pl.k_comp_off[pl.nblk] = recs + co[(size_t)k] - data;
+              pl.k_comp_len[pl.nblk] = cl[(size_t)k];
+              pl.k_stored[pl.nblk] = 3;
+              pl.k_out_off[pl.nblk] = pl.out_bytes;
+              pl.k_cap[pl.nblk] = ol[(size_t)k];
+            }
+            if (ol[(size_t)k] > pl.max_block) pl.max_block = (int32_t)ol[(size_t)k];
+            pl.out_bytes += ol[(size_t)k];
+            ++pl.nblk;
+          }
+        } else {
+          const int64_t m = dxa::snappy::raw_length(recs, bend - recs, nullptr);
+          if (m < 0) return -7;
+          if (pl.write) {
+            pl.k_comp_off[pl.nblk] = recs - data;
+            pl.k_comp_len[pl.nblk] = (int32_t)(bend - recs);
+            pl.k_stored[pl.nblk] = 3;
+            pl.k_out_off[pl.nblk] = pl.out_bytes;
+            pl.k_cap[pl.nblk] = m;
+          }
+          if (m > pl.max_block) pl.max_block = (int32_t)m;
+          pl.out_bytes += m;
+          ++pl.nblk;
+        }
+      } else if (codec == 4) {
+        // zstd: one slot per frame (its blocks share the window, repeat offsets and entropy tables, so one wave
+        // decodes the whole frame — zstd.hip); the slot is the frame's bound and the kernel reports the size
+        const uint8_t* f = recs;
+        while (f < bend) {
+          dxa::zstd::FrameInfo fi;
+          if (dxa::zstd::frame_info(f, bend - f, &fi) != 0) return -5;
+          if (pl.write) {
+            pl.k_comp_off[pl.nblk] = f - data;
+            pl.k_comp_len[pl.nblk] = (int32_t)fi.end;
+            pl.k_stored[pl.nblk] = 4;
+            pl.k_out_off[pl.nblk] = pl.out_bytes;
+            pl.k_cap[pl.nblk] = fi.bound;
+          }
+          if (fi.bound > pl.max_block) pl.max_block = (int32_t)fi.bound;
+          pl.out_bytes += fi.bound;
+          ++pl.nblk;
+          f += fi.end;
+        }
       } else {
         return -5;
       }
@@ -454,8 +528,12 @@ __attribute__((visibility("default"))) int dxa_kafka_extract(const uint8_t* data
   return rc;
 }
 
-// Encode n values (vals + offs[n+1]) as one v2 batch (codec 0 none, 1 gzip, 3 lz4) (baseOffset 0); returns malloc'd
-// bytes.  lz4: one frame of `block_size` blocks at compression `level` (Kafka compression.lz4.level).
+int64_t dxa_zstd_compress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t level, int32_t flags);
+int64_t dxa_zstd_compress_bound(int64_t n);
+
+// Encode n values (vals + offs[n+1]) as one v2 batch (codec 0 none, 1 gzip, 2 snappy, 3 lz4, 4 zstd) (baseOffset 0);
+// returns malloc'd bytes.  lz4: one frame of `block_size` blocks at compression `level` (Kafka
+// compression.lz4.level); zstd: one frame at zstd `level`.
 __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode_lz4(const uint8_t* vals, const int64_t* offs,
                                                                     int64_t n, int64_t timestamp_ms, int32_t codec,
                                                                     int32_t level, int32_t block_size,
@@ -493,6 +571,23 @@ __attribute__((visibility("default"))) uint8_t* dxa_kafka_encode_lz4(const uint8
     std::string z((size_t)dxa::lz4::frame_bound((int64_t)recs.size(), block_size), '\0');
     const int64_t m = dxa::lz4::compress_frame((const uint8_t*)recs.data(), (int64_t)recs.size(), (uint8_t*)&z[0],
                                                (int64_t)z.size(), block_size, 1, level);
+    if (m < 0) return nullptr;
+    z.resize((size_t)m);
+    recs.swap(z);
+  } else if (codec == 2) {
+    // snappy as the Java producer writes it: snappy-java's xerial stream of 32 KiB chunks
+    std::string z((size_t)dxa::snappy::xerial_bound((int64_t)recs.size()), '\0');
+    const int64_t m = dxa::snappy::xerial_compress((const uint8_t*)recs.data(), (int64_t)recs.size(),
+                                                   (uint8_t*)&z[0]);
+    z.resize((size_t)m);
+    recs.swap(z);
+  } else if (codec == 4) {
+    // zstd at `level` (Kafka compression.zstd.level, default 3) through the system libzstd, as zstd-jni would
+    const int64_t bound = dxa_zstd_compress_bound((int64_t)recs.size());
+    if (bound < 0) return nullptr;
+    std::string z((size_t)bound, '\0');
+    const int64_t m = dxa_zstd_compress((const uint8_t*)recs.data(), (int64_t)recs.size(), (uint8_t*)&z[0], bound,
+                                        level, 0);          // no content size, no checksum: zstd-jni's stream
     if (m < 0) return nullptr;
     z.resize((size_t)m);
     recs.swap(z);
