@@ -209,7 +209,7 @@ def main():
         native.lib()
     from dxa.engine.processor import Processor, RawBatch
     from dxa.models import iot
-    from dxa.simulate.datagen import generate, generate_begin, generate_finish, generate_slotted
+    from dxa.simulate.datagen import generate, generate_begin, generate_finish
     from dxa import parallel
 
     if world > 1:
@@ -359,18 +359,6 @@ def main():
             def gen_args(j):
                 return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=batch_time(j) // 1000 - 1000,
                             step_us=max(1, interval_us // E))
-            if os.environ.get("DXA_GEN_SLOTTED", "0") == "1":
-                # one render launch per batch into fixed-size slots (no length pass, scan or host size read); off by
-                # default: measured within run-to-run noise of the two-pass path (profiles/gen_slot)
-                ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
-                with ctx:
-                    db, do, de = generate_slotted(prog, E, device, **gen_args(i))
-                    ev = None
-                    if side is not None:
-                        ev = torch.cuda.Event()
-                        ev.record(side)
-                staged[i] = (RawBatch(db, do, E, ends=de), None, ev)
-                return
             if side is None:
                 staged[i] = generate(prog, E, device, **gen_args(i)) + (None,)
                 return
@@ -485,10 +473,6 @@ def main():
 
     from dxa.utils import settle_gc
     settle_gc()
-    if on_gpu and os.environ.get("DXA_BENCH_HIPRIO", "0") == "1":
-        # the batch's query kernels on a high-priority stream: the parse-ahead and generator streams (normal
-        # priority) fill the CUs the small query kernels leave idle without delaying them
-        torch.cuda.set_stream(torch.cuda.Stream(device, priority=torch.cuda.Stream.priority_range()[1]))
     depth = max(1, args.prefetch)
     for i in range(depth):
         stage(i)

@@ -217,6 +217,7 @@ __device__ bool build_fse(ZTables& T, int nsym, int log, uint32_t* tab) {
   int high = size - 1;
   for (int s = 0; s < nsym; ++s) {
     if (T.norm[s] == -1) {
+      if (high < 0) return false;
       tab[high--] = (uint32_t)s << 8;
       T.nxt[s] = 1;
     } else {
@@ -225,8 +226,12 @@ __device__ bool build_fse(ZTables& T, int nsym, int log, uint32_t* tab) {
   }
   const int step = (size >> 1) + (size >> 3) + 3;
   int pos = 0;
+  if (high < 0) return false;
+  int placed = 0;
   for (int s = 0; s < nsym; ++s) {
     const int cnt = T.norm[s];
+    placed += cnt > 0 ? cnt : 0;
+    if (placed > high + 1) return false;                  // more cells than the table holds
     for (int i = 0; i < cnt; ++i) {
       tab[pos] = (uint32_t)s << 8;
       do { pos = (pos + step) & (size - 1); } while (pos > high);
