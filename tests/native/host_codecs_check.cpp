@@ -93,10 +93,55 @@ static void lz4_checks(uint32_t seed) {
   }
 }
 
+extern "C" {
+int64_t dxa_snappy_compress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t xerial);
+int64_t dxa_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
+int64_t dxa_zstd_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
+int64_t dxa_zstd_compress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t level, int32_t flags);
+}
+
+// snappy and zstd: round trips, truncated streams and garbage inputs return errors, never overrun
+static void snappy_zstd_checks(uint32_t seed) {
+  for (int64_t n : {0, 1, 100, 5000, 40000, 140000}) {
+    std::vector<uint8_t> src((size_t)n);
+    for (auto& b : src) { seed = seed * 1664525u + 1013904223u; b = (uint8_t)"{\"a\":12,"[(seed >> 24) % 8]; }
+    for (int xer : {0, 1}) {
+      std::vector<uint8_t> z((size_t)(256 + 2 * n)), out((size_t)n + 1);
+      const int64_t m = dxa_snappy_compress(src.data(), n, z.data(), (int64_t)z.size(), xer);
+      CHECK(m > 0);
+      CHECK(dxa_snappy_decompress(z.data(), m, out.data(), n) == n);
+      CHECK(n == 0 || std::memcmp(out.data(), src.data(), (size_t)n) == 0);
+      for (int64_t cut = 0; cut < m; cut += 1 + m / 7) CHECK(dxa_snappy_decompress(z.data(), cut, out.data(), n) != n ||
+                                                              cut == m);
+    }
+    std::vector<uint8_t> z((size_t)(1024 + 2 * n)), out((size_t)n + 64);
+    const int64_t m = dxa_zstd_compress(src.data(), n, z.data(), (int64_t)z.size(), 3, 0);
+    if (m > 0) {                                                 // libzstd present
+      CHECK(dxa_zstd_decompress(z.data(), m, out.data(), (int64_t)out.size()) == n);
+      CHECK(n == 0 || std::memcmp(out.data(), src.data(), (size_t)n) == 0);
+      for (int64_t cut = 0; cut < m; cut += 1 + m / 9) {
+        const int64_t r = dxa_zstd_decompress(z.data(), cut, out.data(), (int64_t)out.size());
+        CHECK(r < 0 || r <= (int64_t)out.size());
+      }
+    }
+  }
+  std::vector<uint8_t> junk(4096), out(70000);
+  for (int t = 0; t < 300; ++t) {
+    for (auto& b : junk) { seed = seed * 1664525u + 1013904223u; b = (uint8_t)(seed >> 24); }
+    if (t & 1) { junk[0] = 0x28; junk[1] = 0xB5; junk[2] = 0x2F; junk[3] = 0xFD; }   // zstd magic, garbage body
+    const int64_t len = (int64_t)(seed % 4096);
+    const int64_t r = dxa_zstd_decompress(junk.data(), len, out.data(), (int64_t)out.size());
+    CHECK(r <= (int64_t)out.size());
+    const int64_t q = dxa_snappy_decompress(junk.data(), len, out.data(), (int64_t)out.size());
+    CHECK(q <= (int64_t)out.size());
+  }
+}
+
 int main() {
+  snappy_zstd_checks(5u);
   CHECK(dxa_crc32c((const uint8_t*)"123456789", 9) == 0xE3069283u);
   CHECK(dxa_crc32c((const uint8_t*)"", 0) == 0u);
-  for (int codec : {0, 1, 3})
+  for (int codec : {0, 1, 2, 3, 4})
     for (int n : {0, 1, 2, 17, 200}) kafka_roundtrip(n, 7u + n, codec);
   lz4_checks(99u);
   char buf[64];
