@@ -22,6 +22,7 @@ namespace {
 enum : int32_t {
   FT_STRUCT = 0, FT_BOOL = 1, FT_LONG = 2, FT_DOUBLE = 3, FT_STRING = 4, FT_RAW = 5,
   FT_TIMESTAMP = 6, FT_INT = 7, FT_DATE = 8, FT_DECIMAL = 9,   // FT_DECIMAL: the number token's text (decimal.hip)
+  FT_SKIP = 10,               // a pruned field: matched in schema order (cheap), its value skipped unstored
 };
 
 struct ParseArgs {
@@ -814,7 +815,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
       ++r.p;
       r.skip_ws();
       c = r.cur();
-      if (node < 0) goto skip_any;
+      if (node < 0 || (tb.node_type[node] & 0xff) == FT_SKIP) goto skip_any;
       const int t = tb.node_type[node] & 0xff;
       const bool raw_arr = (tb.node_type[node] & 0x100) != 0;
       const int vs = tb.val_slot[node];

@@ -24,6 +24,9 @@ from ..engine.types import ArrayType, MapType, StructField, StructType
 FT = {"struct": 0, "boolean": 1, "long": 2, "double": 3, "float": 3, "decimal": 3, "string": 4, "raw": 5,
       "timestamp": 6, "int": 7, "date": 8, "decimal_exact": 9}
 FT_DECIMAL = 9          # decimal(p,s): the kernel keeps the number token's text; decimal.hip converts it exactly
+FT_SKIP = 10            # a field no statement reads (column pruning): its key still matches in schema order, its value
+#                         is skipped unstored — dropping the node instead would make every such key a failed
+#                         speculation plus a full-key hash (measured: -2.4 % on the groupby flow)
 
 FNV_BASIS = 0xcbf29ce484222325
 FNV_PRIME = 0x100000001b3
@@ -70,7 +73,7 @@ class ParsePlan:
         self._build(schema, 0, ())
         nv = nl = 0
         for nd in self.nodes[1:]:
-            if nd.code != 0:
+            if nd.code not in (0, FT_SKIP):
                 nd.val_slot = nv
                 nv += 1
                 if nd.code in (4, 5, FT_DECIMAL):
@@ -122,6 +125,7 @@ class ParsePlan:
         for f in st.fields:
             path = prefix + (f.name,)
             if not self._wanted(path):
+                self.nodes.append(Node(path, parent, f.name, f.dtype, FT_SKIP))     # a whole subtree, unread
                 continue
             if isinstance(f.dtype, StructType):
                 self.nodes.append(Node(path, parent, f.name, f.dtype, 0))
@@ -327,9 +331,12 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
     cols: Dict[int, object] = {}
     for idx in range(len(plan.nodes) - 1, 0, -1):
         nd = plan.nodes[idx]
+        if nd.code == FT_SKIP:
+            continue
         v = valid[idx] if (nulls is None or nulls[idx]) else None   # complete columns carry no mask
         if nd.code == 0:
-            kids = [(plan.nodes[j].name, cols[j]) for j in range(len(plan.nodes)) if plan.nodes[j].parent == idx]
+            kids = [(plan.nodes[j].name, cols[j]) for j in range(len(plan.nodes))
+                    if plan.nodes[j].parent == idx and j in cols]
             cols[idx] = StructColumn([k for k, _ in kids], [c for _, c in kids], n, v, False, None, device)
             continue
         raw = vals[nd.val_slot]
@@ -346,7 +353,7 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
             cols[idx] = PrimColumn("boolean", raw != 0, v)
         else:
             cols[idx] = PrimColumn(nd.dtype, raw, v)
-    kids = [(plan.nodes[j].name, cols[j]) for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == 0]
+    kids = [(plan.nodes[j].name, cols[j]) for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == 0 and j in cols]
     root_valid = valid[0] if (nulls is None or nulls[0]) else None
     return StructColumn([k for k, _ in kids], [c for _, c in kids], n, root_valid, False, None, device)
 
@@ -463,7 +470,7 @@ def _parse_cpu(buf, offs, n, plan: ParsePlan, ends=None):
             ok.append(False)
 
     def build(idx, getters):
-        kids = [j for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == idx]
+        kids = [j for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == idx and plan.nodes[j].code != FT_SKIP]
         names, cols = [], []
         for j in kids:
             nd = plan.nodes[j]
