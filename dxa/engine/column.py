@@ -124,15 +124,16 @@ def _plan_take(c: "Column", idx: torch.Tensor, leaves: List[torch.Tensor]):
         n = int(idx.shape[0])
         return lambda g: StructColumn(c.names, [b(g) for b in kids], n, g[i] if has_v else None, c.is_map,
                                       c.dtype, c.device)
+    if isinstance(c, ArrayColumn) and c.present is not None:
+        taken = c.take(idx)                   # a [rows x slots] presence mask: not a 1-D leaf of the batched gather
+        return lambda g: taken
     if isinstance(c, ArrayColumn):
         i = len(leaves)
         if c.valid is not None:
             leaves.append(c.valid)
         has_v = c.valid is not None
         ip = len(leaves)
-        if c.present is not None:
-            leaves.append(c.present)
-        has_p = c.present is not None
+        has_p = False
         els = [_plan_take(e, idx, leaves) for e in c.elements]
         n = int(idx.shape[0])
         return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device,
@@ -345,9 +346,9 @@ class StructColumn(Column):
         return None
 
     def take(self, idx):
-        if idx.device.type == "cuda":
-            return take_columns([self], idx)[0]
-        return StructColumn(self.names, [c.take(idx) for c in self.children], int(idx.shape[0]),
+        # children through one batched gather on the GPU (take_columns); never take_columns([self]) here: its
+        # fallback for a layout it cannot batch is this method
+        return StructColumn(self.names, take_columns(self.children, idx), int(idx.shape[0]),
                             _take_valid(self.valid, idx), self.is_map, self.dtype, self._device)
 
     def with_valid(self, extra):
@@ -417,9 +418,7 @@ class ArrayColumn(Column):
         return None if self.present is None else self.present[:, j]
 
     def take(self, idx):
-        if idx.device.type == "cuda":
-            return take_columns([self], idx)[0]
-        return ArrayColumn([e.take(idx) for e in self.elements], int(idx.shape[0]), _take_valid(self.valid, idx),
+        return ArrayColumn(take_columns(self.elements, idx), int(idx.shape[0]), _take_valid(self.valid, idx),
                            self.drop_nulls, self._device,
                            present=None if self.present is None else self.present[idx])
 
