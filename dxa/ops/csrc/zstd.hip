@@ -90,26 +90,28 @@ struct BitB {
   const uint8_t* ptr;
   uint64_t c;
   int32_t used;                         // bits consumed from the top of c
+  int32_t pad;                          // zero bits below the stream start at the bottom of c (streams < 8 bytes)
   __device__ bool init(const uint8_t* s, int32_t n) {
     start = s;
     if (n <= 0) return false;
     const uint32_t last = s[n - 1];
     if (last == 0) return false;
+    used = 8 - highbit32(last);         // the zero bits above the end marker, and the marker
     if (n >= 8) {
       ptr = s + n - 8;
       c = ld64(ptr);
-      used = 8 - highbit32(last);
+      pad = 0;
     } else {
       ptr = s;
       uint64_t v = 0;
       for (int k = 0; k < n; ++k) v |= (uint64_t)s[k] << (8 * k);
-      c = v << (8 * (8 - n));
-      used = 8 * (8 - n) + 8 - highbit32(last);
+      c = v << (8 * (8 - n));            // the stream's bytes at the top, as an 8-byte load would hold them
+      pad = 8 * (8 - n);
     }
     return true;
   }
   // bits remaining (negative once more were read than the stream holds)
-  __device__ __forceinline__ int32_t left() const { return (int32_t)(ptr - start) * 8 + 64 - used; }
+  __device__ __forceinline__ int32_t left() const { return (int32_t)(ptr - start) * 8 + 64 - used - pad; }
   __device__ __forceinline__ void reload() {
     if (used < 8) return;
     int32_t nb = used >> 3;
