@@ -217,7 +217,7 @@ Tagged = ProcessRules(DataXProcessedInput);
 --DataXQuery--
 UnhealthyDevices = SELECT deviceName, deviceType, homeId, AvgHealth
     FROM DeviceNamed
-    WHERE AvgHealth < 45;
+    WHERE AvgHealth < 49.8;
 
 OUTPUT UnhealthyDevices TO Metrics;
 """
