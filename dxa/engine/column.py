@@ -244,6 +244,8 @@ class StrColumn(Column):
         starts = self.starts.cpu().tolist()
         lens = self.lens.cpu().tolist()
         valid = self.valid.cpu().tolist() if self.valid is not None else [True] * self.length
+        if self.dtype == "binary":
+            return [arena[s:s + l] if ok else None for s, l, ok in zip(starts, lens, valid)]
         out = []
         for s, l, ok in zip(starts, lens, valid):
             out.append(arena[s:s + l].decode("utf-8", errors="replace") if ok else None)

@@ -273,6 +273,11 @@ def _relation(src, catalog: Catalog, ctx: EvalContext) -> Scope:
         t = execute(src.query, catalog, ctx)
         if src.sample:
             t = _sample(t, src.sample)
+        if src.columns:
+            if len(src.columns) != len(t.columns):
+                raise QueryError(f"{src.alias}({', '.join(src.columns)}) names {len(src.columns)} columns; "
+                                 f"the relation has {len(t.columns)}")
+            t = Table(list(src.columns), t.columns, t.length, t.device)
         sc = Scope.of_table(t, src.alias)
         sc.dist = P.dist_of(t)
         return sc

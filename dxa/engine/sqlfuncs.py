@@ -608,7 +608,7 @@ def _sha2(s, bits=256):
     bits = int(bits)
     h = {224: hashlib.sha224, 256: hashlib.sha256, 0: hashlib.sha256, 384: hashlib.sha384,
          512: hashlib.sha512}.get(bits)
-    return None if h is None else h(str(s).encode()).hexdigest()
+    return None if h is None else h(_bytes_of(s)).hexdigest()
 
 
 def _java_regex(p):
@@ -708,7 +708,12 @@ def _f_digest(kind, host, out_type="string"):
 def _hex(v):
     if isinstance(v, (int, bool)) and not isinstance(v, bool):
         return format(v & 0xFFFFFFFFFFFFFFFF, "X") if v < 0 else format(v, "X")
-    return str(v).encode().hex().upper()
+    return _bytes_of(v).hex().upper()
+
+
+def _bytes_of(v) -> bytes:
+    """A string's UTF-8 bytes, or a binary value's own bytes (encode / unhex / unbase64 results)."""
+    return bytes(v) if isinstance(v, (bytes, bytearray)) else str(v).encode()
 
 
 def _initcap(s):
@@ -1319,11 +1324,11 @@ def _register():
     reg("regexp_extract", _f_regexp("extract"))
     reg("regexp_replace", _f_regexp("replace"))
     reg("sha2", _f_digest(_sha2_kind, _sha2))
-    reg("sha", _f_digest(1, lambda s: hashlib.sha1(str(s).encode()).hexdigest()))
-    reg("sha1", _f_digest(1, lambda s: hashlib.sha1(str(s).encode()).hexdigest()))
-    reg("md5", _f_digest(0, lambda s: hashlib.md5(str(s).encode()).hexdigest()))
-    reg("crc32", _f_digest("crc32", lambda s: zlib.crc32(str(s).encode()) & 0xFFFFFFFF, "long"))
-    reg("base64", _f_digest("base64", lambda s: _b64.b64encode(str(s).encode()).decode()))
+    reg("sha", _f_digest(1, lambda s: hashlib.sha1(_bytes_of(s)).hexdigest()))
+    reg("sha1", _f_digest(1, lambda s: hashlib.sha1(_bytes_of(s)).hexdigest()))
+    reg("md5", _f_digest(0, lambda s: hashlib.md5(_bytes_of(s)).hexdigest()))
+    reg("crc32", _f_digest("crc32", lambda s: zlib.crc32(_bytes_of(s)) & 0xFFFFFFFF, "long"))
+    reg("base64", _f_digest("base64", lambda s: _b64.b64encode(_bytes_of(s)).decode()))
     reg("unbase64", _host_string_fn(lambda s: _unbase64(s)))
     reg("hex", _f_digest("hex", _hex))
     reg("unhex", _host_string_fn(lambda s: _unhex(s)))

@@ -238,6 +238,7 @@ class SubqueryRef:
     query: "Query"
     alias: Optional[str] = None
     sample: Optional[tuple] = None
+    columns: Optional[tuple] = None        # ``(…) AS t(x, y)``: the output columns renamed positionally
 
 
 @dataclass(eq=False)

@@ -566,38 +566,31 @@ class Parser:
         t = self.peek()
         return t.kind in ("id", "kw") and t.text.lower() in ("select", "with", "values")
 
-    def _rename_columns(self, q: A.Query, alias, names):
-        """``… AS t(x, y)``: the relation's columns renamed positionally (a projection over it)."""
-        inner = A.SubqueryRef(q, "__v")
-        items = [A.SelectItem(A.Ident(("__v", f"col{i + 1}")), nm) for i, nm in enumerate(names)]
-        return A.SubqueryRef(A.Query(A.Select(items=items, from_=inner)), alias)
+    def _alias_columns(self):
+        """``AS t`` / ``t`` / ``AS t(x, y)`` after a derived table → (alias, column names or None)."""
+        alias, cols = None, []
+        if self.accept_kw("as"):
+            alias = self.ident()
+        elif self._alias_word_ok():
+            alias = self.advance().text
+        if alias is not None and self.accept_op("("):
+            cols.append(self.ident())
+            while self.accept_op(","):
+                cols.append(self.ident())
+            self.expect_op(")")
+        return alias, (tuple(cols) or None)
 
     def parse_table_primary(self):
         if self.is_word("values") and (self.is_op("(", tok=self.peek()) or self.peek().kind in ("num", "str")):
             q = self._parse_values()
-            alias, cols = None, []
-            if self.accept_kw("as"):
-                alias = self.ident()
-            elif self._alias_word_ok():
-                alias = self.advance().text
-            if alias is not None and self.accept_op("("):
-                cols.append(self.ident())
-                while self.accept_op(","):
-                    cols.append(self.ident())
-                self.expect_op(")")
-            if cols:
-                return self._rename_columns(q, alias, cols)
-            return A.SubqueryRef(q, alias)
+            alias, cols = self._alias_columns()
+            return A.SubqueryRef(q, alias, None, cols)
         if self.accept_op("("):
             q = self.parse_query()
             self.expect_op(")")
             sample = self.parse_sample()
-            alias = None
-            if self.accept_kw("as"):
-                alias = self.ident()
-            elif self._alias_word_ok():
-                alias = self.advance().text
-            return A.SubqueryRef(q, alias, sample)
+            alias, cols = self._alias_columns()
+            return A.SubqueryRef(q, alias, sample, cols)
         name = self.ident()
         while self.accept_op("."):
             name += "." + self.ident()
