@@ -173,14 +173,13 @@ class PanedTable(Table):
 
 
 _TS_SCRATCH: Dict = {}
-_TS_KERNEL = __import__("os").environ.get("DXA_TS_STATS_KERNEL", "1") != "0"          # A/B switch
 
 
 def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int, lens_all: Optional[torch.Tensor] = None) -> List[int]:
     """[min, max, count] of the valid timestamps and the count of valid ones >= E — one reduction launch and one
     4-word read on the GPU (reduce_stats.hip), tensor ops on the CPU.  With ``lens_all`` (the pane's string lengths)
     a fifth word, their sum, comes back in the same read: the pane's compaction then needs no read of its own."""
-    if ts.is_cuda and ts.numel() and _TS_KERNEL:
+    if ts.is_cuda and ts.numel():
         from ..ops import native as N
         dev = ts.device
         scratch = _TS_SCRATCH.get(dev)

@@ -79,9 +79,8 @@ struct Tables {
 };
 
 template <bool WRITE>
-__device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int64_t i, uint8_t* dst,
-                                          uint8_t* stage = nullptr) {
-  dxa::Emitter<WRITE> e(dst, stage);
+__device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int64_t i, uint8_t* dst) {
+  dxa::Emitter<WRITE> e(dst);
   const uint64_t* pool64 = t.pool64;
   const int64_t row = g.row0 + i;
   int skip = 0;
@@ -218,18 +217,12 @@ __global__ __launch_bounds__(256) void gen_len_kernel(GenArgs g) {
   g.lens[i] = render<false>(g, t, i, nullptr);
 }
 
-// the lane's 64-B emitter staging slot, after the tables (lds_bytes, 16-B aligned)
-__device__ __forceinline__ uint8_t* stage_slot(const GenArgs& g, uint64_t* smem) {
-  const size_t tables = (lds_bytes_dev(g.nops, g.pool_words, g.table_ints) + 15) & ~(size_t)15;
-  return reinterpret_cast<uint8_t*>(smem) + tables + (size_t)threadIdx.x * dxa::kEmitStageBytes;
-}
-
 __global__ __launch_bounds__(256) void gen_write_kernel(GenArgs g) {
   extern __shared__ uint64_t smem[];
   const Tables t = stage_tables(g, smem);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.n) return;
-  render<true>(g, t, i, g.out + g.offs[i], stage_slot(g, smem));
+  render<true>(g, t, i, g.out + g.offs[i]);
 }
 
 // One pass, no length pass or scan: event i renders into its own 16-B aligned slot [i*stride, i*stride+len) (the
@@ -250,12 +243,6 @@ __global__ __launch_bounds__(256) void gen_slot_kernel(GenArgs g) {
 }
 
 size_t lds_bytes(int32_t nops, int32_t pool_words, int32_t table_ints) { return lds_bytes_dev(nops, pool_words, table_ints); }
-
-// the write pass adds the emitters' staging slots (DXA_EMIT_STAGE)
-size_t write_lds_bytes(int32_t nops, int32_t pool_words, int32_t table_ints) {
-  return DXA_EMIT_STAGE ? ((lds_bytes(nops, pool_words, table_ints) + 15) & ~(size_t)15) + 256 * dxa::kEmitStageBytes
-                        : lds_bytes(nops, pool_words, table_ints);
-}
 
 constexpr size_t kMaxLds = 64 * 1024;
 
@@ -284,7 +271,7 @@ DXA_API int dxa_datagen_write(const void* ops, int32_t nops, const uint8_t* pool
   GenArgs g{(const Op*)ops, nops, pool, table, pool_words, table_ints, seed, row0, n, base_ms, step_us, offs, out,
             nullptr, 0, nullptr};
   hipLaunchKernelGGL(gen_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),
-                     write_lds_bytes(nops, pool_words, table_ints), (hipStream_t)st, g);
+                     lds, (hipStream_t)st, g);
   return (int)hipGetLastError();
 }
 

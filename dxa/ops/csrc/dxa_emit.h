@@ -2,28 +2,14 @@
 #pragma once
 #include "dxa_common.h"
 
-// Full-word stores are ordinary write-back stores by default: a record's 16-B words arrive at one 128-B line over
-// several store instructions, and the L2 merges them into whole-line writes.  Nontemporal stores (DXA_EMIT_NT=1)
-// stream each 16-B piece past the L2 as its own partial-line write: the generator's write pass measured 1.79 ms
-// per 1 M IoT events with them vs 0.77 ms without (tools/gpu/gpu_gen_ab.sh).
-#ifndef DXA_EMIT_NT
-#define DXA_EMIT_NT 0
-#endif
-// Staged 64-B segments (DXA_EMIT_STAGE=1, an Emitter given an LDS slot): with ~64 K lanes per XCD each filling its
-// own line, half-written lines are evicted from the L2 and written back as partial-sector requests — PMC WRITE_SIZE
-// of the generator's write pass is 1.70 GB for 0.61 GB of text (2.8x), the serializer's 1.54 GB for 0.66 GB.  With
-// a slot, a lane's full words wait in LDS (64 B per lane, kEmitStageBytes) until their 64-B segment is complete and
-// leave as four back-to-back 16-B stores: measured on MI355X (profiles/pmc/passthrough_r4.md) that cuts the write
-// traffic to 0.72 / 0.75 GB, but the kernels do not get faster (gen_write 559 vs 544 us, ser_write 1134 vs 1043 us:
-// they are issue-bound, and the staging costs VGPRs — 71 -> 82 and 95 -> 103, one wave per SIMD less).  Off by
-// default; the variant build keeps it measurable.
-#ifndef DXA_EMIT_STAGE
-#define DXA_EMIT_STAGE 0
-#endif
+// Full-word stores are ordinary write-back stores: a record's 16-B words arrive at one 128-B line over several store
+// instructions and the L2 merges them into whole-line writes.  Measured and dropped: nontemporal stores (each 16-B
+// piece leaves as its own partial-line write: the generator's write pass 1.79 ms per 1 M IoT events vs 0.77 ms,
+// tools/gpu/gpu_gen_ab.sh) and LDS-staged 64-B segments per lane (PMC write traffic 1.70 -> 0.72 GB, but the
+// kernels are issue-bound and the staging cost VGPRs: gen_write 559 vs 544 us, ser_write 1134 vs 1043 us,
+// profiles/pmc/passthrough_r4.md).
 
 namespace dxa {
-
-constexpr int kEmitStageBytes = 64;     // LDS per lane for a staged Emitter
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
@@ -52,15 +38,9 @@ struct Emitter {
   bool first;          // still on the record's first word
   uint64_t a0, a1;     // current word
   uint64_t h0, h1;     // the first word, once full (written by finish)
-  uint8_t* stg;        // this lane's 64-B LDS staging slot, or null (direct 16-B stores)
-  uint32_t swz;        // slot swizzle (lane & 3): spreads the lanes' 16-B LDS writes over the banks
 
   __device__ __forceinline__ explicit Emitter(uint8_t* dst)
-      : Emitter(dst, nullptr) {}
-
-  __device__ __forceinline__ Emitter(uint8_t* dst, uint8_t* stage)
-      : len(0), lead(0), nacc(0), first(true), a0(0), a1(0), h0(0), h1(0), stg(DXA_EMIT_STAGE ? stage : nullptr),
-        swz(threadIdx.x & 3u) {
+      : len(0), lead(0), nacc(0), first(true), a0(0), a1(0), h0(0), h1(0) {
     if (WRITE) {
       lead = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
       wbase = hbase = dst - lead;
@@ -97,26 +77,7 @@ struct Emitter {
     u64x2 v;
     v.x = x0;
     v.y = x1;
-#if DXA_EMIT_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(w));
-#else
     *reinterpret_cast<u64x2*>(w) = v;
-#endif
-  }
-
-  __device__ __forceinline__ u64x2 staged(uint32_t slot) const {
-    return *reinterpret_cast<const u64x2*>(stg + 16 * (slot ^ swz));
-  }
-
-  // the staged words in slots [0, nslots) of the segment holding wbase that lie past the record's first word
-  __device__ __forceinline__ void flush_segment(uint32_t nslots) {
-    uint8_t* seg = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(wbase) & ~(uintptr_t)63);
-    for (uint32_t j = 0; j < 3; ++j) {
-      if (j < nslots && seg + 16 * j > hbase) {
-        const u64x2 v = staged(j);
-        store16(seg + 16 * j, v.x, v.y);
-      }
-    }
   }
 
   __device__ __forceinline__ void flush_full() {
@@ -124,17 +85,6 @@ struct Emitter {
       h0 = a0;
       h1 = a1;
       first = false;
-    } else if (stg != nullptr) {
-      const uint32_t slot = (uint32_t)(reinterpret_cast<uintptr_t>(wbase) >> 4) & 3u;
-      if (slot == 3) {                   // segment complete: slots 0..2 from LDS, slot 3 from registers
-        flush_segment(3);
-        store16(wbase, a0, a1);
-      } else {
-        u64x2 v;
-        v.x = a0;
-        v.y = a1;
-        *reinterpret_cast<u64x2*>(stg + 16 * (slot ^ swz)) = v;
-      }
     } else {
       store16(wbase, a0, a1);
     }
@@ -179,7 +129,6 @@ struct Emitter {
       if (first) {                       // the record never left its first word
         if (nacc > lead) store_range(hbase, a0, a1, lead, nacc);
       } else {
-        if (stg != nullptr) flush_segment((uint32_t)(reinterpret_cast<uintptr_t>(wbase) >> 4) & 3u);  // staged words
         if (lead == 0) {
           store16(hbase, h0, h1);
         } else {

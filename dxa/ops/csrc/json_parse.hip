@@ -169,36 +169,21 @@ __device__ __forceinline__ Tables<true> load_tables<true>(const GArgs& a) {
 
 constexpr int kMaxDepth = 8;
 
-// Per-lane byte window over the lane's record.  DXA_PARSE_REGWIN: 32 bytes in registers (two global_load_dwordx4 per refill).  Every byte and
-// 8-byte read (SWAR scans, key compares, timestamps) is served from it: lanes read 64 unrelated records, so each
-// load instruction touches 64 cache lines and the per-CU address path, not VALU, bounds the parser — reloading
-// only when the window is exhausted keeps that to ~2 loads per 32 record bytes.
-//
-// Default: a 64-byte per-lane window in LDS ([dword][lane], conflict-free), topped up at the
-// start of every field for all lanes that are low on bytes (``top_up``).  Lanes sit at different offsets of their
-// records, so per-lane refills stall a wave once per distinct refill point; refilling every low lane in the same
-// instruction makes that about one stall per field.  (A 64-byte *register* window needs 217 VGPRs.)  Measured on
-// the bench batch: 2.30 -> 1.75 ms, VMEM reads per wave 344 -> 220, VALU per wave 24.3 K -> 14.7 K.
-// DXA_PARSE_REGWIN selects the 32-byte register window (A/B runs).
-#if !defined(DXA_PARSE_REGWIN)
-#define DXA_PARSE_LDSWIN 1
-#endif
-#ifdef DXA_PARSE_LDSWIN
+// Per-lane byte window over the lane's record: 64 bytes in LDS ([dword][lane], conflict-free), topped up at the
+// start of every field for all lanes that are low on bytes (``top_up``).  Lanes read 64 unrelated records, so each
+// window load touches 64 cache lines and the per-CU address path, not VALU, bounds the parser.  Lanes sit at
+// different offsets of their records, so per-lane refills stall a wave once per distinct refill point; refilling
+// every low lane in the same instruction makes that about one stall per field.  (A 64-byte *register* window needs
+// 217 VGPRs.)  Measured on the bench batch against the previous 32-byte register window (two global_load_dwordx4
+// per refill): 2.30 -> 1.75 ms, VMEM reads per wave 344 -> 220, VALU per wave 24.3 K -> 14.7 K.
 constexpr uint32_t kWin = 64;
 #define G3U32 __attribute__((address_space(3))) uint32_t
-#else
-constexpr uint32_t kWin = 32;
-#endif
 struct Reader {
   gu8* buf;
   int64_t p, end;
   int64_t wb;                                             // window base offset (16-B aligned in memory)
   int64_t lim;                                            // window loads stay below buf + lim (last record + pad)
-#ifdef DXA_PARSE_LDSWIN
   G3U32* win;                                             // dword j of this lane's window at win[j * 256]
-#else
-  uint64_t w0, w1, w2, w3;
-#endif
 
   __device__ __forceinline__ void fill(int64_t q) {
     const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(buf + q) & 15);
@@ -206,7 +191,6 @@ struct Reader {
     // near the end of the batch buffer, slide the window back so its loads stay inside the 16-B padding
     const int64_t hi = lim - (int64_t)kWin - (int64_t)(reinterpret_cast<uintptr_t>(buf + lim) & 15);
     if (wb > hi && hi >= 0) wb = hi;
-#ifdef DXA_PARSE_LDSWIN
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const G1 u32x4* w = (const G1 u32x4*)(buf + wb);
     const u32x4 a = w[0], b = w[1], c = w[2], d = w[3];
@@ -214,21 +198,11 @@ struct Reader {
     win[4 * 256] = b.x; win[5 * 256] = b.y; win[6 * 256] = b.z; win[7 * 256] = b.w;
     win[8 * 256] = c.x; win[9 * 256] = c.y; win[10 * 256] = c.z; win[11 * 256] = c.w;
     win[12 * 256] = d.x; win[13 * 256] = d.y; win[14 * 256] = d.z; win[15 * 256] = d.w;
-#else
-    const G1 uint64_t* w = (const G1 uint64_t*)(buf + wb);  // pointer arithmetic: stays global
-    w0 = w[0];
-    w1 = w[1];
-    w2 = w[2];
-    w3 = w[3];
-#endif
   }
   // wave-synchronous refill: every lane with fewer than `need` bytes left in its window reloads in one instruction
   __device__ __forceinline__ void top_up(uint32_t need) {
-#ifdef DXA_PARSE_LDSWIN
     if ((uint64_t)(p - wb) > (uint64_t)(kWin - need)) fill(p);
-#endif
   }
-#ifdef DXA_PARSE_LDSWIN
   __device__ __forceinline__ uint32_t at(int64_t q) {
     if ((uint64_t)(q - wb) >= kWin) fill(q);
     const uint32_t o = (uint32_t)(q - wb);
@@ -244,31 +218,6 @@ struct Reader {
     const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
     return (uint64_t)lo | ((uint64_t)hi << 32);
   }
-#else
-  // word k (0..3) of the window: mask blends, not selects (a select of adjacent fields becomes a dynamically
-  // indexed private array — scratch — in the compiler)
-  __device__ __forceinline__ uint64_t word(uint32_t k) const {
-    const uint64_t m0 = 0ull - (uint64_t)(k & 1u);
-    const uint64_t lo = w0 ^ ((w0 ^ w1) & m0);
-    const uint64_t hi = w2 ^ ((w2 ^ w3) & m0);
-    const uint64_t m1 = 0ull - (uint64_t)((k >> 1) & 1u);
-    return lo ^ ((lo ^ hi) & m1);
-  }
-  __device__ __forceinline__ uint32_t at(int64_t q) {
-    if ((uint64_t)(q - wb) >= kWin) fill(q);
-    const uint32_t o = (uint32_t)(q - wb);
-    return (uint32_t)(word(o >> 3) >> ((o & 7u) * 8u)) & 0xffu;
-  }
-  // 8 bytes starting at q (the batch buffer carries >= 16 bytes of tail padding)
-  __device__ __forceinline__ uint64_t load8(int64_t q) {
-    if ((uint64_t)(q - wb) > kWin - 8u) fill(q);
-    const uint32_t o = (uint32_t)(q - wb);
-    const uint32_t k = o >> 3, sh = (o & 7u) * 8u;
-    const uint64_t lo = word(k);
-    if (sh == 0) return lo;
-    return (lo >> sh) | (word(k + 1) << (64u - sh));
-  }
-#endif
   __device__ __forceinline__ uint32_t cur() { return p < end ? at(p) : 0u; }
   __device__ __forceinline__ void skip_ws() {
     while (p < end) {
@@ -721,16 +670,10 @@ __device__ __forceinline__ bool parse_iso_ts(Reader& rd, int64_t s, int64_t e, i
 // spilled on cold paths) for 5 waves per SIMD (LDS: 25 KiB per 256-lane workgroup).  Bench batch (2 M events,
 // profiles/parse/parse_variants.md): register window 2.29 ms; LDS window 4 waves 1.76 ms; 5 waves 1.59 ms; 6 waves
 // 1.76 ms (12 dwords spilled); top-up threshold 48/40/32/24/16/1 bytes -> 1.72/1.64/1.58/1.58/1.66/1.73 ms.
-#ifndef DXA_PARSE_WPE
-#define DXA_PARSE_WPE 5
-#endif
-#ifdef DXA_PARSE_STACK32
-typedef int StackT;
-#else
+constexpr uint32_t kTopUp = 32;
 typedef int16_t StackT;                               // node ids < 32767 (checked by the host entry point)
-#endif
 template <bool LDS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_WPE))) void json_parse_kernel(ParseArgs pa) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void json_parse_kernel(ParseArgs pa) {
   const GArgs a = to_global(pa);
   const Tables<LDS> tb = load_tables<LDS>(a);                   // (LDS: whole workgroup, before any early exit)
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -742,12 +685,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
   r.end = a.ends ? a.ends[row] : a.offs[row + 1];
   r.wb = -256;
   r.lim = a.offs[n] + 16;
-#ifdef DXA_PARSE_LDSWIN
   __shared__ uint32_t s_win[17][256];
   r.win = (G3U32*)&s_win[0][threadIdx.x];
-#else
-  r.w0 = r.w1 = r.w2 = r.w3 = 0;
-#endif
 
   // schema-tracked nesting is kept in registers (deeper objects are skipped as unknown values)
   // nesting state in LDS, [level][lane] (consecutive lanes → consecutive banks): dynamically indexed per-lane
@@ -773,10 +712,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DXA_PARSE_W
   depth = 1;
   a.valid[row] = 1;  // root struct present
   while (true) {
-#ifndef DXA_PARSE_TOPUP
-#define DXA_PARSE_TOPUP 32
-#endif
-    r.top_up(DXA_PARSE_TOPUP);                        // key + typical value of the next field, all low lanes at once
+    r.top_up(kTopUp);                        // key + typical value of the next field, all low lanes at once
     r.skip_ws();
     uint32_t c = r.cur();
     if (c == '}') {

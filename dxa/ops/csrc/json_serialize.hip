@@ -56,7 +56,6 @@ struct SerArgs {
   int64_t* lens;          // length pass (line length incl. the newline)
   const int64_t* ends;    // write pass: inclusive scan of lens (line i starts at ends[i] - lens[i])
   uint8_t* out;
-  int32_t stage_off;      // write pass: LDS offset of the emitters' 64-B staging slots (0: direct stores)
   SerSegs seg;
 };
 
@@ -294,9 +293,8 @@ __device__ __forceinline__ Tables stage_tables(const SerArgs& a, uint64_t* smem)
 }
 
 template <bool W>
-__device__ __forceinline__ int64_t render_row(const Tables& t, int pc0, int pc1, int64_t row, uint8_t* dst,
-                                              uint8_t* stage = nullptr) {
-  dxa::Emitter<W> e(dst, stage);
+__device__ __forceinline__ int64_t render_row(const Tables& t, int pc0, int pc1, int64_t row, uint8_t* dst) {
+  dxa::Emitter<W> e(dst);
   e.put('{');
   uint32_t first = 1u;                                      // bit d: nothing written yet at nesting depth d
   for (int pc = pc0; pc < pc1; ++pc) {
@@ -370,9 +368,7 @@ __global__ __launch_bounds__(256) void ser_write_kernel(SerArgs a) {
   int s;
   int64_t local, row;
   if (!seg_row(a.seg, s, local, row)) return;
-  uint8_t* stage = a.stage_off ? reinterpret_cast<uint8_t*>(smem) + a.stage_off + threadIdx.x * dxa::kEmitStageBytes
-                               : nullptr;
-  render_row<true>(t, a.seg.pc[s], a.seg.pc[s + 1], local, a.out + (a.ends[row] - a.lens[row]), stage);
+  render_row<true>(t, a.seg.pc[s], a.seg.pc[s + 1], local, a.out + (a.ends[row] - a.lens[row]));
 }
 
 size_t ser_lds_bytes(int32_t nnodes, int32_t nprog, int32_t text_words) {
@@ -434,13 +430,10 @@ DXA_API int dxa_serialize_rows(int32_t write, const void* tables, int32_t nnodes
   const uint8_t* base = (const uint8_t*)tables;
   const size_t prog_off = (size_t)nnodes * sizeof(DevNode);
   const size_t text_off = prog_off + (size_t)((nprog * 4 + 1) / 2) * 8;
-  const size_t stage_off = (lds + 15) & ~(size_t)15;
-  const bool stage = write && DXA_EMIT_STAGE && stage_off + 256 * dxa::kEmitStageBytes <= kMaxLds;
   SerArgs a{(const DevNode*)base, nnodes, (const int32_t*)(base + prog_off), nprog, base + text_off, text_words,
-            lens, ends, out, stage ? (int32_t)stage_off : 0, g};
+            lens, ends, out, g};
   if (write)
-    hipLaunchKernelGGL(ser_write_kernel, dim3((unsigned)blocks), dim3(256),
-                       stage ? stage_off + 256 * dxa::kEmitStageBytes : lds, (hipStream_t)st, a);
+    hipLaunchKernelGGL(ser_write_kernel, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)st, a);
   else hipLaunchKernelGGL(ser_len_kernel, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)st, a);
   return (int)hipGetLastError();
 }

@@ -1,23 +1,11 @@
 // LZ4 block decoder for gfx950: compressed ingest (LZ4-frame event batches, Kafka compression codec 3) is
 // decompressed in HBM after a compressed H2D copy, so PCIe carries ~2.5x fewer bytes per event.
 //
-// Main path (blocks <= 64 KiB decompressed): ONE WAVE PER BLOCK, output staged in LDS.
-//   * The sequence headers (token, length bytes, offset) are a serial chain, so they are parsed as wave-uniform
-//     (scalar) values from a 512-byte register window over the compressed bytes: lane j holds dword j of two
-//     256-byte halves and a header byte is one v_readlane.  The window advances 256 B at a time with one
-//     coalesced dword load per lane into the retired half, so the chain never waits on a global load per
-//     sequence.
-//   * Literal runs are copied 64 bytes per step: lane k pulls its byte out of the window with ds_bpermute and
-//     writes it to the block's LDS output buffer.
-//   * Match copies read earlier output from LDS (period-`off` replication for off < 64) 64 bytes per step; a
-//     wave's LDS operations execute in order, so bytes written by one step are visible to the next.
-//   * When the block is done its LDS buffer is flushed to HBM with 16-byte stores (fully coalesced).
-//   LDS per wave = the block's decompressed size (16 KiB frames from our producer: 2 waves / 32 KiB per
-//   workgroup -> 5 workgroups per CU).
-// Fallback (bigger blocks): one lane per block with register-window input and 16-B packed output stores.
-// A size pass (no stores) serves frames whose blocks do not carry decompressed sizes.
+// Decoder: 16 lanes per block, output straight to HBM (lz4_decode_group_kernel, design notes below).  A size pass
+// (one lane per block, register-window input, no stores) serves frames whose blocks do not carry decompressed sizes.
+// Measured and dropped (profiles/kafka_batching/README.md): one wave per block with LDS-staged output, one lane per
+// block, 8 lanes per block.
 #include "dxa_common.h"
-#include <stdlib.h>
 
 namespace {
 
@@ -152,195 +140,6 @@ __global__ __launch_bounds__(256) void lz4_sizes_kernel(const uint8_t* __restric
   status[b] = rc;
 }
 
-__global__ __launch_bounds__(256) void lz4_decode_kernel(const uint8_t* __restrict__ src,
-                                                         const int64_t* __restrict__ comp_off,
-                                                         const int32_t* __restrict__ comp_len,
-                                                         const uint8_t* __restrict__ stored,
-                                                         const int64_t* __restrict__ out_off,
-                                                         const int64_t* __restrict__ out_len, int64_t nb,
-                                                         uint8_t* dst, int32_t* __restrict__ status) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
-  const uint8_t* s = src + comp_off[b];
-  const int64_t n = comp_len[b];
-  uint8_t* d = dst + out_off[b];
-  const int64_t cap = out_len[b];
-  if (stored[b]) {
-    if (n != cap) { status[b] = LZ_SIZE; return; }
-    InWin in{s, 0, make_uint4(0, 0, 0, 0)};
-    OutBuf out;
-    out.init(d);
-    for (int64_t k = 0; k < n; ++k) out.put(in.at(k));
-    out.finish();
-    status[b] = LZ_OK;
-    return;
-  }
-  int64_t produced = 0;
-  int32_t rc = run_block<true>(s, n, d, cap, produced);
-  if (rc == LZ_OK && produced != cap) rc = LZ_SIZE;
-  status[b] = rc;
-}
-
-
-// ---- one wave per block, LDS-staged output -------------------------------------------------------------------
-// All sequence state is 32-bit and wave-uniform (SGPRs, SALU compares, SCC branches): a bench block has ~1400
-// sequences of ~1.7 literal + ~10 match bytes, so the per-sequence instruction count is what sets the speed.
-template <int WPG>
-__global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t* __restrict__ src,
-                                                                   const int64_t* __restrict__ comp_off,
-                                                                   const int32_t* __restrict__ comp_len,
-                                                                   const uint8_t* __restrict__ stored,
-                                                                   const int64_t* __restrict__ out_off,
-                                                                   const int64_t* __restrict__ out_len, int64_t nb,
-                                                                   int32_t lds_block, uint8_t* dst,
-                                                                   int32_t* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  // readfirstlane: the wave index is uniform, so everything derived from it stays scalar
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int lane = (int)(threadIdx.x & 63);
-  const int64_t b = (int64_t)blockIdx.x * WPG + wave;
-  if (b >= nb) return;
-  const int32_t n = comp_len[b];
-  const int64_t cap64 = out_len[b];
-  const uint8_t* sb = src + comp_off[b];
-  uint8_t* d = dst + out_off[b];
-  if (stored[b]) {
-    for (int32_t k = lane; k < n; k += 64) d[k] = sb[k];
-    if (lane == 0) status[b] = (n == cap64) ? LZ_OK : LZ_SIZE;
-    return;
-  }
-  if (cap64 > lds_block || cap64 < 0 || n < 0) {
-    if (lane == 0) status[b] = LZ_OVERFLOW;
-    return;
-  }
-  const int32_t cap = (int32_t)cap64;
-  uint8_t* ob = lds + wave * lds_block;
-
-  // Input window: positions are counted from a0 = sb rounded down to 4 B (derived from the kernel argument, so
-  // the loads stay global_load and LDS waits never drain them).  Halves WA/WB hold [w, w+256) and [w+256,
-  // w+512) in the order given by `alo`; advancing reloads the retired half in place.
-  const int32_t shift = (int32_t)(reinterpret_cast<uintptr_t>(sb) & 3);
-  const uint8_t* a0 = sb - shift;
-  const int32_t lim = shift + n + 16;                       // frames carry >= 16 readable bytes past any block
-  auto ld = [&](int32_t w0) -> uint32_t {
-    const int32_t q = w0 + 4 * lane;
-    return (q + 4 <= lim) ? *reinterpret_cast<const uint32_t*>(a0 + q) : 0u;
-  };
-  int32_t w = 0;
-  uint32_t WA = ld(0), WB = ld(256);
-  bool alo = true;
-  auto ensure = [&](int32_t p) {                            // afterwards w <= p < w + 256
-    const int32_t r = p - w;
-    if (r >= 256) {
-      if (r < 512) {
-        w += 256;
-        if (alo) WA = ld(w + 256); else WB = ld(w + 256);
-        alo = !alo;
-      } else {
-        w = p & ~3;
-        WA = ld(w);
-        WB = ld(w + 256);
-        alo = true;
-      }
-    }
-  };
-  auto byte_at = [&](int32_t p) -> uint32_t {              // needs w <= p < w + 512
-    const int32_t r = p - w;
-    const int32_t dw = r >> 2;
-    const uint32_t v = ((dw < 64) == alo) ? (uint32_t)__builtin_amdgcn_readlane((int)WA, dw & 63)
-                                          : (uint32_t)__builtin_amdgcn_readlane((int)WB, dw & 63);
-    return (v >> ((r & 3) * 8)) & 0xffu;
-  };
-
-  int32_t ip = shift, op = 0;                               // ip: window position of the next input byte
-  const int32_t iend = shift + n;
-  int32_t rc = LZ_OK;
-  while (ip < iend) {
-    ensure(ip);
-    const uint32_t token = byte_at(ip);
-    ++ip;
-    int32_t lit = (int32_t)(token >> 4);
-    if (lit == 15) {
-      uint32_t x;
-      do {
-        if (ip >= iend) { rc = LZ_TRUNC; break; }
-        ensure(ip);
-        x = byte_at(ip);
-        ++ip;
-        lit += (int32_t)x;
-      } while (x == 255);
-      if (rc != LZ_OK) break;
-    }
-    if (lit > iend - ip) { rc = LZ_TRUNC; break; }
-    if (lit > cap - op) { rc = LZ_OVERFLOW; break; }
-    for (int32_t c = 0; c < lit; c += 64) {
-      ensure(ip + c);
-      const int32_t r0 = ip + c - w;                        // < 256
-      const int32_t r = r0 + lane;                          // < 320
-      const int32_t sel = ((r >> 2) & 63) << 2;
-      uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(sel, (int)(alo ? WA : WB));
-      if (r0 + 63 >= 256) {                                 // chunk reaches into the high half
-        const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute(sel, (int)(alo ? WB : WA));
-        v = (r >> 2) >= 64 ? v1 : v;
-      }
-      if (c + lane < lit) ob[op + c + lane] = (uint8_t)(v >> ((r & 3) * 8));
-    }
-    ip += lit;
-    op += lit;
-    if (ip >= iend) break;                                  // last sequence: literals only
-    if (iend - ip < 2) { rc = LZ_TRUNC; break; }
-    ensure(ip);
-    const int32_t off = (int32_t)(byte_at(ip) | (byte_at(ip + 1) << 8));
-    ip += 2;
-    if (off == 0 || off > op) { rc = LZ_OFFSET; break; }
-    int32_t ml = (int32_t)(token & 15);
-    if (ml == 15) {
-      uint32_t x;
-      do {
-        if (ip >= iend) { rc = LZ_TRUNC; break; }
-        ensure(ip);
-        x = byte_at(ip);
-        ++ip;
-        ml += (int32_t)x;
-      } while (x == 255);
-      if (rc != LZ_OK) break;
-    }
-    ml += 4;
-    if (ml > cap - op) { rc = LZ_OVERFLOW; break; }
-    const int32_t s0 = op - off;
-    if (off >= ml || off >= 64) {
-      // every source byte precedes the 64-byte step that reads it
-      for (int32_t c = 0; c < ml; c += 64) {
-        if (c + lane < ml) ob[op + c + lane] = ob[s0 + c + lane];
-        asm volatile("" ::: "memory");                     // keep step order (LDS runs a wave's ops in order)
-      }
-    } else {
-      // overlapping short period: replicate the off-byte pattern
-      for (int32_t c = 0; c < ml; c += 64) {
-        const uint32_t i = (uint32_t)(c + lane);
-        if ((int32_t)i < ml) ob[op + i] = ob[s0 + (int32_t)(i % (uint32_t)off)];
-        asm volatile("" ::: "memory");
-      }
-    }
-    op += ml;
-  }
-  if (rc == LZ_OK && op != cap) rc = LZ_SIZE;
-  asm volatile("" ::: "memory");
-  if (rc == LZ_OK) {
-    if ((reinterpret_cast<uintptr_t>(d) & 15) == 0) {
-      const int32_t nfull = op >> 4;
-      for (int32_t k = lane; k < nfull; k += 64) {
-        const uint4 v = *reinterpret_cast<const uint4*>(ob + 16 * k);
-        *reinterpret_cast<uint4*>(d + 16 * k) = v;
-      }
-      for (int32_t k = (nfull << 4) + lane; k < op; k += 64) d[k] = ob[k];
-    } else {
-      for (int32_t k = lane; k < op; k += 64) d[k] = ob[k];
-    }
-  }
-  if (lane == 0) status[b] = rc;
-}
-
 // ---- 16 lanes per block, output straight to HBM -----------------------------------------------------------
 // Bench blocks have ~1400 sequences of ~1.7 literal + ~10 match bytes, so neither 64-wide copies nor a
 // wave-uniform (scalar-unit) parser pays: the per-CU scalar unit serialises every wave's header chain.  Here a
@@ -358,8 +157,7 @@ __global__ __launch_bounds__(64 * WPG) void lz4_decode_wave_kernel(const uint8_t
 //     known complete at the last such wait, so the wait is only taken when a source reaches past it — about
 //     once per `off` bytes (~600 B, one record) for JSON.
 //   * The group width is a template parameter: G = 8 (eight blocks per instruction, a 2-dword window per lane,
-//     4-byte-per-lane match copies) measured 6.07 ms against 4.72 ms for G = 16 on the bench batch (DXA_LZ4_LANES=8
-//     selects it for comparison).
+//     4-byte-per-lane match copies) measured 6.07 ms against 4.72 ms for G = 16 on the bench batch.
 //   * Measured and dropped (profiles/kafka_batching/README.md): an LDS history ring for match sources (the byte
 //     stores to LDS and the occupancy it costs outweigh the HBM round trips it saves: 8.13 -> 8.71 / 12.61 ms per
 //     groupby step with a 1 / 2 KiB ring) and branch-free masked stores (below).
@@ -601,17 +399,6 @@ DXA_API int dxa_lz4_block_sizes(const void* src, const void* comp_off, const voi
   return (int)hipGetLastError();
 }
 
-// DXA_LZ4_LANES selects the decoder for measurements: 16 lanes per block (default), 8, 64 = one wave per block
-// with LDS-staged output, 1 = one lane per block
-static int lz4_lanes() {
-  static const int lanes = [] {
-    const char* e = getenv("DXA_LZ4_LANES");
-    const int v = e ? atoi(e) : 16;
-    return (v == 1 || v == 8 || v == 16 || v == 64) ? v : 16;
-  }();
-  return lanes;
-}
-
 // launch the G-lane group decoder (one block per G lanes)
 template <int G>
 static int launch_group(int64_t nb, hipStream_t s, const uint8_t* src, const int64_t* co, const int32_t* cl,
@@ -628,41 +415,13 @@ DXA_API int dxa_lz4_decode(const void* src, const void* comp_off, const void* co
                            void* status, void* st) {
   if (nb <= 0) return 0;
   const hipStream_t s = (hipStream_t)st;
-  const int lanes = lz4_lanes();
-  const uint8_t* s8 = (const uint8_t*)src;
-  const int64_t* co = (const int64_t*)comp_off;
-  const int32_t* cl = (const int32_t*)comp_len;
-  const uint8_t* sd = (const uint8_t*)stored;
-  const int64_t* oo = (const int64_t*)out_off;
-  const int64_t* ol = (const int64_t*)out_len;
-  if (lanes == 8 || lanes == 16) {
-    if (lanes == 8)
-      launch_group<8>(nb, s, s8, co, cl, sd, oo, ol, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
-    else
-      launch_group<16>(nb, s, s8, co, cl, sd, oo, ol, (uint8_t*)dst, (int32_t*)status, (int64_t*)nullptr);
-    return (int)hipGetLastError();
-  }
-  const int64_t lb = (max_out + 15) & ~(int64_t)15;         // LDS bytes per wave (16-B aligned slices)
-  if (lanes == 64 && max_out >= 0 && lb <= 65536) {
-    const int32_t lds_block = (int32_t)(lb < 16 ? 16 : lb);
-#define DXA_LZ4_WAVE(W)                                                                                     \
-    hipLaunchKernelGGL(lz4_decode_wave_kernel<W>, dim3((unsigned)((nb + (W) - 1) / (W))), dim3(64 * (W)),   \
-                       (size_t)(W) * lds_block, s, s8, co, cl, sd, oo, ol, nb, lds_block, (uint8_t*)dst,    \
-                       (int32_t*)status)
-    // <= 32 KiB of LDS per workgroup keeps 5 workgroups resident per CU
-    if (lds_block <= 8192) DXA_LZ4_WAVE(4);
-    else if (lds_block <= 16384) DXA_LZ4_WAVE(2);
-    else DXA_LZ4_WAVE(1);
-#undef DXA_LZ4_WAVE
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(lz4_decode_kernel, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, s, s8, co, cl, sd, oo, ol,
-                     nb, (uint8_t*)dst, (int32_t*)status);
-  return (int)hipGetLastError();
+  return launch_group<16>(nb, s, (const uint8_t*)src, (const int64_t*)comp_off, (const int32_t*)comp_len,
+                          (const uint8_t*)stored, (const int64_t*)out_off, (const int64_t*)out_len, (uint8_t*)dst,
+                          (int32_t*)status, (int64_t*)nullptr);
 }
 
 // Blocks with a capacity instead of a known size (Kafka LZ4 frames): `cap[b]` bytes reserved at out_off[b], the
-// decompressed size comes back in produced[b].  The group decoder, 16 lanes per block (8 with DXA_LZ4_LANES=8).
+// decompressed size comes back in produced[b].  The group decoder, 16 lanes per block.
 DXA_API int dxa_lz4_decode_into(const void* src, const void* comp_off, const void* comp_len, const void* stored,
                                 const void* out_off, const void* cap, int64_t nb, void* dst, void* produced,
                                 void* status, void* st) {
@@ -674,11 +433,7 @@ DXA_API int dxa_lz4_decode_into(const void* src, const void* comp_off, const voi
   const uint8_t* sd = (const uint8_t*)stored;
   const int64_t* oo = (const int64_t*)out_off;
   const int64_t* cp = (const int64_t*)cap;
-  if (lz4_lanes() == 8)
-    launch_group<8>(nb, s, s8, co, cl, sd, oo, cp, (uint8_t*)dst, (int32_t*)status, (int64_t*)produced);
-  else
-    launch_group<16>(nb, s, s8, co, cl, sd, oo, cp, (uint8_t*)dst, (int32_t*)status, (int64_t*)produced);
-  return (int)hipGetLastError();
+  return launch_group<16>(nb, s, s8, co, cl, sd, oo, cp, (uint8_t*)dst, (int32_t*)status, (int64_t*)produced);
 }
 
 // Async H2D copy of a byte range of a pinned host buffer on `st` (torch's copy_ of a pinned *slice* falls back

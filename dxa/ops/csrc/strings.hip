@@ -110,23 +110,7 @@ __global__ void str_eq_col_kernel(const uint8_t* __restrict__ aa, const int64_t*
   }
 }
 
-// Copy each view's bytes to dst + dst_off[i] (compaction / concat of arenas).
-__global__ void str_gather_kernel(const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
-                                  const int32_t* __restrict__ lens, int64_t n, const int64_t* __restrict__ dst_off,
-                                  uint8_t* __restrict__ dst) {
-  // one wave per string keeps copies coalesced for long strings and lanes busy for short ones
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i = wave; i < n; i += nwaves) {
-    const uint8_t* s = arena + starts[i];
-    uint8_t* d = dst + dst_off[i];
-    const int32_t l = lens[i];
-    for (int32_t k = lane; k < l; k += 64) d[k] = s[k];
-  }
-}
-
-// Lane-per-string gather (the default): window panes and exchanges compact millions of short strings (device
+// Copy each view's bytes to dst + dst_off[i] (compaction / concat of arenas), one lane per string: window panes and exchanges compact millions of short strings (device
 // types, regions, ids: 4-20 B), where a wave per string leaves 60 of 64 lanes idle.  Each lane copies its string
 // with unaligned 8-byte global loads/stores and a 4/2/1-byte tail (stores never touch a neighbour's bytes);
 // strings longer than 128 B are copied afterwards by the whole wave, one at a time (ballot loop).
@@ -524,12 +508,7 @@ DXA_API int dxa_str_cmp_col(const uint8_t* aa, const int64_t* as, const int32_t*
 DXA_API int dxa_str_gather(const uint8_t* arena, const int64_t* starts, const int32_t* lens, int64_t n,
                            const int64_t* dst_off, uint8_t* dst, void* st) {
   if (n <= 0) return 0;
-  static const bool wave_per_string = getenv("DXA_STR_GATHER_WAVE") != nullptr;     // A/B: previous kernel
-  if (wave_per_string)
-    hipLaunchKernelGGL(str_gather_kernel, dim3(dxa_blocks(n * 64, 256)), dim3(256), 0, (hipStream_t)st, arena, starts,
-                       lens, n, dst_off, dst);
-  else
-    hipLaunchKernelGGL(str_gather_lane_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st,
+  hipLaunchKernelGGL(str_gather_lane_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st,
                        arena, starts, lens, n, dst_off, dst);
   return (int)hipGetLastError();
 }

@@ -90,7 +90,7 @@ def group_rows(keys: List, ordered: bool = True) -> Groups:
             return _exact_groups(keys, device)
         if not ordered:
             return Groups(gid, ng, rep[:ng].to(torch.int64))
-        if 0 < ng and (n <= _RENUMBER_BITMAP_ROWS or ng <= _RENUMBER_MAX) and _RENUMBER_KERNEL:
+        if 0 < ng and (n <= _RENUMBER_BITMAP_ROWS or ng <= _RENUMBER_MAX):
             inv = torch.empty(ng, dtype=torch.int32, device=device)
             rep_out = torch.empty(ng, dtype=torch.int64, device=device)
             N.call("dxa_group_renumber", N.ptr(gid), n, N.ptr(rep), ng, N.ptr(inv), N.ptr(rep_out), st)
@@ -284,7 +284,6 @@ def _host_minmax(groups, col, func, device):
 _MA_ADD_U64, _MA_ADD_F64, _MA_MAX = 0, 1, 2
 _RENUMBER_MAX = 4096          # hash_groupby.hip kRenumberMax: one-workgroup bitonic renumbering
 _RENUMBER_BITMAP_ROWS = 8192 * 64   # kBitmapRows: first-row bitmap renumbering (any number of groups)
-_RENUMBER_KERNEL = __import__("os").environ.get("DXA_RENUMBER_KERNEL", "1") != "0"        # A/B switch
 _MV_COUNT, _MV_I64, _MV_F64, _MV_F64_ORD, _MV_NOT = 0, 1, 2, 3, 4
 _F_COUNT, _F_I64, _F_F64, _F_AVG, _F_F64_ORD, _F_NOT = 0, 1, 2, 3, 4, 8       # hash_groupby.hip agg_finish_kernel
 _FUSABLE = ("count_star", "count", "sum", "min", "max", "avg", "mean")

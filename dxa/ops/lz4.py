@@ -1,7 +1,7 @@
 """LZ4 frames: host codec (``host_lz4.cpp``) and the device block decoder (``lz4.hip``).
 
 Compressed ingest: a batch of newline-delimited events travels host → HBM as an LZ4 frame (≈2.5x fewer PCIe bytes
-for SimulatedData-shaped JSON), is decoded by one wave per 16 KiB block (LDS-staged), and framed into records on the device.
+for SimulatedData-shaped JSON), is decoded by 16 lanes per block, and framed into records on the device.
 The same frames are Kafka's compression codec 3 payload (``io/kafka.py``).
 """
 from __future__ import annotations

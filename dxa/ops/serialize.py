@@ -458,16 +458,12 @@ _side_lock = threading.Lock()
 
 
 def _side_stream(device):
-    """The output stream.  ``DXA_SINK_STREAM_PRIORITY=1`` creates it at high priority, so that batch t's render
-    kernels get workgroup slots ahead of batch t+1's decode / parse.  Measured on MI355X (profiles/gc/README.md) the
-    effect on Latency-Process and throughput was within run-to-run noise, so normal priority stays the default."""
+    """The output stream, at normal priority (a high-priority render stream measured within run-to-run noise on
+    Latency-Process and throughput, profiles/gc/README.md)."""
     with _side_lock:
         s = _side_streams.get(device)
         if s is None:
-            prio = 0
-            if os.environ.get("DXA_SINK_STREAM_PRIORITY", "0") != "0":
-                prio = torch.cuda.Stream.priority_range()[1]          # (least, greatest): greatest is highest
-            s = _side_streams[device] = torch.cuda.Stream(device, priority=prio)
+            s = _side_streams[device] = torch.cuda.Stream(device)
         return s
 
 

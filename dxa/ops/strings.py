@@ -74,21 +74,11 @@ class _StrPart(ctypes.Structure):
                 ("dst_off", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row0", ctypes.c_int64)]
 
 
-_PARTS = __import__("os").environ.get("DXA_STR_PARTS", "1") != "0"
-
-
 def _gather_parts(parts, device) -> None:
     """One ``dxa_str_gather_parts`` launch (per 32 parts) for many string gathers.  ``parts``: (StrColumn view,
-    destination offsets tensor, destination arena) triples; offsets are per row of the part.  ``DXA_STR_PARTS=0``:
-    one ``dxa_str_gather`` per part (A/B)."""
+    destination offsets tensor, destination arena) triples; offsets are per row of the part."""
     parts = [p for p in parts if p[0].length]
     if not parts:
-        return
-    if not _PARTS:
-        st = N.stream_handle(device)
-        for c, off, dst in parts:
-            N.call("dxa_str_gather", N.ptr(c.arena), N.ptr(c.starts), N.ptr(c.lens), c.length, N.ptr(off),
-                   N.ptr(dst), st)
         return
     if N.lib().dxa_str_part_size() != ctypes.sizeof(_StrPart):
         raise N.NativeError("StrPart layout mismatch between strings.py and strings.hip")
