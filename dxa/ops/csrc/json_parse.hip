@@ -219,6 +219,15 @@ struct Reader {
     return (uint64_t)lo | ((uint64_t)hi << 32);
   }
   __device__ __forceinline__ uint32_t cur() { return p < end ? at(p) : 0u; }
+  // skip whitespace and return the character there (0 at the end): one window read in the common no-space case
+  __device__ __forceinline__ uint32_t ws_cur() {
+    while (p < end) {
+      const uint32_t c = at(p);
+      if (c != ' ' && c != '\n' && c != '\r' && c != '\t') return c;
+      ++p;
+    }
+    return 0u;
+  }
   __device__ __forceinline__ void skip_ws() {
     while (p < end) {
       const uint32_t c = at(p);
@@ -472,25 +481,36 @@ __device__ __forceinline__ bool take_literal(Reader& r, uint32_t c) {
   return good && r.p <= r.end;
 }
 
-// A JSON number's syntax (-? int frac? exp?) without its value: the skipping paths need no mantissa registers.
+// A run of digits at r.p, eight characters per step (SWAR digit test); false when there is none.
+__device__ __forceinline__ bool skip_digits(Reader& r) {
+  const int64_t s = r.p;
+  while (r.p < r.end) {
+    const uint64_t nm = swar_nondigit(r.load8(r.p));
+    if (nm) { r.p += __builtin_ctzll(nm) >> 3; break; }
+    r.p += 8;
+  }
+  if (r.p > r.end) r.p = r.end;                           // digits past the record's end are not its own
+  return r.p > s;
+}
+
+// A JSON number's syntax (-? int frac? exp?) without its value: the skipping paths (pruned fields, unknown keys)
+// need no mantissa registers, and digit runs go eight at a time.
 __device__ __forceinline__ bool skip_number(Reader& r) {
   if (r.cur() == '-') ++r.p;
-  if (!is_digit(r.cur())) return false;
-  if (r.cur() == '0') {
+  const int64_t s = r.p;
+  if (!skip_digits(r)) return false;
+  if (r.p - s > 1 && r.at(s) == '0') return false;        // leading zero
+  uint32_t c = r.cur();
+  if (c == '.') {
     ++r.p;
-    if (is_digit(r.cur())) return false;                  // leading zero
+    if (!skip_digits(r)) return false;
+    c = r.cur();
   }
-  while (is_digit(r.cur())) ++r.p;
-  if (r.cur() == '.') {
+  if ((c | 0x20u) == 'e') {
     ++r.p;
-    if (!is_digit(r.cur())) return false;
-    while (is_digit(r.cur())) ++r.p;
-  }
-  if ((r.cur() | 0x20u) == 'e') {
-    ++r.p;
-    if (r.cur() == '-' || r.cur() == '+') ++r.p;
-    if (!is_digit(r.cur())) return false;
-    while (is_digit(r.cur())) ++r.p;
+    c = r.cur();
+    if (c == '-' || c == '+') ++r.p;
+    if (!skip_digits(r)) return false;
   }
   return true;
 }
@@ -509,9 +529,8 @@ __device__ __forceinline__ bool skip_value(Reader& r) {
   uint32_t obj = 0;                                       // bit d: level d is an object
   int depth = 0, st = kVal;
   while (true) {
-    r.skip_ws();
-    if (r.p >= r.end) return false;
-    c = r.at(r.p);
+    c = r.ws_cur();
+    if (c == 0u) return false;
     switch (st) {
       case kVal:
       case kValOrClose:
@@ -704,8 +723,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
   __shared__ uint64_t s_seen[256];                        // schema nodes (< 64) already assigned in this record
   s_seen[threadIdx.x] = 0;                                // (per lane in LDS: keeps the loop's VGPR budget)
 
-  r.skip_ws();
-  if (r.cur() != '{') goto done;
+  if (r.ws_cur() != '{') goto done;
   ++r.p;
   stack(0) = 0;  // root node
   expect(0) = tb.first_child[0];
@@ -713,8 +731,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
   a.valid[row] = 1;  // root struct present
   while (true) {
     r.top_up(kTopUp);                        // key + typical value of the next field, all low lanes at once
-    r.skip_ws();
-    uint32_t c = r.cur();
+    uint32_t c = r.ws_cur();
     if (c == '}') {
       if (comma) break;       // trailing comma: {"a":1,}
       ++r.p;
@@ -746,17 +763,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
         node = lookup(tb, stack(depth - 1), h);
       }
       if (node >= 0) expect(depth - 1) = tb.next_sib[node];
-      r.skip_ws();
-      if (r.cur() != ':') break;
+      if (r.ws_cur() != ':') break;
       ++r.p;
-      r.skip_ws();
-      c = r.cur();
-      if (node < 0 || (tb.node_type[node] & 0xff) == FT_SKIP) goto skip_any;
+      c = r.ws_cur();
+      if (node < 0) goto skip_any;
       const int t = tb.node_type[node] & 0xff;
+      // a pruned field's scalar runs through the typed scanners below, which store nothing for FT_SKIP: cheaper
+      // than the container-capable skipper, which only its containers need
+      if (t == FT_SKIP && (c == '{' || c == '[')) goto skip_any;
       const bool raw_arr = (tb.node_type[node] & 0x100) != 0;
       const int vs = tb.val_slot[node];
       const int ls = tb.len_slot[node];
-      if (node < 64) {                                    // a repeated key: its last occurrence decides (null on a
+      if (node < 64 && t != FT_SKIP) {                    // a repeated key: its last occurrence decides (null on a
         const uint64_t bit = 1ull << node;                // mismatch), as a tokenizing parser's last write would
         const uint64_t seen = s_seen[threadIdx.x];
         if (seen & bit) a.valid[(int64_t)node * n + row] = 0;
@@ -853,8 +871,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       }
     }
   after_value:
-    r.skip_ws();
-    c = r.cur();
+    c = r.ws_cur();
     if (c == ',') { ++r.p; comma = true; continue; }
     if (c == '}') continue;  // closes the current object at loop top
     break;

@@ -382,10 +382,20 @@ struct FrameState {
   int hufbits;
 };
 
+// Optional per-frame phase counters (tools/zstd_bench.py): cycles in the Huffman table build, the literal streams,
+// the sequence-table builds and the sequence loop, plus the frame's block / sequence / literal counts.
+enum { P_TOTAL, P_HUFTAB, P_LITS, P_SEQTAB, P_SEQ, P_NBLK, P_NSEQ, P_NLIT, P_N };
+struct Prof {
+  int64_t v[P_N];
+  bool on;
+  __device__ __forceinline__ static int64_t now() { return (int64_t)__builtin_readcyclecounter(); }
+};
+
 // One compressed block at in[0, n) → out[op, ...); returns Z_OK and advances op, or an error.  `done`: output known
 // complete (visible to every lane) at the last wait.
 __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int32_t& op, int32_t cap,
-                                ZTables& T, FrameState& fs, int gl, int32_t& done) {
+                                ZTables& T, FrameState& fs, int gl, int32_t& done, Prof& pf) {
+  int64_t t0 = pf.on ? Prof::now() : 0;
   if (n < 1) return Z_TRUNC;
   const uint32_t b0 = in[0];
   const int lt = (int)(b0 & 3), sf = (int)((b0 >> 2) & 3);
@@ -438,6 +448,7 @@ __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int3
     } else if (!fs.hufv) {
       return Z_HUF;
     }
+    if (pf.on) { const int64_t t = Prof::now(); pf.v[P_HUFTAB] += t - t0; t0 = t; pf.v[P_NLIT] += regen; }
     uint8_t* lbuf = out + (cap - regen);
     const uint8_t* sp = in + hdr + tree;
     const int32_t sn = csize - tree;
@@ -463,6 +474,7 @@ __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int3
     if ((bad >> grp) & 0xFFFFull) return Z_HUF;
     stores_visible();
     lit = lbuf;
+    if (pf.on) { const int64_t t = Prof::now(); pf.v[P_LITS] += t - t0; t0 = t; }
   }
   // ---- sequences
   const uint8_t* sp = in + hdr + csize;
@@ -493,6 +505,7 @@ __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int3
         < 0)
       return Z_FSE;
     q += d;
+    if (pf.on) { const int64_t t = Prof::now(); pf.v[P_SEQTAB] += t - t0; t0 = t; pf.v[P_NSEQ] += nseq; }
     BitB b;
     if (!b.init(sp + q, sn - q)) return Z_SEQ;
     uint32_t sll = b.read(fs.llog), sof = b.read(fs.olog), sml = b.read(fs.mlog);
@@ -546,6 +559,7 @@ __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int3
       op += ml;
     }
     if (b.left() != 0) return Z_SEQ;
+    if (pf.on) pf.v[P_SEQ] += Prof::now() - t0;
   }
   const int32_t rest = regen - lpos;
   if (rest > cap - op) return Z_OVERFLOW;
@@ -561,7 +575,7 @@ __global__ __launch_bounds__(ZWG) void zstd_frame_kernel(const uint8_t* __restri
                                                           const int64_t* __restrict__ out_off,
                                                           const int64_t* __restrict__ cap_arr, int64_t nb,
                                                           uint8_t* __restrict__ dst, int64_t* __restrict__ produced,
-                                                          int32_t* __restrict__ status) {
+                                                          int32_t* __restrict__ status, int64_t* __restrict__ prof) {
   __shared__ ZTables tabs[ZWG / ZG];
   ZTables& T = tabs[threadIdx.x / ZG];
   const int64_t b = ((int64_t)blockIdx.x * ZWG + threadIdx.x) / ZG;
@@ -610,6 +624,10 @@ __global__ __launch_bounds__(ZWG) void zstd_frame_kernel(const uint8_t* __restri
     if (single) window = fcs;
     if (window > 0 && window < bmax) bmax = (int32_t)window;
   }
+  Prof pf;
+  pf.on = prof != nullptr;
+  for (int k = 0; k < P_N; ++k) pf.v[k] = 0;
+  const int64_t tf = pf.on ? Prof::now() : 0;
   FrameState fs;
   fs.rep0 = 1; fs.rep1 = 4; fs.rep2 = 8;
   fs.llog = fs.olog = fs.mlog = 0;
@@ -639,7 +657,8 @@ __global__ __launch_bounds__(ZWG) void zstd_frame_kernel(const uint8_t* __restri
     } else if (type == 2) {
       if (size > bmax || ip + size > n) { rc = Z_BLOCK; break; }
       const int32_t op0 = op;
-      rc = decode_block(in + ip, size, out, op, cap, T, fs, gl, done);
+      rc = decode_block(in + ip, size, out, op, cap, T, fs, gl, done, pf);
+      ++pf.v[P_NBLK];
       if (rc == Z_OK && op - op0 > bmax) rc = Z_BLOCK;
       ip += size;
     } else {
@@ -653,6 +672,10 @@ __global__ __launch_bounds__(ZWG) void zstd_frame_kernel(const uint8_t* __restri
   if (gl == 0) {
     status[b] = rc;
     produced[b] = rc == Z_OK ? op : 0;
+    if (pf.on) {
+      pf.v[P_TOTAL] = Prof::now() - tf;
+      for (int k = 0; k < P_N; ++k) prof[b * P_N + k] = pf.v[k];
+    }
   }
 }
 
@@ -667,6 +690,19 @@ DXA_API int dxa_zstd_decode_into(const void* src, const void* comp_off, const vo
   hipLaunchKernelGGL(zstd_frame_kernel, dim3((unsigned)((nb * ZG + ZWG - 1) / ZWG)), dim3(ZWG), 0, (hipStream_t)st,
                      (const uint8_t*)src, (const int64_t*)comp_off, (const int32_t*)comp_len, (const uint8_t*)kind,
                      (const int64_t*)out_off, (const int64_t*)cap, nb, (uint8_t*)dst, (int64_t*)produced,
-                     (int32_t*)status);
+                     (int32_t*)status, (int64_t*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// The same decode with per-frame phase counters: prof[b * 8 + k] (k: total / Huffman table / literal streams /
+// sequence tables / sequence loop cycles, blocks, sequences, literals).  Measurement tool only.
+DXA_API int dxa_zstd_decode_prof(const void* src, const void* comp_off, const void* comp_len, const void* kind,
+                                 const void* out_off, const void* cap, int64_t nb, void* dst, void* produced,
+                                 void* status, void* prof, void* st) {
+  if (nb <= 0) return 0;
+  hipLaunchKernelGGL(zstd_frame_kernel, dim3((unsigned)((nb * ZG + ZWG - 1) / ZWG)), dim3(ZWG), 0, (hipStream_t)st,
+                     (const uint8_t*)src, (const int64_t*)comp_off, (const int32_t*)comp_len, (const uint8_t*)kind,
+                     (const int64_t*)out_off, (const int64_t*)cap, nb, (uint8_t*)dst, (int64_t*)produced,
+                     (int32_t*)status, (int64_t*)prof);
   return (int)hipGetLastError();
 }

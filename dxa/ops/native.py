@@ -35,6 +35,7 @@ _SIGS = {
     "dxa_inflate_into": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p],
     "dxa_snappy_decode_into": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p],
     "dxa_zstd_decode_into": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p],
+    "dxa_zstd_decode_prof": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
     "dxa_kafka_records": [c_p, c_i64] + [c_p] * 14,
     "dxa_kafka_crc": [c_p, c_i64, c_p, c_p, c_p, c_p, c_p],
     "dxa_csv_tokenize": [c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p],
