@@ -753,6 +753,15 @@ def scalar_to(v, t: DecimalType, to: str):
     raise TypeError(to)
 
 
+def true_div(x: torch.Tensor, d: float) -> torch.Tensor:
+    """x / d correctly rounded on every device.  PyTorch's GPU division by a Python scalar multiplies by the
+    reciprocal (1/d is inexact for d = 10^k, so e.g. 201 / 200 comes out one ulp off); a 0-dim device tensor as the
+    divisor takes the true division."""
+    if x.device.type == "cpu":
+        return x / d
+    return x / torch.full((), d, dtype=x.dtype, device=x.device)
+
+
 def to_double(col):
     """decimal column → double column (correctly rounded while |unscaled| < 2^53, i.e. all narrow values up to
     15-16 digits; wide values round once more)."""
@@ -760,7 +769,7 @@ def to_double(col):
     t: DecimalType = col.dtype
     h, l = lanes(col.data)
     f = l.to(torch.float64) if t.narrow else to_float64(h, l)
-    return PrimColumn("double", f / float(10 ** t.scale) if t.scale else f, col.valid)
+    return PrimColumn("double", true_div(f, float(10 ** t.scale)) if t.scale else f, col.valid)
 
 
 def to_integral(col, to: str):

@@ -1009,7 +1009,7 @@ def cast_column(col: Column, to: str) -> Column:
             return PrimColumn(to, r, col.valid)
         if to in ("double", "float", "decimal"):
             if col.dtype == "timestamp":
-                return PrimColumn(to, d.to(torch.float64) / 1e6, col.valid)
+                return PrimColumn(to, D.true_div(d.to(torch.float64), 1e6), col.valid)
             return PrimColumn(to, d.to(torch.float64), col.valid)
         if to == "boolean":
             return PrimColumn("boolean", d != 0, col.valid)
@@ -1037,7 +1037,7 @@ def _cast_decimal(col: Column, to) -> Optional[Column]:
         if col.dtype in ("double", "float") and isinstance(col, PrimColumn):
             return D.from_double(col, to)
         if col.dtype == "timestamp" and isinstance(col, PrimColumn):
-            return D.from_double(PrimColumn("double", col.data.to(torch.float64) / 1e6, col.valid), to)
+            return D.from_double(PrimColumn("double", D.true_div(col.data.to(torch.float64), 1e6), col.valid), to)
         if col.dtype == "string" and isinstance(col, StrColumn):
             return D.from_text(col, to)
         raise EvalError(f"cannot cast {col.dtype} to {to}")
@@ -1515,17 +1515,18 @@ def _f_round(e, scope, ctx, subst):
         return PrimColumn(a.dtype, res.to(a.data.dtype), a.valid)
     x = a.data.to(torch.float64)
     ax = x.abs()
+    # (divisions through D.true_div: the GPU's scalar division is a reciprocal multiply, an ulp off at the ties)
     if digits >= 0:
         sc = 10.0 ** digits
         f = torch.floor(ax * sc)
-        t = (2 * f + 1) / (2 * sc)
+        t = D.true_div(2 * f + 1, 2 * sc)
     else:
         sc = 10.0 ** (-digits)
-        f = torch.floor(ax / sc)
+        f = torch.floor(D.true_div(ax, sc))
         t = (2 * f + 1) * sc / 2
     tie_up = (torch.remainder(f, 2) == 1) if half_even else torch.ones_like(ax, dtype=torch.bool)
     r = f + ((ax > t) | ((ax == t) & tie_up)).to(torch.float64)
-    res = torch.sign(x) * (r / sc if digits >= 0 else r * sc)
+    res = torch.sign(x) * (D.true_div(r, sc) if digits >= 0 else r * sc)
     res = torch.where(torch.isfinite(x), res, x)                  # NaN / ±Infinity pass through
     rt = "float" if a.dtype == "float" else "double"
     if rt == "float":

@@ -22,6 +22,7 @@ import torch
 
 from ..sql import ast as A
 from . import functions as F
+from .decimal import true_div as _true_div
 from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, column_from_pylist,
                      materialize, strings_from_pylist)
 from .expr import (EvalError, _args, _host_string_fn, _slot_present, bool_col, cast_column, evaluate,
@@ -214,7 +215,7 @@ def _f_months_between(e, scope, ctx, subst):
     def parts(us):
         days = F.floor_div(us, F.US_PER_DAY)
         y, m, d = F.civil_from_days(days)
-        sec = (us - days * F.US_PER_DAY).to(torch.float64) / 1e6
+        sec = _true_div((us - days * F.US_PER_DAY).to(torch.float64), 1e6)
         return y, m, d, sec, _month_len(y, m)
     ya, ma, da, sa, la = parts(a.data)
     yb, mb, db, sb, lb = parts(b.data)

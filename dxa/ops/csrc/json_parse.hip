@@ -766,15 +766,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       if (r.ws_cur() != ':') break;
       ++r.p;
       c = r.ws_cur();
-      if (node < 0) goto skip_any;
+      if (node < 0 || (tb.node_type[node] & 0xff) == FT_SKIP) goto skip_any;
       const int t = tb.node_type[node] & 0xff;
-      // a pruned field's scalar runs through the typed scanners below, which store nothing for FT_SKIP: cheaper
-      // than the container-capable skipper, which only its containers need
-      if (t == FT_SKIP && (c == '{' || c == '[')) goto skip_any;
       const bool raw_arr = (tb.node_type[node] & 0x100) != 0;
       const int vs = tb.val_slot[node];
       const int ls = tb.len_slot[node];
-      if (node < 64 && t != FT_SKIP) {                    // a repeated key: its last occurrence decides (null on a
+      if (node < 64) {                                    // a repeated key: its last occurrence decides (null on a
         const uint64_t bit = 1ull << node;                // mismatch), as a tokenizing parser's last write would
         const uint64_t seen = s_seen[threadIdx.x];
         if (seen & bit) a.valid[(int64_t)node * n + row] = 0;
