@@ -393,8 +393,15 @@ struct Prof {
 
 // One compressed block at in[0, n) → out[op, ...); returns Z_OK and advances op, or an error.  `done`: output known
 // complete (visible to every lane) at the last wait.
+// Literal-length / match-length codes → base | extra bits << 24, staged in LDS per workgroup: the sequence loop's
+// lookups are indexed by decoded values, and from __constant__ memory each would be a dependent global load.
+struct CodeTabs {
+  uint32_t ll[36];
+  uint32_t ml[53];
+};
+
 __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int32_t& op, int32_t cap,
-                                ZTables& T, FrameState& fs, int gl, int32_t& done, Prof& pf) {
+                                ZTables& T, const CodeTabs& C, FrameState& fs, int gl, int32_t& done, Prof& pf) {
   int64_t t0 = pf.on ? Prof::now() : 0;
   if (n < 1) return Z_TRUNC;
   const uint32_t b0 = in[0];
@@ -520,8 +527,9 @@ __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int3
       } else {
         ofv = (1u << ofc) + b.read((int)ofc);
       }
-      const int32_t ml = (int32_t)(kMLBase[mlc] + b.read(kMLBits[mlc]));
-      const int32_t ll = (int32_t)(kLLBase[llc] + b.read(kLLBits[llc]));
+      const uint32_t cm = C.ml[mlc], cl = C.ll[llc];
+      const int32_t ml = (int32_t)((cm & 0xFFFFFFu) + b.read((int)(cm >> 24)));
+      const int32_t ll = (int32_t)((cl & 0xFFFFFFu) + b.read((int)(cl >> 24)));
       uint32_t off;
       if (ofv > 3) {
         off = ofv - 3;
@@ -555,7 +563,7 @@ __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int3
         stores_visible();
         done = op;
       }
-      for (int32_t c = gl; c < ml; c += ZG) out[op + c] = out[s + (c % (int32_t)off)];
+      for (int32_t c = gl; c < ml; c += ZG) out[op + c] = out[s + (c < (int32_t)off ? c : c % (int32_t)off)];
       op += ml;
     }
     if (b.left() != 0) return Z_SEQ;
@@ -577,7 +585,13 @@ __global__ __launch_bounds__(ZWG) void zstd_frame_kernel(const uint8_t* __restri
                                                           uint8_t* __restrict__ dst, int64_t* __restrict__ produced,
                                                           int32_t* __restrict__ status, int64_t* __restrict__ prof) {
   __shared__ ZTables tabs[ZWG / ZG];
+  __shared__ CodeTabs codes;
   ZTables& T = tabs[threadIdx.x / ZG];
+  for (int k = threadIdx.x; k < 36 + 53; k += ZWG) {       // (whole workgroup, before any early exit)
+    if (k < 36) codes.ll[k] = kLLBase[k] | ((uint32_t)kLLBits[k] << 24);
+    else codes.ml[k - 36] = kMLBase[k - 36] | ((uint32_t)kMLBits[k - 36] << 24);
+  }
+  __syncthreads();
   const int64_t b = ((int64_t)blockIdx.x * ZWG + threadIdx.x) / ZG;
   const int gl = (int)(threadIdx.x & (ZG - 1));
   if (b >= nb || kind[b] != 4) return;
@@ -657,7 +671,7 @@ __global__ __launch_bounds__(ZWG) void zstd_frame_kernel(const uint8_t* __restri
     } else if (type == 2) {
       if (size > bmax || ip + size > n) { rc = Z_BLOCK; break; }
       const int32_t op0 = op;
-      rc = decode_block(in + ip, size, out, op, cap, T, fs, gl, done, pf);
+      rc = decode_block(in + ip, size, out, op, cap, T, codes, fs, gl, done, pf);
       ++pf.v[P_NBLK];
       if (rc == Z_OK && op - op0 > bmax) rc = Z_BLOCK;
       ip += size;
