@@ -55,18 +55,41 @@ def _hash_bytes_np(b: bytes) -> np.uint64:
         return _fmix64(np.array([h ^ np.uint64(n)], dtype=np.uint64))[0]
 
 
+def _hash_strs_np(arena: np.ndarray, starts: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """``_hash_bytes_np`` of every string at once: word k of all strings in one vector step (little-endian 8-byte
+    words, the short tail word zero-extended), so the CPU path costs O(longest / 8) numpy passes, not a Python loop
+    per string."""
+    n = len(lens)
+    lens = lens.astype(np.int64)
+    starts = starts.astype(np.int64)
+    pad = np.zeros(arena.size + 8, dtype=np.uint8)
+    pad[:arena.size] = arena
+    nw = lens // 8
+    tail = lens - nw * 8
+    lane = np.arange(8, dtype=np.int64)
+
+    def word(off):
+        return pad[off[:, None] + lane].view(np.uint64).reshape(-1)
+
+    with np.errstate(over="ignore"):
+        h = SEED ^ (lens.astype(np.uint64) * GOLD)
+        for k in range(int(nw.max()) if n else 0):
+            m = nw > k
+            h[m] = _fmix64(h[m] ^ word(starts[m] + 8 * k))
+        m = tail > 0
+        if m.any():
+            w = word(starts[m] + 8 * nw[m])
+            keep = (np.uint64(1) << (tail[m].astype(np.uint64) * np.uint64(8))) - np.uint64(1)
+            h[m] = _fmix64(h[m] ^ (w & keep))
+        return _fmix64(h ^ lens.astype(np.uint64))
+
+
 def _col_hash_np(col) -> np.ndarray:
     from ..engine.column import PrimColumn, StrColumn, ConstColumn, materialize
     col = materialize(col)
     n = col.length
     if isinstance(col, StrColumn):
-        arena = col.arena.cpu().numpy().tobytes()
-        starts = col.starts.cpu().numpy()
-        lens = col.lens.cpu().numpy()
-        out = np.empty(n, dtype=np.uint64)
-        for i in range(n):
-            s = int(starts[i])
-            out[i] = _hash_bytes_np(arena[s:s + int(lens[i])])
+        out = _hash_strs_np(col.arena.cpu().numpy(), col.starts.cpu().numpy(), col.lens.cpu().numpy())
     elif isinstance(col, PrimColumn):
         d = col.data.cpu()
         if d.dtype == torch.float64:
