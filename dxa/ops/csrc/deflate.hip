@@ -280,7 +280,7 @@ template <bool kDyn>
 __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restrict__ in, int64_t n_in, int32_t chunk,
                                                          int64_t n_chunks, uint8_t* __restrict__ slots,
                                                          int64_t slot_bytes, int32_t* __restrict__ out_len,
-                                                         CrcPow pw) {
+                                                         CrcPow pw, uint32_t* __restrict__ toks) {
   extern __shared__ uint32_t gz_sh[];
   __shared__ uint32_t crc_tab[256];
   const int lane = threadIdx.x;
@@ -361,9 +361,13 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
     // pass 1: parse, count symbols
     for (int k = lane; k < kNSym; k += 64) hist[k] = 0;
     __syncthreads();
+    uint32_t* tk = toks + c * chunk;
     for (int32_t g = 0; g < L; g += 64) {
       uint32_t lit; int32_t len, dist;
       const int t = parse_group(dat32, head, L, g, carry, lane, lit, len, dist);
+      // the parse, kept for pass 2 (coalesced, 256 B per group): type << 30 | literal, or len << 15 | dist
+      if (g + lane < L)
+        tk[g + lane] = t == 1 ? (1u << 30) | lit : t == 2 ? (2u << 30) | ((uint32_t)len << 15) | (uint32_t)dist : 0u;
       if (t == 1) {
         atomicAdd(&hist[lit], 1u);
       } else if (t == 2) {
@@ -436,11 +440,20 @@ __global__ void __launch_bounds__(64) gzip_chunks_kernel(const uint8_t* __restri
     o.emit(lane == 0 ? 3u : 0u, lane == 0 ? 3u : 0u, 0, 0, lane);      // BFINAL, BTYPE = 01
   }
 
-  // pass 2: the same parse, coded
+  // pass 2: the parse coded (dynamic: read back from pass 1's tokens instead of parsing again)
   carry = 0;
   for (int32_t g = 0; g < L; g += 64) {
-    uint32_t lit; int32_t len, dist;
-    const int t = parse_group(dat32, head, L, g, carry, lane, lit, len, dist);
+    uint32_t lit = 0; int32_t len = 0, dist = 0;
+    int t;
+    if constexpr (kDyn) {
+      const uint32_t w = g + lane < L ? toks[c * chunk + g + lane] : 0u;
+      t = (int)(w >> 30);
+      lit = w & 0xffu;
+      len = (int32_t)((w >> 15) & 0x1ffu);
+      dist = (int32_t)(w & 0x7fffu);
+    } else {
+      t = parse_group(dat32, head, L, g, carry, lane, lit, len, dist);
+    }
     uint32_t a = 0, na = 0, b = 0, nb = 0;
     if (t == 1) {
       const uint32_t e = kDyn ? tab[lit] : fixed_code(lit);
@@ -493,10 +506,13 @@ DXA_API int64_t dxa_gzip_slot_bytes(int32_t chunk) {
   return ((int64_t)kHdr + ((int64_t)chunk * 9 + 7) / 8 + 32 + 15) & ~(int64_t)15;
 }
 
+// dynamic: per-member Huffman tables from a counting pass (the block keeps the fixed code when that is smaller);
+// `toks` (n_chunks x chunk words) holds the counting pass's parse, so the coding pass does not parse again.
 DXA_API int dxa_gzip_chunks(const uint8_t* in, int64_t n_in, int32_t chunk, uint8_t* slots, int32_t* out_len,
-                            int32_t dynamic, void* st) {
+                            int32_t dynamic, uint32_t* toks, void* st) {
   if (n_in <= 0) return 0;
   if (chunk < 64 || chunk > 32768 || (chunk & 63)) return (int)hipErrorInvalidValue;   // deflate window
+  if (dynamic && toks == nullptr) return (int)hipErrorInvalidValue;
   const int64_t n_chunks = (n_in + chunk - 1) / chunk;
   const int64_t slot = dxa_gzip_slot_bytes(chunk);
   const size_t lds = ((size_t)(chunk >> 2) + 4 + kHashSize / 2 + kRing + (dynamic ? 3 * kNSym + 16 : 0)) * 4;
@@ -507,10 +523,10 @@ DXA_API int dxa_gzip_chunks(const uint8_t* in, int64_t n_in, int32_t chunk, uint
   for (int l = 0; l < 6; ++l) pw.x[l] = host_x8n((uint64_t)pw.slice << l);
   if (dynamic)
     hipLaunchKernelGGL(gzip_chunks_kernel<true>, dim3((unsigned)n_chunks), dim3(64), lds, (hipStream_t)st, in, n_in,
-                       chunk, n_chunks, slots, slot, out_len, pw);
+                       chunk, n_chunks, slots, slot, out_len, pw, toks);
   else
     hipLaunchKernelGGL(gzip_chunks_kernel<false>, dim3((unsigned)n_chunks), dim3(64), lds, (hipStream_t)st, in, n_in,
-                       chunk, n_chunks, slots, slot, out_len, pw);
+                       chunk, n_chunks, slots, slot, out_len, pw, (uint32_t*)nullptr);
   return (int)hipGetLastError();
 }
 

@@ -13,8 +13,10 @@ import torch
 from . import native as N
 
 CHUNK = int(os.environ.get("DXA_GZIP_CHUNK", "8192"))
-# dynamic Huffman tables per member (a counting pass first): ~1.2x smaller on serialized events, ~2x the kernel time
-DYNAMIC = os.environ.get("DXA_GZIP_DYNAMIC", "0") != "0"
+# dynamic Huffman tables per member (a counting pass whose parse the coding pass reuses), the default: on the
+# passthrough output 3.18x vs 2.53x with the fixed code, 54.7 vs 91.9 GB/s, and the blob-sink flow at 40.8 vs
+# 43.3 M events/s (profiles/round5/blob/README.md).  DXA_GZIP_DYNAMIC=0 selects the fixed code.
+DYNAMIC = os.environ.get("DXA_GZIP_DYNAMIC", "1") != "0"
 
 
 def slot_bytes(chunk: int) -> int:
@@ -35,7 +37,10 @@ def gzip_device(buf: torch.Tensor, n: int, chunk: int = CHUNK, dynamic: bool = D
     slots = torch.empty(nch * slot_bytes(chunk), dtype=torch.uint8, device=dev)
     out_len = torch.empty(nch, dtype=torch.int32, device=dev)
     st = N.stream_handle(dev)
-    N.call("dxa_gzip_chunks", N.ptr(buf), n, chunk, N.ptr(slots), N.ptr(out_len), int(dynamic), st)
+    # dynamic: the counting pass's parse (one word per input byte), read back by the coding pass
+    toks = torch.empty(nch * chunk, dtype=torch.int32, device=dev) if dynamic else None
+    N.call("dxa_gzip_chunks", N.ptr(buf), n, chunk, N.ptr(slots), N.ptr(out_len), int(dynamic),
+           N.ptr(toks) if dynamic else None, st)
     ends = torch.cumsum(out_len.to(torch.int64), 0)
     offs = ends - out_len
     total = int(ends[-1].item())

@@ -79,7 +79,7 @@ _SIGS = {
     "dxa_str_rlike": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_i32, c_i32, c_p, c_p],
     "dxa_str_regex": [c_p, c_p, c_p, c_i64, c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p,
                       c_p, c_p],
-    "dxa_gzip_chunks": [c_p, c_i64, c_i32, c_p, c_p, c_i32, c_p],
+    "dxa_gzip_chunks": [c_p, c_i64, c_i32, c_p, c_p, c_i32, c_p, c_p],
     "dxa_gzip_pack": [c_p, c_i32, c_p, c_p, c_i64, c_p, c_p],
     "dxa_str_digest": [c_p, c_p, c_p, c_i64, c_i32, c_p, c_p],
     "dxa_str_crc32": [c_p, c_p, c_p, c_i64, c_p, c_p],
