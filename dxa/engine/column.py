@@ -773,6 +773,7 @@ def concat_tables(tables: List[Table]) -> Table:
         for (at, parts), (arena, starts, lens) in zip(str_groups, got):
             valid, _ = valid_segments(parts, device, segs)
             cols[at] = type(parts[0])(arena, starts, lens, valid, parts[0].dtype)
+            cols[at]._compact = True        # disjoint, in order in a fresh arena: its size bounds the bytes
     if segs:
         segs.launch(device)                         # every fixed-width leaf of every table: one launch
     return Table(names, cols, sum(t.length for t in tables), device)

@@ -138,7 +138,13 @@ def concat_multi(groups: Sequence[Sequence]):
                  torch.zeros(0, dtype=torch.int32, device=device)) for _ in groups]
     cs = torch.cumsum(lens_all, 0, dtype=torch.int64)
     ex = cs - lens_all
-    dst = _alloc_arena(int(cs[-1].item()), device)
+    if all(getattr(c, "_compact", False) for c in flat):
+        # every part's arena holds exactly its rows' bytes (compaction outputs: window panes): their sizes bound the
+        # total on the host, so the batch thread does not wait for the scan
+        total = sum(int(c.arena.numel()) for c in flat)
+    else:
+        total = int(cs[-1].item())
+    dst = _alloc_arena(total, device)
     out, parts, pos = [], [], 0
     for g in groups:
         n = sum(c.length for c in g)
