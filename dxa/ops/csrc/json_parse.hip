@@ -252,6 +252,32 @@ __device__ __forceinline__ bool key_matches(Reader& r, int64_t q, int64_t end, K
   return ((tail ^ want) & mask) == 0;
 }
 
+// The expected key at q, its closing quote and — in the same 8-byte compare when it lies in the key's last word —
+// the ':' right after it (compact JSON: no blank between key and colon).  Returns 0: no match; 1: key, quote and
+// colon (r.p is then past the colon, and `next` holds the byte after the colon when that byte was in the compared
+// word, else 256); 2: key and quote only (the colon, after blanks, is left to the generic path).
+template <typename KW>
+__device__ __forceinline__ int key_colon_matches(Reader& r, int64_t q, int64_t end, KW kw, int L, uint32_t& next) {
+  if (q + L >= end) return 0;
+  int i = 0;
+  for (; i + 8 <= L; i += 8)
+    if (r.load8(q + i) != kw[i >> 3]) return 0;
+  const uint64_t tail = r.load8(q + i);
+  const int rem = L - i;                                   // 0..7 key bytes, then the quote (and the colon)
+  const uint64_t want = (rem ? kw[i >> 3] : 0ull) | ((uint64_t)'"' << (8 * rem));
+  const uint64_t mq = rem == 7 ? ~0ull : ((1ull << (8 * (rem + 1))) - 1);
+  if ((tail ^ want) & mq) return 0;
+  next = 256u;
+  if (rem == 7) {                                          // the colon is the next word's first byte
+    if (q + L + 1 >= end || r.at(q + L + 1) != ':') return 2;
+  } else {
+    if (q + L + 1 >= end || ((tail >> (8 * (rem + 1))) & 0xffu) != ':') return 2;
+    if (rem <= 5 && q + L + 2 < end) next = (uint32_t)((tail >> (8 * (rem + 2))) & 0xffu);
+  }
+  r.p = q + L + 2;
+  return 1;
+}
+
 // SWAR byte tests on 8 bytes (little-endian: byte 0 = first char): high bit of each byte lane flags the property.
 __device__ __forceinline__ uint64_t swar_eq(uint64_t x, uint64_t pat) {
   const uint64_t v = x ^ pat;
@@ -277,18 +303,27 @@ __device__ __forceinline__ uint64_t swar_ctl(uint64_t x) {
 // Scan a string whose opening quote is at r.p.  On return r.p is past the closing quote.  Eight bytes per step:
 // the first quote, backslash or control character is found with SWAR compares (a string of ~10 chars is one or
 // two steps).  An unescaped control character makes the record malformed (strict JSON, as Jackson's default).
-__device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, bool& esc) {
+// `after`: the byte following the closing quote when the compared word holds it (256 otherwise) — the caller's
+// next token without another window read.
+__device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, bool& esc, uint32_t& after) {
   ++r.p;
   s = r.p;
   esc = false;
+  after = 256u;
   while (r.p < r.end) {
     const uint64_t x = r.load8(r.p);
     const uint64_t m = swar_eq(x, 0x2222222222222222ull) | swar_eq(x, 0x5C5C5C5C5C5C5C5Cull) | swar_ctl(x);
     if (m == 0) { r.p += 8; continue; }
-    r.p += __builtin_ctzll(m) >> 3;
+    const int j = __builtin_ctzll(m) >> 3;
+    r.p += j;
     if (r.p >= r.end) break;
-    const uint32_t c = (uint32_t)((x >> (8 * ((__builtin_ctzll(m) >> 3)))) & 0xff);
-    if (c == '"') { e = r.p; ++r.p; return true; }
+    const uint32_t c = (uint32_t)((x >> (8 * j)) & 0xff);
+    if (c == '"') {
+      e = r.p;
+      ++r.p;
+      if (j < 7 && r.p < r.end) after = (uint32_t)((x >> (8 * (j + 1))) & 0xff);
+      return true;
+    }
     if (c < 0x20u) break;                                 // raw control character inside a string
     esc = true;
     if (r.p + 1 >= r.end) break;
@@ -309,6 +344,10 @@ __device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, b
   }
   r.p = r.end;
   return false;
+}
+__device__ __forceinline__ bool scan_string(Reader& r, int64_t& s, int64_t& e, bool& esc) {
+  uint32_t after;
+  return scan_string(r, s, e, esc, after);
 }
 
 __device__ __forceinline__ uint32_t hexval(uint32_t c) {
@@ -374,15 +413,21 @@ __device__ __forceinline__ int64_t unescape_inplace(Reader& r, int64_t s, int64_
 // Run of decimal digits at r.p, accumulated into (mant, nd, exp10) exactly as a digit-serial loop would: at most
 // 19 significant digits kept (leading zeros are not significant); integer-part digits beyond that raise exp10 and
 // set `lost`; fraction digits beyond it are dropped.  Eight characters per step (SWAR digit test + conversion).
+// `first`: the run's first character; `term`: the character that ended it when the last compared word holds it
+// (256 otherwise: the record's end, or a word boundary).
 __device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, int& exp10, bool& lost, bool frac,
-                                            uint64_t& tail, int& nt) {
+                                            uint64_t& tail, int& nt, uint32_t& first, uint32_t& term) {
   bool any = false;
+  term = 256u;
   while (r.p < r.end) {
     const uint64_t x = r.load8(r.p);
     const uint64_t nm = swar_nondigit(x);
     int k = nm ? (__builtin_ctzll(nm) >> 3) : 8;
-    if (k > r.end - r.p) k = (int)(r.end - r.p);
+    const bool clamped = k > r.end - r.p;
+    if (clamped) k = (int)(r.end - r.p);
+    if (!clamped && k < 8) term = (uint32_t)((x >> (8 * k)) & 0xff);
     if (k == 0) break;
+    if (!any) first = (uint32_t)(x & 0xff);
     any = true;
     const uint64_t chunk = swar_digits(x, k);
     int sig = k;                                          // significant digits this chunk adds
@@ -419,22 +464,30 @@ __device__ __forceinline__ bool scan_digits(Reader& r, uint64_t& mant, int& nd, 
   return any;
 }
 
-// Parse a JSON number at r.p.  Returns false on syntax error.
-__device__ __forceinline__ bool scan_number(Reader& r, bool& is_int, bool& overflow, int64_t& iv, double& dv) {
+// Parse a JSON number at r.p, whose first character c the caller has read.  Returns false on syntax error.
+// `term`: the character after the number when a digit scan saw it (256: unknown).
+__device__ __forceinline__ bool scan_number(Reader& r, uint32_t c, bool& is_int, bool& overflow, int64_t& iv,
+                                            double& dv, uint32_t& term) {
   bool neg = false;
-  if (r.cur() == '-') { neg = true; ++r.p; }
-  if (r.cur() == '0' && r.p + 1 < r.end && is_digit(r.at(r.p + 1))) return false;    // JSON: no leading zeros
+  if (c == '-') { neg = true; ++r.p; }
   uint64_t mant = 0, tail = 0;
   int nd = 0, exp10 = 0, nt = 0;
   bool lost = false;
   is_int = true;
-  if (!scan_digits(r, mant, nd, exp10, lost, false, tail, nt)) return false;
-  if (r.p < r.end && r.at(r.p) == '.') {
+  const int64_t s0 = r.p;
+  uint32_t first = 0;
+  if (!scan_digits(r, mant, nd, exp10, lost, false, tail, nt, first, term)) return false;
+  if (first == '0' && r.p - s0 > 1) return false;                                     // JSON: no leading zeros
+  if (term == 256u) term = r.cur();
+  if (term == '.') {
     is_int = false;
     ++r.p;
-    if (!scan_digits(r, mant, nd, exp10, lost, true, tail, nt)) return false;
+    uint32_t f2;
+    if (!scan_digits(r, mant, nd, exp10, lost, true, tail, nt, f2, term)) return false;
+    if (term == 256u) term = r.cur();
   }
-  if (r.p < r.end && (r.at(r.p) | 0x20u) == 'e') {
+  if ((term | 0x20u) == 'e') {
+    term = 256u;
     is_int = false;
     ++r.p;
     bool eneg = false;
@@ -729,8 +782,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
   expect(0) = tb.first_child[0];
   depth = 1;
   a.valid[row] = 1;  // root struct present
+  uint32_t nextc;             // the character after a scanned value when its scanner saw it (256: read it)
   while (true) {
     r.top_up(kTopUp);                        // key + typical value of the next field, all low lanes at once
+    nextc = 256u;
     uint32_t c = r.ws_cur();
     if (c == '}') {
       if (comma) break;       // trailing comma: {"a":1,}
@@ -746,7 +801,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       ++r.p;
       int node = -1;
       const int ex = expect(depth - 1);
-      if (ex >= 0 && key_matches(r, r.p, r.end, tb.key_words + tb.key_word[ex], tb.key_len[ex])) {
+      int km = 0;
+      uint32_t nx = 256u;
+      if (ex >= 0) km = key_colon_matches(r, r.p, r.end, tb.key_words + tb.key_word[ex], tb.key_len[ex], nx);
+      if (km == 1) {                                      // `"key":` in one go: straight to the value
+        node = ex;
+        expect(depth - 1) = tb.next_sib[node];
+        c = (nx == 256u || nx == ' ' || nx == '\n' || nx == '\r' || nx == '\t') ? r.ws_cur() : nx;
+        goto have_value;
+      }
+      if (km == 2) {
         node = ex;
         r.p += tb.key_len[ex] + 1;
       } else {
@@ -766,6 +830,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       if (r.ws_cur() != ':') break;
       ++r.p;
       c = r.ws_cur();
+    have_value:
       if (node < 0 || (tb.node_type[node] & 0xff) == FT_SKIP) goto skip_any;
       const int t = tb.node_type[node] & 0xff;
       const bool raw_arr = (tb.node_type[node] & 0x100) != 0;
@@ -793,7 +858,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       if (c == '"') {
         int64_t s, e;
         bool esc;
-        if (!scan_string(r, s, e, esc)) break;
+        if (!scan_string(r, s, e, esc, nextc)) break;
         if (t == FT_STRING) {
           const int64_t len = esc ? unescape_inplace(r, s, e) : (e - s);
           a.vals[(int64_t)vs * n + row] = s;
@@ -815,7 +880,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
         bool is_int, of;
         int64_t iv = 0;
         double dv = 0.0;
-        if (!scan_number(r, is_int, of, iv, dv)) break;
+        if (!scan_number(r, c, is_int, of, iv, dv, nextc)) break;
         if (t == FT_LONG || t == FT_INT) {
           if (is_int && !of && (t == FT_LONG || (iv >= -2147483648ll && iv <= 2147483647ll))) {
             a.vals[(int64_t)vs * n + row] = iv;
@@ -868,7 +933,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       }
     }
   after_value:
-    c = r.ws_cur();
+    c = (nextc == 256u || nextc == ' ' || nextc == '\n' || nextc == '\r' || nextc == '\t') ? r.ws_cur() : nextc;
     if (c == ',') { ++r.p; comma = true; continue; }
     if (c == '}') continue;  // closes the current object at loop top
     break;
