@@ -153,6 +153,8 @@ def main():
     ap.add_argument("--crc", choices=["host", "device", "off"], default="host",
                     help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): host planner "
                          "threads (default), the GPU (kafka_crc_kernel), or not at all")
+    ap.add_argument("--column-pruning", choices=["on", "off"], default="on",
+                    help="datax.job.process.columnpruning: parse and retain only the raw fields statements read")
     ap.add_argument("--sink", choices=["null", "blob"], default="null",
                     help="output sink: null (rendered JSON lands in host memory) or blob (gzip files under /tmp)")
     ap.add_argument("--profile-stages", action="store_true")
@@ -218,7 +220,8 @@ def main():
     # passthrough is bound by the D2H of its rendered JSON: two batches' outputs in flight overlap one batch's copy
     # with the next one's rendering (profiles/round4/output_depth/: 64.5 -> 71.8 M ev/s); the other flows keep one
     # (no gain measured, lower latency).  DXA_OUTPUT_DEPTH overrides.
-    depth_extra = {"datax.job.process.outputdepth": "2"} if flow == "passthrough" else None
+    depth_extra = {"datax.job.process.outputdepth": "2"} if flow == "passthrough" else {}
+    depth_extra["datax.job.process.columnpruning"] = "true" if args.column_pruning == "on" else "false"
     settings = iot.flow_settings(workdir=f"/tmp/dxa_bench_{flow}_{rank}", variant=flow, sink=args.sink,
                                  ref_rows=args.ref_rows, extra=depth_extra)
     ref_write_s = None

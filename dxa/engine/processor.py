@@ -136,6 +136,9 @@ class Processor:
             init_pool.shutdown(wait=True)
         from ..telemetry.metrics import MetricLogger
         self.metric_logger = MetricLogger.from_settings(d, metric_store)
+        # column pruning (datax.job.process.columnpruning, default on): the parser extracts and windows retain only
+        # the raw fields the live statements can read
+        parse_prune = parse_prune and d.get_bool(S.PROCESS_PREFIX + "columnpruning", True)
         self.parse_plan = ParsePlan(self.raw_schema, self._needed_raw_paths() if parse_prune else None)
         # input rebalance across ranks (reference: datax.job.input.default.eventhub.repartition → rdd.repartition)
         rp = d.get(S.INPUT_PREFIX + "eventhub.repartition") or d.get(S.INPUT_PREFIX + "repartition")

@@ -278,6 +278,32 @@ __device__ __forceinline__ int key_colon_matches(Reader& r, int64_t q, int64_t e
   return 1;
 }
 
+// After a member separator: the expected key's whole `"key":` at q (no blank before the quote or the colon), the
+// pattern's words shifted out of the key words on the fly.  True: r.p is past the colon and `next` holds the byte
+// after it when the last compared word holds it (256 otherwise).  False: nothing consumed.
+template <typename KW>
+__device__ __forceinline__ bool quote_key_colon(Reader& r, int64_t q, int64_t end, KW kw, int L, uint32_t& next) {
+  const int P = L + 3;                                     // '"' key '"' ':'
+  if (q + P > end) return false;
+  const int nkw = (L + 7) >> 3;
+  uint64_t x = 0;
+  int j = 0;
+  for (; 8 * j < P; ++j) {
+    x = r.load8(q + 8 * j);
+    uint64_t w = (j < nkw ? kw[j] << 8 : 0ull) | (j == 0 ? (uint64_t)'"' : (kw[j - 1] >> 56));
+    const int t0 = L + 1 - 8 * j, t1 = L + 2 - 8 * j;     // the closing quote and the colon in this word
+    if (t0 >= 0 && t0 < 8) w |= (uint64_t)'"' << (8 * t0);
+    if (t1 >= 0 && t1 < 8) w |= (uint64_t)':' << (8 * t1);
+    const int nb = P - 8 * j;                              // pattern bytes in this word
+    const uint64_t m = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+    if ((x ^ w) & m) return false;
+  }
+  const int used = P - 8 * (j - 1);                        // pattern bytes in the last word (1..8)
+  next = (used < 8 && q + P < end) ? (uint32_t)((x >> (8 * used)) & 0xffu) : 256u;
+  r.p = q + P;
+  return true;
+}
+
 // SWAR byte tests on 8 bytes (little-endian: byte 0 = first char): high bit of each byte lane flags the property.
 __device__ __forceinline__ uint64_t swar_eq(uint64_t x, uint64_t pat) {
   const uint64_t v = x ^ pat;
@@ -534,16 +560,53 @@ __device__ __forceinline__ bool take_literal(Reader& r, uint32_t c) {
   return good && r.p <= r.end;
 }
 
-// A run of digits at r.p, eight characters per step (SWAR digit test); false when there is none.
-__device__ __forceinline__ bool skip_digits(Reader& r) {
+// A run of digits at r.p, eight characters per step (SWAR digit test); false when there is none.  `first` / `term`
+// as in scan_digits: the run's first character, and the character that ended it when a compared word held it (256
+// otherwise).
+__device__ __forceinline__ bool skip_digits(Reader& r, uint32_t& first, uint32_t& term) {
   const int64_t s = r.p;
+  term = 256u;
   while (r.p < r.end) {
-    const uint64_t nm = swar_nondigit(r.load8(r.p));
-    if (nm) { r.p += __builtin_ctzll(nm) >> 3; break; }
+    const uint64_t x = r.load8(r.p);
+    if (r.p == s) first = (uint32_t)(x & 0xff);
+    const uint64_t nm = swar_nondigit(x);
+    if (nm) {
+      const int k = __builtin_ctzll(nm) >> 3;
+      r.p += k;
+      if (r.p < r.end) term = (uint32_t)((x >> (8 * k)) & 0xff);
+      break;
+    }
     r.p += 8;
   }
-  if (r.p > r.end) r.p = r.end;                           // digits past the record's end are not its own
+  if (r.p > r.end) { r.p = r.end; term = 256u; }          // digits past the record's end are not its own
   return r.p > s;
+}
+__device__ __forceinline__ bool skip_digits(Reader& r) {
+  uint32_t first, term;
+  return skip_digits(r, first, term);
+}
+
+// skip_number with the first character known (the caller's) and the following one reported when a digit scan saw
+// it (`term`, 256 otherwise): a pruned number costs its digit words and no single-byte reads.
+__device__ __forceinline__ bool skip_number(Reader& r, uint32_t c, uint32_t& term) {
+  if (c == '-') ++r.p;
+  const int64_t s = r.p;
+  uint32_t first = 0;
+  if (!skip_digits(r, first, term)) return false;
+  if (first == '0' && r.p - s > 1) return false;           // leading zero
+  if (term == 256u) term = r.cur();
+  if (term == '.') {
+    ++r.p;
+    if (!skip_digits(r, first, term)) return false;
+    if (term == 256u) term = r.cur();
+  }
+  if ((term | 0x20u) == 'e') {
+    ++r.p;
+    term = r.cur();
+    if (term == '-' || term == '+') ++r.p;
+    if (!skip_digits(r, first, term)) return false;
+  }
+  return true;
 }
 
 // A JSON number's syntax (-? int frac? exp?) without its value: the skipping paths (pruned fields, unknown keys)
@@ -786,7 +849,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
   while (true) {
     r.top_up(kTopUp);                        // key + typical value of the next field, all low lanes at once
     nextc = 256u;
-    uint32_t c = r.ws_cur();
+    uint32_t c;
+    int node;
+    if (comma) {                             // the member after a separator: `"key":` of the expected key at once
+      const int ex = expect(depth - 1);
+      uint32_t nx = 256u;
+      if (ex >= 0 && quote_key_colon(r, r.p, r.end, tb.key_words + tb.key_word[ex], tb.key_len[ex], nx)) {
+        comma = false;
+        store_node = -1;
+        node = ex;
+        expect(depth - 1) = tb.next_sib[node];
+        c = (nx == 256u || nx == ' ' || nx == '\n' || nx == '\r' || nx == '\t') ? r.ws_cur() : nx;
+        goto have_value;
+      }
+    }
+    c = r.ws_cur();
     if (c == '}') {
       if (comma) break;       // trailing comma: {"a":1,}
       ++r.p;
@@ -798,8 +875,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
     store_node = -1;
     {
       // ---- key: speculate the expected key first, fall back to hashing the key text
+     {
       ++r.p;
-      int node = -1;
+      node = -1;
       const int ex = expect(depth - 1);
       int km = 0;
       uint32_t nx = 256u;
@@ -830,9 +908,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       if (r.ws_cur() != ':') break;
       ++r.p;
       c = r.ws_cur();
+     }
     have_value:
-      if (node < 0 || (tb.node_type[node] & 0xff) == FT_SKIP) goto skip_any;
+      if (node < 0) goto skip_any;
       const int t = tb.node_type[node] & 0xff;
+      if (t == FT_SKIP) {
+        // a pruned struct keeps its schema children (all FT_SKIP) in the plan: walk it like a struct, so key
+        // speculation keeps matching inside it, and store nothing; other pruned values go to the skipper
+        if (c == '{' && tb.first_child[node] >= 0 && depth < kMaxDepth) {
+          expect(depth) = tb.first_child[node];
+          stack(depth) = node;
+          ++depth;
+          ++r.p;
+          continue;
+        }
+        goto skip_any;
+      }
       const bool raw_arr = (tb.node_type[node] & 0x100) != 0;
       const int vs = tb.val_slot[node];
       const int ls = tb.len_slot[node];
@@ -925,7 +1016,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
     // the validating skipper keeps the loop's code and register footprint small
   skip_any: {
       const int64_t s0 = r.p;
-      if (!skip_value(r)) break;
+      if (c == '-' || is_digit(c)) {                       // scalars without the container state machine
+        if (!skip_number(r, c, nextc)) break;
+      } else if (c == '"') {
+        int64_t s, e;
+        bool esc;
+        if (!scan_string(r, s, e, esc, nextc)) break;
+      } else if (!skip_value(r)) {
+        break;
+      }
       if (store_node >= 0) {
         a.vals[(int64_t)tb.val_slot[store_node] * n + row] = s0;
         a.lens[(int64_t)tb.len_slot[store_node] * n + row] = (int32_t)(r.p - s0);

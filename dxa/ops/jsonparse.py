@@ -63,13 +63,21 @@ class Node:
     code: int
     val_slot: int = -1
     len_slot: int = -1
+    dropped: bool = False      # parsed (typed), but not part of the assembled struct: a column no statement reads
 
 
 class ParsePlan:
-    def __init__(self, schema: StructType, keep: Optional[Set[Tuple[str, ...]]] = None):
+    """The parser's node table for a schema.  ``keep`` (column pruning): the raw paths statements can read; the
+    other fields are either parsed as usual and dropped when the struct is assembled (the default — on MI355X the
+    typed scanners beat the skipper: the groupby flow's 23 unread leaves parse in 1.57 ms per 2 M events parsed,
+    1.81 ms skipped, and the headline runs 3 % faster, profiles/round5/parser/README.md), or, with
+    ``skip_unread``, matched by key and skipped unstored (FT_SKIP nodes)."""
+
+    def __init__(self, schema: StructType, keep: Optional[Set[Tuple[str, ...]]] = None, skip_unread: bool = False):
         self.schema = schema
         self.nodes: List[Node] = [Node((), -1, "", schema, 0)]
         self.keep = keep
+        self.skip_unread = skip_unread
         self._build(schema, 0, ())
         nv = nl = 0
         for nd in self.nodes[1:]:
@@ -121,20 +129,31 @@ class ParsePlan:
             return True
         return any(k[:len(path)] == path or path[:len(k)] == k for k in self.keep)
 
-    def _build(self, st: StructType, parent: int, prefix):
+    def _build(self, st: StructType, parent: int, prefix, dropped: bool = False):
         for f in st.fields:
             path = prefix + (f.name,)
-            if not self._wanted(path):
-                self.nodes.append(Node(path, parent, f.name, f.dtype, FT_SKIP))     # a whole subtree, unread
+            drop = dropped or not self._wanted(path)
+            if drop and self.skip_unread:
+                # unread; a pruned struct keeps its schema children as FT_SKIP nodes, so the kernel walks it with
+                # key speculation instead of the generic skipper (the CPU reference never visits them)
+                self.nodes.append(Node(path, parent, f.name, f.dtype, FT_SKIP))
+                if isinstance(f.dtype, StructType):
+                    self._build_skipped(f.dtype, len(self.nodes) - 1, path)
                 continue
             if isinstance(f.dtype, StructType):
-                self.nodes.append(Node(path, parent, f.name, f.dtype, 0))
-                self._build(f.dtype, len(self.nodes) - 1, path)
+                self.nodes.append(Node(path, parent, f.name, f.dtype, 0, dropped=drop))
+                self._build(f.dtype, len(self.nodes) - 1, path, drop)
             elif isinstance(f.dtype, (MapType, ArrayType)):
-                self.nodes.append(Node(path, parent, f.name, f.dtype, FT["raw"]))
+                self.nodes.append(Node(path, parent, f.name, f.dtype, FT["raw"], dropped=drop))
             else:
                 code = FT_DECIMAL if is_decimal(f.dtype) else FT.get(f.dtype, FT["string"])
-                self.nodes.append(Node(path, parent, f.name, f.dtype, code))
+                self.nodes.append(Node(path, parent, f.name, f.dtype, code, dropped=drop))
+
+    def _build_skipped(self, st: StructType, parent: int, prefix):
+        for f in st.fields:
+            self.nodes.append(Node(prefix + (f.name,), parent, f.name, f.dtype, FT_SKIP))
+            if isinstance(f.dtype, StructType):
+                self._build_skipped(f.dtype, len(self.nodes) - 1, prefix + (f.name,))
 
     def string_val_slots(self, device) -> Optional[torch.Tensor]:
         """Value-slot rows holding string starts (string and raw-JSON fields), as a device index tensor."""
@@ -331,7 +350,7 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
     cols: Dict[int, object] = {}
     for idx in range(len(plan.nodes) - 1, 0, -1):
         nd = plan.nodes[idx]
-        if nd.code == FT_SKIP:
+        if nd.code == FT_SKIP or nd.dropped:
             continue
         v = valid[idx] if (nulls is None or nulls[idx]) else None   # complete columns carry no mask
         if nd.code == 0:
@@ -470,7 +489,8 @@ def _parse_cpu(buf, offs, n, plan: ParsePlan, ends=None):
             ok.append(False)
 
     def build(idx, getters):
-        kids = [j for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == idx and plan.nodes[j].code != FT_SKIP]
+        kids = [j for j in range(1, len(plan.nodes))
+                if plan.nodes[j].parent == idx and plan.nodes[j].code != FT_SKIP and not plan.nodes[j].dropped]
         names, cols = [], []
         for j in kids:
             nd = plan.nodes[j]

@@ -6,6 +6,7 @@ import json
 import torch
 
 from dxa.models import iot
+from dxa.ops.jsonparse import FT_SKIP
 
 
 def _run(variant, prune, tmp_path):
@@ -38,7 +39,11 @@ def test_pruned_outputs_equal_unpruned(tmp_path):
         p1, a = _run(variant, True, tmp_path)
         p0, b = _run(variant, False, tmp_path)
         assert a == b, variant
-        assert p1.parse_plan.keep and p1.parse_plan.nval < p0.parse_plan.nval
+        # unread fields are parsed and dropped when the struct is assembled (the faster form on MI355X), so the
+        # pruned plan assembles fewer leaves than the unpruned one
+        def assembled(plan):
+            return sum(1 for nd in plan.nodes[1:] if nd.code != 0 and not nd.dropped and nd.code != FT_SKIP)
+        assert p1.parse_plan.keep and assembled(p1.parse_plan) < assembled(p0.parse_plan)
         leaves = {path[-1] for path in p1.parse_plan.keep}
         assert "deviceType" in leaves and "temperature" in leaves and "firmware" not in leaves
         if variant == "window":

@@ -18,7 +18,9 @@ def main():
     ap.add_argument("--events", type=int, default=2_000_000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pruned", action="store_true",
-                    help="keep only the groupby flow's fields (the rest parse as FT_SKIP nodes, as after pruning)")
+                    help="keep only the groupby flow's fields (the rest parsed and dropped at assembly, as after pruning)")
+    ap.add_argument("--skip-unread", action="store_true",
+                    help="with --pruned: the unread fields as FT_SKIP nodes (matched by key, skipped unstored)")
     a = ap.parse_args()
     from dxa.models import iot
     from dxa.ops import native
@@ -31,7 +33,7 @@ def main():
     if a.pruned:
         keep = {("deviceDetails", f) for f in ("deviceId", "deviceType", "homeId", "status", "eventTime")} | \
                {("telemetry", f) for f in ("temperature", "humidity", "power", "batteryLevel")}
-    plan = ParsePlan(iot.iot_spark_schema(), keep)
+    plan = ParsePlan(iot.iot_spark_schema(), keep, skip_unread=a.skip_unread)
     parse(buf, offs, plan)
     torch.cuda.synchronize()
     t = []
@@ -42,7 +44,7 @@ def main():
         torch.cuda.synchronize()
         t.append(time.perf_counter() - t0)
     total = int(offs[-1])
-    print(json.dumps({"events": a.events, "pruned": a.pruned, "bytes": total, "best_ms": round(min(t) * 1e3, 3),
+    print(json.dumps({"events": a.events, "pruned": a.pruned, "skip_unread": a.skip_unread, "bytes": total, "best_ms": round(min(t) * 1e3, 3),
                       "median_ms": round(sorted(t)[len(t) // 2] * 1e3, 3),
                       "gbps": round(total / min(t) / 1e9, 1)}))
 
