@@ -1617,6 +1617,9 @@ def _f_string_to_ts(e, scope, ctx, subst):
     if isinstance(a, ConstColumn):
         from ..ops.strings import py_string_to_timestamp_us
         return ConstColumn(py_string_to_timestamp_us(a.value), "timestamp", scope.length, scope.device)
+    pre = getattr(a, "_parsed_ts", None)          # converted by the JSON parser from the same bytes (ParsePlan)
+    if pre is not None and pre.length == a.length:
+        return pre
     from ..ops import strings as S
     r = S.to_timestamp(a)
     return r

@@ -139,7 +139,8 @@ class Processor:
         # column pruning (datax.job.process.columnpruning, default on): the parser extracts and windows retain only
         # the raw fields the live statements can read
         parse_prune = parse_prune and d.get_bool(S.PROCESS_PREFIX + "columnpruning", True)
-        self.parse_plan = ParsePlan(self.raw_schema, self._needed_raw_paths() if parse_prune else None)
+        self.parse_plan = ParsePlan(self.raw_schema, self._needed_raw_paths() if parse_prune else None,
+                                    ts_shadow=self._string_to_ts_paths())
         # input rebalance across ranks (reference: datax.job.input.default.eventhub.repartition → rdd.repartition)
         rp = d.get(S.INPUT_PREFIX + "eventhub.repartition") or d.get(S.INPUT_PREFIX + "repartition")
         self.repartition = bool(rp) and rp.strip().lower() not in ("0", "false", "")
@@ -186,6 +187,18 @@ class Processor:
                                  (sub.get("header") or "true").lower() == "true", self.device,
                                  schema=sub.get("schema"), stats=stats)
             self.reference_stats[name] = stats
+        return out
+
+    def _string_to_ts_paths(self) -> set:
+        """Raw string fields a projection line feeds to ``stringToTimestamp`` (the IoT flows' eventTime): the parser
+        converts them while their bytes are in cache, and ``stringToTimestamp`` takes that column (dxa_ts.h, the
+        same grammar as the string kernel)."""
+        import re
+        out = set()
+        for t in (l for p in self.projections for l in p):
+            for m in re.finditer(r"stringToTimestamp\s*\(\s*Raw((?:\s*\.\s*[A-Za-z_`][A-Za-z0-9_`]*)+)\s*\)", t,
+                                 flags=re.I):
+                out.add(tuple(p.strip().strip("`") for p in m.group(1).split(".") if p.strip()))
         return out
 
     def _needed_raw_paths(self):

@@ -16,6 +16,7 @@
 #include "dxa_common.h"
 #include <type_traits>
 #include "decimal_dd.h"
+#include "dxa_ts.h"
 
 namespace {
 
@@ -955,6 +956,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
           a.vals[(int64_t)vs * n + row] = s;
           a.lens[(int64_t)ls * n + row] = (int32_t)len;
           a.valid[(int64_t)node * n + row] = 1;
+          const int sh = tb.node_type[node] >> 16;      // timestamp shadow: stringToTimestamp of this field, here
+          if (sh) {                                       // while its bytes are in cache (no separate kernel)
+            int64_t us;
+            if (dxa::string_to_ts((const uint8_t*)(r.buf + s), (int32_t)len, us)) {
+              a.vals[(int64_t)tb.val_slot[sh] * n + row] = us;
+              a.valid[(int64_t)sh * n + row] = 1;
+            }
+          }
         } else if (t == FT_TIMESTAMP || t == FT_DATE) {
           int64_t us;
           if (parse_iso_ts(r, s, e, us, true)) {

@@ -64,6 +64,8 @@ class Node:
     val_slot: int = -1
     len_slot: int = -1
     dropped: bool = False      # parsed (typed), but not part of the assembled struct: a column no statement reads
+    shadow: int = 0            # string leaf: index of its timestamp-shadow node (stringToTimestamp parsed in place)
+    shadow_of: int = -1        # a timestamp-shadow node: the string leaf it belongs to (no key, no struct position)
 
 
 class ParsePlan:
@@ -73,12 +75,22 @@ class ParsePlan:
     1.81 ms skipped, and the headline runs 3 % faster, profiles/round5/parser/README.md), or, with
     ``skip_unread``, matched by key and skipped unstored (FT_SKIP nodes)."""
 
-    def __init__(self, schema: StructType, keep: Optional[Set[Tuple[str, ...]]] = None, skip_unread: bool = False):
+    def __init__(self, schema: StructType, keep: Optional[Set[Tuple[str, ...]]] = None, skip_unread: bool = False,
+                 ts_shadow: Optional[Set[Tuple[str, ...]]] = None):
         self.schema = schema
         self.nodes: List[Node] = [Node((), -1, "", schema, 0)]
         self.keep = keep
         self.skip_unread = skip_unread
         self._build(schema, 0, ())
+        # timestamp shadows: string leaves a projection feeds to stringToTimestamp get a timestamp value slot the
+        # kernel fills from the same bytes (dxa_ts.h); the column carries it as `_parsed_ts`
+        for path in sorted(ts_shadow or ()):
+            low = tuple(p.lower() for p in path)
+            for idx, nd in enumerate(self.nodes[1:], start=1):
+                if tuple(p.lower() for p in nd.path) == low and nd.code == FT["string"] and not nd.shadow:
+                    self.nodes.append(Node(nd.path + ("#ts",), -1, "", "timestamp", FT["timestamp"], shadow_of=idx))
+                    nd.shadow = len(self.nodes) - 1
+                    break
         nv = nl = 0
         for nd in self.nodes[1:]:
             if nd.code not in (0, FT_SKIP):
@@ -93,6 +105,8 @@ class ParsePlan:
         keys = [0] * cap
         node_of = [-1] * cap
         for idx, nd in enumerate(self.nodes[1:], start=1):
+            if nd.shadow_of >= 0:
+                continue
             k = _fmix64(_fnv1a(nd.name.encode("utf-8")) ^ (((nd.parent + 1) * GOLD) & M64))
             if k == 0:
                 k = 1
@@ -110,6 +124,8 @@ class ParsePlan:
         self.next_sib = [-1] * nn
         last = {}
         for idx, nd in enumerate(self.nodes[1:], start=1):
+            if nd.shadow_of >= 0:
+                continue
             if nd.parent in last:
                 self.next_sib[last[nd.parent]] = idx
             else:
@@ -171,7 +187,7 @@ class ParsePlan:
                  torch.tensor(self.lut_node, dtype=torch.int32, device=device),
                  # raw-JSON leaves: bit 8 marks an array type (the value must be '[…]'; maps take '{…}')
                  torch.tensor([n.code | (0x100 if n.code == FT["raw"] and isinstance(n.dtype, ArrayType) else 0)
-                               for n in self.nodes], dtype=torch.int32, device=device),
+                               | (n.shadow << 16) for n in self.nodes], dtype=torch.int32, device=device),
                  torch.tensor([n.val_slot for n in self.nodes], dtype=torch.int32, device=device),
                  torch.tensor([n.len_slot for n in self.nodes], dtype=torch.int32, device=device),
                  torch.tensor(self.first_child, dtype=torch.int32, device=device),
@@ -350,7 +366,7 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
     cols: Dict[int, object] = {}
     for idx in range(len(plan.nodes) - 1, 0, -1):
         nd = plan.nodes[idx]
-        if nd.code == FT_SKIP or nd.dropped:
+        if nd.code == FT_SKIP or nd.dropped or nd.shadow_of >= 0:
             continue
         v = valid[idx] if (nulls is None or nulls[idx]) else None   # complete columns carry no mask
         if nd.code == 0:
@@ -361,6 +377,10 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
         raw = vals[nd.val_slot]
         if nd.code == FT["string"]:
             cols[idx] = StrColumn(arena, raw, lens[nd.len_slot], v)
+            if nd.shadow:
+                sh = nd.shadow
+                cols[idx]._parsed_ts = PrimColumn("timestamp", vals[plan.nodes[sh].val_slot],
+                                                  valid[sh] if (nulls is None or nulls[sh]) else None)
         elif nd.code == FT["raw"]:
             cols[idx] = JsonColumn(arena, raw, lens[nd.len_slot], v, nd.dtype)
         elif nd.code == FT_DECIMAL:

@@ -549,3 +549,34 @@ def test_string_concat_and_compact_many_parts(gpu):
     many = S.compact_many(gpu_cols)
     assert [c.to_pylist() for c in many] == [c.to_pylist() for c in cpu_cols]
     assert nn == got.length
+
+
+@pytest.mark.gpu
+def test_parser_timestamp_shadow_matches_string_kernel(gpu):
+    """A string field a projection feeds to stringToTimestamp is converted by the parser from the same bytes
+    (ParsePlan ts_shadow, dxa_ts.h): the shadow column equals the string kernel's conversion of the parsed column
+    for every accepted form, escapes, nulls, type mismatches and rejects."""
+    from dxa.engine.types import StructField, StructType
+    from dxa.ops import strings as S
+    sch = StructType((StructField("a", StructType((StructField("t", "string"), StructField("k", "long")))),
+                      StructField("u", "string")))
+    forms = ["2023-11-14T22:13:20Z", "2023-11-14 22:13:20", "2023-11-14 22:13:20.123456", "2023-1-4 2:3:4",
+             "11/14/2023 22:13:20", "2023-11-14T22:13:20", "2023-13-14 22:13:20", "bad", "", "2023-11-14",
+             "2023-11-14T22:13:20Z ", "\\u0032023-11-14T22:13:20Z", "1999-12-31 23:59:59.9"]
+    recs = []
+    for i in range(3000):
+        f = forms[i % len(forms)]
+        t = "null" if i % 17 == 0 else (str(i) if i % 23 == 0 else f'"{f}"')
+        recs.append(('{"a":{"t":%s,"k":%d},"u":"x%d"}' % (t, i, i)).encode())
+    bg, og = frame_records(recs, device=gpu)
+    plan = ParsePlan(sch, ts_shadow={("a", "t")})
+    col, ok = parse(bg, og, plan)
+    t = col.child("a").child("t")
+    assert getattr(t, "_parsed_ts", None) is not None
+    want = S.to_timestamp(t)
+    got = t._parsed_ts
+    wv = want.valid_mask().cpu()
+    gv = got.valid_mask().cpu()
+    assert torch.equal(wv, gv)
+    assert torch.equal(want.data.cpu()[wv], got.data.cpu()[gv])
+    assert int(wv.sum()) > 1000
