@@ -222,7 +222,12 @@ def main():
     # (no gain measured, lower latency).  DXA_OUTPUT_DEPTH overrides.
     depth_extra = {"datax.job.process.outputdepth": "2"} if flow == "passthrough" else {}
     depth_extra["datax.job.process.columnpruning"] = "true" if args.column_pruning == "on" else "false"
-    settings = iot.flow_settings(workdir=f"/tmp/dxa_bench_{flow}_{rank}", variant=flow, sink=args.sink,
+    workdir = f"/tmp/dxa_bench_{flow}_{rank}"
+    # every run starts from an empty accumulator: a state table a previous run left in the workdir would otherwise
+    # be reloaded and change the first batches' work (and make back-to-back A/B runs order-dependent)
+    import shutil
+    shutil.rmtree(os.path.join(workdir, "state"), ignore_errors=True)
+    settings = iot.flow_settings(workdir=workdir, variant=flow, sink=args.sink,
                                  ref_rows=args.ref_rows, extra=depth_extra)
     ref_write_s = None
     if flow == "join":

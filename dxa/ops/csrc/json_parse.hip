@@ -51,6 +51,13 @@ struct ParseArgs {
   int32_t nkey_words;
   const int64_t* ends;          // [n] record ends when records are not back to back (Kafka values), else null;
                                 // offs[n] is then the end of the bytes
+  // outputs split in two: rows of the assembled columns (value slots < nkv, length slots < nkl, nodes < nkn) in
+  // vals / lens / valid, the parsed-but-dropped ones (column pruning) in vals2 / lens2 / valid2, so a retained
+  // column pins only its own batch's kept rows
+  int64_t* vals2;
+  int32_t* lens2;
+  uint8_t* valid2;
+  int32_t nkv, nkl, nkn;
 };
 
 // The same arguments as explicitly global (address space 1) pointers.  Pointers read out of a by-value struct
@@ -80,6 +87,20 @@ struct GArgs {
   const G1 uint64_t* key_words;
   int32_t nkey_words;
   const G1 int64_t* ends;
+  G1 int64_t* vals2;
+  G1 int32_t* lens2;
+  gu8* valid2;
+  int32_t nkv, nkl, nkn;
+  // row pointers of value slot v, length slot l, node k
+  __device__ __forceinline__ G1 int64_t* vrow(int v) const {
+    return v < nkv ? vals + (int64_t)v * n : vals2 + (int64_t)(v - nkv) * n;
+  }
+  __device__ __forceinline__ G1 int32_t* lrow(int l) const {
+    return l < nkl ? lens + (int64_t)l * n : lens2 + (int64_t)(l - nkl) * n;
+  }
+  __device__ __forceinline__ gu8* drow(int k) const {
+    return k < nkn ? valid + (int64_t)k * n : valid2 + (int64_t)(k - nkn) * n;
+  }
 };
 
 __device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
@@ -105,6 +126,12 @@ __device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
   g.key_words = (const G1 uint64_t*)p.key_words;
   g.nkey_words = p.nkey_words;
   g.ends = (const G1 int64_t*)p.ends;
+  g.vals2 = (G1 int64_t*)p.vals2;
+  g.lens2 = (G1 int32_t*)p.lens2;
+  g.valid2 = (gu8*)p.valid2;
+  g.nkv = p.nkv;
+  g.nkl = p.nkl;
+  g.nkn = p.nkn;
   return g;
 }
 
@@ -845,7 +872,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
   stack(0) = 0;  // root node
   expect(0) = tb.first_child[0];
   depth = 1;
-  a.valid[row] = 1;  // root struct present
+  a.drow(0)[row] = 1;  // root struct present
   uint32_t nextc;             // the character after a scanned value when its scanner saw it (256: read it)
   while (true) {
     r.top_up(kTopUp);                        // key + typical value of the next field, all low lanes at once
@@ -931,12 +958,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       if (node < 64) {                                    // a repeated key: its last occurrence decides (null on a
         const uint64_t bit = 1ull << node;                // mismatch), as a tokenizing parser's last write would
         const uint64_t seen = s_seen[threadIdx.x];
-        if (seen & bit) a.valid[(int64_t)node * n + row] = 0;
+        if (seen & bit) a.drow(node)[row] = 0;
         s_seen[threadIdx.x] = seen | bit;
       }
       if (c == '{' && t == FT_STRUCT) {
         if (depth >= kMaxDepth) goto skip_any;
-        a.valid[(int64_t)node * n + row] = 1;
+        a.drow(node)[row] = 1;
         expect(depth) = tb.first_child[node];
         stack(depth) = node;
         ++depth;
@@ -953,24 +980,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
         if (!scan_string(r, s, e, esc, nextc)) break;
         if (t == FT_STRING) {
           const int64_t len = esc ? unescape_inplace(r, s, e) : (e - s);
-          a.vals[(int64_t)vs * n + row] = s;
-          a.lens[(int64_t)ls * n + row] = (int32_t)len;
-          a.valid[(int64_t)node * n + row] = 1;
+          a.vrow(vs)[row] = s;
+          a.lrow(ls)[row] = (int32_t)len;
+          a.drow(node)[row] = 1;
           const int sh = tb.node_type[node] >> 16;      // timestamp shadow: stringToTimestamp of this field, here
           if (sh) {                                       // while its bytes are in cache (no separate kernel)
             int64_t us;
             if (dxa::string_to_ts((const uint8_t*)(r.buf + s), (int32_t)len, us)) {
-              a.vals[(int64_t)tb.val_slot[sh] * n + row] = us;
-              a.valid[(int64_t)sh * n + row] = 1;
+              a.vrow(tb.val_slot[sh])[row] = us;
+              a.drow(sh)[row] = 1;
             }
           }
         } else if (t == FT_TIMESTAMP || t == FT_DATE) {
           int64_t us;
           if (parse_iso_ts(r, s, e, us, true)) {
-            a.vals[(int64_t)vs * n + row] = (t == FT_DATE) ? (us >= 0 ? us / 86400000000ll
+            a.vrow(vs)[row] = (t == FT_DATE) ? (us >= 0 ? us / 86400000000ll
                                                                      : -((-us + 86399999999ll) / 86400000000ll))
                                                            : us;
-            a.valid[(int64_t)node * n + row] = 1;
+            a.drow(node)[row] = 1;
           }
         }
         goto after_value;
@@ -983,21 +1010,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
         if (!scan_number(r, c, is_int, of, iv, dv, nextc)) break;
         if (t == FT_LONG || t == FT_INT) {
           if (is_int && !of && (t == FT_LONG || (iv >= -2147483648ll && iv <= 2147483647ll))) {
-            a.vals[(int64_t)vs * n + row] = iv;
-            a.valid[(int64_t)node * n + row] = 1;
+            a.vrow(vs)[row] = iv;
+            a.drow(node)[row] = 1;
           }
         } else if (t == FT_DOUBLE) {
-          a.vals[(int64_t)vs * n + row] = __double_as_longlong(dv);
-          a.valid[(int64_t)node * n + row] = 1;
+          a.vrow(vs)[row] = __double_as_longlong(dv);
+          a.drow(node)[row] = 1;
         } else if (t == FT_TIMESTAMP) {
           if (is_int && !of) {
-            a.vals[(int64_t)vs * n + row] = iv * 1000000ll;
-            a.valid[(int64_t)node * n + row] = 1;
+            a.vrow(vs)[row] = iv * 1000000ll;
+            a.drow(node)[row] = 1;
           }
         } else if (t == FT_STRING || t == FT_DECIMAL) {
-          a.vals[(int64_t)vs * n + row] = s;
-          a.lens[(int64_t)ls * n + row] = (int32_t)(r.p - s);
-          a.valid[(int64_t)node * n + row] = 1;
+          a.vrow(vs)[row] = s;
+          a.lrow(ls)[row] = (int32_t)(r.p - s);
+          a.drow(node)[row] = 1;
         }
         goto after_value;
       }
@@ -1006,12 +1033,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
         const bool v = (c == 't');
         if (!take_literal(r, c)) break;
         if (t == FT_BOOL) {
-          a.vals[(int64_t)vs * n + row] = v ? 1 : 0;
-          a.valid[(int64_t)node * n + row] = 1;
+          a.vrow(vs)[row] = v ? 1 : 0;
+          a.drow(node)[row] = 1;
         } else if (t == FT_STRING) {
-          a.vals[(int64_t)vs * n + row] = s;
-          a.lens[(int64_t)ls * n + row] = v ? 4 : 5;
-          a.valid[(int64_t)node * n + row] = 1;
+          a.vrow(vs)[row] = s;
+          a.lrow(ls)[row] = v ? 4 : 5;
+          a.drow(node)[row] = 1;
         }
         goto after_value;
       }
@@ -1035,9 +1062,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
         break;
       }
       if (store_node >= 0) {
-        a.vals[(int64_t)tb.val_slot[store_node] * n + row] = s0;
-        a.lens[(int64_t)tb.len_slot[store_node] * n + row] = (int32_t)(r.p - s0);
-        a.valid[(int64_t)store_node * n + row] = 1;
+        a.vrow(tb.val_slot[store_node])[row] = s0;
+        a.lrow(tb.len_slot[store_node])[row] = (int32_t)(r.p - s0);
+        a.drow(store_node)[row] = 1;
       }
     }
   after_value:
@@ -1053,7 +1080,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
 done:
   a.row_ok[row] = ok ? 1 : 0;
   if (!ok) {
-    for (int k = 0; k < a.nnodes; ++k) a.valid[(int64_t)k * n + row] = 0;
+    for (int k = 0; k < a.nnodes; ++k) a.drow(k)[row] = 0;
   }
 #undef stack
 #undef expect
@@ -1164,14 +1191,21 @@ DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const u
                            const int32_t* val_slot, const int32_t* len_slot, int32_t nnodes, int64_t* vals,
                            int32_t* lens, uint8_t* valid, uint8_t* row_ok, const int32_t* first_child,
                            const int32_t* next_sib, const int32_t* key_word, const int32_t* key_len,
-                           const uint64_t* key_words, int32_t nkey_words, const int64_t* ends, void* stream) {
+                           const uint64_t* key_words, int32_t nkey_words, const int64_t* ends, int64_t* vals2,
+                           int32_t* lens2, uint8_t* valid2, int32_t nkv, int32_t nkl, int32_t nkn, void* stream) {
   if (n <= 0) return 0;
   if (nnodes >= 32767) return (int)hipErrorInvalidValue;   // node ids live in 16-bit LDS nesting slots
+  if (nkn < 1 || nkn > nnodes) return (int)hipErrorInvalidValue;
   ParseArgs a{buf, offs, n, lut_keys, lut_node, lut_cap, node_type, val_slot, len_slot, nnodes, vals, lens,
-              valid, row_ok, first_child, next_sib, key_word, key_len, key_words, nkey_words, ends};
+              valid, row_ok, first_child, next_sib, key_word, key_len, key_words, nkey_words, ends, vals2, lens2,
+              valid2, nkv, nkl, nkn};
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(valid, 0, (size_t)nnodes * (size_t)n, s);
+  hipError_t e = hipMemsetAsync(valid, 0, (size_t)nkn * (size_t)n, s);
   if (e != hipSuccess) return (int)e;
+  if (nnodes > nkn) {
+    e = hipMemsetAsync(valid2, 0, (size_t)(nnodes - nkn) * (size_t)n, s);
+    if (e != hipSuccess) return (int)e;
+  }
   const int block = 256;
   const int64_t grid = (n + block - 1) / block;
   const int64_t tab_bytes = tables_lds_bytes(nnodes, nkey_words, lut_cap);

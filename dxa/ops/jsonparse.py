@@ -66,6 +66,7 @@ class Node:
     dropped: bool = False      # parsed (typed), but not part of the assembled struct: a column no statement reads
     shadow: int = 0            # string leaf: index of its timestamp-shadow node (stringToTimestamp parsed in place)
     shadow_of: int = -1        # a timestamp-shadow node: the string leaf it belongs to (no key, no struct position)
+    order: int = 0             # position in the schema walk (sibling order for key speculation)
 
 
 class ParsePlan:
@@ -91,6 +92,7 @@ class ParsePlan:
                     self.nodes.append(Node(nd.path + ("#ts",), -1, "", "timestamp", FT["timestamp"], shadow_of=idx))
                     nd.shadow = len(self.nodes) - 1
                     break
+        self._kept_first()
         nv = nl = 0
         for nd in self.nodes[1:]:
             if nd.code not in (0, FT_SKIP):
@@ -100,6 +102,10 @@ class ParsePlan:
                     nd.len_slot = nl
                     nl += 1
         self.nval, self.nlen = nv, nl
+        # output rows of the assembled columns come first (value / length slots, nodes): the kernel writes them to
+        # one set of buffers and the dropped fields' rows to another, so kept columns pin only kept rows
+        self.nkv = sum(1 for nd in self.nodes[:self.nkn] if nd.val_slot >= 0)
+        self.nkl = sum(1 for nd in self.nodes[:self.nkn] if nd.len_slot >= 0)
         self.max_depth = max((len(nd.path) for nd in self.nodes if nd.code == 0), default=0)
         cap = 1 << max(4, math.ceil(math.log2(max(2, 2 * len(self.nodes)))))
         keys = [0] * cap
@@ -123,7 +129,8 @@ class ParsePlan:
         self.first_child = [-1] * nn
         self.next_sib = [-1] * nn
         last = {}
-        for idx, nd in enumerate(self.nodes[1:], start=1):
+        for idx in sorted(range(1, nn), key=lambda i: self.nodes[i].order):       # schema order
+            nd = self.nodes[idx]
             if nd.shadow_of >= 0:
                 continue
             if nd.parent in last:
@@ -139,6 +146,27 @@ class ParsePlan:
             words += [int.from_bytes(b[i:i + 8], "little") for i in range(0, len(b), 8)]
         self.key_words = [_to_i64(w) for w in words] or [0]
         self._dev: Dict[str, Tuple[torch.Tensor, ...]] = {}
+
+    def _kept_first(self):
+        """Renumber the nodes: the root, then every assembled node (kept fields, their structs, timestamp shadows),
+        then the parsed-but-dropped and FT_SKIP ones — each group in schema order.  ``order`` keeps the schema walk
+        for the sibling chains."""
+        for i, nd in enumerate(self.nodes):
+            nd.order = i
+        kept = lambda nd: not nd.dropped and nd.code != FT_SKIP           # noqa: E731
+        new = [0] + [i for i in range(1, len(self.nodes)) if kept(self.nodes[i])] + \
+            [i for i in range(1, len(self.nodes)) if not kept(self.nodes[i])]
+        remap = {old: k for k, old in enumerate(new)}
+        nodes = [self.nodes[i] for i in new]
+        for nd in nodes:
+            if nd.parent >= 0:
+                nd.parent = remap[nd.parent]
+            if nd.shadow:
+                nd.shadow = remap[nd.shadow]
+            if nd.shadow_of >= 0:
+                nd.shadow_of = remap[nd.shadow_of]
+        self.nodes = nodes
+        self.nkn = 1 + sum(1 for nd in nodes[1:] if kept(nd))
 
     def _wanted(self, path) -> bool:
         if self.keep is None:
@@ -175,7 +203,7 @@ class ParsePlan:
         """Value-slot rows holding string starts (string and raw-JSON fields), as a device index tensor."""
         key = ("sslots", str(device))
         if key not in self._dev:
-            sl = sorted({nd.val_slot for nd in self.nodes[1:] if nd.code in (4, 5, FT_DECIMAL)})
+            sl = sorted({nd.val_slot for nd in self.nodes[1:self.nkn] if nd.code in (4, 5, FT_DECIMAL)})
             self._dev[key] = torch.tensor(sl, dtype=torch.int64, device=device) if sl else None
         return self._dev[key]
 
@@ -333,11 +361,17 @@ def _parse_gpu(buf, offs, n, plan: ParsePlan, ends=None):
 def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
     lut_k, lut_n, types, vslot, lslot, fchild, nsib, kword, klen, kwords = plan.device_tables(buf.device)
     nn = len(plan.nodes)
-    vals = torch.empty((max(1, plan.nval), max(n, 1)), dtype=torch.int64, device=buf.device)
+    m = max(n, 1)
+    vals = torch.empty((max(1, plan.nkv), m), dtype=torch.int64, device=buf.device)
     # string lengths start at 0: the kernel writes only present fields, and a null string must still be a valid
     # (empty) view for the kernels that copy / hash / split every row of a column without looking at validity
-    lens = torch.zeros((max(1, plan.nlen), max(n, 1)), dtype=torch.int32, device=buf.device)
-    valid = torch.empty((nn, max(n, 1)), dtype=torch.uint8, device=buf.device)
+    lens = torch.zeros((max(1, plan.nkl), m), dtype=torch.int32, device=buf.device)
+    valid = torch.empty((plan.nkn, m), dtype=torch.uint8, device=buf.device)
+    # rows of parsed-but-dropped fields (column pruning): written by the kernel, never assembled, freed with this
+    # frame (their block goes back to this stream's pool behind the kernel)
+    vals2 = torch.empty((max(1, plan.nval - plan.nkv), m), dtype=torch.int64, device=buf.device)
+    lens2 = torch.empty((max(1, plan.nlen - plan.nkl), m), dtype=torch.int32, device=buf.device)
+    valid2 = torch.empty((max(1, nn - plan.nkn), m), dtype=torch.uint8, device=buf.device)
     row_ok = torch.empty(max(n, 1), dtype=torch.uint8, device=buf.device)
     sslots = plan.string_val_slots(buf.device)
     if sslots is not None:
@@ -348,10 +382,12 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
         N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
                N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
                N.ptr(fchild), N.ptr(nsib), N.ptr(kword), N.ptr(klen), N.ptr(kwords), int(kwords.numel()),
-               None if ends is None else N.ptr(ends), st)
-        cnt = torch.empty(nn, dtype=torch.int64, device=buf.device)
-        N.call("dxa_null_counts", N.ptr(valid), n, nn, N.ptr(cnt), st)
-        counts = torch.empty(nn, dtype=torch.int64, pin_memory=True)
+               None if ends is None else N.ptr(ends), N.ptr(vals2), N.ptr(lens2), N.ptr(valid2), plan.nkv,
+               plan.nkl, plan.nkn, st)
+        nk = plan.nkn
+        cnt = torch.empty(nk, dtype=torch.int64, device=buf.device)
+        N.call("dxa_null_counts", N.ptr(valid), n, nk, N.ptr(cnt), st)      # the assembled nodes only
+        counts = torch.empty(nk, dtype=torch.int64, pin_memory=True)
         counts.copy_(cnt, non_blocking=True)     # a few bytes behind the kernels; read in result()
         event = torch.cuda.Event()
         event.record(torch.cuda.current_stream(buf.device))
