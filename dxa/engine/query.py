@@ -939,27 +939,33 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
         cached = (sig, proto.take(torch.empty(0, dtype=torch.int64, device=proto.device)))
         t.store._empty_proto = cached
     empty = cached[1]
-    items = _expand_items(sel, Scope.of_table(empty, alias))
-    aggs: Dict = {}
-    for e, _ in items:
-        _collect_aggs(e, ctx, aggs)
-    if sel.having is not None:
-        _collect_aggs(sel.having, ctx, aggs)
-    if not aggs and not sel.group_by:
+    # the statement's paned plan (select items, aggregates, cacheability, fingerprint) depends only on the
+    # statement, the window's schema and the session's functions: derived once, not re-walked every batch
+    plans = t.store.__dict__.setdefault("_paned_plans", {})
+    pkey = (id(sel), alias, sig, id(ctx.udfs), id(ctx.udafs) if hasattr(ctx, "udafs") else None)
+    plan_ent = plans.get(pkey)
+    if plan_ent is None or plan_ent[0] is not sel:
+        items = _expand_items(sel, Scope.of_table(empty, alias))
+        aggs: Dict = {}
+        for e, _ in items:
+            _collect_aggs(e, ctx, aggs)
+        if sel.having is not None:
+            _collect_aggs(sel.having, ctx, aggs)
+        ok = bool(aggs or sel.group_by) and not any(W.window_calls(e) for e, _ in items) and \
+            D.decomposable(aggs, ctx)
+        exprs = [e for e, _ in items] + list(sel.group_by) + ([sel.where] if sel.where is not None else []) + (
+            [sel.having] if sel.having is not None else [])
+        cacheable = True
+        for e in exprs:
+            for node in A.walk(e):
+                if isinstance(node, A.Call) and (node.name in NONDETERMINISTIC or (
+                        node.name in ctx.udfs and not getattr(ctx.udfs[node.name], "deterministic", False))):
+                    cacheable = False
+        fp = repr((alias, [e.key() for e in exprs], sel.where is not None, [nm for _, nm in items]))
+        plan_ent = plans[pkey] = (sel, ok, items, aggs, cacheable, fp)
+    _, ok, items, aggs, cacheable, fp = plan_ent
+    if not ok:
         return None
-    if any(W.window_calls(e) for e, _ in items):
-        return None
-    if not D.decomposable(aggs, ctx):
-        return None
-    exprs = [e for e, _ in items] + list(sel.group_by) + ([sel.where] if sel.where is not None else []) + (
-        [sel.having] if sel.having is not None else [])
-    cacheable = True
-    for e in exprs:
-        for node in A.walk(e):
-            if isinstance(node, A.Call) and (node.name in NONDETERMINISTIC or (
-                    node.name in ctx.udfs and not getattr(ctx.udfs[node.name], "deterministic", False))):
-                cacheable = False
-    fp = repr((alias, [e.key() for e in exprs], sel.where is not None, [nm for _, nm in items]))
     state = {}
 
     def pane_partial(pane, full):
