@@ -51,6 +51,12 @@ __device__ __forceinline__ uint64_t rnd(uint64_t seed, int64_t row, int k) {
   return dxa::fmix64(seed ^ dxa::fmix64((uint64_t)row * dxa::kGold + (uint64_t)k * 0x632BE59BD9B4E019ull));
 }
 
+// A value in [0, span) from 64 random bits: multiply-shift of the top 32 bits for spans below 2^32 (no 64-bit
+// software division per field; datagen.py _pick is the host twin), the remainder above.
+__device__ __forceinline__ uint64_t pick(uint64_t r, uint64_t span) {
+  return span <= 0xffffffffull ? ((r >> 32) * span) >> 32 : r % span;
+}
+
 __device__ __forceinline__ void civil(int64_t days, int64_t& y, int& m, int& d) {
   days += 719468;
   const int64_t era = (days >= 0 ? days : days - 146096) / 146097;
@@ -93,7 +99,7 @@ __device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int
         break;
       case OP_INT: {
         const uint64_t span = (uint64_t)(op.y - op.x);
-        const int64_t v = op.x + (int64_t)(span ? rnd(g.seed, row, k) % span : 0);
+        const int64_t v = op.x + (int64_t)(span ? pick(rnd(g.seed, row, k), span) : 0);
         e.put_i64(v);
         break;
       }
@@ -130,7 +136,7 @@ __device__ __forceinline__ int64_t render(const GenArgs& g, const Tables& t, int
         break;
       }
       case OP_CHOICE: {
-        const int idx = (int)(rnd(g.seed, row, k) % (uint64_t)op.b);
+        const int idx = (int)pick(rnd(g.seed, row, k), (uint64_t)op.b);
         const int off = t.table[2 * (op.a + idx)], len = t.table[2 * (op.a + idx) + 1];
         e.put_text_words(pool64 + (off >> 3), len);
         break;

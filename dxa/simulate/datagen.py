@@ -348,6 +348,11 @@ def generate_slotted(prog: GenProgram, n: int, device, seed: int = 1, row0: int 
 
 
 M64 = (1 << 64) - 1
+
+
+def _pick(r: int, span: int) -> int:
+    """A value in [0, span) from 64 random bits (datagen.hip pick): multiply-shift of the top 32 bits below 2^32."""
+    return ((r >> 32) * span) >> 32 if span <= 0xFFFFFFFF else r % span
 GOLD = 0x9E3779B97F4A7C15
 
 
@@ -382,7 +387,7 @@ def render_cpu(prog: GenProgram, row: int, seed: int, base_ms: int, step_us: int
             out += pool[a:a + b]
         elif code == OP_INT:
             span = (y - x) & M64
-            out += str(x + (_rnd(seed, row, k) % span if span else 0)).encode()
+            out += str(x + (_pick(_rnd(seed, row, k), span) if span else 0)).encode()
         elif code == OP_DBL:
             lo, hi = struct.unpack("<d", struct.pack("<q", x))[0], struct.unpack("<d", struct.pack("<q", y))[0]
             u = (_rnd(seed, row, k) >> 11) * (1.0 / 9007199254740992.0)
@@ -396,7 +401,7 @@ def render_cpu(prog: GenProgram, row: int, seed: int, base_ms: int, step_us: int
                 s += "." + str(af % scale).rjust(a, "0")
             out += s.encode()
         elif code == OP_CHOICE:
-            idx = _rnd(seed, row, k) % b
+            idx = _pick(_rnd(seed, row, k), b)
             off, ln = prog.table[a + idx]
             out += pool[off:off + ln]
         elif code == OP_TS_MS:
