@@ -58,6 +58,10 @@ struct ParseArgs {
   int32_t* lens2;
   uint8_t* valid2;
   int32_t nkv, nkl, nkn;
+  // (value slot, length slot) of every assembled string-like field: zeroed per row first, so a missing or null
+  // string is an empty view at offset 0, never a stale address (the buffers are not pre-filled)
+  const int32_t* zslots;
+  int32_t nz;
 };
 
 // The same arguments as explicitly global (address space 1) pointers.  Pointers read out of a by-value struct
@@ -91,6 +95,8 @@ struct GArgs {
   G1 int32_t* lens2;
   gu8* valid2;
   int32_t nkv, nkl, nkn;
+  const G1 int32_t* zslots;
+  int32_t nz;
   // row pointers of value slot v, length slot l, node k
   __device__ __forceinline__ G1 int64_t* vrow(int v) const {
     return v < nkv ? vals + (int64_t)v * n : vals2 + (int64_t)(v - nkv) * n;
@@ -132,6 +138,8 @@ __device__ __forceinline__ GArgs to_global(const ParseArgs& p) {
   g.nkv = p.nkv;
   g.nkl = p.nkl;
   g.nkn = p.nkn;
+  g.zslots = (const G1 int32_t*)p.zslots;
+  g.nz = p.nz;
   return g;
 }
 
@@ -841,6 +849,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
   const Tables<LDS> tb = load_tables<LDS>(a);                   // (LDS: whole workgroup, before any early exit)
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= a.n) return;
+  for (int j = 0; j < a.nz; ++j) {
+    a.vrow(a.zslots[2 * j])[row] = 0;
+    a.lrow(a.zslots[2 * j + 1])[row] = 0;
+  }
   const int64_t n = a.n;
   Reader r;
   r.buf = a.buf;
@@ -1192,13 +1204,14 @@ DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const u
                            int32_t* lens, uint8_t* valid, uint8_t* row_ok, const int32_t* first_child,
                            const int32_t* next_sib, const int32_t* key_word, const int32_t* key_len,
                            const uint64_t* key_words, int32_t nkey_words, const int64_t* ends, int64_t* vals2,
-                           int32_t* lens2, uint8_t* valid2, int32_t nkv, int32_t nkl, int32_t nkn, void* stream) {
+                           int32_t* lens2, uint8_t* valid2, int32_t nkv, int32_t nkl, int32_t nkn,
+                           const int32_t* zslots, int32_t nz, void* stream) {
   if (n <= 0) return 0;
   if (nnodes >= 32767) return (int)hipErrorInvalidValue;   // node ids live in 16-bit LDS nesting slots
   if (nkn < 1 || nkn > nnodes) return (int)hipErrorInvalidValue;
   ParseArgs a{buf, offs, n, lut_keys, lut_node, lut_cap, node_type, val_slot, len_slot, nnodes, vals, lens,
               valid, row_ok, first_child, next_sib, key_word, key_len, key_words, nkey_words, ends, vals2, lens2,
-              valid2, nkv, nkl, nkn};
+              valid2, nkv, nkl, nkn, zslots, nz};
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(valid, 0, (size_t)nkn * (size_t)n, s);
   if (e != hipSuccess) return (int)e;

@@ -199,12 +199,14 @@ class ParsePlan:
             if isinstance(f.dtype, StructType):
                 self._build_skipped(f.dtype, len(self.nodes) - 1, prefix + (f.name,))
 
-    def string_val_slots(self, device) -> Optional[torch.Tensor]:
-        """Value-slot rows holding string starts (string and raw-JSON fields), as a device index tensor."""
-        key = ("sslots", str(device))
+    def string_slot_pairs(self, device) -> Optional[torch.Tensor]:
+        """(value slot, length slot) of every assembled string-like field (string, raw JSON, decimal text), as a
+        device int32 tensor: the kernel zeroes them per row before parsing it."""
+        key = ("zslots", str(device))
         if key not in self._dev:
-            sl = sorted({nd.val_slot for nd in self.nodes[1:self.nkn] if nd.code in (4, 5, FT_DECIMAL)})
-            self._dev[key] = torch.tensor(sl, dtype=torch.int64, device=device) if sl else None
+            pairs = [(nd.val_slot, nd.len_slot) for nd in self.nodes[1:self.nkn] if nd.code in (4, 5, FT_DECIMAL)]
+            self._dev[key] = torch.tensor([v for p in pairs for v in p], dtype=torch.int32, device=device) \
+                if pairs else None
         return self._dev[key]
 
     def device_tables(self, device):
@@ -363,9 +365,9 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
     nn = len(plan.nodes)
     m = max(n, 1)
     vals = torch.empty((max(1, plan.nkv), m), dtype=torch.int64, device=buf.device)
-    # string lengths start at 0: the kernel writes only present fields, and a null string must still be a valid
-    # (empty) view for the kernels that copy / hash / split every row of a column without looking at validity
-    lens = torch.zeros((max(1, plan.nkl), m), dtype=torch.int32, device=buf.device)
+    # a null string must still be a valid (empty) view for the kernels that copy / hash / split every row of a
+    # column without looking at validity: the kernel zeroes every assembled string's start and length per row
+    lens = torch.empty((max(1, plan.nkl), m), dtype=torch.int32, device=buf.device)
     valid = torch.empty((plan.nkn, m), dtype=torch.uint8, device=buf.device)
     # rows of parsed-but-dropped fields (column pruning): written by the kernel, never assembled, freed with this
     # frame (their block goes back to this stream's pool behind the kernel)
@@ -373,9 +375,7 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
     lens2 = torch.empty((max(1, plan.nlen - plan.nkl), m), dtype=torch.int32, device=buf.device)
     valid2 = torch.empty((max(1, nn - plan.nkn), m), dtype=torch.uint8, device=buf.device)
     row_ok = torch.empty(max(n, 1), dtype=torch.uint8, device=buf.device)
-    sslots = plan.string_val_slots(buf.device)
-    if sslots is not None:
-        vals.index_fill_(0, sslots, 0)            # null strings: start 0 (with length 0), never a wild address
+    zs = plan.string_slot_pairs(buf.device)
     counts = event = None
     if n:
         st = N.stream_handle(buf.device)
@@ -383,7 +383,7 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
                N.ptr(vslot), N.ptr(lslot), nn, N.ptr(vals), N.ptr(lens), N.ptr(valid), N.ptr(row_ok),
                N.ptr(fchild), N.ptr(nsib), N.ptr(kword), N.ptr(klen), N.ptr(kwords), int(kwords.numel()),
                None if ends is None else N.ptr(ends), N.ptr(vals2), N.ptr(lens2), N.ptr(valid2), plan.nkv,
-               plan.nkl, plan.nkn, st)
+               plan.nkl, plan.nkn, N.ptr(zs), 0 if zs is None else zs.numel() // 2, st)
         nk = plan.nkn
         cnt = torch.empty(nk, dtype=torch.int64, device=buf.device)
         N.call("dxa_null_counts", N.ptr(valid), n, nk, N.ptr(cnt), st)      # the assembled nodes only

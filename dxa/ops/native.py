@@ -45,7 +45,8 @@ _SIGS = {
     "dxa_java_double_dev": [c_p, c_i64, c_p, c_p, c_p],
     "dxa_java_double_hostcheck": [c_p, c_i64, c_p, c_p],
     "dxa_json_parse": [c_p, c_p, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p,
-                       c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_p],
+                       c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_p, c_i32,
+                       c_p],
     "dxa_count_newlines": [c_p, c_i64, c_i64, c_p, c_p, c_p],
     "dxa_write_newlines_bits": [c_p, c_i64, c_i64, c_p, c_p, c_i64, c_i64, c_p],
     "dxa_null_counts": [c_p, c_i64, c_i32, c_p, c_p],
