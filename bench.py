@@ -153,6 +153,9 @@ def main():
     ap.add_argument("--crc", choices=["host", "device", "off"], default="host",
                     help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): host planner "
                          "threads (default), the GPU (kafka_crc_kernel), or not at all")
+    ap.add_argument("--workdir", default=None,
+                    help="keep the run's files (state table, sink output) here, rank r in <dir>_<r>, cleared of state "
+                         "at start; default: a fresh temporary directory per rank, removed at the end")
     ap.add_argument("--column-pruning", choices=["on", "off"], default="on",
                     help="datax.job.process.columnpruning: parse and retain only the raw fields statements read")
     ap.add_argument("--sink", choices=["null", "blob"], default="null",
@@ -222,11 +225,16 @@ def main():
     # (no gain measured, lower latency).  DXA_OUTPUT_DEPTH overrides.
     depth_extra = {"datax.job.process.outputdepth": "2"} if flow == "passthrough" else {}
     depth_extra["datax.job.process.columnpruning"] = "true" if args.column_pruning == "on" else "false"
-    workdir = f"/tmp/dxa_bench_{flow}_{rank}"
-    # every run starts from an empty accumulator: a state table a previous run left in the workdir would otherwise
-    # be reloaded and change the first batches' work (and make back-to-back A/B runs order-dependent)
+    # a fresh work directory per run and rank: every run starts from an empty accumulator (a state table left by an
+    # earlier run would be reloaded and change the first batches' work, making back-to-back A/B runs
+    # order-dependent), and concurrent runs never share state or output files
     import shutil
-    shutil.rmtree(os.path.join(workdir, "state"), ignore_errors=True)
+    import tempfile
+    if args.workdir:
+        workdir = f"{args.workdir}_{rank}"
+        shutil.rmtree(os.path.join(workdir, "state"), ignore_errors=True)
+    else:
+        workdir = tempfile.mkdtemp(prefix=f"dxa_bench_{flow}_r{rank}_", dir="/tmp")
     settings = iot.flow_settings(workdir=workdir, variant=flow, sink=args.sink,
                                  ref_rows=args.ref_rows, extra=depth_extra)
     ref_write_s = None
@@ -657,6 +665,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if not args.workdir:
+        shutil.rmtree(workdir, ignore_errors=True)
 
 
 if __name__ == "__main__":
