@@ -580,3 +580,40 @@ def test_parser_timestamp_shadow_matches_string_kernel(gpu):
     assert torch.equal(wv, gv)
     assert torch.equal(want.data.cpu()[wv], got.data.cpu()[gv])
     assert int(wv.sum()) > 1000
+
+
+@pytest.mark.gpu
+def test_parser_null_strings_are_empty_views(gpu):
+    """The parse kernel zeroes every assembled string's (start, length) per row itself (no fill kernels): a
+    missing, null, mistyped or malformed-row string is an empty view at offset 0, also for decimal text and raw
+    JSON fields, with kept and dropped (column-pruned) fields mixed in the plan."""
+    from dxa.engine.decimal import parse_decimal_type
+    from dxa.engine.types import StructField, StructType
+    sch = StructType((StructField("a", StructType((StructField("s", "string"),
+                                                   StructField("d", parse_decimal_type("decimal(10,2)")),
+                                                   StructField("k", "long")))),
+                      StructField("u", "string"), StructField("v", "string")))
+    recs = []
+    for i in range(4000):
+        parts = []
+        if i % 3:
+            parts.append('"a":{"s":%s,"d":%s,"k":%d}' % ("null" if i % 7 == 0 else f'"s{i}"',
+                                                           "1.25" if i % 5 else "null", i))
+        if i % 4:
+            parts.append('"u":%s' % ("7" if i % 11 == 0 else f'"u{i}"'))
+        parts.append('"v":"w%d"' % i)
+        recs.append(("{" + ",".join(parts) + "}" if i % 97 else "{bad").encode())
+    bg, og = frame_records(recs, device=gpu)
+    for keep in (None, {("a", "s"), ("a", "d"), ("u",)}):
+        plan = ParsePlan(sch, keep)
+        junk = torch.full((1 << 22,), -1, dtype=torch.int64, device=gpu)   # the allocator hands this back dirty
+        del junk
+        col, ok = parse(bg, og, plan)
+        for path in (("a", "s"), ("u",)):
+            c = col
+            for p in path:
+                c = c.child(p)
+            null = ~c.valid_mask().cpu()
+            assert int(null.sum()) > 100
+            assert int(c.lens.cpu()[null].abs().sum()) == 0
+            assert int(c.starts.cpu()[null].abs().sum()) == 0
