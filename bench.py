@@ -373,7 +373,11 @@ def main():
             return
         if source == "gpu-sim":
             def gen_args(j):
-                return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=batch_time(j) // 1000 - 1000,
+                # event time of row r is base_ms + r * step_us / 1000 and batch j's rows are r = j*E .. j*E + E-1, so
+                # a constant base puts batch j's events in the second before its batch time [bt_j - 1 s, bt_j) (a
+                # base that advanced with j as well would run event time at twice the batch clock, and a 5-min
+                # window would then hold ~120 of the retained panes instead of 300)
+                return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=clock0_us // 1000 - 1000,
                             step_us=max(1, interval_us // E))
             if side is None:
                 staged[i] = generate(prog, E, device, **gen_args(i)) + (None,)
@@ -431,6 +435,7 @@ def main():
         if t_arr is not None:
             lat_batch.append(proc.last_done_perf - t_arr)
     host_trace = [] if os.environ.get("DXA_BENCH_HOST_TRACE") else None
+    host_sections_trace = []     # DXA_BENCH_HOST_TRACE: per step, the host sections' ms (DXA_HOST_TIMERS=1 for more)
     proc.on_batch_complete = on_complete
 
     ready = {}
@@ -484,6 +489,13 @@ def main():
             ready[i + 1] = proc.prepare(take(i + 1))
         if host_trace is not None:
             host_trace.append((i, round((t_p - t_s) * 1e3, 2), round((time.perf_counter() - t_p) * 1e3, 2)))
+            acc = dict(getattr(proc, "host_acc", {}))
+            from dxa.telemetry import tracing as _trs
+            acc.update(_trs.HOST_ACC)
+            prev = host_sections_trace[-1][1] if host_sections_trace else {}
+            host_sections_trace.append((i, {k: v for k, v in acc.items()}))
+            host_sections_trace[-1] = (i, acc, {k: round((v - prev.get(k, 0.0)) * 1e3, 3) for k, v in acc.items()
+                                                if v - prev.get(k, 0.0) > 5e-5})
         sizes.append(kafka_json[i % len(pool)] + 16 if source == "kafka" else rb.buf.shape[0])
         return m
 
@@ -627,6 +639,7 @@ def main():
             out["config"]["zstd_level"] = args.zstd_level
     if host_trace is not None:
         out["host_trace_ms"] = host_trace[-8:]           # (batch, stage() host ms, process_batch() host ms)
+        out["host_sections_trace_ms"] = [(i, d) for i, _, d in host_sections_trace[-4:]]
         out["latency_trace_ms"] = [round(x * 1e3, 2) for x in lat]
     if last:
         out["last_batch_outputs"] = {k: v for k, v in last.items() if k.startswith("Output_")}
