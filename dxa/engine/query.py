@@ -1000,25 +1000,32 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     by_block: Dict[int, list] = {}
     sec = host_section("paned:partials")
     sec.__enter__()
+    # parts are ordered by event time (a block by its first slot): the merge input does not depend on the order
+    # the views list their panes in, and from one batch to the next the list keeps one long common run (the newest
+    # pane joins at the end, the oldest leave at the front) for _concat_panes to reuse
+    keyed = []
     try:
+        use_blocks = cacheable and store.interval_us
         for pane, full in t.pieces():
-            if full and cacheable and store.interval_us:
+            if full and use_blocks:
                 by_block.setdefault(pane.key // span, []).append(pane)
             else:
-                parts.append(pane_partial(pane, full))
+                keyed.append((pane.key, pane_partial(pane, full)))
         for bid, panes in by_block.items():
             if len(panes) == BLOCK:
                 members = tuple(sorted(p.key for p in panes))
                 ent = store.blocks.get((fp, bid))
                 if ent is None or ent[0] != members:
-                    ps = [pane_partial(p, True) for p in panes]
+                    ps = [pane_partial(p, True) for p in sorted(panes, key=lambda p: p.key)]
                     pl, kn, _ = state["meta"]
                     ent = (members, D.combine_partials(concat_tables(ps), pl, kn, bool(sel.group_by)), state["meta"])
                     store.blocks[(fp, bid)] = ent
                 state.setdefault("meta", ent[2])
-                parts.append(ent[1])
+                keyed.append((bid * span, ent[1]))
             else:
-                parts.extend(pane_partial(p, True) for p in panes)
+                keyed.extend((p.key, pane_partial(p, True)) for p in panes)
+        keyed.sort(key=lambda kv: kv[0])
+        parts = [tb for _, tb in keyed]
         if "meta" not in state:
             # nothing of this rank's window is in range: still produce (empty) partials, so every rank runs the
             # same exchange — the choice of plan must not depend on a rank's data
