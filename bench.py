@@ -113,6 +113,16 @@ def launch_ranks(n):
     return rc
 
 
+def sim_gen_args(j: int, rank: int, E: int, clock0_us: int, interval_us: int) -> dict:
+    """Generator arguments of batch ``j`` for the ``gpu-sim`` source.  The event time of row r is
+    base_ms + r * step_us / 1000 and batch j renders rows j*E .. j*E + E-1, so a constant base puts batch j's events
+    in the interval before its batch time, [clock0 + j*interval - interval, clock0 + j*interval).  (A base that
+    advanced with j as well ran event time at twice the batch clock: a 5-min window then held ~120 of its 300
+    panes, profiles/round5/evtime/.)"""
+    return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=(clock0_us - interval_us) // 1000,
+                step_us=max(1, interval_us // E))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -373,12 +383,7 @@ def main():
             return
         if source == "gpu-sim":
             def gen_args(j):
-                # event time of row r is base_ms + r * step_us / 1000 and batch j's rows are r = j*E .. j*E + E-1, so
-                # a constant base puts batch j's events in the second before its batch time [bt_j - 1 s, bt_j) (a
-                # base that advanced with j as well would run event time at twice the batch clock, and a 5-min
-                # window would then hold ~120 of the retained panes instead of 300)
-                return dict(seed=7919 * rank + j + 1, row0=j * E, base_ms=clock0_us // 1000 - 1000,
-                            step_us=max(1, interval_us // E))
+                return sim_gen_args(j, rank, E, clock0_us, interval_us)
             if side is None:
                 staged[i] = generate(prog, E, device, **gen_args(i)) + (None,)
                 return
