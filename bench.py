@@ -334,6 +334,28 @@ def main():
         torch.cuda.synchronize(device)
     gen_s = time.perf_counter() - t_gen
 
+    # this box's own pinned H2D bandwidth, measured once before the timed region on a copy of the size one step
+    # ingests (best of 3): the record then says whether a step was bound by the link or by the code
+    # (pcie_fraction = ingest bytes per step / (h2d_gb_s * step time))
+    h2d_gb_s = None
+    if on_gpu and comp_bytes:
+        kmax = max(range(len(comp_bytes)), key=comp_bytes.__getitem__)
+        nb = comp_bytes[kmax]
+        hsrc = pool[kmax] if isinstance(pool[kmax], torch.Tensor) else torch.empty(nb, dtype=torch.uint8,
+                                                                                   pin_memory=True)
+        hsrc = hsrc[:nb]
+        ddst = torch.empty(nb, dtype=torch.uint8, device=device)
+        best = None
+        for _ in range(3):
+            torch.cuda.synchronize(device)
+            t_c = time.perf_counter()
+            ddst.copy_(hsrc, non_blocking=True)
+            torch.cuda.synchronize(device)
+            dt = time.perf_counter() - t_c
+            best = dt if best is None else min(best, dt)
+        h2d_gb_s = nb / best / 1e9
+        del ddst
+
     side = torch.cuda.Stream(device) if (on_gpu and source in ("pinned", "pinned-lz4", "kafka", "gpu-sim")) else None
     ingest = lz4.ChunkedIngest(device, chunks=args.lz4_chunks, copy_stream=side) \
         if (on_gpu and source == "pinned-lz4") else None
@@ -633,6 +655,11 @@ def main():
                                                    2)
         out["config"]["lz4_level"] = args.lz4_level
         out["config"]["lz4_block_bytes"] = lz4_block_k
+        if h2d_gb_s:
+            step_bytes = sum(comp_bytes) / len(comp_bytes)
+            out["h2d_gb_s"] = round(h2d_gb_s, 2)
+            out["ingest_mb_per_step"] = round(step_bytes / 1e6, 1)
+            out["pcie_fraction"] = round(step_bytes / (h2d_gb_s * 1e9 * elapsed / args.steps), 3)
     if source == "kafka":
         out["config"]["kafka_partitions"] = args.kafka_partitions
         out["config"]["kafka_batch_records"] = args.kafka_batch_records

@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 _PLAN_ERRS = {-2: "message format is not v2", -3: "CRC mismatch", -5: "codec decoded on the host only",
-              -7: "malformed LZ4 frame", -8: "dependent-block LZ4 frame", -9: "offset deltas with gaps"}
+              -7: "malformed compressed payload (LZ4 / snappy / zstd)", -8: "dependent-block LZ4 frame", -9: "offset deltas with gaps"}
 
 
 TORCH_DT = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64, np.dtype(np.uint8): torch.uint8}

@@ -24,6 +24,10 @@
 
 namespace {
 
+// largest decoded record-batch payload the host walker allocates (a batch's declared sizes are untrusted: a corrupt
+// header must return an error code, never throw bad_alloc through the C entry points)
+constexpr int64_t kMaxDecoded = (int64_t)1 << 31;
+
 uint32_t g_crc_table[8][256];
 
 // table for the portable path, built once (thread-safe static init)
@@ -145,6 +149,7 @@ bool lz4_unframe(const uint8_t* src, size_t n, std::string& out) {
                                             &frame_end);
   if (nb == -1) return false;
   const int64_t cap = content >= 0 ? content : (nb > 0 ? nb : 1) * (int64_t)max_block;
+  if (cap > kMaxDecoded || (content >= 0 && content > (nb > 0 ? nb : 1) * (int64_t)max_block)) return false;
   out.resize((size_t)cap);
   const int64_t m = dxa::lz4::decompress_frame(src, (int64_t)n, (uint8_t*)&out[0], cap);
   if (m < 0) return false;
@@ -249,7 +254,7 @@ int walk_batches(const uint8_t* data, int64_t len, int64_t min_offset, int64_t m
       } else if (codec == 2) {
         // snappy: snappy-java's xerial stream (Java producers) or one raw block (librdkafka)
         const int64_t m = dxa::snappy::payload_length(recs, bend - recs);
-        if (m < 0) return -6;
+        if (m < 0 || m > kMaxDecoded) return -6;
         std::string raw((size_t)m, '\0');
         if (dxa::snappy::decompress_payload(recs, bend - recs, (uint8_t*)&raw[0], m) != m) return -6;
         rc = walk_records((const uint8_t*)raw.data(), (const uint8_t*)raw.data() + raw.size(), count, base,
@@ -257,7 +262,7 @@ int walk_batches(const uint8_t* data, int64_t len, int64_t min_offset, int64_t m
       } else if (codec == 4) {
         // zstd: one frame (zstd-jni's ZstdOutputStream; no content size, so decode into a bound-sized buffer)
         const int64_t bound = dxa::zstd::decompressed_bound(recs, bend - recs);
-        if (bound < 0) return -6;
+        if (bound < 0 || bound > kMaxDecoded) return -6;
         std::string raw((size_t)bound, '\0');
         const int64_t m = dxa::zstd::decompress(recs, bend - recs, (uint8_t*)&raw[0], bound);
         if (m < 0) return -6;
@@ -281,7 +286,7 @@ int walk_batches(const uint8_t* data, int64_t len, int64_t min_offset, int64_t m
 // output slot: the frame's maximum block size for LZ4 blocks (every block of a frame but the last is full, so a
 // frame's bytes are contiguous from its first slot), its own length for stored data, the gzip trailer's ISIZE for
 // a gzip member (kind 2: inflated by inflate.hip).  Returns 0, or
-// -2 bad magic, -3 CRC, -5 codec the GPU path does not take (snappy / zstd, odd gzip headers), -7 malformed LZ4 frame,
+// -2 bad magic, -3 CRC, -5 codec the GPU path does not take (snappy / zstd, odd gzip headers), -7 malformed LZ4 / snappy / zstd payload,
 // -8 dependent-block frame, -9 offset deltas that are not 0..count-1 (compacted batch) — the caller decodes such
 // fetches on the host.
 struct Plan {
@@ -430,7 +435,10 @@ int plan_batches(const uint8_t* data, int64_t len, int64_t min_offset, Plan& pl,
         const uint8_t* f = recs;
         while (f < bend) {
           dxa::zstd::FrameInfo fi;
-          if (dxa::zstd::frame_info(f, bend - f, &fi) != 0) return -5;
+          const int fr = dxa::zstd::frame_info(f, bend - f, &fi);
+          if (fr == -2) return -5;                     // dictionary frames: host decoder only
+          if (fr != 0) return -7;                      // malformed (incl. a content size beyond its blocks)
+          if (fi.bound > INT32_MAX) return -7;         // a slot's capacity is an int32 (k_cap, max_block)
           if (pl.write) {
             pl.k_comp_off[pl.nblk] = f - data;
             pl.k_comp_len[pl.nblk] = (int32_t)fi.end;

@@ -118,6 +118,11 @@ int64_t raw_length(const uint8_t* src, int64_t n, int32_t* hdr) {
     v |= (uint64_t)(src[k] & 127) << shift;
     if (!(src[k] & 128)) {
       if (hdr) *hdr = (int32_t)(k + 1);
+      // the declared length is untrusted: no element expands more than a 3-byte copy of 64 bytes does, so a block of
+      // c element bytes decodes to at most c*64/3 (+ one copy's slack); a larger claim is corrupt and must not size
+      // an allocation
+      const uint64_t body = (uint64_t)(n - (k + 1));
+      if (v > body * 64 / 3 + 64) return -1;
       return v > 0x7fffffffull ? -1 : (int64_t)v;
     }
     shift += 7;

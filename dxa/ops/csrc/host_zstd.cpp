@@ -521,7 +521,7 @@ int frame_info(const uint8_t* src, int64_t n, FrameInfo* fi) {
     if (type == 3) return -1;
     p += 3;
     const int64_t body = type == 1 ? 1 : size;
-    if (p + body > n) return -1;
+    if (size > bmax || p + body > n) return -1;            // RFC 8878 3.1.1.2.3: no block exceeds Block_Maximum_Size
     p += body;
     bound += type == 2 ? bmax : size;
     ++nb;
@@ -531,6 +531,9 @@ int frame_info(const uint8_t* src, int64_t n, FrameInfo* fi) {
   if (p > n) return -1;
   fi->end = p;
   fi->nblocks = nb;
+  // the header's content size is untrusted: a frame can never decode to more than its blocks' maxima, so a larger
+  // claim is a corrupt frame (and must not size an allocation)
+  if (fi->content_size > bound) return -1;
   fi->bound = fi->content_size >= 0 ? fi->content_size : bound;
   return 0;
 }

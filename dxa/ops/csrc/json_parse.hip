@@ -970,7 +970,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void j
       if (node < 64) {                                    // a repeated key: its last occurrence decides (null on a
         const uint64_t bit = 1ull << node;                // mismatch), as a tokenizing parser's last write would
         const uint64_t seen = s_seen[threadIdx.x];
-        if (seen & bit) a.drow(node)[row] = 0;
+        if (seen & bit) {
+          a.drow(node)[row] = 0;
+          const int sh = tb.node_type[node] >> 16;        // its timestamp shadow follows the last occurrence too
+          if (sh) a.drow(sh)[row] = 0;
+        }
         s_seen[threadIdx.x] = seen | bit;
       }
       if (c == '{' && t == FT_STRUCT) {

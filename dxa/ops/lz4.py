@@ -81,14 +81,19 @@ def compress_frame(data, block_size: int = DEFAULT_BLOCK, threads: Optional[int]
 
 def decompress_frame(data, size_hint: Optional[int] = None) -> bytes:
     a = _as_np(data)
-    t = frame_table(a)
-    cap = t.content_size if t.content_size >= 0 else (size_hint or max(1, a.size) * 8)
+    try:
+        content = frame_table(a).content_size
+    except Lz4Error as e:
+        if "dependent" not in str(e):
+            raise
+        content = -1          # linked blocks (liblz4's default above one block): host decode, size unknown up front
+    cap = content if content >= 0 else (size_hint or max(1, a.size) * 8)
     while True:
         out = np.empty(max(cap, 1), dtype=np.uint8)
         m = _host().dxa_lz4_decompress_frame(a.ctypes.data, a.size, out.ctypes.data, cap)
         if m >= 0:
             return out[:m].tobytes()
-        if t.content_size >= 0 or cap > (1 << 34):
+        if content >= 0 or cap > (1 << 34):
             raise Lz4Error(f"lz4 frame decode failed ({m})")
         cap *= 4
 

@@ -137,8 +137,56 @@ static void snappy_zstd_checks(uint32_t seed) {
   }
 }
 
+// A CRC-valid v2 batch around a records payload whose declared decoded size is absurd: a zstd frame header claiming
+// 2^62 bytes of content, a snappy varint claiming 2^31-1 bytes for 4 literal bytes.  The walker must return an error
+// code (no bad_alloc / length_error escaping the C entry point, no huge allocation).
+static void put_be(std::vector<uint8_t>& b, uint64_t v, int n) {
+  for (int k = n - 1; k >= 0; --k) b.push_back((uint8_t)(v >> (8 * k)));
+}
+static std::vector<uint8_t> raw_batch(const std::vector<uint8_t>& payload, int codec) {
+  std::vector<uint8_t> tail;
+  put_be(tail, (uint64_t)codec, 2);        // attributes
+  put_be(tail, 0, 4);                      // last offset delta (one record)
+  put_be(tail, 1234, 8);
+  put_be(tail, 1234, 8);
+  put_be(tail, ~0ull, 8);                  // producer id -1
+  put_be(tail, 0xffff, 2);
+  put_be(tail, 0xffffffffu, 4);
+  put_be(tail, 1, 4);                      // record count
+  tail.insert(tail.end(), payload.begin(), payload.end());
+  std::vector<uint8_t> b;
+  put_be(b, 0, 8);
+  put_be(b, (uint64_t)(4 + 1 + 4 + tail.size()), 4);
+  put_be(b, 0, 4);                         // partition leader epoch
+  b.push_back(2);                          // magic
+  put_be(b, dxa_crc32c(tail.data(), (int64_t)tail.size()), 4);
+  b.insert(b.end(), tail.begin(), tail.end());
+  return b;
+}
+static void oversized_declared_sizes() {
+  // zstd: single-segment frame, 8-byte content size 2^62, one raw block "abcd"
+  std::vector<uint8_t> z = {0x28, 0xB5, 0x2F, 0xFD, 0xE0};
+  for (int k = 0; k < 8; ++k) z.push_back((uint8_t)(((uint64_t)1 << 62) >> (8 * k)));
+  const uint32_t bh = 1 | (0 << 1) | (4 << 3);
+  z.push_back((uint8_t)bh); z.push_back((uint8_t)(bh >> 8)); z.push_back((uint8_t)(bh >> 16));
+  for (char c : std::string("abcd")) z.push_back((uint8_t)c);
+  std::vector<uint8_t> out(64);
+  CHECK(dxa_zstd_decompress(z.data(), (int64_t)z.size(), out.data(), (int64_t)out.size()) < 0);
+  // snappy: varint 2^31-1, then a 4-byte literal
+  std::vector<uint8_t> s = {0xFF, 0xFF, 0xFF, 0xFF, 0x07, 3 << 2, 'a', 'b', 'c', 'd'};
+  CHECK(dxa_snappy_decompress(s.data(), (int64_t)s.size(), out.data(), (int64_t)out.size()) < 0);
+  for (const auto& pc : {std::make_pair(z, 4), std::make_pair(s, 2)}) {
+    const std::vector<uint8_t> b = raw_batch(pc.first, pc.second);
+    int64_t n = 0, nb = 0, nxt = 0;
+    const int rc = dxa_kafka_count(b.data(), (int64_t)b.size(), 0, &n, &nb, &nxt, 1);
+    CHECK(rc == -6);
+    if (rc != -6) std::fprintf(stderr, "oversized codec %d rc %d\n", pc.second, rc);
+  }
+}
+
 int main() {
   snappy_zstd_checks(5u);
+  oversized_declared_sizes();
   CHECK(dxa_crc32c((const uint8_t*)"123456789", 9) == 0xE3069283u);
   CHECK(dxa_crc32c((const uint8_t*)"", 0) == 0u);
   for (int codec : {0, 1, 2, 3, 4})

@@ -568,6 +568,10 @@ def test_parser_timestamp_shadow_matches_string_kernel(gpu):
         f = forms[i % len(forms)]
         t = "null" if i % 17 == 0 else (str(i) if i % 23 == 0 else f'"{f}"')
         recs.append(('{"a":{"t":%s,"k":%d},"u":"x%d"}' % (t, i, i)).encode())
+    # a repeated key: the last occurrence decides the string and its shadow alike (a junk, null, numeric or valid
+    # second value after a valid first one)
+    for i, second in enumerate(['"junk"', "null", "17", '"2020-02-02 02:02:02"', '{"x":1}'] * 40):
+        recs.append(('{"a":{"t":"2023-11-14T22:13:20Z","k":%d,"t":%s},"u":"d"}' % (i, second)).encode())
     bg, og = frame_records(recs, device=gpu)
     plan = ParsePlan(sch, ts_shadow={("a", "t")})
     col, ok = parse(bg, og, plan)

@@ -4,8 +4,9 @@ from the snappy format description and RFC 8878) and the GPU decoders (snappy.hi
 The reference's Kafka source uses kafka-clients 2.4.1 (DataProcessing/datax-host/pom.xml:164-167), which decodes
 both codecs (KafkaStreamingFactory.scala:70-74).  Oracles: the system libzstd compresses the frames a zstd-jni
 producer would write (no content size, no checksum) and our decoders must return the input; frames and blocks
-hand-assembled here from the format descriptions check the decoders independently of any encoder; the GPU decode
-is compared with the host decode of the same fetch."""
+hand-assembled here from the format descriptions check the decoders independently of any encoder; pyarrow's
+bundled snappy / zstd / lz4 codecs (independent implementations) are a second oracle on the host and the GPU; the GPU
+decode is compared with the host decode of the same fetch."""
 import json
 import random
 
@@ -210,6 +211,76 @@ def test_big_batches_make_multi_block_frames_and_chunks():
     assert [buf[x:y].tobytes() for x, y in zip(s, e)] == vals + vals
 
 
+# ---- independent oracle: pyarrow's bundled codecs -------------------------------------------------------------
+
+pa = pytest.importorskip("pyarrow")
+
+
+def _pa_compress(codec, data, level=None):
+    c = pa.Codec(codec, compression_level=level) if level is not None else pa.Codec(codec)
+    return c.compress(data).to_pybytes()
+
+
+@pytest.mark.parametrize("level", [1, 3, 6, 9, 12, 19])
+def test_zstd_host_decoder_matches_pyarrow(level):
+    """pyarrow's zstd frames (content size in the header, single segment) decode with host_zstd.cpp; frames from
+    our producer path decode with pyarrow."""
+    for data in _samples():
+        assert K.zstd_decompress(_pa_compress("zstd", data, level)) == data, (level, len(data))
+    try:
+        ours = K.zstd_compress(_samples()[4], level)
+    except K.KafkaError:
+        return
+    assert pa.Codec("zstd").decompress(ours, decompressed_size=len(_samples()[4])).to_pybytes() == _samples()[4]
+
+
+def test_snappy_host_decoder_matches_pyarrow():
+    """Raw snappy blocks from pyarrow decode with host_snappy.cpp, and ours decode with pyarrow."""
+    for data in _samples():
+        assert K.snappy_decompress(_pa_compress("snappy", data)) == data, len(data)
+        ours = K.snappy_compress(data, False)
+        assert pa.Codec("snappy").decompress(ours, decompressed_size=len(data)).to_pybytes() == data
+
+
+def test_lz4_frames_match_pyarrow():
+    """LZ4 frames (the Kafka codec-3 payload) from pyarrow decode with host_lz4.cpp; ours decode with pyarrow."""
+    from dxa.ops import lz4
+    for data in _samples()[1:]:
+        assert lz4.decompress_frame(_pa_compress("lz4", data)) == data, len(data)
+        ours = lz4.compress_frame(np.frombuffer(data, np.uint8), 65536).tobytes()
+        assert pa.Codec("lz4").decompress(ours, decompressed_size=len(data)).to_pybytes() == data
+
+
+def _raw_batch(payload, count, codec, ts=1_700_000_000_000):
+    """A v2 record batch around an already-compressed records payload, with a valid CRC-32C."""
+    import struct
+    tail = struct.pack(">hiqqqhii", codec, count - 1, ts, ts, -1, -1, -1, count) + payload
+    crc = K.crc32c(tail)
+    body = struct.pack(">ibI", 0, 2, crc) + tail
+    return struct.pack(">qi", 0, len(body)) + body
+
+
+def test_corrupt_declared_sizes_are_errors_not_allocations():
+    """A zstd frame header claiming more content than its blocks can hold, and a snappy varint claiming more than its
+    elements can expand to, are reported as malformed (never sized into an allocation), in the codec entry points and
+    in a CRC-valid Kafka batch walked by the planner / host decoder."""
+    frame = bytearray(_pa_compress("zstd", b"hello world " * 40, 3))
+    assert frame[4] & 0xC0 == 0x40                         # 2-byte FCS (+256)
+    frame[4] = (frame[4] & 0x3F) | 0xC0                   # 8-byte FCS, claims ~2^62 bytes
+    huge = bytes(frame[:5]) + (1 << 62).to_bytes(8, "little") + bytes(frame[7:])
+    with pytest.raises(K.KafkaError):
+        K.zstd_decompress(huge)
+    blk = bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x07]) + bytes([3 << 2]) + b"abcd"   # varint 2^31-1 for 4 literal bytes
+    with pytest.raises(K.KafkaError):
+        K.snappy_decompress(blk)
+    for codec, payload in (("zstd", huge), ("snappy", blk)):
+        rs = _raw_batch(payload, 1, K.CODECS[codec])
+        with pytest.raises(K.KafkaError):
+            K.decode_records(rs, 0, pad=0)
+        with pytest.raises(KD.Unsupported, match="malformed"):   # the device planner refuses it too
+            KD.plan_fetch(rs, 0)
+
+
 # ---- GPU decoders ---------------------------------------------------------------------------------------------
 
 def _device_decode(gpu, rs, plan, chunks=2):
@@ -299,3 +370,39 @@ def test_device_decodes_hand_assembled_frames(gpu):
     assert status.tolist() == [0, 0] and produced.tolist() == [len(content), len(want_snappy)]
     o = out.cpu().numpy().tobytes()
     assert o[:len(content)] == content and o[64:64 + len(want_snappy)] == want_snappy
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level", [1, 3, 9, 19])
+def test_device_decodes_pyarrow_frames(gpu, level):
+    """zstd frames and snappy raw blocks written by pyarrow's codecs (independent of this package's encoders) through
+    the device kernels, one table entry per frame / block."""
+    from dxa.ops import native as N
+    datas = _samples()[1:] + [b"\n".join(_values(26, seed=s)) for s in range(20)]
+    for codec, kind, entry in (("zstd", 4, "dxa_zstd_decode_into"), ("snappy", 3, "dxa_snappy_decode_into")):
+        comp = [_pa_compress(codec, d, level if codec == "zstd" else None) for d in datas]
+        co, pos = [], 0
+        for c in comp:
+            co.append(pos)
+            pos += len(c)
+        src = torch.zeros(pos + 64, dtype=torch.uint8)
+        src[:pos] = torch.frombuffer(bytearray(b"".join(comp)), dtype=torch.uint8)
+        oo, opos = [], 0
+        for d in datas:
+            oo.append(opos)
+            opos += (len(d) + 63) // 64 * 64
+        dev = lambda xs, dt: torch.tensor(xs, dtype=dt, device=gpu)                  # noqa: E731
+        n = len(datas)
+        out = torch.zeros(opos + 64, dtype=torch.uint8, device=gpu)
+        produced = torch.zeros(n, dtype=torch.int64, device=gpu)
+        status = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+        N.call(entry, N.ptr(src.to(gpu)), N.ptr(dev(co, torch.int64)), N.ptr(dev([len(c) for c in comp], torch.int32)),
+               N.ptr(dev([kind] * n, torch.uint8)), N.ptr(dev(oo, torch.int64)),
+               N.ptr(dev([len(d) for d in datas], torch.int64)), n, N.ptr(out), N.ptr(produced), N.ptr(status),
+               N.stream_handle(gpu))
+        torch.cuda.synchronize(gpu)
+        assert status.tolist() == [0] * n, (codec, status.tolist())
+        assert produced.tolist() == [len(d) for d in datas]
+        o = out.cpu().numpy().tobytes()
+        for d, off in zip(datas, oo):
+            assert o[off:off + len(d)] == d, (codec, len(d))
