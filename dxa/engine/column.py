@@ -32,7 +32,8 @@ from .types import (ArrayType, MapType, StructField, StructType, is_integral, is
 EPOCH = _dt.datetime(1970, 1, 1)
 
 TORCH_DTYPE = {
-    "boolean": torch.bool, "int": torch.int64, "long": torch.int64, "float": torch.float64,
+    "boolean": torch.bool, "byte": torch.int64, "short": torch.int64, "int": torch.int64, "long": torch.int64,
+    "float": torch.float64,
     "double": torch.float64, "decimal": torch.float64, "timestamp": torch.int64, "date": torch.int64,
     "null": torch.bool,
 }
@@ -490,7 +491,7 @@ def _py_to_storage(v, dtype):
         return int(v)
     if dtype == "boolean":
         return bool(v)
-    if dtype in ("int", "long"):
+    if dtype in ("byte", "short", "int", "long"):
         return int(v)
     return float(v)
 

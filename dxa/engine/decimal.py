@@ -86,7 +86,8 @@ def bounded(p: int, s: int) -> DecimalType:
 
 
 def of_integral(t: str) -> DecimalType:
-    return DecimalType(10, 0) if t == "int" else DecimalType(20, 0)
+    """Spark DecimalType.forType: tinyint → decimal(3,0), smallint → (5,0), int → (10,0), bigint → (20,0)."""
+    return DecimalType({"byte": 3, "short": 5, "int": 10}.get(t, 20), 0)
 
 
 def result_add(a: DecimalType, b: DecimalType) -> DecimalType:
@@ -740,10 +741,9 @@ def scalar_to(v, t: DecimalType, to: str):
     """A decimal value → another type (Spark Decimal.toLong/toInt truncate toward zero; toDouble rounds)."""
     if v is None:
         return None
-    if to in ("int", "long"):
-        r = int(v)                                   # truncates toward zero
-        r = ((r + 2**63) % 2**64) - 2**63
-        return ((r + 2**31) % 2**32) - 2**31 if to == "int" else r
+    if to in ("byte", "short", "int", "long"):
+        from .types import wrap_int_value
+        return wrap_int_value(int(v), to)            # truncates toward zero, then the low bits (Decimal.toLong)
     if to in ("double", "float"):
         return float(v)
     if to == "boolean":
@@ -785,9 +785,31 @@ def to_integral(col, to: str):
         k -= step
     nh, nl = neg128(ah, al)
     r = torch.where(neg, nl, al)
-    if to == "int":
-        r = ((r + 2**31) % 2**32) - 2**31
-    return PrimColumn(to, r, col.valid)
+    from .types import wrap_int_tensor
+    return PrimColumn(to, wrap_int_tensor(r, to), col.valid)
+
+
+def ceil_floor_column(col, up: bool):
+    """ceil / floor of decimal(p, s): Spark 2.4's Ceil / Floor keep a decimal, decimal(p - s + 1, 0) (bounded),
+    exact: the value truncated toward zero, plus one unit away from zero when dropped digits were nonzero and the
+    direction (up for ceil on positives, down for floor on negatives) leaves zero behind."""
+    from .column import PrimColumn
+    t: DecimalType = col.dtype
+    rt = bounded(t.precision - t.scale + 1, 0)
+    h, l = lanes(col.data)
+    ah, al, neg = abs128(h, l)
+    sticky = torch.zeros_like(neg)
+    k = t.scale
+    while k > 0:
+        step = min(k, 9)
+        ah, al, r = divmod_small_u(ah, al, 10 ** step)
+        sticky |= r != 0
+        k -= step
+    bump = sticky & (~neg if up else neg)
+    ah, al = add128(ah, al, torch.zeros_like(ah), bump.to(torch.int64))
+    nh, nl = neg128(ah, al)
+    h, l = torch.where(neg, nh, ah), torch.where(neg, nl, al)
+    return PrimColumn(rt, pack(h, l, rt), col.valid)
 
 
 def to_boolean(col):

@@ -24,7 +24,8 @@ from . import jit as _jit_mod
 from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, LazyColumns, PrimColumn, StrColumn,
                      StructColumn, TORCH_DTYPE, and_valid, column_from_pylist, concat_columns, materialize, strings_from_pylist,
                      take_columns)
-from .types import (ArrayType, MapType, StructType, common_type, is_integral, is_nested, is_numeric)
+from .types import (INT_RANGE, INTEGRAL, ArrayType, MapType, StructType, common_type, is_integral, is_nested,
+                    is_numeric, wrap_int_tensor, wrap_int_value)
 from . import decimal as D
 from .decimal import is_decimal
 
@@ -330,7 +331,7 @@ def _coerce_const_for(col_other: Column, const: ConstColumn) -> ConstColumn:
 _DECIMAL_AWARE = frozenset({"round", "bround", "hash", "typeof",
                             "coalesce", "if", "nvl", "ifnull", "nullif", "nvl2", "to_json", "named_struct", "struct",
                             "array", "map", "concat", "concat_ws", "isnull", "isnotnull", "string", "abs",
-                            "negative", "positive"})
+                            "negative", "positive", "ceil", "ceiling", "floor"})
 
 _DEMOTE: "contextvars.ContextVar" = contextvars.ContextVar("dxa_decimal_demote", default=None)
 
@@ -379,9 +380,14 @@ def _evaluate_node(e: A.Expr, scope: Scope, ctx: EvalContext, subst: Optional[Di
             return bool_col(~(v.data.bool()), v.valid)
         if e.op == "-":
             if isinstance(v, ConstColumn):
-                return ConstColumn(None if v.value is None else -v.value, v.dtype, n, dev)
+                if v.value is None:
+                    return ConstColumn(None, v.dtype, n, dev)
+                return ConstColumn(wrap_int_value(-v.value, v.dtype) if v.dtype in INTEGRAL else -v.value, v.dtype,
+                                   n, dev)
             if is_decimal(v.dtype):
                 return D.negate(v)
+            if v.dtype in INTEGRAL:                     # -MIN_VALUE is MIN_VALUE (two's complement)
+                return PrimColumn(v.dtype, wrap_int_tensor(-v.data, v.dtype), v.valid)
             return PrimColumn(v.dtype, -v.data, v.valid)
         if e.op == "~":
             if isinstance(v, ConstColumn):
@@ -470,7 +476,7 @@ def _dec_operands(a: Column, b: Column):
     side is fractional (or a string / anything non-integral), else ('decimal', a, b) with integral sides widened to
     decimal(10,0) / decimal(20,0)."""
     other = b if is_decimal(a.dtype) else a
-    if not (is_decimal(other.dtype) or other.dtype in ("int", "long", "null")):
+    if not (is_decimal(other.dtype) or other.dtype in INTEGRAL + ("null",)):
         return "double", _dec_to_double(a), _dec_to_double(b)
     return "decimal", _to_dec(a), _to_dec(b)
 
@@ -524,7 +530,9 @@ def _arith(op: str, a: Column, b: Column, n, dev) -> Column:
     rt = common_type(a.dtype if a.dtype != "interval" else "long", b.dtype if b.dtype != "interval" else "long")
     if op == "/":
         rt = "double"
-    if rt not in ("int", "long", "double", "float", "decimal", "null"):
+    if rt == "null":
+        rt = "int"                                      # NULL op NULL: Spark types the untyped NULLs as INT
+    if rt not in INTEGRAL + ("double", "float", "decimal"):
         if a.dtype == "string" or b.dtype == "string":
             rt = "double"
             a = cast_column(a, "double")
@@ -532,20 +540,21 @@ def _arith(op: str, a: Column, b: Column, n, dev) -> Column:
         else:
             raise EvalError(f"cannot apply {op} to {a.dtype} and {b.dtype}")
     st = "double" if rt in ("double", "float", "decimal") else "long"
-    if rt == "int":
-        rt = "int" if (a.dtype == "int" and b.dtype == "int") else "long"
     x, y = _num_value(a, st), _num_value(b, st)
     if x is None or y is None:
-        return ConstColumn(None, rt, n, dev)
+        return ConstColumn(None, rt if op != "div" else "long", n, dev)
     valid = _result_valid(a, b)
     if _all_const(a, b):
         if op in ("/", "%", "div") and y == 0:
             return ConstColumn(None, rt, n, dev)
         r = {"+": lambda: x + y, "-": lambda: x - y, "*": lambda: x * y, "/": lambda: x / y,
-             "%": lambda: math.fmod(x, y) if st == "double" else int(math.fmod(x, y)),
+             "%": lambda: math.fmod(x, y) if st == "double" else (0 if y == -1 else int(math.fmod(x, y))),
              "div": lambda: int(x // y) if (x >= 0) == (y >= 0) else -int(abs(x) // abs(y)),
              "&": lambda: int(x) & int(y), "|": lambda: int(x) | int(y), "^": lambda: int(x) ^ int(y)}[op]()
-        return ConstColumn(r, rt if op != "div" else "long", n, dev)
+        if op == "div":
+            return ConstColumn(wrap_int_value(r, "long"), "long", n, dev)
+        # constant folding stays inside the result type: integer overflow wraps as the JVM's does
+        return ConstColumn(wrap_int_value(r, rt) if st == "long" and op != "/" else r, rt, n, dev)
     if op == "+":
         r = x + y
     elif op == "-":
@@ -588,12 +597,14 @@ def _arith(op: str, a: Column, b: Column, n, dev) -> Column:
         r = torch.full((n,), r, device=dev)
     if r.dim() == 0:
         r = r.expand(n).clone()
+    if op in ("+", "-", "*") and st == "long":
+        r = wrap_int_tensor(r, rt)                      # int / smallint / tinyint overflow wraps to the width
     return PrimColumn(rt, r, valid)
 
 
 def _ts_arith(op, a, b, n, dev):
     # timestamp ± interval, timestamp - timestamp (→ interval µs as long)
-    if a.dtype == "timestamp" and b.dtype in ("interval", "long", "int") and op in ("+", "-"):
+    if a.dtype == "timestamp" and b.dtype in ("interval",) + INTEGRAL and op in ("+", "-"):
         x, y = _num_value(a, "long"), _num_value(b, "long")
         if x is None or y is None:
             return ConstColumn(None, "timestamp", n, dev)
@@ -938,8 +949,83 @@ def _const_str(c: ConstColumn) -> str:
 # casts
 # ---------------------------------------------------------------------------------------------------------------
 
+def _complex_str(v, t) -> str:
+    """Spark 2.4 ``Cast.castToString`` of an array / map / struct value (no spark.sql.legacy flag existed yet, this
+    is the behaviour Spark 3.0 kept behind spark.sql.legacy.castComplexTypesToString.enabled): arrays ``[a, b]``,
+    maps ``[k1 -> v1, k2 -> v2]``, structs ``[f1, f2]`` (maps and structs in brackets, not braces); a NULL element,
+    map value or struct field is omitted, its separator kept (``array(1, NULL)`` → ``[1,]``); elements render as
+    their own cast to string (no quotes).  JSON-text columns carry their parsed value with the schema type."""
+    if v is None:
+        return ""
+    if isinstance(t, ArrayType) or (isinstance(v, list) and not isinstance(t, (MapType, StructType))):
+        et = t.element if isinstance(t, ArrayType) else None
+        out = "["
+        for i, x in enumerate(v):
+            if i:
+                out += ","
+            if x is not None:
+                out += (" " if i else "") + _complex_str(x, et)
+        return out + "]"
+    if isinstance(t, MapType) or (isinstance(v, dict) and not isinstance(t, StructType)):
+        kt, vt = (t.key, t.value) if isinstance(t, MapType) else (None, None)
+        parts = []
+        for k, x in v.items():
+            parts.append(_complex_str(k, kt) + " ->" + ("" if x is None else " " + _complex_str(x, vt)))
+        return "[" + ", ".join(parts) + "]"
+    if isinstance(t, StructType) or isinstance(v, dict):
+        fts = {f.name: f.dtype for f in t.fields} if isinstance(t, StructType) else {}
+        out = "["
+        for i, (k, x) in enumerate(v.items()):
+            if i:
+                out += ","
+            if x is not None:
+                out += (" " if i else "") + _complex_str(x, fts.get(k))
+        return out + "]"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, float):
+        return F.java_double_str(v)
+    import datetime as _dtm
+    if isinstance(v, _dtm.datetime):
+        return F.format_timestamp_us(int(round((v.replace(tzinfo=None) - _dtm.datetime(1970, 1, 1))
+                                               .total_seconds() * 1e6)), iso=False)
+    if isinstance(v, _dtm.date):
+        return v.isoformat()
+    if is_decimal(t):
+        import decimal as _pd
+        return D.render(_pd.Decimal(v), t.scale)
+    return str(v)
+
+
+def _d2i_value(v: float, to: str) -> int:
+    """JVM double → integral conversion (Scala's ``toInt`` / ``toLong``, i.e. d2i / d2l): NaN → 0, saturating at the
+    int (long) range, truncating toward zero; ``toShort`` / ``toByte`` are ``toInt`` then the low 16 / 8 bits."""
+    if v != v:
+        return 0
+    lo, hi = INT_RANGE["long" if to == "long" else "int"]
+    if v >= hi:
+        r = hi
+    elif v <= lo:
+        r = lo
+    else:
+        r = int(v)
+    return wrap_int_value(r, to)
+
+
+def _d2i(d: torch.Tensor, to: str) -> torch.Tensor:
+    """``_d2i_value`` over a float64 tensor."""
+    lo, hi = INT_RANGE["long" if to == "long" else "int"]
+    z = torch.where(torch.isnan(d), torch.zeros_like(d), d)
+    # float(hi) rounds up to 2^63 for long: anything at or above it saturates to hi exactly
+    r = torch.clamp(z, min=float(lo)).trunc()
+    over = r >= float(hi)
+    r = torch.where(over, torch.zeros_like(r), r).to(torch.int64)
+    r = torch.where(over, torch.full_like(r, hi), r)
+    return wrap_int_tensor(r, to)
+
+
 def cast_column(col: Column, to: str) -> Column:
-    to = {"integer": "int", "bigint": "long", "bool": "boolean"}.get(to, to)
+    to = {"integer": "int", "bigint": "long", "bool": "boolean", "smallint": "short", "tinyint": "byte"}.get(to, to)
     n, dev = col.length, col.device
     if col.dtype == to or (to == "string" and isinstance(col, StrColumn) and col.dtype == "string"):
         return col
@@ -951,7 +1037,7 @@ def cast_column(col: Column, to: str) -> Column:
             return r
     if to == "string":
         if isinstance(col, PrimColumn):
-            if col.dtype in ("int", "long"):
+            if col.dtype in INTEGRAL:
                 from ..ops import strings as S
                 return S.from_int64(col.data, col.valid)
             if col.dtype in ("double", "float", "decimal") and col.data.is_cuda:
@@ -974,39 +1060,37 @@ def cast_column(col: Column, to: str) -> Column:
             return strings_from_pylist([None if v is None else _cast_value(_storage_of(v, col.dtype), col.dtype,
                                                                           "string") for v in vals], dev)
         if isinstance(col, (StructColumn, ArrayColumn, JsonColumn)):
-            from .serialize import column_json_values
-            return strings_from_pylist(column_json_values(col), dev)
+            t = col.dtype
+            return strings_from_pylist([None if v is None else _complex_str(v, t) for v in col.to_pylist()], dev)
         raise EvalError(f"cannot cast {col.dtype} to string")
     if isinstance(col, StrColumn):
         if to == "timestamp":
             from ..ops import strings as S
             return S.to_timestamp(col)
-        if to in ("int", "long", "double", "float", "decimal") and col.starts.is_cuda:
+        if to in INTEGRAL + ("double", "float", "decimal") and col.starts.is_cuda:
             from ..ops import native as N
-            mode = {"long": 0, "int": 1}.get(to, 2)
+            mode = 0 if to == "long" else (1 if to in INTEGRAL else 2)
             out = torch.empty(n, dtype=torch.int64, device=dev)
             ok = torch.empty(n, dtype=torch.uint8, device=dev)
             N.call("dxa_str_to_num", N.ptr(col.arena), N.ptr(col.starts), N.ptr(col.lens), N.ptr(N.u8(col.valid)),
                    n, mode, N.ptr(out), N.ptr(ok), N.stream_handle(dev))
-            return PrimColumn(to, out.view(torch.float64) if mode == 2 else out, ok.view(torch.bool))
+            okb = ok.view(torch.bool)
+            if to in ("byte", "short"):                 # UTF8String.toByte / toShort: NULL outside the range
+                lo, hi = INT_RANGE[to]
+                okb = okb & (out >= lo) & (out <= hi)
+            return PrimColumn(to, out.view(torch.float64) if mode == 2 else out, okb)
         vals = col.to_pylist()
         conv = [_cast_value(v, "string", to) for v in vals]
         return column_from_pylist(conv, to, dev)
     if isinstance(col, PrimColumn):
         d = col.data
-        if to in ("int", "long"):
-            if col.dtype == "timestamp":
-                return PrimColumn(to, torch.div(d, 1_000_000, rounding_mode="floor"), col.valid)
+        if to in INTEGRAL:
+            if col.dtype == "timestamp":              # seconds (floor), then the width's low bits
+                return PrimColumn(to, wrap_int_tensor(torch.div(d, 1_000_000, rounding_mode="floor"), to),
+                                  col.valid)
             if d.dtype == torch.float64:
-                ok = torch.isfinite(d)
-                r = torch.where(ok, d, torch.zeros_like(d)).trunc().to(torch.int64)
-                if to == "int":
-                    r = ((r + 2**31) % 2**32) - 2**31
-                return PrimColumn(to, r, and_valid(col.valid, None if bool(ok.all()) else ok))
-            r = d.to(torch.int64)
-            if to == "int":
-                r = ((r + 2**31) % 2**32) - 2**31
-            return PrimColumn(to, r, col.valid)
+                return PrimColumn(to, _d2i(d, to), col.valid)
+            return PrimColumn(to, wrap_int_tensor(d.to(torch.int64), to), col.valid)
         if to in ("double", "float", "decimal"):
             if col.dtype == "timestamp":
                 return PrimColumn(to, D.true_div(d.to(torch.float64), 1e6), col.valid)
@@ -1032,7 +1116,7 @@ def _cast_decimal(col: Column, to) -> Optional[Column]:
     if is_decimal(to):
         if is_decimal(col.dtype):
             return D.change_type(col, to)
-        if col.dtype in ("int", "long", "boolean") and isinstance(col, PrimColumn):
+        if col.dtype in INTEGRAL + ("boolean",) and isinstance(col, PrimColumn):
             return D.from_integral(col, to)
         if col.dtype in ("double", "float") and isinstance(col, PrimColumn):
             return D.from_double(col, to)
@@ -1041,7 +1125,7 @@ def _cast_decimal(col: Column, to) -> Optional[Column]:
         if col.dtype == "string" and isinstance(col, StrColumn):
             return D.from_text(col, to)
         raise EvalError(f"cannot cast {col.dtype} to {to}")
-    if to in ("int", "long"):
+    if to in INTEGRAL:
         return D.to_integral(col, to)
     if to in ("double", "float"):
         return D.to_double(col)
@@ -1093,18 +1177,21 @@ def _cast_value(v, frm, to):
             if isinstance(v, float):
                 return F.java_double_str(v)
             return str(v)
-        if to in ("int", "long"):
+        if to in INTEGRAL:
             if isinstance(v, str):
-                # Spark (non-ANSI): [+-]digits[.digits] after trimming; the fraction truncates; no exponent
+                # Spark (non-ANSI): [+-]digits[.digits] after trimming; the fraction truncates; no exponent; NULL
+                # outside the type's range (UTF8String.toLong / toInt / toShort / toByte)
                 m = _INT_STR.match(v.strip(_CAST_WS))
                 if not m or not (m.group(2) or m.group(3)):
                     return None
                 r = int((m.group(1) or "") + (m.group(2) or "0"))
-                lo, hi = (-2**31, 2**31 - 1) if to == "int" else (-2**63, 2**63 - 1)
+                lo, hi = INT_RANGE[to]
                 return r if lo <= r <= hi else None
             if frm == "timestamp":
-                return int(v) // 1_000_000
-            return int(v)
+                return wrap_int_value(int(v) // 1_000_000, to)
+            if isinstance(v, float):
+                return _d2i_value(v, to)
+            return wrap_int_value(int(v), to)
         if to in ("double", "float", "decimal"):
             if isinstance(v, str):
                 t = v.strip(_CAST_WS)
@@ -1456,7 +1543,44 @@ def _f_abs(e, scope, ctx, subst):
         if isinstance(a, ConstColumn):
             return ConstColumn(None if a.value is None else abs(a.value), a.dtype, a.length, a.device)
         return D.absolute(a)
-    return _ABS_NUM(e, scope, ctx, subst)
+    r = _ABS_NUM(e, scope, ctx, subst)
+    if r.dtype in INTEGRAL:                             # abs(MIN_VALUE) is MIN_VALUE (Java Math.abs)
+        if isinstance(r, ConstColumn):
+            return ConstColumn(None if r.value is None else wrap_int_value(r.value, r.dtype), r.dtype, r.length,
+                               r.device)
+        return PrimColumn(r.dtype, wrap_int_tensor(r.data, r.dtype), r.valid)
+    return r
+
+
+def _f_ceil_floor(up: bool):
+    """ceil / floor: a decimal stays a decimal, decimal(p - s + 1, 0) (Spark 2.4 Ceil / Floor); a double (and
+    anything implicitly cast to one) becomes a BIGINT by ``Math.ceil(x).toLong`` (saturating, NaN → 0); a BIGINT is
+    unchanged."""
+    base = _unary_num(torch.ceil if up else torch.floor, "long")
+
+    def f(e, scope, ctx, subst):
+        (a,) = _args(e, scope, ctx, subst)
+        if is_decimal(a.dtype):
+            if isinstance(a, ConstColumn):
+                import decimal as _pd
+                rt = D.bounded(a.dtype.precision - a.dtype.scale + 1, 0)
+                if a.value is None:
+                    return ConstColumn(None, rt, a.length, a.device)
+                v = _pd.Decimal(a.value).to_integral_value(_pd.ROUND_CEILING if up else _pd.ROUND_FLOOR)
+                return ConstColumn(v, rt, a.length, a.device)
+            return D.ceil_floor_column(a, up)
+        if a.dtype in INTEGRAL:
+            return cast_column(a, "long")
+        if isinstance(a, ConstColumn):
+            if a.value is None:
+                return ConstColumn(None, "long", a.length, a.device)
+            x = float(a.value)
+            return ConstColumn(_d2i_value(math.ceil(x) if up and math.isfinite(x) else
+                                          (math.floor(x) if math.isfinite(x) else x), "long"), "long", a.length,
+                               a.device)
+        x = a.data.to(torch.float64)
+        return PrimColumn("long", _d2i(torch.ceil(x) if up else torch.floor(x), "long"), a.valid)
+    return f
 
 
 def _unary_num(fn, out_type=None):
@@ -1476,7 +1600,7 @@ def _unary_num(fn, out_type=None):
             d = d.to(torch.float64)
         r = fn(d)
         rt = out_type or a.dtype
-        if rt in ("int", "long") and r.dtype == torch.float64:
+        if rt in INTEGRAL and r.dtype == torch.float64:
             r = r.to(torch.int64)
         return PrimColumn(rt, r, a.valid)
     return f
@@ -1633,6 +1757,8 @@ def _f_concat_ws(e, scope, ctx, subst):
     n, dev = scope.length, scope.device
     args = _args(e, scope, ctx, subst)
     sep = args[0]
+    if isinstance(sep, ConstColumn) and sep.value is None:
+        return ConstColumn(None, "string", n, dev)
     parts = []
     for i, a in enumerate(args[1:]):
         if i:
@@ -1650,10 +1776,34 @@ def _f_concat_ws(e, scope, ctx, subst):
                 continue
             ps.append(p if isinstance(p, StrColumn) else cast_column(p, "string"))
         return S.concat_ws(_const_str(sep), ps, n, dev)
-    if any(not isinstance(p, ConstColumn) and p.valid is not None for p in args[1:]):
-        cols = [p.to_pylist() if not isinstance(p, ConstColumn) else [p.value] * n for p in args[1:]]
-        s = _const_str(sep)
-        out = [s.join(str(c[i]) for c in cols if c[i] is not None) for i in range(n)]
+    nullable = any((p.value is None) if isinstance(p, ConstColumn) else p.valid is not None for p in args[1:])
+    if nullable or any(isinstance(p, ArrayColumn) for p in args[1:]) or not isinstance(sep, ConstColumn):
+        # host: NULL arguments (and NULL array elements) are skipped, array<string> arguments contribute their
+        # elements; a NULL separator makes the result NULL (Spark ConcatWs)
+        seps = sep.to_pylist() if not isinstance(sep, ConstColumn) else [sep.value] * n
+        cols = []
+        for p in args[1:]:
+            if isinstance(p, ArrayColumn):
+                cols.append(("arr", p.to_pylist()))
+            elif isinstance(p, ConstColumn):
+                cols.append(("val", [None if p.value is None else _const_str(p)] * n))
+            else:
+                cols.append(("val", cast_column(p, "string").to_pylist()))
+        out = []
+        for i in range(n):
+            if seps[i] is None:
+                out.append(None)
+                continue
+            items = []
+            for kind, c in cols:
+                v = c[i]
+                if v is None:
+                    continue
+                if kind == "arr":
+                    items.extend(x if isinstance(x, str) else _complex_str(x, None) for x in v if x is not None)
+                else:
+                    items.append(v)
+            out.append(str(seps[i]).join(items))
         return strings_from_pylist(out, dev)
     return _concat(parts, n, dev)
 
@@ -1782,8 +1932,8 @@ _FUNCS: Dict[str, Callable] = {
     "nullif": _f_nullif, "nvl2": _f_nvl2, "isnull": _f_isnull(False), "isnotnull": _f_isnull(True),
     "map": _f_map, "struct": _f_struct, "named_struct": _f_named_struct, "array": _f_array,
     "filternull": _f_filternull, "size": _f_size, "cardinality": _f_size, "element_at": _f_element_at,
-    "abs": _f_abs, "floor": _unary_num(torch.floor, "long"), "ceil": _unary_num(torch.ceil, "long"),
-    "ceiling": _unary_num(torch.ceil, "long"), "sqrt": _unary_num(torch.sqrt, "double"),
+    "abs": _f_abs, "floor": _f_ceil_floor(False), "ceil": _f_ceil_floor(True), "ceiling": _f_ceil_floor(True),
+    "sqrt": _unary_num(torch.sqrt, "double"),
     "exp": _unary_num(torch.exp, "double"), "ln": _unary_num(torch.log, "double"),
     "log10": _unary_num(torch.log10, "double"), "log2": _unary_num(torch.log2, "double"),
     "sign": _unary_num(torch.sign, "double"), "signum": _unary_num(torch.sign, "double"),

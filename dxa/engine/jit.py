@@ -33,9 +33,16 @@ from .column import Column, ConstColumn, PrimColumn
 from .decimal import is_decimal
 from .types import common_type
 
-NUMERIC = {"int", "long", "double", "float", "decimal"}
+NUMERIC = {"byte", "short", "int", "long", "double", "float", "decimal"}
 FRACTIONAL = {"double", "float", "decimal"}
-INTEGRAL_STORAGE = {"int", "long", "timestamp", "date"}
+INTEGRAL_STORAGE = {"byte", "short", "int", "long", "timestamp", "date"}
+# int64 storage of a narrower logical integer: the C cast that wraps a result to the width (JVM overflow)
+_NARROW_C = {"int": "int", "short": "short", "byte": "signed char"}
+
+
+def _wrap(v: str, dtype: str) -> str:
+    c = _NARROW_C.get(dtype)
+    return f"(long long)({c})({v})" if c else v
 CTYPE = {torch.float64: "double", torch.int64: "long long", torch.bool: "unsigned char"}
 MIN_ROWS = int(os.environ.get("DXA_JIT_MIN_ROWS", "65536"))
 MIN_OPS = 2
@@ -171,10 +178,10 @@ class _Gen:
                 self.nops += 1
                 if v.dtype in FRACTIONAL:
                     return R(self.tmp("double", f"-{v.val}"), v.ok, v.dtype, v.nullable)
-                return R(self.tmp("long long", f"(long long)(0ULL - (unsigned long long){v.val})"), v.ok, v.dtype,
-                         v.nullable)
+                return R(self.tmp("long long", _wrap(f"(long long)(0ULL - (unsigned long long){v.val})", v.dtype)),
+                         v.ok, v.dtype, v.nullable)
             if e.op == "~":
-                self._need(v, {"int", "long"})
+                self._need(v, {"byte", "short", "int", "long"})
                 self.nops += 1
                 return R(self.tmp("long long", f"~{v.val}"), v.ok, v.dtype, v.nullable)
             if e.op == "+":
@@ -299,9 +306,9 @@ class _Gen:
         rt = common_type(a.dtype, b.dtype)
         if op == "/":
             rt = "double"
+        if rt == "null":
+            rt = "int"
         st = "double" if rt in FRACTIONAL else "long"
-        if rt == "int":
-            rt = "int" if (a.dtype == "int" and b.dtype == "int") else "long"
         if op in ("&", "|", "^") and st != "long":
             raise NotFusible("bitwise on fractional")
         if (a.const is not None and a.const.value is None) or (b.const is not None and b.const.value is None):
@@ -316,7 +323,7 @@ class _Gen:
             if st == "double":
                 v = f"{x} {op} {y}"
             else:
-                v = f"(long long)((unsigned long long){x} {op} (unsigned long long){y})"
+                v = _wrap(f"(long long)((unsigned long long){x} {op} (unsigned long long){y})", rt)
             return R(self.tmp(ct, v), ok, rt, nullable)
         if op in ("&", "|", "^"):
             return R(self.tmp(ct, f"{x} {op} {y}"), ok, rt, nullable)

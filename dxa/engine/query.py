@@ -898,6 +898,8 @@ def _expand_items(sel: A.Select, scope: Scope) -> List[Tuple[A.Expr, str]]:
                     items.append((A.Ident(q + (nm,)), nm))
                 continue
             raise QueryError(f"cannot expand {'.'.join(q)}.*")
+        if isinstance(it.alias, tuple) and not (isinstance(e, A.Call) and e.name in _GENERATOR_NAMES):
+            raise QueryError(f"a multi-alias AS ({', '.join(it.alias)}) is only allowed on a generator function")
         items.append((e, it.alias or output_name(e)))
     return items
 
@@ -1320,7 +1322,11 @@ def _exec_generator_select(sel: A.Select, items, gen_at, scope: Scope, ctx) -> T
     k = gen_at[0]
     call, alias = items[k]
     rows, names, gcols = GEN.generate(call, scope, ctx)
-    if alias != output_name(call):
+    if isinstance(alias, tuple):
+        if len(alias) != len(names):
+            raise QueryError(f"{call.name}() produces {len(names)} column(s), but {len(alias)} alias(es) were given")
+        names = list(alias)
+    elif alias != output_name(call):
         names = [alias] if len(names) == 1 else names
     sub = Scope(scope.names, TakenColumns(scope.cols, rows), scope.quals, int(rows.shape[0]), scope.device)
     sub.dist = getattr(scope, "dist", P.REPLICATED)
@@ -1693,7 +1699,7 @@ def _percentile(groups: G.Groups, arg, p, exact: bool):
         return _take_nullable(arg, torch.where(has, at, torch.full_like(at, -1)))
     r = v[torch.clamp(start + k, max=max(0, v.numel() - 1))] if v.numel() else torch.zeros(ng, dtype=torch.float64,
                                                                                           device=dev)
-    if arg.dtype in ("int", "long"):
+    if arg.dtype in ("byte", "short", "int", "long"):
         return PrimColumn(arg.dtype, r.to(torch.int64), has)
     return PrimColumn(arg.dtype if arg.dtype in ("double", "float") else "double", r, has)
 

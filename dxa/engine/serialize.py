@@ -57,7 +57,7 @@ def _frag_values(col: Column) -> List[Optional[str]]:
         dt = col.dtype
         if dt == "boolean":
             fmt = lambda v: "true" if v else "false"
-        elif dt in ("int", "long"):
+        elif dt in ("byte", "short", "int", "long"):
             fmt = str
         elif dt == "timestamp":
             fmt = lambda v: '"' + F.format_timestamp_us(v) + '"'

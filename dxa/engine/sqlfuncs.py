@@ -23,6 +23,7 @@ import torch
 from ..sql import ast as A
 from . import functions as F
 from .decimal import true_div as _true_div
+from .types import INTEGRAL, SIMPLE_NAME, ArrayType, MapType, StructField, StructType, wrap_int_tensor
 from .column import (ArrayColumn, Column, ConstColumn, PrimColumn, StrColumn, StructColumn, column_from_pylist,
                      materialize, strings_from_pylist)
 from .expr import (EvalError, _args, _host_string_fn, _slot_present, bool_col, cast_column, evaluate,
@@ -88,7 +89,7 @@ def _f_mod(positive: bool):
     def f(e, scope, ctx, subst):
         n, dev = scope.length, scope.device
         a, b = (_num(c, n, dev) for c in _args(e, scope, ctx, subst))
-        integral = a.dtype in ("int", "long") and b.dtype in ("int", "long")
+        integral = a.dtype in INTEGRAL and b.dtype in INTEGRAL
         x = a.data if integral else a.data.to(torch.float64)
         y = b.data if integral else b.data.to(torch.float64)
         zero = y == 0
@@ -326,9 +327,35 @@ def _java_format(us: int, fmt: str) -> str:
             out.append("Z" if c == "X" else "+0000")
         elif c == "z":
             out.append("UTC")
+        elif c == "u":                                 # day number of week, 1 = Monday … 7 = Sunday
+            out.append(f"{t.isoweekday():0{k}d}")
+        elif c == "F":                                 # day of week in month (the n-th such weekday)
+            out.append(f"{(t.day - 1) // 7 + 1:0{k}d}")
+        elif c == "k":                                 # hour 1-24
+            out.append(f"{t.hour or 24:0{k}d}")
+        elif c == "K":                                 # hour 0-11
+            out.append(f"{t.hour % 12:0{k}d}")
+        elif c == "L":                                 # stand-alone month
+            out.append(t.strftime("%B") if k >= 4 else t.strftime("%b") if k == 3 else f"{t.month:0{k}d}")
+        elif c == "G":
+            out.append("AD")
+        elif c in "wW":
+            out.append(f"{_us_week(t.date(), c == 'W'):0{k}d}")
         else:
             raise EvalError(f"unsupported date pattern letter {c!r}")
     return "".join(out)
+
+
+def _us_week(d: "_dt.date", in_month: bool) -> int:
+    """SimpleDateFormat 'w' / 'W' in the US locale Spark 2.4's formatter uses: weeks start on Sunday and the week
+    holding the 1st (of the year / month) is week 1; late-December days in the week that holds the next January 1st
+    are week 1 of that year."""
+    sun = d - _dt.timedelta(days=(d.weekday() + 1) % 7)
+    if not in_month and (sun + _dt.timedelta(days=6)).year > d.year:
+        return 1
+    first = _dt.date(d.year, d.month if in_month else 1, 1)
+    first_sun = first - _dt.timedelta(days=(first.weekday() + 1) % 7)
+    return (sun - first_sun).days // 7 + 1
 
 
 def format_timestamps(ts: Column, fmt: str) -> Column:
@@ -788,7 +815,7 @@ def spark_hash_value(v, dtype, seed):
     import struct
     if v is None:
         return seed
-    if dtype in ("int", "date") or isinstance(v, bool):
+    if dtype in ("byte", "short", "int", "date") or isinstance(v, bool):
         return _hash_int(int(v), seed)
     if dtype in ("long", "timestamp"):
         return _hash_long(int(v), seed)
@@ -825,7 +852,7 @@ def _is_dec(t):
     return is_decimal(t)
 
 
-_HASH_KIND = {"int": 0, "date": 0, "long": 1, "timestamp": 1, "double": 2, "float": 3, "boolean": 4}
+_HASH_KIND = {"byte": 0, "short": 0, "int": 0, "date": 0, "long": 1, "timestamp": 1, "double": 2, "float": 3, "boolean": 4}
 
 
 def _hash_device(args, n, dev):
@@ -1284,6 +1311,7 @@ def _register():
     reg("bin", _host_string_fn(lambda x: format(int(x) & 0xFFFFFFFFFFFFFFFF, "b") if int(x) < 0
                                else format(int(x), "b")))
     for nm, to in (("string", "string"), ("int", "int"), ("integer", "int"), ("bigint", "long"), ("long", "long"),
+                   ("smallint", "short"), ("short", "short"), ("tinyint", "byte"), ("byte", "byte"),
                    ("double", "double"), ("float", "double"), ("boolean", "boolean"), ("date", "date"),
                    ("timestamp", "timestamp")):
         reg(nm, _f_cast_to(to))
@@ -1372,6 +1400,17 @@ def _f_shift(kind):
         a, k = _args(e, scope, ctx, subst)
         a, k = materialize(_num(a, n, dev)), materialize(_num(k, n, dev))
         x = a.data.to(torch.int64)
+        if a.dtype in ("byte", "short", "int"):
+            # Spark ShiftLeft / ShiftRight(Unsigned) on an INT (smaller types widen to it): Java's 32-bit shifts,
+            # the count taken mod 32, the result an INT
+            s = (k.data.to(torch.int64) & 31)
+            if kind == "left":
+                r = wrap_int_tensor(torch.bitwise_left_shift(x, s), "int")
+            elif kind == "right":
+                r = torch.bitwise_right_shift(x, s)
+            else:
+                r = wrap_int_tensor(torch.bitwise_right_shift(x & 0xFFFFFFFF, s), "int")
+            return PrimColumn("int", r, _and(a.valid, k.valid))
         s = (k.data.to(torch.int64) & 63)
         if kind == "left":
             r = torch.bitwise_left_shift(x, s)
@@ -1438,8 +1477,8 @@ def _f_next_day(e, scope, ctx, subst):
 
 def _f_typeof(e, scope, ctx, subst):
     (a,) = _args(e, scope, ctx, subst)
-    t = {"long": "bigint", "int": "int", "double": "double", "string": "string", "boolean": "boolean",
-         "timestamp": "timestamp", "date": "date"}.get(str(a.dtype), str(a.dtype))
+    t = dict(SIMPLE_NAME, double="double", string="string", boolean="boolean", timestamp="timestamp",
+             date="date").get(str(a.dtype), str(a.dtype))
     return ConstColumn(t, "string", scope.length, scope.device)
 
 
@@ -1931,7 +1970,7 @@ def _conv_device(col, fb, tb):
 def _f_format_number(e, scope, ctx, subst):
     args = _args(e, scope, ctx, subst)
     x = args[0] if args else None
-    if (len(args) == 2 and isinstance(x, PrimColumn) and x.data.is_cuda and x.dtype in ("int", "long", "double", "float")
+    if (len(args) == 2 and isinstance(x, PrimColumn) and x.data.is_cuda and x.dtype in INTEGRAL + ("double", "float")
             and isinstance(args[1], ConstColumn) and isinstance(args[1].value, int)):
         from ..ops import strfuncs as SF
         out = SF.format_number(x, int(args[1].value))
@@ -1942,7 +1981,7 @@ def _f_format_number(e, scope, ctx, subst):
 
 def _f_bin(e, scope, ctx, subst):
     (x,) = _args(e, scope, ctx, subst)
-    if isinstance(x, PrimColumn) and x.data.is_cuda and x.dtype in ("int", "long", "double", "float"):
+    if isinstance(x, PrimColumn) and x.data.is_cuda and x.dtype in INTEGRAL + ("double", "float"):
         from ..ops import strfuncs as SF
         if x.data.dtype == torch.float64:             # Spark casts to bigint (truncation)
             x = cast_column(x, "long")
@@ -2222,7 +2261,7 @@ def _xpath_scalar(kind):
         if kind == "boolean":
             return bool(v) if k == "nodes" else v != 0
         num = v if k == "number" else (float(v[0]) if v else float("nan"))
-        if kind in ("int", "long", "short"):
+        if kind in INTEGRAL:
             return 0 if num != num else int(num)
         return num
     return fn
@@ -2271,3 +2310,114 @@ def _register_spark24_more():
 
 
 _register_spark24_more()
+
+
+# ---- round-6 Spark 2.4 built-ins: arrays_zip, shuffle, map_from_entries, space; reverse on arrays --------------
+
+def _f_arrays_zip(e, scope, ctx, subst):
+    """arrays_zip(a1, …, ak) → array<struct<n1, …, nk>>: the i-th struct holds every array's i-th element, NULL past a
+    shorter array's end; NULL when any argument is NULL.  Field names: a column argument's name, else its position
+    ("0", "1", …) — Spark 2.4 ArraysZip."""
+    n, dev = scope.length, scope.device
+    args = _args(e, scope, ctx, subst)
+    if not args:
+        return ConstColumn([], ArrayType(StructType(())), n, dev)
+    for a in args:
+        if not (isinstance(a, ArrayColumn) or (isinstance(a, ConstColumn) and a.value is None)):
+            raise EvalError("arrays_zip() expects array arguments")
+    names = [x.parts[-1] if isinstance(x, A.Ident) else str(i) for i, x in enumerate(e.args)]
+    ftypes = [a.dtype.element if isinstance(a.dtype, ArrayType) else "null" for a in args]
+    st = StructType(tuple(StructField(nm, t) for nm, t in zip(names, ftypes)))
+    lists = [a.to_pylist() if not isinstance(a, ConstColumn) else [None] * n for a in args]
+    out = []
+    for i in range(n):
+        row = [l[i] for l in lists]
+        if any(r is None for r in row):
+            out.append(None)
+            continue
+        k = max((len(r) for r in row), default=0)
+        out.append([{nm: (r[j] if j < len(r) else None) for nm, r in zip(names, row)} for j in range(k)])
+    return array_from_pylist(out, st, dev)
+
+
+def _f_shuffle(e, scope, ctx, subst):
+    """shuffle(array): a random permutation of each row's elements (non-deterministic, like Spark's Shuffle; the
+    optional seed argument makes it repeatable here)."""
+    import random as _rnd
+    args = _args(e, scope, ctx, subst)
+    arr = args[0]
+    if isinstance(arr, ConstColumn) and arr.value is None:
+        return arr
+    if not isinstance(arr, ArrayColumn):
+        raise EvalError("shuffle() expects an array")
+    seed = args[1].value if len(args) > 1 and isinstance(args[1], ConstColumn) else None
+    rng = _rnd.Random(seed)
+    out = []
+    for l in arr.to_pylist():
+        if l is not None:
+            l = list(l)
+            rng.shuffle(l)
+        out.append(l)
+    return array_from_pylist(out, arr.dtype.element, scope.device)
+
+
+def _f_map_from_entries(e, scope, ctx, subst):
+    """map_from_entries(array<struct<k, v>>) → map<k, v>; a NULL entry makes the row NULL, a NULL key is an error
+    (Spark 2.4 MapFromEntries); a repeated key keeps its last value."""
+    (arr,) = _args(e, scope, ctx, subst)
+    if isinstance(arr, ConstColumn) and arr.value is None:
+        return arr
+    if not isinstance(arr, ArrayColumn) or not isinstance(arr.dtype.element, StructType) or \
+            len(arr.dtype.element.fields) != 2:
+        raise EvalError("map_from_entries() expects an array of two-field structs")
+    kf, vf = arr.dtype.element.fields
+    out = []
+    for l in arr.to_pylist():
+        if l is None or any(x is None for x in l):
+            out.append(None)
+            continue
+        m = {}
+        for x in l:
+            k = x[kf.name]
+            if k is None:
+                raise EvalError("map_from_entries(): cannot use null as map key")
+            m[k] = x[vf.name]
+        out.append(m)
+    return column_from_pylist(out, MapType(kf.dtype, vf.dtype), scope.device)
+
+
+def _f_space(e, scope, ctx, subst):
+    """space(n): n spaces (none for n <= 0)."""
+    n, dev = scope.length, scope.device
+    (k,) = _args(e, scope, ctx, subst)
+    if isinstance(k, ConstColumn):
+        return ConstColumn(None if k.value is None else " " * max(0, int(k.value)), "string", n, dev)
+    return strings_from_pylist([None if v is None else " " * max(0, int(v)) for v in k.to_pylist()], dev)
+
+
+def _array_reverse(arr: ArrayColumn) -> ArrayColumn:
+    """reverse(array): the slot order reversed — a row's array is its present slots left to right, so reversing the
+    slots (and the presence mask's columns) reverses every row's array, on the device, without a host round trip."""
+    pres = None if arr.present is None else torch.flip(arr.present, dims=[1])
+    return ArrayColumn(list(reversed(arr.elements)), arr.length, arr.valid, arr.drop_nulls, arr.device, present=pres)
+
+
+def _register_round6():
+    reg = register_function
+    reg("arrays_zip", _f_arrays_zip)
+    reg("shuffle", _f_shuffle)
+    reg("map_from_entries", _f_map_from_entries)
+    reg("space", _f_space)
+    reg("xpath_short", _host_string_fn(_xpath_scalar("short"), "short"))
+    from .expr import _FUNCS
+    string_reverse = _FUNCS["reverse"]
+
+    def _f_reverse(e, scope, ctx, subst):
+        args = _args(e, scope, ctx, subst)
+        if args and isinstance(args[0], ArrayColumn):
+            return _array_reverse(args[0])
+        return string_reverse(e, scope, ctx, subst)
+    reg("reverse", _f_reverse)
+
+
+_register_round6()

@@ -5,7 +5,9 @@ scala/datax/input/SchemaFile.scala:22-26), optionally carrying SimulatedData/Dat
 (minValue/maxValue/allowedValues/useCurrentTimeMillis, datax-utility/.../DataGenerator.scala:20-26).
 
 Physical mapping (device columns):
-  boolean → torch.bool; int/long → int64; float/double → float64; timestamp → int64 µs since epoch (UTC);
+  boolean → torch.bool; byte/short/int/long → int64 holding a value of the logical width (Spark's ByteType,
+  ShortType, IntegerType, LongType: every operator that can leave the range wraps two's-complement to it —
+  ``wrap_int_tensor`` / ``wrap_int_value``); float/double → float64; timestamp → int64 µs since epoch (UTC);
   date → int64 days; string → (arena uint8, starts int64, lens int32); struct/map → child columns;
   array → fixed-arity element columns or raw JSON text.
 """
@@ -15,9 +17,37 @@ import json
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
-SCALAR_TYPES = ("boolean", "int", "long", "float", "double", "string", "timestamp", "date", "null", "binary",
-                "decimal")
-INTEGRAL = ("int", "long")
+SCALAR_TYPES = ("boolean", "byte", "short", "int", "long", "float", "double", "string", "timestamp", "date", "null",
+                "binary", "decimal")
+INTEGRAL = ("byte", "short", "int", "long")
+INT_BITS = {"byte": 8, "short": 16, "int": 32, "long": 64}
+INT_RANGE = {t: (-(1 << (b - 1)), (1 << (b - 1)) - 1) for t, b in INT_BITS.items()}
+# Spark's simpleString of each logical type (typeof, schema strings, generated column names)
+SIMPLE_NAME = {"byte": "tinyint", "short": "smallint", "int": "int", "long": "bigint"}
+
+
+def wrap_int_value(v: int, dtype: str) -> int:
+    """A Python integer reduced to the two's-complement range of ``dtype`` (JVM int/long/short/byte overflow)."""
+    b = INT_BITS.get(dtype, 64)
+    m = 1 << b
+    v = int(v) & (m - 1)
+    return v - m if v >= (m >> 1) else v
+
+
+def wrap_int_tensor(t, dtype: str):
+    """An int64 tensor reduced to the range of ``dtype``: the low bits, sign-extended (shift left, arithmetic shift
+    right — two elementwise kernels, on the host or the device).  ``long`` is already int64."""
+    b = INT_BITS.get(dtype, 64)
+    if b == 64:
+        return t
+    s = 64 - b
+    return (t << s) >> s
+
+
+def int_type_of_value(v: int) -> str:
+    """Spark's type of an integer literal: INT when it fits, else BIGINT (larger ones become decimals in the
+    parser)."""
+    return "int" if INT_RANGE["int"][0] <= v <= INT_RANGE["int"][1] else "long"
 FRACTIONAL = ("float", "double", "decimal")
 NUMERIC = INTEGRAL + FRACTIONAL
 
@@ -91,8 +121,8 @@ def is_nested(t) -> bool:
     return isinstance(t, (StructType, MapType, ArrayType))
 
 
-_SPARK_NAMES = {"integer": "int", "bigint": "long", "short": "int", "byte": "int", "smallint": "int",
-                "tinyint": "int", "real": "float", "bool": "boolean", "str": "string", "varchar": "string"}
+_SPARK_NAMES = {"integer": "int", "bigint": "long", "smallint": "short", "tinyint": "byte", "real": "float",
+                "bool": "boolean", "str": "string", "varchar": "string"}
 
 
 def from_json_obj(o) -> Any:
@@ -209,7 +239,7 @@ def common_type(a, b):
             return _wider_decimal(a, b)
         if a in FRACTIONAL or b in FRACTIONAL:
             return "double"
-        return "long"
+        return a if INT_BITS.get(a, 64) >= INT_BITS.get(b, 64) else b      # the wider integral type
     if {a, b} <= {"timestamp", "date"}:
         return "timestamp"
     if "string" in (a, b) and not is_nested(a) and not is_nested(b):

@@ -22,7 +22,8 @@ from ..engine.decimal import from_text as decimal_from_text, is_decimal, quantiz
 from ..engine.types import ArrayType, MapType, StructField, StructType
 
 FT = {"struct": 0, "boolean": 1, "long": 2, "double": 3, "float": 3, "decimal": 3, "string": 4, "raw": 5,
-      "timestamp": 6, "int": 7, "date": 8, "decimal_exact": 9}
+      "timestamp": 6, "int": 7, "date": 8, "decimal_exact": 9,
+      "short": 7, "byte": 7}      # smallint / tinyint: parsed as int, then range-checked (``_narrow``)
 FT_DECIMAL = 9          # decimal(p,s): the kernel keeps the number token's text; decimal.hip converts it exactly
 FT_SKIP = 10            # a field no statement reads (column pruning): its key still matches in schema order, its value
 #                         is skipped unstored — dropping the node instead would make every such key a failed
@@ -426,6 +427,13 @@ def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):
                                    raw.view(torch.float64), v)
         elif nd.code == FT["boolean"]:
             cols[idx] = PrimColumn("boolean", raw != 0, v)
+        elif nd.dtype in ("short", "byte"):
+            # the kernel range-checks as int; a smallint / tinyint outside its own range is null, as in the
+            # host parser (_convert)
+            from ..engine.types import INT_RANGE
+            lo, hi = INT_RANGE[nd.dtype]
+            inr = (raw >= lo) & (raw <= hi)
+            cols[idx] = PrimColumn(nd.dtype, raw, inr if v is None else v & inr)
         else:
             cols[idx] = PrimColumn(nd.dtype, raw, v)
     kids = [(plan.nodes[j].name, cols[j]) for j in range(1, len(plan.nodes)) if plan.nodes[j].parent == 0 and j in cols]
@@ -477,10 +485,11 @@ def _convert(v, dtype):
     """Python JSON value → storage value for a leaf, or None (null / mismatch)."""
     if v is None:
         return None
-    if dtype in ("long", "int"):
+    if dtype in ("long", "int", "short", "byte"):
         if isinstance(v, bool) or not isinstance(v, int):
             return None
-        if dtype == "int" and not (-2**31 <= v < 2**31):
+        from ..engine.types import INT_RANGE
+        if not (INT_RANGE[dtype][0] <= v <= INT_RANGE[dtype][1]):
             return None
         if not (-2**63 <= v < 2**63):
             return None

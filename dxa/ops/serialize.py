@@ -121,7 +121,7 @@ class _Builder:
             if dt == "boolean":
                 nd["kind"] = K_BOOL
                 d = d.to(torch.uint8) if d.dtype == torch.bool else (d != 0).to(torch.uint8)
-            elif dt in ("int", "long"):
+            elif dt in ("byte", "short", "int", "long"):
                 nd["kind"] = K_I64
             elif dt == "timestamp":
                 nd["kind"] = K_TS
@@ -237,7 +237,7 @@ class _DevBuilder:
             if dt == "boolean":
                 nd["kind"] = K_BOOL
                 d = d.to(torch.uint8)
-            elif dt in ("int", "long"):
+            elif dt in ("byte", "short", "int", "long"):
                 nd["kind"] = K_I64
                 d = d.to(torch.int64)
             elif dt == "timestamp":

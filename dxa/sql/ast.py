@@ -23,7 +23,9 @@ class Expr:
 @dataclass(eq=False)
 class Literal(Expr):
     value: Any
-    type: str  # 'long' | 'int' | 'double' | 'string' | 'boolean' | 'null' | 'decimal'
+    type: str  # 'long' | 'int' | 'short' | 'byte' | 'double' | 'string' | 'boolean' | 'null' | decimal(p,s)
+    suffixed: bool = False      # typed by a suffix (10L, 10S, 10Y, 1.0D, 1BD): a folded minus keeps the type
+    integral: bool = False      # an unsuffixed integer literal (its type follows its value, the sign included)
 
     def key(self):
         return ("lit", self.type, self.value)
@@ -222,7 +224,7 @@ class Interval(Expr):
 @dataclass(eq=False)
 class SelectItem:
     expr: Expr
-    alias: Optional[str] = None
+    alias: Optional[str] = None      # a tuple of names: a generator's multi-alias ``AS (a, b)``
 
 
 @dataclass(eq=False)

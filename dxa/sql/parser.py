@@ -454,7 +454,15 @@ class Parser:
         e = self.parse_expr()
         alias = None
         if self.accept_kw("as"):
-            alias = self.ident()
+            if self.accept_op("("):
+                # multi-alias of a generator: stack(2, 1, 'a', 2, 'b') AS (x, y)
+                names = [self.ident()]
+                while self.accept_op(","):
+                    names.append(self.ident())
+                self.expect_op(")")
+                alias = tuple(names)
+            else:
+                alias = self.ident()
         elif self.cur.kind == "id":
             alias = self.advance().text
         return A.SelectItem(e, alias)
@@ -813,9 +821,17 @@ class Parser:
         if self.is_op("-"):
             self.advance()
             operand = self.parse_unary()
-            if isinstance(operand, A.Literal) and (operand.type in ("long", "int", "double")
+            if isinstance(operand, A.Literal) and operand.integral:
+                # Spark's grammar reads the minus into the literal (number: MINUS? INTEGER_VALUE), so the type is
+                # that of the negative value: -2147483648 is an INT, -9223372036854775808 a BIGINT
+                return _integer_literal(-int(operand.value))
+            if isinstance(operand, A.Literal) and (operand.type in ("long", "int", "short", "byte", "double")
                                                    or str(operand.type).startswith("decimal(")):
-                return A.Literal(-operand.value, operand.type)
+                from ..engine.types import INT_RANGE
+                if operand.type in INT_RANGE and not (INT_RANGE[operand.type][0] <= -operand.value
+                                                      <= INT_RANGE[operand.type][1]):
+                    self.error(f"numeric literal -{operand.value} does not fit in range of {operand.type}")
+                return A.Literal(-operand.value, operand.type, suffixed=operand.suffixed)
             return A.UnaryOp("-", operand)
         if self.accept_op("+"):
             return self.parse_unary()
@@ -950,7 +966,7 @@ class Parser:
                 return DecimalType(*(int(a) for a in args[:2])) if args else DecimalType(10, 0)
             except ValueError:
                 self.error(f"invalid decimal type {name}({', '.join(args)})")
-        return {"integer": "int", "bigint": "long", "smallint": "int", "tinyint": "int", "real": "float",
+        return {"integer": "int", "bigint": "long", "smallint": "short", "tinyint": "byte", "real": "float",
                 "varchar": "string", "char": "string", "text": "string", "bool": "boolean",
                 "numeric": "decimal", "dec": "decimal"}.get(name, name)
 
@@ -1173,19 +1189,41 @@ def _number_literal(text: str) -> A.Literal:
         return A.Literal(_pd.Decimal(text[:-2]), t)
     suffix = up[-1]
     if suffix in "LSY":
-        return A.Literal(int(text[:-1]), "long")
+        # 10L BIGINT, 10S SMALLINT, 10Y TINYINT (Spark: a value outside the type's range is a parse error)
+        from ..engine.types import INT_RANGE
+        t = {"L": "long", "S": "short", "Y": "byte"}[suffix]
+        v = int(text[:-1])
+        if not (INT_RANGE[t][0] <= v <= INT_RANGE[t][1] + 1):     # +1: the minus sign folds in afterwards
+            raise SqlError(f"numeric literal {text} does not fit in range of {t}")
+        return A.Literal(v, t, suffixed=True)
     if suffix == "D":
-        return A.Literal(float(text[:-1]), "double")
-    if "e" in text.lower():
-        return A.Literal(float(text), "double")
-    if "." in text:
-        # Spark: an unsuffixed fractional literal is an exact decimal of its own digits (over 38 digits: double)
+        return A.Literal(float(text[:-1]), "double", suffixed=True)
+    if "." in text or "e" in text.lower():
+        # Spark 2.4: an unsuffixed fractional or exponent literal (DECIMAL_VALUE) is an exact decimal of its own
+        # digits, BigDecimal(text); 1e20 is 10^20 as decimal(21,0) (Spark's decimal(1,-20) holds the same value);
+        # over 38 digits it is a double.  (Exponent literals became doubles only in Spark 3.0, SPARK-29956.)
         from ..engine.decimal import literal_type
         import decimal as _pd
         t = literal_type(text)
-        return A.Literal(_pd.Decimal(text), t) if t is not None else A.Literal(float(text), "double")
-    v = int(text)
-    return A.Literal(v, "int" if -2**31 <= v < 2**31 else "long")
+        if t is None:
+            return A.Literal(float(text), "double")
+        v = _pd.Decimal(text)
+        return A.Literal(v if t.scale else _pd.Decimal(int(v)), t)
+    return _integer_literal(int(text))
+
+
+def _integer_literal(v: int) -> A.Literal:
+    """Spark's visitIntegerLiteral: INT when the value fits, else BIGINT, else decimal(digits, 0)."""
+    if -2**31 <= v < 2**31:
+        return A.Literal(v, "int", integral=True)
+    if -2**63 <= v < 2**63:
+        return A.Literal(v, "long", integral=True)
+    from ..engine.decimal import DecimalType
+    import decimal as _pd
+    nd = len(str(abs(v)))
+    if nd > 38:
+        return A.Literal(float(v), "double")
+    return A.Literal(_pd.Decimal(v), DecimalType(nd, 0), integral=True)
 
 
 def parse_query(sql: str) -> A.Query:

@@ -36,6 +36,12 @@ EXPRS = [
     "d AND NULL",
     "d OR NULL",
     "c > 1e300 OR c < -1e300 OR c = c",
+    # Spark integer widths: INT / SMALLINT / TINYINT arithmetic wraps to its own width (two's complement)
+    "i + i > e OR i * 3 < 0",
+    "-i * 2 + h",
+    "h * h + t * t - 1",
+    "t + t + t",
+    "i + 1 < i AND h - 1 > h OR t * 2 = t + t",
 ]
 
 
@@ -46,6 +52,13 @@ def _table(n, seed, device):
         vals = [rnd.choice([0, 1, -1, 2, 3, 7, 40, -(1 << 63), (1 << 63) - 1, rnd.randint(-50, 50)]) for _ in range(n)]
         return PrimColumn("long", torch.tensor(vals, dtype=torch.int64, device=device),
                           torch.tensor([rnd.random() > 0.2 for _ in range(n)], device=device))
+
+    def narrow(t):
+        bits = {"int": 32, "short": 16, "byte": 8}[t]
+        lo, hi = -(1 << (bits - 1)), (1 << (bits - 1)) - 1
+        vals = [rnd.choice([lo, hi, lo + 1, hi - 1, 0, -1, 1, rnd.randint(lo, hi)]) for _ in range(n)]
+        return PrimColumn(t, torch.tensor(vals, dtype=torch.int64, device=device),
+                          torch.tensor([rnd.random() > 0.1 for _ in range(n)], device=device))
 
     c_vals = [rnd.choice([0.0, -0.0, 1.5, -2.25, float("nan"), float("inf"), 1e308, rnd.uniform(-3, 3)])
               for _ in range(n)]
@@ -60,6 +73,7 @@ def _table(n, seed, device):
         "e": PrimColumn("int", torch.tensor([rnd.randint(0, 200) for _ in range(n)], dtype=torch.int64,
                                             device=device)),
         "s": column_from_pylist([rnd.choice(["x", "y", None]) for _ in range(n)], "string", device),
+        "i": narrow("int"), "h": narrow("short"), "t": narrow("byte"),
     }
     names = list(cols)
     return Scope(names, [cols[k] for k in names], [None] * len(names), n, torch.device(device))
@@ -93,8 +107,12 @@ def test_host_codegen_matches_evaluator(sql):
     got = jit.try_fused(e, scope, ctx, None, evaluate, backend="host")
     if got is None:
         pytest.skip("not fused (too few operators)")
-    assert got.dtype == want.dtype or {got.dtype, want.dtype} <= {"int", "long"}
+    assert got.dtype == want.dtype
     assert _norm(got, n) == _norm(want, n), sql
+    from dxa.engine.types import INT_RANGE
+    if got.dtype in INT_RANGE:                      # every value inside its type's range
+        lo, hi = INT_RANGE[got.dtype]
+        assert all(v is None or lo <= v <= hi for v in _norm(got, n)), sql
 
 
 def test_string_subtree_is_an_input_column():
