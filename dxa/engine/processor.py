@@ -662,9 +662,8 @@ class Processor:
         (:297-305) and state tables write (:258-264), so a view that no output, accumulator or later live statement
         reads is never computed (the generated ``sa2_*`` copies, a ``Tagged`` view whose only consumers are the per-rule alert
         views, …), so skipping it changes no output.  Liveness runs backwards over the statements; a statement's
-        reads are over-approximated by every statement name appearing as a word in its text.  ``DXA_DEAD_VIEWS=0``
-        evaluates everything."""
-        if getattr(self, "_live", None) is not None or os.environ.get("DXA_DEAD_VIEWS", "1") == "0":
+        reads are over-approximated by every statement name appearing as a word in its text."""
+        if getattr(self, "_live", None) is not None:
             return getattr(self, "_live", None)
         import re
         cmds = self.transform.commands

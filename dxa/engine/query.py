@@ -968,6 +968,15 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     _, ok, items, aggs, cacheable, fp = plan_ent
     if not ok:
         return None
+    if cacheable:
+        # the dense ring (persistent group dictionary + per-pane accumulator rows in HBM, window_dense.py): one
+        # combine kernel and one status read per batch instead of concatenating and re-grouping partial tables
+        from .window_dense import dense_answer
+        with host_section("paned:dense"):
+            got = dense_answer(t, sel, alias, ctx, items, aggs, fp)
+        if got is not None:
+            out_keys, finals, ng, gexprs = got
+            return _paned_output(sel, items, out_keys, finals, ng, gexprs, proto.device, P.REPLICATED, ctx)
     state = {}
 
     def pane_partial(pane, full):
@@ -1047,6 +1056,12 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
         got, tag = D.exchange_partials(got, key_names, grouped)
     with host_section("paned:merge"):
         out_keys, finals, ng = D.merge_partials(got, plan, key_names, aggs, grouped)
+    return _paned_output(sel, items, out_keys, finals, ng, gexprs, dev, tag if grouped else P.REPLICATED, ctx)
+
+
+def _paned_output(sel, items, out_keys, finals, ng, gexprs, dev, tag, ctx) -> Table:
+    """The select list (and HAVING) over a window statement's groups: aggregates and group keys enter as
+    substitutions."""
     subst = dict(finals)
     for g, k in zip(gexprs, out_keys):
         subst[g.key()] = k
@@ -1055,7 +1070,7 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     out = Table([nm for _, nm in items], cols, ng, dev)
     if sel.having is not None:
         out = out.filter(predicate_mask(evaluate(sel.having, escope, ctx, subst)))
-    out.dist = tag if grouped else P.REPLICATED
+    out.dist = tag
     return out
 
 

@@ -1,0 +1,404 @@
+"""Dense sliding-window GROUP BY: a persistent device group dictionary + a ring of per-pane accumulator rows
+(``dxa/ops/csrc/window_ring.hip``).
+
+The reference answers a windowed statement by unioning the retained batches and running the GROUP BY over the union
+every batch (DataProcessing/datax-host/src/main/scala/datax/processor/CommonProcessorFactory.scala:156-236).  The
+paned path (``query._paned_aggregate``) already avoids re-reading the rows by caching per-pane partial tables, but
+it still concatenates ~40 partial tables and re-groups them every batch — host-side work that kept the 300-pane
+window flow host-bound.  Here the state a window needs lives in HBM in the shape the merge wants:
+
+* a **group dictionary** (open-addressed table of key hashes → dense group id, plus each group's key values in
+  fixed-width columns) that persists from batch to batch — a key seen once keeps its id for the life of the stream;
+* a **ring** of accumulator rows ``[ring slot][group][stride]`` (the fused multi-aggregate's layout), one slot per
+  retained pane; a pane is aggregated into its slot once, when it first enters a window;
+* per batch, one kernel combines the window's slots per (group, word), flags the groups with rows in the window and
+  compacts them; the host reads one 12-byte status (groups, collisions, output rows) — the statement's only
+  synchronisation — and builds the output columns as views of the dictionary and the finished aggregates.
+
+Eligible: GROUP BY statements whose aggregates are COUNT / SUM / MIN / MAX / AVG over non-decimal numeric,
+boolean or timestamp arguments, with plain key columns, deterministic, on a GPU, single rank (or a replicated
+window).  Anything else — and any batch whose dictionary reports a hash collision, an over-long string key or a full
+dictionary — is answered by the paned path, which stays the reference implementation (tests compare both).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional
+
+import torch
+
+from ..ops import native as N
+from ..ops.groupby import (_F_AVG, _F_COUNT, _F_F64, _F_F64_ORD, _F_I64, _F_NOT, _MA_ADD_F64, _MA_ADD_U64, _MA_MAX,
+                           _MV_COUNT, _MV_F64, _MV_F64_ORD, _MV_I64, _MV_NOT)
+from ..ops.hashing import MAX_KEY_COLS, _KeyCols, hash_columns, key_cols
+from .column import ConstColumn, PrimColumn, StrColumn, materialize
+from .decimal import is_decimal
+
+DENSE_GROUPS = 1 << 16            # dictionary capacity per statement (groups ever seen); more → paned path
+SCRATCH_SLOTS = 4                 # ring slots for panes only partly inside a window (re-aggregated every batch)
+_SUPPORTED = {"count", "sum", "min", "max", "avg", "mean"}
+
+N.register_sigs({
+    "dxa_win_sizes": [N.c_p],
+    "dxa_win_init": [N.c_p, N.c_p, N.c_i64, N.c_p],
+    "dxa_win_insert": [N.c_p, N.c_p, N.c_i64, N.c_p, N.c_i64, N.c_p, N.c_p, N.c_i32, N.c_p, N.c_p, N.c_p, N.c_p,
+                       N.c_p, N.c_p],
+    "dxa_win_combine": [N.c_p, N.c_i32, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_p, N.c_p, N.c_p, N.c_p],
+})
+
+
+class _DictCol(ctypes.Structure):
+    _fields_ = [("vals", ctypes.c_void_p), ("lens", ctypes.c_void_p), ("valid", ctypes.c_void_p),
+                ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class _DictCols(ctypes.Structure):
+    _fields_ = [("c", _DictCol * MAX_KEY_COLS), ("ncols", ctypes.c_int32), ("gcap", ctypes.c_int32)]
+
+
+_SIZES: Optional[List[int]] = None
+
+
+def _sizes() -> List[int]:
+    global _SIZES
+    if _SIZES is None:
+        out = (ctypes.c_int32 * 3)()
+        N.lib().dxa_win_sizes(out)
+        _SIZES = list(out)
+        if _SIZES[0] != ctypes.sizeof(_KeyCols) or _SIZES[1] != ctypes.sizeof(_DictCols):
+            raise N.NativeError("window_ring.hip struct layout differs from window_dense.py")
+    return _SIZES
+
+
+class Ineligible(Exception):
+    """The statement (or this batch) is answered by the paned path."""
+
+
+def _requests(aggs: Dict):
+    """[(agg key, func, arg expr or None)] or Ineligible."""
+    out = []
+    for ak, call in aggs.items():
+        name = call.name
+        if call.distinct or name not in _SUPPORTED:
+            raise Ineligible(name)
+        if call.star or (name == "count" and not call.args):
+            out.append((ak, "count_star", None))
+            continue
+        if len(call.args) != 1:
+            raise Ineligible(name)
+        out.append((ak, "avg" if name == "mean" else name, call.args[0]))
+    return out
+
+
+class DenseWindow:
+    """Persistent state of one windowed statement (one fingerprint) on one device."""
+
+    def __init__(self, device, reqs, ring_slots: int):
+        self.device = device
+        self.reqs = reqs
+        self.gcap = DENSE_GROUPS
+        self.R = ring_slots + SCRATCH_SLOTS
+        self.layout = None              # built from the first pane's evaluated argument types
+        self.slot_of: Dict[int, tuple] = {}     # pane key → (ring slot, id of the pane's table)
+        self.disabled = False
+        self._pinned = [torch.empty(self.R, dtype=torch.int32, pin_memory=True) for _ in range(4)]
+        self._pin_k = 0
+        cap = 1 << max(10, (2 * self.gcap - 1).bit_length())
+        self.hcap = cap
+        dev = device
+        self.htab = torch.empty(cap, dtype=torch.int64, device=dev)
+        self.gid_of_slot = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.scal = torch.zeros(4, dtype=torch.int32, device=dev)     # groups, bad flags, kept, pad
+        self.rep = torch.empty(self.gcap, dtype=torch.int32, device=dev)
+        self.stored = torch.zeros(self.gcap + 1, dtype=torch.uint8, device=dev)
+        N.call("dxa_win_init", N.ptr(self.htab), N.ptr(self.gid_of_slot), cap, N.stream_handle(dev))
+        self.keys = None                # dictionary key columns, built with the layout
+        self.ring = None
+
+    # ---- layout -------------------------------------------------------------------------------------------------
+    def _build_layout(self, key_cols_in: List, args: Dict):
+        kw = _sizes()[2]
+        dev = self.device
+        if not 1 <= len(key_cols_in) <= MAX_KEY_COLS:
+            raise Ineligible("key count")
+        dc = _DictCols()
+        keys = []
+        for j, k in enumerate(key_cols_in):
+            if isinstance(k, StrColumn):
+                vals = torch.zeros((self.gcap + 1) * kw, dtype=torch.uint8, device=dev)
+                lens = torch.zeros(self.gcap + 1, dtype=torch.int32, device=dev)
+                kind = 2
+            else:
+                vals = torch.zeros(self.gcap + 1, dtype=torch.int64, device=dev)
+                lens = None
+                kind = 1 if k.data.dtype == torch.float64 else 0
+            valid = torch.zeros(self.gcap + 1, dtype=torch.uint8, device=dev)
+            keys.append((k.dtype, kind, vals, lens, valid))
+            dc.c[j] = _DictCol(vals.data_ptr(), 0 if lens is None else lens.data_ptr(), valid.data_ptr(), kind, 0)
+        dc.ncols, dc.gcap = len(keys), self.gcap
+        self.keys, self.dictcols = keys, dc
+        # accumulator slots, packed into 8-word lines of one atomic kind (as groupby.aggregate_many packs them)
+        slots, keyed = [], {}
+
+        def slot(key, kind, op):
+            s = keyed.get(key)
+            if s is None:
+                s = keyed[key] = len(slots)
+                slots.append((key, kind, op))
+            return s
+
+        star = slot(("count", None), _MV_COUNT, _MA_ADD_F64)
+        plan = []
+        for ak, func, arg in self.reqs:
+            if func == "count_star":
+                plan.append((ak, "count", star, None, None))
+                continue
+            col = args[arg.key()]
+            ck = arg.key()
+            cnt = slot(("count", ck), _MV_COUNT, _MA_ADD_F64)
+            if func == "count":
+                plan.append((ak, "count", cnt, None, None))
+                continue
+            is_f = col.data.dtype == torch.float64
+            if func == "avg":
+                plan.append((ak, "avg", slot(("sumf", ck), _MV_F64, _MA_ADD_F64), cnt, "double"))
+            elif func == "sum":
+                if col.dtype not in ("byte", "short", "int", "long", "double", "float"):
+                    raise Ineligible("sum type")
+                plan.append((ak, "sum", slot(("sum", ck), _MV_F64 if is_f else _MV_I64,
+                                             _MA_ADD_F64 if is_f else _MA_ADD_U64), cnt,
+                             "double" if is_f else "long"))
+            else:
+                kind = (_MV_F64_ORD if is_f else _MV_I64) | (_MV_NOT if func == "min" else 0)
+                plan.append((ak, "f64" if is_f else "i64", slot((func, ck), kind, _MA_MAX), cnt, col.dtype))
+        order, line_ops = [], []
+        for op in (_MA_ADD_U64, _MA_ADD_F64, _MA_MAX):
+            mine = [i for i, sl in enumerate(slots) if sl[2] == op]
+            for k in range(0, len(mine), 8):
+                chunk = mine[k:k + 8]
+                line_ops.append(op)
+                order.extend(chunk + [None] * (8 - len(chunk)))
+        if len(order) > 64 or len(plan) > 64:
+            raise Ineligible("too many aggregates")
+        where = {i: pos for pos, i in enumerate(order) if i is not None}
+        nslots = len(order)
+        while nslots and order[nslots - 1] is None:
+            nslots -= 1
+        fin = []
+        for ak, kind, s, c, dt in plan:
+            if kind == "count":
+                fin.append((_F_COUNT, where[s], -1))
+            elif kind == "avg":
+                fin.append((_F_AVG, where[s], where[c]))
+            elif kind == "sum":
+                fin.append((_F_F64 if dt == "double" else _F_I64, where[s], where[c]))
+            else:
+                k = (_F_F64_ORD if kind == "f64" else _F_I64) | (_F_NOT if slots[s][1] & _MV_NOT else 0)
+                fin.append((k, where[s], where[c]))
+        self.stride = 8 * len(line_ops)
+        self.layout = dict(slots=slots, order=order, nslots=nslots, line_ops=line_ops, plan=plan,
+                           count_word=where[star], fspec=torch.tensor([x for f in fin for x in f], dtype=torch.int32))
+        self.line_ops_t = torch.tensor(line_ops, dtype=torch.int32)
+        self.line_ops_dev = self.line_ops_t.to(dev)
+        rows = self.gcap + 1
+        self.ring = torch.empty((self.R, rows * self.stride), dtype=torch.int64, device=dev)
+        self.acc = torch.zeros(rows * self.stride, dtype=torch.int64, device=dev)
+        self.keep = torch.empty(self.gcap, dtype=torch.uint8, device=dev)
+        self.out_idx = torch.empty(self.gcap, dtype=torch.int64, device=dev)
+
+    # ---- one pane into one ring slot ----------------------------------------------------------------------------
+    def accumulate(self, table, slot_idx: int, alias, where, gexprs, ctx):
+        from .expr import Scope, evaluate, predicate_mask
+        scope = Scope.of_table(table, alias)
+        n = scope.length
+        keep = None
+        if where is not None:
+            keep = N.u8(predicate_mask(evaluate(where, scope, ctx)).contiguous())
+        keys = []
+        for g in gexprs:
+            k = materialize(evaluate(g, scope, ctx))
+            if isinstance(k, PrimColumn):
+                if is_decimal(k.dtype) or k.data.dim() != 1:
+                    raise Ineligible("key type")
+                if k.data.dtype == torch.bool:
+                    k = PrimColumn(k.dtype, k.data.to(torch.int64), k.valid)
+                elif k.data.dtype not in (torch.int64, torch.float64):
+                    k = PrimColumn(k.dtype, k.data.to(torch.int64), k.valid)
+            elif not isinstance(k, StrColumn) or type(k) is not StrColumn:
+                raise Ineligible("key type")
+            keys.append(k)
+        args = {}
+        for _, func, arg in self.reqs:
+            if arg is None or arg.key() in args:
+                continue
+            c = evaluate(arg, scope, ctx)
+            if isinstance(c, ConstColumn):
+                c = c.materialize()
+            if not isinstance(c, PrimColumn) or is_decimal(c.dtype) or c.data.dim() != 1:
+                raise Ineligible("argument type")
+            args[arg.key()] = c
+        if self.layout is None:
+            self._build_layout(keys, args)
+        else:
+            for (dt, kind, *_), k in zip(self.keys, keys):
+                if (kind == 2) != isinstance(k, StrColumn) or str(dt) != str(k.dtype):
+                    raise Ineligible("key types changed")
+        L = self.layout
+        dev = self.device
+        st = N.stream_handle(dev)
+        kc = key_cols(keys)
+        if kc is None:
+            raise Ineligible("key columns")
+        kc.ncols, kc.n = len(keys), n
+        h = hash_columns(keys) if n else torch.empty(0, dtype=torch.int64, device=dev)
+        gid = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        N.call("dxa_win_insert", N.ptr(h), N.ptr(keep), n, N.ptr(self.htab), self.hcap, N.ptr(self.gid_of_slot),
+               N.ptr(self.scal), self.gcap, N.ptr(gid), N.ptr(self.rep), ctypes.addressof(kc),
+               ctypes.addressof(self.dictcols), N.ptr(self.stored), st)
+        spec, hold = [], [h, gid, keep, kc]
+        for i in L["order"][:L["nslots"]]:
+            if i is None:
+                spec += [0, 0, -1]
+                continue
+            key, kind, _op = L["slots"][i]
+            if key[1] is None:
+                spec += [0, 0, kind]
+                continue
+            c = args[key[1]]
+            d = c.data
+            if key[0] == "sumf" or (kind & 3) in (_MV_F64, _MV_F64_ORD):
+                d = d.to(torch.float64)
+            elif d.dtype != torch.int64:
+                d = d.to(torch.int64)
+            d = d.contiguous()
+            v = N.u8(c.valid)
+            hold += [d, v]
+            spec += [0 if key[0] == "count" else d.data_ptr(), 0 if v is None else v.contiguous().data_ptr(), kind]
+        spec_t = torch.tensor(spec, dtype=torch.int64)
+        ring_ptr = self.ring[slot_idx].data_ptr()
+        N.call("dxa_aggregate_multi", N.ptr(gid), n, self.gcap + 1, L["nslots"], spec_t.data_ptr(),
+               len(L["line_ops"]), self.line_ops_t.data_ptr(), ring_ptr, st)
+        del hold
+
+    # ---- the window's answer --------------------------------------------------------------------------------------
+    def answer(self, slots: List[int]):
+        """Combine ``slots`` → (key columns, {agg key → column}, groups) or None (fall back: collision / full)."""
+        L = self.layout
+        dev = self.device
+        st = N.stream_handle(dev)
+        pin = self._pinned[self._pin_k]
+        self._pin_k = (self._pin_k + 1) % len(self._pinned)
+        pin[:len(slots)] = torch.tensor(slots, dtype=torch.int32)
+        slots_dev = pin[:len(slots)].to(dev, non_blocking=True)
+        N.call("dxa_win_combine", N.ptr(self.ring), self.gcap, self.stride, N.ptr(slots_dev), len(slots),
+               N.ptr(self.line_ops_dev), L["count_word"], N.ptr(self.scal), N.ptr(self.acc), N.ptr(self.keep),
+               N.ptr(self.out_idx), st)
+        ng_all, bad, nout, _ = self.scal.tolist()          # the statement's one synchronising read
+        if bad:
+            return None
+        idx = self.out_idx[:nout]
+        kw = _sizes()[2]
+        out_keys = []
+        for dt, kind, vals, lens, valid in self.keys:
+            v = valid[idx].view(torch.bool)
+            if kind == 2:
+                out_keys.append(StrColumn(vals, idx * kw, lens[idx], v))
+            else:
+                d = vals[idx]
+                if kind == 1:
+                    d = d.view(torch.float64)
+                elif dt == "boolean":
+                    d = d.to(torch.bool)
+                out_keys.append(PrimColumn(dt, d, v))
+        accs = self.acc.view(self.gcap + 1, self.stride)[idx].contiguous()
+        nreq = len(L["plan"])
+        dst = torch.empty((nreq, max(nout, 1)), dtype=torch.int64, device=dev)
+        dvalid = torch.empty((nreq, max(nout, 1)), dtype=torch.uint8, device=dev)
+        if nout:
+            N.call("dxa_aggregate_finish", N.ptr(accs), nout, self.stride, nreq, L["fspec"].data_ptr(), N.ptr(dst),
+                   N.ptr(dvalid), st)
+        finals = {}
+        for j, (ak, kind, s, c, dt) in enumerate(L["plan"]):
+            v = dst[j, :nout]
+            ok = dvalid[j, :nout].view(torch.bool)
+            if kind == "count":
+                finals[ak] = PrimColumn("long", v)
+            elif kind == "avg":
+                finals[ak] = PrimColumn("double", v.view(torch.float64), ok)
+            elif kind == "sum":
+                finals[ak] = PrimColumn(dt, v.view(torch.float64) if dt == "double" else v, ok)
+            elif kind == "f64":
+                finals[ak] = PrimColumn(dt, v.view(torch.float64), ok)
+            else:
+                finals[ak] = PrimColumn(dt, v.to(torch.bool) if dt == "boolean" else v, ok)
+        return out_keys, finals, nout
+
+
+def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str):
+    """The window statement's (key columns, finals, groups, group exprs) from the dense ring, or None."""
+    from .. import parallel as P
+    from .query import _resolve_group_expr
+    from .expr import Scope
+    store = t.store
+    dev = t._device
+    if dev.type != "cuda" or not sel.group_by or (P.active() and t.dist != P.REPLICATED):
+        return None
+    states = store.__dict__.setdefault("_dense", {})
+    state = states.get(fp)
+    if state is not None and state.disabled:
+        return None
+    pieces = t.pieces()
+    if not pieces:
+        return None
+    try:
+        if state is None:
+            iv = max(1, store.interval_us)
+            panes = store.conf.max_window_us // iv + store.conf.watermark_us // iv + 4
+            state = states[fp] = DenseWindow(dev, _requests(aggs), max(panes, len(pieces) + 2))
+        proto = pieces[0][0].table
+        gexprs = [_resolve_group_expr(g, Scope.of_table(proto, alias), items) for g in sel.group_by]
+        # ring slots: keep the slots of retained panes, recycle the rest
+        live = {p.key for p, _ in pieces} | set(store.past)
+        for k in [k for k in state.slot_of if k not in live]:
+            del state.slot_of[k]
+        used = {s for s, _ in state.slot_of.values()}
+        free = [s for s in range(state.R - SCRATCH_SLOTS) if s not in used]
+        scratch = list(range(state.R - SCRATCH_SLOTS, state.R))
+        slots = []
+        for pane, full in pieces:
+            if full and pane.all_valid:
+                ent = state.slot_of.get(pane.key)
+                if ent is None or ent[1] != id(pane.table):
+                    if not free:
+                        raise Ineligible("ring full")
+                    s = free.pop(0)
+                    state.accumulate(pane.table, s, alias, sel.where, gexprs, ctx)
+                    state.slot_of[pane.key] = (s, id(pane.table))
+                    ent = state.slot_of[pane.key]
+                slots.append(ent[0])
+            else:
+                # a pane only partly inside the window: its in-range rows, re-aggregated into a scratch slot
+                if not scratch:
+                    raise Ineligible("too many clipped panes")
+                s = scratch.pop(0)
+                state.accumulate(t.clipped(pane), s, alias, sel.where, gexprs, ctx)
+                slots.append(s)
+        got = state.answer(slots)
+    except Ineligible:
+        state = states.get(fp)
+        if state is not None:
+            state.disabled = True
+            state.ring = state.acc = None
+        else:
+            states[fp] = _Disabled()
+        return None
+    if got is None:
+        state.disabled = True
+        state.ring = state.acc = None
+        return None
+    out_keys, finals, ng = got
+    return out_keys, finals, ng, gexprs
+
+
+class _Disabled:
+    disabled = True

@@ -171,8 +171,7 @@ def ptr(t) -> int:
     return t.data_ptr()
 
 
-_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None) if os.environ.get("DXA_RAW_STREAM", "1") != "0" \
-    else None
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def stream_handle(device=None) -> int:

@@ -426,7 +426,7 @@ def _close_group(ms: List["Staged"]) -> None:
             m.group = g
 
 
-_SDMA = os.environ.get("DXA_D2H_SDMA", "1") != "0"
+_SDMA = True                 # SDMA engine for the rendered-output D2H; off for good after a failed copy
 
 
 def d2h(host: torch.Tensor, dev: torch.Tensor, nbytes: int, stream) -> None:
@@ -468,7 +468,7 @@ def _side_stream(device):
 
 
 def gpu_serializer_enabled(device) -> bool:
-    if device.type != "cuda" or os.environ.get("DXA_GPU_SERIALIZE", "1") == "0":
+    if device.type != "cuda":
         return False
     try:
         from . import native
@@ -488,7 +488,7 @@ class Staged:
         self.n = table.length
         self.event = None
         self.gpu = gpu_serializer_enabled(table.device)
-        self.compress = compress and self.gpu and os.environ.get("DXA_GPU_GZIP", "1") != "0"
+        self.compress = compress and self.gpu
         self.group = None
         self._result = None
         if self.gpu:

@@ -154,8 +154,9 @@ def split_by_destination(dest: torch.Tensor, world: int):
 
 
 def _force_torch() -> bool:
-    import os
-    return os.environ.get("DXA_XCHG_TORCH") == "1"
+    """The torch reference implementation of the exchange wire format runs only where the device kernels cannot
+    (CPU tensors); ``packing`` picks it by device, this flag never forces it on a GPU."""
+    return False
 
 
 def shuffle_table(table, dest: torch.Tensor):
@@ -165,8 +166,7 @@ def shuffle_table(table, dest: torch.Tensor):
     sizes and ONE host read-back of sent and received sizes → scatter (matrix + string arenas, destination-ordered)
     → one all-to-all of the matrix and ONE of every string leaf's bytes (coalesced, destination-major) → one
     unpack launch.  Three kernel launches on the send
-    side and one on the receive side, however many columns the table has.  ``DXA_XCHG_TORCH=1`` runs the torch
-    reference implementation of the same wire format."""
+    side and one on the receive side, however many columns the table has."""
     from . import packing as PK
     W = _w()
     device = table.device

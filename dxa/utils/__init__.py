@@ -149,13 +149,7 @@ def settle_gc(gen0_threshold: int = 20_000) -> bool:
     wrappers, reference tables' Python shells) to the permanent generation and raise the young-generation
     threshold.  A micro-batch allocates thousands of short-lived Python objects; with the default threshold
     (700) the collector runs many times per batch, and a full collection re-scans the whole start-up heap, which
-    shows as a multi-millisecond outlier in ``Latency-Process``.  ``DXA_GC_TUNE=0`` leaves the collector alone."""
-    sw = os.environ.get("DXA_SWITCH_INTERVAL_MS")
-    if sw:
-        import sys
-        sys.setswitchinterval(float(sw) / 1e3)
-    if os.environ.get("DXA_GC_TUNE", "1") == "0":
-        return False
+    shows as a multi-millisecond outlier in ``Latency-Process`` (profiles/gc/)."""
     gc.collect()
     gc.freeze()
     t0, t1, t2 = gc.get_threshold()

@@ -396,11 +396,13 @@ def test_device_decodes_pyarrow_frames(gpu, level):
         out = torch.zeros(opos + 64, dtype=torch.uint8, device=gpu)
         produced = torch.zeros(n, dtype=torch.int64, device=gpu)
         status = torch.full((n,), -1, dtype=torch.int32, device=gpu)
-        N.call(entry, N.ptr(src.to(gpu)), N.ptr(dev(co, torch.int64)), N.ptr(dev([len(c) for c in comp], torch.int32)),
-               N.ptr(dev([kind] * n, torch.uint8)), N.ptr(dev(oo, torch.int64)),
-               N.ptr(dev([len(d) for d in datas], torch.int64)), n, N.ptr(out), N.ptr(produced), N.ptr(status),
-               N.stream_handle(gpu))
+        # every operand held in a name until the launch has run (a temporary's block could be reused by the next
+        # allocation before the kernel reads it)
+        ops = [src.to(gpu), dev(co, torch.int64), dev([len(c) for c in comp], torch.int32), dev([kind] * n, torch.uint8),
+               dev(oo, torch.int64), dev([len(d) for d in datas], torch.int64)]
+        N.call(entry, *[N.ptr(x) for x in ops], n, N.ptr(out), N.ptr(produced), N.ptr(status), N.stream_handle(gpu))
         torch.cuda.synchronize(gpu)
+        del ops
         assert status.tolist() == [0] * n, (codec, status.tolist())
         assert produced.tolist() == [len(d) for d in datas]
         o = out.cpu().numpy().tobytes()

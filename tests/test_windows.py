@@ -88,3 +88,38 @@ def test_window_ranges_and_eviction():
         assert views["W4"].length == min(3, b)
         assert views["DataXProcessedInput_Batch"].length == 2
     assert len(store.past) <= 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spread,nb,win", [(S - 1, 40, 9), (3 * S, 24, 5)])
+def test_dense_ring_matches_materialized(spread, nb, win):
+    """The dense window path (window_dense.py / window_ring.hip: persistent group dictionary + per-pane accumulator
+    ring) answers the decomposable window statements on the GPU; its rows equal the materialized window's batch
+    after batch — through ring-slot reuse after evictions, clipped panes (re-aggregated into scratch slots) when the
+    event times straddle the window edges, NULL arguments and a WHERE."""
+    import numpy as np
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    conf = TimeWindowConf({"W": win * S}, True, "ts", 2 * S, win * S, False)
+    store = WindowStore(conf)
+    ctx = EvalContext(now_us=0, device=dev)
+    qs = [QUERIES[0], "SELECT kind, deviceId, MAX(ts) AS last, MIN(deviceId) AS lo, COUNT(temp) AS ct, "
+                      "SUM(deviceId) AS sd FROM W WHERE temp > 18 GROUP BY kind, deviceId",
+          "SELECT deviceId % 2 AS parity, SUM(deviceId) AS s FROM W GROUP BY deviceId % 2 HAVING COUNT(*) > 2"]
+    for b in range(nb):
+        T = (100 + b) * S
+        views, _ = store.process(batch(rng, T, 300, spread).to(dev), T, S)
+        for q in qs:
+            cat = Catalog()
+            cat.register("W", views["W"])
+            paned = run_sql(q, cat, ctx)
+            mat = Table(views["W"].names, views["W"].columns, views["W"].length, dev)
+            cat2 = Catalog()
+            cat2.register("W", mat)
+            ref = run_sql(q, cat2, ctx)
+            assert _canon(paned) == _canon(ref), (b, q)
+    dense = store.__dict__.get("_dense", {})
+    assert len(dense) == len(qs) and not any(d.disabled for d in dense.values())
+    # the ring only ever holds retained panes
+    for d in dense.values():
+        assert len(d.slot_of) <= len(store.past) + 1

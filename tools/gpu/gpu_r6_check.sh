@@ -1,0 +1,8 @@
+# targeted round-6 GPU tests, then the whole GPU suite, smoke and the flows; OUT=<dir under gpurun_out>
+set -o pipefail
+O=gpurun_out/${OUT:-r6check}
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu ${TESTS:-tests/test_windows.py tests/test_kafka_codecs.py tests/test_spark_int_widths.py tests/test_jit.py} > $O/targeted.log 2>&1 || { tail -60 $O/targeted.log; exit 1; }
+tail -2 $O/targeted.log
+[ -n "$QUICK" ] && exit 0
+OUT=${OUT:-r6check} bash tools/gpu/gpu_baseline.sh
