@@ -133,12 +133,9 @@ def _plan_take(c: "Column", idx: torch.Tensor, leaves: List[torch.Tensor]):
         if c.valid is not None:
             leaves.append(c.valid)
         has_v = c.valid is not None
-        ip = len(leaves)
-        has_p = False
         els = [_plan_take(e, idx, leaves) for e in c.elements]
         n = int(idx.shape[0])
-        return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device,
-                                     present=g[ip] if has_p else None)
+        return lambda g: ArrayColumn([b(g) for b in els], n, g[i] if has_v else None, c.drop_nulls, c.device)
     taken = c.take(idx)                       # constants and other kinds: their own take
     return lambda g: taken
 

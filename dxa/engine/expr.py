@@ -1641,16 +1641,23 @@ def _f_round(e, scope, ctx, subst):
     ax = x.abs()
     # (divisions through D.true_div: the GPU's scalar division is a reciprocal multiply, an ulp off at the ties)
     if digits >= 0:
-        sc = 10.0 ** digits
-        f = torch.floor(ax * sc)
+        sc = 10.0 ** digits if digits <= 308 else float("inf")
+        scaled = ax * sc
+        f = torch.floor(scaled)
         t = D.true_div(2 * f + 1, 2 * sc)
     else:
-        sc = 10.0 ** (-digits)
+        sc = 10.0 ** (-digits) if digits >= -308 else float("inf")
         f = torch.floor(D.true_div(ax, sc))
         t = (2 * f + 1) * sc / 2
     tie_up = (torch.remainder(f, 2) == 1) if half_even else torch.ones_like(ax, dtype=torch.bool)
     r = f + ((ax > t) | ((ax == t) & tie_up)).to(torch.float64)
     res = torch.sign(x) * (D.true_div(r, sc) if digits >= 0 else r * sc)
+    if digits >= 0:
+        # |x|·10^d beyond 2^53 (or overflowing): x has no digits below 10^-d, so BigDecimal(x).setScale(d) is x
+        keep = ~torch.isfinite(scaled) | (scaled >= 2.0 ** 53)
+        res = torch.where(keep, x, res)
+    elif sc == float("inf"):
+        res = torch.zeros_like(x)                                 # rounded left of every digit a double has
     res = torch.where(torch.isfinite(x), res, x)                  # NaN / ±Infinity pass through
     rt = "float" if a.dtype == "float" else "double"
     if rt == "float":
@@ -2018,9 +2025,15 @@ def _window_sql(w: A.WindowCall) -> str:
     if name in _RANKING_FNS:
         parts.append("ROWS BETWEEN UNBOUNDED PRECEDING AND CURRENT ROW")
     elif name in ("lag", "lead"):
-        k = output_name(w.func.args[1]) if len(w.func.args) > 1 else "1"
-        k = f"-{k}" if name == "lag" else k
-        bound = f"{k} {'PRECEDING' if name == 'lag' else 'FOLLOWING'}"
+        # OffsetWindowFunction.frame: lag's boundary is UnaryMinus(offset) folded to a literal, and
+        # SpecifiedWindowFrame.boundarySql prints any non-UnaryMinus boundary as "<value> FOLLOWING"
+        a = w.func.args[1] if len(w.func.args) > 1 else None
+        k = 1 if a is None else (int(a.value) if isinstance(a, A.Literal) and isinstance(a.value, int) else None)
+        if k is None:
+            k_txt = output_name(a) if a is not None else "1"
+            bound = f"{k_txt} PRECEDING" if name == "lag" else f"{k_txt} FOLLOWING"
+        else:
+            bound = f"{-k if name == 'lag' else k} FOLLOWING"
         parts.append(f"ROWS BETWEEN {bound} AND {bound}")
     elif w.frame is not None:
         kind, lo, hi = w.frame
@@ -2052,7 +2065,12 @@ def output_name(e: A.Expr) -> str:
             return F.java_double_str(e.value)
         return str(e.value)
     if isinstance(e, A.WindowCall):
-        return f"{output_name(e.func)} OVER {_window_sql(e)}"
+        f = e.func
+        if f.name in ("lag", "lead") and 1 <= len(f.args) < 3:
+            # Spark prints the defaulted arguments: lag(x) → lag(x, 1, NULL)
+            f = A.Call(f.name, list(f.args) + [A.Literal(1, "int"), A.Literal(None, "null")][len(f.args) - 1:],
+                       f.distinct, f.star)
+        return f"{output_name(f)} OVER {_window_sql(e)}"
     if isinstance(e, A.Call):
         name = _PRETTY_FN.get(e.name, e.name)
         if e.star:
@@ -2066,7 +2084,7 @@ def output_name(e: A.Expr) -> str:
         return f"CAST({output_name(e.operand)} AS {_type_sql(e.to)})"
     if isinstance(e, A.BinOp):
         op = e.op.upper() if e.op in ("and", "or", "div") else e.op
-        op = "=" if op == "==" else ("NOT (" if False else op)
+        op = "=" if op == "==" else op
         if e.op in ("!=", "<>"):
             return f"(NOT ({output_name(e.left)} = {output_name(e.right)}))"
         return f"({output_name(e.left)} {op} {output_name(e.right)})"

@@ -17,8 +17,6 @@ from .column import (ArrayColumn, Column, ConstColumn, JsonColumn, PrimColumn, S
                      datetime_to_us)
 from .types import ArrayType, MapType, StructType
 
-_ESC = json.encoder.ESCAPE_ASCII if False else None
-
 
 def _jstr(s: str) -> str:
     return json.dumps(s, ensure_ascii=False)

@@ -2087,7 +2087,7 @@ def _f_encode(e, scope, ctx, subst):
         elif py == "utf-16":
             out.append(b"\xfe\xff" + str(v).encode("utf-16-be"))
         else:
-            out.append(str(v).encode(py, errors="replace").replace(b"\\ufffd", b"?"))
+            out.append(str(v).encode(py, errors="replace"))
     return _binary_column(out, scope.device)
 
 

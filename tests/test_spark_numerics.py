@@ -182,3 +182,13 @@ def test_array_literals_in_array_contains_and_if(device):
     assert types[1:5] == ["boolean", "boolean", "array<int>", "int"]
     assert rows[0] == (1, True, True, [2, 3], 2, "[2,null]", -1)
     assert rows[-1] == (3, True, False, [1], 1, "[1]", 1)
+
+
+@pytest.mark.parametrize("device", DEV)
+def test_round_of_huge_doubles_is_identity(device):
+    """round(x, d) on a double whose |x|·10^d passes 2^53 (or overflows) is x: BigDecimal(x).setScale(d) keeps a
+    value with no digits below 10^-d (the scaled form must not become ±Infinity or NaN); far left of every digit the
+    result is 0.0."""
+    _, _, rows = q("SELECT round(1e300D, 10) a, round(1.5e300D, 400) b, round(123.456D, -400) c, "
+                   "round(-1e300D, 2) d, bround(9007199254740993D, 1) e FROM T", _dev(device))
+    assert rows[0] == (1e300, 1.5e300, 0.0, -1e300, 9007199254740992.0)

@@ -239,3 +239,16 @@ def test_range_interval_offsets_over_timestamps():
     assert [(g["x"], g["s"]) for g in got] == [(1, 1), (2, 3), (3, 6), (4, 4), (5, 9)]
     with pytest.raises(Exception):
         q(c, "SELECT sum(x) OVER (ORDER BY ts, x RANGE BETWEEN 1 PRECEDING AND CURRENT ROW) AS s FROM E")
+
+
+def test_lag_lead_generated_names_spark24():
+    """Un-aliased lag / lead columns are named as Spark 2.4 names them: the defaulted offset and default printed
+    (``lag(v, 1, NULL)``) and the frame from OffsetWindowFunction — lag's boundary is the folded literal -offset,
+    printed by boundarySql as ``-1 FOLLOWING`` (a computed expression, not a literal, from the reference's Spark;
+    parity unpinned by any reference fixture)."""
+    out = run_sql("SELECT lag(v) OVER (PARTITION BY k ORDER BY id), lead(v) OVER (ORDER BY id), "
+                  "lag(v, 2, 0) OVER (ORDER BY id) FROM T", _cat(ROWS), EvalContext())
+    assert out.names == [
+        "lag(v, 1, NULL) OVER (PARTITION BY k ORDER BY id ASC NULLS FIRST ROWS BETWEEN -1 FOLLOWING AND -1 FOLLOWING)",
+        "lead(v, 1, NULL) OVER (ORDER BY id ASC NULLS FIRST ROWS BETWEEN 1 FOLLOWING AND 1 FOLLOWING)",
+        "lag(v, 2, 0) OVER (ORDER BY id ASC NULLS FIRST ROWS BETWEEN -2 FOLLOWING AND -2 FOLLOWING)"]
