@@ -968,15 +968,25 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
     _, ok, items, aggs, cacheable, fp = plan_ent
     if not ok:
         return None
-    if cacheable:
+    if cacheable and sel.group_by:
         # the dense ring (persistent group dictionary + per-pane accumulator rows in HBM, window_dense.py): one
         # combine kernel and one status read per batch instead of concatenating and re-grouping partial tables
-        from .window_dense import dense_answer
-        with host_section("paned:dense"):
-            got = dense_answer(t, sel, alias, ctx, items, aggs, fp)
-        if got is not None:
-            out_keys, finals, ng, gexprs = got
-            return _paned_output(sel, items, out_keys, finals, ng, gexprs, proto.device, P.REPLICATED, ctx)
+        from .window_dense import dense_answer, dense_partials
+        if P.active() and t.dist != P.REPLICATED:
+            with host_section("paned:dense"):
+                got = dense_partials(t, sel, alias, ctx, items, aggs, fp, empty)
+            if got is not None:
+                partial, plan, key_names, gexprs = got
+                got, tag = D.exchange_partials(partial, key_names, True)
+                with host_section("paned:merge"):
+                    out_keys, finals, ng = D.merge_partials(got, plan, key_names, aggs, True)
+                return _paned_output(sel, items, out_keys, finals, ng, gexprs, proto.device, tag, ctx)
+        else:
+            with host_section("paned:dense"):
+                got = dense_answer(t, sel, alias, ctx, items, aggs, fp)
+            if got is not None:
+                out_keys, finals, ng, gexprs = got
+                return _paned_output(sel, items, out_keys, finals, ng, gexprs, proto.device, P.REPLICATED, ctx)
     state = {}
 
     def pane_partial(pane, full):

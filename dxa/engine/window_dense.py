@@ -16,8 +16,9 @@ window flow host-bound.  Here the state a window needs lives in HBM in the shape
   synchronisation — and builds the output columns as views of the dictionary and the finished aggregates.
 
 Eligible: GROUP BY statements whose aggregates are COUNT / SUM / MIN / MAX / AVG over non-decimal numeric,
-boolean or timestamp arguments, with plain key columns, deterministic, on a GPU, single rank (or a replicated
-window).  Anything else — and any batch whose dictionary reports a hash collision, an over-long string key or a full
+boolean or timestamp arguments, with plain key columns, deterministic, on a GPU.  With N ranks each rank's window
+comes out of its ring as a partial table of ``distagg.local_partials``' layout and goes through the same key
+exchange and merge as the paned path (``dense_partials``).  Anything else — and any batch whose dictionary reports a hash collision, an over-long string key or a full
 dictionary — is answered by the paned path, which stays the reference implementation (tests compare both).
 """
 from __future__ import annotations
@@ -196,8 +197,20 @@ class DenseWindow:
                 k = (_F_F64_ORD if kind == "f64" else _F_I64) | (_F_NOT if slots[s][1] & _MV_NOT else 0)
                 fin.append((k, where[s], where[c]))
         self.stride = 8 * len(line_ops)
+        # partial states per aggregate (distagg._partials' suffixes): "cnt" a count, "v" the SUM / MIN / MAX value,
+        # "s" AVG's raw double sum
+        pfin = {}
+        for ak, kind, s, c, dt in plan:
+            if kind == "count":
+                pfin[ak] = {"cnt": (_F_COUNT, where[s], -1)}
+            elif kind == "avg":
+                pfin[ak] = {"s": (_F_F64, where[s], where[c]), "cnt": (_F_COUNT, where[c], -1)}
+            else:
+                pfin[ak] = {"v": fin[len(pfin)], "cnt": (_F_COUNT, where[c], -1)}
+        self.stride = 8 * len(line_ops)
         self.layout = dict(slots=slots, order=order, nslots=nslots, line_ops=line_ops, plan=plan,
-                           count_word=where[star], fspec=torch.tensor([x for f in fin for x in f], dtype=torch.int32))
+                           count_word=where[star], fspec=torch.tensor([x for f in fin for x in f], dtype=torch.int32),
+                           pfin=pfin)
         self.line_ops_t = torch.tensor(line_ops, dtype=torch.int32)
         self.line_ops_dev = self.line_ops_t.to(dev)
         rows = self.gcap + 1
@@ -281,8 +294,10 @@ class DenseWindow:
         del hold
 
     # ---- the window's answer --------------------------------------------------------------------------------------
-    def answer(self, slots: List[int]):
-        """Combine ``slots`` → (key columns, {agg key → column}, groups) or None (fall back: collision / full)."""
+    def answer(self, slots: List[int], partial_proto=None):
+        """Combine ``slots`` → (key columns, {agg key → column}, groups) or None (fall back: collision / full).
+        With ``partial_proto`` (an empty partial table of ``distagg.local_partials``' layout, and its plan) the
+        result is instead this rank's window as a partial table of exactly that layout, for the key exchange."""
         L = self.layout
         dev = self.device
         st = N.stream_handle(dev)
@@ -311,6 +326,8 @@ class DenseWindow:
                     d = d.to(torch.bool)
                 out_keys.append(PrimColumn(dt, d, v))
         accs = self.acc.view(self.gcap + 1, self.stride)[idx].contiguous()
+        if partial_proto is not None:
+            return self._partials(accs, out_keys, nout, *partial_proto)
         nreq = len(L["plan"])
         dst = torch.empty((nreq, max(nout, 1)), dtype=torch.int64, device=dev)
         dvalid = torch.empty((nreq, max(nout, 1)), dtype=torch.uint8, device=dev)
@@ -334,14 +351,76 @@ class DenseWindow:
         return out_keys, finals, nout
 
 
-def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str):
+    def _partials(self, accs, out_keys, nout, proto, pplan, key_names):
+        """This rank's kept groups as a partial table shaped like ``proto`` (column names, types, order)."""
+        from .column import Table
+        L = self.layout
+        dev = self.device
+        cols = {nm: k for nm, k in zip(key_names, out_keys)}
+        spec, names = [], []
+        for ak, entries in pplan.items():
+            for nm, suffix, _op in entries:
+                f = L["pfin"].get(ak, {}).get(suffix)
+                if f is None:
+                    raise Ineligible(f"partial {suffix}")
+                spec.append(f)
+                names.append(nm)
+        dst = torch.empty((len(spec), max(nout, 1)), dtype=torch.int64, device=dev)
+        dvalid = torch.empty((len(spec), max(nout, 1)), dtype=torch.uint8, device=dev)
+        if nout and spec:
+            fs = torch.tensor([x for f in spec for x in f], dtype=torch.int32)
+            N.call("dxa_aggregate_finish", N.ptr(accs), nout, self.stride, len(spec), fs.data_ptr(), N.ptr(dst),
+                   N.ptr(dvalid), N.stream_handle(dev))
+        for j, nm in enumerate(names):
+            like = proto.column(nm)
+            v, ok = dst[j, :nout], dvalid[j, :nout].view(torch.bool)
+            k = spec[j][0] & 7
+            if k == _F_COUNT:
+                cols[nm] = PrimColumn(like.dtype, v)
+            elif k in (_F_F64, _F_F64_ORD) or (isinstance(like, PrimColumn) and like.data.dtype == torch.float64):
+                cols[nm] = PrimColumn(like.dtype, v.view(torch.float64), ok)
+            elif like.dtype == "boolean":
+                cols[nm] = PrimColumn(like.dtype, v.to(torch.bool), ok)
+            else:
+                cols[nm] = PrimColumn(like.dtype, v, ok)
+        return Table(list(proto.names), [cols[nm] for nm in proto.names], nout, dev)
+
+
+def dense_partials(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, empty):
+    """Multi-rank window: this rank's window groups from the dense ring as a ``distagg.local_partials``-shaped
+    partial table → (partial table, plan, key names, group exprs), or None.  The caller exchanges and merges the
+    partials exactly as the paned path does, so both paths issue the same collectives (a rank that falls back
+    stays in step with the others)."""
+    from . import distagg as D
+    from .query import _resolve_group_expr
+    from .expr import Scope, evaluate
+    states = t.store.__dict__.setdefault("_dense", {})
+    st = states.get(fp)
+    if st is not None and getattr(st, "disabled", False):
+        return None
+    proto_key = "_dense_proto_" + fp
+    pp = t.store.__dict__.get(proto_key)
+    if pp is None:
+        scope = Scope.of_table(empty, alias)
+        gx = [_resolve_group_expr(g, scope, items) for g in sel.group_by]
+        keys = [materialize(evaluate(g, scope, ctx)) for g in gx]
+        proto, plan, key_names = D.local_partials(gx, keys, aggs, scope, ctx)
+        pp = t.store.__dict__[proto_key] = (proto, plan, key_names)
+    got = dense_answer(t, sel, alias, ctx, items, aggs, fp, partial_proto=pp)
+    if got is None:
+        return None
+    table, gexprs = got
+    return table, pp[1], pp[2], gexprs
+
+
+def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_proto=None):
     """The window statement's (key columns, finals, groups, group exprs) from the dense ring, or None."""
     from .. import parallel as P
     from .query import _resolve_group_expr
     from .expr import Scope
     store = t.store
     dev = t._device
-    if dev.type != "cuda" or not sel.group_by or (P.active() and t.dist != P.REPLICATED):
+    if dev.type != "cuda" or not sel.group_by or (partial_proto is None and P.active() and t.dist != P.REPLICATED):
         return None
     states = store.__dict__.setdefault("_dense", {})
     state = states.get(fp)
@@ -383,7 +462,7 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str):
                 s = scratch.pop(0)
                 state.accumulate(t.clipped(pane), s, alias, sel.where, gexprs, ctx)
                 slots.append(s)
-        got = state.answer(slots)
+        got = state.answer(slots, partial_proto)
     except Ineligible:
         state = states.get(fp)
         if state is not None:
@@ -396,6 +475,8 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str):
         state.disabled = True
         state.ring = state.acc = None
         return None
+    if partial_proto is not None:
+        return got, gexprs
     out_keys, finals, ng = got
     return out_keys, finals, ng, gexprs
 
