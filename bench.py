@@ -170,6 +170,10 @@ def main():
                     help="datax.job.process.columnpruning: parse and retain only the raw fields statements read")
     ap.add_argument("--sink", choices=["null", "blob"], default="null",
                     help="output sink: null (rendered JSON lands in host memory) or blob (gzip files under /tmp)")
+    ap.add_argument("--compute-priority", choices=["high", "normal"], default="high",
+                    help="HIP priority of the stream the batch's statements run on: high lets the critical path's "
+                         "short kernels (and the syncs waiting on them) go ahead of the ingest / generator / "
+                         "parse-ahead streams, which stay at normal priority and fill the rest of the chip")
     ap.add_argument("--profile-stages", action="store_true")
     ap.add_argument("--sync-outputs", action="store_true",
                     help="finish each batch's sink writes before the next batch starts (default: pipelined)")
@@ -216,6 +220,11 @@ def main():
         else:
             dist.init_process_group("gloo")                              # CPU rehearsal of the same code path
     on_gpu = device.type == "cuda"
+    if on_gpu and args.compute_priority == "high":
+        # the batch's own kernels (parse result assembly, projection, statements, the syncs that wait on them) on a
+        # high-priority stream; every helper stream created later (ingest copies, generator, parse-ahead, output
+        # rendering) is a normal one
+        torch.cuda.set_stream(torch.cuda.Stream(device, priority=-1))
     if os.environ.get("DXA_BENCH_FAIL_RANK") == str(rank):        # fault injection (tests): this rank dies
         raise SystemExit(f"bench.py: rank {rank} failing on request (DXA_BENCH_FAIL_RANK)")
 
@@ -638,7 +647,7 @@ def main():
                    "outputs": "sync" if args.sync_outputs else (
                        "pipelined (batch t sinks overlap batch t+1)" if proc.output_depth == 1 else
                        f"pipelined, {proc.output_depth} batches' outputs in flight"),
-                   "sink": args.sink},
+                   "sink": args.sink, "compute_stream_priority": args.compute_priority},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),
         "p50_latency_batch_ms": pct(50, latb_sorted),

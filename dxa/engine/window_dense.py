@@ -37,6 +37,8 @@ from .decimal import is_decimal
 
 DENSE_GROUPS = 1 << 16            # dictionary capacity per statement (groups ever seen); more → paned path
 SCRATCH_SLOTS = 4                 # ring slots for panes only partly inside a window (re-aggregated every batch)
+BLOCK = 16                        # consecutive in-window panes pre-combined into one block slot, once
+N.register_sigs({"dxa_win_combine_block": [N.c_p, N.c_i32, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p]})
 _SUPPORTED = {"count", "sum", "min", "max", "avg", "mean"}
 
 N.register_sigs({
@@ -99,6 +101,8 @@ class DenseWindow:
         self.reqs = reqs
         self.gcap = DENSE_GROUPS
         self.R = ring_slots + SCRATCH_SLOTS
+        self.NB = ring_slots // BLOCK + 4              # block slots after the pane and scratch slots
+        self.blocks: Dict[int, tuple] = {}             # block id → (members, block slot)
         self.layout = None              # built from the first pane's evaluated argument types
         self.slot_of: Dict[int, tuple] = {}     # pane key → (ring slot, id of the pane's table)
         self.disabled = False
@@ -214,7 +218,7 @@ class DenseWindow:
         self.line_ops_t = torch.tensor(line_ops, dtype=torch.int32)
         self.line_ops_dev = self.line_ops_t.to(dev)
         rows = self.gcap + 1
-        self.ring = torch.empty((self.R, rows * self.stride), dtype=torch.int64, device=dev)
+        self.ring = torch.empty((self.R + self.NB, rows * self.stride), dtype=torch.int64, device=dev)
         self.acc = torch.zeros(rows * self.stride, dtype=torch.int64, device=dev)
         self.keep = torch.empty(self.gcap, dtype=torch.uint8, device=dev)
         self.out_idx = torch.empty(self.gcap, dtype=torch.int64, device=dev)
@@ -293,6 +297,28 @@ class DenseWindow:
                len(L["line_ops"]), self.line_ops_t.data_ptr(), ring_ptr, st)
         del hold
 
+    def _dev_slots(self, slots: List[int]) -> torch.Tensor:
+        pin = self._pinned[self._pin_k]
+        self._pin_k = (self._pin_k + 1) % len(self._pinned)
+        pin[:len(slots)] = torch.tensor(slots, dtype=torch.int32)
+        return pin[:len(slots)].to(self.device, non_blocking=True)
+
+    def block_slot(self, bid: int, members: tuple, member_slots: List[int]) -> int:
+        """The ring slot holding the pre-combined rows of a complete block of panes (combined once, when the block
+        is first complete in a window; reused until a member leaves)."""
+        ent = self.blocks.get(bid)
+        if ent is not None and ent[0] == members:
+            return ent[1]
+        used = {b[1] for k, b in self.blocks.items() if k != bid}
+        free = [s for s in range(self.R, self.R + self.NB) if s not in used]
+        if not free:
+            raise Ineligible("block slots")
+        dst = free[0]
+        N.call("dxa_win_combine_block", N.ptr(self.ring), self.gcap, self.stride, N.ptr(self._dev_slots(member_slots)),
+               len(member_slots), N.ptr(self.line_ops_dev), dst, N.stream_handle(self.device))
+        self.blocks[bid] = (members, dst)
+        return dst
+
     # ---- the window's answer --------------------------------------------------------------------------------------
     def answer(self, slots: List[int], partial_proto=None):
         """Combine ``slots`` → (key columns, {agg key → column}, groups) or None (fall back: collision / full).
@@ -301,10 +327,7 @@ class DenseWindow:
         L = self.layout
         dev = self.device
         st = N.stream_handle(dev)
-        pin = self._pinned[self._pin_k]
-        self._pin_k = (self._pin_k + 1) % len(self._pinned)
-        pin[:len(slots)] = torch.tensor(slots, dtype=torch.int32)
-        slots_dev = pin[:len(slots)].to(dev, non_blocking=True)
+        slots_dev = self._dev_slots(slots)
         N.call("dxa_win_combine", N.ptr(self.ring), self.gcap, self.stride, N.ptr(slots_dev), len(slots),
                N.ptr(self.line_ops_dev), L["count_word"], N.ptr(self.scal), N.ptr(self.acc), N.ptr(self.keep),
                N.ptr(self.out_idx), st)
@@ -444,6 +467,8 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
         free = [s for s in range(state.R - SCRATCH_SLOTS) if s not in used]
         scratch = list(range(state.R - SCRATCH_SLOTS, state.R))
         slots = []
+        span = BLOCK * max(1, store.interval_us)
+        by_block: Dict[int, list] = {}
         for pane, full in pieces:
             if full and pane.all_valid:
                 ent = state.slot_of.get(pane.key)
@@ -454,7 +479,7 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
                     state.accumulate(pane.table, s, alias, sel.where, gexprs, ctx)
                     state.slot_of[pane.key] = (s, id(pane.table))
                     ent = state.slot_of[pane.key]
-                slots.append(ent[0])
+                by_block.setdefault(pane.key // span, []).append((pane.key, ent))
             else:
                 # a pane only partly inside the window: its in-range rows, re-aggregated into a scratch slot
                 if not scratch:
@@ -462,6 +487,18 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
                 s = scratch.pop(0)
                 state.accumulate(t.clipped(pane), s, alias, sel.where, gexprs, ctx)
                 slots.append(s)
+        # complete blocks of BLOCK consecutive panes: one pre-combined slot each (the per-batch combine then reads
+        # ~20 block slots and the loose panes at the window's edges instead of 300 pane slots)
+        for bid in [b for b in state.blocks if b not in by_block]:
+            del state.blocks[bid]
+        for bid, mem in by_block.items():
+            if len(mem) == BLOCK:
+                mem.sort()
+                members = tuple((k, e[1]) for k, e in mem)
+                slots.append(state.block_slot(bid, members, [e[0] for _, e in mem]))
+            else:
+                state.blocks.pop(bid, None)
+                slots.extend(e[0] for _, e in mem)
         got = state.answer(slots, partial_proto)
     except Ineligible:
         state = states.get(fp)

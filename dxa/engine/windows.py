@@ -16,6 +16,7 @@ copy), so a window view is a device-side concat + one timestamp-range mask.  Siz
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -186,6 +187,51 @@ class PanedTable(Table):
 
 
 _TS_SCRATCH: Dict = {}
+# pane statistics computed ahead, on the parse stream, by the JSON parse that produced a timestamp column
+# (``queue_pane_stats``): (data pointer, rows) → (min, max, valid count, string bytes of the parse, parse arena)
+_PANE_STATS: Dict = {}
+
+
+def _scratch(dev, stream_key):
+    """A ts_stats scratch (partials + a self-resetting ticket) per (device, stream): launches on different streams
+    must not share the ticket."""
+    from ..ops import native as N
+    key = (dev, stream_key)
+    scratch = _TS_SCRATCH.get(key)
+    if scratch is None:
+        N.register_sigs({"dxa_ts_stats_scratch_bytes": [],
+                         "dxa_ts_stats": [N.c_p, N.c_p, N.c_i64, N.c_i64, N.c_p, N.c_p, N.c_p],
+                         "dxa_ts_stats_lens": [N.c_p, N.c_p, N.c_i64, N.c_i64, N.c_p, N.c_p, N.c_i32, N.c_p,
+                                               N.c_p, N.c_p]})
+        scratch = _TS_SCRATCH[key] = torch.zeros(N.lib().dxa_ts_stats_scratch_bytes(), dtype=torch.uint8,
+                                                 device=dev)
+    return scratch
+
+
+def queue_pane_stats(vals: torch.Tensor, valid: torch.Tensor, lens: torch.Tensor, n: int, shadows) -> torch.Tensor:
+    """On the current (parse) stream, behind the parse kernel: for every timestamp-shadow row ``(val_slot,
+    valid_row)`` of the parse output, [min, max, valid count, count, total bytes of every assembled string] —
+    what a window pane of this batch needs (``WindowStore.process``), computed while the previous batch's
+    statements still run, so the batch thread reads it without waiting.  Returns the device tensor [k, 5]."""
+    from ..ops import native as N
+    dev = vals.device
+    st = N.stream_handle(dev)
+    scratch = _scratch(dev, st)
+    out = torch.zeros((len(shadows), 5), dtype=torch.int64, device=dev)
+    la = lens.reshape(-1)
+    lp = (ctypes.c_int64 * 1)(la.data_ptr())
+    ln = (ctypes.c_int64 * 1)(la.numel())
+    for k, (slot, row) in enumerate(shadows):
+        N.call("dxa_ts_stats_lens", N.ptr(vals[slot]), N.ptr(valid[row]), n, -(1 << 63), ctypes.addressof(lp),
+               ctypes.addressof(ln), 1 if la.numel() else 0, N.ptr(scratch), N.ptr(out[k]), st)
+    return out
+
+
+def register_pane_stats(ts_ptr: int, n: int, stats, arena_ptr: int) -> None:
+    """The parse's statistics of one timestamp column, read back behind the parse (PendingParse.result)."""
+    if len(_PANE_STATS) > 16:
+        _PANE_STATS.clear()
+    _PANE_STATS[(ts_ptr, n)] = (int(stats[0]), int(stats[1]), int(stats[2]), int(stats[4]), arena_ptr)
 
 
 def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int, lens_all: Optional[torch.Tensor] = None) -> List[int]:
@@ -195,17 +241,18 @@ def _ts_stats(ts: torch.Tensor, ok: torch.Tensor, E: int, lens_all: Optional[tor
     if ts.is_cuda and ts.numel():
         from ..ops import native as N
         dev = ts.device
-        scratch = _TS_SCRATCH.get(dev)
-        if scratch is None:
-            N.register_sigs({"dxa_ts_stats_scratch_bytes": [],
-                             "dxa_ts_stats": [N.c_p, N.c_p, N.c_i64, N.c_i64, N.c_p, N.c_p, N.c_p]})
-            scratch = _TS_SCRATCH[dev] = torch.zeros(N.lib().dxa_ts_stats_scratch_bytes(), dtype=torch.uint8,
-                                                     device=dev)
+        scratch = _scratch(dev, N.stream_handle(dev))
         out = torch.empty(4 if lens_all is None else 5, dtype=torch.int64, device=dev)
-        N.call("dxa_ts_stats", N.ptr(ts.contiguous()), N.ptr(N.u8(ok.contiguous())), ts.numel(), int(E),
-               N.ptr(scratch), N.ptr(out), N.stream_handle(dev))
-        if lens_all is not None:
-            torch.sum(lens_all, 0, dtype=torch.int64, out=out[4])
+        if lens_all is None:
+            N.call("dxa_ts_stats", N.ptr(ts.contiguous()), N.ptr(N.u8(ok.contiguous())), ts.numel(), int(E),
+                   N.ptr(scratch), N.ptr(out), N.stream_handle(dev))
+        else:
+            # the string bytes' total in the same pass (no separate reduction launch)
+            la = lens_all.contiguous()
+            lp = (ctypes.c_int64 * 1)(la.data_ptr())
+            ln = (ctypes.c_int64 * 1)(la.numel())
+            N.call("dxa_ts_stats_lens", N.ptr(ts.contiguous()), N.ptr(N.u8(ok.contiguous())), ts.numel(), int(E),
+                   ctypes.addressof(lp), ctypes.addressof(ln), 1, N.ptr(scratch), N.ptr(out), N.stream_handle(dev))
         return out.tolist()
     big = torch.iinfo(torch.int64).max
     vals = [torch.where(ok, ts, torch.full_like(ts, big)).min(), torch.where(ok, ts, torch.full_like(ts, -big)).max(),
@@ -246,6 +293,24 @@ class WindowStore:
             return t
         return t.filter(m)
 
+    def _stats_ahead(self, projected: Table, ts: torch.Tensor, E: int):
+        """The statistics the parse already queued for this timestamp column (``queue_pane_stats``), when they
+        answer the common case — every event valid and none late (min ≥ E) — and every string leaf of the pane
+        views the parse's bytes (so the parse's string total bounds the compaction); else None (read them now)."""
+        pre = _PANE_STATS.pop((ts.data_ptr(), projected.length), None) if ts.is_cuda else None
+        if pre is None:
+            return None
+        mn, mx, cnt, total, arena = pre
+        n = projected.length
+        if cnt != n or mn < E:
+            return None
+        leaves: List[StrColumn] = []
+        for c in projected.columns:
+            _str_leaves(c, leaves)
+        if any(c.arena.data_ptr() != arena for c in leaves):
+            return None
+        return [mn, mx, cnt, n, total]
+
     def _pane(self, key: int, t: Table) -> Pane:
         if t.length == 0:
             return Pane(key, t, 0, -1, True)
@@ -265,7 +330,9 @@ class WindowStore:
             with host_section("windows:stats"):
                 ts, ok = self._ts(projected)
                 lens_all = _str_lens_all(projected)
-                got = _ts_stats(ts, ok, E, lens_all)
+                got = self._stats_ahead(projected, ts, E)
+                if got is None:
+                    got = _ts_stats(ts, ok, E, lens_all)
                 lo_, hi_, nok, nkeep = got[:4]
             if int(nkeep) == projected.length:
                 with host_section("windows:compact"):

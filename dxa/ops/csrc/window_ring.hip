@@ -183,9 +183,9 @@ __global__ __launch_bounds__(256) void win_combine_kernel(const unsigned long lo
                                                           int32_t nslots, int32_t stride,
                                                           const int32_t* __restrict__ line_op,
                                                           const int32_t* __restrict__ scal, int32_t gcap,
-                                                          unsigned long long* __restrict__ out) {
-  int32_t ng = scal[0];
-  if (ng > gcap) ng = gcap;
+                                                          int32_t fixed_rows, unsigned long long* __restrict__ out) {
+  int32_t ng = fixed_rows > 0 ? fixed_rows : scal[0];
+  if (fixed_rows <= 0 && ng > gcap) ng = gcap;
   const int64_t total = (int64_t)ng * stride;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -304,10 +304,23 @@ DXA_API int dxa_win_combine(const void* ring, int32_t gcap, int32_t stride, cons
   const int64_t slot_words = (int64_t)(gcap + 1) * stride;
   hipMemsetAsync(scal + 2, 0, 4, s);
   hipLaunchKernelGGL(win_combine_kernel, dim3(dxa_blocks((int64_t)gcap * stride, 256, 256 * 64)), dim3(256), 0, s,
-                     (const unsigned long long*)ring, slot_words, slots, nslots, stride, line_op, scal, gcap,
+                     (const unsigned long long*)ring, slot_words, slots, nslots, stride, line_op, scal, gcap, 0,
                      (unsigned long long*)acc);
   hipLaunchKernelGGL(win_keep_kernel, dim3(dxa_blocks(gcap, 256)), dim3(256), 0, s,
                      (const unsigned long long*)acc, stride, count_word, scal, gcap, keep, scal);
   hipLaunchKernelGGL(win_compact_kernel, dim3(1), dim3(256), 0, s, keep, gcap, scal, out_idx);
+  return (int)hipGetLastError();
+}
+
+// a block of ring slots pre-combined into another ring slot (every row, so groups the dictionary gains later read
+// the identity there): out = ring slot ``dst``
+DXA_API int dxa_win_combine_block(void* ring, int32_t gcap, int32_t stride, const int32_t* slots, int32_t nslots,
+                                  const int32_t* line_op, int32_t dst, void* st) {
+  hipStream_t s = (hipStream_t)st;
+  const int64_t slot_words = (int64_t)(gcap + 1) * stride;
+  unsigned long long* r = (unsigned long long*)ring;
+  hipLaunchKernelGGL(win_combine_kernel, dim3(dxa_blocks((int64_t)(gcap + 1) * stride, 256, 256 * 64)), dim3(256), 0,
+                     s, (const unsigned long long*)r, slot_words, slots, nslots, stride, line_op, (const int32_t*)nullptr,
+                     gcap, gcap + 1, r + (int64_t)dst * slot_words);
   return (int)hipGetLastError();
 }

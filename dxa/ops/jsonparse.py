@@ -337,6 +337,11 @@ class PendingParse:
                     # parse stream while the consumer's kernels may still read them
                     for t in (vals, lens, valid, row_ok, self.arena):
                         t.record_stream(cur)
+            ps = getattr(self, "pane_stats", None)
+            if ps is not None:
+                from ..engine.windows import register_pane_stats
+                for (slot, _row), st in zip(ps[0], ps[1].tolist()):
+                    register_pane_stats(vals[slot].data_ptr(), self.n, st, self.arena.data_ptr())
             self._done = (_assemble(self.plan, self.arena, vals, lens, valid, self.n, nulls), row_ok)
             self.parts = self.arena = self.counts = self.event = self.stream = None
         return self._done
@@ -377,7 +382,7 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
     valid2 = torch.empty((max(1, nn - plan.nkn), m), dtype=torch.uint8, device=buf.device)
     row_ok = torch.empty(max(n, 1), dtype=torch.uint8, device=buf.device)
     zs = plan.string_slot_pairs(buf.device)
-    counts = event = None
+    counts = event = pane_stats = None
     if n:
         st = N.stream_handle(buf.device)
         N.call("dxa_json_parse", N.ptr(buf), N.ptr(offs), n, N.ptr(lut_k), N.ptr(lut_n), plan.cap, N.ptr(types),
@@ -390,11 +395,20 @@ def _parse_gpu_async(buf, offs, n, plan: ParsePlan, ends=None) -> PendingParse:
         N.call("dxa_null_counts", N.ptr(valid), n, nk, N.ptr(cnt), st)      # the assembled nodes only
         counts = torch.empty(nk, dtype=torch.int64, pin_memory=True)
         counts.copy_(cnt, non_blocking=True)     # a few bytes behind the kernels; read in result()
+        shadows = [(plan.nodes[i].val_slot, i) for i in range(1, plan.nkn) if plan.nodes[i].shadow_of >= 0]
+        if shadows:
+            # a window pane's statistics of every timestamp shadow, queued here with the parse (windows.py)
+            from ..engine.windows import queue_pane_stats
+            pst = queue_pane_stats(vals, valid, lens[:plan.nkl] if plan.nkl else lens[:0], n, shadows)
+            pane_stats = (shadows, torch.empty(pst.shape, dtype=torch.int64, pin_memory=True))
+            pane_stats[1].copy_(pst, non_blocking=True)
         event = torch.cuda.Event()
         event.record(torch.cuda.current_stream(buf.device))
     parts = (vals[:, :n], lens[:, :n], valid[:, :n].view(torch.bool), row_ok[:n].view(torch.bool))
-    return PendingParse(plan=plan, arena=buf, parts=parts, n=n, counts=counts, event=event,
-                        stream=torch.cuda.current_stream(buf.device))
+    pp = PendingParse(plan=plan, arena=buf, parts=parts, n=n, counts=counts, event=event,
+                      stream=torch.cuda.current_stream(buf.device))
+    pp.pane_stats = pane_stats
+    return pp
 
 
 def _assemble(plan: ParsePlan, arena, vals, lens, valid, n, nulls=None):

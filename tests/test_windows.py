@@ -91,13 +91,16 @@ def test_window_ranges_and_eviction():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("spread,nb,win", [(S - 1, 40, 9), (3 * S, 24, 5)])
-def test_dense_ring_matches_materialized(spread, nb, win):
+@pytest.mark.parametrize("spread,nb,win,block", [(S - 1, 40, 9, 16), (S - 1, 40, 11, 3), (3 * S, 24, 5, 2)])
+def test_dense_ring_matches_materialized(spread, nb, win, block, monkeypatch):
     """The dense window path (window_dense.py / window_ring.hip: persistent group dictionary + per-pane accumulator
     ring) answers the decomposable window statements on the GPU; its rows equal the materialized window's batch
     after batch — through ring-slot reuse after evictions, clipped panes (re-aggregated into scratch slots) when the
-    event times straddle the window edges, NULL arguments and a WHERE."""
+    event times straddle the window edges, NULL arguments and a WHERE; with small ``block`` sizes through block
+    slots pre-combined, reused and dropped as the window slides."""
     import numpy as np
+    from dxa.engine import window_dense
+    monkeypatch.setattr(window_dense, "BLOCK", block)
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(11)
     conf = TimeWindowConf({"W": win * S}, True, "ts", 2 * S, win * S, False)
@@ -123,3 +126,5 @@ def test_dense_ring_matches_materialized(spread, nb, win):
     # the ring only ever holds retained panes
     for d in dense.values():
         assert len(d.slot_of) <= len(store.past) + 1
+    if block < win:
+        assert any(d.blocks for d in dense.values())
