@@ -170,7 +170,7 @@ def main():
                     help="datax.job.process.columnpruning: parse and retain only the raw fields statements read")
     ap.add_argument("--sink", choices=["null", "blob"], default="null",
                     help="output sink: null (rendered JSON lands in host memory) or blob (gzip files under /tmp)")
-    ap.add_argument("--compute-priority", choices=["high", "normal"], default="high",
+    ap.add_argument("--compute-priority", choices=["high", "normal"], default="normal",
                     help="HIP priority of the stream the batch's statements run on: high lets the critical path's "
                          "short kernels (and the syncs waiting on them) go ahead of the ingest / generator / "
                          "parse-ahead streams, which stay at normal priority and fill the rest of the chip")

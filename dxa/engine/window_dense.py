@@ -31,7 +31,7 @@ import torch
 from ..ops import native as N
 from ..ops.groupby import (_F_AVG, _F_COUNT, _F_F64, _F_F64_ORD, _F_I64, _F_NOT, _MA_ADD_F64, _MA_ADD_U64, _MA_MAX,
                            _MV_COUNT, _MV_F64, _MV_F64_ORD, _MV_I64, _MV_NOT)
-from ..ops.hashing import MAX_KEY_COLS, _KeyCols, hash_columns, key_cols
+from ..ops.hashing import MAX_KEY_COLS, _KeyCols, key_cols
 from .column import ConstColumn, PrimColumn, StrColumn, materialize
 from .decimal import is_decimal
 
@@ -44,9 +44,11 @@ _SUPPORTED = {"count", "sum", "min", "max", "avg", "mean"}
 N.register_sigs({
     "dxa_win_sizes": [N.c_p],
     "dxa_win_init": [N.c_p, N.c_p, N.c_i64, N.c_p],
-    "dxa_win_insert": [N.c_p, N.c_p, N.c_i64, N.c_p, N.c_i64, N.c_p, N.c_p, N.c_i32, N.c_p, N.c_p, N.c_p, N.c_p,
-                       N.c_p, N.c_p],
     "dxa_win_combine": [N.c_p, N.c_i32, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_p, N.c_p, N.c_p, N.c_p],
+    "dxa_win_insert_fused": [N.c_p, N.c_p, N.c_p, N.c_p, N.c_i64, N.c_p, N.c_p, N.c_p, N.c_p],
+    "dxa_win_answer": [N.c_p, N.c_i32, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_i32, N.c_p, N.c_p, N.c_p, N.c_p, N.c_p,
+                       N.c_p, N.c_p],
+    "dxa_win_emit_size": [],
 })
 
 
@@ -59,6 +61,14 @@ class _DictCols(ctypes.Structure):
     _fields_ = [("c", _DictCol * MAX_KEY_COLS), ("ncols", ctypes.c_int32), ("gcap", ctypes.c_int32)]
 
 
+class _EmitArgs(ctypes.Structure):
+    _fields_ = [("acc", ctypes.c_void_p), ("stride", ctypes.c_int32), ("nreq", ctypes.c_int32),
+                ("kind", ctypes.c_int32 * 64), ("pos", ctypes.c_int32 * 64), ("cnt", ctypes.c_int32 * 64),
+                ("dst", ctypes.c_void_p), ("dvalid", ctypes.c_void_p), ("okey", ctypes.c_void_p * MAX_KEY_COLS),
+                ("olen", ctypes.c_void_p * MAX_KEY_COLS), ("ovalid", ctypes.c_void_p * MAX_KEY_COLS),
+                ("out_idx", ctypes.c_void_p), ("scal", ctypes.c_void_p), ("gcap", ctypes.c_int32)]
+
+
 _SIZES: Optional[List[int]] = None
 
 
@@ -68,7 +78,8 @@ def _sizes() -> List[int]:
         out = (ctypes.c_int32 * 3)()
         N.lib().dxa_win_sizes(out)
         _SIZES = list(out)
-        if _SIZES[0] != ctypes.sizeof(_KeyCols) or _SIZES[1] != ctypes.sizeof(_DictCols):
+        if _SIZES[0] != ctypes.sizeof(_KeyCols) or _SIZES[1] != ctypes.sizeof(_DictCols) or \
+                N.lib().dxa_win_emit_size() != ctypes.sizeof(_EmitArgs):
             raise N.NativeError("window_ring.hip struct layout differs from window_dense.py")
     return _SIZES
 
@@ -114,8 +125,6 @@ class DenseWindow:
         self.htab = torch.empty(cap, dtype=torch.int64, device=dev)
         self.gid_of_slot = torch.empty(cap, dtype=torch.int32, device=dev)
         self.scal = torch.zeros(4, dtype=torch.int32, device=dev)     # groups, bad flags, kept, pad
-        self.rep = torch.empty(self.gcap, dtype=torch.int32, device=dev)
-        self.stored = torch.zeros(self.gcap + 1, dtype=torch.uint8, device=dev)
         N.call("dxa_win_init", N.ptr(self.htab), N.ptr(self.gid_of_slot), cap, N.stream_handle(dev))
         self.keys = None                # dictionary key columns, built with the layout
         self.ring = None
@@ -213,8 +222,7 @@ class DenseWindow:
                 pfin[ak] = {"v": fin[len(pfin)], "cnt": (_F_COUNT, where[c], -1)}
         self.stride = 8 * len(line_ops)
         self.layout = dict(slots=slots, order=order, nslots=nslots, line_ops=line_ops, plan=plan,
-                           count_word=where[star], fspec=torch.tensor([x for f in fin for x in f], dtype=torch.int32),
-                           pfin=pfin)
+                           count_word=where[star], fin=fin, pfin=pfin, pspec_of=self._partial_spec)
         self.line_ops_t = torch.tensor(line_ops, dtype=torch.int32)
         self.line_ops_dev = self.line_ops_t.to(dev)
         rows = self.gcap + 1
@@ -267,12 +275,11 @@ class DenseWindow:
         if kc is None:
             raise Ineligible("key columns")
         kc.ncols, kc.n = len(keys), n
-        h = hash_columns(keys) if n else torch.empty(0, dtype=torch.int64, device=dev)
         gid = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        N.call("dxa_win_insert", N.ptr(h), N.ptr(keep), n, N.ptr(self.htab), self.hcap, N.ptr(self.gid_of_slot),
-               N.ptr(self.scal), self.gcap, N.ptr(gid), N.ptr(self.rep), ctypes.addressof(kc),
-               ctypes.addressof(self.dictcols), N.ptr(self.stored), st)
-        spec, hold = [], [h, gid, keep, kc]
+        # hash + dictionary lookup / claim + key store + verify: one launch (window_ring.hip win_insert_kernel)
+        N.call("dxa_win_insert_fused", ctypes.addressof(kc), ctypes.addressof(self.dictcols), N.ptr(keep),
+               N.ptr(self.htab), self.hcap, N.ptr(self.gid_of_slot), N.ptr(self.scal), N.ptr(gid), st)
+        spec, hold = [], [gid, keep, kc]
         for i in L["order"][:L["nslots"]]:
             if i is None:
                 spec += [0, 0, -1]
@@ -328,39 +335,32 @@ class DenseWindow:
         dev = self.device
         st = N.stream_handle(dev)
         slots_dev = self._dev_slots(slots)
-        N.call("dxa_win_combine", N.ptr(self.ring), self.gcap, self.stride, N.ptr(slots_dev), len(slots),
+        fin = L["pspec_of"](partial_proto) if partial_proto is not None else L["fin"]
+        e, bufs = self._emit_args(fin)
+        N.call("dxa_win_answer", N.ptr(self.ring), self.gcap, self.stride, N.ptr(slots_dev), len(slots),
                N.ptr(self.line_ops_dev), L["count_word"], N.ptr(self.scal), N.ptr(self.acc), N.ptr(self.keep),
-               N.ptr(self.out_idx), st)
+               N.ptr(self.out_idx), ctypes.addressof(e), ctypes.addressof(self.dictcols), st)
         ng_all, bad, nout, _ = self.scal.tolist()          # the statement's one synchronising read
         if bad:
             return None
-        idx = self.out_idx[:nout]
-        kw = _sizes()[2]
+        okey, olen, ovalid, dst, dvalid = bufs
         out_keys = []
-        for dt, kind, vals, lens, valid in self.keys:
-            v = valid[idx].view(torch.bool)
+        for j, (dt, kind, vals, lens, valid) in enumerate(self.keys):
+            v = ovalid[j, :nout].view(torch.bool)
             if kind == 2:
-                out_keys.append(StrColumn(vals, idx * kw, lens[idx], v))
+                out_keys.append(StrColumn(vals, okey[j, :nout], olen[j, :nout], v))
             else:
-                d = vals[idx]
+                d = okey[j, :nout]
                 if kind == 1:
                     d = d.view(torch.float64)
                 elif dt == "boolean":
                     d = d.to(torch.bool)
                 out_keys.append(PrimColumn(dt, d, v))
-        accs = self.acc.view(self.gcap + 1, self.stride)[idx].contiguous()
+        cols = [(dst[r, :nout], dvalid[r, :nout].view(torch.bool)) for r in range(len(fin))]
         if partial_proto is not None:
-            return self._partials(accs, out_keys, nout, *partial_proto)
-        nreq = len(L["plan"])
-        dst = torch.empty((nreq, max(nout, 1)), dtype=torch.int64, device=dev)
-        dvalid = torch.empty((nreq, max(nout, 1)), dtype=torch.uint8, device=dev)
-        if nout:
-            N.call("dxa_aggregate_finish", N.ptr(accs), nout, self.stride, nreq, L["fspec"].data_ptr(), N.ptr(dst),
-                   N.ptr(dvalid), st)
+            return self._partials(cols, out_keys, nout, *partial_proto)
         finals = {}
-        for j, (ak, kind, s, c, dt) in enumerate(L["plan"]):
-            v = dst[j, :nout]
-            ok = dvalid[j, :nout].view(torch.bool)
+        for (ak, kind, s, c, dt), (v, ok) in zip(L["plan"], cols):
             if kind == "count":
                 finals[ak] = PrimColumn("long", v)
             elif kind == "avg":
@@ -373,40 +373,58 @@ class DenseWindow:
                 finals[ak] = PrimColumn(dt, v.to(torch.bool) if dt == "boolean" else v, ok)
         return out_keys, finals, nout
 
+    def _emit_args(self, fin):
+        """The emit kernel's descriptor and this batch's output buffers ([gcap]-strided, fresh per batch: the
+        previous batch's outputs may still be rendering on the output stream)."""
+        g, dev = self.gcap, self.device
+        nk, nr = len(self.keys), len(fin)
+        words = torch.empty((nk + nr, g), dtype=torch.int64, device=dev)
+        flags = torch.empty((nk + nr, g), dtype=torch.uint8, device=dev)
+        olen = torch.empty((max(1, nk), g), dtype=torch.int32, device=dev)
+        okey, dst = words[:nk], words[nk:]
+        ovalid, dvalid = flags[:nk], flags[nk:]
+        e = _EmitArgs()
+        e.acc, e.stride, e.nreq = self.acc.data_ptr(), self.stride, nr
+        for r, (k, pos, cnt) in enumerate(fin):
+            e.kind[r], e.pos[r], e.cnt[r] = k, pos, cnt
+        e.dst, e.dvalid = dst.data_ptr(), dvalid.data_ptr()
+        for j in range(nk):
+            e.okey[j], e.olen[j], e.ovalid[j] = okey[j].data_ptr(), olen[j].data_ptr(), ovalid[j].data_ptr()
+        e.out_idx, e.scal, e.gcap = self.out_idx.data_ptr(), self.scal.data_ptr(), g
+        return e, (okey, olen, ovalid, dst, dvalid)
 
-    def _partials(self, accs, out_keys, nout, proto, pplan, key_names):
-        """This rank's kept groups as a partial table shaped like ``proto`` (column names, types, order)."""
-        from .column import Table
+    def _partial_spec(self, partial_proto):
+        """Finishing spec of the partial states, in the partial table's entry order."""
+        _proto, pplan, _kn = partial_proto
         L = self.layout
-        dev = self.device
-        cols = {nm: k for nm, k in zip(key_names, out_keys)}
-        spec, names = [], []
+        out = []
         for ak, entries in pplan.items():
             for nm, suffix, _op in entries:
                 f = L["pfin"].get(ak, {}).get(suffix)
                 if f is None:
                     raise Ineligible(f"partial {suffix}")
-                spec.append(f)
-                names.append(nm)
-        dst = torch.empty((len(spec), max(nout, 1)), dtype=torch.int64, device=dev)
-        dvalid = torch.empty((len(spec), max(nout, 1)), dtype=torch.uint8, device=dev)
-        if nout and spec:
-            fs = torch.tensor([x for f in spec for x in f], dtype=torch.int32)
-            N.call("dxa_aggregate_finish", N.ptr(accs), nout, self.stride, len(spec), fs.data_ptr(), N.ptr(dst),
-                   N.ptr(dvalid), N.stream_handle(dev))
-        for j, nm in enumerate(names):
-            like = proto.column(nm)
-            v, ok = dst[j, :nout], dvalid[j, :nout].view(torch.bool)
-            k = spec[j][0] & 7
-            if k == _F_COUNT:
-                cols[nm] = PrimColumn(like.dtype, v)
-            elif k in (_F_F64, _F_F64_ORD) or (isinstance(like, PrimColumn) and like.data.dtype == torch.float64):
-                cols[nm] = PrimColumn(like.dtype, v.view(torch.float64), ok)
-            elif like.dtype == "boolean":
-                cols[nm] = PrimColumn(like.dtype, v.to(torch.bool), ok)
-            else:
-                cols[nm] = PrimColumn(like.dtype, v, ok)
-        return Table(list(proto.names), [cols[nm] for nm in proto.names], nout, dev)
+                out.append(f)
+        return out
+
+    def _partials(self, cols, out_keys, nout, proto, pplan, key_names):
+        """This rank's kept groups as a partial table shaped like ``proto`` (column names, types, order)."""
+        from .column import Table
+        got = {nm: k for nm, k in zip(key_names, out_keys)}
+        j = 0
+        for ak, entries in pplan.items():
+            for nm, suffix, _op in entries:
+                like = proto.column(nm)
+                v, ok = cols[j]
+                j += 1
+                if suffix == "cnt":
+                    got[nm] = PrimColumn(like.dtype, v)
+                elif isinstance(like, PrimColumn) and like.data.dtype == torch.float64:
+                    got[nm] = PrimColumn(like.dtype, v.view(torch.float64), ok)
+                elif like.dtype == "boolean":
+                    got[nm] = PrimColumn(like.dtype, v.to(torch.bool), ok)
+                else:
+                    got[nm] = PrimColumn(like.dtype, v, ok)
+        return Table(list(proto.names), [got[nm] for nm in proto.names], nout, self.device)
 
 
 def dense_partials(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, empty):
