@@ -160,9 +160,10 @@ def main():
                          "Kafka endpoint's codec, inflate.hip; snappy = snappy-java's xerial stream, snappy.hip; "
                          "zstd = zstd-jni's frames, zstd.hip)")
     ap.add_argument("--zstd-level", type=int, default=3, help="kafka zstd: producer compression.zstd.level")
-    ap.add_argument("--crc", choices=["host", "device", "off"], default="host",
-                    help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): host planner "
-                         "threads (default), the GPU (kafka_crc_kernel), or not at all")
+    ap.add_argument("--crc", choices=["auto", "host", "device", "off"], default="auto",
+                    help="kafka: where record batches' CRC-32C is checked (consumer check.crcs): auto (default: host "
+                         "planner threads while the node's host memory budget covers this rank, else the GPU — "
+                         "dxa.parallel.affinity.crc_placement), host, the GPU (kafka_crc_kernel), or not at all")
     ap.add_argument("--workdir", default=None,
                     help="keep the run's files (state table, sink output) here, rank r in <dir>_<r>, cleared of state "
                          "at start; default: a fresh temporary directory per rank, removed at the end")
@@ -207,8 +208,10 @@ def main():
     numa_cpus = bind_to_device(dev_index) if ndev > dev_index else None
     # host worker threads (producer-side compression before the timed region, Kafka batch planning inside it): this
     # rank's share of the CPUs its socket's ranks are bound to — 16 on a 1-GPU run
-    from dxa.parallel.affinity import host_threads
+    from dxa.parallel.affinity import crc_placement, host_threads
     host_thr = host_threads(dev_index, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    if args.crc == "auto":
+        args.crc = crc_placement(local, int(os.environ.get("LOCAL_WORLD_SIZE", "1")), host_thr)
     device = torch.device("cuda", dev_index) if torch.cuda.is_available() else torch.device("cpu")
     if world > 1:
         if device.type == "cuda":

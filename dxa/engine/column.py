@@ -115,7 +115,8 @@ def _plan_take(c: "Column", idx: torch.Tensor, leaves: List[torch.Tensor]):
         if c.valid is not None:
             leaves.append(c.valid)
         has_v = c.valid is not None
-        return lambda g: type(c)(c.arena, g[i], g[i + 1], g[i + 2] if has_v else None, c.dtype)
+        return lambda g: _with_max_len(type(c)(c.arena, g[i], g[i + 1], g[i + 2] if has_v else None, c.dtype),
+                                       c.max_len)
     if isinstance(c, StructColumn):
         i = len(leaves)
         if c.valid is not None:
@@ -196,8 +197,18 @@ class PrimColumn(Column):
         return f"PrimColumn({self.dtype}, n={self.length})"
 
 
+def _with_max_len(c, m):
+    if m is not None:
+        c.max_len = m
+    return c
+
+
 class StrColumn(Column):
     dtype = "string"
+    # a known bound on every row's byte length (None: unknown).  Rows viewing a window dictionary's fixed-width key
+    # slots have one; it survives gathers and concatenations, so their string bytes can be sized on the host
+    # without reading the exact total back (strings.concat_multi)
+    max_len: Optional[int] = None
 
     def __init__(self, arena: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor,
                  valid: Optional[torch.Tensor] = None, dtype: Any = "string"):
@@ -215,12 +226,12 @@ class StrColumn(Column):
 
     def take(self, idx):
         c = type(self)(self.arena, self.starts[idx], self.lens[idx], _take_valid(self.valid, idx), self.dtype)
-        return c
+        return _with_max_len(c, self.max_len)
 
     def with_valid(self, extra):
         c = type(self)(self.arena, self.starts, self.lens, and_valid(self.valid, extra), self.dtype)
         c._hash = self._hash
-        return c
+        return _with_max_len(c, self.max_len)
 
     def to(self, device):
         c = self.compact()
@@ -772,6 +783,8 @@ def concat_tables(tables: List[Table]) -> Table:
             valid, _ = valid_segments(parts, device, segs)
             cols[at] = type(parts[0])(arena, starts, lens, valid, parts[0].dtype)
             cols[at]._compact = True        # disjoint, in order in a fresh arena: its size bounds the bytes
+            if all(p.max_len is not None for p in parts):
+                cols[at].max_len = max(p.max_len for p in parts)
     if segs:
         segs.launch(device)                         # every fixed-width leaf of every table: one launch
     return Table(names, cols, sum(t.length for t in tables), device)

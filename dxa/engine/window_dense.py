@@ -348,7 +348,9 @@ class DenseWindow:
         for j, (dt, kind, vals, lens, valid) in enumerate(self.keys):
             v = ovalid[j, :nout].view(torch.bool)
             if kind == 2:
-                out_keys.append(StrColumn(vals, okey[j, :nout], olen[j, :nout], v))
+                sc = StrColumn(vals, okey[j, :nout], olen[j, :nout], v)
+                sc.max_len = _sizes()[2]               # a dictionary key slot: bytes per row are bounded
+                out_keys.append(sc)
             else:
                 d = okey[j, :nout]
                 if kind == 1:

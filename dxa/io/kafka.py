@@ -716,7 +716,14 @@ def build_kafka_source(inp, device, kind: str, rank: int = 0, world: int = 1) ->
         ckpt = inp.get("kafka.checkpointdir")
         rate = inp.get("kafka.maxrate")
         flush = (inp.get("kafka.flushexistingcheckpoints") or "false").lower() == "true"
-    crcs = (inp.get(f"{kind}.checkcrcs") or "true").lower()          # true (host) | device | false
+    crcs = (inp.get(f"{kind}.checkcrcs") or "true").lower()          # true (host) | device | auto | false
+    if crcs == "auto":
+        # per rank from the node's planner threads and host memory budget (affinity.crc_placement)
+        import os
+        from ..parallel.affinity import crc_placement, host_threads
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        crcs = crc_placement(lr, lw, host_threads(lr, lw))
     start = start_position(inp.get(f"{kind}.startenqueuetime"), inp.get(f"{kind}.autooffsetreset"))
     return KafkaSource(client, topics, device, ckpt, int(rate) if rate else None, start=start,
                        flush_existing=flush, rank=rank, world=world, check_crcs=crcs)

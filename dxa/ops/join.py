@@ -189,7 +189,8 @@ def hash_join(lkeys: List, rkeys: List, kind: str, built: Optional[BuiltSide] = 
         built = build_side(rkeys)
     li, ri = probe(built, lkeys, outer=False)
     ok = keys_equal(lkeys, rkeys, li, ri)
-    li, ri = li[ok], ri[ok]
+    keep = torch.nonzero(ok).flatten()          # one count read for both sides (two boolean indexings read twice)
+    li, ri = li[keep], ri[keep]
     if kind == "inner":
         return li, ri
     matched_l = torch.zeros(nl, dtype=torch.bool, device=device)

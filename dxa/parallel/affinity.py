@@ -158,3 +158,29 @@ def host_threads(index: int, local_world: int = 1, cap: int = 16, floor: int = 2
     elif local_world > 1:
         share = local_world
     return max(floor, min(cap, cpus // share))
+
+
+# Host CRC-32C capacity, measured on an MI355X box (profiles/round6/host8/README.md): ~9 GB/s per planner thread
+# when 16 threads check concurrently (11.5 GB/s for one), and the PCIe-bound ingest one rank checks (57 GB/s).
+CRC_GBS_PER_THREAD = 9.0
+INGEST_GBS_PER_RANK = 57.0
+# Host memory traffic a node's ranks may spend on ingest: every host-checked byte is read twice (the CRC, then the
+# DMA to the GPU).  1000 GB/s is ~85 % of a 2-socket DDR5-6400 node's peak; the 1-GPU box gives no way to measure the
+# whole node (its 16-CPU share checked 144 GB/s without saturating), so it is a setting, not a measurement.
+HOST_INGEST_BUDGET_GBS = 1000.0
+
+
+def crc_placement(local_rank: int, local_world: int, threads: int, budget_gbs: float = HOST_INGEST_BUDGET_GBS,
+                  need_gbs: float = INGEST_GBS_PER_RANK, per_thread_gbs: float = CRC_GBS_PER_THREAD) -> str:
+    """``check.crcs=auto``: where the node's ranks check their Kafka batches' CRC-32C.
+
+    The ranks of a job step in lockstep (every batch ends in collectives), so the slowest rank sets everyone's pace
+    and all ranks of a node take the same decision:
+
+    * ``"host"`` when a rank's planner threads check at its ingest rate (threads x per-thread rate ≥ the need) and
+      the node's host memory budget covers every local rank's two reads of its ingest (CRC + DMA);
+    * ``"device"`` otherwise — the GPU kernel costs ~20 % of a PCIe-bound step (profiles/crc/README.md), less than
+      a starved host planner would."""
+    if threads * per_thread_gbs < need_gbs:
+        return "device"
+    return "host" if local_world * 2.0 * need_gbs <= budget_gbs else "device"

@@ -224,3 +224,14 @@ def test_send_side_is_three_launches():
         PK.scatter(lay, state, [r[0] for r in sz], [[r[1 + s] for r in sz] for s in range(lay.S)])
     # dxa_xchg_plan = histogram + scan kernels
     assert log == ["dxa_xchg_plan"] and log2 == ["dxa_xchg_scatter"], (log, log2)
+
+
+def test_crc_placement_rule():
+    """check.crcs=auto (dxa.parallel.affinity.crc_placement): host while the planner threads keep up with the ingest
+    and the node's host memory budget covers every local rank's CRC + DMA reads; the same answer on every local
+    rank (lockstep ranks run at the slowest one's pace); device otherwise (profiles/round6/host8/README.md)."""
+    from dxa.parallel.affinity import crc_placement
+    assert crc_placement(0, 1, 16) == "host"
+    assert [crc_placement(r, 8, 16) for r in range(8)] == ["host"] * 8          # 8 x 2 x 57 = 912 <= 1000 GB/s
+    assert [crc_placement(r, 8, 16, budget_gbs=600) for r in range(8)] == ["device"] * 8
+    assert crc_placement(0, 1, 4) == "device"                                    # 4 x 9 GB/s < 57 GB/s
