@@ -178,7 +178,8 @@ def _rows_equal(got, want, path):
 
 @pytest.mark.parametrize("world,device", [(2, "cpu"), (3, "cpu"), (4, "cpu"),
                                           pytest.param(2, "cuda", marks=pytest.mark.gpu),
-                                          pytest.param(3, "cuda", marks=pytest.mark.gpu)])
+                                          pytest.param(3, "cuda", marks=pytest.mark.gpu),
+                                          pytest.param(4, "cuda", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("variant", ["groupby", "window", "join", "full", "passthrough"])
 def test_flow_ranks_match_one(variant, world, device, tmp_path):
     """W ranks (2, 3 — a world that is not a power of two, so ``owner_of``'s modulo is uneven — and 4), the last
