@@ -783,8 +783,9 @@ def concat_tables(tables: List[Table]) -> Table:
             valid, _ = valid_segments(parts, device, segs)
             cols[at] = type(parts[0])(arena, starts, lens, valid, parts[0].dtype)
             cols[at]._compact = True        # disjoint, in order in a fresh arena: its size bounds the bytes
-            if all(p.max_len is not None for p in parts):
-                cols[at].max_len = max(p.max_len for p in parts)
+            bounded = [p.max_len for p in parts if p.length]
+            if all(m is not None for m in bounded):
+                cols[at].max_len = max(bounded, default=0)
     if segs:
         segs.launch(device)                         # every fixed-width leaf of every table: one launch
     return Table(names, cols, sum(t.length for t in tables), device)

@@ -119,6 +119,7 @@ class Scope:
         self.quals = quals
         self.length = int(length)
         self.device = torch.device(device)
+        self._index: Optional[Dict[str, List[int]]] = None
 
     def with_bindings(self, names: List[str], cols: List[Column]) -> "Scope":
         """This scope plus ``names`` bound to ``cols`` (lambda parameters), which shadow same-named columns."""
@@ -133,15 +134,24 @@ class Scope:
         return Scope(list(table.names), cols, [qual] * len(table.names), table.length, table.device)
 
     def qualifiers(self):
-        return {q.lower() for q in self.quals if q}
+        got = self.__dict__.get("_quals")
+        if got is None:
+            got = self._quals = {q.lower() for q in self.quals if q}
+        return got
 
     def _find(self, name: str, qual: Optional[str] = None) -> List[int]:
-        low = name.lower()
-        out = [i for i, n in enumerate(self.names) if n.lower() == low and
-               (qual is None or (self.quals[i] or "").lower() == qual.lower())]
-        if qual is None:
+        index = self._index
+        if index is None:
+            index = self._index = _name_index(self.names)
+        out = index.get(name.lower())
+        if not out:
+            return []
+        if qual is not None:
+            ql = qual.lower()
+            out = [i for i in out if (self.quals[i] or "").lower() == ql]
+        else:
             vis = [i for i in out if not isinstance(self.quals[i], HiddenQual)]
-            out = vis or out
+            out = vis or list(out)
         exact = [i for i in out if self.names[i] == name]
         return exact or out
 
@@ -194,6 +204,24 @@ class Scope:
             if len(quals) > 1:
                 raise EvalError(f"reference '{parts[0]}' is ambiguous")
         return _navigate(self.cols[hits[0]], parts[1:])
+
+
+_NAME_INDEX: Dict[Tuple[str, ...], Dict[str, List[int]]] = {}
+
+
+def _name_index(names: List[str]) -> Dict[str, List[int]]:
+    """lower-cased column name → its positions, shared by every scope over the same names (statements resolve
+    dozens of references per batch against scopes of ~30 columns)."""
+    key = tuple(names)
+    got = _NAME_INDEX.get(key)
+    if got is None:
+        got = {}
+        for i, n in enumerate(names):
+            got.setdefault(n.lower(), []).append(i)
+        if len(_NAME_INDEX) >= 512:
+            _NAME_INDEX.clear()
+        _NAME_INDEX[key] = got
+    return got
 
 
 def _navigate(col: Column, rest: Tuple[str, ...]) -> Column:

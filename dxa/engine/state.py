@@ -27,7 +27,7 @@ import torch
 
 from .. import parallel as P
 from ..io import fs
-from .column import Table, concat_tables
+from .column import StrColumn, Table, concat_tables
 from .types import StructType, parse_ddl_schema
 
 _writer = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dxa-state")
@@ -92,9 +92,20 @@ class StateTable:
         p = self._path(suffix, part)
         if not fs.exists(p):
             return None
+        import pyarrow.compute as pc
         import pyarrow.parquet as pq
         from ..io.arrow import table_from_arrow
-        return table_from_arrow(pq.read_table(str(fs.local_path(p))), self.schema, self.device)
+        at = pq.read_table(str(fs.local_path(p)))
+        t = table_from_arrow(at, self.schema, self.device)
+        # the string columns' longest value, read here on the host once: the per-batch UNION with this table then
+        # bounds its bytes without waiting for a device scan (strings.concat_multi)
+        arrow_name = {n.lower(): n for n in at.column_names}
+        for name, c in zip(t.names, t.columns):
+            src = arrow_name.get(name.lower())
+            if type(c) is StrColumn and src is not None and c.length:
+                m = pc.max(pc.binary_length(at.column(src))).as_py()
+                c.max_len = int(m or 0)
+        return t
 
     def _load(self, suffix: str) -> Table:
         parts_written = int(self.params.get("parts", "1"))

@@ -24,6 +24,7 @@ dictionary — is answered by the paned path, which stays the reference implemen
 from __future__ import annotations
 
 import ctypes
+import heapq
 from typing import Dict, List, Optional
 
 import torch
@@ -115,7 +116,8 @@ class DenseWindow:
         self.NB = ring_slots // BLOCK + 4              # block slots after the pane and scratch slots
         self.blocks: Dict[int, tuple] = {}             # block id → (members, block slot)
         self.layout = None              # built from the first pane's evaluated argument types
-        self.slot_of: Dict[int, tuple] = {}     # pane key → (ring slot, id of the pane's table)
+        self.slot_of: Dict[int, tuple] = {}     # pane key → (ring slot, id of the pane's table, block id, pane key)
+        self.free = list(range(ring_slots))    # free pane slots (a heap: the lowest is taken first)
         self.disabled = False
         self._pinned = [torch.empty(self.R, dtype=torch.int32, pin_memory=True) for _ in range(4)]
         self._pin_k = 0
@@ -310,9 +312,10 @@ class DenseWindow:
         pin[:len(slots)] = torch.tensor(slots, dtype=torch.int32)
         return pin[:len(slots)].to(self.device, non_blocking=True)
 
-    def block_slot(self, bid: int, members: tuple, member_slots: List[int]) -> int:
+    def block_slot(self, bid: int, mem: list) -> int:
         """The ring slot holding the pre-combined rows of a complete block of panes (combined once, when the block
-        is first complete in a window; reused until a member leaves)."""
+        is first complete in a window; reused until a member leaves).  ``mem``: the members' slot entries."""
+        members = frozenset((e[3], e[1]) for e in mem)          # (pane key, table id): order-free
         ent = self.blocks.get(bid)
         if ent is not None and ent[0] == members:
             return ent[1]
@@ -321,6 +324,7 @@ class DenseWindow:
         if not free:
             raise Ineligible("block slots")
         dst = free[0]
+        member_slots = [e[0] for e in sorted(mem, key=lambda e: e[3])]
         N.call("dxa_win_combine_block", N.ptr(self.ring), self.gcap, self.stride, N.ptr(self._dev_slots(member_slots)),
                len(member_slots), N.ptr(self.line_ops_dev), dst, N.stream_handle(self.device))
         self.blocks[bid] = (members, dst)
@@ -479,46 +483,50 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
             state = states[fp] = DenseWindow(dev, _requests(aggs), max(panes, len(pieces) + 2))
         proto = pieces[0][0].table
         gexprs = [_resolve_group_expr(g, Scope.of_table(proto, alias), items) for g in sel.group_by]
-        # ring slots: keep the slots of retained panes, recycle the rest
-        live = {p.key for p, _ in pieces} | set(store.past)
-        for k in [k for k in state.slot_of if k not in live]:
-            del state.slot_of[k]
-        used = {s for s, _ in state.slot_of.values()}
-        free = [s for s in range(state.R - SCRATCH_SLOTS) if s not in used]
+        # ring slots: a pane keeps its slot while the store retains it (panes are immutable; the table id guards a
+        # re-created pane), an expired pane's slot goes back to the free heap.  One pass over the window's panes.
+        slot_of = state.slot_of
+        past = store.past
+        for k in [k for k in slot_of if k not in past]:
+            heapq.heappush(state.free, slot_of.pop(k)[0])
         scratch = list(range(state.R - SCRATCH_SLOTS, state.R))
         slots = []
         span = BLOCK * max(1, store.interval_us)
         by_block: Dict[int, list] = {}
         for pane, full in pieces:
-            if full and pane.all_valid:
-                ent = state.slot_of.get(pane.key)
+            if full:                                   # (pieces' "full" includes every row having a timestamp)
+                ent = slot_of.get(pane.key)
                 if ent is None or ent[1] != id(pane.table):
-                    if not free:
+                    if ent is not None:
+                        heapq.heappush(state.free, ent[0])
+                        del slot_of[pane.key]
+                    if not state.free:
                         raise Ineligible("ring full")
-                    s = free.pop(0)
-                    state.accumulate(pane.table, s, alias, sel.where, gexprs, ctx)
-                    state.slot_of[pane.key] = (s, id(pane.table))
-                    ent = state.slot_of[pane.key]
-                by_block.setdefault(pane.key // span, []).append((pane.key, ent))
+                    sl = heapq.heappop(state.free)
+                    state.accumulate(pane.table, sl, alias, sel.where, gexprs, ctx)
+                    ent = slot_of[pane.key] = (sl, id(pane.table), pane.key // span, pane.key)
+                mem = by_block.get(ent[2])
+                if mem is None:
+                    by_block[ent[2]] = [ent]
+                else:
+                    mem.append(ent)
             else:
                 # a pane only partly inside the window: its in-range rows, re-aggregated into a scratch slot
                 if not scratch:
                     raise Ineligible("too many clipped panes")
-                s = scratch.pop(0)
-                state.accumulate(t.clipped(pane), s, alias, sel.where, gexprs, ctx)
-                slots.append(s)
+                sl = scratch.pop(0)
+                state.accumulate(t.clipped(pane), sl, alias, sel.where, gexprs, ctx)
+                slots.append(sl)
         # complete blocks of BLOCK consecutive panes: one pre-combined slot each (the per-batch combine then reads
         # ~20 block slots and the loose panes at the window's edges instead of 300 pane slots)
         for bid in [b for b in state.blocks if b not in by_block]:
             del state.blocks[bid]
         for bid, mem in by_block.items():
             if len(mem) == BLOCK:
-                mem.sort()
-                members = tuple((k, e[1]) for k, e in mem)
-                slots.append(state.block_slot(bid, members, [e[0] for _, e in mem]))
+                slots.append(state.block_slot(bid, mem))
             else:
                 state.blocks.pop(bid, None)
-                slots.extend(e[0] for _, e in mem)
+                slots.extend(e[0] for e in mem)
         got = state.answer(slots, partial_proto)
     except Ineligible:
         state = states.get(fp)

@@ -29,24 +29,33 @@ def _chunk_size() -> int:
 
 
 class Segments:
-    """Copy / fill segments accumulated as flat arrays (source pointer or 0 for a fill, destination pointer, bytes,
-    fill byte): a table concatenation appends one array block per column instead of a Python tuple per part."""
+    """Copy / fill segments accumulated as flat lists (source pointer or 0 for a fill, destination pointer, bytes,
+    fill byte): a table concatenation appends one block per column instead of a Python tuple per part, and the few
+    segments of a typical concatenation never pay numpy's per-call overhead until the one conversion at launch."""
 
     def __init__(self):
-        self.src: List[np.ndarray] = []
-        self.dst: List[np.ndarray] = []
-        self.nb: List[np.ndarray] = []
-        self.fill: List[np.ndarray] = []
+        self.src: List[int] = []
+        self.dst: List[int] = []
+        self.nb: List[int] = []
+        self.fill: List[int] = []
         self.keep: List[torch.Tensor] = []        # temporaries the segments read (alive until the launch is queued)
 
+    @staticmethod
+    def _as_list(v, k: int) -> List[int]:
+        if isinstance(v, (list, tuple)):
+            return [int(x) for x in v]
+        if isinstance(v, np.ndarray) and v.ndim:
+            return v.astype(np.int64, copy=False).tolist()
+        return [int(v)] * k
+
     def add(self, src, dst, nb, fill=0) -> None:
-        nb = np.asarray(nb, dtype=np.int64)
-        k = nb.shape[0] if nb.ndim else 1
-        nb = nb.reshape(k)
-        self.src.append(np.broadcast_to(np.asarray(src, dtype=np.int64), (k,)))
-        self.dst.append(np.broadcast_to(np.asarray(dst, dtype=np.int64), (k,)))
-        self.nb.append(nb)
-        self.fill.append(np.broadcast_to(np.asarray(fill, dtype=np.int64), (k,)))
+        """Scalars or length-k sequences (lists / numpy arrays); scalars repeat for every segment."""
+        nbl = self._as_list(nb, 1)
+        k = len(nbl)
+        self.nb.extend(nbl)
+        self.src.extend(self._as_list(src, k))
+        self.dst.extend(self._as_list(dst, k))
+        self.fill.extend(self._as_list(fill, k))
 
     def extend(self, segments: Sequence[Segment]) -> None:
         for src, so, dst, do, nb, fill in segments:
@@ -59,8 +68,8 @@ class Segments:
         if not self.nb:
             return
         chunk = _chunk_size()
-        src, dst = np.concatenate(self.src), np.concatenate(self.dst)
-        nb, fill = np.concatenate(self.nb), np.concatenate(self.fill)
+        src, dst = np.array(self.src, dtype=np.int64), np.array(self.dst, dtype=np.int64)
+        nb, fill = np.array(self.nb, dtype=np.int64), np.array(self.fill, dtype=np.int64)
         keep = nb > 0
         if not keep.all():
             src, dst, nb, fill = src[keep], dst[keep], nb[keep], fill[keep]
@@ -99,39 +108,43 @@ def copy_batch(segments, device) -> None:
 
 def concat_prims(parts: Sequence, device, segs: Optional[Segments] = None):
     """Row-concatenation of 1-D / [n, 2] PrimColumns of one storage dtype → (data, valid or None, segments), every
-    part's bytes as one block of segment arrays (None when the parts do not share a storage layout)."""
+    part's bytes as one block of segments (None when the parts do not share a storage layout)."""
     d0 = parts[0].data
     dt, dim, tail = d0.dtype, d0.dim(), d0.shape[1:]
-    lens = np.empty(len(parts), dtype=np.int64)
-    ptrs = np.empty(len(parts), dtype=np.int64)
+    lens, ptrs, starts = [], [], []
+    total = 0
     any_null = False
-    for k, p in enumerate(parts):
+    for p in parts:
         d = p.data
         if d.dtype != dt or d.dim() != dim or d.shape[1:] != tail or not d.is_contiguous():
             return None
-        lens[k] = p.length
-        ptrs[k] = d.data_ptr()
+        starts.append(total)
+        lens.append(p.length)
+        total += p.length
+        ptrs.append(d.data_ptr())
         any_null = any_null or p.valid is not None
-    total = int(lens.sum())
     data = torch.empty((total,) + tuple(tail), dtype=dt, device=device)
     row_bytes = d0.element_size() * (d0.shape[1] if dim == 2 else 1)
     segs = Segments() if segs is None else segs
-    starts = np.cumsum(lens) - lens
-    segs.add(ptrs, data.data_ptr() + starts * row_bytes, lens * row_bytes)
+    base = data.data_ptr()
+    segs.add(ptrs, [base + s0 * row_bytes for s0 in starts], [n * row_bytes for n in lens])
     valid = _valid_into(parts, lens, starts, total, device, segs) if any_null else None
     return data, valid, segs
 
 
 def _valid_into(parts, lens, starts, total, device, segs: Segments):
     valid = torch.empty(total, dtype=torch.bool, device=device)
-    vp = np.zeros(len(parts), dtype=np.int64)
-    for k, p in enumerate(parts):
-        if p.valid is not None:
-            v = p.valid if p.valid.is_contiguous() else p.valid.contiguous()
-            vp[k] = v.data_ptr()
-            if v is not p.valid:
-                segs.keep.append(v)                  # a contiguous copy must outlive the launch
-    segs.add(vp, valid.data_ptr() + starts, lens, np.where(vp == 0, 1, 0))
+    vp = []
+    for p in parts:
+        if p.valid is None:
+            vp.append(0)
+            continue
+        v = p.valid if p.valid.is_contiguous() else p.valid.contiguous()
+        vp.append(v.data_ptr())
+        if v is not p.valid:
+            segs.keep.append(v)                      # a contiguous copy must outlive the launch
+    base = valid.data_ptr()
+    segs.add(vp, [base + s0 for s0 in starts], list(lens), [1 if q == 0 else 0 for q in vp])
     return valid
 
 
@@ -140,6 +153,9 @@ def valid_segments(parts: Sequence, device, segs: Optional[Segments] = None):
     segs = Segments() if segs is None else segs
     if not any(p.valid is not None for p in parts):
         return None, segs
-    lens = np.fromiter((p.length for p in parts), dtype=np.int64, count=len(parts))
-    starts = np.cumsum(lens) - lens
-    return _valid_into(parts, lens, starts, int(lens.sum()), device, segs), segs
+    lens, starts, total = [], [], 0
+    for p in parts:
+        starts.append(total)
+        lens.append(p.length)
+        total += p.length
+    return _valid_into(parts, lens, starts, total, device, segs), segs

@@ -4,19 +4,20 @@
 // after a compressed H2D copy.  At ~4.5x on SimulatedData batches zstd moves ~40 % fewer PCIe bytes per event than
 // LZ4 (2.7x), which is what bounds the Kafka ingest.
 //
-// Layout: 16 lanes own one frame (4 frames per wave, 4 per 64-thread workgroup).  A frame's blocks share the window,
+// Layout: ZG = 32 lanes own one frame (2 frames per 64-thread workgroup).  A frame's blocks share the window,
 // the repeat offsets and the entropy tables (treeless literals, repeat-mode sequence tables), so one group decodes
 // the whole frame in order.  The entropy decoding is a serial chain per bitstream, so the group runs it redundantly
 // on group-uniform state; the lanes split what is parallel:
 //   * Huffman literals: the four streams of a 4-stream literals section are decoded by lanes 0..3 at once (one
 //     stream each, same instruction stream), into the TAIL of the frame's output slot — sequence execution then
 //     moves them forward (the output position never passes the unread literal, so no scratch buffer is needed);
-//   * Huffman decode-table fill (2^maxBits entries), raw / RLE block copies, literal runs and match copies, 16 bytes
+//   * Huffman decode-table fill (2^maxBits entries), raw / RLE block copies, literal runs and match copies, ZG bytes
 //     per step.  A match copy reads dst[s + (i mod off)], which is always before the copy's own start, so a copy has
 //     no internal dependency; a `s_waitcnt vmcnt(0)` makes the group's earlier stores visible only when a source
 //     reaches past the output known complete at the last wait (as lz4.hip / inflate.hip).
 //   * Tables live in LDS per group: the Huffman table (2048 x u16), the LL / ML / OF FSE tables (512 / 512 / 256
-//     cells of base | symbol | bits) and the Huffman-weight FSE table — 9.7 KiB, 4 workgroups per CU.
+//     cells of base | symbol | bits) and the Huffman-weight FSE table — 9.7 KiB per frame, 16 frames per CU (the
+//     180-VGPR kernel runs 2 waves per SIMD).
 // Bit reading: a 64-bit container over the backward bitstream (zstd's BIT_DStream shape): n bits are the container's
 // top bits after `consumed`, reloaded from 8 bytes further back when more than 64 would be needed; bits below the
 // stream start read as zeros and leave the remaining count negative (the overflow the weight decoder and the
@@ -28,8 +29,14 @@
 
 namespace {
 
-constexpr int ZG = 16;                  // lanes per frame
-constexpr int ZWG = 64;                 // threads per workgroup: 4 frames
+// lanes per frame: 32, two frames per wave (profiles/round6/codecs/README.md: 16 lanes put 4 divergent frames in a
+// wave at one wave per SIMD; 32 halves the divergence and doubles the waves per SIMD for the same frames per CU)
+#ifndef DXA_ZSTD_ZG
+#define DXA_ZSTD_ZG 32
+#endif
+constexpr int ZG = DXA_ZSTD_ZG;         // a power of two, at most a wave
+constexpr uint64_t kGroupMask = ZG == 64 ? ~0ull : ((1ull << ZG) - 1);
+constexpr int ZWG = 64;                 // threads per workgroup: ZWG / ZG frames
 constexpr int kWaitVm0 = 0xF70;         // s_waitcnt vmcnt(0) (gfx9 encoding)
 constexpr int32_t kBlockMax = 128 * 1024;
 
@@ -478,7 +485,7 @@ __device__ int32_t decode_block(const uint8_t* in, int32_t n, uint8_t* out, int3
     // every lane learns whether any stream failed; the literals become visible to the group
     const uint64_t bad = __ballot(!ok);
     const int grp = (int)((threadIdx.x & 63) & ~(ZG - 1));
-    if ((bad >> grp) & 0xFFFFull) return Z_HUF;
+    if ((bad >> grp) & kGroupMask) return Z_HUF;
     stores_visible();
     lit = lbuf;
     if (pf.on) { const int64_t t = Prof::now(); pf.v[P_LITS] += t - t0; t0 = t; }

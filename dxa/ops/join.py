@@ -30,6 +30,7 @@ class BuiltSide:
     start: Optional[torch.Tensor] = None
     rows: Optional[torch.Tensor] = None
     null_rows: Optional[torch.Tensor] = None
+    max_mult: Optional[int] = None          # most build rows behind one hash (read once, on a cached build side)
 
 
 def _any_null(cols) -> Optional[torch.Tensor]:
@@ -177,6 +178,37 @@ def keys_equal(lcols: List, rcols: List, li: torch.Tensor, ri: torch.Tensor) -> 
     return ok & has
 
 
+def _unique_join(built: BuiltSide, lkeys: List, rkeys: List, kind: str) -> Tuple[torch.Tensor, torch.Tensor]:
+    """A build side with at most one row per hash (a keyed reference table): every probe row has one candidate or
+    none, so the pairs are positional — (i, candidate or -1) — with no count pass.  A left join reads nothing back;
+    inner / semi / anti read one count."""
+    keys = _flat_keys(lkeys)
+    n = keys[0].length
+    device = keys[0].device
+    st = N.stream_handle(device)
+    h = hash_columns(keys)
+    pnull = _any_null(keys)
+    slot = torch.empty(n, dtype=torch.int32, device=device)
+    ocnt = torch.empty(n, dtype=torch.int64, device=device)
+    N.call("dxa_probe_count", N.ptr(h), N.ptr(N.u8(pnull)), n, N.ptr(built.table), built.cap, N.ptr(built.cnt),
+           N.ptr(slot), N.ptr(ocnt), 1, st)
+    off = torch.arange(n, dtype=torch.int64, device=device)    # outer counts are all 1: row i writes pair i
+    li = torch.empty(n, dtype=torch.int64, device=device)
+    ri = torch.empty(n, dtype=torch.int64, device=device)
+    N.call("dxa_probe_write", N.ptr(slot), n, N.ptr(off), N.ptr(built.start), N.ptr(built.cnt), N.ptr(built.rows),
+           N.ptr(li), N.ptr(ri), 1, st)
+    ok = keys_equal(lkeys, rkeys, li, ri)
+    if kind == "left":
+        return li, torch.where(ok, ri, torch.full_like(ri, -1))
+    if kind == "anti":
+        idx = torch.nonzero(~ok).flatten()
+        return idx, torch.full_like(idx, -1)
+    keep = torch.nonzero(ok).flatten()
+    if kind == "semi":
+        return keep, torch.full_like(keep, -1)
+    return keep, ri[keep]
+
+
 def hash_join(lkeys: List, rkeys: List, kind: str, built: Optional[BuiltSide] = None
               ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Row pairs of an equi-join.  kind: inner | left | right | full | semi | anti.  -1 marks a missing side."""
@@ -187,6 +219,11 @@ def hash_join(lkeys: List, rkeys: List, kind: str, built: Optional[BuiltSide] = 
         return l, r
     if built is None:
         built = build_side(rkeys)
+    elif kind in ("inner", "left", "semi", "anti") and _on_gpu(device) and built.n and nl:
+        if built.max_mult is None:
+            built.max_mult = int(built.cnt.max())       # once per cached (stream-static) build side
+        if built.max_mult <= 1:
+            return _unique_join(built, lkeys, rkeys, kind)
     li, ri = probe(built, lkeys, outer=False)
     ok = keys_equal(lkeys, rkeys, li, ri)
     keep = torch.nonzero(ok).flatten()          # one count read for both sides (two boolean indexings read twice)

@@ -140,11 +140,12 @@ def concat_multi(groups: Sequence[Sequence]):
                  torch.zeros(0, dtype=torch.int32, device=device)) for _ in groups]
     cs = torch.cumsum(lens_all, 0, dtype=torch.int64)
     ex = cs - lens_all
-    if all(getattr(c, "_compact", False) or c.max_len is not None for c in flat):
+    if all(c.length == 0 or getattr(c, "_compact", False) or c.max_len is not None for c in flat):
         # every part's bytes are bounded on the host — a compacted arena holds exactly its rows' bytes (window
-        # panes), rows with a known length bound (a window dictionary's key slots) at most rows x bound — so the
-        # batch thread does not wait for the scan
-        total = sum(int(c.arena.numel()) if getattr(c, "_compact", False) else c.length * c.max_len for c in flat)
+        # panes), rows with a known length bound (a window dictionary's key slots) at most rows x bound, an empty
+        # part none — so the batch thread does not wait for the scan
+        total = sum(0 if c.length == 0 else int(c.arena.numel()) if getattr(c, "_compact", False)
+                    else c.length * c.max_len for c in flat)
     else:
         total = int(cs[-1].item())
     dst = _alloc_arena(total, device)

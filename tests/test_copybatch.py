@@ -98,3 +98,16 @@ def test_chunk_rows_split_segments_cpu():
             assert (mine[:, 0] - src[k] == mine[:, 1] - dst[k]).all()
     one = chunk_rows(src, dst, nb, fill, 64)
     assert one.shape == (4, 4) and (one[:, 2] == nb).all()
+
+
+def test_segments_accumulate_scalars_lists_and_arrays_cpu():
+    """Segments.add takes scalars (repeated per segment), lists and numpy arrays; launch converts once."""
+    import numpy as np
+    from dxa.ops.copybatch import Segments
+    sg = Segments()
+    sg.add(0, 100, 8, 1)                                     # one fill segment
+    sg.add([10, 20], np.array([200, 300]), np.array([4, 0]))  # two copies, one empty
+    sg.add(np.array([5]), 400, [16], np.array([0]))
+    assert sg.src == [0, 10, 20, 5] and sg.dst == [100, 200, 300, 400]
+    assert sg.nb == [8, 4, 0, 16] and sg.fill == [1, 0, 0, 0]
+    assert all(isinstance(v, int) for v in sg.src + sg.dst + sg.nb + sg.fill)

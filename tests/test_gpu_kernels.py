@@ -154,6 +154,25 @@ def test_join_matches_cpu(gpu, kind):
     assert pa == pb
 
 
+@pytest.mark.parametrize("kind", ["inner", "left", "semi", "anti"])
+@pytest.mark.parametrize("unique", [True, False])
+def test_cached_build_join_matches_cpu(gpu, kind, unique):
+    """A cached build side (stream–static join): a keyed table takes the positional one-candidate path
+    (join.py _unique_join), a table with duplicate keys the count / write path; both against the CPU join."""
+    rnd = random.Random(2)
+    lk = [rnd.randrange(500) for _ in range(3000)] + [None]
+    rk = (rnd.sample(range(400), 350) if unique else [rnd.randrange(400) for _ in range(700)]) + [None]
+    lc = [column_from_pylist(lk, "long"), strings_from_pylist([None if k is None else f"s{k}" for k in lk], "cpu")]
+    rc = [column_from_pylist(rk, "long"), strings_from_pylist([None if k is None else f"s{k}" for k in rk], "cpu")]
+    a = J.hash_join(lc, rc, kind)
+    glc, grc = [c.to(gpu) for c in lc], [c.to(gpu) for c in rc]
+    built = J.build_side(grc)
+    for _ in range(2):                              # the multiplicity is read on first use, then reused
+        b = J.hash_join(glc, grc, kind, built)
+        assert (built.max_mult <= 1) == unique
+        assert sorted(zip(a[0].tolist(), a[1].tolist())) == sorted(zip(b[0].cpu().tolist(), b[1].cpu().tolist()))
+
+
 def test_string_ops_match_cpu(gpu):
     vals = ["DoorLock", "Door", "", "Heating", None, "doorlock", "Zebra", "DoorLocks"]
     c = strings_from_pylist(vals, "cpu")
