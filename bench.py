@@ -175,6 +175,9 @@ def main():
                     help="HIP priority of the stream the batch's statements run on: high lets the critical path's "
                          "short kernels (and the syncs waiting on them) go ahead of the ingest / generator / "
                          "parse-ahead streams, which stay at normal priority and fill the rest of the chip")
+    ap.add_argument("--switch-interval-ms", type=float, default=None,
+                    help="the interpreter's GIL switch interval (default: Python's 5 ms); the batch thread shares the "
+                         "GIL with the output, state-writer and planner threads")
     ap.add_argument("--profile-stages", action="store_true")
     ap.add_argument("--sync-outputs", action="store_true",
                     help="finish each batch's sink writes before the next batch starts (default: pipelined)")
@@ -540,6 +543,8 @@ def main():
 
     from dxa.utils import settle_gc
     settle_gc()
+    if args.switch_interval_ms is not None:
+        sys.setswitchinterval(args.switch_interval_ms / 1e3)
     depth = max(1, args.prefetch)
     for i in range(depth):
         stage(i)
@@ -650,7 +655,8 @@ def main():
                    "outputs": "sync" if args.sync_outputs else (
                        "pipelined (batch t sinks overlap batch t+1)" if proc.output_depth == 1 else
                        f"pipelined, {proc.output_depth} batches' outputs in flight"),
-                   "sink": args.sink, "compute_stream_priority": args.compute_priority},
+                   "sink": args.sink, "compute_stream_priority": args.compute_priority,
+                   "gil_switch_interval_ms": round(sys.getswitchinterval() * 1e3, 3)},
         "p50_latency_process_ms": pct(50),
         "p99_latency_process_ms": pct(99),
         "p50_latency_batch_ms": pct(50, latb_sorted),

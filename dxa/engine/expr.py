@@ -47,6 +47,7 @@ class EvalContext:
     udafs: Dict[str, Any] = field(default_factory=dict)
     device: Any = "cpu"
     catalog: Any = None                   # tables visible to sub-queries (set by query.execute)
+    prefilter: Dict[int, Any] = field(default_factory=dict)   # id(Select) → early WHERE mask (query.prefilter)
 
 
 class TakenColumns(LazyColumns):

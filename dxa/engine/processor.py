@@ -34,7 +34,7 @@ from ..ops.jsonparse import ParsePlan, parse, parse_async
 from ..sql.transform import COMMAND_COMMAND, parse_transform
 from .column import ConstColumn, PrimColumn, StructColumn, Table, concat_tables
 from .expr import EvalContext, EvalError
-from .query import Catalog, execute, run_sql
+from .query import Catalog, execute, prefilter, run_sql
 from .serialize import table_to_json_lines
 from .state import create_state_tables
 from .types import MapType, StructType, schema_from_json
@@ -427,7 +427,14 @@ class Processor:
         if self.transform is not None:
             live = None if self.keep_views else self._live_statements()
             cmds = self.transform.commands
-            for step in self._view_schedule(live):
+            schedule = list(self._view_schedule(live))
+            if self.device.type == "cuda" and not any(cmds[k].command_type == COMMAND_COMMAND
+                                                       for step in schedule for k in step):
+                # the WHERE masks of statements over tables present now, with one count read for all of them
+                # (not with SET / CREATE commands in the batch: those run first and may change what a predicate means)
+                with tracing.host_section("prefilter"):
+                    prefilter([self._query(cmds[k]) for step in schedule for k in step], cat, ctx)
+            for step in schedule:
                 if len(step) > 1:
                     # independent views: each on a side HIP stream, forked from and joined back to this stream
                     results = self._run_concurrent([cmds[k] for k in step], cat, ctx)

@@ -811,10 +811,8 @@ class _JoinColumns(LazyColumns):
 # ---------------------------------------------------------------------------------------------------------------
 
 def _contains_agg(e: A.Expr, ctx) -> bool:
-    for node in A.walk(e):
-        if isinstance(node, A.Call) and (node.name in AGG_FUNCS or node.name in ctx.udafs):
-            return True
-    return False
+    calls = A.summary(e)[0]
+    return any(n in AGG_FUNCS or n in ctx.udafs for n in calls)
 
 
 def _collect_aggs(e: A.Expr, ctx, out: Dict):
@@ -868,8 +866,7 @@ def _expand_call_stars(e: A.Expr, scope: Scope) -> A.Expr:
 
 
 def _has_call_star(e: A.Expr) -> bool:
-    return any(isinstance(x, A.Call) and ((x.star and x.name != "count") or any(isinstance(a, A.Star) for a in x.args))
-               for x in A.walk(e))
+    return A.summary(e)[2]
 
 
 def _expand_items(sel: A.Select, scope: Scope) -> List[Tuple[A.Expr, str]]:
@@ -1199,6 +1196,67 @@ def _exec_grouping_sets(sel: A.Select, catalog, ctx):
     return distinct(out) if sel.distinct else out
 
 
+class _Prefiltered:
+    """A statement's WHERE mask evaluated at the start of the batch, its row count on its way to pinned memory."""
+    __slots__ = ("sel", "table", "mask", "counts", "k", "event")
+
+    def __init__(self, sel, table, mask, counts, k, event):
+        self.sel, self.table, self.mask, self.counts, self.k, self.event = sel, table, mask, counts, k, event
+
+    def indices(self) -> torch.Tensor:
+        self.event.synchronize()          # long complete by the time the statement runs: no queue drain
+        n = int(self.counts[self.k])
+        return torch.nonzero_static(self.mask, size=n).flatten()
+
+
+def _plain_predicate(e: A.Expr, ctx) -> bool:
+    """A WHERE that reads only its row (no sub-query, window or aggregate): evaluable before its statement runs."""
+    calls, wins, _star = A.summary(e)
+    if wins or any(n in AGG_FUNCS or n in ctx.udafs for n in calls):
+        return False
+    return not any(isinstance(n, A.SubqueryExpr) for n in A.walk(e))
+
+
+def prefilter(queries, catalog, ctx) -> None:
+    """Evaluate the WHERE of every statement that filters a table already in ``catalog`` (the batch's input view,
+    reference and state tables) at the start of the batch, and bring all their row counts to pinned memory with ONE
+    copy.  Each such statement later reads its count without draining the stream (``_Prefiltered.indices``), where a
+    filter otherwise waits for its own mask kernels (``torch.nonzero``) — the rule alerts' filters of the full flow.
+    Each predicate is still evaluated exactly once; statements whose predicate does not evaluate here keep the
+    usual path (and report their error there)."""
+    from .windows import PanedTable
+    found = []
+    for q in queries:
+        if q is None or q.ctes or not isinstance(q.body, A.Select):
+            continue
+        sel = q.body
+        src = sel.from_
+        if sel.where is None or sel.grouping_sets is not None or not isinstance(src, A.TableRef) or src.sample or \
+                src.timewindow:
+            continue
+        t = catalog.get(src.name)
+        if t is None or t.device.type != "cuda" or not _plain_predicate(sel.where, ctx):
+            continue
+        if isinstance(t, PanedTable) and (sel.group_by or any(
+                not isinstance(it.expr, A.Star) and _contains_agg(it.expr, ctx) for it in sel.items)):
+            continue                       # a windowed aggregate: the paned / dense path applies WHERE per pane
+        try:
+            scope = Scope.of_table(t, src.alias or src.name.split(".")[-1])
+            mask = predicate_mask(evaluate(sel.where, scope, ctx))
+        except Exception:  # noqa: BLE001 — the statement's own evaluation reports it
+            continue
+        found.append((sel, t, mask))
+    if not found:
+        return
+    dev = found[0][2].device
+    counts = torch.empty(len(found), dtype=torch.int64, pin_memory=True)
+    counts.copy_(torch.stack([m.sum() for _, _, m in found]), non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    for k, (sel, t, mask) in enumerate(found):
+        ctx.prefilter[id(sel)] = _Prefiltered(sel, t, mask, counts, k, ev)
+
+
 def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     if sel.grouping_sets is not None:
         return _exec_grouping_sets(sel, catalog, ctx), None
@@ -1215,9 +1273,14 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     scope = _relation(sel.from_, catalog, ctx)
     sdist = getattr(scope, "dist", P.REPLICATED)
     if sel.where is not None:
-        scope.prefetch([sel.where])
-        mask = predicate_mask(evaluate(sel.where, scope, ctx))
-        idx = torch.nonzero(mask).flatten()
+        pf = ctx.prefilter.pop(id(sel), None) if ctx.prefilter else None
+        if pf is not None and pf.sel is sel and pf.table is _lookup(sel.from_, catalog) and \
+                pf.mask.shape[0] == scope.length:
+            idx = pf.indices()
+        else:
+            scope.prefetch([sel.where])
+            mask = predicate_mask(evaluate(sel.where, scope, ctx))
+            idx = torch.nonzero(mask).flatten()
         scope = Scope(scope.names, TakenColumns(scope.cols, idx), scope.quals, int(idx.shape[0]), scope.device)
         scope.dist = sdist
     # the columns the statement reads in one gather (a SELECT * stays deferred: its consumer may read few columns)
@@ -1289,6 +1352,8 @@ def _sliding_windows(sel: A.Select, scope: Scope, ctx):
     exprs = [it.expr for it in sel.items] + list(sel.group_by) + ([sel.having] if sel.having is not None else [])
     found = {}
     for e in exprs:
+        if "window" not in A.summary(e)[0]:
+            continue
         for node in A.walk(e):
             if isinstance(node, A.Call) and node.name == "window" and len(node.args) >= 3:
                 size, slide, _ = SF.window_params(node, scope, ctx)

@@ -40,11 +40,7 @@ class WindowError(Exception):
 
 
 def window_calls(e: A.Expr) -> List[A.WindowCall]:
-    out = []
-    for node in A.walk(e):
-        if isinstance(node, A.WindowCall):
-            out.append(node)
-    return out
+    return list(A.summary(e)[1])
 
 
 def _sort_key(col: Column):

@@ -343,10 +343,39 @@ class LateralView:
 
 
 def walk(e: Expr):
-    """Pre-order traversal of an expression tree."""
-    yield e
-    for c in e.children():
-        yield from walk(c)
+    """Pre-order traversal of an expression tree (an explicit stack: no generator chain per tree level)."""
+    stack = [e]
+    pop, extend = stack.pop, stack.extend
+    while stack:
+        n = pop()
+        yield n
+        ch = n.children()
+        if ch:
+            extend(reversed(ch))
+
+
+_SUMMARY: dict = {}
+
+
+def summary(e: Expr):
+    """(names of the calls in ``e``, its window calls, whether a call takes a ``*`` argument) — read by every
+    statement of every batch, computed once per expression node (statement ASTs live for the flow)."""
+    got = _SUMMARY.get(id(e))
+    if got is not None and got[0] is e:
+        return got[1]
+    calls, wins, star = set(), [], False
+    for n in walk(e):
+        if isinstance(n, Call):
+            calls.add(n.name)
+            if not star and ((n.star and n.name != "count") or any(isinstance(a, Star) for a in n.args)):
+                star = True
+        elif isinstance(n, WindowCall):
+            wins.append(n)
+    out = (frozenset(calls), tuple(wins), star)
+    if len(_SUMMARY) >= 8192:
+        _SUMMARY.clear()
+    _SUMMARY[id(e)] = (e, out)
+    return out
 
 
 def replace(e, fn):

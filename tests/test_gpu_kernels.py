@@ -640,3 +640,30 @@ def test_parser_null_strings_are_empty_views(gpu):
             assert int(null.sum()) > 100
             assert int(c.lens.cpu()[null].abs().sum()) == 0
             assert int(c.starts.cpu()[null].abs().sum()) == 0
+
+
+def test_prefiltered_where_matches_plain_filter(gpu):
+    """query.prefilter: WHERE masks of statements over present tables evaluated at batch start with one count
+    copy; the statement then takes its rows without a stream drain, and the result equals the plain filter."""
+    from dxa.engine.query import execute, prefilter
+    from dxa.sql.parser import parse_query
+    rnd = random.Random(3)
+    n = 5000
+    a = [None if rnd.random() < 0.05 else rnd.randint(0, 20) for _ in range(n)]
+    b = [rnd.choice(["x", "yy", None, "zzz"]) for _ in range(n)]
+    t = Table(["a", "b"], [column_from_pylist(a, "long", gpu), strings_from_pylist(b, gpu)], n, gpu)
+    qs = [parse_query("SELECT a, b FROM T WHERE a > 5 AND b IS NOT NULL"),
+          parse_query("SELECT b, a * 2 AS a2 FROM T WHERE length(b) = 2 OR a IS NULL"),
+          parse_query("SELECT COUNT(*) AS c FROM T WHERE a < 3"),
+          parse_query("SELECT a FROM T WHERE a IN (SELECT a FROM T WHERE a = 1)")]     # sub-query: not early
+    cat = Catalog()
+    cat.register("T", t)
+    ctx = EvalContext(device=gpu)
+    prefilter(qs, cat, ctx)
+    assert {id(q.body) for q in qs[:3]} == set(ctx.prefilter)
+    got = [execute(q, cat, ctx) for q in qs]
+    assert not ctx.prefilter                                      # every early mask was consumed
+    want = [execute(q, cat, EvalContext(device=gpu)) for q in qs]
+    for g, w in zip(got, want):
+        assert g.names == w.names and g.length == w.length
+        assert [c.to_pylist() for c in g.columns] == [c.to_pylist() for c in w.columns]
