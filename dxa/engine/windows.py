@@ -98,7 +98,8 @@ def _str_lens_all(t: Table):
         _str_leaves(c, leaves)
     if len(leaves) < 2:
         return None
-    return torch.cat([c.lens for c in leaves])
+    from ..ops.strings import lens_concat
+    return lens_concat([c.lens for c in leaves])
 
 
 @dataclass

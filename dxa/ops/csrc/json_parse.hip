@@ -1200,6 +1200,30 @@ __global__ __launch_bounds__(256) void write_newlines_bits_kernel(const uint16_t
   }
 }
 
+// Zero `nbytes` at `p` with 16-byte stores (the runtime's byte-pattern fill ran at ~0.3 TB/s on the validity planes:
+// ~125 us per 33 MB plane per batch, profiles/round6/parse/README.md).  Head / tail bytes outside the aligned body
+// are stored singly.
+__global__ void zero_bytes_kernel(uint8_t* __restrict__ p, int64_t nbytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const int64_t head = (int64_t)((16 - (a & 15)) & 15) < nbytes ? (int64_t)((16 - (a & 15)) & 15) : nbytes;
+  const int64_t body = (nbytes - head) / 16;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  for (int64_t i = tid; i < body; i += stride) q[i] = make_uint4(0, 0, 0, 0);
+  const int64_t tail0 = head + body * 16;
+  if (tid < head) p[tid] = 0;
+  if (tid < nbytes - tail0) p[tail0 + tid] = 0;
+}
+
+hipError_t zero_bytes(uint8_t* p, int64_t nbytes, hipStream_t s) {
+  if (nbytes <= 0) return hipSuccess;
+  const int64_t body = nbytes / 16 + 1;
+  const int64_t blocks = (body + 255) / 256 < 4096 ? (body + 255) / 256 : 4096;
+  hipLaunchKernelGGL(zero_bytes_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, nbytes);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const uint64_t* lut_keys,
@@ -1217,10 +1241,10 @@ DXA_API int dxa_json_parse(uint8_t* buf, const int64_t* offs, int64_t n, const u
               valid, row_ok, first_child, next_sib, key_word, key_len, key_words, nkey_words, ends, vals2, lens2,
               valid2, nkv, nkl, nkn, zslots, nz};
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(valid, 0, (size_t)nkn * (size_t)n, s);
+  hipError_t e = zero_bytes(valid, (int64_t)nkn * n, s);
   if (e != hipSuccess) return (int)e;
   if (nnodes > nkn) {
-    e = hipMemsetAsync(valid2, 0, (size_t)(nnodes - nkn) * (size_t)n, s);
+    e = zero_bytes(valid2, (int64_t)(nnodes - nkn) * n, s);
     if (e != hipSuccess) return (int)e;
   }
   const int block = 256;

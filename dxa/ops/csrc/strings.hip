@@ -170,6 +170,10 @@ struct StrPart {
   const int64_t* dst_off;
   uint8_t* dst;
   int64_t row0;
+  // compaction form (dst_off null): the destination offset is incl[r] - lens[r] of an inclusive byte scan, and is
+  // also stored to ex_out[r] (the compacted column's starts) — no separate subtraction pass
+  const int64_t* incl;
+  int64_t* ex_out;
 };
 
 struct StrParts {
@@ -190,7 +194,14 @@ __global__ __launch_bounds__(256) void str_gather_parts_kernel(const StrParts a)
     const int64_t r = i - P.row0;
     l = P.lens[r];
     s = (const SG1 uint8_t*)P.arena + P.starts[r];
-    d = (SG1 uint8_t*)P.dst + P.dst_off[r];
+    int64_t doff;
+    if (P.dst_off) {
+      doff = P.dst_off[r];
+    } else {
+      doff = P.incl[r] - (int64_t)l;
+      P.ex_out[r] = doff;
+    }
+    d = (SG1 uint8_t*)P.dst + doff;
   }
   const bool lng = l > 128;
   if (!lng && l > 0) copy_short(s, d, l);

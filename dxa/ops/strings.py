@@ -73,12 +73,15 @@ def compact_known(col, total: int):
 
 class _StrPart(ctypes.Structure):
     _fields_ = [("arena", ctypes.c_void_p), ("starts", ctypes.c_void_p), ("lens", ctypes.c_void_p),
-                ("dst_off", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row0", ctypes.c_int64)]
+                ("dst_off", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row0", ctypes.c_int64),
+                ("incl", ctypes.c_void_p), ("ex_out", ctypes.c_void_p)]
 
 
 def _gather_parts(parts, device) -> None:
     """One ``dxa_str_gather_parts`` launch (per 32 parts) for many string gathers.  ``parts``: (StrColumn view,
-    destination offsets tensor, destination arena) triples; offsets are per row of the part."""
+    destination offsets tensor, destination arena) triples; offsets are per row of the part — or (StrColumn view,
+    (inclusive byte scan, starts out), destination arena): the kernel derives each row's offset from the scan and
+    stores it as the compacted column's starts."""
     parts = [p for p in parts if p[0].length]
     if not parts:
         return
@@ -87,11 +90,33 @@ def _gather_parts(parts, device) -> None:
     arr = (_StrPart * (len(parts) + 1))()
     row = 0
     for j, (c, off, dst) in enumerate(parts):
-        arr[j] = _StrPart(c.arena.data_ptr(), c.starts.data_ptr(), c.lens.data_ptr(), off.data_ptr(),
-                          dst.data_ptr(), row)
+        if isinstance(off, tuple):
+            incl, ex = off
+            arr[j] = _StrPart(c.arena.data_ptr(), c.starts.data_ptr(), c.lens.data_ptr(), None, dst.data_ptr(), row,
+                              incl.data_ptr(), ex.data_ptr())
+        else:
+            arr[j] = _StrPart(c.arena.data_ptr(), c.starts.data_ptr(), c.lens.data_ptr(), off.data_ptr(),
+                              dst.data_ptr(), row, None, None)
         row += c.length
     arr[len(parts)].row0 = row                      # end sentinel
     N.call("dxa_str_gather_parts", ctypes.cast(arr, ctypes.c_void_p), len(parts), N.stream_handle(device))
+
+
+def lens_concat(lens: Sequence[torch.Tensor]) -> torch.Tensor:
+    """The rows' lengths of several string columns end to end (int32).  Columns parsed from one batch hold their
+    lengths as consecutive full-width rows of the parser's length matrix: then this is a view of that block, not a
+    copy (a 1 M-event batch's five string leaves: a 20 MB concatenation kernel per batch)."""
+    if len(lens) > 1 and all(t.dtype == torch.int32 and t.dim() == 1 and t.is_contiguous() for t in lens):
+        base = lens[0]
+        step = base.shape[0] * 4
+        p0 = base.data_ptr()
+        st = base.untyped_storage()
+        if all(t.shape[0] == base.shape[0] and t.data_ptr() == p0 + k * step and
+               t.untyped_storage().data_ptr() == st.data_ptr() for k, t in enumerate(lens)):
+            end = base.storage_offset() + len(lens) * base.shape[0]
+            if end * 4 <= st.nbytes():
+                return torch.as_strided(base, (len(lens) * base.shape[0],), (1,), base.storage_offset())
+    return torch.cat(list(lens))
 
 
 def compact_many(cols: Sequence, lens_all: Optional[torch.Tensor] = None, total: Optional[int] = None) -> list:
@@ -109,18 +134,18 @@ def compact_many(cols: Sequence, lens_all: Optional[torch.Tensor] = None, total:
     if total_rows == 0:
         return [compact(c) for c in cols]
     if lens_all is None:
-        lens_all = torch.cat([c.lens for c in cols])
+        lens_all = lens_concat([c.lens for c in cols])
     cs = torch.cumsum(lens_all, 0, dtype=torch.int64)
-    ex = cs - lens_all
+    ex = torch.empty_like(cs)                      # the compacted starts: written by the gather (cs - lens)
     if total is None:
         total = int(cs[-1].item())
     dst = _alloc_arena(total, device)
     out, parts, r = [], [], 0
     for c in cols:
         off = ex[r:r + c.length]
-        r += c.length
         if c.length:
-            parts.append((c, off, dst))
+            parts.append((c, (cs[r:r + c.length], off), dst))
+        r += c.length
         o = type(c)(dst, off, c.lens, c.valid, c.dtype)
         o._compact = True
         out.append(o)
