@@ -742,6 +742,35 @@ class Table:
         return f"Table(n={self.length}, cols={self.names})"
 
 
+class DeferredTable(Table):
+    """A statement's result whose host-side completion — a status read behind its own kernels — runs on first use
+    of any attribute (``length``, ``columns``, ``names``, ``dist`` …); it then becomes the completed table (its class
+    and attributes).  The batch thread plans the statements that do not read it in the meantime, so the read finds
+    the kernels done instead of draining the stream (query._exec_select, processor.route)."""
+
+    def __init__(self, finish):                 # noqa: no Table.__init__: every attribute comes from ``finish``
+        self.__dict__["_finish"] = finish
+
+    def resolve(self) -> Table:
+        f = self.__dict__.pop("_finish", None)
+        if f is None:
+            return self
+        t = f()
+        if isinstance(t, DeferredTable):
+            t = t.resolve()
+        extra = dict(self.__dict__)            # attributes set while pending win over the completed table's
+        self.__class__ = type(t)
+        self.__dict__.update(t.__dict__)
+        self.__dict__.update(extra)
+        return self
+
+    def __getattr__(self, name):
+        if name != "_finish" and "_finish" in self.__dict__:
+            self.resolve()
+            return getattr(self, name)
+        raise AttributeError(name)
+
+
 def concat_tables(tables: List[Table]) -> Table:
     tables = [t for t in tables]
     if not tables:

@@ -32,7 +32,7 @@ from ..config.secrets import resolve
 from ..io import fs
 from ..ops.jsonparse import ParsePlan, parse, parse_async
 from ..sql.transform import COMMAND_COMMAND, parse_transform
-from .column import ConstColumn, PrimColumn, StructColumn, Table, concat_tables
+from .column import ConstColumn, DeferredTable, PrimColumn, StructColumn, Table, concat_tables
 from .expr import EvalContext, EvalError
 from .query import Catalog, execute, prefilter, run_sql
 from .serialize import table_to_json_lines
@@ -428,12 +428,14 @@ class Processor:
             live = None if self.keep_views else self._live_statements()
             cmds = self.transform.commands
             schedule = list(self._view_schedule(live))
-            if self.device.type == "cuda" and not any(cmds[k].command_type == COMMAND_COMMAND
-                                                       for step in schedule for k in step):
+            # windowed GROUP BYs may complete lazily (one rank, sequential views): see query._deferred_select
+            defer_ok = self.device.type == "cuda" and not P.active() and not self._concurrent_views()
+            if self.device.type == "cuda":
                 # the WHERE masks of statements over tables present now, with one count read for all of them
-                # (not with SET / CREATE commands in the batch: those run first and may change what a predicate means)
+                # (command statements change nothing a predicate reads: _run_command)
                 with tracing.host_section("prefilter"):
-                    prefilter([self._query(cmds[k]) for step in schedule for k in step], cat, ctx)
+                    prefilter([self._query(cmds[k]) for step in schedule for k in step
+                               if cmds[k].command_type != COMMAND_COMMAND], cat, ctx)
             for step in schedule:
                 if len(step) > 1:
                     # independent views: each on a side HIP stream, forked from and joined back to this stream
@@ -444,8 +446,12 @@ class Processor:
                         self._run_command(cmd.text)
                         continue
                     ts = time.perf_counter()
+                    q = self._query(cmd)
+                    ctx.defer_dense = defer_ok and not (q.order_by or q.limit is not None or q.sort_by or
+                                                        q.distribute_by)
                     with tracing.stage(f"sql:{cmd.name}"):
-                        results = [execute(self._query(cmd), cat, ctx)]
+                        results = [execute(q, cat, ctx)]
+                    ctx.defer_dense = False
                     self.host_acc[f"sql:{cmd.name}"] += time.perf_counter() - ts
                     if _SYNC_STAGES:
                         self._sync()
@@ -460,6 +466,11 @@ class Processor:
                             result = st.overwrite(result, tag=batch_time_us)
                     cat.register(cmd.name, result)
                     views[cmd.name] = result
+            with tracing.host_section("deferred:finish"):
+                while ctx.pending:                  # results no later statement read: complete them now
+                    d = ctx.pending.pop(0)
+                    if isinstance(d, DeferredTable):
+                        d.resolve()
         self._sync()
         self.stage_times["transform"] = time.perf_counter() - t0
         # outputs: device half staged here (filters + async D2H into pinned memory), host half (JSON rendering +
@@ -550,7 +561,7 @@ class Processor:
         if getattr(self, "_sched", (None,))[0] == key:
             return self._sched[1]
         cmds = self.transform.commands
-        if not key[2]:
+        if not key[2] and self.window_store is None:
             steps = [[k] for k, c in enumerate(cmds)
                      if c.command_type == COMMAND_COMMAND or live is None or k in live]
             self._sched = (key, steps)
@@ -585,7 +596,9 @@ class Processor:
             ks = [k for k in sorted(lv) if lv[k] == L]
             plain = [k for k in ks if cmds[k].name not in self.state_tables]
             if plain:
-                steps.append(plain)
+                # sequential mode with a window: one statement per step, level by level — a windowed statement's
+                # readers run after the statements that do not read it, while its kernels finish (DeferredTable)
+                steps += [plain] if key[2] else [[k] for k in plain]
             steps += [[k] for k in ks if cmds[k].name in self.state_tables]
         self._sched = (key, steps)
         return steps

@@ -20,8 +20,8 @@ from ..ops.hashing import hash_columns
 from ..sql import ast as A
 from ..sql.parser import parse_query
 from ..telemetry.tracing import host_section
-from .column import (ArrayColumn, Column, ConstColumn, LazyColumns, PrimColumn, StrColumn, StructColumn, Table,
-                     concat_columns, concat_tables, materialize, take_columns)
+from .column import (ArrayColumn, Column, ConstColumn, DeferredTable, LazyColumns, PrimColumn, StrColumn,
+                     StructColumn, Table, concat_columns, concat_tables, materialize, take_columns)
 from .expr import (AGG_FUNCS, DeferredColumns, EvalContext, EvalError, HiddenQual, Scope, TakenColumns, cast_column,
                    evaluate, output_name, predicate_mask)
 from . import windowfn as W
@@ -979,8 +979,17 @@ def _paned_aggregate(sel: A.Select, t, alias: str, ctx) -> Optional[Table]:
                     out_keys, finals, ng = D.merge_partials(got, plan, key_names, aggs, True)
                 return _paned_output(sel, items, out_keys, finals, ng, gexprs, proto.device, tag, ctx)
         else:
+            defer = ctx.defer_dense
             with host_section("paned:dense"):
-                got = dense_answer(t, sel, alias, ctx, items, aggs, fp)
+                got = dense_answer(t, sel, alias, ctx, items, aggs, fp, defer=defer)
+            if callable(got):
+                def finish():
+                    res = got()
+                    if res is None:
+                        return None                 # collision / overflow: the caller re-runs the paned path
+                    out_keys, finals, ng, gexprs = res
+                    return _paned_output(sel, items, out_keys, finals, ng, gexprs, proto.device, P.REPLICATED, ctx)
+                return _PendingDense(finish)
             if got is not None:
                 out_keys, finals, ng, gexprs = got
                 return _paned_output(sel, items, out_keys, finals, ng, gexprs, proto.device, P.REPLICATED, ctx)
@@ -1257,6 +1266,36 @@ def prefilter(queries, catalog, ctx) -> None:
         ctx.prefilter[id(sel)] = _Prefiltered(sel, t, mask, counts, k, ev)
 
 
+class _PendingDense:
+    """A windowed GROUP BY whose dense-ring kernels are queued; ``finish()`` reads the status → Table or None."""
+    __slots__ = ("finish",)
+
+    def __init__(self, finish):
+        self.finish = finish
+
+
+def _deferred_select(sel: A.Select, catalog, ctx, pending: _PendingDense) -> DeferredTable:
+    """The statement's result as a ``DeferredTable``, registered on ``ctx.pending`` (the processor completes any left
+    at the end of the batch's statements).  When the dictionary reports a collision the statement runs again on
+    the paned path — against the catalog as it was here, so statements planned meanwhile cannot change its
+    inputs."""
+    snap = catalog.child()
+
+    def finish():
+        prev_cat, prev_defer = ctx.catalog, ctx.defer_dense
+        ctx.catalog, ctx.defer_dense = snap, False
+        try:
+            out = pending.finish()
+            if out is None:
+                out, _ = _exec_select(sel, snap, ctx)
+        finally:
+            ctx.catalog, ctx.defer_dense = prev_cat, prev_defer
+        return out
+    d = DeferredTable(finish)
+    ctx.pending.append(d)
+    return d
+
+
 def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     if sel.grouping_sets is not None:
         return _exec_grouping_sets(sel, catalog, ctx), None
@@ -1264,10 +1303,15 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
         from .windows import PanedTable
         t = _lookup(sel.from_, catalog)
         if isinstance(t, PanedTable):
+            alias = sel.from_.alias or sel.from_.name.split(".")[-1]
             try:
-                out = _paned_aggregate(sel, t, sel.from_.alias or sel.from_.name.split(".")[-1], ctx)
+                out = _paned_aggregate(sel, t, alias, ctx)
             except EvalError:
                 out = None
+            if isinstance(out, _PendingDense):
+                out = _deferred_select(sel, catalog, ctx, out)
+                if not sel.distinct:
+                    return out, None
             if out is not None:
                 return (distinct(out) if sel.distinct else out), None
     scope = _relation(sel.from_, catalog, ctx)

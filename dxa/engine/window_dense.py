@@ -120,6 +120,8 @@ class DenseWindow:
         self.free = list(range(ring_slots))    # free pane slots (a heap: the lowest is taken first)
         self.disabled = False
         self._pinned = [torch.empty(self.R, dtype=torch.int32, pin_memory=True) for _ in range(4)]
+        self._scal_pin = [torch.empty(4, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        self._scal_k = 0
         self._pin_k = 0
         cap = 1 << max(10, (2 * self.gcap - 1).bit_length())
         self.hcap = cap
@@ -331,10 +333,12 @@ class DenseWindow:
         return dst
 
     # ---- the window's answer --------------------------------------------------------------------------------------
-    def answer(self, slots: List[int], partial_proto=None):
+    def answer(self, slots: List[int], partial_proto=None, defer: bool = False):
         """Combine ``slots`` → (key columns, {agg key → column}, groups) or None (fall back: collision / full).
         With ``partial_proto`` (an empty partial table of ``distagg.local_partials``' layout, and its plan) the
-        result is instead this rank's window as a partial table of exactly that layout, for the key exchange."""
+        result is instead this rank's window as a partial table of exactly that layout, for the key exchange.
+        ``defer``: return a function that completes the answer later — the kernels are queued and the status is on
+        its way to pinned memory, so the batch thread can plan independent statements while they run."""
         L = self.layout
         dev = self.device
         st = N.stream_handle(dev)
@@ -344,7 +348,23 @@ class DenseWindow:
         N.call("dxa_win_answer", N.ptr(self.ring), self.gcap, self.stride, N.ptr(slots_dev), len(slots),
                N.ptr(self.line_ops_dev), L["count_word"], N.ptr(self.scal), N.ptr(self.acc), N.ptr(self.keep),
                N.ptr(self.out_idx), ctypes.addressof(e), ctypes.addressof(self.dictcols), st)
-        ng_all, bad, nout, _ = self.scal.tolist()          # the statement's one synchronising read
+        if not defer:
+            # the statement's one synchronising read
+            return self._finish(self.scal.tolist(), bufs, fin, partial_proto)
+        pin = self._scal_pin[self._scal_k]
+        self._scal_k ^= 1
+        pin.copy_(self.scal, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+
+        def finish():
+            ev.synchronize()
+            return self._finish(pin.tolist(), bufs, fin, partial_proto)
+        return finish
+
+    def _finish(self, status, bufs, fin, partial_proto):
+        L = self.layout
+        ng_all, bad, nout, _ = status
         if bad:
             return None
         okey, olen, ovalid, dst, dvalid = bufs
@@ -460,8 +480,9 @@ def dense_partials(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, empty):
     return table, pp[1], pp[2], gexprs
 
 
-def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_proto=None):
-    """The window statement's (key columns, finals, groups, group exprs) from the dense ring, or None."""
+def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_proto=None, defer: bool = False):
+    """The window statement's (key columns, finals, groups, group exprs) from the dense ring, or None.
+    ``defer``: instead a function returning that tuple (or None: fall back) once the status read completes."""
     from .. import parallel as P
     from .query import _resolve_group_expr
     from .expr import Scope
@@ -527,7 +548,7 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
             else:
                 state.blocks.pop(bid, None)
                 slots.extend(e[0] for e in mem)
-        got = state.answer(slots, partial_proto)
+        got = state.answer(slots, partial_proto, defer=defer and partial_proto is None)
     except Ineligible:
         state = states.get(fp)
         if state is not None:
@@ -536,6 +557,16 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
         else:
             states[fp] = _Disabled()
         return None
+    if callable(got):
+        def finish():
+            res = got()
+            if res is None:
+                state.disabled = True
+                state.ring = state.acc = None
+                return None
+            out_keys, finals, ng = res
+            return out_keys, finals, ng, gexprs
+        return finish
     if got is None:
         state.disabled = True
         state.ring = state.acc = None

@@ -16,11 +16,31 @@ def _names(p, steps):
 
 
 def test_sequential_by_default(tmp_path):
-    p = _proc(tmp_path, "full")
-    assert not p._concurrent_views()                  # default: statement order
+    p = _proc(tmp_path, "groupby")
+    assert not p._concurrent_views() and p.window_store is None    # default: statement order
     steps = p._view_schedule(p._live_statements())
     assert all(len(s) == 1 for s in steps)
     assert [k for s in steps for k in s] == sorted(k for s in steps for k in s)
+
+
+def test_sequential_level_order_with_a_window(tmp_path):
+    """With a time window, sequential views run level by level (one per step): a windowed statement's readers
+    come after the statements that do not read it, so its deferred completion finds its kernels done."""
+    p = _proc(tmp_path, "full")
+    assert not p._concurrent_views() and p.window_store is not None
+    live = p._live_statements()
+    steps = p._view_schedule(live)
+    assert all(len(s) == 1 for s in steps)
+    names = [n for s in _names(p, steps) for n in s]
+    from dxa.sql.transform import COMMAND_COMMAND
+    assert sorted(k for s in steps for k in s) == [k for k, c in enumerate(p.transform.commands)
+                                                   if c.command_type == COMMAND_COMMAND or k in live]
+    pos = {n: i for i, n in enumerate(names)}
+    assert pos["DeviceWindow"] < pos["DeviceNamed"] < pos["UnhealthyDevices"]
+    assert pos["DeviceWindow"] < pos["DeviceState"]
+    # a statement that reads only the input runs before DeviceWindow's first reader
+    indep = [n for n in names if n and n.startswith("sa1_")]
+    assert indep and all(pos[n] < pos["DeviceNamed"] for n in indep)
 
 
 def test_levels_and_accumulator(tmp_path, monkeypatch):
