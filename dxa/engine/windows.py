@@ -270,7 +270,9 @@ class WindowStore:
         self.interval_us = 0
         self.blocks: Dict = {}               # (query fingerprint, block id) → pre-combined partials of a pane block
 
-    def _ts(self, t: Table) -> Tuple[torch.Tensor, torch.Tensor]:
+    def _ts(self, t: Table, lazy_valid: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(timestamps, validity); with ``lazy_valid`` the validity is None when every row has one (no all-true
+        mask is filled unless a caller needs it)."""
         c = t.column(self.conf.timestamp_column)
         if c is None:
             raise EvalError(f"timestamp column {self.conf.timestamp_column} not found in {t.names}")
@@ -279,7 +281,7 @@ class WindowStore:
         if c.dtype != "timestamp":
             from .expr import cast_column
             c = cast_column(c, "timestamp")
-        return c.data, c.valid_mask()
+        return c.data, (c.valid if lazy_valid else c.valid_mask())
 
     def _range(self, t: Table, lo: Optional[int], hi: Optional[int]) -> Table:
         if t.length == 0:
@@ -329,9 +331,11 @@ class WindowStore:
             # one host read for the common case (every event valid and not late): the batch's pane statistics and
             # the late-event check come back together; otherwise filter, then take the kept rows' statistics
             with host_section("windows:stats"):
-                ts, ok = self._ts(projected)
+                ts, ok = self._ts(projected, lazy_valid=True)
                 lens_all = _str_lens_all(projected)
                 got = self._stats_ahead(projected, ts, E)
+                if ok is None and got is None:
+                    ok = torch.ones(projected.length, dtype=torch.bool, device=ts.device)
                 if got is None:
                     got = _ts_stats(ts, ok, E, lens_all)
                 lo_, hi_, nok, nkeep = got[:4]
@@ -340,7 +344,7 @@ class WindowStore:
                     kept = _compact_table(projected, None if lens_all is None else (lens_all, int(got[4])))
                 cur = Pane(batch_time_us, kept, int(lo_), int(hi_), True)
             else:
-                kept = _compact_table(projected.filter(ok & (ts >= E)))
+                kept = _compact_table(projected.filter((ts >= E) if ok is None else ok & (ts >= E)))
         else:
             kept = _compact_table(projected)
         kept.dist = projected.dist
