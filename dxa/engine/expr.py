@@ -48,6 +48,7 @@ class EvalContext:
     device: Any = "cpu"
     catalog: Any = None                   # tables visible to sub-queries (set by query.execute)
     prefilter: Dict[int, Any] = field(default_factory=dict)   # id(Select) → early WHERE mask (query.prefilter)
+    prefilter_cands: Dict[int, Any] = field(default_factory=dict)   # id(table) → filters over it, not yet run
     defer_dense: bool = False             # a windowed GROUP BY may return a DeferredTable (query._deferred_select)
     pending: List[Any] = field(default_factory=list)           # DeferredTables of this batch not yet completed
 

@@ -1227,14 +1227,13 @@ def _plain_predicate(e: A.Expr, ctx) -> bool:
 
 
 def prefilter(queries, catalog, ctx) -> None:
-    """Evaluate the WHERE of every statement that filters a table already in ``catalog`` (the batch's input view,
-    reference and state tables) at the start of the batch, and bring all their row counts to pinned memory with ONE
-    copy.  Each such statement later reads its count without draining the stream (``_Prefiltered.indices``), where a
-    filter otherwise waits for its own mask kernels (``torch.nonzero``) — the rule alerts' filters of the full flow.
-    Each predicate is still evaluated exactly once; statements whose predicate does not evaluate here keep the
-    usual path (and report their error there)."""
+    """Note the statements that filter a table already in ``catalog`` (the batch's input views, reference and state
+    tables).  When the first of them runs, the WHERE masks of all of them over that same table are evaluated
+    together and their row counts come to pinned memory in ONE copy (``_run_prefilters``): the statements after
+    it take their rows without draining the stream.  Each predicate is still evaluated exactly once; a statement
+    whose predicate fails there keeps the usual path (and reports its error there)."""
     from .windows import PanedTable
-    found = []
+    cands: Dict[int, list] = {}
     for q in queries:
         if q is None or q.ctes or not isinstance(q.body, A.Select):
             continue
@@ -1249,9 +1248,15 @@ def prefilter(queries, catalog, ctx) -> None:
         if isinstance(t, PanedTable) and (sel.group_by or any(
                 not isinstance(it.expr, A.Star) and _contains_agg(it.expr, ctx) for it in sel.items)):
             continue                       # a windowed aggregate: the paned / dense path applies WHERE per pane
+        cands.setdefault(id(t), []).append((sel, t, src.alias or src.name.split(".")[-1]))
+    ctx.prefilter_cands = {k: v for k, v in cands.items() if len(v) > 1}    # one filter alone gains nothing
+
+
+def _run_prefilters(cands, ctx) -> None:
+    found = []
+    for sel, t, alias in cands:
         try:
-            scope = Scope.of_table(t, src.alias or src.name.split(".")[-1])
-            mask = predicate_mask(evaluate(sel.where, scope, ctx))
+            mask = predicate_mask(evaluate(sel.where, Scope.of_table(t, alias), ctx))
         except Exception:  # noqa: BLE001 — the statement's own evaluation reports it
             continue
         found.append((sel, t, mask))
@@ -1318,6 +1323,13 @@ def _exec_select(sel: A.Select, catalog, ctx, want_scope=False):
     sdist = getattr(scope, "dist", P.REPLICATED)
     if sel.where is not None:
         pf = ctx.prefilter.pop(id(sel), None) if ctx.prefilter else None
+        if pf is None and ctx.prefilter_cands and isinstance(sel.from_, A.TableRef):
+            src_t = _lookup(sel.from_, catalog)
+            cands = ctx.prefilter_cands.get(id(src_t))
+            if cands and any(c[0] is sel and c[1] is src_t for c in cands):
+                del ctx.prefilter_cands[id(src_t)]
+                _run_prefilters(cands, ctx)
+                pf = ctx.prefilter.pop(id(sel), None)
         if pf is not None and pf.sel is sel and pf.table is _lookup(sel.from_, catalog) and \
                 pf.mask.shape[0] == scope.length:
             idx = pf.indices()

@@ -643,8 +643,8 @@ def test_parser_null_strings_are_empty_views(gpu):
 
 
 def test_prefiltered_where_matches_plain_filter(gpu):
-    """query.prefilter: WHERE masks of statements over present tables evaluated at batch start with one count
-    copy; the statement then takes its rows without a stream drain, and the result equals the plain filter."""
+    """query.prefilter: the filters over one present table have their WHERE masks evaluated together when the first
+    runs, with one count copy; the later ones take their rows without a stream drain; results equal plain filters."""
     from dxa.engine.query import execute, prefilter
     from dxa.sql.parser import parse_query
     rnd = random.Random(3)
@@ -660,9 +660,11 @@ def test_prefiltered_where_matches_plain_filter(gpu):
     cat.register("T", t)
     ctx = EvalContext(device=gpu)
     prefilter(qs, cat, ctx)
-    assert {id(q.body) for q in qs[:3]} == set(ctx.prefilter)
-    got = [execute(q, cat, ctx) for q in qs]
-    assert not ctx.prefilter                                      # every early mask was consumed
+    assert [c[0] for c in ctx.prefilter_cands[id(t)]] == [q.body for q in qs[:3]]   # the sub-query filter: not
+    got = [execute(qs[0], cat, ctx)]
+    assert {id(q.body) for q in qs[1:3]} == set(ctx.prefilter)   # the first ran all three masks, one count copy
+    got += [execute(q, cat, ctx) for q in qs[1:]]
+    assert not ctx.prefilter and not ctx.prefilter_cands          # every early mask was consumed
     want = [execute(q, cat, EvalContext(device=gpu)) for q in qs]
     for g, w in zip(got, want):
         assert g.names == w.names and g.length == w.length

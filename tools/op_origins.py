@@ -1,0 +1,71 @@
+"""Where do a flow's framework ("glue") kernels come from?  Runs bench.py's flow for a few batches under a
+TorchDispatchMode that records every ATen op launched on a large CUDA tensor (copies, casts, fills, cats,
+arithmetic, scans) with the engine frame that called it, and prints the origins by count.
+
+    python tools/op_origins.py --flow window [--batches 4] [--min-numel 100000]
+"""
+import argparse
+import collections
+import os
+import sys
+import traceback
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
+
+WATCH = ("copy", "_to_copy", "cat", "fill", "zero", "sub", "add", "cumsum", "ones", "full", "clone", "where",
+         "index", "masked", "nonzero", "mul", "eq", "ne", "lt", "gt", "le", "ge", "bitwise", "logical", "arange")
+
+
+class Origins(TorchDispatchMode):
+    def __init__(self, min_numel):
+        super().__init__()
+        self.min = min_numel
+        self.hits = collections.Counter()
+        self.on = False
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        if self.on:
+            name = func.overloadpacket.__name__
+            big = any(isinstance(t, torch.Tensor) and t.is_cuda and t.numel() >= self.min
+                      for t in list(args) + [out] if isinstance(t, torch.Tensor))
+            if big and any(w in name for w in WATCH):
+                frames = [f for f in traceback.extract_stack()[:-2] if "/dxa/" in f.filename]
+                where = " <- ".join(f"{f.filename.split('/dxa/')[-1]}:{f.lineno}({f.name})" for f in frames[-3:][::-1])
+                self.hits[(name, where)] += 1
+        return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flow", default="window")
+    ap.add_argument("--batches", type=int, default=4)
+    ap.add_argument("--min-numel", type=int, default=100_000)
+    a = ap.parse_args()
+    from dxa.engine.processor import Processor, RawBatch
+    from dxa.models import iot
+    from dxa.simulate.datagen import generate
+    dev = torch.device("cuda", 0)
+    extra = {"datax.job.process.pipelineoutputs": "false"}
+    proc = Processor(iot.flow_settings(variant=a.flow, sink="null", extra=extra, ref_rows=100_000), dev)
+    prog = iot.program()
+    n = 1_000_000
+    mode = Origins(a.min_numel)
+    t0 = 1_700_000_000_000_000
+    with mode:
+        for i in range(a.batches + 2):
+            bt = t0 + i * 1_000_000
+            buf, offs = generate(prog, n, dev, seed=11 + i, row0=i * n, base_ms=bt // 1000 - 1000, step_us=1)
+            mode.on = i >= 2                                     # after the first batches (layouts, caches)
+            proc.process_batch(RawBatch(buf, offs, n), bt, 1_000_000)
+            proc.drain()
+            torch.cuda.synchronize()
+    for (name, where), k in mode.hits.most_common(40):
+        print(f"{k / a.batches:5.1f}/batch  {name:18s} {where}")
+
+
+if __name__ == "__main__":
+    main()
