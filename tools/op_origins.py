@@ -15,8 +15,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
 
-WATCH = ("copy", "_to_copy", "cat", "fill", "zero", "sub", "add", "cumsum", "ones", "full", "clone", "where",
-         "index", "masked", "nonzero", "mul", "eq", "ne", "lt", "gt", "le", "ge", "bitwise", "logical", "arange")
+# ops that only make views (no kernel)
+VIEWS = {"select", "slice", "view", "_unsafe_view", "as_strided", "t", "transpose", "unsqueeze", "squeeze", "expand",
+         "alias", "detach", "permute", "narrow", "unbind", "split", "split_with_sizes", "lift_fresh", "empty",
+         "empty_strided", "_local_scalar_dense", "is_nonzero", "unfold", "view_as_real", "view_as_complex",
+         "empty_like", "new_empty", "new_empty_strided", "record_stream", "set_", "resize_", "_reshape_alias"}
 
 
 class Origins(TorchDispatchMode):
@@ -32,7 +35,7 @@ class Origins(TorchDispatchMode):
             name = func.overloadpacket.__name__
             big = any(isinstance(t, torch.Tensor) and t.is_cuda and t.numel() >= self.min
                       for t in list(args) + [out] if isinstance(t, torch.Tensor))
-            if big and any(w in name for w in WATCH):
+            if big and name not in VIEWS:
                 frames = [f for f in traceback.extract_stack()[:-2] if "/dxa/" in f.filename]
                 where = " <- ".join(f"{f.filename.split('/dxa/')[-1]}:{f.lineno}({f.name})" for f in frames[-3:][::-1])
                 self.hits[(name, where)] += 1
