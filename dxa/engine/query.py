@@ -1214,7 +1214,7 @@ class _Prefiltered:
 
     def indices(self) -> torch.Tensor:
         self.event.synchronize()          # long complete by the time the statement runs: no queue drain
-        n = int(self.counts[self.k])
+        n = int(self.mask.shape[0]) - int(self.counts[self.k])       # counts: the mask's false rows
         return torch.nonzero_static(self.mask, size=n).flatten()
 
 
@@ -1262,9 +1262,16 @@ def _run_prefilters(cands, ctx) -> None:
         found.append((sel, t, mask))
     if not found:
         return
+    from ..ops import native as N
     dev = found[0][2].device
+    st = N.stream_handle(dev)
+    # false rows per mask (null_count_kernel: one small launch each, where a torch bool sum is a 50 us reduction)
+    falses = torch.empty(len(found), dtype=torch.int64, device=dev)
+    for k, (_, _, m) in enumerate(found):
+        m = m.contiguous()
+        N.call("dxa_null_counts", N.ptr(N.u8(m)), int(m.shape[0]), 1, falses[k:].data_ptr(), st)
     counts = torch.empty(len(found), dtype=torch.int64, pin_memory=True)
-    counts.copy_(torch.stack([m.sum() for _, _, m in found]), non_blocking=True)
+    counts.copy_(falses, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     for k, (sel, t, mask) in enumerate(found):

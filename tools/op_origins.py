@@ -37,8 +37,12 @@ class Origins(TorchDispatchMode):
                       for t in list(args) + [out] if isinstance(t, torch.Tensor))
             if big and name not in VIEWS:
                 frames = [f for f in traceback.extract_stack()[:-2] if "/dxa/" in f.filename]
-                where = " <- ".join(f"{f.filename.split('/dxa/')[-1]}:{f.lineno}({f.name})" for f in frames[-3:][::-1])
-                self.hits[(name, where)] += 1
+                where = " <- ".join(f"{f.filename.split('/dxa/')[-1]}:{f.lineno}({f.name})" for f in frames[-4:][::-1])
+                t0 = next((t for t in args if isinstance(t, torch.Tensor)), None)
+                sig = "" if t0 is None else f"{str(t0.dtype)[6:]}{list(t0.shape)}{'' if t0.is_contiguous() else '!c'}"
+                if isinstance(out, torch.Tensor):
+                    sig += f"->{str(out.dtype)[6:]}{'=' if t0 is not None and out.data_ptr() == t0.data_ptr() else ''}"
+                self.hits[(f"{name} {sig}", where)] += 1
         return out
 
 
@@ -67,7 +71,7 @@ def main():
             proc.drain()
             torch.cuda.synchronize()
     for (name, where), k in mode.hits.most_common(40):
-        print(f"{k / a.batches:5.1f}/batch  {name:18s} {where}")
+        print(f"{k / a.batches:5.1f}/batch  {name:40s} {where}")
 
 
 if __name__ == "__main__":
