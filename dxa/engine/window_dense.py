@@ -293,15 +293,21 @@ class DenseWindow:
                 spec += [0, 0, kind]
                 continue
             c = args[key[1]]
+            v = N.u8(c.valid)
+            if v is not None:
+                v = v.contiguous()
+            if key[0] == "count":                  # a count reads only the validity: no value conversion
+                hold.append(v)
+                spec += [0, 0 if v is None else v.data_ptr(), kind]
+                continue
             d = c.data
             if key[0] == "sumf" or (kind & 3) in (_MV_F64, _MV_F64_ORD):
                 d = d.to(torch.float64)
             elif d.dtype != torch.int64:
                 d = d.to(torch.int64)
             d = d.contiguous()
-            v = N.u8(c.valid)
             hold += [d, v]
-            spec += [0 if key[0] == "count" else d.data_ptr(), 0 if v is None else v.contiguous().data_ptr(), kind]
+            spec += [d.data_ptr(), 0 if v is None else v.data_ptr(), kind]
         spec_t = torch.tensor(spec, dtype=torch.int64)
         ring_ptr = self.ring[slot_idx].data_ptr()
         N.call("dxa_aggregate_multi", N.ptr(gid), n, self.gcap + 1, L["nslots"], spec_t.data_ptr(),
