@@ -9,7 +9,8 @@ cat $O/box.txt
 for v in default omp1; do
   cat $CG/cpu.stat > $O/stat_${v}_before.txt 2>/dev/null
   if [ $v = omp1 ]; then export OMP_NUM_THREADS=1 ARROW_NUM_THREADS=1; fi
-  /usr/bin/time -v timeout -k 10 420 python bench.py --flow ${FLOW:-full} --steps 60 > $O/bench_$v.log 2> $O/time_$v.txt || { tail -20 $O/time_$v.txt; exit 1; }
+  TIMEFORMAT="%R %U %S"
+  { time timeout -k 10 420 python bench.py --flow ${FLOW:-full} --steps 60 > $O/bench_$v.log 2> $O/err_$v.txt ; } 2> $O/time_$v.txt || { tail -20 $O/err_$v.txt; exit 1; }
   cat $CG/cpu.stat > $O/stat_${v}_after.txt 2>/dev/null
   python - $O $v <<'PY'
 import json, sys
@@ -21,10 +22,10 @@ def stat(p):
     except OSError:
         return {}
 b, a = stat(f"{o}/stat_{v}_before.txt"), stat(f"{o}/stat_{v}_after.txt")
-t = {l.split(":")[0].strip(): l.split(":", 1)[1].strip() for l in open(f"{o}/time_{v}.txt") if ":" in l}
+real, user, sys_ = (float(x) for x in open(f"{o}/time_{v}.txt").read().split()[-3:])
 print(v, round(d["value"] / 1e6, 1), "M ev/s", round(d["ms_per_step"], 2), "ms", "p99", round(d["p99_latency_process_ms"], 1),
       "| throttled periods", a.get("nr_throttled", 0) - b.get("nr_throttled", 0), "of", a.get("nr_periods", 0) - b.get("nr_periods", 0),
       "throttled ms", round((a.get("throttled_usec", 0) - b.get("throttled_usec", 0)) / 1e3, 1),
-      "| cpu%", t.get("Percent of CPU this job got"), "wall", t.get("Elapsed (wall clock) time (h:mm:ss or m:ss)"))
+      "| wall", real, "s, cpu", round(user + sys_, 1), "s =", round((user + sys_) / real, 1), "CPUs")
 PY
 done

@@ -2,7 +2,7 @@
 # 300-pane window with its idle-gap summary.  OUT=<dir under gpurun_out>
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/${OUT:-r6host}
+O=gpurun_out/${OUT:-host}
 mkdir -p $O
 for f in ${FLOWS:-window full}; do
   DXA_HOST_TIMERS=1 DXA_BENCH_HOST_TRACE=1 timeout -k 10 420 python bench.py --flow $f --steps 40 --profile-stages > $O/host_$f.log 2>&1 || { tail -20 $O/host_$f.log; exit 1; }
