@@ -20,6 +20,7 @@ import ctypes
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from .column import PrimColumn, StrColumn, StructColumn, Table, concat_tables, ConstColumn
@@ -55,6 +56,11 @@ class TimeWindowConf:
             return TimeWindowConf({}, False, None, 0, 0, quirk)
         from ..sql.parser import parse_duration_micros
         return TimeWindowConf(wins, True, ts, parse_duration_micros(wm), max(wins.values()), quirk)
+
+
+def _pane_meta(p: "Pane"):
+    """The fields ``PanedTable.pieces`` tests: (lo, hi, non-empty, every row has a timestamp)."""
+    return p.lo, p.hi, p.table.length > 0, bool(p.all_valid)
 
 
 def _str_leaves(c, out: List[StrColumn]):
@@ -143,7 +149,22 @@ class PanedTable(Table):
     def pieces(self) -> List[Tuple[Pane, bool]]:
         """(pane, fully inside) for every pane that intersects the range (``Pane.outside`` / ``Pane.inside``, inlined:
         a 5-minute window walks 300 panes, and its statements ask more than once per batch).  The view's panes and
-        range are fixed for its batch, so the list is computed once."""
+        range are fixed for its batch, so the list is computed once — from the store's bound arrays when the view
+        holds the batch's pane list (``WindowStore._batch_meta``)."""
+        bm = getattr(self.store, "_batch_meta", None)
+        if self._pieces is None and bm is not None and bm[0] is self.panes:
+            _, plo, phi, ne, av = bm
+            keep = ne & (plo <= phi)
+            full = av.copy()
+            if self.lo is not None:
+                keep &= phi >= self.lo
+                full &= plo >= self.lo
+            if self.hi is not None:
+                keep &= plo < self.hi
+                full &= phi < self.hi
+            idx = np.flatnonzero(keep)
+            panes = self.panes
+            self._pieces = [(panes[i], f) for i, f in zip(idx.tolist(), full[idx].tolist())]
         if self._pieces is None:
             lo, hi = self.lo, self.hi
             out = []
@@ -349,8 +370,10 @@ class WindowStore:
             kept = _compact_table(projected)
         kept.dist = projected.dist
         cut = batch_time_us - (c.watermark_us + c.max_window_us)
-        for t in [t for t in self.past if t <= cut]:
+        gone = [t for t in self.past if t <= cut]
+        for t in gone:
             del self.past[t]
+        self._meta_drop(gone)
         self.interval_us = interval_us
         if self.blocks:
             live = set(self.past)
@@ -371,8 +394,48 @@ class WindowStore:
             views[name] = PanedTable(self, panes, E - w, E, names, dev)
         views[base] = PanedTable(self, panes, E - interval_us, E, names, dev)
         views[f"{base}_Batch"] = projected
-        self.past[batch_time_us] = cur
+        # the batch's pane bounds as arrays, in the views' pane order (PanedTable.pieces)
+        m = self._meta
+        cm = _pane_meta(cur)
+        if len(panes) == 1:
+            self._batch_meta = (panes, *(np.array([v]) for v in cm))
+        else:
+            self._batch_meta = (panes, *(np.concatenate(([v], a)) for v, a in zip(cm, m[1:])))
+        if batch_time_us in self.past:             # a repeated batch time replaces its pane: rebuild the arrays
+            self.past[batch_time_us] = cur
+            self._meta = None
+        else:
+            self.past[batch_time_us] = cur
+            if m is not None:
+                self._meta = (m[0] + [batch_time_us], *(np.append(a, v) for v, a in zip(cm, m[1:])))
         return views, kept.length
+
+    # ---- pane bounds as arrays (the window's pieces without a Python pass over 300 panes) ----------------------
+    @property
+    def _meta(self):
+        """(keys, lo, hi, non-empty, all-valid) of ``past`` in its order; rebuilt when not maintained."""
+        m = self.__dict__.get("_pmeta")
+        if m is None or len(m[0]) != len(self.past):
+            keys = list(self.past)
+            cols = list(zip(*(_pane_meta(self.past[k]) for k in keys))) if keys else [(), (), (), ()]
+            m = (keys, np.array(cols[0], dtype=np.int64), np.array(cols[1], dtype=np.int64),
+                 np.array(cols[2], dtype=bool), np.array(cols[3], dtype=bool))
+            self.__dict__["_pmeta"] = m
+        return m
+
+    @_meta.setter
+    def _meta(self, m):
+        self.__dict__["_pmeta"] = m
+
+    def _meta_drop(self, gone):
+        m = self.__dict__.get("_pmeta")
+        if not gone or m is None:
+            return
+        k = len(gone)
+        if m[0][:k] == gone:                       # the oldest panes leave from the front (keys ascend)
+            self.__dict__["_pmeta"] = (m[0][k:], *(a[k:] for a in m[1:]))
+        else:
+            self.__dict__["_pmeta"] = None
 
     def retained_rows(self) -> int:
         return sum(p.table.length for p in self.past.values())

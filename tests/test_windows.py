@@ -128,3 +128,32 @@ def test_dense_ring_matches_materialized(spread, nb, win, block, monkeypatch):
         assert len(d.slot_of) <= len(store.past) + 1
     if block < win:
         assert any(d.blocks for d in dense.values())
+
+
+def test_pieces_from_bound_arrays_match_the_pane_loop():
+    """PanedTable.pieces from the store's maintained pane-bound arrays equals the per-pane loop: empty panes,
+    inverted bounds, panes with untimed rows, open and closed ranges."""
+    import random
+    import numpy as np
+    from dxa.engine.column import Table, column_from_pylist
+    from dxa.engine.windows import Pane, PanedTable, WindowStore, _pane_meta
+    rnd = random.Random(0)
+    st = WindowStore.__new__(WindowStore)
+    st.past = {}
+    panes = []
+    for k in range(60):
+        n = rnd.choice([0, 3])
+        lo = rnd.randint(0, 100)
+        p = Pane(k, Table(["a"], [column_from_pylist(list(range(n)), "long")], n), lo, lo + rnd.randint(-5, 30),
+                 rnd.random() < 0.8)
+        if k:
+            st.past[k] = p
+        panes.append(p)
+    m = st._meta
+    st._batch_meta = (panes, *(np.concatenate(([v], a)) for v, a in zip(_pane_meta(panes[0]), m[1:])))
+    for lo, hi in [(None, None), (10, 60), (50, None), (None, 40), (200, 300), (30, 31)]:
+        fast = PanedTable(st, panes, lo, hi, ["a"], "cpu").pieces()
+        saved, st._batch_meta = st._batch_meta, None
+        slow = PanedTable(st, panes, lo, hi, ["a"], "cpu").pieces()
+        st._batch_meta = saved
+        assert [(p.key, f) for p, f in fast] == [(p.key, f) for p, f in slow], (lo, hi)
