@@ -103,7 +103,10 @@ class StateTable:
         for name, c in zip(t.names, t.columns):
             src = arrow_name.get(name.lower())
             if type(c) is StrColumn and src is not None and c.length:
-                m = pc.max(pc.binary_length(at.column(src))).as_py()
+                try:
+                    m = pc.max(pc.binary_length(at.column(src))).as_py()
+                except Exception:  # noqa: BLE001 — e.g. a dictionary-encoded column: leave it unbounded
+                    continue
                 c.max_len = int(m or 0)
         return t
 
