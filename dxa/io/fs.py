@@ -11,7 +11,6 @@ from __future__ import annotations
 import gzip
 import os
 import re
-import tempfile
 import threading
 from concurrent.futures import ThreadPoolExecutor, TimeoutError as _Timeout
 from pathlib import Path
@@ -84,6 +83,9 @@ def gzip_parallel(data, level: int = 6, chunk: int = _GZ_CHUNK) -> bytes:
     return b"".join(parts)
 
 
+_DIRS_MADE: set = set()
+
+
 def write_atomic(path: str, data: bytes | str, gzip_it: bool = False, gzipped: bool = False) -> Path:
     """Write to a temp file in the destination folder, then rename (never leaves a partial file).  A blob PUT is
     atomic on the service side, so remote paths are written in one request.  ``gzipped``: ``data`` is already a
@@ -100,8 +102,17 @@ def write_atomic(path: str, data: bytes | str, gzip_it: bool = False, gzipped: b
                         "gzip" if gzip_it else None)
         return Path(path)
     p = local_path(path)
-    p.parent.mkdir(parents=True, exist_ok=True)
-    fd, tmp = tempfile.mkstemp(prefix="." + p.name + ".", dir=str(p.parent))
+    parent = str(p.parent)
+    if parent not in _DIRS_MADE:
+        p.parent.mkdir(parents=True, exist_ok=True)
+        _DIRS_MADE.add(parent)
+    # a temp name unique per process and thread (no random-name search): every batch's state flip writes one
+    tmp = os.path.join(parent, f".{p.name}.{os.getpid()}.{threading.get_ident()}.tmp")
+    try:
+        fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    except FileNotFoundError:                    # the directory went away since it was made: make it again
+        p.parent.mkdir(parents=True, exist_ok=True)
+        fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
     with os.fdopen(fd, "wb") as f:
         f.write(data)
     os.replace(tmp, p)
