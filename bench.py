@@ -481,15 +481,13 @@ def main():
     proc.on_batch_complete = on_complete
 
     ready = {}
-    parse_ahead = on_gpu and os.environ.get("DXA_PARSE_AHEAD", "1") != "0"
+    parse_ahead = on_gpu
     # parse-ahead on its own stream, queued BEFORE the previous batch's process_batch so the parse overlaps that
     # batch's query kernels — for the device-resident source, where the parse is on the critical path.  With a
     # PCIe-bound ingest (kafka / pinned sources) it measured no throughput gain and higher latency
     # (profiles/round4/parse_stream/: passthrough 64 -> 61 M ev/s, join p50 8.9 -> 13.7 ms), so there the parse is
-    # queued behind the batch's kernels after process_batch.  DXA_PARSE_STREAM=1 / 0 forces either.
-    ps_env = os.environ.get("DXA_PARSE_STREAM", "auto")
-    use_ps = ps_env == "1" or (ps_env == "auto" and source == "gpu-sim")
-    parse_stream = torch.cuda.Stream(device) if parse_ahead and use_ps else None
+    # queued behind the batch's kernels after process_batch.
+    parse_stream = torch.cuda.Stream(device) if parse_ahead and source == "gpu-sim" else None
 
     def take(i):
         db, do, ev = staged.pop(i)

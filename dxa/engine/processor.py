@@ -42,7 +42,6 @@ from .windows import TimeWindowConf, WindowStore
 from ..telemetry import tracing
 
 log = logging.getLogger("dxa.processor")
-_INFERENCE = os.environ.get("DXA_INFERENCE_MODE", "1") != "0"
 _SYNC_STAGES = os.environ.get("DXA_SYNC_STAGES") == "1"
 
 
@@ -311,7 +310,7 @@ class Processor:
         batch's query kernels, which leave most of the chip idle (profiles/round4: the ``full`` flow's kernels keep
         the GPU busy ~35 % of the step), and ``project`` no longer waits a whole parse per batch."""
         if raw.pending is None and self.normalizer is None and raw.buf.device.type == "cuda":
-            with torch.inference_mode(_INFERENCE):
+            with torch.inference_mode():
                 self._prepare(raw, stream)
         return raw
 
@@ -786,7 +785,7 @@ class Processor:
         Runs under ``torch.inference_mode``: nothing here is differentiated, and without the autograd / version-
         counter dispatch every tensor op costs ~1 us less host time (hundreds of ops per batch on the planning
         thread, which bounds the device-resident flows)."""
-        with torch.inference_mode(_INFERENCE):
+        with torch.inference_mode():
             return self._process_batch(raw, batch_time_us, interval_us, partition_time)
 
     def _process_batch(self, raw: RawBatch, batch_time_us: int, interval_us: int,

@@ -15,8 +15,8 @@ from . import native as N
 CHUNK = int(os.environ.get("DXA_GZIP_CHUNK", "8192"))
 # dynamic Huffman tables per member (a counting pass whose parse the coding pass reuses), the default: on the
 # passthrough output 3.18x vs 2.53x with the fixed code, 54.7 vs 91.9 GB/s, and the blob-sink flow at 40.8 vs
-# 43.3 M events/s (profiles/round5/blob/README.md).  DXA_GZIP_DYNAMIC=0 selects the fixed code.
-DYNAMIC = os.environ.get("DXA_GZIP_DYNAMIC", "1") != "0"
+# 43.3 M events/s (profiles/round5/blob/README.md).  ``dynamic=False`` (the fixed code) stays for tests.
+DYNAMIC = True
 
 
 def slot_bytes(chunk: int) -> int:

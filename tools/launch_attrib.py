@@ -5,8 +5,8 @@ syncs (``_local_scalar_dense`` = .item()/.tolist(), D2H copies) are counted sepa
     python tools/launch_attrib.py --flow full --batches 8 [--events 1000000] > attrib.txt
 
 Runs the bench's gpu-sim batches through the Processor like tests/test_flows_gpu.py; the first two batches are warmup
-(not counted).  Run it with DXA_INFERENCE_MODE=0: under torch.inference_mode the dispatch mode sees composite ops
-before they decompose (``to.dtype`` no-ops, ``item``), which miscounts launches and syncs."""
+(not counted).  The Processor's ``torch.inference_mode`` is replaced by a no-op context here: under it the dispatch
+mode sees composite ops before they decompose (``to.dtype`` no-ops, ``item``), which miscounts launches and syncs."""
 from __future__ import annotations
 
 import argparse
@@ -78,6 +78,8 @@ class Counter(TorchDispatchMode):
 
 
 def main():
+    import contextlib
+    torch.inference_mode = lambda *a, **k: contextlib.nullcontext()      # see the module docstring
     ap = argparse.ArgumentParser()
     ap.add_argument("--flow", default="full")
     ap.add_argument("--batches", type=int, default=8)

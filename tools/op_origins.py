@@ -46,7 +46,15 @@ class Origins(TorchDispatchMode):
         return out
 
 
+def _no_inference_mode():
+    """The Processor runs batches under torch.inference_mode, where the dispatch mode sees composite ops before
+    they decompose (``to`` that copies nothing); attribute the decomposed ops instead."""
+    import contextlib
+    torch.inference_mode = lambda *a, **k: contextlib.nullcontext()
+
+
 def main():
+    _no_inference_mode()
     ap = argparse.ArgumentParser()
     ap.add_argument("--flow", default="window")
     ap.add_argument("--batches", type=int, default=4)
