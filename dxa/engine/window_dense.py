@@ -114,7 +114,7 @@ class DenseWindow:
         self.gcap = DENSE_GROUPS
         self.R = ring_slots + SCRATCH_SLOTS
         self.NB = ring_slots // BLOCK + 4              # block slots after the pane and scratch slots
-        self.blocks: Dict[int, tuple] = {}             # block id → (members, block slot)
+        self.blocks: Dict[int, tuple] = {}             # block id → (member entry ids, block slot, entries)
         self.layout = None              # built from the first pane's evaluated argument types
         self.slot_of: Dict[int, tuple] = {}     # pane key → (ring slot, id of the pane's table, block id, pane key)
         self.free = list(range(ring_slots))    # free pane slots (a heap: the lowest is taken first)
@@ -323,7 +323,9 @@ class DenseWindow:
     def block_slot(self, bid: int, mem: list) -> int:
         """The ring slot holding the pre-combined rows of a complete block of panes (combined once, when the block
         is first complete in a window; reused until a member leaves).  ``mem``: the members' slot entries."""
-        members = frozenset((e[3], e[1]) for e in mem)          # (pane key, table id): order-free
+        # members by the identity of their slot entries: an entry is made once per pane assignment and lives in
+        # slot_of while the pane is retained; the cache holds the entries too, so no id is reused while cached
+        members = frozenset(map(id, mem))
         ent = self.blocks.get(bid)
         if ent is not None and ent[0] == members:
             return ent[1]
@@ -335,7 +337,7 @@ class DenseWindow:
         member_slots = [e[0] for e in sorted(mem, key=lambda e: e[3])]
         N.call("dxa_win_combine_block", N.ptr(self.ring), self.gcap, self.stride, N.ptr(self._dev_slots(member_slots)),
                len(member_slots), N.ptr(self.line_ops_dev), dst, N.stream_handle(self.device))
-        self.blocks[bid] = (members, dst)
+        self.blocks[bid] = (members, dst, list(mem))
         return dst
 
     # ---- the window's answer --------------------------------------------------------------------------------------
