@@ -157,3 +157,22 @@ def test_pieces_from_bound_arrays_match_the_pane_loop():
         slow = PanedTable(st, panes, lo, hi, ["a"], "cpu").pieces()
         st._batch_meta = saved
         assert [(p.key, f) for p, f in fast] == [(p.key, f) for p, f in slow], (lo, hi)
+
+
+def test_pieces_bound_arrays_track_process_across_expiry():
+    """The store's pane-bound arrays stay aligned with its panes as batches arrive and expire (WindowStore.process):
+    every view's pieces equal the per-pane loop over a copy of its pane list."""
+    import torch
+    from dxa.engine.column import PrimColumn, Table, column_from_pylist
+    from dxa.engine.windows import PanedTable, TimeWindowConf, WindowStore
+    st = WindowStore(TimeWindowConf({"W_5s": 5_000_000}, True, "ts", 0, 5_000_000, False))
+    t0 = 1_700_000_000_000_000
+    for i in range(12):
+        bt = t0 + i * 1_000_000
+        ts = torch.arange(1000, dtype=torch.int64) * 1000 + bt - (400_000 if i % 3 == 0 else 0)   # some late rows
+        tab = Table(["ts", "v"], [PrimColumn("timestamp", ts), column_from_pylist(list(range(1000)), "long")], 1000)
+        views, _ = st.process(tab, bt, 1_000_000)
+        for v in views.values():
+            if isinstance(v, PanedTable):
+                slow = PanedTable(st, list(v.panes), v.lo, v.hi, v.names, "cpu").pieces()
+                assert [(p.key, f) for p, f in v.pieces()] == [(p.key, f) for p, f in slow]
