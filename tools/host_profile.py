@@ -39,7 +39,7 @@ def main():
     bufs = []
     for i in range(a.warmup + a.batches):
         bufs.append(generate(prog, a.events, dev, seed=i + 1, row0=i * a.events,
-                             base_ms=t0 // 1000 + i * 1000 - 1000, step_us=max(1, 1_000_000 // a.events)))
+                             base_ms=t0 // 1000 - 1000, step_us=max(1, 1_000_000 // a.events)))
     sync()
     for i in range(a.warmup):
         proc.process_batch(RawBatch(bufs[i][0], bufs[i][1], a.events), t0 + i * 1_000_000, 1_000_000)

@@ -119,7 +119,7 @@ def main():
     with cnt:
         for i in range(a.batches + 2):
             bt = t0 + i * interval
-            buf, offs = generate(prog, a.events, dev, seed=7919 + i, row0=i * a.events, base_ms=bt // 1000 - 1000,
+            buf, offs = generate(prog, a.events, dev, seed=7919 + i, row0=i * a.events, base_ms=t0 // 1000 - interval // 1000,
                                  step_us=max(1, interval // a.events))
             if dev.type == "cuda":
                 torch.cuda.synchronize()

@@ -73,7 +73,8 @@ def main():
     with mode:
         for i in range(a.batches + 2):
             bt = t0 + i * 1_000_000
-            buf, offs = generate(prog, n, dev, seed=11 + i, row0=i * n, base_ms=bt // 1000 - 1000, step_us=1)
+            # bench.py sim_gen_args: a constant base, so batch i's events fall in the interval before its batch time
+            buf, offs = generate(prog, n, dev, seed=11 + i, row0=i * n, base_ms=(t0 - 1_000_000) // 1000, step_us=1)
             mode.on = i >= 2                                     # after the first batches (layouts, caches)
             proc.process_batch(RawBatch(buf, offs, n), bt, 1_000_000)
             proc.drain()

@@ -46,7 +46,7 @@ def main():
             sites[("<other>", 0, str(message)[:60])] += 1
 
     for i in range(a.batches + 1):
-        buf, offs = generate(prog, a.events, dev, seed=i + 1, row0=i * a.events, base_ms=t0 // 1000 + i * 1000 - 1000,
+        buf, offs = generate(prog, a.events, dev, seed=i + 1, row0=i * a.events, base_ms=t0 // 1000 - 1000,
                              step_us=max(1, 1_000_000 // a.events))
         torch.cuda.synchronize()
         if i == 1:
