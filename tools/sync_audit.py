@@ -43,6 +43,8 @@ def main():
 
     def hook(message, category, filename, lineno, file=None, line=None):
         import threading
+        if "prototype feature" in str(message):       # the mode's own notice when it is switched on
+            return
         where = sites if threading.current_thread() is threading.main_thread() else other
         st = traceback.extract_stack()[:-1]
         frames = [f for f in st if "/dxa/" in f.filename]
