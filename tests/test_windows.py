@@ -130,6 +130,40 @@ def test_dense_ring_matches_materialized(spread, nb, win, block, monkeypatch):
         assert any(d.blocks for d in dense.values())
 
 
+@pytest.mark.gpu
+def test_dense_deferred_completion_and_collision_fallback(monkeypatch):
+    """A deferred windowed statement (ctx.defer_dense: the status read waits for first use, query._deferred_select)
+    equals the materialized window; when the status reports a collision the DeferredTable re-runs the statement on
+    the paned path against the catalog it was planned with, and the dense state is disabled from then on."""
+    import numpy as np
+    from dxa.engine import window_dense
+    from dxa.engine.column import DeferredTable
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    store = WindowStore(TimeWindowConf({"W": 6 * S}, True, "ts", 2 * S, 6 * S, False))
+    q = QUERIES[0]
+    finish = window_dense.DenseWindow._finish
+    for b in range(14):
+        T = (100 + b) * S
+        views, _ = store.process(batch(rng, T, 300, S - 1).to(dev), T, S)
+        if b == 10:                                  # this batch's status reads as a dictionary collision
+            monkeypatch.setattr(window_dense.DenseWindow, "_finish", lambda self, st, *a: finish(self, [0, 1, 0, 0], *a))
+        ctx = EvalContext(now_us=0, device=dev)
+        ctx.defer_dense = True
+        cat = Catalog()
+        cat.register("W", views["W"])
+        got = run_sql(q, cat, ctx)
+        if 4 <= b < 10:
+            assert isinstance(got, DeferredTable) and ctx.pending
+        mat = Table(views["W"].names, views["W"].columns, views["W"].length, dev)
+        cat2 = Catalog()
+        cat2.register("W", mat)
+        assert _canon(got) == _canon(run_sql(q, cat2, EvalContext(now_us=0, device=dev))), b
+        if b == 10:
+            monkeypatch.setattr(window_dense.DenseWindow, "_finish", finish)
+    assert all(d.disabled for d in store.__dict__["_dense"].values())
+
+
 def test_pieces_from_bound_arrays_match_the_pane_loop():
     """PanedTable.pieces from the store's maintained pane-bound arrays equals the per-pane loop: empty panes,
     inverted bounds, panes with untimed rows, open and closed ranges."""
