@@ -35,11 +35,16 @@ __host__ __device__ __forceinline__ uint64_t hash_combine(uint64_t acc, uint64_t
 // Never let a real key collide with the empty-slot sentinel.
 __host__ __device__ __forceinline__ uint64_t fix_key(uint64_t h) { return h == kEmpty ? (kEmpty - 1) : h; }
 
-// Unaligned little-endian byte fetch of up to 8 bytes starting at p (n in [1,8]).
+// Unaligned little-endian fetch of n bytes (1..8) starting at p: one or two aligned 8-byte loads and a funnel shift
+// instead of n byte loads.  Only aligned words that hold at least one of the n bytes are read, so every load stays
+// inside the allocation that holds the bytes (allocations are at least 8-byte aligned).
 __device__ __forceinline__ uint64_t load_le(const uint8_t* p, int n) {
-  uint64_t w = 0;
-  for (int i = 0; i < n; ++i) w |= (uint64_t)p[i] << (8 * i);
-  return w;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t o = (uint32_t)(a & 7u);
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(a - o);
+  uint64_t v = w[0] >> (8u * o);
+  if (o + (uint32_t)n > 8u) v |= w[1] << (64u - 8u * o);
+  return n < 8 ? v & ((1ull << (8 * n)) - 1ull) : v;
 }
 
 __device__ __forceinline__ uint64_t hash_bytes(const uint8_t* p, int64_t len) {

@@ -199,10 +199,14 @@ __device__ __forceinline__ bool key_differs(const KeyCols& a, const DictCols& d,
     if (k.kind == KC_STR) {
       const int32_t l = k.lens[i];
       if (l != e.lens[g] || l > kKeyWidth) return true;
+      // 8 bytes per step (dxa::load_le): the slot is 8-byte aligned, the row's bytes are not
       const uint8_t* x = (const uint8_t*)k.data + k.starts[i];
-      const uint8_t* y = (const uint8_t*)e.vals + (int64_t)g * kKeyWidth;
-      for (int32_t q = 0; q < l; ++q)
-        if (x[q] != y[q]) return true;
+      const uint64_t* y = (const uint64_t*)((const uint8_t*)e.vals + (int64_t)g * kKeyWidth);
+      for (int32_t q = 0; q < l; q += 8) {
+        const int32_t nb = l - q < 8 ? l - q : 8;
+        const uint64_t yw = nb < 8 ? y[q >> 3] & ((1ull << (8 * nb)) - 1ull) : y[q >> 3];
+        if (dxa::load_le(x + q, nb) != yw) return true;
+      }
     } else if ((int64_t)key_word(k, i) != ((const int64_t*)e.vals)[g]) {
       return true;
     }
