@@ -470,6 +470,8 @@ class Processor:
                     d = ctx.pending.pop(0)
                     if isinstance(d, DeferredTable):
                         d.resolve()
+        if self.window_store is not None:
+            self.window_store.settle()              # the new pane's compaction, queued behind the statements
         self._sync()
         self.stage_times["transform"] = time.perf_counter() - t0
         # outputs: device half staged here (filters + async D2H into pinned memory), host half (JSON rendering +

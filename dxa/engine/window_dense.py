@@ -116,7 +116,7 @@ class DenseWindow:
         self.NB = ring_slots // BLOCK + 4              # block slots after the pane and scratch slots
         self.blocks: Dict[int, tuple] = {}             # block id → (member entry ids, block slot, entries)
         self.layout = None              # built from the first pane's evaluated argument types
-        self.slot_of: Dict[int, tuple] = {}     # pane key → (ring slot, id of the pane's table, block id, pane key)
+        self.slot_of: Dict[int, tuple] = {}     # pane key → (ring slot, the pane, block id, pane key)
         self.free = list(range(ring_slots))    # free pane slots (a heap: the lowest is taken first)
         self.disabled = False
         self._pinned = [torch.empty(self.R, dtype=torch.int32, pin_memory=True) for _ in range(4)]
@@ -512,8 +512,9 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
             state = states[fp] = DenseWindow(dev, _requests(aggs), max(panes, len(pieces) + 2))
         proto = pieces[0][0].table
         gexprs = [_resolve_group_expr(g, Scope.of_table(proto, alias), items) for g in sel.group_by]
-        # ring slots: a pane keeps its slot while the store retains it (panes are immutable; the table id guards a
-        # re-created pane), an expired pane's slot goes back to the free heap.  One pass over the window's panes.
+        # ring slots: a pane keeps its slot while the store retains it (a pane's rows never change — its table is only
+        # compacted once; the pane object guards a re-created pane), an expired pane's slot goes back to the free
+        # heap.  One pass over the window's panes.
         slot_of = state.slot_of
         past = store.past
         for k in [k for k in slot_of if k not in past]:
@@ -525,7 +526,7 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
         for pane, full in pieces:
             if full:                                   # (pieces' "full" includes every row having a timestamp)
                 ent = slot_of.get(pane.key)
-                if ent is None or ent[1] != id(pane.table):
+                if ent is None or ent[1] is not pane:
                     if ent is not None:
                         heapq.heappush(state.free, ent[0])
                         del slot_of[pane.key]
@@ -533,7 +534,7 @@ def dense_answer(t, sel, alias: str, ctx, items, aggs: Dict, fp: str, partial_pr
                         raise Ineligible("ring full")
                     sl = heapq.heappop(state.free)
                     state.accumulate(pane.table, sl, alias, sel.where, gexprs, ctx)
-                    ent = slot_of[pane.key] = (sl, id(pane.table), pane.key // span, pane.key)
+                    ent = slot_of[pane.key] = (sl, pane, pane.key // span, pane.key)
                 mem = by_block.get(ent[2])
                 if mem is None:
                     by_block[ent[2]] = [ent]

@@ -344,6 +344,7 @@ class WindowStore:
 
     def process(self, projected: Table, batch_time_us: int, interval_us: int):
         """Returns (views: name → Table, current_count).  Window views are ``PanedTable``s (virtual unions)."""
+        self.settle()                             # a batch that ended early left its pane uncompacted
         c = self.conf
         E = batch_time_us - c.watermark_us
         S = E - c.max_window_us
@@ -361,9 +362,12 @@ class WindowStore:
                     got = _ts_stats(ts, ok, E, lens_all)
                 lo_, hi_, nok, nkeep = got[:4]
             if int(nkeep) == projected.length:
-                with host_section("windows:compact"):
-                    kept = _compact_table(projected, None if lens_all is None else (lens_all, int(got[4])))
+                # the new pane starts as the batch's own rows (views into the parse output); its compaction into an
+                # arena of its own is queued by ``settle`` after the batch's statements, so their kernels (and the
+                # status reads waiting on them) are not queued behind it
+                kept = projected
                 cur = Pane(batch_time_us, kept, int(lo_), int(hi_), True)
+                self._pending = (cur, None if lens_all is None else (lens_all, int(got[4])))
             else:
                 kept = _compact_table(projected.filter((ts >= E) if ok is None else ok & (ts >= E)))
         else:
@@ -436,6 +440,18 @@ class WindowStore:
             self.__dict__["_pmeta"] = (m[0][k:], *(a[k:] for a in m[1:]))
         else:
             self.__dict__["_pmeta"] = None
+
+    def settle(self) -> None:
+        """Compact the batch's new pane (``process``): its string views move from the batch's input buffer to an
+        arena of their own, so the pane outlives the batch without pinning that buffer."""
+        p = self.__dict__.pop("_pending", None)
+        if p is None:
+            return
+        pane, known = p
+        with host_section("windows:compact"):
+            t = _compact_table(pane.table, known)
+        t.dist = pane.table.dist
+        pane.table = t
 
     def retained_rows(self) -> int:
         return sum(p.table.length for p in self.past.values())
