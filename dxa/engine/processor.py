@@ -470,8 +470,6 @@ class Processor:
                     d = ctx.pending.pop(0)
                     if isinstance(d, DeferredTable):
                         d.resolve()
-        if self.window_store is not None:
-            self.window_store.settle()              # the new pane's compaction, queued behind the statements
         self._sync()
         self.stage_times["transform"] = time.perf_counter() - t0
         # outputs: device half staged here (filters + async D2H into pinned memory), host half (JSON rendering +
@@ -487,6 +485,10 @@ class Processor:
             staged.append((op.name, op.stage(t, ctx)))
         from ..ops.serialize import link_render_groups
         link_render_groups([p for _, st in staged for p in st.payloads()])    # one render launch pair per batch
+        if self.window_store is not None:
+            # the new pane's compaction: queued behind the statements AND the outputs' staging, so neither the
+            # statements' status reads nor the outputs' renders wait for it
+            self.window_store.settle()
         t2 = time.perf_counter()
         self.host_acc["outputs:stage"] += t2 - t1
         while len(self._inflights) >= self.output_depth:
