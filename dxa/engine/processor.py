@@ -151,6 +151,7 @@ class Processor:
         # host wall time per phase / statement, summed over batches (no device syncs): where the planning thread
         # spends a batch (bench.py --profile-stages prints it per step)
         self.host_acc: Dict[str, float] = collections.defaultdict(float)
+        self._t_route_end = self._c_route_end = 0.0
         self._parsed: Dict[str, object] = {}
         # output pipelining: batch t's sink work overlaps batch t+1's device work (at most one batch in flight)
         self.pipeline_outputs = pipeline_outputs if pipeline_outputs is not None else \
@@ -493,7 +494,8 @@ class Processor:
         self.host_acc["outputs:stage"] += t2 - t1
         while len(self._inflights) >= self.output_depth:
             self._complete_inflight()
-        self.host_acc["outputs:complete_previous"] += time.perf_counter() - t2
+        t3 = time.perf_counter()
+        self.host_acc["outputs:complete_previous"] += t3 - t2
         from ..io.sinks import _pool
         target = getattr(self, "_batch_target", None)
         fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(_timed, st.finish, partition_time, target))
@@ -502,6 +504,7 @@ class Processor:
         fl.stages = dict(self.stage_times)
         self._inflights.append(fl)
         self.stage_times["output_stage"] = time.perf_counter() - t1
+        self.host_acc["outputs:submit"] += fl.t_staged - t3
         if self.keep_views:
             self.last_views = {**{k: cat.get(k) for k in cat.names()}, **views}
         if not self.pipeline_outputs:
@@ -509,6 +512,8 @@ class Processor:
                 self._complete_inflight()
             self._sync()
             self.stage_times["output"] = time.perf_counter() - t1
+        self._t_route_end = time.perf_counter()
+        self._c_route_end = time.thread_time()
         return fl.metrics
 
     def declare_source_metrics(self, names) -> None:
@@ -812,7 +817,12 @@ class Processor:
             tr = time.perf_counter()
             metrics = self.route(projected, batch_time_us, interval_us, ctx,
                                  partition_time or _dt.datetime.utcnow(), t0)
-            self.host_acc["route"] += time.perf_counter() - tr
+            t_ret = time.perf_counter()
+            self.host_acc["route"] += t_ret - tr
+            # from route's return to here: the batch thread waiting for the GIL an output thread took (wall) and
+            # the release of route's locals (CPU)
+            self.host_acc["route:release"] += t_ret - self._t_route_end
+            self.host_acc["route:release_cpu"] += time.thread_time() - self._c_route_end
             self.batches += 1
             return metrics
         except Exception:

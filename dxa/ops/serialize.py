@@ -325,30 +325,22 @@ def _render_members(members: List["Staged"]) -> None:
     with torch.inference_mode(), torch.cuda.stream(side):
         for m in members:
             side.wait_event(m.event)
-        b = _DevBuilder()
-        progs = []
-        for m in members:
-            top = [b.add(c, nm) for nm, c in zip(m.table.names, m.table.columns)]
-            progs.append(b.program(top))
-        prog = [v for p in progs for v in p]
-        nprog = len(prog) // 4
-        blob = b.tables_blob(prog)
-        tw = (len(blob) - ctypes.sizeof(DevNode) * len(b.nodes) - ((len(prog) * 4 + 7) // 8) * 8) // 8
+        plan, keep = _plan_of(members)
+        blob, nnodes, nprog, tw, pcs = plan
         segs = _SerSegs()
         segs.nseg = len(members)
-        r = pc = 0
+        r = 0
         for k, m in enumerate(members):
-            segs.row[k], segs.pc[k] = r, pc
+            segs.row[k], segs.pc[k] = r, pcs[k]
             r += m.n
-            pc += len(progs[k]) // 4
-        segs.row[len(members)], segs.pc[len(members)] = r, pc
+        segs.row[len(members)], segs.pc[len(members)] = r, pcs[len(members)]
         n = r
         lens_h = torch.empty(n, dtype=torch.int64, pin_memory=True)
         if n:
             tables = N.h2d(blob, torch.uint8, dev)
             st = N.stream_handle(dev)
             lens = torch.empty(n, dtype=torch.int64, device=dev)
-            N.call("dxa_serialize_rows", 0, N.ptr(tables), len(b.nodes), nprog, tw, ctypes.addressof(segs), N.ptr(lens),
+            N.call("dxa_serialize_rows", 0, N.ptr(tables), nnodes, nprog, tw, ctypes.addressof(segs), N.ptr(lens),
                    None, None, st)
             ends = torch.cumsum(lens, 0)
             lens_h.copy_(lens, non_blocking=True)
@@ -359,7 +351,7 @@ def _render_members(members: List["Staged"]) -> None:
         STATS["launch_pairs"] += 1
         if n:
             out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-            N.call("dxa_serialize_rows", 1, N.ptr(tables), len(b.nodes), nprog, tw, ctypes.addressof(segs), N.ptr(lens),
+            N.call("dxa_serialize_rows", 1, N.ptr(tables), nnodes, nprog, tw, ctypes.addressof(segs), N.ptr(lens),
                    N.ptr(ends), N.ptr(out), st)
         if len(members) == 1 and members[0].compress and total > 1:
             # gzip of the newline-joined documents (no trailing newline: what a blob sink writes), on the GPU;
@@ -382,6 +374,117 @@ def _render_members(members: List["Staged"]) -> None:
         m._done(JsonLines(blob_np[off:off + size], ln - 1))
         r += m.n
         off += size
+
+
+def _build_plan(members: List["Staged"]):
+    """The render tables of ``members`` through ``_DevBuilder``: (blob, nodes, program ops, text words, per-member
+    program starts + total), and the converted tensors the blob points at (alive until the kernels ran)."""
+    b = _DevBuilder()
+    progs = []
+    for m in members:
+        top = [b.add(c, nm) for nm, c in zip(m.table.names, m.table.columns)]
+        progs.append(b.program(top))
+    prog = [v for p in progs for v in p]
+    blob = b.tables_blob(prog)
+    tw = (len(blob) - ctypes.sizeof(DevNode) * len(b.nodes) - ((len(prog) * 4 + 7) // 8) * 8) // 8
+    pcs, pc = [], 0
+    for p in progs:
+        pcs.append(pc)
+        pc += len(p) // 4
+    pcs.append(pc)
+    return (blob, len(b.nodes), len(prog) // 4, tw, pcs), b.keep
+
+
+# Render plans of flat tables (one node per column) by their shape — names, column kinds, constant values: the
+# node array, program and text pool are the same every batch, only the five buffer pointers of each node change.
+# A batch's outputs then cost a signature and the pointer reads instead of a walk of the builder per column.
+_PLANS: dict = {}
+_PLAN_MAX = 64
+_PTR_COLS = 5                        # DevNode's pointer fields (data, valid, arena, starts, lens): its last 5 words
+_INT_KINDS = {"byte": K_I64, "short": K_I64, "int": K_I64, "long": K_I64, "date": K_DATE}
+
+
+def _flat_signature(members: List["Staged"]):
+    from ..engine.column import ConstColumn, JsonColumn, PrimColumn, StrColumn
+    from ..engine.decimal import is_decimal
+    sig = []
+    for m in members:
+        for nm, c in zip(m.table.names, m.table.columns):
+            tc = type(c)
+            if tc is PrimColumn:
+                if is_decimal(c.dtype):
+                    return None
+                sig.append((nm, c.dtype))
+            elif tc is StrColumn or tc is JsonColumn:
+                sig.append((nm, tc))
+            elif tc is ConstColumn:
+                v = c.value
+                if v is not None and type(v) not in (str, int, float, bool):
+                    return None
+                sig.append((nm, c.dtype, type(v), v))
+            else:
+                return None
+        sig.append(len(m.table.columns))
+    return tuple(sig)
+
+
+def _flat_pointers(members: List["Staged"], keep: list) -> List[int]:
+    """(data, valid, arena, starts, lens) of every column, converted as ``_DevBuilder.add`` converts them."""
+    from ..engine.column import ConstColumn, PrimColumn
+    out = []
+    for m in members:
+        for c in m.table.columns:
+            if type(c) is ConstColumn:
+                out += (0, 0, 0, 0, 0)
+                continue
+            v = c.valid
+            if v is not None:
+                v = (v.view(torch.uint8) if v.dtype == torch.bool else v).contiguous()
+                keep.append(v)
+            vp = 0 if v is None else v.data_ptr()
+            if type(c) is PrimColumn:
+                dt, d = c.dtype, c.data
+                if dt == "boolean":
+                    d = d.to(torch.uint8)
+                elif dt in _INT_KINDS:
+                    d = d.to(torch.int64)
+                elif dt != "timestamp":
+                    d = d.to(torch.float64)
+                d = d.contiguous()
+                keep.append(d)
+                out += (d.data_ptr(), vp, 0, 0, 0)
+            else:
+                a, st, ln = c.arena.contiguous(), c.starts.to(torch.int64).contiguous(), c.lens.to(torch.int32).contiguous()
+                keep += (a, st, ln)
+                out += (0, vp, a.data_ptr(), st.data_ptr(), ln.data_ptr())
+    return out
+
+
+def _plan_of(members: List["Staged"]):
+    """The render plan of ``members`` (``_build_plan``'s tuple, the blob with this batch's pointers) and the tensors
+    to keep alive; flat shapes reuse a cached template."""
+    sig = _flat_signature(members)
+    if sig is None:
+        return _build_plan(members)
+    tmpl = _PLANS.get(sig)
+    if tmpl is None:
+        plan, keep = _build_plan(members)
+        blob, nnodes = plan[0], plan[1]
+        t = np.frombuffer(blob, dtype=np.uint8).copy()
+        words = t[:ctypes.sizeof(DevNode) * nnodes].view(np.uint64).reshape(nnodes, -1)
+        words[:, -_PTR_COLS:] = 0
+        if len(_PLANS) >= _PLAN_MAX:
+            _PLANS.clear()
+        _PLANS[sig] = (t, plan)
+        return plan, keep
+    t, plan = tmpl
+    nnodes = plan[1]
+    keep: list = []
+    ptrs = _flat_pointers(members, keep)
+    buf = t.copy()
+    buf[:ctypes.sizeof(DevNode) * nnodes].view(np.uint64).reshape(nnodes, -1)[:, -_PTR_COLS:] = \
+        np.array(ptrs, dtype=np.uint64).reshape(nnodes, _PTR_COLS)
+    return (torch.from_numpy(buf),) + plan[1:], keep
 
 
 class RenderGroup:
