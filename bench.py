@@ -571,6 +571,8 @@ def main():
     from dxa.ops import serialize as _ser0
     ser_stats0 = dict(_ser0.STATS)
     host0 = dict(getattr(proc, "host_acc", {}))
+    from dxa.engine import processor as _pm
+    out_cpu0 = _pm.OUTPUT_CPU[0]
     from dxa.telemetry import tracing as _tr
     _tr.time_host_syncs()
     sec0 = dict(_tr.HOST_ACC)
@@ -718,6 +720,8 @@ def main():
         out["stage_s"] = {k: round(v, 5) for k, v in proc.stage_times.items()}
         out["host_ms_per_step"] = {k: round((v - host0.get(k, 0.0)) / args.steps * 1e3, 3)
                                    for k, v in getattr(proc, "host_acc", {}).items()}
+        from dxa.engine import processor as _pm
+        out["host_ms_per_step"]["outputs:thread_cpu"] = round((_pm.OUTPUT_CPU[0] - out_cpu0) / args.steps * 1e3, 3)
         if _tr.HOST_ACC:
             out["host_sections_ms_per_step"] = {k: round((v - sec0.get(k, 0.0)) / args.steps * 1e3, 3)
                                                 for k, v in sorted(_tr.HOST_ACC.items())}

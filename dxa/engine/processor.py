@@ -855,8 +855,13 @@ def _maybe_inject_fault(batch_index: int):
     raise RuntimeError(f"injected fault at batch {batch_index}")
 
 
+OUTPUT_CPU = [0.0]             # output threads' CPU time (time.thread_time) in the outputs' host halves, summed
+
+
 def _timed(fn, *args):
+    c0 = time.thread_time()
     out = fn(*args)
+    OUTPUT_CPU[0] += time.thread_time() - c0
     return out, time.perf_counter()
 
 
