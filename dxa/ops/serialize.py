@@ -395,19 +395,23 @@ def _build_plan(members: List["Staged"]):
     return (blob, len(b.nodes), len(prog) // 4, tw, pcs), b.keep
 
 
-# Render plans of flat tables (one node per column) by their shape — names, column kinds, constant values: the
-# node array, program and text pool are the same every batch, only the five buffer pointers of each node change.
-# A batch's outputs then cost a signature and the pointer reads instead of a walk of the builder per column.
+# Render plans of flat tables (one node per column) by their shape — names, column kinds, constants' types: the
+# node array, program and text pool are the same every batch; only the five buffer pointers of each node change, and
+# a constant whose text differs from the template's (a batch time in an alert row) gets its text appended to the
+# pool.  A batch's outputs then cost a signature and the pointer reads instead of a walk of the builder per column.
 _PLANS: dict = {}
 _PLAN_MAX = 64
 _PTR_COLS = 5                        # DevNode's pointer fields (data, valid, arena, starts, lens): its last 5 words
 _INT_KINDS = {"byte": K_I64, "short": K_I64, "int": K_I64, "long": K_I64, "date": K_DATE}
 
 
-def _flat_signature(members: List["Staged"]):
+def _flat_signature(members: List["Staged"], consts: Optional[list] = None):
+    """The plan-cache key of ``members`` (None: not flat); ``consts`` collects (node index, value, type) of every
+    constant column."""
     from ..engine.column import ConstColumn, JsonColumn, PrimColumn, StrColumn
     from ..engine.decimal import is_decimal
     sig = []
+    k = 0
     for m in members:
         for nm, c in zip(m.table.names, m.table.columns):
             tc = type(c)
@@ -421,11 +425,29 @@ def _flat_signature(members: List["Staged"]):
                 v = c.value
                 if v is not None and type(v) not in (str, int, float, bool):
                     return None
-                sig.append((nm, c.dtype, type(v), v))
+                sig.append((nm, c.dtype, type(v)))
+                if consts is not None and v is not None:
+                    consts.append((k, v, c.dtype))
             else:
                 return None
+            k += 1
         sig.append(len(m.table.columns))
     return tuple(sig)
+
+
+_CONST_TEXT: dict = {}
+
+
+def _const_text(v, dtype) -> bytes:
+    """A constant's rendered text (``_DevBuilder.add``'s), memoised: alert rows carry a new batch time each batch."""
+    key = (type(v), v, str(dtype))
+    t = _CONST_TEXT.get(key)
+    if t is None:
+        from ..engine.serialize import _scalar_text
+        if len(_CONST_TEXT) >= 4096:
+            _CONST_TEXT.clear()
+        t = _CONST_TEXT[key] = _scalar_text(v, dtype).encode("utf-8")
+    return t
 
 
 def _flat_pointers(members: List["Staged"], keep: list) -> List[int]:
@@ -463,7 +485,8 @@ def _flat_pointers(members: List["Staged"], keep: list) -> List[int]:
 def _plan_of(members: List["Staged"]):
     """The render plan of ``members`` (``_build_plan``'s tuple, the blob with this batch's pointers) and the tensors
     to keep alive; flat shapes reuse a cached template."""
-    sig = _flat_signature(members)
+    consts: list = []
+    sig = _flat_signature(members, consts)
     if sig is None:
         return _build_plan(members)
     tmpl = _PLANS.get(sig)
@@ -475,16 +498,34 @@ def _plan_of(members: List["Staged"]):
         words[:, -_PTR_COLS:] = 0
         if len(_PLANS) >= _PLAN_MAX:
             _PLANS.clear()
-        _PLANS[sig] = (t, plan)
+        _PLANS[sig] = (t, plan, [(k, _const_text(v, dt)) for k, v, dt in consts])
         return plan, keep
-    t, plan = tmpl
-    nnodes = plan[1]
+    t, plan, texts = tmpl
+    nnodes, tw = plan[1], plan[3]
     keep: list = []
     ptrs = _flat_pointers(members, keep)
-    buf = t.copy()
-    buf[:ctypes.sizeof(DevNode) * nnodes].view(np.uint64).reshape(nnodes, -1)[:, -_PTR_COLS:] = \
-        np.array(ptrs, dtype=np.uint64).reshape(nnodes, _PTR_COLS)
-    return (torch.from_numpy(buf),) + plan[1:], keep
+    extra, patches = bytearray(), []
+    for (k, v, dt), (_, old) in zip(consts, texts):
+        txt = _const_text(v, dt)
+        if txt != old:
+            patches.append((k, tw * 8 + len(extra), len(txt)))
+            extra += txt + b"\0" * (-len(txt) % 8)
+    if patches:
+        extra += b"\0" * 8                      # the zero word the text pool ends with
+        if len(t) + len(extra) > _LDS_LIMIT:    # the kernels stage the tables in 64 KiB of LDS
+            return _build_plan(members)
+        buf = np.concatenate([t, np.frombuffer(bytes(extra), dtype=np.uint8)])
+        tw += len(extra) // 8
+    else:
+        buf = t.copy()
+    nb = ctypes.sizeof(DevNode) * nnodes
+    buf[:nb].view(np.uint64).reshape(nnodes, -1)[:, -_PTR_COLS:] = np.array(ptrs, dtype=np.uint64).reshape(nnodes,
+                                                                                                           _PTR_COLS)
+    if patches:
+        ints = buf[:nb].view(np.int32).reshape(nnodes, -1)
+        for k, off, ln in patches:
+            ints[k, 6], ints[k, 7] = off, ln           # DevNode.const_off / const_len
+    return (torch.from_numpy(buf), nnodes, plan[2], tw, plan[4]), keep
 
 
 class RenderGroup:

@@ -75,3 +75,30 @@ def test_shape_change_misses_and_unsupported_columns_walk():
     assert bytes(plan[0])[nb:] == want[nb:]
     assert S._flat_signature([_M(Table(["x"], [PrimColumn(parse_decimal_type("decimal(10,2)"), torch.zeros(3, dtype=torch.int64))],
                                              3, "cpu"))]) is None
+
+
+def _const_texts(blob, nnodes, tw):
+    """Each node's constant text, read back through its const_off / const_len."""
+    nb = S.ctypes.sizeof(S.DevNode) * nnodes
+    raw = blob if isinstance(blob, bytes) else bytes(blob.numpy()) if isinstance(blob, torch.Tensor) else bytes(blob)
+    ints = np.frombuffer(raw[:nb], dtype=np.int32).reshape(nnodes, -1)
+    text = raw[len(raw) - tw * 8:]
+    return [text[o:o + n] for o, n in zip(ints[:, 6], ints[:, 7])]
+
+
+def test_changing_constant_reuses_plan_with_patched_text():
+    """An alert row's batch time is a constant that changes every batch: the plan is reused and the new value's text
+    is appended to the pool, so the rendered constants are the builder's."""
+    S._PLANS.clear()
+
+    def alert(ts):
+        cols = [ConstColumn(ts, "timestamp", 1, "cpu"), ConstColumn("HotAlert", "string", 1, "cpu"),
+                ConstColumn(0, "long", 1, "cpu"), PrimColumn("double", torch.tensor([1.5], dtype=torch.float64))]
+        return [_M(Table(["EventTime", "MetricName", "Metric", "v"], cols, 1, "cpu")), _M(_table(5, 9))]
+
+    S._plan_of(alert(1792358528000000))
+    for ts in (1792358529000000, 1792358530123000):
+        plan, _ = S._plan_of(alert(ts))
+        assert len(S._PLANS) == 1
+        want, rest, _ = _fresh(alert(ts))
+        assert _const_texts(plan[0], plan[1], plan[3]) == _const_texts(want, rest[0], rest[2])
