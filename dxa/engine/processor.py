@@ -498,8 +498,14 @@ class Processor:
         self.host_acc["outputs:complete_previous"] += t3 - t2
         from ..io.sinks import _pool
         target = getattr(self, "_batch_target", None)
-        fl = _InFlight(batch_time_us, metrics, [(name, _pool.submit(_timed, st.finish, partition_time, target))
-                                                 for name, st in staged], t_start)
+        local = [k for k, (_, st) in enumerate(staged) if st.op.local]
+        futs = {}
+        if len(local) > 1:
+            together = _pool.submit(_finish_local, [staged[k][1] for k in local], partition_time, target)
+            futs = {k: _Part(together, j) for j, k in enumerate(local)}
+        fl = _InFlight(batch_time_us, metrics, [(name, futs.get(k) or _pool.submit(_timed, st.finish, partition_time,
+                                                                                   target))
+                                                for k, (name, st) in enumerate(staged)], t_start)
         fl.t_staged = time.perf_counter()
         fl.stages = dict(self.stage_times)
         self._inflights.append(fl)
@@ -863,6 +869,22 @@ def _timed(fn, *args):
     out = fn(*args)
     OUTPUT_CPU[0] += time.thread_time() - c0
     return out, time.perf_counter()
+
+
+def _finish_local(items, partition_time, target):
+    """The host halves of a batch's outputs whose sinks never block (``OutputOperator.local``), on one thread."""
+    return [_timed(st.finish, partition_time, target) for st in items]
+
+
+class _Part:
+    """One output's (metrics, end time) out of a ``_finish_local`` future."""
+    __slots__ = ("fut", "k")
+
+    def __init__(self, fut, k):
+        self.fut, self.k = fut, k
+
+    def result(self):
+        return self.fut.result()[self.k]
 
 
 class _InFlight:

@@ -333,12 +333,21 @@ def register_sink(kind: str, factory: Callable):
     SINK_FACTORIES[kind.lower()] = factory
 
 
+# sinks that never block on I/O: a batch's outputs writing only to these finish on one output thread, one after
+# another (a thread per output then only adds wake-ups and GIL hand-offs against the batch thread)
+LOCAL_SINKS = frozenset({"Null", "Memory", "Console"})
+
+
 class OutputOperator:
     def __init__(self, name: str, sinks: List[Sink], processed_schema_path: Optional[str] = None):
         self.name = name
         self.sinks = sinks
         self.processed_schema_path = processed_schema_path
         self._schema_written = False
+
+    @property
+    def local(self) -> bool:
+        return all(s.name in LOCAL_SINKS for s in self.sinks)
 
     def stage(self, table: Table, ctx=None) -> "StagedOutput":
         """Device-side half of an output (runs on the batch's thread/stream): drop internal columns, evaluate
