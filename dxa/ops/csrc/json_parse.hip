@@ -1200,9 +1200,10 @@ __global__ __launch_bounds__(256) void write_newlines_bits_kernel(const uint16_t
   }
 }
 
-// Zero `nbytes` at `p` with 16-byte stores (the runtime's byte-pattern fill ran at ~0.3 TB/s on the validity planes:
-// ~125 us per 33 MB plane per batch, profiles/round6/parse/README.md).  Head / tail bytes outside the aligned body
-// are stored singly.
+// Zero `nbytes` at `p` with 16-byte stores: the validity planes' clear as a kernel of the parse library.  On an idle
+// GPU it and hipMemsetAsync both clear a 33 MB plane in ~6.8 us (tools/gpu/zero_probe.hip); inside the flows either
+// one's duration is inflated by the kernels other streams run meanwhile (profiles/round6/parse/README.md).  Head /
+// tail bytes outside the aligned body are stored singly.
 __global__ void zero_bytes_kernel(uint8_t* __restrict__ p, int64_t nbytes) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   const int64_t head = (int64_t)((16 - (a & 15)) & 15) < nbytes ? (int64_t)((16 - (a & 15)) & 15) : nbytes;
