@@ -585,6 +585,13 @@ class Processor:
         reads: List[Tuple[int, set]] = []
         lv: Dict[int, int] = {}
         commands = []
+        # statements that read a time window, directly or through another statement: a windowed GROUP BY completes
+        # lazily (DeferredTable), so within a level they go after the others — a statement that synchronises on its
+        # own inputs (a WHERE count) then does not wait for the window's kernels, and the window's readers find them
+        # finished
+        wnames = {"timewindow", f"{S.NAME_PREFIX}ProcessedInput_Window".lower()} | (
+            {n.lower() for n in self.window_store.conf.windows} if self.window_store is not None else set())
+        windowed: set = set()
         for k, c in enumerate(cmds):
             if c.command_type == COMMAND_COMMAND:
                 commands.append(k)
@@ -605,10 +612,14 @@ class Processor:
             lv[k] = lk
             level[nm] = lk
             reads.append((k, words))
+            if words & wnames or any(w in windowed and w != nm for w in words):
+                windowed.add(nm)
         steps = [[k] for k in commands]
         for L in sorted(set(lv.values())):
             ks = [k for k in sorted(lv) if lv[k] == L]
             plain = [k for k in ks if cmds[k].name not in self.state_tables]
+            if not key[2]:
+                plain.sort(key=lambda k: cmds[k].name.lower() in windowed)      # stable: text order otherwise
             if plain:
                 # sequential mode with a window: one statement per step, level by level — a windowed statement's
                 # readers run after the statements that do not read it, while its kernels finish (DeferredTable)
