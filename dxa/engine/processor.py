@@ -34,7 +34,7 @@ from ..ops.jsonparse import ParsePlan, parse, parse_async
 from ..sql.transform import COMMAND_COMMAND, parse_transform
 from .column import ConstColumn, DeferredTable, PrimColumn, StructColumn, Table, concat_tables
 from .expr import EvalContext, EvalError
-from .query import Catalog, execute, prefilter, run_sql
+from .query import Catalog, execute, filter_readers, prefilter, prefilter_result, run_sql
 from .serialize import table_to_json_lines
 from .state import create_state_tables
 from .types import MapType, StructType, schema_from_json
@@ -430,12 +430,21 @@ class Processor:
             schedule = list(self._view_schedule(live))
             # windowed GROUP BYs may complete lazily (one rank, sequential views): see query._deferred_select
             defer_ok = self.device.type == "cuda" and not P.active() and not self._concurrent_views()
+            readers = {}
             if self.device.type == "cuda":
                 # the WHERE masks of statements over tables present now, with one count read for all of them
                 # (command statements change nothing a predicate reads: _run_command)
                 with tracing.host_section("prefilter"):
                     prefilter([self._query(cmds[k]) for step in schedule for k in step
                                if cmds[k].command_type != COMMAND_COMMAND], cat, ctx)
+                if not self._concurrent_views():
+                    # statements filtering a view this batch produces: their masks start when the view is registered
+                    order = [k for step in schedule for k in step if cmds[k].command_type != COMMAND_COMMAND]
+                    key = ("readers", tuple(order))
+                    if getattr(self, "_readers", (None,))[0] != key:
+                        self._readers = (key, filter_readers([(k, self._query(cmds[k])) for k in order], ctx))
+                    readers = self._readers[1]
+                    rank = {k: i for i, k in enumerate(order)}
             for step in schedule:
                 if len(step) > 1:
                     # independent views: each on a side HIP stream, forked from and joined back to this stream
@@ -466,6 +475,12 @@ class Processor:
                             result = st.overwrite(result, tag=batch_time_us)
                     cat.register(cmd.name, result)
                     views[cmd.name] = result
+                    later = readers.get(cmd.name.lower()) if readers else None
+                    if later and not isinstance(result, DeferredTable):
+                        later = [r for r in later if rank.get(r[0], -1) > rank.get(k, -1)]
+                        if later:
+                            with tracing.host_section("prefilter"):
+                                prefilter_result(result, later, ctx)
             with tracing.host_section("deferred:finish"):
                 while ctx.pending:                  # results no later statement read: complete them now
                     d = ctx.pending.pop(0)

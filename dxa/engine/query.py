@@ -1252,6 +1252,31 @@ def prefilter(queries, catalog, ctx) -> None:
     ctx.prefilter_cands = {k: v for k, v in cands.items() if len(v) > 1}    # one filter alone gains nothing
 
 
+def filter_readers(queries, ctx) -> Dict[str, list]:
+    """Statements (index, SELECT, alias) whose plain WHERE filters a named table, by that name (lower case): the
+    candidates ``prefilter_result`` starts as soon as a statement registers the table they read."""
+    out: Dict[str, list] = {}
+    for k, q in queries:
+        if q is None or q.ctes or not isinstance(q.body, A.Select):
+            continue
+        sel = q.body
+        src = sel.from_
+        if sel.where is None or sel.grouping_sets is not None or not isinstance(src, A.TableRef) or src.sample or \
+                src.timewindow or not _plain_predicate(sel.where, ctx):
+            continue
+        out.setdefault(src.name.lower(), []).append((k, sel, src.alias or src.name.split(".")[-1]))
+    return out
+
+
+def prefilter_result(table, readers, ctx) -> None:
+    """A statement's result just registered: the WHERE masks of the later statements that filter it (``readers``)
+    are queued now, their counts on the way to pinned memory — by the time those statements run, the statements in
+    between have synchronised the stream, and they take their rows without a wait of their own."""
+    if table.device.type != "cuda" or not table.length:
+        return
+    _run_prefilters([(sel, table, alias) for _, sel, alias in readers if id(sel) not in ctx.prefilter], ctx)
+
+
 def _run_prefilters(cands, ctx) -> None:
     found = []
     for sel, t, alias in cands:

@@ -80,3 +80,17 @@ def test_write_after_read(tmp_path, monkeypatch):
     names = _names(p, p._view_schedule(None))
     pos = {n: i for i, s in enumerate(names) for n in s}
     assert pos["A"] < pos["B"] < pos["Old"] < pos["DeviceState"]
+
+
+def test_filter_readers_of_produced_views(tmp_path):
+    """Statements with a plain WHERE over a view the batch produces are found by that view's name
+    (query.filter_readers): the processor queues their masks when the view is registered."""
+    from dxa.engine.expr import EvalContext
+    from dxa.engine.query import filter_readers
+    p = _proc(tmp_path, "full")
+    cmds = p.transform.commands
+    order = [k for s in p._view_schedule(p._live_statements()) for k in s if cmds[k].name]
+    got = filter_readers([(k, p._query(cmds[k])) for k in order], EvalContext())
+    assert [cmds[k].name for k, _, _ in got.get("devicenamed", [])] == ["UnhealthyDevices"]
+    # the windowed GROUP BY is not a filter of its input (the dense / paned path applies its WHERE per pane)
+    assert all(cmds[k].name != "DeviceWindow" for v in got.values() for k, _, _ in v)
