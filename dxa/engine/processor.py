@@ -444,7 +444,7 @@ class Processor:
                     if getattr(self, "_readers", (None,))[0] != key:
                         self._readers = (key, filter_readers([(k, self._query(cmds[k])) for k in order], ctx))
                     readers = self._readers[1]
-                    rank = {k: i for i, k in enumerate(order)}
+                    step_of = {k: i for i, k in enumerate(order)}
             for step in schedule:
                 if len(step) > 1:
                     # independent views: each on a side HIP stream, forked from and joined back to this stream
@@ -477,7 +477,7 @@ class Processor:
                     views[cmd.name] = result
                     later = readers.get(cmd.name.lower()) if readers else None
                     if later and not isinstance(result, DeferredTable):
-                        later = [r for r in later if rank.get(r[0], -1) > rank.get(k, -1)]
+                        later = [r for r in later if step_of.get(r[0], -1) > step_of.get(k, -1)]
                         if later:
                             with tracing.host_section("prefilter"):
                                 prefilter_result(result, later, ctx)
