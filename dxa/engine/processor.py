@@ -34,7 +34,7 @@ from ..ops.jsonparse import ParsePlan, parse, parse_async
 from ..sql.transform import COMMAND_COMMAND, parse_transform
 from .column import ConstColumn, DeferredTable, PrimColumn, StructColumn, Table, concat_tables
 from .expr import EvalContext, EvalError
-from .query import Catalog, execute, filter_readers, prefilter, prefilter_result, run_sql
+from .query import Catalog, _run_prefilters, execute, filter_readers, prefilter, prefilter_result, run_sql
 from .serialize import table_to_json_lines
 from .state import create_state_tables
 from .types import MapType, StructType, schema_from_json
@@ -434,9 +434,16 @@ class Processor:
             if self.device.type == "cuda":
                 # the WHERE masks of statements over tables present now, with one count read for all of them
                 # (command statements change nothing a predicate reads: _run_command)
+                # with a window (sequential views): every such mask is queued right now, ahead of the windowed
+                # statements' kernels (which the schedule starts first), so the count read finds them done
+                eager = self.window_store is not None and not self._concurrent_views()
                 with tracing.host_section("prefilter"):
                     prefilter([self._query(cmds[k]) for step in schedule for k in step
-                               if cmds[k].command_type != COMMAND_COMMAND], cat, ctx)
+                               if cmds[k].command_type != COMMAND_COMMAND], cat, ctx, min_group=1 if eager else 2)
+                    if eager:
+                        for group in list(ctx.prefilter_cands.values()):
+                            _run_prefilters(group, ctx)
+                        ctx.prefilter_cands = {}
                 if not self._concurrent_views():
                     # statements filtering a view this batch produces: their masks start when the view is registered
                     order = [k for step in schedule for k in step if cmds[k].command_type != COMMAND_COMMAND]
@@ -600,13 +607,14 @@ class Processor:
         reads: List[Tuple[int, set]] = []
         lv: Dict[int, int] = {}
         commands = []
-        # statements that read a time window, directly or through another statement: a windowed GROUP BY completes
-        # lazily (DeferredTable), so within a level they go after the others — a statement that synchronises on its
-        # own inputs (a WHERE count) then does not wait for the window's kernels, and the window's readers find them
-        # finished
+        # statements that read a time window directly run first in their level (a windowed GROUP BY completes lazily,
+        # DeferredTable: its kernels start soonest), and the statements reading their results run last in theirs, so
+        # the status read finds the kernels finished.  The WHERE masks over the batch's tables are queued before all
+        # of it (route: prefilter), so their count reads do not wait for the window's kernels
         wnames = {"timewindow", f"{S.NAME_PREFIX}ProcessedInput_Window".lower()} | (
             {n.lower() for n in self.window_store.conf.windows} if self.window_store is not None else set())
         windowed: set = set()
+        direct: set = set()
         for k, c in enumerate(cmds):
             if c.command_type == COMMAND_COMMAND:
                 commands.append(k)
@@ -627,6 +635,8 @@ class Processor:
             lv[k] = lk
             level[nm] = lk
             reads.append((k, words))
+            if words & wnames:
+                direct.add(nm)
             if words & wnames or any(w in windowed and w != nm for w in words):
                 windowed.add(nm)
         steps = [[k] for k in commands]
@@ -634,7 +644,9 @@ class Processor:
             ks = [k for k in sorted(lv) if lv[k] == L]
             plain = [k for k in ks if cmds[k].name not in self.state_tables]
             if not key[2]:
-                plain.sort(key=lambda k: cmds[k].name.lower() in windowed)      # stable: text order otherwise
+                # windowed statements first (their kernels start soonest), their readers last; stable otherwise
+                plain.sort(key=lambda k: 0 if cmds[k].name.lower() in direct else
+                           2 if cmds[k].name.lower() in windowed else 1)
             if plain:
                 # sequential mode with a window: one statement per step, level by level — a windowed statement's
                 # readers run after the statements that do not read it, while its kernels finish (DeferredTable)

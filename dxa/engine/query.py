@@ -1226,7 +1226,7 @@ def _plain_predicate(e: A.Expr, ctx) -> bool:
     return not any(isinstance(n, A.SubqueryExpr) for n in A.walk(e))
 
 
-def prefilter(queries, catalog, ctx) -> None:
+def prefilter(queries, catalog, ctx, min_group: int = 2) -> None:
     """Note the statements that filter a table already in ``catalog`` (the batch's input views, reference and state
     tables).  When the first of them runs, the WHERE masks of all of them over that same table are evaluated
     together and their row counts come to pinned memory in ONE copy (``_run_prefilters``): the statements after
@@ -1249,7 +1249,8 @@ def prefilter(queries, catalog, ctx) -> None:
                 not isinstance(it.expr, A.Star) and _contains_agg(it.expr, ctx) for it in sel.items)):
             continue                       # a windowed aggregate: the paned / dense path applies WHERE per pane
         cands.setdefault(id(t), []).append((sel, t, src.alias or src.name.split(".")[-1]))
-    ctx.prefilter_cands = {k: v for k, v in cands.items() if len(v) > 1}    # one filter alone gains nothing
+    # lazily run, one filter alone gains nothing (``min_group`` 2); run at once ahead of a window's kernels, it does
+    ctx.prefilter_cands = {k: v for k, v in cands.items() if len(v) >= min_group}
 
 
 def filter_readers(queries, ctx) -> Dict[str, list]:

@@ -41,9 +41,9 @@ def test_sequential_level_order_with_a_window(tmp_path):
     # a statement that reads only the input runs before DeviceWindow's first reader
     indep = [n for n in names if n and n.startswith("sa1_")]
     assert indep and all(pos[n] < pos["DeviceNamed"] for n in indep)
-    # within a level the windowed statements come last: the rules' filters before DeviceWindow, the alerts before
-    # DeviceWindow's readers
-    assert all(pos[n] < pos["DeviceWindow"] for n in indep)
+    # within a level the windowed statement comes first and its readers last: DeviceWindow before the rules'
+    # filters, the alerts before DeviceWindow's readers
+    assert all(pos["DeviceWindow"] < pos[n] for n in indep)
     assert pos["HotAlert"] < pos["DeviceNamed"] and pos["LowBatteryAlert"] < pos["DeviceNamed"]
 
 
